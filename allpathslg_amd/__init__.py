@@ -1,0 +1,23 @@
+"""allpathslg_amd — MI355X-native k-mer spectrum / correction / unipath engine.
+
+The compute lives in libapg.so (HIP kernels for gfx950 behind the C ABI of
+include/apg.h).  This package is the Python host layer used by tests, the
+benchmark and the multi-GPU driver.
+"""
+from ._lib import ApgError, lib  # noqa: F401
+from .engine import DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, shard_bins  # noqa: F401
+from .reads import ReadSet, synth_genome, synth_reads  # noqa: F401
+
+__all__ = [
+    "ApgError",
+    "Context",
+    "DeviceReads",
+    "DEFAULT_HIST_LEN",
+    "ReadSet",
+    "kmer_hash",
+    "kmer_unhash",
+    "lib",
+    "shard_bins",
+    "synth_genome",
+    "synth_reads",
+]

@@ -1,0 +1,154 @@
+"""ctypes binding of libapg.so (the C ABI declared in include/apg.h).
+
+The shared library is built in-tree (``allpathslg_amd/libapg.so``) by
+``__graft_entry__.build()`` / ``make -C allpathslg_amd/csrc``.  There is no
+fallback: if the library is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libapg.so")
+
+APG_OK = 0
+ERRORS = {
+    -1: "APG_E_ARG",
+    -2: "APG_E_HIP",
+    -3: "APG_E_IO",
+    -4: "APG_E_STATE",
+    -5: "APG_E_NOMEM",
+    -6: "APG_E_UNSUPPORTED",
+}
+
+
+class ApgError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where}: {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class apg_config(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("timing", C.c_int32),
+        ("verbose", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("reserved", C.c_uint64 * 6),
+    ]
+
+
+class apg_reads(C.Structure):
+    _fields_ = [
+        ("n_reads", C.c_uint64),
+        ("base_off", C.POINTER(C.c_uint64)),
+        ("byte_off", C.POINTER(C.c_uint64)),
+        ("packed", C.POINTER(C.c_uint8)),
+        ("quals", C.POINTER(C.c_uint8)),
+    ]
+
+
+class apg_kstats(C.Structure):
+    _fields_ = [
+        ("n_kmers", C.c_uint64),
+        ("n_distinct", C.c_uint64),
+        ("n_buckets", C.c_uint64),
+        ("n_overflow", C.c_uint64),
+        ("max_bucket", C.c_uint64),
+        ("reserved", C.c_uint64 * 3),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
+
+
+class apg_synth_params(C.Structure):
+    _fields_ = [
+        ("genome_len", C.c_uint64),
+        ("seed", C.c_uint64),
+        ("n_pairs", C.c_uint64),
+        ("read_len", C.c_uint32),
+        ("insert_mean", C.c_uint32),
+        ("insert_sd", C.c_uint32),
+        ("threads", C.c_uint32),
+        ("err_lo", C.c_double),
+        ("err_hi", C.c_double),
+        ("first_pair", C.c_uint64),
+    ]
+
+
+_P = C.c_void_p
+_u64p = C.POINTER(C.c_uint64)
+_u32p = C.POINTER(C.c_uint32)
+_u8p = C.POINTER(C.c_uint8)
+
+# name -> (restype, argtypes).  Every symbol of include/apg.h is listed here;
+# tests/test_abi.py checks the two stay in sync.
+SIGNATURES = {
+    "apg_abi_version": (C.c_int, []),
+    "apg_last_error": (C.c_char_p, []),
+    "apg_create": (C.c_int, [C.POINTER(apg_config), C.POINTER(_P)]),
+    "apg_destroy": (None, [_P]),
+    "apg_trim": (C.c_int, [_P]),
+    "apg_timing_get": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_double), _u64p, _u64p]),
+    "apg_timing_reset": (C.c_int, [_P]),
+    "apg_reads_upload": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(_P)]),
+    "apg_reads_free": (None, [_P]),
+    "apg_dreads_count": (C.c_uint64, [_P]),
+    "apg_byte_offsets": (C.c_int, [_u64p, C.c_uint64, _u64p]),
+    "apg_kmer_hash": (C.c_uint64, [C.c_int, C.c_uint64]),
+    "apg_kmer_unhash": (C.c_uint64, [C.c_int, C.c_uint64]),
+    "apg_kmer_spectrum": (C.c_int, [_P, C.POINTER(apg_reads), C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats)]),
+    "apg_kmer_spectrum_dev": (C.c_int, [_P, _P, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats)]),
+    "apg_kmer_count": (
+        C.c_int,
+        [_P, C.POINTER(apg_reads), C.c_int, C.POINTER(_u64p), C.POINTER(_u32p), _u64p, C.POINTER(apg_kstats)],
+    ),
+    "apg_free": (None, [_P]),
+    "apg_shard_bins": (C.c_int, [C.c_int, C.c_int]),
+    "apg_shard_count": (C.c_int, [_P, _P, C.c_int, C.c_int, _u64p]),
+    "apg_shard_scatter": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_void_p]),
+    "apg_shard_spectrum": (
+        C.c_int,
+        [_P, C.c_void_p, _u64p, C.c_int, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats)],
+    ),
+    "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
+    "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
+    "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),
+    "apg_fastb_write": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
+    "apg_qualb_write": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
+    "apg_fastb_read": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
+    "apg_qualb_read": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
+    "apg_reads_release": (None, [C.POINTER(apg_reads)]),
+    "apg_kspec_write": (C.c_int, [C.c_char_p, C.c_int, _u64p, C.c_size_t]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libapg.so (once).  Raises if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"libapg.so not found at {LIB_PATH}: build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)"
+                )
+            handle = C.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def check(rc: int, where: str) -> None:
+    if rc != APG_OK:
+        msg = lib().apg_last_error()
+        raise ApgError(rc, where, msg.decode() if msg else "")

@@ -1,0 +1,266 @@
+// apg_core.cpp — context lifecycle, errors, workspaces, kernel timing, uploads.
+#include "apg_core.hpp"
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+namespace apg {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* get_error() { return g_err.c_str(); }
+
+int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
+  auto& b = ctx->ws[name];
+  if (b.bytes < bytes) {
+    if (b.p) APG_CHECK_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    // Grow by 1/8 headroom so steadily growing calls do not realloc each time.
+    size_t want = bytes + bytes / 8;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      want = bytes;
+      e = hipMalloc(&b.p, want);
+    }
+    if (e != hipSuccess) {
+      b.p = nullptr;
+      set_error(std::string("hipMalloc(") + std::to_string(bytes) + ") for workspace '" + name +
+                "' failed: " + hipGetErrorString(e));
+      return APG_E_HIP;
+    }
+    b.bytes = want;
+  }
+  *out = b.p;
+  return APG_OK;
+}
+
+static hipEvent_t take_event(apg_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes) {
+  if (!ctx->timing) return;
+  apg_ctx::Pending p;
+  p.name = name;
+  p.bytes = bytes;
+  p.a = take_event(ctx);
+  p.b = take_event(ctx);
+  (void)hipEventRecord(p.a, ctx->stream);
+  ctx->pending.push_back(p);
+}
+
+void kend(apg_ctx* ctx) {
+  if (!ctx->timing || ctx->pending.empty()) return;
+  (void)hipEventRecord(ctx->pending.back().b, ctx->stream);
+}
+
+int kflush(apg_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    float ms = 0;
+    APG_CHECK_HIP(hipEventSynchronize(p.b));
+    APG_CHECK_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    auto it = ctx->kstats.find(p.name);
+    if (it == ctx->kstats.end()) {
+      ctx->korder.push_back(p.name);
+      it = ctx->kstats.emplace(p.name, KernelStat{}).first;
+    }
+    it->second.ms += ms;
+    it->second.launches += 1;
+    it->second.bytes += p.bytes;
+    ctx->event_pool.push_back(p.a);
+    ctx->event_pool.push_back(p.b);
+  }
+  ctx->pending.clear();
+  return APG_OK;
+}
+
+int sync(apg_ctx* ctx) {
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  APG_CHECK_HIP(hipGetLastError());
+  return kflush(ctx);
+}
+
+}  // namespace apg
+
+using namespace apg;
+
+extern "C" {
+
+int apg_abi_version(void) { return APG_ABI_VERSION; }
+const char* apg_last_error(void) { return get_error(); }
+
+int apg_create(const apg_config* cfg, apg_ctx** out) {
+  APG_REQUIRE(out != nullptr, "apg_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) {
+    set_error(std::string("apg_create: no HIP device available (") +
+              (e != hipSuccess ? hipGetErrorString(e) : "0 devices") + ")");
+    return APG_E_HIP;
+  }
+  const int dev = cfg ? cfg->device : 0;
+  APG_REQUIRE(dev >= 0 && dev < ndev, "apg_create: device ordinal out of range");
+  APG_CHECK_HIP(hipSetDevice(dev));
+  apg_ctx* ctx = new (std::nothrow) apg_ctx();
+  if (!ctx) return APG_E_NOMEM;
+  ctx->device = dev;
+  ctx->timing = cfg && cfg->timing;
+  ctx->verbose = cfg && cfg->verbose;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
+  if (ctx->n_cu <= 0) ctx->n_cu = 256;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    set_error("apg_create: hipStreamCreate failed");
+    return APG_E_HIP;
+  }
+  *out = ctx;
+  return APG_OK;
+}
+
+int apg_trim(apg_ctx* ctx) {
+  APG_REQUIRE(ctx, "apg_trim: ctx is NULL");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& kv : ctx->ws)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  ctx->ws.clear();
+  return APG_OK;
+}
+
+void apg_destroy(apg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->ws)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  for (auto& p : ctx->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int apg_timing_get(apg_ctx* ctx, int idx, char* name, size_t name_len, double* total_ms,
+                   uint64_t* launches, uint64_t* bytes) {
+  APG_REQUIRE(ctx, "apg_timing_get: ctx is NULL");
+  APG_TRY(kflush(ctx));
+  if (idx < 0 || idx >= (int)ctx->korder.size()) return APG_E_ARG;
+  const std::string& n = ctx->korder[idx];
+  const KernelStat& s = ctx->kstats[n];
+  if (name && name_len) {
+    std::strncpy(name, n.c_str(), name_len - 1);
+    name[name_len - 1] = 0;
+  }
+  if (total_ms) *total_ms = s.ms;
+  if (launches) *launches = s.launches;
+  if (bytes) *bytes = s.bytes;
+  return APG_OK;
+}
+
+int apg_timing_reset(apg_ctx* ctx) {
+  APG_REQUIRE(ctx, "apg_timing_reset: ctx is NULL");
+  APG_TRY(kflush(ctx));
+  ctx->korder.clear();
+  ctx->kstats.clear();
+  return APG_OK;
+}
+
+int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_off) {
+  APG_REQUIRE(base_off && byte_off, "apg_byte_offsets: NULL pointer");
+  byte_off[0] = 0;
+  for (uint64_t i = 0; i < n_reads; ++i) {
+    APG_REQUIRE(base_off[i + 1] >= base_off[i], "apg_byte_offsets: base_off not monotone");
+    byte_off[i + 1] = byte_off[i] + (base_off[i + 1] - base_off[i] + 3) / 4;
+  }
+  return APG_OK;
+}
+
+int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
+  APG_REQUIRE(ctx && r && out, "apg_reads_upload: NULL argument");
+  APG_REQUIRE(r->n_reads == 0 || (r->base_off && r->byte_off && r->packed),
+              "apg_reads_upload: missing base_off/byte_off/packed");
+  *out = nullptr;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  auto* d = new (std::nothrow) apg_dreads();
+  if (!d) return APG_E_NOMEM;
+  d->ctx = ctx;
+  static std::atomic<uint64_t> g_gen{1};
+  d->gen = g_gen.fetch_add(1);
+  const uint64_t n = r->n_reads;
+  d->n_reads = n;
+  d->h_base_off.assign(r->base_off ? r->base_off : nullptr, r->base_off ? r->base_off + n + 1 : nullptr);
+  if (d->h_base_off.empty()) d->h_base_off.push_back(0);
+  d->n_bases = d->h_base_off[n] - d->h_base_off[0];
+  d->n_bytes = n ? r->byte_off[n] : 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t len = r->base_off[i + 1] - r->base_off[i];
+    if ((r->byte_off[i + 1] - r->byte_off[i]) * 4 < len) {
+      delete d;
+      set_error("apg_reads_upload: byte_off inconsistent with base_off (read " + std::to_string(i) + ")");
+      return APG_E_ARG;
+    }
+    if (len > d->max_len) d->max_len = len;
+  }
+  auto fail = [&](hipError_t e) {
+    set_error(std::string("apg_reads_upload: ") + hipGetErrorString(e));
+    apg_reads_free(d);
+    return APG_E_HIP;
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&d->d_base_off, (n + 1) * 8)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&d->d_byte_off, (n + 1) * 8)) != hipSuccess) return fail(e);
+  // +16 bytes of slack: kernels may issue aligned 4/16-byte loads past the end.
+  if ((e = hipMalloc(&d->d_packed, d->n_bytes + 64)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(d->d_packed, 0, d->n_bytes + 64, ctx->stream)) != hipSuccess) return fail(e);
+  if (n) {
+    if ((e = hipMemcpyAsync(d->d_base_off, r->base_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+      return fail(e);
+    if ((e = hipMemcpyAsync(d->d_byte_off, r->byte_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+      return fail(e);
+    if ((e = hipMemcpyAsync(d->d_packed, r->packed, d->n_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+      return fail(e);
+  } else {
+    uint64_t z = 0;
+    if ((e = hipMemcpyAsync(d->d_base_off, &z, 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(d->d_byte_off, &z, 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return fail(e);
+  }
+  if (r->quals && n) {
+    if ((e = hipMalloc(&d->d_quals, d->h_base_off[n] + 64)) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(d->d_quals, r->quals, d->h_base_off[n], hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+      return fail(e);
+  }
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail(e);
+  *out = d;
+  return APG_OK;
+}
+
+void apg_reads_free(apg_dreads* d) {
+  if (!d) return;
+  if (d->ctx) (void)hipSetDevice(d->ctx->device);
+  if (d->d_base_off) (void)hipFree(d->d_base_off);
+  if (d->d_byte_off) (void)hipFree(d->d_byte_off);
+  if (d->d_packed) (void)hipFree(d->d_packed);
+  if (d->d_quals) (void)hipFree(d->d_quals);
+  delete d;
+}
+
+uint64_t apg_dreads_count(const apg_dreads* d) { return d ? d->n_reads : 0; }
+
+void apg_free(void* p) { std::free(p); }
+
+}  // extern "C"

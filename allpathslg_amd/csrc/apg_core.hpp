@@ -1,0 +1,138 @@
+// apg_core.hpp — internal context, error and workspace plumbing of libapg.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/apg.h"
+
+namespace apg {
+
+// Thread-local last-error message behind apg_last_error().
+void set_error(const std::string& msg);
+const char* get_error();
+
+struct Status {
+  int code;
+};
+
+#define APG_CHECK_HIP(expr)                                                       \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      ::apg::set_error(std::string(#expr " failed: ") + hipGetErrorString(_e) +   \
+                       " (" __FILE__ ":" + std::to_string(__LINE__) + ")");     \
+      return APG_E_HIP;                                                           \
+    }                                                                             \
+  } while (0)
+
+#define APG_TRY(expr)            \
+  do {                           \
+    int _rc = (expr);            \
+    if (_rc != APG_OK) return _rc; \
+  } while (0)
+
+#define APG_REQUIRE(cond, msg)              \
+  do {                                      \
+    if (!(cond)) {                          \
+      ::apg::set_error(std::string(msg));   \
+      return APG_E_ARG;                     \
+    }                                       \
+  } while (0)
+
+struct KernelStat {
+  double ms = 0;
+  uint64_t launches = 0;
+  uint64_t bytes = 0;
+};
+
+}  // namespace apg
+
+// Device-resident read set.
+struct apg_dreads {
+  apg_ctx* ctx = nullptr;
+  uint64_t gen = 0;  // unique per upload (cache key for per-read-set plans)
+  uint64_t n_reads = 0;
+  uint64_t n_bases = 0;
+  uint64_t n_bytes = 0;
+  uint64_t max_len = 0;
+  uint64_t* d_base_off = nullptr;  // n+1
+  uint64_t* d_byte_off = nullptr;  // n+1
+  uint8_t* d_packed = nullptr;
+  uint8_t* d_quals = nullptr;      // optional
+  std::vector<uint64_t> h_base_off;  // kept for host-side sizing
+};
+
+struct apg_ctx {
+  int device = 0;
+  bool timing = false;
+  bool verbose = false;
+  hipStream_t stream = nullptr;
+  int n_cu = 0;
+
+  // Grow-only named device workspaces.
+  struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<std::string, Buf> ws;
+
+  // Per-kernel timing.
+  std::vector<std::string> korder;
+  std::map<std::string, apg::KernelStat> kstats;
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+    uint64_t bytes;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+
+  // Stage-A plan of the last extract_count (reused by extract_scatter).
+  struct XState {
+    bool valid = false;
+    uint64_t gen = 0;
+    int K = 0, P = 0, dshift = 0;
+    uint32_t G = 0, ndig = 0;
+    uint64_t total = 0;
+  } xstate;
+};
+
+namespace apg {
+
+// Device workspace `name` of at least `bytes`; contents are undefined.
+int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out);
+template <typename T>
+int workspace_t(apg_ctx* ctx, const char* name, size_t count, T** out) {
+  void* p = nullptr;
+  int rc = workspace(ctx, name, count * sizeof(T) + 16, &p);
+  *out = static_cast<T*>(p);
+  return rc;
+}
+
+// Bracket a launch with timing events when ctx->timing.
+void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes);
+void kend(apg_ctx* ctx);
+// Resolve pending events into kstats (call after a stream sync).
+int kflush(apg_ctx* ctx);
+int sync(apg_ctx* ctx);
+
+inline void vlog(apg_ctx* ctx, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+}  // namespace apg
+
+#include <cstdarg>
+inline void apg::vlog(apg_ctx* ctx, const char* fmt, ...) {
+  if (!ctx || !ctx->verbose) return;
+  va_list ap;
+  va_start(ap, fmt);
+  std::fputs("[apg] ", stderr);
+  std::vfprintf(stderr, fmt, ap);
+  std::fputc('\n', stderr);
+  va_end(ap);
+}

@@ -1,0 +1,225 @@
+// apg_formats.cpp — read/write the on-disk read formats.
+//
+// "APG-fastb v0" / "APG-qualb v0" carry the same content as ALLPATHS-LG's
+// feudal vecbasevector (.fastb) / vecqualvector (.qualb) ([R:M] src/feudal/,
+// src/Basevector.h, src/Qualvector.h).  The feudal byte layout itself is
+// unpinned (reference absent), so the header is versioned: a feudal-compatible
+// v1 reader can be added without touching callers.
+//
+//   offset  size            field
+//   0       8               magic "APGFB\0\0\0" | "APGQB\0\0\0"
+//   8       4               version (0)
+//   12      4               reserved (0)
+//   16      8               n_reads
+//   24      8               total_bases
+//   32      8*(n_reads+1)   base_off (read i = bases [base_off[i], base_off[i+1]))
+//   ...     payload         fastb: packed 2-bit bases, each read byte-aligned
+//                           (byte_off[i] = sum_{j<i} ceil(len_j/4));
+//                           qualb: one Phred byte per base
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/apg.h"
+
+namespace apg {
+void set_error(const std::string& msg);
+}
+
+namespace {
+
+const char kFastbMagic[8] = {'A', 'P', 'G', 'F', 'B', 0, 0, 0};
+const char kQualbMagic[8] = {'A', 'P', 'G', 'Q', 'B', 0, 0, 0};
+
+struct File {
+  FILE* f = nullptr;
+  ~File() {
+    if (f) std::fclose(f);
+  }
+};
+
+int io_fail(const std::string& what) {
+  apg::set_error(what);
+  return APG_E_IO;
+}
+
+int write_common(const char* path, const char* magic, const apg_reads* r, const void* payload,
+                 uint64_t payload_bytes) {
+  if (!path || !r) return APG_E_ARG;
+  const uint64_t n = r->n_reads;
+  if (n && !r->base_off) return APG_E_ARG;
+  const std::string tmp = std::string(path) + ".tmp";
+  File fh;
+  fh.f = std::fopen(tmp.c_str(), "wb");
+  if (!fh.f) return io_fail("cannot open " + tmp + " for writing");
+  const uint32_t ver = 0, res = 0;
+  const uint64_t zero = 0;
+  const uint64_t total = n ? r->base_off[n] - r->base_off[0] : 0;
+  bool ok = std::fwrite(magic, 1, 8, fh.f) == 8 && std::fwrite(&ver, 4, 1, fh.f) == 1 &&
+            std::fwrite(&res, 4, 1, fh.f) == 1 && std::fwrite(&n, 8, 1, fh.f) == 1 &&
+            std::fwrite(&total, 8, 1, fh.f) == 1;
+  if (ok) {
+    if (n) {
+      // Normalise so base_off[0] == 0 on disk.
+      std::vector<uint64_t> bo(r->base_off, r->base_off + n + 1);
+      const uint64_t b0 = bo[0];
+      for (auto& v : bo) v -= b0;
+      ok = std::fwrite(bo.data(), 8, n + 1, fh.f) == n + 1;
+    } else {
+      ok = std::fwrite(&zero, 8, 1, fh.f) == 1;
+    }
+  }
+  if (ok && payload_bytes) ok = std::fwrite(payload, 1, payload_bytes, fh.f) == payload_bytes;
+  if (!ok) return io_fail("short write to " + tmp);
+  if (std::fclose(fh.f) != 0) {
+    fh.f = nullptr;
+    return io_fail("close failed for " + tmp);
+  }
+  fh.f = nullptr;
+  // write-then-rename: a module killed mid-write never leaves a torn output.
+  if (std::rename(tmp.c_str(), path) != 0) return io_fail("rename " + tmp + " -> " + path + " failed");
+  return APG_OK;
+}
+
+int read_header(FILE* f, const char* magic, const char* path, uint64_t* n, uint64_t* total,
+                std::vector<uint64_t>* base_off) {
+  char m[8];
+  uint32_t ver = 0, res = 0;
+  if (std::fread(m, 1, 8, f) != 8 || std::memcmp(m, magic, 8) != 0)
+    return io_fail(std::string("bad magic in ") + path);
+  if (std::fread(&ver, 4, 1, f) != 1 || std::fread(&res, 4, 1, f) != 1 || ver != 0)
+    return io_fail(std::string("unsupported version in ") + path);
+  if (std::fread(n, 8, 1, f) != 1 || std::fread(total, 8, 1, f) != 1)
+    return io_fail(std::string("truncated header in ") + path);
+  if (*n > (1ull << 40)) return io_fail(std::string("implausible read count in ") + path);
+  base_off->resize(*n + 1);
+  if (std::fread(base_off->data(), 8, *n + 1, f) != *n + 1)
+    return io_fail(std::string("truncated offsets in ") + path);
+  if ((*base_off)[*n] != *total) return io_fail(std::string("offset table/total mismatch in ") + path);
+  for (uint64_t i = 0; i < *n; ++i)
+    if ((*base_off)[i + 1] < (*base_off)[i]) return io_fail(std::string("non-monotone offsets in ") + path);
+  return APG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int apg_fastb_write(const char* path, const apg_reads* r) {
+  if (!r) return APG_E_ARG;
+  const uint64_t bytes = r->n_reads ? r->byte_off[r->n_reads] - r->byte_off[0] : 0;
+  return write_common(path, kFastbMagic, r, r->n_reads ? r->packed + r->byte_off[0] : nullptr, bytes);
+}
+
+int apg_qualb_write(const char* path, const apg_reads* r) {
+  if (!r) return APG_E_ARG;
+  if (r->n_reads && !r->quals) return APG_E_ARG;
+  const uint64_t bytes = r->n_reads ? r->base_off[r->n_reads] - r->base_off[0] : 0;
+  return write_common(path, kQualbMagic, r, r->quals, bytes);
+}
+
+int apg_fastb_read(const char* path, apg_reads* out) {
+  if (!path || !out) return APG_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  File fh;
+  fh.f = std::fopen(path, "rb");
+  if (!fh.f) return io_fail(std::string("cannot open ") + path);
+  uint64_t n = 0, total = 0;
+  std::vector<uint64_t> bo;
+  int rc = read_header(fh.f, kFastbMagic, path, &n, &total, &bo);
+  if (rc) return rc;
+  auto* base_off = (uint64_t*)std::malloc((n + 1) * 8);
+  auto* byte_off = (uint64_t*)std::malloc((n + 1) * 8);
+  if (!base_off || !byte_off) {
+    std::free(base_off);
+    std::free(byte_off);
+    return APG_E_NOMEM;
+  }
+  std::memcpy(base_off, bo.data(), (n + 1) * 8);
+  apg_byte_offsets(base_off, n, byte_off);
+  const uint64_t bytes = byte_off[n];
+  auto* packed = (uint8_t*)std::malloc(bytes + 64);
+  if (!packed) {
+    std::free(base_off);
+    std::free(byte_off);
+    return APG_E_NOMEM;
+  }
+  if (bytes && std::fread(packed, 1, bytes, fh.f) != bytes) {
+    std::free(base_off);
+    std::free(byte_off);
+    std::free(packed);
+    return io_fail(std::string("truncated payload in ") + path);
+  }
+  std::memset(packed + bytes, 0, 64);
+  out->n_reads = n;
+  out->base_off = base_off;
+  out->byte_off = byte_off;
+  out->packed = packed;
+  out->quals = nullptr;
+  return APG_OK;
+}
+
+int apg_qualb_read(const char* path, apg_reads* io) {
+  if (!path || !io) return APG_E_ARG;
+  File fh;
+  fh.f = std::fopen(path, "rb");
+  if (!fh.f) return io_fail(std::string("cannot open ") + path);
+  uint64_t n = 0, total = 0;
+  std::vector<uint64_t> bo;
+  int rc = read_header(fh.f, kQualbMagic, path, &n, &total, &bo);
+  if (rc) return rc;
+  if (io->base_off) {
+    if (io->n_reads != n) return io_fail(std::string("qualb/fastb read count mismatch: ") + path);
+    for (uint64_t i = 0; i <= n; ++i)
+      if (io->base_off[i] - io->base_off[0] != bo[i])
+        return io_fail(std::string("qualb/fastb length mismatch: ") + path);
+  }
+  auto* q = (uint8_t*)std::malloc(total + 64);
+  if (!q) return APG_E_NOMEM;
+  if (total && std::fread(q, 1, total, fh.f) != total) {
+    std::free(q);
+    return io_fail(std::string("truncated payload in ") + path);
+  }
+  if (io->quals) std::free((void*)io->quals);
+  io->quals = q;
+  if (!io->base_off) {
+    auto* base_off = (uint64_t*)std::malloc((n + 1) * 8);
+    if (!base_off) return APG_E_NOMEM;
+    std::memcpy(base_off, bo.data(), (n + 1) * 8);
+    io->base_off = base_off;
+    io->n_reads = n;
+  }
+  return APG_OK;
+}
+
+void apg_reads_release(apg_reads* r) {
+  if (!r) return;
+  std::free((void*)r->base_off);
+  std::free((void*)r->byte_off);
+  std::free((void*)r->packed);
+  std::free((void*)r->quals);
+  std::memset(r, 0, sizeof(*r));
+}
+
+int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_len) {
+  if (!path || (!hist && hist_len)) return APG_E_ARG;
+  const std::string tmp = std::string(path) + ".tmp";
+  File fh;
+  fh.f = std::fopen(tmp.c_str(), "w");
+  if (!fh.f) return io_fail("cannot open " + tmp);
+  std::fprintf(fh.f, "# KmerSpectrum K=%d bins=%zu (last bin = count >= %zu)\n", K, hist_len,
+               hist_len ? hist_len - 1 : 0);
+  for (size_t m = 0; m < hist_len; ++m)
+    if (hist[m]) std::fprintf(fh.f, "%zu\t%llu\n", m, (unsigned long long)hist[m]);
+  if (std::fclose(fh.f) != 0) {
+    fh.f = nullptr;
+    return io_fail("close failed: " + tmp);
+  }
+  fh.f = nullptr;
+  if (std::rename(tmp.c_str(), path) != 0) return io_fail("rename failed: " + tmp);
+  return APG_OK;
+}
+
+}  // extern "C"

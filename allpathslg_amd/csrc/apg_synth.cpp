@@ -1,0 +1,167 @@
+// apg_synth.cpp — deterministic synthetic genome + paired-read simulator
+// (SURVEY.md §B).  Stands in for PrepareAllPathsInputs' real data, which is not
+// in the container.  Host-only; every pair is generated from its own
+// xoshiro256** stream seeded by (seed, pair index), so any rank regenerates any
+// slice without coordination and results do not depend on the thread count.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/apg.h"
+
+namespace {
+
+inline uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+struct Xoshiro256ss {
+  uint64_t s[4];
+  explicit Xoshiro256ss(uint64_t seed) {
+    uint64_t t = seed;
+    for (auto& v : s) v = splitmix64(t);
+  }
+  static inline uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+  inline uint64_t next() {
+    const uint64_t r = rotl(s[1] * 5, 7) * 9;
+    const uint64_t t = s[1] << 17;
+    s[2] ^= s[0];
+    s[3] ^= s[1];
+    s[1] ^= s[2];
+    s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = rotl(s[3], 45);
+    return r;
+  }
+  // Uniform double in [0, 1) from the top 53 bits.
+  inline double uniform() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
+  // Uniform integer in [0, n) (n > 0), multiply-shift (bias < 2^-64 * n).
+  inline uint64_t below(uint64_t n) { return (uint64_t)(((__uint128_t)next() * n) >> 64); }
+  inline double gaussian() {
+    double u1 = uniform();
+    double u2 = uniform();
+    if (u1 < 1e-300) u1 = 1e-300;
+    return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+  }
+};
+
+constexpr uint64_t kGenomeBlock = 1ull << 20;
+
+inline uint64_t stream_seed(uint64_t seed, uint64_t salt, uint64_t idx) {
+  uint64_t t = seed ^ (salt * 0xd1b54a32d192ed03ull);
+  t += idx * 0x9e3779b97f4a7c15ull;
+  return splitmix64(t);
+}
+
+unsigned n_threads(uint32_t want) {
+  unsigned hw = std::thread::hardware_concurrency();
+  if (hw == 0) hw = 4;
+  unsigned t = want ? want : hw;
+  return std::max(1u, std::min(t, 64u));
+}
+
+template <typename F>
+void parallel_for(uint64_t n, unsigned threads, F f) {
+  if (n == 0) return;
+  threads = (unsigned)std::min<uint64_t>(threads, n);
+  if (threads <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  const uint64_t chunk = (n + threads - 1) / threads;
+  for (unsigned t = 0; t < threads; ++t) {
+    uint64_t a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    ts.emplace_back([=] { f(a, b); });
+  }
+  for (auto& th : ts) th.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int apg_synth_genome(uint64_t genome_len, uint64_t seed, uint8_t* out) {
+  if (!out && genome_len) return APG_E_ARG;
+  const uint64_t nblocks = (genome_len + kGenomeBlock - 1) / kGenomeBlock;
+  parallel_for(nblocks, n_threads(0), [&](uint64_t a, uint64_t b) {
+    for (uint64_t blk = a; blk < b; ++blk) {
+      Xoshiro256ss rng(stream_seed(seed, 1, blk));
+      const uint64_t s = blk * kGenomeBlock, e = std::min(genome_len, s + kGenomeBlock);
+      for (uint64_t i = s; i < e; i += 32) {
+        uint64_t w = rng.next();
+        for (uint64_t j = i; j < std::min(e, i + 32); ++j, w >>= 2) out[j] = (uint8_t)(w & 3);
+      }
+    }
+  });
+  return APG_OK;
+}
+
+int apg_synth_sizes(const apg_synth_params* p, uint64_t* n_reads, uint64_t* n_bases,
+                    uint64_t* n_packed_bytes) {
+  if (!p) return APG_E_ARG;
+  const uint64_t nr = 2 * p->n_pairs;
+  if (n_reads) *n_reads = nr;
+  if (n_bases) *n_bases = nr * p->read_len;
+  if (n_packed_bytes) *n_packed_bytes = nr * ((p->read_len + 3) / 4);
+  return APG_OK;
+}
+
+int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome, uint64_t* base_off,
+                    uint64_t* byte_off, uint8_t* packed, uint8_t* quals) {
+  if (!p || !genome || !base_off || !byte_off || !packed) return APG_E_ARG;
+  const uint64_t L = p->read_len, G = p->genome_len;
+  if (L == 0 || G < L) return APG_E_ARG;
+  const uint64_t rb = (L + 3) / 4;
+  const uint64_t nr = 2 * p->n_pairs;
+  for (uint64_t i = 0; i <= nr; ++i) {
+    base_off[i] = i * L;
+    byte_off[i] = i * rb;
+  }
+  const double lo = p->err_lo, hi = p->err_hi;
+  parallel_for(p->n_pairs, n_threads(p->threads), [&](uint64_t a, uint64_t b) {
+    std::vector<uint8_t> r1(L), r2(L), q1(L), q2(L);
+    for (uint64_t k = a; k < b; ++k) {
+      Xoshiro256ss rng(stream_seed(p->seed, 2, p->first_pair + k));
+      // Fragment length ~ N(mean, sd), clamped to [L, min(G, 10*mean + L)].
+      double f = p->insert_mean + p->insert_sd * rng.gaussian();
+      uint64_t flen = (uint64_t)std::llround(std::max<double>(f, (double)L));
+      flen = std::min<uint64_t>(flen, std::min<uint64_t>(G, 10ull * p->insert_mean + L));
+      const uint64_t start = rng.below(G - flen + 1);
+      const bool flip = rng.next() & 1;  // fragment from the reverse strand
+      // FR pair: read A = forward of [start, start+L), read B = rc of [start+flen-L, start+flen).
+      for (uint64_t i = 0; i < L; ++i) {
+        r1[i] = genome[start + i];
+        r2[i] = (uint8_t)(3 - genome[start + flen - 1 - i]);
+      }
+      if (flip) std::swap(r1, r2);
+      for (int rd = 0; rd < 2; ++rd) {
+        auto& r = rd ? r2 : r1;
+        auto& q = rd ? q2 : q1;
+        for (uint64_t i = 0; i < L; ++i) {
+          const double e = L > 1 ? lo + (hi - lo) * (double)i / (double)(L - 1) : lo;
+          if (rng.uniform() < e) {
+            r[i] = (uint8_t)((r[i] + 1 + rng.below(3)) & 3);
+            q[i] = (uint8_t)(2 + rng.below(19));
+          } else {
+            q[i] = 40;
+          }
+        }
+        const uint64_t ridx = 2 * k + rd;
+        uint8_t* dst = packed + ridx * rb;
+        std::memset(dst, 0, rb);
+        for (uint64_t i = 0; i < L; ++i) dst[i >> 2] |= (uint8_t)(r[i] << (2 * (i & 3)));
+        if (quals) std::memcpy(quals + ridx * L, q.data(), L);
+      }
+    }
+  });
+  return APG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+"""Multi-GPU k-mer spectrum: one process per GPU, canonical k-mers
+hash-partitioned across ranks.
+
+  rank r:  local reads --shard_count/shard_scatter--> records grouped by
+           (owner shard, L1 group)
+           all_to_all(count matrix)        (P x B u64 per rank)
+           all_to_all(records)             (the one real exchange; RCCL/xGMI)
+           shard_spectrum(received)        (this shard's distinct k-mers)
+           all_reduce(spectrum)            (<= 64 Ki u64)
+
+torch.distributed is plumbing here (device buffers + collectives; backend
+"nccl" is RCCL on ROCm, "gloo" on CPU for tests); all k-mer compute is in
+libapg.  `backend` is any object with shard_count / shard_scatter /
+shard_spectrum taking torch tensors — `HipShardBackend` in production; the
+CPU tests plug in an oracle-backed one to exercise the exchange logic.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .engine import DEFAULT_HIST_LEN, Context, DeviceReads, shard_bins
+
+
+class HipShardBackend:
+    """libapg's sharded stages on this rank's GPU."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.device = torch.device("cuda", ctx.device)
+
+    def alloc(self, n: int) -> torch.Tensor:
+        return torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+
+    def shard_count(self, dreads: DeviceReads, K: int, P: int) -> np.ndarray:
+        return self.ctx.shard_count(dreads, K, P)
+
+    def shard_scatter(self, dreads: DeviceReads, K: int, P: int, send: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)  # libapg runs on its own stream
+        self.ctx.shard_scatter(dreads, K, P, send.data_ptr())
+
+    def shard_spectrum(self, recv: torch.Tensor, recv_counts: np.ndarray, K: int, P: int, hist_len: int):
+        torch.cuda.synchronize(self.device)
+        return self.ctx.shard_spectrum(recv.data_ptr(), recv_counts, K, P, hist_len)
+
+
+def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
+                     group: Optional[dist.ProcessGroup] = None) -> Tuple[np.ndarray, dict]:
+    """Global spectrum of the union of every rank's reads.  Returns the same
+    (hist, stats) on every rank; stats are summed over ranks."""
+    P = dist.get_world_size(group)
+    if P & (P - 1):
+        raise ValueError(f"world size {P} must be a power of two (k-mer hash shards)")
+    B = shard_bins(K, P)
+    dev = backend.alloc(1).device
+    counts = backend.shard_count(reads, K, P)  # [dest * B + l1]
+    send = backend.alloc(int(counts.sum()))
+    backend.shard_scatter(reads, K, P, send)
+
+    cnt_t = torch.from_numpy(counts.astype(np.int64)).to(dev)
+    recv_cnt_t = torch.empty_like(cnt_t)
+    dist.all_to_all_single(recv_cnt_t, cnt_t, group=group)  # equal splits of B
+    recv_counts = recv_cnt_t.cpu().numpy().astype(np.uint64)  # [src * B + l1]
+
+    in_splits = counts.reshape(P, B).sum(axis=1).astype(np.int64).tolist()
+    out_splits = recv_counts.reshape(P, B).sum(axis=1).astype(np.int64).tolist()
+    recv = backend.alloc(int(sum(out_splits)))
+    n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
+    dist.all_to_all_single(recv[:n_out] if n_out else recv[:0], send[:n_in] if n_in else send[:0],
+                           out_splits, in_splits, group=group)
+
+    hist, st = backend.shard_spectrum(recv, recv_counts, K, P, hist_len)
+    hist_t = torch.from_numpy(hist.astype(np.int64)).to(dev)
+    dist.all_reduce(hist_t, group=group)
+    keys = ["n_kmers", "n_distinct", "n_overflow"]
+    st_t = torch.tensor([int(st[k]) for k in keys], dtype=torch.int64, device=dev)
+    dist.all_reduce(st_t, group=group)
+    out = dict(st)
+    out.update({k: int(v) for k, v in zip(keys, st_t.cpu().tolist())})
+    out["n_shards"] = P
+    out["records_sent"] = n_in
+    out["records_received"] = n_out
+    return hist_t.cpu().numpy().astype(np.uint64), out

@@ -1,0 +1,179 @@
+"""Python face of libapg: a device context and the k-mer operations.
+
+Mirrors the reference's module operations ([R:M] KmerSpectrum / naif_kmerize /
+KernelKmerStorer): same argument meaning (K, histogram length), same error
+behaviour (an exception where the module would FatalErr and exit non-zero).
+All compute runs in libapg's HIP kernels; nothing here computes k-mers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from ._lib import apg_config, apg_kstats, check, lib
+from .reads import ReadSet
+
+_u64p = C.POINTER(C.c_uint64)
+_u32p = C.POINTER(C.c_uint32)
+
+DEFAULT_HIST_LEN = 1 << 16  # bins 0..65535, last bin = count >= 65535
+
+
+def kmer_hash(K: int, canonical: int) -> int:
+    return int(lib().apg_kmer_hash(K, canonical))
+
+
+def kmer_unhash(K: int, h: int) -> int:
+    return int(lib().apg_kmer_unhash(K, h))
+
+
+def shard_bins(K: int, n_shards: int) -> int:
+    b = lib().apg_shard_bins(K, n_shards)
+    check(0 if b > 0 else b, "apg_shard_bins")
+    return int(b)
+
+
+class DeviceReads:
+    """A read set resident in HBM (apg_dreads)."""
+
+    def __init__(self, ctx: "Context", reads: ReadSet):
+        self.ctx = ctx
+        self.reads = reads
+        self._h = C.c_void_p()
+        r = reads.c_struct()
+        check(lib().apg_reads_upload(ctx.handle, C.byref(r), C.byref(self._h)), "apg_reads_upload")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def free(self):
+        if self._h:
+            lib().apg_reads_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """One HIP device + stream (apg_ctx).  One per host thread."""
+
+    def __init__(self, device: int = 0, timing: bool = False, verbose: bool = False):
+        cfg = apg_config()
+        cfg.device = device
+        cfg.timing = int(timing)
+        cfg.verbose = int(verbose)
+        self._h = C.c_void_p()
+        check(lib().apg_create(C.byref(cfg), C.byref(self._h)), "apg_create")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().apg_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- timing ------------------------------------------------------------
+    def kernel_times(self) -> Dict[str, Tuple[float, int, int]]:
+        """name -> (total_ms, launches, algorithmic_bytes)."""
+        out = {}
+        L = lib()
+        i = 0
+        name = C.create_string_buffer(128)
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_uint64()
+        while L.apg_timing_get(self._h, i, name, 128, C.byref(ms), C.byref(n), C.byref(b)) == 0:
+            out[name.value.decode()] = (ms.value, int(n.value), int(b.value))
+            i += 1
+        return out
+
+    def reset_timing(self):
+        check(lib().apg_timing_reset(self._h), "apg_timing_reset")
+
+    def trim(self):
+        check(lib().apg_trim(self._h), "apg_trim")
+
+    # -- k-mers --------------------------------------------------------------
+    def upload(self, reads: ReadSet) -> DeviceReads:
+        return DeviceReads(self, reads)
+
+    def kmer_spectrum(self, reads, K: int, hist_len: int = DEFAULT_HIST_LEN):
+        """Spectrum h[m] of canonical K-mers (K <= 32).  `reads` is a ReadSet
+        (host; includes H2D) or DeviceReads (HBM-resident).  Returns
+        (hist, stats)."""
+        hist = np.zeros(hist_len, dtype=np.uint64)
+        st = apg_kstats()
+        L = lib()
+        if isinstance(reads, DeviceReads):
+            rc = L.apg_kmer_spectrum_dev(self._h, reads.handle, K, hist.ctypes.data_as(_u64p), hist_len, C.byref(st))
+        else:
+            r = reads.c_struct()
+            rc = L.apg_kmer_spectrum(self._h, C.byref(r), K, hist.ctypes.data_as(_u64p), hist_len, C.byref(st))
+        check(rc, "apg_kmer_spectrum")
+        return hist, st.as_dict()
+
+    def kmer_count(self, reads: ReadSet, K: int):
+        """(keys, counts, stats): distinct canonical K-mers in ascending
+        kmer_hash order and their multiplicities."""
+        L = lib()
+        r = reads.c_struct()
+        kp, cp = _u64p(), _u32p()
+        nd = C.c_uint64()
+        st = apg_kstats()
+        check(L.apg_kmer_count(self._h, C.byref(r), K, C.byref(kp), C.byref(cp), C.byref(nd), C.byref(st)),
+              "apg_kmer_count")
+        try:
+            n = int(nd.value)
+            keys = np.ctypeslib.as_array(kp, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
+            counts = np.ctypeslib.as_array(cp, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+        finally:
+            L.apg_free(C.cast(kp, C.c_void_p))
+            L.apg_free(C.cast(cp, C.c_void_p))
+        return keys, counts, st.as_dict()
+
+    # -- sharded (multi-GPU) stages ------------------------------------------
+    def shard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
+        B = shard_bins(K, n_shards)
+        counts = np.zeros(n_shards * B, dtype=np.uint64)
+        check(lib().apg_shard_count(self._h, dreads.handle, K, n_shards, counts.ctypes.data_as(_u64p)),
+              "apg_shard_count")
+        return counts
+
+    def shard_scatter(self, dreads: DeviceReads, K: int, n_shards: int, d_send_ptr: int) -> None:
+        check(lib().apg_shard_scatter(self._h, dreads.handle, K, n_shards, C.c_void_p(d_send_ptr)),
+              "apg_shard_scatter")
+
+    def shard_spectrum(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int,
+                       hist_len: int = DEFAULT_HIST_LEN):
+        rc_arr = np.ascontiguousarray(recv_counts, dtype=np.uint64)
+        hist = np.zeros(hist_len, dtype=np.uint64)
+        st = apg_kstats()
+        check(lib().apg_shard_spectrum(self._h, C.c_void_p(d_recv_ptr), rc_arr.ctypes.data_as(_u64p), K, n_shards,
+                                       hist.ctypes.data_as(_u64p), hist_len, C.byref(st)),
+              "apg_shard_spectrum")
+        return hist, st.as_dict()
+
+
+def write_kspec(path: str, K: int, hist: np.ndarray) -> None:
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    check(lib().apg_kspec_write(path.encode(), K, h.ctypes.data_as(_u64p), len(h)), "apg_kspec_write")

@@ -1,0 +1,199 @@
+/*
+ * apg.h — C ABI of libapg, the MI355X-native k-mer spectrum / correction /
+ * unipath engine that stands in for ALLPATHS-LG's first-third pipeline modules.
+ *
+ * Boundary.  ALLPATHS-LG has no in-process plugin API: every
+ * module is an executable driven by RunAllPathsLG with KEY=VALUE arguments,
+ * exchanging .fastb/.qualb/... files in the RUN directory.  The reference
+ * snapshot mounted for this project is EMPTY, so no file:line
+ * exists to cite; each entry point below names the *recalled* module/function
+ * it replaces ([R:M] = recalled, medium confidence — grep targets for when the
+ * source appears).  The drop-in CLIs under tools/ call exactly these entries.
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no C++/torch types, no exceptions.
+ *   - every function returns int: 0 = APG_OK, < 0 = APG_E_*; the message of the
+ *     last failure on the calling thread is apg_last_error().
+ *   - one context per host thread; a context owns one HIP device and stream.
+ *   - calls are synchronous: when they return, outputs are complete.
+ *   - "_dev" entry points take device-resident inputs (HBM) and are what the
+ *     benchmark times; the plain forms take host buffers and include H2D/D2H.
+ */
+#ifndef APG_H
+#define APG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define APG_ABI_VERSION 1
+
+enum {
+  APG_OK = 0,
+  APG_E_ARG = -1,      /* bad argument (null pointer, K out of range, ...) */
+  APG_E_HIP = -2,      /* HIP runtime failure (no device, OOM, launch error) */
+  APG_E_IO = -3,       /* file open/read/write failure or bad magic */
+  APG_E_STATE = -4,    /* call out of order (e.g. table not built) */
+  APG_E_NOMEM = -5,    /* host allocation failure */
+  APG_E_UNSUPPORTED = -6
+};
+
+/* ------------------------------------------------------------------------- */
+/* Context                                                                    */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_ctx apg_ctx;
+
+typedef struct apg_config {
+  int32_t device;   /* HIP device ordinal */
+  int32_t timing;   /* 1 = record per-kernel HIP-event durations */
+  int32_t verbose;  /* 1 = stage log lines on stderr */
+  int32_t reserved0;
+  uint64_t reserved[6];
+} apg_config;
+
+int apg_abi_version(void);
+const char* apg_last_error(void);
+int apg_create(const apg_config* cfg, apg_ctx** out);
+void apg_destroy(apg_ctx* ctx);
+/* Release every cached device workspace of the context. */
+int apg_trim(apg_ctx* ctx);
+
+/* Per-kernel timing (cfg.timing = 1).  idx enumerates kernels seen so far;
+ * returns APG_E_ARG past the end.  bytes = algorithmic HBM bytes (inputs read
+ * once + outputs written once) summed over the launches. */
+int apg_timing_get(apg_ctx* ctx, int idx, char* name, size_t name_len,
+                   double* total_ms, uint64_t* launches, uint64_t* bytes);
+int apg_timing_reset(apg_ctx* ctx);
+
+/* ------------------------------------------------------------------------- */
+/* Read sets (replaces vecbasevector / vecqualvector in memory;              */
+/* [R:M] src/Basevector.h, src/Qualvector.h, src/feudal/)                    */
+/*                                                                            */
+/* Bases are 2-bit coded A=0 C=1 G=2 T=3, 4 per byte, base i of a read at     */
+/* bits 2*(i%4) of byte i/4 (LSB first).  Every read starts on a byte         */
+/* boundary: byte_off[i] = sum_{j<i} ceil(len_j/4).                           */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_reads {
+  uint64_t n_reads;
+  const uint64_t* base_off; /* n_reads+1: read i = bases [base_off[i], base_off[i+1]) */
+  const uint64_t* byte_off; /* n_reads+1: packed bytes of read i start at byte_off[i] */
+  const uint8_t* packed;    /* byte_off[n_reads] bytes */
+  const uint8_t* quals;     /* optional: base_off[n_reads] Phred bytes, or NULL */
+} apg_reads;
+
+/* Device-resident copy of a read set. */
+typedef struct apg_dreads apg_dreads;
+int apg_reads_upload(apg_ctx* ctx, const apg_reads* reads, apg_dreads** out);
+void apg_reads_free(apg_dreads* dr);
+uint64_t apg_dreads_count(const apg_dreads* dr);
+
+/* Fill byte_off[0..n] from base_off[0..n]. */
+int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_off);
+
+/* ------------------------------------------------------------------------- */
+/* K-mer counting and spectrum, K <= 32                                       */
+/* Replaces: naif_kmerize + KernelKmerStorer ([R:M] src/kmers/naif_kmer/)     */
+/* and KmerSpectrum ([R:M] src/kmers/KmerSpectra.h), module KmerSpectrum.     */
+/*                                                                            */
+/* Canonical k-mer = min(fw, rc) with fw = sum b[i+j]*4^(K-1-j). */
+/* Table order: ascending apg_kmer_hash(K, canonical), a bijection on 2K bits */
+/* (so the order is total and independent of bucketing / shard count).        */
+/* Spectrum: hist[m] = #distinct canonical k-mers seen m times; the last bin  */
+/* hist[hist_len-1] accumulates every m >= hist_len-1; hist[0] = 0.           */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_kstats {
+  uint64_t n_kmers;    /* k-mer instances (sum over reads of max(0, len-K+1)) */
+  uint64_t n_distinct; /* distinct canonical k-mers */
+  uint64_t n_buckets;  /* hash buckets used */
+  uint64_t n_overflow; /* buckets sorted by the out-of-LDS fallback */
+  uint64_t max_bucket; /* largest bucket (records) */
+  uint64_t reserved[3];
+} apg_kstats;
+
+uint64_t apg_kmer_hash(int K, uint64_t canonical);
+uint64_t apg_kmer_unhash(int K, uint64_t hash);
+
+int apg_kmer_spectrum(apg_ctx* ctx, const apg_reads* reads, int K,
+                      uint64_t* hist, size_t hist_len, apg_kstats* stats);
+int apg_kmer_spectrum_dev(apg_ctx* ctx, const apg_dreads* reads, int K,
+                          uint64_t* hist, size_t hist_len, apg_kstats* stats);
+
+/* Counted table (host outputs, library-allocated; release with apg_free).
+ * keys[i] (canonical k-mers) in ascending apg_kmer_hash order, counts[i] >= 1. */
+int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K,
+                   uint64_t** keys, uint32_t** counts, uint64_t* n_distinct,
+                   apg_kstats* stats);
+void apg_free(void* p);
+
+/* ------------------------------------------------------------------------- */
+/* Sharded counting (multi-GPU, one process per GPU).  SURVEY §8e.            */
+/* Shard s owns the canonical k-mers whose hash has top log2(P) bits == s;   */
+/* the next log2(B) bits (B = apg_shard_bins(K, P)) are the L1 group.        */
+/* The caller moves bytes between ranks (torch.distributed all_to_all over    */
+/* RCCL/xGMI); libapg only reads and writes device buffers.                   */
+/*   1. apg_shard_count  : counts[s*B + l1] of local reads' records          */
+/*   2. apg_shard_scatter: records grouped by (s, l1) into d_send            */
+/*   3. (caller) all_to_all of counts, then of d_send -> d_recv (src-major) */
+/*   4. apg_shard_spectrum: count this shard's records; recv_counts[src*B+l1]*/
+/* Records are 8-byte hashes.  P must be a power of two, 1 <= P <= 64.       */
+/* Spectra of the shards add up (all_reduce sum) to the global spectrum.     */
+/* ------------------------------------------------------------------------- */
+int apg_shard_bins(int K, int n_shards);
+int apg_shard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
+                    uint64_t* counts /* host, n_shards * apg_shard_bins */);
+int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
+                      uint64_t* d_send /* device, sum(counts) records */);
+int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv,
+                       const uint64_t* recv_counts /* host, n_shards * bins */,
+                       int K, int n_shards, uint64_t* hist, size_t hist_len,
+                       apg_kstats* stats);
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */
+/* insert N(mean, sd), FR orientation, substitution error rate rising        */
+/* linearly err_lo -> err_hi along the read; Q40 on correct bases, Q2..20 on */
+/* errors.  Deterministic per (seed, read index): any shard regenerates its  */
+/* slice.  Host-only (no GPU).                                               */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_synth_params {
+  uint64_t genome_len;
+  uint64_t seed;
+  uint64_t n_pairs;
+  uint32_t read_len;
+  uint32_t insert_mean;
+  uint32_t insert_sd;
+  uint32_t threads;     /* 0 = hardware concurrency */
+  double err_lo;
+  double err_hi;
+  uint64_t first_pair;  /* generate pairs [first_pair, first_pair+n_pairs) */
+} apg_synth_params;
+
+/* Genome (2 bits/base, one byte per base in out) */
+int apg_synth_genome(uint64_t genome_len, uint64_t seed, uint8_t* out_bases);
+/* Sizes for a synth call: n_reads = 2*n_pairs, packed bytes. */
+int apg_synth_sizes(const apg_synth_params* p, uint64_t* n_reads, uint64_t* n_bases,
+                    uint64_t* n_packed_bytes);
+/* Writes base_off[n+1], byte_off[n+1], packed[], quals[] (quals may be NULL). */
+int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome,
+                    uint64_t* base_off, uint64_t* byte_off, uint8_t* packed,
+                    uint8_t* quals);
+
+/* ------------------------------------------------------------------------- */
+/* On-disk formats ("APG-fastb v0"; feudal byte layout unpinned) */
+/* ------------------------------------------------------------------------- */
+int apg_fastb_write(const char* path, const apg_reads* reads);
+int apg_qualb_write(const char* path, const apg_reads* reads);
+/* Library-allocated; free with apg_reads_release. */
+int apg_fastb_read(const char* path, apg_reads* out);
+int apg_qualb_read(const char* path, apg_reads* inout /* fills quals */);
+void apg_reads_release(apg_reads* r);
+/* Spectrum text file (.kspec): "m\tcount" lines for nonzero bins. */
+int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* APG_H */

@@ -1,0 +1,18 @@
+/* oracle/oracle.h — CPU restatement (TEST INFRASTRUCTURE ONLY; parity unpinned,
+ * see kmer_oracle.c header).  Loaded by tests/ and bench.py's cpu_baseline. */
+#ifndef APG_ORACLE_H
+#define APG_ORACLE_H
+#include <stdint.h>
+
+uint64_t ork_hash(int K, uint64_t canonical);
+uint64_t ork_unhash(int K, uint64_t hash);
+uint64_t ork_count_instances(uint64_t n_reads, const uint64_t* base_off, int K);
+uint64_t ork_extract_hashes(uint64_t n_reads, const uint64_t* base_off,
+                            const uint64_t* byte_off, const uint8_t* packed, int K,
+                            uint64_t* out);
+uint64_t ork_kmer_count(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off,
+                        const uint8_t* packed, int K, uint64_t** hashes, uint32_t** counts);
+void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t hist_len);
+void ork_free(void* p);
+
+#endif

@@ -1,0 +1,115 @@
+"""Oracle checks (CPU only): the C restatement against first-principles
+known-answer tests, against an independent pure-Python
+restatement, and against the committed golden fixtures.
+
+Parity vs the real ALLPATHS-LG is UNPINNED: /root/reference is empty
+(SURVEY §0.1), so no reference tests or golden vectors exist to pin to.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from allpathslg_amd import ReadSet, synth_genome, synth_reads
+from tests import pyoracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("K", [1, 2, 5, 13, 16, 24, 25, 31, 32])
+def test_hash_is_bijection(K):
+    rng = np.random.default_rng(K)
+    w = 2 * K
+    xs = rng.integers(0, 2**63, size=2000, dtype=np.uint64) & np.uint64((1 << w) - 1 if w < 64 else 2**64 - 1)
+    for x in xs[:300]:
+        h = oracle.kmer_hash(K, int(x))
+        assert h < 2**w
+        assert oracle.kmer_unhash(K, h) == int(x)
+    if w <= 12:  # exhaustive: a permutation of [0, 4^K)
+        hs = {oracle.kmer_hash(K, x) for x in range(1 << w)}
+        assert hs == set(range(1 << w))
+
+
+def test_hash_k32_is_splitmix64_finaliser():
+    def sm(x):
+        m = 2**64 - 1
+        x ^= x >> 30
+        x = (x * 0xBF58476D1CE4E5B9) & m
+        x ^= x >> 27
+        x = (x * 0x94D049BB133111EB) & m
+        return x ^ (x >> 31)
+
+    for x in [0, 1, 12345, 2**63 + 7, 2**64 - 1]:
+        assert oracle.kmer_hash(32, x) == sm(x)
+
+
+@pytest.mark.parametrize("K", [3, 11, 25])
+def test_oracle_matches_python_restatement(K):
+    rng = np.random.default_rng(100 + K)
+    seqs = [rng.integers(0, 4, size=int(rng.integers(0, 60))) for _ in range(80)]
+    seqs += [rng.integers(0, 4, size=40)] * 5  # duplicates
+    reads = ReadSet.from_sequences(seqs)
+    h, c = oracle.kmer_count(reads, K)
+    assert np.all(np.diff(h.astype(np.float64)) > 0) or len(h) <= 1  # strictly ascending hash
+    pc = pyoracle.count(reads, K)
+    got = {oracle.kmer_unhash(K, int(x)): int(y) for x, y in zip(h, c)}
+    assert got == dict(pc)
+    hist = oracle.spectrum_from_counts(c, 64)
+    assert np.array_equal(hist, pyoracle.spectrum(pc, 64))
+
+
+def test_kat_error_free_tiling():
+    """reads at every start of a random genome with no repeated
+    K-mer: every genomic K-mer away from the ends is seen L-K+1 times."""
+    G, L, K = 3000, 50, 21
+    g = synth_genome(G, 7)
+    seqs = [g[s : s + L] for s in range(G - L + 1)]
+    reads = ReadSet.from_sequences(seqs)
+    _, c = oracle.kmer_count(reads, K)
+    hist = oracle.spectrum_from_counts(c, 256)
+    n_kmers = G - K + 1
+    # k-mer at genome position p is covered by reads starting in [p-(L-K), p] ∩ [0, G-L]
+    expect = np.zeros(256, dtype=np.uint64)
+    for p in range(n_kmers):
+        lo, hi = max(0, p - (L - K)), min(p, G - L)
+        expect[hi - lo + 1] += 1
+    assert np.array_equal(hist, expect)
+    assert int(hist[L - K + 1]) == n_kmers - 2 * (L - K)
+
+
+def test_kat_reverse_complement_symmetry():
+    """A read and its reverse complement have identical canonical spectra."""
+    rng = np.random.default_rng(3)
+    s = rng.integers(0, 4, size=200)
+    rc = (3 - s[::-1]).copy()
+    a = oracle.kmer_count(ReadSet.from_sequences([s]), 17)
+    b = oracle.kmer_count(ReadSet.from_sequences([rc]), 17)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_conservation_on_synthetic():
+    g = synth_genome(50_000, 11)
+    reads = synth_reads(g, 2000, seed=5)
+    for K in (16, 25):
+        h, c = oracle.kmer_count(reads, K)
+        assert int(c.sum()) == reads.n_reads * (100 - K + 1)
+        hist = oracle.spectrum_from_counts(c, 1 << 16)
+        assert int((hist * np.arange(len(hist), dtype=np.uint64)).sum()) == int(c.sum())
+
+
+def _golden(name):
+    p = os.path.join(GOLDEN, name)
+    if not os.path.exists(p):
+        pytest.skip(f"golden fixture {name} missing (run tests/golden/make_golden.py)")
+    return p
+
+
+def test_oracle_against_golden():
+    reads = ReadSet.load(_golden("frag_small.fastb"), _golden("frag_small.qualb"))
+    z = np.load(_golden("kmer_small.npz"))
+    for K in (16, 25):
+        h, c = oracle.kmer_count(reads, K)
+        assert np.array_equal(h, z[f"hash_k{K}"])
+        assert np.array_equal(c, z[f"count_k{K}"])
+        assert np.array_equal(oracle.spectrum_from_counts(c, 1 << 16)[:4096], z[f"spec_k{K}"])
