@@ -7,17 +7,21 @@
 // Pipeline (all records are w-bit hashes, w = 2K, of canonical k-mers; the
 // hash is a bijection so grouping by hash == grouping by k-mer):
 //   A  extract_count / extract_scatter: one thread per read rolls the k-mer,
-//      hashes it and scatters the hash into 2^D "digit" groups, D = top bits
-//      of the hash = [shard bits | L1 bits].  Per-(digit, block) counts form
-//      a count matrix whose exclusive scan places every block's records
-//      deterministically: no global atomics.
+//      hashes it and scatters the hash into 2^D groups, D = top bits of the
+//      hash = [shard bits | 5 - shard bits L1 bits].  Per-(digit, block)
+//      counts form a count matrix whose exclusive scan places every block's
+//      records: no global atomics, and with 32 digits the per-block write
+//      frontier stays L2-resident.
 //   (multi-GPU: each shard's contiguous range travels by all_to_all)
-//   B  rec_count / rec_scatter: the next b2 hash bits split every L1 group
-//      into LDS-sized buckets (same count-matrix scheme over chunks).
-//   C  sort_count: one workgroup per bucket loads it into LDS, LSD-radix-sorts
-//      the low bits with a wave64 ballot multisplit, run-length counts equal
-//      hashes and bins the counts into the spectrum.  Oversized buckets go to
-//      sort_count_global (same algorithm on global scratch).
+//   B  part_count / part_scatter levels (<= 8 bits each): chunks of a parent
+//      group are counted into a [digit][chunk] matrix, scanned, and scattered
+//      through an LDS-staged 4096-record tile sorted by digit, so waves write
+//      contiguous runs.  Levels stop when mean bucket size ~ kBucketTarget.
+//   C  bucket_count: one workgroup per bucket counts it in an LDS
+//      open-addressing table keyed on the hash bits below the bucket prefix,
+//      bins counts into the spectrum and (table mode) writes distinct
+//      (hash, count) in hash order via rank-by-broadcast.  Buckets over kCap
+//      records (very repeated k-mers) take the global-scratch radix fallback.
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -30,12 +34,8 @@ namespace apg {
 
 constexpr int kExtractThreads = 256;
 constexpr int kMaxExtractBlocks = 2048;
-constexpr int kSortThreads = 512;
-constexpr uint32_t kSortCap = 4096;        // records per LDS-resident bucket
 constexpr uint32_t kBucketTarget = 1536;   // mean bucket size the planner aims for
 constexpr int kLdsHistBins = 1024;         // spectrum bins kept in LDS
-constexpr int kMaxL1Bits = 10;
-constexpr int kMaxL2Bits = 11;
 
 // ------------------------------------------------------------------------
 // scan: u32 counts[n] -> u64 exclusive offsets[n+1] (offsets[n] = total)
@@ -170,59 +170,276 @@ __global__ void k_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig,
 }
 
 // ------------------------------------------------------------------------
-// Stage B: record chunks -> buckets (count matrix over chunks)
+// Stage B: partition levels.  Records of each parent bucket are split by the
+// next `bits` (<= 8) hash bits.  A chunk (<= kChunk records, inside one
+// parent) is counted into a [digit][chunk-of-parent] matrix; after the scan
+// every (chunk, digit) owns a contiguous output range.  The scatter stages a
+// kTile-record tile in LDS sorted by digit, so each wave writes contiguous
+// runs (coalesced) instead of 8-byte scattered stores.
 // ------------------------------------------------------------------------
+constexpr int kPartThreads = 256;
+constexpr int kPartItems = 16;
+constexpr int kTile = kPartThreads * kPartItems;  // 4096 records = 32 KiB of LDS
+constexpr uint32_t kChunk = 4 * kTile;
+constexpr int kMaxLevelBits = 8;
+
 struct Chunk {
   uint64_t start;   // first record
-  uint64_t mat;     // count-matrix index of (l1, digit 0, this chunk)
+  uint64_t mat;     // count-matrix index of (parent, digit 0, this chunk)
   uint32_t len;     // records
-  uint32_t stride;  // chunks of this l1 (matrix stride between digits)
+  uint32_t stride;  // chunks of this parent (matrix stride between digits)
 };
 
-__global__ void __launch_bounds__(256) k_rec_count(const uint64_t* __restrict__ rec, const Chunk* __restrict__ ch,
-                                                   int dshift, uint32_t ndig, uint32_t* __restrict__ cmat) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
+__global__ void __launch_bounds__(kPartThreads) k_part_count(const uint64_t* __restrict__ rec,
+                                                             const Chunk* __restrict__ ch, int shift, uint32_t ndig,
+                                                             uint32_t* __restrict__ cmat) {
+  __shared__ uint32_t hist[256];
   const Chunk c = ch[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = 0;
+  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t dmask = ndig - 1;
   const uint64_t* p = rec + c.start;
-  for (uint32_t i = threadIdx.x; i < c.len; i += blockDim.x) atomicAdd(&hist[(p[i] >> dshift) & dmask], 1u);
+  for (uint32_t i = threadIdx.x; i < c.len; i += blockDim.x) atomicAdd(&hist[(p[i] >> shift) & dmask], 1u);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) cmat[c.mat + (uint64_t)i * c.stride] = hist[i];
 }
 
-__global__ void __launch_bounds__(256) k_rec_scatter(const uint64_t* __restrict__ rec, const Chunk* __restrict__ ch,
-                                                     int dshift, uint32_t ndig, const uint64_t* __restrict__ omat,
-                                                     uint64_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long cur[];
+__global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* __restrict__ rec,
+                                                               const Chunk* __restrict__ ch, int shift, uint32_t ndig,
+                                                               const uint64_t* __restrict__ omat,
+                                                               uint64_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kTile];
+  __shared__ unsigned long long cur[256];
+  __shared__ uint32_t lcnt[256];
+  __shared__ uint32_t lstart[256];
+  __shared__ uint32_t scan_sm[64];
   const Chunk c = ch[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) cur[i] = omat[c.mat + (uint64_t)i * c.stride];
-  __syncthreads();
+  const uint32_t tid = threadIdx.x;
   const uint64_t dmask = ndig - 1;
-  const uint64_t* p = rec + c.start;
-  for (uint32_t i = threadIdx.x; i < c.len; i += blockDim.x) {
-    const uint64_t h = p[i];
-    out[atomicAdd(&cur[(h >> dshift) & dmask], 1ull)] = h;
+  for (uint32_t d = tid; d < ndig; d += blockDim.x) cur[d] = omat[c.mat + (uint64_t)d * c.stride];
+  for (uint32_t t0 = 0; t0 < c.len; t0 += kTile) {
+    const uint32_t tn = min((uint32_t)kTile, c.len - t0);
+    lcnt[tid] = 0;
+    __syncthreads();
+    uint64_t v[kPartItems];
+    uint32_t pos[kPartItems];
+    const uint64_t* p = rec + c.start + t0;
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+      const uint32_t idx = i * kPartThreads + tid;
+      v[i] = idx < tn ? p[idx] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+      const uint32_t idx = i * kPartThreads + tid;
+      if (idx < tn) pos[i] = atomicAdd(&lcnt[(v[i] >> shift) & dmask], 1u);
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<uint32_t>(lcnt[tid], scan_sm, &tot);
+    lstart[tid] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+      const uint32_t idx = i * kPartThreads + tid;
+      if (idx < tn) stage[lstart[(v[i] >> shift) & dmask] + pos[i]] = v[i];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < tn; i += kPartThreads) {
+      const uint64_t x = stage[i];
+      const uint32_t d = (uint32_t)((x >> shift) & dmask);
+      out[cur[d] + (i - lstart[d])] = x;
+    }
+    __syncthreads();
+    if (tid < ndig) cur[tid] += lcnt[tid];
+    __syncthreads();
   }
 }
 
-// boff[l1 * B2 + l2] = omat[l1_base[l1] + l2 * nch[l1]];  boff[B1*B2] = total.
-__global__ void k_bucket_offsets(const uint64_t* __restrict__ omat, const uint64_t* __restrict__ l1_base,
-                                 const uint32_t* __restrict__ nch, uint32_t B1, uint32_t B2, uint64_t total,
+// boff[p * ndig + d] = omat[pbase[p] + d * nch[p]];  boff[nparents*ndig] = total.
+__global__ void k_bucket_offsets(const uint64_t* __restrict__ omat, const uint64_t* __restrict__ pbase,
+                                 const uint32_t* __restrict__ nch, uint64_t nparents, uint32_t ndig, uint64_t total,
                                  uint64_t* __restrict__ boff) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nb = (uint64_t)B1 * B2;
+  const uint64_t nb = nparents * ndig;
   if (i < nb) {
-    const uint32_t l1 = (uint32_t)(i / B2), l2 = (uint32_t)(i % B2);
-    boff[i] = omat[l1_base[l1] + (uint64_t)l2 * nch[l1]];
+    const uint64_t p = i / ndig;
+    const uint32_t d = (uint32_t)(i % ndig);
+    boff[i] = omat[pbase[p] + (uint64_t)d * nch[p]];
   } else if (i == nb) {
     boff[nb] = total;
   }
 }
 
 // ------------------------------------------------------------------------
-// Stage C: per-bucket radix sort + run-length count + spectrum
+// Stage C: per-bucket counting in LDS.  All records of a bucket share the
+// hash bits above `remb`, so a bucket is counted on the low remb bits
+// (rem) in an LDS open-addressing table (linear probing, CAS insert, atomic
+// count).  Distinct entries are compacted in place, then (TABLE) each one's
+// rank among the bucket's distinct keys — computed with broadcast LDS reads —
+// places it at off + rank, i.e. in ascending-hash order, independent of the
+// insertion order.  Counts are binned into the spectrum.
+// ------------------------------------------------------------------------
+constexpr int kCountThreads = 512;
+constexpr uint32_t kCap = 4096;            // max records of an LDS-counted bucket
+constexpr uint32_t kTabMax = 2 * kCap;     // table slots (load factor <= 0.5)
+constexpr int kCapItems = kCap / kCountThreads;
+constexpr int kSlotItems = kTabMax / kCountThreads;
+
+template <typename KT>
+struct KeyTraits;
+template <>
+struct KeyTraits<uint32_t> {
+  static constexpr uint32_t empty = 0xffffffffu;
+};
+template <>
+struct KeyTraits<unsigned long long> {
+  static constexpr unsigned long long empty = ~0ull;
+};
+
+struct CountOut {
+  uint64_t* tab_hash;            // in place over rec (TABLE)
+  uint32_t* tab_cnt;             // parallel to rec (TABLE)
+  uint32_t* bucket_nd;           // distinct per bucket
+  unsigned long long* ghist;     // spectrum
+  uint64_t hist_len;
+  unsigned long long* gstats;    // [0] n_distinct, [1] overflow count, [2] max bucket
+  uint32_t* ovf_list;
+};
+
+__device__ __forceinline__ void spectrum_add(uint32_t c, uint32_t* lhist, unsigned long long* ghist,
+                                             uint64_t hist_len) {
+  uint64_t m = c;
+  if (m >= hist_len - 1) m = hist_len - 1;
+  if (m < (uint64_t)kLdsHistBins)
+    atomicAdd(&lhist[m], 1u);
+  else
+    atomicAdd(&ghist[m], 1ull);
+}
+
+template <typename KT, bool TABLE>
+__global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __restrict__ rec,
+                                                                const uint64_t* __restrict__ boff, uint64_t nbuckets,
+                                                                int remb, CountOut o) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  KT* tkey = reinterpret_cast<KT*>(smem_raw);                              // kTabMax
+  uint32_t* tcnt = reinterpret_cast<uint32_t*>(tkey + kTabMax);            // kTabMax
+  uint32_t* lhist = tcnt + kTabMax;                                        // kLdsHistBins
+  uint32_t* scan_sm = lhist + kLdsHistBins;                                // 64
+  constexpr KT EMPTY = KeyTraits<KT>::empty;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t remmask = remb >= 64 ? ~0ull : ((1ull << remb) - 1);
+  for (uint32_t i = tid; i < kLdsHistBins; i += kCountThreads) lhist[i] = 0;
+  unsigned long long nd_sum = 0, maxb = 0;
+  __syncthreads();
+  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
+    const uint64_t off = boff[bkt];
+    const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
+    if (n > maxb) maxb = n;
+    if (n == 0) {
+      if (tid == 0) o.bucket_nd[bkt] = 0;
+      continue;
+    }
+    if (n > kCap) {
+      if (tid == 0) {
+        const unsigned long long k = atomicAdd(&o.gstats[1], 1ull);
+        o.ovf_list[k] = (uint32_t)bkt;
+      }
+      continue;
+    }
+    // table size: power of two >= 2n (>= 2 slots per thread)
+    uint32_t T = 2 * kCountThreads;
+    while (T < 2 * n) T <<= 1;
+    const uint32_t tmask = T - 1;
+    uint64_t v[kCapItems];
+#pragma unroll
+    for (int i = 0; i < kCapItems; ++i) {
+      const uint32_t idx = i * kCountThreads + tid;
+      v[i] = idx < n ? rec[off + idx] : 0;
+    }
+    for (uint32_t s = tid; s < T; s += kCountThreads) {
+      tkey[s] = EMPTY;
+      tcnt[s] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kCapItems; ++i) {
+      const uint32_t idx = i * kCountThreads + tid;
+      if (idx < n) {
+        const KT key = (KT)(v[i] & remmask);
+        uint32_t s = (uint32_t)key & tmask;
+        for (;;) {
+          const KT old = atomicCAS(&tkey[s], EMPTY, key);
+          if (old == EMPTY || old == key) {
+            atomicAdd(&tcnt[s], 1u);
+            break;
+          }
+          s = (s + 1) & tmask;
+        }
+      }
+    }
+    __syncthreads();
+    // compact occupied slots to the front of the table (in place)
+    const uint32_t spt = T / kCountThreads;
+    KT ks[kSlotItems];
+    uint32_t cs[kSlotItems];
+    uint32_t occ = 0;
+#pragma unroll
+    for (int i = 0; i < kSlotItems; ++i) {
+      if ((uint32_t)i < spt) {
+        const uint32_t s = tid * spt + i;
+        ks[i] = tkey[s];
+        cs[i] = tcnt[s];
+        occ += ks[i] != EMPTY;
+      }
+    }
+    uint32_t d;
+    uint32_t j = block_exclusive_scan<uint32_t>(occ, scan_sm, &d);  // ends with a barrier
+#pragma unroll
+    for (int i = 0; i < kSlotItems; ++i) {
+      if ((uint32_t)i < spt && ks[i] != EMPTY) {
+        tkey[j] = ks[i];
+        tcnt[j] = cs[i];
+        ++j;
+      }
+    }
+    __syncthreads();
+    const uint64_t prefix = v[0] & ~remmask;  // valid for tid < n; only such threads emit
+    for (uint32_t e = tid; e < d; e += kCountThreads) {
+      const KT key = tkey[e];
+      const uint32_t c = tcnt[e];
+      if (TABLE) {
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < d; ++i) r += tkey[i] < key;
+        o.tab_hash[off + r] = prefix | (uint64_t)key;
+        o.tab_cnt[off + r] = c;
+      }
+      spectrum_add(c, lhist, o.ghist, o.hist_len);
+    }
+    if (tid == 0) {
+      o.bucket_nd[bkt] = d;
+      nd_sum += d;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  const uint64_t lim = o.hist_len < (uint64_t)kLdsHistBins ? o.hist_len : (uint64_t)kLdsHistBins;
+  for (uint32_t i = tid; i < lim; i += kCountThreads)
+    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
+  if (tid == 0) {
+    atomicAdd(&o.gstats[0], nd_sum);
+    atomicMax(&o.gstats[2], maxb);
+  }
+}
+
+template <typename KT>
+constexpr size_t bucket_count_lds() {
+  return kTabMax * sizeof(KT) + kTabMax * 4 + kLdsHistBins * 4 + 64 * 4;
+}
+
+// ------------------------------------------------------------------------
+// Stage C fallback: buckets over kCap records (highly repeated k-mers) are
+// radix-sorted in global scratch by one workgroup each, then run-length counted.
 // ------------------------------------------------------------------------
 
 // LSD radix sort of A[0..n) on bits [0, sortbits), 8 bits a pass, stable,
@@ -288,98 +505,15 @@ __device__ uint64_t* block_radix_sort(uint64_t* A, uint64_t* B, uint32_t n, int 
   return A;
 }
 
-__device__ __forceinline__ void spectrum_add(uint32_t c, uint32_t* lhist, unsigned long long* ghist,
-                                             uint64_t hist_len) {
-  uint64_t m = c;
-  if (m >= hist_len - 1) m = hist_len - 1;
-  if (m < (uint64_t)kLdsHistBins)
-    atomicAdd(&lhist[m], 1u);
-  else
-    atomicAdd(&ghist[m], 1ull);
-}
-
-struct SortOut {
-  uint64_t* tab_hash;            // in place over rec
-  uint32_t* tab_cnt;             // parallel to rec
-  uint32_t* bucket_nd;           // distinct per bucket
-  unsigned long long* ghist;     // spectrum
-  uint64_t hist_len;
-  unsigned long long* gstats;    // [0] n_distinct, [1] overflow count, [2] max bucket
-  uint32_t* ovf_list;
-};
-
-__global__ void __launch_bounds__(kSortThreads) k_sort_count(uint64_t* __restrict__ rec,
-                                                             const uint64_t* __restrict__ boff, uint64_t nbuckets,
-                                                             int sortbits, SortOut o) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-  uint64_t* A = smem;
-  uint64_t* B = smem + kSortCap;
-  uint32_t* whist = reinterpret_cast<uint32_t*>(smem + 2 * kSortCap);          // 8 waves x 256
-  uint32_t* lhist = whist + (kSortThreads / 64) * 256;                         // kLdsHistBins
-  uint32_t* scan_sm = lhist + kLdsHistBins;                                    // 64
-  for (int i = threadIdx.x; i < kLdsHistBins; i += blockDim.x) lhist[i] = 0;
-  unsigned long long nd_sum = 0, maxb = 0;
-  __syncthreads();
-  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
-    const uint64_t off = boff[bkt];
-    const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
-    if (n > maxb) maxb = n;
-    if (n == 0) {
-      if (threadIdx.x == 0) o.bucket_nd[bkt] = 0;
-      continue;
-    }
-    if (n > kSortCap) {
-      if (threadIdx.x == 0) {
-        const unsigned long long k = atomicAdd(&o.gstats[1], 1ull);
-        o.ovf_list[k] = (uint32_t)bkt;
-      }
-      continue;
-    }
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) A[i] = rec[off + i];
-    __syncthreads();
-    uint64_t* S = block_radix_sort(A, B, n, sortbits, whist, scan_sm);
-    uint32_t* H = reinterpret_cast<uint32_t*>(S == A ? B : A);
-    // run heads -> distinct index
-    const uint32_t ipt = (n + blockDim.x - 1) / blockDim.x;
-    const uint32_t i0 = min(n, threadIdx.x * ipt), i1 = min(n, i0 + ipt);
-    uint32_t cnt = 0;
-    for (uint32_t i = i0; i < i1; ++i) cnt += (i == 0 || S[i] != S[i - 1]);
-    uint32_t nd;
-    uint32_t j = block_exclusive_scan<uint32_t>(cnt, scan_sm, &nd);
-    for (uint32_t i = i0; i < i1; ++i)
-      if (i == 0 || S[i] != S[i - 1]) H[j++] = i;
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nd; k += blockDim.x) {
-      const uint32_t s = H[k], e = k + 1 < nd ? H[k + 1] : n;
-      o.tab_hash[off + k] = S[s];
-      o.tab_cnt[off + k] = e - s;
-      spectrum_add(e - s, lhist, o.ghist, o.hist_len);
-    }
-    if (threadIdx.x == 0) {
-      o.bucket_nd[bkt] = nd;
-      nd_sum += nd;
-    }
-    __syncthreads();
-  }
-  __syncthreads();
-  const uint64_t lim = o.hist_len < (uint64_t)kLdsHistBins ? o.hist_len : (uint64_t)kLdsHistBins;
-  for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x)
-    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
-  if (threadIdx.x == 0) {
-    atomicAdd(&o.gstats[0], nd_sum);
-    atomicMax(&o.gstats[2], maxb);
-  }
-}
-
 // Oversized buckets: one workgroup each, same algorithm on global scratch.
 // scratch: u64 region parallel to rec (free after stage B); heads: u32 region
 // parallel to rec.
-__global__ void __launch_bounds__(kSortThreads) k_sort_count_global(uint64_t* __restrict__ rec,
+__global__ void __launch_bounds__(kCountThreads) k_sort_count_global(uint64_t* __restrict__ rec,
                                                                     const uint64_t* __restrict__ boff,
                                                                     uint64_t* __restrict__ scratch,
                                                                     uint32_t* __restrict__ heads, int sortbits,
-                                                                    SortOut o) {
-  __shared__ uint32_t whist[(kSortThreads / 64) * 256];
+                                                                    CountOut o) {
+  __shared__ uint32_t whist[(kCountThreads / 64) * 256];
   __shared__ uint32_t lhist[kLdsHistBins];
   __shared__ uint32_t scan_sm[64];
   for (int i = threadIdx.x; i < kLdsHistBins; i += blockDim.x) lhist[i] = 0;
@@ -445,21 +579,15 @@ static int ceil_log2(uint64_t x) {
   return b;
 }
 
-struct Plan {
-  int K = 0, w = 0, P = 1, pbits = 0, b1 = 0, b2 = 0;
-  uint32_t B1 = 1, B2 = 1;
-  int shift2 = 0, sortbits = 0;
-};
-
-// L1 bits after the shard bits; the stage-A digit (shard | L1) is capped at
-// kMaxDigitBits so its LDS histogram / cursor array stays small.
-constexpr int kMaxDigitBits = 12;
+// Stage-A fanout below the shard bits: small, so the LDS-cursor scatter's
+// write frontier (digits x blocks x one 128-B line) stays L2-resident.
+constexpr int kExtractDigitBits = 5;
 static int l1_bits(int K, int P) {
   const int w = 2 * K, pbits = ceil_log2((uint64_t)P);
-  return std::max(0, std::min({kMaxL1Bits, kMaxDigitBits - pbits, w - pbits}));
+  return std::max(0, std::min(kExtractDigitBits - pbits, w - pbits));
 }
 
-// Stage A.  Digit = top (pbits + b1) bits.  extract_count returns per-digit
+// Stage A.  Digit = top (pbits + l1) bits.  extract_count returns per-digit
 // record counts (host, 2^D) and leaves the scanned count matrix in the "x_omat"
 // workspace; extract_scatter reuses it when called for the same (reads, K, P).
 static int extract_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* digit_counts) {
@@ -519,7 +647,7 @@ static int extract_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, uin
 }
 
 struct CountResult {
-  uint64_t* rec = nullptr;        // tab_hash (in place)
+  uint64_t* rec = nullptr;        // final records; tab_hash in place (table mode)
   uint32_t* tab_cnt = nullptr;
   uint32_t* bucket_nd = nullptr;
   uint64_t* boff = nullptr;
@@ -528,140 +656,193 @@ struct CountResult {
   apg_kstats st{};
 };
 
+struct Seg {
+  uint64_t start, len;
+};
+
+// One partition level: every parent's segments -> ndig children per parent.
+// Writes device child offsets to d_boff (nparents*ndig + 1) and, if
+// host_boff, copies them to the host.
+static int part_level(apg_ctx* ctx, const uint64_t* src, uint64_t* dst, const std::vector<std::vector<Seg>>& parents,
+                      int shift, int bits, uint64_t n, uint64_t* d_boff, std::vector<uint64_t>* host_boff) {
+  const uint32_t ndig = 1u << bits;
+  const uint64_t np = parents.size();
+  std::vector<Chunk> chunks;
+  std::vector<uint64_t> pbase(np);
+  std::vector<uint32_t> nch(np);
+  uint64_t mat = 0;
+  for (uint64_t p = 0; p < np; ++p) {
+    const size_t first = chunks.size();
+    for (const Seg& s : parents[p])
+      for (uint64_t o = 0; o < s.len; o += kChunk)
+        chunks.push_back(Chunk{s.start + o, 0, (uint32_t)std::min<uint64_t>(kChunk, s.len - o), 0});
+    if (chunks.size() == first) chunks.push_back(Chunk{0, 0, 0, 0});  // every parent owns matrix columns
+    const uint32_t k = (uint32_t)(chunks.size() - first);
+    for (uint32_t i = 0; i < k; ++i) {
+      chunks[first + i].mat = mat + i;
+      chunks[first + i].stride = k;
+    }
+    pbase[p] = mat;
+    nch[p] = k;
+    mat += (uint64_t)k * ndig;
+  }
+  Chunk* d_chunks = nullptr;
+  uint64_t *d_pbase = nullptr, *omat = nullptr;
+  uint32_t *d_nch = nullptr, *cmat = nullptr;
+  APG_TRY(workspace_t(ctx, "p_chunks", chunks.size(), &d_chunks));
+  APG_TRY(workspace_t(ctx, "p_pbase", np, &d_pbase));
+  APG_TRY(workspace_t(ctx, "p_nch", np, &d_nch));
+  APG_TRY(workspace_t(ctx, "p_cmat", mat, &cmat));
+  APG_TRY(workspace_t(ctx, "p_omat", mat + 1, &omat));
+  APG_CHECK_HIP(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice,
+                               ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(d_pbase, pbase.data(), np * 8, hipMemcpyHostToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(d_nch, nch.data(), np * 4, hipMemcpyHostToDevice, ctx->stream));
+  const uint32_t nchunks = (uint32_t)chunks.size();
+  kbegin(ctx, "part_count", n * 8 + mat * 4);
+  k_part_count<<<nchunks, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, cmat);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, cmat, mat, omat, "p"));
+  kbegin(ctx, "part_scatter", n * 16 + mat * 8);
+  k_part_scatter<<<nchunks, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, omat, dst);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  const uint64_t nb = np * ndig;
+  k_bucket_offsets<<<(nb + 1 + 255) / 256, 256, 0, ctx->stream>>>(omat, d_pbase, d_nch, np, ndig, n, d_boff);
+  APG_CHECK_HIP(hipGetLastError());
+  if (host_boff) {
+    host_boff->resize(nb + 1);
+    APG_CHECK_HIP(hipMemcpyAsync(host_boff->data(), d_boff, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+  }
+  return APG_OK;
+}
+
 // Stages B + C on records held in `src`, laid out as P source blocks, each
-// grouped by l1: recv_counts[src * B1 + l1].
-static int stage_count(apg_ctx* ctx, const uint64_t* src, const std::vector<uint64_t>& recv_counts, int K, int P,
-                       uint64_t* hist, size_t hist_len, CountResult* res) {
-  Plan pl;
-  pl.K = K;
-  pl.w = 2 * K;
-  pl.P = P;
-  pl.pbits = ceil_log2((uint64_t)P);
-  pl.b1 = l1_bits(K, P);
-  pl.B1 = 1u << pl.b1;
-  if (recv_counts.size() != (size_t)P * pl.B1) {
+// grouped by L1 group: recv_counts[src * B1 + l1].  `spare` (may be null) is
+// a library buffer of >= n records that may be overwritten (ping-pong).
+static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const std::vector<uint64_t>& recv_counts,
+                       int K, int P, bool table, uint64_t* hist, size_t hist_len, CountResult* res) {
+  const int w = 2 * K, pbits = ceil_log2((uint64_t)P), l1 = l1_bits(K, P);
+  const uint32_t B1 = 1u << l1;
+  if (recv_counts.size() != (size_t)P * B1) {
     set_error("stage_count: recv_counts has wrong size");
     return APG_E_ARG;
   }
   uint64_t n = 0;
   for (auto c : recv_counts) n += c;
-  const int room = pl.w - pl.pbits - pl.b1;
-  const uint64_t want = (n + (uint64_t)pl.B1 * kBucketTarget - 1) / ((uint64_t)pl.B1 * kBucketTarget);
-  pl.b2 = std::max(0, std::min({kMaxL2Bits, room, ceil_log2(std::max<uint64_t>(1, want))}));
-  pl.B2 = 1u << pl.b2;
-  pl.shift2 = room - pl.b2;
-  pl.sortbits = pl.shift2;
+  const uint64_t need = (n + kBucketTarget - 1) / kBucketTarget;
+  const int bb = std::min(w - pbits, std::max(l1, ceil_log2(std::max<uint64_t>(1, need))));
+  const int rem = bb - l1;
+  int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  if (nlev == 0 && P > 1) nlev = 1;  // regroup the P source segments of each L1 group
+  std::vector<int> lbits(nlev, 0);
+  for (int i = 0; i < nlev; ++i) lbits[i] = rem / nlev + (i < rem % nlev ? 1 : 0);
+  const int remb = w - pbits - bb;
   res->n_records = n;
-  vlog(ctx, "count: K=%d P=%d records=%llu b1=%d b2=%d sortbits=%d", K, P, (unsigned long long)n, pl.b1, pl.b2,
-       pl.sortbits);
+  vlog(ctx, "count: K=%d P=%d records=%llu l1=%d levels=%d bucket_bits=%d remb=%d table=%d", K, P,
+       (unsigned long long)n, l1, nlev, bb, remb, (int)table);
 
-  // Segments of each l1 in source order -> chunks.
-  std::vector<uint64_t> src_base(P + 1, 0);
-  for (int s = 0; s < P; ++s) {
-    uint64_t t = 0;
-    for (uint32_t l = 0; l < pl.B1; ++l) t += recv_counts[(size_t)s * pl.B1 + l];
-    src_base[s + 1] = src_base[s] + t;
+  // parents = L1 groups, each with its P source segments
+  std::vector<std::vector<Seg>> parents(B1);
+  {
+    uint64_t pos = 0;
+    for (int s = 0; s < P; ++s)
+      for (uint32_t l = 0; l < B1; ++l) {
+        const uint64_t c = recv_counts[(size_t)s * B1 + l];
+        parents[l].push_back(Seg{pos, c});
+        pos += c;
+      }
   }
-  std::vector<uint64_t> seg_start((size_t)P * pl.B1);
-  for (int s = 0; s < P; ++s) {
-    uint64_t pos = src_base[s];
-    for (uint32_t l = 0; l < pl.B1; ++l) {
-      seg_start[(size_t)s * pl.B1 + l] = pos;
-      pos += recv_counts[(size_t)s * pl.B1 + l];
-    }
+  uint64_t *bufA = nullptr, *bufB = nullptr;
+  APG_TRY(workspace_t(ctx, "c_recA", std::max<uint64_t>(n, 1), &bufA));
+  if (spare) {
+    bufB = spare;
+  } else {
+    APG_TRY(workspace_t(ctx, "c_recB", std::max<uint64_t>(n, 1), &bufB));
   }
-  const uint64_t max_chunks = 32768;
-  uint64_t C = std::max<uint64_t>(8192, (n + max_chunks - 1) / max_chunks);
-  C = std::min<uint64_t>(C, 1u << 30);
-  std::vector<Chunk> chunks;
-  std::vector<uint64_t> l1_base(pl.B1);
-  std::vector<uint32_t> nch(pl.B1);
-  uint64_t mat_base = 0;
-  for (uint32_t l = 0; l < pl.B1; ++l) {
-    const size_t first = chunks.size();
-    for (int s = 0; s < P; ++s) {
-      const uint64_t st = seg_start[(size_t)s * pl.B1 + l], len = recv_counts[(size_t)s * pl.B1 + l];
-      for (uint64_t o = 0; o < len; o += C) chunks.push_back(Chunk{st + o, 0, (uint32_t)std::min(C, len - o), 0});
-    }
-    if (chunks.size() == first) chunks.push_back(Chunk{0, 0, 0, 0});  // every l1 gets a matrix column
-    const uint32_t k = (uint32_t)(chunks.size() - first);
-    for (uint32_t i = 0; i < k; ++i) {
-      chunks[first + i].mat = mat_base + i;
-      chunks[first + i].stride = k;
-    }
-    l1_base[l] = mat_base;
-    nch[l] = k;
-    mat_base += (uint64_t)k * pl.B2;
+  uint64_t nb = B1;
+  uint64_t* boff = nullptr;
+  APG_TRY(workspace_t(ctx, "c_boff", (1ull << bb) + 1, &boff));
+  const uint64_t* cur = src;
+  uint64_t* other = nullptr;  // buffer not holding `cur`
+  int consumed = pbits + l1;
+  if (nlev == 0) {
+    // P == 1 and no further split: stage-A groups are the buckets.
+    std::vector<uint64_t> hb(B1 + 1, 0);
+    for (uint32_t l = 0; l < B1; ++l) hb[l + 1] = hb[l] + recv_counts[l];
+    APG_CHECK_HIP(hipMemcpyAsync(boff, hb.data(), (B1 + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    other = bufA;
   }
-  const uint64_t nmat = mat_base;
+  for (int lev = 0; lev < nlev; ++lev) {
+    consumed += lbits[lev];
+    const int shift = w - consumed;
+    uint64_t* dst = (lev % 2 == 0) ? bufA : bufB;
+    std::vector<uint64_t> hb;
+    const bool last = lev + 1 == nlev;
+    APG_TRY(part_level(ctx, cur, dst, parents, shift, lbits[lev], n, boff, last ? nullptr : &hb));
+    nb = parents.size() << lbits[lev];
+    if (!last) {
+      parents.assign(nb, {});
+      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
+    }
+    other = (dst == bufA) ? bufB : bufA;
+    cur = dst;
+  }
+  uint64_t* rec = const_cast<uint64_t*>(cur);  // library-owned here unless nlev == 0 (P == 1, src = spare)
 
-  uint64_t *rec = nullptr, *boff = nullptr, *omat = nullptr, *d_l1_base = nullptr;
-  uint32_t *cmat = nullptr, *d_nch = nullptr, *tab_cnt = nullptr, *bucket_nd = nullptr, *ovf_list = nullptr;
-  Chunk* d_chunks = nullptr;
-  const uint64_t nb = (uint64_t)pl.B1 * pl.B2;
-  APG_TRY(workspace_t(ctx, "c_rec", std::max<uint64_t>(n, 1), &rec));
-  APG_TRY(workspace_t(ctx, "c_tabcnt", std::max<uint64_t>(n, 1), &tab_cnt));
-  APG_TRY(workspace_t(ctx, "c_cmat", nmat, &cmat));
-  APG_TRY(workspace_t(ctx, "c_omat", nmat + 1, &omat));
-  APG_TRY(workspace_t(ctx, "c_chunks", chunks.size(), &d_chunks));
-  APG_TRY(workspace_t(ctx, "c_l1base", pl.B1, &d_l1_base));
-  APG_TRY(workspace_t(ctx, "c_nch", pl.B1, &d_nch));
-  APG_TRY(workspace_t(ctx, "c_boff", nb + 1, &boff));
-  APG_TRY(workspace_t(ctx, "c_bnd", nb, &bucket_nd));
-  APG_TRY(workspace_t(ctx, "c_ovf", nb, &ovf_list));
+  uint32_t *tab_cnt = nullptr, *bucket_nd = nullptr, *ovf_list = nullptr;
   unsigned long long *ghist = nullptr, *gstats = nullptr;
   const uint64_t hl = std::max<uint64_t>(hist_len, 2);
+  APG_TRY(workspace_t(ctx, "c_tabcnt", table ? std::max<uint64_t>(n, 1) : 1, &tab_cnt));
+  APG_TRY(workspace_t(ctx, "c_bnd", nb, &bucket_nd));
+  APG_TRY(workspace_t(ctx, "c_ovf", nb, &ovf_list));
   APG_TRY(workspace_t(ctx, "c_hist", hl, &ghist));
   APG_TRY(workspace_t(ctx, "c_gstats", 4, &gstats));
-  APG_CHECK_HIP(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice,
-                               ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(d_l1_base, l1_base.data(), pl.B1 * 8, hipMemcpyHostToDevice, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(d_nch, nch.data(), pl.B1 * 4, hipMemcpyHostToDevice, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
 
-  // Stage B
-  const uint32_t nchunks = (uint32_t)chunks.size();
-  kbegin(ctx, "rec_count", n * 8 + nmat * 4);
-  k_rec_count<<<nchunks, 256, pl.B2 * 4, ctx->stream>>>(src, d_chunks, pl.shift2, pl.B2, cmat);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  APG_TRY(scan_u32_u64(ctx, cmat, nmat, omat, "c"));
-  kbegin(ctx, "rec_scatter", n * 16 + nmat * 8);
-  k_rec_scatter<<<nchunks, 256, pl.B2 * 8, ctx->stream>>>(src, d_chunks, pl.shift2, pl.B2, omat, rec);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  k_bucket_offsets<<<(nb + 1 + 255) / 256, 256, 0, ctx->stream>>>(omat, d_l1_base, d_nch, pl.B1, pl.B2, n, boff);
-  APG_CHECK_HIP(hipGetLastError());
-
-  // Stage C
-  SortOut so{rec, tab_cnt, bucket_nd, ghist, hl, gstats, ovf_list};
-  const size_t lds = 2 * kSortCap * 8 + (kSortThreads / 64) * 256 * 4 + kLdsHistBins * 4 + 64 * 4;
-  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * 8));
-  kbegin(ctx, "sort_count", n * 8 + n * 12 + (nb + 1) * 8 + nb * 4);
-  k_sort_count<<<grid, kSortThreads, lds, ctx->stream>>>(rec, boff, nb, pl.sortbits, so);
+  CountOut co{rec, tab_cnt, bucket_nd, ghist, hl, gstats, ovf_list};
+  const bool narrow = remb <= 31;
+  const size_t lds = narrow ? bucket_count_lds<uint32_t>() : bucket_count_lds<unsigned long long>();
+  const int per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
+  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * per_cu * 2));
+  kbegin(ctx, "bucket_count", n * 8 + (table ? n * 12 : 0) + (nb + 1) * 8 + nb * 4);
+  if (narrow && table)
+    k_bucket_count<uint32_t, true><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
+  else if (narrow)
+    k_bucket_count<uint32_t, false><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
+  else if (table)
+    k_bucket_count<unsigned long long, true><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
+  else
+    k_bucket_count<unsigned long long, false><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hs[4];
   APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
   if (hs[1]) {
-    // Oversized buckets: scratch = a u64 region parallel to rec.
-    uint64_t* scratch = nullptr;
+    // Oversized buckets: radix sort in global scratch (the ping-pong buffer not
+    // holding rec is free now).
+    uint64_t* scratch = other;
+    if (scratch == nullptr || scratch == rec) APG_TRY(workspace_t(ctx, "c_recB", std::max<uint64_t>(n, 1), &scratch));
     uint32_t* heads = nullptr;
-    APG_TRY(workspace_t(ctx, "c_scratch", n, &scratch));
-    APG_TRY(workspace_t(ctx, "c_heads", n, &heads));
-    vlog(ctx, "count: %llu oversized buckets -> global sort", hs[1]);
-    kbegin(ctx, "sort_count_global", 0);
-    k_sort_count_global<<<(uint32_t)hs[1], kSortThreads, 0, ctx->stream>>>(rec, boff, scratch, heads, pl.sortbits,
-                                                                          so);
+    APG_TRY(workspace_t(ctx, "c_heads", std::max<uint64_t>(n, 1), &heads));
+    uint32_t* tcnt_full = tab_cnt;
+    if (!table) {
+      APG_TRY(workspace_t(ctx, "c_tabcnt", std::max<uint64_t>(n, 1), &tcnt_full));
+      co.tab_cnt = tcnt_full;
+    }
+    vlog(ctx, "count: %llu oversized buckets -> global radix path", hs[1]);
+    kbegin(ctx, "bucket_count_global", 0);
+    k_sort_count_global<<<(uint32_t)hs[1], kCountThreads, 0, ctx->stream>>>(rec, boff, scratch, heads, remb, co);
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+    tab_cnt = co.tab_cnt;
   }
-  if (hist && hist_len) {
-    APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
-  }
+  if (hist && hist_len) APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
   if (hist && hist_len) hist[0] = 0;
   res->rec = rec;
@@ -677,7 +858,7 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, const std::vector<uint
   return APG_OK;
 }
 
-static int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, uint64_t* hist, size_t hist_len,
+static int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
                          CountResult* res) {
   APG_REQUIRE(ctx && dr, "spectrum: NULL ctx/reads");
   APG_REQUIRE(K >= 1 && K <= 32, "spectrum: K must be in [1, 32] for the 64-bit path");
@@ -688,7 +869,7 @@ static int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, uint64_t* hi
   uint64_t* buf = nullptr;
   APG_TRY(workspace_t(ctx, "x_records", std::max<uint64_t>(ctx->xstate.total, 1), &buf));
   APG_TRY(extract_scatter(ctx, dr, K, 1, buf));
-  return stage_count(ctx, buf, counts, K, 1, hist, hist_len, res);
+  return stage_count(ctx, buf, buf, counts, K, 1, table, hist, hist_len, res);
 }
 
 }  // namespace apg
@@ -710,7 +891,7 @@ uint64_t apg_kmer_unhash(int K, uint64_t hash) {
 int apg_kmer_spectrum_dev(apg_ctx* ctx, const apg_dreads* reads, int K, uint64_t* hist, size_t hist_len,
                           apg_kstats* stats) {
   CountResult r;
-  APG_TRY(spectrum_impl(ctx, reads, K, hist, hist_len, &r));
+  APG_TRY(spectrum_impl(ctx, reads, K, false, hist, hist_len, &r));
   if (stats) *stats = r.st;
   return APG_OK;
 }
@@ -733,7 +914,7 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
   apg_dreads* dr = nullptr;
   APG_TRY(apg_reads_upload(ctx, reads, &dr));
   CountResult r;
-  int rc = spectrum_impl(ctx, dr, K, nullptr, 0, &r);
+  int rc = spectrum_impl(ctx, dr, K, true, nullptr, 0, &r);
   apg_reads_free(dr);
   if (rc) return rc;
   const uint64_t nd = r.st.n_distinct;
@@ -772,12 +953,22 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
   return APG_OK;
 }
 
+static int check_shards(int K, int n_shards) {
+  APG_REQUIRE(K >= 1 && K <= 32, "K must be in [1, 32]");
+  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
+              "n_shards must be a power of two in [1, 64]");
+  APG_REQUIRE(2 * K >= ceil_log2((uint64_t)n_shards), "K too small for n_shards");
+  return APG_OK;
+}
+
+int apg_shard_bins(int K, int n_shards) {
+  if (check_shards(K, n_shards) != APG_OK) return APG_E_ARG;
+  return 1 << l1_bits(K, n_shards);
+}
+
 int apg_shard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* send_counts) {
   APG_REQUIRE(ctx && reads && send_counts, "apg_shard_count: NULL argument");
-  APG_REQUIRE(K >= 1 && K <= 32, "apg_shard_count: K must be in [1, 32]");
-  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
-              "apg_shard_count: n_shards must be a power of two in [1, 64]");
-  APG_REQUIRE(2 * K >= ceil_log2((uint64_t)n_shards), "apg_shard_count: K too small for n_shards");
+  APG_TRY(check_shards(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   std::vector<uint64_t> dc;
   APG_TRY(extract_count(ctx, reads, K, n_shards, &dc));
@@ -787,9 +978,7 @@ int apg_shard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, 
 
 int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* d_send) {
   APG_REQUIRE(ctx && reads, "apg_shard_scatter: NULL argument");
-  APG_REQUIRE(K >= 1 && K <= 32, "apg_shard_scatter: K must be in [1, 32]");
-  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
-              "apg_shard_scatter: n_shards must be a power of two in [1, 64]");
+  APG_TRY(check_shards(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   APG_TRY(extract_scatter(ctx, reads, K, n_shards, d_send));
   return sync(ctx);
@@ -798,9 +987,7 @@ int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards
 int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                        uint64_t* hist, size_t hist_len, apg_kstats* stats) {
   APG_REQUIRE(ctx && recv_counts, "apg_shard_spectrum: NULL argument");
-  APG_REQUIRE(K >= 1 && K <= 32, "apg_shard_spectrum: K must be in [1, 32]");
-  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
-              "apg_shard_spectrum: n_shards must be a power of two in [1, 64]");
+  APG_TRY(check_shards(K, n_shards));
   APG_REQUIRE(hist_len == 0 || hist_len >= 2, "apg_shard_spectrum: hist_len must be 0 or >= 2");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const uint32_t B1 = 1u << l1_bits(K, n_shards);
@@ -809,14 +996,9 @@ int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* rec
   for (auto c : rc) n += c;
   APG_REQUIRE(n == 0 || d_recv, "apg_shard_spectrum: d_recv is NULL");
   CountResult r;
-  APG_TRY(stage_count(ctx, d_recv, rc, K, n_shards, hist, hist_len, &r));
+  APG_TRY(stage_count(ctx, d_recv, nullptr, rc, K, n_shards, false, hist, hist_len, &r));
   if (stats) *stats = r.st;
   return APG_OK;
-}
-
-int apg_shard_bins(int K, int n_shards) {
-  if (K < 1 || K > 32 || n_shards < 1) return APG_E_ARG;
-  return 1 << l1_bits(K, n_shards);
 }
 
 }  // extern "C"
