@@ -82,6 +82,39 @@ __device__ __forceinline__ void for_each_kmer_hash(const uint8_t* __restrict__ r
   }
 }
 
+// Incremental form of for_each_kmer_hash: a thread's rolling state over one
+// read, so k-mers can be produced a few at a time (staged scatter rounds).
+struct KmerRoller {
+  const uint8_t* read;
+  uint32_t len, i, byte;
+  uint64_t fw, rc;
+  int K;
+
+  __device__ __forceinline__ void init(const uint8_t* r, uint32_t n, int k, const HashP& hp) {
+    read = r;
+    len = n;
+    K = k;
+    i = 0;
+    byte = 0;
+    fw = rc = 0;
+    const uint32_t prime = n < (uint32_t)(k - 1) ? n : (uint32_t)(k - 1);
+    for (uint32_t j = 0; j < prime; ++j) roll(hp);
+  }
+  __device__ __forceinline__ void roll(const HashP& hp) {
+    if ((i & 3) == 0) byte = read[i >> 2];
+    const uint64_t b = (byte >> (2 * (i & 3))) & 3;
+    fw = ((fw << 2) | b) & hp.mask;
+    rc = (rc >> 2) | ((3 - b) << (2 * K - 2));
+    ++i;
+  }
+  __device__ __forceinline__ bool more() const { return i < len; }
+  // Next k-mer hash (call only when more()).
+  __device__ __forceinline__ uint64_t next(const HashP& hp) {
+    roll(hp);
+    return khash(hp, fw < rc ? fw : rc);
+  }
+};
+
 // ---- wave / block primitives (wave64) -------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }

@@ -141,24 +141,65 @@ __global__ void __launch_bounds__(kExtractThreads) k_extract_count(ReadsView rv,
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) cmat[(uint64_t)i * G + b] = hist[i];
 }
 
+// Staged scatter: each thread rolls its read 16 k-mers per round; the
+// block's round (<= 4096 records) is counting-sorted by digit in LDS and
+// written as contiguous per-digit runs.
+constexpr int kXItems = 16;
+
 __global__ void __launch_bounds__(kExtractThreads) k_extract_scatter(ReadsView rv, int K, HashP hp, int dshift,
                                                                      uint32_t ndig,
                                                                      const uint64_t* __restrict__ omat,
                                                                      uint64_t* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long cur[];
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) cur[i] = omat[(uint64_t)i * G + b];
-  __syncthreads();
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kExtractThreads * kXItems];
+  __shared__ unsigned long long cur[256];
+  __shared__ uint32_t lcnt[256];
+  __shared__ uint32_t lstart[256];
+  __shared__ uint32_t scan_sm[64];
+  const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  const uint64_t dmask = ndig - 1;
+  for (uint32_t d = tid; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
   uint64_t r0, r1;
   block_read_range(rv.n_reads, G, b, &r0, &r1);
-  const uint64_t dmask = ndig - 1;
-  for (uint64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-    const uint64_t s = rv.base_off[r];
-    const uint32_t len = (uint32_t)(rv.base_off[r + 1] - s);
-    for_each_kmer_hash(rv.packed + rv.byte_off[r], len, K, hp, [&](uint64_t h) {
-      const unsigned long long pos = atomicAdd(&cur[(h >> dshift) & dmask], 1ull);
-      out[pos] = h;
-    });
+  for (uint64_t rb = r0; rb < r1; rb += kExtractThreads) {
+    const uint64_t r = rb + tid;
+    KmerRoller kr;
+    kr.i = 0;
+    kr.len = 0;
+    if (r < r1) {
+      const uint64_t s = rv.base_off[r];
+      kr.init(rv.packed + rv.byte_off[r], (uint32_t)(rv.base_off[r + 1] - s), K, hp);
+    }
+    while (__syncthreads_or(kr.more())) {
+      lcnt[tid] = 0;
+      __syncthreads();
+      uint64_t v[kXItems];
+      uint32_t pos[kXItems];
+      uint32_t nv = 0;
+#pragma unroll
+      for (int j = 0; j < kXItems; ++j) {
+        if (kr.more()) {
+          v[j] = kr.next(hp);
+          pos[j] = atomicAdd(&lcnt[(v[j] >> dshift) & dmask], 1u);
+          nv = j + 1;
+        }
+      }
+      __syncthreads();
+      uint32_t tot;
+      const uint32_t ex = block_exclusive_scan<uint32_t>(lcnt[tid], scan_sm, &tot);
+      lstart[tid] = ex;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kXItems; ++j)
+        if ((uint32_t)j < nv) stage[lstart[(v[j] >> dshift) & dmask] + pos[j]] = v[j];
+      __syncthreads();
+      for (uint32_t i = tid; i < tot; i += kExtractThreads) {
+        const uint64_t x = stage[i];
+        const uint32_t d = (uint32_t)((x >> dshift) & dmask);
+        out[cur[d] + (i - lstart[d])] = x;
+      }
+      __syncthreads();
+      if (tid < ndig) cur[tid] += lcnt[tid];
+    }
   }
 }
 
@@ -170,24 +211,24 @@ __global__ void k_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig,
 }
 
 // ------------------------------------------------------------------------
-// Stage B: partition levels.  Records of each parent bucket are split by the
-// next `bits` (<= 8) hash bits.  A chunk (<= kChunk records, inside one
-// parent) is counted into a [digit][chunk-of-parent] matrix; after the scan
-// every (chunk, digit) owns a contiguous output range.  The scatter stages a
+// Stage B: partition levels.  Records of each parent group are split by the
+// next `bits` (<= 8) hash bits.  Chunks (runs of records inside one parent)
+// are counted into a row-major [chunk][digit] matrix (one coalesced row per
+// chunk); a per-parent column scan turns it into each chunk's starting offset
+// inside every child, and the children's starts.  The scatter stages a
 // kTile-record tile in LDS sorted by digit, so each wave writes contiguous
-// runs (coalesced) instead of 8-byte scattered stores.
+// per-child runs instead of 8-byte scattered stores.
 // ------------------------------------------------------------------------
 constexpr int kPartThreads = 256;
 constexpr int kPartItems = 16;
 constexpr int kTile = kPartThreads * kPartItems;  // 4096 records = 32 KiB of LDS
-constexpr uint32_t kChunk = 4 * kTile;
 constexpr int kMaxLevelBits = 8;
+constexpr int kScanGroups = 4;                    // 1024-thread column scan
 
 struct Chunk {
   uint64_t start;   // first record
-  uint64_t mat;     // count-matrix index of (parent, digit 0, this chunk)
   uint32_t len;     // records
-  uint32_t stride;  // chunks of this parent (matrix stride between digits)
+  uint32_t parent;  // parent group
 };
 
 __global__ void __launch_bounds__(kPartThreads) k_part_count(const uint64_t* __restrict__ rec,
@@ -195,18 +236,60 @@ __global__ void __launch_bounds__(kPartThreads) k_part_count(const uint64_t* __r
                                                              uint32_t* __restrict__ cmat) {
   __shared__ uint32_t hist[256];
   const Chunk c = ch[blockIdx.x];
-  if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+  hist[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t dmask = ndig - 1;
   const uint64_t* p = rec + c.start;
   for (uint32_t i = threadIdx.x; i < c.len; i += blockDim.x) atomicAdd(&hist[(p[i] >> shift) & dmask], 1u);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) cmat[c.mat + (uint64_t)i * c.stride] = hist[i];
+  if (threadIdx.x < ndig) cmat[(uint64_t)blockIdx.x * ndig + threadIdx.x] = hist[threadIdx.x];
+}
+
+// One workgroup per parent: pre[row][d] = sum of column d over the parent's
+// earlier rows; child[p*ndig + d] = pstart[p] + sum_{d' < d} column total(d').
+__global__ void __launch_bounds__(kPartThreads* kScanGroups) k_part_scan(const uint32_t* __restrict__ cmat,
+                                                                         const uint32_t* __restrict__ prow,
+                                                                         const uint64_t* __restrict__ pstart,
+                                                                         uint32_t ndig, uint32_t* __restrict__ pre,
+                                                                         uint64_t* __restrict__ child) {
+  __shared__ uint32_t gsum[kScanGroups][256];
+  __shared__ unsigned long long scan_sm[64];
+  const uint32_t p = blockIdx.x, tid = threadIdx.x, d = tid & 255, g = tid >> 8;
+  const uint32_t r0 = prow[p], r1 = prow[p + 1], nr = r1 - r0;
+  const uint32_t q = (nr + kScanGroups - 1) / kScanGroups;
+  const uint32_t a = min(r1, r0 + g * q), b = min(r1, a + q);
+  const bool col = d < ndig;
+  uint32_t s = 0;
+  if (col) {
+#pragma unroll 8
+    for (uint32_t r = a; r < b; ++r) s += cmat[(uint64_t)r * ndig + d];
+  }
+  gsum[g][d] = s;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (uint32_t k = 0; k < kScanGroups; ++k) {
+    if (k < g) run += gsum[k][d];
+    tot += gsum[k][d];
+  }
+  if (col) {
+#pragma unroll 8
+    for (uint32_t r = a; r < b; ++r) {
+      const uint64_t i = (uint64_t)r * ndig + d;
+      const uint32_t x = cmat[i];
+      pre[i] = run;
+      run += x;
+    }
+  }
+  unsigned long long all;
+  const unsigned long long ex =
+      block_exclusive_scan<unsigned long long>((g == 0 && col) ? (unsigned long long)tot : 0ull, scan_sm, &all);
+  if (g == 0 && col) child[(uint64_t)p * ndig + d] = pstart[p] + ex;
 }
 
 __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* __restrict__ rec,
                                                                const Chunk* __restrict__ ch, int shift, uint32_t ndig,
-                                                               const uint64_t* __restrict__ omat,
+                                                               const uint32_t* __restrict__ pre,
+                                                               const uint64_t* __restrict__ child,
                                                                uint64_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint64_t stage[kTile];
   __shared__ unsigned long long cur[256];
@@ -216,7 +299,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* _
   const Chunk c = ch[blockIdx.x];
   const uint32_t tid = threadIdx.x;
   const uint64_t dmask = ndig - 1;
-  for (uint32_t d = tid; d < ndig; d += blockDim.x) cur[d] = omat[c.mat + (uint64_t)d * c.stride];
+  if (tid < ndig) cur[tid] = child[(uint64_t)c.parent * ndig + tid] + pre[(uint64_t)blockIdx.x * ndig + tid];
   for (uint32_t t0 = 0; t0 < c.len; t0 += kTile) {
     const uint32_t tn = min((uint32_t)kTile, c.len - t0);
     lcnt[tid] = 0;
@@ -253,21 +336,6 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* _
     __syncthreads();
     if (tid < ndig) cur[tid] += lcnt[tid];
     __syncthreads();
-  }
-}
-
-// boff[p * ndig + d] = omat[pbase[p] + d * nch[p]];  boff[nparents*ndig] = total.
-__global__ void k_bucket_offsets(const uint64_t* __restrict__ omat, const uint64_t* __restrict__ pbase,
-                                 const uint32_t* __restrict__ nch, uint64_t nparents, uint32_t ndig, uint64_t total,
-                                 uint64_t* __restrict__ boff) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nb = nparents * ndig;
-  if (i < nb) {
-    const uint64_t p = i / ndig;
-    const uint32_t d = (uint32_t)(i % ndig);
-    boff[i] = omat[pbase[p] + (uint64_t)d * nch[p]];
-  } else if (i == nb) {
-    boff[nb] = total;
   }
 }
 
@@ -331,105 +399,130 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
   const uint64_t remmask = remb >= 64 ? ~0ull : ((1ull << remb) - 1);
   for (uint32_t i = tid; i < kLdsHistBins; i += kCountThreads) lhist[i] = 0;
   unsigned long long nd_sum = 0, maxb = 0;
-  __syncthreads();
-  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
-    const uint64_t off = boff[bkt];
-    const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
-    if (n > maxb) maxb = n;
-    if (n == 0) {
-      if (tid == 0) o.bucket_nd[bkt] = 0;
-      continue;
+
+  // Records of bucket `b` into registers (n <= kCap; larger buckets are not loaded).
+  auto load = [&](uint64_t b, uint64_t& off, uint32_t& n, uint64_t (&v)[kCapItems]) {
+    n = 0;
+    off = 0;
+    if (b < nbuckets) {
+      off = boff[b];
+      n = (uint32_t)(boff[b + 1] - off);
     }
+    const uint32_t nl = n <= kCap ? n : 0;
+#pragma unroll
+    for (int i = 0; i < kCapItems; ++i) {
+      const uint32_t idx = i * kCountThreads + tid;
+      v[i] = idx < nl ? rec[off + idx] : 0;
+    }
+  };
+
+  uint64_t v[kCapItems], vn[kCapItems];
+  uint64_t off, offn;
+  uint32_t n, nn;
+  uint64_t bkt = blockIdx.x;
+  load(bkt, off, n, v);
+  __syncthreads();
+  for (; bkt < nbuckets; bkt += gridDim.x) {
+    load(bkt + gridDim.x, offn, nn, vn);  // prefetch: in flight while this bucket is counted
+    if (n > maxb) maxb = n;
     if (n > kCap) {
       if (tid == 0) {
         const unsigned long long k = atomicAdd(&o.gstats[1], 1ull);
         o.ovf_list[k] = (uint32_t)bkt;
       }
-      continue;
-    }
-    // table size: power of two >= 2n (>= 2 slots per thread)
-    uint32_t T = 2 * kCountThreads;
-    while (T < 2 * n) T <<= 1;
-    const uint32_t tmask = T - 1;
-    uint64_t v[kCapItems];
+    } else if (n == 0) {
+      if (TABLE && tid == 0) o.bucket_nd[bkt] = 0;
+    } else {
+      // table size: power of two >= 2n (>= 2 slots per thread)
+      uint32_t T = 2 * kCountThreads;
+      while (T < 2 * n) T <<= 1;
+      const uint32_t tmask = T - 1;
+      for (uint32_t s = tid; s < T; s += kCountThreads) {
+        tkey[s] = EMPTY;
+        tcnt[s] = 0;
+      }
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kCapItems; ++i) {
-      const uint32_t idx = i * kCountThreads + tid;
-      v[i] = idx < n ? rec[off + idx] : 0;
-    }
-    for (uint32_t s = tid; s < T; s += kCountThreads) {
-      tkey[s] = EMPTY;
-      tcnt[s] = 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kCapItems; ++i) {
-      const uint32_t idx = i * kCountThreads + tid;
-      if (idx < n) {
-        const KT key = (KT)(v[i] & remmask);
-        uint32_t s = (uint32_t)key & tmask;
-        for (;;) {
-          const KT old = atomicCAS(&tkey[s], EMPTY, key);
-          if (old == EMPTY || old == key) {
-            atomicAdd(&tcnt[s], 1u);
-            break;
+      for (int i = 0; i < kCapItems; ++i) {
+        const uint32_t idx = i * kCountThreads + tid;
+        if (idx < n) {
+          const KT key = (KT)(v[i] & remmask);
+          uint32_t s = (uint32_t)key & tmask;
+          for (;;) {
+            const KT old = atomicCAS(&tkey[s], EMPTY, key);
+            if (old == EMPTY || old == key) {
+              atomicAdd(&tcnt[s], 1u);
+              break;
+            }
+            s = (s + 1) & tmask;
           }
-          s = (s + 1) & tmask;
         }
       }
-    }
-    __syncthreads();
-    // compact occupied slots to the front of the table (in place)
-    const uint32_t spt = T / kCountThreads;
-    KT ks[kSlotItems];
-    uint32_t cs[kSlotItems];
-    uint32_t occ = 0;
+      __syncthreads();
+      if (!TABLE) {
+        // spectrum only: every occupied slot is one distinct k-mer
+        for (uint32_t s = tid; s < T; s += kCountThreads) {
+          if (tkey[s] != EMPTY) {
+            spectrum_add(tcnt[s], lhist, o.ghist, o.hist_len);
+            ++nd_sum;
+          }
+        }
+      } else {
+        // compact occupied slots to the front of the table (in place)
+        const uint32_t spt = T / kCountThreads;
+        KT ks[kSlotItems];
+        uint32_t cs[kSlotItems];
+        uint32_t occ = 0;
 #pragma unroll
-    for (int i = 0; i < kSlotItems; ++i) {
-      if ((uint32_t)i < spt) {
-        const uint32_t s = tid * spt + i;
-        ks[i] = tkey[s];
-        cs[i] = tcnt[s];
-        occ += ks[i] != EMPTY;
-      }
-    }
-    uint32_t d;
-    uint32_t j = block_exclusive_scan<uint32_t>(occ, scan_sm, &d);  // ends with a barrier
+        for (int i = 0; i < kSlotItems; ++i) {
+          if ((uint32_t)i < spt) {
+            const uint32_t s = tid * spt + i;
+            ks[i] = tkey[s];
+            cs[i] = tcnt[s];
+            occ += ks[i] != EMPTY;
+          }
+        }
+        uint32_t d;
+        uint32_t j = block_exclusive_scan<uint32_t>(occ, scan_sm, &d);  // ends with a barrier
 #pragma unroll
-    for (int i = 0; i < kSlotItems; ++i) {
-      if ((uint32_t)i < spt && ks[i] != EMPTY) {
-        tkey[j] = ks[i];
-        tcnt[j] = cs[i];
-        ++j;
+        for (int i = 0; i < kSlotItems; ++i) {
+          if ((uint32_t)i < spt && ks[i] != EMPTY) {
+            tkey[j] = ks[i];
+            tcnt[j] = cs[i];
+            ++j;
+          }
+        }
+        __syncthreads();
+        const uint64_t prefix = v[0] & ~remmask;  // valid for tid < n; only such threads emit
+        for (uint32_t e = tid; e < d; e += kCountThreads) {
+          const KT key = tkey[e];
+          const uint32_t c = tcnt[e];
+          uint32_t r = 0;
+          for (uint32_t i = 0; i < d; ++i) r += tkey[i] < key;
+          o.tab_hash[off + r] = prefix | (uint64_t)key;
+          o.tab_cnt[off + r] = c;
+          spectrum_add(c, lhist, o.ghist, o.hist_len);
+        }
+        if (tid == 0) {
+          o.bucket_nd[bkt] = d;
+          nd_sum += d;
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
-    const uint64_t prefix = v[0] & ~remmask;  // valid for tid < n; only such threads emit
-    for (uint32_t e = tid; e < d; e += kCountThreads) {
-      const KT key = tkey[e];
-      const uint32_t c = tcnt[e];
-      if (TABLE) {
-        uint32_t r = 0;
-        for (uint32_t i = 0; i < d; ++i) r += tkey[i] < key;
-        o.tab_hash[off + r] = prefix | (uint64_t)key;
-        o.tab_cnt[off + r] = c;
-      }
-      spectrum_add(c, lhist, o.ghist, o.hist_len);
-    }
-    if (tid == 0) {
-      o.bucket_nd[bkt] = d;
-      nd_sum += d;
-    }
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kCapItems; ++i) v[i] = vn[i];
+    off = offn;
+    n = nn;
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kLdsHistBins ? o.hist_len : (uint64_t)kLdsHistBins;
   for (uint32_t i = tid; i < lim; i += kCountThreads)
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
-  if (tid == 0) {
-    atomicAdd(&o.gstats[0], nd_sum);
-    atomicMax(&o.gstats[2], maxb);
-  }
+  // distinct counts: per-thread partials (spectrum path) or thread 0 (table path)
+  for (int o2 = 32; o2 > 0; o2 >>= 1) nd_sum += __shfl_down(nd_sum, o2, 64);
+  if ((tid & 63) == 0 && nd_sum) atomicAdd(&o.gstats[0], nd_sum);
+  if (tid == 0) atomicMax(&o.gstats[2], maxb);
 }
 
 template <typename KT>
@@ -639,7 +732,7 @@ static int extract_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, uin
   APG_TRY(workspace_t(ctx, "x_omat", (uint64_t)xs.ndig * xs.G + 1, &omat));
   ReadsView rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   kbegin(ctx, "extract_scatter", dr->n_bytes + 16 * dr->n_reads + xs.total * 8);
-  k_extract_scatter<<<xs.G, kExtractThreads, xs.ndig * 8, ctx->stream>>>(rv, K, make_hashp(K), xs.dshift, xs.ndig,
+  k_extract_scatter<<<xs.G, kExtractThreads, 0, ctx->stream>>>(rv, K, make_hashp(K), xs.dshift, xs.ndig,
                                                                         omat, d_out);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
@@ -661,59 +754,63 @@ struct Seg {
 };
 
 // One partition level: every parent's segments -> ndig children per parent.
-// Writes device child offsets to d_boff (nparents*ndig + 1) and, if
-// host_boff, copies them to the host.
+// Writes the children's start offsets to d_child (nparents*ndig + 1) and, if
+// host_child, copies them to the host.
 static int part_level(apg_ctx* ctx, const uint64_t* src, uint64_t* dst, const std::vector<std::vector<Seg>>& parents,
-                      int shift, int bits, uint64_t n, uint64_t* d_boff, std::vector<uint64_t>* host_boff) {
+                      int shift, int bits, uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child) {
   const uint32_t ndig = 1u << bits;
   const uint64_t np = parents.size();
+  // ~24K chunks per level: enough workgroups, short count-matrix rows
+  const uint64_t chunk = std::max<uint64_t>(4 * kTile, ((n / 24576) + kTile - 1) / kTile * kTile);
   std::vector<Chunk> chunks;
-  std::vector<uint64_t> pbase(np);
-  std::vector<uint32_t> nch(np);
-  uint64_t mat = 0;
+  std::vector<uint32_t> prow(np + 1);
+  std::vector<uint64_t> pstart(np);
+  uint64_t pos = 0;
   for (uint64_t p = 0; p < np; ++p) {
-    const size_t first = chunks.size();
-    for (const Seg& s : parents[p])
-      for (uint64_t o = 0; o < s.len; o += kChunk)
-        chunks.push_back(Chunk{s.start + o, 0, (uint32_t)std::min<uint64_t>(kChunk, s.len - o), 0});
-    if (chunks.size() == first) chunks.push_back(Chunk{0, 0, 0, 0});  // every parent owns matrix columns
-    const uint32_t k = (uint32_t)(chunks.size() - first);
-    for (uint32_t i = 0; i < k; ++i) {
-      chunks[first + i].mat = mat + i;
-      chunks[first + i].stride = k;
+    prow[p] = (uint32_t)chunks.size();
+    pstart[p] = pos;
+    for (const Seg& s : parents[p]) {
+      if (s.len >= (1ull << 32)) {
+        set_error("part_level: parent group exceeds 2^32 records");
+        return APG_E_UNSUPPORTED;
+      }
+      for (uint64_t o = 0; o < s.len; o += chunk)
+        chunks.push_back(Chunk{s.start + o, (uint32_t)std::min<uint64_t>(chunk, s.len - o), (uint32_t)p});
+      pos += s.len;
     }
-    pbase[p] = mat;
-    nch[p] = k;
-    mat += (uint64_t)k * ndig;
   }
+  prow[np] = (uint32_t)chunks.size();
+  if (chunks.empty()) chunks.push_back(Chunk{0, 0, 0});  // keep launches non-empty
+  const uint64_t nrow = chunks.size();
   Chunk* d_chunks = nullptr;
-  uint64_t *d_pbase = nullptr, *omat = nullptr;
-  uint32_t *d_nch = nullptr, *cmat = nullptr;
-  APG_TRY(workspace_t(ctx, "p_chunks", chunks.size(), &d_chunks));
-  APG_TRY(workspace_t(ctx, "p_pbase", np, &d_pbase));
-  APG_TRY(workspace_t(ctx, "p_nch", np, &d_nch));
-  APG_TRY(workspace_t(ctx, "p_cmat", mat, &cmat));
-  APG_TRY(workspace_t(ctx, "p_omat", mat + 1, &omat));
-  APG_CHECK_HIP(hipMemcpyAsync(d_chunks, chunks.data(), chunks.size() * sizeof(Chunk), hipMemcpyHostToDevice,
-                               ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(d_pbase, pbase.data(), np * 8, hipMemcpyHostToDevice, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(d_nch, nch.data(), np * 4, hipMemcpyHostToDevice, ctx->stream));
-  const uint32_t nchunks = (uint32_t)chunks.size();
-  kbegin(ctx, "part_count", n * 8 + mat * 4);
-  k_part_count<<<nchunks, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, cmat);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  APG_TRY(scan_u32_u64(ctx, cmat, mat, omat, "p"));
-  kbegin(ctx, "part_scatter", n * 16 + mat * 8);
-  k_part_scatter<<<nchunks, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, omat, dst);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
+  uint64_t* d_pstart = nullptr;
+  uint32_t *d_prow = nullptr, *cmat = nullptr, *pre = nullptr;
+  APG_TRY(workspace_t(ctx, "p_chunks", nrow, &d_chunks));
+  APG_TRY(workspace_t(ctx, "p_prow", np + 1, &d_prow));
+  APG_TRY(workspace_t(ctx, "p_pstart", np, &d_pstart));
+  APG_TRY(workspace_t(ctx, "p_cmat", nrow * ndig, &cmat));
+  APG_TRY(workspace_t(ctx, "p_pre", nrow * ndig, &pre));
+  APG_CHECK_HIP(hipMemcpyAsync(d_chunks, chunks.data(), nrow * sizeof(Chunk), hipMemcpyHostToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(d_prow, prow.data(), (np + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(d_pstart, pstart.data(), np * 8, hipMemcpyHostToDevice, ctx->stream));
   const uint64_t nb = np * ndig;
-  k_bucket_offsets<<<(nb + 1 + 255) / 256, 256, 0, ctx->stream>>>(omat, d_pbase, d_nch, np, ndig, n, d_boff);
+  APG_CHECK_HIP(hipMemcpyAsync(d_child + nb, &n, 8, hipMemcpyHostToDevice, ctx->stream));
+  kbegin(ctx, "part_count", n * 8 + nrow * ndig * 4);
+  k_part_count<<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, cmat);
+  kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
-  if (host_boff) {
-    host_boff->resize(nb + 1);
-    APG_CHECK_HIP(hipMemcpyAsync(host_boff->data(), d_boff, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  kbegin(ctx, "part_scan", nrow * ndig * 12 + nb * 8);
+  k_part_scan<<<(uint32_t)np, kPartThreads * kScanGroups, 0, ctx->stream>>>(cmat, d_prow, d_pstart, ndig, pre,
+                                                                             d_child);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  kbegin(ctx, "part_scatter", n * 16 + nrow * ndig * 4);
+  k_part_scatter<<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, pre, d_child, dst);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  if (host_child) {
+    host_child->resize(nb + 1);
+    APG_CHECK_HIP(hipMemcpyAsync(host_child->data(), d_child, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
   }
   return APG_OK;
