@@ -300,18 +300,25 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* _
   const uint32_t tid = threadIdx.x;
   const uint64_t dmask = ndig - 1;
   if (tid < ndig) cur[tid] = child[(uint64_t)c.parent * ndig + tid] + pre[(uint64_t)blockIdx.x * ndig + tid];
+  const uint64_t* base = rec + c.start;
+  uint64_t v[kPartItems], vn[kPartItems];
+#pragma unroll
+  for (int i = 0; i < kPartItems; ++i) {
+    const uint32_t idx = i * kPartThreads + tid;
+    v[i] = idx < c.len ? base[idx] : 0;
+  }
   for (uint32_t t0 = 0; t0 < c.len; t0 += kTile) {
     const uint32_t tn = min((uint32_t)kTile, c.len - t0);
-    lcnt[tid] = 0;
-    __syncthreads();
-    uint64_t v[kPartItems];
-    uint32_t pos[kPartItems];
-    const uint64_t* p = rec + c.start + t0;
+    // prefetch the next tile: its loads stay in flight through this tile's work
+    const uint32_t t1 = t0 + kTile;
 #pragma unroll
     for (int i = 0; i < kPartItems; ++i) {
       const uint32_t idx = i * kPartThreads + tid;
-      v[i] = idx < tn ? p[idx] : 0;
+      vn[i] = t1 + idx < c.len ? base[t1 + idx] : 0;
     }
+    lcnt[tid] = 0;
+    __syncthreads();
+    uint32_t pos[kPartItems];
 #pragma unroll
     for (int i = 0; i < kPartItems; ++i) {
       const uint32_t idx = i * kPartThreads + tid;
@@ -335,7 +342,8 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* _
     }
     __syncthreads();
     if (tid < ndig) cur[tid] += lcnt[tid];
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) v[i] = vn[i];
   }
 }
 
@@ -349,9 +357,9 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const uint64_t* _
 // insertion order.  Counts are binned into the spectrum.
 // ------------------------------------------------------------------------
 constexpr int kCountThreads = 512;
-constexpr uint32_t kCap = 4096;            // max records of an LDS-counted bucket
-constexpr uint32_t kTabMax = 2 * kCap;     // table slots (load factor <= 0.5)
-constexpr int kCapItems = kCap / kCountThreads;
+constexpr uint32_t kCap = 4095;            // max records of an LDS-counted bucket
+constexpr uint32_t kTabMax = 4096;         // table slots: > n >= distinct, so a bucket always fits
+constexpr int kCapItems = (kCap + kCountThreads - 1) / kCountThreads;
 constexpr int kSlotItems = kTabMax / kCountThreads;
 
 template <typename KT>
@@ -400,14 +408,9 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
   for (uint32_t i = tid; i < kLdsHistBins; i += kCountThreads) lhist[i] = 0;
   unsigned long long nd_sum = 0, maxb = 0;
 
-  // Records of bucket `b` into registers (n <= kCap; larger buckets are not loaded).
-  auto load = [&](uint64_t b, uint64_t& off, uint32_t& n, uint64_t (&v)[kCapItems]) {
-    n = 0;
-    off = 0;
-    if (b < nbuckets) {
-      off = boff[b];
-      n = (uint32_t)(boff[b + 1] - off);
-    }
+  // Records of bucket `b` (offsets off/n already known) into registers
+  // (n <= kCap; larger buckets are not loaded).
+  auto load = [&](uint64_t off, uint32_t n, uint64_t (&v)[kCapItems]) {
     const uint32_t nl = n <= kCap ? n : 0;
 #pragma unroll
     for (int i = 0; i < kCapItems; ++i) {
@@ -416,14 +419,27 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
     }
   };
 
+  auto bounds = [&](uint64_t b, uint64_t& off, uint32_t& n) {
+    off = 0;
+    n = 0;
+    if (b < nbuckets) {
+      off = boff[b];
+      n = (uint32_t)(boff[b + 1] - off);
+    }
+  };
   uint64_t v[kCapItems], vn[kCapItems];
-  uint64_t off, offn;
-  uint32_t n, nn;
+  uint64_t off, offn, off2;
+  uint32_t n, nn, n2;
   uint64_t bkt = blockIdx.x;
-  load(bkt, off, n, v);
+  bounds(bkt, off, n);
+  bounds(bkt + gridDim.x, offn, nn);
+  load(off, n, v);
   __syncthreads();
   for (; bkt < nbuckets; bkt += gridDim.x) {
-    load(bkt + gridDim.x, offn, nn, vn);  // prefetch: in flight while this bucket is counted
+    // pipeline: records of the next bucket and offsets of the one after are
+    // in flight while this bucket is counted
+    load(offn, nn, vn);
+    bounds(bkt + 2 * (uint64_t)gridDim.x, off2, n2);
     if (n > maxb) maxb = n;
     if (n > kCap) {
       if (tid == 0) {
@@ -433,9 +449,10 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
     } else if (n == 0) {
       if (TABLE && tid == 0) o.bucket_nd[bkt] = 0;
     } else {
-      // table size: power of two >= 2n (>= 2 slots per thread)
+      // table size: power of two > n (>= 2 slots per thread); the load factor
+      // is distinct/T, typically ~0.2 at genomic coverage
       uint32_t T = 2 * kCountThreads;
-      while (T < 2 * n) T <<= 1;
+      while (T <= n) T <<= 1;
       const uint32_t tmask = T - 1;
       for (uint32_t s = tid; s < T; s += kCountThreads) {
         tkey[s] = EMPTY;
@@ -514,6 +531,8 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
     for (int i = 0; i < kCapItems; ++i) v[i] = vn[i];
     off = offn;
     n = nn;
+    offn = off2;
+    nn = n2;
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kLdsHistBins ? o.hist_len : (uint64_t)kLdsHistBins;
