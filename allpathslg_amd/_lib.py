@@ -64,6 +64,30 @@ class apg_kstats(C.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
 
 
+class apg_pc_params(C.Structure):
+    _fields_ = [
+        ("K", C.c_int32),
+        ("min_solid", C.c_uint32),
+        ("max_q_suspect", C.c_uint32),
+        ("n_cycles", C.c_uint32),
+        ("reserved", C.c_uint64 * 4),
+    ]
+
+
+class apg_pc_stats(C.Structure):
+    _fields_ = [
+        ("n_suspect", C.c_uint64),
+        ("n_corrected", C.c_uint64),
+        ("n_ambiguous", C.c_uint64),
+        ("n_uncorrectable", C.c_uint64),
+        ("n_solid", C.c_uint64),
+        ("reserved", C.c_uint64 * 3),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
+
+
 class apg_synth_params(C.Structure):
     _fields_ = [
         ("genome_len", C.c_uint64),
@@ -114,6 +138,10 @@ SIGNATURES = {
         C.c_int,
         [_P, C.c_void_p, _u64p, C.c_int, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats)],
     ),
+    "apg_pc_defaults": (None, [C.POINTER(apg_pc_params)]),
+    "apg_precorrect": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_pc_params), _u8p, _u8p, C.POINTER(apg_pc_stats)]),
+    "apg_precorrect_dev": (C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
+    "apg_reads_download": (C.c_int, [_P, _P, _u8p, _u8p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),

@@ -194,6 +194,8 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
   APG_REQUIRE(ctx && r && out, "apg_reads_upload: NULL argument");
   APG_REQUIRE(r->n_reads == 0 || (r->base_off && r->byte_off && r->packed),
               "apg_reads_upload: missing base_off/byte_off/packed");
+  APG_REQUIRE(r->n_reads == 0 || (r->base_off[0] == 0 && r->byte_off[0] == 0),
+              "apg_reads_upload: base_off[0] and byte_off[0] must be 0");
   *out = nullptr;
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   auto* d = new (std::nothrow) apg_dreads();

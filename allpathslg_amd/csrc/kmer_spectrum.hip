@@ -29,6 +29,7 @@
 
 #include "apg_core.hpp"
 #include "kmer_common.hpp"
+#include "kmer_internal.hpp"
 
 namespace apg {
 
@@ -758,16 +759,6 @@ static int extract_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, uin
   return APG_OK;
 }
 
-struct CountResult {
-  uint64_t* rec = nullptr;        // final records; tab_hash in place (table mode)
-  uint32_t* tab_cnt = nullptr;
-  uint32_t* bucket_nd = nullptr;
-  uint64_t* boff = nullptr;
-  uint64_t nbuckets = 0;
-  uint64_t n_records = 0;
-  apg_kstats st{};
-};
-
 struct Seg {
   uint64_t start, len;
 };
@@ -974,7 +965,7 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   return APG_OK;
 }
 
-static int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
+int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
                          CountResult* res) {
   APG_REQUIRE(ctx && dr, "spectrum: NULL ctx/reads");
   APG_REQUIRE(K >= 1 && K <= 32, "spectrum: K must be in [1, 32] for the 64-bit path");

@@ -12,7 +12,7 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from ._lib import apg_config, apg_kstats, check, lib
+from ._lib import apg_config, apg_kstats, apg_pc_params, apg_pc_stats, check, lib
 from .reads import ReadSet
 
 _u64p = C.POINTER(C.c_uint64)
@@ -150,6 +150,41 @@ class Context:
             L.apg_free(C.cast(kp, C.c_void_p))
             L.apg_free(C.cast(cp, C.c_void_p))
         return keys, counts, st.as_dict()
+
+    # -- error correction ------------------------------------------------------
+    @staticmethod
+    def pc_params(K: int = 24, min_solid: int = 3, max_q_suspect: int = 20, n_cycles: int = 1) -> apg_pc_params:
+        p = apg_pc_params()
+        lib().apg_pc_defaults(C.byref(p))
+        p.K, p.min_solid, p.max_q_suspect, p.n_cycles = K, min_solid, max_q_suspect, n_cycles
+        return p
+
+    def precorrect(self, reads, K: int = 24, min_solid: int = 3, max_q_suspect: int = 20, n_cycles: int = 1):
+        """PreCorrect (n_cycles=1) / FindErrors (n_cycles=2), SURVEY §A.4.
+        ReadSet -> (corrected ReadSet, stats); DeviceReads -> corrected in
+        place, returns (same DeviceReads, stats)."""
+        p = self.pc_params(K, min_solid, max_q_suspect, n_cycles)
+        st = apg_pc_stats()
+        if isinstance(reads, DeviceReads):
+            check(lib().apg_precorrect_dev(self._h, reads.handle, C.byref(p), C.byref(st)), "apg_precorrect_dev")
+            return reads, st.as_dict()
+        if reads.quals is None:
+            raise ValueError("precorrect needs qualities")
+        pk = reads.packed.copy()
+        q = reads.quals.copy()
+        r = reads.c_struct()
+        check(lib().apg_precorrect(self._h, C.byref(r), C.byref(p), pk.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                   q.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(st)), "apg_precorrect")
+        return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), st.as_dict()
+
+    def download(self, dreads: DeviceReads) -> ReadSet:
+        r = dreads.reads
+        pk = np.zeros_like(r.packed)
+        q = np.zeros_like(r.quals) if r.quals is not None else None
+        check(lib().apg_reads_download(self._h, dreads.handle, pk.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                       q.ctypes.data_as(C.POINTER(C.c_uint8)) if q is not None else None),
+              "apg_reads_download")
+        return ReadSet(r.base_off.copy(), r.byte_off.copy(), pk, q)
 
     # -- sharded (multi-GPU) stages ------------------------------------------
     def shard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:

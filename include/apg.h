@@ -152,6 +152,48 @@ int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv,
                        apg_kstats* stats);
 
 /* ------------------------------------------------------------------------- */
+/* Read error correction (restated; semantics unpinned).         */
+/* Replaces module PreCorrect ([R:M-L] src/PreCorrect.cc; n_cycles = 1) and  */
+/* the spectrum part of FindErrors ([R:M] src/FindErrors.cc,                  */
+/* naif_kmer/KernelErrorFinder; n_cycles = 2, recounting between passes).    */
+/*                                                                            */
+/* Solid = canonical K-mer with count >= min_solid over the whole read set.  */
+/* Per read, positions left to right on the current (partly corrected) read: */
+/* a base with Q < max_q_suspect whose every covering K-mer is weak is       */
+/* suspect; of the 3 alternatives (A<C<G<T) the unique one making every      */
+/* covering K-mer solid replaces it and its Q becomes min(Q of neighbours);  */
+/* ambiguous / no candidate: left unchanged.  Counts are fixed within a pass.*/
+/* ------------------------------------------------------------------------- */
+typedef struct apg_pc_params {
+  int32_t K;               /* default 24 */
+  uint32_t min_solid;      /* default 3 */
+  uint32_t max_q_suspect;  /* default 20 */
+  uint32_t n_cycles;       /* 1 = PreCorrect, 2 = FindErrors */
+  uint64_t reserved[4];
+} apg_pc_params;
+
+typedef struct apg_pc_stats {
+  uint64_t n_suspect;       /* suspect positions examined (summed over cycles) */
+  uint64_t n_corrected;
+  uint64_t n_ambiguous;     /* > 1 alternative made every covering K-mer solid */
+  uint64_t n_uncorrectable; /* no alternative did */
+  uint64_t n_solid;         /* solid K-mers of the last cycle */
+  uint64_t reserved[3];
+} apg_pc_stats;
+
+void apg_pc_defaults(apg_pc_params* p);
+/* Host buffers: out_packed has reads->byte_off[n] bytes, out_quals
+ * reads->base_off[n] bytes; reads->quals is required. */
+int apg_precorrect(apg_ctx* ctx, const apg_reads* reads, const apg_pc_params* p,
+                   uint8_t* out_packed, uint8_t* out_quals, apg_pc_stats* stats);
+/* In place on a device read set (which must carry qualities). */
+int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
+                       apg_pc_stats* stats);
+/* Copy a device read set's (possibly corrected) bases/quals back to host
+ * buffers of the upload's sizes (quals may be NULL). */
+int apg_reads_download(apg_ctx* ctx, const apg_dreads* reads, uint8_t* packed, uint8_t* quals);
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */
 /* insert N(mean, sd), FR orientation, substitution error rate rising        */
 /* linearly err_lo -> err_hi along the read; Q40 on correct bases, Q2..20 on */

@@ -44,6 +44,9 @@ def lib() -> C.CDLL:
         L.ork_kmer_count.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, C.POINTER(_u64p), C.POINTER(_u32p)]
         L.ork_spectrum.restype = None
         L.ork_spectrum.argtypes = [_u32p, C.c_uint64, _u64p, C.c_uint64]
+        L.ork_precorrect.restype = C.c_int
+        L.ork_precorrect.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, _u8p, C.c_int, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, _u64p]
         L.ork_free.restype = None
         L.ork_free.argtypes = [C.c_void_p]
         _lib = L
@@ -103,3 +106,19 @@ def spectrum_from_counts(counts: np.ndarray, hist_len: int) -> np.ndarray:
 def kmer_spectrum(reads, K: int, hist_len: int = 1 << 16) -> np.ndarray:
     _, c = kmer_count(reads, K)
     return spectrum_from_counts(c, hist_len)
+
+
+def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1):
+    """Corrected copy of `reads` (needs quals) and stats dict."""
+    from allpathslg_amd.reads import ReadSet  # plain data container
+
+    pk = reads.packed.copy()
+    q = reads.quals.copy()
+    st = np.zeros(5, dtype=np.uint64)
+    rc = lib().ork_precorrect(reads.n_reads, reads.base_off.ctypes.data_as(_u64p), reads.byte_off.ctypes.data_as(_u64p),
+                              pk.ctypes.data_as(_u8p), q.ctypes.data_as(_u8p), K, min_solid, max_q, n_cycles,
+                              st.ctypes.data_as(_u64p))
+    if rc:
+        raise MemoryError("oracle precorrect failed")
+    keys = ["n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"]
+    return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), {k: int(v) for k, v in zip(keys, st)}

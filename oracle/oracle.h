@@ -14,5 +14,7 @@ uint64_t ork_kmer_count(uint64_t n_reads, const uint64_t* base_off, const uint64
                         const uint8_t* packed, int K, uint64_t** hashes, uint32_t** counts);
 void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t hist_len);
 void ork_free(void* p);
+int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                   uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint32_t n_cycles, uint64_t* stats);
 
 #endif

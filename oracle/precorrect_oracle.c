@@ -1,0 +1,112 @@
+/*
+ * oracle/precorrect_oracle.c — CPU restatement of PreCorrect / FindErrors
+ * (SURVEY.md §A.4 as pinned in include/apg.h).  TEST INFRASTRUCTURE ONLY.
+ *
+ * PARITY UNPINNED: the reference snapshot is empty; the recalled
+ * modules are [R:M-L] src/PreCorrect.cc and [R:M] src/FindErrors.cc /
+ * naif_kmer/KernelErrorFinder (grep targets, no line citations possible).
+ * The rule restated here: solid = canonical K-mer count >= min_solid; per
+ * read, left to right on the current read, a base with Q < max_q whose every
+ * covering K-mer is weak is suspect; the unique alternative (A<C<G<T) making
+ * every covering K-mer solid replaces it, Q := min(Q of neighbours).
+ * Solid lookup: the sorted (hash, count) table from ork_kmer_count, binary
+ * searched — deliberately a different structure from the GPU hash table.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+static int get_base(const uint8_t* rd, uint32_t i) { return (rd[i >> 2] >> (2 * (i & 3))) & 3; }
+
+static uint64_t kmer_hash_at(const uint8_t* rd, uint32_t j, int K, uint32_t p, int alt) {
+  const uint64_t m = K >= 32 ? ~0ull : ((1ull << (2 * K)) - 1);
+  uint64_t fw = 0, rc = 0;
+  for (int t = 0; t < K; ++t) {
+    const uint32_t i = j + (uint32_t)t;
+    const uint64_t b = (i == p) ? (uint64_t)alt : (uint64_t)get_base(rd, i);
+    fw = ((fw << 2) | b) & m;
+    rc = (rc >> 2) | ((3 - b) << (2 * K - 2));
+  }
+  return ork_hash(K, fw < rc ? fw : rc);
+}
+
+/* binary search of h in the ascending solid-hash array */
+static int is_solid(const uint64_t* solid, uint64_t ns, uint64_t h) {
+  uint64_t lo = 0, hi = ns;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (solid[mid] < h)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo < ns && solid[lo] == h;
+}
+
+static int pass(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint64_t* stats) {
+  uint64_t *h = NULL;
+  uint32_t* c = NULL;
+  const uint64_t nd = ork_kmer_count(n_reads, base_off, byte_off, packed, K, &h, &c);
+  if (nd == UINT64_MAX) return -1;
+  uint64_t ns = 0;
+  for (uint64_t i = 0; i < nd; ++i)
+    if (c[i] >= min_solid) h[ns++] = h[i]; /* stays ascending */
+  free(c);
+  stats[4] = ns;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    const uint32_t L = (uint32_t)(base_off[r + 1] - base_off[r]);
+    if (L < (uint32_t)K) continue;
+    uint8_t* rd = packed + byte_off[r];
+    uint8_t* q = quals + base_off[r];
+    for (uint32_t p = 0; p < L; ++p) {
+      if (q[p] >= maxq) continue;
+      const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - (uint32_t)K : 0;
+      const uint32_t jhi = p < L - (uint32_t)K ? p : L - (uint32_t)K;
+      int weak = 1;
+      for (uint32_t j = jlo; j <= jhi && weak; ++j)
+        if (is_solid(h, ns, kmer_hash_at(rd, j, K, 0xffffffffu, 0))) weak = 0;
+      if (!weak) continue;
+      stats[0]++;
+      const int orig = get_base(rd, p);
+      int ncand = 0, cand = 0;
+      for (int alt = 0; alt < 4; ++alt) {
+        if (alt == orig) continue;
+        int ok = 1;
+        for (uint32_t j = jlo; j <= jhi && ok; ++j)
+          if (!is_solid(h, ns, kmer_hash_at(rd, j, K, p, alt))) ok = 0;
+        if (ok) {
+          ++ncand;
+          cand = alt;
+        }
+      }
+      if (ncand == 1) {
+        const int sh = 2 * (int)(p & 3);
+        rd[p >> 2] = (uint8_t)((rd[p >> 2] & ~(3u << sh)) | ((unsigned)cand << sh));
+        uint32_t nq = 255;
+        if (p > 0 && q[p - 1] < nq) nq = q[p - 1];
+        if (p + 1 < L && q[p + 1] < nq) nq = q[p + 1];
+        q[p] = (uint8_t)nq;
+        stats[1]++;
+      } else if (ncand > 1) {
+        stats[2]++;
+      } else {
+        stats[3]++;
+      }
+    }
+  }
+  free(h);
+  return 0;
+}
+
+/* In place.  stats[0..4] = suspect, corrected, ambiguous, uncorrectable,
+ * solid-in-last-cycle (summed over cycles except [4]). */
+int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                   uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint32_t n_cycles, uint64_t* stats) {
+  memset(stats, 0, 5 * sizeof(uint64_t));
+  for (uint32_t c = 0; c < n_cycles; ++c)
+    if (pass(n_reads, base_off, byte_off, packed, quals, K, min_solid, maxq, stats)) return -1;
+  return 0;
+}

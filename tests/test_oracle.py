@@ -113,3 +113,51 @@ def test_oracle_against_golden():
         assert np.array_equal(h, z[f"hash_k{K}"])
         assert np.array_equal(c, z[f"count_k{K}"])
         assert np.array_equal(oracle.spectrum_from_counts(c, 1 << 16)[:4096], z[f"spec_k{K}"])
+
+
+def test_precorrect_kat_single_substitutions():
+    """substitutions at known positions (low Q) under ~50x
+    coverage are corrected back to the genome."""
+    from allpathslg_amd import synth_genome
+
+    rng = np.random.default_rng(77)
+    G, L = 4000, 100
+    g = synth_genome(G, 99)
+    starts = rng.integers(0, G - L + 1, size=2000)
+    seqs, quals, truth, errpos = [], [], [], []
+    for i, s in enumerate(starts):
+        r = g[s : s + L].copy()
+        q = np.full(L, 40, dtype=np.uint8)
+        truth.append(r.copy())
+        if i % 10 == 0:
+            p = int(rng.integers(0, L))
+            r[p] = (r[p] + 1 + rng.integers(0, 3)) % 4
+            q[p] = 10
+            errpos.append((i, p))
+        seqs.append(r)
+        quals.append(q)
+    reads = ReadSet.from_sequences(seqs, quals)
+    fixed, st = oracle.precorrect(reads, K=24)
+    assert st["n_corrected"] == len(errpos)
+    for i in range(reads.n_reads):
+        assert np.array_equal(fixed.read(i), truth[i])
+    for i, p in errpos:
+        assert fixed.quals[int(fixed.base_off[i]) + p] == 40
+
+
+def test_precorrect_leaves_high_quality_and_is_idempotent():
+    from allpathslg_amd import synth_genome, synth_reads
+
+    g = synth_genome(30_000, 5)
+    reads = synth_reads(g, 6000, seed=6)
+    fixed, st = oracle.precorrect(reads, K=24)
+    assert st["n_corrected"] > 0
+    hq = reads.quals >= 20
+    assert np.array_equal(fixed.quals[hq], reads.quals[hq])
+    # bases at high-quality positions never change
+    for i in range(0, reads.n_reads, 97):
+        a, b = reads.read(i), fixed.read(i)
+        qq = reads.quals[int(reads.base_off[i]) : int(reads.base_off[i + 1])]
+        assert np.array_equal(a[qq >= 20], b[qq >= 20])
+    again, st2 = oracle.precorrect(fixed, K=24)
+    assert st2["n_corrected"] <= st["n_corrected"] // 10
