@@ -88,6 +88,51 @@ class apg_pc_stats(C.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
 
 
+class apg_unipath_params(C.Structure):
+    _fields_ = [("K", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint64 * 4)]
+
+
+class apg_unipath_stats(C.Structure):
+    _fields_ = [
+        ("n_instances", C.c_uint64),
+        ("n_nodes", C.c_uint64),
+        ("n_links", C.c_uint64),
+        ("n_cycles_cut", C.c_uint64),
+        ("n_unipaths", C.c_uint64),
+        ("n_vertices", C.c_uint64),
+        ("n_intervals", C.c_uint64),
+        ("max_len", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
+class apg_unipath_graph(C.Structure):
+    _fields_ = [
+        ("K", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("n_nodes", C.c_uint64),
+        ("n_unipaths", C.c_uint64),
+        ("len", C.POINTER(C.c_uint64)),
+        ("id_base", C.POINTER(C.c_uint64)),
+        ("rc", C.POINTER(C.c_uint64)),
+        ("ub_off", C.POINTER(C.c_uint64)),
+        ("unibases", C.POINTER(C.c_uint8)),
+        ("n_vertices", C.c_uint64),
+        ("frm", C.POINTER(C.c_uint64)),
+        ("to", C.POINTER(C.c_uint64)),
+        ("n_reads", C.c_uint64),
+        ("path_off", C.POINTER(C.c_uint64)),
+        ("n_intervals", C.c_uint64),
+        ("path_start", C.POINTER(C.c_uint64)),
+        ("path_len", C.POINTER(C.c_uint64)),
+    ]
+
+
+APG_UNIPATH_READ_PATHS = 1
+
+
 class apg_synth_params(C.Structure):
     _fields_ = [
         ("genome_len", C.c_uint64),
@@ -142,6 +187,17 @@ SIGNATURES = {
     "apg_precorrect": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_pc_params), _u8p, _u8p, C.POINTER(apg_pc_stats)]),
     "apg_precorrect_dev": (C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
     "apg_reads_download": (C.c_int, [_P, _P, _u8p, _u8p]),
+    "apg_unipath_defaults": (None, [C.POINTER(apg_unipath_params)]),
+    "apg_unipaths": (
+        C.c_int,
+        [_P, C.POINTER(apg_reads), C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),
+         C.POINTER(apg_unipath_stats)],
+    ),
+    "apg_unipaths_dev": (
+        C.c_int,
+        [_P, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph), C.POINTER(apg_unipath_stats)],
+    ),
+    "apg_unipath_graph_free": (None, [C.POINTER(apg_unipath_graph)]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),

@@ -56,17 +56,28 @@ void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes) {
   p.bytes = bytes;
   p.a = take_event(ctx);
   p.b = take_event(ctx);
+  p.closed = false;
   (void)hipEventRecord(p.a, ctx->stream);
   ctx->pending.push_back(p);
 }
 
 void kend(apg_ctx* ctx) {
-  if (!ctx->timing || ctx->pending.empty()) return;
-  (void)hipEventRecord(ctx->pending.back().b, ctx->stream);
+  if (!ctx->timing) return;
+  for (auto it = ctx->pending.rbegin(); it != ctx->pending.rend(); ++it)
+    if (!it->closed) {  // innermost open bracket
+      (void)hipEventRecord(it->b, ctx->stream);
+      it->closed = true;
+      return;
+    }
 }
 
 int kflush(apg_ctx* ctx) {
+  std::vector<apg_ctx::Pending> open;
   for (auto& p : ctx->pending) {
+    if (!p.closed) {  // still bracketing work: keep for a later flush
+      open.push_back(p);
+      continue;
+    }
     float ms = 0;
     APG_CHECK_HIP(hipEventSynchronize(p.b));
     APG_CHECK_HIP(hipEventElapsedTime(&ms, p.a, p.b));
@@ -81,7 +92,7 @@ int kflush(apg_ctx* ctx) {
     ctx->event_pool.push_back(p.a);
     ctx->event_pool.push_back(p.b);
   }
-  ctx->pending.clear();
+  ctx->pending.swap(open);
   return APG_OK;
 }
 

@@ -89,6 +89,7 @@ struct apg_ctx {
     std::string name;
     hipEvent_t a, b;
     uint64_t bytes;
+    bool closed;
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;

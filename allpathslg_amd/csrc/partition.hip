@@ -1,0 +1,298 @@
+// partition.hip — the device-wide scan and the LDS-staged hash-partition
+// level shared by the k-mer spectrum (8-byte records) and the unipath
+// builder (32-byte KRec records).  See partition.hpp.
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "apg_core.hpp"
+#include "kmer_common.hpp"
+#include "partition.hpp"
+
+namespace apg {
+
+// ------------------------------------------------------------------------
+// scan: u32 counts[n] -> u64 exclusive offsets[n+1] (offsets[n] = total)
+// ------------------------------------------------------------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__global__ void __launch_bounds__(kScanThreads) k_scan_tiles(const uint32_t* __restrict__ in, uint64_t n,
+                                                             uint64_t* __restrict__ tsum) {
+  __shared__ uint64_t sm[32];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i)
+    if (base + i < n) s += in[base + i];
+  uint64_t tot;
+  block_exclusive_scan<uint64_t>(s, sm, &tot);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_tsum(uint64_t* __restrict__ tsum, uint64_t nt) {
+  __shared__ uint64_t sm[32];
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < nt; b += blockDim.x) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t v = i < nt ? tsum[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan<uint64_t>(v, sm, &tot);
+    if (i < nt) tsum[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) tsum[nt] = carry;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_scan_apply(const uint32_t* __restrict__ in, uint64_t n,
+                                                             const uint64_t* __restrict__ tsum,
+                                                             uint64_t* __restrict__ out, uint64_t nt) {
+  __shared__ uint64_t sm[32];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t tot;
+  uint64_t run = block_exclusive_scan<uint64_t>(s, sm, &tot) + tsum[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tsum[nt];
+}
+
+int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out, const char* tag) {
+  const uint64_t nt = std::max<uint64_t>(1, (n + kScanTile - 1) / kScanTile);
+  uint64_t* tsum = nullptr;
+  APG_TRY(workspace_t(ctx, (std::string("scan_tsum_") + tag).c_str(), nt + 1, &tsum));
+  kbegin(ctx, "scan", n * 4 * 2 + (n + 1) * 8);
+  k_scan_tiles<<<nt, kScanThreads, 0, ctx->stream>>>(d_in, n, tsum);
+  k_scan_tsum<<<1, 1024, 0, ctx->stream>>>(tsum, nt);
+  k_scan_apply<<<nt, kScanThreads, 0, ctx->stream>>>(d_in, n, tsum, d_out, nt);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
+// ------------------------------------------------------------------------
+// Stage B: partition levels.  Records of each parent group are split by the
+// next `bits` (<= 8) hash bits.  Chunks (runs of records inside one parent)
+// are counted into a row-major [chunk][digit] matrix (one coalesced row per
+// chunk); a per-parent column scan turns it into each chunk's starting offset
+// inside every child, and the children's starts.  The scatter stages a
+// kTile-record tile in LDS sorted by digit, so each wave writes contiguous
+// per-child runs instead of 8-byte scattered stores.
+// ------------------------------------------------------------------------
+constexpr int kPartThreads = 256;
+constexpr int kScanGroups = 4;                    // 1024-thread column scan
+
+struct Chunk {
+  uint64_t start;   // first record
+  uint32_t len;     // records
+  uint32_t parent;  // parent group
+};
+
+template <typename R>
+struct PartGeom {
+  static constexpr int items = (32768 / (int)sizeof(R)) / kPartThreads;  // 32 KiB LDS tile
+  static constexpr int tile = items * kPartThreads;
+};
+
+template <typename R>
+__global__ void __launch_bounds__(kPartThreads) k_part_count(const R* __restrict__ rec,
+                                                             const Chunk* __restrict__ ch, int shift, uint32_t ndig,
+                                                             uint32_t* __restrict__ cmat) {
+  __shared__ uint32_t hist[256];
+  const Chunk c = ch[blockIdx.x];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t dmask = ndig - 1;
+  const R* p = rec + c.start;
+  for (uint32_t i = threadIdx.x; i < c.len; i += blockDim.x) atomicAdd(&hist[(rkey(p[i]) >> shift) & dmask], 1u);
+  __syncthreads();
+  if (threadIdx.x < ndig) cmat[(uint64_t)blockIdx.x * ndig + threadIdx.x] = hist[threadIdx.x];
+}
+
+// One workgroup per parent: pre[row][d] = sum of column d over the parent's
+// earlier rows; child[p*ndig + d] = pstart[p] + sum_{d' < d} column total(d').
+__global__ void __launch_bounds__(kPartThreads* kScanGroups) k_part_scan(const uint32_t* __restrict__ cmat,
+                                                                         const uint32_t* __restrict__ prow,
+                                                                         const uint64_t* __restrict__ pstart,
+                                                                         uint32_t ndig, uint32_t* __restrict__ pre,
+                                                                         uint64_t* __restrict__ child) {
+  __shared__ uint32_t gsum[kScanGroups][256];
+  __shared__ unsigned long long scan_sm[64];
+  const uint32_t p = blockIdx.x, tid = threadIdx.x, d = tid & 255, g = tid >> 8;
+  const uint32_t r0 = prow[p], r1 = prow[p + 1], nr = r1 - r0;
+  const uint32_t q = (nr + kScanGroups - 1) / kScanGroups;
+  const uint32_t a = min(r1, r0 + g * q), b = min(r1, a + q);
+  const bool col = d < ndig;
+  uint32_t s = 0;
+  if (col) {
+#pragma unroll 8
+    for (uint32_t r = a; r < b; ++r) s += cmat[(uint64_t)r * ndig + d];
+  }
+  gsum[g][d] = s;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (uint32_t k = 0; k < kScanGroups; ++k) {
+    if (k < g) run += gsum[k][d];
+    tot += gsum[k][d];
+  }
+  if (col) {
+#pragma unroll 8
+    for (uint32_t r = a; r < b; ++r) {
+      const uint64_t i = (uint64_t)r * ndig + d;
+      const uint32_t x = cmat[i];
+      pre[i] = run;
+      run += x;
+    }
+  }
+  unsigned long long all;
+  const unsigned long long ex =
+      block_exclusive_scan<unsigned long long>((g == 0 && col) ? (unsigned long long)tot : 0ull, scan_sm, &all);
+  if (g == 0 && col) child[(uint64_t)p * ndig + d] = pstart[p] + ex;
+}
+
+template <typename R>
+__global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restrict__ rec,
+                                                               const Chunk* __restrict__ ch, int shift, uint32_t ndig,
+                                                               const uint32_t* __restrict__ pre,
+                                                               const uint64_t* __restrict__ child,
+                                                               R* __restrict__ out) {
+  constexpr int kPartItems = PartGeom<R>::items;
+  constexpr int kTile = PartGeom<R>::tile;
+  __shared__ __attribute__((aligned(16))) R stage[kTile];
+  __shared__ unsigned long long cur[256];
+  __shared__ uint32_t lcnt[256];
+  __shared__ uint32_t lstart[256];
+  __shared__ uint32_t scan_sm[64];
+  const Chunk c = ch[blockIdx.x];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t dmask = ndig - 1;
+  if (tid < ndig) cur[tid] = child[(uint64_t)c.parent * ndig + tid] + pre[(uint64_t)blockIdx.x * ndig + tid];
+  const R* base = rec + c.start;
+  R v[kPartItems], vn[kPartItems];
+#pragma unroll
+  for (int i = 0; i < kPartItems; ++i) {
+    const uint32_t idx = i * kPartThreads + tid;
+    if (idx < c.len) v[i] = base[idx];
+  }
+  for (uint32_t t0 = 0; t0 < c.len; t0 += kTile) {
+    const uint32_t tn = min((uint32_t)kTile, c.len - t0);
+    // prefetch the next tile: its loads stay in flight through this tile's work
+    const uint32_t t1 = t0 + kTile;
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+      const uint32_t idx = i * kPartThreads + tid;
+      if (t1 + idx < c.len) vn[i] = base[t1 + idx];
+    }
+    lcnt[tid] = 0;
+    __syncthreads();
+    uint32_t pos[kPartItems];
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+      const uint32_t idx = i * kPartThreads + tid;
+      if (idx < tn) pos[i] = atomicAdd(&lcnt[(rkey(v[i]) >> shift) & dmask], 1u);
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<uint32_t>(lcnt[tid], scan_sm, &tot);
+    lstart[tid] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+      const uint32_t idx = i * kPartThreads + tid;
+      if (idx < tn) stage[lstart[(rkey(v[i]) >> shift) & dmask] + pos[i]] = v[i];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < tn; i += kPartThreads) {
+      const R x = stage[i];
+      const uint32_t d = (uint32_t)((rkey(x) >> shift) & dmask);
+      out[cur[d] + (i - lstart[d])] = x;
+    }
+    __syncthreads();
+    if (tid < ndig) cur[tid] += lcnt[tid];
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) v[i] = vn[i];
+  }
+}
+
+// One partition level: every parent's segments -> ndig children per parent.
+// Writes the children's start offsets to d_child (nparents*ndig + 1) and, if
+// host_child, copies them to the host.
+template <typename R>
+int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
+               uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag) {
+  constexpr int kTile = PartGeom<R>::tile;
+  const uint32_t ndig = 1u << bits;
+  const uint64_t np = parents.size();
+  // ~24K chunks per level: enough workgroups, short count-matrix rows
+  const uint64_t chunk = std::max<uint64_t>(4 * kTile, ((n / 24576) + kTile - 1) / kTile * kTile);
+  std::vector<Chunk> chunks;
+  std::vector<uint32_t> prow(np + 1);
+  std::vector<uint64_t> pstart(np);
+  uint64_t pos = 0;
+  for (uint64_t p = 0; p < np; ++p) {
+    prow[p] = (uint32_t)chunks.size();
+    pstart[p] = pos;
+    for (const Seg& s : parents[p]) {
+      if (s.len >= (1ull << 32)) {
+        set_error("part_level: parent group exceeds 2^32 records");
+        return APG_E_UNSUPPORTED;
+      }
+      for (uint64_t o = 0; o < s.len; o += chunk)
+        chunks.push_back(Chunk{s.start + o, (uint32_t)std::min<uint64_t>(chunk, s.len - o), (uint32_t)p});
+      pos += s.len;
+    }
+  }
+  prow[np] = (uint32_t)chunks.size();
+  if (chunks.empty()) chunks.push_back(Chunk{0, 0, 0});  // keep launches non-empty
+  const uint64_t nrow = chunks.size();
+  Chunk* d_chunks = nullptr;
+  uint64_t* d_pstart = nullptr;
+  uint32_t *d_prow = nullptr, *cmat = nullptr, *pre = nullptr;
+  APG_TRY(workspace_t(ctx, (std::string(tag) + "p_chunks").c_str(), nrow, &d_chunks));
+  APG_TRY(workspace_t(ctx, (std::string(tag) + "p_prow").c_str(), np + 1, &d_prow));
+  APG_TRY(workspace_t(ctx, (std::string(tag) + "p_pstart").c_str(), np, &d_pstart));
+  APG_TRY(workspace_t(ctx, (std::string(tag) + "p_cmat").c_str(), nrow * ndig, &cmat));
+  APG_TRY(workspace_t(ctx, (std::string(tag) + "p_pre").c_str(), nrow * ndig, &pre));
+  APG_CHECK_HIP(hipMemcpyAsync(d_chunks, chunks.data(), nrow * sizeof(Chunk), hipMemcpyHostToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(d_prow, prow.data(), (np + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(d_pstart, pstart.data(), np * 8, hipMemcpyHostToDevice, ctx->stream));
+  const uint64_t nb = np * ndig;
+  APG_CHECK_HIP(hipMemcpyAsync(d_child + nb, &n, 8, hipMemcpyHostToDevice, ctx->stream));
+  kbegin(ctx, (std::string(tag) + "_part_count").c_str(), n * sizeof(R) + nrow * ndig * 4);
+  k_part_count<R><<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, cmat);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  kbegin(ctx, (std::string(tag) + "_part_scan").c_str(), nrow * ndig * 12 + nb * 8);
+  k_part_scan<<<(uint32_t)np, kPartThreads * kScanGroups, 0, ctx->stream>>>(cmat, d_prow, d_pstart, ndig, pre,
+                                                                             d_child);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  kbegin(ctx, (std::string(tag) + "_part_scatter").c_str(), n * 2 * sizeof(R) + nrow * ndig * 4);
+  k_part_scatter<R><<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, pre, d_child, dst);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  if (host_child) {
+    host_child->resize(nb + 1);
+    APG_CHECK_HIP(hipMemcpyAsync(host_child->data(), d_child, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+  }
+  return APG_OK;
+}
+
+
+template int part_level<uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&, int, int,
+                                  uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<KRec>(apg_ctx*, const KRec*, KRec*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
+                              uint64_t*, std::vector<uint64_t>*, const char*);
+
+}  // namespace apg

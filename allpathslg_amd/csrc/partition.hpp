@@ -1,0 +1,43 @@
+// partition.hpp — device-wide building blocks shared by the k-mer modules:
+// the u32 -> u64 exclusive scan and the LDS-staged hash-partition level,
+// for 8-byte hash records (K <= 32 spectrum) and 32-byte K <= 96 records.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "apg_core.hpp"
+
+namespace apg {
+
+// 32-byte record of one K-mer instance for K <= 96: canonical key as three
+// big-endian 64-bit limbs (k0 most significant; value = sum b[i] 4^(K-1-i))
+// and meta = (56-bit key hash << 8) | extension bits (left nibble = bases
+// preceding the canonical K-mer, right nibble = bases following it).
+struct __attribute__((aligned(16))) KRec {
+  uint64_t k0, k1, k2, meta;
+};
+
+// The partition digit source of a record.
+__host__ __device__ inline uint64_t rkey(uint64_t r) { return r; }
+__host__ __device__ inline uint64_t rkey(const KRec& r) { return r.meta; }
+
+constexpr int kMaxLevelBits = 8;  // max digit bits of one partition level (LDS-staged scatter)
+
+struct Seg {
+  uint64_t start, len;
+};
+
+// d_out[0..n] = exclusive prefix sums of d_in[0..n) (d_out[n] = total).
+int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out, const char* tag);
+
+// One partition level: the records of every parent (a list of segments of
+// `src`) are split by bits [shift, shift+bits) of rkey() into ndig = 2^bits
+// children, written contiguously to `dst` in (parent, digit) order.  Writes
+// the children's starts to d_child[0 .. nparents*ndig] (last = n) and, if
+// host_child, copies them to the host.  Order inside a child is unspecified.
+template <typename R>
+int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
+               uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag);
+
+}  // namespace apg

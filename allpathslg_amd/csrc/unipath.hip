@@ -1,0 +1,1474 @@
+// unipath.hip — MI355X-native unipath graph builder for K <= 96.
+//
+// Replaces CommonPather/ReadsToPaths, Unipather and the unipath adjacency ->
+// HyperKmerPath step of RunAllPathsLG ([R:M] src/paths/ReadsToPathsCoreX.cc,
+// src/paths/Unipath.cc, src/paths/HyperKmerPath.h; reference snapshot empty,
+// SURVEY §0.1).  Semantics: SURVEY §A.5-A.6 as made operational in DESIGN.md
+// and restated on the CPU in oracle/unipath_oracle.cpp.
+//
+// Pipeline (U = unipath stage):
+//   U1 uext_count / uext_scatter  one thread per read rolls the 192-bit fw/rc
+//      K-mer, emits a 32-byte KRec {canonical key, hash56 | ext bits} into 32
+//      hash groups through an LDS-staged round (1024 records / round)
+//   U2 part_level<KRec>            LDS-staged hash-partition levels
+//   U3 ugroup                      per bucket: LDS owner table, full-key
+//      compare, OR of extension bits -> distinct nodes (sparse, in place)
+//   U4 ucompact + node_insert      dense node array + open-addressing index
+//   U5 links                       unique successor/predecessor per directed
+//      node (v = 2*node + orientation)
+//   U6 ranking                     sparse ruling set: heads + every 32nd node
+//      walk their segment; pointer jumping over rulers; cycles are cut before
+//      their min K-mer (min found by pointer jumping) and ranking reruns
+//   U7 pairs                       (u, rc u) keys, LSD radix sort on 192 bits
+//   U8 outputs                     ids, unibases, HyperKmerPath vertices
+//      (lock-free union-find over unipath ends), per-read KmerPaths
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "apg_core.hpp"
+#include "kmer_common.hpp"
+#include "partition.hpp"
+
+namespace apg {
+
+constexpr uint32_t kNone = 0xffffffffu;
+
+// ---------------------------------------------------------------------------
+// 192-bit K-mer keys: limbs (a, b, c), a most significant, value right-aligned
+// ---------------------------------------------------------------------------
+struct K3 {
+  uint64_t a, b, c;
+};
+
+struct KeyP {
+  int K;
+  uint64_t ma, mb, mc;  // masks of the 2K-bit value per limb
+};
+
+static KeyP make_keyp(int K) {
+  KeyP p;
+  p.K = K;
+  const int bits = 2 * K;
+  p.mc = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+  p.mb = bits >= 128 ? ~0ull : bits <= 64 ? 0 : ((1ull << (bits - 64)) - 1);
+  p.ma = bits >= 192 ? ~0ull : bits <= 128 ? 0 : ((1ull << (bits - 128)) - 1);
+  return p;
+}
+
+__device__ __forceinline__ bool k3_lt(const K3& x, const K3& y) {
+  if (x.a != y.a) return x.a < y.a;
+  if (x.b != y.b) return x.b < y.b;
+  return x.c < y.c;
+}
+__device__ __forceinline__ bool k3_eq(const K3& x, const K3& y) { return x.a == y.a && x.b == y.b && x.c == y.c; }
+
+__device__ __forceinline__ K3 push_right(const K3& k, uint64_t base, const KeyP& p) {
+  K3 r;
+  r.a = ((k.a << 2) | (k.b >> 62)) & p.ma;
+  r.b = ((k.b << 2) | (k.c >> 62)) & p.mb;
+  r.c = ((k.c << 2) | base) & p.mc;
+  return r;
+}
+
+// rc of the K-mer after appending `base` to the fw K-mer: shift right 2, put
+// the complement at the top (bit 2K-2).
+__device__ __forceinline__ K3 rc_roll(const K3& r, uint64_t base, const KeyP& p) {
+  K3 o;
+  o.c = (r.c >> 2) | (r.b << 62);
+  o.b = (r.b >> 2) | (r.a << 62);
+  o.a = r.a >> 2;
+  const int pos = 2 * p.K - 2;
+  const uint64_t x = 3 - base;
+  if (pos >= 128)
+    o.a |= x << (pos - 128);
+  else if (pos >= 64)
+    o.b |= x << (pos - 64);
+  else
+    o.c |= x << pos;
+  o.a &= p.ma;
+  o.b &= p.mb;
+  o.c &= p.mc;
+  return o;
+}
+
+__device__ __forceinline__ uint64_t rev2(uint64_t x) {  // reverse the 32 2-bit groups
+  x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+  x = ((x >> 4) & 0x0f0f0f0f0f0f0f0full) | ((x & 0x0f0f0f0f0f0f0f0full) << 4);
+  return __builtin_bswap64(x);
+}
+
+__device__ __forceinline__ K3 revcomp(const K3& k, const KeyP& p) {
+  // complement + reverse all 96 2-bit groups, then right-align the 2K bits
+  uint64_t a = rev2(~k.c), b = rev2(~k.b), c = rev2(~k.a);
+  const int s = 192 - 2 * p.K;  // 0 <= s < 192
+  K3 r;
+  if (s == 0) {
+    r = {a, b, c};
+  } else if (s < 64) {
+    r.c = (c >> s) | (b << (64 - s));
+    r.b = (b >> s) | (a << (64 - s));
+    r.a = a >> s;
+  } else if (s == 64) {
+    r = {0, a, b};
+  } else if (s < 128) {
+    const int t = s - 64;
+    r.c = (b >> t) | (a << (64 - t));
+    r.b = a >> t;
+    r.a = 0;
+  } else if (s == 128) {
+    r = {0, 0, a};
+  } else {
+    r = {0, 0, a >> (s - 128)};
+  }
+  r.a &= p.ma;
+  r.b &= p.mb;
+  r.c &= p.mc;
+  return r;
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+// Partition / index hash of a canonical key: top 56 bits used (low byte holds
+// the extension bits in KRec.meta).
+__device__ __forceinline__ uint64_t key_hash(const K3& k) {
+  return fmix64(k.a ^ fmix64(k.b ^ fmix64(k.c ^ 0x5851f42d4c957f2dull))) & ~0xffull;
+}
+
+__device__ __forceinline__ K3 rec_key(const KRec& r) { return K3{r.k0, r.k1, r.k2}; }
+__device__ __forceinline__ uint32_t comp4(uint32_t s) {  // bit b -> bit 3-b
+  return ((s & 1) << 3) | ((s & 2) << 1) | ((s & 4) >> 1) | ((s & 8) >> 3);
+}
+__device__ __forceinline__ uint32_t read_base(const uint8_t* rd, uint32_t i) {
+  return (rd[i >> 2] >> (2 * (i & 3))) & 3;
+}
+
+// canonical key, orientation (0: fw is canonical, incl. palindromes) and the
+// instance's extension bits in canonical orientation (left | right << 4)
+__device__ __forceinline__ void canon_ext(const K3& fw, const K3& rc, int a, int b, K3* key, uint32_t* ext) {
+  const bool pal = k3_eq(fw, rc);
+  const bool fwc = pal || k3_lt(fw, rc);
+  const uint32_t la = a >= 0 ? 1u << a : 0, rb = b >= 0 ? 1u << b : 0;
+  const uint32_t ca = a >= 0 ? 1u << (3 - a) : 0, cb = b >= 0 ? 1u << (3 - b) : 0;
+  uint32_t L, R;
+  if (pal) {
+    L = la | cb;
+    R = rb | ca;
+  } else if (fwc) {
+    L = la;
+    R = rb;
+  } else {
+    L = cb;
+    R = ca;
+  }
+  *key = fwc ? fw : rc;
+  *ext = L | (R << 4);
+}
+
+struct ReadsV {
+  const uint64_t* base_off;
+  const uint64_t* byte_off;
+  const uint8_t* packed;
+  uint64_t n_reads;
+};
+
+// Rolling state over one read for 192-bit K-mers.
+struct Roller3 {
+  const uint8_t* rd;
+  uint32_t len, i;
+  K3 fw, rc;
+  __device__ __forceinline__ void init(const uint8_t* r, uint32_t n, const KeyP& p) {
+    rd = r;
+    len = n;
+    i = 0;
+    fw = K3{0, 0, 0};
+    rc = K3{0, 0, 0};
+    const uint32_t prime = n < (uint32_t)(p.K - 1) ? n : (uint32_t)(p.K - 1);
+    for (uint32_t j = 0; j < prime; ++j) step(p);
+  }
+  __device__ __forceinline__ void step(const KeyP& p) {
+    const uint64_t b = read_base(rd, i);
+    fw = push_right(fw, b, p);
+    rc = rc_roll(rc, b, p);
+    ++i;
+  }
+  __device__ __forceinline__ bool more() const { return i < len; }
+  // next K-mer instance as a KRec
+  __device__ __forceinline__ KRec next(const KeyP& p) {
+    step(p);
+    const uint32_t j = i - p.K;  // start of this K-mer
+    const int a = j > 0 ? (int)read_base(rd, j - 1) : -1;
+    const int b = i < len ? (int)read_base(rd, i) : -1;
+    K3 key;
+    uint32_t ext;
+    canon_ext(fw, rc, a, b, &key, &ext);
+    return KRec{key.a, key.b, key.c, key_hash(key) | ext};
+  }
+};
+
+// ---------------------------------------------------------------------------
+// U1: extraction into 2^D hash groups (count matrix [digit][block])
+// ---------------------------------------------------------------------------
+constexpr int kUThreads = 256;
+constexpr int kUItems = 4;  // KRec per thread per round: 1024 records = 32 KiB
+constexpr int kUDigitBits = 5;
+constexpr int kUMaxBlocks = 2048;
+
+__device__ __forceinline__ void read_range(uint64_t n, uint32_t G, uint32_t b, uint64_t* r0, uint64_t* r1) {
+  *r0 = (n * b) / G;
+  *r1 = (n * (b + 1)) / G;
+}
+
+__global__ void __launch_bounds__(kUThreads) k_uext_count(ReadsV rv, KeyP kp, uint32_t* __restrict__ cmat) {
+  __shared__ uint32_t hist[1 << kUDigitBits];
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  if (threadIdx.x < (1 << kUDigitBits)) hist[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t r0, r1;
+  read_range(rv.n_reads, G, b, &r0, &r1);
+  for (uint64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+    const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+    if (len < (uint32_t)kp.K) continue;
+    Roller3 ro;
+    ro.init(rv.packed + rv.byte_off[r], len, kp);
+    while (ro.more()) {
+      const KRec x = ro.next(kp);
+      atomicAdd(&hist[x.meta >> (64 - kUDigitBits)], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < (1 << kUDigitBits)) cmat[(uint64_t)threadIdx.x * G + b] = hist[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kUThreads) k_uext_scatter(ReadsV rv, KeyP kp, const uint64_t* __restrict__ omat,
+                                                            KRec* __restrict__ out) {
+  constexpr uint32_t ndig = 1u << kUDigitBits;
+  __shared__ KRec stage[kUThreads * kUItems];
+  __shared__ unsigned long long cur[ndig];
+  __shared__ uint32_t lcnt[256], lstart[256];
+  __shared__ uint32_t scan_sm[64];
+  const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  if (tid < ndig) cur[tid] = omat[(uint64_t)tid * G + b];
+  uint64_t r0, r1;
+  read_range(rv.n_reads, G, b, &r0, &r1);
+  for (uint64_t rb = r0; rb < r1; rb += kUThreads) {
+    const uint64_t r = rb + tid;
+    Roller3 ro;
+    ro.i = 0;
+    ro.len = 0;
+    if (r < r1) {
+      const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+      if (len >= (uint32_t)kp.K) ro.init(rv.packed + rv.byte_off[r], len, kp);
+    }
+    while (__syncthreads_or(ro.more())) {
+      lcnt[tid] = 0;
+      __syncthreads();
+      KRec v[kUItems];
+      uint32_t pos[kUItems];
+      uint32_t nv = 0;
+#pragma unroll
+      for (int j = 0; j < kUItems; ++j) {
+        if (ro.more()) {
+          v[j] = ro.next(kp);
+          pos[j] = atomicAdd(&lcnt[v[j].meta >> (64 - kUDigitBits)], 1u);
+          nv = j + 1;
+        }
+      }
+      __syncthreads();
+      uint32_t tot;
+      const uint32_t ex = block_exclusive_scan<uint32_t>(lcnt[tid], scan_sm, &tot);
+      lstart[tid] = ex;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kUItems; ++j)
+        if ((uint32_t)j < nv) stage[lstart[v[j].meta >> (64 - kUDigitBits)] + pos[j]] = v[j];
+      __syncthreads();
+      for (uint32_t i = tid; i < tot; i += kUThreads) {
+        const KRec x = stage[i];
+        const uint32_t d = (uint32_t)(x.meta >> (64 - kUDigitBits));
+        out[cur[d] + (i - lstart[d])] = x;
+      }
+      __syncthreads();
+      if (tid < ndig) cur[tid] += lcnt[tid];
+    }
+  }
+}
+
+__global__ void k_digit_starts_u(const uint64_t* __restrict__ omat, uint32_t ndig, uint32_t G,
+                                 uint64_t* __restrict__ ds) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d <= ndig) ds[d] = omat[(uint64_t)d * G];
+}
+
+// ---------------------------------------------------------------------------
+// U3: per-bucket grouping of instances into distinct nodes
+// ---------------------------------------------------------------------------
+constexpr int kGThreads = 256;
+constexpr uint32_t kGCap = 1023;   // records of an LDS-resident bucket
+constexpr uint32_t kGTab = 1024;   // LDS owner-table slots (> kGCap)
+
+struct GroupOut {
+  KRec* nodes;             // sparse: bucket b's distinct nodes at boff[b] + i
+  uint32_t* ncnt;          // parallel counts
+  uint32_t* bucket_nd;
+  unsigned long long* gstats;  // [0] distinct, [1] overflow buckets, [2] max bucket
+  uint32_t* ovf_list;
+};
+
+// Small buckets: records and owner table in LDS.
+__global__ void __launch_bounds__(kGThreads) k_ugroup(const KRec* __restrict__ rec, const uint64_t* __restrict__ boff,
+                                                     uint64_t nbuckets, GroupOut o) {
+  __shared__ KRec R[kGCap];
+  __shared__ uint32_t tab[kGTab];
+  __shared__ uint32_t rep[kGCap];
+  __shared__ uint32_t ext[kGCap];
+  __shared__ uint32_t cnt[kGCap];
+  __shared__ uint32_t scan_sm[64];
+  const uint32_t tid = threadIdx.x;
+  unsigned long long nd_sum = 0, maxb = 0;
+  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
+    const uint64_t off = boff[bkt];
+    const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
+    if (n > maxb) maxb = n;
+    if (n > kGCap) {
+      if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+      continue;
+    }
+    if (n == 0) {
+      if (tid == 0) o.bucket_nd[bkt] = 0;
+      continue;
+    }
+    uint32_t T = 64;
+    while (T <= n) T <<= 1;
+    for (uint32_t s = tid; s < T; s += kGThreads) tab[s] = kNone;
+    for (uint32_t i = tid; i < n; i += kGThreads) {
+      R[i] = rec[off + i];
+      ext[i] = 0;
+      cnt[i] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kGThreads) {
+      const K3 k = rec_key(R[i]);
+      uint32_t s = (uint32_t)(R[i].meta >> 8) & (T - 1);
+      for (;;) {
+        const uint32_t ow = atomicCAS(&tab[s], kNone, i);
+        if (ow == kNone) {
+          rep[i] = i;
+          break;
+        }
+        if (k3_eq(rec_key(R[ow]), k)) {
+          rep[i] = ow;
+          break;
+        }
+        s = (s + 1) & (T - 1);
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kGThreads) {
+      atomicOr(&ext[rep[i]], (uint32_t)(R[i].meta & 0xff));
+      atomicAdd(&cnt[rep[i]], 1u);
+    }
+    __syncthreads();
+    // compact representatives in index order
+    const uint32_t ipt = (n + kGThreads - 1) / kGThreads;
+    const uint32_t i0 = min(n, tid * ipt), i1 = min(n, i0 + ipt);
+    uint32_t c = 0;
+    for (uint32_t i = i0; i < i1; ++i) c += rep[i] == i;
+    uint32_t d;
+    uint32_t j = block_exclusive_scan<uint32_t>(c, scan_sm, &d);
+    for (uint32_t i = i0; i < i1; ++i) {
+      if (rep[i] != i) continue;
+      KRec x = R[i];
+      x.meta = (x.meta & ~0xffull) | ext[i];
+      o.nodes[off + j] = x;
+      o.ncnt[off + j] = cnt[i];
+      ++j;
+    }
+    if (tid == 0) {
+      o.bucket_nd[bkt] = d;
+      nd_sum += d;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    atomicAdd(&o.gstats[0], nd_sum);
+    atomicMax(&o.gstats[2], maxb);
+  }
+}
+
+// Oversized buckets: one workgroup each, owner table and per-record scratch
+// in global memory (scratch regions parallel to the bucket's records).
+__global__ void __launch_bounds__(kGThreads) k_ugroup_big(const KRec* __restrict__ rec,
+                                                         const uint64_t* __restrict__ boff, uint32_t* __restrict__ gtab,
+                                                         uint32_t* __restrict__ grep, uint32_t* __restrict__ gext,
+                                                         uint32_t* __restrict__ gcnt, GroupOut o) {
+  __shared__ uint32_t scan_sm[64];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t bkt = o.ovf_list[blockIdx.x];
+  const uint64_t off = boff[bkt];
+  const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
+  uint32_t T = 64;
+  while (T <= n) T <<= 1;  // T <= 2n: table lives in gtab[2*off ...]
+  uint32_t* tab = gtab + 2 * off;
+  uint32_t* rep = grep + off;
+  uint32_t* ext = gext + off;
+  uint32_t* cnt = gcnt + off;
+  for (uint32_t s = tid; s < T; s += kGThreads) tab[s] = kNone;
+  for (uint32_t i = tid; i < n; i += kGThreads) {
+    ext[i] = 0;
+    cnt[i] = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kGThreads) {
+    const K3 k = rec_key(rec[off + i]);
+    uint32_t s = (uint32_t)(rec[off + i].meta >> 8) & (T - 1);
+    for (;;) {
+      const uint32_t ow = atomicCAS(&tab[s], kNone, i);
+      if (ow == kNone) {
+        rep[i] = i;
+        break;
+      }
+      if (k3_eq(rec_key(rec[off + ow]), k)) {
+        rep[i] = ow;
+        break;
+      }
+      s = (s + 1) & (T - 1);
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kGThreads) {
+    atomicOr(&ext[rep[i]], (uint32_t)(rec[off + i].meta & 0xff));
+    atomicAdd(&cnt[rep[i]], 1u);
+  }
+  __syncthreads();
+  const uint32_t ipt = (n + kGThreads - 1) / kGThreads;
+  const uint32_t i0 = min(n, tid * ipt), i1 = min(n, i0 + ipt);
+  uint32_t c = 0;
+  for (uint32_t i = i0; i < i1; ++i) c += rep[i] == i;
+  uint32_t d;
+  uint32_t j = block_exclusive_scan<uint32_t>(c, scan_sm, &d);
+  for (uint32_t i = i0; i < i1; ++i) {
+    if (rep[i] != i) continue;
+    KRec x = rec[off + i];
+    x.meta = (x.meta & ~0xffull) | ext[i];
+    o.nodes[off + j] = x;
+    o.ncnt[off + j] = cnt[i];
+    ++j;
+  }
+  if (tid == 0) {
+    o.bucket_nd[bkt] = d;
+    atomicAdd(&o.gstats[0], (unsigned long long)d);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// U4: dense nodes + index
+// ---------------------------------------------------------------------------
+__global__ void k_ucompact(const KRec* __restrict__ sp, const uint32_t* __restrict__ spc,
+                           const uint64_t* __restrict__ boff, const uint32_t* __restrict__ bucket_nd,
+                           const uint64_t* __restrict__ nbase, uint64_t nbuckets, KRec* __restrict__ nodes,
+                           uint32_t* __restrict__ ncnt) {
+  for (uint64_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
+    const uint64_t s = boff[b], d = nbase[b];
+    const uint32_t nd = bucket_nd[b];
+    for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) {
+      nodes[d + i] = sp[s + i];
+      ncnt[d + i] = spc[s + i];
+    }
+  }
+}
+
+__global__ void k_node_insert(const KRec* __restrict__ nodes, uint64_t N, uint32_t* __restrict__ idx, uint64_t tmask) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t s = (nodes[i].meta >> 8) & tmask;
+    while (atomicCAS(&idx[s], kNone, (uint32_t)i) != kNone) s = (s + 1) & tmask;
+  }
+}
+
+struct NodeIdx {
+  const KRec* nodes;
+  const uint32_t* idx;
+  uint64_t tmask;
+  __device__ __forceinline__ uint32_t find(const K3& k) const {
+    uint64_t s = (key_hash(k) >> 8) & tmask;
+    for (;;) {
+      const uint32_t i = idx[s];
+      if (i == kNone) return kNone;
+      const KRec& r = nodes[i];
+      if (r.k0 == k.a && r.k1 == k.b && r.k2 == k.c) return i;
+      s = (s + 1) & tmask;
+    }
+  }
+};
+
+__device__ __forceinline__ K3 dseq(const KRec* nodes, uint32_t v, const KeyP& p) {
+  const K3 k = rec_key(nodes[v >> 1]);
+  return (v & 1) ? revcomp(k, p) : k;
+}
+__device__ __forceinline__ uint32_t out_set(uint32_t ext, uint32_t o) { return o ? comp4(ext & 15) : (ext >> 4); }
+__device__ __forceinline__ uint32_t in_set(uint32_t ext, uint32_t o) { return o ? comp4(ext >> 4) : (ext & 15); }
+
+// directed node whose sequence is s (kNone if absent)
+__device__ __forceinline__ uint32_t directed_of(const NodeIdx& ni, const K3& s, const KeyP& p) {
+  const K3 r = revcomp(s, p);
+  const bool fw = !k3_lt(r, s);
+  const uint32_t n = ni.find(fw ? s : r);
+  return n == kNone ? kNone : 2 * n + (fw ? 0 : 1);
+}
+
+// ---------------------------------------------------------------------------
+// U5: unique links
+// ---------------------------------------------------------------------------
+__global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, uint32_t* __restrict__ nxt, uint32_t* __restrict__ prv,
+                        unsigned long long* __restrict__ stat) {
+  unsigned long long nl = 0, bad = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    const KRec x = ni.nodes[i];
+    const K3 key = rec_key(x);
+    if (k3_eq(key, revcomp(key, kp))) continue;  // palindromic K-mers never link
+    const uint32_t ext = (uint32_t)(x.meta & 0xff);
+    for (uint32_t o = 0; o < 2; ++o) {
+      const uint32_t out = out_set(ext, o);
+      if (__popc(out) != 1) continue;
+      const uint32_t b = __ffs(out) - 1;
+      const K3 s = o ? revcomp(key, kp) : key;
+      const K3 t = push_right(s, b, kp);
+      const uint32_t w = directed_of(ni, t, kp);
+      if (w == kNone) {
+        ++bad;
+        continue;
+      }
+      const K3 wk = rec_key(ni.nodes[w >> 1]);
+      if (k3_eq(wk, revcomp(wk, kp))) continue;
+      const uint32_t wext = (uint32_t)(ni.nodes[w >> 1].meta & 0xff);
+      if (__popc(in_set(wext, w & 1)) != 1) continue;
+      nxt[2 * i + o] = w;
+      prv[w] = (uint32_t)(2 * i + o);
+      ++nl;
+    }
+  }
+  for (int s = 32; s > 0; s >>= 1) {
+    nl += __shfl_down(nl, s, 64);
+    bad += __shfl_down(bad, s, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (nl) atomicAdd(&stat[0], nl);
+    if (bad) atomicAdd(&stat[1], bad);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// U6: ranking (ruling set + pointer jumping), cycle cutting
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRulerMask = 31;  // sampled rulers: 1 in 32
+
+__device__ __forceinline__ bool is_ruler(uint32_t v, const uint32_t* prv) {
+  return prv[v] == kNone || ((uint32_t)fmix64(v) & kRulerMask) == 0;
+}
+
+struct RankBufs {
+  uint32_t *nxt, *prv;
+  uint32_t *ruler_of, *lrank, *rnext, *seglen;
+  uint32_t *ptr0, *ptr1, *hd0, *hd1;
+  uint64_t *off0, *off1;
+  uint32_t* rlist;
+};
+
+__global__ void k_rank_init(uint64_t D, RankBufs rb) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < D; v += (uint64_t)gridDim.x * blockDim.x)
+    rb.ruler_of[v] = kNone;
+}
+
+// Each ruler walks its segment (up to the next ruler / end).
+__global__ void k_walk(uint64_t D, RankBufs rb, unsigned long long* __restrict__ nrul) {
+  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = (uint32_t)v0;
+    if (!is_ruler(v, rb.prv)) continue;
+    rb.rlist[atomicAdd(nrul, 1ull)] = v;
+    uint32_t x = v, r = 0;
+    for (uint64_t guard = 0; guard <= D; ++guard) {
+      rb.ruler_of[x] = v;
+      rb.lrank[x] = r++;
+      const uint32_t y = rb.nxt[x];
+      if (y == kNone || is_ruler(y, rb.prv)) {
+        rb.rnext[v] = y;
+        break;
+      }
+      x = y;
+    }
+    rb.seglen[v] = r;
+  }
+}
+
+__global__ void k_ruler_init(uint64_t R, RankBufs rb) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = rb.rlist[i];
+    rb.ptr0[r] = kNone;
+    rb.off0[r] = 0;
+    rb.hd0[r] = r;
+  }
+}
+__global__ void k_ruler_link(uint64_t R, RankBufs rb) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = rb.rlist[i];
+    const uint32_t s = rb.rnext[r];
+    if (s != kNone) {  // s is a ruler with unique ruler predecessor r
+      rb.ptr0[s] = r;
+      rb.off0[s] = rb.seglen[r];
+      rb.hd0[s] = kNone;
+    }
+  }
+}
+// one pointer-jumping round: (ptr0, off0, hd0) -> (ptr1, off1, hd1)
+__global__ void k_ruler_jump(uint64_t R, const uint32_t* __restrict__ rlist, const uint32_t* __restrict__ ptr0,
+                             const uint64_t* __restrict__ off0, const uint32_t* __restrict__ hd0,
+                             uint32_t* __restrict__ ptr1, uint64_t* __restrict__ off1, uint32_t* __restrict__ hd1) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = rlist[i];
+    const uint32_t q = ptr0[r];
+    if (q == kNone) {
+      ptr1[r] = kNone;
+      off1[r] = off0[r];
+      hd1[r] = hd0[r];
+    } else {
+      const uint32_t qq = ptr0[q];
+      off1[r] = off0[r] + off0[q];
+      ptr1[r] = qq;
+      hd1[r] = qq == kNone ? hd0[q] : kNone;
+    }
+  }
+}
+
+// cyclic directed nodes: unvisited, or on a ruler whose pointer never ended
+__global__ void k_mark_cyclic(uint64_t D, RankBufs rb, const uint32_t* __restrict__ ptr, uint32_t* __restrict__ clist,
+                              unsigned long long* __restrict__ ncyc) {
+  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = (uint32_t)v0;
+    const uint32_t r = rb.ruler_of[v];
+    if (r == kNone || ptr[r] != kNone) clist[atomicAdd(ncyc, 1ull)] = v;
+  }
+}
+
+__device__ __forceinline__ uint32_t seq_min(const KRec* nodes, uint32_t x, uint32_t y, const KeyP& p) {
+  return k3_lt(dseq(nodes, y, p), dseq(nodes, x, p)) ? y : x;
+}
+__global__ void k_cyc_init(uint64_t C, const uint32_t* __restrict__ clist, const uint32_t* __restrict__ nxt,
+                           uint32_t* __restrict__ cm, uint32_t* __restrict__ cn) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = clist[i];
+    cm[v] = v;
+    cn[v] = nxt[v];
+  }
+}
+__global__ void k_cyc_jump(uint64_t C, const uint32_t* __restrict__ clist, const KRec* __restrict__ nodes, KeyP kp,
+                           const uint32_t* __restrict__ cm0, const uint32_t* __restrict__ cn0, uint32_t* __restrict__ cm1,
+                           uint32_t* __restrict__ cn1) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = clist[i];
+    const uint32_t n = cn0[v];
+    cm1[v] = seq_min(nodes, cm0[v], cm0[n], kp);
+    cn1[v] = cn0[n];
+  }
+}
+// Cut each (C, rc C) pair once, before the smaller of the two cycles' minima.
+__global__ void k_cyc_cut(uint64_t C, const uint32_t* __restrict__ clist, const KRec* __restrict__ nodes, KeyP kp,
+                          const uint32_t* __restrict__ cm, uint32_t* __restrict__ nxt, uint32_t* __restrict__ prv,
+                          unsigned long long* __restrict__ ncut) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = clist[i];
+    if (cm[v] != v) continue;
+    const uint32_t mr = cm[v ^ 1];
+    if (mr != v && !k3_lt(dseq(nodes, v, kp), dseq(nodes, mr, kp))) continue;
+    const uint32_t p = prv[v];
+    const bool mirror = nxt[v ^ 1] == (p ^ 1) && (v ^ 1) != p;
+    nxt[p] = kNone;
+    prv[v] = kNone;
+    if (mirror) {
+      nxt[v ^ 1] = kNone;
+      prv[p ^ 1] = kNone;
+    }
+    atomicAdd(ncut, 1ull);
+  }
+}
+
+// final per-node head and rank; tails record their chain's length
+__global__ void k_rank_final(uint64_t D, RankBufs rb, const uint32_t* __restrict__ hd, const uint64_t* __restrict__ off,
+                             uint32_t* __restrict__ head, uint32_t* __restrict__ rank, uint32_t* __restrict__ chainlen,
+                             uint32_t* __restrict__ tail_of) {
+  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = (uint32_t)v0;
+    const uint32_t r = rb.ruler_of[v];
+    const uint32_t h = hd[r];
+    const uint32_t k = (uint32_t)(off[r] + rb.lrank[v]);
+    head[v] = h;
+    rank[v] = k;
+    if (rb.nxt[v] == kNone) {
+      chainlen[h] = k + 1;
+      tail_of[h] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// U7: unipath pairs and their order
+// ---------------------------------------------------------------------------
+__global__ void k_pairs(uint64_t D, const uint32_t* __restrict__ prv, const uint32_t* __restrict__ tail_of,
+                        const KRec* __restrict__ nodes, KeyP kp, uint64_t* __restrict__ pk0, uint64_t* __restrict__ pk1,
+                        uint64_t* __restrict__ pk2, uint32_t* __restrict__ ph, unsigned long long* __restrict__ np,
+                        unsigned long long* __restrict__ nu) {
+  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = (uint32_t)v0;
+    if (prv[h] != kNone) continue;
+    const uint32_t rh = tail_of[h] ^ 1;  // head of the rc path
+    const K3 hs = dseq(nodes, h, kp);
+    if (rh != h) {  // emit once per (u, rc u): smaller head K-mer; equal only for a palindromic K-mer's two nodes
+      const K3 rs = dseq(nodes, rh, kp);
+      if (!(k3_lt(hs, rs) || (k3_eq(hs, rs) && h < rh))) continue;
+    }
+    const unsigned long long j = atomicAdd(np, 1ull);
+    pk0[j] = hs.a;
+    pk1[j] = hs.b;
+    pk2[j] = hs.c;
+    ph[j] = h;
+    atomicAdd(nu, rh == h ? 1ull : 2ull);
+  }
+}
+
+// Stable LSD radix pass over (key, payload) columns: digit = (key[sel] >> shift) & 255.
+constexpr int kSortThreads = 256;
+constexpr int kSortTile = 4096;
+
+__global__ void __launch_bounds__(kSortThreads) k_lsd_count(const uint64_t* __restrict__ key, uint64_t n, int shift,
+                                                            uint32_t* __restrict__ cmat) {
+  __shared__ uint32_t hist[256];
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t s = (uint64_t)b * kSortTile, e = min(n, s + kSortTile);
+  for (uint64_t i = s + threadIdx.x; i < e; i += kSortThreads) atomicAdd(&hist[(key[i] >> shift) & 255], 1u);
+  __syncthreads();
+  cmat[(uint64_t)threadIdx.x * G + b] = hist[threadIdx.x];
+}
+
+struct SortCols {
+  const uint64_t *k0, *k1, *k2;
+  const uint32_t* pay;
+  uint64_t *o0, *o1, *o2;
+  uint32_t* opay;
+};
+
+__global__ void __launch_bounds__(kSortThreads) k_lsd_scatter(SortCols c, int sel, uint64_t n, int shift,
+                                                              const uint64_t* __restrict__ omat) {
+  constexpr int nw = kSortThreads / 64;
+  __shared__ uint32_t wh[nw][256];
+  __shared__ unsigned long long base[256];
+  const uint32_t G = gridDim.x, b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t s = (uint64_t)b * kSortTile, e = min(n, s + kSortTile);
+  const uint32_t tn = (uint32_t)(e - s);
+  const uint64_t* key = sel == 0 ? c.k0 : sel == 1 ? c.k1 : c.k2;
+  base[threadIdx.x] = omat[(uint64_t)threadIdx.x * G + b];
+  for (int d = lane; d < 256; d += 64) wh[w][d] = 0;
+  const uint32_t rows = (tn + 63) / 64, rpw = (rows + nw - 1) / nw;
+  const uint32_t r0 = min(rows, w * rpw), r1 = min(rows, r0 + rpw);
+  const uint64_t lt = (1ull << lane) - 1;
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t idx = r * 64 + lane;
+    const bool valid = idx < tn;
+    const uint32_t d = valid ? (uint32_t)((key[s + idx] >> shift) & 255) : 0;
+    const uint64_t peers = wave_match(d, valid, 8);
+    if (valid && (peers & lt) == 0) wh[w][d] += __popcll(peers);
+  }
+  __syncthreads();
+  {  // wave offsets within the block, in wave order (stability)
+    const uint32_t d = threadIdx.x;
+    uint32_t run = 0;
+    for (int k = 0; k < nw; ++k) {
+      const uint32_t x = wh[k][d];
+      wh[k][d] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t idx = r * 64 + lane;
+    const bool valid = idx < tn;
+    const uint32_t d = valid ? (uint32_t)((key[s + idx] >> shift) & 255) : 0;
+    const uint64_t peers = wave_match(d, valid, 8);
+    if (valid) {
+      const uint64_t pos = base[d] + wh[w][d] + __popcll(peers & lt);
+      c.o0[pos] = c.k0[s + idx];
+      c.o1[pos] = c.k1[s + idx];
+      c.o2[pos] = c.k2[s + idx];
+      c.opay[pos] = c.pay[s + idx];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (peers & lt) == 0) wh[w][d] += __popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ void k_digit_or(const uint64_t* __restrict__ k0, const uint64_t* __restrict__ k1,
+                           const uint64_t* __restrict__ k2, uint64_t n, unsigned long long* __restrict__ orv,
+                           unsigned long long* __restrict__ andv) {
+  unsigned long long o[3] = {0, 0, 0}, a[3] = {~0ull, ~0ull, ~0ull};
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    o[0] |= k0[i];
+    o[1] |= k1[i];
+    o[2] |= k2[i];
+    a[0] &= k0[i];
+    a[1] &= k1[i];
+    a[2] &= k2[i];
+  }
+  for (int j = 0; j < 3; ++j) {
+    atomicOr(&orv[j], o[j]);
+    atomicAnd(&andv[j], a[j]);
+  }
+}
+
+// emitted unipath indices of every pair and of both paths' heads
+__global__ void k_assign(uint64_t P, const uint32_t* __restrict__ ph, const uint32_t* __restrict__ tail_of,
+                         const uint64_t* __restrict__ ustart, const uint32_t* __restrict__ chainlen,
+                         uint32_t* __restrict__ uni_of_head, uint32_t* __restrict__ uhead, uint64_t* __restrict__ ulen,
+                         uint64_t* __restrict__ urc) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < P; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = ph[j];
+    const uint32_t rh = tail_of[h] ^ 1;
+    const uint64_t u = ustart[j];
+    uni_of_head[h] = (uint32_t)u;
+    uhead[u] = h;
+    ulen[u] = chainlen[h];
+    if (rh == h) {
+      urc[u] = u;
+    } else {
+      uni_of_head[rh] = (uint32_t)(u + 1);
+      uhead[u + 1] = rh;
+      ulen[u + 1] = chainlen[rh];
+      urc[u] = u + 1;
+      urc[u + 1] = u;
+    }
+  }
+}
+
+__global__ void k_pair_sizes(uint64_t P, const uint32_t* __restrict__ ph, const uint32_t* __restrict__ tail_of,
+                             uint32_t* __restrict__ sz) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < P; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = ph[j];
+    sz[j] = (tail_of[h] ^ 1) == h ? 1u : 2u;
+  }
+}
+
+__global__ void k_u32_of(const uint64_t* __restrict__ x, uint64_t n, uint32_t add, uint32_t* __restrict__ y) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    y[i] = (uint32_t)x[i] + add;
+}
+
+// ---------------------------------------------------------------------------
+// U8: outputs
+// ---------------------------------------------------------------------------
+__global__ void k_unibases(uint64_t D, const KRec* __restrict__ nodes, KeyP kp, const uint32_t* __restrict__ head,
+                           const uint32_t* __restrict__ rank, const uint32_t* __restrict__ uni_of_head,
+                           const uint64_t* __restrict__ ub_off, uint8_t* __restrict__ ub) {
+  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = (uint32_t)v0;
+    const uint32_t u = uni_of_head[head[v]];
+    const K3 s = dseq(nodes, v, kp);
+    const uint64_t o = ub_off[u] + rank[v];
+    ub[o + kp.K - 1] = (uint8_t)(s.c & 3);
+    if (rank[v] == 0) {
+      for (int t = 0; t < kp.K - 1; ++t) {  // base t of the K-mer
+        const int bit = 2 * (kp.K - 1 - t);
+        const uint64_t limb = bit >= 128 ? s.a : bit >= 64 ? s.b : s.c;
+        ub[o + t] = (uint8_t)((limb >> (bit & 63)) & 3);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
+  for (;;) {
+    const uint32_t p = par[x];
+    if (p == x) return x;
+    const uint32_t g = par[p];
+    if (g != p) atomicCAS(&par[x], p, g);  // path halving
+    x = p;
+  }
+}
+__device__ __forceinline__ void uf_union(uint32_t* par, uint32_t x, uint32_t y) {
+  for (;;) {
+    x = uf_find(par, x);
+    y = uf_find(par, y);
+    if (x == y) return;
+    if (x > y) {
+      const uint32_t t = x;
+      x = y;
+      y = t;
+    }
+    // hook the larger root under the smaller: roots stay class minima
+    if (atomicCAS(&par[y], y, x) == y) return;
+  }
+}
+
+__global__ void k_uf_init(uint64_t n, uint32_t* __restrict__ par) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    par[i] = (uint32_t)i;
+}
+
+__global__ void k_adjacency(uint64_t U, NodeIdx ni, KeyP kp, const uint32_t* __restrict__ uhead,
+                            const uint32_t* __restrict__ tail_of, const uint32_t* __restrict__ head,
+                            const uint32_t* __restrict__ uni_of_head, uint32_t* __restrict__ par,
+                            unsigned long long* __restrict__ bad) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t t = tail_of[uhead[u]];
+    const uint32_t ext = (uint32_t)(ni.nodes[t >> 1].meta & 0xff);
+    const uint32_t out = out_set(ext, t & 1);
+    if (!out) continue;
+    const K3 s = dseq(ni.nodes, t, kp);
+    for (uint32_t b = 0; b < 4; ++b) {
+      if (!(out & (1u << b))) continue;
+      const uint32_t w = directed_of(ni, push_right(s, b, kp), kp);
+      if (w == kNone) {
+        atomicAdd(bad, 1ull);
+        continue;
+      }
+      uf_union(par, (uint32_t)(2 * u + 1), 2 * uni_of_head[head[w]]);
+    }
+  }
+}
+
+__global__ void k_uf_roots(uint64_t n, uint32_t* __restrict__ par, uint32_t* __restrict__ is_root) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = uf_find(par, (uint32_t)i);
+    is_root[i] = r == i;
+  }
+}
+
+__global__ void k_hkp_edges(uint64_t U, uint32_t* __restrict__ par, const uint64_t* __restrict__ vid,
+                            uint64_t* __restrict__ from, uint64_t* __restrict__ to) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x) {
+    from[u] = vid[uf_find(par, (uint32_t)(2 * u))];
+    to[u] = vid[uf_find(par, (uint32_t)(2 * u + 1))];
+  }
+}
+
+// Per-read KmerPath: ids of the read's K-mers, run-length compressed into
+// intervals of consecutive ids.  WRITE = false counts intervals only.
+template <bool WRITE>
+__global__ void k_read_paths(ReadsV rv, NodeIdx ni, KeyP kp, const uint32_t* __restrict__ head,
+                             const uint32_t* __restrict__ rank, const uint32_t* __restrict__ uni_of_head,
+                             const uint64_t* __restrict__ id_base, uint32_t* __restrict__ nint,
+                             const uint64_t* __restrict__ ioff, uint64_t* __restrict__ istart,
+                             uint64_t* __restrict__ ilen, unsigned long long* __restrict__ bad) {
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+    uint32_t k = 0;
+    uint64_t cs = 0, cl = 0;
+    const uint64_t o = WRITE ? ioff[r] : 0;
+    if (len >= (uint32_t)kp.K) {
+      Roller3 ro;
+      ro.init(rv.packed + rv.byte_off[r], len, kp);
+      while (ro.more()) {
+        ro.step(kp);
+        const uint32_t v = directed_of(ni, ro.fw, kp);
+        if (v == kNone) {
+          atomicAdd(bad, 1ull);
+          continue;
+        }
+        const uint64_t id = id_base[uni_of_head[head[v]]] + rank[v];
+        if (cl && cs + cl == id) {
+          ++cl;
+        } else {
+          if (cl && WRITE) {
+            istart[o + k - 1] = cs;
+            ilen[o + k - 1] = cl;
+          }
+          cs = id;
+          cl = 1;
+          ++k;
+        }
+      }
+      if (cl && WRITE) {
+        istart[o + k - 1] = cs;
+        ilen[o + k - 1] = cl;
+      }
+    }
+    if (!WRITE) nint[r] = k;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host
+// ---------------------------------------------------------------------------
+static int ceil_log2_u(uint64_t x) {
+  int b = 0;
+  while ((1ull << b) < x) ++b;
+  return b;
+}
+static uint32_t grid_for(apg_ctx* ctx, uint64_t n, int per = 256) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, (uint64_t)ctx->n_cu * 16));
+}
+
+constexpr uint64_t kUBucketTarget = 640;
+
+template <typename T>
+static T* host_dup(const T* d, uint64_t n, apg_ctx* ctx, int* rc) {
+  T* h = (T*)std::malloc(std::max<uint64_t>(n, 1) * sizeof(T));
+  if (!h) {
+    *rc = APG_E_NOMEM;
+    return nullptr;
+  }
+  if (n) {
+    hipError_t e = hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream);
+    if (e != hipSuccess) {
+      set_error(std::string("D2H failed: ") + hipGetErrorString(e));
+      *rc = APG_E_HIP;
+    }
+  }
+  return h;
+}
+
+static int d2h_u64(apg_ctx* ctx, const unsigned long long* d, unsigned long long* h, int n) {
+  APG_CHECK_HIP(hipMemcpyAsync(h, d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  return sync(ctx);
+}
+
+static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
+                         apg_unipath_stats* st) {
+  const int K = prm.K;
+  const KeyP kp = make_keyp(K);
+  std::memset(st, 0, sizeof(*st));
+  ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  unsigned long long* gs = nullptr;  // general device counters
+  APG_TRY(workspace_t(ctx, "u_gs", 32, &gs));
+  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 32 * 8, ctx->stream));
+
+  // ---- U1 --------------------------------------------------------------------
+  const uint32_t ndig = 1u << kUDigitBits;
+  const uint32_t G =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUMaxBlocks, (dr->n_reads + 255) / 256));
+  uint32_t* cmat = nullptr;
+  uint64_t *omat = nullptr, *dstart = nullptr;
+  APG_TRY(workspace_t(ctx, "u_cmat", (uint64_t)ndig * G, &cmat));
+  APG_TRY(workspace_t(ctx, "u_omat", (uint64_t)ndig * G + 1, &omat));
+  APG_TRY(workspace_t(ctx, "u_dstart", ndig + 1, &dstart));
+  kbegin(ctx, "u_ext_count", dr->n_bytes + 16 * dr->n_reads);
+  k_uext_count<<<G, kUThreads, 0, ctx->stream>>>(rv, kp, cmat);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "u"));
+  k_digit_starts_u<<<1, 64, 0, ctx->stream>>>(omat, ndig, G, dstart);
+  std::vector<uint64_t> ds(ndig + 1);
+  APG_CHECK_HIP(hipMemcpyAsync(ds.data(), dstart, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  const uint64_t n = ds[ndig];
+  st->n_instances = n;
+  KRec *bufA = nullptr, *bufB = nullptr;
+  APG_TRY(workspace_t(ctx, "u_recA", std::max<uint64_t>(n, 1), &bufA));
+  APG_TRY(workspace_t(ctx, "u_recB", std::max<uint64_t>(n, 1), &bufB));
+  kbegin(ctx, "u_ext_scatter", dr->n_bytes + 16 * dr->n_reads + n * sizeof(KRec));
+  k_uext_scatter<<<G, kUThreads, 0, ctx->stream>>>(rv, kp, omat, bufA);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+
+  // ---- U2 --------------------------------------------------------------------
+  const int bb = std::max(kUDigitBits, ceil_log2_u(std::max<uint64_t>(1, (n + kUBucketTarget - 1) / kUBucketTarget)));
+  const int bb_c = std::min(bb, 40);
+  const int rem = bb_c - kUDigitBits;
+  const int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  uint64_t* boff = nullptr;
+  APG_TRY(workspace_t(ctx, "u_boff", (1ull << bb_c) + 1, &boff));
+  std::vector<std::vector<Seg>> parents(ndig);
+  for (uint32_t d = 0; d < ndig; ++d) parents[d].push_back(Seg{ds[d], ds[d + 1] - ds[d]});
+  KRec* cur = bufA;
+  KRec* other = bufB;
+  uint64_t nb = ndig;
+  int consumed = kUDigitBits;
+  if (nlev == 0) APG_CHECK_HIP(hipMemcpyAsync(boff, ds.data(), (ndig + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  for (int lev = 0; lev < nlev; ++lev) {
+    const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
+    consumed += bits;
+    std::vector<uint64_t> hb;
+    const bool last = lev + 1 == nlev;
+    APG_TRY(part_level<KRec>(ctx, cur, other, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "u"));
+    nb = parents.size() << bits;
+    if (!last) {
+      parents.assign(nb, {});
+      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
+    }
+    std::swap(cur, other);
+  }
+
+  // ---- U3 --------------------------------------------------------------------
+  uint32_t *spc = nullptr, *bnd = nullptr, *ovf = nullptr;
+  APG_TRY(workspace_t(ctx, "u_spc", std::max<uint64_t>(n, 1), &spc));
+  APG_TRY(workspace_t(ctx, "u_bnd", nb, &bnd));
+  APG_TRY(workspace_t(ctx, "u_ovf", nb, &ovf));
+  GroupOut go{other, spc, bnd, gs, ovf};  // sparse nodes go to the free ping-pong buffer
+  kbegin(ctx, "u_group", n * sizeof(KRec) * 2);
+  k_ugroup<<<grid_for(ctx, nb, 1), kGThreads, 0, ctx->stream>>>(cur, boff, nb, go);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long h3[3];
+  APG_TRY(d2h_u64(ctx, gs, h3, 3));
+  if (h3[1]) {
+    uint32_t *gtab = nullptr, *grep = nullptr, *gext = nullptr, *gcnt = nullptr;
+    APG_TRY(workspace_t(ctx, "u_gtab", 2 * std::max<uint64_t>(n, 1) + 64, &gtab));
+    APG_TRY(workspace_t(ctx, "u_grep", std::max<uint64_t>(n, 1), &grep));
+    APG_TRY(workspace_t(ctx, "u_gext", std::max<uint64_t>(n, 1), &gext));
+    APG_TRY(workspace_t(ctx, "u_gcnt", std::max<uint64_t>(n, 1), &gcnt));
+    vlog(ctx, "unipaths: %llu oversized buckets -> global grouping", h3[1]);
+    k_ugroup_big<<<(uint32_t)h3[1], kGThreads, 0, ctx->stream>>>(cur, boff, gtab, grep, gext, gcnt, go);
+    APG_CHECK_HIP(hipGetLastError());
+    APG_TRY(d2h_u64(ctx, gs, h3, 3));
+  }
+  const uint64_t N = h3[0];
+  st->n_nodes = N;
+  if (N >= (1ull << 31)) {
+    set_error("unipaths: more than 2^31 distinct K-mers on one device");
+    return APG_E_UNSUPPORTED;
+  }
+  const uint64_t D = 2 * N;
+
+  // ---- U4 --------------------------------------------------------------------
+  uint64_t* nbase = nullptr;
+  KRec* nodes = nullptr;
+  uint32_t* ncnt = nullptr;
+  APG_TRY(workspace_t(ctx, "u_nbase", nb + 1, &nbase));
+  APG_TRY(scan_u32_u64(ctx, bnd, nb, nbase, "un"));
+  APG_TRY(workspace_t(ctx, "u_nodes", std::max<uint64_t>(N, 1), &nodes));
+  APG_TRY(workspace_t(ctx, "u_ncnt", std::max<uint64_t>(N, 1), &ncnt));
+  k_ucompact<<<grid_for(ctx, nb, 1), 256, 0, ctx->stream>>>(other, spc, boff, bnd, nbase, nb, nodes, ncnt);
+  APG_CHECK_HIP(hipGetLastError());
+  uint64_t T = 1024;
+  while (T < 2 * N) T <<= 1;
+  uint32_t* idx = nullptr;
+  APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
+  APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 4, ctx->stream));
+  k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, N, idx, T - 1);
+  APG_CHECK_HIP(hipGetLastError());
+  const NodeIdx ni{nodes, idx, T - 1};
+
+  // ---- U5 --------------------------------------------------------------------
+  RankBufs rb{};
+  APG_TRY(workspace_t(ctx, "u_nxt", std::max<uint64_t>(D, 1), &rb.nxt));
+  APG_TRY(workspace_t(ctx, "u_prv", std::max<uint64_t>(D, 1), &rb.prv));
+  APG_CHECK_HIP(hipMemsetAsync(rb.nxt, 0xff, D * 4, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(rb.prv, 0xff, D * 4, ctx->stream));
+  kbegin(ctx, "u_links", N * 64);
+  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.nxt, rb.prv, gs + 4);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hl[2];
+  APG_TRY(d2h_u64(ctx, gs + 4, hl, 2));
+  st->n_links = hl[0];
+  if (hl[1]) {
+    set_error("unipaths: read-supported edge to a missing K-mer (internal error)");
+    return APG_E_STATE;
+  }
+
+  // ---- U6 --------------------------------------------------------------------
+  APG_TRY(workspace_t(ctx, "u_rulerof", std::max<uint64_t>(D, 1), &rb.ruler_of));
+  APG_TRY(workspace_t(ctx, "u_lrank", std::max<uint64_t>(D, 1), &rb.lrank));
+  APG_TRY(workspace_t(ctx, "u_rnext", std::max<uint64_t>(D, 1), &rb.rnext));
+  APG_TRY(workspace_t(ctx, "u_seglen", std::max<uint64_t>(D, 1), &rb.seglen));
+  APG_TRY(workspace_t(ctx, "u_ptr0", std::max<uint64_t>(D, 1), &rb.ptr0));
+  APG_TRY(workspace_t(ctx, "u_ptr1", std::max<uint64_t>(D, 1), &rb.ptr1));
+  APG_TRY(workspace_t(ctx, "u_hd0", std::max<uint64_t>(D, 1), &rb.hd0));
+  APG_TRY(workspace_t(ctx, "u_hd1", std::max<uint64_t>(D, 1), &rb.hd1));
+  APG_TRY(workspace_t(ctx, "u_off0", std::max<uint64_t>(D, 1), &rb.off0));
+  APG_TRY(workspace_t(ctx, "u_off1", std::max<uint64_t>(D, 1), &rb.off1));
+  APG_TRY(workspace_t(ctx, "u_rlist", std::max<uint64_t>(D, 1), &rb.rlist));
+  uint32_t *fin_ptr = nullptr, *fin_hd = nullptr;
+  uint64_t* fin_off = nullptr;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    APG_CHECK_HIP(hipMemsetAsync(gs + 8, 0, 8 * 8, ctx->stream));
+    k_rank_init<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb);
+    kbegin(ctx, "u_walk", D * 16);
+    k_walk<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, gs + 8);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    unsigned long long hr;
+    APG_TRY(d2h_u64(ctx, gs + 8, &hr, 1));
+    const uint64_t R = hr;
+    if (R) {
+      k_ruler_init<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb);
+      k_ruler_link<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb);
+    }
+    uint32_t *p0 = rb.ptr0, *p1 = rb.ptr1, *h0 = rb.hd0, *h1 = rb.hd1;
+    uint64_t *o0 = rb.off0, *o1 = rb.off1;
+    const int rounds = ceil_log2_u(R + 1) + 1;
+    kbegin(ctx, "u_ruler_jump", (uint64_t)rounds * R * 32);
+    for (int it = 0; it < rounds && R; ++it) {
+      k_ruler_jump<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb.rlist, p0, o0, h0, p1, o1, h1);
+      std::swap(p0, p1);
+      std::swap(o0, o1);
+      std::swap(h0, h1);
+    }
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    fin_ptr = p0;
+    fin_hd = h0;
+    fin_off = o0;
+    // cycles?
+    uint32_t* clist = nullptr;
+    APG_TRY(workspace_t(ctx, "u_clist", std::max<uint64_t>(D, 1), &clist));
+    k_mark_cyclic<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, fin_ptr, clist, gs + 9);
+    APG_CHECK_HIP(hipGetLastError());
+    unsigned long long hc;
+    APG_TRY(d2h_u64(ctx, gs + 9, &hc, 1));
+    if (hc == 0) break;
+    if (attempt == 2) {
+      set_error("unipaths: cycles remain after cutting (internal error)");
+      return APG_E_STATE;
+    }
+    // min K-mer of every cycle by pointer jumping, then cut
+    const uint64_t C = hc;
+    uint32_t *cm0 = rb.ptr1, *cn0 = rb.hd1, *cm1 = rb.seglen, *cn1 = rb.rnext;  // free D-sized scratch
+    k_cyc_init<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, rb.nxt, cm0, cn0);
+    const int cr = ceil_log2_u(C + 1) + 1;
+    for (int it = 0; it < cr; ++it) {
+      k_cyc_jump<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, nodes, kp, cm0, cn0, cm1, cn1);
+      std::swap(cm0, cm1);
+      std::swap(cn0, cn1);
+    }
+    k_cyc_cut<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, nodes, kp, cm0, rb.nxt, rb.prv, gs + 10);
+    APG_CHECK_HIP(hipGetLastError());
+    unsigned long long hcut;
+    APG_TRY(d2h_u64(ctx, gs + 10, &hcut, 1));
+    st->n_cycles_cut += hcut;
+    vlog(ctx, "unipaths: %llu cyclic directed nodes, %llu cuts", hc, hcut);
+  }
+  uint32_t *head = nullptr, *rank = nullptr, *chainlen = nullptr, *tail_of = nullptr;
+  APG_TRY(workspace_t(ctx, "u_head", std::max<uint64_t>(D, 1), &head));
+  APG_TRY(workspace_t(ctx, "u_rank", std::max<uint64_t>(D, 1), &rank));
+  APG_TRY(workspace_t(ctx, "u_chainlen", std::max<uint64_t>(D, 1), &chainlen));
+  APG_TRY(workspace_t(ctx, "u_tailof", std::max<uint64_t>(D, 1), &tail_of));
+  k_rank_final<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, fin_hd, fin_off, head, rank, chainlen, tail_of);
+  APG_CHECK_HIP(hipGetLastError());
+
+  // ---- U7 --------------------------------------------------------------------
+  // pair keys (one per (u, rc u)): at most N pairs
+  uint64_t *pk[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint32_t *ph = nullptr, *ph2 = nullptr;
+  const uint64_t PM = std::max<uint64_t>(N, 1);
+  const char* pkn[6] = {"u_pk0", "u_pk1", "u_pk2", "u_pk3", "u_pk4", "u_pk5"};
+  for (int i = 0; i < 6; ++i) APG_TRY(workspace_t(ctx, pkn[i], PM, &pk[i]));
+  APG_TRY(workspace_t(ctx, "u_ph", PM, &ph));
+  APG_TRY(workspace_t(ctx, "u_ph2", PM, &ph2));
+  kbegin(ctx, "u_pairs", D * 12);
+  k_pairs<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb.prv, tail_of, nodes, kp, pk[0], pk[1], pk[2], ph, gs + 12,
+                                                     gs + 13);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hp[2];
+  APG_TRY(d2h_u64(ctx, gs + 12, hp, 2));
+  const uint64_t P = hp[0], U = hp[1];
+  st->n_unipaths = U;
+  // LSD radix sort of (k0, k1, k2) with payload h, skipping constant digits
+  {
+    APG_CHECK_HIP(hipMemsetAsync(gs + 16, 0, 3 * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gs + 20, 0xff, 3 * 8, ctx->stream));
+    k_digit_or<<<grid_for(ctx, P), 256, 0, ctx->stream>>>(pk[0], pk[1], pk[2], P, gs + 16, gs + 20);
+    unsigned long long ho[7];
+    APG_TRY(d2h_u64(ctx, gs + 16, ho, 7));
+    const uint64_t Gs = std::max<uint64_t>(1, (P + kSortTile - 1) / kSortTile);
+    uint32_t* scm = nullptr;
+    uint64_t* som = nullptr;
+    APG_TRY(workspace_t(ctx, "u_scm", 256 * Gs, &scm));
+    APG_TRY(workspace_t(ctx, "u_som", 256 * Gs + 1, &som));
+    uint64_t *a0 = pk[0], *a1 = pk[1], *a2 = pk[2], *b0 = pk[3], *b1 = pk[4], *b2 = pk[5];
+    uint32_t *ap = ph, *bp = ph2;
+      for (int sel = 2; sel >= 0 && P > 1; --sel) {
+      const uint64_t varying = ho[sel] ^ ho[4 + sel];  // bits not constant over all keys
+      for (int shift = 0; shift < 64; shift += 8) {
+        if (((varying >> shift) & 255) == 0) continue;
+        const uint64_t* key = sel == 0 ? a0 : sel == 1 ? a1 : a2;
+        kbegin(ctx, "u_sort_count", P * 8);
+        k_lsd_count<<<Gs, kSortThreads, 0, ctx->stream>>>(key, P, shift, scm);
+        kend(ctx);
+        APG_TRY(scan_u32_u64(ctx, scm, 256 * Gs, som, "us"));
+        SortCols c{a0, a1, a2, ap, b0, b1, b2, bp};
+        kbegin(ctx, "u_sort_scatter", P * 28 * 2);
+        k_lsd_scatter<<<Gs, kSortThreads, 0, ctx->stream>>>(c, sel, P, shift, som);
+        kend(ctx);
+        std::swap(a0, b0);
+        std::swap(a1, b1);
+        std::swap(a2, b2);
+        std::swap(ap, bp);
+      }
+    }
+    APG_CHECK_HIP(hipGetLastError());
+    ph = ap;  // sorted heads
+  }
+  uint32_t *sz = nullptr, *uni_of_head = nullptr, *uhead = nullptr;
+  uint64_t *ustart = nullptr, *ulen = nullptr, *urc = nullptr, *id_base = nullptr, *ub_off = nullptr;
+  APG_TRY(workspace_t(ctx, "u_sz", PM, &sz));
+  APG_TRY(workspace_t(ctx, "u_ustart", PM + 1, &ustart));
+  APG_TRY(workspace_t(ctx, "u_uoh", std::max<uint64_t>(D, 1), &uni_of_head));
+  APG_TRY(workspace_t(ctx, "u_uhead", std::max<uint64_t>(U, 1), &uhead));
+  APG_TRY(workspace_t(ctx, "u_ulen", std::max<uint64_t>(U, 1), &ulen));
+  APG_TRY(workspace_t(ctx, "u_urc", std::max<uint64_t>(U, 1), &urc));
+  APG_TRY(workspace_t(ctx, "u_idbase", U + 1, &id_base));
+  APG_TRY(workspace_t(ctx, "u_uboff", U + 1, &ub_off));
+  k_pair_sizes<<<grid_for(ctx, P), 256, 0, ctx->stream>>>(P, ph, tail_of, sz);
+  APG_TRY(scan_u32_u64(ctx, sz, P, ustart, "ua"));
+  k_assign<<<grid_for(ctx, P), 256, 0, ctx->stream>>>(P, ph, tail_of, ustart, chainlen, uni_of_head, uhead, ulen, urc);
+  APG_CHECK_HIP(hipGetLastError());
+  // ids and unibase offsets: scans over lengths (u32 copies of ulen)
+  uint32_t* lens32 = nullptr;
+  APG_TRY(workspace_t(ctx, "u_lens32", std::max<uint64_t>(U, 1), &lens32));
+  k_u32_of<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(ulen, U, 0, lens32);
+  APG_TRY(scan_u32_u64(ctx, lens32, U, id_base, "ui"));
+  k_u32_of<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(ulen, U, (uint32_t)(K - 1), lens32);
+  APG_TRY(scan_u32_u64(ctx, lens32, U, ub_off, "uu"));
+  APG_CHECK_HIP(hipGetLastError());
+
+  // ---- U8 --------------------------------------------------------------------
+  uint64_t tot_ub = 0;
+  APG_CHECK_HIP(hipMemcpyAsync(&tot_ub, ub_off + U, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  uint8_t* ub = nullptr;
+  APG_TRY(workspace_t(ctx, "u_ub", std::max<uint64_t>(tot_ub, 1), &ub));
+  kbegin(ctx, "u_unibases", D * 16 + tot_ub);
+  k_unibases<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, nodes, kp, head, rank, uni_of_head, ub_off, ub);
+  kend(ctx);
+  uint32_t *par = nullptr, *isroot = nullptr;
+  uint64_t *vid = nullptr, *from = nullptr, *to = nullptr;
+  APG_TRY(workspace_t(ctx, "u_par", std::max<uint64_t>(2 * U, 1), &par));
+  APG_TRY(workspace_t(ctx, "u_isroot", std::max<uint64_t>(2 * U, 1), &isroot));
+  APG_TRY(workspace_t(ctx, "u_vid", 2 * U + 1, &vid));
+  APG_TRY(workspace_t(ctx, "u_from", std::max<uint64_t>(U, 1), &from));
+  APG_TRY(workspace_t(ctx, "u_to", std::max<uint64_t>(U, 1), &to));
+  k_uf_init<<<grid_for(ctx, 2 * U), 256, 0, ctx->stream>>>(2 * U, par);
+  kbegin(ctx, "u_adjacency", U * 64);
+  k_adjacency<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(U, ni, kp, uhead, tail_of, head, uni_of_head, par, gs + 24);
+  kend(ctx);
+  k_uf_roots<<<grid_for(ctx, 2 * U), 256, 0, ctx->stream>>>(2 * U, par, isroot);
+  APG_TRY(scan_u32_u64(ctx, isroot, 2 * U, vid, "uv"));
+  k_hkp_edges<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(U, par, vid, from, to);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hv[2];
+  APG_CHECK_HIP(hipMemcpyAsync(hv, vid + 2 * U, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(hv + 1, gs + 24, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  st->n_vertices = hv[0];
+  if (hv[1]) {
+    set_error("unipaths: adjacency edge to a missing K-mer (internal error)");
+    return APG_E_STATE;
+  }
+  // read paths
+  uint32_t* nint = nullptr;
+  uint64_t *ioff = nullptr, *istart = nullptr, *ilen = nullptr;
+  uint64_t NI = 0;
+  const bool want_paths = (prm.flags & APG_UNIPATH_READ_PATHS) != 0;
+  if (want_paths) {
+    APG_TRY(workspace_t(ctx, "u_nint", std::max<uint64_t>(dr->n_reads, 1), &nint));
+    APG_TRY(workspace_t(ctx, "u_ioff", dr->n_reads + 1, &ioff));
+    const uint32_t rg = grid_for(ctx, dr->n_reads);
+    kbegin(ctx, "u_read_paths_count", dr->n_bytes + n * 8);
+    k_read_paths<false><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, nint, nullptr,
+                                                     nullptr, nullptr, gs + 25);
+    kend(ctx);
+    APG_TRY(scan_u32_u64(ctx, nint, dr->n_reads, ioff, "up"));
+    APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    APG_TRY(workspace_t(ctx, "u_istart", std::max<uint64_t>(NI, 1), &istart));
+    APG_TRY(workspace_t(ctx, "u_ilen", std::max<uint64_t>(NI, 1), &ilen));
+    kbegin(ctx, "u_read_paths_write", dr->n_bytes + n * 8 + NI * 16);
+    k_read_paths<true><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, nullptr, ioff,
+                                                    istart, ilen, gs + 25);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    st->n_intervals = NI;
+  }
+  APG_TRY(sync(ctx));
+  if (!out) return APG_OK;
+
+  // ---- host copies ------------------------------------------------------------
+  int rc = APG_OK;
+  std::memset(out, 0, sizeof(*out));
+  out->K = K;
+  out->n_nodes = N;
+  out->n_unipaths = U;
+  out->len = host_dup(ulen, U, ctx, &rc);
+  out->id_base = host_dup(id_base, U, ctx, &rc);
+  out->rc = host_dup(urc, U, ctx, &rc);
+  out->ub_off = host_dup(ub_off, U + 1, ctx, &rc);
+  out->unibases = host_dup(ub, tot_ub, ctx, &rc);
+  out->n_vertices = hv[0];
+  out->from = host_dup(from, U, ctx, &rc);
+  out->to = host_dup(to, U, ctx, &rc);
+  out->n_reads = want_paths ? dr->n_reads : 0;
+  out->n_intervals = NI;
+  if (want_paths) {
+    out->path_off = host_dup(ioff, dr->n_reads + 1, ctx, &rc);
+    out->path_start = host_dup(istart, NI, ctx, &rc);
+    out->path_len = host_dup(ilen, NI, ctx, &rc);
+  }
+  if (rc == APG_OK) rc = sync(ctx);
+  if (rc == APG_OK)
+    for (uint64_t i = 0; i < U; ++i) st->max_len = std::max<uint64_t>(st->max_len, out->len[i]);
+  return rc;
+}
+
+}  // namespace apg
+
+using namespace apg;
+
+extern "C" {
+
+void apg_unipath_defaults(apg_unipath_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->K = 96;
+  p->flags = APG_UNIPATH_READ_PATHS;
+}
+
+void apg_unipath_graph_free(apg_unipath_graph* g) {
+  if (!g) return;
+  std::free(g->len);
+  std::free(g->id_base);
+  std::free(g->rc);
+  std::free(g->ub_off);
+  std::free(g->unibases);
+  std::free(g->from);
+  std::free(g->to);
+  std::free(g->path_off);
+  std::free(g->path_start);
+  std::free(g->path_len);
+  std::memset(g, 0, sizeof(*g));
+}
+
+int apg_unipaths_dev(apg_ctx* ctx, const apg_dreads* reads, const apg_unipath_params* pp, apg_unipath_graph* out,
+                     apg_unipath_stats* stats) {
+  APG_REQUIRE(ctx && reads, "apg_unipaths: NULL argument");
+  apg_unipath_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_unipath_defaults(&p);
+  APG_REQUIRE(p.K >= 1 && p.K <= 96, "apg_unipaths: K must be in [1, 96]");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_unipath_stats st;
+  const int rc = unipaths_impl(ctx, reads, p, out, &st);
+  if (rc != APG_OK && out) apg_unipath_graph_free(out);
+  if (stats) *stats = st;
+  return rc;
+}
+
+int apg_unipaths(apg_ctx* ctx, const apg_reads* reads, const apg_unipath_params* p, apg_unipath_graph* out,
+                 apg_unipath_stats* stats) {
+  APG_REQUIRE(ctx && reads && out, "apg_unipaths: NULL argument");
+  apg_dreads* dr = nullptr;
+  APG_TRY(apg_reads_upload(ctx, reads, &dr));
+  const int rc = apg_unipaths_dev(ctx, dr, p, out, stats);
+  apg_reads_free(dr);
+  return rc;
+}
+
+}  // extern "C"

@@ -186,6 +186,34 @@ class Context:
               "apg_reads_download")
         return ReadSet(r.base_off.copy(), r.byte_off.copy(), pk, q)
 
+    # -- unipaths -------------------------------------------------------------
+    def unipaths(self, reads, K: int = 96, read_paths: bool = True, fetch: bool = True):
+        """Unipath graph (Unipather + HyperKmerPath).
+        Returns (graph dict of numpy arrays or None if fetch=False, stats)."""
+        from ._lib import APG_UNIPATH_READ_PATHS, apg_unipath_graph, apg_unipath_params, apg_unipath_stats
+
+        p = apg_unipath_params()
+        lib().apg_unipath_defaults(C.byref(p))
+        p.K = K
+        p.flags = APG_UNIPATH_READ_PATHS if read_paths else 0
+        g = apg_unipath_graph()
+        st = apg_unipath_stats()
+        gp = C.byref(g) if fetch else None
+        L = lib()
+        if isinstance(reads, DeviceReads):
+            check(L.apg_unipaths_dev(self._h, reads.handle, C.byref(p), gp, C.byref(st)), "apg_unipaths_dev")
+        else:
+            if not fetch:
+                raise ValueError("host read sets always fetch the graph")
+            r = reads.c_struct()
+            check(L.apg_unipaths(self._h, C.byref(r), C.byref(p), gp, C.byref(st)), "apg_unipaths")
+        if not fetch:
+            return None, st.as_dict()
+        try:
+            return graph_arrays(g), st.as_dict()
+        finally:
+            L.apg_unipath_graph_free(C.byref(g))
+
     # -- sharded (multi-GPU) stages ------------------------------------------
     def shard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
         B = shard_bins(K, n_shards)
@@ -207,6 +235,33 @@ class Context:
                                        hist.ctypes.data_as(_u64p), hist_len, C.byref(st)),
               "apg_shard_spectrum")
         return hist, st.as_dict()
+
+
+def _arr(p, n, dt):
+    return np.ctypeslib.as_array(p, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+
+
+def graph_arrays(g) -> dict:
+    """apg_unipath_graph -> dict of numpy arrays (same keys as oracle.unipaths)."""
+    U = int(g.n_unipaths)
+    out = {
+        "n_nodes": int(g.n_nodes),
+        "n_unipaths": U,
+        "len": _arr(g.len, U, np.uint64),
+        "id_base": _arr(g.id_base, U, np.uint64),
+        "rc": _arr(g.rc, U, np.uint64),
+        "ub_off": _arr(g.ub_off, U + 1, np.uint64),
+        "n_vertices": int(g.n_vertices),
+        "from": _arr(g.frm, U, np.uint64),
+        "to": _arr(g.to, U, np.uint64),
+    }
+    out["unibases"] = _arr(g.unibases, int(out["ub_off"][-1]) if U else 0, np.uint8)
+    nr = int(g.n_reads)
+    if g.path_off:
+        out["path_off"] = _arr(g.path_off, nr + 1, np.uint64)
+        out["path_start"] = _arr(g.path_start, int(g.n_intervals), np.uint64)
+        out["path_len"] = _arr(g.path_len, int(g.n_intervals), np.uint64)
+    return out
 
 
 def write_kspec(path: str, K: int, hist: np.ndarray) -> None:

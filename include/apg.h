@@ -194,6 +194,70 @@ int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
 int apg_reads_download(apg_ctx* ctx, const apg_dreads* reads, uint8_t* packed, uint8_t* quals);
 
 /* ------------------------------------------------------------------------- */
+/* Unipath graph, 1 <= K <= 96 (default 96).  Replaces CommonPather /        */
+/* ReadsToPathsCoreX ([R:M] src/paths/ReadsToPathsCoreX.cc; .paths.kN),     */
+/* MakeRcDb (.pathsdb.kN, see apg_pathsdb), Unipather ([R:M]                 */
+/* src/paths/Unipath.cc; .unipaths.kN, .unibases.kN via KmerBaseBroker) and  */
+/* the unipath adjacency -> HyperKmerPath ([R:M] src/paths/HyperKmerPath.h). */
+/* Spec: SURVEY §A.5-A.6 made operational in DESIGN.md §Unipaths (node =     */
+/* canonical K-mer of the reads, read-supported edges via extension bits,    */
+/* palindromic K-mers never link, cycles cut before their min K-mer, pairs  */
+/* (u, rc u) sorted by min(first K-mer of u, of rc u), contiguous k-mer ids).*/
+/* ------------------------------------------------------------------------- */
+typedef struct apg_unipath_params {
+  int32_t K;       /* default 96 */
+  uint32_t flags;  /* APG_UNIPATH_* */
+  uint64_t reserved[4];
+} apg_unipath_params;
+
+#define APG_UNIPATH_READ_PATHS 1u /* also compute every read's KmerPath */
+
+typedef struct apg_unipath_stats {
+  uint64_t n_instances;  /* K-mer occurrences in the reads */
+  uint64_t n_nodes;      /* distinct canonical K-mers */
+  uint64_t n_links;      /* unique-successor links (directed) */
+  uint64_t n_cycles_cut; /* cycle pairs broken */
+  uint64_t n_unipaths;
+  uint64_t n_vertices;   /* HyperKmerPath vertices */
+  uint64_t n_intervals;  /* read-path intervals (if requested) */
+  uint64_t max_len;      /* longest unipath (K-mers) */
+} apg_unipath_stats;
+
+/* Library-allocated outputs (release with apg_unipath_graph_free).  Unipath i
+ * has len[i] K-mers with ids [id_base[i], id_base[i]+len[i]), reverse
+ * complement partner rc[i] (== i when palindromic), bases
+ * unibases[ub_off[i] .. ub_off[i+1]) (codes 0..3, K-1+len[i] of them), and is
+ * HyperKmerPath edge from[i] -> to[i].  Read r's KmerPath is intervals
+ * [path_off[r], path_off[r+1]) of (path_start, path_len). */
+typedef struct apg_unipath_graph {
+  int32_t K;
+  int32_t reserved0;
+  uint64_t n_nodes;
+  uint64_t n_unipaths;
+  uint64_t* len;
+  uint64_t* id_base;
+  uint64_t* rc;
+  uint64_t* ub_off;
+  uint8_t* unibases;
+  uint64_t n_vertices;
+  uint64_t* from;
+  uint64_t* to;
+  uint64_t n_reads;
+  uint64_t* path_off;
+  uint64_t n_intervals;
+  uint64_t* path_start;
+  uint64_t* path_len;
+} apg_unipath_graph;
+
+void apg_unipath_defaults(apg_unipath_params* p);
+int apg_unipaths(apg_ctx* ctx, const apg_reads* reads, const apg_unipath_params* p,
+                 apg_unipath_graph* out, apg_unipath_stats* stats);
+/* out may be NULL: build on the device, report stats only (benchmark). */
+int apg_unipaths_dev(apg_ctx* ctx, const apg_dreads* reads, const apg_unipath_params* p,
+                     apg_unipath_graph* out, apg_unipath_stats* stats);
+void apg_unipath_graph_free(apg_unipath_graph* g);
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */
 /* insert N(mean, sd), FR orientation, substitution error rate rising        */
 /* linearly err_lo -> err_hi along the read; Q40 on correct bases, Q2..20 on */

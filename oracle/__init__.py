@@ -122,3 +122,63 @@ def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1):
         raise MemoryError("oracle precorrect failed")
     keys = ["n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"]
     return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), {k: int(v) for k, v in zip(keys, st)}
+
+
+class _OruResult(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_uint64),
+        ("n_unipaths", C.c_uint64),
+        ("len", _u64p),
+        ("id_base", _u64p),
+        ("rc", _u64p),
+        ("ub_off", _u64p),
+        ("unibases", _u8p),
+        ("n_vertices", C.c_uint64),
+        ("frm", _u64p),
+        ("to", _u64p),
+        ("n_reads", C.c_uint64),
+        ("path_off", _u64p),
+        ("n_intervals", C.c_uint64),
+        ("path_start", _u64p),
+        ("path_len", _u64p),
+    ]
+
+
+def _arr(p, n, dt):
+    return np.ctypeslib.as_array(p, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+
+
+def unipaths(reads, K: int = 96) -> dict:
+    """The unipath graph of `reads` as numpy arrays."""
+    L = lib()
+    if not hasattr(L, "_oru"):
+        L.oru_build.restype = C.c_int
+        L.oru_build.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, C.POINTER(_OruResult)]
+        L.oru_free.restype = None
+        L.oru_free.argtypes = [C.POINTER(_OruResult)]
+        L._oru = True
+    res = _OruResult()
+    n, bo, yo, pk = _rp(reads)
+    rc = L.oru_build(n, bo, yo, pk, K, C.byref(res))
+    if rc:
+        raise RuntimeError(f"oracle unipaths failed ({rc})")
+    try:
+        U = int(res.n_unipaths)
+        out = {
+            "n_nodes": int(res.n_nodes),
+            "n_unipaths": U,
+            "len": _arr(res.len, U, np.uint64),
+            "id_base": _arr(res.id_base, U, np.uint64),
+            "rc": _arr(res.rc, U, np.uint64),
+            "ub_off": _arr(res.ub_off, U + 1, np.uint64),
+            "n_vertices": int(res.n_vertices),
+            "from": _arr(res.frm, U, np.uint64),
+            "to": _arr(res.to, U, np.uint64),
+            "path_off": _arr(res.path_off, int(res.n_reads) + 1, np.uint64),
+            "path_start": _arr(res.path_start, int(res.n_intervals), np.uint64),
+            "path_len": _arr(res.path_len, int(res.n_intervals), np.uint64),
+        }
+        out["unibases"] = _arr(res.unibases, int(out["ub_off"][-1]) if U else 0, np.uint8)
+        return out
+    finally:
+        L.oru_free(C.byref(res))

@@ -1,0 +1,79 @@
+"""GPU parity: the unipath graph (nodes, unipaths in emitted order, ids,
+rc partners, unibases, HyperKmerPath vertices/edges, read KmerPaths) from
+libapg's HIP kernels vs oracle/unipath_oracle.cpp — exact equality."""
+import numpy as np
+import pytest
+
+import oracle
+from allpathslg_amd import synth_genome, synth_reads
+from tests.unipath_cases import circular_reads, noisy_reads, palindrome_reads, repeat_genome, tiling
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ["n_nodes", "n_unipaths", "len", "id_base", "rc", "ub_off", "unibases", "n_vertices", "from", "to",
+        "path_off", "path_start", "path_len"]
+
+
+def assert_graph_equal(got, exp):
+    for k in KEYS:
+        a, b = got[k], exp[k]
+        if isinstance(a, np.ndarray):
+            assert a.shape == b.shape, (k, a.shape, b.shape)
+            if not np.array_equal(a, b):
+                bad = np.nonzero(a != b)[0][:5]
+                raise AssertionError(f"{k} differs at {bad.tolist()}: got {a[bad]} expected {b[bad]}")
+        else:
+            assert a == b, (k, a, b)
+
+
+def run(ctx, reads, K):
+    got, st = ctx.unipaths(reads, K)
+    exp = oracle.unipaths(reads, K)
+    assert_graph_equal(got, exp)
+    assert st["n_unipaths"] == exp["n_unipaths"] and st["n_nodes"] == exp["n_nodes"]
+    return got, st
+
+
+def test_linear_genome(gpu_ctx):
+    g = synth_genome(20_000, 3)
+    got, st = run(gpu_ctx, tiling(g), 96)
+    assert got["n_unipaths"] == 2 and st["max_len"] == 20_000 - 96 + 1
+
+
+def test_repeat_genome(gpu_ctx):
+    run(gpu_ctx, tiling(repeat_genome(), L=200, step=5), 96)
+
+
+@pytest.mark.parametrize("K", [31, 63, 96])
+def test_circular_genome_cycles(gpu_ctx, K):
+    got, st = run(gpu_ctx, circular_reads(synth_genome(3000, 11)), K)
+    assert st["n_cycles_cut"] >= 1
+
+
+def test_palindromes_small_k(gpu_ctx):
+    for K in (2, 4, 6):
+        run(gpu_ctx, palindrome_reads(), K)
+
+
+@pytest.mark.parametrize("K", [1, 5, 25, 32, 33, 64, 65, 95, 96])
+def test_noisy_reads(gpu_ctx, K):
+    run(gpu_ctx, noisy_reads(G=30_000, n=6000), K)
+
+
+def test_synthetic_library_and_device_path(gpu_ctx):
+    g = synth_genome(300_000, 51)
+    reads = synth_reads(g, 40_000, seed=52)
+    run(gpu_ctx, reads, 96)
+    d = gpu_ctx.upload(reads)
+    none, st = gpu_ctx.unipaths(d, 96, read_paths=False, fetch=False)
+    assert none is None and st["n_unipaths"] > 0
+    again, _ = gpu_ctx.unipaths(d, 96)
+    assert_graph_equal(again, oracle.unipaths(reads, 96))
+    d.free()
+
+
+def test_empty_and_short(gpu_ctx):
+    from allpathslg_amd import ReadSet
+
+    for reads in (ReadSet.from_sequences([]), ReadSet.from_sequences([[0, 1, 2], [], [3] * 50])):
+        run(gpu_ctx, reads, 96)
