@@ -84,3 +84,7 @@ def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
     out["records_sent"] = n_in
     out["records_received"] = n_out
     return hist_t.cpu().numpy().astype(np.uint64), out
+
+
+def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGroup] = None) -> dict:
+    raise NotImplementedError("multi-GPU unipath build: see DESIGN.md (next)")
