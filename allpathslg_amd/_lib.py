@@ -198,6 +198,16 @@ SIGNATURES = {
         [_P, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph), C.POINTER(apg_unipath_stats)],
     ),
     "apg_unipath_graph_free": (None, [C.POINTER(apg_unipath_graph)]),
+    "apg_ushard_bins": (C.c_int, [C.c_int]),
+    "apg_ushard_count": (C.c_int, [_P, _P, C.c_int, C.c_int, _u64p]),
+    "apg_ushard_scatter": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_void_p]),
+    "apg_ushard_nodes": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, _u64p]),
+    "apg_ushard_export": (C.c_int, [_P, C.c_void_p]),
+    "apg_unipaths_from_nodes": (
+        C.c_int,
+        [_P, C.c_void_p, C.c_uint64, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),
+         C.POINTER(apg_unipath_stats)],
+    ),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),

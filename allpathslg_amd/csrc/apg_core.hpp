@@ -102,6 +102,17 @@ struct apg_ctx {
     uint32_t G = 0, ndig = 0;
     uint64_t total = 0;
   } xstate;
+
+  // Unipath-stage plan of the last apg_ushard_count / apg_ushard_nodes.
+  struct UState {
+    bool valid = false;
+    uint64_t gen = 0;
+    int K = 0;
+    uint32_t G = 0;
+    uint64_t n = 0;        // instances extracted
+    uint64_t n_nodes = 0;  // nodes of the last apg_ushard_nodes
+    uint64_t n_recv = 0;
+  } ustate;
 };
 
 namespace apg {

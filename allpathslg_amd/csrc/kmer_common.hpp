@@ -132,6 +132,45 @@ __device__ __forceinline__ uint64_t wave_match(uint32_t d, bool valid, int nb) {
   return valid ? peers : 0;
 }
 
+// Wave-aggregated append: every active lane calls it (converged); lanes with
+// pred get consecutive slots from ONE atomicAdd per wave on *ctr.  Returns
+// the lane's slot (meaningless where !pred).
+__device__ __forceinline__ unsigned long long wave_append(unsigned long long* ctr, bool pred,
+                                                          unsigned long long amount = 1) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0) return 0;
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m) * amount);
+  base = __shfl(base, leader, 64);
+  return base + (unsigned long long)__popcll(m & lanemask_lt()) * amount;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* smem, T* total);
+
+// Block-aggregated append: every thread of the block calls it with its count
+// of items to append; ONE atomicAdd per block call reserves the block's
+// slots (same-address atomics serialise chip-wide, so per-wave appends over
+// hundreds of millions of items are contention-bound).  sm: >= 32 u32 of LDS
+// scan scratch; sbase: one LDS u64.  Returns the thread's first slot.
+__device__ __forceinline__ unsigned long long block_append(unsigned long long* ctr, uint32_t count, uint32_t* sm,
+                                                           unsigned long long* sbase) {
+  uint32_t tot;
+  const uint32_t ex = block_exclusive_scan<uint32_t>(count, sm, &tot);
+  if (threadIdx.x == 0) *sbase = tot ? atomicAdd(ctr, (unsigned long long)tot) : 0ull;
+  __syncthreads();
+  const unsigned long long b = *sbase + ex;
+  __syncthreads();
+  return b;
+}
+
+// Wave-aggregated add of per-lane values: one atomic per wave.
+__device__ __forceinline__ void wave_add(unsigned long long* ctr, unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if (lane_id() == 0 && v) atomicAdd(ctr, v);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_scan(T x) {
   const int lane = lane_id();

@@ -524,7 +524,13 @@ __device__ __forceinline__ uint32_t directed_of(const NodeIdx& ni, const K3& s, 
 // ---------------------------------------------------------------------------
 // U5: unique links
 // ---------------------------------------------------------------------------
-__global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, uint32_t* __restrict__ nxt, uint32_t* __restrict__ prv,
+// Per directed node ranking state, one 16-byte record: a walk step touches
+// one cache line instead of four arrays.
+struct DN {
+  uint32_t nxt, prv, ruler, lrank;
+};
+
+__global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, DN* __restrict__ dn,
                         unsigned long long* __restrict__ stat) {
   unsigned long long nl = 0, bad = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -547,8 +553,8 @@ __global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, uint32_t* __restrict__ 
       if (k3_eq(wk, revcomp(wk, kp))) continue;
       const uint32_t wext = (uint32_t)(ni.nodes[w >> 1].meta & 0xff);
       if (__popc(in_set(wext, w & 1)) != 1) continue;
-      nxt[2 * i + o] = w;
-      prv[w] = (uint32_t)(2 * i + o);
+      dn[2 * i + o].nxt = w;
+      dn[w].prv = (uint32_t)(2 * i + o);
       ++nl;
     }
   }
@@ -567,35 +573,63 @@ __global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, uint32_t* __restrict__ 
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRulerMask = 31;  // sampled rulers: 1 in 32
 
-__device__ __forceinline__ bool is_ruler(uint32_t v, const uint32_t* prv) {
-  return prv[v] == kNone || ((uint32_t)fmix64(v) & kRulerMask) == 0;
+__device__ __forceinline__ bool is_ruler(uint32_t v, const DN* dn) {
+  return dn[v].prv == kNone || ((uint32_t)fmix64(v) & kRulerMask) == 0;
 }
 
 struct RankBufs {
-  uint32_t *nxt, *prv;
-  uint32_t *ruler_of, *lrank, *rnext, *seglen;
-  uint32_t *ptr0, *ptr1, *hd0, *hd1;
-  uint64_t *off0, *off1;
-  uint32_t* rlist;
+  DN* dn;
+  uint32_t *rnext, *seglen;
+  unsigned long long* state;  // per ruler: x (ptr or head) | done << 32 | off << 33
+  uint32_t *rlist, *alist0, *alist1;
 };
 
-__global__ void k_rank_init(uint64_t D, RankBufs rb) {
-  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < D; v += (uint64_t)gridDim.x * blockDim.x)
-    rb.ruler_of[v] = kNone;
+__device__ __forceinline__ unsigned long long st_pack(uint32_t x, bool done, uint64_t off) {
+  return (unsigned long long)x | ((unsigned long long)done << 32) | ((unsigned long long)off << 33);
+}
+__device__ __forceinline__ uint32_t st_x(unsigned long long s) { return (uint32_t)s; }
+__device__ __forceinline__ bool st_done(unsigned long long s) { return (s >> 32) & 1; }
+__device__ __forceinline__ uint64_t st_off(unsigned long long s) { return s >> 33; }
+
+constexpr int kTI = 16;                 // items per thread per tile
+constexpr uint64_t kTileN = 256 * kTI;  // items per block tile (one append atomic each)
+
+__global__ void __launch_bounds__(256) k_find_rulers(uint64_t D, RankBufs rb, unsigned long long* __restrict__ nrul) {
+  __shared__ uint32_t sm[64];
+  __shared__ unsigned long long sb;
+  const uint64_t ntiles = (D + kTileN - 1) / kTileN;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint32_t flags = 0, cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kTI; ++i) {
+      const uint64_t v = t * kTileN + (uint64_t)i * 256 + threadIdx.x;
+      if (v < D) {
+        rb.dn[v].ruler = kNone;
+        if (is_ruler((uint32_t)v, rb.dn)) {
+          flags |= 1u << i;
+          ++cnt;
+        }
+      }
+    }
+    unsigned long long j = block_append(nrul, cnt, sm, &sb);
+#pragma unroll
+    for (int i = 0; i < kTI; ++i)
+      if (flags & (1u << i)) rb.rlist[j++] = (uint32_t)(t * kTileN + (uint64_t)i * 256 + threadIdx.x);
+  }
 }
 
-// Each ruler walks its segment (up to the next ruler / end).
-__global__ void k_walk(uint64_t D, RankBufs rb, unsigned long long* __restrict__ nrul) {
-  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t v = (uint32_t)v0;
-    if (!is_ruler(v, rb.prv)) continue;
-    rb.rlist[atomicAdd(nrul, 1ull)] = v;
+// Each ruler walks its segment (up to the next ruler / end): one thread per
+// ruler, so every lane of a wave walks.
+__global__ void k_walk(uint64_t R, uint64_t D, RankBufs rb) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = rb.rlist[i];
     uint32_t x = v, r = 0;
     for (uint64_t guard = 0; guard <= D; ++guard) {
-      rb.ruler_of[x] = v;
-      rb.lrank[x] = r++;
-      const uint32_t y = rb.nxt[x];
-      if (y == kNone || is_ruler(y, rb.prv)) {
+      DN& d = rb.dn[x];
+      d.ruler = v;
+      d.lrank = r++;
+      const uint32_t y = d.nxt;
+      if (y == kNone || is_ruler(y, rb.dn)) {
         rb.rnext[v] = y;
         break;
       }
@@ -605,64 +639,113 @@ __global__ void k_walk(uint64_t D, RankBufs rb, unsigned long long* __restrict__
   }
 }
 
-__global__ void k_ruler_init(uint64_t R, RankBufs rb) {
+// every ruler starts as a finished head; ruler successors are then linked
+__global__ void k_ruler_state0(uint64_t R, RankBufs rb) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t r = rb.rlist[i];
-    rb.ptr0[r] = kNone;
-    rb.off0[r] = 0;
-    rb.hd0[r] = r;
+    rb.state[r] = st_pack(r, true, 0);
   }
 }
-__global__ void k_ruler_link(uint64_t R, RankBufs rb) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = rb.rlist[i];
-    const uint32_t s = rb.rnext[r];
-    if (s != kNone) {  // s is a ruler with unique ruler predecessor r
-      rb.ptr0[s] = r;
-      rb.off0[s] = rb.seglen[r];
-      rb.hd0[s] = kNone;
+__global__ void __launch_bounds__(256) k_ruler_state1(uint64_t R, RankBufs rb, unsigned long long* __restrict__ nact) {
+  __shared__ uint32_t sm[64];
+  __shared__ unsigned long long sb;
+  const uint64_t ntiles = (R + kTileN - 1) / kTileN;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint32_t flags = 0, cnt = 0;
+    uint32_t ss[kTI];
+#pragma unroll
+    for (int i = 0; i < kTI; ++i) {
+      const uint64_t k = t * kTileN + (uint64_t)i * 256 + threadIdx.x;
+      ss[i] = kNone;
+      if (k < R) {
+        const uint32_t r = rb.rlist[k];
+        const uint32_t s = rb.rnext[r];  // a ruler whose unique ruler predecessor is r
+        if (s != kNone) {
+          rb.state[s] = st_pack(r, false, rb.seglen[r]);
+          ss[i] = s;
+          flags |= 1u << i;
+          ++cnt;
+        }
+      }
     }
-  }
-}
-// one pointer-jumping round: (ptr0, off0, hd0) -> (ptr1, off1, hd1)
-__global__ void k_ruler_jump(uint64_t R, const uint32_t* __restrict__ rlist, const uint32_t* __restrict__ ptr0,
-                             const uint64_t* __restrict__ off0, const uint32_t* __restrict__ hd0,
-                             uint32_t* __restrict__ ptr1, uint64_t* __restrict__ off1, uint32_t* __restrict__ hd1) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = rlist[i];
-    const uint32_t q = ptr0[r];
-    if (q == kNone) {
-      ptr1[r] = kNone;
-      off1[r] = off0[r];
-      hd1[r] = hd0[r];
-    } else {
-      const uint32_t qq = ptr0[q];
-      off1[r] = off0[r] + off0[q];
-      ptr1[r] = qq;
-      hd1[r] = qq == kNone ? hd0[q] : kNone;
-    }
+    unsigned long long j = block_append(nact, cnt, sm, &sb);
+#pragma unroll
+    for (int i = 0; i < kTI; ++i)
+      if (flags & (1u << i)) rb.alist0[j++] = ss[i];
   }
 }
 
-// cyclic directed nodes: unvisited, or on a ruler whose pointer never ended
-__global__ void k_mark_cyclic(uint64_t D, RankBufs rb, const uint32_t* __restrict__ ptr, uint32_t* __restrict__ clist,
-                              unsigned long long* __restrict__ ncyc) {
-  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t v = (uint32_t)v0;
-    const uint32_t r = rb.ruler_of[v];
-    if (r == kNone || ptr[r] != kNone) clist[atomicAdd(ncyc, 1ull)] = v;
+// Asynchronous pointer jumping over the still-active rulers.  A state word is
+// a consistent (pointer, distance) pair read and written as one 8-byte
+// access, so a stale read is still a valid jump.
+__global__ void __launch_bounds__(256) k_ruler_jump(uint64_t n, const uint32_t* __restrict__ ain,
+                                                    unsigned long long* __restrict__ state, uint32_t* __restrict__ aout,
+                                                    unsigned long long* __restrict__ nout) {
+  __shared__ uint32_t sm[64];
+  __shared__ unsigned long long sb;
+  const uint64_t ntiles = (n + kTileN - 1) / kTileN;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint32_t flags = 0, cnt = 0;
+    uint32_t rr[kTI];
+#pragma unroll
+    for (int i = 0; i < kTI; ++i) {
+      const uint64_t k = t * kTileN + (uint64_t)i * 256 + threadIdx.x;
+      rr[i] = 0;
+      if (k < n) {
+        const uint32_t r = ain[k];
+        const unsigned long long s = __hip_atomic_load(&state[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long q = __hip_atomic_load(&state[st_x(s)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&state[r], st_pack(st_x(q), st_done(q), st_off(s) + st_off(q)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        rr[i] = r;
+        if (!st_done(q)) {
+          flags |= 1u << i;
+          ++cnt;
+        }
+      }
+    }
+    unsigned long long j = block_append(nout, cnt, sm, &sb);
+#pragma unroll
+    for (int i = 0; i < kTI; ++i)
+      if (flags & (1u << i)) aout[j++] = rr[i];
+  }
+}
+
+// cyclic directed nodes: unvisited, or on a ruler that never reached a head
+__global__ void __launch_bounds__(256) k_mark_cyclic(uint64_t D, RankBufs rb, uint32_t* __restrict__ clist,
+                                                     unsigned long long* __restrict__ ncyc) {
+  __shared__ uint32_t sm[64];
+  __shared__ unsigned long long sb;
+  const uint64_t ntiles = (D + kTileN - 1) / kTileN;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint32_t flags = 0, cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kTI; ++i) {
+      const uint64_t v = t * kTileN + (uint64_t)i * 256 + threadIdx.x;
+      if (v < D) {
+        const uint32_t r = rb.dn[v].ruler;
+        if (r == kNone || !st_done(rb.state[r])) {
+          flags |= 1u << i;
+          ++cnt;
+        }
+      }
+    }
+    unsigned long long j = block_append(ncyc, cnt, sm, &sb);
+#pragma unroll
+    for (int i = 0; i < kTI; ++i)
+      if (flags & (1u << i)) clist[j++] = (uint32_t)(t * kTileN + (uint64_t)i * 256 + threadIdx.x);
   }
 }
 
 __device__ __forceinline__ uint32_t seq_min(const KRec* nodes, uint32_t x, uint32_t y, const KeyP& p) {
   return k3_lt(dseq(nodes, y, p), dseq(nodes, x, p)) ? y : x;
 }
-__global__ void k_cyc_init(uint64_t C, const uint32_t* __restrict__ clist, const uint32_t* __restrict__ nxt,
+__global__ void k_cyc_init(uint64_t C, const uint32_t* __restrict__ clist, const DN* __restrict__ dn,
                            uint32_t* __restrict__ cm, uint32_t* __restrict__ cn) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t v = clist[i];
     cm[v] = v;
-    cn[v] = nxt[v];
+    cn[v] = dn[v].nxt;
   }
 }
 __global__ void k_cyc_jump(uint64_t C, const uint32_t* __restrict__ clist, const KRec* __restrict__ nodes, KeyP kp,
@@ -677,37 +760,37 @@ __global__ void k_cyc_jump(uint64_t C, const uint32_t* __restrict__ clist, const
 }
 // Cut each (C, rc C) pair once, before the smaller of the two cycles' minima.
 __global__ void k_cyc_cut(uint64_t C, const uint32_t* __restrict__ clist, const KRec* __restrict__ nodes, KeyP kp,
-                          const uint32_t* __restrict__ cm, uint32_t* __restrict__ nxt, uint32_t* __restrict__ prv,
+                          const uint32_t* __restrict__ cm, DN* __restrict__ dn,
                           unsigned long long* __restrict__ ncut) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t v = clist[i];
     if (cm[v] != v) continue;
     const uint32_t mr = cm[v ^ 1];
     if (mr != v && !k3_lt(dseq(nodes, v, kp), dseq(nodes, mr, kp))) continue;
-    const uint32_t p = prv[v];
-    const bool mirror = nxt[v ^ 1] == (p ^ 1) && (v ^ 1) != p;
-    nxt[p] = kNone;
-    prv[v] = kNone;
+    const uint32_t p = dn[v].prv;
+    const bool mirror = dn[v ^ 1].nxt == (p ^ 1) && (v ^ 1) != p;
+    dn[p].nxt = kNone;
+    dn[v].prv = kNone;
     if (mirror) {
-      nxt[v ^ 1] = kNone;
-      prv[p ^ 1] = kNone;
+      dn[v ^ 1].nxt = kNone;
+      dn[p ^ 1].prv = kNone;
     }
     atomicAdd(ncut, 1ull);
   }
 }
 
 // final per-node head and rank; tails record their chain's length
-__global__ void k_rank_final(uint64_t D, RankBufs rb, const uint32_t* __restrict__ hd, const uint64_t* __restrict__ off,
-                             uint32_t* __restrict__ head, uint32_t* __restrict__ rank, uint32_t* __restrict__ chainlen,
-                             uint32_t* __restrict__ tail_of) {
+__global__ void k_rank_final(uint64_t D, RankBufs rb, uint32_t* __restrict__ head, uint32_t* __restrict__ rank,
+                             uint32_t* __restrict__ chainlen, uint32_t* __restrict__ tail_of) {
   for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t v = (uint32_t)v0;
-    const uint32_t r = rb.ruler_of[v];
-    const uint32_t h = hd[r];
-    const uint32_t k = (uint32_t)(off[r] + rb.lrank[v]);
+    const DN d = rb.dn[v];
+    const unsigned long long s = rb.state[d.ruler];
+    const uint32_t h = st_x(s);
+    const uint32_t k = (uint32_t)(st_off(s) + d.lrank);
     head[v] = h;
     rank[v] = k;
-    if (rb.nxt[v] == kNone) {
+    if (d.nxt == kNone) {
       chainlen[h] = k + 1;
       tail_of[h] = v;
     }
@@ -717,26 +800,50 @@ __global__ void k_rank_final(uint64_t D, RankBufs rb, const uint32_t* __restrict
 // ---------------------------------------------------------------------------
 // U7: unipath pairs and their order
 // ---------------------------------------------------------------------------
-__global__ void k_pairs(uint64_t D, const uint32_t* __restrict__ prv, const uint32_t* __restrict__ tail_of,
-                        const KRec* __restrict__ nodes, KeyP kp, uint64_t* __restrict__ pk0, uint64_t* __restrict__ pk1,
-                        uint64_t* __restrict__ pk2, uint32_t* __restrict__ ph, unsigned long long* __restrict__ np,
-                        unsigned long long* __restrict__ nu) {
-  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t h = (uint32_t)v0;
-    if (prv[h] != kNone) continue;
-    const uint32_t rh = tail_of[h] ^ 1;  // head of the rc path
-    const K3 hs = dseq(nodes, h, kp);
-    if (rh != h) {  // emit once per (u, rc u): smaller head K-mer; equal only for a palindromic K-mer's two nodes
-      const K3 rs = dseq(nodes, rh, kp);
-      if (!(k3_lt(hs, rs) || (k3_eq(hs, rs) && h < rh))) continue;
+__device__ __forceinline__ bool pair_emit(uint32_t h, const DN* dn, const uint32_t* tail_of, const KRec* nodes,
+                                          const KeyP& kp) {
+  if (dn[h].prv != kNone) return false;
+  const uint32_t rh = tail_of[h] ^ 1;  // head of the rc path
+  if (rh == h) return true;            // palindromic path: its own partner
+  // once per (u, rc u): smaller head K-mer; equal only for a palindromic K-mer's two nodes
+  const K3 hs = dseq(nodes, h, kp), rs = dseq(nodes, rh, kp);
+  return k3_lt(hs, rs) || (k3_eq(hs, rs) && h < rh);
+}
+
+__global__ void __launch_bounds__(256) k_pairs(uint64_t D, const DN* __restrict__ dn,
+                                               const uint32_t* __restrict__ tail_of, const KRec* __restrict__ nodes,
+                                               KeyP kp, uint64_t* __restrict__ pk0, uint64_t* __restrict__ pk1,
+                                               uint64_t* __restrict__ pk2, uint32_t* __restrict__ ph,
+                                               unsigned long long* __restrict__ np, unsigned long long* __restrict__ nu) {
+  __shared__ uint32_t sm[64];
+  __shared__ unsigned long long sb;
+  unsigned long long units = 0;
+  const uint64_t ntiles = (D + kTileN - 1) / kTileN;
+  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    uint32_t flags = 0, cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kTI; ++i) {
+      const uint64_t v = t * kTileN + (uint64_t)i * 256 + threadIdx.x;
+      if (v < D && pair_emit((uint32_t)v, dn, tail_of, nodes, kp)) {
+        flags |= 1u << i;
+        ++cnt;
+      }
     }
-    const unsigned long long j = atomicAdd(np, 1ull);
-    pk0[j] = hs.a;
-    pk1[j] = hs.b;
-    pk2[j] = hs.c;
-    ph[j] = h;
-    atomicAdd(nu, rh == h ? 1ull : 2ull);
+    unsigned long long j = block_append(np, cnt, sm, &sb);
+#pragma unroll
+    for (int i = 0; i < kTI; ++i) {
+      if (!(flags & (1u << i))) continue;
+      const uint32_t h = (uint32_t)(t * kTileN + (uint64_t)i * 256 + threadIdx.x);
+      const K3 hs = dseq(nodes, h, kp);
+      pk0[j] = hs.a;
+      pk1[j] = hs.b;
+      pk2[j] = hs.c;
+      ph[j] = h;
+      ++j;
+      units += (tail_of[h] ^ 1) == h ? 1 : 2;
+    }
   }
+  wave_add(nu, units);
 }
 
 // Stable LSD radix pass over (key, payload) columns: digit = (key[sel] >> shift) & 255.
@@ -876,10 +983,14 @@ __global__ void k_unibases(uint64_t D, const KRec* __restrict__ nodes, KeyP kp, 
   for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t v = (uint32_t)v0;
     const uint32_t u = uni_of_head[head[v]];
-    const K3 s = dseq(nodes, v, kp);
     const uint64_t o = ub_off[u] + rank[v];
-    ub[o + kp.K - 1] = (uint8_t)(s.c & 3);
+    const KRec& x = nodes[v >> 1];
+    // last base of seq(v): of the key (fw), or the complement of its first base (rc)
+    const int tb = 2 * (kp.K - 1);
+    const uint64_t first = ((tb >= 128 ? x.k0 : tb >= 64 ? x.k1 : x.k2) >> (tb & 63)) & 3;
+    ub[o + kp.K - 1] = (uint8_t)((v & 1) ? 3 - first : (x.k2 & 3));
     if (rank[v] == 0) {
+      const K3 s = dseq(nodes, v, kp);
       for (int t = 0; t < kp.K - 1; ++t) {  // base t of the K-mer
         const int bit = 2 * (kp.K - 1 - t);
         const uint64_t limb = bit >= 128 ? s.a : bit >= 64 ? s.b : s.c;
@@ -1037,17 +1148,11 @@ static int d2h_u64(apg_ctx* ctx, const unsigned long long* d, unsigned long long
   return sync(ctx);
 }
 
-static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
-                         apg_unipath_stats* st) {
-  const int K = prm.K;
-  const KeyP kp = make_keyp(K);
-  std::memset(st, 0, sizeof(*st));
+// U1 count: per-digit instance counts (2^kUDigitBits digits, host) and the
+// scanned [digit][block] matrix left in workspace "u_omat" for u_extract_scatter.
+static int u_extract_count(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, std::vector<uint64_t>* counts,
+                           uint32_t* Gout) {
   ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  unsigned long long* gs = nullptr;  // general device counters
-  APG_TRY(workspace_t(ctx, "u_gs", 32, &gs));
-  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 32 * 8, ctx->stream));
-
-  // ---- U1 --------------------------------------------------------------------
   const uint32_t ndig = 1u << kUDigitBits;
   const uint32_t G =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUMaxBlocks, (dr->n_reads + 255) / 256));
@@ -1065,50 +1170,77 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   std::vector<uint64_t> ds(ndig + 1);
   APG_CHECK_HIP(hipMemcpyAsync(ds.data(), dstart, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  const uint64_t n = ds[ndig];
-  st->n_instances = n;
+  counts->resize(ndig);
+  for (uint32_t d = 0; d < ndig; ++d) (*counts)[d] = ds[d + 1] - ds[d];
+  *Gout = G;
+  return APG_OK;
+}
+
+// U1 scatter (after u_extract_count on the same reads): instances grouped by digit.
+static int u_extract_scatter(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, uint32_t G, uint64_t n, KRec* out) {
+  ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  const uint32_t ndig = 1u << kUDigitBits;
+  uint64_t* omat = nullptr;
+  APG_TRY(workspace_t(ctx, "u_omat", (uint64_t)ndig * G + 1, &omat));
+  kbegin(ctx, "u_ext_scatter", dr->n_bytes + 16 * dr->n_reads + n * sizeof(KRec));
+  k_uext_scatter<<<G, kUThreads, 0, ctx->stream>>>(rv, kp, omat, out);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
+// U2 + U3 + compaction: the distinct nodes (key, OR of extension bits) of
+// the instances in `src`, laid out as `parents` (groups of segments whose top
+// `consumed` meta bits are fixed).  src is never written.  Nodes land in
+// workspace "u_nodes".
+static int u_build_nodes(apg_ctx* ctx, const KRec* src, std::vector<std::vector<Seg>> parents, uint64_t n, int consumed,
+                         KRec** nodes_out, uint64_t* N_out) {
+  unsigned long long* gs = nullptr;
+  APG_TRY(workspace_t(ctx, "u_gs_nodes", 4, &gs));
+  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));
+  const int bb = std::max(consumed, ceil_log2_u(std::max<uint64_t>(1, (n + kUBucketTarget - 1) / kUBucketTarget)));
+  const int bb_c = std::min(bb, 40);
+  const int rem = bb_c - consumed;
+  int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  bool split = false;
+  for (const auto& pp : parents) split |= pp.size() > 1;
+  if (nlev == 0 && split) nlev = 1;  // regroup multi-segment parents
   KRec *bufA = nullptr, *bufB = nullptr;
   APG_TRY(workspace_t(ctx, "u_recA", std::max<uint64_t>(n, 1), &bufA));
   APG_TRY(workspace_t(ctx, "u_recB", std::max<uint64_t>(n, 1), &bufB));
-  kbegin(ctx, "u_ext_scatter", dr->n_bytes + 16 * dr->n_reads + n * sizeof(KRec));
-  k_uext_scatter<<<G, kUThreads, 0, ctx->stream>>>(rv, kp, omat, bufA);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-
-  // ---- U2 --------------------------------------------------------------------
-  const int bb = std::max(kUDigitBits, ceil_log2_u(std::max<uint64_t>(1, (n + kUBucketTarget - 1) / kUBucketTarget)));
-  const int bb_c = std::min(bb, 40);
-  const int rem = bb_c - kUDigitBits;
-  const int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
   uint64_t* boff = nullptr;
   APG_TRY(workspace_t(ctx, "u_boff", (1ull << bb_c) + 1, &boff));
-  std::vector<std::vector<Seg>> parents(ndig);
-  for (uint32_t d = 0; d < ndig; ++d) parents[d].push_back(Seg{ds[d], ds[d + 1] - ds[d]});
-  KRec* cur = bufA;
-  KRec* other = bufB;
-  uint64_t nb = ndig;
-  int consumed = kUDigitBits;
-  if (nlev == 0) APG_CHECK_HIP(hipMemcpyAsync(boff, ds.data(), (ndig + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  const KRec* cur = src;
+  uint64_t nb = parents.size();
+  if (nlev == 0) {
+    std::vector<uint64_t> hb(nb + 1, 0);
+    for (uint64_t q = 0; q < nb; ++q) {
+      hb[q] = parents[q].empty() ? (q ? hb[q - 1] : 0) : parents[q][0].start;
+      hb[q + 1] = hb[q] + (parents[q].empty() ? 0 : parents[q][0].len);
+    }
+    hb[nb] = n;
+    APG_CHECK_HIP(hipMemcpyAsync(boff, hb.data(), (nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  }
   for (int lev = 0; lev < nlev; ++lev) {
     const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
     consumed += bits;
     std::vector<uint64_t> hb;
     const bool last = lev + 1 == nlev;
-    APG_TRY(part_level<KRec>(ctx, cur, other, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "u"));
+    KRec* dst = (cur == bufA) ? bufB : bufA;
+    APG_TRY(part_level<KRec>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "u"));
     nb = parents.size() << bits;
     if (!last) {
       parents.assign(nb, {});
       for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
     }
-    std::swap(cur, other);
+    cur = dst;
   }
-
-  // ---- U3 --------------------------------------------------------------------
+  KRec* other = (cur == bufA) ? bufB : bufA;  // free buffer: sparse nodes
   uint32_t *spc = nullptr, *bnd = nullptr, *ovf = nullptr;
   APG_TRY(workspace_t(ctx, "u_spc", std::max<uint64_t>(n, 1), &spc));
   APG_TRY(workspace_t(ctx, "u_bnd", nb, &bnd));
   APG_TRY(workspace_t(ctx, "u_ovf", nb, &ovf));
-  GroupOut go{other, spc, bnd, gs, ovf};  // sparse nodes go to the free ping-pong buffer
+  GroupOut go{other, spc, bnd, gs, ovf};
   kbegin(ctx, "u_group", n * sizeof(KRec) * 2);
   k_ugroup<<<grid_for(ctx, nb, 1), kGThreads, 0, ctx->stream>>>(cur, boff, nb, go);
   kend(ctx);
@@ -1127,14 +1259,6 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
     APG_TRY(d2h_u64(ctx, gs, h3, 3));
   }
   const uint64_t N = h3[0];
-  st->n_nodes = N;
-  if (N >= (1ull << 31)) {
-    set_error("unipaths: more than 2^31 distinct K-mers on one device");
-    return APG_E_UNSUPPORTED;
-  }
-  const uint64_t D = 2 * N;
-
-  // ---- U4 --------------------------------------------------------------------
   uint64_t* nbase = nullptr;
   KRec* nodes = nullptr;
   uint32_t* ncnt = nullptr;
@@ -1144,23 +1268,48 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   APG_TRY(workspace_t(ctx, "u_ncnt", std::max<uint64_t>(N, 1), &ncnt));
   k_ucompact<<<grid_for(ctx, nb, 1), 256, 0, ctx->stream>>>(other, spc, boff, bnd, nbase, nb, nodes, ncnt);
   APG_CHECK_HIP(hipGetLastError());
+  *nodes_out = nodes;
+  *N_out = N;
+  return APG_OK;
+}
+
+// U4 index + U5..U8 on a complete node set; read KmerPaths for `dr` (may be
+// null when no read paths are requested).
+static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads* dr, const apg_unipath_params& prm,
+                   apg_unipath_graph* out, apg_unipath_stats* st) {
+  const int K = prm.K;
+  const KeyP kp = make_keyp(K);
+  st->n_nodes = N;
+  if (N >= (1ull << 31)) {
+    set_error("unipaths: more than 2^31 distinct K-mers on one device");
+    return APG_E_UNSUPPORTED;
+  }
+  const uint64_t D = 2 * N;
+  const uint64_t n = st->n_instances;
+  unsigned long long* gs = nullptr;  // general device counters
+  APG_TRY(workspace_t(ctx, "u_gs", 32, &gs));
+  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 32 * 8, ctx->stream));
+  ReadsV rv{nullptr, nullptr, nullptr, 0};
+  if (dr) rv = ReadsV{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+
+  // ---- U4 index --------------------------------------------------------------
   uint64_t T = 1024;
   while (T < 2 * N) T <<= 1;
   uint32_t* idx = nullptr;
   APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
   APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 4, ctx->stream));
+  kbegin(ctx, "u_node_insert", N * 40);
   k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, N, idx, T - 1);
+  kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   const NodeIdx ni{nodes, idx, T - 1};
 
   // ---- U5 --------------------------------------------------------------------
   RankBufs rb{};
-  APG_TRY(workspace_t(ctx, "u_nxt", std::max<uint64_t>(D, 1), &rb.nxt));
-  APG_TRY(workspace_t(ctx, "u_prv", std::max<uint64_t>(D, 1), &rb.prv));
-  APG_CHECK_HIP(hipMemsetAsync(rb.nxt, 0xff, D * 4, ctx->stream));
-  APG_CHECK_HIP(hipMemsetAsync(rb.prv, 0xff, D * 4, ctx->stream));
+  APG_TRY(workspace_t(ctx, "u_dn", std::max<uint64_t>(D, 1), &rb.dn));
+  APG_CHECK_HIP(hipMemsetAsync(rb.dn, 0xff, D * sizeof(DN), ctx->stream));
   kbegin(ctx, "u_links", N * 64);
-  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.nxt, rb.prv, gs + 4);
+  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.dn, gs + 4);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hl[2];
@@ -1172,74 +1321,65 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   }
 
   // ---- U6 --------------------------------------------------------------------
-  APG_TRY(workspace_t(ctx, "u_rulerof", std::max<uint64_t>(D, 1), &rb.ruler_of));
-  APG_TRY(workspace_t(ctx, "u_lrank", std::max<uint64_t>(D, 1), &rb.lrank));
   APG_TRY(workspace_t(ctx, "u_rnext", std::max<uint64_t>(D, 1), &rb.rnext));
   APG_TRY(workspace_t(ctx, "u_seglen", std::max<uint64_t>(D, 1), &rb.seglen));
-  APG_TRY(workspace_t(ctx, "u_ptr0", std::max<uint64_t>(D, 1), &rb.ptr0));
-  APG_TRY(workspace_t(ctx, "u_ptr1", std::max<uint64_t>(D, 1), &rb.ptr1));
-  APG_TRY(workspace_t(ctx, "u_hd0", std::max<uint64_t>(D, 1), &rb.hd0));
-  APG_TRY(workspace_t(ctx, "u_hd1", std::max<uint64_t>(D, 1), &rb.hd1));
-  APG_TRY(workspace_t(ctx, "u_off0", std::max<uint64_t>(D, 1), &rb.off0));
-  APG_TRY(workspace_t(ctx, "u_off1", std::max<uint64_t>(D, 1), &rb.off1));
+  APG_TRY(workspace_t(ctx, "u_state", std::max<uint64_t>(D, 1), &rb.state));
   APG_TRY(workspace_t(ctx, "u_rlist", std::max<uint64_t>(D, 1), &rb.rlist));
-  uint32_t *fin_ptr = nullptr, *fin_hd = nullptr;
-  uint64_t* fin_off = nullptr;
+  APG_TRY(workspace_t(ctx, "u_alist0", std::max<uint64_t>(D, 1), &rb.alist0));
+  APG_TRY(workspace_t(ctx, "u_alist1", std::max<uint64_t>(D, 1), &rb.alist1));
   for (int attempt = 0; attempt < 3; ++attempt) {
     APG_CHECK_HIP(hipMemsetAsync(gs + 8, 0, 8 * 8, ctx->stream));
-    k_rank_init<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb);
-    kbegin(ctx, "u_walk", D * 16);
-    k_walk<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, gs + 8);
+    kbegin(ctx, "u_find_rulers", D * 12);
+    k_find_rulers<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, gs + 8);
     kend(ctx);
-    APG_CHECK_HIP(hipGetLastError());
     unsigned long long hr;
     APG_TRY(d2h_u64(ctx, gs + 8, &hr, 1));
     const uint64_t R = hr;
-    if (R) {
-      k_ruler_init<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb);
-      k_ruler_link<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb);
-    }
-    uint32_t *p0 = rb.ptr0, *p1 = rb.ptr1, *h0 = rb.hd0, *h1 = rb.hd1;
-    uint64_t *o0 = rb.off0, *o1 = rb.off1;
-    const int rounds = ceil_log2_u(R + 1) + 1;
-    kbegin(ctx, "u_ruler_jump", (uint64_t)rounds * R * 32);
-    for (int it = 0; it < rounds && R; ++it) {
-      k_ruler_jump<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb.rlist, p0, o0, h0, p1, o1, h1);
-      std::swap(p0, p1);
-      std::swap(o0, o1);
-      std::swap(h0, h1);
-    }
+    kbegin(ctx, "u_walk", D * 16);
+    k_walk<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, D, rb);
     kend(ctx);
+    k_ruler_state0<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb);
+    k_ruler_state1<<<grid_for(ctx, R), 256, 0, ctx->stream>>>(R, rb, gs + 9);
     APG_CHECK_HIP(hipGetLastError());
-    fin_ptr = p0;
-    fin_hd = h0;
-    fin_off = o0;
+    unsigned long long na;
+    APG_TRY(d2h_u64(ctx, gs + 9, &na, 1));
+    uint32_t *ain = rb.alist0, *aout = rb.alist1;
+    const int max_rounds = ceil_log2_u(R + 1) + 2;
+    for (int it = 0; it < max_rounds && na; ++it) {
+      APG_CHECK_HIP(hipMemsetAsync(gs + 11, 0, 8, ctx->stream));
+      kbegin(ctx, "u_ruler_jump", na * 48);
+      k_ruler_jump<<<grid_for(ctx, na), 256, 0, ctx->stream>>>(na, ain, rb.state, aout, gs + 11);
+      kend(ctx);
+      APG_TRY(d2h_u64(ctx, gs + 11, &na, 1));
+      std::swap(ain, aout);
+    }
+    APG_CHECK_HIP(hipGetLastError());
     // cycles?
     uint32_t* clist = nullptr;
     APG_TRY(workspace_t(ctx, "u_clist", std::max<uint64_t>(D, 1), &clist));
-    k_mark_cyclic<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, fin_ptr, clist, gs + 9);
+    k_mark_cyclic<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, clist, gs + 12);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hc;
-    APG_TRY(d2h_u64(ctx, gs + 9, &hc, 1));
+    APG_TRY(d2h_u64(ctx, gs + 12, &hc, 1));
     if (hc == 0) break;
     if (attempt == 2) {
       set_error("unipaths: cycles remain after cutting (internal error)");
       return APG_E_STATE;
     }
-    // min K-mer of every cycle by pointer jumping, then cut
+    // min K-mer of every cycle by pointer jumping, then cut; ranking reruns
     const uint64_t C = hc;
-    uint32_t *cm0 = rb.ptr1, *cn0 = rb.hd1, *cm1 = rb.seglen, *cn1 = rb.rnext;  // free D-sized scratch
-    k_cyc_init<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, rb.nxt, cm0, cn0);
+    uint32_t *cm0 = rb.alist0, *cn0 = rb.alist1, *cm1 = rb.rnext, *cn1 = rb.seglen;  // free D-sized scratch
+    k_cyc_init<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, rb.dn, cm0, cn0);
     const int cr = ceil_log2_u(C + 1) + 1;
     for (int it = 0; it < cr; ++it) {
       k_cyc_jump<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, nodes, kp, cm0, cn0, cm1, cn1);
       std::swap(cm0, cm1);
       std::swap(cn0, cn1);
     }
-    k_cyc_cut<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, nodes, kp, cm0, rb.nxt, rb.prv, gs + 10);
+    k_cyc_cut<<<grid_for(ctx, C), 256, 0, ctx->stream>>>(C, clist, nodes, kp, cm0, rb.dn, gs + 13);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hcut;
-    APG_TRY(d2h_u64(ctx, gs + 10, &hcut, 1));
+    APG_TRY(d2h_u64(ctx, gs + 13, &hcut, 1));
     st->n_cycles_cut += hcut;
     vlog(ctx, "unipaths: %llu cyclic directed nodes, %llu cuts", hc, hcut);
   }
@@ -1248,7 +1388,9 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   APG_TRY(workspace_t(ctx, "u_rank", std::max<uint64_t>(D, 1), &rank));
   APG_TRY(workspace_t(ctx, "u_chainlen", std::max<uint64_t>(D, 1), &chainlen));
   APG_TRY(workspace_t(ctx, "u_tailof", std::max<uint64_t>(D, 1), &tail_of));
-  k_rank_final<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, fin_hd, fin_off, head, rank, chainlen, tail_of);
+  kbegin(ctx, "u_rank_final", D * 24);
+  k_rank_final<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, head, rank, chainlen, tail_of);
+  kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
 
   // ---- U7 --------------------------------------------------------------------
@@ -1261,12 +1403,12 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   APG_TRY(workspace_t(ctx, "u_ph", PM, &ph));
   APG_TRY(workspace_t(ctx, "u_ph2", PM, &ph2));
   kbegin(ctx, "u_pairs", D * 12);
-  k_pairs<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb.prv, tail_of, nodes, kp, pk[0], pk[1], pk[2], ph, gs + 12,
-                                                     gs + 13);
+  k_pairs<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb.dn, tail_of, nodes, kp, pk[0], pk[1], pk[2], ph, gs + 14,
+                                                     gs + 15);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hp[2];
-  APG_TRY(d2h_u64(ctx, gs + 12, hp, 2));
+  APG_TRY(d2h_u64(ctx, gs + 14, hp, 2));
   const uint64_t P = hp[0], U = hp[1];
   st->n_unipaths = U;
   // LSD radix sort of (k0, k1, k2) with payload h, skipping constant digits
@@ -1365,7 +1507,7 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   uint32_t* nint = nullptr;
   uint64_t *ioff = nullptr, *istart = nullptr, *ilen = nullptr;
   uint64_t NI = 0;
-  const bool want_paths = (prm.flags & APG_UNIPATH_READ_PATHS) != 0;
+  const bool want_paths = dr && (prm.flags & APG_UNIPATH_READ_PATHS) != 0;
   if (want_paths) {
     APG_TRY(workspace_t(ctx, "u_nint", std::max<uint64_t>(dr->n_reads, 1), &nint));
     APG_TRY(workspace_t(ctx, "u_ioff", dr->n_reads + 1, &ioff));
@@ -1414,6 +1556,31 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   if (rc == APG_OK)
     for (uint64_t i = 0; i < U; ++i) st->max_len = std::max<uint64_t>(st->max_len, out->len[i]);
   return rc;
+}
+
+static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
+                         apg_unipath_stats* st) {
+  const KeyP kp = make_keyp(prm.K);
+  std::memset(st, 0, sizeof(*st));
+  std::vector<uint64_t> counts;
+  uint32_t G = 0;
+  APG_TRY(u_extract_count(ctx, dr, kp, &counts, &G));
+  uint64_t n = 0;
+  for (auto c : counts) n += c;
+  st->n_instances = n;
+  KRec* ext = nullptr;
+  APG_TRY(workspace_t(ctx, "u_ext", std::max<uint64_t>(n, 1), &ext));
+  APG_TRY(u_extract_scatter(ctx, dr, kp, G, n, ext));
+  std::vector<std::vector<Seg>> parents(counts.size());
+  uint64_t pos = 0;
+  for (size_t d = 0; d < counts.size(); ++d) {
+    parents[d].push_back(Seg{pos, counts[d]});
+    pos += counts[d];
+  }
+  KRec* nodes = nullptr;
+  uint64_t N = 0;
+  APG_TRY(u_build_nodes(ctx, ext, parents, n, kUDigitBits, &nodes, &N));
+  return u_graph(ctx, nodes, N, dr, prm, out, st);
 }
 
 }  // namespace apg
@@ -1468,6 +1635,119 @@ int apg_unipaths(apg_ctx* ctx, const apg_reads* reads, const apg_unipath_params*
   APG_TRY(apg_reads_upload(ctx, reads, &dr));
   const int rc = apg_unipaths_dev(ctx, dr, p, out, stats);
   apg_reads_free(dr);
+  return rc;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Sharded (multi-GPU) unipath build: instance counting sharded by hash,
+// distinct nodes gathered by the caller, graph compacted on every rank.
+// ---------------------------------------------------------------------------
+namespace apg {
+static int ushard_check(int K, int P) {
+  APG_REQUIRE(K >= 1 && K <= 96, "unipath shard: K must be in [1, 96]");
+  APG_REQUIRE(P >= 1 && P <= (1 << kUDigitBits) && (P & (P - 1)) == 0,
+              "unipath shard: n_shards must be a power of two in [1, 32]");
+  return APG_OK;
+}
+}  // namespace apg
+
+extern "C" {
+
+int apg_ushard_bins(int n_shards) {
+  if (ushard_check(96, n_shards) != APG_OK) return APG_E_ARG;
+  return (1 << kUDigitBits) / n_shards;
+}
+
+int apg_ushard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* counts) {
+  APG_REQUIRE(ctx && reads && counts, "apg_ushard_count: NULL argument");
+  APG_TRY(ushard_check(K, n_shards));
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::vector<uint64_t> c;
+  uint32_t G = 0;
+  APG_TRY(u_extract_count(ctx, reads, make_keyp(K), &c, &G));
+  uint64_t n = 0;
+  for (size_t i = 0; i < c.size(); ++i) {
+    counts[i] = c[i];  // digit = shard * bins + group: shard-major already
+    n += c[i];
+  }
+  auto& us = ctx->ustate;
+  us.valid = true;
+  us.gen = reads->gen;
+  us.K = K;
+  us.G = G;
+  us.n = n;
+  return APG_OK;
+}
+
+int apg_ushard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, void* d_send) {
+  APG_REQUIRE(ctx && reads, "apg_ushard_scatter: NULL argument");
+  APG_TRY(ushard_check(K, n_shards));
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  auto& us = ctx->ustate;
+  if (!us.valid || us.gen != reads->gen || us.K != K) {
+    std::vector<uint64_t> c(1 << kUDigitBits);
+    APG_TRY(apg_ushard_count(ctx, reads, K, n_shards, c.data()));
+  }
+  APG_REQUIRE(us.n == 0 || d_send, "apg_ushard_scatter: d_send is NULL");
+  APG_TRY(u_extract_scatter(ctx, reads, make_keyp(K), us.G, us.n, static_cast<KRec*>(d_send)));
+  return sync(ctx);
+}
+
+int apg_ushard_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+                     uint64_t* n_nodes) {
+  APG_REQUIRE(ctx && recv_counts && n_nodes, "apg_ushard_nodes: NULL argument");
+  APG_TRY(ushard_check(K, n_shards));
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const int P = n_shards, B = (1 << kUDigitBits) / P;
+  std::vector<std::vector<Seg>> parents(B);
+  uint64_t pos = 0;
+  for (int s = 0; s < P; ++s)
+    for (int l = 0; l < B; ++l) {
+      const uint64_t c = recv_counts[(size_t)s * B + l];
+      parents[l].push_back(Seg{pos, c});
+      pos += c;
+    }
+  APG_REQUIRE(pos == 0 || d_recv, "apg_ushard_nodes: d_recv is NULL");
+  KRec* nodes = nullptr;
+  uint64_t N = 0;
+  APG_TRY(u_build_nodes(ctx, static_cast<const KRec*>(d_recv), parents, pos, kUDigitBits, &nodes, &N));
+  APG_TRY(sync(ctx));
+  ctx->ustate.n_nodes = N;
+  ctx->ustate.n_recv = pos;
+  *n_nodes = N;
+  return APG_OK;
+}
+
+int apg_ushard_export(apg_ctx* ctx, void* d_out) {
+  APG_REQUIRE(ctx, "apg_ushard_export: NULL ctx");
+  const uint64_t N = ctx->ustate.n_nodes;
+  if (N == 0) return APG_OK;
+  APG_REQUIRE(d_out, "apg_ushard_export: d_out is NULL");
+  KRec* nodes = nullptr;
+  APG_TRY(workspace_t(ctx, "u_nodes", N, &nodes));
+  APG_CHECK_HIP(hipMemcpyAsync(d_out, nodes, N * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
+  return sync(ctx);
+}
+
+int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes, const apg_dreads* reads,
+                            const apg_unipath_params* pp, apg_unipath_graph* out, apg_unipath_stats* stats) {
+  APG_REQUIRE(ctx, "apg_unipaths_from_nodes: NULL ctx");
+  APG_REQUIRE(n_nodes == 0 || d_nodes, "apg_unipaths_from_nodes: d_nodes is NULL");
+  apg_unipath_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_unipath_defaults(&p);
+  APG_REQUIRE(p.K >= 1 && p.K <= 96, "apg_unipaths_from_nodes: K must be in [1, 96]");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_unipath_stats st;
+  std::memset(&st, 0, sizeof st);
+  st.n_instances = ctx->ustate.n_recv;
+  const int rc = u_graph(ctx, static_cast<const KRec*>(d_nodes), n_nodes, reads, p, out, &st);
+  if (rc != APG_OK && out) apg_unipath_graph_free(out);
+  if (stats) *stats = st;
   return rc;
 }
 

@@ -46,6 +46,26 @@ class HipShardBackend:
         torch.cuda.synchronize(self.device)
         return self.ctx.shard_spectrum(recv.data_ptr(), recv_counts, K, P, hist_len)
 
+    # unipath stages
+    def ushard_count(self, dreads: DeviceReads, K: int, P: int) -> np.ndarray:
+        return self.ctx.ushard_count(dreads, K, P)
+
+    def ushard_scatter(self, dreads: DeviceReads, K: int, P: int, send: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)
+        self.ctx.ushard_scatter(dreads, K, P, send.data_ptr())
+
+    def ushard_nodes(self, recv: torch.Tensor, recv_counts: np.ndarray, K: int, P: int) -> int:
+        torch.cuda.synchronize(self.device)
+        return self.ctx.ushard_nodes(recv.data_ptr(), recv_counts, K, P)
+
+    def ushard_export(self, out: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)
+        self.ctx.ushard_export(out.data_ptr())
+
+    def graph_from_nodes(self, nodes: torch.Tensor, n_nodes: int, dreads, K: int, fetch: bool):
+        torch.cuda.synchronize(self.device)
+        return self.ctx.unipaths_from_nodes(nodes.data_ptr(), n_nodes, dreads, K, read_paths=True, fetch=fetch)
+
 
 def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
                      group: Optional[dist.ProcessGroup] = None) -> Tuple[np.ndarray, dict]:
@@ -86,5 +106,58 @@ def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
     return hist_t.cpu().numpy().astype(np.uint64), out
 
 
-def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGroup] = None) -> dict:
-    raise NotImplementedError("multi-GPU unipath build: see DESIGN.md (next)")
+def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGroup] = None,
+                     fetch: bool = False):
+    """Global unipath graph of every rank's reads ("shard the
+    counting, replicate the compaction"):
+
+      rank r: K-mer instances (32-byte records) -> hash shards
+              all_to_all(records)          instances of this shard's K-mers
+              ushard_nodes                 this shard's distinct nodes
+              all_gather(nodes)            the full node set on every rank
+              unipaths_from_nodes          graph (identical on every rank) +
+                                           KmerPaths of this rank's reads
+
+    Returns (graph dict or None, stats); graph stats are per rank (identical),
+    n_instances is summed over ranks."""
+    P = dist.get_world_size(group)
+    if P & (P - 1) or P > 32:
+        raise ValueError(f"world size {P} must be a power of two <= 32")
+    B = 32 // P
+    dev = backend.alloc(1).device
+    counts = backend.ushard_count(reads, K, P)  # [dest * B + group]
+    n_send = int(counts.sum())
+    send = backend.alloc(4 * n_send)  # 4 x int64 per record
+    backend.ushard_scatter(reads, K, P, send)
+
+    cnt_t = torch.from_numpy(counts.astype(np.int64)).to(dev)
+    recv_cnt_t = torch.empty_like(cnt_t)
+    dist.all_to_all_single(recv_cnt_t, cnt_t, group=group)
+    recv_counts = recv_cnt_t.cpu().numpy().astype(np.uint64)  # [src * B + group]
+    in_splits = (counts.reshape(P, B).sum(axis=1) * 4).astype(np.int64).tolist()
+    out_splits = (recv_counts.reshape(P, B).sum(axis=1) * 4).astype(np.int64).tolist()
+    n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
+    recv = backend.alloc(n_out)
+    dist.all_to_all_single(recv[:n_out], send[:n_in], out_splits, in_splits, group=group)
+    del send
+
+    n_local = backend.ushard_nodes(recv, recv_counts, K, P)
+    del recv
+    sizes_t = torch.tensor([n_local], dtype=torch.int64, device=dev)
+    all_sizes = [torch.empty_like(sizes_t) for _ in range(P)]
+    dist.all_gather(all_sizes, sizes_t, group=group)
+    sizes = [int(x.item()) for x in all_sizes]
+    maxn = max(max(sizes), 1)
+    local = backend.alloc(4 * maxn)
+    backend.ushard_export(local)
+    gathered = backend.alloc(4 * maxn * P)
+    dist.all_gather_into_tensor(gathered[: 4 * maxn * P], local[: 4 * maxn], group=group)
+    nodes = torch.cat([gathered[4 * maxn * r : 4 * maxn * r + 4 * sizes[r]] for r in range(P)])
+    del gathered, local
+    graph, st = backend.graph_from_nodes(nodes, sum(sizes), reads, K, fetch)
+    inst = torch.tensor([n_send], dtype=torch.int64, device=dev)
+    dist.all_reduce(inst, group=group)
+    st = dict(st)
+    st["n_instances"] = int(inst.item())
+    st["n_shards"] = P
+    return (graph, st) if fetch else st

@@ -214,6 +214,47 @@ class Context:
         finally:
             L.apg_unipath_graph_free(C.byref(g))
 
+    # -- sharded unipath stages (multi-GPU) -------------------------------------
+    def ushard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
+        counts = np.zeros(32, dtype=np.uint64)
+        check(lib().apg_ushard_count(self._h, dreads.handle, K, n_shards, counts.ctypes.data_as(_u64p)),
+              "apg_ushard_count")
+        return counts
+
+    def ushard_scatter(self, dreads: DeviceReads, K: int, n_shards: int, d_send_ptr: int) -> None:
+        check(lib().apg_ushard_scatter(self._h, dreads.handle, K, n_shards, C.c_void_p(d_send_ptr)),
+              "apg_ushard_scatter")
+
+    def ushard_nodes(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int) -> int:
+        rc = np.ascontiguousarray(recv_counts, dtype=np.uint64)
+        n = C.c_uint64()
+        check(lib().apg_ushard_nodes(self._h, C.c_void_p(d_recv_ptr), rc.ctypes.data_as(_u64p), K, n_shards,
+                                     C.byref(n)), "apg_ushard_nodes")
+        return int(n.value)
+
+    def ushard_export(self, d_out_ptr: int) -> None:
+        check(lib().apg_ushard_export(self._h, C.c_void_p(d_out_ptr)), "apg_ushard_export")
+
+    def unipaths_from_nodes(self, d_nodes_ptr: int, n_nodes: int, dreads, K: int = 96, read_paths: bool = True,
+                            fetch: bool = False):
+        from ._lib import APG_UNIPATH_READ_PATHS, apg_unipath_graph, apg_unipath_params, apg_unipath_stats
+
+        p = apg_unipath_params()
+        lib().apg_unipath_defaults(C.byref(p))
+        p.K = K
+        p.flags = APG_UNIPATH_READ_PATHS if read_paths else 0
+        g = apg_unipath_graph()
+        st = apg_unipath_stats()
+        check(lib().apg_unipaths_from_nodes(self._h, C.c_void_p(d_nodes_ptr), n_nodes,
+                                            dreads.handle if dreads is not None else None, C.byref(p),
+                                            C.byref(g) if fetch else None, C.byref(st)), "apg_unipaths_from_nodes")
+        if not fetch:
+            return None, st.as_dict()
+        try:
+            return graph_arrays(g), st.as_dict()
+        finally:
+            lib().apg_unipath_graph_free(C.byref(g))
+
     # -- sharded (multi-GPU) stages ------------------------------------------
     def shard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
         B = shard_bins(K, n_shards)

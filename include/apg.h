@@ -257,6 +257,31 @@ int apg_unipaths_dev(apg_ctx* ctx, const apg_dreads* reads, const apg_unipath_pa
                      apg_unipath_graph* out, apg_unipath_stats* stats);
 void apg_unipath_graph_free(apg_unipath_graph* g);
 
+/* Sharded unipath build (multi-GPU, one process per GPU).  The
+ * K-mer instances (32-byte records: 3 x u64 canonical key + hash/extension
+ * word) are hash-sharded like the spectrum: shard = top log2(P) bits of the
+ * 5-bit instance digit, B = apg_ushard_bins(P) groups per shard.
+ *   1. apg_ushard_count / apg_ushard_scatter: local reads -> d_send
+ *   2. (caller) all_to_all of counts, then of records -> d_recv (src-major)
+ *   3. apg_ushard_nodes: this shard's distinct nodes (key + OR of ext bits)
+ *   4. apg_ushard_export -> (caller) all_gather of every shard's nodes
+ *   5. apg_unipaths_from_nodes: the graph of the full node set (identical on
+ *      every rank) + KmerPaths of this rank's reads.
+ * Node sets of different shards are disjoint, so their concatenation in any
+ * order gives the same graph as apg_unipaths on all reads. */
+int apg_ushard_bins(int n_shards);
+int apg_ushard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
+                     uint64_t* counts /* host, 32 entries: shard-major */);
+int apg_ushard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
+                       void* d_send /* device, sum(counts) x 32 bytes */);
+int apg_ushard_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts /* 32 */,
+                     int K, int n_shards, uint64_t* n_nodes);
+int apg_ushard_export(apg_ctx* ctx, void* d_out /* device, n_nodes x 32 bytes */);
+int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes,
+                            const apg_dreads* reads /* KmerPaths for these, or NULL */,
+                            const apg_unipath_params* p, apg_unipath_graph* out,
+                            apg_unipath_stats* stats);
+
 /* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */
 /* insert N(mean, sd), FR orientation, substitution error rate rising        */

@@ -182,3 +182,65 @@ def unipaths(reads, K: int = 96) -> dict:
         return out
     finally:
         L.oru_free(C.byref(res))
+
+
+def instances(reads, K: int = 96):
+    """All K-mer instances: (keys [n,3] u64, ext [n] u8, hash [n] u64)."""
+    L = lib()
+    if not hasattr(L, "_oi"):
+        L.oru_instances.restype = C.c_uint64
+        L.oru_instances.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, _u8p, _u64p]
+        L.oru_graph_from_nodes.restype = C.c_int
+        L.oru_graph_from_nodes.argtypes = [C.c_uint64, _u64p, _u8p, C.c_uint64, _u64p, _u64p, _u8p, C.c_int,
+                                           C.POINTER(_OruResult)]
+        L._oi = True
+    n, bo, yo, pk = _rp(reads)
+    m = int(L.oru_instances(n, bo, yo, pk, K, None, None, None))
+    keys = np.zeros((max(m, 1), 3), dtype=np.uint64)
+    ext = np.zeros(max(m, 1), dtype=np.uint8)
+    h = np.zeros(max(m, 1), dtype=np.uint64)
+    L.oru_instances(n, bo, yo, pk, K, keys.ctypes.data_as(_u64p), ext.ctypes.data_as(_u8p), h.ctypes.data_as(_u64p))
+    return keys[:m], ext[:m], h[:m]
+
+
+def group_nodes(keys, ext):
+    """Distinct keys with the OR of their instances' extension bits."""
+    if len(keys) == 0:
+        return np.zeros((0, 3), np.uint64), np.zeros(0, np.uint8)
+    order = np.lexsort((keys[:, 2], keys[:, 1], keys[:, 0]))
+    k = keys[order]
+    e = ext[order]
+    new = np.ones(len(k), dtype=bool)
+    new[1:] = np.any(k[1:] != k[:-1], axis=1)
+    gid = np.cumsum(new) - 1
+    out_e = np.zeros(int(gid[-1]) + 1, dtype=np.uint8)
+    np.bitwise_or.at(out_e, gid, e)
+    return k[new], out_e
+
+
+def graph_from_nodes(keys, ext, reads, K: int = 96) -> dict:
+    instances(reads, K)  # binds the entry points
+    L = lib()
+    res = _OruResult()
+    kk = np.ascontiguousarray(keys, dtype=np.uint64)
+    ee = np.ascontiguousarray(ext, dtype=np.uint8)
+    n, bo, yo, pk = _rp(reads)
+    rc = L.oru_graph_from_nodes(len(ee), kk.ctypes.data_as(_u64p), ee.ctypes.data_as(_u8p), n, bo, yo, pk, K,
+                                C.byref(res))
+    if rc:
+        raise RuntimeError(f"oracle graph_from_nodes failed ({rc})")
+    try:
+        U = int(res.n_unipaths)
+        out = {
+            "n_nodes": int(res.n_nodes), "n_unipaths": U,
+            "len": _arr(res.len, U, np.uint64), "id_base": _arr(res.id_base, U, np.uint64),
+            "rc": _arr(res.rc, U, np.uint64), "ub_off": _arr(res.ub_off, U + 1, np.uint64),
+            "n_vertices": int(res.n_vertices), "from": _arr(res.frm, U, np.uint64), "to": _arr(res.to, U, np.uint64),
+            "path_off": _arr(res.path_off, int(res.n_reads) + 1, np.uint64),
+            "path_start": _arr(res.path_start, int(res.n_intervals), np.uint64),
+            "path_len": _arr(res.path_len, int(res.n_intervals), np.uint64),
+        }
+        out["unibases"] = _arr(res.unibases, int(out["ub_off"][-1]) if U else 0, np.uint8)
+        return out
+    finally:
+        L.oru_free(C.byref(res))

@@ -164,6 +164,9 @@ static T* dup(const std::vector<T>& v) {
   return p;
 }
 
+static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
+                       int K, oru_result* out);
+
 extern "C" {
 
 int oru_build(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
@@ -215,6 +218,77 @@ int oru_build(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_o
     i = j;
   }
   std::vector<Inst>().swap(inst);
+  return build_graph(n_reads, base_off, byte_off, packed, K, out);
+}
+
+// Graph of an explicit node set (keys: 3 limbs each, ext: left | right << 4)
+// plus KmerPaths of the given reads — the multi-GPU path's "gathered nodes".
+int oru_graph_from_nodes(uint64_t n_nodes, const uint64_t* keys, const uint8_t* ext, uint64_t n_reads,
+                         const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
+                         oru_result* out) {
+  if (K < 1 || K > 96 || !out) return -1;
+  g_K = K;
+  std::memset(out, 0, sizeof(*out));
+  g_nodes.clear();
+  for (uint64_t i = 0; i < n_nodes; ++i)
+    g_nodes.push_back(Node{Key{keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]}, (uint8_t)(ext[i] & 15),
+                           (uint8_t)(ext[i] >> 4), 0});
+  std::sort(g_nodes.begin(), g_nodes.end(), [](const Node& x, const Node& y) { return x.key < y.key; });
+  out->n_nodes = n_nodes;
+  return build_graph(n_reads, base_off, byte_off, packed, K, out);
+}
+
+static uint64_t fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// Every K-mer instance of the reads: canonical key limbs, instance extension
+// bits (left | right << 4) and the 56-bit partition hash of the key (same
+// function as the GPU's key_hash: shard = top bits).  Returns the count;
+// outputs may be NULL to size.
+uint64_t oru_instances(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
+                       int K, uint64_t* keys, uint8_t* ext, uint64_t* hash) {
+  g_K = K;
+  uint64_t n = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    const uint64_t L = base_off[r + 1] - base_off[r];
+    const uint8_t* rd = packed + byte_off[r];
+    if (L < (uint64_t)K) continue;
+    Key f{0, 0, 0};
+    for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) f = push_right(f, read_base(rd, i));
+    for (uint64_t i = 0; i + K <= L; ++i, ++n) {
+      f = push_right(f, read_base(rd, i + K - 1));
+      if (!keys) continue;
+      const Key rc = revcomp(f);
+      const int a = i > 0 ? read_base(rd, i - 1) : -1;
+      const int b = i + K < L ? read_base(rd, i + K) : -1;
+      const uint8_t la = a >= 0 ? 1 << a : 0, rb = b >= 0 ? 1 << b : 0;
+      const uint8_t ca = a >= 0 ? 1 << (3 - a) : 0, cb = b >= 0 ? 1 << (3 - b) : 0;
+      Key k;
+      uint8_t L4, R4;
+      if (f == rc) {
+        k = f, L4 = la | cb, R4 = rb | ca;
+      } else if (f < rc) {
+        k = f, L4 = la, R4 = rb;
+      } else {
+        k = rc, L4 = cb, R4 = ca;
+      }
+      keys[3 * n] = k.a;
+      keys[3 * n + 1] = k.b;
+      keys[3 * n + 2] = k.c;
+      ext[n] = (uint8_t)(L4 | (R4 << 4));
+      hash[n] = fmix64(k.a ^ fmix64(k.b ^ fmix64(k.c ^ 0x5851f42d4c957f2dull))) & ~0xffull;
+    }
+  }
+  return n;
+}
+
+}  // extern "C"
+
+static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
+                       int K, oru_result* out) {
   const int64_t N = (int64_t)g_nodes.size(), D = 2 * N;
   out->n_nodes = (uint64_t)N;
   // ---- 2. unique links --------------------------------------------------
@@ -411,6 +485,8 @@ int oru_build(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_o
   g_nodes.shrink_to_fit();
   return 0;
 }
+
+extern "C" {
 
 void oru_free(oru_result* r) {
   if (!r) return;

@@ -100,3 +100,90 @@ def test_sharded_spectrum_gloo(world):
         assert np.array_equal(hist, expect)
         assert st["n_kmers"] == reads.n_reads * (100 - K + 1)
         assert st["n_distinct"] == int(expect.sum())
+
+
+class OracleUnipathBackend(OracleShardBackend):
+    """CPU stand-in for libapg's ushard_* stages (same record layout:
+    4 x int64 = canonical key limbs + (56-bit hash | ext bits))."""
+
+    def _inst(self, reads, K):
+        key = ("u", id(reads), K)
+        if key not in self.cache:
+            self.cache[key] = oracle.instances(reads, K)
+        return self.cache[key]
+
+    def ushard_count(self, reads, K, P):
+        _, _, h = self._inst(reads, K)
+        return np.bincount((h >> np.uint64(59)).astype(np.int64), minlength=32).astype(np.uint64)
+
+    def ushard_scatter(self, reads, K, P, send):
+        k, e, h = self._inst(reads, K)
+        order = np.argsort((h >> np.uint64(59)).astype(np.int64), kind="stable")
+        rec = np.zeros((len(h), 4), dtype=np.uint64)
+        rec[:, :3] = k[order]
+        rec[:, 3] = h[order] | e[order].astype(np.uint64)
+        send[: 4 * len(h)] = torch.from_numpy(rec.reshape(-1).view(np.int64))
+
+    def ushard_nodes(self, recv, recv_counts, K, P):
+        n = int(recv_counts.sum())
+        rec = recv[: 4 * n].numpy().view(np.uint64).reshape(n, 4)
+        pbits = int(np.log2(P))
+        if n and pbits:
+            assert np.all((rec[:, 3] >> np.uint64(64 - pbits)) == dist.get_rank())
+        self.nodes = oracle.group_nodes(rec[:, :3].copy(), (rec[:, 3] & np.uint64(0xFF)).astype(np.uint8))
+        return len(self.nodes[1])
+
+    def ushard_export(self, out):
+        k, e = self.nodes
+        rec = np.zeros((len(e), 4), dtype=np.uint64)
+        rec[:, :3] = k
+        rec[:, 3] = e.astype(np.uint64)
+        out[: 4 * len(e)] = torch.from_numpy(rec.reshape(-1).view(np.int64))
+
+    def graph_from_nodes(self, nodes, n_nodes, reads, K, fetch):
+        rec = nodes[: 4 * n_nodes].numpy().view(np.uint64).reshape(n_nodes, 4)
+        g = oracle.graph_from_nodes(rec[:, :3].copy(), (rec[:, 3] & np.uint64(0xFF)).astype(np.uint8), reads, K)
+        return g, {"n_unipaths": g["n_unipaths"], "n_nodes": g["n_nodes"]}
+
+
+def _uworker(rank, world, port, K, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from allpathslg_amd.distributed import sharded_unipaths
+        from tests.unipath_cases import noisy_reads
+
+        reads = noisy_reads(G=15_000, n=2000)
+        parts = np.array_split(np.arange(reads.n_reads), world)
+        mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
+        g, st = sharded_unipaths(OracleUnipathBackend(), mine, K, fetch=True)
+        q.put((rank, int(parts[rank][0]), int(parts[rank][-1]) + 1, g, st))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_unipaths_gloo(world):
+    from tests.unipath_cases import noisy_reads
+
+    K = 63
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uworker, args=(r, world, port, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    reads = noisy_reads(G=15_000, n=2000)
+    exp = oracle.unipaths(reads, K)
+    for rank, a, b, g, st in res:
+        for k in ("len", "id_base", "rc", "ub_off", "unibases", "from", "to"):
+            assert np.array_equal(g[k], exp[k]), k
+        assert st["n_instances"] == reads.n_reads * (100 - K + 1)
+        lo, hi = int(exp["path_off"][a]), int(exp["path_off"][b])
+        assert np.array_equal(g["path_start"], exp["path_start"][lo:hi])
+        assert np.array_equal(g["path_len"], exp["path_len"][lo:hi])

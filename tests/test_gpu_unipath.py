@@ -77,3 +77,52 @@ def test_empty_and_short(gpu_ctx):
 
     for reads in (ReadSet.from_sequences([]), ReadSet.from_sequences([[0, 1, 2], [], [3] * 50])):
         run(gpu_ctx, reads, 96)
+
+
+@pytest.mark.parametrize("P", [1, 2, 4])
+def test_shard_path_loopback(gpu_ctx, P):
+    """Multi-GPU unipath data path on one GPU: P read slices -> ushard_count /
+    ushard_scatter -> loopback all_to_all -> ushard_nodes per shard -> gather
+    -> unipaths_from_nodes == single-call build (graph and read paths)."""
+    import torch
+
+    K = 96
+    reads = noisy_reads(G=40_000, n=8000)
+    B = 32 // P
+    parts = np.array_split(np.arange(reads.n_reads), P)
+    subs = [reads.subset(int(ix[0]), int(ix[-1]) + 1) for ix in parts]
+    dsubs = [gpu_ctx.upload(s) for s in subs]
+    sends, counts = [], []
+    for d in dsubs:
+        c = gpu_ctx.ushard_count(d, K, P)
+        buf = torch.empty(max(4 * int(c.sum()), 1), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.ushard_scatter(d, K, P, buf.data_ptr())
+        sends.append(buf)
+        counts.append(c.reshape(P, B))
+    node_chunks = []
+    for s in range(P):
+        pieces, rc = [], []
+        for p in range(P):
+            starts = np.concatenate([[0], np.cumsum(counts[p].reshape(-1))]).astype(np.int64)
+            a, b = starts[s * B], starts[(s + 1) * B]
+            pieces.append(sends[p][4 * a : 4 * b])
+            rc.append(counts[p][s])
+        recv = torch.cat(pieces) if sum(x.numel() for x in pieces) else torch.empty(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        n = gpu_ctx.ushard_nodes(recv.data_ptr(), np.concatenate(rc), K, P)
+        out = torch.empty(max(4 * n, 1), dtype=torch.int64, device="cuda")
+        gpu_ctx.ushard_export(out.data_ptr())
+        node_chunks.append(out[: 4 * n])
+    nodes = torch.cat(node_chunks)
+    torch.cuda.synchronize()
+    exp = oracle.unipaths(reads, K)
+    lo = 0
+    for i, d in enumerate(dsubs):
+        g, st = gpu_ctx.unipaths_from_nodes(nodes.data_ptr(), nodes.numel() // 4, d, K, fetch=True)
+        for k in ("n_nodes", "n_unipaths", "len", "id_base", "rc", "ub_off", "unibases", "n_vertices", "from", "to"):
+            a = g[k]
+            assert (np.array_equal(a, exp[k]) if isinstance(a, np.ndarray) else a == exp[k]), k
+        a, b = int(parts[i][0]), int(parts[i][-1]) + 1
+        assert np.array_equal(g["path_start"], exp["path_start"][int(exp["path_off"][a]) : int(exp["path_off"][b])])
+        d.free()
