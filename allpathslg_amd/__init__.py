@@ -6,7 +6,7 @@ benchmark and the multi-GPU driver.
 """
 from ._lib import ApgError, lib  # noqa: F401
 from .engine import DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, shard_bins  # noqa: F401
-from .reads import ReadSet, synth_genome, synth_reads  # noqa: F401
+from .reads import ReadSet, synth_fragments, synth_genome, synth_reads  # noqa: F401
 
 __all__ = [
     "ApgError",
@@ -20,4 +20,5 @@ __all__ = [
     "shard_bins",
     "synth_genome",
     "synth_reads",
+    "synth_fragments",
 ]

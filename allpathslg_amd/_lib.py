@@ -166,6 +166,7 @@ SIGNATURES = {
     "apg_reads_upload": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(_P)]),
     "apg_reads_free": (None, [_P]),
     "apg_dreads_count": (C.c_uint64, [_P]),
+    "apg_reads_copy_dev": (C.c_int, [_P, _P, _P]),
     "apg_byte_offsets": (C.c_int, [_u64p, C.c_uint64, _u64p]),
     "apg_kmer_hash": (C.c_uint64, [C.c_int, C.c_uint64]),
     "apg_kmer_unhash": (C.c_uint64, [C.c_int, C.c_uint64]),
@@ -187,6 +188,11 @@ SIGNATURES = {
     "apg_precorrect": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_pc_params), _u8p, _u8p, C.POINTER(apg_pc_stats)]),
     "apg_precorrect_dev": (C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
     "apg_reads_download": (C.c_int, [_P, _P, _u8p, _u8p]),
+    "apg_shard_solid": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, C.c_uint32, _u64p]),
+    "apg_solid_export": (C.c_int, [_P, C.c_void_p]),
+    "apg_precorrect_solid": (
+        C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.c_void_p, C.c_uint64, C.POINTER(apg_pc_stats)]
+    ),
     "apg_unipath_defaults": (None, [C.POINTER(apg_unipath_params)]),
     "apg_unipaths": (
         C.c_int,
@@ -211,6 +217,7 @@ SIGNATURES = {
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),
+    "apg_synth_fragments": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u8p, _u8p]),
     "apg_fastb_write": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
     "apg_qualb_write": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
     "apg_fastb_read": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),

@@ -33,6 +33,11 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
       return APG_E_HIP;
     }
     b.bytes = want;
+    if (ctx->verbose) {
+      size_t tot = 0;
+      for (auto& kv : ctx->ws) tot += kv.second.bytes;
+      vlog(ctx, "workspace %s -> %.3f GB (all workspaces %.3f GB)", name, want / 1e9, tot / 1e9);
+    }
   }
   *out = b.p;
   return APG_OK;
@@ -273,6 +278,21 @@ void apg_reads_free(apg_dreads* d) {
 }
 
 uint64_t apg_dreads_count(const apg_dreads* d) { return d ? d->n_reads : 0; }
+
+int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
+  APG_REQUIRE(ctx && dst && src, "apg_reads_copy_dev: NULL argument");
+  APG_REQUIRE(dst->n_reads == src->n_reads && dst->n_bases == src->n_bases && dst->n_bytes == src->n_bytes &&
+                  dst->h_base_off == src->h_base_off,
+              "apg_reads_copy_dev: read sets differ in shape");
+  APG_REQUIRE(!src->d_quals || dst->d_quals, "apg_reads_copy_dev: destination has no qualities");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  if (src->n_bytes)
+    APG_CHECK_HIP(hipMemcpyAsync(dst->d_packed, src->d_packed, src->n_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  if (src->d_quals && src->n_bases)
+    APG_CHECK_HIP(hipMemcpyAsync(dst->d_quals, src->d_quals, src->n_bases, hipMemcpyDeviceToDevice, ctx->stream));
+  dst->gen = src->gen;  // same bases: plans made for src are valid for dst's contents
+  return APG_OK;
+}
 
 void apg_free(void* p) { std::free(p); }
 

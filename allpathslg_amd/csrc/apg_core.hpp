@@ -113,9 +113,19 @@ struct apg_ctx {
     uint64_t n_nodes = 0;  // nodes of the last apg_ushard_nodes
     uint64_t n_recv = 0;
   } ustate;
+
+  // Solid K-mer list of the last apg_shard_solid ("pc_solid" workspace).
+  uint64_t n_solid = 0;
+  bool solid_valid = false;
 };
 
 namespace apg {
+
+// Grid of a grid-stride kernel over n items, `per` items per block, capped at
+// 16 blocks per CU.
+inline uint32_t grid_for(apg_ctx* ctx, uint64_t n, int per = 256) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, (uint64_t)ctx->n_cu * 16));
+}
 
 // Device workspace `name` of at least `bytes`; contents are undefined.
 int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out);

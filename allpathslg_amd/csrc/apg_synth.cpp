@@ -83,6 +83,24 @@ void parallel_for(uint64_t n, unsigned threads, F f) {
   for (auto& th : ts) th.join();
 }
 
+struct Fragment {
+  uint64_t start, len;
+  bool flip;  // read A comes from the reverse strand
+};
+
+// The first draws of pair k's stream: fragment length ~ N(mean, sd) clamped to
+// [L, min(G, 10*mean + L)], start, strand.  Shared by the read and the
+// fragment generators so a fragment is exactly its pair's insert.
+inline Fragment draw_fragment(Xoshiro256ss& rng, const apg_synth_params* p) {
+  const uint64_t L = p->read_len, G = p->genome_len;
+  double f = p->insert_mean + p->insert_sd * rng.gaussian();
+  uint64_t flen = (uint64_t)std::llround(std::max<double>(f, (double)L));
+  flen = std::min<uint64_t>(flen, std::min<uint64_t>(G, 10ull * p->insert_mean + L));
+  const uint64_t start = rng.below(G - flen + 1);
+  const bool flip = rng.next() & 1;
+  return {start, flen, flip};
+}
+
 }  // namespace
 
 extern "C" {
@@ -129,12 +147,9 @@ int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome, uint64_t* 
     std::vector<uint8_t> r1(L), r2(L), q1(L), q2(L);
     for (uint64_t k = a; k < b; ++k) {
       Xoshiro256ss rng(stream_seed(p->seed, 2, p->first_pair + k));
-      // Fragment length ~ N(mean, sd), clamped to [L, min(G, 10*mean + L)].
-      double f = p->insert_mean + p->insert_sd * rng.gaussian();
-      uint64_t flen = (uint64_t)std::llround(std::max<double>(f, (double)L));
-      flen = std::min<uint64_t>(flen, std::min<uint64_t>(G, 10ull * p->insert_mean + L));
-      const uint64_t start = rng.below(G - flen + 1);
-      const bool flip = rng.next() & 1;  // fragment from the reverse strand
+      const Fragment fr = draw_fragment(rng, p);
+      const uint64_t start = fr.start, flen = fr.len;
+      const bool flip = fr.flip;
       // FR pair: read A = forward of [start, start+L), read B = rc of [start+flen-L, start+flen).
       for (uint64_t i = 0; i < L; ++i) {
         r1[i] = genome[start + i];
@@ -158,6 +173,43 @@ int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome, uint64_t* 
         std::memset(dst, 0, rb);
         for (uint64_t i = 0; i < L; ++i) dst[i >> 2] |= (uint8_t)(r[i] << (2 * (i & 3)));
         if (quals) std::memcpy(quals + ridx * L, q.data(), L);
+      }
+    }
+  });
+  return APG_OK;
+}
+
+int apg_synth_fragments(const apg_synth_params* p, uint64_t* base_off, uint64_t* byte_off, const uint8_t* genome,
+                        uint8_t* packed) {
+  if (!p || !base_off || !byte_off) return APG_E_ARG;
+  const uint64_t L = p->read_len, G = p->genome_len, n = p->n_pairs;
+  if (L == 0 || G < L) return APG_E_ARG;
+  if (!packed) {  // sizing pass: offsets only
+    std::vector<uint64_t> len(n);
+    parallel_for(n, n_threads(p->threads), [&](uint64_t a, uint64_t b) {
+      for (uint64_t k = a; k < b; ++k) {
+        Xoshiro256ss rng(stream_seed(p->seed, 2, p->first_pair + k));
+        len[k] = draw_fragment(rng, p).len;
+      }
+    });
+    base_off[0] = byte_off[0] = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+      base_off[k + 1] = base_off[k] + len[k];
+      byte_off[k + 1] = byte_off[k] + (len[k] + 3) / 4;
+    }
+    return APG_OK;
+  }
+  if (!genome) return APG_E_ARG;
+  parallel_for(n, n_threads(p->threads), [&](uint64_t a, uint64_t b) {
+    for (uint64_t k = a; k < b; ++k) {
+      Xoshiro256ss rng(stream_seed(p->seed, 2, p->first_pair + k));
+      const Fragment fr = draw_fragment(rng, p);
+      if (fr.len != base_off[k + 1] - base_off[k]) continue;  // offsets not from the sizing pass
+      uint8_t* dst = packed + byte_off[k];
+      std::memset(dst, 0, (fr.len + 3) / 4);
+      for (uint64_t i = 0; i < fr.len; ++i) {
+        const uint8_t b = fr.flip ? (uint8_t)(3 - genome[fr.start + fr.len - 1 - i]) : genome[fr.start + i];
+        dst[i >> 2] |= (uint8_t)(b << (2 * (i & 3)));
       }
     }
   });

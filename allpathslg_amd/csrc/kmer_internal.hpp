@@ -25,4 +25,9 @@ struct CountResult {
 int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
                   CountResult* res);
 
+// Table-mode count of records received by shard `P`-way exchange
+// (apg_shard_scatter layout, recv_counts[src * B1 + l1]).
+int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P,
+                     CountResult* res);
+
 }  // namespace apg

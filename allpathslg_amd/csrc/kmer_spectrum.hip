@@ -498,6 +498,15 @@ static int l1_bits(int K, int P) {
 // Stage A.  Digit = top (pbits + l1) bits.  extract_count returns per-digit
 // record counts (host, 2^D) and leaves the scanned count matrix in the "x_omat"
 // workspace; extract_scatter reuses it when called for the same (reads, K, P).
+static int check_shards(int K, int n_shards) {
+  APG_REQUIRE(K >= 1 && K <= 32, "K must be in [1, 32]");
+  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
+              "n_shards must be a power of two in [1, 64]");
+  APG_REQUIRE(2 * K >= ceil_log2((uint64_t)n_shards), "K too small for n_shards");
+  return APG_OK;
+}
+
+
 static int extract_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* digit_counts) {
   const int w = 2 * K, pbits = ceil_log2((uint64_t)P), D = pbits + l1_bits(K, P);
   const uint32_t ndig = 1u << D;
@@ -693,6 +702,18 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   return APG_OK;
 }
 
+int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P,
+                     CountResult* res) {
+  APG_TRY(check_shards(K, P));
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const uint32_t B1 = 1u << l1_bits(K, P);
+  std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)P * B1);
+  uint64_t n = 0;
+  for (auto c : rc) n += c;
+  APG_REQUIRE(n == 0 || d_recv, "shard table: d_recv is NULL");
+  return stage_count(ctx, d_recv, nullptr, rc, K, P, true, nullptr, 0, res);
+}
+
 int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
                          CountResult* res) {
   APG_REQUIRE(ctx && dr, "spectrum: NULL ctx/reads");
@@ -785,14 +806,6 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
   *counts = hc;
   *n_distinct = nd;
   if (stats) *stats = r.st;
-  return APG_OK;
-}
-
-static int check_shards(int K, int n_shards) {
-  APG_REQUIRE(K >= 1 && K <= 32, "K must be in [1, 32]");
-  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
-              "n_shards must be a power of two in [1, 64]");
-  APG_REQUIRE(2 * K >= ceil_log2((uint64_t)n_shards), "K too small for n_shards");
   return APG_OK;
 }
 

@@ -18,37 +18,63 @@
 #include "apg_core.hpp"
 #include "kmer_common.hpp"
 #include "kmer_internal.hpp"
+#include "partition.hpp"
 
 namespace apg {
 
 constexpr uint64_t kSolidEmpty = ~0ull;
 
-__global__ void k_count_solid(const uint32_t* __restrict__ tab_cnt, const uint64_t* __restrict__ boff,
-                              const uint32_t* __restrict__ bucket_nd, uint64_t nbuckets, uint32_t min_solid,
-                              unsigned long long* __restrict__ n_solid) {
-  unsigned long long local = 0;
+// Solid hashes per table bucket (one block per bucket).
+__global__ void __launch_bounds__(256) k_bucket_solid(const uint32_t* __restrict__ tab_cnt,
+                                                      const uint64_t* __restrict__ boff,
+                                                      const uint32_t* __restrict__ bucket_nd, uint64_t nbuckets,
+                                                      uint32_t min_solid, uint32_t* __restrict__ nsolid) {
+  __shared__ uint32_t part[4];
   for (uint64_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
     const uint64_t off = boff[b];
     const uint32_t nd = bucket_nd[b];
+    uint32_t local = 0;
     for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) local += tab_cnt[off + i] >= min_solid;
+    for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
+    if (lane_id() == 0) part[wave_id()] = local;
+    __syncthreads();
+    if (threadIdx.x == 0) nsolid[b] = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
   }
-  for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
-  if ((threadIdx.x & 63) == 0 && local) atomicAdd(n_solid, local);
 }
 
-__global__ void k_solid_insert(const uint64_t* __restrict__ tab_hash, const uint32_t* __restrict__ tab_cnt,
-                               const uint64_t* __restrict__ boff, const uint32_t* __restrict__ bucket_nd,
-                               uint64_t nbuckets, uint32_t min_solid, unsigned long long* __restrict__ table,
-                               uint64_t tmask) {
+// Solid hashes in (bucket, table slot) order: list[soff[b] + j].
+__global__ void __launch_bounds__(256) k_solid_collect(const uint64_t* __restrict__ tab_hash,
+                                                       const uint32_t* __restrict__ tab_cnt,
+                                                       const uint64_t* __restrict__ boff,
+                                                       const uint32_t* __restrict__ bucket_nd, uint64_t nbuckets,
+                                                       uint32_t min_solid, const uint64_t* __restrict__ soff,
+                                                       uint64_t* __restrict__ list) {
+  __shared__ uint32_t sm[32];
   for (uint64_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
     const uint64_t off = boff[b];
     const uint32_t nd = bucket_nd[b];
-    for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) {
-      if (tab_cnt[off + i] < min_solid) continue;
-      const unsigned long long h = tab_hash[off + i];
-      uint64_t s = h & tmask;
-      while (atomicCAS(&table[s], (unsigned long long)kSolidEmpty, h) != kSolidEmpty) s = (s + 1) & tmask;
+    uint64_t out = soff[b];
+    for (uint32_t i0 = 0; i0 < nd; i0 += blockDim.x) {
+      const uint32_t i = i0 + threadIdx.x;
+      const bool keep = i < nd && tab_cnt[off + i] >= min_solid;
+      uint32_t tot;
+      const uint32_t ex = block_exclusive_scan<uint32_t>(keep ? 1u : 0u, sm, &tot);
+      if (keep) list[out + ex] = tab_hash[off + i];
+      out += tot;
+      __syncthreads();
     }
+  }
+}
+
+// Open-addressing table of a solid hash list (linear probing, load <= 0.5;
+// hashes are uniformly mixed, so the home slot is the hash's low bits).
+__global__ void k_solid_insert(const uint64_t* __restrict__ list, uint64_t n, unsigned long long* __restrict__ table,
+                               uint64_t tmask) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long h = list[i];
+    uint64_t s = h & tmask;
+    while (atomicCAS(&table[s], (unsigned long long)kSolidEmpty, h) != kSolidEmpty) s = (s + 1) & tmask;
   }
 }
 
@@ -87,13 +113,13 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
                                                     const uint64_t* __restrict__ byte_off, uint8_t* __restrict__ packed,
                                                     uint8_t* __restrict__ quals, uint64_t n_reads, int K, HashP hp,
                                                     uint32_t maxq, const unsigned long long* __restrict__ table,
-                                                    uint64_t tmask, PcCounters* __restrict__ cnt) {
+                                                    uint64_t tmask, uint32_t min_len, PcCounters* __restrict__ cnt) {
   unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads;
        r += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t q0 = base_off[r];
     const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
-    if (L < (uint32_t)K) continue;
+    if (L < (uint32_t)K || L < min_len) continue;
     uint8_t* rd = packed + byte_off[r];
     uint8_t* q = quals + q0;
     for (uint32_t p = 0; p < L; ++p) {
@@ -146,35 +172,200 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
   }
 }
 
-static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st) {
-  CountResult cr;
-  APG_TRY(spectrum_impl(ctx, dr, p.K, true, nullptr, 0, &cr));
+// ---------------------------------------------------------------------------
+// Wave-per-read correction (reads of <= kPcMaxL bases).  Same rule and order
+// as k_precorrect (which still handles longer reads), restructured for
+// memory-level parallelism: the read's bases live in the wave's registers
+// (lane i holds packed bases [16i, 16i+16) as one u32), suspects are found
+// 64 positions at a time by ballot, and for each suspect in left-to-right
+// order the <= K covering K-mers (weak test) and then the <= 3K
+// (alternative, K-mer) pairs are looked up ONE PER LANE in parallel instead
+// of one dependent probe at a time.  A K-mer window is cut from the packed
+// words (LSB-first: window value W = sum b[j+t] 4^t), so
+//   fw = rev2(W) >> (64 - 2K),   rc = W ^ mask(2K).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPcMaxL = 1024;  // 64 lanes x 16 bases
+
+__device__ __forceinline__ uint64_t rev2(uint64_t x) {
+  x = __builtin_bitreverse64(x);
+  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+}
+
+// 2K-bit window starting at base j of the read whose packed u32 words are
+// spread one per lane (word i in lane i's `word`).
+__device__ __forceinline__ uint64_t window_at(uint32_t word, uint32_t j, uint64_t mask) {
+  const uint32_t bit = 2 * j, wi = bit >> 5, sh = bit & 31;
+  const uint32_t w0 = (uint32_t)__shfl((int)word, (int)min(wi, 63u), 64);
+  const uint32_t w1 = (uint32_t)__shfl((int)word, (int)min(wi + 1, 63u), 64);
+  const uint32_t w2 = (uint32_t)__shfl((int)word, (int)min(wi + 2, 63u), 64);
+  const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+  uint64_t W = lo >> sh;
+  if (sh) W |= (uint64_t)w2 << (64 - sh);
+  return W & mask;
+}
+
+__device__ __forceinline__ uint64_t canon_hash(uint64_t W, int K, const HashP& hp) {
+  const uint64_t fw = rev2(W) >> (64 - 2 * K);
+  const uint64_t rc = W ^ hp.mask;
+  return khash(hp, fw < rc ? fw : rc);
+}
+
+__global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restrict__ base_off,
+                                                         const uint64_t* __restrict__ byte_off,
+                                                         uint8_t* __restrict__ packed, uint8_t* __restrict__ quals,
+                                                         uint64_t n_reads, int K, HashP hp, uint32_t maxq,
+                                                         const unsigned long long* __restrict__ table, uint64_t tmask,
+                                                         PcCounters* __restrict__ cnt) {
+  const int lane = lane_id();
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;  // lane 0's
+  for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave_id(); r < n_reads; r += nwaves) {
+    const uint64_t q0 = base_off[r];
+    const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
+    if (L < (uint32_t)K || L > kPcMaxL) continue;  // wave-uniform
+    uint8_t* rd = packed + byte_off[r];
+    uint8_t* q = quals + q0;
+    const uint32_t nbytes = (L + 3) >> 2;
+    uint32_t word = 0;
+    if (4u * lane < nbytes) {
+      const uint32_t b = 4u * lane;
+      word = (uint32_t)rd[b] | (b + 1 < nbytes ? (uint32_t)rd[b + 1] << 8 : 0u) |
+             (b + 2 < nbytes ? (uint32_t)rd[b + 2] << 16 : 0u) | (b + 3 < nbytes ? (uint32_t)rd[b + 3] << 24 : 0u);
+    }
+    for (uint32_t c = 0; c < L; c += 64) {
+      const uint32_t pl = c + lane;
+      uint64_t m = __ballot(pl < L && q[pl] < maxq);
+      while (m) {
+        const uint32_t p = c + (uint32_t)(__ffsll((long long)m) - 1);
+        m &= m - 1;
+        const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - K : 0;
+        const uint32_t jhi = min(p, L - (uint32_t)K);
+        const uint32_t nk = jhi - jlo + 1;  // <= K <= 32
+        // every lane takes part in the shuffles; lanes >= nk repeat the last K-mer
+        const uint64_t Wk = window_at(word, jlo + min((uint32_t)lane, nk - 1), hp.mask);
+        bool solid = false;
+        if ((uint32_t)lane < nk) solid = is_solid(table, tmask, canon_hash(Wk, K, hp));
+        if (__ballot(solid)) continue;
+        ++n_sus;
+        const uint32_t orig = (__shfl((int)word, (int)(p >> 4), 64) >> (2 * (p & 15))) & 3;
+        // (alternative a in 0..2, covering K-mer t) -> flat index a*nk + t; two rounds of 64 lanes
+        uint64_t fail[2] = {0, 0};
+        for (int rnd = 0; rnd < 2; ++rnd) {
+          const uint32_t f = rnd * 64 + lane;
+          bool bad = false;
+          uint64_t W = 0;
+          const bool act = f < 3 * nk;
+          const uint32_t a = act ? f / nk : 0, t = act ? f - a * nk : 0;
+          W = window_at(word, jlo + t, hp.mask);
+          if (act) {
+            const uint32_t alt = a + (a >= orig ? 1u : 0u);
+            const uint32_t sh = 2 * (p - (jlo + t));
+            W = (W & ~(3ull << sh)) | ((uint64_t)alt << sh);
+            bad = !is_solid(table, tmask, canon_hash(W, K, hp));
+          }
+          fail[rnd] = __ballot(bad);
+          if (3 * nk <= 64) break;
+        }
+        uint32_t ncand = 0, cand = 0;
+        for (uint32_t a = 0; a < 3; ++a) {
+          const uint32_t lo = a * nk, hi = lo + nk;  // flat range [lo, hi)
+          bool any = false;
+          for (int rnd = 0; rnd < 2; ++rnd) {
+            const uint32_t b0 = rnd * 64;
+            if (hi <= b0 || lo >= b0 + 64) continue;
+            const uint32_t s0 = lo > b0 ? lo - b0 : 0, s1 = min(hi - b0, 64u);
+            const uint64_t rm = (s1 - s0 == 64 ? ~0ull : ((1ull << (s1 - s0)) - 1)) << s0;
+            any |= (fail[rnd] & rm) != 0;
+          }
+          if (!any) {
+            ++ncand;
+            cand = a + (a >= orig ? 1u : 0u);
+          }
+        }
+        if (ncand == 1) {
+          if ((uint32_t)lane == (p >> 4)) {
+            const uint32_t sh = 2 * (p & 15);
+            word = (word & ~(3u << sh)) | (cand << sh);
+          }
+          const uint32_t nw = (uint32_t)__shfl((int)word, (int)(p >> 4), 64);
+          if (lane == 0) {
+            rd[p >> 2] = (uint8_t)(nw >> (8 * ((p >> 2) & 3)));
+            uint32_t nq = 255;
+            if (p > 0) nq = min(nq, (uint32_t)q[p - 1]);
+            if (p + 1 < L) nq = min(nq, (uint32_t)q[p + 1]);
+            q[p] = (uint8_t)nq;
+            ++n_cor;
+          }
+        } else if (ncand > 1) {
+          ++n_amb;
+        } else {
+          ++n_unc;
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    if (n_sus) atomicAdd(&cnt->suspect, n_sus);
+    if (n_cor) atomicAdd(&cnt->corrected, n_cor);
+    if (n_amb) atomicAdd(&cnt->ambiguous, n_amb);
+    if (n_unc) atomicAdd(&cnt->uncorrectable, n_unc);
+  }
+}
+
+// Solid list of a table-mode count into the "pc_solid" workspace.
+static int collect_solid(apg_ctx* ctx, const CountResult& cr, uint32_t min_solid, uint64_t** list, uint64_t* n) {
+  const uint64_t NB = cr.nbuckets;
+  uint32_t* bsolid = nullptr;
+  uint64_t* soff = nullptr;
+  APG_TRY(workspace_t(ctx, "pc_bsolid", std::max<uint64_t>(NB, 1), &bsolid));
+  APG_TRY(workspace_t(ctx, "pc_soff", NB + 1, &soff));
+  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(NB, (uint64_t)ctx->n_cu * 16));
+  if (NB) k_bucket_solid<<<grid, 256, 0, ctx->stream>>>(cr.tab_cnt, cr.boff, cr.bucket_nd, NB, min_solid, bsolid);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, bsolid, NB, soff, "pc"));
+  uint64_t ns = 0;
+  APG_CHECK_HIP(hipMemcpyAsync(&ns, soff + NB, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  APG_TRY(workspace_t(ctx, "pc_solid", std::max<uint64_t>(ns, 1), list));
+  kbegin(ctx, "solid_collect", cr.st.n_distinct * 12 + ns * 8);
+  if (NB)
+    k_solid_collect<<<grid, 256, 0, ctx->stream>>>(cr.rec, cr.tab_cnt, cr.boff, cr.bucket_nd, NB, min_solid, soff,
+                                                   *list);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  *n = ns;
+  return APG_OK;
+}
+
+// One correction pass of every read of `dr` against the solid hash list.
+static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const uint64_t* list, uint64_t n_solid,
+                        apg_pc_stats* st) {
   unsigned long long* dcnt = nullptr;
   APG_TRY(workspace_t(ctx, "pc_counters", 8, &dcnt));
   APG_CHECK_HIP(hipMemsetAsync(dcnt, 0, 8 * 8, ctx->stream));
-  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(cr.nbuckets, (uint64_t)ctx->n_cu * 16));
-  k_count_solid<<<grid, 256, 0, ctx->stream>>>(cr.tab_cnt, cr.boff, cr.bucket_nd, cr.nbuckets, p.min_solid, dcnt + 4);
-  APG_CHECK_HIP(hipGetLastError());
-  unsigned long long n_solid = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&n_solid, dcnt + 4, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
   uint64_t T = 1024;
   while (T < 2 * n_solid) T <<= 1;
   unsigned long long* table = nullptr;
   APG_TRY(workspace_t(ctx, "pc_table", T, &table));
   APG_CHECK_HIP(hipMemsetAsync(table, 0xff, T * 8, ctx->stream));
   kbegin(ctx, "solid_insert", n_solid * 8 * 2);
-  k_solid_insert<<<grid, 256, 0, ctx->stream>>>(cr.rec, cr.tab_cnt, cr.boff, cr.bucket_nd, cr.nbuckets, p.min_solid,
-                                                table, T - 1);
+  if (n_solid) k_solid_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, table, T - 1);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
-  const uint64_t rgrid =
-      std::max<uint64_t>(1, std::min<uint64_t>((dr->n_reads + 255) / 256, (uint64_t)ctx->n_cu * 32));
-  kbegin(ctx, "precorrect", dr->n_bytes * 2 + dr->n_bases * 2);
-  k_precorrect<<<rgrid, 256, 0, ctx->stream>>>(dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals,
-                                               dr->n_reads, p.K, make_hashp(p.K), p.max_q_suspect, table, T - 1,
-                                               reinterpret_cast<PcCounters*>(dcnt));
+  const HashP hp = make_hashp(p.K);
+  kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases);
+  if (dr->n_reads)
+    k_precorrect_wave<<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
+        dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, table,
+        T - 1, reinterpret_cast<PcCounters*>(dcnt));
   kend(ctx);
+  if (dr->max_len > kPcMaxL) {  // reads longer than one wave's registers: thread per read
+    const uint64_t rgrid =
+        std::max<uint64_t>(1, std::min<uint64_t>((dr->n_reads + 255) / 256, (uint64_t)ctx->n_cu * 32));
+    k_precorrect<<<rgrid, 256, 0, ctx->stream>>>(dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals,
+                                                 dr->n_reads, p.K, hp, p.max_q_suspect, table, T - 1, kPcMaxL + 1,
+                                                 reinterpret_cast<PcCounters*>(dcnt));
+  }
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long h[4];
   APG_CHECK_HIP(hipMemcpyAsync(h, dcnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
@@ -184,8 +375,27 @@ static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p,
   st->n_ambiguous += h[2];
   st->n_uncorrectable += h[3];
   st->n_solid = n_solid;
-  vlog(ctx, "precorrect pass: solid=%llu suspect=%llu corrected=%llu ambiguous=%llu none=%llu", n_solid, h[0], h[1],
-       h[2], h[3]);
+  vlog(ctx, "precorrect pass: solid=%llu suspect=%llu corrected=%llu ambiguous=%llu none=%llu",
+       (unsigned long long)n_solid, h[0], h[1], h[2], h[3]);
+  static std::atomic<uint64_t> g_edit{1ull << 62};
+  dr->gen = g_edit.fetch_add(1);  // bases changed: invalidate per-read-set plans
+  return APG_OK;
+}
+
+static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st) {
+  CountResult cr;
+  APG_TRY(spectrum_impl(ctx, dr, p.K, true, nullptr, 0, &cr));
+  uint64_t* list = nullptr;
+  uint64_t ns = 0;
+  APG_TRY(collect_solid(ctx, cr, p.min_solid, &list, &ns));
+  ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
+  return correct_pass(ctx, dr, p, list, ns, st);
+}
+
+static int check_pc(const apg_pc_params& p) {
+  APG_REQUIRE(p.K >= 1 && p.K <= 32, "apg_precorrect: K must be in [1, 32]");
+  APG_REQUIRE(p.min_solid >= 1, "apg_precorrect: min_solid must be >= 1");
+  APG_REQUIRE(p.n_cycles >= 1 && p.n_cycles <= 16, "apg_precorrect: n_cycles must be in [1, 16]");
   return APG_OK;
 }
 
@@ -211,18 +421,59 @@ int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, ap
     p = *pp;
   else
     apg_pc_defaults(&p);
-  APG_REQUIRE(p.K >= 1 && p.K <= 32, "apg_precorrect: K must be in [1, 32]");
-  APG_REQUIRE(p.min_solid >= 1, "apg_precorrect: min_solid must be >= 1");
-  APG_REQUIRE(p.n_cycles >= 1 && p.n_cycles <= 16, "apg_precorrect: n_cycles must be in [1, 16]");
+  APG_TRY(check_pc(p));
   APG_REQUIRE(dr->n_reads == 0 || dr->d_quals, "apg_precorrect: read set has no qualities");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   apg_pc_stats st;
   std::memset(&st, 0, sizeof st);
-  for (uint32_t c = 0; c < p.n_cycles; ++c) {
-    APG_TRY(precorrect_pass(ctx, dr, p, &st));
-    static std::atomic<uint64_t> g_edit{1ull << 62};
-    dr->gen = g_edit.fetch_add(1);  // bases changed: invalidate per-read-set plans
-  }
+  for (uint32_t c = 0; c < p.n_cycles; ++c) APG_TRY(precorrect_pass(ctx, dr, p, &st));
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+                    uint32_t min_solid, uint64_t* n_solid) {
+  APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid: NULL argument");
+  APG_REQUIRE(min_solid >= 1, "apg_shard_solid: min_solid must be >= 1");
+  ctx->solid_valid = false;
+  CountResult cr;
+  APG_TRY(shard_table_impl(ctx, static_cast<const uint64_t*>(d_recv), recv_counts, K, n_shards, &cr));
+  uint64_t* list = nullptr;
+  uint64_t ns = 0;
+  APG_TRY(collect_solid(ctx, cr, min_solid, &list, &ns));
+  APG_TRY(sync(ctx));
+  ctx->n_solid = ns;
+  ctx->solid_valid = true;
+  *n_solid = ns;
+  return APG_OK;
+}
+
+int apg_solid_export(apg_ctx* ctx, void* d_out) {
+  APG_REQUIRE(ctx, "apg_solid_export: NULL ctx");
+  APG_REQUIRE(ctx->solid_valid, "apg_solid_export: no apg_shard_solid result on this context");
+  if (ctx->n_solid == 0) return APG_OK;
+  APG_REQUIRE(d_out, "apg_solid_export: d_out is NULL");
+  uint64_t* list = nullptr;
+  APG_TRY(workspace_t(ctx, "pc_solid", ctx->n_solid, &list));
+  APG_CHECK_HIP(hipMemcpyAsync(d_out, list, ctx->n_solid * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  return sync(ctx);
+}
+
+int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, const void* d_solid,
+                         uint64_t n_solid, apg_pc_stats* stats) {
+  APG_REQUIRE(ctx && dr, "apg_precorrect_solid: NULL argument");
+  APG_REQUIRE(n_solid == 0 || d_solid, "apg_precorrect_solid: d_solid is NULL");
+  apg_pc_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_pc_defaults(&p);
+  APG_TRY(check_pc(p));
+  APG_REQUIRE(dr->n_reads == 0 || dr->d_quals, "apg_precorrect_solid: read set has no qualities");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_pc_stats st;
+  std::memset(&st, 0, sizeof st);
+  APG_TRY(correct_pass(ctx, dr, p, static_cast<const uint64_t*>(d_solid), n_solid, &st));
   if (stats) *stats = st;
   return APG_OK;
 }

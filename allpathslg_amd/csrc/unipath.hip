@@ -198,6 +198,13 @@ struct Roller3 {
     ++i;
   }
   __device__ __forceinline__ bool more() const { return i < len; }
+  // reposition so that the next step() completes the K-mer starting at base j
+  __device__ __forceinline__ void seek(uint32_t j, const KeyP& p) {
+    i = j;
+    fw = K3{0, 0, 0};
+    rc = K3{0, 0, 0};
+    for (int t = 0; t < p.K - 1; ++t) step(p);
+  }
   // next K-mer instance as a KRec
   __device__ __forceinline__ KRec next(const KeyP& p) {
     step(p);
@@ -1068,12 +1075,20 @@ __global__ void k_hkp_edges(uint64_t U, uint32_t* __restrict__ par, const uint64
 
 // Per-read KmerPath: ids of the read's K-mers, run-length compressed into
 // intervals of consecutive ids.  WRITE = false counts intervals only.
+// Read KmerPaths.  One index lookup per interval, not per K-mer: if the read's
+// K-mer at j is node v at rank r of unipath u, its next K-mers are the next
+// nodes of u for as long as both last — every interior node of a unipath has
+// a single out-extension and the read's next base is one of v's recorded
+// out-extensions — so the run is min(K-mers left in the read, len(u) - r)
+// consecutive ids.  Runs whose ids continue each other merge (as per-K-mer
+// appending would).
 template <bool WRITE>
 __global__ void k_read_paths(ReadsV rv, NodeIdx ni, KeyP kp, const uint32_t* __restrict__ head,
                              const uint32_t* __restrict__ rank, const uint32_t* __restrict__ uni_of_head,
-                             const uint64_t* __restrict__ id_base, uint32_t* __restrict__ nint,
-                             const uint64_t* __restrict__ ioff, uint64_t* __restrict__ istart,
-                             uint64_t* __restrict__ ilen, unsigned long long* __restrict__ bad) {
+                             const uint64_t* __restrict__ id_base, const uint64_t* __restrict__ ulen,
+                             uint32_t* __restrict__ nint, const uint64_t* __restrict__ ioff,
+                             uint64_t* __restrict__ istart, uint64_t* __restrict__ ilen,
+                             unsigned long long* __restrict__ bad) {
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads;
        r += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
@@ -1081,27 +1096,34 @@ __global__ void k_read_paths(ReadsV rv, NodeIdx ni, KeyP kp, const uint32_t* __r
     uint64_t cs = 0, cl = 0;
     const uint64_t o = WRITE ? ioff[r] : 0;
     if (len >= (uint32_t)kp.K) {
+      const uint32_t nk = len - kp.K + 1;
       Roller3 ro;
       ro.init(rv.packed + rv.byte_off[r], len, kp);
-      while (ro.more()) {
+      uint32_t j = 0;  // K-mer index the next step() completes
+      while (j < nk) {
         ro.step(kp);
         const uint32_t v = directed_of(ni, ro.fw, kp);
         if (v == kNone) {
           atomicAdd(bad, 1ull);
+          ++j;
           continue;
         }
-        const uint64_t id = id_base[uni_of_head[head[v]]] + rank[v];
+        const uint32_t u = uni_of_head[head[v]];
+        const uint64_t id = id_base[u] + rank[v];
+        const uint32_t run = (uint32_t)min((uint64_t)(nk - j), ulen[u] - rank[v]);
         if (cl && cs + cl == id) {
-          ++cl;
+          cl += run;
         } else {
           if (cl && WRITE) {
             istart[o + k - 1] = cs;
             ilen[o + k - 1] = cl;
           }
           cs = id;
-          cl = 1;
+          cl = run;
           ++k;
         }
+        j += run;
+        if (run > 1 && j < nk) ro.seek(j, kp);
       }
       if (cl && WRITE) {
         istart[o + k - 1] = cs;
@@ -1119,9 +1141,6 @@ static int ceil_log2_u(uint64_t x) {
   int b = 0;
   while ((1ull << b) < x) ++b;
   return b;
-}
-static uint32_t grid_for(apg_ctx* ctx, uint64_t n, int per = 256) {
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, (uint64_t)ctx->n_cu * 16));
 }
 
 constexpr uint64_t kUBucketTarget = 640;
@@ -1513,8 +1532,8 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     APG_TRY(workspace_t(ctx, "u_ioff", dr->n_reads + 1, &ioff));
     const uint32_t rg = grid_for(ctx, dr->n_reads);
     kbegin(ctx, "u_read_paths_count", dr->n_bytes + n * 8);
-    k_read_paths<false><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, nint, nullptr,
-                                                     nullptr, nullptr, gs + 25);
+    k_read_paths<false><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, ulen, nint,
+                                                     nullptr, nullptr, nullptr, gs + 25);
     kend(ctx);
     APG_TRY(scan_u32_u64(ctx, nint, dr->n_reads, ioff, "up"));
     APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1522,8 +1541,8 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     APG_TRY(workspace_t(ctx, "u_istart", std::max<uint64_t>(NI, 1), &istart));
     APG_TRY(workspace_t(ctx, "u_ilen", std::max<uint64_t>(NI, 1), &ilen));
     kbegin(ctx, "u_read_paths_write", dr->n_bytes + n * 8 + NI * 16);
-    k_read_paths<true><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, nullptr, ioff,
-                                                    istart, ilen, gs + 25);
+    k_read_paths<true><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, ulen, nullptr,
+                                                    ioff, istart, ilen, gs + 25);
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     st->n_intervals = NI;

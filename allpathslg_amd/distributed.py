@@ -46,6 +46,19 @@ class HipShardBackend:
         torch.cuda.synchronize(self.device)
         return self.ctx.shard_spectrum(recv.data_ptr(), recv_counts, K, P, hist_len)
 
+    # correction stages
+    def shard_solid(self, recv: torch.Tensor, recv_counts: np.ndarray, K: int, P: int, min_solid: int) -> int:
+        torch.cuda.synchronize(self.device)
+        return self.ctx.shard_solid(recv.data_ptr(), recv_counts, K, P, min_solid)
+
+    def solid_export(self, out: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)
+        self.ctx.solid_export(out.data_ptr())
+
+    def precorrect_solid(self, dreads: DeviceReads, solid: torch.Tensor, n_solid: int, prm: dict) -> dict:
+        torch.cuda.synchronize(self.device)
+        return self.ctx.precorrect_solid(dreads, solid.data_ptr(), n_solid, **prm)
+
     # unipath stages
     def ushard_count(self, dreads: DeviceReads, K: int, P: int) -> np.ndarray:
         return self.ctx.ushard_count(dreads, K, P)
@@ -67,13 +80,9 @@ class HipShardBackend:
         return self.ctx.unipaths_from_nodes(nodes.data_ptr(), n_nodes, dreads, K, read_paths=True, fetch=fetch)
 
 
-def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
-                     group: Optional[dist.ProcessGroup] = None) -> Tuple[np.ndarray, dict]:
-    """Global spectrum of the union of every rank's reads.  Returns the same
-    (hist, stats) on every rank; stats are summed over ranks."""
-    P = dist.get_world_size(group)
-    if P & (P - 1):
-        raise ValueError(f"world size {P} must be a power of two (k-mer hash shards)")
+def _exchange_kmers(backend, reads, K: int, P: int, group):
+    """K <= 32 hash records of this rank's reads -> their owner shards.
+    Returns (recv tensor, recv_counts [src * B + l1], records sent, received)."""
     B = shard_bins(K, P)
     dev = backend.alloc(1).device
     counts = backend.shard_count(reads, K, P)  # [dest * B + l1]
@@ -91,7 +100,22 @@ def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
     n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
     dist.all_to_all_single(recv[:n_out] if n_out else recv[:0], send[:n_in] if n_in else send[:0],
                            out_splits, in_splits, group=group)
+    return recv, recv_counts, n_in, n_out
 
+
+def _check_pow2(P: int) -> None:
+    if P & (P - 1):
+        raise ValueError(f"world size {P} must be a power of two (k-mer hash shards)")
+
+
+def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
+                     group: Optional[dist.ProcessGroup] = None) -> Tuple[np.ndarray, dict]:
+    """Global spectrum of the union of every rank's reads.  Returns the same
+    (hist, stats) on every rank; stats are summed over ranks."""
+    P = dist.get_world_size(group)
+    _check_pow2(P)
+    dev = backend.alloc(1).device
+    recv, recv_counts, n_in, n_out = _exchange_kmers(backend, reads, K, P, group)
     hist, st = backend.shard_spectrum(recv, recv_counts, K, P, hist_len)
     hist_t = torch.from_numpy(hist.astype(np.int64)).to(dev)
     dist.all_reduce(hist_t, group=group)
@@ -104,6 +128,43 @@ def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
     out["records_sent"] = n_in
     out["records_received"] = n_out
     return hist_t.cpu().numpy().astype(np.uint64), out
+
+
+def sharded_precorrect(backend, reads, K: int = 24, min_solid: int = 3, max_q_suspect: int = 20, n_cycles: int = 1,
+                       group: Optional[dist.ProcessGroup] = None) -> dict:
+    """PreCorrect / FindErrors over every rank's reads: per pass,
+    K-mers are counted on their owner shards, each shard's solid set is
+    all_gathered (the replicated solid set), and every rank corrects its own
+    reads in place.  Returns stats summed over ranks (n_solid = global)."""
+    P = dist.get_world_size(group)
+    _check_pow2(P)
+    dev = backend.alloc(1).device
+    tot = {"n_suspect": 0, "n_corrected": 0, "n_ambiguous": 0, "n_uncorrectable": 0, "n_solid": 0}
+    for _ in range(n_cycles):
+        recv, recv_counts, _, _ = _exchange_kmers(backend, reads, K, P, group)
+        n_local = backend.shard_solid(recv, recv_counts, K, P, min_solid)
+        del recv
+        sizes_t = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        all_sizes = [torch.empty_like(sizes_t) for _ in range(P)]
+        dist.all_gather(all_sizes, sizes_t, group=group)
+        sizes = [int(x.item()) for x in all_sizes]
+        maxn = max(max(sizes), 1)
+        local = backend.alloc(maxn)
+        backend.solid_export(local)
+        gathered = backend.alloc(maxn * P)
+        dist.all_gather_into_tensor(gathered[: maxn * P], local[:maxn], group=group)
+        solid = torch.cat([gathered[maxn * r : maxn * r + sizes[r]] for r in range(P)])
+        del gathered, local
+        st = backend.precorrect_solid(reads, solid, sum(sizes),
+                                      {"K": K, "min_solid": min_solid, "max_q_suspect": max_q_suspect})
+        for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
+            tot[k] += int(st[k])
+        tot["n_solid"] = sum(sizes)
+    keys = ["n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"]
+    st_t = torch.tensor([tot[k] for k in keys], dtype=torch.int64, device=dev)
+    dist.all_reduce(st_t, group=group)
+    tot.update({k: int(v) for k, v in zip(keys, st_t.cpu().tolist())})
+    return tot
 
 
 def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGroup] = None,

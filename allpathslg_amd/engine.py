@@ -177,6 +177,29 @@ class Context:
                                    q.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(st)), "apg_precorrect")
         return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), st.as_dict()
 
+    def copy_reads(self, dst: DeviceReads, src: DeviceReads) -> None:
+        """dst := src (device-to-device; same read lengths)."""
+        check(lib().apg_reads_copy_dev(self._h, dst.handle, src.handle), "apg_reads_copy_dev")
+
+    # multi-GPU correction stages (allpathslg_amd.distributed.sharded_precorrect)
+    def shard_solid(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int, min_solid: int) -> int:
+        rc = np.ascontiguousarray(recv_counts, dtype=np.uint64)
+        n = C.c_uint64()
+        check(lib().apg_shard_solid(self._h, C.c_void_p(d_recv_ptr), rc.ctypes.data_as(_u64p), K, n_shards,
+                                    min_solid, C.byref(n)), "apg_shard_solid")
+        return int(n.value)
+
+    def solid_export(self, d_out_ptr: int) -> None:
+        check(lib().apg_solid_export(self._h, C.c_void_p(d_out_ptr)), "apg_solid_export")
+
+    def precorrect_solid(self, dreads: DeviceReads, d_solid_ptr: int, n_solid: int, K: int = 24, min_solid: int = 3,
+                         max_q_suspect: int = 20) -> dict:
+        p = self.pc_params(K, min_solid, max_q_suspect, 1)
+        st = apg_pc_stats()
+        check(lib().apg_precorrect_solid(self._h, dreads.handle, C.byref(p), C.c_void_p(d_solid_ptr), n_solid,
+                                         C.byref(st)), "apg_precorrect_solid")
+        return st.as_dict()
+
     def download(self, dreads: DeviceReads) -> ReadSet:
         r = dreads.reads
         pk = np.zeros_like(r.packed)

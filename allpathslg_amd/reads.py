@@ -192,3 +192,37 @@ def synth_reads(
         "apg_synth_reads",
     )
     return ReadSet(base_off, byte_off, packed, quals)
+
+
+def synth_fragments(
+    genome: np.ndarray,
+    n_pairs: int,
+    seed: int,
+    read_len: int = 100,
+    insert_mean: int = 180,
+    insert_sd: int = 18,
+    first_pair: int = 0,
+    threads: int = 0,
+) -> ReadSet:
+    """The error-free insert of each pair synth_reads(genome, n_pairs, seed, ...)
+    generates, in read A's orientation — the "oracle fill" that stands in for
+    FillFragments as K=96 unipath input.  No qualities."""
+    p = apg_synth_params()
+    p.genome_len = len(genome)
+    p.seed = seed
+    p.n_pairs = n_pairs
+    p.read_len = read_len
+    p.insert_mean = insert_mean
+    p.insert_sd = insert_sd
+    p.threads = threads
+    p.first_pair = first_pair
+    L = lib()
+    base_off = np.empty(n_pairs + 1, dtype=np.uint64)
+    byte_off = np.empty(n_pairs + 1, dtype=np.uint64)
+    check(L.apg_synth_fragments(C.byref(p), _ptr(base_off, C.c_uint64), _ptr(byte_off, C.c_uint64), None, None),
+          "apg_synth_fragments")
+    packed = np.zeros(int(byte_off[-1]) + 64, dtype=np.uint8)
+    g = np.ascontiguousarray(genome, dtype=np.uint8)
+    check(L.apg_synth_fragments(C.byref(p), _ptr(base_off, C.c_uint64), _ptr(byte_off, C.c_uint64),
+                                _ptr(g, C.c_uint8), _ptr(packed, C.c_uint8)), "apg_synth_fragments")
+    return ReadSet(base_off, byte_off, packed, None)

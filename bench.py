@@ -1,13 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark: reads/s of the k-mer spectrum hot path on MI355X.
+"""Benchmark: reads/s of the k-mer spectrum + error correction + unipath
+build hot path on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "Human chr20: 40 M 100 bp paired frag
-reads, 1x MI355X k-mer spectrum"): a chr20-size synthetic genome
-(64,444,167 bp), 20 M read pairs (40 M x 100 bp reads) per GPU generated by
-the deterministic simulator, canonical K=25 k-mer counting and
-spectrum.  One "step" = the whole spectrum of the rank's 40 M reads, inputs
-resident in HBM.  N > 1: weak scaling (40 M reads per GPU), k-mers
-hash-sharded across ranks with one all_to_all over RCCL, spectra all_reduced.
+Workload (BASELINE.json configs[1] + configs[2], chr20): a chr20-size
+synthetic genome (64,444,167 bp), 20 M read pairs (40 M x 100 bp reads) per
+GPU from the deterministic simulator.  One "step", inputs resident
+in HBM:
+  1. restore the rank's reads to their uploaded state (device copy)
+  2. K=25 canonical k-mer count + spectrum of the 40 M reads
+  3. K=24 PreCorrect of the 40 M reads (count, solid set, per-read correction)
+  4. K=96 unipaths + unibases + HyperKmerPath + KmerPaths of the 20 M pair
+     fragments.  The fragments are the simulator's true inserts ("oracle
+     fill", SURVEY §8d: K=96 needs ~180 bp fragments; FillFragments is §8f
+     next #1), generated once outside the timed region.
+N > 1: weak scaling (40 M reads per GPU); k-mers hash-sharded across ranks
+with all_to_all over RCCL, solid sets all_gathered, spectra all_reduced,
+unipath nodes all_gathered.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -27,8 +35,9 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from allpathslg_amd import Context, synth_genome, synth_reads  # noqa: E402
-from allpathslg_amd.distributed import HipShardBackend, sharded_spectrum, sharded_unipaths  # noqa: E402
+from allpathslg_amd import Context, synth_fragments, synth_genome, synth_reads  # noqa: E402
+from allpathslg_amd.distributed import (  # noqa: E402
+    HipShardBackend, sharded_precorrect, sharded_spectrum, sharded_unipaths)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -43,9 +52,11 @@ def parse():
     p.add_argument("--K", type=int, default=25)
     p.add_argument("--seed", type=int, default=0xA11BA7)
     p.add_argument("--K-unipath", type=int, default=96)
+    p.add_argument("--K-correct", type=int, default=24)
     p.add_argument("--spectrum-only", action="store_true")
     p.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
-    p.add_argument("--cpu-unipath-sample-reads", type=int, default=200_000)
+    p.add_argument("--cpu-correct-sample-reads", type=int, default=1_000_000)
+    p.add_argument("--cpu-unipath-sample-frags", type=int, default=20_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
@@ -71,28 +82,36 @@ def main():
     t0 = time.time()
     genome = synth_genome(a.genome_len, a.seed)
     n_pairs = a.reads_per_gpu // 2
-    reads = synth_reads(genome, n_pairs, seed=a.seed + 1, first_pair=rank * n_pairs, with_quals=False, threads=16)
-    log(rank, f"synth {reads.n_reads} reads in {time.time() - t0:.1f}s")
+    reads = synth_reads(genome, n_pairs, seed=a.seed + 1, first_pair=rank * n_pairs, with_quals=True, threads=16)
+    frags = None if a.spectrum_only else synth_fragments(genome, n_pairs, seed=a.seed + 1,
+                                                         first_pair=rank * n_pairs, threads=16)
+    log(rank, f"synth {reads.n_reads} reads + fragments in {time.time() - t0:.1f}s")
 
     ctx = Context(device=local, timing=True, verbose=a.verbose)
+    dsrc = ctx.upload(reads)
     dreads = ctx.upload(reads)
+    dfrags = None if frags is None else ctx.upload(frags)
     backend = HipShardBackend(ctx)
 
     def step():
+        ctx.copy_reads(dreads, dsrc)
         if world == 1:
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
             hist, st = sharded_spectrum(backend, dreads, a.K)
-        ust = None
+        pst = ust = None
         if not a.spectrum_only:
             if world == 1:
-                _, ust = ctx.unipaths(dreads, a.K_unipath, read_paths=True, fetch=False)
+                _, pst = ctx.precorrect(dreads, K=a.K_correct)
+                _, ust = ctx.unipaths(dfrags, a.K_unipath, read_paths=True, fetch=False)
             else:
-                ust = sharded_unipaths(backend, dreads, a.K_unipath)
-        return hist, st, ust
+                pst = sharded_precorrect(backend, dreads, K=a.K_correct)
+                ust = sharded_unipaths(backend, dfrags, a.K_unipath)
+        return hist, st, pst, ust
 
     for _ in range(a.warmup):
-        hist, st, ust = step()
+        hist, st, pst, ust = step()
+    free_b, total_b = torch.cuda.mem_get_info()
     torch.cuda.synchronize()
     ctx.reset_timing()
 
@@ -101,7 +120,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(a.steps):
-        hist, st, ust = step()
+        hist, st, pst, ust = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -121,6 +140,10 @@ def main():
         "kmers_equals_reads_x_76": st["n_kmers"] == world * reads.n_reads * (100 - a.K + 1),
         "bounded": bool(conserved),
     }
+    if pst is not None:
+        checks["precorrect_corrected_most_suspects"] = pst["n_corrected"] > 0.5 * pst["n_suspect"]
+        n_inst = world * int((np.maximum(frags.lengths().astype(np.int64) - a.K_unipath + 1, 0)).sum())
+        checks["unipath_instances_equal_sum_len_minus_K_plus_1"] = ust["n_instances"] == n_inst
 
     # Roofline of the dominant kernel, from HIP events on libapg's stream.
     kt = ctx.kernel_times()
@@ -146,16 +169,23 @@ def main():
         desc = (f"spectrum: first {sample.n_reads} reads, K={a.K} ({tc:.2f} s)")
         rate = spec_rate
         if not a.spectrum_only:
-            usample = reads.subset(0, min(a.cpu_unipath_sample_reads, reads.n_reads))
+            csample = reads.subset(0, min(a.cpu_correct_sample_reads, reads.n_reads))
+            tp = time.perf_counter()
+            oracle.precorrect(csample, K=a.K_correct)
+            tp = time.perf_counter() - tp
+            pc_rate = csample.n_reads / tp
+            usample = frags.subset(0, min(a.cpu_unipath_sample_frags, frags.n_reads))
             tu = time.perf_counter()
             oracle.unipaths(usample, a.K_unipath)
             tu = time.perf_counter() - tu
-            uni_rate = usample.n_reads / tu
-            rate = 1.0 / (1.0 / spec_rate + 1.0 / uni_rate)
-            desc += f"; unipaths: first {usample.n_reads} reads, K={a.K_unipath} ({tu:.2f} s)"
+            uni_rate = 2 * usample.n_reads / tu  # two reads per fragment
+            rate = 1.0 / (1.0 / spec_rate + 1.0 / pc_rate + 1.0 / uni_rate)
+            desc += (f"; PreCorrect: first {csample.n_reads} reads, K={a.K_correct} against their own "
+                     f"solid set ({tp:.2f} s); unipaths: first {usample.n_reads} fragments "
+                     f"(= {2 * usample.n_reads} reads), K={a.K_unipath} ({tu:.2f} s)")
         cpu = {"value": rate, "unit": "reads/s", "cores": 1, "kind": "port",
-               "sample": "oracle/ CPU restatement, single-threaded, same synthetic reads; " + desc +
-                         "; value = 1/(1/spectrum_rate + 1/unipath_rate)"}
+               "sample": "oracle/ CPU restatement, single-threaded, same synthetic inputs; " + desc +
+                         "; value = 1/(sum of 1/stage_rate)"}
 
     if rank == 0:
         total_reads = world * reads.n_reads * a.steps
@@ -171,17 +201,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (deterministic simulator, SURVEY §B; uniform genome, 0.2-2% substitution ramp)",
+            "data": "synthetic (deterministic simulator, SURVEY §B; uniform genome, 0.2-2% substitution ramp, "
+                    "Q40 / Q2-20 on errors)",
             "config": {
-                "workload": "C2 chr20-size: 40M x 100bp paired frag reads per GPU; K=25 k-mer spectrum + "
-                            "K=96 unipath build (unipaths, unibases, HyperKmerPath, read KmerPaths)",
+                "workload": "C2/C3 chr20-size: 40M x 100bp paired frag reads per GPU; K=25 k-mer spectrum + "
+                            "K=24 PreCorrect + K=96 unipath build (unipaths, unibases, HyperKmerPath, "
+                            "fragment KmerPaths) on the 20M pair fragments",
                 "reads_per_gpu": reads.n_reads,
                 "genome_len": a.genome_len,
                 "K": a.K,
+                "K_correct": None if a.spectrum_only else a.K_correct,
                 "K_unipath": None if a.spectrum_only else a.K_unipath,
-                "stages_timed": ["kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
-                    "unipath_kmers", "unipaths", "unibases", "hyperkmerpath", "read_kmerpaths"]),
-                "unipath_input": "raw reads (PreCorrect/FillFragments not in the timed step)",
+                "stages_timed": ["restore_reads", "kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
+                    "precorrect", "unipath_kmers", "unipaths", "unibases", "hyperkmerpath", "fragment_kmerpaths"]),
+                "unipath_input": "simulator's true pair inserts (oracle fill standing in for FillFragments, "
+                                 "SURVEY §8d), generated outside the timed region",
+                "hbm_used_gb": (total_b - free_b) / 1e9,
                 "parallelism": f"kmer-hash shards x{world} + all_to_all" if world > 1 else "single GPU",
             },
             "roofline": {
@@ -198,11 +233,15 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},
+            "precorrect_stats": pst,
             "unipath_stats": ust,
             "checks": checks,
         }
         print(json.dumps(out), flush=True)
     dreads.free()
+    dsrc.free()
+    if dfrags is not None:
+        dfrags.free()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

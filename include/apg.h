@@ -89,6 +89,10 @@ typedef struct apg_dreads apg_dreads;
 int apg_reads_upload(apg_ctx* ctx, const apg_reads* reads, apg_dreads** out);
 void apg_reads_free(apg_dreads* dr);
 uint64_t apg_dreads_count(const apg_dreads* dr);
+/* Copy bases (and qualities) between two device read sets of the same shape
+ * (same read lengths), on the context's stream.  Used to restore a corrected
+ * read set to its uploaded state without a host round trip. */
+int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src);
 
 /* Fill byte_off[0..n] from base_off[0..n]. */
 int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_off);
@@ -192,6 +196,21 @@ int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
 /* Copy a device read set's (possibly corrected) bases/quals back to host
  * buffers of the upload's sizes (quals may be NULL). */
 int apg_reads_download(apg_ctx* ctx, const apg_dreads* reads, uint8_t* packed, uint8_t* quals);
+
+/* Multi-GPU correction (replicate the solid set, reads stay
+ * sharded).  Per pass: apg_shard_count / apg_shard_scatter at K -> all_to_all
+ * -> apg_shard_solid (this shard's solid K-mer hashes, in table order) ->
+ * apg_solid_export into a device buffer -> all_gather -> apg_precorrect_solid
+ * on every rank's own reads with the union.  The solid set is a set: the
+ * gathered order does not change any result. */
+int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts /* host */,
+                    int K, int n_shards, uint32_t min_solid, uint64_t* n_solid);
+/* d_out: device buffer of n_solid u64 (the hash of each solid K-mer). */
+int apg_solid_export(apg_ctx* ctx, void* d_out);
+/* One correction pass (p->n_cycles is ignored) against the given solid
+ * hashes (apg_kmer_hash of canonical K-mers, device memory). */
+int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
+                         const void* d_solid, uint64_t n_solid, apg_pc_stats* stats);
 
 /* ------------------------------------------------------------------------- */
 /* Unipath graph, 1 <= K <= 96 (default 96).  Replaces CommonPather /        */
@@ -311,6 +330,13 @@ int apg_synth_sizes(const apg_synth_params* p, uint64_t* n_reads, uint64_t* n_ba
 int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome,
                     uint64_t* base_off, uint64_t* byte_off, uint8_t* packed,
                     uint8_t* quals);
+/* The error-free fragment (insert) of each pair, in read A's orientation: the
+ * "oracle fill" standing in for FillFragments (SURVEY §8d K=96 caveat) until
+ * that module exists.  Call once with packed = NULL to get base_off/byte_off
+ * (n_pairs + 1 each), then again with the same offsets and packed sized
+ * byte_off[n_pairs] (+ slack) to fill the bases. */
+int apg_synth_fragments(const apg_synth_params* p, uint64_t* base_off, uint64_t* byte_off,
+                        const uint8_t* genome, uint8_t* packed);
 
 /* ------------------------------------------------------------------------- */
 /* On-disk formats ("APG-fastb v0"; feudal byte layout unpinned) */

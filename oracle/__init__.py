@@ -47,6 +47,9 @@ def lib() -> C.CDLL:
         L.ork_precorrect.restype = C.c_int
         L.ork_precorrect.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, _u8p, C.c_int, C.c_uint32, C.c_uint32,
                                      C.c_uint32, _u64p]
+        L.ork_precorrect_solid.restype = C.c_int
+        L.ork_precorrect_solid.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, _u8p, C.c_int, C.c_uint32, _u64p,
+                                           C.c_uint64, _u64p]
         L.ork_free.restype = None
         L.ork_free.argtypes = [C.c_void_p]
         _lib = L
@@ -118,6 +121,24 @@ def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1):
     rc = lib().ork_precorrect(reads.n_reads, reads.base_off.ctypes.data_as(_u64p), reads.byte_off.ctypes.data_as(_u64p),
                               pk.ctypes.data_as(_u8p), q.ctypes.data_as(_u8p), K, min_solid, max_q, n_cycles,
                               st.ctypes.data_as(_u64p))
+    if rc:
+        raise MemoryError("oracle precorrect failed")
+    keys = ["n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"]
+    return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), {k: int(v) for k, v in zip(keys, st)}
+
+
+def precorrect_solid(reads, solid_hashes, K=24, max_q=20):
+    """One correction pass of `reads` against a given solid hash set."""
+    from allpathslg_amd.reads import ReadSet
+
+    pk = reads.packed.copy()
+    q = reads.quals.copy()
+    st = np.zeros(5, dtype=np.uint64)
+    sh = np.ascontiguousarray(solid_hashes, dtype=np.uint64)
+    rc = lib().ork_precorrect_solid(reads.n_reads, reads.base_off.ctypes.data_as(_u64p),
+                                    reads.byte_off.ctypes.data_as(_u64p), pk.ctypes.data_as(_u8p),
+                                    q.ctypes.data_as(_u8p), K, max_q, sh.ctypes.data_as(_u64p), len(sh),
+                                    st.ctypes.data_as(_u64p))
     if rc:
         raise MemoryError("oracle precorrect failed")
     keys = ["n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"]

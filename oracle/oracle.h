@@ -16,5 +16,7 @@ void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t 
 void ork_free(void* p);
 int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
                    uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint32_t n_cycles, uint64_t* stats);
+int ork_precorrect_solid(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                         uint8_t* quals, int K, uint32_t maxq, const uint64_t* solid, uint64_t ns, uint64_t* stats);
 
 #endif

@@ -45,17 +45,9 @@ static int is_solid(const uint64_t* solid, uint64_t ns, uint64_t h) {
   return lo < ns && solid[lo] == h;
 }
 
-static int pass(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
-                uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint64_t* stats) {
-  uint64_t *h = NULL;
-  uint32_t* c = NULL;
-  const uint64_t nd = ork_kmer_count(n_reads, base_off, byte_off, packed, K, &h, &c);
-  if (nd == UINT64_MAX) return -1;
-  uint64_t ns = 0;
-  for (uint64_t i = 0; i < nd; ++i)
-    if (c[i] >= min_solid) h[ns++] = h[i]; /* stays ascending */
-  free(c);
-  stats[4] = ns;
+/* One correction pass against the ascending solid-hash array h[0..ns). */
+static void correct(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                    uint8_t* quals, int K, uint32_t maxq, const uint64_t* h, uint64_t ns, uint64_t* stats) {
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint32_t L = (uint32_t)(base_off[r + 1] - base_off[r]);
     if (L < (uint32_t)K) continue;
@@ -97,6 +89,39 @@ static int pass(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte
       }
     }
   }
+}
+
+static int pass(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint64_t* stats) {
+  uint64_t *h = NULL;
+  uint32_t* c = NULL;
+  const uint64_t nd = ork_kmer_count(n_reads, base_off, byte_off, packed, K, &h, &c);
+  if (nd == UINT64_MAX) return -1;
+  uint64_t ns = 0;
+  for (uint64_t i = 0; i < nd; ++i)
+    if (c[i] >= min_solid) h[ns++] = h[i]; /* stays ascending */
+  free(c);
+  stats[4] = ns;
+  correct(n_reads, base_off, byte_off, packed, quals, K, maxq, h, ns, stats);
+  free(h);
+  return 0;
+}
+
+static int cmp_u64(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* One pass against a caller-given solid hash set (any order; sorted here). */
+int ork_precorrect_solid(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                         uint8_t* quals, int K, uint32_t maxq, const uint64_t* solid, uint64_t ns, uint64_t* stats) {
+  memset(stats, 0, 5 * sizeof(uint64_t));
+  uint64_t* h = (uint64_t*)malloc((ns ? ns : 1) * sizeof(uint64_t));
+  if (!h) return -1;
+  if (ns) memcpy(h, solid, ns * sizeof(uint64_t));
+  qsort(h, ns, sizeof(uint64_t), cmp_u64);
+  stats[4] = ns;
+  correct(n_reads, base_off, byte_off, packed, quals, K, maxq, h, ns, stats);
   free(h);
   return 0;
 }

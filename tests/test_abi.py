@@ -126,3 +126,23 @@ def test_create_fails_loudly_without_gpu():
         Context(0)
     assert e.value.code == -2
     assert "HIP" in str(e.value) or "device" in str(e.value)
+
+
+def test_synth_fragments_are_the_pairs_inserts():
+    """Each fragment starts with read A and ends with rc(read B) (error-free
+    reads), so the oracle fill is exactly the simulated insert."""
+    from allpathslg_amd import synth_fragments
+
+    g = synth_genome(20_000, 5)
+    reads = synth_reads(g, 500, seed=6, err_lo=0.0, err_hi=0.0)
+    frags = synth_fragments(g, 500, seed=6)
+    assert frags.n_reads == 500
+    lens = np.diff(frags.base_off)
+    assert lens.min() >= 100 and abs(lens.mean() - 180) < 5
+    for k in range(500):
+        f = frags.read(k)
+        a, b = reads.read(2 * k), reads.read(2 * k + 1)
+        assert np.array_equal(f[:100], a)
+        assert np.array_equal(f[-100:], (3 - b)[::-1])
+    part = synth_fragments(g, 100, seed=6, first_pair=200)
+    assert np.array_equal(part.read(7), frags.read(207))

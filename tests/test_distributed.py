@@ -56,6 +56,24 @@ class OracleShardBackend:
         hist = oracle.spectrum_from_counts(c.astype(np.uint32), hist_len)
         return hist, {"n_kmers": n, "n_distinct": len(c), "n_overflow": 0}
 
+    # correction stages: solid set of the received records, pass on own reads
+    def shard_solid(self, recv, recv_counts, K, P, min_solid):
+        n = int(recv_counts.sum())
+        u, c = np.unique(recv[:n].numpy().view(np.uint64), return_counts=True)
+        self.solid = u[c >= min_solid]
+        return len(self.solid)
+
+    def solid_export(self, out):
+        out[: len(self.solid)] = torch.from_numpy(self.solid.view(np.int64))
+
+    def precorrect_solid(self, reads, solid, n_solid, prm):
+        fixed, st = oracle.precorrect_solid(reads, solid[:n_solid].numpy().view(np.uint64), prm["K"],
+                                            prm["max_q_suspect"])
+        reads.packed[:] = fixed.packed  # in place, like the device path
+        reads.quals[:] = fixed.quals
+        self.cache.clear()  # bases changed
+        return st
+
 
 def _free_port():
     s = socket.socket()
@@ -187,3 +205,42 @@ def test_sharded_unipaths_gloo(world):
         lo, hi = int(exp["path_off"][a]), int(exp["path_off"][b])
         assert np.array_equal(g["path_start"], exp["path_start"][lo:hi])
         assert np.array_equal(g["path_len"], exp["path_len"][lo:hi])
+
+
+def _pcworker(rank, world, port, n_cycles, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from allpathslg_amd.distributed import sharded_precorrect
+
+        reads = synth_reads(synth_genome(30_000, 31), 3000, seed=32)
+        parts = np.array_split(np.arange(reads.n_reads), world)
+        mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
+        st = sharded_precorrect(OracleShardBackend(), mine, K=24, n_cycles=n_cycles)
+        q.put((rank, mine.packed[: int(mine.byte_off[-1])].copy(), mine.quals.copy(), st))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_cycles", [(2, 1), (4, 2)])
+def test_sharded_precorrect_gloo(world, n_cycles):
+    """Replicated-solid-set correction == single-process PreCorrect/FindErrors."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pcworker, args=(r, world, port, n_cycles, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    reads = synth_reads(synth_genome(30_000, 31), 3000, seed=32)
+    exp, est = oracle.precorrect(reads, K=24, n_cycles=n_cycles)
+    assert est["n_corrected"] > 0
+    assert np.array_equal(np.concatenate([r[1] for r in res]), exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(np.concatenate([r[2] for r in res]), exp.quals)
+    for _, _, _, st in res:
+        for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+            assert st[k] == est[k], k

@@ -70,3 +70,99 @@ def test_precorrect_requires_quals(gpu_ctx):
     reads = ReadSet.from_sequences([[0, 1, 2, 3] * 10])
     with pytest.raises((ApgError, ValueError)):
         gpu_ctx.precorrect(reads)
+
+
+@pytest.mark.parametrize("P", [1, 2, 4])
+def test_sharded_solid_loopback(gpu_ctx, P):
+    """Multi-GPU correction data path on one GPU: P read slices -> shard_count /
+    shard_scatter at K=24 -> loopback all_to_all -> shard_solid per shard ->
+    gathered solid set -> precorrect_solid on every slice == monolithic
+    PreCorrect (bases, quals, counters); the union of shard solid sets is the
+    oracle's solid set."""
+    import torch
+
+    from allpathslg_amd import shard_bins
+
+    K = 24
+    reads = synth_reads(synth_genome(150_000, 61), 30_000, seed=62)
+    B = shard_bins(K, P)
+    parts = np.array_split(np.arange(reads.n_reads), P)
+    subs = [reads.subset(int(ix[0]), int(ix[-1]) + 1) for ix in parts]
+    dsubs = [gpu_ctx.upload(s) for s in subs]
+    sends, counts = [], []
+    for d in dsubs:
+        c = gpu_ctx.shard_count(d, K, P)
+        buf = torch.empty(max(int(c.sum()), 1), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.shard_scatter(d, K, P, buf.data_ptr())
+        sends.append(buf)
+        counts.append(c.reshape(P, B))
+    solids = []
+    for s in range(P):
+        pieces, rc = [], []
+        for p in range(P):
+            starts = np.concatenate([[0], np.cumsum(counts[p].reshape(-1))]).astype(np.int64)
+            pieces.append(sends[p][starts[s * B] : starts[(s + 1) * B]])
+            rc.append(counts[p][s])
+        recv = torch.cat(pieces) if sum(x.numel() for x in pieces) else torch.empty(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        n = gpu_ctx.shard_solid(recv.data_ptr(), np.concatenate(rc), K, P, 3)
+        out = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+        gpu_ctx.solid_export(out.data_ptr())
+        solids.append(out[:n])
+    solid = torch.cat(solids)
+    keys, cnt = oracle.kmer_count(reads, K)
+    assert np.array_equal(np.sort(solid.cpu().numpy().view(np.uint64)), keys[cnt >= 3])
+    exp, est = oracle.precorrect(reads, K=K)
+    tot = {"n_suspect": 0, "n_corrected": 0, "n_ambiguous": 0, "n_uncorrectable": 0}
+    fixed = []
+    for d in dsubs:
+        st = gpu_ctx.precorrect_solid(d, solid.data_ptr(), solid.numel(), K=K)
+        assert st["n_solid"] == est["n_solid"]
+        for k in tot:
+            tot[k] += st[k]
+        fixed.append(gpu_ctx.download(d))
+        d.free()
+    assert tot == {k: est[k] for k in tot}
+    assert np.array_equal(np.concatenate([f.packed[: int(f.byte_off[-1])] for f in fixed]),
+                          exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(np.concatenate([f.quals for f in fixed]), exp.quals)
+
+
+def test_copy_reads_restores(gpu_ctx):
+    reads = synth_reads(synth_genome(50_000, 71), 8000, seed=72)
+    src = gpu_ctx.upload(reads)
+    work = gpu_ctx.upload(reads)
+    exp, _ = oracle.precorrect(reads, K=24)
+    for _ in range(2):  # correct, restore, correct again: same result
+        gpu_ctx.copy_reads(work, src)
+        gpu_ctx.precorrect(work, K=24)
+        assert_same(gpu_ctx.download(work), exp)
+    assert_same(gpu_ctx.download(src), reads)
+    src.free()
+    work.free()
+
+
+def test_precorrect_long_and_boundary_reads(gpu_ctx):
+    """Reads around the wave kernel's 1024-base limit (longer ones take the
+    thread-per-read kernel) and K from 1 to 32 (1 or 2 lane rounds)."""
+    rng = np.random.default_rng(81)
+    g = synth_genome(30_000, 82)
+    seqs, quals = [], []
+    for L in [1023, 1024, 1025, 1500, 64, 65, 128, 2000] * 6 + list(rng.integers(20, 300, size=300)):
+        s = int(rng.integers(0, 30_000 - int(L)))
+        r = g[s : s + int(L)].copy()
+        q = np.full(int(L), 40, np.uint8)
+        flip = rng.random(int(L)) < 0.01
+        r[flip] = (r[flip] + 1 + rng.integers(0, 3, size=int(flip.sum()))) % 4
+        q[flip] = rng.integers(2, 20, size=int(flip.sum()))
+        low = rng.random(int(L)) < 0.01
+        q[low] = 10
+        seqs.append(r)
+        quals.append(q)
+    reads = ReadSet.from_sequences(seqs, quals)
+    for K in (1, 12, 21, 22, 24, 32):
+        got, st = gpu_ctx.precorrect(reads, K=K, min_solid=2)
+        exp, est = oracle.precorrect(reads, K=K, min_solid=2)
+        assert_same(got, exp)
+        assert st == {**st, **est}
