@@ -205,7 +205,7 @@ SIGNATURES = {
     ),
     "apg_unipath_graph_free": (None, [C.POINTER(apg_unipath_graph)]),
     "apg_ushard_bins": (C.c_int, [C.c_int]),
-    "apg_ushard_count": (C.c_int, [_P, _P, C.c_int, C.c_int, _u64p]),
+    "apg_ushard_count": (C.c_int, [_P, _P, C.c_int, C.c_int, _u64p, _u64p]),
     "apg_ushard_scatter": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_void_p]),
     "apg_ushard_nodes": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, _u64p]),
     "apg_ushard_export": (C.c_int, [_P, C.c_void_p]),

@@ -110,6 +110,8 @@ struct apg_ctx {
     int K = 0;
     uint32_t G = 0;
     uint64_t n = 0;        // instances extracted
+    uint64_t n_local = 0;  // distinct local nodes of the last apg_ushard_count
+    bool local_ready = false;  // "u_nodes" holds those local nodes
     uint64_t n_nodes = 0;  // nodes of the last apg_ushard_nodes
     uint64_t n_recv = 0;
   } ustate;
@@ -120,6 +122,18 @@ struct apg_ctx {
 };
 
 namespace apg {
+
+// The large record buffers are shared by name across modules, so a context
+// holds max(module sizes) instead of their sum (spectrum: 8-byte records,
+// unipaths: 32-byte records).  Nothing in them outlives the call that fills
+// them, except a CountResult, which is consumed before the next module runs:
+//   kBig0: spectrum stage-A records / count ping-pong B; unipath extraction /
+//          partition ping-pong B
+//   kBig1: spectrum / unipath partition ping-pong A
+//   kBig2: spectrum table-mode counts
+constexpr const char* kBig0 = "big0";
+constexpr const char* kBig1 = "big1";
+constexpr const char* kBig2 = "big2";
 
 // Grid of a grid-stride kernel over n items, `per` items per block, capped at
 // 16 blocks per CU.

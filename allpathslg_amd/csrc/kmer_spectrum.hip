@@ -600,11 +600,11 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
       }
   }
   uint64_t *bufA = nullptr, *bufB = nullptr;
-  APG_TRY(workspace_t(ctx, "c_recA", std::max<uint64_t>(n, 1), &bufA));
+  APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1), &bufA));
   if (spare) {
     bufB = spare;
   } else {
-    APG_TRY(workspace_t(ctx, "c_recB", std::max<uint64_t>(n, 1), &bufB));
+    APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &bufB));
   }
   uint64_t nb = B1;
   uint64_t* boff = nullptr;
@@ -639,7 +639,7 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   uint32_t *tab_cnt = nullptr, *bucket_nd = nullptr, *ovf_list = nullptr;
   unsigned long long *ghist = nullptr, *gstats = nullptr;
   const uint64_t hl = std::max<uint64_t>(hist_len, 2);
-  APG_TRY(workspace_t(ctx, "c_tabcnt", table ? std::max<uint64_t>(n, 1) : 1, &tab_cnt));
+  APG_TRY(workspace_t(ctx, kBig2, table ? std::max<uint64_t>(n, 1) : 1, &tab_cnt));
   APG_TRY(workspace_t(ctx, "c_bnd", nb, &bucket_nd));
   APG_TRY(workspace_t(ctx, "c_ovf", nb, &ovf_list));
   APG_TRY(workspace_t(ctx, "c_hist", hl, &ghist));
@@ -670,12 +670,12 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
     // Oversized buckets: radix sort in global scratch (the ping-pong buffer not
     // holding rec is free now).
     uint64_t* scratch = other;
-    if (scratch == nullptr || scratch == rec) APG_TRY(workspace_t(ctx, "c_recB", std::max<uint64_t>(n, 1), &scratch));
+    if (scratch == nullptr || scratch == rec) APG_TRY(workspace_t(ctx, "c_scratch", std::max<uint64_t>(n, 1), &scratch));
     uint32_t* heads = nullptr;
     APG_TRY(workspace_t(ctx, "c_heads", std::max<uint64_t>(n, 1), &heads));
     uint32_t* tcnt_full = tab_cnt;
     if (!table) {
-      APG_TRY(workspace_t(ctx, "c_tabcnt", std::max<uint64_t>(n, 1), &tcnt_full));
+      APG_TRY(workspace_t(ctx, kBig2, std::max<uint64_t>(n, 1), &tcnt_full));
       co.tab_cnt = tcnt_full;
     }
     vlog(ctx, "count: %llu oversized buckets -> global radix path", hs[1]);
@@ -723,7 +723,7 @@ int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_
   std::vector<uint64_t> counts;
   APG_TRY(extract_count(ctx, dr, K, 1, &counts));
   uint64_t* buf = nullptr;
-  APG_TRY(workspace_t(ctx, "x_records", std::max<uint64_t>(ctx->xstate.total, 1), &buf));
+  APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(ctx->xstate.total, 1), &buf));
   APG_TRY(extract_scatter(ctx, dr, K, 1, buf));
   return stage_count(ctx, buf, buf, counts, K, 1, table, hist, hist_len, res);
 }

@@ -1,6 +1,6 @@
 // partition.hip — the device-wide scan and the LDS-staged hash-partition
-// level shared by the k-mer spectrum (8-byte records) and the unipath
-// builder (32-byte KRec records).  See partition.hpp.
+// level of the k-mer counting pipeline (8-byte records; the level is a
+// template over the record type).  See partition.hpp.
 #include <algorithm>
 #include <string>
 #include <vector>
@@ -292,7 +292,5 @@ int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector
 
 template int part_level<uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&, int, int,
                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
-template int part_level<KRec>(apg_ctx*, const KRec*, KRec*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
-                              uint64_t*, std::vector<uint64_t>*, const char*);
 
 }  // namespace apg

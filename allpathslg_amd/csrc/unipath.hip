@@ -7,13 +7,14 @@
 // and restated on the CPU in oracle/unipath_oracle.cpp.
 //
 // Pipeline (U = unipath stage):
-//   U1 uext_count / uext_scatter  one thread per read rolls the 192-bit fw/rc
-//      K-mer, emits a 32-byte KRec {canonical key, hash56 | ext bits} into 32
-//      hash groups through an LDS-staged round (1024 records / round)
-//   U2 part_level<KRec>            LDS-staged hash-partition levels
-//   U3 ugroup                      per bucket: LDS owner table, full-key
-//      compare, OR of extension bits -> distinct nodes (sparse, in place)
-//   U4 ucompact + node_insert      dense node array + open-addressing index
+//   U1 uhll                        sizing pass: one thread per read rolls the
+//      192-bit fw/rc K-mer; instance count + HyperLogLog distinct estimate
+//   U2 uinsert_reads               every instance {canonical key, hash56 |
+//      extension bits} goes into a global open-addressing node table (claim
+//      by CAS on a tag, full-key compare, OR of new extension bits)
+//   U3 tab_count / tab_scatter     table -> dense node array grouped by the
+//      top 5 hash bits (the shard order of the multi-GPU exchange)
+//   U4 node_insert                 open-addressing index of the node array
 //   U5 links                       unique successor/predecessor per directed
 //      node (v = 2*node + orientation)
 //   U6 ranking                     sparse ruling set: heads + every 32nd node
@@ -100,33 +101,39 @@ __device__ __forceinline__ uint64_t rev2(uint64_t x) {  // reverse the 32 2-bit 
   return __builtin_bswap64(x);
 }
 
+// x >> s for a 192-bit (a:b:c) value, 0 <= s <= 192
+__device__ __forceinline__ K3 shr192(const K3& x, int s) {
+  if (s == 0) return x;
+  if (s >= 192) return K3{0, 0, 0};
+  if (s < 64) return K3{x.a >> s, (x.b >> s) | (x.a << (64 - s)), (x.c >> s) | (x.b << (64 - s))};
+  if (s == 64) return K3{0, x.a, x.b};
+  if (s < 128) return K3{0, x.a >> (s - 64), (x.b >> (s - 64)) | (x.a << (128 - s))};
+  if (s == 128) return K3{0, 0, x.a};
+  return K3{0, 0, x.a >> (s - 128)};
+}
+
 __device__ __forceinline__ K3 revcomp(const K3& k, const KeyP& p) {
   // complement + reverse all 96 2-bit groups, then right-align the 2K bits
-  uint64_t a = rev2(~k.c), b = rev2(~k.b), c = rev2(~k.a);
-  const int s = 192 - 2 * p.K;  // 0 <= s < 192
-  K3 r;
-  if (s == 0) {
-    r = {a, b, c};
-  } else if (s < 64) {
-    r.c = (c >> s) | (b << (64 - s));
-    r.b = (b >> s) | (a << (64 - s));
-    r.a = a >> s;
-  } else if (s == 64) {
-    r = {0, a, b};
-  } else if (s < 128) {
-    const int t = s - 64;
-    r.c = (b >> t) | (a << (64 - t));
-    r.b = a >> t;
-    r.a = 0;
-  } else if (s == 128) {
-    r = {0, 0, a};
-  } else {
-    r = {0, 0, a >> (s - 128)};
-  }
+  K3 r = shr192(K3{rev2(~k.c), rev2(~k.b), rev2(~k.a)}, 192 - 2 * p.K);
   r.a &= p.ma;
   r.b &= p.mb;
   r.c &= p.mc;
   return r;
+}
+
+// The 96 bases [j, j+96) of a 2-bit LSB-first packed read as a 192-bit
+// LSB-first value (base j in the low bits of .c).  Reads up to 28 bytes from
+// the 4-byte-aligned word holding base j (device read buffers carry slack).
+__device__ __forceinline__ K3 load_lsb192(const uint8_t* rd, uint32_t j) {
+  const uintptr_t addr = (uintptr_t)(rd + (j >> 2));
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  const int sh = (int)(addr & 3) * 8 + 2 * (int)(j & 3);  // < 32
+  const uint64_t q0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  const uint64_t q1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  const uint64_t q2 = (uint64_t)w[4] | ((uint64_t)w[5] << 32);
+  const uint64_t q3 = (uint64_t)w[6];
+  if (sh == 0) return K3{q2, q1, q0};
+  return K3{(q2 >> sh) | (q3 << (64 - sh)), (q1 >> sh) | (q2 << (64 - sh)), (q0 >> sh) | (q1 << (64 - sh))};
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
@@ -185,11 +192,29 @@ struct Roller3 {
   __device__ __forceinline__ void init(const uint8_t* r, uint32_t n, const KeyP& p) {
     rd = r;
     len = n;
+    if (n >= (uint32_t)p.K) {
+      prime(0, p);
+      return;
+    }
     i = 0;
     fw = K3{0, 0, 0};
     rc = K3{0, 0, 0};
-    const uint32_t prime = n < (uint32_t)(p.K - 1) ? n : (uint32_t)(p.K - 1);
-    for (uint32_t j = 0; j < prime; ++j) step(p);
+    const uint32_t m = n < (uint32_t)(p.K - 1) ? n : (uint32_t)(p.K - 1);
+    for (uint32_t j = 0; j < m; ++j) step(p);
+  }
+  // State after stepping through the K-1 bases [j, j+K-1) (needs j+K-1 <=
+  // len), built from packed words instead of K-1 single-base steps:
+  //   fw = those bases MSB-first;  rc = complement of them LSB-first, << 2.
+  __device__ __forceinline__ void prime(uint32_t j, const KeyP& p) {
+    const int bits = 2 * (p.K - 1);
+    const K3 W = load_lsb192(rd, j);
+    const uint64_t mc = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+    const uint64_t mb = bits >= 128 ? ~0ull : bits <= 64 ? 0 : ((1ull << (bits - 64)) - 1);
+    const uint64_t ma = bits <= 128 ? 0 : ((1ull << (bits - 128)) - 1);  // bits <= 190
+    fw = shr192(K3{rev2(W.c), rev2(W.b), rev2(W.a)}, 192 - bits);
+    const K3 R{(W.a ^ ~0ull) & ma, (W.b ^ ~0ull) & mb, (W.c ^ ~0ull) & mc};
+    rc = K3{((R.a << 2) | (R.b >> 62)) & p.ma, ((R.b << 2) | (R.c >> 62)) & p.mb, (R.c << 2) & p.mc};
+    i = j + (uint32_t)(p.K - 1);
   }
   __device__ __forceinline__ void step(const KeyP& p) {
     const uint64_t b = read_base(rd, i);
@@ -199,12 +224,7 @@ struct Roller3 {
   }
   __device__ __forceinline__ bool more() const { return i < len; }
   // reposition so that the next step() completes the K-mer starting at base j
-  __device__ __forceinline__ void seek(uint32_t j, const KeyP& p) {
-    i = j;
-    fw = K3{0, 0, 0};
-    rc = K3{0, 0, 0};
-    for (int t = 0; t < p.K - 1; ++t) step(p);
-  }
+  __device__ __forceinline__ void seek(uint32_t j, const KeyP& p) { prime(j, p); }
   // next K-mer instance as a KRec
   __device__ __forceinline__ KRec next(const KeyP& p) {
     step(p);
@@ -219,90 +239,245 @@ struct Roller3 {
 };
 
 // ---------------------------------------------------------------------------
-// U1: extraction into 2^D hash groups (count matrix [digit][block])
+// U1-U3: distinct nodes through one global open-addressing table.
+//
+// Every K-mer instance (rolled from the reads, or a received record) is
+// inserted into a table of 64-byte slots {tag, key, hash56 | OR of extension
+// bits}; tag 0 = empty, hash56 | 1 = being written, hash56 | 2 = published.
+// An instance probes from mulhi(hash, T), loading tag and key of a slot in
+// one round trip: an empty slot is claimed by CAS on the tag, the key
+// written with coherent stores and the tag published; a published slot with
+// the same hash and key gets the instance's extension bits OR-ed in (only
+// when new).  All table traffic uses agent-scope (cross-XCD coherent)
+// accesses, no cache-maintenance fences.  With coverage c the table sees c
+// reads per write, so the 1.7 G x 32-byte instances of the bench never touch
+// HBM as records: only the reads (0.9 GB) and one slot line per probe move.
+// The probe loop is wave-uniform (one probe per pending lane per trip) so a
+// lane waiting on a slot another lane of its own wave is writing never
+// blocks that writer.  A distinct-count estimate (HyperLogLog over the same
+// hash, taken in the sizing pass) sets T ~ 2x distinct; a probe run longer
+// than kMaxProbe marks overflow and the host rebuilds with 2T.
 // ---------------------------------------------------------------------------
 constexpr int kUThreads = 256;
-constexpr int kUItems = 4;  // KRec per thread per round: 1024 records = 32 KiB
-constexpr int kUDigitBits = 5;
-constexpr int kUMaxBlocks = 2048;
+constexpr int kUDigitBits = 5;  // node groups (top hash bits): shard-major order for the exchange
+constexpr int kHllBits = 12;    // 4096 HyperLogLog registers
+constexpr uint32_t kMaxProbe = 1u << 14;
 
-__device__ __forceinline__ void read_range(uint64_t n, uint32_t G, uint32_t b, uint64_t* r0, uint64_t* r1) {
-  *r0 = (n * b) / G;
-  *r1 = (n * (b + 1)) / G;
+// One table slot per 64-byte line: a probe's tag and key share one HBM access.
+struct __attribute__((aligned(64))) USlot {
+  uint64_t k0, k1, k2, meta;
+  unsigned long long tag;  // 0 empty, hash56 | 1 being written, hash56 | 2 published
+  uint64_t pad[3];
+};
+
+struct UTab {
+  USlot* slot;
+  uint64_t T;
+  unsigned long long* ovf;
+};
+
+__device__ __forceinline__ uint64_t tab_home(uint64_t h, uint64_t T) { return __umul64hi(h, T); }
+
+// Table words are read and written with agent-scope (cross-XCD coherent)
+// loads/stores instead of cache-invalidating acquire/release fences: a slot's
+// key is written once, before its tag is published, and never changes.
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return (uint64_t)ld_agent(reinterpret_cast<const unsigned long long*>(p));
+}
+__device__ __forceinline__ void st_agent64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void __launch_bounds__(kUThreads) k_uext_count(ReadsV rv, KeyP kp, uint32_t* __restrict__ cmat) {
-  __shared__ uint32_t hist[1 << kUDigitBits];
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  if (threadIdx.x < (1 << kUDigitBits)) hist[threadIdx.x] = 0;
+// One probe step of a pending instance (key k, hash h with low byte 0,
+// extension bits e) at slot *s.  Returns true when the instance is settled.
+//
+// Fast path: one plain (L2-cacheable, wide) read of the slot line.  A
+// published slot never changes key, so a line cached after the publish is
+// exact; a line cached before it shows the tag as empty or busy, which sends
+// the probe down the coherent path (CAS / agent-scope re-read).  `coh` makes
+// the next probe of a busy slot coherent, so a stale "busy" cannot loop.
+__device__ __forceinline__ bool tab_probe(const UTab& t, const K3& k, uint64_t h, uint32_t e, uint64_t* s,
+                                          uint32_t* probes, bool* coh) {
+  USlot* sl = t.slot + *s;
+  unsigned long long cur;
+  uint64_t a, b, c, m;
+  if (*coh) {
+    cur = ld_agent(&sl->tag);
+    a = ld_agent64(&sl->k0);
+    b = ld_agent64(&sl->k1);
+    c = ld_agent64(&sl->k2);
+    m = ld_agent64(&sl->meta);
+  } else {
+    const USlot x = *sl;
+    cur = x.tag;
+    a = x.k0;
+    b = x.k1;
+    c = x.k2;
+    m = x.meta;
+  }
+  if (cur == 0) {
+    const unsigned long long prev = atomicCAS(&sl->tag, 0ull, (unsigned long long)(h | 1));
+    if (prev == 0) {
+      st_agent64(&sl->k0, k.a);
+      st_agent64(&sl->k1, k.b);
+      st_agent64(&sl->k2, k.c);
+      st_agent64(&sl->meta, h | e);
+      // the four coherent stores complete before the tag is published
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_store(&sl->tag, (unsigned long long)(h | 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    cur = prev;  // coherent: the key is re-read below if it must be compared
+    a = b = c = ~0ull;
+  }
+  if ((cur & ~0xffull) == h) {
+    if ((cur & 0xff) == 1) {  // being written: look again next trip, coherently
+      *coh = true;
+      return false;
+    }
+    if (!((a == k.a) & (b == k.b) & (c == k.c))) {  // stale line or a true hash collision: re-read
+      a = ld_agent64(&sl->k0);
+      b = ld_agent64(&sl->k1);
+      c = ld_agent64(&sl->k2);
+      m = ld_agent64(&sl->meta);
+    }
+    if ((a == k.a) & (b == k.b) & (c == k.c)) {
+      if (e & ~(uint32_t)m & 0xff) atomicOr(reinterpret_cast<unsigned long long*>(&sl->meta), (unsigned long long)e);
+      return true;
+    }
+  }
+  *coh = false;
+  *s = *s + 1 == t.T ? 0 : *s + 1;
+  if (++*probes > kMaxProbe) {
+    atomicOr(t.ovf, 1ull);
+    return true;  // dropped: the host rebuilds with a larger table
+  }
+  return false;
+}
+
+// Sizing pass: instance count and HyperLogLog registers of the key hashes.
+__global__ void __launch_bounds__(kUThreads) k_uhll(ReadsV rv, KeyP kp, uint32_t* __restrict__ hll,
+                                                   unsigned long long* __restrict__ n_inst) {
+  __shared__ uint32_t reg[1 << kHllBits];
+  for (uint32_t i = threadIdx.x; i < (1u << kHllBits); i += blockDim.x) reg[i] = 0;
   __syncthreads();
-  uint64_t r0, r1;
-  read_range(rv.n_reads, G, b, &r0, &r1);
-  for (uint64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
+  unsigned long long cnt = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
     if (len < (uint32_t)kp.K) continue;
     Roller3 ro;
     ro.init(rv.packed + rv.byte_off[r], len, kp);
     while (ro.more()) {
-      const KRec x = ro.next(kp);
-      atomicAdd(&hist[x.meta >> (64 - kUDigitBits)], 1u);
+      const uint64_t h = ro.next(kp).meta & ~0xffull;
+      const uint32_t j = (uint32_t)(h >> (64 - kHllBits));
+      const uint32_t rho = (uint32_t)__clzll((long long)((h << kHllBits) | (1ull << (kHllBits + 7)))) + 1;
+      atomicMax(&reg[j], rho);
+      ++cnt;
     }
   }
+  wave_add(n_inst, cnt);
   __syncthreads();
-  if (threadIdx.x < (1 << kUDigitBits)) cmat[(uint64_t)threadIdx.x * G + b] = hist[threadIdx.x];
+  for (uint32_t i = threadIdx.x; i < (1u << kHllBits); i += blockDim.x)
+    if (reg[i]) atomicMax(&hll[i], reg[i]);
 }
 
-__global__ void __launch_bounds__(kUThreads) k_uext_scatter(ReadsV rv, KeyP kp, const uint64_t* __restrict__ omat,
-                                                            KRec* __restrict__ out) {
-  constexpr uint32_t ndig = 1u << kUDigitBits;
-  __shared__ KRec stage[kUThreads * kUItems];
-  __shared__ unsigned long long cur[ndig];
-  __shared__ uint32_t lcnt[256], lstart[256];
-  __shared__ uint32_t scan_sm[64];
-  const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
-  if (tid < ndig) cur[tid] = omat[(uint64_t)tid * G + b];
-  uint64_t r0, r1;
-  read_range(rv.n_reads, G, b, &r0, &r1);
-  for (uint64_t rb = r0; rb < r1; rb += kUThreads) {
-    const uint64_t r = rb + tid;
-    Roller3 ro;
-    ro.i = 0;
-    ro.len = 0;
-    if (r < r1) {
-      const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
-      if (len >= (uint32_t)kp.K) ro.init(rv.packed + rv.byte_off[r], len, kp);
-    }
-    while (__syncthreads_or(ro.more())) {
-      lcnt[tid] = 0;
-      __syncthreads();
-      KRec v[kUItems];
-      uint32_t pos[kUItems];
-      uint32_t nv = 0;
-#pragma unroll
-      for (int j = 0; j < kUItems; ++j) {
-        if (ro.more()) {
-          v[j] = ro.next(kp);
-          pos[j] = atomicAdd(&lcnt[v[j].meta >> (64 - kUDigitBits)], 1u);
-          nv = j + 1;
+// Insert every K-mer instance of the reads.
+__global__ void __launch_bounds__(kUThreads) k_uinsert_reads(ReadsV rv, KeyP kp, UTab t) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  Roller3 ro;
+  ro.i = ro.len = 0;
+  bool started = false, pend = false, live = true;
+  K3 k{0, 0, 0};
+  uint64_t h = 0, s = 0;
+  uint32_t e = 0, probes = 0;
+  bool coh = false;
+  for (;;) {
+    while (!pend && live) {  // per lane: next instance, or next read
+      if (started && ro.more()) {
+        const KRec x = ro.next(kp);
+        k = rec_key(x);
+        h = x.meta & ~0xffull;
+        e = (uint32_t)(x.meta & 0xff);
+        s = tab_home(h, t.T);
+        probes = 0;
+        coh = false;
+        pend = true;
+      } else {
+        if (started) r += stride;
+        started = true;
+        if (r >= rv.n_reads) {
+          live = false;
+        } else {
+          const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+          ro.i = ro.len = 0;
+          if (len >= (uint32_t)kp.K) ro.init(rv.packed + rv.byte_off[r], len, kp);
         }
       }
-      __syncthreads();
-      uint32_t tot;
-      const uint32_t ex = block_exclusive_scan<uint32_t>(lcnt[tid], scan_sm, &tot);
-      lstart[tid] = ex;
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kUItems; ++j)
-        if ((uint32_t)j < nv) stage[lstart[v[j].meta >> (64 - kUDigitBits)] + pos[j]] = v[j];
-      __syncthreads();
-      for (uint32_t i = tid; i < tot; i += kUThreads) {
-        const KRec x = stage[i];
-        const uint32_t d = (uint32_t)(x.meta >> (64 - kUDigitBits));
-        out[cur[d] + (i - lstart[d])] = x;
-      }
-      __syncthreads();
-      if (tid < ndig) cur[tid] += lcnt[tid];
     }
+    if (!__ballot(pend)) break;
+    if (pend && tab_probe(t, k, h, e, &s, &probes, &coh)) pend = false;
+  }
+}
+
+// Insert records (32-byte KRec with extension bits), e.g. received nodes.
+__global__ void __launch_bounds__(kUThreads) k_uinsert_recs(const KRec* __restrict__ rec, uint64_t n, UTab t) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool pend = false;
+  K3 k{0, 0, 0};
+  uint64_t h = 0, s = 0;
+  uint32_t e = 0, probes = 0;
+  bool coh = false;
+  for (;;) {
+    if (!pend && i < n) {
+      const KRec x = rec[i];
+      i += stride;
+      k = rec_key(x);
+      h = x.meta & ~0xffull;
+      e = (uint32_t)(x.meta & 0xff);
+      s = tab_home(h, t.T);
+      probes = 0;
+      coh = false;
+      pend = true;
+    }
+    if (!__ballot(pend)) break;
+    if (pend && tab_probe(t, k, h, e, &s, &probes, &coh)) pend = false;
+  }
+}
+
+// Compaction: published slots grouped by the top kUDigitBits hash bits.
+// Pass 1 counts per (digit, block) into cmat[digit * G + block].
+__global__ void __launch_bounds__(kUThreads) k_tab_count(const USlot* __restrict__ slot, uint64_t T,
+                                                        uint32_t* __restrict__ cmat) {
+  __shared__ uint32_t hist[1 << kUDigitBits];
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  if (threadIdx.x < (1u << kUDigitBits)) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t s0 = T * b / G, s1 = T * (b + 1) / G;
+  for (uint64_t s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
+    const unsigned long long x = slot[s].tag;
+    if (x) atomicAdd(&hist[x >> (64 - kUDigitBits)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < (1u << kUDigitBits)) cmat[(uint64_t)threadIdx.x * G + b] = hist[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kUThreads) k_tab_scatter(const USlot* __restrict__ slot, uint64_t T,
+                                                          const uint64_t* __restrict__ omat, KRec* __restrict__ out) {
+  __shared__ unsigned long long cur[1 << kUDigitBits];
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  if (threadIdx.x < (1u << kUDigitBits)) cur[threadIdx.x] = omat[(uint64_t)threadIdx.x * G + b];
+  __syncthreads();
+  const uint64_t s0 = T * b / G, s1 = T * (b + 1) / G;
+  for (uint64_t s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
+    const USlot& x = slot[s];
+    if (x.tag) out[atomicAdd(&cur[x.tag >> (64 - kUDigitBits)], 1ull)] = KRec{x.k0, x.k1, x.k2, x.meta};
   }
 }
 
@@ -310,184 +485,6 @@ __global__ void k_digit_starts_u(const uint64_t* __restrict__ omat, uint32_t ndi
                                  uint64_t* __restrict__ ds) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d <= ndig) ds[d] = omat[(uint64_t)d * G];
-}
-
-// ---------------------------------------------------------------------------
-// U3: per-bucket grouping of instances into distinct nodes
-// ---------------------------------------------------------------------------
-constexpr int kGThreads = 256;
-constexpr uint32_t kGCap = 1023;   // records of an LDS-resident bucket
-constexpr uint32_t kGTab = 1024;   // LDS owner-table slots (> kGCap)
-
-struct GroupOut {
-  KRec* nodes;             // sparse: bucket b's distinct nodes at boff[b] + i
-  uint32_t* ncnt;          // parallel counts
-  uint32_t* bucket_nd;
-  unsigned long long* gstats;  // [0] distinct, [1] overflow buckets, [2] max bucket
-  uint32_t* ovf_list;
-};
-
-// Small buckets: records and owner table in LDS.
-__global__ void __launch_bounds__(kGThreads) k_ugroup(const KRec* __restrict__ rec, const uint64_t* __restrict__ boff,
-                                                     uint64_t nbuckets, GroupOut o) {
-  __shared__ KRec R[kGCap];
-  __shared__ uint32_t tab[kGTab];
-  __shared__ uint32_t rep[kGCap];
-  __shared__ uint32_t ext[kGCap];
-  __shared__ uint32_t cnt[kGCap];
-  __shared__ uint32_t scan_sm[64];
-  const uint32_t tid = threadIdx.x;
-  unsigned long long nd_sum = 0, maxb = 0;
-  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
-    const uint64_t off = boff[bkt];
-    const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
-    if (n > maxb) maxb = n;
-    if (n > kGCap) {
-      if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
-      continue;
-    }
-    if (n == 0) {
-      if (tid == 0) o.bucket_nd[bkt] = 0;
-      continue;
-    }
-    uint32_t T = 64;
-    while (T <= n) T <<= 1;
-    for (uint32_t s = tid; s < T; s += kGThreads) tab[s] = kNone;
-    for (uint32_t i = tid; i < n; i += kGThreads) {
-      R[i] = rec[off + i];
-      ext[i] = 0;
-      cnt[i] = 0;
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += kGThreads) {
-      const K3 k = rec_key(R[i]);
-      uint32_t s = (uint32_t)(R[i].meta >> 8) & (T - 1);
-      for (;;) {
-        const uint32_t ow = atomicCAS(&tab[s], kNone, i);
-        if (ow == kNone) {
-          rep[i] = i;
-          break;
-        }
-        if (k3_eq(rec_key(R[ow]), k)) {
-          rep[i] = ow;
-          break;
-        }
-        s = (s + 1) & (T - 1);
-      }
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += kGThreads) {
-      atomicOr(&ext[rep[i]], (uint32_t)(R[i].meta & 0xff));
-      atomicAdd(&cnt[rep[i]], 1u);
-    }
-    __syncthreads();
-    // compact representatives in index order
-    const uint32_t ipt = (n + kGThreads - 1) / kGThreads;
-    const uint32_t i0 = min(n, tid * ipt), i1 = min(n, i0 + ipt);
-    uint32_t c = 0;
-    for (uint32_t i = i0; i < i1; ++i) c += rep[i] == i;
-    uint32_t d;
-    uint32_t j = block_exclusive_scan<uint32_t>(c, scan_sm, &d);
-    for (uint32_t i = i0; i < i1; ++i) {
-      if (rep[i] != i) continue;
-      KRec x = R[i];
-      x.meta = (x.meta & ~0xffull) | ext[i];
-      o.nodes[off + j] = x;
-      o.ncnt[off + j] = cnt[i];
-      ++j;
-    }
-    if (tid == 0) {
-      o.bucket_nd[bkt] = d;
-      nd_sum += d;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    atomicAdd(&o.gstats[0], nd_sum);
-    atomicMax(&o.gstats[2], maxb);
-  }
-}
-
-// Oversized buckets: one workgroup each, owner table and per-record scratch
-// in global memory (scratch regions parallel to the bucket's records).
-__global__ void __launch_bounds__(kGThreads) k_ugroup_big(const KRec* __restrict__ rec,
-                                                         const uint64_t* __restrict__ boff, uint32_t* __restrict__ gtab,
-                                                         uint32_t* __restrict__ grep, uint32_t* __restrict__ gext,
-                                                         uint32_t* __restrict__ gcnt, GroupOut o) {
-  __shared__ uint32_t scan_sm[64];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t bkt = o.ovf_list[blockIdx.x];
-  const uint64_t off = boff[bkt];
-  const uint32_t n = (uint32_t)(boff[bkt + 1] - off);
-  uint32_t T = 64;
-  while (T <= n) T <<= 1;  // T <= 2n: table lives in gtab[2*off ...]
-  uint32_t* tab = gtab + 2 * off;
-  uint32_t* rep = grep + off;
-  uint32_t* ext = gext + off;
-  uint32_t* cnt = gcnt + off;
-  for (uint32_t s = tid; s < T; s += kGThreads) tab[s] = kNone;
-  for (uint32_t i = tid; i < n; i += kGThreads) {
-    ext[i] = 0;
-    cnt[i] = 0;
-  }
-  __syncthreads();
-  for (uint32_t i = tid; i < n; i += kGThreads) {
-    const K3 k = rec_key(rec[off + i]);
-    uint32_t s = (uint32_t)(rec[off + i].meta >> 8) & (T - 1);
-    for (;;) {
-      const uint32_t ow = atomicCAS(&tab[s], kNone, i);
-      if (ow == kNone) {
-        rep[i] = i;
-        break;
-      }
-      if (k3_eq(rec_key(rec[off + ow]), k)) {
-        rep[i] = ow;
-        break;
-      }
-      s = (s + 1) & (T - 1);
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = tid; i < n; i += kGThreads) {
-    atomicOr(&ext[rep[i]], (uint32_t)(rec[off + i].meta & 0xff));
-    atomicAdd(&cnt[rep[i]], 1u);
-  }
-  __syncthreads();
-  const uint32_t ipt = (n + kGThreads - 1) / kGThreads;
-  const uint32_t i0 = min(n, tid * ipt), i1 = min(n, i0 + ipt);
-  uint32_t c = 0;
-  for (uint32_t i = i0; i < i1; ++i) c += rep[i] == i;
-  uint32_t d;
-  uint32_t j = block_exclusive_scan<uint32_t>(c, scan_sm, &d);
-  for (uint32_t i = i0; i < i1; ++i) {
-    if (rep[i] != i) continue;
-    KRec x = rec[off + i];
-    x.meta = (x.meta & ~0xffull) | ext[i];
-    o.nodes[off + j] = x;
-    o.ncnt[off + j] = cnt[i];
-    ++j;
-  }
-  if (tid == 0) {
-    o.bucket_nd[bkt] = d;
-    atomicAdd(&o.gstats[0], (unsigned long long)d);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// U4: dense nodes + index
-// ---------------------------------------------------------------------------
-__global__ void k_ucompact(const KRec* __restrict__ sp, const uint32_t* __restrict__ spc,
-                           const uint64_t* __restrict__ boff, const uint32_t* __restrict__ bucket_nd,
-                           const uint64_t* __restrict__ nbase, uint64_t nbuckets, KRec* __restrict__ nodes,
-                           uint32_t* __restrict__ ncnt) {
-  for (uint64_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
-    const uint64_t s = boff[b], d = nbase[b];
-    const uint32_t nd = bucket_nd[b];
-    for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) {
-      nodes[d + i] = sp[s + i];
-      ncnt[d + i] = spc[s + i];
-    }
-  }
 }
 
 __global__ void k_node_insert(const KRec* __restrict__ nodes, uint64_t N, uint32_t* __restrict__ idx, uint64_t tmask) {
@@ -1143,7 +1140,6 @@ static int ceil_log2_u(uint64_t x) {
   return b;
 }
 
-constexpr uint64_t kUBucketTarget = 640;
 
 template <typename T>
 static T* host_dup(const T* d, uint64_t n, apg_ctx* ctx, int* rc) {
@@ -1167,126 +1163,108 @@ static int d2h_u64(apg_ctx* ctx, const unsigned long long* d, unsigned long long
   return sync(ctx);
 }
 
-// U1 count: per-digit instance counts (2^kUDigitBits digits, host) and the
-// scanned [digit][block] matrix left in workspace "u_omat" for u_extract_scatter.
-static int u_extract_count(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, std::vector<uint64_t>* counts,
-                           uint32_t* Gout) {
+// HyperLogLog estimate of the distinct count from 2^kHllBits registers.
+static double hll_estimate(const std::vector<uint32_t>& reg) {
+  const double m = (double)reg.size();
+  double sum = 0;
+  uint64_t zeros = 0;
+  for (uint32_t r : reg) {
+    sum += std::ldexp(1.0, -(int)r);
+    zeros += r == 0;
+  }
+  const double alpha = 0.7213 / (1.0 + 1.079 / m);
+  double e = alpha * m * m / sum;
+  if (e <= 2.5 * m && zeros) e = m * std::log(m / (double)zeros);
+  return e;
+}
+
+// Sizing pass over reads: instance count and distinct estimate.
+static int u_size(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, uint64_t* n_inst, double* est) {
   ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  uint32_t* hll = nullptr;
+  unsigned long long* cnt = nullptr;
+  APG_TRY(workspace_t(ctx, "u_hll", 1u << kHllBits, &hll));
+  APG_TRY(workspace_t(ctx, "u_ninst", 1, &cnt));
+  APG_CHECK_HIP(hipMemsetAsync(hll, 0, (1u << kHllBits) * 4, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(cnt, 0, 8, ctx->stream));
+  kbegin(ctx, "u_size", dr->n_bytes + 16 * dr->n_reads);
+  if (dr->n_reads) k_uhll<<<grid_for(ctx, dr->n_reads), kUThreads, 0, ctx->stream>>>(rv, kp, hll, cnt);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  std::vector<uint32_t> reg(1u << kHllBits);
+  unsigned long long n = 0;
+  APG_CHECK_HIP(hipMemcpyAsync(reg.data(), hll, reg.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&n, cnt, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  *n_inst = n;
+  *est = n ? std::min<double>((double)n, hll_estimate(reg)) : 0.0;
+  return APG_OK;
+}
+
+// Distinct nodes of reads (dr) or of records (rec, n_rec) into workspace
+// "u_nodes", grouped by the top kUDigitBits hash bits; digit_counts (may be
+// null) receives the per-group node counts.
+static int u_build_nodes(apg_ctx* ctx, const apg_dreads* dr, const KRec* rec, uint64_t n_rec, const KeyP& kp,
+                         double est, KRec** nodes_out, uint64_t* N_out, std::vector<uint64_t>* digit_counts) {
   const uint32_t ndig = 1u << kUDigitBits;
-  const uint32_t G =
-      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUMaxBlocks, (dr->n_reads + 255) / 256));
+  uint64_t T = std::max<uint64_t>(4096, (uint64_t)(2.0 * est * 1.05) + 1);
+  UTab t{};
+  unsigned long long* ovf = nullptr;
+  APG_TRY(workspace_t(ctx, "u_tabovf", 1, &ovf));
+  for (int attempt = 0;; ++attempt) {
+    APG_TRY(workspace_t(ctx, "u_tabslot", T, &t.slot));
+    t.T = T;
+    t.ovf = ovf;
+    APG_CHECK_HIP(hipMemsetAsync(t.slot, 0, T * sizeof(USlot), ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(ovf, 0, 8, ctx->stream));
+    if (dr) {
+      ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+      kbegin(ctx, "u_insert", dr->n_bytes + 16 * dr->n_reads + (uint64_t)(est * 64));
+      if (dr->n_reads) k_uinsert_reads<<<grid_for(ctx, dr->n_reads), kUThreads, 0, ctx->stream>>>(rv, kp, t);
+      kend(ctx);
+    } else {
+      kbegin(ctx, "u_insert_recs", n_rec * sizeof(KRec) + (uint64_t)(est * 64));
+      if (n_rec) k_uinsert_recs<<<grid_for(ctx, n_rec), kUThreads, 0, ctx->stream>>>(rec, n_rec, t);
+      kend(ctx);
+    }
+    APG_CHECK_HIP(hipGetLastError());
+    unsigned long long of = 0;
+    APG_CHECK_HIP(hipMemcpyAsync(&of, ovf, 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    if (!of) break;
+    if (attempt >= 6) {
+      set_error("unipaths: node table overflow persists");
+      return APG_E_STATE;
+    }
+    vlog(ctx, "unipaths: node table of %llu slots overflowed, rebuilding at 2x", (unsigned long long)T);
+    T *= 2;
+  }
+  // compaction, grouped by digit
+  const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, T / 4096));
   uint32_t* cmat = nullptr;
   uint64_t *omat = nullptr, *dstart = nullptr;
   APG_TRY(workspace_t(ctx, "u_cmat", (uint64_t)ndig * G, &cmat));
   APG_TRY(workspace_t(ctx, "u_omat", (uint64_t)ndig * G + 1, &omat));
   APG_TRY(workspace_t(ctx, "u_dstart", ndig + 1, &dstart));
-  kbegin(ctx, "u_ext_count", dr->n_bytes + 16 * dr->n_reads);
-  k_uext_count<<<G, kUThreads, 0, ctx->stream>>>(rv, kp, cmat);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "u"));
+  kbegin(ctx, "u_tab_compact", T * 8 + (uint64_t)(est * 72));
+  k_tab_count<<<G, kUThreads, 0, ctx->stream>>>(t.slot, T, cmat);
+  APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "ut"));
   k_digit_starts_u<<<1, 64, 0, ctx->stream>>>(omat, ndig, G, dstart);
   std::vector<uint64_t> ds(ndig + 1);
   APG_CHECK_HIP(hipMemcpyAsync(ds.data(), dstart, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  counts->resize(ndig);
-  for (uint32_t d = 0; d < ndig; ++d) (*counts)[d] = ds[d + 1] - ds[d];
-  *Gout = G;
-  return APG_OK;
-}
-
-// U1 scatter (after u_extract_count on the same reads): instances grouped by digit.
-static int u_extract_scatter(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, uint32_t G, uint64_t n, KRec* out) {
-  ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  const uint32_t ndig = 1u << kUDigitBits;
-  uint64_t* omat = nullptr;
-  APG_TRY(workspace_t(ctx, "u_omat", (uint64_t)ndig * G + 1, &omat));
-  kbegin(ctx, "u_ext_scatter", dr->n_bytes + 16 * dr->n_reads + n * sizeof(KRec));
-  k_uext_scatter<<<G, kUThreads, 0, ctx->stream>>>(rv, kp, omat, out);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  return APG_OK;
-}
-
-// U2 + U3 + compaction: the distinct nodes (key, OR of extension bits) of
-// the instances in `src`, laid out as `parents` (groups of segments whose top
-// `consumed` meta bits are fixed).  src is never written.  Nodes land in
-// workspace "u_nodes".
-static int u_build_nodes(apg_ctx* ctx, const KRec* src, std::vector<std::vector<Seg>> parents, uint64_t n, int consumed,
-                         KRec** nodes_out, uint64_t* N_out) {
-  unsigned long long* gs = nullptr;
-  APG_TRY(workspace_t(ctx, "u_gs_nodes", 4, &gs));
-  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));
-  const int bb = std::max(consumed, ceil_log2_u(std::max<uint64_t>(1, (n + kUBucketTarget - 1) / kUBucketTarget)));
-  const int bb_c = std::min(bb, 40);
-  const int rem = bb_c - consumed;
-  int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
-  bool split = false;
-  for (const auto& pp : parents) split |= pp.size() > 1;
-  if (nlev == 0 && split) nlev = 1;  // regroup multi-segment parents
-  KRec *bufA = nullptr, *bufB = nullptr;
-  APG_TRY(workspace_t(ctx, "u_recA", std::max<uint64_t>(n, 1), &bufA));
-  APG_TRY(workspace_t(ctx, "u_recB", std::max<uint64_t>(n, 1), &bufB));
-  uint64_t* boff = nullptr;
-  APG_TRY(workspace_t(ctx, "u_boff", (1ull << bb_c) + 1, &boff));
-  const KRec* cur = src;
-  uint64_t nb = parents.size();
-  if (nlev == 0) {
-    std::vector<uint64_t> hb(nb + 1, 0);
-    for (uint64_t q = 0; q < nb; ++q) {
-      hb[q] = parents[q].empty() ? (q ? hb[q - 1] : 0) : parents[q][0].start;
-      hb[q + 1] = hb[q] + (parents[q].empty() ? 0 : parents[q][0].len);
-    }
-    hb[nb] = n;
-    APG_CHECK_HIP(hipMemcpyAsync(boff, hb.data(), (nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-  }
-  for (int lev = 0; lev < nlev; ++lev) {
-    const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
-    consumed += bits;
-    std::vector<uint64_t> hb;
-    const bool last = lev + 1 == nlev;
-    KRec* dst = (cur == bufA) ? bufB : bufA;
-    APG_TRY(part_level<KRec>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "u"));
-    nb = parents.size() << bits;
-    if (!last) {
-      parents.assign(nb, {});
-      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
-    }
-    cur = dst;
-  }
-  KRec* other = (cur == bufA) ? bufB : bufA;  // free buffer: sparse nodes
-  uint32_t *spc = nullptr, *bnd = nullptr, *ovf = nullptr;
-  APG_TRY(workspace_t(ctx, "u_spc", std::max<uint64_t>(n, 1), &spc));
-  APG_TRY(workspace_t(ctx, "u_bnd", nb, &bnd));
-  APG_TRY(workspace_t(ctx, "u_ovf", nb, &ovf));
-  GroupOut go{other, spc, bnd, gs, ovf};
-  kbegin(ctx, "u_group", n * sizeof(KRec) * 2);
-  k_ugroup<<<grid_for(ctx, nb, 1), kGThreads, 0, ctx->stream>>>(cur, boff, nb, go);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  unsigned long long h3[3];
-  APG_TRY(d2h_u64(ctx, gs, h3, 3));
-  if (h3[1]) {
-    uint32_t *gtab = nullptr, *grep = nullptr, *gext = nullptr, *gcnt = nullptr;
-    APG_TRY(workspace_t(ctx, "u_gtab", 2 * std::max<uint64_t>(n, 1) + 64, &gtab));
-    APG_TRY(workspace_t(ctx, "u_grep", std::max<uint64_t>(n, 1), &grep));
-    APG_TRY(workspace_t(ctx, "u_gext", std::max<uint64_t>(n, 1), &gext));
-    APG_TRY(workspace_t(ctx, "u_gcnt", std::max<uint64_t>(n, 1), &gcnt));
-    vlog(ctx, "unipaths: %llu oversized buckets -> global grouping", h3[1]);
-    k_ugroup_big<<<(uint32_t)h3[1], kGThreads, 0, ctx->stream>>>(cur, boff, gtab, grep, gext, gcnt, go);
-    APG_CHECK_HIP(hipGetLastError());
-    APG_TRY(d2h_u64(ctx, gs, h3, 3));
-  }
-  const uint64_t N = h3[0];
-  uint64_t* nbase = nullptr;
+  const uint64_t N = ds[ndig];
   KRec* nodes = nullptr;
-  uint32_t* ncnt = nullptr;
-  APG_TRY(workspace_t(ctx, "u_nbase", nb + 1, &nbase));
-  APG_TRY(scan_u32_u64(ctx, bnd, nb, nbase, "un"));
   APG_TRY(workspace_t(ctx, "u_nodes", std::max<uint64_t>(N, 1), &nodes));
-  APG_TRY(workspace_t(ctx, "u_ncnt", std::max<uint64_t>(N, 1), &ncnt));
-  k_ucompact<<<grid_for(ctx, nb, 1), 256, 0, ctx->stream>>>(other, spc, boff, bnd, nbase, nb, nodes, ncnt);
+  k_tab_scatter<<<G, kUThreads, 0, ctx->stream>>>(t.slot, T, omat, nodes);
+  kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
+  if (digit_counts) {
+    digit_counts->resize(ndig);
+    for (uint32_t d = 0; d < ndig; ++d) (*digit_counts)[d] = ds[d + 1] - ds[d];
+  }
+  vlog(ctx, "unipaths: %llu distinct nodes (estimate %.0f), table %llu slots", (unsigned long long)N, est,
+       (unsigned long long)T);
   *nodes_out = nodes;
   *N_out = N;
   return APG_OK;
@@ -1581,24 +1559,13 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
                          apg_unipath_stats* st) {
   const KeyP kp = make_keyp(prm.K);
   std::memset(st, 0, sizeof(*st));
-  std::vector<uint64_t> counts;
-  uint32_t G = 0;
-  APG_TRY(u_extract_count(ctx, dr, kp, &counts, &G));
   uint64_t n = 0;
-  for (auto c : counts) n += c;
+  double est = 0;
+  APG_TRY(u_size(ctx, dr, kp, &n, &est));
   st->n_instances = n;
-  KRec* ext = nullptr;
-  APG_TRY(workspace_t(ctx, "u_ext", std::max<uint64_t>(n, 1), &ext));
-  APG_TRY(u_extract_scatter(ctx, dr, kp, G, n, ext));
-  std::vector<std::vector<Seg>> parents(counts.size());
-  uint64_t pos = 0;
-  for (size_t d = 0; d < counts.size(); ++d) {
-    parents[d].push_back(Seg{pos, counts[d]});
-    pos += counts[d];
-  }
   KRec* nodes = nullptr;
   uint64_t N = 0;
-  APG_TRY(u_build_nodes(ctx, ext, parents, n, kUDigitBits, &nodes, &N));
+  APG_TRY(u_build_nodes(ctx, dr, nullptr, 0, kp, est, &nodes, &N, nullptr));
   return u_graph(ctx, nodes, N, dr, prm, out, st);
 }
 
@@ -1679,24 +1646,29 @@ int apg_ushard_bins(int n_shards) {
   return (1 << kUDigitBits) / n_shards;
 }
 
-int apg_ushard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* counts) {
+int apg_ushard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* counts,
+                     uint64_t* n_instances) {
   APG_REQUIRE(ctx && reads && counts, "apg_ushard_count: NULL argument");
   APG_TRY(ushard_check(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
-  std::vector<uint64_t> c;
-  uint32_t G = 0;
-  APG_TRY(u_extract_count(ctx, reads, make_keyp(K), &c, &G));
-  uint64_t n = 0;
-  for (size_t i = 0; i < c.size(); ++i) {
-    counts[i] = c[i];  // digit = shard * bins + group: shard-major already
-    n += c[i];
-  }
+  const KeyP kp = make_keyp(K);
   auto& us = ctx->ustate;
+  us.valid = false;
+  uint64_t n = 0;
+  double est = 0;
+  APG_TRY(u_size(ctx, reads, kp, &n, &est));
+  KRec* nodes = nullptr;
+  uint64_t N = 0;
+  std::vector<uint64_t> c;
+  APG_TRY(u_build_nodes(ctx, reads, nullptr, 0, kp, est, &nodes, &N, &c));
+  for (size_t i = 0; i < c.size(); ++i) counts[i] = c[i];  // digit = shard * bins + group: shard-major
+  if (n_instances) *n_instances = n;
   us.valid = true;
   us.gen = reads->gen;
   us.K = K;
-  us.G = G;
   us.n = n;
+  us.n_local = N;
+  us.local_ready = true;
   return APG_OK;
 }
 
@@ -1705,12 +1677,15 @@ int apg_ushard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shard
   APG_TRY(ushard_check(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   auto& us = ctx->ustate;
-  if (!us.valid || us.gen != reads->gen || us.K != K) {
+  if (!us.valid || !us.local_ready || us.gen != reads->gen || us.K != K) {
     std::vector<uint64_t> c(1 << kUDigitBits);
-    APG_TRY(apg_ushard_count(ctx, reads, K, n_shards, c.data()));
+    APG_TRY(apg_ushard_count(ctx, reads, K, n_shards, c.data(), nullptr));
   }
-  APG_REQUIRE(us.n == 0 || d_send, "apg_ushard_scatter: d_send is NULL");
-  APG_TRY(u_extract_scatter(ctx, reads, make_keyp(K), us.G, us.n, static_cast<KRec*>(d_send)));
+  APG_REQUIRE(us.n_local == 0 || d_send, "apg_ushard_scatter: d_send is NULL");
+  KRec* nodes = nullptr;
+  APG_TRY(workspace_t(ctx, "u_nodes", std::max<uint64_t>(us.n_local, 1), &nodes));
+  if (us.n_local)
+    APG_CHECK_HIP(hipMemcpyAsync(d_send, nodes, us.n_local * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
   return sync(ctx);
 }
 
@@ -1720,21 +1695,17 @@ int apg_ushard_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_coun
   APG_TRY(ushard_check(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const int P = n_shards, B = (1 << kUDigitBits) / P;
-  std::vector<std::vector<Seg>> parents(B);
-  uint64_t pos = 0;
-  for (int s = 0; s < P; ++s)
-    for (int l = 0; l < B; ++l) {
-      const uint64_t c = recv_counts[(size_t)s * B + l];
-      parents[l].push_back(Seg{pos, c});
-      pos += c;
-    }
-  APG_REQUIRE(pos == 0 || d_recv, "apg_ushard_nodes: d_recv is NULL");
+  uint64_t n = 0;
+  for (int i = 0; i < P * B; ++i) n += recv_counts[i];
+  APG_REQUIRE(n == 0 || d_recv, "apg_ushard_nodes: d_recv is NULL");
   KRec* nodes = nullptr;
   uint64_t N = 0;
-  APG_TRY(u_build_nodes(ctx, static_cast<const KRec*>(d_recv), parents, pos, kUDigitBits, &nodes, &N));
+  ctx->ustate.local_ready = false;  // "u_nodes" is about to hold this shard's merged nodes
+  APG_TRY(u_build_nodes(ctx, nullptr, static_cast<const KRec*>(d_recv), n, make_keyp(K), (double)n, &nodes, &N,
+                        nullptr));
   APG_TRY(sync(ctx));
   ctx->ustate.n_nodes = N;
-  ctx->ustate.n_recv = pos;
+  ctx->ustate.n_recv = n;
   *n_nodes = N;
   return APG_OK;
 }

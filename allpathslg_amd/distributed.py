@@ -60,7 +60,7 @@ class HipShardBackend:
         return self.ctx.precorrect_solid(dreads, solid.data_ptr(), n_solid, **prm)
 
     # unipath stages
-    def ushard_count(self, dreads: DeviceReads, K: int, P: int) -> np.ndarray:
+    def ushard_count(self, dreads: DeviceReads, K: int, P: int) -> Tuple[np.ndarray, int]:
         return self.ctx.ushard_count(dreads, K, P)
 
     def ushard_scatter(self, dreads: DeviceReads, K: int, P: int, send: torch.Tensor) -> None:
@@ -172,8 +172,8 @@ def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGr
     """Global unipath graph of every rank's reads ("shard the
     counting, replicate the compaction"):
 
-      rank r: K-mer instances (32-byte records) -> hash shards
-              all_to_all(records)          instances of this shard's K-mers
+      rank r: K-mer instances -> distinct local nodes (32-byte records)
+              all_to_all(records)          local nodes of this shard's K-mers
               ushard_nodes                 this shard's distinct nodes
               all_gather(nodes)            the full node set on every rank
               unipaths_from_nodes          graph (identical on every rank) +
@@ -186,7 +186,7 @@ def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGr
         raise ValueError(f"world size {P} must be a power of two <= 32")
     B = 32 // P
     dev = backend.alloc(1).device
-    counts = backend.ushard_count(reads, K, P)  # [dest * B + group]
+    counts, n_inst = backend.ushard_count(reads, K, P)  # [dest * B + group]
     n_send = int(counts.sum())
     send = backend.alloc(4 * n_send)  # 4 x int64 per record
     backend.ushard_scatter(reads, K, P, send)
@@ -216,7 +216,7 @@ def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGr
     nodes = torch.cat([gathered[4 * maxn * r : 4 * maxn * r + 4 * sizes[r]] for r in range(P)])
     del gathered, local
     graph, st = backend.graph_from_nodes(nodes, sum(sizes), reads, K, fetch)
-    inst = torch.tensor([n_send], dtype=torch.int64, device=dev)
+    inst = torch.tensor([n_inst], dtype=torch.int64, device=dev)
     dist.all_reduce(inst, group=group)
     st = dict(st)
     st["n_instances"] = int(inst.item())

@@ -238,11 +238,13 @@ class Context:
             L.apg_unipath_graph_free(C.byref(g))
 
     # -- sharded unipath stages (multi-GPU) -------------------------------------
-    def ushard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
+    def ushard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> Tuple[np.ndarray, int]:
+        """(distinct local nodes per digit [32, shard-major], K-mer instances)."""
         counts = np.zeros(32, dtype=np.uint64)
-        check(lib().apg_ushard_count(self._h, dreads.handle, K, n_shards, counts.ctypes.data_as(_u64p)),
+        n = C.c_uint64()
+        check(lib().apg_ushard_count(self._h, dreads.handle, K, n_shards, counts.ctypes.data_as(_u64p), C.byref(n)),
               "apg_ushard_count")
-        return counts
+        return counts, int(n.value)
 
     def ushard_scatter(self, dreads: DeviceReads, K: int, n_shards: int, d_send_ptr: int) -> None:
         check(lib().apg_ushard_scatter(self._h, dreads.handle, K, n_shards, C.c_void_p(d_send_ptr)),

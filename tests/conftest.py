@@ -4,6 +4,11 @@ import sys
 
 import pytest
 
+# One HIP runtime per process: torch ships its own libamdhip64, and libapg
+# binds to whichever copy is loaded first.  Load torch first (as bench.py
+# does) so tests that mix libapg with torch device buffers see one runtime.
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

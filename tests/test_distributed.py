@@ -130,17 +130,31 @@ class OracleUnipathBackend(OracleShardBackend):
             self.cache[key] = oracle.instances(reads, K)
         return self.cache[key]
 
+    def _local(self, reads, K):
+        """This rank's distinct local nodes (key, ext, hash) in digit order."""
+        key = ("n", id(reads), K)
+        if key not in self.cache:
+            k, e, h = self._inst(reads, K)
+            nk, ne = oracle.group_nodes(k.copy(), e.astype(np.uint8))
+            # hash of each distinct key = the hash of any of its instances
+            uk, first = np.unique(k, axis=0, return_index=True)
+            assert np.array_equal(uk, nk)
+            hh = h[first]
+            d = (hh >> np.uint64(59)).astype(np.int64)
+            o = np.argsort(d, kind="stable")
+            out = np.zeros((len(ne), 4), dtype=np.uint64)
+            out[:, :3] = nk[o]
+            out[:, 3] = hh[o] | ne[o].astype(np.uint64)
+            self.cache[key] = (out, np.bincount(d, minlength=32).astype(np.uint64), len(h))
+        return self.cache[key]
+
     def ushard_count(self, reads, K, P):
-        _, _, h = self._inst(reads, K)
-        return np.bincount((h >> np.uint64(59)).astype(np.int64), minlength=32).astype(np.uint64)
+        out, counts, n_inst = self._local(reads, K)
+        return counts, n_inst
 
     def ushard_scatter(self, reads, K, P, send):
-        k, e, h = self._inst(reads, K)
-        order = np.argsort((h >> np.uint64(59)).astype(np.int64), kind="stable")
-        rec = np.zeros((len(h), 4), dtype=np.uint64)
-        rec[:, :3] = k[order]
-        rec[:, 3] = h[order] | e[order].astype(np.uint64)
-        send[: 4 * len(h)] = torch.from_numpy(rec.reshape(-1).view(np.int64))
+        out, _, _ = self._local(reads, K)
+        send[: 4 * len(out)] = torch.from_numpy(out.reshape(-1).view(np.int64))
 
     def ushard_nodes(self, recv, recv_counts, K, P):
         n = int(recv_counts.sum())

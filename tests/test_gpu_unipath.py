@@ -94,7 +94,7 @@ def test_shard_path_loopback(gpu_ctx, P):
     dsubs = [gpu_ctx.upload(s) for s in subs]
     sends, counts = [], []
     for d in dsubs:
-        c = gpu_ctx.ushard_count(d, K, P)
+        c, _ = gpu_ctx.ushard_count(d, K, P)
         buf = torch.empty(max(4 * int(c.sum()), 1), dtype=torch.int64, device="cuda")
         torch.cuda.synchronize()
         gpu_ctx.ushard_scatter(d, K, P, buf.data_ptr())
