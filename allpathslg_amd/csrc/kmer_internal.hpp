@@ -8,6 +8,12 @@
 
 namespace apg {
 
+// Counting modes: spectrum only; full table (every distinct hash + count, in
+// hash order); solid (only hashes with count >= min_solid, + count,
+// unordered — buckets counted by the global fallback still list every
+// distinct hash, so consumers filter on the count).
+constexpr int kCountSpectrum = 0, kCountTable = 1, kCountSolid = 2;
+
 // Result of the counting pipeline (device pointers into ctx workspaces; valid
 // until the next counting call on the same context).
 struct CountResult {
@@ -22,12 +28,12 @@ struct CountResult {
 
 // Count canonical K-mers (K <= 32) of a device read set.  table = true also
 // materialises the sparse (hash, count) table described in CountResult.
-int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
-                  CountResult* res);
+int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint32_t min_solid, uint64_t* hist,
+                  size_t hist_len, CountResult* res);
 
 // Table-mode count of records received by shard `P`-way exchange
 // (apg_shard_scatter layout, recv_counts[src * B1 + l1]).
-int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P,
-                     CountResult* res);
+int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P, int mode,
+                     uint32_t min_solid, CountResult* res);
 
 }  // namespace apg

@@ -147,7 +147,7 @@ __global__ void k_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig,
 // Stage C: per-bucket counting in LDS.  All records of a bucket share the
 // hash bits above `remb`, so a bucket is counted on the low remb bits
 // (rem) in an LDS open-addressing table (linear probing, CAS insert, atomic
-// count).  Distinct entries are compacted in place, then (TABLE) each one's
+// count).  Distinct entries are compacted in place, then (table mode) each one's
 // rank among the bucket's distinct keys — computed with broadcast LDS reads —
 // places it at off + rank, i.e. in ascending-hash order, independent of the
 // insertion order.  Counts are binned into the spectrum.
@@ -170,13 +170,14 @@ struct KeyTraits<unsigned long long> {
 };
 
 struct CountOut {
-  uint64_t* tab_hash;            // in place over rec (TABLE)
-  uint32_t* tab_cnt;             // parallel to rec (TABLE)
+  uint64_t* tab_hash;            // in place over rec (table / solid modes)
+  uint32_t* tab_cnt;             // parallel to rec (table / solid modes)
   uint32_t* bucket_nd;           // distinct per bucket
   unsigned long long* ghist;     // spectrum
   uint64_t hist_len;
   unsigned long long* gstats;    // [0] n_distinct, [1] overflow count, [2] max bucket
   uint32_t* ovf_list;
+  uint32_t min_solid;            // SOLID mode
 };
 
 __device__ __forceinline__ void spectrum_add(uint32_t c, uint32_t* lhist, unsigned long long* ghist,
@@ -189,7 +190,10 @@ __device__ __forceinline__ void spectrum_add(uint32_t c, uint32_t* lhist, unsign
     atomicAdd(&ghist[m], 1ull);
 }
 
-template <typename KT, bool TABLE>
+// MODE: kCountSpectrum (histogram only), kCountTable (every distinct hash +
+// count, hash order inside the bucket), kCountSolid (only hashes with count
+// >= min_solid, + count, unordered).
+template <typename KT, int MODE>
 __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __restrict__ rec,
                                                                 const uint64_t* __restrict__ boff, uint64_t nbuckets,
                                                                 int remb, CountOut o) {
@@ -243,7 +247,7 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
         o.ovf_list[k] = (uint32_t)bkt;
       }
     } else if (n == 0) {
-      if (TABLE && tid == 0) o.bucket_nd[bkt] = 0;
+      if (MODE != kCountSpectrum && tid == 0) o.bucket_nd[bkt] = 0;
     } else {
       // table size: power of two > n (>= 2 slots per thread); the load factor
       // is distinct/T, typically ~0.2 at genomic coverage
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
         }
       }
       __syncthreads();
-      if (!TABLE) {
+      if (MODE == kCountSpectrum) {
         // spectrum only: every occupied slot is one distinct k-mer
         for (uint32_t s = tid; s < T; s += kCountThreads) {
           if (tkey[s] != EMPTY) {
@@ -280,6 +284,32 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
             ++nd_sum;
           }
         }
+      } else if (MODE == kCountSolid) {
+        // solid hashes only, compacted to the bucket's front in slot order
+        const uint32_t spt = T / kCountThreads;
+        uint32_t ns = 0;
+        for (uint32_t i = 0; i < spt; ++i) {
+          const uint32_t s = tid * spt + i;
+          if (tkey[s] != EMPTY) {
+            spectrum_add(tcnt[s], lhist, o.ghist, o.hist_len);
+            ++nd_sum;
+            ns += tcnt[s] >= o.min_solid;
+          }
+        }
+        uint32_t d;
+        uint32_t j = block_exclusive_scan<uint32_t>(ns, scan_sm, &d);
+        if (tid == 0) scan_sm[32] = (uint32_t)(v[0] >> 32), scan_sm[33] = (uint32_t)v[0];
+        __syncthreads();
+        const uint64_t prefix = (((uint64_t)scan_sm[32] << 32) | scan_sm[33]) & ~remmask;
+        for (uint32_t i = 0; i < spt; ++i) {
+          const uint32_t s = tid * spt + i;
+          if (tkey[s] != EMPTY && tcnt[s] >= o.min_solid) {
+            o.tab_hash[off + j] = prefix | (uint64_t)tkey[s];
+            o.tab_cnt[off + j] = tcnt[s];
+            ++j;
+          }
+        }
+        if (tid == 0) o.bucket_nd[bkt] = d;
       } else {
         // compact occupied slots to the front of the table (in place)
         const uint32_t spt = T / kCountThreads;
@@ -567,7 +597,9 @@ static int extract_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, uin
 // grouped by L1 group: recv_counts[src * B1 + l1].  `spare` (may be null) is
 // a library buffer of >= n records that may be overwritten (ping-pong).
 static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const std::vector<uint64_t>& recv_counts,
-                       int K, int P, bool table, uint64_t* hist, size_t hist_len, CountResult* res) {
+                       int K, int P, int mode, uint32_t min_solid, uint64_t* hist, size_t hist_len,
+                       CountResult* res) {
+  const bool table = mode != kCountSpectrum;
   const int w = 2 * K, pbits = ceil_log2((uint64_t)P), l1 = l1_bits(K, P);
   const uint32_t B1 = 1u << l1;
   if (recv_counts.size() != (size_t)P * B1) {
@@ -586,7 +618,7 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   const int remb = w - pbits - bb;
   res->n_records = n;
   vlog(ctx, "count: K=%d P=%d records=%llu l1=%d levels=%d bucket_bits=%d remb=%d table=%d", K, P,
-       (unsigned long long)n, l1, nlev, bb, remb, (int)table);
+       (unsigned long long)n, l1, nlev, bb, remb, mode);
 
   // parents = L1 groups, each with its P source segments
   std::vector<std::vector<Seg>> parents(B1);
@@ -647,20 +679,31 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
 
-  CountOut co{rec, tab_cnt, bucket_nd, ghist, hl, gstats, ovf_list};
+  CountOut co{rec, tab_cnt, bucket_nd, ghist, hl, gstats, ovf_list, min_solid};
   const bool narrow = remb <= 31;
   const size_t lds = narrow ? bucket_count_lds<uint32_t>() : bucket_count_lds<unsigned long long>();
   const int per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * per_cu * 2));
-  kbegin(ctx, "bucket_count", n * 8 + (table ? n * 12 : 0) + (nb + 1) * 8 + nb * 4);
-  if (narrow && table)
-    k_bucket_count<uint32_t, true><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
-  else if (narrow)
-    k_bucket_count<uint32_t, false><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
-  else if (table)
-    k_bucket_count<unsigned long long, true><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
-  else
-    k_bucket_count<unsigned long long, false><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co);
+  kbegin(ctx, mode == kCountSolid ? "bucket_count_solid" : mode == kCountTable ? "bucket_count_table" : "bucket_count",
+         n * 8 + (mode == kCountTable ? n * 12 : 0) + (nb + 1) * 8 + nb * 4);
+#define APG_COUNT_LAUNCH(KT, M) \
+  k_bucket_count<KT, M><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co)
+  if (narrow) {
+    if (mode == kCountTable)
+      APG_COUNT_LAUNCH(uint32_t, kCountTable);
+    else if (mode == kCountSolid)
+      APG_COUNT_LAUNCH(uint32_t, kCountSolid);
+    else
+      APG_COUNT_LAUNCH(uint32_t, kCountSpectrum);
+  } else {
+    if (mode == kCountTable)
+      APG_COUNT_LAUNCH(unsigned long long, kCountTable);
+    else if (mode == kCountSolid)
+      APG_COUNT_LAUNCH(unsigned long long, kCountSolid);
+    else
+      APG_COUNT_LAUNCH(unsigned long long, kCountSpectrum);
+  }
+#undef APG_COUNT_LAUNCH
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hs[4];
@@ -702,8 +745,8 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   return APG_OK;
 }
 
-int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P,
-                     CountResult* res) {
+int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P, int mode,
+                     uint32_t min_solid, CountResult* res) {
   APG_TRY(check_shards(K, P));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const uint32_t B1 = 1u << l1_bits(K, P);
@@ -711,11 +754,11 @@ int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_
   uint64_t n = 0;
   for (auto c : rc) n += c;
   APG_REQUIRE(n == 0 || d_recv, "shard table: d_recv is NULL");
-  return stage_count(ctx, d_recv, nullptr, rc, K, P, true, nullptr, 0, res);
+  return stage_count(ctx, d_recv, nullptr, rc, K, P, mode, min_solid, nullptr, 0, res);
 }
 
-int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_t* hist, size_t hist_len,
-                         CountResult* res) {
+int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint32_t min_solid, uint64_t* hist,
+                  size_t hist_len, CountResult* res) {
   APG_REQUIRE(ctx && dr, "spectrum: NULL ctx/reads");
   APG_REQUIRE(K >= 1 && K <= 32, "spectrum: K must be in [1, 32] for the 64-bit path");
   APG_REQUIRE(hist_len == 0 || hist_len >= 2, "spectrum: hist_len must be 0 or >= 2");
@@ -725,7 +768,7 @@ int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, bool table, uint64_
   uint64_t* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(ctx->xstate.total, 1), &buf));
   APG_TRY(extract_scatter(ctx, dr, K, 1, buf));
-  return stage_count(ctx, buf, buf, counts, K, 1, table, hist, hist_len, res);
+  return stage_count(ctx, buf, buf, counts, K, 1, mode, min_solid, hist, hist_len, res);
 }
 
 }  // namespace apg
@@ -747,7 +790,7 @@ uint64_t apg_kmer_unhash(int K, uint64_t hash) {
 int apg_kmer_spectrum_dev(apg_ctx* ctx, const apg_dreads* reads, int K, uint64_t* hist, size_t hist_len,
                           apg_kstats* stats) {
   CountResult r;
-  APG_TRY(spectrum_impl(ctx, reads, K, false, hist, hist_len, &r));
+  APG_TRY(spectrum_impl(ctx, reads, K, kCountSpectrum, 0, hist, hist_len, &r));
   if (stats) *stats = r.st;
   return APG_OK;
 }
@@ -770,7 +813,7 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
   apg_dreads* dr = nullptr;
   APG_TRY(apg_reads_upload(ctx, reads, &dr));
   CountResult r;
-  int rc = spectrum_impl(ctx, dr, K, true, nullptr, 0, &r);
+  int rc = spectrum_impl(ctx, dr, K, kCountTable, 0, nullptr, 0, &r);
   apg_reads_free(dr);
   if (rc) return rc;
   const uint64_t nd = r.st.n_distinct;
@@ -844,7 +887,7 @@ int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* rec
   for (auto c : rc) n += c;
   APG_REQUIRE(n == 0 || d_recv, "apg_shard_spectrum: d_recv is NULL");
   CountResult r;
-  APG_TRY(stage_count(ctx, d_recv, nullptr, rc, K, n_shards, false, hist, hist_len, &r));
+  APG_TRY(stage_count(ctx, d_recv, nullptr, rc, K, n_shards, kCountSpectrum, 0, hist, hist_len, &r));
   if (stats) *stats = r.st;
   return APG_OK;
 }

@@ -248,38 +248,31 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         if (__ballot(solid)) continue;
         ++n_sus;
         const uint32_t orig = (__shfl((int)word, (int)(p >> 4), 64) >> (2 * (p & 15))) & 3;
-        // (alternative a in 0..2, covering K-mer t) -> flat index a*nk + t; two rounds of 64 lanes
-        uint64_t fail[2] = {0, 0};
-        for (int rnd = 0; rnd < 2; ++rnd) {
-          const uint32_t f = rnd * 64 + lane;
-          bool bad = false;
-          uint64_t W = 0;
-          const bool act = f < 3 * nk;
-          const uint32_t a = act ? f / nk : 0, t = act ? f - a * nk : 0;
-          W = window_at(word, jlo + t, hp.mask);
-          if (act) {
-            const uint32_t alt = a + (a >= orig ? 1u : 0u);
-            const uint32_t sh = 2 * (p - (jlo + t));
-            W = (W & ~(3ull << sh)) | ((uint64_t)alt << sh);
-            bad = !is_solid(table, tmask, canon_hash(W, K, hp));
-          }
-          fail[rnd] = __ballot(bad);
-          if (3 * nk <= 64) break;
+        // Alternatives in two rounds of lookups: (A) the first covering K-mer
+        // of each of the 3 alternatives (lanes 0..2); (B) the remaining nk-1
+        // K-mers of each survivor of (A) — usually one — one per lane.
+        const uint64_t W0 = window_at(word, jlo, hp.mask);
+        const uint32_t sh0 = 2 * (p - jlo);
+        bool badA = false;
+        if (lane < 3) {
+          const uint32_t alt = (uint32_t)lane + ((uint32_t)lane >= orig ? 1u : 0u);
+          badA = !is_solid(table, tmask, canon_hash((W0 & ~(3ull << sh0)) | ((uint64_t)alt << sh0), K, hp));
         }
+        uint32_t surv = (uint32_t)(~__ballot(badA)) & 7u;
         uint32_t ncand = 0, cand = 0;
-        for (uint32_t a = 0; a < 3; ++a) {
-          const uint32_t lo = a * nk, hi = lo + nk;  // flat range [lo, hi)
-          bool any = false;
-          for (int rnd = 0; rnd < 2; ++rnd) {
-            const uint32_t b0 = rnd * 64;
-            if (hi <= b0 || lo >= b0 + 64) continue;
-            const uint32_t s0 = lo > b0 ? lo - b0 : 0, s1 = min(hi - b0, 64u);
-            const uint64_t rm = (s1 - s0 == 64 ? ~0ull : ((1ull << (s1 - s0)) - 1)) << s0;
-            any |= (fail[rnd] & rm) != 0;
-          }
-          if (!any) {
+        const uint32_t t1 = jlo + 1 + min((uint32_t)lane, nk > 1 ? nk - 2 : 0u);
+        const uint64_t W1 = window_at(word, t1, hp.mask);  // every lane joins the shuffles
+        const uint32_t sh1 = 2 * (p - t1);
+        while (surv) {
+          const uint32_t a = (uint32_t)(__ffs((int)surv) - 1);
+          surv &= surv - 1;
+          const uint32_t alt = a + (a >= orig ? 1u : 0u);
+          bool bad = false;
+          if ((uint32_t)lane + 1 < nk)
+            bad = !is_solid(table, tmask, canon_hash((W1 & ~(3ull << sh1)) | ((uint64_t)alt << sh1), K, hp));
+          if (!__ballot(bad)) {
             ++ncand;
-            cand = a + (a >= orig ? 1u : 0u);
+            cand = alt;
           }
         }
         if (ncand == 1) {
@@ -384,7 +377,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
 
 static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st) {
   CountResult cr;
-  APG_TRY(spectrum_impl(ctx, dr, p.K, true, nullptr, 0, &cr));
+  APG_TRY(spectrum_impl(ctx, dr, p.K, kCountSolid, p.min_solid, nullptr, 0, &cr));
   uint64_t* list = nullptr;
   uint64_t ns = 0;
   APG_TRY(collect_solid(ctx, cr, p.min_solid, &list, &ns));
@@ -437,7 +430,8 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid: min_solid must be >= 1");
   ctx->solid_valid = false;
   CountResult cr;
-  APG_TRY(shard_table_impl(ctx, static_cast<const uint64_t*>(d_recv), recv_counts, K, n_shards, &cr));
+  APG_TRY(shard_table_impl(ctx, static_cast<const uint64_t*>(d_recv), recv_counts, K, n_shards, kCountSolid, min_solid,
+                           &cr));
   uint64_t* list = nullptr;
   uint64_t ns = 0;
   APG_TRY(collect_solid(ctx, cr, min_solid, &list, &ns));

@@ -293,32 +293,34 @@ __device__ __forceinline__ void st_agent64(uint64_t* p, uint64_t v) {
 }
 
 // One probe step of a pending instance (key k, hash h with low byte 0,
-// extension bits e) at slot *s.  Returns true when the instance is settled.
+// extension bits e) at slot *s, given the slot's view.  Returns true when the
+// instance is settled.
 //
 // Fast path: one plain (L2-cacheable, wide) read of the slot line.  A
 // published slot never changes key, so a line cached after the publish is
 // exact; a line cached before it shows the tag as empty or busy, which sends
 // the probe down the coherent path (CAS / agent-scope re-read).  `coh` makes
 // the next probe of a busy slot coherent, so a stale "busy" cannot loop.
-__device__ __forceinline__ bool tab_probe(const UTab& t, const K3& k, uint64_t h, uint32_t e, uint64_t* s,
-                                          uint32_t* probes, bool* coh) {
-  USlot* sl = t.slot + *s;
-  unsigned long long cur;
+// The slot line as the probe sees it (plain or coherent read).
+struct SlotView {
   uint64_t a, b, c, m;
-  if (*coh) {
-    cur = ld_agent(&sl->tag);
-    a = ld_agent64(&sl->k0);
-    b = ld_agent64(&sl->k1);
-    c = ld_agent64(&sl->k2);
-    m = ld_agent64(&sl->meta);
-  } else {
-    const USlot x = *sl;
-    cur = x.tag;
-    a = x.k0;
-    b = x.k1;
-    c = x.k2;
-    m = x.meta;
-  }
+  unsigned long long tag;
+};
+
+__device__ __forceinline__ SlotView slot_read(const USlot* sl, bool coh) {
+  if (coh)
+    return SlotView{ld_agent64(&sl->k0), ld_agent64(&sl->k1), ld_agent64(&sl->k2), ld_agent64(&sl->meta),
+                    ld_agent(&sl->tag)};
+  const USlot x = *sl;
+  return SlotView{x.k0, x.k1, x.k2, x.meta, x.tag};
+}
+
+// Settle (or advance) one probe given the slot view v read at *s.
+__device__ __forceinline__ bool tab_probe(const UTab& t, const K3& k, uint64_t h, uint32_t e, uint64_t* s,
+                                          uint32_t* probes, bool* coh, const SlotView& v) {
+  USlot* sl = t.slot + *s;
+  unsigned long long cur = v.tag;
+  uint64_t a = v.a, b = v.b, c = v.c, m = v.m;
   if (cur == 0) {
     const unsigned long long prev = atomicCAS(&sl->tag, 0ull, (unsigned long long)(h | 1));
     if (prev == 0) {
@@ -386,42 +388,66 @@ __global__ void __launch_bounds__(kUThreads) k_uhll(ReadsV rv, KeyP kp, uint32_t
     if (reg[i]) atomicMax(&hll[i], reg[i]);
 }
 
-// Insert every K-mer instance of the reads.
+// Insert every K-mer instance of the reads.  Each lane keeps kPend
+// instances in flight: per trip it refills its empty entries from its read
+// (rolling; next read when exhausted), issues all their slot reads, then
+// settles them — kPend slot lines in flight per lane instead of one.
+constexpr int kPend = 1;  // measured: 4 in flight (142 VGPRs, 3 waves/SIMD) is slower than 1 at 8 waves
+
 __global__ void __launch_bounds__(kUThreads) k_uinsert_reads(ReadsV rv, KeyP kp, UTab t) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   Roller3 ro;
   ro.i = ro.len = 0;
-  bool started = false, pend = false, live = true;
-  K3 k{0, 0, 0};
-  uint64_t h = 0, s = 0;
-  uint32_t e = 0, probes = 0;
-  bool coh = false;
+  bool started = false, live = true;
+  bool pend[kPend], coh[kPend];
+  K3 k[kPend];
+  uint64_t h[kPend], s[kPend];
+  uint32_t e[kPend], probes[kPend];
+#pragma unroll
+  for (int q = 0; q < kPend; ++q) {
+    pend[q] = coh[q] = false;
+    h[q] = s[q] = 0;
+    e[q] = probes[q] = 0;
+    k[q] = K3{0, 0, 0};
+  }
   for (;;) {
-    while (!pend && live) {  // per lane: next instance, or next read
-      if (started && ro.more()) {
-        const KRec x = ro.next(kp);
-        k = rec_key(x);
-        h = x.meta & ~0xffull;
-        e = (uint32_t)(x.meta & 0xff);
-        s = tab_home(h, t.T);
-        probes = 0;
-        coh = false;
-        pend = true;
-      } else {
-        if (started) r += stride;
-        started = true;
-        if (r >= rv.n_reads) {
-          live = false;
+#pragma unroll
+    for (int q = 0; q < kPend; ++q) {
+      while (!pend[q] && live) {  // per lane: next instance, or next read
+        if (started && ro.more()) {
+          const KRec x = ro.next(kp);
+          k[q] = rec_key(x);
+          h[q] = x.meta & ~0xffull;
+          e[q] = (uint32_t)(x.meta & 0xff);
+          s[q] = tab_home(h[q], t.T);
+          probes[q] = 0;
+          coh[q] = false;
+          pend[q] = true;
         } else {
-          const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
-          ro.i = ro.len = 0;
-          if (len >= (uint32_t)kp.K) ro.init(rv.packed + rv.byte_off[r], len, kp);
+          if (started) r += stride;
+          started = true;
+          if (r >= rv.n_reads) {
+            live = false;
+          } else {
+            const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+            ro.i = ro.len = 0;
+            if (len >= (uint32_t)kp.K) ro.init(rv.packed + rv.byte_off[r], len, kp);
+          }
         }
       }
     }
-    if (!__ballot(pend)) break;
-    if (pend && tab_probe(t, k, h, e, &s, &probes, &coh)) pend = false;
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < kPend; ++q) any |= pend[q];
+    if (!__ballot(any)) break;
+    SlotView v[kPend];
+#pragma unroll
+    for (int q = 0; q < kPend; ++q)
+      if (pend[q]) v[q] = slot_read(t.slot + s[q], coh[q]);
+#pragma unroll
+    for (int q = 0; q < kPend; ++q)
+      if (pend[q] && tab_probe(t, k[q], h[q], e[q], &s[q], &probes[q], &coh[q], v[q])) pend[q] = false;
   }
 }
 
@@ -447,7 +473,7 @@ __global__ void __launch_bounds__(kUThreads) k_uinsert_recs(const KRec* __restri
       pend = true;
     }
     if (!__ballot(pend)) break;
-    if (pend && tab_probe(t, k, h, e, &s, &probes, &coh)) pend = false;
+    if (pend && tab_probe(t, k, h, e, &s, &probes, &coh, slot_read(t.slot + s, coh))) pend = false;
   }
 }
 
