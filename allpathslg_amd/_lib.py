@@ -133,6 +133,22 @@ class apg_unipath_graph(C.Structure):
 APG_UNIPATH_READ_PATHS = 1
 
 
+APG_ALN_RC = 1
+
+
+class apg_aln_pair(C.Structure):
+    _fields_ = [("s_id", C.c_uint32), ("t_id", C.c_uint32), ("offset", C.c_int32), ("flags", C.c_uint32)]
+
+
+class apg_gapfree_hit(C.Structure):
+    _fields_ = [("overlap", C.c_uint32), ("mismatches", C.c_uint32), ("qsum", C.c_uint32), ("offset", C.c_int32)]
+
+
+class apg_sw_hit(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in ("cost", "t_begin", "t_end", "mismatches", "gaps_s", "gaps_t", "n_blocks",
+                                         "status")]
+
+
 class apg_synth_params(C.Structure):
     _fields_ = [
         ("genome_len", C.c_uint64),
@@ -214,6 +230,17 @@ SIGNATURES = {
         [_P, C.c_void_p, C.c_uint64, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),
          C.POINTER(apg_unipath_stats)],
     ),
+    "apg_gapfree": (
+        C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64,
+                  C.POINTER(apg_gapfree_hit)]),
+    "apg_gapfree_dev": (C.c_int, [_P, _P, _P, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "apg_banded_sw": (
+        C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64, C.c_int,
+                  C.POINTER(apg_sw_hit), C.POINTER(C.c_int32), C.c_uint32]),
+    "apg_banded_sw_dev": (C.c_int, [_P, _P, _P, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "apg_consensus": (
+        C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64, _u8p, _u8p]),
+    "apg_consensus_dev": (C.c_int, [_P, _P, _P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),

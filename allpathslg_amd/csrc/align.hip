@@ -1,0 +1,517 @@
+// align.hip — read-to-unibase aligners and column consensus on MI355X.
+//
+// Replaces the pairwise aligners feeding CRefMerger / LongReadConsensus
+// ([R:M] src/pairwise_aligners/PerfectAlignment*, KmerAligner,
+// SmithWatBanded.cc; [R:L] CRefMerger / LongReadConsensus; reference snapshot
+// empty).  Semantics: SURVEY §A.7 as pinned in include/apg.h;
+// CPU restatement in oracle/align_oracle.c.
+//
+//   gap-free   one thread per (read, target, offset): 32 bases per XOR +
+//              popcount of the 2-bit difference mask; qualities summed only
+//              over mismatch bits.  VALU/latency bound, not HBM.
+//   banded SW  one wavefront per pair, one lane per band diagonal (chunks of
+//              64 diagonals): a DP row is one step per lane (diagonal and
+//              vertical predecessors are the lane's own and its neighbour's
+//              previous-row values) plus a wave min-plus prefix scan for the
+//              horizontal chain (D[i][k] = min_{k'<=k} X[k'] + 3 (k - k')).
+//              Directions (2 bits/cell) are ballot-packed per row into a
+//              per-wave scratch; lane 0 walks the traceback.  Max-plus, not a
+//              sum of products: no MFMA formulation applies.
+//   consensus  per placed base an atomic add of its quality into the target
+//              column's 4 vote counters, then one thread per column decides.
+#include <algorithm>
+#include <cstring>
+
+#include "apg_core.hpp"
+#include "kmer_common.hpp"
+
+namespace apg {
+
+struct AlnPair {  // == apg_aln_pair
+  uint32_t s, t;
+  int32_t off;
+  uint32_t flags;
+};
+
+struct SeqSet {
+  const uint64_t* base_off;
+  const uint64_t* byte_off;
+  const uint8_t* packed;
+  const uint8_t* quals;
+};
+
+__device__ __forceinline__ uint32_t abase(const uint8_t* rd, uint32_t i) { return (rd[i >> 2] >> (2 * (i & 3))) & 3; }
+
+__device__ __forceinline__ uint64_t rev2a(uint64_t x) {  // reverse the 32 2-bit groups
+  x = __builtin_bitreverse64(x);
+  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+}
+
+// 32 bases [j, j+32) of a packed read, LSB-first (base j in bits 0-1).  Reads
+// 12 bytes from the aligned word holding base j (device buffers have slack).
+__device__ __forceinline__ uint64_t load_lsb64(const uint8_t* rd, uint32_t j) {
+  const uintptr_t addr = (uintptr_t)(rd + (j >> 2));
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  const int sh = (int)(addr & 3) * 8 + 2 * (int)(j & 3);
+  const uint64_t q0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  return sh ? (q0 >> sh) | ((uint64_t)w[2] << (64 - sh)) : q0;
+}
+
+// n <= 32 bases [i, i+n) of the aligned S (reverse complement if rc) in the
+// low 2n bits, LSB-first.
+__device__ __forceinline__ uint64_t s_window(const uint8_t* rd, uint32_t L, uint32_t i, uint32_t n, bool rc) {
+  if (!rc) return load_lsb64(rd, i);
+  // S'[i + t] = 3 - S[L-1-i-t]: the window of S at a = L-i-n, reversed, complemented
+  const uint64_t W = load_lsb64(rd, L - i - n);
+  return ~rev2a(W) >> (2 * (32 - n));
+}
+
+__global__ void __launch_bounds__(256) k_gapfree(SeqSet S, SeqSet T, const AlnPair* __restrict__ pairs, uint64_t n,
+                                                 uint32_t* __restrict__ out) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const AlnPair pr = pairs[k];
+    const uint32_t Ls = (uint32_t)(S.base_off[pr.s + 1] - S.base_off[pr.s]);
+    const uint32_t Lt = (uint32_t)(T.base_off[pr.t + 1] - T.base_off[pr.t]);
+    const uint8_t* sr = S.packed + S.byte_off[pr.s];
+    const uint8_t* tr = T.packed + T.byte_off[pr.t];
+    const uint8_t* sq = S.quals ? S.quals + S.base_off[pr.s] : nullptr;
+    const bool rc = pr.flags & 1;
+    const int64_t lo = std::max<int64_t>(0, -(int64_t)pr.off);
+    const int64_t hi = std::min<int64_t>((int64_t)Ls, (int64_t)Lt - pr.off);
+    uint32_t ov = 0, mm = 0, qs = 0;
+    for (int64_t i0 = lo; i0 < hi; i0 += 32) {
+      const uint32_t nb = (uint32_t)std::min<int64_t>(32, hi - i0);
+      const uint64_t mask = nb == 32 ? ~0ull : ((1ull << (2 * nb)) - 1);
+      const uint64_t x = (s_window(sr, Ls, (uint32_t)i0, nb, rc) ^ load_lsb64(tr, (uint32_t)(i0 + pr.off))) & mask;
+      uint64_t bits = (x | (x >> 1)) & 0x5555555555555555ull;
+      ov += nb;
+      mm += (uint32_t)__popcll(bits);
+      if (sq) {
+        while (bits) {
+          const uint32_t t = (uint32_t)__ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          const uint32_t i = (uint32_t)i0 + (t >> 1);
+          qs += rc ? sq[Ls - 1 - i] : sq[i];
+        }
+      }
+    }
+    uint4 o;
+    o.x = ov;
+    o.y = mm;
+    o.z = qs;
+    o.w = (uint32_t)pr.off;
+    reinterpret_cast<uint4*>(out)[k] = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Banded Smith-Waterman (semi-global: all of S, free ends in T)
+// ---------------------------------------------------------------------------
+constexpr int kSwChunks = 4;  // band <= 256 diagonals (w <= 127)
+constexpr int32_t kSwInf = 1 << 29;
+constexpr uint32_t DIR_START = 0, DIR_DIAG = 1, DIR_HORZ = 2, DIR_VERT = 3;
+
+struct SwOut {
+  int32_t* res;     // 8 per pair
+  int32_t* blocks;  // max_blocks x (gap, len) per pair, or null
+  uint32_t max_blocks;
+};
+
+__host__ __device__ inline uint64_t sw_scratch_words(uint32_t rows_cap, int nch) {
+  return (uint64_t)(rows_cap + 1) * nch * 2 + (2ull * rows_cap + 64 * kSwChunks + 64) / 8;
+}
+
+// Wave inclusive prefix min.
+__device__ __forceinline__ int32_t wave_prefix_min(int32_t x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x = min(x, y);
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(256) k_banded_sw(SeqSet S, SeqSet T, const AlnPair* __restrict__ pairs, uint64_t n,
+                                                   int w, uint64_t* __restrict__ scratch, uint32_t rows_cap,
+                                                   SwOut o) {
+  const int lane = lane_id();
+  const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const int band = 2 * w + 1;
+  const int nch = (band + 63) >> 6;
+  // per-wave scratch: directions [row][chunk] (bit0 mask, bit1 mask), then
+  // the traceback's move bytes (<= 2 rows + band)
+  uint64_t* dirs = scratch + wid * sw_scratch_words(rows_cap, nch);
+  uint8_t* moves = reinterpret_cast<uint8_t*>(dirs + (uint64_t)(rows_cap + 1) * nch * 2);
+  for (uint64_t k = wid; k < n; k += nw) {
+    const AlnPair pr = pairs[k];
+    const int Ls = (int)(S.base_off[pr.s + 1] - S.base_off[pr.s]);
+    const int Lt = (int)(T.base_off[pr.t + 1] - T.base_off[pr.t]);
+    const uint8_t* sr = S.packed + S.byte_off[pr.s];
+    const uint8_t* tr = T.packed + T.byte_off[pr.t];
+    const bool rc = pr.flags & 1;
+    const int dmin = pr.off - w;
+    // row 0: free T prefix
+    int32_t Dp[kSwChunks];
+#pragma unroll
+    for (int c = 0; c < kSwChunks; ++c) {
+      const int kk = c * 64 + lane;
+      const int j = dmin + kk;
+      Dp[c] = (c < nch && kk < band && j >= 0 && j <= Lt) ? 0 : kSwInf;
+    }
+    for (int i = 1; i <= Ls; ++i) {
+      const uint32_t sb = rc ? 3 - abase(sr, (uint32_t)(Ls - i)) : abase(sr, (uint32_t)(i - 1));
+      int32_t Dn[kSwChunks];
+      int32_t carry = kSwInf;  // D[i] of the previous chunk's last diagonal (horizontal chain)
+#pragma unroll
+      for (int c = 0; c < kSwChunks; ++c) {
+        if (c >= nch) {
+          Dn[c] = kSwInf;
+          continue;
+        }
+        const int kk = c * 64 + lane;
+        const int j = i + dmin + kk;
+        const bool valid = kk < band && j >= 0 && j <= Lt;
+        // vertical predecessor D[i-1][j] sits on diagonal kk+1
+        int32_t up = __shfl_down(Dp[c], 1, 64);
+        const int32_t nxt0 = (c + 1 < kSwChunks) ? __shfl(Dp[c + 1 < kSwChunks ? c + 1 : c], 0, 64) : kSwInf;
+        if (lane == 63) up = (c + 1 < nch) ? nxt0 : kSwInf;
+        int32_t diagC = kSwInf, vertC = kSwInf;
+        if (valid && j >= 1 && Dp[c] < kSwInf) diagC = Dp[c] + (sb == abase(tr, (uint32_t)(j - 1)) ? 0 : 2);
+        if (valid && up < kSwInf) vertC = up + 3;
+        const int32_t X = valid ? min(diagC, vertC) : kSwInf;
+        // horizontal chain: D[kk] = min(X[kk], D[kk-1] + 3) = min_{k'<=kk} X[k'] + 3 (kk - k')
+        const int32_t Y = X >= kSwInf ? kSwInf : X - 3 * lane;
+        int32_t pm = wave_prefix_min(Y);
+        int32_t D = pm >= kSwInf / 2 ? kSwInf : pm + 3 * lane;
+        if (carry < kSwInf) D = min(D, carry + 3 * (lane + 1));
+        if (!valid) D = kSwInf;
+        // direction, with the oracle's tie order: diagonal > gap in S > gap in T
+        int32_t left = __shfl_up(D, 1, 64);
+        if (lane == 0) left = carry;
+        const int32_t horzC = (valid && j >= 1 && left < kSwInf) ? left + 3 : kSwInf;
+        uint32_t dir = DIR_START;
+        if (D < kSwInf) dir = diagC == D ? DIR_DIAG : horzC == D ? DIR_HORZ : DIR_VERT;
+        const uint64_t b0 = __ballot(dir & 1), b1 = __ballot(dir & 2);
+        if (lane == 0) {
+          uint64_t* row = dirs + ((uint64_t)i * nch + c) * 2;
+          row[0] = b0;
+          row[1] = b1;
+        }
+        carry = __shfl(D, 63, 64);
+        Dn[c] = D;
+      }
+#pragma unroll
+      for (int c = 0; c < kSwChunks; ++c) Dp[c] = Dn[c];
+    }
+    // end: min over the last row, ties to the smallest j (= smallest diagonal)
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int c = 0; c < kSwChunks; ++c) {
+      if (c < nch && Dp[c] < kSwInf) {
+        const unsigned long long key = ((unsigned long long)(uint32_t)Dp[c] << 32) | (uint32_t)(c * 64 + lane);
+        best = min(best, key);
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) best = min(best, (unsigned long long)__shfl_xor((long long)best, off, 64));
+    if (lane == 0) {
+      int32_t* r = o.res + 8 * k;
+      for (int q = 0; q < 8; ++q) r[q] = 0;
+      if (best == ~0ull) {
+        r[7] = 1;
+      } else {
+        int kk = (int)(best & 0xffffffffu);
+        int i = Ls;
+        r[0] = (int32_t)(best >> 32);
+        r[2] = Ls + dmin + kk;
+        // traceback into the wave's move buffer (backwards), then blocks forward
+        int nm = 0, mm = 0, gs = 0, gt = 0;
+        while (i > 0) {
+          const int c = kk >> 6, l = kk & 63;
+          const uint64_t* row = dirs + ((uint64_t)i * nch + c) * 2;
+          const uint32_t d = (uint32_t)((row[0] >> l) & 1) | ((uint32_t)((row[1] >> l) & 1) << 1);
+          if (d == DIR_DIAG) {
+            const int j = i + dmin + kk;
+            const uint32_t sb = rc ? 3 - abase(sr, (uint32_t)(Ls - i)) : abase(sr, (uint32_t)(i - 1));
+            mm += sb != abase(tr, (uint32_t)(j - 1));
+            moves[nm++] = 0;
+            --i;
+          } else if (d == DIR_HORZ) {  // T base against a gap in S
+            moves[nm++] = 1;
+            ++gs;
+            --kk;
+          } else {  // S base against a gap in T
+            moves[nm++] = 2;
+            ++gt;
+            --i;
+            ++kk;
+          }
+        }
+        r[1] = dmin + kk;  // row 0: j = dmin + kk
+        r[3] = mm;
+        r[4] = gs;
+        r[5] = gt;
+        // blocks, forward order (same rule as the oracle)
+        uint32_t nb = 0;
+        int gap = 0, len = 0;
+        bool over = false;
+        int32_t* blk = o.blocks ? o.blocks + 2 * (uint64_t)k * o.max_blocks : nullptr;
+        for (int q = nm - 1; q >= 0; --q) {
+          const uint8_t m = moves[q];
+          if (m == 0) {
+            ++len;
+            continue;
+          }
+          if (len > 0) {
+            if (blk && nb < o.max_blocks) {
+              blk[2 * nb] = gap;
+              blk[2 * nb + 1] = len;
+            } else if (blk) {
+              over = true;
+            }
+            ++nb;
+            gap = 0;
+            len = 0;
+          }
+          gap += m == 1 ? 1 : -1;
+        }
+        if (len > 0 || gap != 0 || nb == 0) {
+          if (blk && nb < o.max_blocks) {
+            blk[2 * nb] = gap;
+            blk[2 * nb + 1] = len;
+          } else if (blk) {
+            over = true;
+          }
+          ++nb;
+        }
+        r[6] = (int32_t)nb;
+        r[7] = over ? 2 : 0;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Consensus
+// ---------------------------------------------------------------------------
+__global__ void k_votes(SeqSet R, SeqSet T, const AlnPair* __restrict__ plc, uint64_t n, uint32_t* __restrict__ votes) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    const AlnPair p = plc[k];
+    const uint32_t L = (uint32_t)(R.base_off[p.s + 1] - R.base_off[p.s]);
+    const uint32_t Lt = (uint32_t)(T.base_off[p.t + 1] - T.base_off[p.t]);
+    const uint8_t* rd = R.packed + R.byte_off[p.s];
+    const uint8_t* q = R.quals + R.base_off[p.s];
+    const bool rc = p.flags & 1;
+    const uint64_t tb = T.base_off[p.t];
+    const int64_t lo = std::max<int64_t>(0, -(int64_t)p.off);
+    const int64_t hi = std::min<int64_t>((int64_t)L, (int64_t)Lt - p.off);
+    for (int64_t i = lo; i < hi; ++i) {
+      const uint32_t b = rc ? 3 - abase(rd, (uint32_t)(L - 1 - i)) : abase(rd, (uint32_t)i);
+      const uint32_t qq = rc ? q[L - 1 - i] : q[i];
+      if (qq) atomicAdd(&votes[(tb + (uint64_t)(i + p.off)) * 4 + b], qq);
+    }
+  }
+}
+
+__global__ void k_decide(SeqSet T, uint64_t n_targets, uint64_t NT, const uint32_t* __restrict__ votes,
+                         uint8_t* __restrict__ cons, uint8_t* __restrict__ cq) {
+  for (uint64_t col = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; col < NT;
+       col += (uint64_t)gridDim.x * blockDim.x) {
+    // target of this column: binary search over base_off
+    uint64_t lo = 0, hi = n_targets;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (T.base_off[mid] <= col)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const uint32_t tbase = abase(T.packed + T.byte_off[lo], (uint32_t)(col - T.base_off[lo]));
+    const uint4 v4 = reinterpret_cast<const uint4*>(votes)[col];
+    const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
+    uint32_t win = tbase;
+    for (uint32_t b = 0; b < 4; ++b)
+      if (v[b] > v[win]) win = b;
+    uint32_t other = 0;
+    for (uint32_t b = 0; b < 4; ++b)
+      if (b != win && v[b] > other) other = v[b];
+    const uint32_t dq = v[win] - other;
+    cons[col] = (uint8_t)win;
+    cq[col] = (uint8_t)(dq > 60 ? 60 : dq);
+  }
+}
+
+}  // namespace apg
+
+using namespace apg;
+
+namespace {
+
+SeqSet seqset(const apg_dreads* d) { return SeqSet{d->d_base_off, d->d_byte_off, d->d_packed, d->d_quals}; }
+
+// Host-side id/offset validation of a pair list (host API variants).
+int check_pairs(const apg_aln_pair* p, uint64_t n, uint64_t nS, uint64_t nT, const char* who) {
+  for (uint64_t k = 0; k < n; ++k)
+    if (p[k].s_id >= nS || p[k].t_id >= nT) {
+      set_error(std::string(who) + ": pair " + std::to_string(k) + " names a sequence out of range");
+      return APG_E_ARG;
+    }
+  return APG_OK;
+}
+
+// Copies a host pair list to a device workspace.
+int pairs_to_dev(apg_ctx* ctx, const apg_aln_pair* p, uint64_t n, AlnPair** d) {
+  APG_TRY(workspace_t(ctx, "a_pairs", std::max<uint64_t>(n, 1), d));
+  if (n) APG_CHECK_HIP(hipMemcpyAsync(*d, p, n * sizeof(AlnPair), hipMemcpyHostToDevice, ctx->stream));
+  return APG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int apg_gapfree_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T, const apg_aln_pair* d_pairs, uint64_t n,
+                    apg_gapfree_hit* d_out) {
+  APG_REQUIRE(ctx && S && T, "apg_gapfree: NULL argument");
+  APG_REQUIRE(n == 0 || (d_pairs && d_out), "apg_gapfree: NULL pairs/out");
+  static_assert(sizeof(apg_aln_pair) == sizeof(AlnPair), "pair layout");
+  static_assert(sizeof(apg_gapfree_hit) == 16, "hit layout");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  kbegin(ctx, "gapfree", n * (16 + 16) + n * 2 * 32);
+  if (n)
+    k_gapfree<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(seqset(S), seqset(T), reinterpret_cast<const AlnPair*>(d_pairs),
+                                                          n, reinterpret_cast<uint32_t*>(d_out));
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return sync(ctx);
+}
+
+int apg_gapfree(apg_ctx* ctx, const apg_reads* S, const apg_reads* T, const apg_aln_pair* pairs, uint64_t n,
+                apg_gapfree_hit* out) {
+  APG_REQUIRE(ctx && S && T && (n == 0 || (pairs && out)), "apg_gapfree: NULL argument");
+  APG_TRY(check_pairs(pairs, n, S->n_reads, T->n_reads, "apg_gapfree"));
+  apg_dreads *dS = nullptr, *dT = nullptr;
+  APG_TRY(apg_reads_upload(ctx, S, &dS));
+  int rc = apg_reads_upload(ctx, T, &dT);
+  AlnPair* dp = nullptr;
+  apg_gapfree_hit* dout = nullptr;
+  if (rc == APG_OK) rc = pairs_to_dev(ctx, pairs, n, &dp);
+  if (rc == APG_OK) rc = workspace_t(ctx, "a_out", std::max<uint64_t>(n, 1), &dout);
+  if (rc == APG_OK) rc = apg_gapfree_dev(ctx, dS, dT, reinterpret_cast<apg_aln_pair*>(dp), n, dout);
+  if (rc == APG_OK && n) {
+    if (hipMemcpy(out, dout, n * sizeof(apg_gapfree_hit), hipMemcpyDeviceToHost) != hipSuccess) {
+      set_error("apg_gapfree: D2H failed");
+      rc = APG_E_HIP;
+    }
+  }
+  apg_reads_free(dS);
+  apg_reads_free(dT);
+  return rc;
+}
+
+int apg_banded_sw_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T, const apg_aln_pair* d_pairs, uint64_t n,
+                      int band_w, apg_sw_hit* d_out, int32_t* d_blocks, uint32_t max_blocks) {
+  APG_REQUIRE(ctx && S && T, "apg_banded_sw: NULL argument");
+  APG_REQUIRE(n == 0 || (d_pairs && d_out), "apg_banded_sw: NULL pairs/out");
+  APG_REQUIRE(band_w >= 0 && 2 * band_w + 1 <= 64 * kSwChunks, "apg_banded_sw: band_w must be in [0, 127]");
+  APG_REQUIRE(!d_blocks || max_blocks > 0, "apg_banded_sw: max_blocks must be > 0 with a block buffer");
+  static_assert(sizeof(apg_sw_hit) == 32, "hit layout");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  if (n == 0) return APG_OK;
+  const int nch = (2 * band_w + 1 + 63) / 64;
+  const uint32_t rows_cap = (uint32_t)std::max<uint64_t>(S->max_len, 1);
+  const uint32_t grid = grid_for(ctx, n, 4);  // 4 waves per block, one pair per wave
+  const uint64_t waves = (uint64_t)grid * 4;
+  uint64_t* scratch = nullptr;
+  APG_TRY(workspace_t(ctx, "a_sw_scratch", waves * sw_scratch_words(rows_cap, nch), &scratch));
+  SwOut o{reinterpret_cast<int32_t*>(d_out), d_blocks, d_blocks ? max_blocks : 0};
+  if (d_blocks)  // entries past a pair's n_blocks read as zero
+    APG_CHECK_HIP(hipMemsetAsync(d_blocks, 0, n * (uint64_t)max_blocks * 8, ctx->stream));
+  kbegin(ctx, "banded_sw", n * (16 + 32) + n * (uint64_t)rows_cap * (2 * band_w + 1) / 4);
+  k_banded_sw<<<grid, 256, 0, ctx->stream>>>(seqset(S), seqset(T), reinterpret_cast<const AlnPair*>(d_pairs), n, band_w,
+                                              scratch, rows_cap, o);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return sync(ctx);
+}
+
+int apg_banded_sw(apg_ctx* ctx, const apg_reads* S, const apg_reads* T, const apg_aln_pair* pairs, uint64_t n,
+                  int band_w, apg_sw_hit* out, int32_t* blocks, uint32_t max_blocks) {
+  APG_REQUIRE(ctx && S && T && (n == 0 || (pairs && out)), "apg_banded_sw: NULL argument");
+  APG_TRY(check_pairs(pairs, n, S->n_reads, T->n_reads, "apg_banded_sw"));
+  apg_dreads *dS = nullptr, *dT = nullptr;
+  APG_TRY(apg_reads_upload(ctx, S, &dS));
+  int rc = apg_reads_upload(ctx, T, &dT);
+  AlnPair* dp = nullptr;
+  apg_sw_hit* dout = nullptr;
+  int32_t* dblk = nullptr;
+  if (rc == APG_OK) rc = pairs_to_dev(ctx, pairs, n, &dp);
+  if (rc == APG_OK) rc = workspace_t(ctx, "a_out", std::max<uint64_t>(n, 1), &dout);
+  if (rc == APG_OK && blocks) rc = workspace_t(ctx, "a_blocks", std::max<uint64_t>(2 * n * max_blocks, 1), &dblk);
+  if (rc == APG_OK)
+    rc = apg_banded_sw_dev(ctx, dS, dT, reinterpret_cast<apg_aln_pair*>(dp), n, band_w, dout, dblk, max_blocks);
+  if (rc == APG_OK && n) {
+    bool ok = hipMemcpy(out, dout, n * sizeof(apg_sw_hit), hipMemcpyDeviceToHost) == hipSuccess;
+    if (blocks) ok = ok && hipMemcpy(blocks, dblk, 2 * n * max_blocks * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    if (!ok) {
+      set_error("apg_banded_sw: D2H failed");
+      rc = APG_E_HIP;
+    }
+  }
+  apg_reads_free(dS);
+  apg_reads_free(dT);
+  return rc;
+}
+
+int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T, const apg_aln_pair* d_plc, uint64_t n,
+                      uint8_t* d_bases, uint8_t* d_quals) {
+  APG_REQUIRE(ctx && R && T, "apg_consensus: NULL argument");
+  APG_REQUIRE(n == 0 || d_plc, "apg_consensus: NULL placements");
+  APG_REQUIRE(n == 0 || R->d_quals, "apg_consensus: the placed reads need qualities");
+  APG_REQUIRE(T->n_bases == 0 || (d_bases && d_quals), "apg_consensus: NULL outputs");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const uint64_t NT = T->n_bases;
+  uint32_t* votes = nullptr;
+  APG_TRY(workspace_t(ctx, "a_votes", std::max<uint64_t>(4 * NT, 4), &votes));
+  APG_CHECK_HIP(hipMemsetAsync(votes, 0, std::max<uint64_t>(4 * NT, 4) * 4, ctx->stream));
+  kbegin(ctx, "consensus_votes", n * 16 + R->n_bytes + R->n_bases);
+  if (n)
+    k_votes<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(seqset(R), seqset(T), reinterpret_cast<const AlnPair*>(d_plc), n,
+                                                        votes);
+  kend(ctx);
+  kbegin(ctx, "consensus_decide", NT * 18);
+  if (NT)
+    k_decide<<<grid_for(ctx, NT), 256, 0, ctx->stream>>>(seqset(T), T->n_reads, NT, votes, d_bases, d_quals);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return sync(ctx);
+}
+
+int apg_consensus(apg_ctx* ctx, const apg_reads* R, const apg_reads* T, const apg_aln_pair* plc, uint64_t n,
+                  uint8_t* bases, uint8_t* quals) {
+  APG_REQUIRE(ctx && R && T && (n == 0 || plc), "apg_consensus: NULL argument");
+  APG_TRY(check_pairs(plc, n, R->n_reads, T->n_reads, "apg_consensus"));
+  apg_dreads *dR = nullptr, *dT = nullptr;
+  APG_TRY(apg_reads_upload(ctx, R, &dR));
+  int rc = apg_reads_upload(ctx, T, &dT);
+  AlnPair* dp = nullptr;
+  uint8_t *db = nullptr, *dq = nullptr;
+  const uint64_t NT = dT ? dT->n_bases : 0;
+  if (rc == APG_OK) rc = pairs_to_dev(ctx, plc, n, &dp);
+  if (rc == APG_OK) rc = workspace_t(ctx, "a_cons", std::max<uint64_t>(NT, 1), &db);
+  if (rc == APG_OK) rc = workspace_t(ctx, "a_consq", std::max<uint64_t>(NT, 1), &dq);
+  if (rc == APG_OK) rc = apg_consensus_dev(ctx, dR, dT, reinterpret_cast<apg_aln_pair*>(dp), n, db, dq);
+  if (rc == APG_OK && NT) {
+    if (hipMemcpy(bases, db, NT, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(quals, dq, NT, hipMemcpyDeviceToHost) != hipSuccess) {
+      set_error("apg_consensus: D2H failed");
+      rc = APG_E_HIP;
+    }
+  }
+  apg_reads_free(dR);
+  apg_reads_free(dT);
+  return rc;
+}
+
+}  // extern "C"

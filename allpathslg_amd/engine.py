@@ -280,6 +280,54 @@ class Context:
         finally:
             lib().apg_unipath_graph_free(C.byref(g))
 
+    # -- alignment and consensus ----------------------------------
+    @staticmethod
+    def _pairs(pairs) -> np.ndarray:
+        """(n, 4) [s_id, t_id, offset, flags] -> contiguous int32 rows (= apg_aln_pair)."""
+        a = np.ascontiguousarray(np.asarray(pairs, dtype=np.int64).reshape(-1, 4).astype(np.int32))
+        return a
+
+    def gapfree(self, S: ReadSet, T: ReadSet, pairs) -> np.ndarray:
+        """Gap-free alignments: (n, 4) uint32 rows [overlap, mismatches, qsum, offset]."""
+        from ._lib import apg_aln_pair, apg_gapfree_hit
+
+        p = self._pairs(pairs)
+        out = np.zeros((len(p), 4), dtype=np.uint32)
+        rs, rt = S.c_struct(), T.c_struct()
+        check(lib().apg_gapfree(self._h, C.byref(rs), C.byref(rt), p.ctypes.data_as(C.POINTER(apg_aln_pair)), len(p),
+                                out.ctypes.data_as(C.POINTER(apg_gapfree_hit))), "apg_gapfree")
+        return out
+
+    def banded_sw(self, S: ReadSet, T: ReadSet, pairs, band_w: int, max_blocks: int = 0):
+        """Banded Smith-Waterman: ((n, 8) int32 rows [cost, t_begin, t_end,
+        mismatches, gaps_s, gaps_t, n_blocks, status], blocks (n, max_blocks, 2)
+        int32 or None)."""
+        from ._lib import apg_aln_pair, apg_sw_hit
+
+        p = self._pairs(pairs)
+        out = np.zeros((len(p), 8), dtype=np.int32)
+        blk = np.zeros((len(p), max_blocks, 2), dtype=np.int32) if max_blocks else None
+        rs, rt = S.c_struct(), T.c_struct()
+        check(lib().apg_banded_sw(self._h, C.byref(rs), C.byref(rt), p.ctypes.data_as(C.POINTER(apg_aln_pair)),
+                                  len(p), band_w, out.ctypes.data_as(C.POINTER(apg_sw_hit)),
+                                  blk.ctypes.data_as(C.POINTER(C.c_int32)) if blk is not None else None, max_blocks),
+              "apg_banded_sw")
+        return out, blk
+
+    def consensus(self, R: ReadSet, T: ReadSet, placements) -> Tuple[np.ndarray, np.ndarray]:
+        """Column consensus of R placed gap-free on T: (bases, quals), one per T base."""
+        from ._lib import apg_aln_pair
+
+        p = self._pairs(placements)
+        nt = T.n_bases
+        b = np.zeros(max(nt, 1), dtype=np.uint8)
+        q = np.zeros(max(nt, 1), dtype=np.uint8)
+        rr, rt = R.c_struct(), T.c_struct()
+        check(lib().apg_consensus(self._h, C.byref(rr), C.byref(rt), p.ctypes.data_as(C.POINTER(apg_aln_pair)), len(p),
+                                  b.ctypes.data_as(C.POINTER(C.c_uint8)), q.ctypes.data_as(C.POINTER(C.c_uint8))),
+              "apg_consensus")
+        return b[:nt], q[:nt]
+
     # -- sharded (multi-GPU) stages ------------------------------------------
     def shard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
         B = shard_bins(K, n_shards)

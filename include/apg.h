@@ -307,6 +307,77 @@ int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes,
                             apg_unipath_stats* stats);
 
 /* ------------------------------------------------------------------------- */
+/* Read-to-unibase alignment and column consensus (restated;    */
+/* semantics unpinned).  Replaces the aligners feeding CRefMerger /          */
+/* LongReadConsensus ([R:M] src/pairwise_aligners/PerfectAlignment*,         */
+/* KmerAligner, SmithWatBanded.cc; [R:L] CRefMerger / LongReadConsensus).    */
+/*                                                                            */
+/* S / R = query reads (an apg_reads / device read set), T = targets (e.g.   */
+/* unibases, same packed layout).  A pair places S (its reverse complement   */
+/* with APG_ALN_RC) against T so that S[0] faces T[offset].                  */
+/* ------------------------------------------------------------------------- */
+#define APG_ALN_RC 1u
+typedef struct apg_aln_pair {
+  uint32_t s_id;
+  uint32_t t_id;
+  int32_t offset;
+  uint32_t flags; /* APG_ALN_RC */
+} apg_aln_pair;
+
+/* Gap-free: over the overlap of S and T at the offset, mismatches = popcount
+ * of the 2-bit difference mask, qsum = sum of S's qualities at mismatches
+ * (0 when S has no qualities).  offset is echoed. */
+typedef struct apg_gapfree_hit {
+  uint32_t overlap;
+  uint32_t mismatches;
+  uint32_t qsum;
+  int32_t offset;
+} apg_gapfree_hit;
+int apg_gapfree(apg_ctx* ctx, const apg_reads* S, const apg_reads* T, const apg_aln_pair* pairs,
+                uint64_t n, apg_gapfree_hit* out);
+/* Device variant: pairs / out are device buffers; ids must be in range. */
+int apg_gapfree_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T,
+                    const apg_aln_pair* d_pairs, uint64_t n, apg_gapfree_hit* d_out);
+
+/* Banded Smith-Waterman, SmithWatBanded semantics as restated: all of S is
+ * aligned, T has free ends; only cells on diagonals d = j - i in
+ * [offset - w, offset + w] exist.  Integer costs: mismatch 2, gap 3 per base;
+ * minimise.  Ties: diagonal > gap in S (T base unmatched) > gap in T (S base
+ * unmatched); among equal end cells the smallest T end wins.
+ * blocks (optional, max_blocks (gap, len) int32 pairs per pair): the
+ * alignment as runs of aligned columns, each preceded by its gap (> 0: T
+ * bases skipped, < 0: S bases skipped); trailing gaps make a final (gap, 0).
+ * status: 0 ok, 1 no cell of the band reaches the end of S, 2 more blocks
+ * than max_blocks (n_blocks still exact).  band_w <= 127. */
+typedef struct apg_sw_hit {
+  int32_t cost;
+  int32_t t_begin; /* T position of the first aligned S base / gap */
+  int32_t t_end;   /* one past the last T base used */
+  int32_t mismatches;
+  int32_t gaps_s;  /* T bases against gaps */
+  int32_t gaps_t;  /* S bases against gaps */
+  int32_t n_blocks;
+  int32_t status;
+} apg_sw_hit;
+int apg_banded_sw(apg_ctx* ctx, const apg_reads* S, const apg_reads* T, const apg_aln_pair* pairs,
+                  uint64_t n, int band_w, apg_sw_hit* out, int32_t* blocks /* may be NULL */,
+                  uint32_t max_blocks);
+int apg_banded_sw_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T,
+                      const apg_aln_pair* d_pairs, uint64_t n, int band_w, apg_sw_hit* d_out,
+                      int32_t* d_blocks, uint32_t max_blocks);
+
+/* Column consensus of reads placed gap-free on targets (pairs = placements):
+ * every placed base votes its quality for its base at target column
+ * offset + i; per column the largest vote sum wins, ties go to the target's
+ * own base, then to the smaller base code; quality = min(60, winner sum -
+ * best other sum).  Columns without votes keep the target base, Q = 0.
+ * bases / quals: one byte per target base (target set's base order). */
+int apg_consensus(apg_ctx* ctx, const apg_reads* R, const apg_reads* T, const apg_aln_pair* placements,
+                  uint64_t n, uint8_t* bases, uint8_t* quals);
+int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T,
+                      const apg_aln_pair* d_placements, uint64_t n, uint8_t* d_bases, uint8_t* d_quals);
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */
 /* insert N(mean, sd), FR orientation, substitution error rate rising        */
 /* linearly err_lo -> err_hi along the read; Q40 on correct bases, Q2..20 on */

@@ -265,3 +265,61 @@ def graph_from_nodes(keys, ext, reads, K: int = 96) -> dict:
         return out
     finally:
         L.oru_free(C.byref(res))
+
+
+def _rs(reads):
+    return (reads.base_off.ctypes.data_as(_u64p), reads.byte_off.ctypes.data_as(_u64p),
+            reads.packed.ctypes.data_as(_u8p))
+
+
+def _bind_align():
+    L = lib()
+    if not hasattr(L, "_al"):
+        L.ora_gapfree.restype = None
+        L.ora_gapfree.argtypes = [_u64p, _u64p, _u8p, _u8p, _u64p, _u64p, _u8p, _u32p, C.c_uint64, _u32p]
+        L.ora_banded_sw.restype = None
+        L.ora_banded_sw.argtypes = [_u64p, _u64p, _u8p, _u64p, _u64p, _u8p, _u32p, C.c_uint64, C.c_int,
+                                    C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_uint32]
+        L.ora_consensus.restype = None
+        L.ora_consensus.argtypes = [_u64p, _u64p, _u8p, _u8p, _u64p, _u64p, _u8p, C.c_uint64, _u32p, C.c_uint64,
+                                    _u8p, _u8p]
+        L._al = True
+    return L
+
+
+def _pairs(pairs):
+    return np.ascontiguousarray(np.asarray(pairs, dtype=np.int64).reshape(-1, 4).astype(np.int32).view(np.uint32))
+
+
+def gapfree(S, T, pairs):
+    """(n, 4) uint32 [overlap, mismatches, qsum, offset]."""
+    L = _bind_align()
+    p = _pairs(pairs)
+    out = np.zeros((len(p), 4), dtype=np.uint32)
+    sq = S.quals.ctypes.data_as(_u8p) if S.quals is not None else None
+    L.ora_gapfree(*_rs(S), sq, *_rs(T), p.ctypes.data_as(_u32p), len(p), out.ctypes.data_as(_u32p))
+    return out
+
+
+def banded_sw(S, T, pairs, band_w, max_blocks=0):
+    """((n, 8) int32 results, (n, max_blocks, 2) blocks or None)."""
+    L = _bind_align()
+    p = _pairs(pairs)
+    res = np.zeros((len(p), 8), dtype=np.int32)
+    blk = np.zeros((len(p), max_blocks, 2), dtype=np.int32) if max_blocks else None
+    L.ora_banded_sw(*_rs(S), *_rs(T), p.ctypes.data_as(_u32p), len(p), band_w,
+                    res.ctypes.data_as(C.POINTER(C.c_int32)),
+                    blk.ctypes.data_as(C.POINTER(C.c_int32)) if blk is not None else None, max_blocks)
+    return res, blk
+
+
+def consensus(R, T, placements):
+    """(bases, quals), one per base of T."""
+    L = _bind_align()
+    p = _pairs(placements)
+    nt = T.n_bases
+    b = np.zeros(max(nt, 1), dtype=np.uint8)
+    q = np.zeros(max(nt, 1), dtype=np.uint8)
+    L.ora_consensus(*_rs(R), R.quals.ctypes.data_as(_u8p), *_rs(T), T.n_reads, p.ctypes.data_as(_u32p), len(p),
+                    b.ctypes.data_as(_u8p), q.ctypes.data_as(_u8p))
+    return b[:nt], q[:nt]

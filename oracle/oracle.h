@@ -19,4 +19,15 @@ int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* b
 int ork_precorrect_solid(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
                          uint8_t* quals, int K, uint32_t maxq, const uint64_t* solid, uint64_t ns, uint64_t* stats);
 
+void ora_gapfree(const uint64_t* s_base_off, const uint64_t* s_byte_off, const uint8_t* s_packed,
+                 const uint8_t* s_quals, const uint64_t* t_base_off, const uint64_t* t_byte_off,
+                 const uint8_t* t_packed, const uint32_t* pairs, uint64_t n, uint32_t* out);
+void ora_banded_sw(const uint64_t* s_base_off, const uint64_t* s_byte_off, const uint8_t* s_packed,
+                   const uint64_t* t_base_off, const uint64_t* t_byte_off, const uint8_t* t_packed,
+                   const uint32_t* pairs, uint64_t n, int w, int32_t* res, int32_t* blocks, uint32_t max_blocks);
+void ora_consensus(const uint64_t* r_base_off, const uint64_t* r_byte_off, const uint8_t* r_packed,
+                   const uint8_t* r_quals, const uint64_t* t_base_off, const uint64_t* t_byte_off,
+                   const uint8_t* t_packed, uint64_t n_targets, const uint32_t* plc, uint64_t n, uint8_t* cons,
+                   uint8_t* cq);
+
 #endif

@@ -1,0 +1,64 @@
+"""GPU parity: gap-free aligner, banded Smith-Waterman (cost, ends,
+counts, blocks) and column consensus through libapg vs
+oracle/align_oracle.c — exact equality (integer costs: tolerance 0)."""
+import numpy as np
+import pytest
+
+import oracle
+from allpathslg_amd import ReadSet
+from tests.align_cases import sw_case
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gapfree_parity(gpu_ctx):
+    S, T, pairs = sw_case(n_targets=30, n_pairs=3000, seed=21)
+    rng = np.random.default_rng(22)
+    pairs = pairs.copy()
+    pairs[::7, 2] += rng.integers(-300, 300, size=len(pairs[::7]))  # partial / empty overlaps
+    got = gpu_ctx.gapfree(S, T, pairs)
+    exp = oracle.gapfree(S, T, pairs)
+    assert np.array_equal(got, exp)
+    noq = ReadSet(S.base_off, S.byte_off, S.packed, None)
+    assert np.array_equal(gpu_ctx.gapfree(noq, T, pairs), oracle.gapfree(noq, T, pairs))
+
+
+@pytest.mark.parametrize("w", [0, 1, 5, 31, 32, 63, 64, 100, 127])
+def test_banded_sw_parity(gpu_ctx, w):
+    S, T, pairs = sw_case(n_targets=12, n_pairs=500, seed=30 + w)
+    got, gb = gpu_ctx.banded_sw(S, T, pairs, band_w=w, max_blocks=16)
+    exp, eb = oracle.banded_sw(S, T, pairs, band_w=w, max_blocks=16)
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    assert len(bad) == 0, (bad[:5].tolist(), got[bad[:3]].tolist(), exp[bad[:3]].tolist())
+    assert np.array_equal(gb, eb)
+    got2, _ = gpu_ctx.banded_sw(S, T, pairs, band_w=w)  # without a block buffer
+    assert np.array_equal(got2[:, :7], exp[:, :7])
+
+
+def test_banded_sw_long_queries(gpu_ctx):
+    S, T, pairs = sw_case(n_targets=4, n_pairs=120, tlen=3000, slen=(800, 1500), seed=44)
+    got, gb = gpu_ctx.banded_sw(S, T, pairs, band_w=20, max_blocks=40)
+    exp, eb = oracle.banded_sw(S, T, pairs, band_w=20, max_blocks=40)
+    assert np.array_equal(got, exp) and np.array_equal(gb, eb)
+
+
+def test_consensus_parity(gpu_ctx):
+    S, T, pairs = sw_case(n_targets=10, n_pairs=4000, seed=50)
+    plc = pairs.copy()
+    got_b, got_q = gpu_ctx.consensus(S, T, plc)
+    exp_b, exp_q = oracle.consensus(S, T, plc)
+    assert np.array_equal(got_b, exp_b) and np.array_equal(got_q, exp_q)
+    e_b, e_q = gpu_ctx.consensus(S, T, plc[:0])
+    assert np.array_equal(e_b, np.concatenate([T.read(i) for i in range(T.n_reads)])) and not e_q.any()
+
+
+def test_aligner_argument_errors(gpu_ctx):
+    from allpathslg_amd import ApgError
+
+    S, T, pairs = sw_case(n_targets=2, n_pairs=4, seed=60)
+    with pytest.raises(ApgError):
+        gpu_ctx.banded_sw(S, T, pairs, band_w=128)
+    bad = pairs.copy()
+    bad[0, 1] = 99
+    with pytest.raises(ApgError):
+        gpu_ctx.gapfree(S, T, bad)
