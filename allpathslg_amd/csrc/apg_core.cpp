@@ -76,6 +76,12 @@ void kend(apg_ctx* ctx) {
     }
 }
 
+void kbytes_add(apg_ctx* ctx, const char* name, uint64_t bytes) {
+  if (!ctx->timing) return;
+  auto it = ctx->kstats.find(name);
+  if (it != ctx->kstats.end()) it->second.bytes += bytes;
+}
+
 int kflush(apg_ctx* ctx) {
   std::vector<apg_ctx::Pending> open;
   for (auto& p : ctx->pending) {

@@ -154,6 +154,9 @@ int workspace_t(apg_ctx* ctx, const char* name, size_t count, T** out) {
 // Bracket a launch with timing events when ctx->timing.
 void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes);
 void kend(apg_ctx* ctx);
+// Add algorithmic bytes to a timed kernel known only after it ran (e.g. 64 B
+// per random touch counted by the kernel itself); call after a sync.
+void kbytes_add(apg_ctx* ctx, const char* name, uint64_t bytes);
 // Resolve pending events into kstats (call after a stream sync).
 int kflush(apg_ctx* ctx);
 int sync(apg_ctx* ctx);

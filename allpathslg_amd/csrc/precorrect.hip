@@ -107,6 +107,7 @@ __device__ __forceinline__ uint64_t kmer_hash_at(const uint8_t* rd, uint32_t j, 
 
 struct PcCounters {
   unsigned long long suspect, corrected, ambiguous, uncorrectable;
+  unsigned long long lookups;  // solid-table probes (random 64-byte touches)
 };
 
 __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__ base_off,
@@ -219,6 +220,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
   const int lane = lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;  // lane 0's
+  unsigned long long n_look = 0;
   for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave_id(); r < n_reads; r += nwaves) {
     const uint64_t q0 = base_off[r];
     const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
@@ -245,6 +247,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         const uint64_t Wk = window_at(word, jlo + min((uint32_t)lane, nk - 1), hp.mask);
         bool solid = false;
         if ((uint32_t)lane < nk) solid = is_solid(table, tmask, canon_hash(Wk, K, hp));
+        n_look += nk;
         if (__ballot(solid)) continue;
         ++n_sus;
         const uint32_t orig = (__shfl((int)word, (int)(p >> 4), 64) >> (2 * (p & 15))) & 3;
@@ -259,6 +262,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           badA = !is_solid(table, tmask, canon_hash((W0 & ~(3ull << sh0)) | ((uint64_t)alt << sh0), K, hp));
         }
         uint32_t surv = (uint32_t)(~__ballot(badA)) & 7u;
+        n_look += 3 + (uint64_t)__popc(surv) * (nk - 1);
         uint32_t ncand = 0, cand = 0;
         const uint32_t t1 = jlo + 1 + min((uint32_t)lane, nk > 1 ? nk - 2 : 0u);
         const uint64_t W1 = window_at(word, t1, hp.mask);  // every lane joins the shuffles
@@ -298,6 +302,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
     }
   }
   if (lane == 0) {
+    if (n_look) atomicAdd(&cnt->lookups, n_look);
     if (n_sus) atomicAdd(&cnt->suspect, n_sus);
     if (n_cor) atomicAdd(&cnt->corrected, n_cor);
     if (n_amb) atomicAdd(&cnt->ambiguous, n_amb);
@@ -360,9 +365,10 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
                                                  reinterpret_cast<PcCounters*>(dcnt));
   }
   APG_CHECK_HIP(hipGetLastError());
-  unsigned long long h[4];
+  unsigned long long h[5];
   APG_CHECK_HIP(hipMemcpyAsync(h, dcnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
+  kbytes_add(ctx, "precorrect", h[4] * 64);  // one 64-byte line per solid-table probe
   st->n_suspect += h[0];
   st->n_corrected += h[1];
   st->n_ambiguous += h[2];

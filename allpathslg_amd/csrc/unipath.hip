@@ -273,7 +273,7 @@ struct __attribute__((aligned(64))) USlot {
 struct UTab {
   USlot* slot;
   uint64_t T;
-  unsigned long long* ovf;
+  unsigned long long* ovf;  // [0] overflow flag, [1] probes (one 64-byte slot line each)
 };
 
 __device__ __forceinline__ uint64_t tab_home(uint64_t h, uint64_t T) { return __umul64hi(h, T); }
@@ -400,6 +400,7 @@ __global__ void __launch_bounds__(kUThreads) k_uinsert_reads(ReadsV rv, KeyP kp,
   Roller3 ro;
   ro.i = ro.len = 0;
   bool started = false, live = true;
+  unsigned long long n_probe = 0;
   bool pend[kPend], coh[kPend];
   K3 k[kPend];
   uint64_t h[kPend], s[kPend];
@@ -446,9 +447,12 @@ __global__ void __launch_bounds__(kUThreads) k_uinsert_reads(ReadsV rv, KeyP kp,
     for (int q = 0; q < kPend; ++q)
       if (pend[q]) v[q] = slot_read(t.slot + s[q], coh[q]);
 #pragma unroll
-    for (int q = 0; q < kPend; ++q)
+    for (int q = 0; q < kPend; ++q) {
+      n_probe += pend[q];
       if (pend[q] && tab_probe(t, k[q], h[q], e[q], &s[q], &probes[q], &coh[q], v[q])) pend[q] = false;
+    }
   }
+  wave_add(t.ovf + 1, n_probe);
 }
 
 // Insert records (32-byte KRec with extension bits), e.g. received nodes.
@@ -460,6 +464,7 @@ __global__ void __launch_bounds__(kUThreads) k_uinsert_recs(const KRec* __restri
   uint64_t h = 0, s = 0;
   uint32_t e = 0, probes = 0;
   bool coh = false;
+  unsigned long long n_probe = 0;
   for (;;) {
     if (!pend && i < n) {
       const KRec x = rec[i];
@@ -473,8 +478,10 @@ __global__ void __launch_bounds__(kUThreads) k_uinsert_recs(const KRec* __restri
       pend = true;
     }
     if (!__ballot(pend)) break;
+    n_probe += pend;
     if (pend && tab_probe(t, k, h, e, &s, &probes, &coh, slot_read(t.slot + s, coh))) pend = false;
   }
+  wave_add(t.ovf + 1, n_probe);
 }
 
 // Compaction: published slots grouped by the top kUDigitBits hash bits.
@@ -1236,28 +1243,29 @@ static int u_build_nodes(apg_ctx* ctx, const apg_dreads* dr, const KRec* rec, ui
   uint64_t T = std::max<uint64_t>(4096, (uint64_t)(2.0 * est * 1.05) + 1);
   UTab t{};
   unsigned long long* ovf = nullptr;
-  APG_TRY(workspace_t(ctx, "u_tabovf", 1, &ovf));
+  APG_TRY(workspace_t(ctx, "u_tabovf", 2, &ovf));
   for (int attempt = 0;; ++attempt) {
     APG_TRY(workspace_t(ctx, "u_tabslot", T, &t.slot));
     t.T = T;
     t.ovf = ovf;
     APG_CHECK_HIP(hipMemsetAsync(t.slot, 0, T * sizeof(USlot), ctx->stream));
-    APG_CHECK_HIP(hipMemsetAsync(ovf, 0, 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(ovf, 0, 16, ctx->stream));
     if (dr) {
       ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-      kbegin(ctx, "u_insert", dr->n_bytes + 16 * dr->n_reads + (uint64_t)(est * 64));
+      kbegin(ctx, "u_insert", dr->n_bytes + 16 * dr->n_reads);
       if (dr->n_reads) k_uinsert_reads<<<grid_for(ctx, dr->n_reads), kUThreads, 0, ctx->stream>>>(rv, kp, t);
       kend(ctx);
     } else {
-      kbegin(ctx, "u_insert_recs", n_rec * sizeof(KRec) + (uint64_t)(est * 64));
+      kbegin(ctx, "u_insert_recs", n_rec * sizeof(KRec));
       if (n_rec) k_uinsert_recs<<<grid_for(ctx, n_rec), kUThreads, 0, ctx->stream>>>(rec, n_rec, t);
       kend(ctx);
     }
     APG_CHECK_HIP(hipGetLastError());
-    unsigned long long of = 0;
-    APG_CHECK_HIP(hipMemcpyAsync(&of, ovf, 8, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long of[2] = {0, 0};
+    APG_CHECK_HIP(hipMemcpyAsync(of, ovf, 16, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
-    if (!of) break;
+    kbytes_add(ctx, dr ? "u_insert" : "u_insert_recs", of[1] * 64);  // one 64-byte slot line per probe
+    if (!of[0]) break;
     if (attempt >= 6) {
       set_error("unipaths: node table overflow persists");
       return APG_E_STATE;
