@@ -30,6 +30,43 @@ def main():
         out[f"spec_k{K}"] = oracle.spectrum_from_counts(c, 1 << 16)[:4096]
     np.savez_compressed(os.path.join(HERE, "kmer_small.npz"), **out)
     print({k: v.shape for k, v in out.items()})
+    write_stage_fixtures(g, reads)
+
+
+def write_stage_fixtures(g, reads):
+    """PreCorrect / FindErrors, unipaths (K = 31, 96) and aligner outputs of
+    the same inputs (+ the pairs' fragments and a small alignment case)."""
+    from allpathslg_amd import synth_fragments
+    from tests.align_cases import sw_case
+
+    out = {}
+    for cyc in (1, 2):
+        fixed, st = oracle.precorrect(reads, K=24, n_cycles=cyc)
+        out[f"pc{cyc}_packed"] = fixed.packed[: int(fixed.byte_off[-1])]
+        out[f"pc{cyc}_quals"] = fixed.quals
+        out[f"pc{cyc}_stats"] = np.array([st[k] for k in ("n_suspect", "n_corrected", "n_ambiguous",
+                                                           "n_uncorrectable", "n_solid")], np.uint64)
+    frags = synth_fragments(g, 500, seed=0xA11A7 + 1)
+    frags.write_fastb(os.path.join(HERE, "frag_small_fill.fastb"))
+    for K, src in ((31, reads), (96, frags)):
+        gr = oracle.unipaths(src, K)
+        for key in ("len", "id_base", "rc", "ub_off", "unibases", "from", "to", "path_off", "path_start",
+                    "path_len"):
+            out[f"u{K}_{key}"] = np.asarray(gr[key])
+    S, T, pairs = sw_case(n_targets=6, n_pairs=200, tlen=300, slen=(40, 120), seed=7)
+    S.write_fastb(os.path.join(HERE, "aln_queries.fastb"))
+    S.write_qualb(os.path.join(HERE, "aln_queries.qualb"))
+    T.write_fastb(os.path.join(HERE, "aln_targets.fastb"))
+    out["aln_pairs"] = pairs
+    out["aln_gapfree"] = oracle.gapfree(S, T, pairs)
+    res, blk = oracle.banded_sw(S, T, pairs, band_w=8, max_blocks=16)
+    out["aln_sw"] = res
+    out["aln_sw_blocks"] = blk
+    b, q = oracle.consensus(S, T, pairs)
+    out["aln_cons_bases"] = b
+    out["aln_cons_quals"] = q
+    np.savez_compressed(os.path.join(HERE, "stages_small.npz"), **out)
+    print({k: v.shape for k, v in out.items()})
 
 
 if __name__ == "__main__":

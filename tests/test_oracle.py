@@ -161,3 +161,32 @@ def test_precorrect_leaves_high_quality_and_is_idempotent():
         assert np.array_equal(a[qq >= 20], b[qq >= 20])
     again, st2 = oracle.precorrect(fixed, K=24)
     assert st2["n_corrected"] <= st["n_corrected"] // 10
+
+
+def _stage_golden():
+    z = np.load(_golden("stages_small.npz"))
+    reads = ReadSet.load(_golden("frag_small.fastb"), _golden("frag_small.qualb"))
+    frags = ReadSet.load(_golden("frag_small_fill.fastb"))
+    S = ReadSet.load(_golden("aln_queries.fastb"), _golden("aln_queries.qualb"))
+    T = ReadSet.load(_golden("aln_targets.fastb"))
+    return z, reads, frags, S, T
+
+
+def test_oracle_stages_against_golden():
+    """PreCorrect (1, 2 cycles), unipaths (K=31 on reads, K=96 on the pair
+    fragments) and the aligners reproduce the committed fixtures."""
+    z, reads, frags, S, T = _stage_golden()
+    for cyc in (1, 2):
+        fixed, st = oracle.precorrect(reads, K=24, n_cycles=cyc)
+        assert np.array_equal(fixed.packed[: int(fixed.byte_off[-1])], z[f"pc{cyc}_packed"])
+        assert np.array_equal(fixed.quals, z[f"pc{cyc}_quals"])
+    for K, src in ((31, reads), (96, frags)):
+        g = oracle.unipaths(src, K)
+        for key in ("len", "id_base", "rc", "ub_off", "unibases", "from", "to", "path_off", "path_start", "path_len"):
+            assert np.array_equal(np.asarray(g[key]), z[f"u{K}_{key}"]), (K, key)
+    pairs = z["aln_pairs"]
+    assert np.array_equal(oracle.gapfree(S, T, pairs), z["aln_gapfree"])
+    res, blk = oracle.banded_sw(S, T, pairs, band_w=8, max_blocks=16)
+    assert np.array_equal(res, z["aln_sw"]) and np.array_equal(blk, z["aln_sw_blocks"])
+    b, q = oracle.consensus(S, T, pairs)
+    assert np.array_equal(b, z["aln_cons_bases"]) and np.array_equal(q, z["aln_cons_quals"])
