@@ -5,7 +5,9 @@ include/apg.h).  This package is the Python host layer used by tests, the
 benchmark and the multi-GPU driver.
 """
 from ._lib import ApgError, lib  # noqa: F401
-from .engine import DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, shard_bins  # noqa: F401
+from .engine import (  # noqa: F401
+    DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, read_graph, read_kmerpaths, shard_bins,
+    write_graph, write_kspec, write_rc_db)
 from .reads import ReadSet, synth_fragments, synth_genome, synth_reads  # noqa: F401
 
 __all__ = [
@@ -21,4 +23,9 @@ __all__ = [
     "synth_genome",
     "synth_reads",
     "synth_fragments",
+    "read_graph",
+    "read_kmerpaths",
+    "write_graph",
+    "write_kspec",
+    "write_rc_db",
 ]

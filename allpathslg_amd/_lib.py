@@ -133,6 +133,26 @@ class apg_unipath_graph(C.Structure):
 APG_UNIPATH_READ_PATHS = 1
 
 
+APG_RPINT_RC = 1
+
+
+class apg_rpint(C.Structure):
+    _fields_ = [("start", C.c_uint64), ("len", C.c_uint32), ("read", C.c_uint32), ("pos", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
+class apg_rc_db(C.Structure):
+    _fields_ = [
+        ("n_reads", C.c_uint64),
+        ("rc_path_off", C.POINTER(C.c_uint64)),
+        ("n_rc_intervals", C.c_uint64),
+        ("rc_start", C.POINTER(C.c_uint64)),
+        ("rc_len", C.POINTER(C.c_uint64)),
+        ("n_entries", C.c_uint64),
+        ("entries", C.POINTER(apg_rpint)),
+    ]
+
+
 APG_ALN_RC = 1
 
 
@@ -230,6 +250,8 @@ SIGNATURES = {
         [_P, C.c_void_p, C.c_uint64, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),
          C.POINTER(apg_unipath_stats)],
     ),
+    "apg_make_rc_db": (C.c_int, [_P, C.POINTER(apg_unipath_graph), C.POINTER(apg_rc_db)]),
+    "apg_rc_db_free": (None, [C.POINTER(apg_rc_db)]),
     "apg_gapfree": (
         C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64,
                   C.POINTER(apg_gapfree_hit)]),
@@ -251,6 +273,12 @@ SIGNATURES = {
     "apg_qualb_read": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
     "apg_reads_release": (None, [C.POINTER(apg_reads)]),
     "apg_kspec_write": (C.c_int, [C.c_char_p, C.c_int, _u64p, C.c_size_t]),
+    "apg_graph_write": (C.c_int, [C.c_char_p, C.POINTER(apg_unipath_graph)]),
+    "apg_graph_read": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(apg_unipath_graph)]),
+    "apg_kmerpaths_write": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, _u64p, _u64p, _u64p]),
+    "apg_kmerpaths_read": (
+        C.c_int, [C.c_char_p, C.POINTER(C.c_int), _u64p, C.POINTER(_u64p), _u64p, C.POINTER(_u64p), C.POINTER(_u64p)]),
+    "apg_rc_db_write": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(apg_rc_db)]),
 }
 
 _lock = threading.Lock()

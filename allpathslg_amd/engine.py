@@ -280,6 +280,42 @@ class Context:
         finally:
             lib().apg_unipath_graph_free(C.byref(g))
 
+    # -- MakeRcDb ------------------------------------------------------------------
+    def make_rc_db(self, g: dict) -> dict:
+        """rc read paths + the sorted (fw + rc) interval index of a graph dict
+        with read paths (as returned by unipaths()).  entries: structured array
+        (start, len, read, pos, flags)."""
+        from ._lib import apg_rc_db, apg_unipath_graph
+
+        keep = {k: np.ascontiguousarray(g[k], dtype=np.uint64)
+                for k in ("len", "id_base", "rc", "path_off", "path_start", "path_len")}
+        gg = apg_unipath_graph()
+        gg.n_unipaths = len(keep["len"])
+        gg.len = keep["len"].ctypes.data_as(_u64p)
+        gg.id_base = keep["id_base"].ctypes.data_as(_u64p)
+        gg.rc = keep["rc"].ctypes.data_as(_u64p)
+        gg.n_reads = len(keep["path_off"]) - 1
+        gg.path_off = keep["path_off"].ctypes.data_as(_u64p)
+        gg.n_intervals = len(keep["path_start"])
+        gg.path_start = keep["path_start"].ctypes.data_as(_u64p)
+        gg.path_len = keep["path_len"].ctypes.data_as(_u64p)
+        db = apg_rc_db()
+        L = lib()
+        check(L.apg_make_rc_db(self._h, C.byref(gg), C.byref(db)), "apg_make_rc_db")
+        try:
+            n = int(db.n_entries)
+            ent = np.zeros(n, dtype=RPINT_DTYPE)
+            if n:
+                C.memmove(ent.ctypes.data, C.cast(db.entries, C.c_void_p), n * RPINT_DTYPE.itemsize)
+            return {
+                "rc_path_off": _arr(db.rc_path_off, int(db.n_reads) + 1, np.uint64),
+                "rc_start": _arr(db.rc_start, int(db.n_rc_intervals), np.uint64),
+                "rc_len": _arr(db.rc_len, int(db.n_rc_intervals), np.uint64),
+                "entries": ent,
+            }
+        finally:
+            L.apg_rc_db_free(C.byref(db))
+
     # -- alignment and consensus (SURVEY §A.7) ----------------------------------
     @staticmethod
     def _pairs(pairs) -> np.ndarray:
@@ -351,6 +387,9 @@ class Context:
         return hist, st.as_dict()
 
 
+RPINT_DTYPE = np.dtype([("start", "<u8"), ("len", "<u4"), ("read", "<u4"), ("pos", "<u4"), ("flags", "<u4")])
+
+
 def _arr(p, n, dt):
     return np.ctypeslib.as_array(p, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
 
@@ -381,3 +420,83 @@ def graph_arrays(g) -> dict:
 def write_kspec(path: str, K: int, hist: np.ndarray) -> None:
     h = np.ascontiguousarray(hist, dtype=np.uint64)
     check(lib().apg_kspec_write(path.encode(), K, h.ctypes.data_as(_u64p), len(h)), "apg_kspec_write")
+
+
+def _graph_struct(g: dict, K: int):
+    """dict of numpy arrays -> (apg_unipath_graph, arrays kept alive)."""
+    from ._lib import apg_unipath_graph
+
+    keep = {k: np.ascontiguousarray(g[k], dtype=np.uint64)
+            for k in ("len", "id_base", "rc", "ub_off", "from", "to", "path_off", "path_start", "path_len") if k in g}
+    keep["unibases"] = np.ascontiguousarray(g["unibases"], dtype=np.uint8)
+    s = apg_unipath_graph()
+    s.K = K
+    s.n_nodes = int(g.get("n_nodes", 0))
+    s.n_unipaths = len(keep["len"])
+    s.len = keep["len"].ctypes.data_as(_u64p)
+    s.id_base = keep["id_base"].ctypes.data_as(_u64p)
+    s.rc = keep["rc"].ctypes.data_as(_u64p)
+    s.ub_off = keep["ub_off"].ctypes.data_as(_u64p)
+    s.unibases = keep["unibases"].ctypes.data_as(C.POINTER(C.c_uint8))
+    s.n_vertices = int(g.get("n_vertices", 0))
+    s.frm = keep["from"].ctypes.data_as(_u64p)
+    s.to = keep["to"].ctypes.data_as(_u64p)
+    if "path_off" in keep:
+        s.n_reads = len(keep["path_off"]) - 1
+        s.path_off = keep["path_off"].ctypes.data_as(_u64p)
+        s.n_intervals = len(keep["path_start"])
+        s.path_start = keep["path_start"].ctypes.data_as(_u64p)
+        s.path_len = keep["path_len"].ctypes.data_as(_u64p)
+    return s, keep
+
+
+def write_graph(head: str, g: dict, K: int) -> None:
+    """<head>.unipaths/.unibases/.hkp(/.paths).k<K> (include/apg.h)."""
+    s, _keep = _graph_struct(g, K)
+    check(lib().apg_graph_write(head.encode(), C.byref(s)), "apg_graph_write")
+
+
+def read_graph(head: str, K: int) -> dict:
+    from ._lib import apg_unipath_graph
+
+    s = apg_unipath_graph()
+    check(lib().apg_graph_read(head.encode(), K, C.byref(s)), "apg_graph_read")
+    try:
+        return graph_arrays(s)
+    finally:
+        lib().apg_unipath_graph_free(C.byref(s))
+
+
+def write_rc_db(head: str, K: int, db: dict) -> None:
+    """<head>.paths_rc.k<K> and <head>.pathsdb.k<K>."""
+    from ._lib import apg_rc_db, apg_rpint
+
+    off = np.ascontiguousarray(db["rc_path_off"], dtype=np.uint64)
+    st = np.ascontiguousarray(db["rc_start"], dtype=np.uint64)
+    ln = np.ascontiguousarray(db["rc_len"], dtype=np.uint64)
+    ent = np.ascontiguousarray(db["entries"], dtype=RPINT_DTYPE)
+    s = apg_rc_db()
+    s.n_reads = len(off) - 1
+    s.rc_path_off = off.ctypes.data_as(_u64p)
+    s.n_rc_intervals = len(st)
+    s.rc_start = st.ctypes.data_as(_u64p)
+    s.rc_len = ln.ctypes.data_as(_u64p)
+    s.n_entries = len(ent)
+    s.entries = ent.ctypes.data_as(C.POINTER(apg_rpint))
+    check(lib().apg_rc_db_write(head.encode(), K, C.byref(s)), "apg_rc_db_write")
+
+
+def read_kmerpaths(path: str):
+    """(K, path_off, start, len) of a .paths / .paths_rc file."""
+    K = C.c_int()
+    n, ni = C.c_uint64(), C.c_uint64()
+    po, ps, pl = _u64p(), _u64p(), _u64p()
+    L = lib()
+    check(L.apg_kmerpaths_read(path.encode(), C.byref(K), C.byref(n), C.byref(po), C.byref(ni), C.byref(ps),
+                               C.byref(pl)), "apg_kmerpaths_read")
+    try:
+        return (int(K.value), _arr(po, int(n.value) + 1, np.uint64), _arr(ps, int(ni.value), np.uint64),
+                _arr(pl, int(ni.value), np.uint64))
+    finally:
+        for p in (po, ps, pl):
+            L.apg_free(C.cast(p, C.c_void_p))

@@ -307,6 +307,37 @@ int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes,
                             apg_unipath_stats* stats);
 
 /* ------------------------------------------------------------------------- */
+/* MakeRcDb ([R:M] tagged_rpint; <reads>.paths_rc.kN, <reads>.pathsdb.kN).    */
+/* From a graph with read paths (apg_unipaths with APG_UNIPATH_READ_PATHS):   */
+/*  - rc paths: each read path walked backwards, every id mapped into the rc  */
+/*    partner unipath (offset o of u <-> offset len(u)-1-o of rc(u)),         */
+/*    consecutive ids merged into intervals;                                  */
+/*  - index: every interval of every forward path (read order, interval       */
+/*    order), then every interval of every rc path, stably sorted by start.  */
+/* ------------------------------------------------------------------------- */
+#define APG_RPINT_RC 1u
+typedef struct apg_rpint {
+  uint64_t start; /* first K-mer id of the interval */
+  uint32_t len;
+  uint32_t read;  /* read index */
+  uint32_t pos;   /* interval index within the read's (fw or rc) path */
+  uint32_t flags; /* APG_RPINT_RC: interval of the read's rc path */
+} apg_rpint;
+
+typedef struct apg_rc_db {
+  uint64_t n_reads;
+  uint64_t* rc_path_off;    /* n_reads + 1 */
+  uint64_t n_rc_intervals;
+  uint64_t* rc_start;
+  uint64_t* rc_len;
+  uint64_t n_entries;       /* fw + rc intervals */
+  apg_rpint* entries;       /* sorted by start (stable) */
+} apg_rc_db;
+
+int apg_make_rc_db(apg_ctx* ctx, const apg_unipath_graph* g, apg_rc_db* out);
+void apg_rc_db_free(apg_rc_db* db);
+
+/* ------------------------------------------------------------------------- */
 /* Read-to-unibase alignment and column consensus (restated;    */
 /* semantics unpinned).  Replaces the aligners feeding CRefMerger /          */
 /* LongReadConsensus ([R:M] src/pairwise_aligners/PerfectAlignment*,         */
@@ -425,6 +456,22 @@ int apg_qualb_read(const char* path, apg_reads* inout /* fills quals */);
 void apg_reads_release(apg_reads* r);
 /* Spectrum text file (.kspec): "m\tcount" lines for nonzero bins. */
 int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_len);
+
+/* Unipath-stage files, "APG v0" array containers:
+ *   <head>.unipaths.k<K>  len / id_base / rc per unipath (+ n_nodes)
+ *   <head>.unibases.k<K>  APG-fastb, one sequence per unipath
+ *   <head>.hkp.k<K>       HyperKmerPath: from / to per edge (= unipath), n_vertices
+ *   <head>.paths.k<K>     read KmerPaths (path_off, start, len), if present
+ * apg_graph_read allocates; release with apg_unipath_graph_free. */
+int apg_graph_write(const char* head, const apg_unipath_graph* g);
+int apg_graph_read(const char* head, int K, apg_unipath_graph* g);
+int apg_kmerpaths_write(const char* path, int K, uint64_t n_paths, const uint64_t* path_off,
+                        const uint64_t* start, const uint64_t* len);
+/* outputs malloc'd: release each with apg_free */
+int apg_kmerpaths_read(const char* path, int* K, uint64_t* n_paths, uint64_t** path_off,
+                       uint64_t* n_intervals, uint64_t** start, uint64_t** len);
+/* <head>.paths_rc.k<K> (KmerPaths) and <head>.pathsdb.k<K> (apg_rpint array) */
+int apg_rc_db_write(const char* head, int K, const apg_rc_db* db);
 
 #ifdef __cplusplus
 }

@@ -323,3 +323,44 @@ def consensus(R, T, placements):
     L.ora_consensus(*_rs(R), R.quals.ctypes.data_as(_u8p), *_rs(T), T.n_reads, p.ctypes.data_as(_u32p), len(p),
                     b.ctypes.data_as(_u8p), q.ctypes.data_as(_u8p))
     return b[:nt], q[:nt]
+
+
+def make_rc_db(g):
+    """MakeRcDb restated in numpy / python loops (small cases): rc paths and
+    the stable start-sorted index of fw then rc intervals (include/apg.h)."""
+    ub = np.asarray(g["id_base"], np.int64)
+    ul = np.asarray(g["len"], np.int64)
+    urc = np.asarray(g["rc"], np.int64)
+    off = np.asarray(g["path_off"], np.int64)
+    ps = np.asarray(g["path_start"], np.int64)
+    pl = np.asarray(g["path_len"], np.int64)
+    R = len(off) - 1
+    rc_off, rc_s, rc_l = [0], [], []
+    for r in range(R):
+        ids = []
+        for q in range(off[r], off[r + 1]):
+            ids.extend(range(ps[q], ps[q] + pl[q]))
+        mapped = []
+        for x in reversed(ids):
+            u = int(np.searchsorted(ub, x, side="right") - 1)
+            mapped.append(ub[urc[u]] + ul[u] - 1 - (x - ub[u]))
+        for x in mapped:
+            if rc_l and len(rc_s) > rc_off[-1] and rc_s[-1] + rc_l[-1] == x:
+                rc_l[-1] += 1
+            else:
+                rc_s.append(x)
+                rc_l.append(1)
+        rc_off.append(len(rc_s))
+    ent = []
+    for r in range(R):
+        for q in range(off[r], off[r + 1]):
+            ent.append((ps[q], pl[q], r, q - off[r], 0))
+    for r in range(R):
+        for q in range(rc_off[r], rc_off[r + 1]):
+            ent.append((rc_s[q], rc_l[q], r, q - rc_off[r], 1))
+    order = sorted(range(len(ent)), key=lambda i: ent[i][0])  # stable
+    from allpathslg_amd.engine import RPINT_DTYPE
+
+    arr = np.array([ent[i] for i in order], dtype=RPINT_DTYPE) if ent else np.zeros(0, RPINT_DTYPE)
+    return {"rc_path_off": np.array(rc_off, np.uint64), "rc_start": np.array(rc_s, np.uint64),
+            "rc_len": np.array(rc_l, np.uint64), "entries": arr}

@@ -1,0 +1,227 @@
+// apg_modules.cpp — drop-in command-line modules for RunAllPathsLG's hot
+// path: KmerSpectrum, PreCorrect, FindErrors, CommonPather,
+// Unipather, MakeRcDb.  Same module names and KEY=VALUE argument style as the
+// reference modules ([R:H] ParsedArgs; PRE/DATA/RUN directories); inputs and
+// outputs are files in the RUN directory (APG v0 formats).
+// One binary, dispatched on the name it is invoked under (bin/<Module> are
+// symlinks).  Exit status 0 on success, 1 with a message on any error.
+#include <sys/stat.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../include/apg.h"
+
+namespace {
+
+struct Args {
+  std::string module;
+  std::map<std::string, std::string> kv;
+  std::map<std::string, bool> used;
+
+  std::string get(const std::string& k, const std::string& def) {
+    used[k] = true;
+    auto it = kv.find(k);
+    return it == kv.end() ? def : it->second;
+  }
+  long num(const std::string& k, long def) {
+    const std::string v = get(k, std::to_string(def));
+    char* end = nullptr;
+    const long x = std::strtol(v.c_str(), &end, 10);
+    if (!end || *end) fail("argument " + k + "=" + v + " is not an integer");
+    return x;
+  }
+  [[noreturn]] void fail(const std::string& msg) {
+    std::fprintf(stderr, "%s: FATAL: %s\n", module.c_str(), msg.c_str());
+    std::exit(1);
+  }
+  void check(int rc, const char* what) {
+    if (rc != APG_OK) fail(std::string(what) + " failed: " + apg_last_error());
+  }
+  void finish() {
+    for (const auto& e : kv)
+      if (!used.count(e.first)) fail("unknown argument " + e.first);
+  }
+  std::string run_dir() {
+    // PRE/DATA/RUN as in RunAllPathsLG, or RUN alone as a path
+    const std::string pre = get("PRE", ""), data = get("DATA", ""), run = get("RUN", ".");
+    std::string d = pre;
+    if (!data.empty()) d += (d.empty() ? "" : "/") + data;
+    if (!run.empty()) d += (d.empty() ? "" : "/") + run;
+    return d.empty() ? "." : d;
+  }
+};
+
+bool exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0;
+}
+
+struct Ctx {
+  apg_ctx* c = nullptr;
+  explicit Ctx(Args& a) {
+    apg_config cfg;
+    std::memset(&cfg, 0, sizeof cfg);
+    cfg.device = (int)a.num("DEVICE", 0);
+    cfg.verbose = (int)a.num("VERBOSE", 0);
+    a.check(apg_create(&cfg, &c), "apg_create");
+  }
+  ~Ctx() { apg_destroy(c); }
+};
+
+struct Reads {
+  apg_reads r{};
+  bool quals = false;
+  ~Reads() { apg_reads_release(&r); }
+};
+
+void load_reads(Args& a, const std::string& head, bool need_quals, Reads* out) {
+  const std::string fb = head + ".fastb", qb = head + ".qualb";
+  if (!exists(fb)) a.fail("missing input " + fb);
+  a.check(apg_fastb_read(fb.c_str(), &out->r), "reading .fastb");
+  if (need_quals) {
+    if (!exists(qb)) a.fail("missing input " + qb);
+    apg_reads q{};
+    a.check(apg_qualb_read(qb.c_str(), &q), "reading .qualb");
+    if (q.n_reads != out->r.n_reads) {
+      apg_reads_release(&q);
+      a.fail(".qualb read count differs from .fastb");
+    }
+    out->r.quals = q.quals;  // adopt the quality buffer
+    q.quals = nullptr;
+    apg_reads_release(&q);
+    out->quals = true;
+  }
+}
+
+int kmer_spectrum(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string head = dir + "/" + a.get("READS", "frag_reads_filt");
+  const int K = (int)a.num("K", 25);
+  const long hist_len = a.num("HIST_LEN", 1 << 16);
+  a.finish();
+  Reads rd;
+  load_reads(a, head, false, &rd);
+  Ctx ctx(a);
+  std::vector<uint64_t> hist((size_t)hist_len);
+  apg_kstats st;
+  a.check(apg_kmer_spectrum(ctx.c, &rd.r, K, hist.data(), hist.size(), &st), "apg_kmer_spectrum");
+  const std::string out = head + ".kspec.k" + std::to_string(K);
+  a.check(apg_kspec_write(out.c_str(), K, hist.data(), hist.size()), "writing .kspec");
+  std::printf("%s: %llu reads, %llu %d-mers, %llu distinct -> %s\n", a.module.c_str(),
+              (unsigned long long)rd.r.n_reads, (unsigned long long)st.n_kmers, K, (unsigned long long)st.n_distinct,
+              out.c_str());
+  return 0;
+}
+
+int precorrect(Args& a, uint32_t default_cycles, const char* default_out) {
+  const std::string dir = a.run_dir();
+  const std::string in = dir + "/" + a.get("HEAD_IN", "frag_reads_filt");
+  const std::string out = dir + "/" + a.get("HEAD_OUT", default_out);
+  apg_pc_params p;
+  apg_pc_defaults(&p);
+  p.K = (int)a.num("K", p.K);
+  p.min_solid = (uint32_t)a.num("MIN_SOLID", p.min_solid);
+  p.max_q_suspect = (uint32_t)a.num("MAX_Q_SUSPECT", p.max_q_suspect);
+  p.n_cycles = (uint32_t)a.num("NUM_CYCLES", default_cycles);
+  a.finish();
+  Reads rd;
+  load_reads(a, in, true, &rd);
+  Ctx ctx(a);
+  const uint64_t n = rd.r.n_reads;
+  const uint64_t nbytes = n ? rd.r.byte_off[n] : 0, nbases = n ? rd.r.base_off[n] : 0;
+  std::vector<uint8_t> pk(nbytes + 64), q(nbases + 1);
+  apg_pc_stats st;
+  a.check(apg_precorrect(ctx.c, &rd.r, &p, pk.data(), q.data(), &st), "apg_precorrect");
+  apg_reads o = rd.r;
+  o.packed = pk.data();
+  o.quals = q.data();
+  a.check(apg_fastb_write((out + ".fastb").c_str(), &o), "writing .fastb");
+  a.check(apg_qualb_write((out + ".qualb").c_str(), &o), "writing .qualb");
+  std::printf("%s: %llu reads, %llu suspect, %llu corrected, %llu ambiguous, %llu uncorrectable -> %s.{fastb,qualb}\n",
+              a.module.c_str(), (unsigned long long)n, (unsigned long long)st.n_suspect,
+              (unsigned long long)st.n_corrected, (unsigned long long)st.n_ambiguous,
+              (unsigned long long)st.n_uncorrectable, out.c_str());
+  return 0;
+}
+
+int unipaths(Args& a, bool read_paths) {
+  const std::string dir = a.run_dir();
+  const std::string head = dir + "/" + a.get("READS", "all_reads");
+  apg_unipath_params p;
+  apg_unipath_defaults(&p);
+  p.K = (int)a.num("K", p.K);
+  p.flags = read_paths ? APG_UNIPATH_READ_PATHS : 0;
+  a.finish();
+  Reads rd;
+  load_reads(a, head, false, &rd);
+  Ctx ctx(a);
+  apg_unipath_graph g;
+  apg_unipath_stats st;
+  a.check(apg_unipaths(ctx.c, &rd.r, &p, &g, &st), "apg_unipaths");
+  const int rc = apg_graph_write(head.c_str(), &g);
+  apg_unipath_graph_free(&g);
+  a.check(rc, "writing unipath files");
+  std::printf("%s: K=%d %llu nodes, %llu unipaths, %llu HKP vertices%s -> %s.*.k%d\n", a.module.c_str(), p.K,
+              (unsigned long long)st.n_nodes, (unsigned long long)st.n_unipaths, (unsigned long long)st.n_vertices,
+              read_paths ? ", read paths" : "", head.c_str(), p.K);
+  return 0;
+}
+
+int make_rc_db(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string head = dir + "/" + a.get("READS", "all_reads");
+  const int K = (int)a.num("K", 96);
+  a.finish();
+  apg_unipath_graph g;
+  a.check(apg_graph_read(head.c_str(), K, &g), "reading unipath files (run CommonPather first)");
+  if (!g.path_off) {
+    apg_unipath_graph_free(&g);
+    a.fail("no " + head + ".paths.k" + std::to_string(K) + " (run CommonPather first)");
+  }
+  Ctx ctx(a);
+  apg_rc_db db;
+  int rc = apg_make_rc_db(ctx.c, &g, &db);
+  apg_unipath_graph_free(&g);
+  a.check(rc, "apg_make_rc_db");
+  rc = apg_rc_db_write(head.c_str(), K, &db);
+  const unsigned long long ne = db.n_entries;
+  apg_rc_db_free(&db);
+  a.check(rc, "writing .paths_rc / .pathsdb");
+  std::printf("%s: %llu index entries -> %s.{paths_rc,pathsdb}.k%d\n", a.module.c_str(), ne, head.c_str(), K);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  const char* slash = std::strrchr(argv[0], '/');
+  a.module = slash ? slash + 1 : argv[0];
+  int first = 1;
+  if (a.module == "apg_modules") {  // apg_modules <Module> KEY=VALUE ...
+    if (argc < 2) {
+      std::fprintf(stderr, "usage: apg_modules <KmerSpectrum|PreCorrect|FindErrors|CommonPather|Unipather|MakeRcDb> "
+                           "KEY=VALUE ...\n");
+      return 1;
+    }
+    a.module = argv[1];
+    first = 2;
+  }
+  for (int i = first; i < argc; ++i) {
+    const char* eq = std::strchr(argv[i], '=');
+    if (!eq || eq == argv[i]) a.fail(std::string("argument '") + argv[i] + "' is not KEY=VALUE");
+    a.kv[std::string(argv[i], eq - argv[i])] = eq + 1;
+  }
+  if (a.module == "KmerSpectrum") return kmer_spectrum(a);
+  if (a.module == "PreCorrect") return precorrect(a, 1, "frag_reads_edit");
+  if (a.module == "FindErrors") return precorrect(a, 2, "frag_reads_corr");
+  if (a.module == "CommonPather") return unipaths(a, true);
+  if (a.module == "Unipather") return unipaths(a, false);
+  if (a.module == "MakeRcDb") return make_rc_db(a);
+  a.fail("unknown module");
+}
