@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--cpu-unipath-sample-frags", type=int, default=20_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v7", "traffic.json"),
+                   help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     return p.parse_args()
 
 
@@ -156,6 +158,25 @@ def main():
                    "GBps": (v[2] / max(v[1], 1)) / max(v[0] / max(v[1], 1) * 1e-3, 1e-12) / 1e9}
                for k, v in kt.items()}
 
+    roofline = {
+        "bound": "hbm",
+        "kernel": name,
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": None,
+        "algorithmic_bytes_per_launch": per_launch_bytes,
+        "ms_per_launch": per_launch_ms,
+    }
+    if os.path.exists(a.traffic_json):
+        tj = json.load(open(a.traffic_json))
+        if name in tj:  # PMC FETCH_SIZE/WRITE_SIZE passes of this kernel (separate rocprofv3 runs)
+            t = tj[name]["traffic_bytes_per_launch"]
+            roofline["traffic"] = t
+            roofline["traffic_source"] = os.path.relpath(a.traffic_json, ROOT)
+            roofline["traffic_over_algorithmic"] = t / max(per_launch_bytes, 1)
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         import oracle
@@ -219,17 +240,7 @@ def main():
                 "hbm_used_gb": (total_b - free_b) / 1e9,
                 "parallelism": f"kmer-hash shards x{world} + all_to_all" if world > 1 else "single GPU",
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": name,
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
-                "algorithmic_bytes_per_launch": per_launch_bytes,
-                "ms_per_launch": per_launch_ms,
-            },
+            "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},

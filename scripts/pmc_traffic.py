@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Reduce rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes to per-launch HBM
+traffic per timed kernel (the `traffic` field of bench.py's roofline).
+
+FETCH_SIZE corrections (MI355X_MICROARCH.md, HBM section): wide coalesced
+streaming reads are tallied at half their bytes on gfx950 (x2); random 64-byte
+line reads are tallied exactly — calibrated here on tools/microbench/randread
+(2^28 random lines = 16 GiB read, FETCH_SIZE = 16.0 GiB per launch; see
+calibration_randread.csv).  Kernels are tagged with their access pattern.
+
+  python scripts/pmc_traffic.py profiles/r01_pmc_v7
+writes <dir>/traffic.json.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+# HIP symbol prefix -> (bench timing label, read pattern)
+KERNELS = {
+    "apg::k_uinsert_reads": ("u_insert", "random"),
+    "apg::k_precorrect_wave": ("precorrect", "random"),
+    "void apg::k_part_scatter<unsigned long>": ("p_part_scatter", "stream"),
+    "void apg::k_part_count<unsigned long>": ("p_part_count", "stream"),
+    "apg::k_extract_scatter": ("extract_scatter", "stream"),
+    "apg::k_links": ("u_links", "random"),
+    "apg::k_walk": ("u_walk", "random"),
+}
+
+
+def load(path):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024.0)  # KB -> bytes
+    return agg
+
+
+def main(d):
+    f = load(os.path.join(d, "fetch.csv"))
+    w = load(os.path.join(d, "write.csv"))
+    out = {}
+    for sym, (label, pattern) in KERNELS.items():
+        if sym not in f:
+            continue
+        fetch = sum(f[sym]) / len(f[sym])
+        write = sum(w.get(sym, [0.0])) / max(len(w.get(sym, [])), 1)
+        corr = 2.0 if pattern == "stream" else 1.0
+        out[label] = {"symbol": sym, "pattern": pattern, "launches": len(f[sym]),
+                      "fetch_size_bytes": fetch, "fetch_correction": corr, "write_size_bytes": write,
+                      "traffic_bytes_per_launch": fetch * corr + write}
+    json.dump(out, open(os.path.join(d, "traffic.json"), "w"), indent=1)
+    for k, v in out.items():
+        print(f"{k:16s} {v['traffic_bytes_per_launch'] / 1e9:9.2f} GB/launch ({v['pattern']})")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
