@@ -78,7 +78,35 @@ __global__ void k_solid_insert(const uint64_t* __restrict__ list, uint64_t n, un
   }
 }
 
-__device__ __forceinline__ bool is_solid(const unsigned long long* __restrict__ table, uint64_t tmask, uint64_t h) {
+// The solid set: the exact open-addressing table behind a prefix bitmap —
+// bit i set iff some solid K-mer's hash has top bits i — sized at ~16 bits
+// per solid K-mer (2^30 bits = 128 MiB for the bench's 66 M solid K-mers), so
+// it stays in the 256 MiB Infinity Cache while the exact table (16 B per key)
+// does not.  The hash is a bijective mixer, so prefixes are uniform: a weak
+// K-mer passes with probability ~1/16.  Most queries of the correction are
+// weak K-mers (every K-mer covering a real error, every wrong alternative);
+// the bitmap answers those without touching HBM, and only bitmap hits probe
+// the table.  The bitmap never changes an answer.
+struct SolidSet {
+  const unsigned long long* table;
+  uint64_t tmask;
+  const uint32_t* bitmap;
+  int shift;  // bit index = hash >> shift
+};
+
+__global__ void k_bitmap_insert(const uint64_t* __restrict__ list, uint64_t n, uint32_t* __restrict__ bm, int shift) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = list[i] >> shift;
+    atomicOr(&bm[b >> 5], 1u << (b & 31));
+  }
+}
+
+__device__ __forceinline__ bool bitmap_maybe(const SolidSet& ss, uint64_t h) {
+  const uint64_t b = h >> ss.shift;
+  return (ss.bitmap[b >> 5] >> (b & 31)) & 1;
+}
+
+__device__ __forceinline__ bool table_has(const unsigned long long* __restrict__ table, uint64_t tmask, uint64_t h) {
   uint64_t s = h & tmask;
   for (;;) {
     const unsigned long long x = table[s];
@@ -86,6 +114,13 @@ __device__ __forceinline__ bool is_solid(const unsigned long long* __restrict__ 
     if (x == kSolidEmpty) return false;
     s = (s + 1) & tmask;
   }
+}
+
+// n_tab counts the table probes (filter hits) of the calling lane.
+__device__ __forceinline__ bool is_solid(const SolidSet& ss, uint64_t h, uint32_t* n_tab) {
+  if (!bitmap_maybe(ss, h)) return false;
+  ++*n_tab;
+  return table_has(ss.table, ss.tmask, h);
 }
 
 __device__ __forceinline__ uint32_t get_base(const uint8_t* rd, uint32_t i) { return (rd[i >> 2] >> (2 * (i & 3))) & 3; }
@@ -107,14 +142,16 @@ __device__ __forceinline__ uint64_t kmer_hash_at(const uint8_t* rd, uint32_t j, 
 
 struct PcCounters {
   unsigned long long suspect, corrected, ambiguous, uncorrectable;
-  unsigned long long lookups;  // solid-table probes (random 64-byte touches)
+  unsigned long long lookups;       // solid-set queries (one bitmap line each)
+  unsigned long long table_probes;  // filter hits that probed the exact table (one 64-byte line each)
 };
 
 __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__ base_off,
                                                     const uint64_t* __restrict__ byte_off, uint8_t* __restrict__ packed,
                                                     uint8_t* __restrict__ quals, uint64_t n_reads, int K, HashP hp,
-                                                    uint32_t maxq, const unsigned long long* __restrict__ table,
-                                                    uint64_t tmask, uint32_t min_len, PcCounters* __restrict__ cnt) {
+                                                    uint32_t maxq, SolidSet ss, uint32_t min_len,
+                                                    PcCounters* __restrict__ cnt) {
+  uint32_t n_tab = 0;
   unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads;
        r += (uint64_t)gridDim.x * blockDim.x) {
@@ -129,7 +166,7 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
       const uint32_t jhi = min(p, L - (uint32_t)K);
       bool weak = true;
       for (uint32_t j = jlo; j <= jhi && weak; ++j)
-        if (is_solid(table, tmask, kmer_hash_at(rd, j, K, hp, 0xffffffffu, 0))) weak = false;
+        if (is_solid(ss, kmer_hash_at(rd, j, K, hp, 0xffffffffu, 0), &n_tab)) weak = false;
       if (!weak) continue;
       ++n_sus;
       const uint32_t orig = get_base(rd, p);
@@ -138,7 +175,7 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
         if (alt == orig) continue;
         bool ok = true;
         for (uint32_t j = jlo; j <= jhi && ok; ++j)
-          if (!is_solid(table, tmask, kmer_hash_at(rd, j, K, hp, p, alt))) ok = false;
+          if (!is_solid(ss, kmer_hash_at(rd, j, K, hp, p, alt), &n_tab)) ok = false;
         if (ok) {
           ++ncand;
           cand = alt;
@@ -171,6 +208,7 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
     if (n_amb) atomicAdd(&cnt->ambiguous, n_amb);
     if (n_unc) atomicAdd(&cnt->uncorrectable, n_unc);
   }
+  wave_add(&cnt->table_probes, n_tab);
 }
 
 // ---------------------------------------------------------------------------
@@ -215,8 +253,8 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
                                                          const uint64_t* __restrict__ byte_off,
                                                          uint8_t* __restrict__ packed, uint8_t* __restrict__ quals,
                                                          uint64_t n_reads, int K, HashP hp, uint32_t maxq,
-                                                         const unsigned long long* __restrict__ table, uint64_t tmask,
-                                                         PcCounters* __restrict__ cnt) {
+                                                         SolidSet ss, PcCounters* __restrict__ cnt) {
+  uint32_t n_tab = 0;
   const int lane = lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;  // lane 0's
@@ -246,7 +284,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         // every lane takes part in the shuffles; lanes >= nk repeat the last K-mer
         const uint64_t Wk = window_at(word, jlo + min((uint32_t)lane, nk - 1), hp.mask);
         bool solid = false;
-        if ((uint32_t)lane < nk) solid = is_solid(table, tmask, canon_hash(Wk, K, hp));
+        if ((uint32_t)lane < nk) solid = is_solid(ss, canon_hash(Wk, K, hp), &n_tab);
         n_look += nk;
         if (__ballot(solid)) continue;
         ++n_sus;
@@ -259,7 +297,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         bool badA = false;
         if (lane < 3) {
           const uint32_t alt = (uint32_t)lane + ((uint32_t)lane >= orig ? 1u : 0u);
-          badA = !is_solid(table, tmask, canon_hash((W0 & ~(3ull << sh0)) | ((uint64_t)alt << sh0), K, hp));
+          badA = !is_solid(ss, canon_hash((W0 & ~(3ull << sh0)) | ((uint64_t)alt << sh0), K, hp), &n_tab);
         }
         uint32_t surv = (uint32_t)(~__ballot(badA)) & 7u;
         n_look += 3 + (uint64_t)__popc(surv) * (nk - 1);
@@ -273,7 +311,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           const uint32_t alt = a + (a >= orig ? 1u : 0u);
           bool bad = false;
           if ((uint32_t)lane + 1 < nk)
-            bad = !is_solid(table, tmask, canon_hash((W1 & ~(3ull << sh1)) | ((uint64_t)alt << sh1), K, hp));
+            bad = !is_solid(ss, canon_hash((W1 & ~(3ull << sh1)) | ((uint64_t)alt << sh1), K, hp), &n_tab);
           if (!__ballot(bad)) {
             ++ncand;
             cand = alt;
@@ -301,6 +339,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
       }
     }
   }
+  wave_add(&cnt->table_probes, n_tab);
   if (lane == 0) {
     if (n_look) atomicAdd(&cnt->lookups, n_look);
     if (n_sus) atomicAdd(&cnt->suspect, n_sus);
@@ -346,29 +385,44 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   unsigned long long* table = nullptr;
   APG_TRY(workspace_t(ctx, "pc_table", T, &table));
   APG_CHECK_HIP(hipMemsetAsync(table, 0xff, T * 8, ctx->stream));
-  kbegin(ctx, "solid_insert", n_solid * 8 * 2);
-  if (n_solid) k_solid_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, table, T - 1);
+  // prefix bitmap: 2^mb bits, ~16 bits per solid K-mer, at most one bit per K-mer
+  int mb = 10;
+  while ((1ull << mb) < 16 * n_solid && mb < 2 * p.K) ++mb;
+  if (mb > 2 * p.K) mb = 2 * p.K;
+  uint32_t* bitmap = nullptr;
+  const uint64_t words = std::max<uint64_t>(1, (1ull << mb) / 32);
+  APG_TRY(workspace_t(ctx, "pc_bitmap", words, &bitmap));
+  APG_CHECK_HIP(hipMemsetAsync(bitmap, 0, words * 4, ctx->stream));
+  kbegin(ctx, "solid_insert", n_solid * (8 + 64 + 64));
+  if (n_solid) {
+    k_solid_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, table, T - 1);
+    k_bitmap_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, bitmap, 2 * p.K - mb);
+  }
   kend(ctx);
+  const SolidSet ss{table, T - 1, bitmap, 2 * p.K - mb};
   APG_CHECK_HIP(hipGetLastError());
   const HashP hp = make_hashp(p.K);
   kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases);
   if (dr->n_reads)
     k_precorrect_wave<<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
-        dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, table,
-        T - 1, reinterpret_cast<PcCounters*>(dcnt));
+        dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss,
+        reinterpret_cast<PcCounters*>(dcnt));
   kend(ctx);
   if (dr->max_len > kPcMaxL) {  // reads longer than one wave's registers: thread per read
     const uint64_t rgrid =
         std::max<uint64_t>(1, std::min<uint64_t>((dr->n_reads + 255) / 256, (uint64_t)ctx->n_cu * 32));
     k_precorrect<<<rgrid, 256, 0, ctx->stream>>>(dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals,
-                                                 dr->n_reads, p.K, hp, p.max_q_suspect, table, T - 1, kPcMaxL + 1,
+                                                 dr->n_reads, p.K, hp, p.max_q_suspect, ss, kPcMaxL + 1,
                                                  reinterpret_cast<PcCounters*>(dcnt));
   }
   APG_CHECK_HIP(hipGetLastError());
-  unsigned long long h[5];
+  unsigned long long h[6];
   APG_CHECK_HIP(hipMemcpyAsync(h, dcnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  kbytes_add(ctx, "precorrect", h[4] * 64);  // one 64-byte line per solid-table probe
+  // a bitmap query reads one word of an L3-resident bitmap (counted 4 B); a
+  // table probe is a random 64-byte HBM line
+  kbytes_add(ctx, "precorrect", h[4] * 4 + h[5] * 64);
+  vlog(ctx, "precorrect: %llu solid-set queries, %llu table probes", h[4], h[5]);
   st->n_suspect += h[0];
   st->n_corrected += h[1];
   st->n_ambiguous += h[2];
