@@ -80,6 +80,74 @@ class HipShardBackend:
         return self.ctx.unipaths_from_nodes(nodes.data_ptr(), n_nodes, dreads, K, read_paths=True, fetch=fetch)
 
 
+# Largest message per peer per collective call, in int64 elements (256 MiB).
+# Single RCCL all_to_all messages around 1 GiB were observed to deliver only
+# part of the data on this stack (sharded unipath exchange, 2 GB to self: the
+# second half arrived as zeros), so every bulk exchange is cut into rounds.
+CHUNK_ELEMS = 1 << 25
+
+
+def _rounds(n_max: int, group, dev) -> int:
+    """Number of chunk rounds every rank agrees on."""
+    r = torch.tensor([(n_max + CHUNK_ELEMS - 1) // CHUNK_ELEMS], dtype=torch.int64, device=dev)
+    dist.all_reduce(r, op=dist.ReduceOp.MAX, group=group)
+    return int(r.item())
+
+
+def all_to_all_chunked(recv: torch.Tensor, send: torch.Tensor, out_splits, in_splits, group=None) -> None:
+    """all_to_all_single(recv, send, out_splits, in_splits) in rounds of at
+    most CHUNK_ELEMS elements per peer: round r moves elements
+    [r*C, (r+1)*C) of every peer segment through contiguous staging buffers."""
+    C = CHUNK_ELEMS
+    P = len(in_splits)
+    in_off = np.concatenate([[0], np.cumsum(in_splits)]).astype(np.int64)
+    out_off = np.concatenate([[0], np.cumsum(out_splits)]).astype(np.int64)
+    R = _rounds(max(max(in_splits), max(out_splits), 0), group, send.device)
+    for r in range(R):
+        lo = r * C
+        ins = [int(min(max(in_splits[d] - lo, 0), C)) for d in range(P)]
+        outs = [int(min(max(out_splits[q] - lo, 0), C)) for q in range(P)]
+        pieces = [send[int(in_off[d]) + lo : int(in_off[d]) + lo + ins[d]] for d in range(P) if ins[d]]
+        sbuf = torch.cat(pieces) if pieces else send.new_empty(0)
+        rbuf = recv.new_empty(sum(outs))
+        dist.all_to_all_single(rbuf, sbuf, outs, ins, group=group)
+        pos = 0
+        for q in range(P):
+            if outs[q]:
+                recv[int(out_off[q]) + lo : int(out_off[q]) + lo + outs[q]].copy_(rbuf[pos : pos + outs[q]])
+                pos += outs[q]
+
+
+def all_gather_var(local: torch.Tensor, n_local: int, group=None):
+    """Concatenation over ranks (rank order) of each rank's first n_local
+    elements of `local`, gathered in rounds of at most CHUNK_ELEMS per rank.
+    Returns (tensor, sizes)."""
+    P = dist.get_world_size(group)
+    dev = local.device
+    sizes_t = torch.tensor([n_local], dtype=torch.int64, device=dev)
+    all_sizes = [torch.empty_like(sizes_t) for _ in range(P)]
+    dist.all_gather(all_sizes, sizes_t, group=group)
+    sizes = [int(x.item()) for x in all_sizes]
+    out = local.new_empty(max(sum(sizes), 1))
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    C = CHUNK_ELEMS
+    R = _rounds(max(sizes), group, dev)
+    for r in range(R):
+        lo = r * C
+        m = min(C, max(max(sizes) - lo, 0))
+        part = local.new_zeros(m)
+        mine = min(max(n_local - lo, 0), m)
+        if mine:
+            part[:mine].copy_(local[lo : lo + mine])
+        buf = local.new_empty(m * P)
+        dist.all_gather_into_tensor(buf, part, group=group)
+        for q in range(P):
+            k = min(max(sizes[q] - lo, 0), m)
+            if k:
+                out[int(off[q]) + lo : int(off[q]) + lo + k].copy_(buf[q * m : q * m + k])
+    return out[: sum(sizes)], sizes
+
+
 def _exchange_kmers(backend, reads, K: int, P: int, group):
     """K <= 32 hash records of this rank's reads -> their owner shards.
     Returns (recv tensor, recv_counts [src * B + l1], records sent, received)."""
@@ -98,8 +166,7 @@ def _exchange_kmers(backend, reads, K: int, P: int, group):
     out_splits = recv_counts.reshape(P, B).sum(axis=1).astype(np.int64).tolist()
     recv = backend.alloc(int(sum(out_splits)))
     n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
-    dist.all_to_all_single(recv[:n_out] if n_out else recv[:0], send[:n_in] if n_in else send[:0],
-                           out_splits, in_splits, group=group)
+    all_to_all_chunked(recv, send, out_splits, in_splits, group=group)
     return recv, recv_counts, n_in, n_out
 
 
@@ -144,17 +211,10 @@ def sharded_precorrect(backend, reads, K: int = 24, min_solid: int = 3, max_q_su
         recv, recv_counts, _, _ = _exchange_kmers(backend, reads, K, P, group)
         n_local = backend.shard_solid(recv, recv_counts, K, P, min_solid)
         del recv
-        sizes_t = torch.tensor([n_local], dtype=torch.int64, device=dev)
-        all_sizes = [torch.empty_like(sizes_t) for _ in range(P)]
-        dist.all_gather(all_sizes, sizes_t, group=group)
-        sizes = [int(x.item()) for x in all_sizes]
-        maxn = max(max(sizes), 1)
-        local = backend.alloc(maxn)
+        local = backend.alloc(n_local)
         backend.solid_export(local)
-        gathered = backend.alloc(maxn * P)
-        dist.all_gather_into_tensor(gathered[: maxn * P], local[:maxn], group=group)
-        solid = torch.cat([gathered[maxn * r : maxn * r + sizes[r]] for r in range(P)])
-        del gathered, local
+        solid, sizes = all_gather_var(local, n_local, group=group)
+        del local
         st = backend.precorrect_solid(reads, solid, sum(sizes),
                                       {"K": K, "min_solid": min_solid, "max_q_suspect": max_q_suspect})
         for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
@@ -199,23 +259,16 @@ def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGr
     out_splits = (recv_counts.reshape(P, B).sum(axis=1) * 4).astype(np.int64).tolist()
     n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
     recv = backend.alloc(n_out)
-    dist.all_to_all_single(recv[:n_out], send[:n_in], out_splits, in_splits, group=group)
+    all_to_all_chunked(recv, send, out_splits, in_splits, group=group)
     del send
 
     n_local = backend.ushard_nodes(recv, recv_counts, K, P)
     del recv
-    sizes_t = torch.tensor([n_local], dtype=torch.int64, device=dev)
-    all_sizes = [torch.empty_like(sizes_t) for _ in range(P)]
-    dist.all_gather(all_sizes, sizes_t, group=group)
-    sizes = [int(x.item()) for x in all_sizes]
-    maxn = max(max(sizes), 1)
-    local = backend.alloc(4 * maxn)
+    local = backend.alloc(4 * n_local)
     backend.ushard_export(local)
-    gathered = backend.alloc(4 * maxn * P)
-    dist.all_gather_into_tensor(gathered[: 4 * maxn * P], local[: 4 * maxn], group=group)
-    nodes = torch.cat([gathered[4 * maxn * r : 4 * maxn * r + 4 * sizes[r]] for r in range(P)])
-    del gathered, local
-    graph, st = backend.graph_from_nodes(nodes, sum(sizes), reads, K, fetch)
+    nodes, sizes4 = all_gather_var(local, 4 * n_local, group=group)
+    del local
+    graph, st = backend.graph_from_nodes(nodes, sum(sizes4) // 4, reads, K, fetch)
     inst = torch.tensor([n_inst], dtype=torch.int64, device=dev)
     dist.all_reduce(inst, group=group)
     st = dict(st)

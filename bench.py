@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--cpu-unipath-sample-frags", type=int, default=20_000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--sharded", action="store_true",
+                   help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v7", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -71,6 +73,12 @@ def log(rank, *a):
 
 def main():
     a = parse()
+    # Exactly one JSON line on stdout: libraries (RCCL prints a version banner
+    # on communicator init) write to fd 1 directly, so point fd 1 at stderr and
+    # keep a private handle on the real stdout for the result line.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -78,7 +86,8 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
     torch.cuda.set_device(local)
-    if world > 1:
+    sharded = world > 1 or a.sharded
+    if sharded:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     t0 = time.time()
@@ -97,13 +106,13 @@ def main():
 
     def step():
         ctx.copy_reads(dreads, dsrc)
-        if world == 1:
+        if not sharded:
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
             hist, st = sharded_spectrum(backend, dreads, a.K)
         pst = ust = None
         if not a.spectrum_only:
-            if world == 1:
+            if not sharded:
                 _, pst = ctx.precorrect(dreads, K=a.K_correct)
                 _, ust = ctx.unipaths(dfrags, a.K_unipath, read_paths=True, fetch=False)
             else:
@@ -117,17 +126,17 @@ def main():
     torch.cuda.synchronize()
     ctx.reset_timing()
 
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(a.steps):
         hist, st, pst, ust = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if sharded:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -238,7 +247,7 @@ def main():
                 "unipath_input": "simulator's true pair inserts (oracle fill standing in for FillFragments, "
                                  "SURVEY §8d), generated outside the timed region",
                 "hbm_used_gb": (total_b - free_b) / 1e9,
-                "parallelism": f"kmer-hash shards x{world} + all_to_all" if world > 1 else "single GPU",
+                "parallelism": f"kmer-hash shards x{world} + all_to_all" if sharded else "single GPU",
             },
             "roofline": roofline,
             "kernels": kernels,
@@ -248,13 +257,13 @@ def main():
             "unipath_stats": ust,
             "checks": checks,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     dreads.free()
     dsrc.free()
     if dfrags is not None:
         dfrags.free()
     ctx.close()
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 

@@ -83,10 +83,18 @@ def _free_port():
     return p
 
 
+def _small_chunks():
+    """Force the chunked collectives through many rounds (odd-sized chunks)."""
+    import allpathslg_amd.distributed as D
+
+    D.CHUNK_ELEMS = 4093
+
+
 def _worker(rank, world, port, K, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    _small_chunks()
     try:
         g = synth_genome(100_000, 21)
         reads = synth_reads(g, 4000, seed=22)
@@ -182,6 +190,7 @@ def _uworker(rank, world, port, K, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    _small_chunks()
     try:
         from allpathslg_amd.distributed import sharded_unipaths
         from tests.unipath_cases import noisy_reads
@@ -225,6 +234,7 @@ def _pcworker(rank, world, port, n_cycles, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    _small_chunks()
     try:
         from allpathslg_amd.distributed import sharded_precorrect
 
