@@ -116,6 +116,15 @@ struct apg_ctx {
     uint64_t n_recv = 0;
   } ustate;
 
+  // Super-k-mer plan of the last sk_count (reused by sk_scatter).
+  struct SkState {
+    bool valid = false;
+    uint64_t gen = 0;
+    int K = 0, P = 0;
+    uint32_t G = 0;
+    uint64_t total = 0;
+  } skstate;
+
   // Solid K-mer list of the last apg_shard_solid ("pc_solid" workspace).
   uint64_t n_solid = 0;
   bool solid_valid = false;

@@ -3,16 +3,15 @@
 #pragma once
 
 #include <cstdint>
+#include <vector>
 
 #include "apg_core.hpp"
 
 namespace apg {
 
-// Counting modes: spectrum only; full table (every distinct hash + count, in
-// hash order); solid (only hashes with count >= min_solid, + count,
-// unordered — buckets counted by the global fallback still list every
-// distinct hash, so consumers filter on the count).
-constexpr int kCountSpectrum = 0, kCountTable = 1, kCountSolid = 2;
+// Counting modes of the hash-record pipeline: spectrum only, or the full
+// table (every distinct hash + count, in hash order; apg_kmer_count).
+constexpr int kCountSpectrum = 0, kCountTable = 1;
 
 // Result of the counting pipeline (device pointers into ctx workspaces; valid
 // until the next counting call on the same context).
@@ -28,12 +27,29 @@ struct CountResult {
 
 // Count canonical K-mers (K <= 32) of a device read set.  table = true also
 // materialises the sparse (hash, count) table described in CountResult.
-int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint32_t min_solid, uint64_t* hist,
-                  size_t hist_len, CountResult* res);
+int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint64_t* hist, size_t hist_len,
+                  CountResult* res);
 
-// Table-mode count of records received by shard `P`-way exchange
-// (apg_shard_scatter layout, recv_counts[src * B1 + l1]).
-int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P, int mode,
-                     uint32_t min_solid, CountResult* res);
+// Minimizer-partitioned counting (superkmer.hip), K <= 32.
+struct SK16;
+struct SkResult {
+  uint64_t* solid = nullptr;  // solid mode: hashes with count >= min_solid ("pc_solid" workspace)
+  uint64_t n_solid = 0;
+  uint64_t n_distinct = 0;
+  uint64_t n_overflow_buckets = 0;  // buckets counted by the global-table fallback
+  uint64_t nbuckets = 0;
+  uint64_t n_kmers = 0;
+  uint64_t n_records = 0;
+};
+int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
+             std::vector<uint64_t>* kmer_counts);
+int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
+int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
+                   uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
+                   SkResult* res);
+int sk_spectrum(apg_ctx* ctx, const apg_dreads* dr, int K, bool solid, uint32_t min_solid, uint64_t* hist,
+                size_t hist_len, SkResult* res);
+uint64_t sk_sum_kmers(apg_ctx* ctx, const SK16* recs, uint64_t n, int* rc);
+constexpr int kSkShardBins = 32;  // per-shard digit groups of the exchange (2^kSkDigitBits)
 
 }  // namespace apg

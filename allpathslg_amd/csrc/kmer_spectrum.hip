@@ -177,7 +177,6 @@ struct CountOut {
   uint64_t hist_len;
   unsigned long long* gstats;    // [0] n_distinct, [1] overflow count, [2] max bucket
   uint32_t* ovf_list;
-  uint32_t min_solid;            // SOLID mode
 };
 
 __device__ __forceinline__ void spectrum_add(uint32_t c, uint32_t* lhist, unsigned long long* ghist,
@@ -190,9 +189,8 @@ __device__ __forceinline__ void spectrum_add(uint32_t c, uint32_t* lhist, unsign
     atomicAdd(&ghist[m], 1ull);
 }
 
-// MODE: kCountSpectrum (histogram only), kCountTable (every distinct hash +
-// count, hash order inside the bucket), kCountSolid (only hashes with count
-// >= min_solid, + count, unordered).
+// MODE: kCountSpectrum (histogram only) or kCountTable (every distinct hash +
+// count, hash order inside the bucket).
 template <typename KT, int MODE>
 __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __restrict__ rec,
                                                                 const uint64_t* __restrict__ boff, uint64_t nbuckets,
@@ -284,32 +282,6 @@ __global__ void __launch_bounds__(kCountThreads) k_bucket_count(uint64_t* __rest
             ++nd_sum;
           }
         }
-      } else if (MODE == kCountSolid) {
-        // solid hashes only, compacted to the bucket's front in slot order
-        const uint32_t spt = T / kCountThreads;
-        uint32_t ns = 0;
-        for (uint32_t i = 0; i < spt; ++i) {
-          const uint32_t s = tid * spt + i;
-          if (tkey[s] != EMPTY) {
-            spectrum_add(tcnt[s], lhist, o.ghist, o.hist_len);
-            ++nd_sum;
-            ns += tcnt[s] >= o.min_solid;
-          }
-        }
-        uint32_t d;
-        uint32_t j = block_exclusive_scan<uint32_t>(ns, scan_sm, &d);
-        if (tid == 0) scan_sm[32] = (uint32_t)(v[0] >> 32), scan_sm[33] = (uint32_t)v[0];
-        __syncthreads();
-        const uint64_t prefix = (((uint64_t)scan_sm[32] << 32) | scan_sm[33]) & ~remmask;
-        for (uint32_t i = 0; i < spt; ++i) {
-          const uint32_t s = tid * spt + i;
-          if (tkey[s] != EMPTY && tcnt[s] >= o.min_solid) {
-            o.tab_hash[off + j] = prefix | (uint64_t)tkey[s];
-            o.tab_cnt[off + j] = tcnt[s];
-            ++j;
-          }
-        }
-        if (tid == 0) o.bucket_nd[bkt] = d;
       } else {
         // compact occupied slots to the front of the table (in place)
         const uint32_t spt = T / kCountThreads;
@@ -530,8 +502,8 @@ static int l1_bits(int K, int P) {
 // workspace; extract_scatter reuses it when called for the same (reads, K, P).
 static int check_shards(int K, int n_shards) {
   APG_REQUIRE(K >= 1 && K <= 32, "K must be in [1, 32]");
-  APG_REQUIRE(n_shards >= 1 && n_shards <= 64 && (n_shards & (n_shards - 1)) == 0,
-              "n_shards must be a power of two in [1, 64]");
+  APG_REQUIRE(n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
+              "n_shards must be a power of two in [1, 8]");  // 2^(3 + kSkDigitBits) <= 256 LDS digits
   APG_REQUIRE(2 * K >= ceil_log2((uint64_t)n_shards), "K too small for n_shards");
   return APG_OK;
 }
@@ -597,7 +569,7 @@ static int extract_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, uin
 // grouped by L1 group: recv_counts[src * B1 + l1].  `spare` (may be null) is
 // a library buffer of >= n records that may be overwritten (ping-pong).
 static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const std::vector<uint64_t>& recv_counts,
-                       int K, int P, int mode, uint32_t min_solid, uint64_t* hist, size_t hist_len,
+                       int K, int P, int mode, uint64_t* hist, size_t hist_len,
                        CountResult* res) {
   const bool table = mode != kCountSpectrum;
   const int w = 2 * K, pbits = ceil_log2((uint64_t)P), l1 = l1_bits(K, P);
@@ -679,27 +651,23 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
 
-  CountOut co{rec, tab_cnt, bucket_nd, ghist, hl, gstats, ovf_list, min_solid};
+  CountOut co{rec, tab_cnt, bucket_nd, ghist, hl, gstats, ovf_list};
   const bool narrow = remb <= 31;
   const size_t lds = narrow ? bucket_count_lds<uint32_t>() : bucket_count_lds<unsigned long long>();
   const int per_cu = std::max<int>(1, (int)((160 * 1024) / lds));
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * per_cu * 2));
-  kbegin(ctx, mode == kCountSolid ? "bucket_count_solid" : mode == kCountTable ? "bucket_count_table" : "bucket_count",
+  kbegin(ctx, mode == kCountTable ? "bucket_count_table" : "bucket_count",
          n * 8 + (mode == kCountTable ? n * 12 : 0) + (nb + 1) * 8 + nb * 4);
 #define APG_COUNT_LAUNCH(KT, M) \
   k_bucket_count<KT, M><<<grid, kCountThreads, lds, ctx->stream>>>(rec, boff, nb, remb, co)
   if (narrow) {
     if (mode == kCountTable)
       APG_COUNT_LAUNCH(uint32_t, kCountTable);
-    else if (mode == kCountSolid)
-      APG_COUNT_LAUNCH(uint32_t, kCountSolid);
     else
       APG_COUNT_LAUNCH(uint32_t, kCountSpectrum);
   } else {
     if (mode == kCountTable)
       APG_COUNT_LAUNCH(unsigned long long, kCountTable);
-    else if (mode == kCountSolid)
-      APG_COUNT_LAUNCH(unsigned long long, kCountSolid);
     else
       APG_COUNT_LAUNCH(unsigned long long, kCountSpectrum);
   }
@@ -745,20 +713,8 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   return APG_OK;
 }
 
-int shard_table_impl(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int P, int mode,
-                     uint32_t min_solid, CountResult* res) {
-  APG_TRY(check_shards(K, P));
-  APG_CHECK_HIP(hipSetDevice(ctx->device));
-  const uint32_t B1 = 1u << l1_bits(K, P);
-  std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)P * B1);
-  uint64_t n = 0;
-  for (auto c : rc) n += c;
-  APG_REQUIRE(n == 0 || d_recv, "shard table: d_recv is NULL");
-  return stage_count(ctx, d_recv, nullptr, rc, K, P, mode, min_solid, nullptr, 0, res);
-}
-
-int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint32_t min_solid, uint64_t* hist,
-                  size_t hist_len, CountResult* res) {
+int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint64_t* hist, size_t hist_len,
+                  CountResult* res) {
   APG_REQUIRE(ctx && dr, "spectrum: NULL ctx/reads");
   APG_REQUIRE(K >= 1 && K <= 32, "spectrum: K must be in [1, 32] for the 64-bit path");
   APG_REQUIRE(hist_len == 0 || hist_len >= 2, "spectrum: hist_len must be 0 or >= 2");
@@ -768,7 +724,7 @@ int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint32_t 
   uint64_t* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(ctx->xstate.total, 1), &buf));
   APG_TRY(extract_scatter(ctx, dr, K, 1, buf));
-  return stage_count(ctx, buf, buf, counts, K, 1, mode, min_solid, hist, hist_len, res);
+  return stage_count(ctx, buf, buf, counts, K, 1, mode, hist, hist_len, res);
 }
 
 }  // namespace apg
@@ -787,11 +743,20 @@ uint64_t apg_kmer_unhash(int K, uint64_t hash) {
   return kunhash(make_hashp(K), hash);
 }
 
+static void sk_stats(const SkResult& r, apg_kstats* st) {
+  std::memset(st, 0, sizeof(*st));
+  st->n_kmers = r.n_kmers;
+  st->n_distinct = r.n_distinct;
+  st->n_buckets = r.nbuckets;
+  st->n_overflow = r.n_overflow_buckets;
+}
+
+// Spectrum: the minimizer-partitioned super-k-mer pipeline (superkmer.hip).
 int apg_kmer_spectrum_dev(apg_ctx* ctx, const apg_dreads* reads, int K, uint64_t* hist, size_t hist_len,
                           apg_kstats* stats) {
-  CountResult r;
-  APG_TRY(spectrum_impl(ctx, reads, K, kCountSpectrum, 0, hist, hist_len, &r));
-  if (stats) *stats = r.st;
+  SkResult r;
+  APG_TRY(sk_spectrum(ctx, reads, K, false, 0, hist, hist_len, &r));
+  if (stats) sk_stats(r, stats);
   return APG_OK;
 }
 
@@ -813,7 +778,7 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
   apg_dreads* dr = nullptr;
   APG_TRY(apg_reads_upload(ctx, reads, &dr));
   CountResult r;
-  int rc = spectrum_impl(ctx, dr, K, kCountTable, 0, nullptr, 0, &r);
+  int rc = spectrum_impl(ctx, dr, K, kCountTable, nullptr, 0, &r);
   apg_reads_free(dr);
   if (rc) return rc;
   const uint64_t nd = r.st.n_distinct;
@@ -854,41 +819,44 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
 
 int apg_shard_bins(int K, int n_shards) {
   if (check_shards(K, n_shards) != APG_OK) return APG_E_ARG;
-  return 1 << l1_bits(K, n_shards);
+  return kSkShardBins;
 }
 
 int apg_shard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* send_counts) {
   APG_REQUIRE(ctx && reads && send_counts, "apg_shard_count: NULL argument");
   APG_TRY(check_shards(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
-  std::vector<uint64_t> dc;
-  APG_TRY(extract_count(ctx, reads, K, n_shards, &dc));
-  std::memcpy(send_counts, dc.data(), dc.size() * 8);
+  std::vector<uint64_t> rc, kc;
+  APG_TRY(sk_count(ctx, reads, K, n_shards, &rc, &kc));
+  std::memcpy(send_counts, rc.data(), rc.size() * 8);
   return APG_OK;
 }
 
-int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* d_send) {
+int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, void* d_send) {
   APG_REQUIRE(ctx && reads, "apg_shard_scatter: NULL argument");
   APG_TRY(check_shards(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
-  APG_TRY(extract_scatter(ctx, reads, K, n_shards, d_send));
+  APG_TRY(sk_scatter(ctx, reads, K, n_shards, static_cast<SK16*>(d_send)));
   return sync(ctx);
 }
 
-int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+int apg_shard_spectrum(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                        uint64_t* hist, size_t hist_len, apg_kstats* stats) {
   APG_REQUIRE(ctx && recv_counts, "apg_shard_spectrum: NULL argument");
   APG_TRY(check_shards(K, n_shards));
   APG_REQUIRE(hist_len == 0 || hist_len >= 2, "apg_shard_spectrum: hist_len must be 0 or >= 2");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
-  const uint32_t B1 = 1u << l1_bits(K, n_shards);
-  std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)n_shards * B1);
+  std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)n_shards * kSkShardBins);
   uint64_t n = 0;
   for (auto c : rc) n += c;
   APG_REQUIRE(n == 0 || d_recv, "apg_shard_spectrum: d_recv is NULL");
-  CountResult r;
-  APG_TRY(stage_count(ctx, d_recv, nullptr, rc, K, n_shards, kCountSpectrum, 0, hist, hist_len, &r));
-  if (stats) *stats = r.st;
+  const SK16* recs = static_cast<const SK16*>(d_recv);
+  int err = APG_OK;
+  const uint64_t nk = sk_sum_kmers(ctx, recs, n, &err);
+  APG_TRY(err);
+  SkResult r;
+  APG_TRY(sk_stage_count(ctx, recs, nullptr, rc, nk, K, n_shards, false, 0, hist, hist_len, &r));
+  if (stats) sk_stats(r, stats);
   return APG_OK;
 }
 

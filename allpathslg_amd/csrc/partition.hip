@@ -1,6 +1,7 @@
 // partition.hip — the device-wide scan and the LDS-staged hash-partition
-// level of the k-mer counting pipeline (8-byte records; the level is a
-// template over the record type).  See partition.hpp.
+// level of the k-mer counting pipelines (8-byte hash records and 16-byte
+// super-k-mer records; the level is a template over the record type).  See
+// partition.hpp.
 #include <algorithm>
 #include <string>
 #include <vector>
@@ -292,5 +293,7 @@ int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector
 
 template int part_level<uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&, int, int,
                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SK16>(apg_ctx*, const SK16*, SK16*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
+                              uint64_t*, std::vector<uint64_t>*, const char*);
 
 }  // namespace apg

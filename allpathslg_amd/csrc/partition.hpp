@@ -18,9 +18,18 @@ struct __attribute__((aligned(16))) KRec {
   uint64_t k0, k1, k2, meta;
 };
 
+// 16-byte super-k-mer record (K <= 32 counting, superkmer.hip): w0 = 32-bit
+// minimizer key | n_kmers << 32 | (reserved 8 bits) | bases 0..7 << 48;
+// w1 = bases 8..39 — up to 40 bases, 2-bit LSB-first, starting at the
+// super-k-mer's first base.
+struct __attribute__((aligned(16))) SK16 {
+  uint64_t w0, w1;
+};
+
 // The partition digit source of a record.
 __host__ __device__ inline uint64_t rkey(uint64_t r) { return r; }
 __host__ __device__ inline uint64_t rkey(const KRec& r) { return r.meta; }
+__host__ __device__ inline uint64_t rkey(const SK16& r) { return r.w0 << 32; }  // the minimizer key
 
 constexpr int kMaxLevelBits = 8;  // max digit bits of one partition level (LDS-staged scatter)
 

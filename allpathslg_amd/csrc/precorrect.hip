@@ -24,49 +24,6 @@ namespace apg {
 
 constexpr uint64_t kSolidEmpty = ~0ull;
 
-// Solid hashes per table bucket (one block per bucket).
-__global__ void __launch_bounds__(256) k_bucket_solid(const uint32_t* __restrict__ tab_cnt,
-                                                      const uint64_t* __restrict__ boff,
-                                                      const uint32_t* __restrict__ bucket_nd, uint64_t nbuckets,
-                                                      uint32_t min_solid, uint32_t* __restrict__ nsolid) {
-  __shared__ uint32_t part[4];
-  for (uint64_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
-    const uint64_t off = boff[b];
-    const uint32_t nd = bucket_nd[b];
-    uint32_t local = 0;
-    for (uint32_t i = threadIdx.x; i < nd; i += blockDim.x) local += tab_cnt[off + i] >= min_solid;
-    for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, 64);
-    if (lane_id() == 0) part[wave_id()] = local;
-    __syncthreads();
-    if (threadIdx.x == 0) nsolid[b] = part[0] + part[1] + part[2] + part[3];
-    __syncthreads();
-  }
-}
-
-// Solid hashes in (bucket, table slot) order: list[soff[b] + j].
-__global__ void __launch_bounds__(256) k_solid_collect(const uint64_t* __restrict__ tab_hash,
-                                                       const uint32_t* __restrict__ tab_cnt,
-                                                       const uint64_t* __restrict__ boff,
-                                                       const uint32_t* __restrict__ bucket_nd, uint64_t nbuckets,
-                                                       uint32_t min_solid, const uint64_t* __restrict__ soff,
-                                                       uint64_t* __restrict__ list) {
-  __shared__ uint32_t sm[32];
-  for (uint64_t b = blockIdx.x; b < nbuckets; b += gridDim.x) {
-    const uint64_t off = boff[b];
-    const uint32_t nd = bucket_nd[b];
-    uint64_t out = soff[b];
-    for (uint32_t i0 = 0; i0 < nd; i0 += blockDim.x) {
-      const uint32_t i = i0 + threadIdx.x;
-      const bool keep = i < nd && tab_cnt[off + i] >= min_solid;
-      uint32_t tot;
-      const uint32_t ex = block_exclusive_scan<uint32_t>(keep ? 1u : 0u, sm, &tot);
-      if (keep) list[out + ex] = tab_hash[off + i];
-      out += tot;
-      __syncthreads();
-    }
-  }
-}
-
 // Open-addressing table of a solid hash list (linear probing, load <= 0.5;
 // hashes are uniformly mixed, so the home slot is the hash's low bits).
 __global__ void k_solid_insert(const uint64_t* __restrict__ list, uint64_t n, unsigned long long* __restrict__ table,
@@ -349,31 +306,6 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
   }
 }
 
-// Solid list of a table-mode count into the "pc_solid" workspace.
-static int collect_solid(apg_ctx* ctx, const CountResult& cr, uint32_t min_solid, uint64_t** list, uint64_t* n) {
-  const uint64_t NB = cr.nbuckets;
-  uint32_t* bsolid = nullptr;
-  uint64_t* soff = nullptr;
-  APG_TRY(workspace_t(ctx, "pc_bsolid", std::max<uint64_t>(NB, 1), &bsolid));
-  APG_TRY(workspace_t(ctx, "pc_soff", NB + 1, &soff));
-  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(NB, (uint64_t)ctx->n_cu * 16));
-  if (NB) k_bucket_solid<<<grid, 256, 0, ctx->stream>>>(cr.tab_cnt, cr.boff, cr.bucket_nd, NB, min_solid, bsolid);
-  APG_CHECK_HIP(hipGetLastError());
-  APG_TRY(scan_u32_u64(ctx, bsolid, NB, soff, "pc"));
-  uint64_t ns = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&ns, soff + NB, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
-  APG_TRY(workspace_t(ctx, "pc_solid", std::max<uint64_t>(ns, 1), list));
-  kbegin(ctx, "solid_collect", cr.st.n_distinct * 12 + ns * 8);
-  if (NB)
-    k_solid_collect<<<grid, 256, 0, ctx->stream>>>(cr.rec, cr.tab_cnt, cr.boff, cr.bucket_nd, NB, min_solid, soff,
-                                                   *list);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  *n = ns;
-  return APG_OK;
-}
-
 // One correction pass of every read of `dr` against the solid hash list.
 static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const uint64_t* list, uint64_t n_solid,
                         apg_pc_stats* st) {
@@ -436,13 +368,10 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
 }
 
 static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st) {
-  CountResult cr;
-  APG_TRY(spectrum_impl(ctx, dr, p.K, kCountSolid, p.min_solid, nullptr, 0, &cr));
-  uint64_t* list = nullptr;
-  uint64_t ns = 0;
-  APG_TRY(collect_solid(ctx, cr, p.min_solid, &list, &ns));
+  SkResult sr;
+  APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
   ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
-  return correct_pass(ctx, dr, p, list, ns, st);
+  return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st);
 }
 
 static int check_pc(const apg_pc_params& p) {
@@ -489,13 +418,21 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid: NULL argument");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid: min_solid must be >= 1");
   ctx->solid_valid = false;
-  CountResult cr;
-  APG_TRY(shard_table_impl(ctx, static_cast<const uint64_t*>(d_recv), recv_counts, K, n_shards, kCountSolid, min_solid,
-                           &cr));
-  uint64_t* list = nullptr;
-  uint64_t ns = 0;
-  APG_TRY(collect_solid(ctx, cr, min_solid, &list, &ns));
+  APG_REQUIRE(K >= 1 && K <= 32 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
+              "apg_shard_solid: K must be in [1, 32], n_shards a power of two <= 8");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)n_shards * kSkShardBins);
+  uint64_t n = 0;
+  for (auto c : rc) n += c;
+  APG_REQUIRE(n == 0 || d_recv, "apg_shard_solid: d_recv is NULL");
+  const SK16* recs = static_cast<const SK16*>(d_recv);
+  int err = APG_OK;
+  const uint64_t nk = sk_sum_kmers(ctx, recs, n, &err);
+  APG_TRY(err);
+  SkResult sr;
+  APG_TRY(sk_stage_count(ctx, recs, nullptr, rc, nk, K, n_shards, true, min_solid, nullptr, 0, &sr));
   APG_TRY(sync(ctx));
+  const uint64_t ns = sr.n_solid;
   ctx->n_solid = ns;
   ctx->solid_valid = true;
   *n_solid = ns;

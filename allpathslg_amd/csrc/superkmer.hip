@@ -1,0 +1,753 @@
+// superkmer.hip — minimizer-partitioned k-mer counting for K <= 32 (spectrum
+// and solid-set modes).
+//
+// Same result as the hash-record pipeline of kmer_spectrum.hip (which keeps
+// serving the hash-ordered table of apg_kmer_count), with a fraction of its
+// HBM traffic: instead of one 8-byte hash per K-mer instance, a read is cut
+// into super-k-mers — maximal runs of consecutive K-mers whose minimizer (the
+// smallest hashed canonical m-mer of the K-mer, m = min(K, max(10, min(16, K-8)));
+// m = 16 for K >= 24 keeps a minimizer's genome occurrences near one, since a
+// bucket must hold every distinct K-mer of its minimizers)
+// is the same — and each run travels as ONE 16-byte record holding its bases.
+// Every K-mer has exactly one minimizer, and a K-mer and its reverse
+// complement contain the same canonical m-mers, so all instances of a
+// canonical K-mer land in the partition of its minimizer key.
+//
+//   sk_count / sk_scatter  tiles of reads staged in LDS, one thread per read
+//                          rolling m-mers with a van Herk / Gil-Werman
+//                          window minimum, and the records scattered into 2^D groups of the key's top bits via
+//                          an LDS-staged round (count matrix + scan, no global
+//                          atomics), D = shard bits + kSkDigitBits
+//   part_level<SK16>       LDS-staged partition levels on the key's next bits
+//                          until a bucket holds ~kSkBucketKmers K-mers
+//   sk_bucket              one workgroup per bucket expands its records'
+//                          K-mers into an LDS open-addressing table (full
+//                          64-bit hash keys, CAS insert, atomic count), bins
+//                          the counts into the spectrum and, in solid mode,
+//                          appends hashes with count >= min_solid (one global
+//                          atomic per bucket)
+//   sk_big                 buckets whose distinct K-mers overflow the LDS
+//                          table are counted together in one global table
+// A record's bases: for K-mers [a, a+n) of the read, bases [a, a+n+K-1),
+// n <= 41 - K.  Algorithmic bytes per 100-bp read at K = 25: ~12 records of
+// 16 B (vs 76 x 8 B hash records).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "apg_core.hpp"
+#include "kmer_common.hpp"
+#include "kmer_internal.hpp"
+#include "partition.hpp"
+
+namespace apg {
+
+constexpr int kSkThreads = 256;
+constexpr int kSkMaxBlocks = 2048;
+constexpr int kSkBases = 40;
+constexpr int kSkDigitBits = 5;
+constexpr uint64_t kSkBucketKmers = 2048;  // K-mer instances per bucket the planner aims for
+constexpr uint32_t kSkTab = 2048;          // LDS table slots (u64 canonical K-mer + u32 count)
+constexpr int kSkHistBins = 256;
+
+struct SkP {
+  int K, m, w, maxnk;
+  uint64_t mmask;  // 2m bits
+  HashP hp;
+};
+
+static SkP make_skp(int K) {
+  SkP p;
+  p.K = K;
+  p.m = std::min(K, std::max(10, std::min(16, K - 8)));
+  p.w = K - p.m + 1;
+  p.maxnk = std::min(kSkBases - K + 1, 255);
+  p.mmask = p.m >= 32 ? ~0ull : ((1ull << (2 * p.m)) - 1);
+  p.hp = make_hashp(K);
+  return p;
+}
+
+__device__ __forceinline__ uint64_t sk_rev2(uint64_t x) {
+  x = __builtin_bitreverse64(x);
+  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+}
+
+// 32 bases [j, j+32) of a packed read, LSB-first (12 bytes read from the
+// aligned word holding base j; device read buffers carry slack).
+__device__ __forceinline__ uint64_t sk_lsb64(const uint8_t* rd, uint32_t j) {
+  const uintptr_t addr = (uintptr_t)(rd + (j >> 2));
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(addr & ~(uintptr_t)3);
+  const int sh = (int)(addr & 3) * 8 + 2 * (int)(j & 3);
+  const uint64_t q0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  return sh ? (q0 >> sh) | ((uint64_t)w[2] << (64 - sh)) : q0;
+}
+
+__device__ __forceinline__ uint64_t sk_fmix(uint64_t z) {
+  z = (z ^ (z >> 33)) * 0xff51afd7ed558ccdull;
+  z = (z ^ (z >> 33)) * 0xc4ceb9fe1a85ec53ull;
+  return z ^ (z >> 33);
+}
+
+// Minimizer order of canonical m-mer c (a 32-bit hash).  The partition key
+// of a super-k-mer is a second, bijective mix of its minimizer's order value:
+// minimizers are window minima, so their order values crowd near zero, and
+// partitioning on them directly would overload the low buckets.
+__device__ __forceinline__ uint32_t sk_fmix32(uint32_t v) {  // murmur3 fmix32: a bijection
+  v ^= v >> 16;
+  v *= 0x85ebca6bu;
+  v ^= v >> 13;
+  v *= 0xc2b2ae35u;
+  v ^= v >> 16;
+  return v;
+}
+__device__ __forceinline__ uint32_t mmer_order(uint64_t c) {  // c < 4^20
+  return sk_fmix32(((uint32_t)c ^ 0x2545f491u) ^ ((uint32_t)(c >> 32) * 0x9e3779b1u));
+}
+__device__ __forceinline__ uint32_t part_key(uint32_t v) { return sk_fmix32(v ^ 0x6b43a9b5u); }
+
+struct SkReads {
+  const uint64_t* base_off;
+  const uint64_t* byte_off;
+  const uint8_t* packed;
+  uint64_t n_reads;
+};
+
+__device__ __forceinline__ SK16 make_rec(const uint8_t* rd, uint32_t a, uint32_t n, uint32_t key, int K) {
+  const uint32_t nb = n + (uint32_t)K - 1;  // <= 40
+  uint64_t lo = sk_lsb64(rd, a);
+  uint64_t hi = nb > 32 ? sk_lsb64(rd, a + 32) : 0;
+  if (nb < 32)
+    lo &= (1ull << (2 * nb)) - 1;
+  else
+    hi &= nb == 32 ? 0ull : ((1ull << (2 * (nb - 32))) - 1);
+  SK16 r;
+  r.w0 = (uint64_t)part_key(key) | ((uint64_t)n << 32) | ((lo & 0xffffull) << 48);
+  r.w1 = (lo >> 16) | (hi << 48);
+  return r;
+}
+
+__device__ __forceinline__ void sk_read_range(uint64_t n, uint32_t G, uint32_t b, uint64_t* r0, uint64_t* r1) {
+  *r0 = (n * b) / G;
+  *r1 = (n * (b + 1)) / G;
+}
+
+// A tile: up to kSkThreads consecutive reads whose packed bytes (plus the
+// 12-byte window overrun) fit kSkTileBytes, copied into LDS with one
+// coalesced pass so the walk below never waits on HBM.  A read too long for
+// a tile is walked from global memory on its own.
+constexpr uint32_t kSkTileBytes = 8192;
+constexpr int kSkMaxW = 17;  // w = K - m + 1 <= 17 for K <= 32
+struct SkTile {
+  uint32_t words[kSkTileBytes / 4];
+  uint32_t rlen[kSkThreads];
+  uint32_t rbo[kSkThreads];  // byte offset of the read in `words`
+};
+
+// Loads the tile starting at read t0 (< r1); returns its read count, or 0
+// when read t0 alone exceeds a tile.  Block-uniform; ends with a barrier.
+__device__ __forceinline__ uint32_t sk_load_tile(const SkReads& rv, uint64_t t0, uint64_t r1, SkTile& T) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t b0 = rv.byte_off[t0] & ~3ull;
+  const uint64_t r = t0 + tid;
+  bool fits = false;
+  if (r < r1) {
+    const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+    const uint64_t bo = rv.byte_off[r] - b0;
+    fits = bo + (len + 3) / 4 + 12 <= kSkTileBytes;
+    T.rlen[tid] = len;
+    T.rbo[tid] = (uint32_t)bo;
+  }
+  const uint32_t n = (uint32_t)__syncthreads_count(fits);
+  if (n) {
+    const uint32_t nw = (T.rbo[n - 1] + (T.rlen[n - 1] + 3) / 4 + 12 + 3) / 4;
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(rv.packed + b0);
+    for (uint32_t i = tid; i < nw; i += kSkThreads) T.words[i] = g[i];
+  }
+  __syncthreads();
+  return n;
+}
+
+// One thread per read of the tile (a GLOBAL tile: thread 0 walks the one long
+// read from HBM).  The read is rolled base by base (fw / rc m-mer, order of
+// the canonical one); the minimum of each window of w orders comes from the
+// van Herk / Gil-Werman block scheme — orders are taken in blocks of w, the
+// finished block is turned into suffix minima in this thread's LDS column
+// (sb[t * kSkThreads], conflict-free), and window [i, i+w-1] = min(suffix of
+// block k-1 from i, prefix of block k up to i+w-1) — so every lane does the
+// same work per base with no rescans.  f(rd, a, n, key) per record: K-mers
+// [a, a+n) sharing minimizer order `key`, n <= maxnk.
+template <bool GLOBAL, typename F>
+__device__ __forceinline__ void sk_walk(const SkReads& rv, const SkP& p, const SkTile& T, uint64_t t0, uint32_t n,
+                                        uint32_t* sb, F f) {
+  const uint32_t q = threadIdx.x;
+  if (q >= (GLOBAL ? 1u : n)) return;
+  const uint32_t L = T.rlen[q];
+  if (L < (uint32_t)p.K) return;
+  const uint8_t* rd = GLOBAL ? rv.packed + rv.byte_off[t0] : reinterpret_cast<const uint8_t*>(T.words) + T.rbo[q];
+  const uint32_t w = (uint32_t)p.w, m = (uint32_t)p.m, maxnk = (uint32_t)p.maxnk;
+  const int rsh = 2 * p.m - 2;
+  uint64_t fw = 0, rc = 0;
+  uint32_t byte = 0, pre = 0, t = 0, key = 0, ra = 0, rn = 0;
+  for (uint32_t j = 0; j < L; ++j) {  // base j
+    if ((j & 3) == 0) byte = rd[j >> 2];
+    const uint64_t b = (byte >> (2 * (j & 3))) & 3;
+    fw = ((fw << 2) | b) & p.mmask;
+    rc = (rc >> 2) | ((3 - b) << rsh);
+    if (j + 1 < m) continue;
+    const uint32_t v = mmer_order(fw < rc ? fw : rc);  // m-mer x = j + 1 - m, offset t in its block
+    pre = t == 0 ? v : min(pre, v);
+    const uint32_t suf = t + 1 < w ? sb[(t + 1) * kSkThreads] : 0xffffffffu;
+    sb[t * kSkThreads] = v;
+    const uint32_t x = j + 1 - m;
+    if (x + 1 >= w) {  // K-mer i = x + 1 - w
+      const uint32_t kk = min(suf, pre);
+      if (x + 1 == w) {
+        key = kk;
+        ra = 0;
+        rn = 1;
+      } else if (kk == key && rn < maxnk) {
+        ++rn;
+      } else {
+        f(rd, ra, rn, key);
+        key = kk;
+        ra = x + 1 - w;
+        rn = 1;
+      }
+    }
+    if (++t == w) {  // block done: suffix minima in place
+      for (int u = (int)w - 2; u >= 0; --u) sb[u * kSkThreads] = min(sb[u * kSkThreads], sb[(u + 1) * kSkThreads]);
+      t = 0;
+    }
+  }
+  f(rd, ra, rn, key);
+}
+
+// cmat[digit * G + block] = records of `block` with key digit `digit`;
+// kdig[digit] += K-mers of those records.  k_sk_scatter walks the same tiles
+// and reads in the same way, so its per-(digit, block) counts match.
+__global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int D, uint32_t* __restrict__ cmat,
+                                                         unsigned long long* __restrict__ kdig) {
+  __shared__ SkTile T;
+  __shared__ uint32_t hist[256], khist[256];
+  __shared__ uint32_t sbuf[kSkMaxW * kSkThreads];
+  const uint32_t ndig = 1u << D;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
+  uint64_t r0, r1;
+  sk_read_range(rv.n_reads, G, b, &r0, &r1);
+  auto f = [&](const uint8_t*, uint32_t, uint32_t n, uint32_t key) {
+    const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
+    atomicAdd(&hist[d], 1u);
+    atomicAdd(&khist[d], n);
+  };
+  for (uint64_t t0 = r0; t0 < r1;) {
+    const uint32_t n = sk_load_tile(rv, t0, r1, T);
+    if (n)
+      sk_walk<false>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+    else
+      sk_walk<true>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+    __syncthreads();
+    t0 += n ? n : 1;
+  }
+  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) {
+    cmat[(uint64_t)i * G + b] = hist[i];
+    if (khist[i]) atomicAdd(&kdig[i], (unsigned long long)khist[i]);
+  }
+}
+
+// Each record goes straight to the next slot of its digit's run for this
+// block (omat, LDS cursor): the run's size is fixed by k_sk_count, the order
+// inside a run is immaterial to counting.
+__global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, int D,
+                                                           const uint64_t* __restrict__ omat, SK16* __restrict__ out) {
+  __shared__ SkTile T;
+  __shared__ unsigned long long cur[256];
+  __shared__ uint32_t sbuf[kSkMaxW * kSkThreads];
+  const uint32_t ndig = 1u << D;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
+  uint64_t r0, r1;
+  sk_read_range(rv.n_reads, G, b, &r0, &r1);
+  auto f = [&](const uint8_t* rd, uint32_t a, uint32_t n, uint32_t key) {
+    const SK16 x = make_rec(rd, a, n, key, p.K);
+    const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
+    out[atomicAdd(&cur[d], 1ull)] = x;
+  };
+  for (uint64_t t0 = r0; t0 < r1;) {
+    const uint32_t n = sk_load_tile(rv, t0, r1, T);
+    if (n)
+      sk_walk<false>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+    else
+      sk_walk<true>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+    __syncthreads();
+    t0 += n ? n : 1;
+  }
+}
+
+__global__ void k_sk_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig, uint32_t G,
+                                  uint64_t* __restrict__ ds) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d <= ndig) ds[d] = omat[(uint64_t)d * G];
+}
+
+// ---------------------------------------------------------------------------
+// Bucket counting
+// ---------------------------------------------------------------------------
+// Canonical K-mer t (t + K <= 40) of a record: the record's bases as an
+// 80-bit LSB-first string, a 64-bit window at base t, fw = rev2 >> (64 - 2K),
+// rc = complement (already most-significant-first).
+__device__ __forceinline__ uint64_t rec_kmer(const SK16& r, uint32_t t, const SkP& p) {
+  const uint64_t lo = (r.w0 >> 48) | (r.w1 << 16), hi = r.w1 >> 48;
+  const uint32_t sh = 2 * t;
+  const uint64_t W = sh == 0 ? lo : sh < 64 ? (lo >> sh) | (hi << (64 - sh)) : hi >> (sh - 64);
+  const uint64_t fw = sk_rev2(W) >> (64 - 2 * p.K);
+  const uint64_t rc = ~W & p.hp.mask;
+  return fw < rc ? fw : rc;
+}
+
+// Slot of a canonical K-mer in a 2^bits table.
+__device__ __forceinline__ uint32_t sk_slot(uint64_t c, int bits) {
+  return sk_fmix32((uint32_t)c ^ ((uint32_t)(c >> 32) * 0x9e3779b1u)) >> (32 - bits);
+}
+
+struct SkOut {
+  unsigned long long* ghist;  // spectrum
+  uint64_t hist_len;
+  unsigned long long* gstats;  // [0] distinct, [1] overflow buckets, [2] solid written, [3] scratch
+  uint32_t* ovf_list;
+  uint64_t* solid;             // solid mode output: khash of the canonical K-mer
+  uint64_t solid_cap;
+  uint32_t min_solid;
+};
+
+__device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, const SkOut& o) {
+  uint64_t m = c;
+  if (m >= o.hist_len - 1) m = o.hist_len - 1;
+  if (m < (uint64_t)kSkHistBins)
+    atomicAdd(&lhist[m], 1u);
+  else
+    atomicAdd(&o.ghist[m], 1ull);
+}
+
+// One workgroup per bucket (grid-stride).  Records come in chunks of
+// kSkThreads; a block scan of their K-mer counts and an LDS owner map
+// flatten the chunk to one K-mer per thread, inserted into the LDS table
+// keyed by the canonical K-mer (CAS, then count).  The occupied slots feed
+// the spectrum; solid mode appends khash of those with count >= min_solid.
+template <bool SOLID>
+__global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict__ rec,
+                                                          const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
+                                                          SkOut o) {
+  __shared__ unsigned long long tkey[kSkTab];
+  __shared__ uint32_t tcnt[kSkTab];
+  __shared__ uint32_t lhist[kSkHistBins];
+  __shared__ __attribute__((aligned(16))) SK16 crec[kSkThreads];
+  __shared__ uint32_t koff[kSkThreads];
+  __shared__ uint8_t owner[kSkThreads * kSkBases];
+  __shared__ uint32_t scan_sm[64];
+  __shared__ int ovf;
+  __shared__ unsigned long long sbase;
+  constexpr unsigned long long EMPTY = ~0ull;
+  constexpr int TB = __builtin_ctz(kSkTab);
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kSkHistBins; i += kSkThreads) lhist[i] = 0;
+  unsigned long long nd = 0;
+  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
+    const uint64_t off = boff[bkt];
+    const uint32_t nr = (uint32_t)(boff[bkt + 1] - off);
+    if (nr == 0) continue;  // block-uniform
+    for (uint32_t s = tid; s < kSkTab; s += kSkThreads) {
+      tkey[s] = EMPTY;
+      tcnt[s] = 0;
+    }
+    if (tid == 0) ovf = 0;
+    for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
+      uint32_t nk = 0;
+      if (c0 + tid < nr) {
+        const SK16 r = rec[off + c0 + tid];
+        nk = (uint32_t)(r.w0 >> 32) & 0xff;
+        crec[tid] = r;
+      }
+      uint32_t tot;
+      const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);  // barrier: table clear visible
+      koff[tid] = ex;
+      for (uint32_t u = 0; u < nk; ++u) owner[ex + u] = (uint8_t)tid;
+      __syncthreads();
+      for (uint32_t f = tid; f < tot; f += kSkThreads) {
+        const uint32_t i = owner[f];
+        const uint64_t c = rec_kmer(crec[i], f - koff[i], p);
+        uint32_t s = sk_slot(c, TB);
+        for (uint32_t probe = 0;; ++probe) {
+          if (probe == kSkTab) {
+            ovf = 1;  // table full: the bucket goes to the global path
+            break;
+          }
+          const unsigned long long old = atomicCAS(&tkey[s], EMPTY, (unsigned long long)c);
+          if (old == EMPTY || old == c) {
+            atomicAdd(&tcnt[s], 1u);
+            break;
+          }
+          s = (s + 1) & (kSkTab - 1);
+        }
+      }
+      __syncthreads();
+    }
+    if (ovf) {
+      if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+      __syncthreads();
+      continue;
+    }
+    uint32_t ns = 0;
+    for (uint32_t s = tid; s < kSkTab; s += kSkThreads)
+      if (tkey[s] != EMPTY) {
+        sk_spectrum_add(tcnt[s], lhist, o);
+        ++nd;
+        if (SOLID) ns += tcnt[s] >= o.min_solid;
+      }
+    if (SOLID) {
+      uint32_t tot;
+      uint32_t j = block_exclusive_scan<uint32_t>(ns, scan_sm, &tot);
+      if (tid == 0) sbase = tot ? atomicAdd(&o.gstats[2], (unsigned long long)tot) : 0ull;
+      __syncthreads();
+      const unsigned long long b = sbase;
+      for (uint32_t s = tid; s < kSkTab; s += kSkThreads)
+        if (tkey[s] != EMPTY && tcnt[s] >= o.min_solid) {
+          const unsigned long long at = b + j++;
+          if (at < o.solid_cap) o.solid[at] = khash(p.hp, tkey[s]);
+        }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
+  for (uint32_t i = tid; i < lim; i += kSkThreads)
+    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
+  wave_add(&o.gstats[0], nd);
+}
+
+// Overflowed buckets: every K-mer of every overflowed bucket into one global
+// open-addressing table keyed by canonical K-mer (distinct buckets never
+// share a K-mer).
+__global__ void k_sk_big_kmers(const SK16* __restrict__ rec, const uint64_t* __restrict__ boff,
+                               const uint32_t* __restrict__ ovf_list, uint32_t n_ovf,
+                               unsigned long long* __restrict__ n_kmers) {
+  unsigned long long c = 0;
+  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
+    const uint32_t b = ovf_list[q];
+    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) c += (uint32_t)(rec[i].w0 >> 32) & 0xff;
+  }
+  wave_add(n_kmers, c);
+}
+
+__global__ void k_sk_big_insert(const SK16* __restrict__ rec, const uint64_t* __restrict__ boff,
+                                const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, SkP p,
+                                unsigned long long* __restrict__ gkey, uint32_t* __restrict__ gcnt, uint64_t gmask) {
+  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
+    const uint32_t b = ovf_list[q];
+    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
+      const SK16 r = rec[i];
+      const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+      for (uint32_t t = 0; t < n; ++t) {
+        const uint64_t c = rec_kmer(r, t, p);
+        uint64_t s = khash(p.hp, c) & gmask;
+        for (;;) {
+          const unsigned long long old = atomicCAS(&gkey[s], ~0ull, (unsigned long long)c);
+          if (old == ~0ull || old == c) {
+            atomicAdd(&gcnt[s], 1u);
+            break;
+          }
+          s = (s + 1) & gmask;
+        }
+      }
+    }
+  }
+}
+
+template <bool SOLID>
+__global__ void k_sk_big_emit(const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
+                              uint64_t T, SkP p, SkOut o) {
+  __shared__ uint32_t lhist[kSkHistBins];
+  for (uint32_t i = threadIdx.x; i < kSkHistBins; i += blockDim.x) lhist[i] = 0;
+  __syncthreads();
+  unsigned long long nd = 0;
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < T; s += (uint64_t)gridDim.x * blockDim.x) {
+    if (gkey[s] == ~0ull) continue;
+    sk_spectrum_add(gcnt[s], lhist, o);
+    ++nd;
+    if (SOLID && gcnt[s] >= o.min_solid) {
+      const unsigned long long at = atomicAdd(&o.gstats[2], 1ull);
+      if (at < o.solid_cap) o.solid[at] = khash(p.hp, gkey[s]);
+    }
+  }
+  __syncthreads();
+  const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
+  for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x)
+    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
+  wave_add(&o.gstats[0], nd);
+}
+
+// ---------------------------------------------------------------------------
+// host
+// ---------------------------------------------------------------------------
+static int sk_ceil_log2(uint64_t x) {
+  int b = 0;
+  while ((1ull << b) < x) ++b;
+  return b;
+}
+
+static uint32_t sk_blocks(uint64_t n_reads) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kSkMaxBlocks, (n_reads + 255) / 256));
+}
+
+// Pass 1 over reads: per-digit record counts (host) and K-mer counts; leaves
+// the scanned [digit][block] matrix in "sk_omat" for sk_scatter.
+int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
+             std::vector<uint64_t>* kmer_counts) {
+  const SkP p = make_skp(K);
+  const int D = sk_ceil_log2((uint64_t)P) + kSkDigitBits;
+  const uint32_t ndig = 1u << D;
+  const uint32_t G = sk_blocks(dr->n_reads);
+  SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  uint32_t* cmat = nullptr;
+  uint64_t *omat = nullptr, *ds = nullptr;
+  unsigned long long* kdig = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_cmat", (uint64_t)ndig * G, &cmat));
+  APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)ndig * G + 1, &omat));
+  APG_TRY(workspace_t(ctx, "sk_ds", ndig + 1, &ds));
+  APG_TRY(workspace_t(ctx, "sk_kdig", ndig, &kdig));
+  APG_CHECK_HIP(hipMemsetAsync(kdig, 0, ndig * 8, ctx->stream));
+  if (!dr->n_reads) APG_CHECK_HIP(hipMemsetAsync(cmat, 0, (uint64_t)ndig * G * 4, ctx->stream));
+  kbegin(ctx, "sk_count", dr->n_bytes + 16 * dr->n_reads);
+  if (dr->n_reads)
+    k_sk_count<<<G, kSkThreads, 0, ctx->stream>>>(rv, p, D, cmat, kdig);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "sk"));
+  k_sk_digit_starts<<<(ndig + 256) / 256, 256, 0, ctx->stream>>>(omat, ndig, G, ds);
+  std::vector<uint64_t> h(ndig + 1), kd(ndig);
+  APG_CHECK_HIP(hipMemcpyAsync(h.data(), ds, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(kd.data(), kdig, ndig * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  rec_counts->resize(ndig);
+  for (uint32_t d = 0; d < ndig; ++d) (*rec_counts)[d] = h[d + 1] - h[d];
+  *kmer_counts = kd;
+  auto& s = ctx->skstate;
+  s.valid = true;
+  s.gen = dr->gen;
+  s.K = K;
+  s.P = P;
+  s.G = G;
+  s.total = h[ndig];
+  return APG_OK;
+}
+
+int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
+  auto& s = ctx->skstate;
+  if (!s.valid || s.gen != dr->gen || s.K != K || s.P != P) {
+    std::vector<uint64_t> rc, kc;
+    APG_TRY(sk_count(ctx, dr, K, P, &rc, &kc));
+  }
+  const SkP p = make_skp(K);
+  const int D = sk_ceil_log2((uint64_t)P) + kSkDigitBits;
+  SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  uint64_t* omat = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)(1u << D) * s.G + 1, &omat));
+  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * sizeof(SK16));
+  if (dr->n_reads) k_sk_scatter<<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
+// Partition levels + bucket counting of records laid out as P source blocks,
+// each grouped by the kSkDigitBits digit below the shard bits:
+// rec_counts[src * B1 + l1].  `spare` (may be null) is a buffer of >= n
+// records that may be overwritten.  Spectrum into hist (may be null); solid
+// mode leaves the solid hashes in "pc_solid" (res->solid, res->n_solid).
+int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
+                   uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
+                   SkResult* res) {
+  const SkP p = make_skp(K);
+  const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
+  const uint32_t B1 = 1u << l1;
+  if (rec_counts.size() != (size_t)P * B1) {
+    set_error("sk_stage_count: rec_counts has wrong size");
+    return APG_E_ARG;
+  }
+  uint64_t n = 0;
+  for (auto c : rec_counts) n += c;
+  const uint64_t need = std::max<uint64_t>(1, (n_kmers + kSkBucketKmers - 1) / kSkBucketKmers);
+  const int bb = std::min(32 - pbits, std::max(l1, sk_ceil_log2(need)));
+  const int rem = bb - l1;
+  int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  if (nlev == 0 && P > 1) nlev = 1;  // regroup the P source segments
+  std::vector<std::vector<Seg>> parents(B1);
+  {
+    uint64_t pos = 0;
+    for (int s = 0; s < P; ++s)
+      for (uint32_t l = 0; l < B1; ++l) {
+        const uint64_t c = rec_counts[(size_t)s * B1 + l];
+        parents[l].push_back(Seg{pos, c});
+        pos += c;
+      }
+  }
+  SK16 *bufA = nullptr, *bufB = spare;
+  APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1), &bufA));
+  if (!bufB) APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &bufB));
+  uint64_t* boff = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_boff", (1ull << bb) + 1, &boff));
+  const SK16* cur = src;
+  uint64_t nb = B1;
+  int consumed = pbits + l1;
+  if (nlev == 0) {
+    std::vector<uint64_t> hb(B1 + 1, 0);
+    for (uint32_t l = 0; l < B1; ++l) hb[l + 1] = hb[l] + rec_counts[l];
+    APG_CHECK_HIP(hipMemcpyAsync(boff, hb.data(), (B1 + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  }
+  for (int lev = 0; lev < nlev; ++lev) {
+    const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
+    consumed += bits;
+    SK16* dst = (cur == bufA) ? bufB : bufA;
+    std::vector<uint64_t> hb;
+    const bool last = lev + 1 == nlev;
+    APG_TRY(part_level<SK16>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "s"));
+    nb = parents.size() << bits;
+    if (!last) {
+      parents.assign(nb, {});
+      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
+    }
+    cur = dst;
+  }
+  // outputs
+  const uint64_t hl = std::max<uint64_t>(hist_len, 2);
+  unsigned long long *ghist = nullptr, *gstats = nullptr;
+  uint32_t* ovf = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_hist", hl, &ghist));
+  APG_TRY(workspace_t(ctx, "sk_gstats", 4, &gstats));
+  APG_TRY(workspace_t(ctx, "sk_ovf", std::max<uint64_t>(nb, 1), &ovf));
+  APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
+  uint64_t solid_cap = 0;
+  uint64_t* sl = nullptr;
+  if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
+    solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
+    APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
+  }
+  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid};
+  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * 8));
+  for (int attempt = 0;; ++attempt) {
+    kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(SK16) + (nb + 1) * 8);
+    if (solid)
+      k_sk_bucket<true><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+    else
+      k_sk_bucket<false><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    unsigned long long hs[4];
+    APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    if (hs[1]) {  // overflowed buckets: one global table
+      unsigned long long* nk = gstats + 3;
+      APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
+      const uint32_t g2 = (uint32_t)std::min<unsigned long long>(hs[1], (unsigned long long)ctx->n_cu * 8);
+      k_sk_big_kmers<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], nk);
+      unsigned long long nbk = 0;
+      APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      uint64_t T = 1024;
+      while (T < 2 * nbk) T <<= 1;
+      unsigned long long* gkey = nullptr;
+      uint32_t* gcnt = nullptr;
+      APG_TRY(workspace_t(ctx, "sk_gkey", T, &gkey));
+      APG_TRY(workspace_t(ctx, "sk_gcnt", T, &gcnt));
+      APG_CHECK_HIP(hipMemsetAsync(gkey, 0xff, T * 8, ctx->stream));
+      APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
+      vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
+      kbegin(ctx, "sk_bucket_global", nbk * 64);
+      k_sk_big_insert<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1);
+      if (solid)
+        k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+      else
+        k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+      kend(ctx);
+      APG_CHECK_HIP(hipGetLastError());
+      APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+    }
+    if (!solid || hs[2] <= solid_cap) {
+      res->n_distinct = hs[0];
+      res->n_overflow_buckets = hs[1];
+      res->n_solid = solid ? hs[2] : 0;
+      res->solid = sl;
+      res->nbuckets = nb;
+      break;
+    }
+    if (attempt >= 2) {
+      set_error("sk count: solid list overflow persists");
+      return APG_E_STATE;
+    }
+    vlog(ctx, "sk count: %llu solid K-mers exceed the list (%llu), recounting", hs[2], (unsigned long long)solid_cap);
+    solid_cap = hs[2] + hs[2] / 8;
+    APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
+    o.solid = sl;
+    o.solid_cap = solid_cap;
+    APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
+  }
+  if (hist && hist_len) {
+    APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    hist[0] = 0;
+  }
+  res->n_kmers = n_kmers;
+  res->n_records = n;
+  vlog(ctx, "sk count: K=%d P=%d records=%llu kmers=%llu levels=%d buckets=%llu distinct=%llu", K, P,
+       (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
+       (unsigned long long)res->n_distinct);
+  return APG_OK;
+}
+
+__global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {
+  unsigned long long c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    c += (uint32_t)(rec[i].w0 >> 32) & 0xff;
+  wave_add(out, c);
+}
+
+// K-mer instances carried by n records (device).
+uint64_t sk_sum_kmers(apg_ctx* ctx, const SK16* recs, uint64_t n, int* rc) {
+  *rc = APG_OK;
+  unsigned long long* d = nullptr;
+  if ((*rc = workspace_t(ctx, "sk_sum", 1, &d)) != APG_OK) return 0;
+  unsigned long long h = 0;
+  if (hipMemsetAsync(d, 0, 8, ctx->stream) != hipSuccess) {
+    *rc = APG_E_HIP;
+    return 0;
+  }
+  if (n) k_sk_sum_kmers<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(recs, n, d);
+  if (hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess || (*rc = sync(ctx)) != APG_OK) {
+    if (*rc == APG_OK) *rc = APG_E_HIP;
+    return 0;
+  }
+  return h;
+}
+
+// Whole-read-set count (P = 1).
+int sk_spectrum(apg_ctx* ctx, const apg_dreads* dr, int K, bool solid, uint32_t min_solid, uint64_t* hist,
+                size_t hist_len, SkResult* res) {
+  APG_REQUIRE(ctx && dr, "spectrum: NULL ctx/reads");
+  APG_REQUIRE(K >= 1 && K <= 32, "spectrum: K must be in [1, 32] for the 64-bit path");
+  APG_REQUIRE(hist_len == 0 || hist_len >= 2, "spectrum: hist_len must be 0 or >= 2");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::vector<uint64_t> rc, kc;
+  APG_TRY(sk_count(ctx, dr, K, 1, &rc, &kc));
+  uint64_t n = 0, nk = 0;
+  for (auto c : rc) n += c;
+  for (auto c : kc) nk += c;
+  SK16* buf = nullptr;
+  APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
+  APG_TRY(sk_scatter(ctx, dr, K, 1, buf));
+  return sk_stage_count(ctx, buf, buf, rc, nk, K, 1, solid, min_solid, hist, hist_len, res);
+}
+
+}  // namespace apg

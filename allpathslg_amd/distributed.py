@@ -28,6 +28,8 @@ from .engine import DEFAULT_HIST_LEN, Context, DeviceReads, shard_bins
 class HipShardBackend:
     """libapg's sharded stages on this rank's GPU."""
 
+    record_words = 2  # K <= 32 exchange records: 16-byte super-k-mers
+
     def __init__(self, ctx: Context):
         self.ctx = ctx
         self.device = torch.device("cuda", ctx.device)
@@ -149,12 +151,14 @@ def all_gather_var(local: torch.Tensor, n_local: int, group=None):
 
 
 def _exchange_kmers(backend, reads, K: int, P: int, group):
-    """K <= 32 hash records of this rank's reads -> their owner shards.
+    """K <= 32 records of this rank's reads -> their owner shards.  A record
+    is backend.record_words int64 words (libapg: 16-byte super-k-mers).
     Returns (recv tensor, recv_counts [src * B + l1], records sent, received)."""
     B = shard_bins(K, P)
+    W = getattr(backend, "record_words", 1)
     dev = backend.alloc(1).device
     counts = backend.shard_count(reads, K, P)  # [dest * B + l1]
-    send = backend.alloc(int(counts.sum()))
+    send = backend.alloc(W * int(counts.sum()))
     backend.shard_scatter(reads, K, P, send)
 
     cnt_t = torch.from_numpy(counts.astype(np.int64)).to(dev)
@@ -162,10 +166,10 @@ def _exchange_kmers(backend, reads, K: int, P: int, group):
     dist.all_to_all_single(recv_cnt_t, cnt_t, group=group)  # equal splits of B
     recv_counts = recv_cnt_t.cpu().numpy().astype(np.uint64)  # [src * B + l1]
 
-    in_splits = counts.reshape(P, B).sum(axis=1).astype(np.int64).tolist()
-    out_splits = recv_counts.reshape(P, B).sum(axis=1).astype(np.int64).tolist()
+    in_splits = (counts.reshape(P, B).sum(axis=1) * W).astype(np.int64).tolist()
+    out_splits = (recv_counts.reshape(P, B).sum(axis=1) * W).astype(np.int64).tolist()
     recv = backend.alloc(int(sum(out_splits)))
-    n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
+    n_in, n_out = int(sum(in_splits)) // W, int(sum(out_splits)) // W
     all_to_all_chunked(recv, send, out_splits, in_splits, group=group)
     return recv, recv_counts, n_in, n_out
 

@@ -134,23 +134,25 @@ void apg_free(void* p);
 
 /* ------------------------------------------------------------------------- */
 /* Sharded counting (multi-GPU, one process per GPU).  SURVEY §8e.            */
-/* Shard s owns the canonical k-mers whose hash has top log2(P) bits == s;   */
-/* the next log2(B) bits (B = apg_shard_bins(K, P)) are the L1 group.        */
-/* The caller moves bytes between ranks (torch.distributed all_to_all over    */
-/* RCCL/xGMI); libapg only reads and writes device buffers.                   */
-/*   1. apg_shard_count  : counts[s*B + l1] of local reads' records          */
-/*   2. apg_shard_scatter: records grouped by (s, l1) into d_send            */
-/*   3. (caller) all_to_all of counts, then of d_send -> d_recv (src-major) */
-/*   4. apg_shard_spectrum: count this shard's records; recv_counts[src*B+l1]*/
-/* Records are 8-byte hashes.  P must be a power of two, 1 <= P <= 64.       */
-/* Spectra of the shards add up (all_reduce sum) to the global spectrum.     */
+/* Records are 16-byte super-k-mers (runs of consecutive K-mers of a read    */
+/* sharing one minimizer, with their bases).  Shard s owns the  */
+/* K-mers whose minimizer key has top log2(P) bits == s — every instance of  */
+/* a canonical K-mer has the same minimizer — and the next 5 bits are the     */
+/* group (B = apg_shard_bins(K, P) = 32).  The caller moves bytes between     */
+/* ranks (torch.distributed all_to_all over RCCL/xGMI).                       */
+/*   1. apg_shard_count  : counts[s*B + g] of local reads' records           */
+/*   2. apg_shard_scatter: records grouped by (s, g) into d_send (16 B each)  */
+/*   3. (caller) all_to_all of counts, then of d_send -> d_recv (src-major)  */
+/*   4. apg_shard_spectrum: count this shard's K-mers; recv_counts[src*B+g]  */
+/* P must be a power of two, 1 <= P <= 8.  Spectra of the shards add up      */
+/* (all_reduce sum) to the global spectrum.                                  */
 /* ------------------------------------------------------------------------- */
 int apg_shard_bins(int K, int n_shards);
 int apg_shard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
                     uint64_t* counts /* host, n_shards * apg_shard_bins */);
 int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
-                      uint64_t* d_send /* device, sum(counts) records */);
-int apg_shard_spectrum(apg_ctx* ctx, const uint64_t* d_recv,
+                      void* d_send /* device, sum(counts) x 16 bytes */);
+int apg_shard_spectrum(apg_ctx* ctx, const void* d_recv,
                        const uint64_t* recv_counts /* host, n_shards * bins */,
                        int K, int n_shards, uint64_t* hist, size_t hist_len,
                        apg_kstats* stats);
@@ -199,7 +201,7 @@ int apg_reads_download(apg_ctx* ctx, const apg_dreads* reads, uint8_t* packed, u
 
 /* Multi-GPU correction (replicate the solid set, reads stay
  * sharded).  Per pass: apg_shard_count / apg_shard_scatter at K -> all_to_all
- * -> apg_shard_solid (this shard's solid K-mer hashes, in table order) ->
+ * -> apg_shard_solid (this shard's solid K-mer hashes, unordered) ->
  * apg_solid_export into a device buffer -> all_gather -> apg_precorrect_solid
  * on every rank's own reads with the union.  The solid set is a set: the
  * gathered order does not change any result. */

@@ -90,9 +90,48 @@ def test_oversized_buckets_take_global_path(gpu_ctx):
     seqs += [rng.integers(0, 4, size=100) for _ in range(20000)]
     reads = ReadSet.from_sequences(seqs)
     hist, st = assert_spectrum_equal(gpu_ctx, reads, 25)
-    assert st["n_overflow"] > 0
     assert hist[6000] >= 70
     assert_table_equal(gpu_ctx, reads, 25)
+
+
+def _min_mmer(m):
+    """The canonical m-mer with the smallest minimizer order (superkmer.hip's
+    mmer_order: murmur3 fmix32 of (lo ^ salt) ^ (hi * golden))."""
+    v = np.arange(4**m, dtype=np.uint64)
+    rc = np.zeros_like(v)
+    x = v.copy()
+    for _ in range(m):
+        rc = (rc << np.uint64(2)) | (np.uint64(3) - (x & np.uint64(3)))
+        x >>= np.uint64(2)
+    c = np.minimum(v, rc)
+    with np.errstate(over="ignore"):
+        h = ((c & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ np.uint32(0x2545F491)) ^ (
+            (c >> np.uint64(32)).astype(np.uint32) * np.uint32(0x9E3779B1))
+        h ^= h >> np.uint32(16)
+        h *= np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h *= np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+    best = int(v[np.argmin(h)])
+    return np.array([(best >> (2 * (m - 1 - i))) & 3 for i in range(m)], dtype=np.uint8)
+
+
+def test_superkmer_bucket_overflow_takes_global_table(gpu_ctx):
+    """Every K-mer containing the globally smallest m-mer shares one
+    minimizer, hence one partition: thousands of distinct K-mers overflow the
+    LDS table of that bucket and are counted in the global fallback table."""
+    K, m = 16, 10
+    mm = _min_mmer(m)
+    rng = np.random.default_rng(15)
+    seqs = []
+    for _ in range(20000):
+        r = rng.integers(0, 4, size=100).astype(np.uint8)
+        p = int(rng.integers(0, 100 - m))
+        r[p : p + m] = mm
+        seqs.append(r)
+    reads = ReadSet.from_sequences(seqs)
+    hist, st = assert_spectrum_equal(gpu_ctx, reads, K)
+    assert st["n_overflow"] > 0
 
 
 def test_small_hist_len_clamps(gpu_ctx):
@@ -133,7 +172,7 @@ def test_shard_path_loopback(gpu_ctx, P):
         sub = reads.subset(int(idx[0]), int(idx[-1]) + 1)
         d = gpu_ctx.upload(sub)
         c = gpu_ctx.shard_count(d, K, P)
-        buf = torch.empty(max(int(c.sum()), 1), dtype=torch.int64, device="cuda")
+        buf = torch.empty(max(2 * int(c.sum()), 1), dtype=torch.int64, device="cuda")  # 16-byte records
         torch.cuda.synchronize()
         gpu_ctx.shard_scatter(d, K, P, buf.data_ptr())
         sends.append(buf)
@@ -146,7 +185,7 @@ def test_shard_path_loopback(gpu_ctx, P):
         for p in range(P):
             starts = np.concatenate([[0], np.cumsum(counts[p].reshape(-1))]).astype(np.int64)
             a, b = starts[s * B], starts[(s + 1) * B]
-            pieces.append(sends[p][a:b])
+            pieces.append(sends[p][2 * a : 2 * b])
             rc.append(counts[p][s])
         recv = torch.cat(pieces) if sum(x.numel() for x in pieces) else torch.empty(1, dtype=torch.int64, device="cuda")
         torch.cuda.synchronize()
@@ -171,3 +210,5 @@ def test_bad_arguments(gpu_ctx):
     d = gpu_ctx.upload(reads)
     with pytest.raises(ApgError):
         gpu_ctx.shard_count(d, 25, 3)
+    with pytest.raises(ApgError):
+        gpu_ctx.shard_count(d, 25, 16)  # one node: <= 8 shards

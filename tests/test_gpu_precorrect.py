@@ -92,7 +92,7 @@ def test_sharded_solid_loopback(gpu_ctx, P):
     sends, counts = [], []
     for d in dsubs:
         c = gpu_ctx.shard_count(d, K, P)
-        buf = torch.empty(max(int(c.sum()), 1), dtype=torch.int64, device="cuda")
+        buf = torch.empty(max(2 * int(c.sum()), 1), dtype=torch.int64, device="cuda")  # 16-byte records
         torch.cuda.synchronize()
         gpu_ctx.shard_scatter(d, K, P, buf.data_ptr())
         sends.append(buf)
@@ -102,7 +102,7 @@ def test_sharded_solid_loopback(gpu_ctx, P):
         pieces, rc = [], []
         for p in range(P):
             starts = np.concatenate([[0], np.cumsum(counts[p].reshape(-1))]).astype(np.int64)
-            pieces.append(sends[p][starts[s * B] : starts[(s + 1) * B]])
+            pieces.append(sends[p][2 * starts[s * B] : 2 * starts[(s + 1) * B]])
             rc.append(counts[p][s])
         recv = torch.cat(pieces) if sum(x.numel() for x in pieces) else torch.empty(1, dtype=torch.int64, device="cuda")
         torch.cuda.synchronize()
