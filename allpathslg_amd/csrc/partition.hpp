@@ -26,10 +26,21 @@ struct __attribute__((aligned(16))) SK16 {
   uint64_t w0, w1;
 };
 
+// 48-byte super-k-mer record of the K <= 96 unipath node builder
+// (unipath.hip): w0 = 32-bit minimizer key | n_kmers << 32 | flags << 40
+// (bit 0: b[] starts one base before the first K-mer, bit 1: it ends one base
+// after the last — the extension bases); b = up to 160 bases, 2-bit
+// LSB-first.
+struct __attribute__((aligned(16))) SK48 {
+  uint64_t w0;
+  uint64_t b[5];
+};
+
 // The partition digit source of a record.
 __host__ __device__ inline uint64_t rkey(uint64_t r) { return r; }
 __host__ __device__ inline uint64_t rkey(const KRec& r) { return r.meta; }
 __host__ __device__ inline uint64_t rkey(const SK16& r) { return r.w0 << 32; }  // the minimizer key
+__host__ __device__ inline uint64_t rkey(const SK48& r) { return r.w0 << 32; }
 
 constexpr int kMaxLevelBits = 8;  // max digit bits of one partition level (LDS-staged scatter)
 

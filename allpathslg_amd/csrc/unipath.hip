@@ -32,6 +32,7 @@
 #include "apg_core.hpp"
 #include "kmer_common.hpp"
 #include "partition.hpp"
+#include "superkmer.hpp"
 
 namespace apg {
 
@@ -1171,6 +1172,287 @@ __global__ void k_read_paths(ReadsV rv, NodeIdx ni, KeyP kp, const uint32_t* __r
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// U1'-U3' (monolithic builds): distinct nodes through minimizer partitions.
+//
+// Each read is cut into super-k-mers (runs of K-mers sharing the minimizer
+// of their canonical m-mers, m = min(31, max(10, K-8)), superkmer.hpp), and
+// each run travels as one 48-byte record carrying its bases plus the base on
+// either side (the extension bases).  Records are partitioned on the
+// minimizer key (every instance of a canonical K-mer has the same minimizer,
+// so a K-mer never spans two buckets) until a bucket holds ~kUskBucketKmers
+// instances; one workgroup per bucket expands its K-mers into an LDS table
+// keyed by the full 192-bit canonical key (OR of extension bits), and
+// appends the bucket's distinct nodes to the node array — one global atomic
+// per bucket.  At coverage c this replaces c random slot-line accesses per
+// node of the global table (U2) by ~48 / (average run) bytes of sequential
+// record traffic per instance.  A bucket whose distinct K-mers overflow the
+// LDS table (low coverage, repeats) is expanded into instances that go
+// through the U2 table instead.
+// ---------------------------------------------------------------------------
+constexpr int kUskThreads = 128;   // walk workgroups: van Herk columns w x 128 x 4 B of LDS
+constexpr int kUskMaxBlocks = 4096;
+constexpr int kUskBases = 160;     // bases per record
+constexpr int kUskMaxW = 66;       // w = K - m + 1
+constexpr int kUskMaxNk = 63;
+constexpr int kUskDigitBits = 5;
+constexpr uint64_t kUskBucketKmers = 2048;
+constexpr uint32_t kUskTab = 1024;  // LDS table slots: tag u32, key 3 x u64, ext u32
+constexpr int kUskChunk = 128;      // records flattened per round
+constexpr int kUskBThreads = 256;
+
+struct UskP {
+  int K, m, w, maxnk;
+  uint64_t mmask;
+};
+
+static UskP make_uskp(int K) {
+  UskP p;
+  p.K = K;
+  p.m = K <= 10 ? K : std::min(31, std::max(10, K - 8));
+  p.w = K - p.m + 1;
+  p.maxnk = std::min(kUskBases - K - 1, kUskMaxNk);
+  p.mmask = (1ull << (2 * p.m)) - 1;
+  return p;
+}
+
+// Record of K-mers [a, a+n) of a read of length L with minimizer order key.
+__device__ __forceinline__ SK48 make_urec(const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key, int K) {
+  const uint32_t hl = a > 0, end = a + n + (uint32_t)K - 1, hr = end < L;
+  const uint32_t s0 = a - hl, nb = hl + n + (uint32_t)K - 1 + hr;
+  SK48 r;
+  r.w0 = (uint64_t)part_key(key) | ((uint64_t)n << 32) | ((uint64_t)(hl | (hr << 1)) << 40);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t lo = 32 * k;
+    uint64_t x = lo < nb ? sk_lsb64(rd, s0 + lo) : 0;
+    if (nb - lo < 32 && lo < nb) x &= (1ull << (2 * (nb - lo))) - 1;
+    r.b[k] = x;
+  }
+  return r;
+}
+
+// Per-(digit, block) record counts and per-digit K-mer counts.
+__global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, int D, uint32_t* __restrict__ cmat,
+                                                           unsigned long long* __restrict__ kdig) {
+  __shared__ SkTile<kUskThreads> T;
+  __shared__ uint32_t hist[256], khist[256];
+  extern __shared__ uint32_t usk_sb[];
+  const uint32_t ndig = 1u << D;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
+  uint64_t r0, r1;
+  sk_read_range(rv.n_reads, G, b, &r0, &r1);
+  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key) {
+    const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
+    atomicAdd(&hist[d], 1u);
+    atomicAdd(&khist[d], n);
+  };
+  for (uint64_t t0 = r0; t0 < r1;) {
+    const uint32_t n = sk_load_tile<kUskThreads>(rv, t0, r1, T);
+    if (n)
+      sk_walk<kUskThreads, false>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
+    else
+      sk_walk<kUskThreads, true>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
+    __syncthreads();
+    t0 += n ? n : 1;
+  }
+  for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) {
+    cmat[(uint64_t)i * G + b] = hist[i];
+    if (khist[i]) atomicAdd(&kdig[i], (unsigned long long)khist[i]);
+  }
+}
+
+__global__ void __launch_bounds__(kUskThreads) k_usk_scatter(SkReads rv, UskP p, int D,
+                                                             const uint64_t* __restrict__ omat, SK48* __restrict__ out) {
+  __shared__ SkTile<kUskThreads> T;
+  __shared__ unsigned long long cur[256];
+  extern __shared__ uint32_t usk_sb[];
+  const uint32_t ndig = 1u << D;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
+  uint64_t r0, r1;
+  sk_read_range(rv.n_reads, G, b, &r0, &r1);
+  auto f = [&](const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key) {
+    const SK48 x = make_urec(rd, L, a, n, key, p.K);
+    const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
+    out[atomicAdd(&cur[d], 1ull)] = x;
+  };
+  for (uint64_t t0 = r0; t0 < r1;) {
+    const uint32_t n = sk_load_tile<kUskThreads>(rv, t0, r1, T);
+    if (n)
+      sk_walk<kUskThreads, false>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
+    else
+      sk_walk<kUskThreads, true>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
+    __syncthreads();
+    t0 += n ? n : 1;
+  }
+}
+
+__global__ void k_usk_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig, uint32_t G,
+                                   uint64_t* __restrict__ ds) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d <= ndig) ds[d] = omat[(uint64_t)d * G];
+}
+
+// 64 bits of a record's base string from bit `bit` (< 320; zeros past it).
+__device__ __forceinline__ uint64_t urec_bits(const SK48& r, uint32_t bit) {
+  const uint32_t q = bit >> 6, s = bit & 63;
+  const uint64_t lo = r.b[q], hi = q < 4 ? r.b[q + 1] : 0;
+  return s ? (lo >> s) | (hi << (64 - s)) : lo;
+}
+
+// K-mer t of a record (K bases from record base hl + t): canonical key and
+// extension bits in canonical orientation.
+__device__ __forceinline__ void urec_kmer(const SK48& r, uint32_t t, const KeyP& kp, K3* key, uint32_t* ext) {
+  const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff, fl = (uint32_t)(r.w0 >> 40) & 3;
+  const uint32_t hl = fl & 1, hr = fl >> 1;
+  const uint32_t K = (uint32_t)kp.K, nb = hl + n + K - 1 + hr, st = hl + t;
+  const K3 W{urec_bits(r, 2 * st + 128), urec_bits(r, 2 * st + 64), urec_bits(r, 2 * st)};
+  const K3 fw = shr192(K3{rev2(W.c), rev2(W.b), rev2(W.a)}, 192 - 2 * kp.K);
+  const K3 rc{~W.a & kp.ma, ~W.b & kp.mb, ~W.c & kp.mc};
+  const int a = st > 0 ? (int)((r.b[(st - 1) >> 5] >> (2 * ((st - 1) & 31))) & 3) : -1;
+  const int b = st + K < nb ? (int)((r.b[(st + K) >> 5] >> (2 * ((st + K) & 31))) & 3) : -1;
+  canon_ext(fw, rc, a, b, key, ext);
+}
+
+__device__ __forceinline__ uint32_t usk_slot_hash(const K3& k) {
+  const uint64_t x = k.c ^ (k.b * 0x9e3779b97f4a7c15ull) ^ (k.a * 0xc2b2ae3d27d4eb4full);
+  return sk_fmix32((uint32_t)x ^ (uint32_t)(x >> 32));
+}
+
+struct UskOut {
+  KRec* nodes;
+  uint64_t cap;
+  unsigned long long* gs;  // [0] nodes appended, [1] overflowed buckets
+  uint32_t* ovf_list;
+};
+
+// One workgroup per bucket (grid-stride).
+__global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restrict__ rec,
+                                                             const uint64_t* __restrict__ boff, uint64_t nbuckets,
+                                                             KeyP kp, UskOut o) {
+  __shared__ uint32_t tag[kUskTab];
+  __shared__ uint64_t ka[kUskTab], kb[kUskTab], kc[kUskTab];
+  __shared__ uint32_t text[kUskTab];
+  __shared__ __attribute__((aligned(16))) SK48 crec[kUskChunk];
+  __shared__ uint32_t koff[kUskChunk];
+  __shared__ uint8_t owner[kUskChunk * kUskMaxNk];
+  __shared__ uint32_t scan_sm[64];
+  __shared__ int ovf;
+  __shared__ unsigned long long sbase;
+  constexpr int TB = __builtin_ctz(kUskTab);
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
+    const uint64_t off = boff[bkt];
+    const uint32_t nr = (uint32_t)(boff[bkt + 1] - off);
+    if (nr == 0) continue;  // block-uniform
+    for (uint32_t s = tid; s < kUskTab; s += kUskBThreads) tag[s] = 0;
+    if (tid == 0) ovf = 0;
+    for (uint32_t c0 = 0; c0 < nr; c0 += kUskChunk) {
+      uint32_t nk = 0;
+      if (tid < kUskChunk && c0 + tid < nr) {
+        const SK48 r = rec[off + c0 + tid];
+        nk = (uint32_t)(r.w0 >> 32) & 0xff;
+        crec[tid] = r;
+      }
+      uint32_t tot;
+      const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);  // barrier: table clear visible
+      if (tid < kUskChunk) koff[tid] = ex;
+      for (uint32_t u = 0; u < nk; ++u) owner[ex + u] = (uint8_t)tid;
+      __syncthreads();
+      for (uint32_t f = tid; f < tot; f += kUskBThreads) {
+        const uint32_t i = owner[f];
+        K3 key;
+        uint32_t e;
+        urec_kmer(crec[i], f - koff[i], kp, &key, &e);
+        const uint32_t h = usk_slot_hash(key);
+        const uint32_t tv = (h & ~3u) | 2u;
+        uint32_t s = h >> (32 - TB);
+        for (uint32_t probe = 0;;) {
+          uint32_t tg = tag[s];
+          if (tg == 0) {
+            const uint32_t prev = atomicCAS(&tag[s], 0u, 1u);
+            if (prev == 0) {
+              ka[s] = key.a;
+              kb[s] = key.b;
+              kc[s] = key.c;
+              text[s] = e;
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+              __hip_atomic_store(&tag[s], tv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            }
+            tg = prev;
+          }
+          if (tg == 1) continue;  // being written by a lane that publishes in the same pass
+          if (tg == tv && ka[s] == key.a && kb[s] == key.b && kc[s] == key.c) {
+            if (e & ~text[s]) atomicOr(&text[s], e);
+            break;
+          }
+          s = (s + 1) & (kUskTab - 1);
+          if (++probe == kUskTab) {
+            ovf = 1;  // table full: the bucket goes through the global table
+            break;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (ovf) {
+      if (tid == 0) o.ovf_list[atomicAdd(&o.gs[1], 1ull)] = (uint32_t)bkt;
+      __syncthreads();
+      continue;
+    }
+    uint32_t nn = 0;
+    for (uint32_t s = tid; s < kUskTab; s += kUskBThreads) nn += tag[s] != 0;
+    uint32_t tot;
+    uint32_t j = block_exclusive_scan<uint32_t>(nn, scan_sm, &tot);
+    if (tid == 0) sbase = tot ? atomicAdd(&o.gs[0], (unsigned long long)tot) : 0ull;
+    __syncthreads();
+    const unsigned long long b = sbase;
+    for (uint32_t s = tid; s < kUskTab; s += kUskBThreads)
+      if (tag[s] != 0) {
+        const unsigned long long at = b + j++;
+        if (at < o.cap) {
+          const K3 k{ka[s], kb[s], kc[s]};
+          o.nodes[at] = KRec{k.a, k.b, k.c, key_hash(k) | text[s]};
+        }
+      }
+    __syncthreads();
+  }
+}
+
+// Instances of the overflowed buckets as 32-byte KRecs (for the U2 table).
+__global__ void k_usk_ovf_count(const SK48* __restrict__ rec, const uint64_t* __restrict__ boff,
+                                const uint32_t* __restrict__ ovf_list, uint32_t n_ovf,
+                                unsigned long long* __restrict__ n_inst) {
+  unsigned long long c = 0;
+  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
+    const uint32_t b = ovf_list[q];
+    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) c += (uint32_t)(rec[i].w0 >> 32) & 0xff;
+  }
+  wave_add(n_inst, c);
+}
+
+__global__ void k_usk_ovf_expand(const SK48* __restrict__ rec, const uint64_t* __restrict__ boff,
+                                 const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, KeyP kp,
+                                 unsigned long long* __restrict__ cursor, KRec* __restrict__ out) {
+  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
+    const uint32_t b = ovf_list[q];
+    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
+      const SK48 r = rec[i];
+      const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+      unsigned long long at = atomicAdd(cursor, (unsigned long long)n);
+      for (uint32_t t = 0; t < n; ++t) {
+        K3 key;
+        uint32_t e;
+        urec_kmer(r, t, kp, &key, &e);
+        out[at + t] = KRec{key.a, key.b, key.c, key_hash(key) | e};
+      }
+    }
+  }
+}
+
 static int ceil_log2_u(uint64_t x) {
   int b = 0;
   while ((1ull << b) < x) ++b;
@@ -1595,17 +1877,145 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   return rc;
 }
 
+// U1'-U3': distinct nodes of the reads into workspace "usk_nodes" (see the
+// device section).  n_inst: K-mer instances.
+static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec** nodes_out, uint64_t* N_out,
+                      uint64_t* n_inst) {
+  const UskP p = make_uskp(kp.K);
+  if (p.w > kUskMaxW) {
+    set_error("unipaths: minimizer window exceeds kUskMaxW");
+    return APG_E_UNSUPPORTED;
+  }
+  const int D = kUskDigitBits;
+  const uint32_t ndig = 1u << D;
+  const uint32_t G =
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUskMaxBlocks, (dr->n_reads + kUskThreads - 1) / kUskThreads));
+  SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  const size_t sb_bytes = (size_t)p.w * kUskThreads * 4;
+  uint32_t* cmat = nullptr;
+  uint64_t *omat = nullptr, *ds = nullptr;
+  unsigned long long* kdig = nullptr;
+  APG_TRY(workspace_t(ctx, "usk_cmat", (uint64_t)ndig * G, &cmat));
+  APG_TRY(workspace_t(ctx, "usk_omat", (uint64_t)ndig * G + 1, &omat));
+  APG_TRY(workspace_t(ctx, "usk_ds", ndig + 1, &ds));
+  APG_TRY(workspace_t(ctx, "usk_kdig", ndig, &kdig));
+  APG_CHECK_HIP(hipMemsetAsync(kdig, 0, ndig * 8, ctx->stream));
+  if (!dr->n_reads) APG_CHECK_HIP(hipMemsetAsync(cmat, 0, (uint64_t)ndig * G * 4, ctx->stream));
+  kbegin(ctx, "usk_count", dr->n_bytes + 16 * dr->n_reads);
+  if (dr->n_reads) k_usk_count<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, cmat, kdig);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "usk"));
+  k_usk_digit_starts<<<(ndig + 256) / 256, 256, 0, ctx->stream>>>(omat, ndig, G, ds);
+  std::vector<uint64_t> h(ndig + 1), kd(ndig);
+  APG_CHECK_HIP(hipMemcpyAsync(h.data(), ds, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(kd.data(), kdig, ndig * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  const uint64_t n = h[ndig];
+  uint64_t nk = 0;
+  for (auto x : kd) nk += x;
+  *n_inst = nk;
+  SK48 *bufA = nullptr, *bufB = nullptr;
+  APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1) + 1, &bufA));
+  APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1) + 1, &bufB));
+  kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + n * sizeof(SK48));
+  if (dr->n_reads) k_usk_scatter<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, omat, bufA);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  // partition levels on the key bits below the D digit bits
+  const uint64_t need = std::max<uint64_t>(1, (nk + kUskBucketKmers - 1) / kUskBucketKmers);
+  const int bb = std::min(32, std::max(D, ceil_log2_u(need)));
+  const int rem = bb - D;
+  const int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  std::vector<std::vector<Seg>> parents(ndig);
+  for (uint32_t d = 0; d < ndig; ++d) parents[d].push_back(Seg{h[d], h[d + 1] - h[d]});
+  uint64_t* boff = nullptr;
+  APG_TRY(workspace_t(ctx, "usk_boff", (1ull << bb) + 1, &boff));
+  if (nlev == 0) APG_CHECK_HIP(hipMemcpyAsync(boff, h.data(), (ndig + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  SK48* cur = bufA;
+  uint64_t nb = ndig;
+  int consumed = D;
+  for (int lev = 0; lev < nlev; ++lev) {
+    const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
+    consumed += bits;
+    SK48* dst = cur == bufA ? bufB : bufA;
+    std::vector<uint64_t> hb;
+    const bool last = lev + 1 == nlev;
+    APG_TRY(part_level<SK48>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "usk"));
+    nb = parents.size() << bits;
+    if (!last) {
+      parents.assign(nb, {});
+      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
+    }
+    cur = dst;
+  }
+  // buckets -> nodes
+  unsigned long long* gs = nullptr;
+  uint32_t* ovf = nullptr;
+  APG_TRY(workspace_t(ctx, "usk_gs", 4, &gs));
+  APG_TRY(workspace_t(ctx, "usk_ovf", std::max<uint64_t>(nb, 1), &ovf));
+  uint64_t cap = std::max<uint64_t>(1 << 20, nk / 4);
+  KRec* nodes = nullptr;
+  unsigned long long hs[4];
+  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * 8));
+  for (;;) {
+    APG_TRY(workspace_t(ctx, "usk_nodes", cap, &nodes));
+    APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));
+    kbegin(ctx, "usk_bucket", n * sizeof(SK48) + (nb + 1) * 8);
+    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, kp, UskOut{nodes, cap, gs, ovf});
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    APG_TRY(d2h_u64(ctx, gs, hs, 4));
+    if (hs[0] <= cap) break;
+    vlog(ctx, "unipaths: %llu nodes exceed the node list (%llu), rerunning", hs[0], (unsigned long long)cap);
+    cap = hs[0] + hs[0] / 8;
+  }
+  uint64_t N = hs[0];
+  kbytes_add(ctx, "usk_bucket", N * sizeof(KRec));
+  if (hs[1]) {  // overflowed buckets: their instances through the U2 table
+    const uint32_t n_ovf = (uint32_t)hs[1];
+    const uint32_t g2 = (uint32_t)std::min<uint64_t>(n_ovf, (uint64_t)ctx->n_cu * 8);
+    APG_CHECK_HIP(hipMemsetAsync(gs + 2, 0, 16, ctx->stream));
+    k_usk_ovf_count<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, n_ovf, gs + 2);
+    unsigned long long ni[2];
+    APG_TRY(d2h_u64(ctx, gs + 2, ni, 2));
+    KRec* inst = nullptr;
+    APG_TRY(workspace_t(ctx, "usk_inst", std::max<unsigned long long>(ni[0], 1), &inst));
+    kbegin(ctx, "usk_ovf_expand", ni[0] * sizeof(KRec));
+    k_usk_ovf_expand<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, n_ovf, kp, gs + 3, inst);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    KRec* fnodes = nullptr;
+    uint64_t fN = 0;
+    APG_TRY(u_build_nodes(ctx, nullptr, inst, ni[0], kp, (double)ni[0], &fnodes, &fN, nullptr));
+    if (N + fN > cap) {  // grow, keeping the bucket nodes
+      KRec* tmp = nullptr;
+      APG_TRY(workspace_t(ctx, "usk_inst", std::max<uint64_t>(N, 1), &tmp));  // inst no longer needed
+      APG_CHECK_HIP(hipMemcpyAsync(tmp, nodes, N * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
+      APG_TRY(workspace_t(ctx, "usk_nodes", N + fN, &nodes));
+      APG_CHECK_HIP(hipMemcpyAsync(nodes, tmp, N * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    APG_CHECK_HIP(hipMemcpyAsync(nodes + N, fnodes, fN * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
+    vlog(ctx, "unipaths: %u buckets overflow the LDS table (%llu instances, %llu nodes) -> global table", n_ovf,
+         ni[0], (unsigned long long)fN);
+    N += fN;
+  }
+  vlog(ctx, "unipaths: K=%d m=%d records=%llu instances=%llu levels=%d buckets=%llu nodes=%llu", kp.K, p.m,
+       (unsigned long long)n, (unsigned long long)nk, nlev, (unsigned long long)nb, (unsigned long long)N);
+  *nodes_out = nodes;
+  *N_out = N;
+  return APG_OK;
+}
+
 static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
                          apg_unipath_stats* st) {
   const KeyP kp = make_keyp(prm.K);
   std::memset(st, 0, sizeof(*st));
   uint64_t n = 0;
-  double est = 0;
-  APG_TRY(u_size(ctx, dr, kp, &n, &est));
-  st->n_instances = n;
   KRec* nodes = nullptr;
   uint64_t N = 0;
-  APG_TRY(u_build_nodes(ctx, dr, nullptr, 0, kp, est, &nodes, &N, nullptr));
+  APG_TRY(u_sk_nodes(ctx, dr, kp, &nodes, &N, &n));
+  st->n_instances = n;
   return u_graph(ctx, nodes, N, dr, prm, out, st);
 }
 
