@@ -47,7 +47,7 @@ constexpr int kSkThreads = 256;
 constexpr int kSkMaxBlocks = 2048;
 constexpr int kSkBases = 40;
 constexpr int kSkDigitBits = 5;
-constexpr uint64_t kSkBucketKmers = 2048;  // K-mer instances per bucket the planner aims for
+constexpr uint64_t kSkBucketKmers = 4096;  // K-mer instances per bucket the planner aims for
 constexpr uint32_t kSkTab = 2048;          // LDS table slots (u64 canonical K-mer + u32 count)
 constexpr int kSkHistBins = 256;
 constexpr int kSkMaxW = 17;  // w = K - m + 1 <= 17 for K <= 32
@@ -215,10 +215,32 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kSkHistBins; i += kSkThreads) lhist[i] = 0;
   unsigned long long nd = 0;
-  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
-    const uint64_t off = boff[bkt];
-    const uint32_t nr = (uint32_t)(boff[bkt + 1] - off);
-    if (nr == 0) continue;  // block-uniform
+  // The block's buckets bkt, bkt + grid, ... are one record stream: the next
+  // chunk's record (this bucket's or the next bucket's first) and the next
+  // bucket's bounds are loaded while the current chunk is counted.
+  uint64_t bkt = blockIdx.x, off = 0;
+  uint32_t nr = 0;
+  if (bkt < nbuckets) {
+    off = boff[bkt];
+    nr = (uint32_t)(boff[bkt + 1] - off);
+  }
+  SK16 pre{0, 0};
+  if (tid < nr) pre = rec[off + tid];
+  for (; bkt < nbuckets;) {
+    const uint64_t nbk = bkt + gridDim.x;
+    uint64_t noff = 0;
+    uint32_t nnr = 0;
+    if (nbk < nbuckets) {
+      noff = boff[nbk];
+      nnr = (uint32_t)(boff[nbk + 1] - noff);
+    }
+    if (nr == 0) {  // block-uniform
+      if (tid < nnr) pre = rec[noff + tid];
+      bkt = nbk;
+      off = noff;
+      nr = nnr;
+      continue;
+    }
     for (uint32_t s = tid; s < kSkTab; s += kSkThreads) {
       tkey[s] = EMPTY;
       tcnt[s] = 0;
@@ -227,9 +249,13 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
     for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
       uint32_t nk = 0;
       if (c0 + tid < nr) {
-        const SK16 r = rec[off + c0 + tid];
-        nk = (uint32_t)(r.w0 >> 32) & 0xff;
-        crec[tid] = r;
+        nk = (uint32_t)(pre.w0 >> 32) & 0xff;
+        crec[tid] = pre;
+      }
+      if (c0 + kSkThreads < nr) {
+        if (c0 + kSkThreads + tid < nr) pre = rec[off + c0 + kSkThreads + tid];
+      } else if (tid < nnr) {
+        pre = rec[noff + tid];
       }
       uint32_t tot;
       const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);  // barrier: table clear visible
@@ -245,7 +271,8 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
             ovf = 1;  // table full: the bucket goes to the global path
             break;
           }
-          const unsigned long long old = atomicCAS(&tkey[s], EMPTY, (unsigned long long)c);
+          unsigned long long old = tkey[s];  // hits (most instances) skip the CAS
+          if (old == EMPTY) old = atomicCAS(&tkey[s], EMPTY, (unsigned long long)c);
           if (old == EMPTY || old == c) {
             atomicAdd(&tcnt[s], 1u);
             break;
@@ -258,6 +285,9 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
     if (ovf) {
       if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
       __syncthreads();
+      bkt = nbk;
+      off = noff;
+      nr = nnr;
       continue;
     }
     uint32_t ns = 0;
@@ -280,6 +310,9 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
         }
     }
     __syncthreads();
+    bkt = nbk;
+    off = noff;
+    nr = nnr;
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;

@@ -1011,6 +1011,14 @@ __global__ void k_pair_sizes(uint64_t P, const uint32_t* __restrict__ ph, const 
   }
 }
 
+__global__ void k_u64_max(const uint64_t* __restrict__ x, uint64_t n, unsigned long long* __restrict__ mx) {
+  unsigned long long m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    m = max(m, (unsigned long long)x[i]);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_down(m, o, 64));
+  if (lane_id() == 0 && m) atomicMax(mx, m);
+}
+
 __global__ void k_u32_of(const uint64_t* __restrict__ x, uint64_t n, uint32_t add, uint32_t* __restrict__ y) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     y[i] = (uint32_t)x[i] + add;
@@ -1787,6 +1795,7 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   APG_TRY(scan_u32_u64(ctx, lens32, U, id_base, "ui"));
   k_u32_of<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(ulen, U, (uint32_t)(K - 1), lens32);
   APG_TRY(scan_u32_u64(ctx, lens32, U, ub_off, "uu"));
+  if (U) k_u64_max<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(ulen, U, gs + 26);
   APG_CHECK_HIP(hipGetLastError());
 
   // ---- U8 --------------------------------------------------------------------
@@ -1847,7 +1856,11 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     APG_CHECK_HIP(hipGetLastError());
     st->n_intervals = NI;
   }
-  APG_TRY(sync(ctx));
+  {
+    unsigned long long ml = 0;
+    APG_TRY(d2h_u64(ctx, gs + 26, &ml, 1));
+    st->max_len = ml;
+  }
   if (!out) return APG_OK;
 
   // ---- host copies ------------------------------------------------------------
@@ -1872,8 +1885,6 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     out->path_len = host_dup(ilen, NI, ctx, &rc);
   }
   if (rc == APG_OK) rc = sync(ctx);
-  if (rc == APG_OK)
-    for (uint64_t i = 0; i < U; ++i) st->max_len = std::max<uint64_t>(st->max_len, out->len[i]);
   return rc;
 }
 

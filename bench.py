@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--sharded", action="store_true",
                    help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v7", "traffic.json"),
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v8", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     return p.parse_args()
 
@@ -155,6 +155,12 @@ def main():
         checks["precorrect_corrected_most_suspects"] = pst["n_corrected"] > 0.5 * pst["n_suspect"]
         n_inst = world * int((np.maximum(frags.lengths().astype(np.int64) - a.K_unipath + 1, 0)).sum())
         checks["unipath_instances_equal_sum_len_minus_K_plus_1"] = ust["n_instances"] == n_inst
+        # iid genome, no K=96 repeat: one unipath pair holding every node, and the
+        # nodes are the genome's K-mers bar a few uncovered at the chromosome ends
+        # (SURVEY A.8 KAT 3)
+        checks["unipaths_one_pair_spanning_genome"] = (
+            ust["n_unipaths"] == 2 and ust["max_len"] == ust["n_nodes"]
+            and 0 <= (a.genome_len - a.K_unipath + 1) - ust["n_nodes"] < 1000)
 
     # Roofline of the dominant kernel, from HIP events on libapg's stream.
     kt = ctx.kernel_times()

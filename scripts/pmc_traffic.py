@@ -24,6 +24,16 @@ KERNELS = {
     "void apg::k_part_scatter<unsigned long>": ("p_part_scatter", "stream"),
     "void apg::k_part_count<unsigned long>": ("p_part_count", "stream"),
     "apg::k_extract_scatter": ("extract_scatter", "stream"),
+    "apg::k_sk_count": ("sk_count", "stream"),
+    "apg::k_sk_scatter": ("sk_scatter", "stream"),
+    "void apg::k_sk_bucket<false>": ("sk_bucket", "stream"),
+    "void apg::k_sk_bucket<true>": ("sk_bucket_solid", "stream"),
+    "void apg::k_part_scatter<apg::SK16>": ("s_part_scatter", "stream"),
+    "void apg::k_part_count<apg::SK16>": ("s_part_count", "stream"),
+    "apg::k_usk_count": ("usk_count", "stream"),
+    "apg::k_usk_scatter": ("usk_scatter", "stream"),
+    "apg::k_usk_bucket": ("usk_bucket", "stream"),
+    "void apg::k_part_scatter<apg::SK48>": ("usk_part_scatter", "stream"),
     "apg::k_links": ("u_links", "random"),
     "apg::k_walk": ("u_walk", "random"),
 }
