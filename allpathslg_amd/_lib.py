@@ -88,6 +88,40 @@ class apg_pc_stats(C.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
 
 
+APG_FILL_LAST_SOLID = 1
+FILL_STATUS = {0: "filled", 1: "none", 2: "ambiguous", 3: "budget", 4: "skip"}
+
+
+class apg_fill_params(C.Structure):
+    _fields_ = [
+        ("K", C.c_int32),
+        ("min_insert", C.c_uint32),
+        ("max_insert", C.c_uint32),
+        ("max_steps", C.c_uint32),
+        ("min_solid", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint64 * 3),
+    ]
+
+
+class apg_fill_stats(C.Structure):
+    _fields_ = [
+        ("n_pairs", C.c_uint64),
+        ("n_filled", C.c_uint64),
+        ("n_none", C.c_uint64),
+        ("n_ambiguous", C.c_uint64),
+        ("n_budget", C.c_uint64),
+        ("n_skip", C.c_uint64),
+        ("filled_bases", C.c_uint64),
+        ("n_solid", C.c_uint64),
+        ("lookups", C.c_uint64),
+        ("reserved", C.c_uint64 * 3),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
+
+
 class apg_unipath_params(C.Structure):
     _fields_ = [("K", C.c_int32), ("flags", C.c_uint32), ("reserved", C.c_uint64 * 4)]
 
@@ -226,9 +260,17 @@ SIGNATURES = {
     "apg_reads_download": (C.c_int, [_P, _P, _u8p, _u8p]),
     "apg_shard_solid": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, C.c_uint32, _u64p]),
     "apg_solid_export": (C.c_int, [_P, C.c_void_p]),
+    "apg_solid_copy": (C.c_int, [_P, C.c_void_p, _u64p]),
     "apg_precorrect_solid": (
         C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.c_void_p, C.c_uint64, C.POINTER(apg_pc_stats)]
     ),
+    "apg_fill_defaults": (None, [C.POINTER(apg_fill_params)]),
+    "apg_fill_fragments": (
+        C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_fill_params), _u64p, C.c_uint64, C.POINTER(apg_reads), _u8p,
+                  C.POINTER(apg_fill_stats)]),
+    "apg_fill_fragments_dev": (
+        C.c_int, [_P, _P, C.POINTER(apg_fill_params), C.c_void_p, C.c_uint64, C.POINTER(_P), C.c_void_p,
+                  C.POINTER(apg_fill_stats)]),
     "apg_unipath_defaults": (None, [C.POINTER(apg_unipath_params)]),
     "apg_unipaths": (
         C.c_int,

@@ -159,6 +159,8 @@ int apg_trim(apg_ctx* ctx) {
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
   ctx->ws.clear();
+  ctx->pc_list_valid = false;
+  ctx->solid_valid = false;
   return APG_OK;
 }
 

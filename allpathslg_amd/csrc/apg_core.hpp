@@ -65,7 +65,11 @@ struct apg_dreads {
   uint64_t* d_byte_off = nullptr;  // n+1
   uint8_t* d_packed = nullptr;
   uint8_t* d_quals = nullptr;      // optional
-  std::vector<uint64_t> h_base_off;  // kept for host-side sizing
+  std::vector<uint64_t> h_base_off;  // kept for host-side sizing (uploads only)
+  // device-produced sets (apg_fill_fragments_dev): buffer capacities, reused
+  // when the same object is passed back in
+  bool fill_owned = false;
+  uint64_t cap_reads = 0, cap_bytes = 0;
 };
 
 struct apg_ctx {
@@ -128,6 +132,13 @@ struct apg_ctx {
   // Solid K-mer list of the last apg_shard_solid ("pc_solid" workspace).
   uint64_t n_solid = 0;
   bool solid_valid = false;
+
+  // Solid list the last correction pass corrected against ("pc_solid", or
+  // the caller's gathered list in the sharded flow); APG_FILL_LAST_SOLID.
+  const uint64_t* pc_list = nullptr;
+  uint64_t pc_n = 0;
+  int pc_K = 0;
+  bool pc_list_valid = false;
 };
 
 namespace apg {

@@ -1,0 +1,622 @@
+// fill.hip — FillFragments on MI355X: close each frag pair (A, B) into the
+// fragment it was read from, through the solid K-mer graph.  Spec: the
+// closure rule and search order pinned in include/apg.h (apg_fill_fragments);
+// CPU restatement oracle/fill_oracle.c (recalled reference: [R:M]
+// src/paths/FillFragments.cc, grep target only — snapshot empty).
+//
+//   1. k_fill_ext_insert: the solid K-mer set (hashes of canonical K-mers) is
+//      turned into a (K-1)-mer extension table: one 8-byte slot per canonical
+//      (K-1)-mer = key << 8 | 4 left + 4 right extension bits.  K-mer x is
+//      solid  <=>  the slot of x's first K-1 bases holds x's last base as a
+//      successor.  One lookup therefore answers all 4 successors of a walk
+//      node, where a hash set of K-mers would need 4.
+//   2. k_fill: one thread per pair.  Overlap closures (I < La+Lf) by 32-base
+//      word compares of A's suffix with F = rc(B)'s prefix, bridge K-mers by
+//      extension lookups; then the depth-first walk from A's last K-1 bases,
+//      entirely in registers: the path is a 128-bit base string, the branch
+//      points a 64-bit depth mask, so backtracking jumps straight to the
+//      deepest open branch (one re-lookup) instead of unwinding a stack.
+//   3. three u32 -> u64 scans (bases, bytes, index of filled pairs) and
+//      k_fill_write: the filled fragments as a device read set (2-bit packed,
+//      byte-aligned, pair order) ready for the K=96 unipath stage.
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "apg_core.hpp"
+#include "kmer_common.hpp"
+#include "kmer_internal.hpp"
+#include "partition.hpp"
+
+namespace apg {
+
+constexpr uint64_t kExtEmpty = ~0ull;
+constexpr uint32_t kFillMaxGap = 63;
+
+__device__ __forceinline__ uint64_t f_rev2(uint64_t x) {
+  x = __builtin_bitreverse64(x);
+  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+}
+
+// reverse complement of an n-base MSB-first value (1 <= n <= 32)
+__host__ __device__ __forceinline__ uint64_t rc_bases(uint64_t w, int n, uint64_t mask) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return (f_rev2(w) >> (64 - 2 * n)) ^ mask;
+#else
+  uint64_t r = 0;
+  for (int i = 0; i < n; ++i) {
+    r = (r << 2) | (3 - (w & 3));
+    w >>= 2;
+  }
+  return r & mask;
+#endif
+}
+
+__device__ __forceinline__ uint32_t rev4(uint32_t x) {
+  return ((x & 1) << 3) | ((x & 2) << 1) | ((x & 4) >> 1) | ((x & 8) >> 3);
+}
+
+struct ExtTab {
+  unsigned long long* slot;
+  uint64_t mask;
+  HashP h1;  // slot hash of canonical (K-1)-mers
+  uint64_t m1;
+  int n1;  // K-1
+};
+
+__device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
+  const unsigned long long want = (key << 8) | bit;
+  uint64_t s = khash(t.h1, key) & t.mask;
+  for (;;) {
+    unsigned long long v = t.slot[s];
+    if (v == kExtEmpty) {
+      v = atomicCAS(&t.slot[s], kExtEmpty, want);
+      if (v == kExtEmpty) return;
+    }
+    if ((v >> 8) == key) {
+      if (!(v & bit)) atomicOr(&t.slot[s], (unsigned long long)bit);
+      return;
+    }
+    s = (s + 1) & t.mask;
+  }
+}
+
+// successor bit b of (K-1)-mer u (MSB-first value) / predecessor bit a
+__device__ __forceinline__ void ext_add_right(const ExtTab& t, uint64_t u, uint32_t b) {
+  const uint64_t r = rc_bases(u, t.n1, t.m1);
+  if (u <= r)
+    ext_set(t, u, 16u << b);
+  else
+    ext_set(t, r, 1u << (3 - b));
+}
+__device__ __forceinline__ void ext_add_left(const ExtTab& t, uint64_t u, uint32_t a) {
+  const uint64_t r = rc_bases(u, t.n1, t.m1);
+  if (u <= r)
+    ext_set(t, u, 1u << a);
+  else
+    ext_set(t, r, 16u << (3 - a));
+}
+
+__global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n, HashP hK, ExtTab t) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = kunhash(hK, solid[i]);
+    ext_add_right(t, c >> 2, (uint32_t)(c & 3));
+    ext_add_left(t, c & t.m1, (uint32_t)(c >> (2 * t.n1)));
+  }
+}
+
+// 4-bit successor mask of the (K-1)-mer w (MSB-first, fw orientation)
+__device__ __forceinline__ uint32_t ext_succ(const ExtTab& t, uint64_t w, uint32_t* nlook) {
+  const uint64_t r = rc_bases(w, t.n1, t.m1);
+  const uint64_t c = w < r ? w : r;
+  uint64_t s = khash(t.h1, c) & t.mask;
+  uint32_t e = 0;
+  for (;;) {
+    const unsigned long long v = t.slot[s];
+    if (v == kExtEmpty) break;
+    if ((v >> 8) == c) {
+      e = (uint32_t)(v & 0xff);
+      break;
+    }
+    s = (s + 1) & t.mask;
+  }
+  ++*nlook;
+  uint32_t m = 0;
+  if (w <= r) m |= e >> 4;
+  if (r <= w) m |= rev4(e & 15);
+  return m;
+}
+
+// 32 bases [pos, pos+32) of a packed read as an LSB-first word (base pos at
+// bits 0-1).  Aligned u32 loads; may read up to 12 bytes past the read (the
+// read sets carry 64 bytes of slack).
+__device__ __forceinline__ uint64_t bases32(const uint8_t* p, uint32_t pos) {
+  const uintptr_t a = (uintptr_t)p + (pos >> 2);
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = 8 * (uint32_t)(a & 3) + 2 * (pos & 3);
+  const uint64_t lo = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+  return sh ? (lo >> sh) | ((uint64_t)q[2] << (64 - sh)) : lo;
+}
+
+__device__ __forceinline__ uint64_t lmask(uint32_t nb) { return nb >= 32 ? ~0ull : ((1ull << (2 * nb)) - 1); }
+
+// F = rc(B): bases [t, t+32) of F as an LSB-first word; bases past F's end
+// are garbage.
+__device__ __forceinline__ uint64_t fwin(const uint8_t* B, uint32_t Lf, uint32_t t) {
+  const uint32_t m = Lf - t;
+  if (m >= 32) return ~f_rev2(bases32(B, Lf - t - 32));
+  return ~(f_rev2(bases32(B, 0) & lmask(m)) >> (2 * (32 - m)));
+}
+
+// Every K-mer of a packed read (L >= K) solid: one extension lookup per
+// K-mer (its first K-1 bases hold its last base as a successor).  Bases are
+// streamed 32 at a time from one LSB-first word.
+__device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, uint32_t L, uint32_t* nlook) {
+  const int n1 = t.n1;
+  uint64_t buf = bases32(R, 0);
+  uint64_t w = f_rev2(buf & lmask(n1)) >> (64 - 2 * n1);  // first K-1 bases, MSB-first
+  for (uint32_t i = n1; i < L; ++i) {
+    if ((i & 31) == 0) buf = bases32(R, i);
+    const uint32_t b = (uint32_t)(((i & 31) == 0 ? buf : buf >> (2 * (i & 31))) & 3);
+    if (!((ext_succ(t, w, nlook) >> b) & 1)) return false;
+    w = ((w << 2) | b) & t.m1;
+  }
+  return true;
+}
+
+struct FillReads {
+  const uint64_t* base_off;
+  const uint64_t* byte_off;
+  const uint8_t* packed;
+  uint64_t n_pairs;
+};
+
+struct FillP {
+  int K;
+  uint32_t min_insert, max_insert, max_steps;
+};
+
+struct FillRec {
+  uint64_t pv_lo, pv_hi;  // gap path bases, MSB-first
+  uint32_t len;           // closure length I (filled) or 0
+  uint32_t meta;          // status | d << 8 | overlap o << 16
+};
+
+enum { kFillOk = 0, kFillNone = 1, kFillAmbiguous = 2, kFillBudget = 3, kFillSkip = 4 };
+
+struct FillCounters {
+  unsigned long long st[5];
+  unsigned long long lookups;
+};
+
+// last K-1 bases of A ++ path[0, d) (MSB-first)
+__device__ __forceinline__ uint64_t walk_window(uint64_t atail, unsigned __int128 pv, uint32_t d, const ExtTab& t) {
+  if (d >= (uint32_t)t.n1) return (uint64_t)pv & t.m1;
+  return ((atail << (2 * d)) | (uint64_t)pv) & t.m1;
+}
+
+__global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
+                                              uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
+                                              uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
+                                              FillCounters* __restrict__ cnt) {
+  uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
+  uint32_t nlook = 0;
+  const int K = p.K, n1 = t.n1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rv.n_pairs;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
+    const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
+    const uint8_t* A = rv.packed + rv.byte_off[2 * i];
+    const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
+    const uint32_t lo = max(p.min_insert, max(La, Lf));
+    FillRec out{0, 0, 0, 0};
+    uint32_t st;
+    if (La < (uint32_t)K || Lf < (uint32_t)K || (p.max_insert >= La + Lf && p.max_insert - (La + Lf) > kFillMaxGap)) {
+      st = kFillSkip;
+    } else if (!read_solid(t, A, La, &nlook) || !read_solid(t, B, Lf, &nlook)) {
+      st = kFillNone;  // S must be a path of solid K-mers: no closure through a weak read K-mer
+    } else {
+      // A's last K-1 bases, MSB-first; F's first 32 bases, LSB-first
+      const uint64_t atail = f_rev2(bases32(A, La - n1) & lmask(n1)) >> (64 - 2 * n1);
+      const uint64_t f0 = fwin(B, Lf, 0);
+      uint32_t n_clos = 0, clos_I = 0, clos_meta = 0;
+      unsigned __int128 clos_pv = 0;
+      bool budget = false;
+      // overlap closures, I ascending (o descending)
+      const uint32_t hi_ov = min(p.max_insert, La + Lf - 1);
+      for (uint32_t I = lo; I <= hi_ov && n_clos < 2; ++I) {
+        const uint32_t o = La + Lf - I;
+        bool match = true;
+        for (uint32_t c = 0; c < o && match; c += 32) {
+          const uint32_t nb = min(32u, o - c);
+          const uint64_t fw = c == 0 ? f0 : fwin(B, Lf, c);
+          match = ((bases32(A, La - o + c) ^ fw) & lmask(nb)) == 0;
+        }
+        if (!match) continue;
+        if (o + 2 <= (uint32_t)K) {  // bridge K-mers: A's tail rolled through F[o, K-1)
+          uint64_t w = atail;
+          for (uint32_t j = 0; j + o + 2 <= (uint32_t)K && match; ++j) {
+            const uint32_t b = (uint32_t)(f0 >> (2 * (o + j))) & 3;
+            match = (ext_succ(t, w, &nlook) >> b) & 1;
+            w = ((w << 2) | b) & t.m1;
+          }
+        }
+        if (match && ++n_clos == 1) {
+          clos_I = I;
+          clos_meta = o << 16;
+        }
+      }
+      // gap closures: depth-first walk, bases A<C<G<T
+      if (n_clos < 2 && p.max_insert >= La + Lf) {
+        const uint32_t gmax = p.max_insert - (La + Lf);
+        const uint32_t dlo = lo > La + Lf ? lo - (La + Lf) : 0;
+        const uint32_t fb0 = (uint32_t)f0 & 3;
+        unsigned __int128 pv = 0;
+        uint64_t brm = 0;  // depths whose node still has unexplored children
+        uint32_t d = 0, steps = 0;
+        for (;;) {
+          const uint64_t w = walk_window(atail, pv, d, t);
+          const uint32_t m = ext_succ(t, w, &nlook);
+          if (d >= dlo && ((m >> fb0) & 1)) {  // closure test: the K-1 bridge K-mers
+            bool ok = true;
+            uint64_t ww = ((w << 2) | fb0) & t.m1;
+            for (int j = 1; j < n1 && ok; ++j) {
+              const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
+              ok = (ext_succ(t, ww, &nlook) >> b) & 1;
+              ww = ((ww << 2) | b) & t.m1;
+            }
+            if (ok && ++n_clos == 1) {
+              clos_I = La + Lf + d;
+              clos_pv = pv;
+              clos_meta = d << 8;
+            }
+            if (n_clos >= 2) break;
+          }
+          bool down = false;
+          if (d < gmax) {
+            if (++steps > p.max_steps) {
+              budget = true;
+              break;
+            }
+            if (m) {
+              const uint32_t b = __ffs(m) - 1;
+              if (m >> (b + 1)) brm |= 1ull << d;
+              pv = (pv << 2) | b;
+              ++d;
+              down = true;
+            }
+          }
+          if (down) continue;
+          if (!brm) break;  // search exhausted
+          const uint32_t dd = 63 - __clzll((long long)brm);
+          const unsigned __int128 pv1 = pv >> (2 * (d - dd - 1));
+          const uint32_t b = (uint32_t)pv1 & 3;
+          const unsigned __int128 pvd = pv1 >> 2;
+          const uint32_t m2 = ext_succ(t, walk_window(atail, pvd, dd, t), &nlook);
+          const uint32_t rest = m2 & ~((2u << b) - 1);
+          const uint32_t b2 = __ffs(rest) - 1;  // rest != 0: dd was marked open
+          if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
+          pv = (pvd << 2) | b2;
+          d = dd + 1;
+        }
+      }
+      if (n_clos >= 2)
+        st = kFillAmbiguous;
+      else if (budget)
+        st = kFillBudget;
+      else if (n_clos == 0)
+        st = kFillNone;
+      else {
+        st = kFillOk;
+        out.len = clos_I;
+        out.pv_lo = (uint64_t)clos_pv;
+        out.pv_hi = (uint64_t)(clos_pv >> 64);
+      }
+      out.meta = st | clos_meta;
+    }
+    if (st != kFillOk) out.meta = st;
+    rec[i] = out;
+    lens[i] = out.len;
+    nbytes[i] = (out.len + 3) >> 2;
+    ones[i] = st == kFillOk;
+    if (status_out) status_out[i] = (uint8_t)st;
+    c_ok += st == kFillOk;
+    c_none += st == kFillNone;
+    c_amb += st == kFillAmbiguous;
+    c_bud += st == kFillBudget;
+    c_skip += st == kFillSkip;
+  }
+  wave_add(&cnt->st[kFillOk], c_ok);
+  wave_add(&cnt->st[kFillNone], c_none);
+  wave_add(&cnt->st[kFillAmbiguous], c_amb);
+  wave_add(&cnt->st[kFillBudget], c_bud);
+  wave_add(&cnt->st[kFillSkip], c_skip);
+  wave_add(&cnt->lookups, nlook);
+}
+
+__device__ __forceinline__ uint32_t packed_base(const uint8_t* r, uint32_t i) { return (r[i >> 2] >> (2 * (i & 3))) & 3; }
+
+__global__ void __launch_bounds__(256) k_fill_write(FillReads rv, const FillRec* __restrict__ rec,
+                                                    const uint64_t* __restrict__ bscan,
+                                                    const uint64_t* __restrict__ yscan,
+                                                    const uint64_t* __restrict__ iscan, uint64_t* __restrict__ out_boff,
+                                                    uint64_t* __restrict__ out_yoff, uint8_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rv.n_pairs;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const FillRec r = rec[i];
+    if (!r.len) continue;
+    const uint64_t j = iscan[i];
+    out_boff[j] = bscan[i];
+    out_yoff[j] = yscan[i];
+    const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
+    const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
+    const uint8_t* A = rv.packed + rv.byte_off[2 * i];
+    const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
+    uint8_t* o = out + yscan[i];
+    const uint32_t I = r.len;
+    const unsigned __int128 pv = ((unsigned __int128)r.pv_hi << 64) | r.pv_lo;
+    const uint32_t ov = r.meta >> 16, d = (r.meta >> 8) & 0xff;
+    // S = A ++ F[ov, Lf) (overlap) or A ++ path[0, d) ++ F (gap, ov = 0)
+    uint32_t t = 0;
+    for (; t + 4 <= La; t += 4) o[t >> 2] = A[t >> 2];  // A is byte-aligned like S
+    uint32_t acc = 0;
+    for (; t < I; ++t) {
+      uint32_t b;
+      if (t < La)
+        b = packed_base(A, t);
+      else if (t < La + d)
+        b = (uint32_t)(pv >> (2 * (d - 1 - (t - La)))) & 3;
+      else
+        b = 3 - packed_base(B, Lf - 1 - (t - La - d + ov));
+      acc |= b << (2 * (t & 3));
+      if ((t & 3) == 3 || t + 1 == I) {
+        o[t >> 2] = (uint8_t)acc;
+        acc = 0;
+      }
+    }
+  }
+}
+
+static int fill_check(const apg_fill_params& p) {
+  APG_REQUIRE(p.K >= 2 && p.K <= 29, "apg_fill_fragments: K must be in [2, 29]");
+  APG_REQUIRE(p.min_insert <= p.max_insert, "apg_fill_fragments: min_insert > max_insert");
+  APG_REQUIRE(p.min_solid >= 1, "apg_fill_fragments: min_solid must be >= 1");
+  return APG_OK;
+}
+
+// Allocate (or reuse) the device read set of the filled fragments.
+static int filled_alloc(apg_ctx* ctx, apg_dreads** io, uint64_t n, uint64_t nbases, uint64_t nbytes) {
+  apg_dreads* d = *io;
+  if (d && (d->ctx != ctx || !d->fill_owned)) {
+    set_error("apg_fill_fragments_dev: *filled must be NULL or a previous apg_fill_fragments_dev output");
+    return APG_E_ARG;
+  }
+  if (!d) {
+    d = new (std::nothrow) apg_dreads();
+    if (!d) return APG_E_NOMEM;
+    d->ctx = ctx;
+    d->fill_owned = true;
+    *io = d;
+  }
+  if (d->cap_reads < n + 1) {
+    if (d->d_base_off) APG_CHECK_HIP(hipFree(d->d_base_off));
+    if (d->d_byte_off) APG_CHECK_HIP(hipFree(d->d_byte_off));
+    d->d_base_off = d->d_byte_off = nullptr;
+    d->cap_reads = 0;
+    const uint64_t c = n + 1 + (n + 1) / 8;
+    APG_CHECK_HIP(hipMalloc(&d->d_base_off, c * 8));
+    APG_CHECK_HIP(hipMalloc(&d->d_byte_off, c * 8));
+    d->cap_reads = c;
+  }
+  if (d->cap_bytes < nbytes + 64) {
+    if (d->d_packed) APG_CHECK_HIP(hipFree(d->d_packed));
+    d->d_packed = nullptr;
+    d->cap_bytes = 0;
+    const uint64_t c = nbytes + nbytes / 8 + 64;
+    APG_CHECK_HIP(hipMalloc(&d->d_packed, c));
+    APG_CHECK_HIP(hipMemsetAsync(d->d_packed, 0, c, ctx->stream));
+    d->cap_bytes = c;
+  }
+  static std::atomic<uint64_t> g_fill{3ull << 61};
+  d->gen = g_fill.fetch_add(1);  // new contents: per-read-set plans are stale
+  d->n_reads = n;
+  d->n_bases = nbases;
+  d->n_bytes = nbytes;
+  d->h_base_off.clear();
+  return APG_OK;
+}
+
+static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& p, const uint64_t* d_solid,
+                     uint64_t n_solid, apg_dreads** filled, uint8_t* d_status, apg_fill_stats* st) {
+  APG_REQUIRE(dr->n_reads % 2 == 0, "apg_fill_fragments: pairs must be an even number of reads (2i, 2i+1)");
+  const uint64_t np = dr->n_reads / 2;
+  std::memset(st, 0, sizeof *st);
+  st->n_pairs = np;
+  const uint64_t* list = d_solid;
+  if (!list && n_solid == 0) {
+    if (p.flags & APG_FILL_LAST_SOLID) {
+      APG_REQUIRE(ctx->pc_list_valid, "apg_fill_fragments: APG_FILL_LAST_SOLID but no correction pass ran on ctx");
+      APG_REQUIRE(ctx->pc_K == p.K, "apg_fill_fragments: last correction pass used another K");
+      list = ctx->pc_list;
+      n_solid = ctx->pc_n;
+    } else {  // the pairs' own solid K-mers
+      SkResult sr;
+      APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
+      list = sr.solid;
+      n_solid = sr.n_solid;
+      ctx->pc_list_valid = false;  // "pc_solid" now holds this list
+    }
+  }
+  APG_REQUIRE(n_solid == 0 || list, "apg_fill_fragments: solid set pointer is NULL");
+  st->n_solid = n_solid;
+  // (K-1)-mer extension table, load <= 0.5 even if no two solid K-mers share a (K-1)-mer
+  uint64_t T = 1024;
+  while (T < 4 * n_solid) T <<= 1;
+  unsigned long long* slot = nullptr;
+  APG_TRY(workspace_t(ctx, "fill_ext", T, &slot));
+  APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));
+  ExtTab et{slot, T - 1, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
+  kbegin(ctx, "fill_ext", n_solid * (8 + 2 * 64));
+  if (n_solid)
+    k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(p.K), et);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+
+  FillRec* rec = nullptr;
+  uint32_t *lens = nullptr, *nby = nullptr, *ones = nullptr;
+  uint64_t *bscan = nullptr, *yscan = nullptr, *iscan = nullptr;
+  unsigned long long* cnt = nullptr;
+  const uint64_t npc = std::max<uint64_t>(np, 1);
+  APG_TRY(workspace_t(ctx, "fill_rec", npc, &rec));
+  APG_TRY(workspace_t(ctx, "fill_lens", npc, &lens));
+  APG_TRY(workspace_t(ctx, "fill_nby", npc, &nby));
+  APG_TRY(workspace_t(ctx, "fill_ones", npc, &ones));
+  APG_TRY(workspace_t(ctx, "fill_bscan", npc + 1, &bscan));
+  APG_TRY(workspace_t(ctx, "fill_yscan", npc + 1, &yscan));
+  APG_TRY(workspace_t(ctx, "fill_iscan", npc + 1, &iscan));
+  APG_TRY(workspace_t(ctx, "fill_cnt", 6, &cnt));
+  APG_CHECK_HIP(hipMemsetAsync(cnt, 0, 6 * 8, ctx->stream));
+  const FillReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, np};
+  const FillP fp{p.K, p.min_insert, p.max_insert, p.max_steps};
+  kbegin(ctx, "fill", dr->n_bytes + 16 * dr->n_reads + np * (sizeof(FillRec) + 12));
+  if (np)
+    k_fill<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status,
+                                                        reinterpret_cast<FillCounters*>(cnt));
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, lens, np, bscan, "fb"));
+  APG_TRY(scan_u32_u64(ctx, nby, np, yscan, "fy"));
+  APG_TRY(scan_u32_u64(ctx, ones, np, iscan, "fi"));
+  unsigned long long hc[6];
+  uint64_t tot[3];
+  APG_CHECK_HIP(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&tot[0], bscan + np, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&tot[1], yscan + np, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&tot[2], iscan + np, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  kbytes_add(ctx, "fill", hc[5] * 64);  // one random 64-byte table line per extension lookup
+  st->n_filled = hc[kFillOk];
+  st->n_none = hc[kFillNone];
+  st->n_ambiguous = hc[kFillAmbiguous];
+  st->n_budget = hc[kFillBudget];
+  st->n_skip = hc[kFillSkip];
+  st->lookups = hc[5];
+  st->filled_bases = tot[0];
+  if (!filled) return APG_OK;
+  const uint64_t nf = tot[2];
+  APG_TRY(filled_alloc(ctx, filled, nf, tot[0], tot[1]));
+  apg_dreads* fd = *filled;
+  fd->max_len = nf ? p.max_insert : 0;
+  kbegin(ctx, "fill_write", np * (sizeof(FillRec) + 24) + tot[1] + nf * 16);
+  if (np)
+    k_fill_write<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, rec, bscan, yscan, iscan, fd->d_base_off,
+                                                              fd->d_byte_off, fd->d_packed);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_CHECK_HIP(hipMemcpyAsync(fd->d_base_off + nf, bscan + np, 8, hipMemcpyDeviceToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(fd->d_byte_off + nf, yscan + np, 8, hipMemcpyDeviceToDevice, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(fd->d_packed + tot[1], 0, 64, ctx->stream));
+  return sync(ctx);
+}
+
+}  // namespace apg
+
+using namespace apg;
+
+extern "C" {
+
+void apg_fill_defaults(apg_fill_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->K = 24;
+  p->min_insert = 126;
+  p->max_insert = 234;
+  p->max_steps = 1024;
+  p->min_solid = 3;
+}
+
+int apg_fill_fragments_dev(apg_ctx* ctx, const apg_dreads* pairs, const apg_fill_params* pp, const void* d_solid,
+                           uint64_t n_solid, apg_dreads** filled, uint8_t* d_status, apg_fill_stats* stats) {
+  APG_REQUIRE(ctx && pairs, "apg_fill_fragments_dev: NULL argument");
+  apg_fill_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_fill_defaults(&p);
+  APG_TRY(fill_check(p));
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_fill_stats st;
+  APG_TRY(fill_impl(ctx, pairs, p, static_cast<const uint64_t*>(d_solid), d_solid ? n_solid : 0, filled, d_status,
+                    &st));
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_fill_fragments(apg_ctx* ctx, const apg_reads* pairs, const apg_fill_params* pp, const uint64_t* solid,
+                       uint64_t n_solid, apg_reads* out, uint8_t* status, apg_fill_stats* stats) {
+  APG_REQUIRE(ctx && pairs && out, "apg_fill_fragments: NULL argument");
+  APG_REQUIRE(n_solid == 0 || solid, "apg_fill_fragments: solid is NULL");
+  std::memset(out, 0, sizeof(*out));
+  apg_fill_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_fill_defaults(&p);
+  APG_TRY(fill_check(p));
+  APG_REQUIRE(!(p.flags & APG_FILL_LAST_SOLID) || solid == nullptr,
+              "apg_fill_fragments: give either a solid set or APG_FILL_LAST_SOLID");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_dreads* dr = nullptr;
+  APG_TRY(apg_reads_upload(ctx, pairs, &dr));
+  uint64_t* d_solid = nullptr;
+  uint8_t* d_status = nullptr;
+  apg_dreads* fd = nullptr;
+  apg_fill_stats st;
+  std::memset(&st, 0, sizeof st);
+  const uint64_t np = pairs->n_reads / 2;
+  int rc = APG_OK;
+  auto hip = [&](hipError_t e) {
+    if (e != hipSuccess && rc == APG_OK) {
+      set_error(std::string("apg_fill_fragments: ") + hipGetErrorString(e));
+      rc = APG_E_HIP;
+    }
+  };
+  if (n_solid) {
+    hip(hipMalloc(&d_solid, n_solid * 8));
+    if (rc == APG_OK) hip(hipMemcpyAsync(d_solid, solid, n_solid * 8, hipMemcpyHostToDevice, ctx->stream));
+  }
+  if (rc == APG_OK && status && np) hip(hipMalloc(&d_status, np));
+  if (rc == APG_OK) rc = apg_fill_fragments_dev(ctx, dr, &p, d_solid, n_solid, &fd, d_status, &st);
+  if (rc == APG_OK) {
+    const uint64_t n = fd->n_reads;
+    out->n_reads = n;
+    uint64_t* bo = (uint64_t*)std::malloc((n + 1) * 8);
+    uint64_t* yo = (uint64_t*)std::malloc((n + 1) * 8);
+    uint8_t* pk = (uint8_t*)std::calloc(fd->n_bytes + 64, 1);
+    out->base_off = bo;
+    out->byte_off = yo;
+    out->packed = pk;
+    if (!bo || !yo || !pk) {
+      set_error("apg_fill_fragments: host allocation failed");
+      rc = APG_E_NOMEM;
+    } else {
+      hip(hipMemcpyAsync(bo, fd->d_base_off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+      hip(hipMemcpyAsync(yo, fd->d_byte_off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+      if (fd->n_bytes) hip(hipMemcpyAsync(pk, fd->d_packed, fd->n_bytes, hipMemcpyDeviceToHost, ctx->stream));
+      if (d_status) hip(hipMemcpyAsync(status, d_status, np, hipMemcpyDeviceToHost, ctx->stream));
+      hip(hipStreamSynchronize(ctx->stream));
+    }
+    if (rc != APG_OK) apg_reads_release(out);
+  }
+  if (d_solid) (void)hipFree(d_solid);
+  if (d_status) (void)hipFree(d_status);
+  apg_reads_free(fd);
+  apg_reads_free(dr);
+  if (rc == APG_OK && stats) *stats = st;
+  return rc;
+}
+
+}  // extern "C"

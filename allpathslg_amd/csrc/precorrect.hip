@@ -360,6 +360,10 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   st->n_ambiguous += h[2];
   st->n_uncorrectable += h[3];
   st->n_solid = n_solid;
+  ctx->pc_list = list;  // APG_FILL_LAST_SOLID (FillFragments after correction)
+  ctx->pc_n = n_solid;
+  ctx->pc_K = p.K;
+  ctx->pc_list_valid = true;
   vlog(ctx, "precorrect pass: solid=%llu suspect=%llu corrected=%llu ambiguous=%llu none=%llu",
        (unsigned long long)n_solid, h[0], h[1], h[2], h[3]);
   static std::atomic<uint64_t> g_edit{1ull << 62};
@@ -447,6 +451,16 @@ int apg_solid_export(apg_ctx* ctx, void* d_out) {
   uint64_t* list = nullptr;
   APG_TRY(workspace_t(ctx, "pc_solid", ctx->n_solid, &list));
   APG_CHECK_HIP(hipMemcpyAsync(d_out, list, ctx->n_solid * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  return sync(ctx);
+}
+
+int apg_solid_copy(apg_ctx* ctx, void* d_out, uint64_t* n_solid) {
+  APG_REQUIRE(ctx && n_solid, "apg_solid_copy: NULL argument");
+  APG_REQUIRE(ctx->pc_list_valid, "apg_solid_copy: no correction pass has run on this context");
+  *n_solid = ctx->pc_n;
+  if (!d_out || ctx->pc_n == 0) return APG_OK;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_CHECK_HIP(hipMemcpyAsync(d_out, ctx->pc_list, ctx->pc_n * 8, hipMemcpyDeviceToDevice, ctx->stream));
   return sync(ctx);
 }
 

@@ -526,6 +526,7 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
   uint64_t solid_cap = 0;
   uint64_t* sl = nullptr;
   if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
+    ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
     solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }

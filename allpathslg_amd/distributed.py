@@ -61,6 +61,11 @@ class HipShardBackend:
         torch.cuda.synchronize(self.device)
         return self.ctx.precorrect_solid(dreads, solid.data_ptr(), n_solid, **prm)
 
+    def fill(self, dreads: DeviceReads, solid: torch.Tensor, n_solid: int, prm: dict, out=None):
+        torch.cuda.synchronize(self.device)
+        filled, _, st = self.ctx.fill_fragments(dreads, (solid.data_ptr(), n_solid), out=out, **prm)
+        return filled, st
+
     # unipath stages
     def ushard_count(self, dreads: DeviceReads, K: int, P: int) -> Tuple[np.ndarray, int]:
         return self.ctx.ushard_count(dreads, K, P)
@@ -202,11 +207,13 @@ def sharded_spectrum(backend, reads, K: int, hist_len: int = DEFAULT_HIST_LEN,
 
 
 def sharded_precorrect(backend, reads, K: int = 24, min_solid: int = 3, max_q_suspect: int = 20, n_cycles: int = 1,
-                       group: Optional[dist.ProcessGroup] = None) -> dict:
+                       group: Optional[dist.ProcessGroup] = None, keep_solid: bool = False):
     """PreCorrect / FindErrors over every rank's reads: per pass,
     K-mers are counted on their owner shards, each shard's solid set is
     all_gathered (the replicated solid set), and every rank corrects its own
-    reads in place.  Returns stats summed over ranks (n_solid = global)."""
+    reads in place.  Returns stats summed over ranks (n_solid = global); with
+    keep_solid, (stats, solid tensor, n_solid) — the last pass's replicated
+    solid set, for sharded_fill."""
     P = dist.get_world_size(group)
     _check_pow2(P)
     dev = backend.alloc(1).device
@@ -228,7 +235,27 @@ def sharded_precorrect(backend, reads, K: int = 24, min_solid: int = 3, max_q_su
     st_t = torch.tensor([tot[k] for k in keys], dtype=torch.int64, device=dev)
     dist.all_reduce(st_t, group=group)
     tot.update({k: int(v) for k, v in zip(keys, st_t.cpu().tolist())})
-    return tot
+    return (tot, solid, tot["n_solid"]) if keep_solid else tot
+
+
+FILL_KEYS = ("n_pairs", "n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases")
+
+
+def sharded_fill(backend, reads, solid, n_solid: int, K: int = 24, min_insert: int = 126, max_insert: int = 234,
+                 max_steps: int = 1024, out=None, group: Optional[dist.ProcessGroup] = None):
+    """FillFragments on every rank's own pairs (ranks hold whole pairs)
+    against the replicated solid set of sharded_precorrect(keep_solid=True):
+    no exchange ("reads sharded, no exchange").  Returns this
+    rank's filled fragments and the stats summed over ranks."""
+    prm = {"K": K, "min_insert": min_insert, "max_insert": max_insert, "max_steps": max_steps}
+    filled, st = backend.fill(reads, solid, n_solid, prm, out)
+    dev = backend.alloc(1).device
+    t = torch.tensor([int(st[k]) for k in FILL_KEYS], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, group=group)
+    tot = dict(st)
+    tot.update({k: int(v) for k, v in zip(FILL_KEYS, t.cpu().tolist())})
+    tot["n_solid"] = n_solid
+    return filled, tot
 
 
 def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGroup] = None,

@@ -38,12 +38,18 @@ def shard_bins(K: int, n_shards: int) -> int:
 class DeviceReads:
     """A read set resident in HBM (apg_dreads)."""
 
-    def __init__(self, ctx: "Context", reads: ReadSet):
+    def __init__(self, ctx: "Context", reads: Optional[ReadSet]):
         self.ctx = ctx
         self.reads = reads
         self._h = C.c_void_p()
+        if reads is None:  # filled in by a device-side producer (apg_fill_fragments_dev)
+            return
         r = reads.c_struct()
         check(lib().apg_reads_upload(ctx.handle, C.byref(r), C.byref(self._h)), "apg_reads_upload")
+
+    @property
+    def n_reads(self) -> int:
+        return int(lib().apg_dreads_count(self._h)) if self._h else 0
 
     @property
     def handle(self):
@@ -192,6 +198,14 @@ class Context:
     def solid_export(self, d_out_ptr: int) -> None:
         check(lib().apg_solid_export(self._h, C.c_void_p(d_out_ptr)), "apg_solid_export")
 
+    def solid_copy(self, d_out_ptr: Optional[int] = None) -> int:
+        """Copy the last correction pass's solid hashes to a device buffer
+        (None: size only); returns their number."""
+        n = C.c_uint64()
+        check(lib().apg_solid_copy(self._h, C.c_void_p(d_out_ptr) if d_out_ptr else None, C.byref(n)),
+              "apg_solid_copy")
+        return int(n.value)
+
     def precorrect_solid(self, dreads: DeviceReads, d_solid_ptr: int, n_solid: int, K: int = 24, min_solid: int = 3,
                          max_q_suspect: int = 20) -> dict:
         p = self.pc_params(K, min_solid, max_q_suspect, 1)
@@ -208,6 +222,62 @@ class Context:
                                        q.ctypes.data_as(C.POINTER(C.c_uint8)) if q is not None else None),
               "apg_reads_download")
         return ReadSet(r.base_off.copy(), r.byte_off.copy(), pk, q)
+
+    # -- FillFragments ---------------------------------------------------------
+    @staticmethod
+    def fill_params(K: int = 24, min_insert: int = 126, max_insert: int = 234, max_steps: int = 1024,
+                    min_solid: int = 3, last_solid: bool = False):
+        from ._lib import APG_FILL_LAST_SOLID, apg_fill_params
+
+        p = apg_fill_params()
+        lib().apg_fill_defaults(C.byref(p))
+        p.K, p.min_insert, p.max_insert, p.max_steps, p.min_solid = K, min_insert, max_insert, max_steps, min_solid
+        p.flags = APG_FILL_LAST_SOLID if last_solid else 0
+        return p
+
+    def fill_fragments(self, pairs, solid=None, K: int = 24, min_insert: int = 126, max_insert: int = 234,
+                       max_steps: int = 1024, min_solid: int = 3, last_solid: bool = False, out=None,
+                       status: bool = False):
+        """FillFragments (include/apg.h): pairs (2i, 2i+1) closed through the
+        solid K-mer graph.  `solid`: hashes of solid canonical K-mers (numpy
+        u64 for host pairs; (device pointer, count) for DeviceReads), or None
+        = last correction pass's set (last_solid=True) / the pairs' own
+        count.  ReadSet -> (filled ReadSet, status u8 or None, stats);
+        DeviceReads -> (DeviceReads of the filled fragments (reusing `out`),
+        None, stats)."""
+        from ._lib import apg_fill_stats
+
+        p = self.fill_params(K, min_insert, max_insert, max_steps, min_solid, last_solid)
+        st = apg_fill_stats()
+        L = lib()
+        if isinstance(pairs, DeviceReads):
+            dptr, ns = solid if solid is not None else (None, 0)
+            fd = out if out is not None else DeviceReads(self, None)
+            check(L.apg_fill_fragments_dev(self._h, pairs.handle, C.byref(p), C.c_void_p(dptr) if dptr else None, ns,
+                                           C.byref(fd._h), None, C.byref(st)), "apg_fill_fragments_dev")
+            return fd, None, st.as_dict()
+        from ._lib import apg_reads
+
+        sh = None if solid is None else np.ascontiguousarray(solid, dtype=np.uint64)
+        r = pairs.c_struct()
+        o = apg_reads()
+        np_ = pairs.n_reads // 2
+        stat = np.zeros(max(np_, 1), dtype=np.uint8) if status else None
+        check(L.apg_fill_fragments(self._h, C.byref(r), C.byref(p), sh.ctypes.data_as(_u64p) if sh is not None else None,
+                                   0 if sh is None else len(sh), C.byref(o),
+                                   stat.ctypes.data_as(C.POINTER(C.c_uint8)) if stat is not None else None,
+                                   C.byref(st)), "apg_fill_fragments")
+        try:
+            n = int(o.n_reads)
+            bo = np.ctypeslib.as_array(o.base_off, shape=(n + 1,)).copy()
+            yo = np.ctypeslib.as_array(o.byte_off, shape=(n + 1,)).copy()
+            nb = int(yo[-1])
+            pk = np.zeros(nb + 64, dtype=np.uint8)
+            if nb:
+                pk[:nb] = np.ctypeslib.as_array(o.packed, shape=(nb,))
+        finally:
+            L.apg_reads_release(C.byref(o))
+        return ReadSet(bo, yo, pk, None), (stat[:np_] if stat is not None else None), st.as_dict()
 
     # -- unipaths -------------------------------------------------------------
     def unipaths(self, reads, K: int = 96, read_paths: bool = True, fetch: bool = True):

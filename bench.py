@@ -9,13 +9,14 @@ in HBM:
   1. restore the rank's reads to their uploaded state (device copy)
   2. K=25 canonical k-mer count + spectrum of the 40 M reads
   3. K=24 PreCorrect of the 40 M reads (count, solid set, per-read correction)
-  4. K=96 unipaths + unibases + HyperKmerPath + KmerPaths of the 20 M pair
-     fragments.  The fragments are the simulator's true inserts ("oracle
-     fill", SURVEY §8d: K=96 needs ~180 bp fragments; FillFragments is §8f
-     next #1), generated once outside the timed region.
+  4. FillFragments of the 20 M corrected pairs (K=24 closures through the
+     PreCorrect solid set) -> ~180 bp fragments
+  5. K=96 unipaths + unibases + HyperKmerPath + KmerPaths of the filled
+     fragments (K=96 needs fragment-length inputs).
+     --oracle-fill substitutes the simulator's true inserts (old bench).
 N > 1: weak scaling (40 M reads per GPU); k-mers hash-sharded across ranks
 with all_to_all over RCCL, solid sets all_gathered, spectra all_reduced,
-unipath nodes all_gathered.
+pairs filled where they live (no exchange), unipath nodes all_gathered.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -37,7 +38,7 @@ sys.path.insert(0, ROOT)
 
 from allpathslg_amd import Context, synth_fragments, synth_genome, synth_reads  # noqa: E402
 from allpathslg_amd.distributed import (  # noqa: E402
-    HipShardBackend, sharded_precorrect, sharded_spectrum, sharded_unipaths)
+    HipShardBackend, sharded_fill, sharded_precorrect, sharded_spectrum, sharded_unipaths)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -56,7 +57,10 @@ def parse():
     p.add_argument("--spectrum-only", action="store_true")
     p.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
     p.add_argument("--cpu-correct-sample-reads", type=int, default=1_000_000)
-    p.add_argument("--cpu-unipath-sample-frags", type=int, default=20_000)
+    p.add_argument("--cpu-unipath-sample-frags", type=int, default=20_000,
+                   help="pairs of the CPU baseline's FillFragments + unipath sample")
+    p.add_argument("--oracle-fill", action="store_true",
+                   help="feed the unipath stage the simulator's true inserts instead of FillFragments (old bench)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--sharded", action="store_true",
@@ -94,7 +98,7 @@ def main():
     genome = synth_genome(a.genome_len, a.seed)
     n_pairs = a.reads_per_gpu // 2
     reads = synth_reads(genome, n_pairs, seed=a.seed + 1, first_pair=rank * n_pairs, with_quals=True, threads=16)
-    frags = None if a.spectrum_only else synth_fragments(genome, n_pairs, seed=a.seed + 1,
+    frags = None if (a.spectrum_only or not a.oracle_fill) else synth_fragments(genome, n_pairs, seed=a.seed + 1,
                                                          first_pair=rank * n_pairs, threads=16)
     log(rank, f"synth {reads.n_reads} reads + fragments in {time.time() - t0:.1f}s")
 
@@ -103,6 +107,7 @@ def main():
     dreads = ctx.upload(reads)
     dfrags = None if frags is None else ctx.upload(frags)
     backend = HipShardBackend(ctx)
+    fill = {"out": None}  # device read set of the filled fragments, reused every step
 
     def step():
         ctx.copy_reads(dreads, dsrc)
@@ -110,18 +115,30 @@ def main():
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
             hist, st = sharded_spectrum(backend, dreads, a.K)
-        pst = ust = None
+        pst = ust = fst = None
         if not a.spectrum_only:
             if not sharded:
                 _, pst = ctx.precorrect(dreads, K=a.K_correct)
-                _, ust = ctx.unipaths(dfrags, a.K_unipath, read_paths=True, fetch=False)
+                if a.oracle_fill:
+                    uin = dfrags
+                else:
+                    fill["out"], _, fst = ctx.fill_fragments(dreads, K=a.K_correct, last_solid=True,
+                                                             out=fill["out"])
+                    uin = fill["out"]
+                _, ust = ctx.unipaths(uin, a.K_unipath, read_paths=True, fetch=False)
             else:
-                pst = sharded_precorrect(backend, dreads, K=a.K_correct)
-                ust = sharded_unipaths(backend, dfrags, a.K_unipath)
-        return hist, st, pst, ust
+                pst, solid, ns = sharded_precorrect(backend, dreads, K=a.K_correct, keep_solid=True)
+                if a.oracle_fill:
+                    uin = dfrags
+                else:
+                    fill["out"], fst = sharded_fill(backend, dreads, solid, ns, K=a.K_correct, out=fill["out"])
+                    uin = fill["out"]
+                del solid
+                ust = sharded_unipaths(backend, uin, a.K_unipath)
+        return hist, st, pst, ust, fst
 
     for _ in range(a.warmup):
-        hist, st, pst, ust = step()
+        hist, st, pst, ust, fst = step()
     free_b, total_b = torch.cuda.mem_get_info()
     torch.cuda.synchronize()
     ctx.reset_timing()
@@ -131,7 +148,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(a.steps):
-        hist, st, pst, ust = step()
+        hist, st, pst, ust, fst = step()
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
@@ -153,7 +170,14 @@ def main():
     }
     if pst is not None:
         checks["precorrect_corrected_most_suspects"] = pst["n_corrected"] > 0.5 * pst["n_suspect"]
-        n_inst = world * int((np.maximum(frags.lengths().astype(np.int64) - a.K_unipath + 1, 0)).sum())
+        if fst is not None:  # every filled fragment is >= min_insert > K_unipath long
+            n_inst = int(fst["filled_bases"]) - (a.K_unipath - 1) * int(fst["n_filled"])
+            checks["fill_statuses_cover_all_pairs"] = (
+                sum(int(fst[k]) for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip"))
+                == world * n_pairs)
+            checks["fill_filled_most_pairs"] = fst["n_filled"] > 0.5 * world * n_pairs
+        else:
+            n_inst = world * int((np.maximum(frags.lengths().astype(np.int64) - a.K_unipath + 1, 0)).sum())
         checks["unipath_instances_equal_sum_len_minus_K_plus_1"] = ust["n_instances"] == n_inst
         # iid genome, no K=96 repeat: one unipath pair holding every node, and the
         # nodes are the genome's K-mers bar a few uncovered at the chromosome ends
@@ -210,15 +234,31 @@ def main():
             oracle.precorrect(csample, K=a.K_correct)
             tp = time.perf_counter() - tp
             pc_rate = csample.n_reads / tp
-            usample = frags.subset(0, min(a.cpu_unipath_sample_frags, frags.n_reads))
+            npair = min(a.cpu_unipath_sample_frags, n_pairs)
+            if frags is not None:  # --oracle-fill: the true inserts
+                usample = frags.subset(0, npair)
+                fill_rate, fdesc = None, ""
+            else:  # FillFragments of the GPU-corrected pairs against the full-size solid set
+                solid_t = torch.empty(max(ctx.solid_copy(None), 1), dtype=torch.int64, device="cuda")
+                ns = ctx.solid_copy(solid_t.data_ptr())
+                solid_h = solid_t[:ns].cpu().numpy().view(np.uint64)
+                del solid_t
+                fixed = ctx.download(dreads).subset(0, 2 * npair)
+                tf = time.perf_counter()
+                usample, _, _, _ = oracle.fill_fragments(fixed, solid_h, K=a.K_correct)
+                tf = time.perf_counter() - tf
+                fill_rate = 2 * npair / tf
+                fdesc = (f"; FillFragments: first {npair} GPU-corrected pairs against the full solid set "
+                         f"({ns} K-mers, binary search) ({tf:.2f} s)")
             tu = time.perf_counter()
             oracle.unipaths(usample, a.K_unipath)
             tu = time.perf_counter() - tu
-            uni_rate = 2 * usample.n_reads / tu  # two reads per fragment
-            rate = 1.0 / (1.0 / spec_rate + 1.0 / pc_rate + 1.0 / uni_rate)
+            uni_rate = 2 * npair / tu  # two reads per pair
+            inv = 1.0 / spec_rate + 1.0 / pc_rate + 1.0 / uni_rate + (1.0 / fill_rate if fill_rate else 0.0)
+            rate = 1.0 / inv
             desc += (f"; PreCorrect: first {csample.n_reads} reads, K={a.K_correct} against their own "
-                     f"solid set ({tp:.2f} s); unipaths: first {usample.n_reads} fragments "
-                     f"(= {2 * usample.n_reads} reads), K={a.K_unipath} ({tu:.2f} s)")
+                     f"solid set ({tp:.2f} s)" + fdesc + f"; unipaths: the {usample.n_reads} fragments of "
+                     f"those {npair} pairs, K={a.K_unipath} ({tu:.2f} s)")
         cpu = {"value": rate, "unit": "reads/s", "cores": 1, "kind": "port",
                "sample": "oracle/ CPU restatement, single-threaded, same synthetic inputs; " + desc +
                          "; value = 1/(sum of 1/stage_rate)"}
@@ -241,17 +281,20 @@ def main():
                     "Q40 / Q2-20 on errors)",
             "config": {
                 "workload": "C2/C3 chr20-size: 40M x 100bp paired frag reads per GPU; K=25 k-mer spectrum + "
-                            "K=24 PreCorrect + K=96 unipath build (unipaths, unibases, HyperKmerPath, "
-                            "fragment KmerPaths) on the 20M pair fragments",
+                            "K=24 PreCorrect + FillFragments + K=96 unipath build (unipaths, unibases, "
+                            "HyperKmerPath, fragment KmerPaths) on the filled fragments",
                 "reads_per_gpu": reads.n_reads,
                 "genome_len": a.genome_len,
                 "K": a.K,
                 "K_correct": None if a.spectrum_only else a.K_correct,
                 "K_unipath": None if a.spectrum_only else a.K_unipath,
                 "stages_timed": ["restore_reads", "kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
-                    "precorrect", "unipath_kmers", "unipaths", "unibases", "hyperkmerpath", "fragment_kmerpaths"]),
-                "unipath_input": "simulator's true pair inserts (oracle fill standing in for FillFragments, "
-                                 "SURVEY §8d), generated outside the timed region",
+                    "precorrect"] + ([] if a.oracle_fill else ["fill_fragments"]) + [
+                    "unipath_kmers", "unipaths", "unibases", "hyperkmerpath", "fragment_kmerpaths"]),
+                "unipath_input": ("simulator's true pair inserts (--oracle-fill), generated outside the timed region"
+                                  if a.oracle_fill else
+                                  "FillFragments of the corrected pairs (K=24 closures, insert 126-234), on GPU "
+                                  "inside the timed step"),
                 "hbm_used_gb": (total_b - free_b) / 1e9,
                 "parallelism": f"kmer-hash shards x{world} + all_to_all" if sharded else "single GPU",
             },
@@ -260,6 +303,7 @@ def main():
             "cpu_baseline": cpu,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},
             "precorrect_stats": pst,
+            "fill_stats": fst,
             "unipath_stats": ust,
             "checks": checks,
         }
@@ -268,6 +312,8 @@ def main():
     dsrc.free()
     if dfrags is not None:
         dfrags.free()
+    if fill["out"] is not None:
+        fill["out"].free()
     ctx.close()
     if sharded:
         dist.destroy_process_group()

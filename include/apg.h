@@ -209,10 +209,80 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
                     int K, int n_shards, uint32_t min_solid, uint64_t* n_solid);
 /* d_out: device buffer of n_solid u64 (the hash of each solid K-mer). */
 int apg_solid_export(apg_ctx* ctx, void* d_out);
+/* The solid set (apg_kmer_hash values, any order) the last correction pass on
+ * this context corrected against — what APG_FILL_LAST_SOLID uses.  d_out:
+ * device buffer of *n_solid u64, or NULL to query the size. */
+int apg_solid_copy(apg_ctx* ctx, void* d_out, uint64_t* n_solid);
 /* One correction pass (p->n_cycles is ignored) against the given solid
  * hashes (apg_kmer_hash of canonical K-mers, device memory). */
 int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
                          const void* d_solid, uint64_t n_solid, apg_pc_stats* stats);
+
+/* ------------------------------------------------------------------------- */
+/* FillFragments (replaces module FillFragments, [R:M]   */
+/* src/paths/FillFragments.cc — recalled, no line exists to cite): close     */
+/* each overlapping / short-gap frag pair into the fragment it was read      */
+/* from, the K=96 unipath stage's input.  Spec (semantics unpinned):         */
+/*   pair i = reads (2i, 2i+1) = (A, B), FR; F = rc(B).  A closure of length */
+/*   I is a sequence S with S[0,La) = A, S[I-Lf,I) = F (equal where they     */
+/*   overlap), I in [max(min_insert, La, Lf), max_insert], and every K-mer   */
+/*   of S solid — S is a path of the solid K-mer graph: A's and F's own      */
+/*   K-mers and the "bridge" K-mers in neither (start in [La-K+1, I-Lf-1]).  */
+/*   Exactly one closure: filled with S (A's orientation).                   */
+/*   Search order: overlap lengths I < La+Lf ascending, then a depth-first   */
+/*   walk from A's last K-1 bases over solid K-mers (bases A<C<G<T, depth    */
+/*   d = I-La-Lf); per node the closure test, then the expansion; more than  */
+/*   max_steps expansions -> BUDGET, a second closure -> AMBIGUOUS.          */
+/*   Pairs with La or Lf < K, or max_insert-(La+Lf) > 63, are SKIP.          */
+/* Solid set: hashes (apg_kmer_hash) of canonical K-mers, given by the       */
+/* caller, or APG_FILL_LAST_SOLID = the set of this context's last           */
+/* PreCorrect / FindErrors pass, or (neither) counted from the pairs         */
+/* themselves with min_solid.                                                */
+/* ------------------------------------------------------------------------- */
+#define APG_FILL_OK 0
+#define APG_FILL_NONE 1
+#define APG_FILL_AMBIGUOUS 2
+#define APG_FILL_BUDGET 3
+#define APG_FILL_SKIP 4
+#define APG_FILL_LAST_SOLID 1u
+
+typedef struct apg_fill_params {
+  int32_t K;            /* default 24, 2 <= K <= 29 */
+  uint32_t min_insert;  /* default 126 (180 - 3 x 18) */
+  uint32_t max_insert;  /* default 234 (180 + 3 x 18) */
+  uint32_t max_steps;   /* walk expansions per pair, default 1024 */
+  uint32_t min_solid;   /* default 3 (own-count mode only) */
+  uint32_t flags;       /* APG_FILL_LAST_SOLID */
+  uint64_t reserved[3];
+} apg_fill_params;
+
+typedef struct apg_fill_stats {
+  uint64_t n_pairs;
+  uint64_t n_filled;
+  uint64_t n_none;
+  uint64_t n_ambiguous;
+  uint64_t n_budget;
+  uint64_t n_skip;
+  uint64_t filled_bases;
+  uint64_t n_solid;   /* size of the solid set used */
+  uint64_t lookups;   /* (K-1)-mer extension-table lookups (implementation statistic) */
+  uint64_t reserved[3];
+} apg_fill_stats;
+
+void apg_fill_defaults(apg_fill_params* p);
+/* Host buffers.  solid: n_solid hashes or NULL.  out: the filled fragments in
+ * pair order (library-allocated, release with apg_reads_release; no quals).
+ * status: n_reads/2 bytes (APG_FILL_*) or NULL. */
+int apg_fill_fragments(apg_ctx* ctx, const apg_reads* pairs, const apg_fill_params* p,
+                       const uint64_t* solid, uint64_t n_solid, apg_reads* out,
+                       uint8_t* status, apg_fill_stats* stats);
+/* Device variant.  d_solid: device hashes or NULL.  *filled: NULL (a new
+ * device read set is created) or a previous output of this call on the same
+ * context (its buffers are reused); release with apg_reads_free.  filled may
+ * be NULL (stats only).  d_status: device n_pairs bytes or NULL. */
+int apg_fill_fragments_dev(apg_ctx* ctx, const apg_dreads* pairs, const apg_fill_params* p,
+                           const void* d_solid, uint64_t n_solid, apg_dreads** filled,
+                           uint8_t* d_status, apg_fill_stats* stats);
 
 /* ------------------------------------------------------------------------- */
 /* Unipath graph, 1 <= K <= 96 (default 96).  Replaces CommonPather /        */

@@ -145,6 +145,60 @@ def precorrect_solid(reads, solid_hashes, K=24, max_q=20):
     return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), {k: int(v) for k, v in zip(keys, st)}
 
 
+FILL_STATUS = {0: "filled", 1: "none", 2: "ambiguous", 3: "budget", 4: "skip"}
+
+
+def solid_hashes(reads, K: int = 24, min_solid: int = 3) -> np.ndarray:
+    """Hashes of the canonical K-mers of `reads` seen >= min_solid times."""
+    h, c = kmer_count(reads, K)
+    return h[c >= min_solid]
+
+
+def fill_fragments(reads, solid, K: int = 24, min_insert: int = 126, max_insert: int = 234,
+                   max_steps: int = 1024):
+    """FillFragments restated (oracle/fill_oracle.c): pairs (2i, 2i+1) closed
+    through the solid K-mer set.  Returns (filled ReadSet in pair order,
+    status uint8[n_pairs], length uint32[n_pairs], stats dict)."""
+    from allpathslg_amd.reads import ReadSet
+
+    L = lib()
+    if not hasattr(L, "_orf"):
+        L.orf_fill.restype = C.c_int
+        L.orf_fill.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, C.c_uint64, C.c_uint32, C.c_uint32,
+                               C.c_uint32, _u8p, _u32p, C.POINTER(_u8p), _u64p]
+        L._orf = True
+    n, bo, yo, pk = _rp(reads)
+    npairs = n // 2
+    status = np.zeros(max(npairs, 1), np.uint8)
+    flen = np.zeros(max(npairs, 1), np.uint32)
+    st = np.zeros(7, np.uint64)
+    sh = np.ascontiguousarray(solid, dtype=np.uint64)
+    outp = _u8p()
+    rc = L.orf_fill(n, bo, yo, pk, K, sh.ctypes.data_as(_u64p), len(sh), min_insert, max_insert, max_steps,
+                    status.ctypes.data_as(_u8p), flen.ctypes.data_as(_u32p), C.byref(outp), st.ctypes.data_as(_u64p))
+    if rc:
+        raise RuntimeError("oracle fill_fragments failed (odd read count, bad K or allocation)")
+    try:
+        nb = int(st[5])
+        codes = np.ctypeslib.as_array(outp, shape=(nb,)).copy() if nb else np.zeros(0, np.uint8)
+    finally:
+        L.ork_free(C.cast(outp, C.c_void_p))
+    status, flen = status[:npairs], flen[:npairs]
+    lens = flen[status == 0].astype(np.uint64)
+    base_off = np.zeros(len(lens) + 1, np.uint64)
+    base_off[1:] = np.cumsum(lens)
+    byte_off = np.zeros(len(lens) + 1, np.uint64)
+    byte_off[1:] = np.cumsum((lens + 3) // 4)
+    packed = np.zeros(int(byte_off[-1]) + 64, np.uint8)
+    for i in range(len(lens)):  # pack each fragment byte-aligned (numpy, small cases)
+        a = codes[int(base_off[i]):int(base_off[i + 1])]
+        a4 = np.concatenate([a, np.zeros((-len(a)) % 4, np.uint8)]).reshape(-1, 4)
+        b = (a4[:, 0] | (a4[:, 1] << 2) | (a4[:, 2] << 4) | (a4[:, 3] << 6)).astype(np.uint8)
+        packed[int(byte_off[i]):int(byte_off[i]) + len(b)] = b
+    keys = ["n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases", "lookups"]
+    return ReadSet(base_off, byte_off, packed, None), status, flen, {k: int(v) for k, v in zip(keys, st)}
+
+
 class _OruResult(C.Structure):
     _fields_ = [
         ("n_nodes", C.c_uint64),

@@ -19,6 +19,10 @@ int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* b
 int ork_precorrect_solid(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
                          uint8_t* quals, int K, uint32_t maxq, const uint64_t* solid, uint64_t ns, uint64_t* stats);
 
+int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
+             const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
+             uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats);
+
 void ora_gapfree(const uint64_t* s_base_off, const uint64_t* s_byte_off, const uint8_t* s_packed,
                  const uint8_t* s_quals, const uint64_t* t_base_off, const uint64_t* t_byte_off,
                  const uint8_t* t_packed, const uint32_t* pairs, uint64_t n, uint32_t* out);

@@ -31,6 +31,21 @@ def main():
     np.savez_compressed(os.path.join(HERE, "kmer_small.npz"), **out)
     print({k: v.shape for k, v in out.items()})
     write_stage_fixtures(g, reads)
+    write_fill_fixture(reads)
+
+
+def write_fill_fixture(reads):
+    """FillFragments of the PreCorrect'ed pairs through the raw reads' solid
+    K=24 set (the bench pipeline's order): status, length and bases."""
+    fixed, _ = oracle.precorrect(reads, K=24)
+    solid = oracle.solid_hashes(reads, 24, 3)
+    filled, status, flen, st = oracle.fill_fragments(fixed, solid, K=24, min_insert=126, max_insert=234)
+    out = {"solid": np.sort(solid), "status": status, "flen": flen,
+           "packed": filled.packed[: int(filled.byte_off[-1])], "base_off": filled.base_off,
+           "stats": np.array([st[k] for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip",
+                                              "filled_bases")], np.uint64)}
+    np.savez_compressed(os.path.join(HERE, "fill_small.npz"), **out)
+    print({k: v.shape for k, v in out.items()}, st)
 
 
 def write_stage_fixtures(g, reads):
@@ -70,4 +85,9 @@ def write_stage_fixtures(g, reads):
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["fill"]:
+        from allpathslg_amd import ReadSet
+
+        write_fill_fixture(ReadSet.load(os.path.join(HERE, "frag_small.fastb"), os.path.join(HERE, "frag_small.qualb")))
+    else:
+        main()

@@ -74,6 +74,11 @@ class OracleShardBackend:
         self.cache.clear()  # bases changed
         return st
 
+    def fill(self, reads, solid, n_solid, prm, out=None):
+        filled, _, _, st = oracle.fill_fragments(reads, solid[:n_solid].numpy().view(np.uint64), **prm)
+        st["n_pairs"] = reads.n_reads // 2
+        return filled, st
+
 
 def _free_port():
     s = socket.socket()
@@ -268,3 +273,49 @@ def test_sharded_precorrect_gloo(world, n_cycles):
     for _, _, _, st in res:
         for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
             assert st[k] == est[k], k
+
+
+def _fillworker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _small_chunks()
+    try:
+        from allpathslg_amd.distributed import sharded_fill, sharded_precorrect
+
+        reads = synth_reads(synth_genome(30_000, 41), 3000, seed=42)
+        pairs = np.array_split(np.arange(reads.n_reads // 2), world)  # ranks hold whole pairs
+        mine = reads.subset(2 * int(pairs[rank][0]), 2 * int(pairs[rank][-1]) + 2)
+        be = OracleShardBackend()
+        _, solid, ns = sharded_precorrect(be, mine, K=24, keep_solid=True)
+        filled, st = sharded_fill(be, mine, solid, ns, K=24)
+        q.put((rank, filled.base_off.copy(), filled.packed[: int(filled.byte_off[-1])].copy(), st))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_fill_gloo(world):
+    """Precorrect with the replicated solid set, then FillFragments per rank
+    == single-process PreCorrect + FillFragments, fragments in pair order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fillworker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    reads = synth_reads(synth_genome(30_000, 41), 3000, seed=42)
+    fixed, _ = oracle.precorrect(reads, K=24)
+    exp, es, _, est = oracle.fill_fragments(fixed, oracle.solid_hashes(reads, 24, 3), K=24)
+    assert est["n_filled"] > 0
+    lens = np.concatenate([np.diff(r[1]) for r in res])
+    assert np.array_equal(lens, np.diff(exp.base_off))
+    assert np.array_equal(np.concatenate([r[2] for r in res]), exp.packed[: int(exp.byte_off[-1])])
+    for _, _, _, st in res:
+        for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases"):
+            assert st[k] == est[k], k
+        assert st["n_pairs"] == reads.n_reads // 2
