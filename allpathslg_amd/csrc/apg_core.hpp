@@ -139,6 +139,11 @@ struct apg_ctx {
   uint64_t pc_n = 0;
   int pc_K = 0;
   bool pc_list_valid = false;
+  // Per-read clean flags of that pass (1: every K-mer solid after correction,
+  // 0: not, 2: not derived), valid for the read set while its gen is clean_gen.
+  const uint8_t* pc_clean = nullptr;
+  uint64_t clean_gen = 0;
+  bool clean_valid = false;
 };
 
 namespace apg {

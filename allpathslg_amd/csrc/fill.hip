@@ -167,6 +167,18 @@ __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, ui
   return true;
 }
 
+// Both reads of a pair solid throughout.  cl (or null): the pair's clean
+// flags from the correction pass that used this solid set (1 clean, 0 not,
+// 2 not derived -> look the read's K-mers up).
+__device__ __forceinline__ bool pair_solid(const ExtTab& t, const uint8_t* A, uint32_t La, const uint8_t* B,
+                                           uint32_t Lf, const uint8_t* cl, uint32_t* nlook) {
+  const uint32_t fa = cl ? cl[0] : 2u, fb = cl ? cl[1] : 2u;
+  if (fa == 0 || fb == 0) return false;
+  if (fa == 2 && !read_solid(t, A, La, nlook)) return false;
+  if (fb == 2 && !read_solid(t, B, Lf, nlook)) return false;
+  return true;
+}
+
 struct FillReads {
   const uint64_t* base_off;
   const uint64_t* byte_off;
@@ -201,7 +213,7 @@ __device__ __forceinline__ uint64_t walk_window(uint64_t atail, unsigned __int12
 __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
                                               uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
-                                              FillCounters* __restrict__ cnt) {
+                                              const uint8_t* __restrict__ clean, FillCounters* __restrict__ cnt) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
@@ -216,7 +228,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     uint32_t st;
     if (La < (uint32_t)K || Lf < (uint32_t)K || (p.max_insert >= La + Lf && p.max_insert - (La + Lf) > kFillMaxGap)) {
       st = kFillSkip;
-    } else if (!read_solid(t, A, La, &nlook) || !read_solid(t, B, Lf, &nlook)) {
+    } else if (!pair_solid(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
       st = kFillNone;  // S must be a path of solid K-mers: no closure through a weak read K-mer
     } else {
       // A's last K-1 bases, MSB-first; F's first 32 bases, LSB-first
@@ -436,12 +448,16 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   std::memset(st, 0, sizeof *st);
   st->n_pairs = np;
   const uint64_t* list = d_solid;
+  const uint8_t* clean = nullptr;
   if (!list && n_solid == 0) {
     if (p.flags & APG_FILL_LAST_SOLID) {
       APG_REQUIRE(ctx->pc_list_valid, "apg_fill_fragments: APG_FILL_LAST_SOLID but no correction pass ran on ctx");
       APG_REQUIRE(ctx->pc_K == p.K, "apg_fill_fragments: last correction pass used another K");
       list = ctx->pc_list;
       n_solid = ctx->pc_n;
+      // the pass's clean flags answer "every K-mer of the read solid" for the
+      // reads it corrected (these very bases: same generation)
+      if (ctx->clean_valid && ctx->clean_gen == dr->gen) clean = ctx->pc_clean;
     } else {  // the pairs' own solid K-mers
       SkResult sr;
       APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
@@ -483,7 +499,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   const FillP fp{p.K, p.min_insert, p.max_insert, p.max_steps};
   kbegin(ctx, "fill", dr->n_bytes + 16 * dr->n_reads + np * (sizeof(FillRec) + 12));
   if (np)
-    k_fill<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status,
+    k_fill<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean,
                                                         reinterpret_cast<FillCounters*>(cnt));
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

@@ -49,6 +49,8 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
                    SkResult* res);
 int sk_spectrum(apg_ctx* ctx, const apg_dreads* dr, int K, bool solid, uint32_t min_solid, uint64_t* hist,
                 size_t hist_len, SkResult* res);
+int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid, unsigned long long* weak,
+                  SkResult* res);
 uint64_t sk_sum_kmers(apg_ctx* ctx, const SK16* recs, uint64_t n, int* rc);
 constexpr int kSkShardBins = 32;  // per-shard digit groups of the exchange (2^kSkDigitBits)
 

@@ -295,6 +295,8 @@ template int part_level<uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const st
                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
 template int part_level<SK16>(apg_ctx*, const SK16*, SK16*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
                               uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SK24>(apg_ctx*, const SK24*, SK24*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
+                              uint64_t*, std::vector<uint64_t>*, const char*);
 template int part_level<SK48>(apg_ctx*, const SK48*, SK48*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
                               uint64_t*, std::vector<uint64_t>*, const char*);
 

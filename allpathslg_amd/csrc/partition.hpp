@@ -26,6 +26,14 @@ struct __attribute__((aligned(16))) SK16 {
   uint64_t w0, w1;
 };
 
+// SK16 + the global base position of the record's first K-mer (read r's
+// K-mer j starts at base base_off[r] + j): the solid-set pass of PreCorrect
+// uses it to mark every weak K-mer instance in a per-base bitmap while
+// counting, so the correction needs no lookups to find weak K-mers.
+struct __attribute__((aligned(8))) SK24 {
+  uint64_t w0, w1, pos;
+};
+
 // 48-byte super-k-mer record of the K <= 96 unipath node builder
 // (unipath.hip): w0 = 32-bit minimizer key | n_kmers << 32 | flags << 40
 // (bit 0: b[] starts one base before the first K-mer, bit 1: it ends one base
@@ -40,6 +48,7 @@ struct __attribute__((aligned(16))) SK48 {
 __host__ __device__ inline uint64_t rkey(uint64_t r) { return r; }
 __host__ __device__ inline uint64_t rkey(const KRec& r) { return r.meta; }
 __host__ __device__ inline uint64_t rkey(const SK16& r) { return r.w0 << 32; }  // the minimizer key
+__host__ __device__ inline uint64_t rkey(const SK24& r) { return r.w0 << 32; }
 __host__ __device__ inline uint64_t rkey(const SK48& r) { return r.w0 << 32; }
 
 constexpr int kMaxLevelBits = 8;  // max digit bits of one partition level (LDS-staged scatter)

@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
                                                     const uint64_t* __restrict__ byte_off, uint8_t* __restrict__ packed,
                                                     uint8_t* __restrict__ quals, uint64_t n_reads, int K, HashP hp,
                                                     uint32_t maxq, SolidSet ss, uint32_t min_len,
-                                                    PcCounters* __restrict__ cnt) {
+                                                    uint8_t* __restrict__ clean, PcCounters* __restrict__ cnt) {
   uint32_t n_tab = 0;
   unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads;
@@ -115,6 +115,7 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
     const uint64_t q0 = base_off[r];
     const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
     if (L < (uint32_t)K || L < min_len) continue;
+    if (clean) clean[r] = 2;  // not derived for long reads: FillFragments checks them itself
     uint8_t* rd = packed + byte_off[r];
     uint8_t* q = quals + q0;
     for (uint32_t p = 0; p < L; ++p) {
@@ -210,7 +211,8 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
                                                          const uint64_t* __restrict__ byte_off,
                                                          uint8_t* __restrict__ packed, uint8_t* __restrict__ quals,
                                                          uint64_t n_reads, int K, HashP hp, uint32_t maxq,
-                                                         SolidSet ss, PcCounters* __restrict__ cnt) {
+                                                         SolidSet ss, const unsigned long long* __restrict__ weak,
+                                                         uint8_t* __restrict__ clean, PcCounters* __restrict__ cnt) {
   uint32_t n_tab = 0;
   const int lane = lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -219,7 +221,11 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
   for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave_id(); r < n_reads; r += nwaves) {
     const uint64_t q0 = base_off[r];
     const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
-    if (L < (uint32_t)K || L > kPcMaxL) continue;  // wave-uniform
+    if (L < (uint32_t)K) {  // wave-uniform; no K-mer, nothing weak
+      if (clean && lane == 0) clean[r] = 1;
+      continue;
+    }
+    if (L > kPcMaxL) continue;  // the thread-per-read kernel's
     uint8_t* rd = packed + byte_off[r];
     uint8_t* q = quals + q0;
     const uint32_t nbytes = (L + 3) >> 2;
@@ -229,6 +235,19 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
       word = (uint32_t)rd[b] | (b + 1 < nbytes ? (uint32_t)rd[b + 1] << 8 : 0u) |
              (b + 2 < nbytes ? (uint32_t)rd[b + 2] << 16 : 0u) | (b + 3 < nbytes ? (uint32_t)rd[b + 3] << 24 : 0u);
     }
+    // Weak-bitmap mode: lane i holds the weak bits of K-mers [16i, 16i+16) as
+    // counted (W16) and the corrected positions [16i, 16i+16) so far (C16).
+    uint32_t W16 = 0, C16 = 0;
+    const uint32_t nK = L - (uint32_t)K + 1;
+    if (weak && 16u * lane < nK) {
+      const uint64_t b = q0 + 16u * lane;
+      const uint32_t sh = (uint32_t)(b & 63);
+      uint64_t x = weak[b >> 6] >> sh;
+      if (sh > 48) x |= weak[(b >> 6) + 1] << (64 - sh);
+      W16 = (uint32_t)x & 0xffffu;
+      if (nK - 16u * lane < 16) W16 &= (1u << (nK - 16u * lane)) - 1;
+    }
+    int last_corr = -1;  // wave-uniform: latest corrected position
     for (uint32_t c = 0; c < L; c += 64) {
       const uint32_t pl = c + lane;
       uint64_t m = __ballot(pl < L && q[pl] < maxq);
@@ -238,12 +257,28 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - K : 0;
         const uint32_t jhi = min(p, L - (uint32_t)K);
         const uint32_t nk = jhi - jlo + 1;  // <= K <= 32
-        // every lane takes part in the shuffles; lanes >= nk repeat the last K-mer
-        const uint64_t Wk = window_at(word, jlo + min((uint32_t)lane, nk - 1), hp.mask);
-        bool solid = false;
-        if ((uint32_t)lane < nk) solid = is_solid(ss, canon_hash(Wk, K, hp), &n_tab);
-        n_look += nk;
-        if (__ballot(solid)) continue;
+        if (weak) {
+          // A covering K-mer holding an earlier correction is solid (it was
+          // checked when that base was corrected); the others are unchanged
+          // since counting, so their weakness is the counted bit.
+          if (last_corr >= 0 && p - (uint32_t)last_corr < (uint32_t)K) continue;
+          const uint32_t li = jlo >> 4;
+          uint64_t x = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < 3; ++k) {
+            const uint32_t v = (uint32_t)__shfl((int)W16, (int)min(li + k, 63u), 64);
+            if (li + k < 64) x |= (uint64_t)v << (16 * k);
+          }
+          const uint64_t need = (1ull << nk) - 1;
+          if (((x >> (jlo & 15)) & need) != need) continue;
+        } else {
+          // every lane takes part in the shuffles; lanes >= nk repeat the last K-mer
+          const uint64_t Wk = window_at(word, jlo + min((uint32_t)lane, nk - 1), hp.mask);
+          bool solid = false;
+          if ((uint32_t)lane < nk) solid = is_solid(ss, canon_hash(Wk, K, hp), &n_tab);
+          n_look += nk;
+          if (__ballot(solid)) continue;
+        }
         ++n_sus;
         const uint32_t orig = (__shfl((int)word, (int)(p >> 4), 64) >> (2 * (p & 15))) & 3;
         // Alternatives in two rounds of lookups: (A) the first covering K-mer
@@ -278,7 +313,9 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           if ((uint32_t)lane == (p >> 4)) {
             const uint32_t sh = 2 * (p & 15);
             word = (word & ~(3u << sh)) | (cand << sh);
+            C16 |= 1u << (p & 15);
           }
+          last_corr = (int)p;
           const uint32_t nw = (uint32_t)__shfl((int)word, (int)(p >> 4), 64);
           if (lane == 0) {
             rd[p >> 2] = (uint8_t)(nw >> (8 * ((p >> 2) & 3)));
@@ -295,6 +332,25 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         }
       }
     }
+    if (clean) {
+      // Clean read (every K-mer solid after correction, the FillFragments
+      // precondition): each counted-weak K-mer holds a corrected base —
+      // K-mer j is covered iff a C bit lies in [j, j+K-1].
+      uint32_t unc = 0;
+      if (weak) {
+        uint64_t X = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 3; ++k) {
+          const uint32_t v = (uint32_t)__shfl((int)C16, (int)min((uint32_t)lane + k, 63u), 64);
+          if ((uint32_t)lane + k < 64) X |= (uint64_t)v << (16 * k);
+        }
+        uint64_t D = 0;
+        for (int s = 0; s < K; ++s) D |= X >> s;
+        unc = W16 & ~(uint32_t)D & 0xffffu;
+      }
+      const bool any = __ballot(unc != 0) != 0;
+      if (lane == 0) clean[r] = weak ? (any ? 0 : 1) : 2;
+    }
   }
   wave_add(&cnt->table_probes, n_tab);
   if (lane == 0) {
@@ -307,8 +363,15 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
 }
 
 // One correction pass of every read of `dr` against the solid hash list.
+// weak: the pass's weak-instance bitmap (sk_solid_weak) or null (weak tests
+// by lookups); with it, the pass also leaves per-read clean flags ("pc_clean":
+// 1 every K-mer solid after correction, 0 not, 2 not derived) for
+// FillFragments.
 static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const uint64_t* list, uint64_t n_solid,
-                        apg_pc_stats* st) {
+                        apg_pc_stats* st, const unsigned long long* weak = nullptr) {
+  ctx->clean_valid = false;
+  uint8_t* clean = nullptr;
+  if (weak) APG_TRY(workspace_t(ctx, "pc_clean", std::max<uint64_t>(dr->n_reads, 1), &clean));
   unsigned long long* dcnt = nullptr;
   APG_TRY(workspace_t(ctx, "pc_counters", 8, &dcnt));
   APG_CHECK_HIP(hipMemsetAsync(dcnt, 0, 8 * 8, ctx->stream));
@@ -334,17 +397,18 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   const SolidSet ss{table, T - 1, bitmap, 2 * p.K - mb};
   APG_CHECK_HIP(hipGetLastError());
   const HashP hp = make_hashp(p.K);
-  kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases);
+  // reads + quals (+ the weak bitmap and the clean flags)
+  kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases + (weak ? dr->n_bases / 8 + dr->n_reads : 0));
   if (dr->n_reads)
     k_precorrect_wave<<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
-        dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss,
-        reinterpret_cast<PcCounters*>(dcnt));
+        dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss, weak,
+        clean, reinterpret_cast<PcCounters*>(dcnt));
   kend(ctx);
   if (dr->max_len > kPcMaxL) {  // reads longer than one wave's registers: thread per read
     const uint64_t rgrid =
         std::max<uint64_t>(1, std::min<uint64_t>((dr->n_reads + 255) / 256, (uint64_t)ctx->n_cu * 32));
     k_precorrect<<<rgrid, 256, 0, ctx->stream>>>(dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals,
-                                                 dr->n_reads, p.K, hp, p.max_q_suspect, ss, kPcMaxL + 1,
+                                                 dr->n_reads, p.K, hp, p.max_q_suspect, ss, kPcMaxL + 1, clean,
                                                  reinterpret_cast<PcCounters*>(dcnt));
   }
   APG_CHECK_HIP(hipGetLastError());
@@ -368,13 +432,25 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
        (unsigned long long)n_solid, h[0], h[1], h[2], h[3]);
   static std::atomic<uint64_t> g_edit{1ull << 62};
   dr->gen = g_edit.fetch_add(1);  // bases changed: invalidate per-read-set plans
+  if (clean) {
+    ctx->pc_clean = clean;
+    ctx->clean_gen = dr->gen;
+    ctx->clean_valid = true;
+  }
   return APG_OK;
 }
 
 static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st) {
   SkResult sr;
+  if (p.K >= 9) {  // count + the weak-instance bitmap (no lookups for the weak tests)
+    unsigned long long* weak = nullptr;
+    APG_TRY(workspace_t(ctx, "pc_weak", dr->n_bases / 64 + 2, &weak));
+    APG_TRY(sk_solid_weak(ctx, dr, p.K, p.min_solid, weak, &sr));
+    ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
+    return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak);
+  }
   APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
-  ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
+  ctx->solid_valid = false;
   return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st);
 }
 

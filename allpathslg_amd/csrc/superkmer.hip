@@ -118,11 +118,20 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
   }
 }
 
+__device__ __forceinline__ void rec_put(SK16* out, uint64_t i, const SK16& x, uint64_t) { out[i] = x; }
+__device__ __forceinline__ void rec_put(SK24* out, uint64_t i, const SK16& x, uint64_t pos) {
+  out[i] = SK24{x.w0, x.w1, pos};
+}
+__device__ __forceinline__ SK16 rec_head(const SK16& r) { return r; }
+__device__ __forceinline__ SK16 rec_head(const SK24& r) { return SK16{r.w0, r.w1}; }
+
 // Each record goes straight to the next slot of its digit's run for this
 // block (omat, LDS cursor): the run's size is fixed by k_sk_count, the order
-// inside a run is immaterial to counting.
+// inside a run is immaterial to counting.  SK24 records also carry the global
+// base position of their first K-mer.
+template <typename R>
 __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, int D,
-                                                           const uint64_t* __restrict__ omat, SK16* __restrict__ out) {
+                                                           const uint64_t* __restrict__ omat, R* __restrict__ out) {
   __shared__ SkTile<kSkThreads> T;
   __shared__ unsigned long long cur[256];
   __shared__ uint32_t sbuf[kSkMaxW * kSkThreads];
@@ -131,13 +140,19 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
   for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
+  uint64_t tile0 = 0;
+  uint32_t tile_n = 0;
   auto f = [&](const uint8_t* rd, uint32_t, uint32_t a, uint32_t n, uint32_t key) {
     const SK16 x = make_rec(rd, a, n, key, p.K);
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
-    out[atomicAdd(&cur[d], 1ull)] = x;
+    uint64_t pos = 0;
+    if (sizeof(R) == sizeof(SK24)) pos = rv.base_off[tile0 + (tile_n ? threadIdx.x : 0)] + a;
+    rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
   };
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
+    tile0 = t0;
+    tile_n = n;
     if (n)
       sk_walk<kSkThreads, false>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
     else
@@ -181,6 +196,7 @@ struct SkOut {
   uint64_t* solid;             // solid mode output: khash of the canonical K-mer
   uint64_t solid_cap;
   uint32_t min_solid;
+  unsigned long long* weak;    // SK24 solid mode: per-base bitmap of weak K-mer instances (or null)
 };
 
 __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, const SkOut& o) {
@@ -197,10 +213,11 @@ __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, con
 // flatten the chunk to one K-mer per thread, inserted into the LDS table
 // keyed by the canonical K-mer (CAS, then count).  The occupied slots feed
 // the spectrum; solid mode appends khash of those with count >= min_solid.
-template <bool SOLID>
-__global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict__ rec,
+template <bool SOLID, typename R>
+__global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ rec,
                                                           const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
                                                           SkOut o) {
+  constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
   __shared__ unsigned long long tkey[kSkTab];
   __shared__ uint32_t tcnt[kSkTab];
   __shared__ uint32_t lhist[kSkHistBins];
@@ -210,6 +227,8 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
   __shared__ uint32_t scan_sm[64];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
+  __shared__ uint64_t cpos[WEAK ? kSkThreads : 1];   // weak pass: records' first-K-mer positions
+  __shared__ uint32_t wmask[WEAK ? kSkThreads : 1];  // weak pass: records' weak K-mer masks
   constexpr unsigned long long EMPTY = ~0ull;
   constexpr int TB = __builtin_ctz(kSkTab);
   const uint32_t tid = threadIdx.x;
@@ -224,7 +243,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
     off = boff[bkt];
     nr = (uint32_t)(boff[bkt + 1] - off);
   }
-  SK16 pre{0, 0};
+  R pre{};
   if (tid < nr) pre = rec[off + tid];
   for (; bkt < nbuckets;) {
     const uint64_t nbk = bkt + gridDim.x;
@@ -250,7 +269,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
       uint32_t nk = 0;
       if (c0 + tid < nr) {
         nk = (uint32_t)(pre.w0 >> 32) & 0xff;
-        crec[tid] = pre;
+        crec[tid] = rec_head(pre);
       }
       if (c0 + kSkThreads < nr) {
         if (c0 + kSkThreads + tid < nr) pre = rec[off + c0 + kSkThreads + tid];
@@ -290,6 +309,45 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
       nr = nnr;
       continue;
     }
+    if constexpr (WEAK) {
+      // Weak pass: the bucket's records again (L2-hot); each K-mer instance
+      // finds its final count in the table, weak ones (count < min_solid) set
+      // their bit at the instance's base position — one 64-bit atomic OR (two
+      // when the run straddles a word) per record holding a weak K-mer.
+      if (o.weak) {
+        for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
+          uint32_t nk = 0;
+          if (c0 + tid < nr) {
+            const R r = rec[off + c0 + tid];
+            crec[tid] = rec_head(r);
+            cpos[tid] = r.pos;
+            nk = (uint32_t)(r.w0 >> 32) & 0xff;
+          }
+          wmask[tid] = 0;
+          uint32_t tot;
+          const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);
+          koff[tid] = ex;
+          for (uint32_t u = 0; u < nk; ++u) owner[ex + u] = (uint8_t)tid;
+          __syncthreads();
+          for (uint32_t f = tid; f < tot; f += kSkThreads) {
+            const uint32_t i = owner[f];
+            const uint32_t t = f - koff[i];
+            const uint64_t c = rec_kmer(crec[i], t, p);
+            uint32_t s = sk_slot(c, TB);
+            while (tkey[s] != c) s = (s + 1) & (kSkTab - 1);  // inserted above: present
+            if (tcnt[s] < o.min_solid) atomicOr(&wmask[i], 1u << t);
+          }
+          __syncthreads();
+          if (c0 + tid < nr && wmask[tid]) {
+            const uint64_t b = cpos[tid], m = wmask[tid];
+            const uint32_t sh = (uint32_t)(b & 63);
+            atomicOr(&o.weak[b >> 6], (unsigned long long)(m << sh));
+            if (sh && (m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)(m >> (64 - sh)));
+          }
+          __syncthreads();
+        }
+      }
+    }
     uint32_t ns = 0;
     for (uint32_t s = tid; s < kSkTab; s += kSkThreads)
       if (tkey[s] != EMPTY) {
@@ -324,7 +382,8 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const SK16* __restrict
 // Overflowed buckets: every K-mer of every overflowed bucket into one global
 // open-addressing table keyed by canonical K-mer (distinct buckets never
 // share a K-mer).
-__global__ void k_sk_big_kmers(const SK16* __restrict__ rec, const uint64_t* __restrict__ boff,
+template <typename R>
+__global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                                const uint32_t* __restrict__ ovf_list, uint32_t n_ovf,
                                unsigned long long* __restrict__ n_kmers) {
   unsigned long long c = 0;
@@ -335,13 +394,14 @@ __global__ void k_sk_big_kmers(const SK16* __restrict__ rec, const uint64_t* __r
   wave_add(n_kmers, c);
 }
 
-__global__ void k_sk_big_insert(const SK16* __restrict__ rec, const uint64_t* __restrict__ boff,
+template <typename R>
+__global__ void k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                                 const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, SkP p,
                                 unsigned long long* __restrict__ gkey, uint32_t* __restrict__ gcnt, uint64_t gmask) {
   for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
     const uint32_t b = ovf_list[q];
     for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
-      const SK16 r = rec[i];
+      const SK16 r = rec_head(rec[i]);
       const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
       for (uint32_t t = 0; t < n; ++t) {
         const uint64_t c = rec_kmer(r, t, p);
@@ -353,6 +413,31 @@ __global__ void k_sk_big_insert(const SK16* __restrict__ rec, const uint64_t* __
             break;
           }
           s = (s + 1) & gmask;
+        }
+      }
+    }
+  }
+}
+
+// Weak bits of the overflowed buckets' K-mer instances (counts from the
+// global table built by k_sk_big_insert).
+__global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __restrict__ boff,
+                              const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, SkP p,
+                              const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
+                              uint64_t gmask, uint32_t min_solid, unsigned long long* __restrict__ weak) {
+  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
+    const uint32_t b = ovf_list[q];
+    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
+      const SK24 r = rec[i];
+      const SK16 h = rec_head(r);
+      const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+      for (uint32_t t = 0; t < n; ++t) {
+        const uint64_t c = rec_kmer(h, t, p);
+        uint64_t s = khash(p.hp, c) & gmask;
+        while (gkey[s] != c) s = (s + 1) & gmask;
+        if (gcnt[s] < min_solid) {
+          const uint64_t x = r.pos + t;
+          atomicOr(&weak[x >> 6], 1ull << (x & 63));
         }
       }
     }
@@ -437,7 +522,8 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   return APG_OK;
 }
 
-int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
+template <typename R>
+static int sk_scatter_t(apg_ctx* ctx, const apg_dreads* dr, int K, int P, R* out) {
   auto& s = ctx->skstate;
   if (!s.valid || s.gen != dr->gen || s.K != K || s.P != P) {
     std::vector<uint64_t> rc, kc;
@@ -448,11 +534,15 @@ int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)(1u << D) * s.G + 1, &omat));
-  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * sizeof(SK16));
-  if (dr->n_reads) k_sk_scatter<<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out);
+  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * sizeof(R));
+  if (dr->n_reads) k_sk_scatter<R><<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;
+}
+
+int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
+  return sk_scatter_t<SK16>(ctx, dr, K, P, out);
 }
 
 // Partition levels + bucket counting of records laid out as P source blocks,
@@ -460,9 +550,12 @@ int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
 // rec_counts[src * B1 + l1].  `spare` (may be null) is a buffer of >= n
 // records that may be overwritten.  Spectrum into hist (may be null); solid
 // mode leaves the solid hashes in "pc_solid" (res->solid, res->n_solid).
-int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
-                   uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
-                   SkResult* res) {
+// weak (SK24 records, solid mode only): per-base bitmap of weak K-mer
+// instances, zeroed by the caller.
+template <typename R>
+static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vector<uint64_t>& rec_counts,
+                            uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist,
+                            size_t hist_len, unsigned long long* weak, SkResult* res) {
   const SkP p = make_skp(K);
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
@@ -487,12 +580,12 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
         pos += c;
       }
   }
-  SK16 *bufA = nullptr, *bufB = spare;
+  R *bufA = nullptr, *bufB = spare;
   APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1), &bufA));
   if (!bufB) APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &bufB));
   uint64_t* boff = nullptr;
   APG_TRY(workspace_t(ctx, "sk_boff", (1ull << bb) + 1, &boff));
-  const SK16* cur = src;
+  const R* cur = src;
   uint64_t nb = B1;
   int consumed = pbits + l1;
   if (nlev == 0) {
@@ -503,10 +596,10 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
   for (int lev = 0; lev < nlev; ++lev) {
     const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
     consumed += bits;
-    SK16* dst = (cur == bufA) ? bufB : bufA;
+    R* dst = (cur == bufA) ? bufB : bufA;
     std::vector<uint64_t> hb;
     const bool last = lev + 1 == nlev;
-    APG_TRY(part_level<SK16>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "s"));
+    APG_TRY(part_level<R>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "s"));
     nb = parents.size() << bits;
     if (!last) {
       parents.assign(nb, {});
@@ -530,14 +623,15 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
     solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }
-  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid};
+  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr};
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * 8));
   for (int attempt = 0;; ++attempt) {
-    kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(SK16) + (nb + 1) * 8);
+    // weak pass: the records a second time (L2-hot) + 8 B per weak-bit word touched
+    kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) * (o.weak ? 2 : 1) + (nb + 1) * 8);
     if (solid)
-      k_sk_bucket<true><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      k_sk_bucket<true, R><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
     else
-      k_sk_bucket<false><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      k_sk_bucket<false, R><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hs[4];
@@ -547,7 +641,7 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
       unsigned long long* nk = gstats + 3;
       APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
       const uint32_t g2 = (uint32_t)std::min<unsigned long long>(hs[1], (unsigned long long)ctx->n_cu * 8);
-      k_sk_big_kmers<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], nk);
+      k_sk_big_kmers<R><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], nk);
       unsigned long long nbk = 0;
       APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
       APG_TRY(sync(ctx));
@@ -561,11 +655,16 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
       APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
       vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
       kbegin(ctx, "sk_bucket_global", nbk * 64);
-      k_sk_big_insert<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1);
+      k_sk_big_insert<R><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1);
       if (solid)
         k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
       else
         k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+      if constexpr (sizeof(R) == sizeof(SK24)) {
+        if (o.weak)
+          k_sk_big_weak<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1,
+                                                      min_solid, o.weak);
+      }
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
       APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
@@ -602,6 +701,34 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
        (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
        (unsigned long long)res->n_distinct);
   return APG_OK;
+}
+
+int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
+                   uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
+                   SkResult* res) {
+  return sk_stage_count_t<SK16>(ctx, src, spare, rec_counts, n_kmers, K, P, solid, min_solid, hist, hist_len, nullptr,
+                                res);
+}
+
+// Solid set of a whole read set (P = 1) plus the weak-instance bitmap: bit
+// base_off[r] + j of `weak` (zeroed here; (n_bases + 63) / 64 + 1 words) is
+// set iff K-mer j of read r has count < min_solid.  Needs K >= 9 (a record's
+// K-mers fit one 32-bit mask).
+int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid, unsigned long long* weak,
+                  SkResult* res) {
+  APG_REQUIRE(K >= 9 && K <= 32, "sk_solid_weak: K must be in [9, 32]");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const uint64_t words = dr->n_bases / 64 + 2;
+  APG_CHECK_HIP(hipMemsetAsync(weak, 0, words * 8, ctx->stream));
+  std::vector<uint64_t> rc, kc;
+  APG_TRY(sk_count(ctx, dr, K, 1, &rc, &kc));
+  uint64_t n = 0, nk = 0;
+  for (auto c : rc) n += c;
+  for (auto c : kc) nk += c;
+  SK24* buf = nullptr;
+  APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
+  APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
+  return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {

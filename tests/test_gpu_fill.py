@@ -146,3 +146,40 @@ def test_fill_full_size_properties(gpu_ctx):
     assert (tl == lens).mean() > 0.999  # filled lengths are the true inserts
     out.free()
     d.free()
+
+
+def test_fill_last_solid_long_and_short_reads(gpu_ctx):
+    """Clean flags of the correction pass (weak-bitmap path, reads <= 1024)
+    and the thread-per-read path (longer reads, flags not derived: the fill
+    looks their K-mers up) give the oracle's fill."""
+    rng = np.random.default_rng(17)
+    G = synth_genome(60_000, 18)
+    seqs, quals = [], []
+    for i in range(1200):
+        La = 1100 if i % 3 == 0 else 100
+        I = int(rng.integers(2 * La - 40, 2 * La + 40))
+        s = int(rng.integers(0, len(G) - I))
+        A = G[s : s + La].copy()
+        F = G[s + I - La : s + I].copy()
+        for r in (A, F):
+            flip = rng.random(La) < 0.01
+            r[flip] = (r[flip] + 1) % 4
+        qa = np.where(rng.random(La) < 0.05, 10, 40).astype(np.uint8)
+        qb = np.where(rng.random(La) < 0.05, 10, 40).astype(np.uint8)
+        seqs += [A, (3 - F)[::-1].copy()]
+        quals += [qa, qb]
+    reads = ReadSet.from_sequences(seqs, quals)
+    fixed, _ = oracle.precorrect(reads, K=24)
+    solid = oracle.solid_hashes(reads, 24, 3)
+    for lo, hi in ((160, 240), (2160, 2240)):
+        d = gpu_ctx.upload(reads)
+        gpu_ctx.precorrect(d, K=24)
+        assert np.array_equal(gpu_ctx.download(d).packed[: int(fixed.byte_off[-1])], fixed.packed[: int(fixed.byte_off[-1])])
+        out, _, st = gpu_ctx.fill_fragments(d, K=24, last_solid=True, min_insert=lo, max_insert=hi)
+        exp, es, _, est = oracle.fill_fragments(fixed, solid, K=24, min_insert=lo, max_insert=hi)
+        assert st["n_filled"] == est["n_filled"] and st["n_skip"] == est["n_skip"]
+        host, hs, _ = gpu_ctx.fill_fragments(fixed, solid, K=24, min_insert=lo, max_insert=hi, status=True)
+        assert np.array_equal(hs, es)
+        same_reads(host, exp)
+        out.free()
+        d.free()
