@@ -160,6 +160,7 @@ int apg_trim(apg_ctx* ctx) {
     if (kv.second.p) (void)hipFree(kv.second.p);
   ctx->ws.clear();
   ctx->pc_list_valid = false;
+  ctx->pc_ext_valid = false;
   ctx->clean_valid = false;
   ctx->solid_valid = false;
   return APG_OK;

@@ -142,6 +142,11 @@ struct apg_ctx {
   // Per-read clean flags of that pass (1: every K-mer solid after correction,
   // 0: not, 2: not derived), valid for the read set while its gen is clean_gen.
   const uint8_t* pc_clean = nullptr;
+  // (K-1)-mer extension table of pc_list (ext_table.hpp; "pc_ext" workspace),
+  // built by the pass when 2 <= K <= 29: FillFragments reuses it.
+  unsigned long long* pc_ext_slot = nullptr;
+  uint64_t pc_ext_mask = 0;
+  bool pc_ext_valid = false;
   uint64_t clean_gen = 0;
   bool clean_valid = false;
 };

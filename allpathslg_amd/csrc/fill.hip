@@ -29,43 +29,12 @@
 #include "apg_core.hpp"
 #include "kmer_common.hpp"
 #include "kmer_internal.hpp"
+#include "ext_table.hpp"
 #include "partition.hpp"
 
 namespace apg {
 
-constexpr uint64_t kExtEmpty = ~0ull;
 constexpr uint32_t kFillMaxGap = 63;
-
-__device__ __forceinline__ uint64_t f_rev2(uint64_t x) {
-  x = __builtin_bitreverse64(x);
-  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
-}
-
-// reverse complement of an n-base MSB-first value (1 <= n <= 32)
-__host__ __device__ __forceinline__ uint64_t rc_bases(uint64_t w, int n, uint64_t mask) {
-#ifdef __HIP_DEVICE_COMPILE__
-  return (f_rev2(w) >> (64 - 2 * n)) ^ mask;
-#else
-  uint64_t r = 0;
-  for (int i = 0; i < n; ++i) {
-    r = (r << 2) | (3 - (w & 3));
-    w >>= 2;
-  }
-  return r & mask;
-#endif
-}
-
-__device__ __forceinline__ uint32_t rev4(uint32_t x) {
-  return ((x & 1) << 3) | ((x & 2) << 1) | ((x & 4) >> 1) | ((x & 8) >> 3);
-}
-
-struct ExtTab {
-  unsigned long long* slot;
-  uint64_t mask;
-  HashP h1;  // slot hash of canonical (K-1)-mers
-  uint64_t m1;
-  int n1;  // K-1
-};
 
 __device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
   const unsigned long long want = (key << 8) | bit;
@@ -108,26 +77,21 @@ __global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n
   }
 }
 
-// 4-bit successor mask of the (K-1)-mer w (MSB-first, fw orientation)
-__device__ __forceinline__ uint32_t ext_succ(const ExtTab& t, uint64_t w, uint32_t* nlook) {
-  const uint64_t r = rc_bases(w, t.n1, t.m1);
-  const uint64_t c = w < r ? w : r;
-  uint64_t s = khash(t.h1, c) & t.mask;
-  uint32_t e = 0;
-  for (;;) {
-    const unsigned long long v = t.slot[s];
-    if (v == kExtEmpty) break;
-    if ((v >> 8) == c) {
-      e = (uint32_t)(v & 0xff);
-      break;
-    }
-    s = (s + 1) & t.mask;
-  }
-  ++*nlook;
-  uint32_t m = 0;
-  if (w <= r) m |= e >> 4;
-  if (r <= w) m |= rev4(e & 15);
-  return m;
+int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const char* ws, const char* kname,
+              ExtTab* out) {
+  // load <= 0.5 even if no two solid K-mers share a (K-1)-mer (~0.25 on a genome)
+  uint64_t T = 1024;
+  while (T < 4 * n_solid) T <<= 1;
+  unsigned long long* slot = nullptr;
+  APG_TRY(workspace_t(ctx, ws, T, &slot));
+  APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));
+  *out = ExtTab{slot, T - 1, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1};
+  kbegin(ctx, kname, n_solid * (8 + 2 * 64));
+  if (n_solid)
+    k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
 }
 
 // 32 bases [pos, pos+32) of a packed read as an LSB-first word (base pos at
@@ -449,6 +413,8 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   st->n_pairs = np;
   const uint64_t* list = d_solid;
   const uint8_t* clean = nullptr;
+  bool have_ext = false;
+  ExtTab et{};
   if (!list && n_solid == 0) {
     if (p.flags & APG_FILL_LAST_SOLID) {
       APG_REQUIRE(ctx->pc_list_valid, "apg_fill_fragments: APG_FILL_LAST_SOLID but no correction pass ran on ctx");
@@ -458,28 +424,23 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
       // the pass's clean flags answer "every K-mer of the read solid" for the
       // reads it corrected (these very bases: same generation)
       if (ctx->clean_valid && ctx->clean_gen == dr->gen) clean = ctx->pc_clean;
+      // ... and the pass's extension table is this very solid set's
+      if (ctx->pc_ext_valid) {
+        et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
+        have_ext = true;
+      }
     } else {  // the pairs' own solid K-mers
       SkResult sr;
       APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
       list = sr.solid;
       n_solid = sr.n_solid;
       ctx->pc_list_valid = false;  // "pc_solid" now holds this list
+      ctx->pc_ext_valid = false;
     }
   }
   APG_REQUIRE(n_solid == 0 || list, "apg_fill_fragments: solid set pointer is NULL");
   st->n_solid = n_solid;
-  // (K-1)-mer extension table, load <= 0.5 even if no two solid K-mers share a (K-1)-mer
-  uint64_t T = 1024;
-  while (T < 4 * n_solid) T <<= 1;
-  unsigned long long* slot = nullptr;
-  APG_TRY(workspace_t(ctx, "fill_ext", T, &slot));
-  APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));
-  ExtTab et{slot, T - 1, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
-  kbegin(ctx, "fill_ext", n_solid * (8 + 2 * 64));
-  if (n_solid)
-    k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(p.K), et);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
+  if (!have_ext) APG_TRY(ext_build(ctx, list, n_solid, p.K, "fill_ext", "fill_ext", &et));
 
   FillRec* rec = nullptr;
   uint32_t *lens = nullptr, *nby = nullptr, *ones = nullptr;

@@ -18,6 +18,7 @@
 #include "apg_core.hpp"
 #include "kmer_common.hpp"
 #include "kmer_internal.hpp"
+#include "ext_table.hpp"
 #include "partition.hpp"
 
 namespace apg {
@@ -183,10 +184,7 @@ __global__ void __launch_bounds__(256) k_precorrect(const uint64_t* __restrict__
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPcMaxL = 1024;  // 64 lanes x 16 bases
 
-__device__ __forceinline__ uint64_t rev2(uint64_t x) {
-  x = __builtin_bitreverse64(x);
-  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
-}
+__device__ __forceinline__ uint64_t rev2(uint64_t x) { return f_rev2(x); }
 
 // 2K-bit window starting at base j of the read whose packed u32 words are
 // spread one per lane (word i in lane i's `word`).
@@ -207,50 +205,142 @@ __device__ __forceinline__ uint64_t canon_hash(uint64_t W, int K, const HashP& h
   return khash(hp, fw < rc ? fw : rc);
 }
 
+// K+1 bases [i-1, i+K) of the read as an LSB-first value (base i-1 at bits
+// 0-1; for i == 0 there is no base i-1 and bits 0-1 are 0), with base p
+// replaced by alt (p = ~0u: no replacement).  Every lane joins the shuffles.
+__device__ __forceinline__ uint64_t ext_window(uint32_t word, uint32_t i, int K, uint32_t p, uint32_t alt) {
+  const uint64_t m = (1ull << (2 * (K + 1))) - 1;  // K <= 29
+  uint64_t W = window_at(word, i ? i - 1 : 0, m);
+  if (!i) W = (W << 2) & m;
+  if (p + 1 >= i && p + 1 <= i + (uint32_t)K) {  // p in [i-1, i+K-1]
+    const uint32_t sh = 2 * (p + 1 - i);
+    W = (W & ~(3ull << sh)) | ((uint64_t)alt << sh);
+  }
+  return W;
+}
+
+// K-mers i-1 (a read K-mer iff i >= 1) and i of the window W = ext_window(i):
+// bit 0 = K-mer i-1 solid (pred of (K-1)-mer i holds base i-1), bit 1 = K-mer
+// i solid (succ holds base i+K-1).  One extension-table lookup.
+__device__ __forceinline__ uint32_t ext_pair(const ExtTab& t, uint64_t W, int K) {
+  const uint32_t e = ext_masks_lsb(t, (W >> 2) & t.m1);
+  const uint32_t pb = (uint32_t)W & 3, sb = (uint32_t)(W >> (2 * K)) & 3;
+  return ((e >> pb) & 1) | (((e >> (4 + sb)) & 1) << 1);
+}
+
+// Offsets of read r (L = 0 past the end) and its register-resident data.
+struct PcMeta {
+  uint64_t q0, bo;
+  uint32_t L;
+};
+struct PcData {
+  uint32_t word, qa, qb, W16;
+};
+
+__device__ __forceinline__ PcMeta pc_meta(const uint64_t* __restrict__ base_off, const uint64_t* __restrict__ byte_off,
+                                          uint64_t n_reads, uint64_t r) {
+  PcMeta m{0, 0, 0};
+  if (r < n_reads) {
+    m.q0 = base_off[r];
+    m.L = (uint32_t)(base_off[r + 1] - m.q0);
+    m.bo = byte_off[r];
+  }
+  return m;
+}
+
+// Lane i: packed bases [16i, 16i+16) (one aligned u32 load per lane, funnel-
+// shifted with the next lane's; the read sets carry 64 bytes of slack), quals
+// i and 64 + i, weak bits of K-mers [16i, 16i+16).  Wave-uniform branches.
+__device__ __forceinline__ PcData pc_data(const PcMeta& m, const uint8_t* __restrict__ packed,
+                                          const uint8_t* __restrict__ quals,
+                                          const unsigned long long* __restrict__ weak, int K) {
+  PcData d{0, 255, 255, 0};
+  if (m.L < (uint32_t)K || m.L > kPcMaxL) return d;
+  const uint32_t lane = (uint32_t)lane_id();
+  const uint32_t nbytes = (m.L + 3) >> 2;
+  const uint32_t s = (uint32_t)(m.bo & 3);
+  const uint32_t* aw = reinterpret_cast<const uint32_t*>(packed + (m.bo - s));
+  const uint32_t naw = (nbytes + s + 3) >> 2;
+  const uint32_t w = lane < naw ? aw[lane] : 0u;
+  const uint32_t wx = (lane == 63 && naw > 64) ? aw[64] : 0u;
+  uint32_t nx = (uint32_t)__shfl((int)w, (int)min(lane + 1, 63u), 64);
+  if (lane == 63) nx = wx;
+  uint32_t word = s ? (w >> (8 * s)) | (nx << (32 - 8 * s)) : w;
+  if (4 * lane >= nbytes)
+    word = 0;
+  else if (nbytes - 4 * lane < 4)
+    word &= (1u << (8 * (nbytes - 4 * lane))) - 1;
+  d.word = word;
+  const uint8_t* q = quals + m.q0;
+  if (lane < m.L) d.qa = q[lane];
+  if (lane + 64 < m.L) d.qb = q[lane + 64];
+  const uint32_t nK = m.L - (uint32_t)K + 1;
+  if (weak && 16u * lane < nK) {
+    const uint64_t b = m.q0 + 16u * lane;
+    const uint32_t sh = (uint32_t)(b & 63);
+    uint64_t x = weak[b >> 6] >> sh;
+    if (sh > 48) x |= weak[(b >> 6) + 1] << (64 - sh);
+    uint32_t W16 = (uint32_t)x & 0xffffu;
+    if (nK - 16u * lane < 16) W16 &= (1u << (nK - 16u * lane)) - 1;
+    d.W16 = W16;
+  }
+  return d;
+}
+
+// EXT = false: solidity by K-mer lookups in the SolidSet (any K <= 32).
+// EXT = true (2 <= K <= 29): by (K-1)-mer extension lookups, each answering
+// two adjacent K-mers — the weak test and an alternative's covering K-mers
+// take half the lookups, and the first and last covering K-mers of a suspect
+// (the (K-1)-mers beside p do not contain p) are answered for all 4 bases at
+// p by two lookups, before any alternative is tried.
+template <bool EXT>
 __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restrict__ base_off,
                                                          const uint64_t* __restrict__ byte_off,
                                                          uint8_t* __restrict__ packed, uint8_t* __restrict__ quals,
                                                          uint64_t n_reads, int K, HashP hp, uint32_t maxq,
-                                                         SolidSet ss, const unsigned long long* __restrict__ weak,
+                                                         SolidSet ss, ExtTab et,
+                                                         const unsigned long long* __restrict__ weak,
                                                          uint8_t* __restrict__ clean, PcCounters* __restrict__ cnt) {
   uint32_t n_tab = 0;
   const int lane = lane_id();
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
   unsigned long long n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;  // lane 0's
   unsigned long long n_look = 0;
-  for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave_id(); r < n_reads; r += nwaves) {
-    const uint64_t q0 = base_off[r];
-    const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
+  // Software pipeline over the wave's reads r, r + nwaves, ...: the next
+  // read's bases, first 128 quals and weak bits are loaded while this read is
+  // corrected, the offsets of the read after it one step earlier still, so a
+  // read costs the round trips of its suspects' lookups and no more.
+  uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave_id();
+  PcMeta m0 = pc_meta(base_off, byte_off, n_reads, r);
+  PcData d0 = pc_data(m0, packed, quals, weak, K);
+  PcMeta m1 = pc_meta(base_off, byte_off, n_reads, r + nwaves);
+  for (; r < n_reads; r += nwaves) {
+    const PcMeta mc = m0;
+    const PcData dc = d0;
+    m0 = m1;
+    d0 = pc_data(m1, packed, quals, weak, K);
+    m1 = pc_meta(base_off, byte_off, n_reads, r + 2 * nwaves);
+    const uint64_t q0 = mc.q0;
+    const uint32_t L = mc.L;
     if (L < (uint32_t)K) {  // wave-uniform; no K-mer, nothing weak
       if (clean && lane == 0) clean[r] = 1;
       continue;
     }
     if (L > kPcMaxL) continue;  // the thread-per-read kernel's
-    uint8_t* rd = packed + byte_off[r];
+    uint8_t* rd = packed + mc.bo;
     uint8_t* q = quals + q0;
-    const uint32_t nbytes = (L + 3) >> 2;
-    uint32_t word = 0;
-    if (4u * lane < nbytes) {
-      const uint32_t b = 4u * lane;
-      word = (uint32_t)rd[b] | (b + 1 < nbytes ? (uint32_t)rd[b + 1] << 8 : 0u) |
-             (b + 2 < nbytes ? (uint32_t)rd[b + 2] << 16 : 0u) | (b + 3 < nbytes ? (uint32_t)rd[b + 3] << 24 : 0u);
-    }
-    // Weak-bitmap mode: lane i holds the weak bits of K-mers [16i, 16i+16) as
-    // counted (W16) and the corrected positions [16i, 16i+16) so far (C16).
-    uint32_t W16 = 0, C16 = 0;
-    const uint32_t nK = L - (uint32_t)K + 1;
-    if (weak && 16u * lane < nK) {
-      const uint64_t b = q0 + 16u * lane;
-      const uint32_t sh = (uint32_t)(b & 63);
-      uint64_t x = weak[b >> 6] >> sh;
-      if (sh > 48) x |= weak[(b >> 6) + 1] << (64 - sh);
-      W16 = (uint32_t)x & 0xffffu;
-      if (nK - 16u * lane < 16) W16 &= (1u << (nK - 16u * lane)) - 1;
-    }
+    // lane i: packed bases [16i, 16i+16) (word), quals of positions i and
+    // 64 + i (qa, qb; 255 past the read); weak-bitmap mode: the weak bits of
+    // K-mers [16i, 16i+16) as counted (W16) and the positions [16i, 16i+16)
+    // corrected so far (C16).
+    uint32_t word = dc.word, qa = dc.qa, qb = dc.qb;
+    const uint32_t W16 = dc.W16;
+    uint32_t C16 = 0;
     int last_corr = -1;  // wave-uniform: latest corrected position
     for (uint32_t c = 0; c < L; c += 64) {
       const uint32_t pl = c + lane;
-      uint64_t m = __ballot(pl < L && q[pl] < maxq);
+      const uint32_t qv = c == 0 ? qa : c == 64 ? qb : (pl < L ? (uint32_t)q[pl] : 255u);
+      uint64_t m = __ballot(qv < maxq);
       while (m) {
         const uint32_t p = c + (uint32_t)(__ffsll((long long)m) - 1);
         m &= m - 1;
@@ -271,6 +361,18 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           }
           const uint64_t need = (1ull << nk) - 1;
           if (((x >> (jlo & 15)) & need) != need) continue;
+        } else if constexpr (EXT) {
+          // K-mers jlo..jhi in pairs: lane l looks up (K-1)-mer jlo + 1 + 2l
+          const uint32_t G = (nk + 1) >> 1;
+          const uint32_t i = jlo + 1 + 2 * min((uint32_t)lane, G - 1);
+          const uint64_t Wk = ext_window(word, i, K, ~0u, 0);
+          bool solid = false;
+          if ((uint32_t)lane < G) {
+            const uint32_t r2 = ext_pair(et, Wk, K);
+            solid = (r2 & 1) || (i <= jhi && (r2 & 2));
+          }
+          n_look += G;
+          if (__ballot(solid)) continue;
         } else {
           // every lane takes part in the shuffles; lanes >= nk repeat the last K-mer
           const uint64_t Wk = window_at(word, jlo + min((uint32_t)lane, nk - 1), hp.mask);
@@ -281,32 +383,82 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
         }
         ++n_sus;
         const uint32_t orig = (__shfl((int)word, (int)(p >> 4), 64) >> (2 * (p & 15))) & 3;
-        // Alternatives in two rounds of lookups: (A) the first covering K-mer
-        // of each of the 3 alternatives (lanes 0..2); (B) the remaining nk-1
-        // K-mers of each survivor of (A) — usually one — one per lane.
-        const uint64_t W0 = window_at(word, jlo, hp.mask);
-        const uint32_t sh0 = 2 * (p - jlo);
-        bool badA = false;
-        if (lane < 3) {
-          const uint32_t alt = (uint32_t)lane + ((uint32_t)lane >= orig ? 1u : 0u);
-          badA = !is_solid(ss, canon_hash((W0 & ~(3ull << sh0)) | ((uint64_t)alt << sh0), K, hp), &n_tab);
-        }
-        uint32_t surv = (uint32_t)(~__ballot(badA)) & 7u;
-        n_look += 3 + (uint64_t)__popc(surv) * (nk - 1);
         uint32_t ncand = 0, cand = 0;
-        const uint32_t t1 = jlo + 1 + min((uint32_t)lane, nk > 1 ? nk - 2 : 0u);
-        const uint64_t W1 = window_at(word, t1, hp.mask);  // every lane joins the shuffles
-        const uint32_t sh1 = 2 * (p - t1);
-        while (surv) {
-          const uint32_t a = (uint32_t)(__ffs((int)surv) - 1);
-          surv &= surv - 1;
-          const uint32_t alt = a + (a >= orig ? 1u : 0u);
-          bool bad = false;
-          if ((uint32_t)lane + 1 < nk)
-            bad = !is_solid(ss, canon_hash((W1 & ~(3ull << sh1)) | ((uint64_t)alt << sh1), K, hp), &n_tab);
-          if (!__ballot(bad)) {
-            ++ncand;
-            cand = alt;
+        if constexpr (EXT) {
+          // (A) the (K-1)-mers beside p: lane 0 the one ending at p - 1 (its
+          // successors answer K-mer p-K+1 for every base at p), lane 1 the one
+          // starting at p + 1 (predecessors: K-mer p).
+          const bool hasA = p + 1 >= (uint32_t)K, hasB = p + (uint32_t)K <= L;
+          const uint32_t iA = lane == 0 ? (hasA ? p + 1 - K : 0) : (hasB ? p + 1 : 0);
+          const uint64_t WA = ext_window(word, iA, K, ~0u, 0);
+          uint32_t mA = 15;
+          if ((lane == 0 && hasA) || (lane == 1 && hasB)) {
+            const uint32_t e = ext_masks_lsb(et, (WA >> 2) & et.m1);
+            mA = lane == 0 ? e >> 4 : e & 15;
+          }
+          const uint32_t allowed = (uint32_t)__shfl((int)mA, 0, 64) & (uint32_t)__shfl((int)mA, 1, 64);
+          const uint32_t surv = allowed & ~(1u << orig) & 15u;
+          const uint32_t ns = __popc(surv);
+          n_look += (hasA ? 1 : 0) + (hasB ? 1 : 0);
+          // (B) the other covering K-mers a..b of every survivor at once: survivor
+          // s on lanes [sG, sG + G), lane sG + l looking up (K-1)-mer a + 1 + 2l.
+          const int ia = (int)jlo + (hasA ? 1 : 0), ib = (int)jhi - (hasB ? 1 : 0);
+          if (ib < ia || ns == 0) {
+            ncand = ns;
+            cand = ns ? (uint32_t)(__ffs((int)surv) - 1) : 0;
+          } else {
+            const uint32_t G = (uint32_t)(ib - ia + 2) >> 1;
+            const uint32_t sidx = min((uint32_t)lane / G, 2u);
+            uint32_t sm = surv;
+            for (uint32_t k = 0; k < sidx && sm; ++k) sm &= sm - 1;
+            const uint32_t alt = sm ? (uint32_t)(__ffs((int)sm) - 1) : orig;
+            const bool act = (uint32_t)lane < ns * G;
+            const uint32_t i = (uint32_t)ia + 1 + 2 * (act ? (uint32_t)lane - sidx * G : 0);
+            const uint64_t WB = ext_window(word, i, K, p, alt);
+            bool bad = false;
+            if (act) {
+              const uint32_t r2 = ext_pair(et, WB, K);
+              bad = !(r2 & 1) || ((int)i <= ib && !(r2 & 2));
+            }
+            const uint64_t badm = __ballot(bad);
+            sm = surv;
+            for (uint32_t s2 = 0; s2 < ns; ++s2) {
+              const uint32_t a2 = (uint32_t)(__ffs((int)sm) - 1);
+              sm &= sm - 1;
+              if (!((badm >> (s2 * G)) & ((1ull << G) - 1))) {
+                ++ncand;
+                cand = a2;
+              }
+            }
+            n_look += (uint64_t)ns * G;
+          }
+        } else {
+          // Alternatives in two rounds of lookups: (A) the first covering K-mer
+          // of each of the 3 alternatives (lanes 0..2); (B) the remaining nk-1
+          // K-mers of each survivor of (A) — usually one — one per lane.
+          const uint64_t W0 = window_at(word, jlo, hp.mask);
+          const uint32_t sh0 = 2 * (p - jlo);
+          bool badA = false;
+          if (lane < 3) {
+            const uint32_t alt = (uint32_t)lane + ((uint32_t)lane >= orig ? 1u : 0u);
+            badA = !is_solid(ss, canon_hash((W0 & ~(3ull << sh0)) | ((uint64_t)alt << sh0), K, hp), &n_tab);
+          }
+          uint32_t surv = (uint32_t)(~__ballot(badA)) & 7u;
+          n_look += 3 + (uint64_t)__popc(surv) * (nk - 1);
+          const uint32_t t1 = jlo + 1 + min((uint32_t)lane, nk > 1 ? nk - 2 : 0u);
+          const uint64_t W1 = window_at(word, t1, hp.mask);  // every lane joins the shuffles
+          const uint32_t sh1 = 2 * (p - t1);
+          while (surv) {
+            const uint32_t a = (uint32_t)(__ffs((int)surv) - 1);
+            surv &= surv - 1;
+            const uint32_t alt = a + (a >= orig ? 1u : 0u);
+            bool bad = false;
+            if ((uint32_t)lane + 1 < nk)
+              bad = !is_solid(ss, canon_hash((W1 & ~(3ull << sh1)) | ((uint64_t)alt << sh1), K, hp), &n_tab);
+            if (!__ballot(bad)) {
+              ++ncand;
+              cand = alt;
+            }
           }
         }
         if (ncand == 1) {
@@ -317,11 +469,19 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           }
           last_corr = (int)p;
           const uint32_t nw = (uint32_t)__shfl((int)word, (int)(p >> 4), 64);
+          // current quals of the neighbours (registers below 128, then memory)
+          auto qat = [&](uint32_t i) -> uint32_t {
+            if (i < 64) return (uint32_t)__shfl((int)qa, (int)i, 64);
+            if (i < 128) return (uint32_t)__shfl((int)qb, (int)(i - 64), 64);
+            return (uint32_t)q[i];
+          };
+          uint32_t nq = 255;
+          if (p > 0) nq = min(nq, qat(p - 1));
+          if (p + 1 < L) nq = min(nq, qat(p + 1));
+          if ((uint32_t)lane == p) qa = nq;
+          if ((uint32_t)lane + 64 == p) qb = nq;
           if (lane == 0) {
             rd[p >> 2] = (uint8_t)(nw >> (8 * ((p >> 2) & 3)));
-            uint32_t nq = 255;
-            if (p > 0) nq = min(nq, (uint32_t)q[p - 1]);
-            if (p + 1 < L) nq = min(nq, (uint32_t)q[p + 1]);
             q[p] = (uint8_t)nq;
             ++n_cor;
           }
@@ -362,6 +522,316 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weak-bitmap + extension-table mode (the bench path: K in [9, 29], reads of
+// <= kPcMaxL bases) in three kernels, so that the random lookups run with one
+// independent work item per lane instead of a wave's dependent chain per read:
+//
+//   k_pc_candidates (thread per read, quals staged through LDS): the
+//     candidates — positions with Q < maxq whose covering K-mers were all
+//     counted weak — each with the 2K+1 bases around it, one contiguous run
+//     per read.
+//   k_pc_decide (thread per candidate): the candidate's decision as if it were
+//     a suspect: its base is unchanged since counting and so are the other
+//     bases of every covering K-mer (corrections go left to right and a
+//     correction within K before it makes it no suspect), so decisions are
+//     independent of each other.
+//   k_pc_apply (thread per read): the sequential rule — a candidate is a
+//     suspect unless a correction lies within K before it — applied in read
+//     order, corrections written, counters and clean flags.
+// ---------------------------------------------------------------------------
+struct PcCand {
+  uint64_t wlo, whi;  // bases [p-K, p+K] LSB-first: base p-K+t at bits 2t (0 outside the read)
+  uint32_t r;
+  uint16_t p, L;
+};
+constexpr uint8_t kPcAmbiguous = 4, kPcNone = 5;
+
+// Covering K-mers [jlo, jhi] of read position p all counted weak: bits
+// q0 + jlo .. q0 + jhi of the weak-instance bitmap (nk <= K <= 32 bits).
+__device__ __forceinline__ bool pc_all_weak(const unsigned long long* __restrict__ weak, uint64_t q0, uint32_t p,
+                                            uint32_t L, int K) {
+  const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - K : 0;
+  const uint32_t jhi = min(p, L - (uint32_t)K);
+  const uint32_t nk = jhi - jlo + 1;
+  const uint64_t b = q0 + jlo;
+  const uint32_t sh = (uint32_t)(b & 63);
+  uint64_t x = weak[b >> 6] >> sh;
+  if (sh + nk > 64) x |= weak[(b >> 6) + 1] << (64 - sh);
+  const uint64_t need = (1ull << nk) - 1;
+  return (x & need) == need;
+}
+
+// Bases [p-K, p+K] of a packed read (LSB-first, base p-K+t at bits 2t; bases
+// before the read 0, after it whatever the slack holds): aligned u32 loads.
+__device__ __forceinline__ unsigned __int128 pc_window(const uint8_t* __restrict__ rd, uint32_t p, int K) {
+  const int st = (int)p - K;
+  const uint32_t s0 = st < 0 ? 0u : (uint32_t)st;  // first base loaded
+  const uintptr_t a = (uintptr_t)rd + (s0 >> 2);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = 8 * (uint32_t)(a & 3) + 2 * (s0 & 3);
+  // 160 bits >= sh + 118: four words as one 128-bit value, the fifth above it
+  unsigned __int128 v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v |= (unsigned __int128)w[i] << (32 * i);
+  v >>= sh;
+  if (sh) v |= (unsigned __int128)w[4] << (128 - sh);
+  if (st < 0) v <<= 2 * (uint32_t)(-st);
+  return v;
+}
+
+// Candidates of reads [r0, r0 + 256) — one thread per read, quals staged
+// through LDS.  The tile's quals are one contiguous range of the flat quals
+// array: the block copies it with coalesced 16-byte loads (tiles longer than
+// kPcTileQ read global memory instead) and each thread scans its read's quals
+// from LDS as aligned u32 words for positions with Q < maxq whose covering
+// K-mers were all counted weak.  WRITE = false: tcnt[tile] = the tile's
+// candidates.  WRITE = true (toff = exclusive scan of tcnt): a block scan of
+// the per-read counts places read r's run at [cstart[r], cstart[r] + ccnt[r]),
+// in read order, and a second scan from LDS writes the records.
+constexpr uint32_t kPcTileReads = 256;
+constexpr uint32_t kPcTileQ = 32768;
+
+template <typename F>
+__device__ __forceinline__ void pc_scan_read(const uint8_t* qb, uint64_t qbase, uint64_t q0, uint32_t L,
+                                             uint32_t maxq, F&& f) {
+  const uint64_t a0 = q0 & ~3ull;
+  for (uint64_t a = a0; a < q0 + L; a += 4) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(qb + (a - qbase));
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint64_t g = a + k;
+      if (g < q0 || g >= q0 + L || ((x >> (8 * k)) & 0xff) >= maxq) continue;
+      f((uint32_t)(g - q0));
+    }
+  }
+}
+
+// weak bits of a staged tile: words [wbase, ...) of the bitmap at wb
+__device__ __forceinline__ bool pc_all_weak_at(const unsigned long long* wb, uint64_t wbase, uint64_t q0, uint32_t p,
+                                               uint32_t L, int K) {
+  const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - K : 0;
+  const uint32_t jhi = min(p, L - (uint32_t)K);
+  const uint32_t nk = jhi - jlo + 1;
+  const uint64_t b = q0 + jlo;
+  const uint32_t sh = (uint32_t)(b & 63);
+  const uint64_t w = (b >> 6) - wbase;
+  uint64_t x = wb[w] >> sh;
+  if (sh + nk > 64) x |= wb[w + 1] << (64 - sh);
+  const uint64_t need = (1ull << nk) - 1;
+  return (x & need) == need;
+}
+
+constexpr uint32_t kPcTileW = kPcTileQ / 64 + 2;  // weak words of a staged tile
+constexpr uint32_t kPcTileList = 2048;            // candidates of a tile written through LDS
+
+template <bool WRITE>
+__global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
+    const uint64_t* __restrict__ base_off, const uint64_t* __restrict__ byte_off, const uint8_t* __restrict__ packed,
+    const uint8_t* __restrict__ quals, uint64_t n_reads, int K, uint32_t maxq,
+    const unsigned long long* __restrict__ weak, uint32_t* __restrict__ tcnt, const uint64_t* __restrict__ toff,
+    PcCand* __restrict__ cand, uint64_t* __restrict__ cstart, uint32_t* __restrict__ ccnt) {
+  __shared__ __attribute__((aligned(16))) uint8_t qs[kPcTileQ + 16];
+  __shared__ unsigned long long ws[kPcTileW];
+  __shared__ uint32_t list[WRITE ? kPcTileList : 1];  // read in tile << 16 | position
+  __shared__ uint32_t scan_sm[64];
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t r0 = (uint64_t)blockIdx.x * kPcTileReads; r0 < n_reads; r0 += (uint64_t)gridDim.x * kPcTileReads) {
+    const uint64_t r = r0 + tid;
+    const uint64_t re = min(r0 + kPcTileReads, n_reads);
+    const uint64_t Q0 = base_off[r0] & ~15ull, Q1 = base_off[re];
+    const bool staged = Q1 - Q0 <= kPcTileQ;
+    const uint64_t W0 = Q0 >> 6;
+    if (staged) {
+      const uint4* src = reinterpret_cast<const uint4*>(quals + Q0);
+      uint4* dst = reinterpret_cast<uint4*>(qs);
+      for (uint32_t i = tid; i < (uint32_t)((Q1 - Q0 + 15) >> 4); i += kPcTileReads) dst[i] = src[i];
+      // K-mer bits of the tile's reads lie in [Q0, Q1)
+      for (uint32_t i = tid; i < (uint32_t)(((Q1 + 63) >> 6) - W0 + 1); i += kPcTileReads) ws[i] = weak[W0 + i];
+    }
+    __syncthreads();
+    const uint8_t* qb = staged ? qs : quals;
+    const uint64_t qbase = staged ? Q0 : 0;
+    const unsigned long long* wb = staged ? ws : weak;
+    const uint64_t wbase = staged ? W0 : 0;
+    uint64_t q0 = 0;
+    uint32_t L = 0;
+    if (r < n_reads) {
+      q0 = base_off[r];
+      L = (uint32_t)(base_off[r + 1] - q0);
+    }
+    const bool scan = r < n_reads && L >= (uint32_t)K && L <= kPcMaxL;
+    uint32_t n = 0;
+    if (scan)
+      pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
+        if (pc_all_weak_at(wb, wbase, q0, p, L, K)) ++n;
+      });
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<uint32_t>(n, scan_sm, &tot);
+    if constexpr (!WRITE) {
+      if (tid == 0) tcnt[r0 / kPcTileReads] = tot;
+    } else {
+      const uint64_t tb = toff[r0 / kPcTileReads];
+      if (r < n_reads) {
+        cstart[r] = tb + ex;
+        ccnt[r] = n;
+      }
+      if (tot <= kPcTileList) {
+        // positions into LDS, then one candidate per thread: independent
+        // window loads, consecutive records from consecutive threads
+        uint32_t at = ex;
+        if (n)
+          pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
+            if (pc_all_weak_at(wb, wbase, q0, p, L, K)) list[at++] = tid << 16 | p;
+          });
+        __syncthreads();
+        for (uint32_t i = tid; i < tot; i += kPcTileReads) {
+          const uint32_t e = list[i];
+          const uint64_t rr = r0 + (e >> 16);
+          const uint32_t pp = e & 0xffff;
+          const uint32_t LL = (uint32_t)(base_off[rr + 1] - base_off[rr]);
+          const unsigned __int128 v = pc_window(packed + byte_off[rr], pp, K);
+          cand[tb + i] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)rr, (uint16_t)pp, (uint16_t)LL};
+        }
+      } else if (n) {
+        uint64_t at = tb + ex;
+        const uint8_t* rd = packed + byte_off[r];
+        pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
+          if (!pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
+          const unsigned __int128 v = pc_window(rd, p, K);
+          cand[at++] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)r, (uint16_t)p, (uint16_t)L};
+        });
+      }
+    }
+    __syncthreads();  // the LDS tiles are rewritten by the next tile
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ cand, uint64_t n, int K, ExtTab et,
+                                                   uint8_t* __restrict__ dec, unsigned long long* __restrict__ looks) {
+  uint32_t nl = 0;
+  const unsigned __int128 km = ((unsigned __int128)1 << (2 * (K + 1))) - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const PcCand c = cand[i];
+    const unsigned __int128 win = ((unsigned __int128)c.whi << 64) | c.wlo;
+    const uint32_t p = c.p, L = c.L;
+    const uint32_t orig = (uint32_t)(win >> (2 * K)) & 3;
+    const bool hasA = p + 1 >= (uint32_t)K, hasB = p + (uint32_t)K <= L;
+    // (A) the (K-1)-mers beside p answer the first and last covering K-mers
+    // for all 4 bases at p: succ of bases [p-K+1, p) and pred of [p+1, p+K)
+    uint32_t allowed = 15;
+    if (hasA) {
+      allowed &= ext_masks_lsb(et, (uint64_t)(win >> 2) & et.m1) >> 4;
+      ++nl;
+    }
+    if (hasB) {
+      allowed &= ext_masks_lsb(et, (uint64_t)(win >> (2 * K + 2)) & et.m1) & 15;
+      ++nl;
+    }
+    uint32_t surv = allowed & ~(1u << orig) & 15u;
+    // (B) the other covering K-mers a..b, two per (K-1)-mer lookup
+    const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - K : 0;
+    const uint32_t jhi = min(p, L - (uint32_t)K);
+    const int ia = (int)jlo + (hasA ? 1 : 0), ib = (int)jhi - (hasB ? 1 : 0);
+    uint32_t ncand = 0, cb = 0;
+    while (surv) {
+      const uint32_t alt = (uint32_t)(__ffs((int)surv) - 1);
+      surv &= surv - 1;
+      const unsigned __int128 wa = (win & ~((unsigned __int128)3 << (2 * K))) | ((unsigned __int128)alt << (2 * K));
+      bool ok = true;
+      for (int j = ia + 1; j <= ib + 1 && ok; j += 2) {
+        // (K-1)-mer j with its pred base j-1 and succ base j+K-1: window bits
+        // from base j-1 = p-K + (j-1-p+K)
+        const uint64_t W = (uint64_t)((wa >> (2 * (uint32_t)(j - 1 - (int)p + K))) & km);
+        const uint32_t r2 = ext_pair(et, W, K);
+        ++nl;
+        ok = (r2 & 1) && (j > ib || (r2 & 2));
+      }
+      if (ok) {
+        ++ncand;
+        cb = alt;
+      }
+    }
+    dec[i] = ncand == 1 ? (uint8_t)cb : ncand > 1 ? kPcAmbiguous : kPcNone;
+  }
+  wave_add(looks, nl);
+}
+
+__global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ base_off,
+                                                  const uint64_t* __restrict__ byte_off, uint8_t* __restrict__ packed,
+                                                  uint8_t* __restrict__ quals, uint64_t n_reads, int K,
+                                                  const unsigned long long* __restrict__ weak,
+                                                  const PcCand* __restrict__ cand, const uint8_t* __restrict__ dec,
+                                                  const uint64_t* __restrict__ cstart,
+                                                  const uint32_t* __restrict__ ccnt, uint8_t* __restrict__ clean,
+                                                  PcCounters* __restrict__ cnt) {
+  uint32_t n_sus = 0, n_cor = 0, n_amb = 0, n_unc = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q0 = base_off[r];
+    const uint32_t L = (uint32_t)(base_off[r + 1] - q0);
+    if (L < (uint32_t)K) {  // no K-mer, nothing weak
+      if (clean) clean[r] = 1;
+      continue;
+    }
+    const uint64_t s0 = cstart[r];
+    const uint32_t n = ccnt[r];
+    uint8_t* rd = packed + byte_off[r];
+    uint8_t* q = quals + q0;
+    int last = -(int)kPcMaxL - 64;  // latest correction
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t p = cand[s0 + i].p;
+      if ((int)p - last < K) continue;  // a covering K-mer holds a correction: solid
+      ++n_sus;
+      const uint8_t d = dec[s0 + i];
+      if (d < 4) {
+        const uint32_t sh = 2 * (p & 3);
+        rd[p >> 2] = (uint8_t)((rd[p >> 2] & ~(3u << sh)) | ((uint32_t)d << sh));
+        uint32_t nq = 255;
+        if (p > 0) nq = min(nq, (uint32_t)q[p - 1]);
+        if (p + 1 < L) nq = min(nq, (uint32_t)q[p + 1]);
+        q[p] = (uint8_t)nq;
+        ++n_cor;
+        last = (int)p;
+      } else if (d == kPcAmbiguous) {
+        ++n_amb;
+      } else {
+        ++n_unc;
+      }
+    }
+    if (!clean) continue;
+    // clean: every counted-weak K-mer j holds a correction c (j <= c < j+K)
+    const uint64_t e = q0 + (L - (uint32_t)K + 1);
+    bool ok = true;
+    for (uint64_t b = q0; b < e && ok; b = (b | 63) + 1) {
+      const uint64_t hi = min(e, (b | 63) + 1);
+      uint64_t W = weak[b >> 6] >> (b & 63);
+      if (hi - b < 64) W &= (1ull << (hi - b)) - 1;
+      if (!W) continue;
+      // K-mers b .. hi-1 (global bit index) covered by the corrections
+      uint64_t D = 0;
+      int lc = -(int)kPcMaxL - 64;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t p = cand[s0 + i].p;
+        if ((int)p - lc < K) continue;
+        if (dec[s0 + i] >= 4) continue;
+        lc = (int)p;
+        // covered K-mers [p-K+1, p] relative to b - q0
+        const int64_t lo = (int64_t)p - K + 1 - (int64_t)(b - q0), up = (int64_t)p - (int64_t)(b - q0);
+        if (up < 0 || lo >= 64) continue;
+        const int a = lo < 0 ? 0 : (int)lo, z = up > 63 ? 63 : (int)up;
+        D |= (z - a == 63 ? ~0ull : ((1ull << (z - a + 1)) - 1)) << a;
+      }
+      ok = (W & ~D) == 0;
+    }
+    clean[r] = ok ? 1 : 0;
+  }
+  wave_add(&cnt->suspect, n_sus);
+  wave_add(&cnt->corrected, n_cor);
+  wave_add(&cnt->ambiguous, n_amb);
+  wave_add(&cnt->uncorrectable, n_unc);
+}
+
 // One correction pass of every read of `dr` against the solid hash list.
 // weak: the pass's weak-instance bitmap (sk_solid_weak) or null (weak tests
 // by lookups); with it, the pass also leaves per-read clean flags ("pc_clean":
@@ -375,49 +845,120 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   unsigned long long* dcnt = nullptr;
   APG_TRY(workspace_t(ctx, "pc_counters", 8, &dcnt));
   APG_CHECK_HIP(hipMemsetAsync(dcnt, 0, 8 * 8, ctx->stream));
-  uint64_t T = 1024;
-  while (T < 2 * n_solid) T <<= 1;
-  unsigned long long* table = nullptr;
-  APG_TRY(workspace_t(ctx, "pc_table", T, &table));
-  APG_CHECK_HIP(hipMemsetAsync(table, 0xff, T * 8, ctx->stream));
-  // prefix bitmap: 2^mb bits, ~16 bits per solid K-mer, at most one bit per K-mer
-  int mb = 10;
-  while ((1ull << mb) < 16 * n_solid && mb < 2 * p.K) ++mb;
-  if (mb > 2 * p.K) mb = 2 * p.K;
-  uint32_t* bitmap = nullptr;
-  const uint64_t words = std::max<uint64_t>(1, (1ull << mb) / 32);
-  APG_TRY(workspace_t(ctx, "pc_bitmap", words, &bitmap));
-  APG_CHECK_HIP(hipMemsetAsync(bitmap, 0, words * 4, ctx->stream));
-  kbegin(ctx, "solid_insert", n_solid * (8 + 64 + 64));
-  if (n_solid) {
-    k_solid_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, table, T - 1);
-    k_bitmap_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, bitmap, 2 * p.K - mb);
-  }
-  kend(ctx);
-  const SolidSet ss{table, T - 1, bitmap, 2 * p.K - mb};
-  APG_CHECK_HIP(hipGetLastError());
   const HashP hp = make_hashp(p.K);
-  // reads + quals (+ the weak bitmap and the clean flags)
-  kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases + (weak ? dr->n_bases / 8 + dr->n_reads : 0));
-  if (dr->n_reads)
-    k_precorrect_wave<<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
-        dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss, weak,
-        clean, reinterpret_cast<PcCounters*>(dcnt));
-  kend(ctx);
-  if (dr->max_len > kPcMaxL) {  // reads longer than one wave's registers: thread per read
-    const uint64_t rgrid =
-        std::max<uint64_t>(1, std::min<uint64_t>((dr->n_reads + 255) / 256, (uint64_t)ctx->n_cu * 32));
-    k_precorrect<<<rgrid, 256, 0, ctx->stream>>>(dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals,
-                                                 dr->n_reads, p.K, hp, p.max_q_suspect, ss, kPcMaxL + 1, clean,
-                                                 reinterpret_cast<PcCounters*>(dcnt));
+  // (K-1)-mer extension lookups (2 <= K <= 29, reads that fit one wave's
+  // registers), else K-mer lookups in a hash set behind a prefix bitmap
+  const bool ext = p.K >= 2 && p.K <= 29 && dr->max_len <= kPcMaxL;
+  SolidSet ss{};
+  ExtTab et{};
+  ctx->pc_ext_valid = false;
+  if (ext) {
+    APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
+  } else {
+    uint64_t T = 1024;
+    while (T < 2 * n_solid) T <<= 1;
+    unsigned long long* table = nullptr;
+    APG_TRY(workspace_t(ctx, "pc_table", T, &table));
+    APG_CHECK_HIP(hipMemsetAsync(table, 0xff, T * 8, ctx->stream));
+    // prefix bitmap: 2^mb bits, ~16 bits per solid K-mer, at most one bit per K-mer
+    int mb = 10;
+    while ((1ull << mb) < 16 * n_solid && mb < 2 * p.K) ++mb;
+    if (mb > 2 * p.K) mb = 2 * p.K;
+    uint32_t* bitmap = nullptr;
+    const uint64_t words = std::max<uint64_t>(1, (1ull << mb) / 32);
+    APG_TRY(workspace_t(ctx, "pc_bitmap", words, &bitmap));
+    APG_CHECK_HIP(hipMemsetAsync(bitmap, 0, words * 4, ctx->stream));
+    kbegin(ctx, "solid_insert", n_solid * (8 + 64 + 64));
+    if (n_solid) {
+      k_solid_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, table, T - 1);
+      k_bitmap_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, bitmap, 2 * p.K - mb);
+    }
+    kend(ctx);
+    ss = SolidSet{table, T - 1, bitmap, 2 * p.K - mb};
+  }
+  APG_CHECK_HIP(hipGetLastError());
+  PcCounters* pcnt = reinterpret_cast<PcCounters*>(dcnt);
+  if (ext && weak) {
+    // candidates -> independent decisions -> sequential rule per read
+    uint32_t* ccnt = nullptr;
+    uint64_t* cstart = nullptr;
+    const uint64_t nr1 = std::max<uint64_t>(dr->n_reads, 1);
+    APG_TRY(workspace_t(ctx, "pc_ccnt", nr1, &ccnt));
+    APG_TRY(workspace_t(ctx, "pc_cstart", nr1, &cstart));
+    const uint64_t ntiles = (dr->n_reads + kPcTileReads - 1) / kPcTileReads;
+    uint32_t* tcnt = nullptr;
+    uint64_t* toff = nullptr;
+    APG_TRY(workspace_t(ctx, "pc_tcnt", std::max<uint64_t>(ntiles, 1), &tcnt));
+    APG_TRY(workspace_t(ctx, "pc_toff", ntiles + 1, &toff));
+    const uint32_t cgrid = grid_for(ctx, dr->n_reads, kPcTileReads);
+    // reads' offsets + quals + weak bits in; tile counts out
+    kbegin(ctx, "pc_candidates", dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads);
+    if (dr->n_reads)
+      k_pc_candidates<false><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
+          dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, tcnt,
+          nullptr, nullptr, nullptr, nullptr);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    APG_TRY(scan_u32_u64(ctx, tcnt, ntiles, toff, "pct"));
+    uint64_t ncand = 0;
+    APG_CHECK_HIP(hipMemcpyAsync(&ncand, toff + ntiles, 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    PcCand* cand = nullptr;
+    APG_TRY(workspace_t(ctx, "pc_cand", std::max<uint64_t>(ncand, 1), &cand));
+    // reads' offsets + quals + weak bits in; runs and records out
+    kbegin(ctx, "pc_cand_write",
+           dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads + 12 * dr->n_reads + ncand * sizeof(PcCand));
+    if (dr->n_reads)
+      k_pc_candidates<true><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
+          dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, nullptr,
+          toff, cand, cstart, ccnt);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    uint8_t* dec = nullptr;
+    APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));
+    // candidate records in, decisions out (+ 64 B per extension lookup, after the sync)
+    kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 1));
+    if (ncand)
+      k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups);
+    kend(ctx);
+    // offsets, runs, the candidates' positions and decisions, weak bits in;
+    // corrected bases and quals, clean flags out
+    kbegin(ctx, "pc_apply", 16 * dr->n_reads + 8 * dr->n_reads + ncand * 9 + dr->n_bases / 8 + dr->n_reads);
+    if (dr->n_reads)
+      k_pc_apply<<<grid_for(ctx, dr->n_reads), 256, 0, ctx->stream>>>(
+          dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, weak, cand, dec, cstart, ccnt,
+          clean, pcnt);
+    kend(ctx);
+  } else {
+    // reads + quals (+ the weak bitmap and the clean flags)
+    kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases + (weak ? dr->n_bases / 8 + dr->n_reads : 0));
+    if (dr->n_reads) {
+      if (ext)
+        k_precorrect_wave<true><<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
+            dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss, et,
+            weak, clean, reinterpret_cast<PcCounters*>(dcnt));
+      else
+        k_precorrect_wave<false><<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
+            dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss, et,
+            weak, clean, reinterpret_cast<PcCounters*>(dcnt));
+    }
+    kend(ctx);
+    if (dr->max_len > kPcMaxL) {  // reads longer than one wave's registers: thread per read
+      const uint64_t rgrid =
+          std::max<uint64_t>(1, std::min<uint64_t>((dr->n_reads + 255) / 256, (uint64_t)ctx->n_cu * 32));
+      k_precorrect<<<rgrid, 256, 0, ctx->stream>>>(dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals,
+                                                   dr->n_reads, p.K, hp, p.max_q_suspect, ss, kPcMaxL + 1, clean,
+                                                   reinterpret_cast<PcCounters*>(dcnt));
+    }
   }
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long h[6];
   APG_CHECK_HIP(hipMemcpyAsync(h, dcnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  // a bitmap query reads one word of an L3-resident bitmap (counted 4 B); a
-  // table probe is a random 64-byte HBM line
-  kbytes_add(ctx, "precorrect", h[4] * 4 + h[5] * 64);
+  // extension lookup: a random 64-byte HBM line; K-mer set: a bitmap query
+  // reads one word of an L3-resident bitmap (counted 4 B), a table probe a
+  // random 64-byte line
+  kbytes_add(ctx, "precorrect", ext ? h[4] * 64 : h[4] * 4 + h[5] * 64);
   vlog(ctx, "precorrect: %llu solid-set queries, %llu table probes", h[4], h[5]);
   st->n_suspect += h[0];
   st->n_corrected += h[1];
@@ -428,6 +969,11 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   ctx->pc_n = n_solid;
   ctx->pc_K = p.K;
   ctx->pc_list_valid = true;
+  if (ext) {
+    ctx->pc_ext_slot = et.slot;
+    ctx->pc_ext_mask = et.mask;
+    ctx->pc_ext_valid = true;
+  }
   vlog(ctx, "precorrect pass: solid=%llu suspect=%llu corrected=%llu ambiguous=%llu none=%llu",
        (unsigned long long)n_solid, h[0], h[1], h[2], h[3]);
   static std::atomic<uint64_t> g_edit{1ull << 62};

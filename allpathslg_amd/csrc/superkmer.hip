@@ -620,6 +620,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   uint64_t* sl = nullptr;
   if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
     ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
+    ctx->pc_ext_valid = false;
     solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }

@@ -166,3 +166,35 @@ def test_precorrect_long_and_boundary_reads(gpu_ctx):
         exp, est = oracle.precorrect(reads, K=K, min_solid=2)
         assert_same(got, exp)
         assert st == {**st, **est}
+
+
+@pytest.mark.gpu
+def test_precorrect_extension_path_short_reads(gpu_ctx):
+    """Reads <= 1024 bases take the (K-1)-mer extension-table path for
+    2 <= K <= 29 (weak tests by lookups below K = 9, by the counted weak
+    bitmap above); reads as short as K and shorter than 2K-1 exercise the
+    clipped covering ranges (no K-mer on one or both sides of a suspect)."""
+    rng = np.random.default_rng(91)
+    g = synth_genome(20_000, 92)
+    seqs, quals = [], []
+    for L in list(rng.integers(2, 120, size=400)) + [1024, 1000, 512] * 4:
+        s = int(rng.integers(0, 20_000 - int(L)))
+        r = g[s : s + int(L)].copy()
+        q = np.full(int(L), 40, np.uint8)
+        flip = rng.random(int(L)) < 0.02
+        r[flip] = (r[flip] + 1 + rng.integers(0, 3, size=int(flip.sum()))) % 4
+        q[flip] = rng.integers(2, 20, size=int(flip.sum()))
+        low = rng.random(int(L)) < 0.02
+        q[low] = 10
+        seqs.append(r)
+        quals.append(q)
+    # the genome itself, tiled, keeps most K-mers solid
+    for s in range(0, 20_000 - 100, 7):
+        seqs.append(g[s : s + 100].copy())
+        quals.append(np.full(100, 40, np.uint8))
+    reads = ReadSet.from_sequences(seqs, quals)
+    for K in (2, 3, 5, 8, 9, 13, 24, 28, 29):
+        got, st = gpu_ctx.precorrect(reads, K=K, min_solid=2)
+        exp, est = oracle.precorrect(reads, K=K, min_solid=2)
+        assert_same(got, exp)
+        assert st == {**st, **est}
