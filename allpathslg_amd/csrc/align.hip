@@ -293,6 +293,203 @@ __global__ void __launch_bounds__(256) k_banded_sw(SeqSet S, SeqSet T, const Aln
 }
 
 // ---------------------------------------------------------------------------
+// Banded SW, one lane per pair (bands of <= BW diagonals, w <= 15): the DP
+// row lives in the lane's registers (D[kk], diagonal kk = j - i - dmin), so a
+// cell is a handful of VALU ops with no cross-lane traffic; 64 pairs per wave
+// instead of one.  Row i: D[kk] = min(D'[kk] + sub, D'[kk+1] + 3, D[kk-1] + 3)
+// (D' = row i-1), the same recurrence, tie order and end rule as k_banded_sw.
+// The 2-bit directions of a row are one u64, stored lane-interleaved
+// (dirs[i * nthr + thread], coalesced); the traceback re-reads them (L2-hot).
+// mismatches = (cost - 3 * gaps) / 2: every path cost is 2 per mismatch plus 3
+// per gap base, so no base is re-read.  Blocks: the traceback sees the moves
+// backwards, so a first pass counts them and a second writes block r - q.
+// ---------------------------------------------------------------------------
+// 32 bases [p, p+32) of a target, p possibly negative (bases before the target
+// read as 0) or past its end (0): reads stay inside the target set's slack.
+__device__ __forceinline__ uint64_t sw_tload(const uint8_t* tr, int Lt, int p) {
+  if (p >= Lt || p <= -32) return 0;
+  if (p < 0) return load_lsb64(tr, 0) << (2 * (-p));
+  return load_lsb64(tr, (uint32_t)p);
+}
+
+template <int BW>
+__global__ void __launch_bounds__(256) k_banded_sw_lane(SeqSet S, SeqSet T, const AlnPair* __restrict__ pairs,
+                                                        uint64_t n, int w, uint64_t* __restrict__ dirs, SwOut o) {
+  const uint64_t gt = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  const int band = 2 * w + 1;
+  for (uint64_t k = gt; k < n; k += nthr) {
+    const AlnPair pr = pairs[k];
+    const int Ls = (int)(S.base_off[pr.s + 1] - S.base_off[pr.s]);
+    const int Lt = (int)(T.base_off[pr.t + 1] - T.base_off[pr.t]);
+    const uint8_t* sr = S.packed + S.byte_off[pr.s];
+    const uint8_t* tr = T.packed + T.byte_off[pr.t];
+    const bool rc = pr.flags & 1;
+    const int dmin = pr.off - w;
+    int32_t D[BW];
+#pragma unroll
+    for (int kk = 0; kk < BW; ++kk) {
+      const int j = dmin + kk;
+      D[kk] = (kk < band && j >= 0 && j <= Lt) ? 0 : kSwInf;
+    }
+    // target bases from tp = i + dmin - 1 (row i's T[j-1] for kk = 0), 64 buffered
+    int tp = dmin;
+    unsigned __int128 tb = (unsigned __int128)sw_tload(tr, Lt, tp) |
+                           ((unsigned __int128)sw_tload(tr, Lt, tp + 32) << 64);
+    int have = 64;
+    uint64_t sw64 = 0;
+    int sq = 0;  // S window start (rc: bases [sq, sq+32) hold S[Ls - i])
+    for (int i = 1; i <= Ls; ++i) {
+      uint32_t sb;
+      if (!rc) {
+        if (((i - 1) & 31) == 0) sw64 = load_lsb64(sr, (uint32_t)(i - 1));
+        sb = (uint32_t)(sw64 >> (2 * ((i - 1) & 31))) & 3;
+      } else {
+        const int q = Ls - i;
+        if (i == 1 || q < sq) {
+          sq = q >= 31 ? q - 31 : 0;
+          sw64 = load_lsb64(sr, (uint32_t)sq);
+        }
+        sb = 3 - ((uint32_t)(sw64 >> (2 * (q - sq))) & 3);
+      }
+      const uint64_t trow = (uint64_t)tb;
+      uint64_t dw = 0;
+      int32_t left = kSwInf;
+      const int j0 = i + dmin;
+#pragma unroll
+      for (int kk = 0; kk < BW; ++kk) {
+        if (kk < band) {  // wave-uniform
+          const int j = j0 + kk;
+          const bool valid = j >= 0 && j <= Lt;
+          const uint32_t tbase = (uint32_t)(trow >> (2 * kk)) & 3;
+          const int32_t diag = (valid && j >= 1) ? D[kk] + (sb == tbase ? 0 : 2) : kSwInf;
+          const int32_t vert = (valid && kk + 1 < band) ? D[kk + 1 < BW ? kk + 1 : kk] + 3 : kSwInf;
+          const int32_t horz = (valid && j >= 1 && kk >= 1) ? left + 3 : kSwInf;
+          int32_t d = min(min(diag, vert), horz);
+          uint32_t dir = DIR_START;
+          if (d >= kSwInf)
+            d = kSwInf;
+          else
+            dir = d == diag ? DIR_DIAG : d == horz ? DIR_HORZ : DIR_VERT;
+          D[kk] = d;
+          left = d;
+          dw |= (uint64_t)dir << (2 * kk);
+        }
+      }
+      dirs[(uint64_t)i * nthr + gt] = dw;
+      tb >>= 2;
+      ++tp;
+      if (--have < 32) {
+        tb |= (unsigned __int128)sw_tload(tr, Lt, tp + have) << (2 * have);
+        have += 32;
+      }
+    }
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int kk = 0; kk < BW; ++kk)
+      if (kk < band && D[kk] < kSwInf) best = min(best, ((unsigned long long)(uint32_t)D[kk] << 32) | (uint32_t)kk);
+    int32_t* r = o.res + 8 * k;
+    if (best == ~0ull) {
+      reinterpret_cast<int4*>(r)[0] = int4{0, 0, 0, 0};
+      reinterpret_cast<int4*>(r)[1] = int4{0, 0, 0, 1};
+      continue;
+    }
+    const int cost = (int)(best >> 32);
+    const int kend = (int)(best & 0xffffffffu);
+    // traceback pass 1: gaps, start, blocks (reverse segmentation, see above)
+    int gs = 0, gtn = 0, nrev = 0;  // nrev: blocks completed before reaching m_0
+    int lastlen = -1, lastgap = 0;  // block r (the forward-last), once complete
+    int len = 0, gap = 0;
+    bool inG = false;
+    int kk = kend, i = Ls, ci = -1;
+    uint64_t dw = 0;
+    while (i > 0) {
+      if (i != ci) {
+        dw = dirs[(uint64_t)i * nthr + gt];
+        ci = i;
+      }
+      const uint32_t d = (uint32_t)(dw >> (2 * kk)) & 3;
+      if (d == DIR_DIAG) {
+        if (inG) {
+          if (nrev == 0) {
+            lastlen = len;
+            lastgap = gap;
+          }
+          ++nrev;
+          len = 0;
+          gap = 0;
+          inG = false;
+        }
+        ++len;
+        --i;
+      } else if (d == DIR_HORZ) {
+        inG = true;
+        ++gap;
+        ++gs;
+        --kk;
+      } else {
+        inG = true;
+        --gap;
+        ++gtn;
+        --i;
+        ++kk;
+      }
+    }
+    // block 0 = (gap, len) now; block r = (lastgap, lastlen) if nrev > 0
+    const bool emit_r = nrev == 0 ? true : (lastlen > 0 || lastgap != 0);
+    const int nb = nrev + (emit_r ? 1 : 0);  // nrev == 0: block 0 is block r, always emitted (nb == 0 rule)
+    reinterpret_cast<int4*>(r)[0] = int4{cost, dmin + kk, Ls + dmin + kend, (cost - 3 * (gs + gtn)) / 2};
+    const bool over = o.blocks && (uint32_t)nb > o.max_blocks;
+    reinterpret_cast<int4*>(r)[1] = int4{gs, gtn, nb, over ? 2 : 0};
+    if (!o.blocks) continue;
+    // pass 2: blocks, forward index r - q for the q-th completed in reverse
+    int32_t* blk = o.blocks + 2 * k * (uint64_t)o.max_blocks;
+    auto put = [&](int idx, int g, int l) {
+      if (idx >= 0 && (uint32_t)idx < o.max_blocks) {
+        blk[2 * idx] = g;
+        blk[2 * idx + 1] = l;
+      }
+    };
+    const int rr = nrev;  // forward index of the reverse-first block
+    int q = 0;
+    len = 0;
+    gap = 0;
+    inG = false;
+    kk = kend;
+    i = Ls;
+    ci = -1;
+    while (i > 0) {
+      if (i != ci) {
+        dw = dirs[(uint64_t)i * nthr + gt];
+        ci = i;
+      }
+      const uint32_t d = (uint32_t)(dw >> (2 * kk)) & 3;
+      if (d == DIR_DIAG) {
+        if (inG) {
+          if (q > 0 || emit_r) put(rr - q, gap, len);
+          ++q;
+          len = 0;
+          gap = 0;
+          inG = false;
+        }
+        ++len;
+        --i;
+      } else if (d == DIR_HORZ) {
+        inG = true;
+        ++gap;
+        --kk;
+      } else {
+        inG = true;
+        --gap;
+        --i;
+        ++kk;
+      }
+    }
+    if (q > 0 || emit_r) put(rr - q, gap, len);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Consensus
 // ---------------------------------------------------------------------------
 __global__ void k_votes(SeqSet R, SeqSet T, const AlnPair* __restrict__ plc, uint64_t n, uint32_t* __restrict__ votes) {
@@ -419,15 +616,38 @@ int apg_banded_sw_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T, co
   static_assert(sizeof(apg_sw_hit) == 32, "hit layout");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   if (n == 0) return APG_OK;
-  const int nch = (2 * band_w + 1 + 63) / 64;
   const uint32_t rows_cap = (uint32_t)std::max<uint64_t>(S->max_len, 1);
+  SwOut o{reinterpret_cast<int32_t*>(d_out), d_blocks, d_blocks ? max_blocks : 0};
+  if (d_blocks)  // entries past a pair's n_blocks read as zero
+    APG_CHECK_HIP(hipMemsetAsync(d_blocks, 0, n * (uint64_t)max_blocks * 8, ctx->stream));
+  if (band_w <= 15) {  // lane per pair: 64 pairs per wave, the row in registers
+    // direction rows for every thread of the grid: <= ~256 MiB
+    const uint64_t per_thread = 8ull * (rows_cap + 1);
+    const uint64_t max_thr = std::max<uint64_t>(256, (256ull << 20) / per_thread);
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>({(n + 255) / 256, (uint64_t)ctx->n_cu * 4, max_thr / 256}));
+    const uint64_t nthr = (uint64_t)grid * 256;
+    uint64_t* dirs = nullptr;
+    APG_TRY(workspace_t(ctx, "a_sw_dirs", nthr * (rows_cap + 1), &dirs));
+    // pairs + results + the S / T bases, and the direction rows written and re-read
+    kbegin(ctx, "banded_sw", n * (16 + 32) + n * (uint64_t)rows_cap * (8 + 8 + 1));
+    const SeqSet ss = seqset(S), ts = seqset(T);
+    const AlnPair* pp = reinterpret_cast<const AlnPair*>(d_pairs);
+    if (band_w <= 7)
+      k_banded_sw_lane<16><<<grid, 256, 0, ctx->stream>>>(ss, ts, pp, n, band_w, dirs, o);
+    else if (band_w <= 11)
+      k_banded_sw_lane<24><<<grid, 256, 0, ctx->stream>>>(ss, ts, pp, n, band_w, dirs, o);
+    else
+      k_banded_sw_lane<32><<<grid, 256, 0, ctx->stream>>>(ss, ts, pp, n, band_w, dirs, o);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    return sync(ctx);
+  }
+  const int nch = (2 * band_w + 1 + 63) / 64;
   const uint32_t grid = grid_for(ctx, n, 4);  // 4 waves per block, one pair per wave
   const uint64_t waves = (uint64_t)grid * 4;
   uint64_t* scratch = nullptr;
   APG_TRY(workspace_t(ctx, "a_sw_scratch", waves * sw_scratch_words(rows_cap, nch), &scratch));
-  SwOut o{reinterpret_cast<int32_t*>(d_out), d_blocks, d_blocks ? max_blocks : 0};
-  if (d_blocks)  // entries past a pair's n_blocks read as zero
-    APG_CHECK_HIP(hipMemsetAsync(d_blocks, 0, n * (uint64_t)max_blocks * 8, ctx->stream));
   kbegin(ctx, "banded_sw", n * (16 + 32) + n * (uint64_t)rows_cap * (2 * band_w + 1) / 4);
   k_banded_sw<<<grid, 256, 0, ctx->stream>>>(seqset(S), seqset(T), reinterpret_cast<const AlnPair*>(d_pairs), n, band_w,
                                               scratch, rows_cap, o);

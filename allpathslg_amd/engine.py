@@ -434,6 +434,22 @@ class Context:
               "apg_consensus")
         return b[:nt], q[:nt]
 
+    # device-resident variants (pairs / outputs are device pointers, e.g.
+    # torch tensors' data_ptr(); ids must be in range)
+    def gapfree_dev(self, dS: DeviceReads, dT: DeviceReads, d_pairs: int, n: int, d_out: int) -> None:
+        check(lib().apg_gapfree_dev(self._h, dS.handle, dT.handle, C.c_void_p(d_pairs), n, C.c_void_p(d_out)),
+              "apg_gapfree_dev")
+
+    def banded_sw_dev(self, dS: DeviceReads, dT: DeviceReads, d_pairs: int, n: int, band_w: int, d_out: int,
+                      d_blocks: int = 0, max_blocks: int = 0) -> None:
+        check(lib().apg_banded_sw_dev(self._h, dS.handle, dT.handle, C.c_void_p(d_pairs), n, band_w,
+                                      C.c_void_p(d_out), C.c_void_p(d_blocks or None), max_blocks),
+              "apg_banded_sw_dev")
+
+    def consensus_dev(self, dR: DeviceReads, dT: DeviceReads, d_plc: int, n: int, d_bases: int, d_quals: int) -> None:
+        check(lib().apg_consensus_dev(self._h, dR.handle, dT.handle, C.c_void_p(d_plc), n, C.c_void_p(d_bases),
+                                      C.c_void_p(d_quals)), "apg_consensus_dev")
+
     # -- sharded (multi-GPU) stages ------------------------------------------
     def shard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> np.ndarray:
         B = shard_bins(K, n_shards)

@@ -83,6 +83,22 @@ class ReadSet:
         return cls(base_off, byte_off, packed, q)
 
     @classmethod
+    def from_matrix(cls, bases: np.ndarray, quals: Optional[np.ndarray] = None):
+        """Build from an (n, L) matrix of base codes (equal-length reads),
+        vectorised; quals (n, L) uint8 or None."""
+        b = np.ascontiguousarray(bases, dtype=np.uint8)
+        n, L = b.shape
+        pad = (-L) % 4
+        if pad:
+            b = np.concatenate([b, np.zeros((n, pad), np.uint8)], axis=1)
+        packed = np.zeros(n * ((L + 3) // 4) + 64, dtype=np.uint8)
+        packed[: n * ((L + 3) // 4)] = (b[:, 0::4] | (b[:, 1::4] << 2) | (b[:, 2::4] << 4) | (b[:, 3::4] << 6)).reshape(-1)
+        base_off = np.arange(n + 1, dtype=np.uint64) * np.uint64(L)
+        byte_off = np.arange(n + 1, dtype=np.uint64) * np.uint64((L + 3) // 4)
+        q = None if quals is None else np.ascontiguousarray(quals, dtype=np.uint8).reshape(-1)
+        return cls(base_off, byte_off, packed, q)
+
+    @classmethod
     def from_strings(cls, seqs: Sequence[str]):
         code = {"A": 0, "C": 1, "G": 2, "T": 3, "N": 0}
         return cls.from_sequences([[code[c] for c in s.upper()] for s in seqs])

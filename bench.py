@@ -62,6 +62,10 @@ def parse():
     p.add_argument("--oracle-fill", action="store_true",
                    help="feed the unipath stage the simulator's true inserts instead of FillFragments (old bench)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--align-pairs", type=int, default=4_000_000,
+                   help="read placements of the aligner line (gap-free, banded SW, consensus); 0 = skip")
+    p.add_argument("--align-band", type=int, default=8)
+    p.add_argument("--align-target-len", type=int, default=50_000)
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--sharded", action="store_true",
                    help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
@@ -73,6 +77,136 @@ def parse():
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+VALU_PEAK_GOPS = 78643.2  # MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes/cycle x 2.4 GHz int32 lane-ops
+
+
+def align_workload(genome: np.ndarray, n: int, Lt: int, seed: int):
+    """Read placements for the aligner line (SURVEY §8f #2 shape): targets =
+    the genome cut into Lt-base unibase-like pieces; n 100-bp reads drawn from
+    them with 1 % substitutions (Q10, else Q40), 20 % with a 1-3 base
+    insertion or deletion, half reverse-complemented; placements = (read,
+    target, true offset, rc flag)."""
+    from allpathslg_amd import ReadSet
+
+    L = 100
+    nT = len(genome) // Lt
+    T = ReadSet.from_matrix(genome[: nT * Lt].reshape(nT, Lt))
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, nT, n)
+    o = rng.integers(8, Lt - L - 8, n)
+    cols = np.broadcast_to(np.arange(L, dtype=np.int64), (n, L)).copy()
+    kind = rng.random(n)
+    ilen = rng.integers(1, 4, n)
+    ipos = rng.integers(30, 70, n)
+    after = np.arange(L)[None, :] >= ipos[:, None]
+    dele = kind < 0.1
+    ins = (kind >= 0.1) & (kind < 0.2)
+    cols += np.where(dele[:, None] & after, ilen[:, None], 0)
+    inserted = ins[:, None] & after & (np.arange(L)[None, :] < (ipos + ilen)[:, None])
+    cols -= np.where(ins[:, None] & after & ~inserted, ilen[:, None], 0)
+    seq = genome[(t * Lt + o)[:, None] + np.maximum(cols, 0)]
+    seq = np.where(inserted, rng.integers(0, 4, (n, L), dtype=np.uint8), seq).astype(np.uint8)
+    sub = rng.random((n, L)) < 0.01
+    seq = np.where(sub, (seq + rng.integers(1, 4, (n, L), dtype=np.uint8)) % 4, seq).astype(np.uint8)
+    q = np.where(sub, 10, 40).astype(np.uint8)
+    rc = rng.random(n) < 0.5
+    seq = np.where(rc[:, None], 3 - seq[:, ::-1], seq).astype(np.uint8)
+    q = np.where(rc[:, None], q[:, ::-1], q).astype(np.uint8)
+    S = ReadSet.from_matrix(seq, q)
+    pairs = np.stack([np.arange(n), t, o, rc.astype(np.int64)], axis=1).astype(np.int32)
+    plain = ~(dele | ins)
+    return S, T, pairs, plain, sub.sum(axis=1)
+
+
+def align_bench(ctx, genome, a, reps: int = 3):
+    """Aligner line: device-resident placements through gap-free, banded SW
+    and column consensus; per-kernel times from libapg's HIP events."""
+    n = a.align_pairs
+    S, T, pairs, plain, nsub = align_workload(genome, n, a.align_target_len, a.seed + 7)
+    dS, dT = ctx.upload(S), ctx.upload(T)
+    dp = torch.from_numpy(pairs).cuda()
+    gf = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+    sw = torch.empty((n, 8), dtype=torch.int32, device="cuda")
+    cb = torch.empty(T.n_bases, dtype=torch.uint8, device="cuda")
+    cq = torch.empty(T.n_bases, dtype=torch.uint8, device="cuda")
+
+    def run():
+        ctx.gapfree_dev(dS, dT, dp.data_ptr(), n, gf.data_ptr())
+        ctx.banded_sw_dev(dS, dT, dp.data_ptr(), n, a.align_band, sw.data_ptr())
+        ctx.consensus_dev(dS, dT, dp.data_ptr(), n, cb.data_ptr(), cq.data_ptr())
+
+    run()
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    kt = ctx.kernel_times()
+    ms = {k: v[0] / max(v[1], 1) for k, v in kt.items()}
+    nb = {k: v[2] / max(v[1], 1) for k, v in kt.items()}
+    gfh, swh = gf.cpu().numpy(), sw.cpu().numpy()
+    band = 2 * a.align_band + 1
+    cells = n * 100 * band  # DP cells of the band (rows x diagonals)
+    sw_ms = ms.get("banded_sw", float("nan"))
+    gcups = cells / (sw_ms * 1e-3) / 1e9
+    # min-plus cell: diagonal + substitution cost, vertical + 3, horizontal
+    # + 3, two minima -> >= 5 int32 lane-ops per cell
+    ops_per_cell = 5
+    gf_ms = ms.get("gapfree", float("nan"))
+    cons_ms = ms.get("consensus_votes", 0.0) + ms.get("consensus_decide", 0.0)
+    out = {
+        "workload": (f"{n} placed 100-bp reads (1% subst, 20% with a 1-3 bp indel, half rc) on "
+                     f"{T.n_reads} x {a.align_target_len}-bp genome pieces; band w={a.align_band}"),
+        "pairs": n,
+        "wall_ms_per_pass": wall * 1e3,
+        "gapfree": {"ms": gf_ms, "alignments_per_s": n / (gf_ms * 1e-3),
+                    "roofline": {"bound": "hbm", "achieved": nb.get("gapfree", 0) / (gf_ms * 1e-3) / 1e9,
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": nb.get("gapfree", 0) / (gf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+        "banded_sw": {"ms": sw_ms, "alignments_per_s": n / (sw_ms * 1e-3), "gcups": gcups,
+                      "roofline": {"bound": "valu", "achieved": gcups * ops_per_cell, "peak": VALU_PEAK_GOPS,
+                                   "unit": "G int32 lane-ops/s", "ops_per_cell": ops_per_cell,
+                                   "frac": gcups * ops_per_cell / VALU_PEAK_GOPS}},
+        "consensus": {"ms": cons_ms, "placed_bases_per_s": n * 100 / (cons_ms * 1e-3)},
+        "checks": {
+            # error-free-indel reads at their true offset: mismatches = substitutions
+            "gapfree_mismatches_equal_substitutions": bool((gfh[plain, 1] == nsub[plain]).all()),
+            "sw_all_reached_end": bool((swh[:, 7] == 0).all()),
+            # an indel read costs at most its substitutions x 2 + the indel x 3
+            "sw_cost_bounded": bool((swh[:, 0] <= 2 * nsub + 9).all()),
+            "sw_plain_cost_is_2x_subst": bool((swh[plain, 0] <= 2 * nsub[plain]).all()),
+        },
+    }
+    dS.free()
+    dT.free()
+    return out, (S, T, pairs)
+
+
+def align_cpu_baseline(S, T, pairs, band_w: int, n: int) -> dict:
+    """The aligner line's CPU baseline: oracle/ restatement, one thread, the
+    first n placements of the same workload."""
+    import oracle
+
+    Ss = S.subset(0, n)
+    p = pairs[:n]
+    rates = {}
+    t = time.perf_counter()
+    oracle.gapfree(Ss, T, p)
+    rates["gapfree_alignments_per_s"] = n / (time.perf_counter() - t)
+    nsw = min(n, 2000)  # the restatement's banded SW runs ~200 alignments/s
+    t = time.perf_counter()
+    oracle.banded_sw(S.subset(0, nsw), T, pairs[:nsw], band_w)
+    rates["banded_sw_alignments_per_s"] = nsw / (time.perf_counter() - t)
+    t = time.perf_counter()
+    oracle.consensus(Ss, T, p)
+    rates["consensus_placed_bases_per_s"] = n * 100 / (time.perf_counter() - t)
+    return {**rates, "cores": 1, "kind": "port",
+            "sample": (f"oracle/ CPU restatement, single-threaded, same workload: first {n} placements "
+                       f"(gap-free, consensus), first {min(n, 2000)} (banded SW)")}
 
 
 def main():
@@ -270,6 +404,13 @@ def main():
                "sample": "oracle/ CPU restatement, single-threaded, same synthetic inputs; " + desc +
                          "; value = 1/(sum of 1/stage_rate)"}
 
+    aligners = None
+    if rank == 0 and a.align_pairs > 0 and not a.spectrum_only:
+        aligners, (aS, aT, apairs) = align_bench(ctx, genome, a)
+        if not a.no_cpu_baseline:
+            aligners["cpu_baseline"] = align_cpu_baseline(aS, aT, apairs, a.align_band, min(20_000, a.align_pairs))
+        del aS, aT, apairs
+
     if rank == 0:
         total_reads = world * reads.n_reads * a.steps
         out = {
@@ -308,6 +449,7 @@ def main():
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
+            "aligners": aligners,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},
             "precorrect_stats": pst,
             "fill_stats": fst,

@@ -23,7 +23,7 @@ def test_gapfree_parity(gpu_ctx):
     assert np.array_equal(gpu_ctx.gapfree(noq, T, pairs), oracle.gapfree(noq, T, pairs))
 
 
-@pytest.mark.parametrize("w", [0, 1, 5, 31, 32, 63, 64, 100, 127])
+@pytest.mark.parametrize("w", [0, 1, 5, 7, 8, 11, 12, 15, 16, 31, 32, 63, 64, 100, 127])
 def test_banded_sw_parity(gpu_ctx, w):
     S, T, pairs = sw_case(n_targets=12, n_pairs=500, seed=30 + w)
     got, gb = gpu_ctx.banded_sw(S, T, pairs, band_w=w, max_blocks=16)
@@ -35,11 +35,24 @@ def test_banded_sw_parity(gpu_ctx, w):
     assert np.array_equal(got2[:, :7], exp[:, :7])
 
 
+@pytest.mark.parametrize("w", [3, 8, 40])
+def test_banded_sw_block_overflow(gpu_ctx, w):
+    """More blocks than max_blocks: status 2, n_blocks exact, the first
+    max_blocks blocks written (lane-per-pair kernel for w <= 15, wave kernel
+    above)."""
+    S, T, pairs = sw_case(n_targets=8, n_pairs=400, seed=70 + w)
+    got, gb = gpu_ctx.banded_sw(S, T, pairs, band_w=w, max_blocks=2)
+    exp, eb = oracle.banded_sw(S, T, pairs, band_w=w, max_blocks=2)
+    assert np.array_equal(got, exp) and np.array_equal(gb, eb)
+    assert (got[:, 7] == 2).any()
+
+
 def test_banded_sw_long_queries(gpu_ctx):
     S, T, pairs = sw_case(n_targets=4, n_pairs=120, tlen=3000, slen=(800, 1500), seed=44)
-    got, gb = gpu_ctx.banded_sw(S, T, pairs, band_w=20, max_blocks=40)
-    exp, eb = oracle.banded_sw(S, T, pairs, band_w=20, max_blocks=40)
-    assert np.array_equal(got, exp) and np.array_equal(gb, eb)
+    for w in (20, 9):  # wave kernel, lane-per-pair kernel (1000+ direction rows per lane)
+        got, gb = gpu_ctx.banded_sw(S, T, pairs, band_w=w, max_blocks=40)
+        exp, eb = oracle.banded_sw(S, T, pairs, band_w=w, max_blocks=40)
+        assert np.array_equal(got, exp) and np.array_equal(gb, eb)
 
 
 def test_consensus_parity(gpu_ctx):
