@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <map>
@@ -167,6 +168,18 @@ constexpr const char* kBig2 = "big2";
 
 // Grid of a grid-stride kernel over n items, `per` items per block, capped at
 // 16 blocks per CU.
+// Grid of a grid-stride kernel over `work` items: exactly the blocks that
+// are resident at once (CUs x the kernel's occupancy), so every block gets
+// the same share and no second, partial round of blocks trails the first.
+template <typename Kern>
+inline uint32_t resident_grid(apg_ctx* ctx, Kern kernel, int threads, uint64_t work) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const uint64_t g = (uint64_t)ctx->n_cu * (uint64_t)per_cu;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(work, g));
+}
+
 inline uint32_t grid_for(apg_ctx* ctx, uint64_t n, int per = 256) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, (uint64_t)ctx->n_cu * 16));
 }

@@ -4,6 +4,7 @@
 // partition.hpp.
 #include <algorithm>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "apg_core.hpp"
@@ -174,6 +175,16 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restri
   __shared__ uint32_t lcnt[256];
   __shared__ uint32_t lstart[256];
   __shared__ uint32_t scan_sm[64];
+  // Records whose size is not 8 or 16 bytes leave the tile as a word stream
+  // (lane i -> word i of a digit run) so every store instruction covers
+  // whole 64-byte lines; record-per-lane stores of 24/48-byte records write
+  // partial lines, which the PMC passes showed as ~2.3x write and read
+  // traffic (profiles/r01_pmc_v10).  sdig: digit of each staged record.
+  constexpr bool kWords = sizeof(R) > 16;
+  using W = std::conditional_t<sizeof(R) % 16 == 0, SK16, uint64_t>;
+  constexpr uint32_t kWpr = sizeof(R) / sizeof(W);
+  static_assert(sizeof(R) % sizeof(W) == 0, "record size must be a multiple of the word");
+  __shared__ uint8_t sdig[kWords ? kTile : 1];
   const Chunk c = ch[blockIdx.x];
   const uint32_t tid = threadIdx.x;
   const uint64_t dmask = ndig - 1;
@@ -210,13 +221,27 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restri
 #pragma unroll
     for (int i = 0; i < kPartItems; ++i) {
       const uint32_t idx = i * kPartThreads + tid;
-      if (idx < tn) stage[lstart[(rkey(v[i]) >> shift) & dmask] + pos[i]] = v[i];
+      if (idx < tn) {
+        const uint32_t d = (uint32_t)((rkey(v[i]) >> shift) & dmask);
+        stage[lstart[d] + pos[i]] = v[i];
+        if constexpr (kWords) sdig[lstart[d] + pos[i]] = (uint8_t)d;
+      }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < tn; i += kPartThreads) {
-      const R x = stage[i];
-      const uint32_t d = (uint32_t)((rkey(x) >> shift) & dmask);
-      out[cur[d] + (i - lstart[d])] = x;
+    if constexpr (kWords) {
+      const W* sw = reinterpret_cast<const W*>(stage);
+      W* ow = reinterpret_cast<W*>(out);
+      for (uint32_t i = tid; i < tn * kWpr; i += kPartThreads) {
+        const uint32_t r = i / kWpr, k = i - r * kWpr;
+        const uint32_t d = sdig[r];
+        ow[(cur[d] + (r - lstart[d])) * kWpr + k] = sw[i];
+      }
+    } else {
+      for (uint32_t i = tid; i < tn; i += kPartThreads) {
+        const R x = stage[i];
+        const uint32_t d = (uint32_t)((rkey(x) >> shift) & dmask);
+        out[cur[d] + (i - lstart[d])] = x;
+      }
     }
     __syncthreads();
     if (tid < ndig) cur[tid] += lcnt[tid];

@@ -49,7 +49,8 @@ constexpr int kSkBases = 40;
 constexpr int kSkDigitBits = 5;
 constexpr uint64_t kSkBucketKmers = 4096;  // K-mer instances per bucket the planner aims for
 constexpr uint32_t kSkTab = 2048;          // LDS table slots (u64 canonical K-mer + u32 count)
-constexpr int kSkHistBins = 256;
+constexpr int kSkHistBins = 128;  // LDS spectrum bins (counts above go to global atomics); keeps k_sk_bucket<false> under 40 KiB LDS = 4 blocks/CU
+constexpr uint32_t kSkSlotCap = 6144;  // weak pass: instances per bucket with a recorded slot (LDS: 3 blocks/CU)
 constexpr int kSkMaxW = 17;  // w = K - m + 1 <= 17 for K <= 32
 
 struct SkP {
@@ -227,8 +228,15 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
   __shared__ uint32_t scan_sm[64];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
-  __shared__ uint64_t cpos[WEAK ? kSkThreads : 1];   // weak pass: records' first-K-mer positions
-  __shared__ uint32_t wmask[WEAK ? kSkThreads : 1];  // weak pass: records' weak K-mer masks
+  // weak pass: table slot of each of the bucket's first kSkSlotCap K-mer
+  // instances (in record order), recorded while counting — slots never move
+  // once claimed, so the weak pass reads final counts without probing.  A
+  // bucket with more instances takes the probing fallback, whose per-chunk
+  // record positions and weak masks reuse the same LDS.
+  __shared__ __attribute__((aligned(16))) uint16_t islot[WEAK ? kSkSlotCap : 4];
+  static_assert(!WEAK || kSkSlotCap * 2 >= kSkThreads * 12, "fallback scratch must fit in islot");
+  uint64_t* cpos = reinterpret_cast<uint64_t*>(islot);               // [kSkThreads]
+  uint32_t* wmask = reinterpret_cast<uint32_t*>(islot + 4 * kSkThreads);  // [kSkThreads]
   constexpr unsigned long long EMPTY = ~0ull;
   constexpr int TB = __builtin_ctz(kSkTab);
   const uint32_t tid = threadIdx.x;
@@ -265,6 +273,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
       tcnt[s] = 0;
     }
     if (tid == 0) ovf = 0;
+    uint32_t ibase = 0;  // the bucket's K-mer instances before this chunk (block-uniform)
     for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
       uint32_t nk = 0;
       if (c0 + tid < nr) {
@@ -294,11 +303,15 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
           if (old == EMPTY) old = atomicCAS(&tkey[s], EMPTY, (unsigned long long)c);
           if (old == EMPTY || old == c) {
             atomicAdd(&tcnt[s], 1u);
+            if constexpr (WEAK) {
+              if (ibase + f < kSkSlotCap) islot[ibase + f] = (uint16_t)s;
+            }
             break;
           }
           s = (s + 1) & (kSkTab - 1);
         }
       }
+      ibase += tot;
       __syncthreads();
     }
     if (ovf) {
@@ -314,7 +327,32 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
       // finds its final count in the table, weak ones (count < min_solid) set
       // their bit at the instance's base position — one 64-bit atomic OR (two
       // when the run straddles a word) per record holding a weak K-mer.
-      if (o.weak) {
+      if (o.weak && ibase <= kSkSlotCap) {
+        // thread per record: its K-mers' slots are islot[ib + ex ..], their
+        // final counts give the record's weak mask directly
+        uint32_t ib = 0;
+        for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
+          uint32_t nk = 0;
+          uint64_t b = 0;
+          if (c0 + tid < nr) {
+            const R r = rec[off + c0 + tid];
+            nk = (uint32_t)(r.w0 >> 32) & 0xff;
+            b = r.pos;
+          }
+          uint32_t tot;
+          const uint32_t ex = ib + block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);
+          uint32_t m = 0;
+          for (uint32_t t = 0; t < nk; ++t)
+            if (tcnt[islot[ex + t]] < o.min_solid) m |= 1u << t;
+          if (m) {
+            const uint32_t sh = (uint32_t)(b & 63);
+            atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
+            if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
+          }
+          ib += tot;
+          __syncthreads();
+        }
+      } else if (o.weak) {
         for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
           uint32_t nk = 0;
           if (c0 + tid < nr) {
@@ -625,7 +663,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }
   SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr};
-  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * 8));
+  const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R>, kSkThreads, nb)
+                              : resident_grid(ctx, k_sk_bucket<false, R>, kSkThreads, nb);
   for (int attempt = 0;; ++attempt) {
     // weak pass: the records a second time (L2-hot) + 8 B per weak-bit word touched
     kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) * (o.weak ? 2 : 1) + (nb + 1) * 8);

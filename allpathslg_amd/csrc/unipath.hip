@@ -1968,7 +1968,7 @@ static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec**
   uint64_t cap = std::max<uint64_t>(1 << 20, nk / 4);
   KRec* nodes = nullptr;
   unsigned long long hs[4];
-  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(nb, (uint64_t)ctx->n_cu * 8));
+  const uint64_t grid = resident_grid(ctx, k_usk_bucket, kUskBThreads, nb);
   for (;;) {
     APG_TRY(workspace_t(ctx, "usk_nodes", cap, &nodes));
     APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));

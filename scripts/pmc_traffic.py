@@ -19,17 +19,18 @@ import sys
 
 # HIP symbol prefix -> (bench timing label, read pattern)
 KERNELS = {
-    "apg::k_uinsert_reads": ("u_insert", "random"),
-    "apg::k_precorrect_wave": ("precorrect", "random"),
-    "void apg::k_part_scatter<unsigned long>": ("p_part_scatter", "stream"),
-    "void apg::k_part_count<unsigned long>": ("p_part_count", "stream"),
-    "apg::k_extract_scatter": ("extract_scatter", "stream"),
+    "void apg::k_sk_bucket<true, apg::SK24>": ("sk_bucket_solid", "stream"),
+    "void apg::k_sk_bucket<false, apg::SK16>": ("sk_bucket", "stream"),
     "apg::k_sk_count": ("sk_count", "stream"),
-    "apg::k_sk_scatter": ("sk_scatter", "stream"),
-    "void apg::k_sk_bucket<false>": ("sk_bucket", "stream"),
-    "void apg::k_sk_bucket<true>": ("sk_bucket_solid", "stream"),
+    "void apg::k_sk_scatter<apg::SK16>": ("sk_scatter", "stream"),
+    "void apg::k_sk_scatter<apg::SK24>": ("sk_scatter_sk24", "stream"),
     "void apg::k_part_scatter<apg::SK16>": ("s_part_scatter", "stream"),
+    "void apg::k_part_scatter<apg::SK24>": ("s_part_scatter_sk24", "stream"),
     "void apg::k_part_count<apg::SK16>": ("s_part_count", "stream"),
+    "apg::k_fill": ("fill", "random"),
+    "apg::k_fill_write": ("fill_write", "stream"),
+    "apg::k_pc_decide": ("precorrect", "random"),
+    "void apg::k_pc_candidates<true>": ("pc_candidates", "stream"),
     "apg::k_usk_count": ("usk_count", "stream"),
     "apg::k_usk_scatter": ("usk_scatter", "stream"),
     "apg::k_usk_bucket": ("usk_bucket", "stream"),
