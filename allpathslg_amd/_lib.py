@@ -194,6 +194,17 @@ class apg_aln_pair(C.Structure):
     _fields_ = [("s_id", C.c_uint32), ("t_id", C.c_uint32), ("offset", C.c_int32), ("flags", C.c_uint32)]
 
 
+APG_ULOCS_RC = 1
+APG_ULOCS_SORTED = 2
+
+
+class apg_uloc_stats(C.Structure):
+    _fields_ = [("n_reads", C.c_uint64), ("n_placed", C.c_uint64), ("n_locs", C.c_uint64), ("n_missing", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
 class apg_gapfree_hit(C.Structure):
     _fields_ = [("overlap", C.c_uint32), ("mismatches", C.c_uint32), ("qsum", C.c_uint32), ("offset", C.c_int32)]
 
@@ -305,6 +316,13 @@ SIGNATURES = {
     "apg_consensus": (
         C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64, _u8p, _u8p]),
     "apg_consensus_dev": (C.c_int, [_P, _P, _P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "apg_unipath_locs": (
+        C.c_int, [_P, C.POINTER(apg_reads), C.c_uint32, C.POINTER(C.POINTER(apg_aln_pair)), _u64p,
+                  C.POINTER(apg_uloc_stats)]),
+    "apg_unipath_locs_dev": (
+        C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_void_p), _u64p, C.POINTER(apg_uloc_stats)]),
+    "apg_unibases_dev": (C.c_int, [_P, C.POINTER(_P)]),
+    "apg_dreads_shape": (C.c_int, [_P, _P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),

@@ -492,21 +492,71 @@ __global__ void __launch_bounds__(256) k_banded_sw_lane(SeqSet S, SeqSet T, cons
 // ---------------------------------------------------------------------------
 // Consensus
 // ---------------------------------------------------------------------------
-__global__ void k_votes(SeqSet R, SeqSet T, const AlnPair* __restrict__ plc, uint64_t n, uint32_t* __restrict__ votes) {
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
-    const AlnPair p = plc[k];
-    const uint32_t L = (uint32_t)(R.base_off[p.s + 1] - R.base_off[p.s]);
-    const uint32_t Lt = (uint32_t)(T.base_off[p.t + 1] - T.base_off[p.t]);
-    const uint8_t* rd = R.packed + R.byte_off[p.s];
-    const uint8_t* q = R.quals + R.base_off[p.s];
-    const bool rc = p.flags & 1;
-    const uint64_t tb = T.base_off[p.t];
-    const int64_t lo = std::max<int64_t>(0, -(int64_t)p.off);
-    const int64_t hi = std::min<int64_t>((int64_t)L, (int64_t)Lt - p.off);
-    for (int64_t i = lo; i < hi; ++i) {
-      const uint32_t b = rc ? 3 - abase(rd, (uint32_t)(L - 1 - i)) : abase(rd, (uint32_t)i);
-      const uint32_t qq = rc ? q[L - 1 - i] : q[i];
-      if (qq) atomicAdd(&votes[(tb + (uint64_t)(i + p.off)) * 4 + b], qq);
+// Votes through an LDS column window: a block takes kVoteChunk consecutive
+// placements (wave per placement, lane per base, so a wave's votes hit
+// consecutive columns), accumulates them in a window of kVoteWin columns
+// starting at the chunk's first placement, and flushes the window's nonzero
+// counters with one coalesced global atomic each.  Correct for any placement
+// order (votes outside the window go straight to global atomics); placements
+// sorted by (target, offset) — apg_unipath_locs with APG_ULOCS_SORTED — land
+// almost entirely in the window, so a column takes one global atomic per
+// chunk instead of one per placed base (coverage x fewer).
+constexpr int kVoteThreads = 256;
+constexpr uint32_t kVoteChunk = 128;
+constexpr uint32_t kVoteWin = 2048;  // columns x 4 u32 counters = 32 KiB of LDS
+
+__global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, const AlnPair* __restrict__ plc,
+                                                        uint64_t n, uint32_t* __restrict__ votes) {
+  __shared__ uint32_t win[kVoteWin * 4];
+  __shared__ unsigned long long g0s;
+  __shared__ uint32_t span;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (uint32_t x = tid; x < kVoteWin * 4; x += kVoteThreads) win[x] = 0;
+  const uint64_t nchunks = (n + kVoteChunk - 1) / kVoteChunk;
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint64_t k0 = c * kVoteChunk, k1 = std::min<uint64_t>(n, k0 + kVoteChunk);
+    if (tid == 0) {
+      const AlnPair p = plc[k0];
+      const int64_t g = (int64_t)T.base_off[p.t] + p.off;
+      g0s = g < 0 ? 0ull : (unsigned long long)g;
+      span = 0;
+    }
+    __syncthreads();  // also orders the previous chunk's window clear
+    const uint64_t g0 = g0s;
+    uint32_t myspan = 0;
+    for (uint64_t k = k0 + wave; k < k1; k += kVoteThreads / 64) {
+      const AlnPair p = plc[k];
+      const uint32_t L = (uint32_t)(R.base_off[p.s + 1] - R.base_off[p.s]);
+      const uint32_t Lt = (uint32_t)(T.base_off[p.t + 1] - T.base_off[p.t]);
+      const uint8_t* rd = R.packed + R.byte_off[p.s];
+      const uint8_t* q = R.quals + R.base_off[p.s];
+      const bool rc = p.flags & 1;
+      const uint64_t tb = T.base_off[p.t];
+      const int64_t lo = std::max<int64_t>(0, -(int64_t)p.off);
+      const int64_t hi = std::min<int64_t>((int64_t)L, (int64_t)Lt - p.off);
+      for (int64_t i = lo + lane; i < hi; i += 64) {
+        const uint32_t b = rc ? 3 - abase(rd, (uint32_t)(L - 1 - i)) : abase(rd, (uint32_t)i);
+        const uint32_t qq = rc ? q[L - 1 - i] : q[i];
+        if (!qq) continue;
+        const uint64_t col = tb + (uint64_t)(i + p.off);
+        const uint64_t d = col - g0;  // wraps (huge) when col < g0
+        if (d < kVoteWin) {
+          atomicAdd(&win[d * 4 + b], qq);
+          myspan = std::max<uint32_t>(myspan, (uint32_t)d + 1);
+        } else {
+          atomicAdd(&votes[col * 4 + b], qq);
+        }
+      }
+    }
+    if (myspan) atomicMax(&span, myspan);
+    __syncthreads();
+    const uint32_t sp = span;
+    for (uint32_t x = tid; x < sp * 4; x += kVoteThreads) {
+      const uint32_t v = win[x];
+      if (v) {
+        atomicAdd(&votes[g0 * 4 + x], v);
+        win[x] = 0;
+      }
     }
   }
 }
@@ -697,8 +747,8 @@ int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T, co
   APG_CHECK_HIP(hipMemsetAsync(votes, 0, std::max<uint64_t>(4 * NT, 4) * 4, ctx->stream));
   kbegin(ctx, "consensus_votes", n * 16 + R->n_bytes + R->n_bases);
   if (n)
-    k_votes<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(seqset(R), seqset(T), reinterpret_cast<const AlnPair*>(d_plc), n,
-                                                        votes);
+    k_votes<<<resident_grid(ctx, k_votes, kVoteThreads, (n + kVoteChunk - 1) / kVoteChunk), kVoteThreads, 0,
+              ctx->stream>>>(seqset(R), seqset(T), reinterpret_cast<const AlnPair*>(d_plc), n, votes);
   kend(ctx);
   kbegin(ctx, "consensus_decide", NT * 18);
   if (NT)

@@ -163,6 +163,7 @@ int apg_trim(apg_ctx* ctx) {
   ctx->pc_ext_valid = false;
   ctx->clean_valid = false;
   ctx->solid_valid = false;
+  ctx->gstate.valid = false;
   return APG_OK;
 }
 
@@ -288,6 +289,21 @@ void apg_reads_free(apg_dreads* d) {
 }
 
 uint64_t apg_dreads_count(const apg_dreads* d) { return d ? d->n_reads : 0; }
+
+int apg_dreads_shape(apg_ctx* ctx, const apg_dreads* d, uint64_t* n_reads, uint64_t* n_bases, uint64_t* n_bytes,
+                     uint64_t* base_off, uint64_t* byte_off) {
+  APG_REQUIRE(ctx && d, "apg_dreads_shape: NULL argument");
+  if (n_reads) *n_reads = d->n_reads;
+  if (n_bases) *n_bases = d->n_bases;
+  if (n_bytes) *n_bytes = d->n_bytes;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  if (base_off)
+    APG_CHECK_HIP(hipMemcpyAsync(base_off, d->d_base_off, (d->n_reads + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (byte_off)
+    APG_CHECK_HIP(hipMemcpyAsync(byte_off, d->d_byte_off, (d->n_reads + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  return APG_OK;
+}
 
 int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
   APG_REQUIRE(ctx && dst && src, "apg_reads_copy_dev: NULL argument");

@@ -130,6 +130,18 @@ struct apg_ctx {
     uint64_t total = 0;
   } skstate;
 
+  // Device graph of the last unipath build ("u_*" workspaces + the node
+  // array it indexed), for apg_unipath_locs / apg_unibases_dev.
+  struct GState {
+    bool valid = false;
+    int K = 0;
+    uint64_t n_nodes = 0, n_unipaths = 0, tmask = 0;
+    const void* nodes = nullptr;  // KRec[n_nodes]
+    const uint32_t *idx = nullptr, *head = nullptr, *rank = nullptr, *uoh = nullptr;
+    const uint64_t *ulen = nullptr, *urc = nullptr, *ub_off = nullptr;
+    const uint8_t* ub = nullptr;  // unibases, one base per byte
+  } gstate;
+
   // Solid K-mer list of the last apg_shard_solid ("pc_solid" workspace).
   uint64_t n_solid = 0;
   bool solid_valid = false;

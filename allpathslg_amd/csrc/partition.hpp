@@ -69,4 +69,9 @@ template <typename R>
 int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag);
 
+// Stable LSD radix sort of (key, val) pairs by key over the key's significant
+// bits (pathsdb.hip): ping-pongs between (k, v) and (k2, v2); *in2 tells
+// which pair holds the result.
+int sort_u64_u32(apg_ctx* ctx, uint64_t* k, uint32_t* v, uint64_t* k2, uint32_t* v2, uint64_t n, bool* in2);
+
 }  // namespace apg

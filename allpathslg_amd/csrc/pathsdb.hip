@@ -101,7 +101,7 @@ __global__ void k_rs_or(const uint64_t* __restrict__ key, uint64_t n, unsigned l
 
 // Stable sort of (key, val) by key: ping-pongs between (k, v) and (k2, v2);
 // returns which pair holds the result (false: k/v, true: k2/v2).
-static int sort_u64_u32(apg_ctx* ctx, uint64_t* k, uint32_t* v, uint64_t* k2, uint32_t* v2, uint64_t n, bool* in2) {
+int sort_u64_u32(apg_ctx* ctx, uint64_t* k, uint32_t* v, uint64_t* k2, uint32_t* v2, uint64_t n, bool* in2) {
   *in2 = false;
   if (n <= 1) return APG_OK;
   unsigned long long* orv = nullptr;

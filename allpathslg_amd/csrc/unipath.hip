@@ -1607,6 +1607,7 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   const int K = prm.K;
   const KeyP kp = make_keyp(K);
   st->n_nodes = N;
+  ctx->gstate.valid = false;
   if (N >= (1ull << 31)) {
     set_error("unipaths: more than 2^31 distinct K-mers on one device");
     return APG_E_UNSUPPORTED;
@@ -1861,6 +1862,23 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     APG_TRY(d2h_u64(ctx, gs + 26, &ml, 1));
     st->max_len = ml;
   }
+  {
+    apg_ctx::GState& g = ctx->gstate;
+    g.K = K;
+    g.n_nodes = N;
+    g.n_unipaths = U;
+    g.tmask = T - 1;
+    g.nodes = nodes;
+    g.idx = idx;
+    g.head = head;
+    g.rank = rank;
+    g.uoh = uni_of_head;
+    g.ulen = ulen;
+    g.urc = urc;
+    g.ub_off = ub_off;
+    g.ub = ub;
+    g.valid = true;
+  }
   if (!out) return APG_OK;
 
   // ---- host copies ------------------------------------------------------------
@@ -2109,6 +2127,7 @@ int apg_ushard_bins(int n_shards) {
 
 int apg_ushard_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* counts,
                      uint64_t* n_instances) {
+  if (ctx) ctx->gstate.valid = false;  // may overwrite the node array of the last graph
   APG_REQUIRE(ctx && reads && counts, "apg_ushard_count: NULL argument");
   APG_TRY(ushard_check(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
@@ -2152,6 +2171,7 @@ int apg_ushard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shard
 
 int apg_ushard_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                      uint64_t* n_nodes) {
+  if (ctx) ctx->gstate.valid = false;  // may overwrite the node array of the last graph
   APG_REQUIRE(ctx && recv_counts && n_nodes, "apg_ushard_nodes: NULL argument");
   APG_TRY(ushard_check(K, n_shards));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
@@ -2200,6 +2220,293 @@ int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes,
   if (rc != APG_OK && out) apg_unipath_graph_free(out);
   if (stats) *stats = st;
   return rc;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// UnipathLocs (apg_unipath_locs, spec in include/apg.h; CPU restatement
+// oracle/locs_oracle.c).  Recalled reference [R:M]: BuildUnipathLocs /
+// ReadLocationLG (src/paths/UnipathLocs*), grep target only.
+//
+//   k_ulocs<false>  thread per read: roll the read's K-mers (read
+//                   orientation), one node-index lookup each (a 100-bp read
+//                   has 5 96-mers, so a lookup per K-mer is cheaper than
+//                   verifying unipath runs), count the (u, s) changes
+//   scan            per-read location offsets
+//   k_ulocs<true>   the same walk, writing 16-byte locations (+ rc mirrors)
+//   sort (flag)     key (u << 32 | s + 2^31), payload = location index,
+//                   stable LSD radix (pathsdb.hip) -> gather
+// ---------------------------------------------------------------------------
+namespace apg {
+
+struct ULoc {  // == apg_aln_pair
+  uint32_t read, unipath;
+  int32_t start;
+  uint32_t flags;
+};
+
+struct GView {
+  NodeIdx ni;
+  const uint32_t *head, *rank, *uoh;
+  const uint64_t *ulen, *urc;
+};
+
+template <bool WRITE>
+__global__ void __launch_bounds__(256) k_ulocs(ReadsV rv, GView g, KeyP kp, uint32_t flags,
+                                               uint32_t* __restrict__ nloc, const uint64_t* __restrict__ loff,
+                                               ULoc* __restrict__ out, unsigned long long* __restrict__ cnt) {
+  const uint32_t per = (flags & APG_ULOCS_RC) ? 2u : 1u;
+  uint64_t missing = 0, placed = 0, lookups = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+    uint32_t k = 0;
+    const uint64_t o = WRITE ? loff[r] : 0;
+    if (len >= (uint32_t)kp.K) {
+      const uint32_t nk = len - kp.K + 1;
+      Roller3 ro;
+      ro.init(rv.packed + rv.byte_off[r], len, kp);
+      uint32_t pu = 0xffffffffu;
+      int64_t ps = 0;
+      lookups += nk;
+      for (uint32_t j = 0; j < nk; ++j) {
+        ro.step(kp);
+        const uint32_t v = directed_of(g.ni, ro.fw, kp);
+        if (v == kNone) {
+          ++missing;
+          continue;
+        }
+        const uint32_t u = g.uoh[g.head[v]];
+        const int64_t st = (int64_t)g.rank[v] - (int64_t)j;
+        if (u == pu && st == ps) continue;
+        pu = u;
+        ps = st;
+        if (WRITE) {
+          out[o + k] = ULoc{(uint32_t)r, u, (int32_t)st, 0u};
+          if (per == 2) {
+            const int64_t ulb = (int64_t)g.ulen[u] + kp.K - 1;
+            out[o + k + 1] = ULoc{(uint32_t)r, (uint32_t)g.urc[u], (int32_t)(ulb - (st + (int64_t)len)), APG_ALN_RC};
+          }
+        }
+        k += per;
+      }
+    }
+    placed += k != 0;
+    if (!WRITE) nloc[r] = k;
+  }
+  if (!WRITE) {
+    wave_add(&cnt[0], missing);
+    wave_add(&cnt[1], placed);
+    wave_add(&cnt[2], lookups);
+  }
+}
+
+__global__ void k_ulocs_keys(const ULoc* __restrict__ loc, uint64_t n, uint64_t* __restrict__ key,
+                             uint32_t* __restrict__ val) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const ULoc x = loc[i];
+    key[i] = ((uint64_t)x.unipath << 32) | (uint32_t)((int64_t)x.start + (1ll << 31));
+    val[i] = (uint32_t)i;
+  }
+}
+
+__global__ void k_ulocs_gather(const ULoc* __restrict__ loc, const uint32_t* __restrict__ perm, uint64_t n,
+                               ULoc* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = loc[perm[i]];
+}
+
+// unibases (one base per byte) -> 2-bit packed reads, one byte-aligned read
+// per unipath: thread per output byte.
+__global__ void k_pack_unibases(const uint8_t* __restrict__ ub, const uint64_t* __restrict__ ub_off, uint64_t U,
+                                const uint64_t* __restrict__ byte_off, uint8_t* __restrict__ packed) {
+  const uint64_t nby = byte_off[U];
+  for (uint64_t y = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; y < nby; y += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t lo = 0, hi = U;  // unipath of byte y: largest u with byte_off[u] <= y
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (byte_off[mid] <= y)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const uint64_t b0 = ub_off[lo] + (y - byte_off[lo]) * 4, e = ub_off[lo + 1];
+    uint8_t x = 0;
+    for (int t = 0; t < 4; ++t)
+      if (b0 + t < e) x |= (uint8_t)((ub[b0 + t] & 3) << (2 * t));
+    packed[y] = x;
+  }
+}
+
+__global__ void k_ub_byte_lens(const uint64_t* __restrict__ ub_off, uint64_t U, uint32_t* __restrict__ nby) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x)
+    nby[u] = (uint32_t)((ub_off[u + 1] - ub_off[u] + 3) / 4);
+}
+
+static int ulocs_run(apg_ctx* ctx, const apg_dreads* dr, uint32_t flags, const ULoc** d_out, uint64_t* n_out,
+                     apg_uloc_stats* st) {
+  const apg_ctx::GState& gs = ctx->gstate;
+  APG_REQUIRE(gs.valid, "apg_unipath_locs: no unipath graph in this context (run apg_unipaths first)");
+  APG_REQUIRE((flags & ~(APG_ULOCS_RC | APG_ULOCS_SORTED)) == 0, "apg_unipath_locs: unknown flags");
+  APG_REQUIRE(dr->n_reads < (1ull << 32), "apg_unipath_locs: more than 2^32 reads");
+  APG_REQUIRE(dr->max_len < (1ull << 30), "apg_unipath_locs: read longer than 2^30 bases");
+  const KeyP kp = make_keyp(gs.K);
+  const GView g{NodeIdx{static_cast<const KRec*>(gs.nodes), gs.idx, gs.tmask}, gs.head, gs.rank, gs.uoh, gs.ulen,
+                gs.urc};
+  const ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  const uint64_t R = dr->n_reads;
+  uint32_t* nloc = nullptr;
+  uint64_t* loff = nullptr;
+  unsigned long long* cnt = nullptr;
+  APG_TRY(workspace_t(ctx, "ul_n", std::max<uint64_t>(R, 1), &nloc));
+  APG_TRY(workspace_t(ctx, "ul_off", R + 1, &loff));
+  APG_TRY(workspace_t(ctx, "ul_cnt", 3, &cnt));
+  APG_CHECK_HIP(hipMemsetAsync(cnt, 0, 24, ctx->stream));
+  const uint32_t grid = grid_for(ctx, R);
+  // algorithmic bytes: packed reads + offsets + per-read count, and one
+  // random 64-byte index line per K-mer lookup (added once counted)
+  kbegin(ctx, "ulocs_count", dr->n_bytes + 20 * R);
+  if (R) k_ulocs<false><<<grid, 256, 0, ctx->stream>>>(rv, g, kp, flags, nloc, nullptr, nullptr, cnt);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, nloc, R, loff, "ul"));
+  uint64_t NL = 0;
+  unsigned long long hc[3] = {0, 0, 0};
+  APG_CHECK_HIP(hipMemcpyAsync(&NL, loff + R, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(hc, cnt, 24, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  const uint64_t nk = hc[2];
+  kbytes_add(ctx, "ulocs_count", nk * 64);
+  APG_REQUIRE(NL < (1ull << 32), "apg_unipath_locs: more than 2^32 locations");
+  ULoc* loc = nullptr;
+  APG_TRY(workspace_t(ctx, "ul_loc", std::max<uint64_t>(NL, 1), &loc));
+  kbegin(ctx, "ulocs_write", dr->n_bytes + 16 * R + nk * 64 + NL * sizeof(ULoc));
+  if (R) k_ulocs<true><<<grid, 256, 0, ctx->stream>>>(rv, g, kp, flags, nullptr, loff, loc, cnt);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  const ULoc* res = loc;
+  if ((flags & APG_ULOCS_SORTED) && NL > 1) {
+    uint64_t *k1 = nullptr, *k2 = nullptr;
+    uint32_t *v1 = nullptr, *v2 = nullptr;
+    ULoc* sorted = nullptr;
+    APG_TRY(workspace_t(ctx, "ul_k1", NL, &k1));
+    APG_TRY(workspace_t(ctx, "ul_k2", NL, &k2));
+    APG_TRY(workspace_t(ctx, "ul_v1", NL, &v1));
+    APG_TRY(workspace_t(ctx, "ul_v2", NL, &v2));
+    APG_TRY(workspace_t(ctx, "ul_sorted", NL, &sorted));
+    k_ulocs_keys<<<grid_for(ctx, NL), 256, 0, ctx->stream>>>(loc, NL, k1, v1);
+    bool in2 = false;
+    kbegin(ctx, "ulocs_sort", NL * 24);
+    APG_TRY(sort_u64_u32(ctx, k1, v1, k2, v2, NL, &in2));
+    kend(ctx);
+    k_ulocs_gather<<<grid_for(ctx, NL), 256, 0, ctx->stream>>>(loc, in2 ? v2 : v1, NL, sorted);
+    APG_CHECK_HIP(hipGetLastError());
+    res = sorted;
+  }
+  APG_TRY(sync(ctx));
+  *d_out = res;
+  *n_out = NL;
+  if (st) {
+    st->n_reads = R;
+    st->n_placed = hc[1];
+    st->n_locs = NL;
+    st->n_missing = hc[0];
+  }
+  return APG_OK;
+}
+
+}  // namespace apg
+
+extern "C" {
+
+int apg_unipath_locs_dev(apg_ctx* ctx, const apg_dreads* reads, uint32_t flags, const apg_aln_pair** d_locs,
+                         uint64_t* n_locs, apg_uloc_stats* stats) {
+  APG_REQUIRE(ctx && reads && d_locs && n_locs, "apg_unipath_locs_dev: NULL argument");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const ULoc* p = nullptr;
+  APG_TRY(ulocs_run(ctx, reads, flags, &p, n_locs, stats));
+  *d_locs = reinterpret_cast<const apg_aln_pair*>(p);
+  return APG_OK;
+}
+
+int apg_unipath_locs(apg_ctx* ctx, const apg_reads* reads, uint32_t flags, apg_aln_pair** locs, uint64_t* n_locs,
+                     apg_uloc_stats* stats) {
+  APG_REQUIRE(ctx && reads && locs && n_locs, "apg_unipath_locs: NULL argument");
+  *locs = nullptr;
+  *n_locs = 0;
+  apg_dreads* d = nullptr;
+  APG_TRY(apg_reads_upload(ctx, reads, &d));
+  const ULoc* p = nullptr;
+  uint64_t n = 0;
+  int rc = ulocs_run(ctx, d, flags, &p, &n, stats);
+  if (rc == APG_OK) {
+    auto* h = static_cast<apg_aln_pair*>(std::malloc(std::max<uint64_t>(n, 1) * sizeof(apg_aln_pair)));
+    if (!h) {
+      rc = APG_E_NOMEM;
+    } else if (n && hipMemcpy(h, p, n * sizeof(apg_aln_pair), hipMemcpyDeviceToHost) != hipSuccess) {
+      std::free(h);
+      set_error("apg_unipath_locs: device-to-host copy failed");
+      rc = APG_E_HIP;
+    } else {
+      *locs = h;
+      *n_locs = n;
+    }
+  }
+  apg_reads_free(d);
+  return rc;
+}
+
+int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out) {
+  APG_REQUIRE(ctx && out, "apg_unibases_dev: NULL argument");
+  *out = nullptr;
+  const apg_ctx::GState& gs = ctx->gstate;
+  APG_REQUIRE(gs.valid, "apg_unibases_dev: no unipath graph in this context (run apg_unipaths first)");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const uint64_t U = gs.n_unipaths;
+  std::vector<uint64_t> hoff(U + 1, 0);
+  if (U) APG_CHECK_HIP(hipMemcpyAsync(hoff.data(), gs.ub_off, (U + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  std::vector<uint64_t> hby(U + 1, 0);
+  APG_TRY(apg_byte_offsets(hoff.data(), U, hby.data()));
+  apg_reads hr;
+  std::memset(&hr, 0, sizeof hr);
+  hr.n_reads = 0;  // shape only: the data is produced on the device below
+  apg_dreads* d = nullptr;
+  APG_TRY(apg_reads_upload(ctx, &hr, &d));
+  hipError_t e = hipSuccess;
+  auto fail = [&](const char* what) {
+    set_error(std::string("apg_unibases_dev: ") + what + ": " + hipGetErrorString(e));
+    apg_reads_free(d);
+    return APG_E_HIP;
+  };
+  (void)hipFree(d->d_base_off);
+  (void)hipFree(d->d_byte_off);
+  (void)hipFree(d->d_packed);
+  d->d_base_off = d->d_byte_off = nullptr;
+  d->d_packed = nullptr;
+  d->n_reads = U;
+  d->h_base_off = hoff;
+  d->n_bases = hoff[U];
+  d->n_bytes = hby[U];
+  for (uint64_t u = 0; u < U; ++u) d->max_len = std::max<uint64_t>(d->max_len, hoff[u + 1] - hoff[u]);
+  if ((e = hipMalloc(&d->d_base_off, (U + 1) * 8)) != hipSuccess) return fail("alloc");
+  if ((e = hipMalloc(&d->d_byte_off, (U + 1) * 8)) != hipSuccess) return fail("alloc");
+  if ((e = hipMalloc(&d->d_packed, d->n_bytes + 64)) != hipSuccess) return fail("alloc");
+  if ((e = hipMemsetAsync(d->d_packed, 0, d->n_bytes + 64, ctx->stream)) != hipSuccess) return fail("memset");
+  if ((e = hipMemcpyAsync(d->d_base_off, gs.ub_off, (U + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream)) != hipSuccess)
+    return fail("copy");
+  if ((e = hipMemcpyAsync(d->d_byte_off, hby.data(), (U + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    return fail("copy");
+  kbegin(ctx, "unibases_pack", d->n_bases + d->n_bytes);
+  if (d->n_bytes)
+    k_pack_unibases<<<grid_for(ctx, d->n_bytes), 256, 0, ctx->stream>>>(gs.ub, d->d_base_off, U, d->d_byte_off,
+                                                                        d->d_packed);
+  kend(ctx);
+  if ((e = hipGetLastError()) != hipSuccess) return fail("pack");
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail("sync");
+  *out = d;
+  return APG_OK;
 }
 
 }  // extern "C"

@@ -216,6 +216,15 @@ class Context:
 
     def download(self, dreads: DeviceReads) -> ReadSet:
         r = dreads.reads
+        if r is None:  # produced on the device: take the shape from the device set
+            n, nb, ny = C.c_uint64(), C.c_uint64(), C.c_uint64()
+            check(lib().apg_dreads_shape(self._h, dreads.handle, C.byref(n), C.byref(nb), C.byref(ny), None, None),
+                  "apg_dreads_shape")
+            bo = np.zeros(n.value + 1, dtype=np.uint64)
+            yo = np.zeros(n.value + 1, dtype=np.uint64)
+            check(lib().apg_dreads_shape(self._h, dreads.handle, None, None, None, bo.ctypes.data_as(_u64p),
+                                         yo.ctypes.data_as(_u64p)), "apg_dreads_shape")
+            r = ReadSet(bo, yo, np.zeros(max(int(ny.value), 1), dtype=np.uint8), None)
         pk = np.zeros_like(r.packed)
         q = np.zeros_like(r.quals) if r.quals is not None else None
         check(lib().apg_reads_download(self._h, dreads.handle, pk.ctypes.data_as(C.POINTER(C.c_uint8)),
@@ -306,6 +315,43 @@ class Context:
             return graph_arrays(g), st.as_dict()
         finally:
             L.apg_unipath_graph_free(C.byref(g))
+
+    def unipath_locs(self, reads, rc: bool = True, sorted: bool = True):
+        """UnipathLocs: placements of `reads` (host ReadSet or DeviceReads) on
+        the unipaths of this context's last unipath build (include/apg.h
+        apg_unipath_locs; [R:M] BuildUnipathLocs / ReadLocationLG).
+
+        Host reads -> ((n, 4) int32 [read, unipath, start, flags], stats).
+        DeviceReads -> (device pointer to n apg_aln_pair, n, stats); the
+        pointer is valid until the next unipath_locs call."""
+        from ._lib import APG_ULOCS_RC, APG_ULOCS_SORTED, apg_aln_pair, apg_uloc_stats
+
+        flags = (APG_ULOCS_RC if rc else 0) | (APG_ULOCS_SORTED if sorted else 0)
+        st = apg_uloc_stats()
+        n = C.c_uint64(0)
+        L = lib()
+        if isinstance(reads, DeviceReads):
+            p = C.c_void_p()
+            check(L.apg_unipath_locs_dev(self._h, reads.handle, flags, C.byref(p), C.byref(n), C.byref(st)),
+                  "apg_unipath_locs_dev")
+            return int(p.value or 0), int(n.value), st.as_dict()
+        r = reads.c_struct()
+        p = C.POINTER(apg_aln_pair)()
+        check(L.apg_unipath_locs(self._h, C.byref(r), flags, C.byref(p), C.byref(n), C.byref(st)),
+              "apg_unipath_locs")
+        try:
+            k = int(n.value)
+            buf = C.cast(p, C.POINTER(C.c_int32 * (4 * k))).contents if k else None
+            out = np.frombuffer(buf, dtype=np.int32).reshape(k, 4).copy() if k else np.zeros((0, 4), np.int32)
+        finally:
+            L.apg_free(p)
+        return out, st.as_dict()
+
+    def unibases_dev(self) -> "DeviceReads":
+        """The last build's unibases as a device read set (aligner targets)."""
+        d = DeviceReads(self, None)
+        check(lib().apg_unibases_dev(self._h, C.byref(d._h)), "apg_unibases_dev")
+        return d
 
     # -- sharded unipath stages (multi-GPU) -------------------------------------
     def ushard_count(self, dreads: DeviceReads, K: int, n_shards: int) -> Tuple[np.ndarray, int]:

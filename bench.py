@@ -66,6 +66,8 @@ def parse():
                    help="read placements of the aligner line (gap-free, banded SW, consensus); 0 = skip")
     p.add_argument("--align-band", type=int, default=8)
     p.add_argument("--align-target-len", type=int, default=50_000)
+    p.add_argument("--no-placement", dest="placement", action="store_false",
+                   help="skip the UnipathLocs line (reads placed on the step's unipaths + aligners)")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--sharded", action="store_true",
                    help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
@@ -184,6 +186,98 @@ def align_bench(ctx, genome, a, reps: int = 3):
     dS.free()
     dT.free()
     return out, (S, T, pairs)
+
+
+def placement_bench(ctx, dreads, a, reps: int = 3):
+    """UnipathLocs line: the step's corrected reads placed on
+    the step's K=96 unipaths (apg_unipath_locs_dev: one node-index lookup per
+    read K-mer, rc mirrors, stable by-unipath sort), then gap-free and column
+    consensus of those placements against the unibases (apg_unibases_dev),
+    all device-resident; per-kernel times from libapg's HIP events."""
+    ctx.reset_timing()
+    dT = ctx.unibases_dev()
+    p, n, st = ctx.unipath_locs(dreads, rc=True, sorted=True)
+    gf = torch.empty((max(n, 1), 4), dtype=torch.int32, device="cuda")
+    ub_host = ctx.download(dT)
+    nt = ub_host.n_bases
+    cb = torch.empty(max(nt, 1), dtype=torch.uint8, device="cuda")
+    cq = torch.empty(max(nt, 1), dtype=torch.uint8, device="cuda")
+
+    def run():
+        pp, nn, ss = ctx.unipath_locs(dreads, rc=True, sorted=True)
+        ctx.gapfree_dev(dreads, dT, pp, nn, gf.data_ptr())
+        ctx.consensus_dev(dreads, dT, pp, nn, cb.data_ptr(), cq.data_ptr())
+        return pp, nn, ss
+
+    run()
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        p, n, st = run()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    kt = ctx.kernel_times()
+    ms = {k: v[0] / max(v[1], 1) for k, v in kt.items()}
+    nb = {k: v[2] / max(v[1], 1) for k, v in kt.items()}
+    loc_ms = ms.get("ulocs_count", 0.0) + ms.get("ulocs_write", 0.0) + ms.get("ulocs_sort", 0.0)
+    gfh = gf[:n].cpu().numpy()
+    # unibase bases (host) vs consensus: the placed reads agree with the graph they built
+    tb = ((ub_host.packed[:, None] >> np.array([0, 2, 4, 6], dtype=np.uint8)) & 3).reshape(-1)
+    lens = ub_host.lengths().astype(np.int64)
+    starts = ub_host.byte_off[:-1].astype(np.int64) * 4
+    idx = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
+    tb = tb[idx]
+    cbh, cqh = cb[:nt].cpu().numpy(), cq[:nt].cpu().numpy()
+    voted = cqh > 0
+    dom = "ulocs_count" if ms.get("ulocs_count", 0) >= ms.get("ulocs_write", 0) else "ulocs_write"
+    out = {
+        "workload": (f"the step's {dreads.n_reads} corrected reads placed on its {dT.n_reads} K={a.K_unipath} "
+                     f"unipaths (+rc mirrors, sorted by unipath), gap-free + consensus on the unibases"),
+        "reads": dreads.n_reads,
+        "stats": st,
+        "wall_ms_per_pass": wall * 1e3,
+        "unipath_locs": {"ms": loc_ms, "reads_per_s": dreads.n_reads / max(loc_ms * 1e-3, 1e-12),
+                         "roofline": {"bound": "hbm", "kernel": dom,
+                                      "achieved": nb.get(dom, 0) / max(ms.get(dom, 0) * 1e-3, 1e-12) / 1e9,
+                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": nb.get(dom, 0) / max(ms.get(dom, 0) * 1e-3, 1e-12) / 1e9 / HBM_PEAK_GBS}},
+        "gapfree": {"ms": ms.get("gapfree", 0.0), "alignments_per_s": n / max(ms.get("gapfree", 0) * 1e-3, 1e-12)},
+        "consensus": {"ms": ms.get("consensus_votes", 0.0) + ms.get("consensus_decide", 0.0)},
+        "kernels_ms": ms,
+        "checks": {
+            "every_location_covers_a_kmer": bool((gfh[:, 0] >= a.K_unipath).all()) if n else True,
+            "mismatches_outside_the_kmer_only": bool((gfh[:, 1] <= 100 - a.K_unipath).all()) if n else True,
+            "most_reads_placed": st["n_placed"] > 0.5 * dreads.n_reads,
+            "consensus_equals_unibases_where_voted": float((cbh[voted] == tb[voted]).mean()) > 0.999,
+        },
+        "consensus_agreement": float((cbh[voted] == tb[voted]).mean()) if voted.any() else None,
+        "columns_voted": float(voted.mean()) if nt else None,
+    }
+    dT.free()
+    return out
+
+
+def placement_cpu_baseline(genome, a, n_reads: int = 100_000) -> dict:
+    """CPU baseline of the placement line: oracle/locs_oracle.c, one thread,
+    on a bounded sample — the graph of a 1 Mb piece of the bench genome (tiled
+    error-free 200-bp fragments) and 100-bp reads drawn from that piece."""
+    import oracle
+    from allpathslg_amd import ReadSet
+
+    piece = genome[:1_000_000]
+    frags = ReadSet.from_matrix(np.lib.stride_tricks.sliding_window_view(piece, 200)[::10].copy())
+    g = oracle.unipaths(frags, a.K_unipath)
+    rng = np.random.default_rng(a.seed + 11)
+    st = rng.integers(0, len(piece) - 100, n_reads)
+    reads = ReadSet.from_matrix(piece[st[:, None] + np.arange(100)[None, :]])
+    t = time.perf_counter()
+    oracle.unipath_locs(g, reads, a.K_unipath, rc=True, sorted=True)
+    t = time.perf_counter() - t
+    return {"value": n_reads / t, "unit": "reads/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/locs_oracle.c, single-threaded: {n_reads} error-free 100-bp reads on the "
+                       f"K={a.K_unipath} graph of the first 1 Mb of the bench genome ({t:.2f} s, incl. the "
+                       f"oracle's index build over the unibases)")}
 
 
 def align_cpu_baseline(S, T, pairs, band_w: int, n: int) -> dict:
@@ -411,6 +505,12 @@ def main():
             aligners["cpu_baseline"] = align_cpu_baseline(aS, aT, apairs, a.align_band, min(20_000, a.align_pairs))
         del aS, aT, apairs
 
+    placement = None
+    if rank == 0 and not sharded and not a.spectrum_only and a.placement:
+        placement = placement_bench(ctx, dreads, a)
+        if not a.no_cpu_baseline:
+            placement["cpu_baseline"] = placement_cpu_baseline(genome, a)
+
     if rank == 0:
         total_reads = world * reads.n_reads * a.steps
         out = {
@@ -450,6 +550,7 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu,
             "aligners": aligners,
+            "placement": placement,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},
             "precorrect_stats": pst,
             "fill_stats": fst,

@@ -89,6 +89,11 @@ typedef struct apg_dreads apg_dreads;
 int apg_reads_upload(apg_ctx* ctx, const apg_reads* reads, apg_dreads** out);
 void apg_reads_free(apg_dreads* dr);
 uint64_t apg_dreads_count(const apg_dreads* dr);
+/* Shape of a device read set (also one produced on the device, e.g. by     */
+/* apg_fill_fragments_dev or apg_unibases_dev): sizes, and the offsets       */
+/* copied to base_off / byte_off (n_reads + 1 each) when those are non-NULL. */
+int apg_dreads_shape(apg_ctx* ctx, const apg_dreads* dr, uint64_t* n_reads, uint64_t* n_bases,
+                     uint64_t* n_bytes, uint64_t* base_off, uint64_t* byte_off);
 /* Copy bases (and qualities) between two device read sets of the same shape
  * (same read lengths), on the context's stream.  Used to restore a corrected
  * read set to its uploaded state without a host round trip. */
@@ -479,6 +484,45 @@ int apg_consensus(apg_ctx* ctx, const apg_reads* R, const apg_reads* T, const ap
                   uint64_t n, uint8_t* bases, uint8_t* quals);
 int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T,
                       const apg_aln_pair* d_placements, uint64_t n, uint8_t* d_bases, uint8_t* d_quals);
+
+/* ------------------------------------------------------------------------- */
+/* UnipathLocs: placement of reads on the unipaths of the context's last     */
+/* unipath build (apg_unipaths / apg_unipaths_dev / apg_unipaths_from_nodes; */
+/* after the latter, the caller's node buffer must still be alive).          */
+/* Replaces BuildUnipathLocs / ReadLocationLG ([R:M] src/paths/UnipathLocs*, */
+/* grep target only: reference snapshot empty).  Spec [D]:                   */
+/*  - every K-mer j of read r (read orientation) found in the graph lies at   */
+/*    rank k of exactly one unipath u: the read is placed at start s = k - j */
+/*    (read base 0 faces unibase base s; s may be negative or run past the  */
+/*    end, as for reads hanging off a unipath end);                          */
+/*  - a location {s_id = r, t_id = u, offset = s, flags = 0} is emitted for  */
+/*    each K-mer whose (u, s) differs from the read's last emitted (u, s);   */
+/*    K-mers absent from the graph are skipped (counted in n_missing);       */
+/*  - APG_ULOCS_RC: each location is followed by its mirror on rc(u):       */
+/*    {r, rc(u), (len(u) + K - 1) - (s + L_r), APG_ALN_RC};                  */
+/*  - order: read order, emission order; APG_ULOCS_SORTED: stably sorted by  */
+/*    (t_id, offset) — the by-unipath index.                                 */
+/* Locations are apg_aln_pair placements: they feed apg_gapfree /            */
+/* apg_banded_sw / apg_consensus against the unibases (apg_unibases_dev).    */
+/* ------------------------------------------------------------------------- */
+#define APG_ULOCS_RC 1u
+#define APG_ULOCS_SORTED 2u
+typedef struct apg_uloc_stats {
+  uint64_t n_reads;
+  uint64_t n_placed;  /* reads with >= 1 location */
+  uint64_t n_locs;
+  uint64_t n_missing; /* read K-mers absent from the graph */
+} apg_uloc_stats;
+/* Host variant: *locs is malloc'd (release with apg_free). */
+int apg_unipath_locs(apg_ctx* ctx, const apg_reads* reads, uint32_t flags, apg_aln_pair** locs,
+                     uint64_t* n_locs, apg_uloc_stats* stats);
+/* Device variant: *d_locs points into a context workspace, valid until the  */
+/* next apg_unipath_locs* call or apg_trim. */
+int apg_unipath_locs_dev(apg_ctx* ctx, const apg_dreads* reads, uint32_t flags, const apg_aln_pair** d_locs,
+                         uint64_t* n_locs, apg_uloc_stats* stats);
+/* The last build's unibases as a new device read set (one read per unipath, */
+/* no qualities; release with apg_reads_free) — the aligners' targets. */
+int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out);
 
 /* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */

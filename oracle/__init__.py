@@ -418,3 +418,39 @@ def make_rc_db(g):
     arr = np.array([ent[i] for i in order], dtype=RPINT_DTYPE) if ent else np.zeros(0, RPINT_DTYPE)
     return {"rc_path_off": np.array(rc_off, np.uint64), "rc_start": np.array(rc_s, np.uint64),
             "rc_len": np.array(rc_l, np.uint64), "entries": arr}
+
+
+def unipath_locs(g: dict, reads, K: int = 96, rc: bool = True, sorted: bool = True):
+    """UnipathLocs restated (oracle/locs_oracle.c): placements of `reads` on
+    graph `g` (dict as returned by unipaths()).  Returns ((n, 4) int32
+    [read, unipath, start, flags], {"n_placed", "n_missing"})."""
+    L = lib()
+    if not hasattr(L, "_orl"):
+        L.orl_locs.restype = C.c_int
+        L.orl_locs.argtypes = [C.c_uint64, _u64p, _u64p, _u64p, _u8p, C.c_int, C.c_uint64, _u64p, _u64p, _u8p,
+                               C.c_uint32, C.POINTER(_u32p), _u64p, _u64p]
+        L._orl = True
+    U = int(g["n_unipaths"])
+    ulen = np.ascontiguousarray(g["len"], dtype=np.uint64)
+    urc = np.ascontiguousarray(g["rc"], dtype=np.uint64)
+    uoff = np.ascontiguousarray(g["ub_off"], dtype=np.uint64)
+    ub = np.ascontiguousarray(g["unibases"], dtype=np.uint8)
+    if ub.size == 0:
+        ub = np.zeros(1, np.uint8)
+    out = _u32p()
+    n = C.c_uint64(0)
+    stats = np.zeros(2, dtype=np.uint64)
+    flags = (1 if rc else 0) | (2 if sorted else 0)
+    rn, bo, yo, pk = _rp(reads)
+    rcode = L.orl_locs(U, ulen.ctypes.data_as(_u64p), urc.ctypes.data_as(_u64p), uoff.ctypes.data_as(_u64p),
+                       ub.ctypes.data_as(_u8p), K, rn, bo, yo, pk, flags, C.byref(out), C.byref(n),
+                       stats.ctypes.data_as(_u64p))
+    if rcode:
+        raise RuntimeError(f"oracle unipath_locs failed ({rcode})")
+    try:
+        k = int(n.value)
+        res = np.ctypeslib.as_array(out, shape=(4 * k,)).view(np.int32).reshape(k, 4).copy() if k else \
+            np.zeros((0, 4), np.int32)
+    finally:
+        L.ork_free(out)
+    return res, {"n_placed": int(stats[0]), "n_missing": int(stats[1])}

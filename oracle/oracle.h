@@ -34,4 +34,8 @@ void ora_consensus(const uint64_t* r_base_off, const uint64_t* r_byte_off, const
                    const uint8_t* t_packed, uint64_t n_targets, const uint32_t* plc, uint64_t n, uint8_t* cons,
                    uint8_t* cq);
 
+int orl_locs(uint64_t U, const uint64_t* ulen, const uint64_t* urc, const uint64_t* ub_off, const uint8_t* ub, int K,
+             uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
+             uint32_t flags, uint32_t** out, uint64_t* n_out, uint64_t* stats);
+
 #endif
