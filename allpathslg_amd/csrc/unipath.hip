@@ -2487,6 +2487,7 @@ int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out) {
   d->d_packed = nullptr;
   d->n_reads = U;
   d->h_base_off = hoff;
+  d->shape_hash = 0;
   d->n_bases = hoff[U];
   d->n_bytes = hby[U];
   for (uint64_t u = 0; u < U; ++u) d->max_len = std::max<uint64_t>(d->max_len, hoff[u + 1] - hoff[u]);
