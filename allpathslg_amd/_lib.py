@@ -88,6 +88,21 @@ class apg_pc_stats(C.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
 
 
+class apg_ecj_params(C.Structure):
+    _fields_ = [("K", C.c_int32), ("min_solid", C.c_uint32), ("max_q_suspect", C.c_uint32), ("min_keep", C.c_uint32),
+                ("reserved", C.c_uint64 * 4)]
+
+
+class apg_ecj_stats(C.Structure):
+    _fields_ = [("pc", apg_pc_stats), ("n_reads", C.c_uint64), ("n_full", C.c_uint64), ("n_trimmed", C.c_uint64),
+                ("n_dropped", C.c_uint64), ("bases_kept", C.c_uint64), ("reserved", C.c_uint64 * 3)]
+
+    def as_dict(self) -> dict:
+        d = {f: int(getattr(self, f)) for f, _ in self._fields_ if f not in ("pc", "reserved")}
+        d["precorrect"] = self.pc.as_dict()
+        return d
+
+
 APG_FILL_LAST_SOLID = 1
 FILL_STATUS = {0: "filled", 1: "none", 2: "ambiguous", 3: "budget", 4: "skip"}
 
@@ -316,6 +331,12 @@ SIGNATURES = {
     "apg_consensus": (
         C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64, _u8p, _u8p]),
     "apg_consensus_dev": (C.c_int, [_P, _P, _P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "apg_ecj_defaults": (None, [C.POINTER(apg_ecj_params)]),
+    "apg_error_correct_jump": (
+        C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_ecj_params), _u8p, _u8p,
+                  C.POINTER(C.c_uint32), C.POINTER(apg_ecj_stats)]),
+    "apg_error_correct_jump_dev": (
+        C.c_int, [_P, _P, _P, C.POINTER(apg_ecj_params), C.c_void_p, C.POINTER(apg_ecj_stats)]),
     "apg_unipath_locs": (
         C.c_int, [_P, C.POINTER(apg_reads), C.c_uint32, C.POINTER(C.POINTER(apg_aln_pair)), _u64p,
                   C.POINTER(apg_uloc_stats)]),

@@ -1007,11 +1007,153 @@ static int check_pc(const apg_pc_params& p) {
   return APG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// ErrorCorrectJump (spec in include/apg.h; CPU restatement oracle/ecj_oracle.c
+// + the PreCorrect restatement).  After the correction pass, k_ecj_trim finds
+// each read's first non-solid K-mer through the pass's (K-1)-mer extension
+// table: K-mer i is solid <=> the successor mask of the (K-1)-mer at i holds
+// base i+K-1, one table line per K-mer, stopping at the first miss.
+// ---------------------------------------------------------------------------
+struct EcjReads {
+  const uint64_t* base_off;
+  const uint64_t* byte_off;
+  const uint8_t* packed;
+  uint64_t n_reads;
+};
+
+__global__ void __launch_bounds__(256) k_ecj_trim(EcjReads rv, ExtTab et, int K, uint32_t min_keep,
+                                                  uint32_t* __restrict__ keep, unsigned long long* __restrict__ cnt) {
+  uint64_t n_full = 0, n_trim = 0, n_drop = 0, kept = 0, looks = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t L = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+    const uint8_t* rd = rv.packed + rv.byte_off[r];
+    uint32_t k = 0;
+    if (L >= (uint32_t)K) {
+      const int n1 = K - 1;
+      uint64_t y = 0;  // (K-1)-mer at i, LSB-first: base i+t at bits 2t
+      for (int t = 0; t < n1; ++t) y |= (uint64_t)((rd[t >> 2] >> (2 * (t & 3))) & 3) << (2 * t);
+      const uint32_t nk = L - K + 1;
+      uint32_t i = 0;
+      for (; i < nk; ++i) {
+        const uint32_t p = i + n1;
+        const uint32_t b = (rd[p >> 2] >> (2 * (p & 3))) & 3;
+        ++looks;
+        if (!((ext_masks_lsb(et, y) >> 4) & (1u << b))) break;
+        y = (y >> 2) | ((uint64_t)b << (2 * (n1 - 1)));
+      }
+      k = i == nk ? L : i + (uint32_t)n1;
+      if (k < min_keep) k = 0;
+    }
+    keep[r] = k;
+    n_full += k == L && L > 0;
+    n_trim += k && k < L;
+    n_drop += k == 0;
+    kept += k;
+  }
+  wave_add(&cnt[0], n_full);
+  wave_add(&cnt[1], n_trim);
+  wave_add(&cnt[2], n_drop);
+  wave_add(&cnt[3], kept);
+  wave_add(&cnt[4], looks);
+}
+
+static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg_ecj_params& e, uint32_t* d_keep,
+                   apg_ecj_stats* st) {
+  APG_REQUIRE(e.K >= 2 && e.K <= 29, "apg_error_correct_jump: K must be in [2, 29]");
+  APG_REQUIRE(e.min_solid >= 1, "apg_error_correct_jump: min_solid must be >= 1");
+  APG_REQUIRE(jr->n_reads == 0 || jr->d_quals, "apg_error_correct_jump: jump reads have no qualities");
+  APG_REQUIRE(jr->n_reads == 0 || d_keep, "apg_error_correct_jump: keep_len is NULL");
+  apg_pc_params p;
+  std::memset(&p, 0, sizeof p);
+  p.K = e.K;
+  p.min_solid = e.min_solid;
+  p.max_q_suspect = e.max_q_suspect;
+  p.n_cycles = 1;
+  // solid set of the fragment reads
+  SkResult sr;
+  APG_TRY(sk_spectrum(ctx, fr, e.K, true, e.min_solid, nullptr, 0, &sr));
+  ctx->solid_valid = false;  // "pc_solid" now holds the fragments' list
+  // one correction pass of the jump reads against it
+  std::memset(st, 0, sizeof *st);
+  APG_TRY(correct_pass(ctx, jr, p, sr.solid, sr.n_solid, &st->pc));
+  ExtTab et{};
+  if (ctx->pc_ext_valid && ctx->pc_list == sr.solid && ctx->pc_K == e.K)
+    et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(e.K - 1), (1ull << (2 * (e.K - 1))) - 1, e.K - 1};
+  else
+    APG_TRY(ext_build(ctx, sr.solid, sr.n_solid, e.K, "ecj_ext", "ecj_ext", &et));
+  unsigned long long* cnt = nullptr;
+  APG_TRY(workspace_t(ctx, "ecj_cnt", 5, &cnt));
+  APG_CHECK_HIP(hipMemsetAsync(cnt, 0, 5 * 8, ctx->stream));
+  kbegin(ctx, "ecj_trim", jr->n_bytes + 20 * jr->n_reads);
+  if (jr->n_reads)
+    k_ecj_trim<<<grid_for(ctx, jr->n_reads), 256, 0, ctx->stream>>>(
+        EcjReads{jr->d_base_off, jr->d_byte_off, jr->d_packed, jr->n_reads}, et, e.K, e.min_keep, d_keep, cnt);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long h[5];
+  APG_CHECK_HIP(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  kbytes_add(ctx, "ecj_trim", h[4] * 64);
+  st->n_reads = jr->n_reads;
+  st->n_full = h[0];
+  st->n_trimmed = h[1];
+  st->n_dropped = h[2];
+  st->bases_kept = h[3];
+  return APG_OK;
+}
+
 }  // namespace apg
 
 using namespace apg;
 
 extern "C" {
+
+void apg_ecj_defaults(apg_ecj_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->K = 24;
+  p->min_solid = 3;
+  p->max_q_suspect = 20;
+  p->min_keep = 40;
+}
+
+int apg_error_correct_jump_dev(apg_ctx* ctx, const apg_dreads* frags, apg_dreads* jumps, const apg_ecj_params* pp,
+                               uint32_t* d_keep_len, apg_ecj_stats* stats) {
+  APG_REQUIRE(ctx && frags && jumps, "apg_error_correct_jump_dev: NULL argument");
+  apg_ecj_params e;
+  if (pp)
+    e = *pp;
+  else
+    apg_ecj_defaults(&e);
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_ecj_stats st;
+  APG_TRY(ecj_run(ctx, frags, jumps, e, d_keep_len, &st));
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_error_correct_jump(apg_ctx* ctx, const apg_reads* frags, const apg_reads* jumps, const apg_ecj_params* p,
+                           uint8_t* out_packed, uint8_t* out_quals, uint32_t* keep_len, apg_ecj_stats* stats) {
+  APG_REQUIRE(ctx && frags && jumps, "apg_error_correct_jump: NULL argument");
+  APG_REQUIRE(jumps->n_reads == 0 || (out_packed && out_quals && keep_len && jumps->quals),
+              "apg_error_correct_jump: NULL output or jump qualities");
+  apg_dreads *dF = nullptr, *dJ = nullptr;
+  APG_TRY(apg_reads_upload(ctx, frags, &dF));
+  int rc = apg_reads_upload(ctx, jumps, &dJ);
+  uint32_t* dk = nullptr;
+  if (rc == APG_OK) rc = workspace_t(ctx, "ecj_keep", std::max<uint64_t>(jumps->n_reads, 1), &dk);
+  if (rc == APG_OK) rc = apg_error_correct_jump_dev(ctx, dF, dJ, p, dk, stats);
+  if (rc == APG_OK) rc = apg_reads_download(ctx, dJ, out_packed, out_quals);
+  if (rc == APG_OK && jumps->n_reads &&
+      hipMemcpy(keep_len, dk, jumps->n_reads * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("apg_error_correct_jump: D2H failed");
+    rc = APG_E_HIP;
+  }
+  apg_reads_free(dF);
+  apg_reads_free(dJ);
+  return rc;
+}
 
 void apg_pc_defaults(apg_pc_params* p) {
   if (!p) return;

@@ -316,6 +316,34 @@ class Context:
         finally:
             L.apg_unipath_graph_free(C.byref(g))
 
+    def error_correct_jump(self, frags, jumps, K: int = 24, min_solid: int = 3, max_q_suspect: int = 20,
+                           min_keep: int = 40, d_keep: Optional[int] = None):
+        """ErrorCorrectJump (include/apg.h apg_error_correct_jump; [R:M]
+        src/paths/ErrorCorrectJump.cc): correct `jumps` against the solid set of
+        `frags`, then trim each to its all-solid prefix.
+
+        Host ReadSets -> (corrected jumps ReadSet (untrimmed layout), keep u32[n],
+        stats).  DeviceReads (jumps corrected in place, keep lengths written to
+        the device buffer d_keep) -> stats."""
+        from ._lib import apg_ecj_params, apg_ecj_stats
+
+        p = apg_ecj_params()
+        lib().apg_ecj_defaults(C.byref(p))
+        p.K, p.min_solid, p.max_q_suspect, p.min_keep = K, min_solid, max_q_suspect, min_keep
+        st = apg_ecj_stats()
+        if isinstance(jumps, DeviceReads):
+            check(lib().apg_error_correct_jump_dev(self._h, frags.handle, jumps.handle, C.byref(p),
+                                                   C.c_void_p(d_keep), C.byref(st)), "apg_error_correct_jump_dev")
+            return st.as_dict()
+        f, j = frags.c_struct(), jumps.c_struct()
+        pk = np.zeros_like(jumps.packed)
+        q = np.zeros_like(jumps.quals)
+        keep = np.zeros(max(jumps.n_reads, 1), dtype=np.uint32)
+        check(lib().apg_error_correct_jump(self._h, C.byref(f), C.byref(j), C.byref(p), pk.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                           q.ctypes.data_as(C.POINTER(C.c_uint8)), keep.ctypes.data_as(_u32p),
+                                           C.byref(st)), "apg_error_correct_jump")
+        return ReadSet(jumps.base_off.copy(), jumps.byte_off.copy(), pk, q), keep[: jumps.n_reads], st.as_dict()
+
     def unipath_locs(self, reads, rc: bool = True, sorted: bool = True):
         """UnipathLocs: placements of `reads` (host ReadSet or DeviceReads) on
         the unipaths of this context's last unipath build (include/apg.h

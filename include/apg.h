@@ -486,6 +486,46 @@ int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T,
                       const apg_aln_pair* d_placements, uint64_t n, uint8_t* d_bases, uint8_t* d_quals);
 
 /* ------------------------------------------------------------------------- */
+/* ErrorCorrectJump ([R:M] src/paths/ErrorCorrectJump.cc, grep target only: */
+/* reference snapshot empty; semantics unpinned).  Spec [D]:                */
+/*  - the solid set is counted on the FRAGMENT reads (canonical K-mers with  */
+/*    count >= min_solid): a jump library's coverage is too low to count;    */
+/*  - one PreCorrect pass (SURVEY §A.4 rule) of the jump reads against it;   */
+/*  - trimming: each corrected jump read keeps its longest prefix whose      */
+/*    K-mers are all solid — keep = L if every K-mer is solid, else          */
+/*    j0 + K - 1 for the first non-solid K-mer j0; keep = 0 when L < K or    */
+/*    keep < min_keep (the read is dropped; pairs keep their indices).       */
+/* Bases and qualities are corrected in place; keep_len[r] gives the trim.   */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_ecj_params {
+  int32_t K;               /* default 24 */
+  uint32_t min_solid;      /* default 3 */
+  uint32_t max_q_suspect;  /* default 20 */
+  uint32_t min_keep;       /* default 40 */
+  uint64_t reserved[4];
+} apg_ecj_params;
+
+typedef struct apg_ecj_stats {
+  apg_pc_stats pc;      /* the correction pass of the jump reads */
+  uint64_t n_reads;
+  uint64_t n_full;      /* every K-mer solid: not trimmed */
+  uint64_t n_trimmed;   /* cut to a prefix >= min_keep */
+  uint64_t n_dropped;   /* keep = 0 */
+  uint64_t bases_kept;
+  uint64_t reserved[3];
+} apg_ecj_stats;
+
+void apg_ecj_defaults(apg_ecj_params* p);
+/* Host variant: frags / jumps in host memory; out_packed / out_quals sized  */
+/* like jumps (corrected, untrimmed layout), keep_len: one u32 per jump read. */
+int apg_error_correct_jump(apg_ctx* ctx, const apg_reads* frags, const apg_reads* jumps,
+                           const apg_ecj_params* p, uint8_t* out_packed, uint8_t* out_quals,
+                           uint32_t* keep_len, apg_ecj_stats* stats);
+/* Device variant: jumps corrected in place; d_keep_len device, n_reads u32. */
+int apg_error_correct_jump_dev(apg_ctx* ctx, const apg_dreads* frags, apg_dreads* jumps,
+                               const apg_ecj_params* p, uint32_t* d_keep_len, apg_ecj_stats* stats);
+
+/* ------------------------------------------------------------------------- */
 /* UnipathLocs: placement of reads on the unipaths of the context's last     */
 /* unipath build (apg_unipaths / apg_unipaths_dev / apg_unipaths_from_nodes; */
 /* after the latter, the caller's node buffer must still be alive).          */

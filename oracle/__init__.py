@@ -454,3 +454,20 @@ def unipath_locs(g: dict, reads, K: int = 96, rc: bool = True, sorted: bool = Tr
     finally:
         L.ork_free(out)
     return res, {"n_placed": int(stats[0]), "n_missing": int(stats[1])}
+
+
+def error_correct_jump(frags, jumps, K: int = 24, min_solid: int = 3, max_q: int = 20, min_keep: int = 40):
+    """ErrorCorrectJump restated: the fragment reads' solid set, one PreCorrect
+    pass of the jump reads against it, prefix trimming (oracle/ecj_oracle.c).
+    Returns (corrected jumps ReadSet (untrimmed layout), keep u32[n], pc stats)."""
+    L = lib()
+    if not hasattr(L, "_oje"):
+        L.oje_trim.restype = None
+        L.oje_trim.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, C.c_uint64, C.c_uint32, _u32p]
+        L._oje = True
+    solid = np.sort(solid_hashes(frags, K, min_solid)).astype(np.uint64)
+    fixed, st = precorrect_solid(jumps, solid, K, max_q)
+    keep = np.zeros(max(fixed.n_reads, 1), dtype=np.uint32)
+    n, bo, yo, pk = _rp(fixed)
+    L.oje_trim(n, bo, yo, pk, K, solid.ctypes.data_as(_u64p), len(solid), min_keep, keep.ctypes.data_as(_u32p))
+    return fixed, keep[: fixed.n_reads], st

@@ -83,3 +83,29 @@ def test_cli_pipeline_matches_oracle(tmp_path):
     assert np.array_equal(off, db["rc_path_off"]) and np.array_equal(st, db["rc_start"])
     raw = np.fromfile(tmp_path / "all_reads.pathsdb.k31", dtype=np.uint8)[48:]
     assert np.array_equal(raw, db["entries"].view(np.uint8))
+
+
+@pytest.mark.gpu
+def test_cli_error_correct_jump_matches_oracle(tmp_path):
+    """ErrorCorrectJump module: jump reads corrected against the frag reads'
+    solid set and written trimmed (one read per input read) = restatement."""
+    import oracle
+    from allpathslg_amd import ReadSet, synth_genome, synth_reads
+
+    g = synth_genome(100_000, 21)
+    frags = synth_reads(g, 20_000, seed=22)
+    jumps = synth_reads(g, 1_500, seed=23, insert_mean=3000, insert_sd=300)
+    frags.write_fastb(str(tmp_path / "frag_reads_edit.fastb"))
+    jumps.write_fastb(str(tmp_path / "jump_reads_filt.fastb"))
+    jumps.write_qualb(str(tmp_path / "jump_reads_filt.qualb"))
+    p = run("ErrorCorrectJump", f"RUN={tmp_path}", "K=24")
+    assert p.returncode == 0, p.stderr
+    out = ReadSet.load(str(tmp_path / "jump_reads_ec.fastb"), str(tmp_path / "jump_reads_ec.qualb"))
+    fixed, keep, _ = oracle.error_correct_jump(frags, jumps, K=24)
+    assert out.n_reads == jumps.n_reads
+    assert np.array_equal(out.lengths(), keep.astype(out.lengths().dtype))
+    for r in range(0, jumps.n_reads, 7):
+        k = int(keep[r])
+        assert np.array_equal(out.read(r), fixed.read(r)[:k])
+        assert np.array_equal(out.quals[int(out.base_off[r]) : int(out.base_off[r + 1])],
+                              fixed.quals[int(fixed.base_off[r]) : int(fixed.base_off[r]) + k])

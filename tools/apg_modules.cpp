@@ -1,6 +1,6 @@
 // apg_modules.cpp — drop-in command-line modules for RunAllPathsLG's hot
-// path: KmerSpectrum, PreCorrect, FindErrors, CommonPather,
-// Unipather, MakeRcDb.  Same module names and KEY=VALUE argument style as the
+// path: KmerSpectrum, PreCorrect, FindErrors, ErrorCorrectJump,
+// CommonPather, Unipather, MakeRcDb.  Same module names and KEY=VALUE argument style as the
 // reference modules ([R:H] ParsedArgs; PRE/DATA/RUN directories); inputs and
 // outputs are files in the RUN directory (APG v0 formats).
 // One binary, dispatched on the name it is invoked under (bin/<Module> are
@@ -149,6 +149,58 @@ int precorrect(Args& a, uint32_t default_cycles, const char* default_out) {
   return 0;
 }
 
+// ErrorCorrectJump: jump reads corrected against the fragment reads' solid
+// set and trimmed to their all-solid prefix; the output keeps one read per
+// input read (a dropped read has length 0) so pairs keep their indices.
+int error_correct_jump(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string fin = dir + "/" + a.get("FRAG_IN", "frag_reads_edit");
+  const std::string jin = dir + "/" + a.get("HEAD_IN", "jump_reads_filt");
+  const std::string out = dir + "/" + a.get("HEAD_OUT", "jump_reads_ec");
+  apg_ecj_params p;
+  apg_ecj_defaults(&p);
+  p.K = (int)a.num("K", p.K);
+  p.min_solid = (uint32_t)a.num("MIN_SOLID", p.min_solid);
+  p.max_q_suspect = (uint32_t)a.num("MAX_Q_SUSPECT", p.max_q_suspect);
+  p.min_keep = (uint32_t)a.num("MIN_KEEP", p.min_keep);
+  a.finish();
+  Reads fr, jr;
+  load_reads(a, fin, false, &fr);
+  load_reads(a, jin, true, &jr);
+  Ctx ctx(a);
+  const uint64_t n = jr.r.n_reads;
+  const uint64_t nbytes = n ? jr.r.byte_off[n] : 0, nbases = n ? jr.r.base_off[n] : 0;
+  std::vector<uint8_t> pk(nbytes + 64), q(nbases + 1);
+  std::vector<uint32_t> keep(n + 1);
+  apg_ecj_stats st;
+  a.check(apg_error_correct_jump(ctx.c, &fr.r, &jr.r, &p, pk.data(), q.data(), keep.data(), &st),
+          "apg_error_correct_jump");
+  // trimmed layout: read r = its first keep[r] bases
+  std::vector<uint64_t> bo(n + 1, 0), yo(n + 1, 0);
+  for (uint64_t r = 0; r < n; ++r) bo[r + 1] = bo[r] + keep[r];
+  a.check(apg_byte_offsets(bo.data(), n, yo.data()), "apg_byte_offsets");
+  std::vector<uint8_t> tp(yo[n] + 64, 0), tq(bo[n] + 1);
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint8_t* src = pk.data() + jr.r.byte_off[r];
+    std::memcpy(tp.data() + yo[r], src, (keep[r] + 3) / 4);
+    if (keep[r] % 4) tp[yo[r] + keep[r] / 4] &= (uint8_t)((1u << (2 * (keep[r] % 4))) - 1);
+    std::memcpy(tq.data() + bo[r], q.data() + jr.r.base_off[r], keep[r]);
+  }
+  apg_reads o{};
+  o.n_reads = n;
+  o.base_off = bo.data();
+  o.byte_off = yo.data();
+  o.packed = tp.data();
+  o.quals = tq.data();
+  a.check(apg_fastb_write((out + ".fastb").c_str(), &o), "writing .fastb");
+  a.check(apg_qualb_write((out + ".qualb").c_str(), &o), "writing .qualb");
+  std::printf("%s: %llu jump reads, %llu corrected, %llu whole, %llu trimmed, %llu dropped -> %s.{fastb,qualb}\n",
+              a.module.c_str(), (unsigned long long)n, (unsigned long long)st.pc.n_corrected,
+              (unsigned long long)st.n_full, (unsigned long long)st.n_trimmed, (unsigned long long)st.n_dropped,
+              out.c_str());
+  return 0;
+}
+
 int unipaths(Args& a, bool read_paths) {
   const std::string dir = a.run_dir();
   const std::string head = dir + "/" + a.get("READS", "all_reads");
@@ -205,7 +257,7 @@ int main(int argc, char** argv) {
   int first = 1;
   if (a.module == "apg_modules") {  // apg_modules <Module> KEY=VALUE ...
     if (argc < 2) {
-      std::fprintf(stderr, "usage: apg_modules <KmerSpectrum|PreCorrect|FindErrors|CommonPather|Unipather|MakeRcDb> "
+      std::fprintf(stderr, "usage: apg_modules <KmerSpectrum|PreCorrect|FindErrors|ErrorCorrectJump|CommonPather|Unipather|MakeRcDb> "
                            "KEY=VALUE ...\n");
       return 1;
     }
@@ -223,5 +275,6 @@ int main(int argc, char** argv) {
   if (a.module == "CommonPather") return unipaths(a, true);
   if (a.module == "Unipather") return unipaths(a, false);
   if (a.module == "MakeRcDb") return make_rc_db(a);
+  if (a.module == "ErrorCorrectJump") return error_correct_jump(a);
   a.fail("unknown module");
 }
