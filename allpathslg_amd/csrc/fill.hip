@@ -315,43 +315,57 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
 
 __device__ __forceinline__ uint32_t packed_base(const uint8_t* r, uint32_t i) { return (r[i >> 2] >> (2 * (i & 3))) & 3; }
 
+// Filled fragments out: kFillWLanes lanes per pair, lane l writes output
+// bytes l, l + kFillWLanes, ... (4 bases each), so a wave's stores cover
+// contiguous 16-byte runs of four fragments instead of 64 byte-by-byte
+// streams.  S = A ++ F[ov, Lf) (overlap closure) or A ++ path[0, d) ++ F
+// (gap closure, ov = 0), F = rc(B).
+constexpr uint32_t kFillWLanes = 16;
+
 __global__ void __launch_bounds__(256) k_fill_write(FillReads rv, const FillRec* __restrict__ rec,
                                                     const uint64_t* __restrict__ bscan,
                                                     const uint64_t* __restrict__ yscan,
                                                     const uint64_t* __restrict__ iscan, uint64_t* __restrict__ out_boff,
                                                     uint64_t* __restrict__ out_yoff, uint8_t* __restrict__ out) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rv.n_pairs;
-       i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint32_t lane = threadIdx.x % kFillWLanes;
+  const uint64_t groups = (uint64_t)gridDim.x * (blockDim.x / kFillWLanes);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / kFillWLanes) + threadIdx.x / kFillWLanes; i < rv.n_pairs;
+       i += groups) {
     const FillRec r = rec[i];
     if (!r.len) continue;
-    const uint64_t j = iscan[i];
-    out_boff[j] = bscan[i];
-    out_yoff[j] = yscan[i];
+    const uint64_t y0 = yscan[i];
+    if (lane == 0) {
+      const uint64_t j = iscan[i];
+      out_boff[j] = bscan[i];
+      out_yoff[j] = y0;
+    }
     const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
     const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
     const uint8_t* A = rv.packed + rv.byte_off[2 * i];
     const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
-    uint8_t* o = out + yscan[i];
+    uint8_t* o = out + y0;
     const uint32_t I = r.len;
     const unsigned __int128 pv = ((unsigned __int128)r.pv_hi << 64) | r.pv_lo;
     const uint32_t ov = r.meta >> 16, d = (r.meta >> 8) & 0xff;
-    // S = A ++ F[ov, Lf) (overlap) or A ++ path[0, d) ++ F (gap, ov = 0)
-    uint32_t t = 0;
-    for (; t + 4 <= La; t += 4) o[t >> 2] = A[t >> 2];  // A is byte-aligned like S
-    uint32_t acc = 0;
-    for (; t < I; ++t) {
-      uint32_t b;
-      if (t < La)
-        b = packed_base(A, t);
-      else if (t < La + d)
-        b = (uint32_t)(pv >> (2 * (d - 1 - (t - La)))) & 3;
-      else
-        b = 3 - packed_base(B, Lf - 1 - (t - La - d + ov));
-      acc |= b << (2 * (t & 3));
-      if ((t & 3) == 3 || t + 1 == I) {
-        o[t >> 2] = (uint8_t)acc;
-        acc = 0;
+    const uint32_t nby = (I + 3) / 4;
+    for (uint32_t y = lane; y < nby; y += kFillWLanes) {
+      const uint32_t t0 = 4 * y;
+      if (t0 + 4 <= La) {  // A is byte-aligned like S
+        o[y] = A[y];
+        continue;
       }
+      uint32_t acc = 0;
+      for (uint32_t t = t0; t < t0 + 4 && t < I; ++t) {
+        uint32_t b;
+        if (t < La)
+          b = packed_base(A, t);
+        else if (t < La + d)
+          b = (uint32_t)(pv >> (2 * (d - 1 - (t - La)))) & 3;
+        else
+          b = 3 - packed_base(B, Lf - 1 - (t - La - d + ov));
+        acc |= b << (2 * (t & 3));
+      }
+      o[y] = (uint8_t)acc;
     }
   }
 }
@@ -490,8 +504,9 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   fd->max_len = nf ? p.max_insert : 0;
   kbegin(ctx, "fill_write", np * (sizeof(FillRec) + 24) + tot[1] + nf * 16);
   if (np)
-    k_fill_write<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, rec, bscan, yscan, iscan, fd->d_base_off,
-                                                              fd->d_byte_off, fd->d_packed);
+    k_fill_write<<<grid_for(ctx, np, 256 / kFillWLanes), 256, 0, ctx->stream>>>(rv, rec, bscan, yscan, iscan,
+                                                                                 fd->d_base_off, fd->d_byte_off,
+                                                                                 fd->d_packed);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   APG_CHECK_HIP(hipMemcpyAsync(fd->d_base_off + nf, bscan + np, 8, hipMemcpyDeviceToDevice, ctx->stream));
