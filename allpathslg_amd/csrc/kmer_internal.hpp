@@ -44,6 +44,11 @@ struct SkResult {
 int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
              std::vector<uint64_t>* kmer_counts);
 int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
+// sk_scatter + pos[i] = global base position of record i's first K-mer
+int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos);
+// solid set of received records + per-record weak masks (receive order)
+int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
+                        int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res);
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
                    uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
                    SkResult* res);

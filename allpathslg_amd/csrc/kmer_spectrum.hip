@@ -840,6 +840,14 @@ int apg_shard_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards
   return sync(ctx);
 }
 
+int apg_shard_scatter_pos(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, void* d_send, void* d_pos) {
+  APG_REQUIRE(ctx && reads, "apg_shard_scatter_pos: NULL argument");
+  APG_TRY(check_shards(K, n_shards));
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_TRY(sk_scatter_pos(ctx, reads, K, n_shards, static_cast<SK16*>(d_send), static_cast<uint64_t*>(d_pos)));
+  return sync(ctx);
+}
+
 int apg_shard_spectrum(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                        uint64_t* hist, size_t hist_len, apg_kstats* stats) {
   APG_REQUIRE(ctx && recv_counts, "apg_shard_spectrum: NULL argument");

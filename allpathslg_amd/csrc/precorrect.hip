@@ -1007,6 +1007,21 @@ static int check_pc(const apg_pc_params& p) {
   return APG_OK;
 }
 
+// Multi-GPU weak-mask return, source side: every sent record whose owner
+// reported weak K-mers ORs its mask into the per-base weak bitmap at the
+// record's position (masks come back in send order).
+__global__ void k_weak_apply(const uint64_t* __restrict__ pos, const uint32_t* __restrict__ mask, uint64_t n,
+                             unsigned long long* __restrict__ weak) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t m = mask[i];
+    if (!m) continue;
+    const uint64_t b = pos[i];
+    const uint32_t sh = (uint32_t)(b & 63);
+    atomicOr(&weak[b >> 6], (unsigned long long)(m << sh));
+    if (sh && (m >> (64 - sh))) atomicOr(&weak[(b >> 6) + 1], (unsigned long long)(m >> (64 - sh)));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // ErrorCorrectJump (spec in include/apg.h; CPU restatement oracle/ecj_oracle.c
 // + the PreCorrect restatement).  After the correction pass, k_ecj_trim finds
@@ -1204,6 +1219,62 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
   ctx->n_solid = ns;
   ctx->solid_valid = true;
   *n_solid = ns;
+  return APG_OK;
+}
+
+int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+                         uint32_t min_solid, void* d_mask, uint64_t* n_solid) {
+  APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid_weak: NULL argument");
+  APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
+  ctx->solid_valid = false;
+  APG_REQUIRE(K >= 9 && K <= 29 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
+              "apg_shard_solid_weak: K must be in [9, 29], n_shards a power of two <= 8");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)n_shards * kSkShardBins);
+  uint64_t n = 0;
+  for (auto c : rc) n += c;
+  APG_REQUIRE(n == 0 || (d_recv && d_mask), "apg_shard_solid_weak: d_recv or d_mask is NULL");
+  const SK16* recs = static_cast<const SK16*>(d_recv);
+  int err = APG_OK;
+  const uint64_t nk = sk_sum_kmers(ctx, recs, n, &err);
+  APG_TRY(err);
+  SkResult sr;
+  APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr));
+  APG_TRY(sync(ctx));
+  ctx->n_solid = sr.n_solid;
+  ctx->solid_valid = true;
+  *n_solid = sr.n_solid;
+  return APG_OK;
+}
+
+int apg_precorrect_weak(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, const void* d_solid, uint64_t n_solid,
+                        const void* d_pos, const void* d_mask, uint64_t n_rec, apg_pc_stats* stats) {
+  APG_REQUIRE(ctx && dr, "apg_precorrect_weak: NULL argument");
+  APG_REQUIRE(n_solid == 0 || d_solid, "apg_precorrect_weak: d_solid is NULL");
+  APG_REQUIRE(n_rec == 0 || (d_pos && d_mask), "apg_precorrect_weak: d_pos or d_mask is NULL");
+  apg_pc_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_pc_defaults(&p);
+  APG_TRY(check_pc(p));
+  APG_REQUIRE(p.K >= 9 && p.K <= 29, "apg_precorrect_weak: K must be in [9, 29]");
+  APG_REQUIRE(dr->n_reads == 0 || dr->d_quals, "apg_precorrect_weak: read set has no qualities");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  unsigned long long* weak = nullptr;
+  const uint64_t words = dr->n_bases / 64 + 2;
+  APG_TRY(workspace_t(ctx, "pc_weak", words, &weak));
+  APG_CHECK_HIP(hipMemsetAsync(weak, 0, words * 8, ctx->stream));
+  kbegin(ctx, "weak_apply", n_rec * 12);
+  if (n_rec)
+    k_weak_apply<<<grid_for(ctx, n_rec), 256, 0, ctx->stream>>>(static_cast<const uint64_t*>(d_pos),
+                                                                static_cast<const uint32_t*>(d_mask), n_rec, weak);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  apg_pc_stats st;
+  std::memset(&st, 0, sizeof st);
+  APG_TRY(correct_pass(ctx, dr, p, static_cast<const uint64_t*>(d_solid), n_solid, &st, weak));
+  if (stats) *stats = st;
   return APG_OK;
 }
 

@@ -119,6 +119,20 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
   }
 }
 
+// Scatter outputs: plain 16-byte records, 24-byte records with the position
+// of their first K-mer, or 16-byte records + the positions in a parallel
+// array (the multi-GPU weak-mask return: records travel, positions stay).
+struct SplitOut {
+  SK16* rec;
+  uint64_t* pos;
+};
+template <typename O> struct OutWantsPos { static constexpr bool value = false; };
+template <> struct OutWantsPos<SK24*> { static constexpr bool value = true; };
+template <> struct OutWantsPos<SplitOut> { static constexpr bool value = true; };
+__device__ __forceinline__ void rec_put(SplitOut out, uint64_t i, const SK16& x, uint64_t pos) {
+  out.rec[i] = x;
+  out.pos[i] = pos;
+}
 __device__ __forceinline__ void rec_put(SK16* out, uint64_t i, const SK16& x, uint64_t) { out[i] = x; }
 __device__ __forceinline__ void rec_put(SK24* out, uint64_t i, const SK16& x, uint64_t pos) {
   out[i] = SK24{x.w0, x.w1, pos};
@@ -130,9 +144,9 @@ __device__ __forceinline__ SK16 rec_head(const SK24& r) { return SK16{r.w0, r.w1
 // block (omat, LDS cursor): the run's size is fixed by k_sk_count, the order
 // inside a run is immaterial to counting.  SK24 records also carry the global
 // base position of their first K-mer.
-template <typename R>
+template <typename O>
 __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, int D,
-                                                           const uint64_t* __restrict__ omat, R* __restrict__ out) {
+                                                           const uint64_t* __restrict__ omat, O out) {
   __shared__ SkTile<kSkThreads> T;
   __shared__ unsigned long long cur[256];
   __shared__ uint32_t sbuf[kSkMaxW * kSkThreads];
@@ -147,7 +161,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
     const SK16 x = make_rec(rd, a, n, key, p.K);
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
     uint64_t pos = 0;
-    if (sizeof(R) == sizeof(SK24)) pos = rv.base_off[tile0 + (tile_n ? threadIdx.x : 0)] + a;
+    if constexpr (OutWantsPos<O>::value) pos = rv.base_off[tile0 + (tile_n ? threadIdx.x : 0)] + a;
     rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
   };
   for (uint64_t t0 = r0; t0 < r1;) {
@@ -198,6 +212,8 @@ struct SkOut {
   uint64_t solid_cap;
   uint32_t min_solid;
   unsigned long long* weak;    // SK24 solid mode: per-base bitmap of weak K-mer instances (or null)
+  uint32_t* wrec;              // SK24 solid mode, instead of `weak`: mask of weak K-mers per record, at
+                               // index record.pos (the multi-GPU owner side: pos = receive index)
 };
 
 __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, const SkOut& o) {
@@ -327,7 +343,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
       // finds its final count in the table, weak ones (count < min_solid) set
       // their bit at the instance's base position — one 64-bit atomic OR (two
       // when the run straddles a word) per record holding a weak K-mer.
-      if (o.weak && ibase <= kSkSlotCap) {
+      if ((o.weak || o.wrec) && ibase <= kSkSlotCap) {
         // thread per record: its K-mers' slots are islot[ib + ex ..], their
         // final counts give the record's weak mask directly
         uint32_t ib = 0;
@@ -344,7 +360,9 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
           uint32_t m = 0;
           for (uint32_t t = 0; t < nk; ++t)
             if (tcnt[islot[ex + t]] < o.min_solid) m |= 1u << t;
-          if (m) {
+          if (o.wrec) {
+            if (c0 + tid < nr) o.wrec[b] = m;
+          } else if (m) {
             const uint32_t sh = (uint32_t)(b & 63);
             atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
             if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
@@ -352,7 +370,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
           ib += tot;
           __syncthreads();
         }
-      } else if (o.weak) {
+      } else if (o.weak || o.wrec) {
         for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
           uint32_t nk = 0;
           if (c0 + tid < nr) {
@@ -376,7 +394,9 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
             if (tcnt[s] < o.min_solid) atomicOr(&wmask[i], 1u << t);
           }
           __syncthreads();
-          if (c0 + tid < nr && wmask[tid]) {
+          if (o.wrec) {
+            if (c0 + tid < nr) o.wrec[cpos[tid]] = wmask[tid];
+          } else if (c0 + tid < nr && wmask[tid]) {
             const uint64_t b = cpos[tid], m = wmask[tid];
             const uint32_t sh = (uint32_t)(b & 63);
             atomicOr(&o.weak[b >> 6], (unsigned long long)(m << sh));
@@ -462,22 +482,28 @@ __global__ void k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __res
 __global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __restrict__ boff,
                               const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, SkP p,
                               const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
-                              uint64_t gmask, uint32_t min_solid, unsigned long long* __restrict__ weak) {
+                              uint64_t gmask, uint32_t min_solid, unsigned long long* __restrict__ weak,
+                              uint32_t* __restrict__ wrec) {
   for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
     const uint32_t b = ovf_list[q];
     for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
       const SK24 r = rec[i];
       const SK16 h = rec_head(r);
       const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+      uint32_t m = 0;
       for (uint32_t t = 0; t < n; ++t) {
         const uint64_t c = rec_kmer(h, t, p);
         uint64_t s = khash(p.hp, c) & gmask;
         while (gkey[s] != c) s = (s + 1) & gmask;
         if (gcnt[s] < min_solid) {
-          const uint64_t x = r.pos + t;
-          atomicOr(&weak[x >> 6], 1ull << (x & 63));
+          m |= 1u << t;
+          if (!wrec) {
+            const uint64_t x = r.pos + t;
+            atomicOr(&weak[x >> 6], 1ull << (x & 63));
+          }
         }
       }
+      if (wrec) wrec[r.pos] = m;
     }
   }
 }
@@ -560,8 +586,8 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   return APG_OK;
 }
 
-template <typename R>
-static int sk_scatter_t(apg_ctx* ctx, const apg_dreads* dr, int K, int P, R* out) {
+template <typename O>
+static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out, size_t out_bytes) {
   auto& s = ctx->skstate;
   if (!s.valid || s.gen != dr->gen || s.K != K || s.P != P) {
     std::vector<uint64_t> rc, kc;
@@ -572,15 +598,24 @@ static int sk_scatter_t(apg_ctx* ctx, const apg_dreads* dr, int K, int P, R* out
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)(1u << D) * s.G + 1, &omat));
-  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * sizeof(R));
-  if (dr->n_reads) k_sk_scatter<R><<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out);
+  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * out_bytes);
+  if (dr->n_reads) k_sk_scatter<O><<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;
 }
 
+template <typename R>
+static int sk_scatter_t(apg_ctx* ctx, const apg_dreads* dr, int K, int P, R* out) {
+  return sk_scatter_o<R*>(ctx, dr, K, P, out, sizeof(R));
+}
+
 int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
   return sk_scatter_t<SK16>(ctx, dr, K, P, out);
+}
+
+int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos) {
+  return sk_scatter_o<SplitOut>(ctx, dr, K, P, SplitOut{out, pos}, sizeof(SK16) + 8);
 }
 
 // Partition levels + bucket counting of records laid out as P source blocks,
@@ -593,7 +628,7 @@ int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
 template <typename R>
 static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vector<uint64_t>& rec_counts,
                             uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist,
-                            size_t hist_len, unsigned long long* weak, SkResult* res) {
+                            size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr) {
   const SkP p = make_skp(K);
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
@@ -662,7 +697,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }
-  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr};
+  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr};
   const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R>, kSkThreads, nb)
                               : resident_grid(ctx, k_sk_bucket<false, R>, kSkThreads, nb);
   for (int attempt = 0;; ++attempt) {
@@ -701,9 +736,9 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       else
         k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
       if constexpr (sizeof(R) == sizeof(SK24)) {
-        if (o.weak)
+        if (o.weak || o.wrec)
           k_sk_big_weak<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1,
-                                                      min_solid, o.weak);
+                                                      min_solid, o.weak, o.wrec);
       }
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
@@ -769,6 +804,34 @@ int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid,
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
   APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
   return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res);
+}
+
+__global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const SK16 x = in[i];
+    out[i] = SK24{x.w0, x.w1, i};
+  }
+}
+
+// Owner side of the multi-GPU weak-mask return: the solid set of the
+// received 16-byte records (as sk_stage_count in solid mode) and, for every
+// received record i, the mask of its K-mers whose count is < min_solid in
+// wrec[i] — the records travel with their receive index as position, so the
+// bucket kernel's weak pass writes each mask with a plain store.
+int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
+                        int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res) {
+  APG_REQUIRE(K >= 9 && K <= 32, "sk_shard_solid_weak: K must be in [9, 32]");
+  uint64_t n = 0;
+  for (auto c : rec_counts) n += c;
+  SK24* buf = nullptr;
+  APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
+  if (n) {
+    APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
+    k_sk_index24<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(recv, n, buf);
+    APG_CHECK_HIP(hipGetLastError());
+  }
+  return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, nullptr, res,
+                                wrec);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {

@@ -53,6 +53,25 @@ class HipShardBackend:
         torch.cuda.synchronize(self.device)
         return self.ctx.shard_solid(recv.data_ptr(), recv_counts, K, P, min_solid)
 
+    # weak-mask return (apg_shard_scatter_pos / apg_shard_solid_weak / apg_precorrect_weak)
+    def shard_scatter_pos(self, dreads: DeviceReads, K: int, P: int, send: torch.Tensor, pos: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)
+        self.ctx.shard_scatter_pos(dreads, K, P, send.data_ptr(), pos.data_ptr())
+
+    def alloc_mask(self, n: int) -> torch.Tensor:
+        return torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
+
+    def shard_solid_weak(self, recv: torch.Tensor, recv_counts: np.ndarray, K: int, P: int, min_solid: int,
+                         mask: torch.Tensor) -> int:
+        torch.cuda.synchronize(self.device)
+        return self.ctx.shard_solid_weak(recv.data_ptr(), recv_counts, K, P, min_solid, mask.data_ptr())
+
+    def precorrect_weak(self, dreads: DeviceReads, solid: torch.Tensor, n_solid: int, pos: torch.Tensor,
+                        mask: torch.Tensor, n_records: int, prm: dict) -> dict:
+        torch.cuda.synchronize(self.device)
+        return self.ctx.precorrect_weak(dreads, solid.data_ptr(), n_solid, pos.data_ptr(), mask.data_ptr(), n_records,
+                                        **prm)
+
     def solid_export(self, out: torch.Tensor) -> None:
         torch.cuda.synchronize(self.device)
         self.ctx.solid_export(out.data_ptr())
@@ -61,9 +80,17 @@ class HipShardBackend:
         torch.cuda.synchronize(self.device)
         return self.ctx.precorrect_solid(dreads, solid.data_ptr(), n_solid, **prm)
 
-    def fill(self, dreads: DeviceReads, solid: torch.Tensor, n_solid: int, prm: dict, out=None):
+    def fill(self, dreads: DeviceReads, solid: torch.Tensor, n_solid: int, prm: dict, out=None,
+             last_solid: bool = False):
+        """last_solid: `solid` is the set the last correction pass on this
+        context used — reuse its extension table and clean flags."""
         torch.cuda.synchronize(self.device)
-        filled, _, st = self.ctx.fill_fragments(dreads, (solid.data_ptr(), n_solid), out=out, **prm)
+        if last_solid:
+            filled, _, st = self.ctx.fill_fragments(dreads, K=prm["K"], min_insert=prm["min_insert"],
+                                                    max_insert=prm["max_insert"], max_steps=prm["max_steps"],
+                                                    last_solid=True, out=out)
+        else:
+            filled, _, st = self.ctx.fill_fragments(dreads, (solid.data_ptr(), n_solid), out=out, **prm)
         return filled, st
 
     # unipath stages
@@ -155,16 +182,22 @@ def all_gather_var(local: torch.Tensor, n_local: int, group=None):
     return out[: sum(sizes)], sizes
 
 
-def _exchange_kmers(backend, reads, K: int, P: int, group):
+def _exchange_kmers(backend, reads, K: int, P: int, group, pos=None):
     """K <= 32 records of this rank's reads -> their owner shards.  A record
     is backend.record_words int64 words (libapg: 16-byte super-k-mers).
+    pos: a one-element list to receive the sent records' base positions
+    (weak-mask return); the record splits are then appended to it.
     Returns (recv tensor, recv_counts [src * B + l1], records sent, received)."""
     B = shard_bins(K, P)
     W = getattr(backend, "record_words", 1)
     dev = backend.alloc(1).device
     counts = backend.shard_count(reads, K, P)  # [dest * B + l1]
     send = backend.alloc(W * int(counts.sum()))
-    backend.shard_scatter(reads, K, P, send)
+    if pos is not None:
+        pos[0] = backend.alloc(int(counts.sum()))
+        backend.shard_scatter_pos(reads, K, P, send, pos[0])
+    else:
+        backend.shard_scatter(reads, K, P, send)
 
     cnt_t = torch.from_numpy(counts.astype(np.int64)).to(dev)
     recv_cnt_t = torch.empty_like(cnt_t)
@@ -176,6 +209,9 @@ def _exchange_kmers(backend, reads, K: int, P: int, group):
     recv = backend.alloc(int(sum(out_splits)))
     n_in, n_out = int(sum(in_splits)) // W, int(sum(out_splits)) // W
     all_to_all_chunked(recv, send, out_splits, in_splits, group=group)
+    if pos is not None:
+        pos.append([x // W for x in in_splits])
+        pos.append([x // W for x in out_splits])
     return recv, recv_counts, n_in, n_out
 
 
@@ -218,16 +254,33 @@ def sharded_precorrect(backend, reads, K: int = 24, min_solid: int = 3, max_q_su
     _check_pow2(P)
     dev = backend.alloc(1).device
     tot = {"n_suspect": 0, "n_corrected": 0, "n_ambiguous": 0, "n_uncorrectable": 0, "n_solid": 0}
+    weak = hasattr(backend, "shard_solid_weak") and 9 <= K <= 29
+    prm = {"K": K, "min_solid": min_solid, "max_q_suspect": max_q_suspect}
     for _ in range(n_cycles):
-        recv, recv_counts, _, _ = _exchange_kmers(backend, reads, K, P, group)
-        n_local = backend.shard_solid(recv, recv_counts, K, P, min_solid)
-        del recv
+        if weak:
+            # weak-mask return: owners report the weak K-mers of every record
+            # they received, so the correction needs no weak-test lookups
+            pos = [None]
+            recv, recv_counts, n_in, n_out = _exchange_kmers(backend, reads, K, P, group, pos=pos)
+            rmask = backend.alloc_mask(n_out)
+            n_local = backend.shard_solid_weak(recv, recv_counts, K, P, min_solid, rmask)
+            del recv
+            smask = backend.alloc_mask(n_in)
+            all_to_all_chunked(smask, rmask, pos[1], pos[2], group=group)  # splits reversed
+            del rmask
+        else:
+            recv, recv_counts, _, _ = _exchange_kmers(backend, reads, K, P, group)
+            n_local = backend.shard_solid(recv, recv_counts, K, P, min_solid)
+            del recv
         local = backend.alloc(n_local)
         backend.solid_export(local)
         solid, sizes = all_gather_var(local, n_local, group=group)
         del local
-        st = backend.precorrect_solid(reads, solid, sum(sizes),
-                                      {"K": K, "min_solid": min_solid, "max_q_suspect": max_q_suspect})
+        if weak:
+            st = backend.precorrect_weak(reads, solid, sum(sizes), pos[0], smask, n_in, prm)
+            del smask, pos
+        else:
+            st = backend.precorrect_solid(reads, solid, sum(sizes), prm)
         for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
             tot[k] += int(st[k])
         tot["n_solid"] = sum(sizes)
@@ -242,13 +295,20 @@ FILL_KEYS = ("n_pairs", "n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip
 
 
 def sharded_fill(backend, reads, solid, n_solid: int, K: int = 24, min_insert: int = 126, max_insert: int = 234,
-                 max_steps: int = 1024, out=None, group: Optional[dist.ProcessGroup] = None):
+                 max_steps: int = 1024, out=None, group: Optional[dist.ProcessGroup] = None,
+                 last_solid: bool = False):
     """FillFragments on every rank's own pairs (ranks hold whole pairs)
     against the replicated solid set of sharded_precorrect(keep_solid=True):
     no exchange ("reads sharded, no exchange").  Returns this
-    rank's filled fragments and the stats summed over ranks."""
+    rank's filled fragments and the stats summed over ranks.  last_solid:
+    `solid` is what the last correction pass on this rank's context used
+    (sharded_precorrect(keep_solid=True) right before) — its extension table
+    and per-read clean flags are reused."""
     prm = {"K": K, "min_insert": min_insert, "max_insert": max_insert, "max_steps": max_steps}
-    filled, st = backend.fill(reads, solid, n_solid, prm, out)
+    if last_solid:
+        filled, st = backend.fill(reads, solid, n_solid, prm, out, last_solid=True)
+    else:
+        filled, st = backend.fill(reads, solid, n_solid, prm, out)
     dev = backend.alloc(1).device
     t = torch.tensor([int(st[k]) for k in FILL_KEYS], dtype=torch.int64, device=dev)
     dist.all_reduce(t, group=group)

@@ -195,6 +195,26 @@ class Context:
                                     min_solid, C.byref(n)), "apg_shard_solid")
         return int(n.value)
 
+    def shard_solid_weak(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int, min_solid: int,
+                         d_mask_ptr: int) -> int:
+        """apg_shard_solid + the weak mask (u32) of every received record."""
+        rc = np.ascontiguousarray(recv_counts, dtype=np.uint64)
+        n = C.c_uint64()
+        check(lib().apg_shard_solid_weak(self._h, C.c_void_p(d_recv_ptr), rc.ctypes.data_as(_u64p), K, n_shards,
+                                         min_solid, C.c_void_p(d_mask_ptr), C.byref(n)), "apg_shard_solid_weak")
+        return int(n.value)
+
+    def precorrect_weak(self, dreads: DeviceReads, d_solid_ptr: int, n_solid: int, d_pos_ptr: int, d_mask_ptr: int,
+                        n_records: int, K: int = 24, min_solid: int = 3, max_q_suspect: int = 20) -> dict:
+        """One correction pass through the weak bitmap built from the returned
+        per-record masks (apg_precorrect_weak)."""
+        p = self.pc_params(K, min_solid, max_q_suspect, 1)
+        st = apg_pc_stats()
+        check(lib().apg_precorrect_weak(self._h, dreads.handle, C.byref(p), C.c_void_p(d_solid_ptr), n_solid,
+                                        C.c_void_p(d_pos_ptr), C.c_void_p(d_mask_ptr), n_records, C.byref(st)),
+              "apg_precorrect_weak")
+        return st.as_dict()
+
     def solid_export(self, d_out_ptr: int) -> None:
         check(lib().apg_solid_export(self._h, C.c_void_p(d_out_ptr)), "apg_solid_export")
 
@@ -535,6 +555,10 @@ class Context:
     def shard_scatter(self, dreads: DeviceReads, K: int, n_shards: int, d_send_ptr: int) -> None:
         check(lib().apg_shard_scatter(self._h, dreads.handle, K, n_shards, C.c_void_p(d_send_ptr)),
               "apg_shard_scatter")
+
+    def shard_scatter_pos(self, dreads: DeviceReads, K: int, n_shards: int, d_send_ptr: int, d_pos_ptr: int) -> None:
+        check(lib().apg_shard_scatter_pos(self._h, dreads.handle, K, n_shards, C.c_void_p(d_send_ptr),
+                                          C.c_void_p(d_pos_ptr)), "apg_shard_scatter_pos")
 
     def shard_spectrum(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int,
                        hist_len: int = DEFAULT_HIST_LEN):

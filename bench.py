@@ -359,7 +359,8 @@ def main():
                 if a.oracle_fill:
                     uin = dfrags
                 else:
-                    fill["out"], fst = sharded_fill(backend, dreads, solid, ns, K=a.K_correct, out=fill["out"])
+                    fill["out"], fst = sharded_fill(backend, dreads, solid, ns, K=a.K_correct, out=fill["out"],
+                                                   last_solid=True)
                     uin = fill["out"]
                 del solid
                 ust = sharded_unipaths(backend, uin, a.K_unipath)

@@ -214,6 +214,28 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
                     int K, int n_shards, uint32_t min_solid, uint64_t* n_solid);
 /* d_out: device buffer of n_solid u64 (the hash of each solid K-mer). */
 int apg_solid_export(apg_ctx* ctx, void* d_out);
+/* Weak-mask return (the multi-GPU form of the weak-instance bitmap that the
+ * single-GPU pass builds while counting):
+ *   1. apg_shard_scatter_pos: as apg_shard_scatter, plus d_pos[i] (u64) =
+ *      base position of sent record i's first K-mer (stays on this rank);
+ *   2. (caller) all_to_all of the records, as for apg_shard_solid;
+ *   3. apg_shard_solid_weak: this shard's solid set (apg_solid_export) and
+ *      d_mask[i] (u32) = mask of received record i's K-mers with count <
+ *      min_solid, in receive order;
+ *   4. (caller) all_to_all of the masks back (splits reversed): each rank
+ *      gets the masks of its sent records in send order;
+ *   5. (caller) all_gather of the solid sets;
+ *   6. apg_precorrect_weak: the per-base weak bitmap from (d_pos, d_mask),
+ *      then one correction pass through it — no weak-test lookups, and the
+ *      pass leaves the clean flags + extension table FillFragments reuses
+ *      (APG_FILL_LAST_SOLID).  Results equal apg_precorrect_solid's.
+ * K in [9, 29]. */
+int apg_shard_scatter_pos(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, void* d_send, void* d_pos);
+int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts /* host */, int K,
+                         int n_shards, uint32_t min_solid, void* d_mask, uint64_t* n_solid);
+int apg_precorrect_weak(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p, const void* d_solid,
+                        uint64_t n_solid, const void* d_pos, const void* d_mask, uint64_t n_records,
+                        apg_pc_stats* stats);
 /* The solid set (apg_kmer_hash values, any order) the last correction pass on
  * this context corrected against — what APG_FILL_LAST_SOLID uses.  d_out:
  * device buffer of *n_solid u64, or NULL to query the size. */

@@ -80,6 +80,50 @@ class OracleShardBackend:
         return filled, st
 
 
+class OracleWeakBackend(OracleShardBackend):
+    """OracleShardBackend + the weak-mask return contract (apg_shard_scatter_pos
+    / apg_shard_solid_weak / apg_precorrect_weak): records are single K-mer
+    hashes, so a record's mask is one bit.  precorrect_weak checks that the
+    bitmap rebuilt from the returned masks is exactly the set of this rank's
+    K-mer instances outside the global solid set, then corrects."""
+
+    def _pos(self, reads, K):
+        L = reads.lengths().astype(np.int64)
+        nk = np.maximum(L - K + 1, 0)
+        start = np.repeat(reads.base_off[:-1].astype(np.int64), nk)
+        return start + (np.arange(int(nk.sum())) - np.repeat(np.cumsum(nk) - nk, nk))
+
+    def shard_scatter_pos(self, reads, K, P, send, pos):
+        h, d = self._digits(reads, K, P)
+        order = np.argsort(d, kind="stable")
+        send[: len(h)] = torch.from_numpy(h[order].view(np.int64))
+        pos[: len(h)] = torch.from_numpy(self._pos(reads, K)[order])
+
+    def alloc_mask(self, n):
+        return torch.zeros(max(n, 1), dtype=torch.int32)
+
+    def shard_solid_weak(self, recv, recv_counts, K, P, min_solid, mask):
+        n = int(recv_counts.sum())
+        h = recv[:n].numpy().view(np.uint64)
+        u, inv, c = np.unique(h, return_inverse=True, return_counts=True)
+        self.solid = u[c >= min_solid]
+        mask[:n] = torch.from_numpy((c[inv] < min_solid).astype(np.int32))
+        return len(self.solid)
+
+    def precorrect_weak(self, reads, solid, n_solid, pos, mask, n_records, prm):
+        K = prm["K"]
+        weak = np.zeros(reads.n_bases + 1, dtype=bool)
+        m = mask[:n_records].numpy() != 0
+        weak[pos[:n_records].numpy()[m]] = True
+        h = oracle.extract_hashes(reads, K)
+        sol = np.isin(h, solid[:n_solid].numpy().view(np.uint64))
+        exp = np.zeros(reads.n_bases + 1, dtype=bool)
+        exp[self._pos(reads, K)[~sol]] = True
+        assert np.array_equal(weak, exp), "weak bitmap from the returned masks differs"
+        self.weak_checked = getattr(self, "weak_checked", 0) + 1
+        return self.precorrect_solid(reads, solid, n_solid, prm)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -235,7 +279,7 @@ def test_sharded_unipaths_gloo(world):
         assert np.array_equal(g["path_len"], exp["path_len"][lo:hi])
 
 
-def _pcworker(rank, world, port, n_cycles, q):
+def _pcworker(rank, world, port, n_cycles, q, weak=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -246,19 +290,23 @@ def _pcworker(rank, world, port, n_cycles, q):
         reads = synth_reads(synth_genome(30_000, 31), 3000, seed=32)
         parts = np.array_split(np.arange(reads.n_reads), world)
         mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
-        st = sharded_precorrect(OracleShardBackend(), mine, K=24, n_cycles=n_cycles)
+        be = OracleWeakBackend() if weak else OracleShardBackend()
+        st = sharded_precorrect(be, mine, K=24, n_cycles=n_cycles)
+        if weak:
+            assert getattr(be, "weak_checked", 0) == n_cycles
         q.put((rank, mine.packed[: int(mine.byte_off[-1])].copy(), mine.quals.copy(), st))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_cycles", [(2, 1), (4, 2)])
-def test_sharded_precorrect_gloo(world, n_cycles):
-    """Replicated-solid-set correction == single-process PreCorrect/FindErrors."""
+@pytest.mark.parametrize("world,n_cycles,weak", [(2, 1, False), (4, 2, False), (2, 1, True), (4, 2, True)])
+def test_sharded_precorrect_gloo(world, n_cycles, weak):
+    """Replicated-solid-set correction == single-process PreCorrect/FindErrors
+    (weak: with the weak-mask return, whose bitmap the backend verifies)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pcworker, args=(r, world, port, n_cycles, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pcworker, args=(r, world, port, n_cycles, q, weak)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])

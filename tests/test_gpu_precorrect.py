@@ -198,3 +198,68 @@ def test_precorrect_extension_path_short_reads(gpu_ctx):
         exp, est = oracle.precorrect(reads, K=K, min_solid=2)
         assert_same(got, exp)
         assert st == {**st, **est}
+
+
+@pytest.mark.parametrize("P", [1, 2, 4])
+def test_sharded_weak_return_loopback(gpu_ctx, P):
+    """The multi-GPU weak-mask return on one GPU: shard_scatter_pos per slice ->
+    loopback all_to_all -> shard_solid_weak per shard (solid set + per-record
+    weak masks) -> masks routed back in send order -> precorrect_weak on every
+    slice == monolithic PreCorrect (bases, quals, counters)."""
+    import torch
+
+    from allpathslg_amd import shard_bins
+
+    K = 24
+    reads = synth_reads(synth_genome(150_000, 71), 30_000, seed=72)
+    B = shard_bins(K, P)
+    parts = np.array_split(np.arange(reads.n_reads), P)
+    subs = [reads.subset(int(ix[0]), int(ix[-1]) + 1) for ix in parts]
+    dsubs = [gpu_ctx.upload(s) for s in subs]
+    sends, poss, counts = [], [], []
+    for d in dsubs:
+        c = gpu_ctx.shard_count(d, K, P)
+        n = int(c.sum())
+        buf = torch.empty(max(2 * n, 1), dtype=torch.int64, device="cuda")
+        pos = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.shard_scatter_pos(d, K, P, buf.data_ptr(), pos.data_ptr())
+        sends.append(buf)
+        poss.append(pos)
+        counts.append(c.reshape(P, B))
+    solids, masks = [], []  # masks[s][p]: shard s's masks for source p's records
+    for s in range(P):
+        pieces, rc, sizes = [], [], []
+        for p in range(P):
+            starts = np.concatenate([[0], np.cumsum(counts[p].reshape(-1))]).astype(np.int64)
+            pieces.append(sends[p][2 * starts[s * B] : 2 * starts[(s + 1) * B]])
+            rc.append(counts[p][s])
+            sizes.append(int(starts[(s + 1) * B] - starts[s * B]))
+        recv = torch.cat(pieces) if sum(x.numel() for x in pieces) else torch.empty(1, dtype=torch.int64, device="cuda")
+        mask = torch.empty(max(sum(sizes), 1), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        n = gpu_ctx.shard_solid_weak(recv.data_ptr(), np.concatenate(rc), K, P, 3, mask.data_ptr())
+        out = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+        gpu_ctx.solid_export(out.data_ptr())
+        solids.append(out[:n])
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        masks.append([mask[int(offs[p]) : int(offs[p + 1])] for p in range(P)])
+    solid = torch.cat(solids)
+    exp, est = oracle.precorrect(reads, K=K)
+    tot = {"n_suspect": 0, "n_corrected": 0, "n_ambiguous": 0, "n_uncorrectable": 0}
+    fixed = []
+    for p, d in enumerate(dsubs):
+        back = torch.cat([masks[s][p] for s in range(P)])  # send order: by destination shard
+        n_rec = int(counts[p].sum())
+        assert back.numel() == n_rec
+        st = gpu_ctx.precorrect_weak(d, solid.data_ptr(), solid.numel(), poss[p].data_ptr(), back.data_ptr(), n_rec,
+                                     K=K)
+        assert st["n_solid"] == est["n_solid"]
+        for k in tot:
+            tot[k] += st[k]
+        fixed.append(gpu_ctx.download(d))
+        d.free()
+    assert tot == {k: est[k] for k in tot}
+    assert np.array_equal(np.concatenate([f.packed[: int(f.byte_off[-1])] for f in fixed]),
+                          exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(np.concatenate([f.quals for f in fixed]), exp.quals)
