@@ -331,6 +331,10 @@ SIGNATURES = {
     "apg_consensus": (
         C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_reads), C.POINTER(apg_aln_pair), C.c_uint64, _u8p, _u8p]),
     "apg_consensus_dev": (C.c_int, [_P, _P, _P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "apg_urec_count": (C.c_int, [_P, _P, C.c_int, C.c_int, _u64p, _u64p]),
+    "apg_urec_scatter": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_void_p]),
+    "apg_urec_nodes": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, _u64p]),
+    "apg_urec_export": (C.c_int, [_P, C.c_void_p]),
     "apg_shard_scatter_pos": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "apg_shard_solid_weak": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, C.c_uint32, C.c_void_p, _u64p]),
     "apg_precorrect_weak": (

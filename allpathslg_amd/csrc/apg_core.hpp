@@ -122,6 +122,16 @@ struct apg_ctx {
     uint64_t n_recv = 0;
   } ustate;
 
+  // K <= 96 super-k-mer plan of the last usk_plan (reused by usk_scatter).
+  struct UrState {
+    bool valid = false;
+    uint64_t gen = 0;
+    int K = 0, P = 0;
+    uint32_t G = 0;
+    uint64_t n = 0;  // records
+    uint64_t n_nodes = 0;  // nodes of the last apg_urec_nodes ("usk_nodes")
+  } urstate;
+
   // Super-k-mer plan of the last sk_count (reused by sk_scatter).
   struct SkState {
     bool valid = false;
@@ -179,8 +189,6 @@ constexpr const char* kBig0 = "big0";
 constexpr const char* kBig1 = "big1";
 constexpr const char* kBig2 = "big2";
 
-// Grid of a grid-stride kernel over n items, `per` items per block, capped at
-// 16 blocks per CU.
 // Grid of a grid-stride kernel over `work` items: exactly the blocks that
 // are resident at once (CUs x the kernel's occupancy), so every block gets
 // the same share and no second, partial round of blocks trails the first.
@@ -193,6 +201,8 @@ inline uint32_t resident_grid(apg_ctx* ctx, Kern kernel, int threads, uint64_t w
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(work, g));
 }
 
+// Grid of a grid-stride kernel over n items, `per` items per block, capped at
+// 16 blocks per CU.
 inline uint32_t grid_for(apg_ctx* ctx, uint64_t n, int per = 256) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + per - 1) / per, (uint64_t)ctx->n_cu * 16));
 }

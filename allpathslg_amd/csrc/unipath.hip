@@ -1906,16 +1906,20 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   return rc;
 }
 
-// U1'-U3': distinct nodes of the reads into workspace "usk_nodes" (see the
-// device section).  n_inst: K-mer instances.
-static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec** nodes_out, uint64_t* N_out,
-                      uint64_t* n_inst) {
-  const UskP p = make_uskp(kp.K);
+// U1'-U3': distinct nodes through minimizer partitions, in three steps that
+// the single-GPU build chains directly and the multi-GPU build splits around
+// an all_to_all of the 48-byte records (P shards = the top log2 P key bits):
+//   usk_plan     count records per (shard, digit) and per-block offsets
+//   usk_scatter  the records, grouped by (shard, digit)
+//   usk_stage    partition levels of one shard's records (P source segments
+//                per digit) + LDS buckets -> distinct nodes in "usk_nodes"
+static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, std::vector<uint64_t>* h,
+                    std::vector<uint64_t>* kd, uint32_t* G_out) {
   if (p.w > kUskMaxW) {
     set_error("unipaths: minimizer window exceeds kUskMaxW");
     return APG_E_UNSUPPORTED;
   }
-  const int D = kUskDigitBits;
+  const int D = ceil_log2_u((uint64_t)P) + kUskDigitBits;
   const uint32_t ndig = 1u << D;
   const uint32_t G =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUskMaxBlocks, (dr->n_reads + kUskThreads - 1) / kUskThreads));
@@ -1936,34 +1940,79 @@ static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec**
   APG_CHECK_HIP(hipGetLastError());
   APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "usk"));
   k_usk_digit_starts<<<(ndig + 256) / 256, 256, 0, ctx->stream>>>(omat, ndig, G, ds);
-  std::vector<uint64_t> h(ndig + 1), kd(ndig);
-  APG_CHECK_HIP(hipMemcpyAsync(h.data(), ds, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(kd.data(), kdig, ndig * 8, hipMemcpyDeviceToHost, ctx->stream));
+  h->assign(ndig + 1, 0);
+  kd->assign(ndig, 0);
+  APG_CHECK_HIP(hipMemcpyAsync(h->data(), ds, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(kd->data(), kdig, ndig * 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  const uint64_t n = h[ndig];
-  uint64_t nk = 0;
-  for (auto x : kd) nk += x;
-  *n_inst = nk;
+  *G_out = G;
+  auto& us = ctx->urstate;
+  us.valid = true;
+  us.gen = dr->gen;
+  us.K = p.K;
+  us.P = P;
+  us.G = G;
+  us.n = (*h)[ndig];
+  return APG_OK;
+}
+
+static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, uint32_t G, SK48* out) {
+  const int D = ceil_log2_u((uint64_t)P) + kUskDigitBits;
+  SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+  const size_t sb_bytes = (size_t)p.w * kUskThreads * 4;
+  uint64_t* omat = nullptr;
+  APG_TRY(workspace_t(ctx, "usk_omat", (uint64_t)(1u << D) * G + 1, &omat));
+  kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + ctx->urstate.n * sizeof(SK48));
+  if (dr->n_reads) k_usk_scatter<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, omat, out);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
+// One shard's records src (rc = counts [src * 32 + digit], src-major layout)
+// -> distinct nodes.  The records' top log2(P) + kUskDigitBits key bits are
+// consumed; `spare` (may be src itself when it may be overwritten) is a
+// second record buffer.
+static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>& rc, uint64_t nk, const KeyP& kp,
+                     int P, KRec** nodes_out, uint64_t* N_out) {
+  const int pbits = ceil_log2_u((uint64_t)P);
+  const int D = kUskDigitBits;
+  const uint32_t ndig = 1u << D;
+  if (rc.size() != (size_t)P * ndig) {
+    set_error("unipaths: record counts have the wrong size");
+    return APG_E_ARG;
+  }
+  uint64_t n = 0;
+  for (auto c : rc) n += c;
   SK48 *bufA = nullptr, *bufB = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1) + 1, &bufA));
   APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1) + 1, &bufB));
-  kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + n * sizeof(SK48));
-  if (dr->n_reads) k_usk_scatter<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, omat, bufA);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  // partition levels on the key bits below the D digit bits
+  // partition levels on the key bits below the shard + digit bits
   const uint64_t need = std::max<uint64_t>(1, (nk + kUskBucketKmers - 1) / kUskBucketKmers);
-  const int bb = std::min(32, std::max(D, ceil_log2_u(need)));
+  const int bb = std::min(32 - pbits, std::max(D, ceil_log2_u(need)));
   const int rem = bb - D;
-  const int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
+  if (nlev == 0 && P > 1) nlev = 1;  // regroup the P source segments
   std::vector<std::vector<Seg>> parents(ndig);
-  for (uint32_t d = 0; d < ndig; ++d) parents[d].push_back(Seg{h[d], h[d + 1] - h[d]});
+  {
+    uint64_t pos = 0;
+    for (int s = 0; s < P; ++s)
+      for (uint32_t d = 0; d < ndig; ++d) {
+        const uint64_t c = rc[(size_t)s * ndig + d];
+        parents[d].push_back(Seg{pos, c});
+        pos += c;
+      }
+  }
   uint64_t* boff = nullptr;
   APG_TRY(workspace_t(ctx, "usk_boff", (1ull << bb) + 1, &boff));
-  if (nlev == 0) APG_CHECK_HIP(hipMemcpyAsync(boff, h.data(), (ndig + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-  SK48* cur = bufA;
+  if (nlev == 0) {
+    std::vector<uint64_t> hb(ndig + 1, 0);
+    for (uint32_t d = 0; d < ndig; ++d) hb[d + 1] = hb[d] + rc[d];
+    APG_CHECK_HIP(hipMemcpyAsync(boff, hb.data(), (ndig + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  }
+  const SK48* cur = src;
   uint64_t nb = ndig;
-  int consumed = D;
+  int consumed = pbits + D;
   for (int lev = 0; lev < nlev; ++lev) {
     const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
     consumed += bits;
@@ -2029,11 +2078,38 @@ static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec**
          ni[0], (unsigned long long)fN);
     N += fN;
   }
-  vlog(ctx, "unipaths: K=%d m=%d records=%llu instances=%llu levels=%d buckets=%llu nodes=%llu", kp.K, p.m,
+  vlog(ctx, "unipaths: K=%d P=%d records=%llu instances=%llu levels=%d buckets=%llu nodes=%llu", kp.K, P,
        (unsigned long long)n, (unsigned long long)nk, nlev, (unsigned long long)nb, (unsigned long long)N);
   *nodes_out = nodes;
   *N_out = N;
   return APG_OK;
+}
+
+__global__ void k_usk_sum(const SK48* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {
+  unsigned long long c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    c += (uint32_t)(rec[i].w0 >> 32) & 0xff;
+  wave_add(out, c);
+}
+
+// Single-GPU: plan + scatter into kBig0 (usk_stage's first buffer) + stage.
+static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec** nodes_out, uint64_t* N_out,
+                      uint64_t* n_inst) {
+  const UskP p = make_uskp(kp.K);
+  std::vector<uint64_t> h, kd;
+  uint32_t G = 0;
+  APG_TRY(usk_plan(ctx, dr, p, 1, &h, &kd, &G));
+  const uint32_t ndig = 1u << kUskDigitBits;
+  const uint64_t n = h[ndig];
+  uint64_t nk = 0;
+  for (auto x : kd) nk += x;
+  *n_inst = nk;
+  SK48* recs = nullptr;
+  APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1) + 1, &recs));
+  APG_TRY(usk_scatter(ctx, dr, p, 1, G, recs));
+  std::vector<uint64_t> rc(ndig);
+  for (uint32_t d = 0; d < ndig; ++d) rc[d] = h[d + 1] - h[d];
+  return usk_stage(ctx, recs, rc, nk, kp, 1, nodes_out, N_out);
 }
 
 static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
@@ -2508,6 +2584,85 @@ int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out) {
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail("sync");
   *out = d;
   return APG_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int apg_urec_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, uint64_t* counts,
+                   uint64_t* n_instances) {
+  APG_REQUIRE(ctx && reads && counts, "apg_urec_count: NULL argument");
+  APG_REQUIRE(K >= 1 && K <= 96, "apg_urec_count: K must be in [1, 96]");
+  APG_REQUIRE(n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
+              "apg_urec_count: n_shards must be a power of two <= 8");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  if (ctx) ctx->gstate.valid = false;
+  const UskP p = make_uskp(K);
+  std::vector<uint64_t> h, kd;
+  uint32_t G = 0;
+  APG_TRY(usk_plan(ctx, reads, p, n_shards, &h, &kd, &G));
+  const uint32_t ndig = (uint32_t)n_shards << kUskDigitBits;
+  uint64_t nk = 0;
+  for (uint32_t d = 0; d < ndig; ++d) {
+    counts[d] = h[d + 1] - h[d];
+    nk += kd[d];
+  }
+  if (n_instances) *n_instances = nk;
+  return APG_OK;
+}
+
+int apg_urec_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, void* d_send) {
+  APG_REQUIRE(ctx && reads, "apg_urec_scatter: NULL argument");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const auto& us = ctx->urstate;
+  if (!us.valid || us.gen != reads->gen || us.K != K || us.P != n_shards) {
+    std::vector<uint64_t> c((size_t)n_shards << kUskDigitBits);
+    APG_TRY(apg_urec_count(ctx, reads, K, n_shards, c.data(), nullptr));
+  }
+  APG_REQUIRE(ctx->urstate.n == 0 || d_send, "apg_urec_scatter: d_send is NULL");
+  APG_TRY(usk_scatter(ctx, reads, make_uskp(K), n_shards, ctx->urstate.G, static_cast<SK48*>(d_send)));
+  return sync(ctx);
+}
+
+int apg_urec_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+                   uint64_t* n_nodes) {
+  APG_REQUIRE(ctx && recv_counts && n_nodes, "apg_urec_nodes: NULL argument");
+  APG_REQUIRE(K >= 1 && K <= 96, "apg_urec_nodes: K must be in [1, 96]");
+  APG_REQUIRE(n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
+              "apg_urec_nodes: n_shards must be a power of two <= 8");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  ctx->gstate.valid = false;  // "usk_nodes" is about to be rewritten
+  ctx->urstate.n_nodes = 0;
+  const size_t nc = (size_t)n_shards << kUskDigitBits;
+  std::vector<uint64_t> rc(recv_counts, recv_counts + nc);
+  uint64_t n = 0;
+  for (auto c : rc) n += c;
+  APG_REQUIRE(n == 0 || d_recv, "apg_urec_nodes: d_recv is NULL");
+  const SK48* recs = static_cast<const SK48*>(d_recv);
+  unsigned long long* sum = nullptr;
+  APG_TRY(workspace_t(ctx, "usk_sum", 1, &sum));
+  APG_CHECK_HIP(hipMemsetAsync(sum, 0, 8, ctx->stream));
+  if (n) k_usk_sum<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(recs, n, sum);
+  unsigned long long nk = 0;
+  APG_TRY(d2h_u64(ctx, sum, &nk, 1));
+  KRec* nodes = nullptr;
+  uint64_t N = 0;
+  APG_TRY(usk_stage(ctx, recs, rc, nk, make_keyp(K), n_shards, &nodes, &N));
+  ctx->urstate.n_nodes = N;
+  *n_nodes = N;
+  return APG_OK;
+}
+
+int apg_urec_export(apg_ctx* ctx, void* d_out) {
+  APG_REQUIRE(ctx, "apg_urec_export: NULL ctx");
+  const uint64_t N = ctx->urstate.n_nodes;
+  if (N == 0) return APG_OK;
+  APG_REQUIRE(d_out, "apg_urec_export: d_out is NULL");
+  KRec* nodes = nullptr;
+  APG_TRY(workspace_t(ctx, "usk_nodes", N, &nodes));
+  APG_CHECK_HIP(hipMemcpyAsync(d_out, nodes, N * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
+  return sync(ctx);
 }
 
 }  // extern "C"

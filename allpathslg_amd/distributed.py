@@ -109,6 +109,24 @@ class HipShardBackend:
         torch.cuda.synchronize(self.device)
         self.ctx.ushard_export(out.data_ptr())
 
+    # minimizer-partition records (apg_urec_*)
+    urec_words = 6  # 48-byte super-k-mer records
+
+    def urec_count(self, dreads: DeviceReads, K: int, P: int) -> Tuple[np.ndarray, int]:
+        return self.ctx.urec_count(dreads, K, P)
+
+    def urec_scatter(self, dreads: DeviceReads, K: int, P: int, send: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)
+        self.ctx.urec_scatter(dreads, K, P, send.data_ptr())
+
+    def urec_nodes(self, recv: torch.Tensor, recv_counts: np.ndarray, K: int, P: int) -> int:
+        torch.cuda.synchronize(self.device)
+        return self.ctx.urec_nodes(recv.data_ptr(), recv_counts, K, P)
+
+    def urec_export(self, out: torch.Tensor) -> None:
+        torch.cuda.synchronize(self.device)
+        self.ctx.urec_export(out.data_ptr())
+
     def graph_from_nodes(self, nodes: torch.Tensor, n_nodes: int, dreads, K: int, fetch: bool):
         torch.cuda.synchronize(self.device)
         return self.ctx.unipaths_from_nodes(nodes.data_ptr(), n_nodes, dreads, K, read_paths=True, fetch=fetch)
@@ -323,9 +341,10 @@ def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGr
     """Global unipath graph of every rank's reads ("shard the
     counting, replicate the compaction"):
 
-      rank r: K-mer instances -> distinct local nodes (32-byte records)
-              all_to_all(records)          local nodes of this shard's K-mers
-              ushard_nodes                 this shard's distinct nodes
+      rank r: reads -> 48-byte super-k-mer records by minimizer shard
+              (urec_*; backends without them: distinct local nodes, 32 B)
+              all_to_all(records)          records of this shard's K-mers
+              urec_nodes                   this shard's distinct nodes
               all_gather(nodes)            the full node set on every rank
               unipaths_from_nodes          graph (identical on every rank) +
                                            KmerPaths of this rank's reads
@@ -335,28 +354,44 @@ def sharded_unipaths(backend, reads, K: int = 96, group: Optional[dist.ProcessGr
     P = dist.get_world_size(group)
     if P & (P - 1) or P > 32:
         raise ValueError(f"world size {P} must be a power of two <= 32")
-    B = 32 // P
+    # minimizer-partition records (48-byte super-k-mers, P <= 8) when the
+    # backend has them, else distinct local nodes (32-byte records)
+    rec = hasattr(backend, "urec_count") and P <= 8
+    B = 32 if rec else 32 // P
+    W = getattr(backend, "urec_words", 6) if rec else 4
     dev = backend.alloc(1).device
-    counts, n_inst = backend.ushard_count(reads, K, P)  # [dest * B + group]
+    if rec:
+        counts, n_inst = backend.urec_count(reads, K, P)  # [dest * 32 + digit]
+    else:
+        counts, n_inst = backend.ushard_count(reads, K, P)  # [dest * B + group]
     n_send = int(counts.sum())
-    send = backend.alloc(4 * n_send)  # 4 x int64 per record
-    backend.ushard_scatter(reads, K, P, send)
+    send = backend.alloc(W * n_send)
+    if rec:
+        backend.urec_scatter(reads, K, P, send)
+    else:
+        backend.ushard_scatter(reads, K, P, send)
 
     cnt_t = torch.from_numpy(counts.astype(np.int64)).to(dev)
     recv_cnt_t = torch.empty_like(cnt_t)
     dist.all_to_all_single(recv_cnt_t, cnt_t, group=group)
     recv_counts = recv_cnt_t.cpu().numpy().astype(np.uint64)  # [src * B + group]
-    in_splits = (counts.reshape(P, B).sum(axis=1) * 4).astype(np.int64).tolist()
-    out_splits = (recv_counts.reshape(P, B).sum(axis=1) * 4).astype(np.int64).tolist()
+    in_splits = (counts.reshape(P, B).sum(axis=1) * W).astype(np.int64).tolist()
+    out_splits = (recv_counts.reshape(P, B).sum(axis=1) * W).astype(np.int64).tolist()
     n_in, n_out = int(sum(in_splits)), int(sum(out_splits))
     recv = backend.alloc(n_out)
     all_to_all_chunked(recv, send, out_splits, in_splits, group=group)
     del send
 
-    n_local = backend.ushard_nodes(recv, recv_counts, K, P)
+    if rec:
+        n_local = backend.urec_nodes(recv, recv_counts, K, P)
+    else:
+        n_local = backend.ushard_nodes(recv, recv_counts, K, P)
     del recv
     local = backend.alloc(4 * n_local)
-    backend.ushard_export(local)
+    if rec:
+        backend.urec_export(local)
+    else:
+        backend.ushard_export(local)
     nodes, sizes4 = all_gather_var(local, 4 * n_local, group=group)
     del local
     graph, st = backend.graph_from_nodes(nodes, sum(sizes4) // 4, reads, K, fetch)

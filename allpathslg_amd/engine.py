@@ -421,6 +421,29 @@ class Context:
                                      C.byref(n)), "apg_ushard_nodes")
         return int(n.value)
 
+    def urec_count(self, dreads: DeviceReads, K: int, n_shards: int) -> Tuple[np.ndarray, int]:
+        """Sharded node build through minimizer partitions, step 1: 48-byte
+        records per (shard, digit) (n_shards * 32, dest-major) and the reads'
+        K-mer instances."""
+        counts = np.zeros(n_shards * 32, dtype=np.uint64)
+        ni = C.c_uint64()
+        check(lib().apg_urec_count(self._h, dreads.handle, K, n_shards, counts.ctypes.data_as(_u64p), C.byref(ni)),
+              "apg_urec_count")
+        return counts, int(ni.value)
+
+    def urec_scatter(self, dreads: DeviceReads, K: int, n_shards: int, d_send_ptr: int) -> None:
+        check(lib().apg_urec_scatter(self._h, dreads.handle, K, n_shards, C.c_void_p(d_send_ptr)), "apg_urec_scatter")
+
+    def urec_nodes(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int) -> int:
+        rc = np.ascontiguousarray(recv_counts, dtype=np.uint64)
+        n = C.c_uint64()
+        check(lib().apg_urec_nodes(self._h, C.c_void_p(d_recv_ptr), rc.ctypes.data_as(_u64p), K, n_shards,
+                                   C.byref(n)), "apg_urec_nodes")
+        return int(n.value)
+
+    def urec_export(self, d_out_ptr: int) -> None:
+        check(lib().apg_urec_export(self._h, C.c_void_p(d_out_ptr)), "apg_urec_export")
+
     def ushard_export(self, d_out_ptr: int) -> None:
         check(lib().apg_ushard_export(self._h, C.c_void_p(d_out_ptr)), "apg_ushard_export")
 

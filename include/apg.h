@@ -405,6 +405,27 @@ int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes,
                             const apg_unipath_params* p, apg_unipath_graph* out,
                             apg_unipath_stats* stats);
 
+/* Sharded unipath nodes through minimizer partitions (the multi-GPU form of
+ * the single-GPU node build).  Records are 48-byte super-k-mers
+ * (runs of K-mers sharing a minimizer, with their extension bases); shard =
+ * top log2(P) bits of the minimizer key, 32 digit groups per shard:
+ *   1. apg_urec_count: records per (shard, digit) into counts[P * 32]
+ *      (dest-major) and the reads' K-mer instances;
+ *   2. apg_urec_scatter: the records, grouped by (shard, digit) -> d_send;
+ *   3. (caller) all_to_all of counts, then of records -> d_recv (src-major);
+ *   4. apg_urec_nodes: this shard's distinct nodes (32-byte records as in
+ *      apg_ushard_export) from the received records; apg_urec_export;
+ *   5. (caller) all_gather of the node sets -> apg_unipaths_from_nodes.
+ * A K-mer's instances share its minimizer, so shards never share a node; the
+ * union over shards equals apg_unipaths' node set. */
+int apg_urec_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
+                   uint64_t* counts /* host, n_shards * 32 */, uint64_t* n_instances /* may be NULL */);
+int apg_urec_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards,
+                     void* d_send /* device, sum(counts) x 48 bytes */);
+int apg_urec_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts /* host, n_shards * 32 */,
+                   int K, int n_shards, uint64_t* n_nodes);
+int apg_urec_export(apg_ctx* ctx, void* d_out /* device, n_nodes x 32 bytes */);
+
 /* ------------------------------------------------------------------------- */
 /* MakeRcDb ([R:M] tagged_rpint; <reads>.paths_rc.kN, <reads>.pathsdb.kN).    */
 /* From a graph with read paths (apg_unipaths with APG_UNIPATH_READ_PATHS):   */

@@ -235,7 +235,50 @@ class OracleUnipathBackend(OracleShardBackend):
         return g, {"n_unipaths": g["n_unipaths"], "n_nodes": g["n_nodes"]}
 
 
-def _uworker(rank, world, port, K, q):
+class OracleRecBackend(OracleUnipathBackend):
+    """OracleUnipathBackend with the minimizer-record contract (urec_*):
+    6-word records, counts per (shard, 32 digits).  The oracle's records are
+    K-mer instances (key limbs, hash | ext, padding) grouped by the top
+    log2(P) + 5 hash bits — any grouping every instance of a K-mer shares
+    satisfies the contract."""
+
+    urec_words = 6
+
+    def _recs(self, reads, K, P):
+        key = ("r", id(reads), K, P)
+        if key not in self.cache:
+            k, e, h = self._inst(reads, K)
+            D = int(np.log2(P)) + 5
+            d = (h >> np.uint64(64 - D)).astype(np.int64)
+            o = np.argsort(d, kind="stable")
+            out = np.zeros((len(h), 6), dtype=np.uint64)
+            out[:, :3] = k[o]
+            out[:, 3] = h[o] | e[o].astype(np.uint64)
+            self.cache[key] = (out, np.bincount(d, minlength=P * 32).astype(np.uint64), len(h))
+        return self.cache[key]
+
+    def urec_count(self, reads, K, P):
+        out, counts, n_inst = self._recs(reads, K, P)
+        return counts, n_inst
+
+    def urec_scatter(self, reads, K, P, send):
+        out, _, _ = self._recs(reads, K, P)
+        send[: 6 * len(out)] = torch.from_numpy(out.reshape(-1).view(np.int64))
+
+    def urec_nodes(self, recv, recv_counts, K, P):
+        n = int(recv_counts.sum())
+        rec = recv[: 6 * n].numpy().view(np.uint64).reshape(n, 6)
+        pbits = int(np.log2(P))
+        if n and pbits:
+            assert np.all((rec[:, 3] >> np.uint64(64 - pbits)) == dist.get_rank())
+        self.nodes = oracle.group_nodes(rec[:, :3].copy(), (rec[:, 3] & np.uint64(0xFF)).astype(np.uint8))
+        return len(self.nodes[1])
+
+    def urec_export(self, out):
+        self.ushard_export(out)
+
+
+def _uworker(rank, world, port, K, q, rec=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -247,21 +290,23 @@ def _uworker(rank, world, port, K, q):
         reads = noisy_reads(G=15_000, n=2000)
         parts = np.array_split(np.arange(reads.n_reads), world)
         mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
-        g, st = sharded_unipaths(OracleUnipathBackend(), mine, K, fetch=True)
+        g, st = sharded_unipaths(OracleRecBackend() if rec else OracleUnipathBackend(), mine, K, fetch=True)
         q.put((rank, int(parts[rank][0]), int(parts[rank][-1]) + 1, g, st))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_unipaths_gloo(world):
+@pytest.mark.parametrize("world,rec", [(2, False), (4, False), (2, True), (4, True)])
+def test_sharded_unipaths_gloo(world, rec):
+    """Sharded unipath graph == single-process graph, with distinct-local-node
+    records or with minimizer-partition records (rec)."""
     from tests.unipath_cases import noisy_reads
 
     K = 63
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_uworker, args=(r, world, port, K, q)) for r in range(world)]
+    procs = [ctx.Process(target=_uworker, args=(r, world, port, K, q, rec)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]

@@ -126,3 +126,55 @@ def test_shard_path_loopback(gpu_ctx, P):
         a, b = int(parts[i][0]), int(parts[i][-1]) + 1
         assert np.array_equal(g["path_start"], exp["path_start"][int(exp["path_off"][a]) : int(exp["path_off"][b])])
         d.free()
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_urec_path_loopback(gpu_ctx, P):
+    """Multi-GPU unipath nodes through minimizer partitions on one GPU: P read
+    slices -> urec_count / urec_scatter (48-byte records by minimizer shard)
+    -> loopback all_to_all -> urec_nodes per shard -> gather ->
+    unipaths_from_nodes == single-call build (graph and read paths)."""
+    import torch
+
+    K = 96
+    reads = noisy_reads(G=40_000, n=8000)
+    B = 32
+    parts = np.array_split(np.arange(reads.n_reads), P)
+    subs = [reads.subset(int(ix[0]), int(ix[-1]) + 1) for ix in parts]
+    dsubs = [gpu_ctx.upload(s) for s in subs]
+    sends, counts, n_inst = [], [], 0
+    for d in dsubs:
+        c, ni = gpu_ctx.urec_count(d, K, P)
+        n_inst += ni
+        buf = torch.empty(max(6 * int(c.sum()), 1), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.urec_scatter(d, K, P, buf.data_ptr())
+        sends.append(buf)
+        counts.append(c.reshape(P, B))
+    assert n_inst == reads.n_reads * (100 - K + 1)
+    node_chunks = []
+    for s in range(P):
+        pieces, rc = [], []
+        for p in range(P):
+            starts = np.concatenate([[0], np.cumsum(counts[p].reshape(-1))]).astype(np.int64)
+            a, b = starts[s * B], starts[(s + 1) * B]
+            pieces.append(sends[p][6 * a : 6 * b])
+            rc.append(counts[p][s])
+        recv = torch.cat(pieces) if sum(x.numel() for x in pieces) else torch.empty(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        n = gpu_ctx.urec_nodes(recv.data_ptr(), np.concatenate(rc), K, P)
+        out = torch.empty(max(4 * n, 1), dtype=torch.int64, device="cuda")
+        gpu_ctx.urec_export(out.data_ptr())
+        node_chunks.append(out[: 4 * n])
+    nodes = torch.cat(node_chunks)
+    torch.cuda.synchronize()
+    exp = oracle.unipaths(reads, K)
+    assert nodes.numel() // 4 == exp["n_nodes"]
+    for i, d in enumerate(dsubs):
+        g, st = gpu_ctx.unipaths_from_nodes(nodes.data_ptr(), nodes.numel() // 4, d, K, fetch=True)
+        for k in ("n_nodes", "n_unipaths", "len", "id_base", "rc", "ub_off", "unibases", "n_vertices", "from", "to"):
+            a = g[k]
+            assert (np.array_equal(a, exp[k]) if isinstance(a, np.ndarray) else a == exp[k]), k
+        a, b = int(parts[i][0]), int(parts[i][-1]) + 1
+        assert np.array_equal(g["path_start"], exp["path_start"][int(exp["path_off"][a]) : int(exp["path_off"][b])])
+        d.free()
