@@ -16,6 +16,7 @@ CPU tests plug in an oracle-backed one to exercise the exchange logic.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -148,26 +149,53 @@ def _rounds(n_max: int, group, dev) -> int:
 
 def all_to_all_chunked(recv: torch.Tensor, send: torch.Tensor, out_splits, in_splits, group=None) -> None:
     """all_to_all_single(recv, send, out_splits, in_splits) in rounds of at
-    most CHUNK_ELEMS elements per peer: round r moves elements
-    [r*C, (r+1)*C) of every peer segment through contiguous staging buffers."""
+    most CHUNK_ELEMS elements per peer, as grouped point-to-point transfers
+    straight between the peer segments of send and recv (no staging copies;
+    the segment to self is one local copy).  Round r moves elements
+    [r*C, (r+1)*C) of every peer segment.  APG_A2A=collective selects staged
+    all_to_all_single rounds instead."""
     C = CHUNK_ELEMS
     P = len(in_splits)
+    me = dist.get_rank(group)
     in_off = np.concatenate([[0], np.cumsum(in_splits)]).astype(np.int64)
     out_off = np.concatenate([[0], np.cumsum(out_splits)]).astype(np.int64)
+    if int(in_splits[me]) != int(out_splits[me]):
+        raise ValueError("all_to_all_chunked: the segment to self must have equal send and receive sizes")
     R = _rounds(max(max(in_splits), max(out_splits), 0), group, send.device)
+    if os.environ.get("APG_A2A", "p2p") == "collective":  # staged all_to_all_single rounds
+        for r in range(R):
+            lo = r * C
+            ins = [int(min(max(in_splits[d] - lo, 0), C)) for d in range(P)]
+            outs = [int(min(max(out_splits[q] - lo, 0), C)) for q in range(P)]
+            pieces = [send[int(in_off[d]) + lo : int(in_off[d]) + lo + ins[d]] for d in range(P) if ins[d]]
+            sbuf = torch.cat(pieces) if pieces else send.new_empty(0)
+            rbuf = recv.new_empty(sum(outs))
+            dist.all_to_all_single(rbuf, sbuf, outs, ins, group=group)
+            pos = 0
+            for q in range(P):
+                if outs[q]:
+                    recv[int(out_off[q]) + lo : int(out_off[q]) + lo + outs[q]].copy_(rbuf[pos : pos + outs[q]])
+                    pos += outs[q]
+        return
+    peer = (lambda q: q) if group is None else (lambda q: dist.get_global_rank(group, q))
     for r in range(R):
         lo = r * C
-        ins = [int(min(max(in_splits[d] - lo, 0), C)) for d in range(P)]
-        outs = [int(min(max(out_splits[q] - lo, 0), C)) for q in range(P)]
-        pieces = [send[int(in_off[d]) + lo : int(in_off[d]) + lo + ins[d]] for d in range(P) if ins[d]]
-        sbuf = torch.cat(pieces) if pieces else send.new_empty(0)
-        rbuf = recv.new_empty(sum(outs))
-        dist.all_to_all_single(rbuf, sbuf, outs, ins, group=group)
-        pos = 0
+        ops = []
         for q in range(P):
-            if outs[q]:
-                recv[int(out_off[q]) + lo : int(out_off[q]) + lo + outs[q]].copy_(rbuf[pos : pos + outs[q]])
-                pos += outs[q]
+            ni = int(min(max(in_splits[q] - lo, 0), C))
+            no = int(min(max(out_splits[q] - lo, 0), C))
+            if q == me:
+                if ni:
+                    recv[int(out_off[q]) + lo : int(out_off[q]) + lo + ni].copy_(
+                        send[int(in_off[q]) + lo : int(in_off[q]) + lo + ni])
+                continue
+            if ni:
+                ops.append(dist.P2POp(dist.isend, send[int(in_off[q]) + lo : int(in_off[q]) + lo + ni], peer(q), group))
+            if no:
+                ops.append(dist.P2POp(dist.irecv, recv[int(out_off[q]) + lo : int(out_off[q]) + lo + no], peer(q), group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
 
 
 def all_gather_var(local: torch.Tensor, n_local: int, group=None):
