@@ -151,6 +151,7 @@ struct apg_ctx {
     const uint32_t *idx = nullptr, *head = nullptr, *rank = nullptr, *uoh = nullptr;
     const uint64_t *ulen = nullptr, *urc = nullptr, *ub_off = nullptr;
     const uint8_t* ub = nullptr;  // unibases, one base per byte
+    const uint64_t* uloc = nullptr;  // apg_unipath_locs' (unipath, rank) table of this graph, once built
   } gstate;
 
   // Solid K-mer list of the last apg_shard_solid ("pc_solid" workspace).

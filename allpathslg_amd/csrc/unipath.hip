@@ -1877,6 +1877,7 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     g.urc = urc;
     g.ub_off = ub_off;
     g.ub = ub;
+    g.uloc = nullptr;  // rebuilt on the next apg_unipath_locs
     g.valid = true;
   }
   if (!out) return APG_OK;
@@ -2324,9 +2325,15 @@ struct ULoc {  // == apg_aln_pair
 
 struct GView {
   NodeIdx ni;
-  const uint32_t *head, *rank, *uoh;
+  const uint64_t* uloc;  // directed node -> unipath << 32 | rank (one line instead of three dependent ones)
   const uint64_t *ulen, *urc;
 };
+
+__global__ void k_uloc_table(uint64_t D, const uint32_t* __restrict__ head, const uint32_t* __restrict__ rank,
+                             const uint32_t* __restrict__ uoh, uint64_t* __restrict__ uloc) {
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < D; v += (uint64_t)gridDim.x * blockDim.x)
+    uloc[v] = (uint64_t)uoh[head[v]] << 32 | rank[v];
+}
 
 template <bool WRITE>
 __global__ void __launch_bounds__(256) k_ulocs(ReadsV rv, GView g, KeyP kp, uint32_t flags,
@@ -2353,8 +2360,9 @@ __global__ void __launch_bounds__(256) k_ulocs(ReadsV rv, GView g, KeyP kp, uint
           ++missing;
           continue;
         }
-        const uint32_t u = g.uoh[g.head[v]];
-        const int64_t st = (int64_t)g.rank[v] - (int64_t)j;
+        const uint64_t ul = g.uloc[v];
+        const uint32_t u = (uint32_t)(ul >> 32);
+        const int64_t st = (int64_t)(uint32_t)ul - (int64_t)j;
         if (u == pu && st == ps) continue;
         pu = u;
         ps = st;
@@ -2428,8 +2436,18 @@ static int ulocs_run(apg_ctx* ctx, const apg_dreads* dr, uint32_t flags, const U
   APG_REQUIRE(dr->n_reads < (1ull << 32), "apg_unipath_locs: more than 2^32 reads");
   APG_REQUIRE(dr->max_len < (1ull << 30), "apg_unipath_locs: read longer than 2^30 bases");
   const KeyP kp = make_keyp(gs.K);
-  const GView g{NodeIdx{static_cast<const KRec*>(gs.nodes), gs.idx, gs.tmask}, gs.head, gs.rank, gs.uoh, gs.ulen,
-                gs.urc};
+  // directed node -> (unipath, rank) table, once per graph
+  uint64_t* uloc = nullptr;
+  const uint64_t D = 2 * gs.n_nodes;
+  APG_TRY(workspace_t(ctx, "ul_uloc", std::max<uint64_t>(D, 1), &uloc));
+  if (ctx->gstate.uloc != uloc) {
+    kbegin(ctx, "ulocs_table", D * 20);
+    if (D) k_uloc_table<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, gs.head, gs.rank, gs.uoh, uloc);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    ctx->gstate.uloc = uloc;
+  }
+  const GView g{NodeIdx{static_cast<const KRec*>(gs.nodes), gs.idx, gs.tmask}, uloc, gs.ulen, gs.urc};
   const ReadsV rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   const uint64_t R = dr->n_reads;
   uint32_t* nloc = nullptr;

