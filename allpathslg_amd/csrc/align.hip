@@ -502,16 +502,28 @@ __global__ void __launch_bounds__(256) k_banded_sw_lane(SeqSet S, SeqSet T, cons
 // almost entirely in the window, so a column takes one global atomic per
 // chunk instead of one per placed base (coverage x fewer).
 constexpr int kVoteThreads = 256;
+struct VoteMeta {
+  uint64_t rbyte, rbase;  // read's packed byte offset and base (quality) offset
+  uint64_t col0;          // global column facing read position 0 (tb + offset; may wrap below 0)
+  uint32_t L;
+  int32_t lo, hi;         // read positions [lo, hi) inside the target
+  uint32_t flags;
+};
 constexpr uint32_t kVoteChunk = 128;
-constexpr uint32_t kVoteWin = 2048;  // columns x 4 u32 counters = 32 KiB of LDS
+constexpr uint32_t kVoteWin = 2048;        // columns x 4 u32 counters = 32 KiB of LDS
+constexpr uint32_t kVoteStride = kVoteWin + 1;  // one counter plane per base, planes offset by one bank
 
 __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, const AlnPair* __restrict__ plc,
                                                         uint64_t n, uint32_t* __restrict__ votes) {
-  __shared__ uint32_t win[kVoteWin * 4];
+  // plane-major counters win[b * kVoteStride + column]: a wave's lanes vote
+  // on consecutive columns, mostly for the same base, so their LDS atomics hit
+  // consecutive banks (column-major [column][4] was a 4-way bank conflict)
+  __shared__ uint32_t win[4 * kVoteStride];
   __shared__ unsigned long long g0s;
   __shared__ uint32_t span;
+  __shared__ VoteMeta pm[kVoteChunk];
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (uint32_t x = tid; x < kVoteWin * 4; x += kVoteThreads) win[x] = 0;
+  for (uint32_t x = tid; x < 4 * kVoteStride; x += kVoteThreads) win[x] = 0;
   const uint64_t nchunks = (n + kVoteChunk - 1) / kVoteChunk;
   for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const uint64_t k0 = c * kVoteChunk, k1 = std::min<uint64_t>(n, k0 + kVoteChunk);
@@ -521,27 +533,36 @@ __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, cons
       g0s = g < 0 ? 0ull : (unsigned long long)g;
       span = 0;
     }
+    // the chunk's placement metadata, one placement per thread: the dependent
+    // offset loads of all placements are in flight at once instead of one
+    // placement after another per wave
+    if (tid < k1 - k0) {
+      const AlnPair p = plc[k0 + tid];
+      const uint64_t rb = R.base_off[p.s], tb = T.base_off[p.t];
+      const uint32_t L = (uint32_t)(R.base_off[p.s + 1] - rb);
+      const uint32_t Lt = (uint32_t)(T.base_off[p.t + 1] - tb);
+      const int32_t lo = std::max<int32_t>(0, -p.off);
+      const int32_t hi = (int32_t)std::min<int64_t>((int64_t)L, (int64_t)Lt - p.off);
+      pm[tid] = VoteMeta{R.byte_off[p.s], rb, tb + (uint64_t)(int64_t)p.off, L, lo, hi, p.flags};
+    }
     __syncthreads();  // also orders the previous chunk's window clear
     const uint64_t g0 = g0s;
     uint32_t myspan = 0;
-    for (uint64_t k = k0 + wave; k < k1; k += kVoteThreads / 64) {
-      const AlnPair p = plc[k];
-      const uint32_t L = (uint32_t)(R.base_off[p.s + 1] - R.base_off[p.s]);
-      const uint32_t Lt = (uint32_t)(T.base_off[p.t + 1] - T.base_off[p.t]);
-      const uint8_t* rd = R.packed + R.byte_off[p.s];
-      const uint8_t* q = R.quals + R.base_off[p.s];
-      const bool rc = p.flags & 1;
-      const uint64_t tb = T.base_off[p.t];
-      const int64_t lo = std::max<int64_t>(0, -(int64_t)p.off);
-      const int64_t hi = std::min<int64_t>((int64_t)L, (int64_t)Lt - p.off);
+    for (uint32_t kk = wave; kk < k1 - k0; kk += kVoteThreads / 64) {
+      const VoteMeta m = pm[kk];
+      const uint32_t L = m.L;
+      const uint8_t* rd = R.packed + m.rbyte;
+      const uint8_t* q = R.quals + m.rbase;
+      const bool rc = m.flags & 1;
+      const int64_t lo = m.lo, hi = m.hi;
       for (int64_t i = lo + lane; i < hi; i += 64) {
         const uint32_t b = rc ? 3 - abase(rd, (uint32_t)(L - 1 - i)) : abase(rd, (uint32_t)i);
         const uint32_t qq = rc ? q[L - 1 - i] : q[i];
         if (!qq) continue;
-        const uint64_t col = tb + (uint64_t)(i + p.off);
+        const uint64_t col = m.col0 + (uint64_t)i;
         const uint64_t d = col - g0;  // wraps (huge) when col < g0
         if (d < kVoteWin) {
-          atomicAdd(&win[d * 4 + b], qq);
+          atomicAdd(&win[b * kVoteStride + d], qq);
           myspan = std::max<uint32_t>(myspan, (uint32_t)d + 1);
         } else {
           atomicAdd(&votes[col * 4 + b], qq);
@@ -551,11 +572,12 @@ __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, cons
     if (myspan) atomicMax(&span, myspan);
     __syncthreads();
     const uint32_t sp = span;
-    for (uint32_t x = tid; x < sp * 4; x += kVoteThreads) {
-      const uint32_t v = win[x];
+    for (uint32_t x = tid; x < sp * 4; x += kVoteThreads) {  // x = column * 4 + base: coalesced global atomics
+      const uint32_t w = (x & 3) * kVoteStride + (x >> 2);
+      const uint32_t v = win[w];
       if (v) {
         atomicAdd(&votes[g0 * 4 + x], v);
-        win[x] = 0;
+        win[w] = 0;
       }
     }
   }
