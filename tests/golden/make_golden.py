@@ -32,6 +32,7 @@ def main():
     print({k: v.shape for k, v in out.items()})
     write_stage_fixtures(g, reads)
     write_fill_fixture(reads)
+    write_locs_ecj_fixture()
 
 
 def write_fill_fixture(reads):
@@ -84,8 +85,33 @@ def write_stage_fixtures(g, reads):
     print({k: v.shape for k, v in out.items()})
 
 
+def write_locs_ecj_fixture():
+    """UnipathLocs of the raw small reads on the K=96 graph of the fixture
+    fragments (rc mirrors, by-unipath order), and ErrorCorrectJump of a small
+    3-kb jump library against the small frag reads."""
+    from allpathslg_amd import ReadSet
+
+    reads = ReadSet.load(os.path.join(HERE, "frag_small.fastb"), os.path.join(HERE, "frag_small.qualb"))
+    frags = ReadSet.load(os.path.join(HERE, "frag_small_fill.fastb"))
+    g = oracle.unipaths(frags, 96)
+    locs, lst = oracle.unipath_locs(g, reads, 96, rc=True, sorted=True)
+    genome = synth_genome(10_000, 0xA11A7)
+    jumps = synth_reads(genome, 150, seed=0xA11A7 + 3, insert_mean=3000, insert_sd=300)
+    jumps.write_fastb(os.path.join(HERE, "jump_small.fastb"))
+    jumps.write_qualb(os.path.join(HERE, "jump_small.qualb"))
+    fixed, keep, st = oracle.error_correct_jump(reads, jumps, K=24)
+    out = {"locs": locs, "locs_stats": np.array([lst["n_placed"], lst["n_missing"]], np.uint64),
+           "ecj_packed": fixed.packed[: int(fixed.byte_off[-1])], "ecj_quals": fixed.quals, "ecj_keep": keep,
+           "ecj_stats": np.array([st[k] for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable",
+                                                  "n_solid")], np.uint64)}
+    np.savez_compressed(os.path.join(HERE, "locs_ecj_small.npz"), **out)
+    print({k: v.shape for k, v in out.items()}, lst, st)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["fill"]:
+    if sys.argv[1:] == ["locs_ecj"]:
+        write_locs_ecj_fixture()
+    elif sys.argv[1:] == ["fill"]:
         from allpathslg_amd import ReadSet
 
         write_fill_fixture(ReadSet.load(os.path.join(HERE, "frag_small.fastb"), os.path.join(HERE, "frag_small.qualb")))

@@ -47,3 +47,17 @@ def test_aligners_golden(gpu_ctx):
     assert np.array_equal(res, z["aln_sw"]) and np.array_equal(blk, z["aln_sw_blocks"])
     b, q = gpu_ctx.consensus(S, T, pairs)
     assert np.array_equal(b, z["aln_cons_bases"]) and np.array_equal(q, z["aln_cons_quals"])
+
+
+def test_locs_and_ecj_golden(gpu_ctx):
+    z = np.load(os.path.join(GOLDEN, "locs_ecj_small.npz"))
+    _, reads, frags, _, _ = _load()
+    gpu_ctx.unipaths(frags, 96)
+    locs, st = gpu_ctx.unipath_locs(reads, rc=True, sorted=True)
+    assert np.array_equal(locs, z["locs"]) and [st["n_placed"], st["n_missing"]] == z["locs_stats"].tolist()
+    jumps = ReadSet.load(os.path.join(GOLDEN, "jump_small.fastb"), os.path.join(GOLDEN, "jump_small.qualb"))
+    fixed, keep, est = gpu_ctx.error_correct_jump(reads, jumps, K=24)
+    assert np.array_equal(fixed.packed[: int(fixed.byte_off[-1])], z["ecj_packed"])
+    assert np.array_equal(fixed.quals, z["ecj_quals"]) and np.array_equal(keep, z["ecj_keep"])
+    keys = ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid")
+    assert [est["precorrect"][k] for k in keys] == z["ecj_stats"].tolist()

@@ -105,3 +105,21 @@ def test_empty_and_short_reads():
     reads = ReadSet.from_sequences([genome[:50], genome[100:196], np.zeros(0, np.uint8)])
     locs, st = oracle.unipath_locs(g, reads, K)
     assert st["n_placed"] == 1 and len(locs) == 2 and locs[0, 0] == 1
+
+
+def test_oracle_against_golden_locs_and_ecj():
+    """The restatements reproduce the committed fixtures (tests/golden,
+    make_golden.py write_locs_ecj_fixture)."""
+    import os
+
+    gdir = os.path.join(os.path.dirname(__file__), "golden")
+    z = np.load(os.path.join(gdir, "locs_ecj_small.npz"))
+    reads = ReadSet.load(os.path.join(gdir, "frag_small.fastb"), os.path.join(gdir, "frag_small.qualb"))
+    frags = ReadSet.load(os.path.join(gdir, "frag_small_fill.fastb"))
+    g = oracle.unipaths(frags, 96)
+    locs, st = oracle.unipath_locs(g, reads, 96, rc=True, sorted=True)
+    assert np.array_equal(locs, z["locs"]) and [st["n_placed"], st["n_missing"]] == z["locs_stats"].tolist()
+    jumps = ReadSet.load(os.path.join(gdir, "jump_small.fastb"), os.path.join(gdir, "jump_small.qualb"))
+    fixed, keep, est = oracle.error_correct_jump(reads, jumps, K=24)
+    assert np.array_equal(fixed.packed[: int(fixed.byte_off[-1])], z["ecj_packed"])
+    assert np.array_equal(fixed.quals, z["ecj_quals"]) and np.array_equal(keep, z["ecj_keep"])
