@@ -352,6 +352,7 @@ SIGNATURES = {
     "apg_unipath_locs_dev": (
         C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_void_p), _u64p, C.POINTER(apg_uloc_stats)]),
     "apg_unibases_dev": (C.c_int, [_P, C.POINTER(_P)]),
+    "apg_device_copy": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
     "apg_dreads_shape": (C.c_int, [_P, _P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),

@@ -326,6 +326,16 @@ int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
   return APG_OK;
 }
 
+int apg_device_copy(apg_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes) {
+  APG_REQUIRE(ctx, "apg_device_copy: NULL ctx");
+  if (!bytes) return APG_OK;
+  APG_REQUIRE(d_dst && d_src, "apg_device_copy: NULL pointer");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_CHECK_HIP(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  return APG_OK;
+}
+
 void apg_free(void* p) { std::free(p); }
 
 }  // extern "C"

@@ -395,6 +395,10 @@ class Context:
             L.apg_free(p)
         return out, st.as_dict()
 
+    def device_copy(self, d_dst: int, d_src: int, nbytes: int) -> None:
+        """Device-to-device copy on libapg's stream (library output -> caller buffer)."""
+        check(lib().apg_device_copy(self._h, C.c_void_p(d_dst), C.c_void_p(d_src), nbytes), "apg_device_copy")
+
     def unibases_dev(self) -> "DeviceReads":
         """The last build's unibases as a device read set (aligner targets)."""
         d = DeviceReads(self, None)

@@ -66,6 +66,8 @@ def parse():
                    help="read placements of the aligner line (gap-free, banded SW, consensus); 0 = skip")
     p.add_argument("--align-band", type=int, default=8)
     p.add_argument("--align-target-len", type=int, default=50_000)
+    p.add_argument("--jump-pairs", type=int, default=2_000_000,
+                   help="jump library of the placement line (0 = none)")
     p.add_argument("--no-placement", dest="placement", action="store_false",
                    help="skip the UnipathLocs line (reads placed on the step's unipaths + aligners)")
     p.add_argument("--verbose", action="store_true")
@@ -255,6 +257,65 @@ def placement_bench(ctx, dreads, a, reps: int = 3):
         "columns_voted": float(voted.mean()) if nt else None,
     }
     dT.free()
+    return out
+
+
+def jump_bench(ctx, dsrc, genome, a, reps: int = 2):
+    """Jump-library line (BASELINE configs[2]): a synthetic 3-kb
+    jump library (2 M pairs, RF-like insert 3000 +- 300 from the simulator)
+    corrected against the frag reads' solid set and trimmed
+    (apg_error_correct_jump_dev), then placed on the step's K=96 unipaths
+    (apg_unipath_locs_dev).  Check: pairs with both ends on one unipath sit
+    ~3 kb apart on opposite strands — the links scaffolding would use."""
+    jumps = synth_reads(genome, a.jump_pairs, seed=a.seed + 17, insert_mean=3000, insert_sd=300, threads=16)
+    djs = ctx.upload(jumps)
+    dj = ctx.upload(jumps)
+    keep = torch.empty(max(jumps.n_reads, 1), dtype=torch.int32, device="cuda")
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.copy_reads(dj, djs)
+        st = ctx.error_correct_jump(dsrc, dj, d_keep=keep.data_ptr())
+        p, n, lst = ctx.unipath_locs(dj, rc=True, sorted=False)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    kt = ctx.kernel_times()
+    ms = {k: v[0] / max(v[1], 1) * v[1] / reps for k, v in kt.items()}
+    # pair links: read A's first forward location (u, s_a) and the rc mirror
+    # of read B's first location (u', s_b'); on one unipath the pair spans
+    # s_b' + L - s_a bases (the simulator's pairs face each other)
+    p, n, lst = ctx.unipath_locs(dj, rc=True, sorted=False)
+    loc = torch.empty((max(n, 1), 4), dtype=torch.int32, device="cuda")
+    ctx.device_copy(loc.data_ptr(), p, 16 * n)
+    Lc = loc[:n].cpu().numpy()
+    nr = jumps.n_reads
+    fu = np.full(nr, -1, np.int64)
+    fs = np.zeros(nr, np.int64)
+    mu = np.full(nr, -1, np.int64)
+    ms_ = np.zeros(nr, np.int64)
+    for flag, U, S in ((0, fu, fs), (1, mu, ms_)):
+        rows = Lc[Lc[:, 3] == flag]
+        if len(rows):
+            _, idx = np.unique(rows[:, 0], return_index=True)
+            U[rows[idx, 0]] = rows[idx, 1]
+            S[rows[idx, 0]] = rows[idx, 2]
+    a_, b_ = np.arange(0, nr - 1, 2), np.arange(1, nr, 2)
+    same = (fu[a_] >= 0) & (fu[a_] == mu[b_])
+    seps = (ms_[b_] + 100 - fs[a_])[same]
+    out = {
+        "workload": (f"{a.jump_pairs} synthetic jump pairs (insert 3000 +- 300) corrected against the step's "
+                     f"{dsrc.n_reads} frag reads (solid set recounted), trimmed, placed on the step's unipaths"),
+        "wall_ms_per_pass": wall * 1e3,
+        "kernels_ms": ms,
+        "ecj_stats": st,
+        "locs_stats": lst,
+        "pairs_on_one_unipath": int(len(seps)),
+        "median_separation": float(np.median(seps)) if len(seps) else None,
+        "checks": {"separation_about_3kb": bool(len(seps) and 2500 < np.median(seps) < 3500),
+                   "most_jump_reads_kept": st["bases_kept"] > 0.5 * jumps.n_bases},
+    }
+    dj.free()
+    djs.free()
     return out
 
 
@@ -520,6 +581,8 @@ def main():
         placement = placement_bench(ctx, dreads, a)
         if not a.no_cpu_baseline:
             placement["cpu_baseline"] = placement_cpu_baseline(genome, a)
+        if a.jump_pairs > 0:
+            placement["jumps"] = jump_bench(ctx, dsrc, genome, a)
 
     if rank == 0:
         total_reads = world * reads.n_reads * a.steps

@@ -99,6 +99,11 @@ int apg_dreads_shape(apg_ctx* ctx, const apg_dreads* dr, uint64_t* n_reads, uint
  * read set to its uploaded state without a host round trip. */
 int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src);
 
+/* Device-to-device copy on the context's stream (synchronous): moves a
+ * library-owned device output (e.g. apg_unipath_locs_dev) into a caller
+ * buffer. */
+int apg_device_copy(apg_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes);
+
 /* Fill byte_off[0..n] from base_off[0..n]. */
 int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_off);
 
