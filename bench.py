@@ -73,7 +73,7 @@ def parse():
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--sharded", action="store_true",
                    help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v11", "traffic.json"),
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v13", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     return p.parse_args()
 
