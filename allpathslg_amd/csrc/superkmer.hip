@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
           for (uint32_t t = 0; t < nk; ++t)
             if (tcnt[islot[ex + t]] < o.min_solid) m |= 1u << t;
           if (o.wrec) {
-            if (c0 + tid < nr) o.wrec[b] = m;
+            if (m) o.wrec[b] = m;  // zeroed beforehand: only records with weak K-mers write
           } else if (m) {
             const uint32_t sh = (uint32_t)(b & 63);
             atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
           }
           __syncthreads();
           if (o.wrec) {
-            if (c0 + tid < nr) o.wrec[cpos[tid]] = wmask[tid];
+            if (c0 + tid < nr && wmask[tid]) o.wrec[cpos[tid]] = wmask[tid];
           } else if (c0 + tid < nr && wmask[tid]) {
             const uint64_t b = cpos[tid], m = wmask[tid];
             const uint32_t sh = (uint32_t)(b & 63);
@@ -503,7 +503,7 @@ __global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __re
           }
         }
       }
-      if (wrec) wrec[r.pos] = m;
+      if (wrec && m) wrec[r.pos] = m;
     }
   }
 }
