@@ -72,6 +72,8 @@ def parse():
                    help="jump library of the placement line (0 = none)")
     p.add_argument("--no-placement", dest="placement", action="store_false",
                    help="skip the UnipathLocs line (reads placed on the step's unipaths + aligners)")
+    p.add_argument("--overlap", action="store_true",
+                   help="run the K=25 spectrum on a second stream concurrently with correction/fill/unipaths")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--sharded", action="store_true",
                    help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
@@ -400,9 +402,23 @@ def main():
     backend = HipShardBackend(ctx)
     fill = {"out": None}  # device read set of the filled fragments, reused every step
 
+    # --overlap: the K=25 spectrum of the pristine reads runs on a second
+    # context (its own HIP stream, host thread) concurrently with the
+    # correction / fill / unipath chain on the working copy
+    overlap = a.overlap and not sharded and not a.spectrum_only
+    ctx_s = Context(device=local, timing=True, verbose=a.verbose) if overlap else None
+    pool = None
+    if overlap:
+        from concurrent.futures import ThreadPoolExecutor
+
+        pool = ThreadPoolExecutor(max_workers=1)
+
     def step():
+        fut = pool.submit(ctx_s.kmer_spectrum, dsrc, a.K) if overlap else None
         ctx.copy_reads(dreads, dsrc)
-        if not sharded:
+        if overlap:
+            pass
+        elif not sharded:
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
             hist, st = sharded_spectrum(backend, dreads, a.K)
@@ -427,6 +443,8 @@ def main():
                     uin = fill["out"]
                 del solid
                 ust = sharded_unipaths(backend, uin, a.K_unipath)
+        if fut is not None:
+            hist, st = fut.result()
         return hist, st, pst, ust, fst
 
     for _ in range(a.warmup):
@@ -434,6 +452,8 @@ def main():
     free_b, total_b = torch.cuda.mem_get_info()
     torch.cuda.synchronize()
     ctx.reset_timing()
+    if ctx_s is not None:
+        ctx_s.reset_timing()
 
     if sharded:
         dist.barrier()
@@ -496,6 +516,10 @@ def main():
 
     # Roofline of the dominant kernel, from HIP events on libapg's stream.
     kt = ctx.kernel_times()
+    if ctx_s is not None:  # the concurrent spectrum context's kernels
+        for k, v in ctx_s.kernel_times().items():
+            o = kt.get(k, (0.0, 0, 0))
+            kt[k] = (o[0] + v[0], o[1] + v[1], o[2] + v[2])
     dom = max(kt.items(), key=lambda kv: kv[1][0])
     name, (ms, launches, nbytes) = dom
     per_launch_ms = ms / max(launches, 1)
@@ -651,6 +675,8 @@ def main():
         dfrags.free()
     if fill["out"] is not None:
         fill["out"].free()
+    if ctx_s is not None:
+        ctx_s.close()
     ctx.close()
     if sharded:
         dist.destroy_process_group()
