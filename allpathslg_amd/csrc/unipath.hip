@@ -2615,7 +2615,6 @@ int apg_urec_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, u
   APG_REQUIRE(n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
               "apg_urec_count: n_shards must be a power of two <= 8");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
-  if (ctx) ctx->gstate.valid = false;
   const UskP p = make_uskp(K);
   std::vector<uint64_t> h, kd;
   uint32_t G = 0;
