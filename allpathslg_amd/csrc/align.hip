@@ -548,25 +548,43 @@ __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, cons
     __syncthreads();  // also orders the previous chunk's window clear
     const uint64_t g0 = g0s;
     uint32_t myspan = 0;
-    for (uint32_t kk = wave; kk < k1 - k0; kk += kVoteThreads / 64) {
-      const VoteMeta m = pm[kk];
-      const uint32_t L = m.L;
+    // two placements per wave step: both placements' bases and qualities are
+    // loaded before either one's votes, so their load latencies overlap
+    constexpr uint32_t NW = kVoteThreads / 64;
+    auto vote = [&](const VoteMeta& m, int64_t i, uint32_t b, uint32_t qq) {
+      const uint64_t col = m.col0 + (uint64_t)i;
+      const uint64_t d = col - g0;  // wraps (huge) when col < g0
+      if (d < kVoteWin) {
+        atomicAdd(&win[b * kVoteStride + d], qq);
+        myspan = std::max<uint32_t>(myspan, (uint32_t)d + 1);
+      } else {
+        atomicAdd(&votes[col * 4 + b], qq);
+      }
+    };
+    auto fetch = [&](const VoteMeta& m, int64_t i, uint32_t* b, uint32_t* qq) {
       const uint8_t* rd = R.packed + m.rbyte;
       const uint8_t* q = R.quals + m.rbase;
-      const bool rc = m.flags & 1;
-      const int64_t lo = m.lo, hi = m.hi;
-      for (int64_t i = lo + lane; i < hi; i += 64) {
-        const uint32_t b = rc ? 3 - abase(rd, (uint32_t)(L - 1 - i)) : abase(rd, (uint32_t)i);
-        const uint32_t qq = rc ? q[L - 1 - i] : q[i];
-        if (!qq) continue;
-        const uint64_t col = m.col0 + (uint64_t)i;
-        const uint64_t d = col - g0;  // wraps (huge) when col < g0
-        if (d < kVoteWin) {
-          atomicAdd(&win[b * kVoteStride + d], qq);
-          myspan = std::max<uint32_t>(myspan, (uint32_t)d + 1);
-        } else {
-          atomicAdd(&votes[col * 4 + b], qq);
-        }
+      if (m.flags & 1) {
+        *b = 3 - abase(rd, (uint32_t)(m.L - 1 - i));
+        *qq = q[m.L - 1 - i];
+      } else {
+        *b = abase(rd, (uint32_t)i);
+        *qq = q[i];
+      }
+    };
+    const uint32_t nk = (uint32_t)(k1 - k0);
+    for (uint32_t kk = wave; kk < nk; kk += 2 * NW) {
+      const bool hasB = kk + NW < nk;
+      const VoteMeta ma = pm[kk];
+      const VoteMeta mb = hasB ? pm[kk + NW] : ma;
+      const int64_t na = (int64_t)ma.hi - ma.lo, nb = hasB ? (int64_t)mb.hi - mb.lo : 0;
+      const int64_t n = na > nb ? na : nb;
+      for (int64_t t = lane; t < n; t += 64) {
+        uint32_t ba = 0, qa = 0, bb = 0, qb = 0;
+        if (t < na) fetch(ma, ma.lo + t, &ba, &qa);
+        if (t < nb) fetch(mb, mb.lo + t, &bb, &qb);
+        if (qa) vote(ma, ma.lo + t, ba, qa);
+        if (qb) vote(mb, mb.lo + t, bb, qb);
       }
     }
     if (myspan) atomicMax(&span, myspan);
