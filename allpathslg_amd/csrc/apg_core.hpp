@@ -174,6 +174,8 @@ struct apg_ctx {
   bool pc_ext_valid = false;
   uint64_t clean_gen = 0;
   bool clean_valid = false;
+  // Capacity for the next single-pass candidate write (last count + 25 %).
+  uint64_t pc_cand_hint = 0;
 };
 
 namespace apg {

@@ -630,7 +630,12 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     const uint64_t* __restrict__ base_off, const uint64_t* __restrict__ byte_off, const uint8_t* __restrict__ packed,
     const uint8_t* __restrict__ quals, uint64_t n_reads, int K, uint32_t maxq,
     const unsigned long long* __restrict__ weak, uint32_t* __restrict__ tcnt, const uint64_t* __restrict__ toff,
-    PcCand* __restrict__ cand, uint64_t* __restrict__ cstart, uint32_t* __restrict__ ccnt) {
+    PcCand* __restrict__ cand, uint64_t* __restrict__ cstart, uint32_t* __restrict__ ccnt,
+    unsigned long long* __restrict__ tctr = nullptr, uint64_t cap = 0) {
+  // tctr (WRITE only): single-pass mode — each tile reserves its run of the
+  // candidate array with one atomic instead of a counted, scanned offset; a
+  // run past `cap` is not written and tctr ends > cap (the host reruns).
+  __shared__ unsigned long long tbase_sm;
   __shared__ __attribute__((aligned(16))) uint8_t qs[kPcTileQ + 16];
   __shared__ unsigned long long ws[kPcTileW];
   __shared__ uint32_t list[WRITE ? kPcTileList : 1];  // read in tile << 16 | position
@@ -671,7 +676,18 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     if constexpr (!WRITE) {
       if (tid == 0) tcnt[r0 / kPcTileReads] = tot;
     } else {
-      const uint64_t tb = toff[r0 / kPcTileReads];
+      uint64_t tb;
+      if (tctr) {
+        if (tid == 0) tbase_sm = tot ? atomicAdd(tctr, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        tb = tbase_sm;
+        if (tb + tot > cap) {  // over capacity: nothing of this tile is written
+          __syncthreads();
+          continue;
+        }
+      } else {
+        tb = toff[r0 / kPcTileReads];
+      }
       if (r < n_reads) {
         cstart[r] = tb + ex;
         ccnt[r] = n;
@@ -891,29 +907,56 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     APG_TRY(workspace_t(ctx, "pc_tcnt", std::max<uint64_t>(ntiles, 1), &tcnt));
     APG_TRY(workspace_t(ctx, "pc_toff", ntiles + 1, &toff));
     const uint32_t cgrid = grid_for(ctx, dr->n_reads, kPcTileReads);
-    // reads' offsets + quals + weak bits in; tile counts out
-    kbegin(ctx, "pc_candidates", dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads);
-    if (dr->n_reads)
-      k_pc_candidates<false><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
-          dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, tcnt,
-          nullptr, nullptr, nullptr, nullptr);
-    kend(ctx);
-    APG_CHECK_HIP(hipGetLastError());
-    APG_TRY(scan_u32_u64(ctx, tcnt, ntiles, toff, "pct"));
+    // Single pass when the previous call's candidate count gives a capacity:
+    // tiles reserve their runs with one atomic each (no counting pass, no
+    // scan); an overflow falls back to count + scan + write.
     uint64_t ncand = 0;
-    APG_CHECK_HIP(hipMemcpyAsync(&ncand, toff + ntiles, 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
     PcCand* cand = nullptr;
-    APG_TRY(workspace_t(ctx, "pc_cand", std::max<uint64_t>(ncand, 1), &cand));
-    // reads' offsets + quals + weak bits in; runs and records out
-    kbegin(ctx, "pc_cand_write",
-           dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads + 12 * dr->n_reads + ncand * sizeof(PcCand));
-    if (dr->n_reads)
+    bool have = false;
+    const uint64_t cap = ctx->pc_cand_hint;
+    if (cap && dr->n_reads) {
+      unsigned long long* ctr = nullptr;
+      APG_TRY(workspace_t(ctx, "pc_cand_ctr", 1, &ctr));
+      APG_CHECK_HIP(hipMemsetAsync(ctr, 0, 8, ctx->stream));
+      APG_TRY(workspace_t(ctx, "pc_cand", cap, &cand));
+      kbegin(ctx, "pc_cand_write",
+             dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads + 12 * dr->n_reads);
       k_pc_candidates<true><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
           dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, nullptr,
-          toff, cand, cstart, ccnt);
-    kend(ctx);
-    APG_CHECK_HIP(hipGetLastError());
+          nullptr, cand, cstart, ccnt, ctr, cap);
+      kend(ctx);
+      APG_CHECK_HIP(hipGetLastError());
+      unsigned long long hn = 0;
+      APG_CHECK_HIP(hipMemcpyAsync(&hn, ctr, 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      ncand = hn;
+      have = ncand <= cap;
+      if (have) kbytes_add(ctx, "pc_cand_write", ncand * sizeof(PcCand));
+    }
+    if (!have) {
+      // reads' offsets + quals + weak bits in; tile counts out
+      kbegin(ctx, "pc_candidates", dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads);
+      if (dr->n_reads)
+        k_pc_candidates<false><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
+            dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, tcnt,
+            nullptr, nullptr, nullptr, nullptr);
+      kend(ctx);
+      APG_CHECK_HIP(hipGetLastError());
+      APG_TRY(scan_u32_u64(ctx, tcnt, ntiles, toff, "pct"));
+      APG_CHECK_HIP(hipMemcpyAsync(&ncand, toff + ntiles, 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      APG_TRY(workspace_t(ctx, "pc_cand", std::max<uint64_t>(ncand, 1), &cand));
+      // reads' offsets + quals + weak bits in; runs and records out
+      kbegin(ctx, "pc_cand_write",
+             dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads + 12 * dr->n_reads + ncand * sizeof(PcCand));
+      if (dr->n_reads)
+        k_pc_candidates<true><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
+            dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak,
+            nullptr, toff, cand, cstart, ccnt);
+      kend(ctx);
+      APG_CHECK_HIP(hipGetLastError());
+    }
+    ctx->pc_cand_hint = ncand + ncand / 4 + 4096;
     uint8_t* dec = nullptr;
     APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));
     // candidate records in, decisions out (+ 64 B per extension lookup, after the sync)
