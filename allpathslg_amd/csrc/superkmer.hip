@@ -155,19 +155,18 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
   for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  uint64_t tile0 = 0;
-  uint32_t tile_n = 0;
+  uint64_t rbase = 0;  // base offset of this thread's read (records with positions)
   auto f = [&](const uint8_t* rd, uint32_t, uint32_t a, uint32_t n, uint32_t key) {
     const SK16 x = make_rec(rd, a, n, key, p.K);
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
-    uint64_t pos = 0;
-    if constexpr (OutWantsPos<O>::value) pos = rv.base_off[tile0 + (tile_n ? threadIdx.x : 0)] + a;
-    rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
+    rec_put(out, atomicAdd(&cur[d], 1ull), x, rbase + a);
   };
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
-    tile0 = t0;
-    tile_n = n;
+    if constexpr (OutWantsPos<O>::value) {  // once per read, not per record
+      const uint64_t r = t0 + (n ? threadIdx.x : 0);
+      rbase = (n ? threadIdx.x < n : threadIdx.x == 0) ? rv.base_off[r] : 0;
+    }
     if (n)
       sk_walk<kSkThreads, false>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
     else
