@@ -354,6 +354,15 @@ __global__ void __launch_bounds__(256) k_fill_write(FillReads rv, const FillRec*
         o[y] = A[y];
         continue;
       }
+      if (t0 >= La + d && t0 + 4 <= I) {  // four bases of F = rc(B): B[S0-3 .. S0] reversed, complemented
+        const uint32_t S0 = Lf - 1 - (t0 - La - d + ov);
+        const uint32_t e = S0 - 3, sh = 2 * (e & 3);
+        const uint32_t w16 = (uint32_t)B[e >> 2] | ((uint32_t)B[(e >> 2) + 1] << 8);
+        const uint32_t x = (w16 >> sh) & 0xff;  // b(S0-3) b(S0-2) b(S0-1) b(S0), LSB-first
+        const uint32_t r = ((x & 3) << 6) | (((x >> 2) & 3) << 4) | (((x >> 4) & 3) << 2) | (x >> 6);
+        o[y] = (uint8_t)(~r & 0xff);
+        continue;
+      }
       uint32_t acc = 0;
       for (uint32_t t = t0; t < t0 + 4 && t < I; ++t) {
         uint32_t b;
