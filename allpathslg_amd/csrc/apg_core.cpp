@@ -228,6 +228,7 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
   auto* d = new (std::nothrow) apg_dreads();
   if (!d) return APG_E_NOMEM;
   d->ctx = ctx;
+  d->device = ctx->device;
   static std::atomic<uint64_t> g_gen{1};
   d->gen = g_gen.fetch_add(1);
   const uint64_t n = r->n_reads;
@@ -239,7 +240,9 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
   uint64_t sh = 0x9e3779b97f4a7c15ull ^ n;
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t len = r->base_off[i + 1] - r->base_off[i];
+    // the byte stride too: padded byte_off layouts with equal lengths differ
     sh = (sh ^ len) * 0x100000001b3ull;
+    sh = (sh ^ (r->byte_off[i + 1] - r->byte_off[i])) * 0x100000001b3ull;
     if ((r->byte_off[i + 1] - r->byte_off[i]) * 4 < len) {
       delete d;
       set_error("apg_reads_upload: byte_off inconsistent with base_off (read " + std::to_string(i) + ")");
@@ -283,7 +286,7 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
 
 void apg_reads_free(apg_dreads* d) {
   if (!d) return;
-  if (d->ctx) (void)hipSetDevice(d->ctx->device);
+  (void)hipSetDevice(d->device);
   if (d->d_base_off) (void)hipFree(d->d_base_off);
   if (d->d_byte_off) (void)hipFree(d->d_byte_off);
   if (d->d_packed) (void)hipFree(d->d_packed);

@@ -56,7 +56,8 @@ struct KernelStat {
 
 // Device-resident read set.
 struct apg_dreads {
-  apg_ctx* ctx = nullptr;
+  apg_ctx* ctx = nullptr;  // producing context: identity only, never dereferenced (it may be destroyed first)
+  int device = 0;          // device ordinal of the buffers (apg_reads_free needs no live context)
   uint64_t gen = 0;  // unique per upload (cache key for per-read-set plans)
   uint64_t n_reads = 0;
   uint64_t n_bases = 0;
@@ -67,7 +68,7 @@ struct apg_dreads {
   uint8_t* d_packed = nullptr;
   uint8_t* d_quals = nullptr;      // optional
   std::vector<uint64_t> h_base_off;  // kept for host-side sizing (uploads only)
-  uint64_t shape_hash = 0;  // hash of the read lengths (uploads; 0 = not known): cheap shape identity
+  uint64_t shape_hash = 0;  // hash of the read lengths and byte strides (uploads; 0 = not known): cheap shape identity
   // device-produced sets (apg_fill_fragments_dev): buffer capacities, reused
   // when the same object is passed back in
   bool fill_owned = false;

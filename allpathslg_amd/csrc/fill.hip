@@ -397,6 +397,7 @@ static int filled_alloc(apg_ctx* ctx, apg_dreads** io, uint64_t n, uint64_t nbas
     d = new (std::nothrow) apg_dreads();
     if (!d) return APG_E_NOMEM;
     d->ctx = ctx;
+    d->device = ctx->device;
     d->fill_owned = true;
     *io = d;
   }

@@ -700,8 +700,13 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R>, kSkThreads, nb)
                               : resident_grid(ctx, k_sk_bucket<false, R>, kSkThreads, nb);
   for (int attempt = 0;; ++attempt) {
-    // weak pass: the records a second time (L2-hot) + 8 B per weak-bit word touched
-    kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) * (o.weak ? 2 : 1) + (nb + 1) * 8);
+    // Algorithmic bytes (inputs read once + outputs written once): the records
+    // and bucket offsets; the weak output (one bit per K-mer instance, or a
+    // 4-byte mask per record in the multi-GPU form); the solid list is added
+    // once its length is known.  The weak pass's L2-hot re-read of the
+    // records is not algorithmic and is not counted.
+    const uint64_t weak_out = o.weak ? n_kmers / 8 : (o.wrec ? n * 4 : 0);
+    kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) + (nb + 1) * 8 + weak_out);
     if (solid)
       k_sk_bucket<true, R><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
     else
@@ -744,6 +749,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
       APG_TRY(sync(ctx));
     }
+    if (solid) kbytes_add(ctx, "sk_bucket_solid", std::min<uint64_t>(hs[2], solid_cap) * 8);
     if (!solid || hs[2] <= solid_cap) {
       res->n_distinct = hs[0];
       res->n_overflow_buckets = hs[1];
