@@ -263,6 +263,7 @@ SIGNATURES = {
     "apg_reads_free": (None, [_P]),
     "apg_dreads_count": (C.c_uint64, [_P]),
     "apg_reads_copy_dev": (C.c_int, [_P, _P, _P]),
+    "apg_reads_concat_dev": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.c_uint32, C.POINTER(_P)]),
     "apg_byte_offsets": (C.c_int, [_u64p, C.c_uint64, _u64p]),
     "apg_kmer_hash": (C.c_uint64, [C.c_int, C.c_uint64]),
     "apg_kmer_unhash": (C.c_uint64, [C.c_int, C.c_uint64]),

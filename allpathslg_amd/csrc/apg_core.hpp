@@ -72,7 +72,8 @@ struct apg_dreads {
   // device-produced sets (apg_fill_fragments_dev): buffer capacities, reused
   // when the same object is passed back in
   bool fill_owned = false;
-  uint64_t cap_reads = 0, cap_bytes = 0;
+  bool concat_owned = false;  // apg_reads_concat_dev output
+  uint64_t cap_reads = 0, cap_bytes = 0, cap_quals = 0;
 };
 
 struct apg_ctx {

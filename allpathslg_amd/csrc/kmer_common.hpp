@@ -118,6 +118,14 @@ struct KmerRoller {
 // ---- wave / block primitives (wave64) -------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// LDS hand-off between the lanes of ONE wave (no block barrier): LDS serves a
+// wave's operations in order, so this only has to stop the compiler from
+// moving LDS accesses across it.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1; }
 
 // Lanes of this wave holding the same nb-bit digit (a 64-wide match_any built
@@ -180,6 +188,22 @@ __device__ __forceinline__ T wave_inclusive_scan(T x) {
     if (lane >= o) x += y;
   }
   return x;
+}
+
+// 32-bit inclusive wave scan on DPP lane moves (no LDS round trips): a
+// Kogge-Stone scan inside each 16-lane row (row_shr 1, 2, 4, 8), then row
+// 15's total broadcast into rows 1 and 3 and row 31's into rows 2 and 3
+// (GFX9 row_bcast, which gfx950 keeps).  Lanes with no source add 0.
+template <>
+__device__ __forceinline__ uint32_t wave_inclusive_scan<uint32_t>(uint32_t x) {
+  int v = (int)x;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)v;
 }
 
 // Exclusive scan across the block (blockDim.x <= 1024, multiple of 64).

@@ -32,6 +32,7 @@
 // n <= 41 - K.  Algorithmic bytes per 100-bp read at K = 25: ~12 records of
 // 16 B (vs 76 x 8 B hash records).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -51,6 +52,7 @@ constexpr uint64_t kSkBucketKmers = 4096;  // K-mer instances per bucket the pla
 constexpr uint32_t kSkTab = 2048;          // LDS table slots (u64 canonical K-mer + u32 count)
 constexpr int kSkHistBins = 128;  // LDS spectrum bins (counts above go to global atomics); keeps k_sk_bucket<false> under 40 KiB LDS = 4 blocks/CU
 constexpr uint32_t kSkSlotCap = 6144;  // weak pass: instances per bucket with a recorded slot (LDS: 3 blocks/CU)
+constexpr uint32_t kSkWaveSlots = kSkSlotCap / (kSkThreads / 64);  // recorded slots per wave
 constexpr int kSkMaxW = 17;  // w = K - m + 1 <= 17 for K <= 32
 
 struct SkP {
@@ -188,18 +190,56 @@ __global__ void k_sk_digit_starts(const uint64_t* __restrict__ omat, uint32_t nd
 // Canonical K-mer t (t + K <= 40) of a record: the record's bases as an
 // 80-bit LSB-first string, a 64-bit window at base t, fw = rev2 >> (64 - 2K),
 // rc = complement (already most-significant-first).
+// Branch-free: the 80-bit string is three 32-bit limbs a0..a2 (a2 holds
+// bases 32..39); t <= 31, so the window is a funnel shift by 2t < 64 —
+// one limb select for 2t >= 32, then two v_alignbit.
 __device__ __forceinline__ uint64_t rec_kmer(const SK16& r, uint32_t t, const SkP& p) {
-  const uint64_t lo = (r.w0 >> 48) | (r.w1 << 16), hi = r.w1 >> 48;
+  const uint32_t a0 = (uint32_t)(r.w0 >> 48) | ((uint32_t)r.w1 << 16);
+  const uint32_t a1 = (uint32_t)(r.w1 >> 16);
+  const uint32_t a2 = (uint32_t)(r.w1 >> 48);
   const uint32_t sh = 2 * t;
-  const uint64_t W = sh == 0 ? lo : sh < 64 ? (lo >> sh) | (hi << (64 - sh)) : hi >> (sh - 64);
+  const bool up = sh >= 32;
+  const uint32_t b0 = up ? a1 : a0, b1 = up ? a2 : a1, b2 = up ? 0u : a2;
+  const uint32_t s5 = sh & 31;
+  const uint32_t w0 = __builtin_amdgcn_alignbit(b1, b0, s5), w1 = __builtin_amdgcn_alignbit(b2, b1, s5);
+  const uint64_t W = (uint64_t)w0 | ((uint64_t)w1 << 32);
   const uint64_t fw = sk_rev2(W) >> (64 - 2 * p.K);
   const uint64_t rc = ~W & p.hp.mask;
   return fw < rc ? fw : rc;
 }
 
-// Slot of a canonical K-mer in a 2^bits table.
+// Home of a canonical K-mer in a 2^bits table: the first slot of its aligned
+// group of kSkGrp slots.  The probe order is linear from there (group by
+// group), so a key sits before any empty slot of its probe sequence.
+constexpr uint32_t kSkGrp = 4;
 __device__ __forceinline__ uint32_t sk_slot(uint64_t c, int bits) {
-  return sk_fmix32((uint32_t)c ^ ((uint32_t)(c >> 32) * 0x9e3779b1u)) >> (32 - bits);
+  return (sk_fmix32((uint32_t)c ^ ((uint32_t)(c >> 32) * 0x9e3779b1u)) >> (32 - bits)) & ~(kSkGrp - 1);
+}
+
+// Find-or-claim the slot of key c in the LDS table: one 32-byte group read
+// (two ds_read_b128) answers most instances — a hit, or the first empty slot
+// to claim with one CAS.  Returns the slot, or kSkTab when the table is full.
+__device__ __forceinline__ uint32_t sk_tab_claim(unsigned long long* tkey, uint64_t c, uint32_t g) {
+  constexpr unsigned long long EMPTY = ~0ull;
+  for (uint32_t n = 0; n < kSkTab + kSkGrp;) {
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(&tkey[g]);
+    const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(&tkey[g + 2]);
+    const unsigned long long k[kSkGrp] = {a.x, a.y, b.x, b.y};
+    uint32_t j = kSkGrp;
+#pragma unroll
+    for (uint32_t q = kSkGrp; q-- > 0;)
+      if (k[q] == c || k[q] == EMPTY) j = q;  // the first in probe order
+    if (j == kSkGrp) {  // group full of other keys: the next group
+      g = (g + kSkGrp) & (kSkTab - 1);
+      n += kSkGrp;
+      continue;
+    }
+    if (k[j] == c) return g + j;
+    const unsigned long long old = atomicCAS(&tkey[g + j], EMPTY, (unsigned long long)c);
+    if (old == EMPTY || old == c) return g + j;
+    ++n;  // another key took that slot: look at the group again
+  }
+  return kSkTab;
 }
 
 struct SkOut {
@@ -229,33 +269,39 @@ __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, con
 // flatten the chunk to one K-mer per thread, inserted into the LDS table
 // keyed by the canonical K-mer (CAS, then count).  The occupied slots feed
 // the spectrum; solid mode appends khash of those with count >= min_solid.
-template <bool SOLID, typename R>
-__global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ rec,
+template <bool SOLID, typename R, int NT>
+__global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
                                                           const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
                                                           SkOut o) {
   constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
-  __shared__ unsigned long long tkey[kSkTab];
+  // recorded slots: kSkWaveSlots per wave (NT = 512: each wave sees ~1/8 of a bucket)
+  constexpr uint32_t kWaveSlots = NT >= 512 ? 1024 : kSkWaveSlots;
+  constexpr uint32_t kSlotCap = kWaveSlots * (NT / 64);
+  __shared__ __attribute__((aligned(16))) unsigned long long tkey[kSkTab];
   __shared__ uint32_t tcnt[kSkTab];
   __shared__ uint32_t lhist[kSkHistBins];
-  __shared__ __attribute__((aligned(16))) SK16 crec[kSkThreads];
-  __shared__ uint32_t koff[kSkThreads];
-  __shared__ uint8_t owner[kSkThreads * kSkBases];
-  __shared__ uint32_t scan_sm[64];
+  __shared__ __attribute__((aligned(16))) SK16 crec[NT];
+  __shared__ uint32_t koff[NT];
+  __shared__ __attribute__((aligned(16))) uint8_t owner[NT * kSkBases];
+  static_assert(64 * kSkBases >= kWaveSlots / 8 + 8, "a wave's weak bit array must fit in its owner-map slice");
+  __shared__ uint32_t scan_sm[32];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
-  // weak pass: table slot of each of the bucket's first kSkSlotCap K-mer
+  // weak pass: table slot of each of the bucket's first kSlotCap K-mer
   // instances (in record order), recorded while counting — slots never move
   // once claimed, so the weak pass reads final counts without probing.  A
   // bucket with more instances takes the probing fallback, whose per-chunk
   // record positions and weak masks reuse the same LDS.
-  __shared__ __attribute__((aligned(16))) uint16_t islot[WEAK ? kSkSlotCap : 4];
-  static_assert(!WEAK || kSkSlotCap * 2 >= kSkThreads * 12, "fallback scratch must fit in islot");
-  uint64_t* cpos = reinterpret_cast<uint64_t*>(islot);               // [kSkThreads]
-  uint32_t* wmask = reinterpret_cast<uint32_t*>(islot + 4 * kSkThreads);  // [kSkThreads]
+  __shared__ __attribute__((aligned(16))) uint16_t islot[WEAK ? kSlotCap : 4];
+  static_assert(!WEAK || kSlotCap * 2 >= NT * 4, "fallback scratch must fit in islot");
+  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  uint8_t* wown = owner + wv * (64 * kSkBases);  // this wave's owner-map slice
+  uint16_t* wslot = islot + (WEAK ? wv * kWaveSlots : 0);  // this wave's recorded slots
+  uint32_t* wmask = reinterpret_cast<uint32_t*>(islot);  // [NT] (probing fallback)
   constexpr unsigned long long EMPTY = ~0ull;
   constexpr int TB = __builtin_ctz(kSkTab);
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < kSkHistBins; i += kSkThreads) lhist[i] = 0;
+  for (uint32_t i = tid; i < kSkHistBins; i += NT) lhist[i] = 0;
   unsigned long long nd = 0;
   // The block's buckets bkt, bkt + grid, ... are one record stream: the next
   // chunk's record (this bucket's or the next bucket's first) and the next
@@ -283,52 +329,52 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
       nr = nnr;
       continue;
     }
-    for (uint32_t s = tid; s < kSkTab; s += kSkThreads) {
+    for (uint32_t s = tid; s < kSkTab; s += NT) {
       tkey[s] = EMPTY;
       tcnt[s] = 0;
     }
     if (tid == 0) ovf = 0;
-    uint32_t ibase = 0;  // the bucket's K-mer instances before this chunk (block-uniform)
-    for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
+    __syncthreads();
+    // Each wave flattens and inserts its own 64 records of every chunk with a
+    // wave scan and its own slice of the owner map: no block barriers until
+    // the bucket's counts are final.
+    uint32_t ibw = 0;  // this wave's K-mer instances before this chunk (wave-uniform)
+    for (uint32_t c0 = 0; c0 < nr; c0 += NT) {
       uint32_t nk = 0;
       if (c0 + tid < nr) {
         nk = (uint32_t)(pre.w0 >> 32) & 0xff;
         crec[tid] = rec_head(pre);
       }
-      if (c0 + kSkThreads < nr) {
-        if (c0 + kSkThreads + tid < nr) pre = rec[off + c0 + kSkThreads + tid];
+      if (c0 + NT < nr) {
+        if (c0 + NT + tid < nr) pre = rec[off + c0 + NT + tid];
       } else if (tid < nnr) {
         pre = rec[noff + tid];
       }
-      uint32_t tot;
-      const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);  // barrier: table clear visible
+      const uint32_t incl = wave_inclusive_scan<uint32_t>(nk);
+      const uint32_t ex = incl - nk;
+      const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
       koff[tid] = ex;
-      for (uint32_t u = 0; u < nk; ++u) owner[ex + u] = (uint8_t)tid;
-      __syncthreads();
-      for (uint32_t f = tid; f < tot; f += kSkThreads) {
-        const uint32_t i = owner[f];
+      for (uint32_t u = 0; u < nk; ++u) wown[ex + u] = (uint8_t)ln;
+      wave_lds_sync();
+      for (uint32_t f = ln; f < tot; f += 64) {
+        const uint32_t i = (wv << 6) + wown[f];
         const uint64_t c = rec_kmer(crec[i], f - koff[i], p);
-        uint32_t s = sk_slot(c, TB);
-        for (uint32_t probe = 0;; ++probe) {
-          if (probe == kSkTab) {
-            ovf = 1;  // table full: the bucket goes to the global path
-            break;
+        const uint32_t s = sk_tab_claim(tkey, c, sk_slot(c, TB));
+        const bool ok = s < kSkTab;
+        if (!ok) ovf = 1;  // table full: the bucket goes to the global path
+        if (ok) {
+          atomicAdd(&tcnt[s], 1u);
+          if constexpr (WEAK) {
+            if (ibw + f < kWaveSlots) wslot[ibw + f] = (uint16_t)s;
           }
-          unsigned long long old = tkey[s];  // hits (most instances) skip the CAS
-          if (old == EMPTY) old = atomicCAS(&tkey[s], EMPTY, (unsigned long long)c);
-          if (old == EMPTY || old == c) {
-            atomicAdd(&tcnt[s], 1u);
-            if constexpr (WEAK) {
-              if (ibase + f < kSkSlotCap) islot[ibase + f] = (uint16_t)s;
-            }
-            break;
-          }
-          s = (s + 1) & (kSkTab - 1);
         }
       }
-      ibase += tot;
-      __syncthreads();
+      ibw += tot;
+      wave_lds_sync();  // the next chunk overwrites this wave's crec / koff / owner slices
     }
+    // counts final; a wave past its recorded-slot capacity sends the whole
+    // bucket's weak pass to the probing fallback
+    const bool unrecorded = __syncthreads_or(WEAK && ibw > kWaveSlots);
     if (ovf) {
       if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
       __syncthreads();
@@ -338,15 +384,28 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
       continue;
     }
     if constexpr (WEAK) {
-      // Weak pass: the bucket's records again (L2-hot); each K-mer instance
-      // finds its final count in the table, weak ones (count < min_solid) set
-      // their bit at the instance's base position — one 64-bit atomic OR (two
-      // when the run straddles a word) per record holding a weak K-mer.
-      if ((o.weak || o.wrec) && ibase <= kSkSlotCap) {
-        // thread per record: its K-mers' slots are islot[ib + ex ..], their
-        // final counts give the record's weak mask directly
+      // Weak pass: each K-mer instance finds its final count in the table,
+      // weak ones (count < min_solid) set their bit at the instance's base
+      // position — one 64-bit atomic OR (two when the run straddles a word)
+      // per record holding a weak K-mer.
+      if ((o.weak || o.wrec) && !unrecorded) {
+        // (1) lane per K-mer instance of the wave: its recorded slot's final
+        // count -> one weak bit; 64 bits land as one ballot word (instances
+        // in record order, so a record's K-mers are consecutive bits).  The
+        // wave's owner-map slice is free by now and holds the bit array.
+        unsigned long long* wbits = reinterpret_cast<unsigned long long*>(wown);
+        for (uint32_t f0 = 0; f0 < ibw; f0 += 64) {
+          const uint32_t f = f0 + ln;
+          const bool wk = f < ibw && tcnt[wslot[f]] < o.min_solid;
+          const unsigned long long bal = __ballot(wk);
+          if (ln == 0) wbits[f0 >> 6] = bal;
+        }
+        wave_lds_sync();
+        // (2) thread per record (the same records the wave inserted): bits
+        // [ex, ex + nk) of the wave's array are its mask; the records are
+        // re-read from L2 for their positions
         uint32_t ib = 0;
-        for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
+        for (uint32_t c0 = 0; c0 < nr; c0 += NT) {
           uint32_t nk = 0;
           uint64_t b = 0;
           if (c0 + tid < nr) {
@@ -354,11 +413,16 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
             nk = (uint32_t)(r.w0 >> 32) & 0xff;
             b = r.pos;
           }
-          uint32_t tot;
-          const uint32_t ex = ib + block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);
+          const uint32_t incl = wave_inclusive_scan<uint32_t>(nk);
+          const uint32_t ex = ib + incl - nk;
+          const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
           uint32_t m = 0;
-          for (uint32_t t = 0; t < nk; ++t)
-            if (tcnt[islot[ex + t]] < o.min_solid) m |= 1u << t;
+          if (nk) {
+            const uint32_t w = ex >> 6, sh = ex & 63;
+            unsigned long long x = wbits[w] >> sh;
+            if (sh + nk > 64) x |= wbits[w + 1] << (64 - sh);
+            m = (uint32_t)x & (nk >= 32 ? ~0u : ((1u << nk) - 1));
+          }
           if (o.wrec) {
             if (m) o.wrec[b] = m;  // zeroed beforehand: only records with weak K-mers write
           } else if (m) {
@@ -367,46 +431,53 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
             if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
           }
           ib += tot;
-          __syncthreads();
         }
+        __syncthreads();
       } else if (o.weak || o.wrec) {
-        for (uint32_t c0 = 0; c0 < nr; c0 += kSkThreads) {
+        // probing fallback (a wave outgrew its recorded slots), wave-local
+        // like the insert loop: each instance looks its key up again
+        for (uint32_t c0 = 0; c0 < nr; c0 += NT) {
           uint32_t nk = 0;
+          uint64_t b = 0;
           if (c0 + tid < nr) {
             const R r = rec[off + c0 + tid];
             crec[tid] = rec_head(r);
-            cpos[tid] = r.pos;
+            b = r.pos;
             nk = (uint32_t)(r.w0 >> 32) & 0xff;
           }
           wmask[tid] = 0;
-          uint32_t tot;
-          const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);
+          const uint32_t incl = wave_inclusive_scan<uint32_t>(nk);
+          const uint32_t ex = incl - nk;
+          const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
           koff[tid] = ex;
-          for (uint32_t u = 0; u < nk; ++u) owner[ex + u] = (uint8_t)tid;
-          __syncthreads();
-          for (uint32_t f = tid; f < tot; f += kSkThreads) {
-            const uint32_t i = owner[f];
+          for (uint32_t u = 0; u < nk; ++u) wown[ex + u] = (uint8_t)ln;
+          wave_lds_sync();
+          for (uint32_t f = ln; f < tot; f += 64) {
+            const uint32_t i = (wv << 6) + wown[f];
             const uint32_t t = f - koff[i];
             const uint64_t c = rec_kmer(crec[i], t, p);
             uint32_t s = sk_slot(c, TB);
             while (tkey[s] != c) s = (s + 1) & (kSkTab - 1);  // inserted above: present
             if (tcnt[s] < o.min_solid) atomicOr(&wmask[i], 1u << t);
           }
-          __syncthreads();
-          if (o.wrec) {
-            if (c0 + tid < nr && wmask[tid]) o.wrec[cpos[tid]] = wmask[tid];
-          } else if (c0 + tid < nr && wmask[tid]) {
-            const uint64_t b = cpos[tid], m = wmask[tid];
-            const uint32_t sh = (uint32_t)(b & 63);
-            atomicOr(&o.weak[b >> 6], (unsigned long long)(m << sh));
-            if (sh && (m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)(m >> (64 - sh)));
+          wave_lds_sync();
+          const uint32_t m = wmask[tid];
+          if (c0 + tid < nr && m) {
+            if (o.wrec) {
+              o.wrec[b] = m;
+            } else {
+              const uint32_t sh = (uint32_t)(b & 63);
+              atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
+              if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
+            }
           }
-          __syncthreads();
+          wave_lds_sync();
         }
+        __syncthreads();
       }
     }
     uint32_t ns = 0;
-    for (uint32_t s = tid; s < kSkTab; s += kSkThreads)
+    for (uint32_t s = tid; s < kSkTab; s += NT)
       if (tkey[s] != EMPTY) {
         sk_spectrum_add(tcnt[s], lhist, o);
         ++nd;
@@ -418,7 +489,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
       if (tid == 0) sbase = tot ? atomicAdd(&o.gstats[2], (unsigned long long)tot) : 0ull;
       __syncthreads();
       const unsigned long long b = sbase;
-      for (uint32_t s = tid; s < kSkTab; s += kSkThreads)
+      for (uint32_t s = tid; s < kSkTab; s += NT)
         if (tkey[s] != EMPTY && tcnt[s] >= o.min_solid) {
           const unsigned long long at = b + j++;
           if (at < o.solid_cap) o.solid[at] = khash(p.hp, tkey[s]);
@@ -431,7 +502,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_bucket(const R* __restrict__ 
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
-  for (uint32_t i = tid; i < lim; i += kSkThreads)
+  for (uint32_t i = tid; i < lim; i += NT)
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
 }
@@ -697,8 +768,12 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }
   SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr};
-  const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R>, kSkThreads, nb)
-                              : resident_grid(ctx, k_sk_bucket<false, R>, kSkThreads, nb);
+  // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
+  // LDS (owner map, recorded slots) and the table amortised over 8 waves give
+  // 16 waves per CU, where 256-thread blocks fit only 3 per CU
+  constexpr int NTB = sizeof(R) == sizeof(SK24) ? 512 : kSkThreads;
+  const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R, NTB>, NTB, nb)
+                              : resident_grid(ctx, k_sk_bucket<false, R, NTB>, NTB, nb);
   for (int attempt = 0;; ++attempt) {
     // Algorithmic bytes (inputs read once + outputs written once): the records
     // and bucket offsets; the weak output (one bit per K-mer instance, or a
@@ -708,9 +783,9 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     const uint64_t weak_out = o.weak ? n_kmers / 8 : (o.wrec ? n * 4 : 0);
     kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) + (nb + 1) * 8 + weak_out);
     if (solid)
-      k_sk_bucket<true, R><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
     else
-      k_sk_bucket<false, R><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      k_sk_bucket<false, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hs[4];

@@ -10,9 +10,14 @@
 
 namespace apg {
 
+// Reverse the order of the 32 2-bit bases of x: bit reversal, then each bit
+// pair swapped back (one v_bfi per 32-bit half).
+__device__ __forceinline__ uint32_t sk_rev2_32(uint32_t x) {
+  x = __builtin_bitreverse32(x);
+  return ((x >> 1) & 0x55555555u) | ((x << 1) & 0xaaaaaaaau);
+}
 __device__ __forceinline__ uint64_t sk_rev2(uint64_t x) {
-  x = __builtin_bitreverse64(x);
-  return ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+  return ((uint64_t)sk_rev2_32((uint32_t)x) << 32) | sk_rev2_32((uint32_t)(x >> 32));
 }
 
 // 32 bases [j, j+32) of a packed read, LSB-first (12 bytes read from the

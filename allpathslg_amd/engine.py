@@ -187,6 +187,23 @@ class Context:
         """dst := src (device-to-device; same read lengths)."""
         check(lib().apg_reads_copy_dev(self._h, dst.handle, src.handle), "apg_reads_copy_dev")
 
+    def concat_reads(self, sets, keeps=None, out: Optional[DeviceReads] = None) -> DeviceReads:
+        """all_reads: the device read sets concatenated in order, set s's reads
+        truncated to the device u32 keep lengths keeps[s] (a device pointer or
+        None) — include/apg.h apg_reads_concat_dev.  `out`: an earlier result
+        to reuse (its buffers are recycled)."""
+        n = len(sets)
+        arr = (C.c_void_p * max(n, 1))(*[d.handle.value for d in sets])
+        karr = None
+        if keeps is not None:
+            karr = (C.c_void_p * max(n, 1))(*[(k if k else None) for k in keeps])
+        if out is None:
+            out = DeviceReads(self, None)
+        check(lib().apg_reads_concat_dev(self._h, C.cast(arr, C.POINTER(C.c_void_p)),
+                                         C.cast(karr, C.POINTER(C.c_void_p)) if karr is not None else None, n,
+                                         C.byref(out._h)), "apg_reads_concat_dev")
+        return out
+
     # multi-GPU correction stages (allpathslg_amd.distributed.sharded_precorrect)
     def shard_solid(self, d_recv_ptr: int, recv_counts: np.ndarray, K: int, n_shards: int, min_solid: int) -> int:
         rc = np.ascontiguousarray(recv_counts, dtype=np.uint64)
@@ -234,7 +251,10 @@ class Context:
                                          C.byref(st)), "apg_precorrect_solid")
         return st.as_dict()
 
-    def download(self, dreads: DeviceReads) -> ReadSet:
+    def download(self, dreads: DeviceReads, with_quals: bool = False) -> ReadSet:
+        """Host copy of a device read set.  Sets produced on the device
+        (FillFragments, concat) come back without qualities unless
+        with_quals (the set must then have them)."""
         r = dreads.reads
         if r is None:  # produced on the device: take the shape from the device set
             n, nb, ny = C.c_uint64(), C.c_uint64(), C.c_uint64()
@@ -244,7 +264,8 @@ class Context:
             yo = np.zeros(n.value + 1, dtype=np.uint64)
             check(lib().apg_dreads_shape(self._h, dreads.handle, None, None, None, bo.ctypes.data_as(_u64p),
                                          yo.ctypes.data_as(_u64p)), "apg_dreads_shape")
-            r = ReadSet(bo, yo, np.zeros(max(int(ny.value), 1), dtype=np.uint8), None)
+            r = ReadSet(bo, yo, np.zeros(max(int(ny.value), 1), dtype=np.uint8),
+                        np.zeros(max(int(nb.value), 1), dtype=np.uint8) if with_quals else None)
         pk = np.zeros_like(r.packed)
         q = np.zeros_like(r.quals) if r.quals is not None else None
         check(lib().apg_reads_download(self._h, dreads.handle, pk.ctypes.data_as(C.POINTER(C.c_uint8)),

@@ -99,6 +99,20 @@ int apg_dreads_shape(apg_ctx* ctx, const apg_dreads* dr, uint64_t* n_reads, uint
  * read set to its uploaded state without a host round trip. */
 int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src);
 
+/* Concatenate device read sets into one: ALLPATHS-LG's all_reads, the K=96
+ * CommonPather input = filled fragments + corrected, trimmed jump reads
+ * ([R:M] RunAllPathsLG's all_reads assembly ahead of CommonPather; SURVEY
+ * §3(1), §8f #3; reference snapshot empty, no file:line).  Read i of
+ * sets[s] becomes read (reads of sets[0..s)) + i; when d_keep and d_keep[s]
+ * are non-NULL it is truncated to d_keep[s][i] bases (device u32, e.g. the
+ * keep lengths of apg_error_correct_jump_dev).  No read is dropped (a read
+ * trimmed to 0 stays as an empty read, so ids stay aligned with the inputs);
+ * bases past a kept length are cleared.  Qualities are carried when every
+ * input has them.  *out: NULL (allocated here; free with apg_reads_free) or
+ * an earlier output of this call on ctx, whose buffers are reused. */
+int apg_reads_concat_dev(apg_ctx* ctx, const apg_dreads* const* sets, const uint32_t* const* d_keep,
+                         uint32_t n_sets, apg_dreads** out);
+
 /* Device-to-device copy on the context's stream (synchronous): moves a
  * library-owned device output (e.g. apg_unipath_locs_dev) into a caller
  * buffer. */

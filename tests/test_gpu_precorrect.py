@@ -28,6 +28,22 @@ def test_precorrect_matches_oracle(gpu_ctx, n_cycles):
         assert st["n_corrected"] > 0.5 * st["n_suspect"]
 
 
+@pytest.mark.parametrize("glen,pairs", [(3_000, 20_000), (40_000, 60_000)])
+def test_precorrect_deep_coverage(gpu_ctx, glen, pairs):
+    """Very deep coverage (1300x / 300x): a bucket's K-mer instances exceed
+    the per-wave recorded-slot capacity of the weak pass, which then takes
+    the probing fallback; a few buckets see counts in the thousands."""
+    g = synth_genome(glen, 77)
+    reads = synth_reads(g, pairs, seed=78)
+    got, st = gpu_ctx.precorrect(reads, K=24)
+    exp, est = oracle.precorrect(reads, K=24)
+    assert_same(got, exp)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+        assert st[k] == est[k], k
+    h, _ = gpu_ctx.kmer_spectrum(reads, 24)
+    assert np.array_equal(h, oracle.kmer_spectrum(reads, 24))
+
+
 def test_precorrect_ragged_and_params(gpu_ctx):
     rng = np.random.default_rng(8)
     g = synth_genome(20_000, 9)
