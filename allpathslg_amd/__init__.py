@@ -8,7 +8,7 @@ from ._lib import ApgError, lib  # noqa: F401
 from .engine import (  # noqa: F401
     DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, read_graph, read_kmerpaths, shard_bins,
     write_graph, write_kspec, write_rc_db)
-from .reads import ReadSet, synth_fragments, synth_genome, synth_reads  # noqa: F401
+from .reads import ReadSet, synth_fragments, synth_genome, synth_layout, synth_reads  # noqa: F401
 
 __all__ = [
     "ApgError",
@@ -23,6 +23,7 @@ __all__ = [
     "synth_genome",
     "synth_reads",
     "synth_fragments",
+    "synth_layout",
     "read_graph",
     "read_kmerpaths",
     "write_graph",

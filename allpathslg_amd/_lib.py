@@ -274,6 +274,10 @@ SIGNATURES = {
         [_P, C.POINTER(apg_reads), C.c_int, C.POINTER(_u64p), C.POINTER(_u32p), _u64p, C.POINTER(apg_kstats)],
     ),
     "apg_free": (None, [_P]),
+    "apg_kmer_count_dev": (
+        C.c_int,
+        [_P, _P, C.c_int, C.c_uint64, C.c_uint64, C.POINTER(_u64p), C.POINTER(_u32p), _u64p, C.POINTER(apg_kstats)],
+    ),
     "apg_shard_bins": (C.c_int, [C.c_int, C.c_int]),
     "apg_shard_count": (C.c_int, [_P, _P, C.c_int, C.c_int, _u64p]),
     "apg_shard_scatter": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_void_p]),
@@ -358,6 +362,7 @@ SIGNATURES = {
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),
+    "apg_synth_layout": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u32p, C.POINTER(C.c_uint8)]),
     "apg_synth_fragments": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u8p, _u8p]),
     "apg_fastb_write": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
     "apg_qualb_write": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),

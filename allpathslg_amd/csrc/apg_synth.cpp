@@ -179,6 +179,21 @@ int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome, uint64_t* 
   return APG_OK;
 }
 
+int apg_synth_layout(const apg_synth_params* p, uint64_t* start, uint32_t* flen, uint8_t* flip) {
+  if (!p || !start || !flen || !flip) return APG_E_ARG;
+  if (p->read_len == 0 || p->genome_len < p->read_len) return APG_E_ARG;
+  parallel_for(p->n_pairs, n_threads(p->threads), [&](uint64_t a, uint64_t b) {
+    for (uint64_t k = a; k < b; ++k) {
+      Xoshiro256ss rng(stream_seed(p->seed, 2, p->first_pair + k));
+      const Fragment fr = draw_fragment(rng, p);
+      start[k] = fr.start;
+      flen[k] = (uint32_t)fr.len;
+      flip[k] = fr.flip ? 1 : 0;
+    }
+  });
+  return APG_OK;
+}
+
 int apg_synth_fragments(const apg_synth_params* p, uint64_t* base_off, uint64_t* byte_off, const uint8_t* genome,
                         uint8_t* packed) {
   if (!p || !base_off || !byte_off) return APG_E_ARG;

@@ -480,6 +480,27 @@ __global__ void k_compact_table(const uint64_t* __restrict__ tab_hash, const uin
   }
 }
 
+// [lower_bound(lo), lower_bound(hi)) of the hash-ordered dense table: two
+// binary searches on khash(key), one lane each.
+__global__ void k_hash_bounds(const uint64_t* __restrict__ keys, uint64_t n, HashP hp, uint64_t lo, uint64_t hi,
+                              unsigned long long* __restrict__ out) {
+  if (threadIdx.x >= 2) return;
+  if (threadIdx.x == 1 && hi == 0) {  // no upper bound
+    out[1] = n;
+    return;
+  }
+  const uint64_t target = threadIdx.x ? hi : lo;
+  uint64_t a = 0, b = n;
+  while (a < b) {
+    const uint64_t m = a + (b - a) / 2;
+    if (khash(hp, keys[m]) < target)
+      a = m + 1;
+    else
+      b = m;
+  }
+  out[threadIdx.x] = a;
+}
+
 // ------------------------------------------------------------------------
 // Host orchestration
 // ------------------------------------------------------------------------
@@ -771,40 +792,60 @@ int apg_kmer_spectrum(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t* his
 
 int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys, uint32_t** counts,
                    uint64_t* n_distinct, apg_kstats* stats) {
-  APG_REQUIRE(keys && counts && n_distinct, "apg_kmer_count: NULL output");
-  *keys = nullptr;
-  *counts = nullptr;
-  *n_distinct = 0;
+  APG_REQUIRE(ctx && reads, "apg_kmer_count: NULL argument");
   apg_dreads* dr = nullptr;
   APG_TRY(apg_reads_upload(ctx, reads, &dr));
-  CountResult r;
-  int rc = spectrum_impl(ctx, dr, K, kCountTable, nullptr, 0, &r);
+  const int rc = apg_kmer_count_dev(ctx, dr, K, 0, 0, keys, counts, n_distinct, stats);
   apg_reads_free(dr);
-  if (rc) return rc;
+  return rc;
+}
+
+int apg_kmer_count_dev(apg_ctx* ctx, const apg_dreads* dr, int K, uint64_t hash_lo, uint64_t hash_hi,
+                       uint64_t** keys, uint32_t** counts, uint64_t* n_out, apg_kstats* stats) {
+  APG_REQUIRE(ctx && dr && keys && counts && n_out, "apg_kmer_count_dev: NULL argument");
+  *keys = nullptr;
+  *counts = nullptr;
+  *n_out = 0;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  CountResult r;
+  APG_TRY(spectrum_impl(ctx, dr, K, kCountTable, nullptr, 0, &r));
   const uint64_t nd = r.st.n_distinct;
   uint64_t* dense_off = nullptr;
   uint64_t* d_keys = nullptr;
   uint32_t* d_cnt = nullptr;
+  unsigned long long* d_bounds = nullptr;
   APG_TRY(workspace_t(ctx, "t_dense_off", r.nbuckets + 1, &dense_off));
   APG_TRY(workspace_t(ctx, "t_keys", std::max<uint64_t>(nd, 1), &d_keys));
   APG_TRY(workspace_t(ctx, "t_cnt", std::max<uint64_t>(nd, 1), &d_cnt));
+  APG_TRY(workspace_t(ctx, "t_bounds", 2, &d_bounds));
   APG_TRY(scan_u32_u64(ctx, r.bucket_nd, r.nbuckets, dense_off, "t"));
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(r.nbuckets, (uint64_t)ctx->n_cu * 16));
+  const HashP hp = make_hashp(K);
   kbegin(ctx, "compact_table", nd * 24);
-  k_compact_table<<<grid, 256, 0, ctx->stream>>>(r.rec, r.tab_cnt, r.boff, r.bucket_nd, dense_off, r.nbuckets,
-                                                  make_hashp(K), d_keys, d_cnt);
+  k_compact_table<<<grid, 256, 0, ctx->stream>>>(r.rec, r.tab_cnt, r.boff, r.bucket_nd, dense_off, r.nbuckets, hp,
+                                                  d_keys, d_cnt);
   kend(ctx);
+  // the parcel [hash_lo, hash_hi) is a contiguous range of the hash-ordered table
+  k_hash_bounds<<<1, 64, 0, ctx->stream>>>(d_keys, nd, hp, hash_lo, hash_hi, d_bounds);
   APG_CHECK_HIP(hipGetLastError());
-  auto* hk = (uint64_t*)std::malloc(std::max<uint64_t>(nd, 1) * 8);
-  auto* hc = (uint32_t*)std::malloc(std::max<uint64_t>(nd, 1) * 4);
+  unsigned long long hb[2];
+  APG_CHECK_HIP(hipMemcpyAsync(hb, d_bounds, sizeof hb, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  const uint64_t a = hb[0], n = hb[1] > hb[0] ? hb[1] - hb[0] : 0;
+  auto* hk = (uint64_t*)std::malloc(std::max<uint64_t>(n, 1) * 8);
+  auto* hc = (uint32_t*)std::malloc(std::max<uint64_t>(n, 1) * 4);
   if (!hk || !hc) {
     std::free(hk);
     std::free(hc);
     return APG_E_NOMEM;
   }
-  APG_CHECK_HIP(hipMemcpyAsync(hk, d_keys, nd * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(hc, d_cnt, nd * 4, hipMemcpyDeviceToHost, ctx->stream));
-  rc = sync(ctx);
+  int rc = APG_OK;
+  if (n && (hipMemcpyAsync(hk, d_keys + a, n * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipMemcpyAsync(hc, d_cnt + a, n * 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)) {
+    set_error("apg_kmer_count_dev: D2H failed");
+    rc = APG_E_HIP;
+  }
+  if (rc == APG_OK) rc = sync(ctx);
   if (rc) {
     std::free(hk);
     std::free(hc);
@@ -812,7 +853,7 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K, uint64_t** keys,
   }
   *keys = hk;
   *counts = hc;
-  *n_distinct = nd;
+  *n_out = n;
   if (stats) *stats = r.st;
   return APG_OK;
 }

@@ -138,16 +138,25 @@ class Context:
         check(rc, "apg_kmer_spectrum")
         return hist, st.as_dict()
 
-    def kmer_count(self, reads: ReadSet, K: int):
+    def kmer_count(self, reads, K: int, hash_range: Optional[Tuple[int, int]] = None):
         """(keys, counts, stats): distinct canonical K-mers in ascending
-        kmer_hash order and their multiplicities."""
+        kmer_hash order and their multiplicities.  `reads`: ReadSet (host) or
+        DeviceReads; hash_range=(lo, hi): only the parcel lo <= hash < hi
+        (hi = 0: no upper bound; device reads only)."""
         L = lib()
-        r = reads.c_struct()
         kp, cp = _u64p(), _u32p()
         nd = C.c_uint64()
         st = apg_kstats()
-        check(L.apg_kmer_count(self._h, C.byref(r), K, C.byref(kp), C.byref(cp), C.byref(nd), C.byref(st)),
-              "apg_kmer_count")
+        if isinstance(reads, DeviceReads):
+            lo, hi = hash_range if hash_range is not None else (0, 0)
+            check(L.apg_kmer_count_dev(self._h, reads.handle, K, lo, hi, C.byref(kp), C.byref(cp), C.byref(nd),
+                                       C.byref(st)), "apg_kmer_count_dev")
+        else:
+            if hash_range is not None:
+                raise ValueError("hash_range needs a DeviceReads input")
+            r = reads.c_struct()
+            check(L.apg_kmer_count(self._h, C.byref(r), K, C.byref(kp), C.byref(cp), C.byref(nd), C.byref(st)),
+                  "apg_kmer_count")
         try:
             n = int(nd.value)
             keys = np.ctypeslib.as_array(kp, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
@@ -287,14 +296,15 @@ class Context:
 
     def fill_fragments(self, pairs, solid=None, K: int = 24, min_insert: int = 126, max_insert: int = 234,
                        max_steps: int = 1024, min_solid: int = 3, last_solid: bool = False, out=None,
-                       status: bool = False):
+                       status: bool = False, d_status: Optional[int] = None):
         """FillFragments (include/apg.h): pairs (2i, 2i+1) closed through the
         solid K-mer graph.  `solid`: hashes of solid canonical K-mers (numpy
         u64 for host pairs; (device pointer, count) for DeviceReads), or None
         = last correction pass's set (last_solid=True) / the pairs' own
         count.  ReadSet -> (filled ReadSet, status u8 or None, stats);
         DeviceReads -> (DeviceReads of the filled fragments (reusing `out`),
-        None, stats)."""
+        None, stats); d_status: a device u8[n_pairs] buffer for the
+        per-pair statuses."""
         from ._lib import apg_fill_stats
 
         p = self.fill_params(K, min_insert, max_insert, max_steps, min_solid, last_solid)
@@ -304,7 +314,8 @@ class Context:
             dptr, ns = solid if solid is not None else (None, 0)
             fd = out if out is not None else DeviceReads(self, None)
             check(L.apg_fill_fragments_dev(self._h, pairs.handle, C.byref(p), C.c_void_p(dptr) if dptr else None, ns,
-                                           C.byref(fd._h), None, C.byref(st)), "apg_fill_fragments_dev")
+                                           C.byref(fd._h), C.c_void_p(d_status) if d_status else None,
+                                           C.byref(st)), "apg_fill_fragments_dev")
             return fd, None, st.as_dict()
         from ._lib import apg_reads
 

@@ -210,6 +210,27 @@ def synth_reads(
     return ReadSet(base_off, byte_off, packed, quals)
 
 
+def synth_layout(genome_len: int, n_pairs: int, seed: int, read_len: int = 100, insert_mean: int = 180,
+                 insert_sd: int = 18, first_pair: int = 0, threads: int = 0):
+    """Simulator truth of synth_reads' pairs: (start u64[n], flen u32[n],
+    flip u8[n]) — each fragment's genome interval and strand."""
+    p = apg_synth_params()
+    p.genome_len = genome_len
+    p.seed = seed
+    p.n_pairs = n_pairs
+    p.read_len = read_len
+    p.insert_mean = insert_mean
+    p.insert_sd = insert_sd
+    p.threads = threads
+    p.first_pair = first_pair
+    start = np.empty(max(n_pairs, 1), dtype=np.uint64)
+    flen = np.empty(max(n_pairs, 1), dtype=np.uint32)
+    flip = np.empty(max(n_pairs, 1), dtype=np.uint8)
+    check(lib().apg_synth_layout(C.byref(p), _ptr(start, C.c_uint64), _ptr(flen, C.c_uint32), _ptr(flip, C.c_uint8)),
+          "apg_synth_layout")
+    return start[:n_pairs], flen[:n_pairs], flip[:n_pairs]
+
+
 def synth_fragments(
     genome: np.ndarray,
     n_pairs: int,

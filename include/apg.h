@@ -156,6 +156,16 @@ int apg_kmer_count(apg_ctx* ctx, const apg_reads* reads, int K,
                    apg_kstats* stats);
 void apg_free(void* p);
 
+/* One parcel of the counted table of a device read set: the (canonical,
+ * count) entries whose apg_kmer_hash lies in [hash_lo, hash_hi), in
+ * ascending hash order (host outputs, release with apg_free).  The K-mer
+ * space split into hash parcels is ALLPATHS-LG's way to bound the table's
+ * memory ([R:M] src/kmers/KmerParcels.h).  hash_hi = 0 means no upper
+ * bound, so (0, 0) is the whole table.
+ * stats: the whole read set's counts. */
+int apg_kmer_count_dev(apg_ctx* ctx, const apg_dreads* reads, int K, uint64_t hash_lo, uint64_t hash_hi,
+                       uint64_t** keys, uint32_t** counts, uint64_t* n_out, apg_kstats* stats);
+
 /* ------------------------------------------------------------------------- */
 /* Sharded counting (multi-GPU, one process per GPU).  SURVEY §8e.            */
 /* Records are 16-byte super-k-mers (runs of consecutive K-mers of a read    */
@@ -655,6 +665,10 @@ int apg_synth_sizes(const apg_synth_params* p, uint64_t* n_reads, uint64_t* n_ba
 int apg_synth_reads(const apg_synth_params* p, const uint8_t* genome,
                     uint64_t* base_off, uint64_t* byte_off, uint8_t* packed,
                     uint8_t* quals);
+/* Simulator truth of each pair (test / bench infrastructure): its fragment's
+ * genome start, length and strand (flip = 1: read A is the reverse strand),
+ * the same draws apg_synth_reads makes for that pair. */
+int apg_synth_layout(const apg_synth_params* p, uint64_t* start, uint32_t* flen, uint8_t* flip);
 /* The error-free fragment (insert) of each pair, in read A's orientation: the
  * "oracle fill" standing in for FillFragments (SURVEY §8d K=96 caveat) until
  * that module exists.  Call once with packed = NULL to get base_off/byte_off

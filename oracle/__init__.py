@@ -42,6 +42,13 @@ def lib() -> C.CDLL:
         L.ork_extract_hashes.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p]
         L.ork_kmer_count.restype = C.c_uint64
         L.ork_kmer_count.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, C.POINTER(_u64p), C.POINTER(_u32p)]
+        L.ork_kmer_count_range.restype = C.c_uint64
+        L.ork_kmer_count_range.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, C.c_uint64, C.c_uint64,
+                                           C.POINTER(_u64p), C.POINTER(_u32p)]
+        L.ork_set_threads.restype = None
+        L.ork_set_threads.argtypes = [C.c_int]
+        L.ork_threads.restype = C.c_int
+        L.ork_threads.argtypes = []
         L.ork_spectrum.restype = None
         L.ork_spectrum.argtypes = [_u32p, C.c_uint64, _u64p, C.c_uint64]
         L.ork_precorrect.restype = C.c_int
@@ -97,6 +104,33 @@ def kmer_count(reads, K: int):
         L.ork_free(C.cast(hp, C.c_void_p))
         L.ork_free(C.cast(cp, C.c_void_p))
     return h, c
+
+
+def kmer_count_range(reads, K: int, lo: int, hi: int):
+    """(hashes, counts) of the parcel lo <= hash < hi, ascending (the CPU
+    side of the sampled full-size parity tests)."""
+    L = lib()
+    n, bo, yo, pk = _rp(reads)
+    hp, cp = _u64p(), _u32p()
+    nd = int(L.ork_kmer_count_range(n, bo, yo, pk, K, lo, hi, C.byref(hp), C.byref(cp)))
+    if nd == 2**64 - 1:
+        raise MemoryError("oracle kmer_count_range allocation failed")
+    try:
+        h = np.ctypeslib.as_array(hp, shape=(nd,)).copy() if nd else np.zeros(0, np.uint64)
+        c = np.ctypeslib.as_array(cp, shape=(nd,)).copy() if nd else np.zeros(0, np.uint32)
+    finally:
+        L.ork_free(C.cast(hp, C.c_void_p))
+        L.ork_free(C.cast(cp, C.c_void_p))
+    return h, c
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads of the restatement's parallel loops (0: leave as is)."""
+    lib().ork_set_threads(int(n))
+
+
+def threads() -> int:
+    return int(lib().ork_threads())
 
 
 def spectrum_from_counts(counts: np.ndarray, hist_len: int) -> np.ndarray:
@@ -466,6 +500,18 @@ def error_correct_jump(frags, jumps, K: int = 24, min_solid: int = 3, max_q: int
         L.oje_trim.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, C.c_uint64, C.c_uint32, _u32p]
         L._oje = True
     solid = np.sort(solid_hashes(frags, K, min_solid)).astype(np.uint64)
+    return error_correct_jump_solid(jumps, solid, K, max_q, min_keep)
+
+
+def error_correct_jump_solid(jumps, solid, K: int = 24, max_q: int = 20, min_keep: int = 40):
+    """error_correct_jump against a given solid hash set (e.g. the GPU's
+    frag-read set, itself checked against kmer_count_range parcels)."""
+    L = lib()
+    if not hasattr(L, "_oje"):
+        L.oje_trim.restype = None
+        L.oje_trim.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, C.c_uint64, C.c_uint32, _u32p]
+        L._oje = True
+    solid = np.sort(np.ascontiguousarray(solid, dtype=np.uint64))
     fixed, st = precorrect_solid(jumps, solid, K, max_q)
     keep = np.zeros(max(fixed.n_reads, 1), dtype=np.uint32)
     n, bo, yo, pk = _rp(fixed)

@@ -154,6 +154,74 @@ static void unpack(const uint8_t* pk, uint32_t L, uint8_t* out) {
  * filled, none, ambiguous, budget, skip, filled bases, solid lookups.
  * Returns 0, or -1 on allocation failure / bad arguments.
  */
+/* One pair (2i, 2i+1): status, closure length (0 unless filled), and for a
+ * gap closure its bridge bases in path[]; returns the solid lookups made.
+ * Pairs are independent: orf_fill runs them on the OpenMP threads. */
+static uint64_t fill_pair(const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
+                          const uint64_t* h, uint64_t ns, uint32_t min_insert, uint32_t max_insert,
+                          uint32_t max_steps, uint64_t i, uint8_t* A, uint8_t* B, uint8_t* F, uint8_t* status,
+                          uint32_t* flen, uint8_t* path) {
+  const uint32_t La = (uint32_t)(base_off[2 * i + 1] - base_off[2 * i]);
+  const uint32_t Lf = (uint32_t)(base_off[2 * i + 2] - base_off[2 * i + 1]);
+  flen[i] = 0;
+  uint32_t lo = min_insert;
+  if (La > lo) lo = La;
+  if (Lf > lo) lo = Lf;
+  if (La < (uint32_t)K || Lf < (uint32_t)K || (max_insert >= La + Lf && max_insert - (La + Lf) > FILL_MAX_GAP)) {
+    status[i] = FILL_SKIP;
+    return 0;
+  }
+  unpack(packed + byte_off[2 * i], La, A);
+  unpack(packed + byte_off[2 * i + 1], Lf, B);
+  for (uint32_t t = 0; t < Lf; ++t) F[t] = (uint8_t)(3 - B[Lf - 1 - t]);
+  FillState s;
+  memset(&s, 0, sizeof s);
+  s.K = K, s.solid = h, s.ns = ns, s.A = A, s.La = La, s.F = F, s.Lf = Lf, s.max_steps = max_steps;
+  /* S must be a path of solid K-mers: A's own and F's own K-mers first */
+  int clean = 1;
+  for (uint32_t j = 0; j + (uint32_t)K <= La && clean; ++j) clean = solid_codes(&s, A + j);
+  for (uint32_t j = 0; j + (uint32_t)K <= Lf && clean; ++j) clean = solid_codes(&s, F + j);
+  if (!clean) {
+    status[i] = FILL_NONE;
+    return s.lookups;
+  }
+  int stop = 0;
+  for (uint32_t I = lo; I <= max_insert && I < La + Lf && !stop; ++I) {
+    if (closure_overlap(&s, La + Lf - I)) {
+      if (++s.n_clos == 1) s.clos_I = I;
+      if (s.n_clos >= 2) stop = 1;
+    }
+  }
+  if (!stop && max_insert >= La + Lf) {
+    s.gmax = max_insert - (La + Lf);
+    s.dlo = lo > La + Lf ? lo - (La + Lf) : 0;
+    dfs(&s, 0);
+  }
+  uint8_t st;
+  if (s.n_clos >= 2)
+    st = FILL_AMBIGUOUS;
+  else if (s.budget_hit)
+    st = FILL_BUDGET;
+  else if (s.n_clos == 0)
+    st = FILL_NONE;
+  else
+    st = FILL_OK;
+  status[i] = st;
+  if (st == FILL_OK) {
+    flen[i] = s.clos_I;
+    memcpy(path, s.clos_path, FILL_MAX_GAP + 1);
+  }
+  return s.lookups;
+}
+
+/*
+ * Pairs (2i, 2i+1) of the read set.  solid: hashes of solid canonical K-mers,
+ * any order.  Outputs per pair: status[i], flen[i] (I when filled, else 0).
+ * *out_bases (malloc'd, release with ork_free): the filled fragments' base
+ * codes, one byte per base, concatenated in pair order.  stats[0..6] =
+ * filled, none, ambiguous, budget, skip, filled bases, solid lookups.
+ * Returns 0, or -1 on allocation failure / bad arguments.
+ */
 int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
              const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
              uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats) {
@@ -169,96 +237,72 @@ int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_of
     const uint32_t L = (uint32_t)(base_off[r + 1] - base_off[r]);
     if (L > maxL) maxL = L;
   }
-  uint8_t* A = (uint8_t*)malloc(maxL + 1);
-  uint8_t* B = (uint8_t*)malloc(maxL + 1);
-  uint8_t* F = (uint8_t*)malloc(maxL + 1);
-  size_t cap = 1 << 16, used = 0;
-  uint8_t* out = (uint8_t*)malloc(cap);
-  if (!A || !B || !F || !out) {
-    free(h), free(A), free(B), free(F), free(out);
+  const uint64_t n_pairs = n_reads / 2;
+  uint8_t* paths = (uint8_t*)malloc((n_pairs ? n_pairs : 1) * (FILL_MAX_GAP + 1));
+  if (!paths) {
+    free(h);
     return -1;
   }
-  const uint64_t n_pairs = n_reads / 2;
+  uint64_t lookups = 0;
+  int fail = 0;
+#pragma omp parallel reduction(+ : lookups)
+  {
+    uint8_t* A = (uint8_t*)malloc(maxL + 1);
+    uint8_t* B = (uint8_t*)malloc(maxL + 1);
+    uint8_t* F = (uint8_t*)malloc(maxL + 1);
+    if (!A || !B || !F) {
+#pragma omp atomic write
+      fail = 1;
+    }
+#pragma omp for schedule(dynamic, 64)
+    for (uint64_t i = 0; i < n_pairs; ++i)
+      if (A && B && F)
+        lookups += fill_pair(base_off, byte_off, packed, K, h, ns, min_insert, max_insert, max_steps, i, A, B, F,
+                             status, flen, paths + i * (FILL_MAX_GAP + 1));
+    free(A), free(B), free(F);
+  }
+  free(h);
+  if (fail) {
+    free(paths);
+    return -1;
+  }
+  stats[6] = lookups;
+  uint64_t total = 0;
   for (uint64_t i = 0; i < n_pairs; ++i) {
+    stats[status[i]]++;
+    total += flen[i];
+  }
+  stats[5] = total;
+  uint8_t* out = (uint8_t*)malloc(total ? total : 1);
+  if (!out) {
+    free(paths);
+    return -1;
+  }
+  /* S = A ++ path ++ F (gap), or A ++ F[o, Lf) (overlap o = La+Lf-I) */
+  uint64_t used = 0;
+  uint8_t* A = (uint8_t*)malloc(maxL + 1);
+  uint8_t* B = (uint8_t*)malloc(maxL + 1);
+  for (uint64_t i = 0; i < n_pairs && A && B; ++i) {
+    const uint32_t I = flen[i];
+    if (!I) continue;
     const uint32_t La = (uint32_t)(base_off[2 * i + 1] - base_off[2 * i]);
     const uint32_t Lf = (uint32_t)(base_off[2 * i + 2] - base_off[2 * i + 1]);
-    flen[i] = 0;
-    uint32_t lo = min_insert;
-    if (La > lo) lo = La;
-    if (Lf > lo) lo = Lf;
-    if (La < (uint32_t)K || Lf < (uint32_t)K ||
-        (max_insert >= La + Lf && max_insert - (La + Lf) > FILL_MAX_GAP)) {
-      status[i] = FILL_SKIP;
-      stats[4]++;
-      continue;
-    }
     unpack(packed + byte_off[2 * i], La, A);
     unpack(packed + byte_off[2 * i + 1], Lf, B);
-    for (uint32_t t = 0; t < Lf; ++t) F[t] = (uint8_t)(3 - B[Lf - 1 - t]);
-    FillState s;
-    memset(&s, 0, sizeof s);
-    s.K = K, s.solid = h, s.ns = ns, s.A = A, s.La = La, s.F = F, s.Lf = Lf, s.max_steps = max_steps;
-    /* S must be a path of solid K-mers: A's own and F's own K-mers first */
-    int clean = 1;
-    for (uint32_t j = 0; j + (uint32_t)K <= La && clean; ++j) clean = solid_codes(&s, A + j);
-    for (uint32_t j = 0; j + (uint32_t)K <= Lf && clean; ++j) clean = solid_codes(&s, F + j);
-    if (!clean) {
-      stats[6] += s.lookups;
-      status[i] = FILL_NONE;
-      stats[FILL_NONE]++;
-      continue;
-    }
-    int stop = 0;
-    for (uint32_t I = lo; I <= max_insert && I < La + Lf && !stop; ++I) {
-      if (closure_overlap(&s, La + Lf - I)) {
-        if (++s.n_clos == 1) s.clos_I = I;
-        if (s.n_clos >= 2) stop = 1;
-      }
-    }
-    if (!stop && max_insert >= La + Lf) {
-      s.gmax = max_insert - (La + Lf);
-      s.dlo = lo > La + Lf ? lo - (La + Lf) : 0;
-      dfs(&s, 0);
-    }
-    stats[6] += s.lookups;
-    uint8_t st;
-    if (s.n_clos >= 2)
-      st = FILL_AMBIGUOUS;
-    else if (s.budget_hit)
-      st = FILL_BUDGET;
-    else if (s.n_clos == 0)
-      st = FILL_NONE;
-    else
-      st = FILL_OK;
-    status[i] = st;
-    stats[st]++;
-    if (st != FILL_OK) continue;
-    const uint32_t I = s.clos_I;
-    flen[i] = I;
-    stats[5] += I;
-    if (used + I > cap) {
-      while (used + I > cap) cap *= 2;
-      uint8_t* nb = (uint8_t*)realloc(out, cap);
-      if (!nb) {
-        free(h), free(A), free(B), free(F), free(out);
-        return -1;
-      }
-      out = nb;
-    }
-    /* S = A ++ path ++ F (gap), or A ++ F[o, Lf) (overlap o = La+Lf-I) */
     uint8_t* S = out + used;
     memcpy(S, A, La);
+    uint8_t* Fp = S + I - Lf; /* F's bases land at the end of S */
     if (I < La + Lf) {
       const uint32_t o = La + Lf - I;
-      memcpy(S + La, F + o, Lf - o);
+      for (uint32_t t = o; t < Lf; ++t) S[La + t - o] = (uint8_t)(3 - B[Lf - 1 - t]);
     } else {
       const uint32_t d = I - La - Lf;
-      memcpy(S + La, s.clos_path, d);
-      memcpy(S + La + d, F, Lf);
+      memcpy(S + La, paths + i * (FILL_MAX_GAP + 1), d);
+      for (uint32_t t = 0; t < Lf; ++t) Fp[t] = (uint8_t)(3 - B[Lf - 1 - t]);
     }
     used += I;
   }
-  free(h), free(A), free(B), free(F);
+  free(A), free(B), free(paths);
   *out_bases = out;
   return 0;
 }

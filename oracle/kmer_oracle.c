@@ -16,8 +16,11 @@
  *   - counting: [R:M] NaifKmerizer block sort + KernelKmerStorer summarize
  *     (sort, merge equal k-mers into (k-mer, frequency)).
  *   - spectrum: [R:M] src/kmers/KmerSpectra.h KmerSpectrum (h[m]).
- * Deliberately simple: one thread, generate -> LSD radix sort -> run-length.
+ * Deliberately simple: generate -> LSD radix sort -> run-length; the
+ * independent per-read extraction and the per-partition sorts run on the
+ * OpenMP threads given (the CPU baseline's host-cores figure).
  */
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -120,17 +123,58 @@ static void radix_sort_u64(uint64_t* a, uint64_t n, int bits) {
   free(tmp);
 }
 
-/* (hash, count) table in ascending hash order.  Returns #distinct, or
- * UINT64_MAX on allocation failure.  Caller frees *hashes / *counts. */
-uint64_t ork_kmer_count(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off,
-                        const uint8_t* packed, int K, uint64_t** hashes, uint32_t** counts) {
-  const uint64_t n = ork_count_instances(n_reads, base_off, K);
-  uint64_t* h = (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
-  if (!h) return UINT64_MAX;
-  ork_extract_hashes(n_reads, base_off, byte_off, packed, K, h);
-  radix_sort_u64(h, n, 2 * K);
+/* Parallel sort: one MSD pass on the top 8 of `bits` bits (per-thread
+ * histograms, stable scatter), then every partition LSD-sorted on its own
+ * thread.  Same result as radix_sort_u64. */
+static int psort_u64(uint64_t* a, uint64_t n, int bits) {
+  const int T = omp_get_max_threads();
+  if (T <= 1 || n < (1u << 20) || bits <= 8) {
+    radix_sort_u64(a, n, bits);
+    return 0;
+  }
+  const int top = bits - 8;
+  uint64_t* tmp = (uint64_t*)malloc(n * sizeof(uint64_t));
+  uint64_t* cnt = (uint64_t*)calloc((size_t)T * 256, sizeof(uint64_t));
+  if (!tmp || !cnt) {
+    free(tmp), free(cnt);
+    return -1;
+  }
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const uint64_t lo = n * (uint64_t)t / T, hi = n * (uint64_t)(t + 1) / T;
+    uint64_t* c = cnt + (size_t)t * 256;
+    for (uint64_t i = lo; i < hi; ++i) c[(a[i] >> top) & 255]++;
+#pragma omp barrier
+#pragma omp single
+    {
+      uint64_t run = 0;
+      for (int d = 0; d < 256; ++d)
+        for (int u = 0; u < T; ++u) {
+          const uint64_t x = cnt[(size_t)u * 256 + d];
+          cnt[(size_t)u * 256 + d] = run;
+          run += x;
+        }
+    }
+    for (uint64_t i = lo; i < hi; ++i) tmp[c[(a[i] >> top) & 255]++] = a[i];
+  }
+  uint64_t start[257];
+  start[0] = 0;
+  for (int d = 0; d < 256; ++d) start[d + 1] = cnt[(size_t)(T - 1) * 256 + d];
+  free(cnt);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int d = 0; d < 256; ++d) {
+    radix_sort_u64(tmp + start[d], start[d + 1] - start[d], top);
+    memcpy(a + start[d], tmp + start[d], (start[d + 1] - start[d]) * sizeof(uint64_t));
+  }
+  free(tmp);
+  return 0;
+}
+
+/* Run-length count of the ascending h[0..n) in place; counts into *counts. */
+static uint64_t run_length(uint64_t* h, uint64_t n, uint32_t** counts) {
   uint32_t* c = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
-  if (!c) { free(h); return UINT64_MAX; }
+  if (!c) return UINT64_MAX;
   uint64_t d = 0;
   for (uint64_t i = 0; i < n;) {
     uint64_t j = i + 1;
@@ -140,9 +184,105 @@ uint64_t ork_kmer_count(uint64_t n_reads, const uint64_t* base_off, const uint64
     ++d;
     i = j;
   }
-  *hashes = h;
   *counts = c;
   return d;
+}
+
+/* (hash, count) table in ascending hash order.  Returns #distinct, or
+ * UINT64_MAX on allocation failure.  Caller frees *hashes / *counts. */
+uint64_t ork_kmer_count(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off,
+                        const uint8_t* packed, int K, uint64_t** hashes, uint32_t** counts) {
+  /* instance offset of every read, then the reads' hashes in parallel */
+  uint64_t* ioff = (uint64_t*)malloc((n_reads + 1) * sizeof(uint64_t));
+  if (!ioff) return UINT64_MAX;
+  ioff[0] = 0;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    const uint64_t len = base_off[r + 1] - base_off[r];
+    ioff[r + 1] = ioff[r] + (len >= (uint64_t)K ? len - K + 1 : 0);
+  }
+  const uint64_t n = ioff[n_reads];
+  uint64_t* h = (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
+  if (!h) {
+    free(ioff);
+    return UINT64_MAX;
+  }
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (uint64_t r = 0; r < n_reads; ++r)
+    ork_extract_hashes(1, base_off + r, byte_off + r, packed, K, h + ioff[r]);
+  free(ioff);
+  if (psort_u64(h, n, 2 * K)) {
+    free(h);
+    return UINT64_MAX;
+  }
+  *hashes = h;
+  return run_length(h, n, counts);
+}
+
+/* Parcel of the counted table (KmerParcels' K-mer-space partition, [R:M]
+ * src/kmers/KmerParcels.h): the (hash, count) entries with lo <= hash < hi,
+ * ascending.  Extraction keeps only the parcel's instances (per-thread
+ * buffers), so a 1/256 parcel of a 40 M-read set needs ~1/256 of the memory. */
+uint64_t ork_kmer_count_range(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off,
+                              const uint8_t* packed, int K, uint64_t lo, uint64_t hi, uint64_t** hashes,
+                              uint32_t** counts) {
+  const uint64_t m = wmask(2 * K);
+  const int T = omp_get_max_threads();
+  uint64_t** buf = (uint64_t**)calloc((size_t)T, sizeof(uint64_t*));
+  uint64_t* len = (uint64_t*)calloc((size_t)T, sizeof(uint64_t));
+  int fail = 0;
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    uint64_t cap = 1 << 16, used = 0;
+    uint64_t* b = (uint64_t*)malloc(cap * sizeof(uint64_t));
+#pragma omp for schedule(dynamic, 4096)
+    for (uint64_t r = 0; r < n_reads; ++r) {
+      const uint64_t L = base_off[r + 1] - base_off[r];
+      uint64_t fw = 0, rc = 0;
+      for (uint64_t i = 0; i < L; ++i) {
+        const uint64_t x = (uint64_t)base_at(packed, byte_off[r], i);
+        fw = ((fw << 2) | x) & m;
+        rc = (rc >> 2) | ((3 - x) << (2 * K - 2));
+        if (i + 1 < (uint64_t)K) continue;
+        const uint64_t hv = ork_hash(K, fw < rc ? fw : rc);
+        if (hv < lo || hv >= hi || !b) continue;
+        if (used == cap) {
+          cap *= 2;
+          uint64_t* nb = (uint64_t*)realloc(b, cap * sizeof(uint64_t));
+          if (!nb) {
+            free(b);
+            b = NULL;
+            continue;
+          }
+          b = nb;
+        }
+        b[used++] = hv;
+      }
+    }
+    if (!b) {
+#pragma omp atomic write
+      fail = 1;
+    }
+    buf[t] = b;
+    len[t] = used;
+  }
+  uint64_t n = 0;
+  for (int t = 0; t < T; ++t) n += len[t];
+  uint64_t* h = fail ? NULL : (uint64_t*)malloc((n ? n : 1) * sizeof(uint64_t));
+  uint64_t at = 0;
+  for (int t = 0; t < T; ++t) {
+    if (h && len[t]) memcpy(h + at, buf[t], len[t] * sizeof(uint64_t));
+    at += len[t];
+    free(buf[t]);
+  }
+  free(buf), free(len);
+  if (!h) return UINT64_MAX;
+  if (psort_u64(h, n, 2 * K)) {
+    free(h);
+    return UINT64_MAX;
+  }
+  *hashes = h;
+  return run_length(h, n, counts);
 }
 
 /* KmerSpectrum: hist[m] += 1 per distinct k-mer of count m; last bin is >=. */
@@ -156,3 +296,9 @@ void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t 
 }
 
 void ork_free(void* p) { free(p); }
+
+/* Host threads of the OpenMP loops (0: OMP_NUM_THREADS / all cores). */
+void ork_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+}
+int ork_threads(void) { return omp_get_max_threads(); }

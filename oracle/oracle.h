@@ -12,6 +12,11 @@ uint64_t ork_extract_hashes(uint64_t n_reads, const uint64_t* base_off,
                             uint64_t* out);
 uint64_t ork_kmer_count(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off,
                         const uint8_t* packed, int K, uint64_t** hashes, uint32_t** counts);
+uint64_t ork_kmer_count_range(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off,
+                              const uint8_t* packed, int K, uint64_t lo, uint64_t hi, uint64_t** hashes,
+                              uint32_t** counts);
+void ork_set_threads(int n);
+int ork_threads(void);
 void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t hist_len);
 void ork_free(void* p);
 int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,

@@ -45,12 +45,29 @@ static int is_solid(const uint64_t* solid, uint64_t ns, uint64_t h) {
   return lo < ns && solid[lo] == h;
 }
 
+static void correct_read(const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed, uint8_t* quals, int K,
+                         uint32_t maxq, const uint64_t* h, uint64_t ns, uint64_t r, uint64_t* stats);
+
 /* One correction pass against the ascending solid-hash array h[0..ns). */
 static void correct(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
                     uint8_t* quals, int K, uint32_t maxq, const uint64_t* h, uint64_t ns, uint64_t* stats) {
+  /* reads are independent (counts are not updated within a pass): one
+   * thread per read, counters reduced */
+  uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma omp parallel for schedule(dynamic, 1024) reduction(+ : s0, s1, s2, s3)
   for (uint64_t r = 0; r < n_reads; ++r) {
+    uint64_t st[4] = {0, 0, 0, 0};
+    correct_read(base_off, byte_off, packed, quals, K, maxq, h, ns, r, st);
+    s0 += st[0], s1 += st[1], s2 += st[2], s3 += st[3];
+  }
+  stats[0] += s0, stats[1] += s1, stats[2] += s2, stats[3] += s3;
+}
+
+static void correct_read(const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed, uint8_t* quals, int K,
+                         uint32_t maxq, const uint64_t* h, uint64_t ns, uint64_t r, uint64_t* stats) {
+  {
     const uint32_t L = (uint32_t)(base_off[r + 1] - base_off[r]);
-    if (L < (uint32_t)K) continue;
+    if (L < (uint32_t)K) return;
     uint8_t* rd = packed + byte_off[r];
     uint8_t* q = quals + base_off[r];
     for (uint32_t p = 0; p < L; ++p) {

@@ -7,7 +7,9 @@
 // targets: [R:M] src/paths/ReadsToPathsCoreX.cc, src/paths/Unipath.cc,
 // src/paths/KmerPath.h, src/paths/HyperKmerPath.h, src/paths/KmerBaseBroker.h.
 //
-// Deliberately simple: sort + binary search, sequential walks.
+// Deliberately simple: sort + binary search, sequential walks; the
+// independent per-read and per-node loops (instances, links, read paths) and
+// the instance sort run on the OpenMP threads given.
 //   nodes      canonical K-mers of the reads; ext bits = read-supported
 //              neighbour bases (left/right of the canonical orientation)
 //   directed   v = 2*node + o (o = 1: reverse complement); seq(v)
@@ -21,6 +23,9 @@
 //   HKP        vertices = union of (end of u) and (start of v) over every
 //              graph edge tail(u) -> head(v); numbered by smallest
 //              (2*unipath + end) member; edge i = unipath i
+#include <omp.h>
+#include <parallel/algorithm>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
@@ -72,16 +77,28 @@ uint64_t get_base(const Key& k, int i) {  // base i (0 = first) of the K-mer
   return (limb >> (bit & 63)) & 3;
 }
 
-Key from_bases(const std::vector<int>& s) {
-  Key k{0, 0, 0};
-  for (int x : s) k = push_right(k, (uint64_t)x);
-  return k;
+// Reverse complement of the K-mer: the 192-bit value's 2-bit groups reversed
+// (limbs swapped, each limb's groups reversed), complemented, then shifted
+// down by the 192 - 2K unused bits.
+uint64_t rev2_limb(uint64_t x) {
+  x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+  x = ((x >> 4) & 0x0f0f0f0f0f0f0f0full) | ((x & 0x0f0f0f0f0f0f0f0full) << 4);
+  return __builtin_bswap64(x);
 }
-
 Key revcomp(const Key& k) {
-  std::vector<int> s(g_K);
-  for (int i = 0; i < g_K; ++i) s[i] = 3 - (int)get_base(k, g_K - 1 - i);
-  return from_bases(s);
+  uint64_t a = ~rev2_limb(k.c), b = ~rev2_limb(k.b), c = ~rev2_limb(k.a);  // full 192-bit reversal
+  const int sh = 192 - 2 * g_K;  // drop the low `sh` bits (the unused high bases, now at the bottom)
+  const int q = sh / 64, r = sh % 64;
+  uint64_t l[3] = {a, b, c};  // l[0] most significant
+  uint64_t o[3] = {0, 0, 0};
+  for (int i = 2; i >= 0; --i) {  // o = l >> sh (192-bit)
+    const int src = i - q;
+    if (src < 0) continue;
+    uint64_t v = r ? (l[src] >> r) : l[src];
+    if (r && src - 1 >= 0) v |= l[src - 1] << (64 - r);
+    o[i] = v;
+  }
+  return mask_key(Key{o[0], o[1], o[2]});
 }
 
 int read_base(const uint8_t* rd, uint64_t i) { return (rd[i >> 2] >> (2 * (i & 3))) & 3; }
@@ -179,7 +196,13 @@ int oru_build(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_o
     Key key;
     uint8_t left, right;
   };
-  std::vector<Inst> inst;
+  std::vector<uint64_t> ioff(n_reads + 1, 0);
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    const uint64_t L = base_off[r + 1] - base_off[r];
+    ioff[r + 1] = ioff[r] + (L >= (uint64_t)K ? L - K + 1 : 0);
+  }
+  std::vector<Inst> inst(ioff[n_reads]);
+#pragma omp parallel for schedule(dynamic, 1024)
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint64_t L = base_off[r + 1] - base_off[r];
     const uint8_t* rd = packed + byte_off[r];
@@ -201,10 +224,10 @@ int oru_build(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_o
       } else {
         x = {rc, cb, ca};
       }
-      inst.push_back(x);
+      inst[ioff[r] + i] = x;
     }
   }
-  std::sort(inst.begin(), inst.end(), [](const Inst& x, const Inst& y) { return x.key < y.key; });
+  __gnu_parallel::sort(inst.begin(), inst.end(), [](const Inst& x, const Inst& y) { return x.key < y.key; });
   g_nodes.clear();
   for (size_t i = 0; i < inst.size();) {
     Node n{inst[i].key, 0, 0, 0};
@@ -293,17 +316,24 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
   out->n_nodes = (uint64_t)N;
   // ---- 2. unique links --------------------------------------------------
   std::vector<int64_t> nxt(D, -1), prv(D, -1);
-  for (int64_t v = 0; v < D; ++v) {
+  int bad = 0;
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (int64_t v = 0; v < D; ++v) {  // w's unique predecessor alone writes prv[w]
     if (palin(v >> 1)) continue;
     const uint8_t o = out_set(v);
     if (popc(o) != 1) continue;
     const int b = __builtin_ctz(o);
     const int64_t w = succ_by(v, b);
-    if (w < 0) return -2;  // read-supported edge must land on a node
+    if (w < 0) {  // read-supported edge must land on a node
+#pragma omp atomic write
+      bad = 1;
+      continue;
+    }
     if (palin(w >> 1) || popc(in_set(w)) != 1) continue;
     nxt[v] = w;
     prv[w] = v;
   }
+  if (bad) return -2;
   // ---- 3. cut cycles ------------------------------------------------------
   {
     std::vector<char> onpath(D, 0);
@@ -445,27 +475,41 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
     to[i] = vid[findp(2 * i + 1)];
   }
   // ---- 6. read paths ---------------------------------------------------------
+  // per read: its id intervals (runs of consecutive ids), then concatenated
   std::vector<uint64_t> poff(n_reads + 1, 0), pst, pln;
+  std::vector<std::vector<uint64_t>> rst(n_reads), rln(n_reads);
+  int miss = 0;
+#pragma omp parallel for schedule(dynamic, 1024)
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint64_t L = base_off[r + 1] - base_off[r];
     const uint8_t* rd = packed + byte_off[r];
-    if (L >= (uint64_t)K) {
-      Key f{0, 0, 0};
-      for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) f = push_right(f, read_base(rd, i));
-      for (uint64_t i = 0; i + K <= L; ++i) {
-        f = push_right(f, read_base(rd, i + K - 1));
-        const int64_t v = directed_of(f);
-        if (v < 0) return -4;
-        const uint64_t id = base[uni_of_path[path_of[v]]] + (uint64_t)rank_of[v];
-        if (!pst.empty() && pln.size() > poff[r] && pst.back() + pln.back() == id)
-          pln.back()++;
-        else {
-          pst.push_back(id);
-          pln.push_back(1);
-        }
+    if (L < (uint64_t)K) continue;
+    Key f{0, 0, 0};
+    for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) f = push_right(f, read_base(rd, i));
+    for (uint64_t i = 0; i + K <= L; ++i) {
+      f = push_right(f, read_base(rd, i + K - 1));
+      const int64_t v = directed_of(f);
+      if (v < 0) {
+#pragma omp atomic write
+        miss = 1;
+        break;
+      }
+      const uint64_t id = base[uni_of_path[path_of[v]]] + (uint64_t)rank_of[v];
+      if (!rst[r].empty() && rst[r].back() + rln[r].back() == id)
+        rln[r].back()++;
+      else {
+        rst[r].push_back(id);
+        rln[r].push_back(1);
       }
     }
+  }
+  if (miss) return -4;
+  for (uint64_t r = 0; r < n_reads; ++r) {
+    pst.insert(pst.end(), rst[r].begin(), rst[r].end());
+    pln.insert(pln.end(), rln[r].begin(), rln[r].end());
     poff[r + 1] = pst.size();
+    std::vector<uint64_t>().swap(rst[r]);
+    std::vector<uint64_t>().swap(rln[r]);
   }
   out->n_unipaths = U;
   out->len = dup(len);
