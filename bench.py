@@ -48,22 +48,28 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--reads-per-gpu", type=int, default=40_000_000)
-    p.add_argument("--genome-len", type=int, default=64_444_167)
+    p.add_argument("--reads-per-gpu", type=int, default=None,
+                   help="default: 40 M (C2, one GPU) / 50 M (C4, N > 1: 400 M reads on 8 GPUs)")
+    p.add_argument("--genome-len", type=int, default=None,
+                   help="default: chr20 64,444,167 bp (C2, one GPU) / D. melanogaster 143,726,002 bp (C4, N > 1)")
     p.add_argument("--K", type=int, default=25)
     p.add_argument("--seed", type=int, default=0xA11BA7)
     p.add_argument("--K-unipath", type=int, default=96)
     p.add_argument("--K-correct", type=int, default=24)
     p.add_argument("--spectrum-only", action="store_true")
-    p.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
-    p.add_argument("--cpu-correct-sample-reads", type=int, default=1_000_000)
-    p.add_argument("--cpu-unipath-sample-frags", type=int, default=20_000,
+    p.add_argument("--cpu-sample-reads", type=int, default=4_000_000)
+    p.add_argument("--cpu-correct-sample-reads", type=int, default=2_000_000)
+    p.add_argument("--cpu-unipath-sample-frags", type=int, default=200_000,
                    help="pairs of the CPU baseline's FillFragments + unipath sample")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="OpenMP threads of the CPU baseline (0: OMP_NUM_THREADS / every CPU of the process)")
+    p.add_argument("--c3-jump-pairs", type=int, default=10_000_000,
+                   help="jump pairs of the C3 line (BASELINE configs[2]; 0 = skip)")
+    p.add_argument("--no-file-to-graph", dest="file_to_graph", action="store_false",
+                   help="skip the host-buffer-to-host-graph (PCIe-inclusive) measurement")
     p.add_argument("--oracle-fill", action="store_true",
                    help="feed the unipath stage the simulator's true inserts instead of FillFragments (old bench)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
-                   help="concurrent single-threaded oracle processes for the host-cores baseline (1 = off)")
     p.add_argument("--align-pairs", type=int, default=4_000_000,
                    help="read placements of the aligner line (gap-free, banded SW, consensus); 0 = skip")
     p.add_argument("--align-band", type=int, default=8)
@@ -323,6 +329,111 @@ def jump_bench(ctx, dsrc, genome, a, reps: int = 2):
     return out
 
 
+def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2):
+    """C3 line (BASELINE configs[2]): chr20 frag reads (the
+    step's 40 M) + a 3-kb jump library (10 M pairs = 20 M reads): PreCorrect
+    of the frags, FillFragments, ErrorCorrectJump of the jumps against the
+    frag reads, all_reads = filled fragments ++ trimmed jumps
+    (apg_reads_concat_dev), K=96 unipaths + unibases + HyperKmerPath +
+    KmerPaths of every all_reads read — inputs resident in HBM."""
+    jumps = synth_reads(genome, a.c3_jump_pairs, seed=a.seed + 23, insert_mean=3000, insert_sd=300, threads=16)
+    dJ0, dJ = ctx.upload(jumps), ctx.upload(jumps)
+    keep = torch.empty(max(jumps.n_reads, 1), dtype=torch.int32, device="cuda")
+    st = {"filled": None, "all": None}
+
+    def step():
+        ctx.copy_reads(dwork, dsrc)
+        ctx.copy_reads(dJ, dJ0)
+        _, pst = ctx.precorrect(dwork, K=a.K_correct)
+        st["filled"], _, fst = ctx.fill_fragments(dwork, K=a.K_correct, last_solid=True, out=st["filled"])
+        est = ctx.error_correct_jump(dwork, dJ, K=a.K_correct, d_keep=keep.data_ptr())
+        st["all"] = ctx.concat_reads([st["filled"], dJ], [None, keep.data_ptr()], out=st["all"])
+        _, ust = ctx.unipaths(st["all"], a.K_unipath, read_paths=True, fetch=False)
+        return pst, fst, est, ust
+
+    step()
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pst, fst, est, ust = step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    kt = ctx.kernel_times()
+    ms = {k: v[0] / max(v[1], 1) * v[1] / reps for k, v in kt.items()}
+    n_in = dsrc.n_reads + jumps.n_reads
+    kl = keep[: jumps.n_reads].cpu().numpy().astype(np.int64)
+    inst = (int(fst["filled_bases"]) - (a.K_unipath - 1) * int(fst["n_filled"])
+            + int(np.maximum(np.minimum(kl, 100) - a.K_unipath + 1, 0).sum()))
+    gk = a.genome_len - a.K_unipath + 1
+    out = {
+        "workload": (f"C3 chr20-size: the step's {dsrc.n_reads} frag reads + {jumps.n_reads} reads of a 3-kb jump "
+                     f"library ({a.c3_jump_pairs} pairs, insert 3000 +- 300): PreCorrect, FillFragments, "
+                     f"ErrorCorrectJump, all_reads = filled ++ trimmed jumps, K={a.K_unipath} unipaths + unibases + "
+                     f"HyperKmerPath + KmerPaths of all_reads"),
+        "reads": n_in,
+        "ms_per_step": wall * 1e3,
+        "reads_per_s": n_in / wall,
+        "kernels_ms": ms,
+        "precorrect_stats": pst,
+        "fill_stats": fst,
+        "ecj_stats": est,
+        "unipath_stats": ust,
+        "all_reads": st["all"].n_reads,
+        "checks": {
+            "all_reads_is_filled_plus_jumps": st["all"].n_reads == int(fst["n_filled"]) + jumps.n_reads,
+            "unipath_instances_equal_sum_len_minus_K_plus_1": ust["n_instances"] == inst,
+            "unipath_nodes_cover_genome": ust["n_nodes"] >= gk - 1000,
+            "unipaths_long": ust["max_len"] >= 10_000,
+            "most_jump_reads_kept": est["bases_kept"] > 0.5 * jumps.n_bases,
+        },
+    }
+    for d in (dJ0, dJ, st["filled"], st["all"]):
+        d.free()
+    return out
+
+
+def file_to_graph(ctx, reads, a) -> dict:
+    """The module-boundary rate beside `value`: .fastb/.qualb files (on
+    /dev/shm, so parsing and PCIe, not a disk, are what is timed) -> host read
+    set -> H2D of bases + qualities -> K=25 spectrum, K=24 PreCorrect,
+    FillFragments -> K=96 unipaths with the graph, unibases, HKP and every
+    fragment's KmerPath copied back to host memory."""
+    from allpathslg_amd import ReadSet
+
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    head = os.path.join(base, f"apg_f2g_{os.getpid()}")
+    reads.write_fastb(head + ".fastb")
+    reads.write_qualb(head + ".qualb")
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        host = ReadSet.load(head + ".fastb", head + ".qualb")
+        t1 = time.perf_counter()
+        d = ctx.upload(host)
+        t2 = time.perf_counter()
+        ctx.kmer_spectrum(d, a.K)
+        ctx.precorrect(d, K=a.K_correct)
+        filled, _, _ = ctx.fill_fragments(d, K=a.K_correct, last_solid=True)
+        t3 = time.perf_counter()
+        g, ust = ctx.unipaths(filled, a.K_unipath, read_paths=True, fetch=True)
+        t4 = time.perf_counter()
+        nb = sum(int(v.nbytes) for v in g.values() if isinstance(v, np.ndarray))
+        d.free()
+        filled.free()
+    finally:
+        for ext in (".fastb", ".qualb"):
+            if os.path.exists(head + ext):
+                os.unlink(head + ext)
+    total = t4 - t0
+    return {"workload": f"{reads.n_reads} reads from .fastb/.qualb on {base} to the K={a.K_unipath} graph in host memory",
+            "ms": total * 1e3, "reads_per_s": reads.n_reads / total,
+            "read_files_ms": (t1 - t0) * 1e3, "h2d_ms": (t2 - t1) * 1e3,
+            "h2d_GBps": (reads.n_bases * 1.25) / max(t2 - t1, 1e-9) / 1e9,
+            "spectrum_precorrect_fill_ms": (t3 - t2) * 1e3, "unipaths_with_d2h_ms": (t4 - t3) * 1e3,
+            "graph_bytes_to_host": nb, "n_unipaths": ust["n_unipaths"]}
+
+
 def placement_cpu_baseline(genome, a, n_reads: int = 100_000) -> dict:
     """CPU baseline of the placement line: oracle/locs_oracle.c, one thread,
     on a bounded sample — the graph of a 1 Mb piece of the bench genome (tiled
@@ -384,6 +495,13 @@ def main():
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
     torch.cuda.set_device(local)
     sharded = world > 1 or a.sharded
+    # BASELINE.json configs: one GPU = C2 (chr20, 40 M reads); N > 1 = C4
+    # (D. melanogaster, 400 M reads over 8 GPUs = 50 M per GPU, weak scaling)
+    c4 = world > 1
+    if a.genome_len is None:
+        a.genome_len = 143_726_002 if c4 else 64_444_167
+    if a.reads_per_gpu is None:
+        a.reads_per_gpu = 50_000_000 if c4 else 40_000_000
     if sharded:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -549,62 +667,17 @@ def main():
             roofline["traffic_over_algorithmic"] = t / max(per_launch_bytes, 1)
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        import oracle
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.spectrum_only and frags is None:
+        # the restatement (OpenMP) on bounded samples of the same reads; FillFragments
+        # against the full-size solid set of the step's last PreCorrect pass
+        from oracle.baseline import cpu_baseline
 
-        sample = reads.subset(0, min(a.cpu_sample_reads, reads.n_reads))
-        oracle.lib()
-        tc = time.perf_counter()
-        oracle.kmer_spectrum(sample, a.K)
-        tc = time.perf_counter() - tc
-        spec_rate = sample.n_reads / tc
-        desc = (f"spectrum: first {sample.n_reads} reads, K={a.K} ({tc:.2f} s)")
-        rate = spec_rate
-        if not a.spectrum_only:
-            csample = reads.subset(0, min(a.cpu_correct_sample_reads, reads.n_reads))
-            tp = time.perf_counter()
-            oracle.precorrect(csample, K=a.K_correct)
-            tp = time.perf_counter() - tp
-            pc_rate = csample.n_reads / tp
-            npair = min(a.cpu_unipath_sample_frags, n_pairs)
-            if frags is not None:  # --oracle-fill: the true inserts
-                usample = frags.subset(0, npair)
-                fill_rate, fdesc = None, ""
-            else:  # FillFragments of the GPU-corrected pairs against the full-size solid set
-                solid_t = torch.empty(max(ctx.solid_copy(None), 1), dtype=torch.int64, device="cuda")
-                ns = ctx.solid_copy(solid_t.data_ptr())
-                solid_h = solid_t[:ns].cpu().numpy().view(np.uint64)
-                del solid_t
-                fixed = ctx.download(dreads).subset(0, 2 * npair)
-                tf = time.perf_counter()
-                usample, _, _, _ = oracle.fill_fragments(fixed, solid_h, K=a.K_correct)
-                tf = time.perf_counter() - tf
-                fill_rate = 2 * npair / tf
-                fdesc = (f"; FillFragments: first {npair} GPU-corrected pairs against the full solid set "
-                         f"({ns} K-mers, binary search) ({tf:.2f} s)")
-            tu = time.perf_counter()
-            oracle.unipaths(usample, a.K_unipath)
-            tu = time.perf_counter() - tu
-            uni_rate = 2 * npair / tu  # two reads per pair
-            inv = 1.0 / spec_rate + 1.0 / pc_rate + 1.0 / uni_rate + (1.0 / fill_rate if fill_rate else 0.0)
-            rate = 1.0 / inv
-            desc += (f"; PreCorrect: first {csample.n_reads} reads, K={a.K_correct} against their own "
-                     f"solid set ({tp:.2f} s)" + fdesc + f"; unipaths: the {usample.n_reads} fragments of "
-                     f"those {npair} pairs, K={a.K_unipath} ({tu:.2f} s)")
-        cpu = {"value": rate, "unit": "reads/s", "cores": 1, "kind": "port",
-               "sample": "oracle/ CPU restatement, single-threaded, same synthetic inputs; " + desc +
-                         "; value = 1/(sum of 1/stage_rate)"}
-        if a.cpu_workers > 1 and not a.spectrum_only and frags is None:
-            # the host's cores all busy: W concurrent copies of the restatement
-            # (reported as the baseline; the single-core figure is kept beside it)
-            try:
-                from oracle.parallel import parallel_baseline
-
-                par = parallel_baseline(ROOT, a.genome_len, a.seed, solid_h, a.cpu_workers)
-                par["single_core"] = cpu
-                cpu = par
-            except Exception as e:  # the single-core baseline stands
-                cpu["parallel_error"] = repr(e)
+        solid_t = torch.empty(max(ctx.solid_copy(None), 1), dtype=torch.int64, device="cuda")
+        ns = ctx.solid_copy(solid_t.data_ptr())
+        solid_h = solid_t[:ns].cpu().numpy().view(np.uint64)
+        del solid_t
+        cpu = cpu_baseline(reads, solid_h, threads=a.cpu_threads, n_spec=a.cpu_sample_reads,
+                           n_pc=a.cpu_correct_sample_reads, n_pairs=a.cpu_unipath_sample_frags)
 
     aligners = None
     if rank == 0 and a.align_pairs > 0 and not a.spectrum_only:
@@ -620,6 +693,14 @@ def main():
             placement["cpu_baseline"] = placement_cpu_baseline(genome, a)
         if a.jump_pairs > 0:
             placement["jumps"] = jump_bench(ctx, dsrc, genome, a)
+
+    c3 = None
+    if rank == 0 and world == 1 and not a.spectrum_only and a.c3_jump_pairs > 0 and frags is None:
+        c3 = c3_bench(ctx, dsrc, dreads, genome, a)
+
+    f2g = None
+    if rank == 0 and world == 1 and not a.spectrum_only and a.file_to_graph and frags is None:
+        f2g = file_to_graph(ctx, reads, a)
 
     if rank == 0:
         total_reads = world * reads.n_reads * a.steps
@@ -638,9 +719,12 @@ def main():
             "data": "synthetic (deterministic simulator, SURVEY §B; uniform genome, 0.2-2% substitution ramp, "
                     "Q40 / Q2-20 on errors)",
             "config": {
-                "workload": "C2/C3 chr20-size: 40M x 100bp paired frag reads per GPU; K=25 k-mer spectrum + "
-                            "K=24 PreCorrect + FillFragments + K=96 unipath build (unipaths, unibases, "
-                            "HyperKmerPath, fragment KmerPaths) on the filled fragments",
+                "workload": ((f"C4 D. melanogaster-size ({a.genome_len} bp): {reads.n_reads // 1_000_000}M x 100bp "
+                              f"paired frag reads per GPU, {world * reads.n_reads // 1_000_000}M in all; " if c4 else
+                              f"C2/C3 chr20-size ({a.genome_len} bp): {reads.n_reads // 1_000_000}M x 100bp paired "
+                              "frag reads per GPU; ") +
+                             "K=25 k-mer spectrum + K=24 PreCorrect + FillFragments + K=96 unipath build (unipaths, "
+                             "unibases, HyperKmerPath, fragment KmerPaths) on the filled fragments"),
                 "reads_per_gpu": reads.n_reads,
                 "genome_len": a.genome_len,
                 "coverage": coverage,
@@ -662,6 +746,8 @@ def main():
             "cpu_baseline": cpu,
             "aligners": aligners,
             "placement": placement,
+            "c3": c3,
+            "file_to_graph": f2g,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},
             "precorrect_stats": pst,
             "fill_stats": fst,

@@ -1,0 +1,87 @@
+"""Host-cores CPU baseline for bench.py (TEST INFRASTRUCTURE: only bench.py's
+cpu_baseline leg imports this; never part of the product path).
+
+Times the CPU restatement (oracle/, OpenMP over its independent per-read /
+per-pair loops and per-partition sorts) on bounded samples of the bench's own
+synthetic reads, stage by stage — K=25 spectrum, K=24 PreCorrect (count +
+correct), FillFragments against the full-size solid set, K=96 unipaths of the
+filled fragments — once with every thread it is given and once on one
+thread, and names the host CPU.  value = 1 / sum(1 / stage rate), as for the
+GPU step.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+
+
+def host_cpu() -> dict:
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"model": model, "logical_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _stages(reads, solid, n_spec, n_pc, n_pairs, K=25, Kc=24, Ku=96):
+    import oracle
+
+    spec = reads.subset(0, min(n_spec, reads.n_reads))
+    t = time.perf_counter()
+    oracle.kmer_count(spec, K)
+    ts = time.perf_counter() - t
+    pcs = reads.subset(0, min(n_pc, reads.n_reads))
+    t = time.perf_counter()
+    fixed, _ = oracle.precorrect(pcs, K=Kc)
+    tp = time.perf_counter() - t
+    npairs = min(n_pairs, fixed.n_reads // 2)
+    t = time.perf_counter()
+    frags, _, _, _ = oracle.fill_fragments(fixed.subset(0, 2 * npairs), solid, K=Kc)
+    tf = time.perf_counter() - t
+    t = time.perf_counter()
+    oracle.unipaths(frags, Ku)
+    tu = time.perf_counter() - t
+    rates = {"spectrum": spec.n_reads / ts, "precorrect": pcs.n_reads / tp, "fill": 2 * npairs / tf,
+             "unipaths": 2 * npairs / tu}
+    desc = (f"spectrum {spec.n_reads} reads K={K} ({ts:.2f} s); PreCorrect {pcs.n_reads} reads K={Kc}, own "
+            f"solid set ({tp:.2f} s); FillFragments {npairs} restatement-corrected pairs against the full-size "
+            f"solid set ({len(solid)} K-mers, binary search) ({tf:.2f} s); unipaths K={Ku} of the "
+            f"{frags.n_reads} filled fragments ({tu:.2f} s)")
+    return rates, desc, ts + tp + tf + tu
+
+
+def cpu_baseline(reads, solid: np.ndarray, threads: int = 0, n_spec: int = 4_000_000, n_pc: int = 2_000_000,
+                 n_pairs: int = 200_000, single=(500_000, 250_000, 5_000)) -> dict:
+    """The restatement on `threads` OpenMP threads (0: OMP_NUM_THREADS or
+    every CPU of the process), then on one thread with the smaller `single`
+    samples (spectrum reads, PreCorrect reads, Fill pairs)."""
+    import oracle
+
+    solid = np.sort(np.ascontiguousarray(solid, dtype=np.uint64))
+    before = oracle.threads()
+    if threads:
+        oracle.set_threads(threads)
+    used = oracle.threads()
+    try:
+        rates, desc, wall = _stages(reads, solid, n_spec, n_pc, n_pairs)
+        oracle.set_threads(1)
+        r1, d1, w1 = _stages(reads, solid, *single)
+    finally:
+        oracle.set_threads(before)
+    value = 1.0 / sum(1.0 / r for r in rates.values())
+    v1 = 1.0 / sum(1.0 / r for r in r1.values())
+    return {"value": value, "unit": "reads/s", "cores": used, "kind": "port",
+            "stage_reads_per_s": rates, "wall_s": wall, "host": host_cpu(),
+            "sample": (f"oracle/ CPU restatement (OpenMP, {used} threads) on the bench's own synthetic reads: "
+                       + desc + "; value = 1/(sum of 1/stage rate)"),
+            "single_core": {"value": v1, "unit": "reads/s", "cores": 1, "kind": "port",
+                            "stage_reads_per_s": r1, "wall_s": w1, "sample": "one thread: " + d1}}
