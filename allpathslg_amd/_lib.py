@@ -376,7 +376,28 @@ SIGNATURES = {
     "apg_kmerpaths_read": (
         C.c_int, [C.c_char_p, C.POINTER(C.c_int), _u64p, C.POINTER(_u64p), _u64p, C.POINTER(_u64p), C.POINTER(_u64p)]),
     "apg_rc_db_write": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(apg_rc_db)]),
+    # communicators + sharded module entry points
+    "apg_comm_unique_id": (C.c_int, [_P]),
+    "apg_comm_init_rccl": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_uint32, C.POINTER(_P)]),
+    "apg_comm_init_tcp": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    "apg_comm_destroy": (None, [_P]),
+    "apg_comm_rank": (C.c_int, [_P]),
+    "apg_comm_world": (C.c_int, [_P]),
+    "apg_comm_alltoallv": (C.c_int, [_P, _P, _u64p, _P, _u64p]),
+    "apg_comm_allgatherv": (C.c_int, [_P, _P, C.c_uint64, _P, _u64p]),
+    "apg_comm_allreduce_u64": (C.c_int, [_P, _u64p, C.c_uint64, C.c_int]),
+    "apg_comm_barrier": (C.c_int, [_P]),
+    "apg_sharded_spectrum": (C.c_int, [_P, _P, _P, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats)]),
+    "apg_sharded_precorrect": (C.c_int, [_P, _P, _P, C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
+    "apg_sharded_fill": (C.c_int, [_P, _P, _P, C.POINTER(apg_fill_params), _P, C.c_uint64, C.POINTER(_P), _P,
+                                   C.POINTER(apg_fill_stats)]),
+    "apg_sharded_unipaths": (C.c_int, [_P, _P, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),
+                                       C.POINTER(apg_unipath_stats)]),
 }
+
+APG_COMM_SELF_P2P = 1
+APG_COMM_SUM = 0
+APG_COMM_MAX = 1
 
 _lock = threading.Lock()
 _lib = None

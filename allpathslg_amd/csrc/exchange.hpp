@@ -1,0 +1,37 @@
+// exchange.hpp — internal interface of libapg's communicators (exchange.cpp).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/apg.h"
+
+struct apg_ctx;
+
+namespace apg {
+
+// One rank of a sharded run.  Device-memory buffers when ctx is set (the
+// stage entry points), host memory otherwise.  Segments of a send / receive
+// buffer are contiguous in peer order; sizes are bytes per peer.
+struct Comm {
+  static constexpr uint64_t kPiece = 1ull << 30;  // largest single transfer (bytes)
+  apg_ctx* ctx = nullptr;
+  int rank = 0, world = 1;
+  virtual ~Comm() = default;
+  virtual int alltoallv(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes) = 0;
+  virtual int allgatherv(const void* send, uint64_t bytes, void* recv, const uint64_t* recv_bytes) = 0;
+  // in place on host memory (small arrays: spectra, counters)
+  virtual int allreduce_u64(uint64_t* data, uint64_t n, int op) = 0;
+  // host-memory forms (counts, sizes), whatever the communicator's memory kind
+  virtual int alltoallv_host(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes) = 0;
+  virtual int allgatherv_host(const void* send, uint64_t bytes, void* recv, const uint64_t* recv_bytes) = 0;
+  virtual int barrier() = 0;
+  uint64_t piece_bytes() const;
+  // m u64 to every peer (host arrays [peer * m + i])
+  int alltoall_u64(const uint64_t* send, uint64_t* recv, uint64_t m);
+  int allgather_u64(uint64_t v, std::vector<uint64_t>* all);
+};
+
+Comm* comm_of(apg_comm* c);
+
+}  // namespace apg

@@ -1,0 +1,278 @@
+// sharded.cpp — the sharded (multi-GPU) forms of the module entry points:
+// spectrum, PreCorrect / FindErrors, FillFragments and the K=96 unipath
+// build over every rank's reads, one process per GPU, every exchange through
+// the rank's communicator (exchange.cpp).  Each rank holds whole
+// read pairs; K-mers are owned by the shard their minimizer key selects, so
+// shards never share a K-mer.
+//
+//   spectrum     local reads -> 16-byte super-k-mer records by owner shard
+//                -> alltoallv -> owner counts its shard -> allreduce of the
+//                spectrum and the counters
+//   PreCorrect   per pass: records out (their positions stay home) -> owner
+//                counts, keeps its solid K-mers and returns each record's
+//                weak-K-mer mask (alltoallv back) -> allgatherv of the solid
+//                sets -> every rank corrects its own reads through the weak
+//                bitmap its masks rebuild (no weak-test lookups) and keeps the
+//                pass's extension table + clean flags for FillFragments
+//   Fill         pairs are local: no exchange but the counters' sum
+//   unipaths     48-byte K=96 super-k-mer records by owner shard -> alltoallv
+//                -> owner's distinct nodes (OR of extension bits) ->
+//                allgatherv of the node sets -> the graph (same on every
+//                rank) + KmerPaths of this rank's reads
+// Results equal the single-GPU entry points on the union of the ranks' reads
+// (tests/test_distributed.py).
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "apg_core.hpp"
+#include "exchange.hpp"
+
+namespace apg {
+namespace {
+
+int check_comm(apg_ctx* ctx, apg_comm* comm, Comm** out) {
+  Comm* c = comm_of(comm);
+  APG_REQUIRE(ctx && c, "apg_sharded: NULL context or communicator");
+  APG_REQUIRE(c->ctx == ctx, "apg_sharded: the communicator belongs to another context");
+  const int P = c->world;
+  APG_REQUIRE(P >= 1 && (P & (P - 1)) == 0 && P <= 32, "apg_sharded: world size must be a power of two <= 32");
+  *out = c;
+  return APG_OK;
+}
+
+// Per-peer byte sizes of B-group count rows (counts[q * B + g] records of
+// rec_bytes each).
+std::vector<uint64_t> seg_bytes(const std::vector<uint64_t>& counts, int P, int B, uint64_t rec_bytes) {
+  std::vector<uint64_t> b(P, 0);
+  for (int q = 0; q < P; ++q)
+    for (int g = 0; g < B; ++g) b[q] += counts[(size_t)q * B + g] * rec_bytes;
+  return b;
+}
+
+uint64_t total(const std::vector<uint64_t>& v) { return std::accumulate(v.begin(), v.end(), 0ull); }
+
+// counts -> send (scatter callback) -> records exchanged; returns the receive
+// buffer, receive counts and both sides' per-peer byte sizes.
+struct Exchanged {
+  void* recv = nullptr;
+  std::vector<uint64_t> recv_counts, sb, rb;
+  uint64_t n_in = 0, n_out = 0;
+};
+
+template <typename Scatter>
+int exchange_records(apg_ctx* ctx, Comm* c, const std::vector<uint64_t>& counts, int B, uint64_t rec_bytes,
+                     const char* send_ws, const char* recv_ws, Scatter scatter, Exchanged* x) {
+  const int P = c->world;
+  x->sb = seg_bytes(counts, P, B, rec_bytes);
+  x->n_in = total(x->sb) / rec_bytes;
+  void* send = nullptr;
+  APG_TRY(workspace(ctx, send_ws, std::max<uint64_t>(x->n_in * rec_bytes, 64), &send));
+  APG_TRY(scatter(send));
+  x->recv_counts.assign((size_t)P * B, 0);
+  APG_TRY(c->alltoall_u64(counts.data(), x->recv_counts.data(), (uint64_t)B));  // counts[dest * B + g] -> [src * B + g]
+  x->rb = seg_bytes(x->recv_counts, P, B, rec_bytes);
+  x->n_out = total(x->rb) / rec_bytes;
+  APG_TRY(workspace(ctx, recv_ws, std::max<uint64_t>(x->n_out * rec_bytes, 64), &x->recv));
+  return c->alltoallv(send, x->sb.data(), x->recv, x->rb.data());
+}
+
+// allgatherv of n_local elements of `bytes` each from every rank into ws.
+int gather_all(apg_ctx* ctx, Comm* c, const void* local, uint64_t n_local, uint64_t bytes, const char* ws,
+               void** out, uint64_t* n_all) {
+  std::vector<uint64_t> sizes;
+  APG_TRY(c->allgather_u64(n_local, &sizes));
+  std::vector<uint64_t> rb(sizes.size());
+  for (size_t q = 0; q < sizes.size(); ++q) rb[q] = sizes[q] * bytes;
+  *n_all = total(sizes);
+  APG_TRY(workspace(ctx, ws, std::max<uint64_t>(*n_all * bytes, 64), out));
+  return c->allgatherv(local, n_local * bytes, *out, rb.data());
+}
+
+}  // namespace
+}  // namespace apg
+
+using namespace apg;
+
+extern "C" {
+
+int apg_sharded_spectrum(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, int K, uint64_t* hist,
+                         size_t hist_len, apg_kstats* stats) {
+  Comm* c = nullptr;
+  APG_TRY(check_comm(ctx, comm, &c));
+  APG_REQUIRE(reads && hist && hist_len >= 2, "apg_sharded_spectrum: NULL argument or hist_len < 2");
+  const int P = c->world, B = apg_shard_bins(K, P);
+  APG_REQUIRE(B > 0, "apg_sharded_spectrum: K / world size unsupported (K <= 32, world <= 8)");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::vector<uint64_t> counts((size_t)P * B);
+  APG_TRY(apg_shard_count(ctx, reads, K, P, counts.data()));
+  Exchanged x;
+  APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
+                           [&](void* send) { return apg_shard_scatter(ctx, reads, K, P, send); }, &x));
+  apg_kstats st;
+  APG_TRY(apg_shard_spectrum(ctx, x.recv, x.recv_counts.data(), K, P, hist, hist_len, &st));
+  APG_TRY(c->allreduce_u64(hist, hist_len, APG_COMM_SUM));
+  uint64_t v[3] = {st.n_kmers, st.n_distinct, st.n_overflow};
+  APG_TRY(c->allreduce_u64(v, 3, APG_COMM_SUM));
+  uint64_t mb = st.max_bucket;
+  APG_TRY(c->allreduce_u64(&mb, 1, APG_COMM_MAX));
+  st.n_kmers = v[0];
+  st.n_distinct = v[1];
+  st.n_overflow = v[2];
+  st.max_bucket = mb;
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_params* pp,
+                           apg_pc_stats* stats) {
+  Comm* c = nullptr;
+  APG_TRY(check_comm(ctx, comm, &c));
+  APG_REQUIRE(reads, "apg_sharded_precorrect: NULL reads");
+  apg_pc_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_pc_defaults(&p);
+  const int P = c->world, K = p.K, B = apg_shard_bins(K, P);
+  APG_REQUIRE(B > 0, "apg_sharded_precorrect: K / world size unsupported (K <= 32, world <= 8)");
+  APG_REQUIRE(p.n_cycles >= 1, "apg_sharded_precorrect: n_cycles must be >= 1");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const bool weak = K >= 9 && K <= 29;  // the weak-mask return (apg_shard_solid_weak)
+  apg_pc_stats tot;
+  std::memset(&tot, 0, sizeof tot);
+  for (uint32_t cyc = 0; cyc < p.n_cycles; ++cyc) {
+    std::vector<uint64_t> counts((size_t)P * B);
+    APG_TRY(apg_shard_count(ctx, reads, K, P, counts.data()));
+    void* pos = nullptr;
+    Exchanged x;
+    uint64_t n_local = 0;
+    void* smask = nullptr;
+    if (weak) {
+      APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
+                               [&](void* send) {
+                                 const uint64_t n = total(seg_bytes(counts, P, B, 1));
+                                 APG_TRY(workspace(ctx, "x_pos", std::max<uint64_t>(n * 8, 64), &pos));
+                                 return apg_shard_scatter_pos(ctx, reads, K, P, send, pos);
+                               },
+                               &x));
+      void* rmask = nullptr;
+      APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>(x.n_out * 4, 64), &rmask));
+      APG_TRY(apg_shard_solid_weak(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local));
+      // masks travel back: the splits reversed, 4 bytes per record
+      std::vector<uint64_t> mb_out(P), mb_in(P);
+      for (int q = 0; q < P; ++q) {
+        mb_out[q] = x.rb[q] / 16 * 4;
+        mb_in[q] = x.sb[q] / 16 * 4;
+      }
+      APG_TRY(workspace(ctx, "x_smask", std::max<uint64_t>(x.n_in * 4, 64), &smask));
+      APG_TRY(c->alltoallv(rmask, mb_out.data(), smask, mb_in.data()));
+    } else {
+      APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
+                               [&](void* send) { return apg_shard_scatter(ctx, reads, K, P, send); }, &x));
+      APG_TRY(apg_shard_solid(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, &n_local));
+    }
+    void* local = nullptr;
+    APG_TRY(workspace(ctx, "x_local", std::max<uint64_t>(n_local * 8, 64), &local));
+    APG_TRY(apg_solid_export(ctx, local));
+    // the replicated solid set; it stays in "x_solid" as the pass's list
+    // (APG_FILL_LAST_SOLID) until the next sharded pass
+    void* solid = nullptr;
+    uint64_t n_solid = 0;
+    APG_TRY(gather_all(ctx, c, local, n_local, 8, "x_solid", &solid, &n_solid));
+    apg_pc_stats st;
+    if (weak)
+      APG_TRY(apg_precorrect_weak(ctx, reads, &p, solid, n_solid, pos, smask, x.n_in, &st));
+    else
+      APG_TRY(apg_precorrect_solid(ctx, reads, &p, solid, n_solid, &st));
+    tot.n_suspect += st.n_suspect;
+    tot.n_corrected += st.n_corrected;
+    tot.n_ambiguous += st.n_ambiguous;
+    tot.n_uncorrectable += st.n_uncorrectable;
+    tot.n_solid = n_solid;
+  }
+  uint64_t v[4] = {tot.n_suspect, tot.n_corrected, tot.n_ambiguous, tot.n_uncorrectable};
+  APG_TRY(c->allreduce_u64(v, 4, APG_COMM_SUM));
+  tot.n_suspect = v[0];
+  tot.n_corrected = v[1];
+  tot.n_ambiguous = v[2];
+  tot.n_uncorrectable = v[3];
+  if (stats) *stats = tot;
+  return APG_OK;
+}
+
+int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, const apg_fill_params* pp,
+                     const void* d_solid, uint64_t n_solid, apg_dreads** filled, uint8_t* d_status,
+                     apg_fill_stats* stats) {
+  Comm* c = nullptr;
+  APG_TRY(check_comm(ctx, comm, &c));
+  apg_fill_stats st;
+  APG_TRY(apg_fill_fragments_dev(ctx, pairs, pp, d_solid, n_solid, filled, d_status, &st));
+  uint64_t v[8] = {st.n_pairs, st.n_filled, st.n_none, st.n_ambiguous, st.n_budget, st.n_skip, st.filled_bases,
+                   st.lookups};
+  APG_TRY(c->allreduce_u64(v, 8, APG_COMM_SUM));
+  st.n_pairs = v[0];
+  st.n_filled = v[1];
+  st.n_none = v[2];
+  st.n_ambiguous = v[3];
+  st.n_budget = v[4];
+  st.n_skip = v[5];
+  st.filled_bases = v[6];
+  st.lookups = v[7];
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, const apg_unipath_params* pp,
+                         apg_unipath_graph* out, apg_unipath_stats* stats) {
+  Comm* c = nullptr;
+  APG_TRY(check_comm(ctx, comm, &c));
+  APG_REQUIRE(reads, "apg_sharded_unipaths: NULL reads");
+  apg_unipath_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_unipath_defaults(&p);
+  const int P = c->world, K = p.K;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  // minimizer-partition records (48-byte super-k-mers) up to 8 shards, else
+  // distinct local nodes (32-byte records, 32 / P digit groups per shard)
+  const bool rec = P <= 8;
+  const int B = rec ? 32 : 32 / P;
+  const uint64_t W = rec ? 48 : 32;
+  std::vector<uint64_t> counts((size_t)P * B);
+  uint64_t n_inst = 0;
+  if (rec)
+    APG_TRY(apg_urec_count(ctx, reads, K, P, counts.data(), &n_inst));
+  else
+    APG_TRY(apg_ushard_count(ctx, reads, K, P, counts.data(), &n_inst));
+  Exchanged x;
+  APG_TRY(exchange_records(ctx, c, counts, B, W, "x_send", "x_recv",
+                           [&](void* send) {
+                             return rec ? apg_urec_scatter(ctx, reads, K, P, send)
+                                        : apg_ushard_scatter(ctx, reads, K, P, send);
+                           },
+                           &x));
+  uint64_t n_local = 0;
+  if (rec)
+    APG_TRY(apg_urec_nodes(ctx, x.recv, x.recv_counts.data(), K, P, &n_local));
+  else
+    APG_TRY(apg_ushard_nodes(ctx, x.recv, x.recv_counts.data(), K, P, &n_local));
+  void* local = nullptr;
+  APG_TRY(workspace(ctx, "x_local", std::max<uint64_t>(n_local * 32, 64), &local));
+  if (rec)
+    APG_TRY(apg_urec_export(ctx, local));
+  else
+    APG_TRY(apg_ushard_export(ctx, local));
+  void* nodes = nullptr;
+  uint64_t n_nodes = 0;
+  APG_TRY(gather_all(ctx, c, local, n_local, 32, "x_nodes", &nodes, &n_nodes));
+  apg_unipath_stats st;
+  APG_TRY(apg_unipaths_from_nodes(ctx, nodes, n_nodes, reads, &p, out, &st));
+  APG_TRY(c->allreduce_u64(&n_inst, 1, APG_COMM_SUM));
+  st.n_instances = n_inst;
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+}  // extern "C"

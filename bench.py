@@ -14,9 +14,11 @@ in HBM:
   5. K=96 unipaths + unibases + HyperKmerPath + KmerPaths of the filled
      fragments (K=96 needs fragment-length inputs).
      --oracle-fill substitutes the simulator's true inserts (old bench).
-N > 1: weak scaling (40 M reads per GPU); k-mers hash-sharded across ranks
-with all_to_all over RCCL, solid sets all_gathered, spectra all_reduced,
-pairs filled where they live (no exchange), unipath nodes all_gathered.
+N > 1: BASELINE configs[3] (C4, D. melanogaster-size genome, 50 M reads per
+GPU = 400 M on 8, weak scaling) through the sharded module entry points
+(include/apg.h apg_sharded_*): K-mers owned by minimizer-key shards, records
+exchanged inside libapg over RCCL (all-to-all), solid and node sets
+all-gathered, spectra summed, pairs filled where they live.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -38,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 from allpathslg_amd import Context, synth_fragments, synth_genome, synth_reads  # noqa: E402
 from allpathslg_amd.distributed import (  # noqa: E402
-    HipShardBackend, sharded_fill, sharded_precorrect, sharded_spectrum, sharded_unipaths)
+    Comm, sharded_fill, sharded_precorrect, sharded_spectrum, sharded_unipaths, unique_id)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -503,7 +505,10 @@ def main():
     if a.reads_per_gpu is None:
         a.reads_per_gpu = 50_000_000 if c4 else 40_000_000
     if sharded:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # torch.distributed (gloo, CPU) only bootstraps: it passes rank 0's RCCL
+        # id to every rank and gives the bench its barrier and max-over-ranks
+        # time; every exchange of the sharded stages runs inside libapg
+        dist.init_process_group("gloo")
 
     t0 = time.time()
     genome = synth_genome(a.genome_len, a.seed)
@@ -517,7 +522,11 @@ def main():
     dsrc = ctx.upload(reads)
     dreads = ctx.upload(reads)
     dfrags = None if frags is None else ctx.upload(frags)
-    backend = HipShardBackend(ctx)
+    comm = None
+    if sharded:
+        uid = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm.rccl(ctx, uid[0], rank, world)
     fill = {"out": None}  # device read set of the filled fragments, reused every step
 
     # --overlap: the K=25 spectrum of the pristine reads runs on a second
@@ -539,7 +548,7 @@ def main():
         elif not sharded:
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
-            hist, st = sharded_spectrum(backend, dreads, a.K)
+            hist, st = sharded_spectrum(ctx, comm, dreads, a.K)
         pst = ust = fst = None
         if not a.spectrum_only:
             if not sharded:
@@ -552,15 +561,14 @@ def main():
                     uin = fill["out"]
                 _, ust = ctx.unipaths(uin, a.K_unipath, read_paths=True, fetch=False)
             else:
-                pst, solid, ns = sharded_precorrect(backend, dreads, K=a.K_correct, keep_solid=True)
+                pst = sharded_precorrect(ctx, comm, dreads, K=a.K_correct)
                 if a.oracle_fill:
                     uin = dfrags
                 else:
-                    fill["out"], fst = sharded_fill(backend, dreads, solid, ns, K=a.K_correct, out=fill["out"],
+                    fill["out"], fst = sharded_fill(ctx, comm, dreads, K=a.K_correct, out=fill["out"],
                                                    last_solid=True)
                     uin = fill["out"]
-                del solid
-                ust = sharded_unipaths(backend, uin, a.K_unipath)
+                _, ust = sharded_unipaths(ctx, comm, uin, a.K_unipath)
         if fut is not None:
             hist, st = fut.result()
         return hist, st, pst, ust, fst
@@ -584,7 +592,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if sharded:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -739,7 +747,8 @@ def main():
                                   "FillFragments of the corrected pairs (K=24 closures, insert 126-234), on GPU "
                                   "inside the timed step"),
                 "hbm_used_gb": (total_b - free_b) / 1e9,
-                "parallelism": f"kmer-hash shards x{world} + all_to_all" if sharded else "single GPU",
+                "parallelism": (f"minimizer-key shards x{world}, libapg exchange over RCCL (apg_sharded_*)" if sharded
+                                else "single GPU"),
             },
             "roofline": roofline,
             "kernels": kernels,
@@ -763,6 +772,8 @@ def main():
         fill["out"].free()
     if ctx_s is not None:
         ctx_s.close()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if sharded:
         dist.destroy_process_group()

@@ -192,6 +192,45 @@ int apg_shard_spectrum(apg_ctx* ctx, const void* d_recv,
                        apg_kstats* stats);
 
 /* ------------------------------------------------------------------------- */
+/* Communicators: the exchange of a sharded run, one process per GPU          */
+/* (SURVEY §8e).  ALLPATHS-LG has no collective layer (single process,        */
+/* OpenMP), so these replace nothing in it: they are what the      */
+/* apg_sharded_* module entry points below exchange through.                  */
+/*   rccl: device buffers over RCCL (xGMI): ranks share the 128-byte id of    */
+/*         apg_comm_unique_id (made on one rank, passed to all by the         */
+/*         launcher); grouped point-to-point transfers of <= 1 GiB pieces on  */
+/*         the context's stream.  APG_COMM_SELF_P2P also routes the segment   */
+/*         to self through RCCL (world-size-1 tests of the transport).        */
+/*   tcp:  host sockets, full mesh through rank 0 at master_addr:master_port. */
+/*         With a ctx, device buffers are staged through pinned host memory; */
+/*         with ctx = NULL the buffers are host memory.  Several ranks may    */
+/*         share one GPU (tests), and the drop-in CLIs use it to bootstrap.   */
+/* Collectives are blocking; every rank must call them in the same order.     */
+/* Byte counts are per peer and u64; segments are contiguous in rank order.   */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_comm apg_comm;
+#define APG_COMM_SELF_P2P 1u
+enum { APG_COMM_SUM = 0, APG_COMM_MAX = 1 };
+int apg_comm_unique_id(void* id128);
+int apg_comm_init_rccl(apg_ctx* ctx, const void* id128, int rank, int world, uint32_t flags, apg_comm** out);
+int apg_comm_init_tcp(apg_ctx* ctx /* or NULL: host buffers */, const char* master_addr, int master_port,
+                      int rank, int world, int timeout_ms /* <= 0: 600 s */, apg_comm** out);
+void apg_comm_destroy(apg_comm* comm);
+int apg_comm_rank(const apg_comm* comm);
+int apg_comm_world(const apg_comm* comm);
+/* send: world segments of send_bytes[q] bytes (segment q goes to rank q);
+ * recv: world segments of recv_bytes[q] bytes (from rank q).  Sizes must
+ * agree pairwise (checked on tcp). */
+int apg_comm_alltoallv(apg_comm* comm, const void* send, const uint64_t* send_bytes, void* recv,
+                       const uint64_t* recv_bytes);
+/* recv: every rank's send_bytes in rank order (recv_bytes[q] from rank q). */
+int apg_comm_allgatherv(apg_comm* comm, const void* send, uint64_t send_bytes, void* recv,
+                        const uint64_t* recv_bytes);
+/* In place on host memory: element-wise sum or max over ranks. */
+int apg_comm_allreduce_u64(apg_comm* comm, uint64_t* data, uint64_t n, int op);
+int apg_comm_barrier(apg_comm* comm);
+
+/* ------------------------------------------------------------------------- */
 /* Read error correction (restated; semantics unpinned).         */
 /* Replaces module PreCorrect ([R:M-L] src/PreCorrect.cc; n_cycles = 1) and  */
 /* the spectrum part of FindErrors ([R:M] src/FindErrors.cc,                  */
@@ -635,6 +674,31 @@ int apg_unipath_locs_dev(apg_ctx* ctx, const apg_dreads* reads, uint32_t flags, 
 /* The last build's unibases as a new device read set (one read per unipath, */
 /* no qualities; release with apg_reads_free) — the aligners' targets. */
 int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out);
+
+/* ------------------------------------------------------------------------- */
+/* Sharded module entry points (multi-GPU, one process per GPU):  */
+/* the same modules over the union of every rank's reads, every exchange     */
+/* through `comm` (which must have been made for ctx).  Each rank passes its */
+/* own reads (whole pairs); results equal the single-GPU entry points on the */
+/* union (tests/test_distributed.py):                                        */
+/*   spectrum   the global spectrum on every rank; stats summed              */
+/*   precorrect every rank's reads corrected in place against the global     */
+/*              solid set (which stays on the context for                    */
+/*              APG_FILL_LAST_SOLID); stats summed, n_solid global           */
+/*   fill       this rank's pairs (no exchange); stats summed                */
+/*   unipaths   the global graph (identical on every rank, out may be NULL)  */
+/*              + KmerPaths of this rank's reads; n_instances summed         */
+/* World size: a power of two <= 8 (spectrum, PreCorrect) / <= 32 (unipaths).*/
+/* ------------------------------------------------------------------------- */
+int apg_sharded_spectrum(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, int K, uint64_t* hist,
+                         size_t hist_len, apg_kstats* stats);
+int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_params* p,
+                           apg_pc_stats* stats);
+int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, const apg_fill_params* p,
+                     const void* d_solid, uint64_t n_solid, apg_dreads** filled, uint8_t* d_status,
+                     apg_fill_stats* stats);
+int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, const apg_unipath_params* p,
+                         apg_unipath_graph* out, apg_unipath_stats* stats);
 
 /* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */

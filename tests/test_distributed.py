@@ -1,130 +1,30 @@
-"""World-size-2 (and 4) gloo tests of the multi-GPU exchange logic on CPU.
+"""Sharded module entry points through the C ABI (include/apg.h
+apg_sharded_*), one process per rank, every exchange inside libapg:
 
-The driver (allpathslg_amd.distributed.sharded_spectrum) is run with an
-oracle-backed shard backend: same contract as libapg's shard_* stages
-(records = k-mer hashes grouped by (owner shard, L1 group)), computed on the
-CPU.  The GPU stages themselves are covered by test_gpu_kmer.py's loopback
-shard test; this covers splits, count-matrix exchange and the all_reduce.
+  * world 2 and 4: ranks share GPU 0 and talk over the TCP communicator;
+    spectrum, PreCorrect (1 and 2 passes), FillFragments and the K=96
+    unipath graph + KmerPaths equal the single-GPU entry points on the union
+    of the ranks' reads;
+  * world 1 over RCCL with the segment to self routed through ncclSend /
+    ncclRecv (APG_COMM_SELF_P2P): the same stages, and one alltoallv of
+    2^31 + 4 KiB bytes compared byte for byte (the size at which the old
+    torch-level exchange once lost data).
 """
+import multiprocessing as mp
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
-import oracle
-from allpathslg_amd import shard_bins, synth_genome, synth_reads
-from allpathslg_amd.distributed import sharded_spectrum
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+GENOME, PAIRS, SEED = 250_000, 48_000, 0xD157
 
 
-class OracleShardBackend:
-    def __init__(self):
-        self.cache = {}
-
-    def alloc(self, n):
-        return torch.empty(max(n, 1), dtype=torch.int64)
-
-    def _digits(self, reads, K, P):
-        key = (id(reads), K, P)
-        if key not in self.cache:
-            h = oracle.extract_hashes(reads, K)
-            D = int(np.log2(P)) + int(np.log2(shard_bins(K, P)))
-            d = (h >> np.uint64(2 * K - D)).astype(np.int64) if D else np.zeros(len(h), np.int64)
-            self.cache[key] = (h, d)
-        return self.cache[key]
-
-    def shard_count(self, reads, K, P):
-        h, d = self._digits(reads, K, P)
-        return np.bincount(d, minlength=P * shard_bins(K, P)).astype(np.uint64)
-
-    def shard_scatter(self, reads, K, P, send):
-        h, d = self._digits(reads, K, P)
-        order = np.argsort(d, kind="stable")
-        send[: len(h)] = torch.from_numpy(h[order].view(np.int64))
-
-    def shard_spectrum(self, recv, recv_counts, K, P, hist_len):
-        n = int(recv_counts.sum())
-        h = recv[:n].numpy().view(np.uint64)
-        rank = dist.get_rank()
-        pbits = int(np.log2(P))
-        if n and pbits:
-            assert np.all((h >> np.uint64(2 * K - pbits)) == rank), "record delivered to the wrong shard"
-        _, c = np.unique(h, return_counts=True)
-        hist = oracle.spectrum_from_counts(c.astype(np.uint32), hist_len)
-        return hist, {"n_kmers": n, "n_distinct": len(c), "n_overflow": 0}
-
-    # correction stages: solid set of the received records, pass on own reads
-    def shard_solid(self, recv, recv_counts, K, P, min_solid):
-        n = int(recv_counts.sum())
-        u, c = np.unique(recv[:n].numpy().view(np.uint64), return_counts=True)
-        self.solid = u[c >= min_solid]
-        return len(self.solid)
-
-    def solid_export(self, out):
-        out[: len(self.solid)] = torch.from_numpy(self.solid.view(np.int64))
-
-    def precorrect_solid(self, reads, solid, n_solid, prm):
-        fixed, st = oracle.precorrect_solid(reads, solid[:n_solid].numpy().view(np.uint64), prm["K"],
-                                            prm["max_q_suspect"])
-        reads.packed[:] = fixed.packed  # in place, like the device path
-        reads.quals[:] = fixed.quals
-        self.cache.clear()  # bases changed
-        return st
-
-    def fill(self, reads, solid, n_solid, prm, out=None):
-        filled, _, _, st = oracle.fill_fragments(reads, solid[:n_solid].numpy().view(np.uint64), **prm)
-        st["n_pairs"] = reads.n_reads // 2
-        return filled, st
-
-
-class OracleWeakBackend(OracleShardBackend):
-    """OracleShardBackend + the weak-mask return contract (apg_shard_scatter_pos
-    / apg_shard_solid_weak / apg_precorrect_weak): records are single K-mer
-    hashes, so a record's mask is one bit.  precorrect_weak checks that the
-    bitmap rebuilt from the returned masks is exactly the set of this rank's
-    K-mer instances outside the global solid set, then corrects."""
-
-    def _pos(self, reads, K):
-        L = reads.lengths().astype(np.int64)
-        nk = np.maximum(L - K + 1, 0)
-        start = np.repeat(reads.base_off[:-1].astype(np.int64), nk)
-        return start + (np.arange(int(nk.sum())) - np.repeat(np.cumsum(nk) - nk, nk))
-
-    def shard_scatter_pos(self, reads, K, P, send, pos):
-        h, d = self._digits(reads, K, P)
-        order = np.argsort(d, kind="stable")
-        send[: len(h)] = torch.from_numpy(h[order].view(np.int64))
-        pos[: len(h)] = torch.from_numpy(self._pos(reads, K)[order])
-
-    def alloc_mask(self, n):
-        return torch.zeros(max(n, 1), dtype=torch.int32)
-
-    def shard_solid_weak(self, recv, recv_counts, K, P, min_solid, mask):
-        n = int(recv_counts.sum())
-        h = recv[:n].numpy().view(np.uint64)
-        u, inv, c = np.unique(h, return_inverse=True, return_counts=True)
-        self.solid = u[c >= min_solid]
-        mask[:n] = torch.from_numpy((c[inv] < min_solid).astype(np.int32))
-        return len(self.solid)
-
-    def precorrect_weak(self, reads, solid, n_solid, pos, mask, n_records, prm):
-        K = prm["K"]
-        weak = np.zeros(reads.n_bases + 1, dtype=bool)
-        m = mask[:n_records].numpy() != 0
-        weak[pos[:n_records].numpy()[m]] = True
-        h = oracle.extract_hashes(reads, K)
-        sol = np.isin(h, solid[:n_solid].numpy().view(np.uint64))
-        exp = np.zeros(reads.n_bases + 1, dtype=bool)
-        exp[self._pos(reads, K)[~sol]] = True
-        assert np.array_equal(weak, exp), "weak bitmap from the returned masks differs"
-        self.weak_checked = getattr(self, "weak_checked", 0) + 1
-        return self.precorrect_solid(reads, solid, n_solid, prm)
-
-
-def _free_port():
+def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
@@ -132,283 +32,159 @@ def _free_port():
     return p
 
 
-def _small_chunks():
-    """Force the chunked collectives through many rounds (odd-sized chunks)."""
-    import allpathslg_amd.distributed as D
-
-    D.CHUNK_ELEMS = 4093
+def rank_pairs(rank, world):
+    return PAIRS * rank // world, PAIRS * (rank + 1) // world
 
 
-def _worker(rank, world, port, K, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    _small_chunks()
+def chain(ctx, comm, reads, n_cycles):
+    """The sharded chain on this rank's reads; host copies of everything."""
+    from allpathslg_amd.distributed import (sharded_fill, sharded_precorrect, sharded_spectrum,
+                                            sharded_unipaths)
+
+    d = ctx.upload(reads)
+    hist, st = sharded_spectrum(ctx, comm, d, 25)
+    pst = sharded_precorrect(ctx, comm, d, K=24, n_cycles=n_cycles)
+    fixed = ctx.download(d)
+    filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
+    ffrag = ctx.download(filled)
+    graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True)
+    d.free()
+    filled.free()
+    return {"hist": hist, "st": st, "pst": pst, "fixed": fixed, "fst": fst, "filled": ffrag, "graph": graph,
+            "ust": ust}
+
+
+def worker(rank, world, port, n_cycles, q):
+    sys.path.insert(0, ROOT)
     try:
-        g = synth_genome(100_000, 21)
-        reads = synth_reads(g, 4000, seed=22)
-        parts = np.array_split(np.arange(reads.n_reads), world)
-        mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
-        hist, st = sharded_spectrum(OracleShardBackend(), mine, K, hist_len=1 << 12)
-        q.put((rank, hist, st))
-    finally:
-        dist.destroy_process_group()
+        from allpathslg_amd import Context, synth_genome, synth_reads
+        from allpathslg_amd.distributed import Comm
+
+        g = synth_genome(GENOME, SEED)
+        a, b = rank_pairs(rank, world)
+        reads = synth_reads(g, b - a, seed=SEED + 1, first_pair=a)
+        with Context(device=0) as ctx:
+            comm = Comm.tcp(ctx, "127.0.0.1", port, rank, world, timeout_ms=240_000)
+            out = chain(ctx, comm, reads, n_cycles)
+            comm.close()
+        q.put((rank, out, ""))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_spectrum_gloo(world):
-    K = 25
+def run_world(world, n_cycles):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, K, q)) for r in range(world)]
-    for p in procs:
+    port = free_port()
+    ps = [ctx.Process(target=worker, args=(r, world, port, n_cycles, q)) for r in range(world)]
+    for p in ps:
         p.start()
-    res = [q.get(timeout=180) for _ in range(world)]
-    for p in procs:
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
         p.join(timeout=60)
-        assert p.exitcode == 0
-    g = synth_genome(100_000, 21)
-    reads = synth_reads(g, 4000, seed=22)
-    expect = oracle.kmer_spectrum(reads, K, 1 << 12)
-    for rank, hist, st in res:
-        assert np.array_equal(hist, expect)
-        assert st["n_kmers"] == reads.n_reads * (100 - K + 1)
-        assert st["n_distinct"] == int(expect.sum())
+    res.sort(key=lambda x: x[0])
+    for rank, out, err in res:
+        assert out is not None, (rank, err)
+    return [r[1] for r in res]
 
 
-class OracleUnipathBackend(OracleShardBackend):
-    """CPU stand-in for libapg's ushard_* stages (same record layout:
-    4 x int64 = canonical key limbs + (56-bit hash | ext bits))."""
+@pytest.fixture(scope="module")
+def mono(gpu_ctx):
+    """The single-GPU entry points on the union of the ranks' reads."""
+    from allpathslg_amd import synth_genome, synth_reads
 
-    def _inst(self, reads, K):
-        key = ("u", id(reads), K)
-        if key not in self.cache:
-            self.cache[key] = oracle.instances(reads, K)
-        return self.cache[key]
-
-    def _local(self, reads, K):
-        """This rank's distinct local nodes (key, ext, hash) in digit order."""
-        key = ("n", id(reads), K)
-        if key not in self.cache:
-            k, e, h = self._inst(reads, K)
-            nk, ne = oracle.group_nodes(k.copy(), e.astype(np.uint8))
-            # hash of each distinct key = the hash of any of its instances
-            uk, first = np.unique(k, axis=0, return_index=True)
-            assert np.array_equal(uk, nk)
-            hh = h[first]
-            d = (hh >> np.uint64(59)).astype(np.int64)
-            o = np.argsort(d, kind="stable")
-            out = np.zeros((len(ne), 4), dtype=np.uint64)
-            out[:, :3] = nk[o]
-            out[:, 3] = hh[o] | ne[o].astype(np.uint64)
-            self.cache[key] = (out, np.bincount(d, minlength=32).astype(np.uint64), len(h))
-        return self.cache[key]
-
-    def ushard_count(self, reads, K, P):
-        out, counts, n_inst = self._local(reads, K)
-        return counts, n_inst
-
-    def ushard_scatter(self, reads, K, P, send):
-        out, _, _ = self._local(reads, K)
-        send[: 4 * len(out)] = torch.from_numpy(out.reshape(-1).view(np.int64))
-
-    def ushard_nodes(self, recv, recv_counts, K, P):
-        n = int(recv_counts.sum())
-        rec = recv[: 4 * n].numpy().view(np.uint64).reshape(n, 4)
-        pbits = int(np.log2(P))
-        if n and pbits:
-            assert np.all((rec[:, 3] >> np.uint64(64 - pbits)) == dist.get_rank())
-        self.nodes = oracle.group_nodes(rec[:, :3].copy(), (rec[:, 3] & np.uint64(0xFF)).astype(np.uint8))
-        return len(self.nodes[1])
-
-    def ushard_export(self, out):
-        k, e = self.nodes
-        rec = np.zeros((len(e), 4), dtype=np.uint64)
-        rec[:, :3] = k
-        rec[:, 3] = e.astype(np.uint64)
-        out[: 4 * len(e)] = torch.from_numpy(rec.reshape(-1).view(np.int64))
-
-    def graph_from_nodes(self, nodes, n_nodes, reads, K, fetch):
-        rec = nodes[: 4 * n_nodes].numpy().view(np.uint64).reshape(n_nodes, 4)
-        g = oracle.graph_from_nodes(rec[:, :3].copy(), (rec[:, 3] & np.uint64(0xFF)).astype(np.uint8), reads, K)
-        return g, {"n_unipaths": g["n_unipaths"], "n_nodes": g["n_nodes"]}
+    g = synth_genome(GENOME, SEED)
+    reads = synth_reads(g, PAIRS, seed=SEED + 1)
+    out = {}
+    for n_cycles in (1, 2):
+        d = gpu_ctx.upload(reads)
+        hist, st = gpu_ctx.kmer_spectrum(d, 25)
+        _, pst = gpu_ctx.precorrect(d, K=24, n_cycles=n_cycles)
+        fixed = gpu_ctx.download(d)
+        filled, _, fst = gpu_ctx.fill_fragments(d, K=24, last_solid=True)
+        ffrag = gpu_ctx.download(filled)
+        graph, ust = gpu_ctx.unipaths(filled, 96)
+        out[n_cycles] = {"reads": reads, "hist": hist, "st": st, "pst": pst, "fixed": fixed, "fst": fst,
+                         "filled": ffrag, "graph": graph, "ust": ust}
+        d.free()
+        filled.free()
+    return out
 
 
-class OracleRecBackend(OracleUnipathBackend):
-    """OracleUnipathBackend with the minimizer-record contract (urec_*):
-    6-word records, counts per (shard, 32 digits).  The oracle's records are
-    K-mer instances (key limbs, hash | ext, padding) grouped by the top
-    log2(P) + 5 hash bits — any grouping every instance of a K-mer shares
-    satisfies the contract."""
-
-    urec_words = 6
-
-    def _recs(self, reads, K, P):
-        key = ("r", id(reads), K, P)
-        if key not in self.cache:
-            k, e, h = self._inst(reads, K)
-            D = int(np.log2(P)) + 5
-            d = (h >> np.uint64(64 - D)).astype(np.int64)
-            o = np.argsort(d, kind="stable")
-            out = np.zeros((len(h), 6), dtype=np.uint64)
-            out[:, :3] = k[o]
-            out[:, 3] = h[o] | e[o].astype(np.uint64)
-            self.cache[key] = (out, np.bincount(d, minlength=P * 32).astype(np.uint64), len(h))
-        return self.cache[key]
-
-    def urec_count(self, reads, K, P):
-        out, counts, n_inst = self._recs(reads, K, P)
-        return counts, n_inst
-
-    def urec_scatter(self, reads, K, P, send):
-        out, _, _ = self._recs(reads, K, P)
-        send[: 6 * len(out)] = torch.from_numpy(out.reshape(-1).view(np.int64))
-
-    def urec_nodes(self, recv, recv_counts, K, P):
-        n = int(recv_counts.sum())
-        rec = recv[: 6 * n].numpy().view(np.uint64).reshape(n, 6)
-        pbits = int(np.log2(P))
-        if n and pbits:
-            assert np.all((rec[:, 3] >> np.uint64(64 - pbits)) == dist.get_rank())
-        self.nodes = oracle.group_nodes(rec[:, :3].copy(), (rec[:, 3] & np.uint64(0xFF)).astype(np.uint8))
-        return len(self.nodes[1])
-
-    def urec_export(self, out):
-        self.ushard_export(out)
+def rows(r, a, b):
+    """Reads [a, b) of a host read set as (lengths, packed bytes, quals)."""
+    s = r.subset(a, b)
+    return s.lengths(), s.packed[: int(s.byte_off[-1])], s.quals
 
 
-def _uworker(rank, world, port, K, q, rec=False):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    _small_chunks()
-    try:
-        from allpathslg_amd.distributed import sharded_unipaths
-        from tests.unipath_cases import noisy_reads
-
-        reads = noisy_reads(G=15_000, n=2000)
-        parts = np.array_split(np.arange(reads.n_reads), world)
-        mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
-        g, st = sharded_unipaths(OracleRecBackend() if rec else OracleUnipathBackend(), mine, K, fetch=True)
-        q.put((rank, int(parts[rank][0]), int(parts[rank][-1]) + 1, g, st))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,rec", [(2, False), (4, False), (2, True), (4, True)])
-def test_sharded_unipaths_gloo(world, rec):
-    """Sharded unipath graph == single-process graph, with distinct-local-node
-    records or with minimizer-partition records (rec)."""
-    from tests.unipath_cases import noisy_reads
-
-    K = 63
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_uworker, args=(r, world, port, K, q, rec)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    reads = noisy_reads(G=15_000, n=2000)
-    exp = oracle.unipaths(reads, K)
-    for rank, a, b, g, st in res:
-        for k in ("len", "id_base", "rc", "ub_off", "unibases", "from", "to"):
-            assert np.array_equal(g[k], exp[k]), k
-        assert st["n_instances"] == reads.n_reads * (100 - K + 1)
-        lo, hi = int(exp["path_off"][a]), int(exp["path_off"][b])
-        assert np.array_equal(g["path_start"], exp["path_start"][lo:hi])
-        assert np.array_equal(g["path_len"], exp["path_len"][lo:hi])
-
-
-def _pcworker(rank, world, port, n_cycles, q, weak=False):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    _small_chunks()
-    try:
-        from allpathslg_amd.distributed import sharded_precorrect
-
-        reads = synth_reads(synth_genome(30_000, 31), 3000, seed=32)
-        parts = np.array_split(np.arange(reads.n_reads), world)
-        mine = reads.subset(int(parts[rank][0]), int(parts[rank][-1]) + 1)
-        be = OracleWeakBackend() if weak else OracleShardBackend()
-        st = sharded_precorrect(be, mine, K=24, n_cycles=n_cycles)
-        if weak:
-            assert getattr(be, "weak_checked", 0) == n_cycles
-        q.put((rank, mine.packed[: int(mine.byte_off[-1])].copy(), mine.quals.copy(), st))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,n_cycles,weak", [(2, 1, False), (4, 2, False), (2, 1, True), (4, 2, True)])
-def test_sharded_precorrect_gloo(world, n_cycles, weak):
-    """Replicated-solid-set correction == single-process PreCorrect/FindErrors
-    (weak: with the weak-mask return, whose bitmap the backend verifies)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_pcworker, args=(r, world, port, n_cycles, q, weak)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    reads = synth_reads(synth_genome(30_000, 31), 3000, seed=32)
-    exp, est = oracle.precorrect(reads, K=24, n_cycles=n_cycles)
-    assert est["n_corrected"] > 0
-    assert np.array_equal(np.concatenate([r[1] for r in res]), exp.packed[: int(exp.byte_off[-1])])
-    assert np.array_equal(np.concatenate([r[2] for r in res]), exp.quals)
-    for _, _, _, st in res:
+def check_against_mono(parts, m, world):
+    graph_keys = ["n_nodes", "n_unipaths", "len", "id_base", "rc", "ub_off", "unibases", "n_vertices", "from", "to"]
+    f_off = 0
+    for rank, p in enumerate(parts):
+        assert np.array_equal(p["hist"], m["hist"])
+        for k in ("n_kmers", "n_distinct"):
+            assert p["st"][k] == m["st"][k], k
         for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
-            assert st[k] == est[k], k
+            assert p["pst"][k] == m["pst"][k], (rank, k)
+        a, b = rank_pairs(rank, world)
+        got, exp = rows(p["fixed"], 0, p["fixed"].n_reads), rows(m["fixed"], 2 * a, 2 * b)
+        for x, y in zip(got, exp):
+            assert np.array_equal(x, y), rank
+        for k in ("n_pairs", "n_filled", "n_none", "n_ambiguous", "filled_bases"):
+            assert p["fst"][k] == m["fst"][k], (rank, k)
+        nf = p["filled"].n_reads
+        gl, gp, _ = rows(p["filled"], 0, nf)
+        el, ep, _ = rows(m["filled"], f_off, f_off + nf)
+        assert np.array_equal(gl, el) and np.array_equal(gp, ep), rank
+        for k in graph_keys:
+            a_, b_ = p["graph"][k], m["graph"][k]
+            assert (np.array_equal(a_, b_) if isinstance(a_, np.ndarray) else a_ == b_), (rank, k)
+        # this rank's fragments' KmerPaths = its slice of the monolithic ones
+        mo, po = m["graph"]["path_off"], p["graph"]["path_off"]
+        lo, hi = int(mo[f_off]), int(mo[f_off + nf])
+        assert np.array_equal(po - po[0], mo[f_off : f_off + nf + 1] - lo)
+        assert np.array_equal(p["graph"]["path_start"], m["graph"]["path_start"][lo:hi])
+        assert np.array_equal(p["graph"]["path_len"], m["graph"]["path_len"][lo:hi])
+        assert p["ust"]["n_instances"] == m["ust"]["n_instances"]
+        f_off += nf
+    assert f_off == m["filled"].n_reads
 
 
-def _fillworker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    _small_chunks()
+@pytest.mark.parametrize("world,n_cycles", [(2, 1), (4, 1), (2, 2)])
+def test_sharded_chain_tcp_equals_single_gpu(mono, world, n_cycles):
+    check_against_mono(run_world(world, n_cycles), mono[n_cycles], world)
+
+
+def test_sharded_chain_rccl_world1_equals_single_gpu(gpu_ctx, mono):
+    from allpathslg_amd.distributed import Comm, unique_id
+
+    comm = Comm.rccl(gpu_ctx, unique_id(), 0, 1, self_p2p=True)
     try:
-        from allpathslg_amd.distributed import sharded_fill, sharded_precorrect
-
-        reads = synth_reads(synth_genome(30_000, 41), 3000, seed=42)
-        pairs = np.array_split(np.arange(reads.n_reads // 2), world)  # ranks hold whole pairs
-        mine = reads.subset(2 * int(pairs[rank][0]), 2 * int(pairs[rank][-1]) + 2)
-        be = OracleShardBackend()
-        _, solid, ns = sharded_precorrect(be, mine, K=24, keep_solid=True)
-        filled, st = sharded_fill(be, mine, solid, ns, K=24)
-        q.put((rank, filled.base_off.copy(), filled.packed[: int(filled.byte_off[-1])].copy(), st))
+        out = chain(gpu_ctx, comm, mono[1]["reads"], 1)
+        check_against_mono([out], mono[1], 1)
     finally:
-        dist.destroy_process_group()
+        comm.close()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_fill_gloo(world):
-    """Precorrect with the replicated solid set, then FillFragments per rank
-    == single-process PreCorrect + FillFragments, fragments in pair order."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_fillworker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    reads = synth_reads(synth_genome(30_000, 41), 3000, seed=42)
-    fixed, _ = oracle.precorrect(reads, K=24)
-    exp, es, _, est = oracle.fill_fragments(fixed, oracle.solid_hashes(reads, 24, 3), K=24)
-    assert est["n_filled"] > 0
-    lens = np.concatenate([np.diff(r[1]) for r in res])
-    assert np.array_equal(lens, np.diff(exp.base_off))
-    assert np.array_equal(np.concatenate([r[2] for r in res]), exp.packed[: int(exp.byte_off[-1])])
-    for _, _, _, st in res:
-        for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases"):
-            assert st[k] == est[k], k
-        assert st["n_pairs"] == reads.n_reads // 2
+def test_rccl_exchange_above_2gib_bytewise(gpu_ctx):
+    import torch
+
+    from allpathslg_amd.distributed import Comm, unique_id
+
+    n = (1 << 31) + 4096
+    comm = Comm.rccl(gpu_ctx, unique_id(), 0, 1, self_p2p=True)
+    try:
+        g = torch.Generator(device="cuda")
+        g.manual_seed(5)
+        src = torch.randint(-(2**31), 2**31 - 1, (n // 4,), dtype=torch.int32, device="cuda", generator=g)
+        dst = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        comm.alltoallv(src.data_ptr(), [n], dst.data_ptr(), [n])
+        assert torch.equal(src, dst)
+        # the same through allgatherv
+        dst.zero_()
+        torch.cuda.synchronize()
+        comm.allgatherv(src.data_ptr(), n, dst.data_ptr(), [n])
+        assert torch.equal(src, dst)
+    finally:
+        comm.close()
