@@ -109,3 +109,66 @@ def test_cli_error_correct_jump_matches_oracle(tmp_path):
         assert np.array_equal(out.read(r), fixed.read(r)[:k])
         assert np.array_equal(out.quals[int(out.base_off[r]) : int(out.base_off[r + 1])],
                               fixed.quals[int(fixed.base_off[r]) : int(fixed.base_off[r]) + k])
+
+
+def test_cli_shard_argument_errors(tmp_path):
+    _stage(tmp_path, "frag_reads_filt")
+    p = run("KmerSpectrum", f"RUN={tmp_path}", "WORLD=2", "RANK=2")
+    assert p.returncode == 1 and "RANK / WORLD" in p.stderr
+    p = run("KmerSpectrum", f"RUN={tmp_path}", "WORLD=2", "RANK=0", "COMM=mpi")
+    assert p.returncode == 1 and "COMM must be" in p.stderr
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run_ranks(module, world, *args):
+    """`world` processes of one module (WORLD/RANK/COMM=tcp on 127.0.0.1),
+    sharing GPU 0; returns their completed processes."""
+    _ensure_bin()
+    port = _free_port()
+    ps = [subprocess.Popen([os.path.join(BIN, module), *args, f"WORLD={world}", f"RANK={r}", "COMM=tcp",
+                            "MASTER_ADDR=127.0.0.1", f"MASTER_PORT={port}"],
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    out = []
+    for p in ps:
+        o, e = p.communicate(timeout=300)
+        out.append((p.returncode, o, e))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_cli_sharded_matches_single_process(tmp_path, world):
+    """RunAllPathsLG-style modules one process per rank (WORLD=N RANK=r): the
+    files they write are byte-identical to the single-process modules'."""
+    import shutil
+
+    one, many = tmp_path / "one", tmp_path / "many"
+    for d in (one, many):
+        d.mkdir()
+        _stage(d, "frag_reads_filt")
+    steps = [("KmerSpectrum", ["K=25"]), ("PreCorrect", ["K=24"]), ("FindErrors", ["K=24"])]
+    for mod, args in steps:
+        p = run(mod, f"RUN={one}", *args)
+        assert p.returncode == 0, p.stderr
+        for rc, o, e in _run_ranks(mod, world, f"RUN={many}", *args):
+            assert rc == 0, (mod, e)
+    for d in (one, many):
+        shutil.copy(d / "frag_reads_corr.fastb", d / "all_reads.fastb")
+    for mod in ("CommonPather", "Unipather"):
+        p = run(mod, f"RUN={one}", "READS=all_reads", "K=96")
+        assert p.returncode == 0, p.stderr
+        for rc, o, e in _run_ranks(mod, world, f"RUN={many}", "READS=all_reads", "K=96"):
+            assert rc == 0, (mod, e)
+        names = sorted(f for f in os.listdir(one) if not f.startswith("all_reads.fastb"))
+        assert names == sorted(f for f in os.listdir(many) if not f.startswith("all_reads.fastb"))
+        for f in names:
+            assert (one / f).read_bytes() == (many / f).read_bytes(), (mod, f)

@@ -79,6 +79,88 @@ struct Reads {
   ~Reads() { apg_reads_release(&r); }
 };
 
+std::string env_or(const char* k, const std::string& def) {
+  const char* v = std::getenv(k);
+  return v && *v ? std::string(v) : def;
+}
+
+// One rank of a sharded run: WORLD=N RANK=r COMM=rccl|tcp
+// MASTER_ADDR MASTER_PORT (defaults from the torchrun-style environment).
+// Rank r takes read pairs [np*r/N, np*(r+1)/N) of the input; every exchange
+// runs inside libapg (apg_sharded_*); rank 0 writes the module's outputs.
+// COMM=rccl: rank 0's RCCL id reaches the others over a short-lived TCP
+// communicator; COMM=tcp: the TCP communicator carries the whole exchange
+// (ranks may then share one GPU).
+struct Shard {
+  int rank = 0, world = 1;
+  std::string mode, addr;
+  int port = 29600;
+  apg_comm* comm = nullptr;
+  explicit Shard(Args& a) {
+    world = (int)a.num("WORLD", std::atol(env_or("WORLD_SIZE", "1").c_str()));
+    rank = (int)a.num("RANK", std::atol(env_or("RANK", "0").c_str()));
+    mode = a.get("COMM", "rccl");
+    addr = a.get("MASTER_ADDR", env_or("MASTER_ADDR", "127.0.0.1"));
+    port = (int)a.num("MASTER_PORT", std::atol(env_or("MASTER_PORT", "29600").c_str()));
+    if (world < 1 || rank < 0 || rank >= world) a.fail("bad RANK / WORLD");
+    if (mode != "rccl" && mode != "tcp") a.fail("COMM must be rccl or tcp");
+  }
+  ~Shard() { apg_comm_destroy(comm); }
+  bool sharded() const { return world > 1; }
+  void connect(Args& a, apg_ctx* ctx) {
+    if (world == 1) return;
+    if (mode == "tcp") {
+      a.check(apg_comm_init_tcp(ctx, addr.c_str(), port, rank, world, 0, &comm), "apg_comm_init_tcp");
+      return;
+    }
+    apg_comm* boot = nullptr;
+    a.check(apg_comm_init_tcp(nullptr, addr.c_str(), port, rank, world, 0, &boot), "apg_comm_init_tcp (bootstrap)");
+    std::vector<uint8_t> id(128, 0), all(128 * (size_t)world);
+    if (rank == 0) a.check(apg_comm_unique_id(id.data()), "apg_comm_unique_id");
+    std::vector<uint64_t> rb(world, 128);
+    const int rc = apg_comm_allgatherv(boot, id.data(), 128, all.data(), rb.data());
+    apg_comm_destroy(boot);
+    a.check(rc, "bootstrap exchange");
+    a.check(apg_comm_init_rccl(ctx, all.data(), rank, world, 0, &comm), "apg_comm_init_rccl");
+  }
+  void barrier(Args& a) {
+    if (comm) a.check(apg_comm_barrier(comm), "apg_comm_barrier");
+  }
+  // this rank's whole pairs of n reads
+  void range(uint64_t n, uint64_t* r0, uint64_t* r1) const {
+    const uint64_t np = n / 2;
+    *r0 = 2 * (np * (uint64_t)rank / (uint64_t)world);
+    *r1 = rank + 1 == world ? n : 2 * (np * (uint64_t)(rank + 1) / (uint64_t)world);
+  }
+};
+
+// Reads [r0, r1) of a loaded set as a standalone apg_reads view (offsets
+// rebased, bases and qualities pointing into the loaded buffers).
+struct Slice {
+  std::vector<uint64_t> bo, yo;
+  apg_reads r{};
+  Slice(const apg_reads& all, uint64_t r0, uint64_t r1) : bo(r1 - r0 + 1), yo(r1 - r0 + 1) {
+    for (uint64_t i = 0; i <= r1 - r0; ++i) {
+      bo[i] = all.base_off[r0 + i] - all.base_off[r0];
+      yo[i] = all.byte_off[r0 + i] - all.byte_off[r0];
+    }
+    r.n_reads = r1 - r0;
+    r.base_off = bo.data();
+    r.byte_off = yo.data();
+    r.packed = all.packed + all.byte_off[r0];
+    r.quals = all.quals ? all.quals + all.base_off[r0] : nullptr;
+  }
+};
+
+struct DReads {
+  apg_dreads* d = nullptr;
+  ~DReads() { apg_reads_free(d); }
+};
+
+std::string part_name(const std::string& head, int rank, int world) {
+  return head + ".part" + std::to_string(rank) + "of" + std::to_string(world);
+}
+
 void load_reads(Args& a, const std::string& head, bool need_quals, Reads* out) {
   const std::string fb = head + ".fastb", qb = head + ".qualb";
   if (!exists(fb)) a.fail("missing input " + fb);
@@ -103,13 +185,25 @@ int kmer_spectrum(Args& a) {
   const std::string head = dir + "/" + a.get("READS", "frag_reads_filt");
   const int K = (int)a.num("K", 25);
   const long hist_len = a.num("HIST_LEN", 1 << 16);
+  Shard sh(a);
   a.finish();
   Reads rd;
   load_reads(a, head, false, &rd);
   Ctx ctx(a);
   std::vector<uint64_t> hist((size_t)hist_len);
   apg_kstats st;
-  a.check(apg_kmer_spectrum(ctx.c, &rd.r, K, hist.data(), hist.size(), &st), "apg_kmer_spectrum");
+  if (sh.sharded()) {
+    sh.connect(a, ctx.c);
+    uint64_t r0, r1;
+    sh.range(rd.r.n_reads, &r0, &r1);
+    Slice sl(rd.r, r0, r1);
+    DReads d;
+    a.check(apg_reads_upload(ctx.c, &sl.r, &d.d), "apg_reads_upload");
+    a.check(apg_sharded_spectrum(ctx.c, sh.comm, d.d, K, hist.data(), hist.size(), &st), "apg_sharded_spectrum");
+    if (sh.rank != 0) return 0;  // every rank holds the global spectrum; rank 0 writes it
+  } else {
+    a.check(apg_kmer_spectrum(ctx.c, &rd.r, K, hist.data(), hist.size(), &st), "apg_kmer_spectrum");
+  }
   const std::string out = head + ".kspec.k" + std::to_string(K);
   a.check(apg_kspec_write(out.c_str(), K, hist.data(), hist.size()), "writing .kspec");
   std::printf("%s: %llu reads, %llu %d-mers, %llu distinct -> %s\n", a.module.c_str(),
@@ -128,6 +222,7 @@ int precorrect(Args& a, uint32_t default_cycles, const char* default_out) {
   p.min_solid = (uint32_t)a.num("MIN_SOLID", p.min_solid);
   p.max_q_suspect = (uint32_t)a.num("MAX_Q_SUSPECT", p.max_q_suspect);
   p.n_cycles = (uint32_t)a.num("NUM_CYCLES", default_cycles);
+  Shard sh(a);
   a.finish();
   Reads rd;
   load_reads(a, in, true, &rd);
@@ -136,7 +231,51 @@ int precorrect(Args& a, uint32_t default_cycles, const char* default_out) {
   const uint64_t nbytes = n ? rd.r.byte_off[n] : 0, nbases = n ? rd.r.base_off[n] : 0;
   std::vector<uint8_t> pk(nbytes + 64), q(nbases + 1);
   apg_pc_stats st;
-  a.check(apg_precorrect(ctx.c, &rd.r, &p, pk.data(), q.data(), &st), "apg_precorrect");
+  if (sh.sharded()) {
+    // this rank's pairs corrected against the global solid set; each rank
+    // writes its corrected slice as a part file, rank 0 assembles the output
+    sh.connect(a, ctx.c);
+    uint64_t r0, r1;
+    sh.range(n, &r0, &r1);
+    Slice sl(rd.r, r0, r1);
+    DReads d;
+    a.check(apg_reads_upload(ctx.c, &sl.r, &d.d), "apg_reads_upload");
+    a.check(apg_sharded_precorrect(ctx.c, sh.comm, d.d, &p, &st), "apg_sharded_precorrect");
+    const uint64_t y0 = rd.r.byte_off[r0], b0 = rd.r.base_off[r0];
+    a.check(apg_reads_download(ctx.c, d.d, pk.data() + y0, q.data() + b0), "apg_reads_download");
+    apg_reads part = sl.r;
+    part.packed = pk.data() + y0;
+    part.quals = q.data() + b0;
+    const std::string ph = part_name(out, sh.rank, sh.world);
+    if (sh.rank != 0) {
+      a.check(apg_fastb_write((ph + ".fastb").c_str(), &part), "writing part .fastb");
+      a.check(apg_qualb_write((ph + ".qualb").c_str(), &part), "writing part .qualb");
+    }
+    sh.barrier(a);
+    if (sh.rank != 0) {
+      sh.barrier(a);  // rank 0 has read every part
+      return 0;
+    }
+    for (int r = 1; r < sh.world; ++r) {  // place every other rank's slice
+      Shard other = sh;
+      other.comm = nullptr;
+      other.rank = r;
+      uint64_t s0, s1;
+      other.range(n, &s0, &s1);
+      const std::string h = part_name(out, r, sh.world);
+      Reads pr;
+      load_reads(a, h, true, &pr);
+      if (pr.r.n_reads != s1 - s0) a.fail("part " + h + " has the wrong read count");
+      const uint64_t py = s1 > s0 ? pr.r.byte_off[s1 - s0] : 0, pb = s1 > s0 ? pr.r.base_off[s1 - s0] : 0;
+      std::memcpy(pk.data() + rd.r.byte_off[s0], pr.r.packed, py);
+      std::memcpy(q.data() + rd.r.base_off[s0], pr.r.quals, pb);
+      std::remove((h + ".fastb").c_str());
+      std::remove((h + ".qualb").c_str());
+    }
+    sh.barrier(a);
+  } else {
+    a.check(apg_precorrect(ctx.c, &rd.r, &p, pk.data(), q.data(), &st), "apg_precorrect");
+  }
   apg_reads o = rd.r;
   o.packed = pk.data();
   o.quals = q.data();
@@ -208,13 +347,69 @@ int unipaths(Args& a, bool read_paths) {
   apg_unipath_defaults(&p);
   p.K = (int)a.num("K", p.K);
   p.flags = read_paths ? APG_UNIPATH_READ_PATHS : 0;
+  Shard sh(a);
   a.finish();
   Reads rd;
   load_reads(a, head, false, &rd);
   Ctx ctx(a);
   apg_unipath_graph g;
   apg_unipath_stats st;
-  a.check(apg_unipaths(ctx.c, &rd.r, &p, &g, &st), "apg_unipaths");
+  if (sh.sharded()) {
+    // the global graph on every rank + KmerPaths of each rank's reads: ranks
+    // > 0 write their KmerPaths as parts, rank 0 joins them in read order
+    sh.connect(a, ctx.c);
+    uint64_t r0, r1;
+    sh.range(rd.r.n_reads, &r0, &r1);
+    Slice sl(rd.r, r0, r1);
+    DReads d;
+    a.check(apg_reads_upload(ctx.c, &sl.r, &d.d), "apg_reads_upload");
+    a.check(apg_sharded_unipaths(ctx.c, sh.comm, d.d, &p, &g, &st), "apg_sharded_unipaths");
+    const std::string pp = part_name(head, sh.rank, sh.world) + ".paths.k" + std::to_string(p.K);
+    if (sh.rank != 0 && read_paths)
+      a.check(apg_kmerpaths_write(pp.c_str(), p.K, g.n_reads, g.path_off, g.path_start, g.path_len),
+              "writing KmerPath part");
+    sh.barrier(a);
+    if (sh.rank != 0) {
+      apg_unipath_graph_free(&g);
+      sh.barrier(a);
+      return 0;
+    }
+    if (read_paths) {
+      std::vector<uint64_t> off(g.path_off, g.path_off + g.n_reads + 1), start(g.path_start, g.path_start + g.n_intervals),
+          len(g.path_len, g.path_len + g.n_intervals);
+      for (int r = 1; r < sh.world; ++r) {
+        const std::string h = part_name(head, r, sh.world) + ".paths.k" + std::to_string(p.K);
+        int pk = 0;
+        uint64_t pn = 0, ni = 0, *po = nullptr, *ps = nullptr, *pl = nullptr;
+        a.check(apg_kmerpaths_read(h.c_str(), &pk, &pn, &po, &ni, &ps, &pl), "reading KmerPath part");
+        const uint64_t base = off.back();
+        for (uint64_t i = 1; i <= pn; ++i) off.push_back(base + po[i] - po[0]);
+        start.insert(start.end(), ps + po[0], ps + po[pn]);
+        len.insert(len.end(), pl + po[0], pl + po[pn]);
+        apg_free(po);
+        apg_free(ps);
+        apg_free(pl);
+        std::remove(h.c_str());
+      }
+      // hand the joined arrays to the graph (malloc'd, freed with it)
+      auto dup = [](const std::vector<uint64_t>& v) {
+        auto* x = static_cast<uint64_t*>(std::malloc(std::max<size_t>(1, v.size()) * 8));
+        if (!v.empty()) std::memcpy(x, v.data(), v.size() * 8);
+        return x;
+      };
+      std::free(g.path_off);
+      std::free(g.path_start);
+      std::free(g.path_len);
+      g.n_reads = off.size() - 1;
+      g.n_intervals = start.size();
+      g.path_off = dup(off);
+      g.path_start = dup(start);
+      g.path_len = dup(len);
+    }
+    sh.barrier(a);
+  } else {
+    a.check(apg_unipaths(ctx.c, &rd.r, &p, &g, &st), "apg_unipaths");
+  }
   const int rc = apg_graph_write(head.c_str(), &g);
   apg_unipath_graph_free(&g);
   a.check(rc, "writing unipath files");
