@@ -51,9 +51,12 @@ def main(d):
     f = load(os.path.join(d, "fetch.csv"))
     w = load(os.path.join(d, "write.csv"))
     out = {}
-    for sym, (label, pattern) in KERNELS.items():
-        if sym not in f:
+    for base, (label, pattern) in KERNELS.items():
+        # template kernels may carry extra arguments (k_sk_bucket<true, SK24, 512>)
+        hits = [k for k in f if k == base or (base.endswith(">") and k.startswith(base[:-1] + ","))]
+        if not hits:
             continue
+        sym = hits[0]
         fetch = sum(f[sym]) / len(f[sym])
         write = sum(w.get(sym, [0.0])) / max(len(w.get(sym, [])), 1)
         corr = 2.0 if pattern == "stream" else 1.0
