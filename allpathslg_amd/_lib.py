@@ -35,7 +35,7 @@ class apg_config(C.Structure):
         ("device", C.c_int32),
         ("timing", C.c_int32),
         ("verbose", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("kmer_dedup", C.c_int32),
         ("reserved", C.c_uint64 * 6),
     ]
 
@@ -57,7 +57,8 @@ class apg_kstats(C.Structure):
         ("n_buckets", C.c_uint64),
         ("n_overflow", C.c_uint64),
         ("max_bucket", C.c_uint64),
-        ("reserved", C.c_uint64 * 3),
+        ("n_redo", C.c_uint64),
+        ("reserved", C.c_uint64 * 2),
     ]
 
     def as_dict(self) -> dict:

@@ -140,6 +140,12 @@ int apg_create(const apg_config* cfg, apg_ctx** out) {
   ctx->device = dev;
   ctx->timing = cfg && cfg->timing;
   ctx->verbose = cfg && cfg->verbose;
+  ctx->kmer_dedup = cfg ? cfg->kmer_dedup : 0;
+  if (ctx->kmer_dedup < 0 || ctx->kmer_dedup > 2) {
+    delete ctx;
+    set_error("apg_create: kmer_dedup must be 0, 1 or 2");
+    return APG_E_ARG;
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
   if (ctx->n_cu <= 0) ctx->n_cu = 256;

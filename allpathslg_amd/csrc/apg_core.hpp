@@ -80,6 +80,7 @@ struct apg_ctx {
   int device = 0;
   bool timing = false;
   bool verbose = false;
+  int kmer_dedup = 0;  // apg_config.kmer_dedup
   hipStream_t stream = nullptr;
   int n_cu = 0;
 

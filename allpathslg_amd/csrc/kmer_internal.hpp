@@ -37,6 +37,7 @@ struct SkResult {
   uint64_t n_solid = 0;
   uint64_t n_distinct = 0;
   uint64_t n_overflow_buckets = 0;  // buckets counted by the global-table fallback
+  uint64_t n_redo_buckets = 0;      // buckets the record-dedup kernel handed back to k_sk_bucket
   uint64_t nbuckets = 0;
   uint64_t n_kmers = 0;
   uint64_t n_records = 0;

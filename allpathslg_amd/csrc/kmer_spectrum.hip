@@ -770,6 +770,7 @@ static void sk_stats(const SkResult& r, apg_kstats* st) {
   st->n_distinct = r.n_distinct;
   st->n_buckets = r.nbuckets;
   st->n_overflow = r.n_overflow_buckets;
+  st->n_redo = r.n_redo_buckets;
 }
 
 // Spectrum: the minimizer-partitioned super-k-mer pipeline (superkmer.hip).

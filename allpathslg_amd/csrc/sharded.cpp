@@ -112,13 +112,14 @@ int apg_sharded_spectrum(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
   apg_kstats st;
   APG_TRY(apg_shard_spectrum(ctx, x.recv, x.recv_counts.data(), K, P, hist, hist_len, &st));
   APG_TRY(c->allreduce_u64(hist, hist_len, APG_COMM_SUM));
-  uint64_t v[3] = {st.n_kmers, st.n_distinct, st.n_overflow};
-  APG_TRY(c->allreduce_u64(v, 3, APG_COMM_SUM));
+  uint64_t v[4] = {st.n_kmers, st.n_distinct, st.n_overflow, st.n_redo};
+  APG_TRY(c->allreduce_u64(v, 4, APG_COMM_SUM));
   uint64_t mb = st.max_bucket;
   APG_TRY(c->allreduce_u64(&mb, 1, APG_COMM_MAX));
   st.n_kmers = v[0];
   st.n_distinct = v[1];
   st.n_overflow = v[2];
+  st.n_redo = v[3];
   st.max_bucket = mb;
   if (stats) *stats = st;
   return APG_OK;

@@ -33,6 +33,7 @@
 // 16 B (vs 76 x 8 B hash records).
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -253,6 +254,8 @@ struct SkOut {
   unsigned long long* weak;    // SK24 solid mode: per-base bitmap of weak K-mer instances (or null)
   uint32_t* wrec;              // SK24 solid mode, instead of `weak`: mask of weak K-mers per record, at
                                // index record.pos (the multi-GPU owner side: pos = receive index)
+  unsigned long long* prof;    // diagnostics (APG_SK_PROF): k_sk_bucket_dd's per-phase clock64 sums, or null
+  uint32_t want_hist;          // k_sk_bucket_dd: bin the spectrum (a solid-set count may not need it)
 };
 
 __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, const SkOut& o) {
@@ -269,10 +272,13 @@ __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, con
 // flatten the chunk to one K-mer per thread, inserted into the LDS table
 // keyed by the canonical K-mer (CAS, then count).  The occupied slots feed
 // the spectrum; solid mode appends khash of those with count >= min_solid.
+// blist (may be null): count only the buckets blist[0 .. *bcount) — the
+// buckets k_sk_bucket_dd handed back.
 template <bool SOLID, typename R, int NT>
 __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
                                                           const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
-                                                          SkOut o) {
+                                                          SkOut o, const uint32_t* __restrict__ blist = nullptr,
+                                                          const unsigned long long* __restrict__ bcount = nullptr) {
   constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
   // recorded slots: kSkWaveSlots per wave (NT = 512: each wave sees ~1/8 of a bucket)
   constexpr uint32_t kWaveSlots = NT >= 512 ? 1024 : kSkWaveSlots;
@@ -306,11 +312,13 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   // The block's buckets bkt, bkt + grid, ... are one record stream: the next
   // chunk's record (this bucket's or the next bucket's first) and the next
   // bucket's bounds are loaded while the current chunk is counted.
+  if (blist) nbuckets = *bcount;
+  auto bid = [&](uint64_t q) -> uint64_t { return blist ? blist[q] : q; };
   uint64_t bkt = blockIdx.x, off = 0;
   uint32_t nr = 0;
   if (bkt < nbuckets) {
-    off = boff[bkt];
-    nr = (uint32_t)(boff[bkt + 1] - off);
+    off = boff[bid(bkt)];
+    nr = (uint32_t)(boff[bid(bkt) + 1] - off);
   }
   R pre{};
   if (tid < nr) pre = rec[off + tid];
@@ -319,8 +327,8 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     uint64_t noff = 0;
     uint32_t nnr = 0;
     if (nbk < nbuckets) {
-      noff = boff[nbk];
-      nnr = (uint32_t)(boff[nbk + 1] - noff);
+      noff = boff[bid(nbk)];
+      nnr = (uint32_t)(boff[bid(nbk) + 1] - noff);
     }
     if (nr == 0) {  // block-uniform
       if (tid < nnr) pre = rec[noff + tid];
@@ -376,7 +384,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     // bucket's weak pass to the probing fallback
     const bool unrecorded = __syncthreads_or(WEAK && ibw > kWaveSlots);
     if (ovf) {
-      if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+      if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bid(bkt);
       __syncthreads();
       bkt = nbk;
       off = noff;
@@ -500,6 +508,343 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     off = noff;
     nr = nnr;
   }
+  __syncthreads();
+  const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
+  for (uint32_t i = tid; i < lim; i += NT)
+    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
+  wave_add(&o.gstats[0], nd);
+}
+
+// ---------------------------------------------------------------------------
+// Record-deduplicating bucket count (K >= 21)
+// ---------------------------------------------------------------------------
+// At genome coverage c most super-k-mer records of a bucket are exact copies:
+// interior super-k-mers are fixed by the genome (their ends are minimizer
+// changes), so every read covering one error-free emits the same record.  On
+// the bench's reads (62x) 36 % of the records are distinct and they carry
+// 36.5 % of the K-mer instances.  A bucket (~kDdBucketKmers instances) is
+// counted by one 256-thread block in two levels:
+//   1. records -> LDS record table keyed by a 64-bit fingerprint of the
+//      record's 96 significant bits (n, 40 bases), counting multiplicity; the
+//      claiming lane stores the record, and after the chunk's barrier every
+//      lane compares its record with the stored one (exact: a fingerprint
+//      collision hands the bucket back);
+//   2. one block scan over the record-table slots gives each distinct record
+//      its first instance index; an LDS owner map (instance -> record slot)
+//      spreads the distinct records' K-mer instances over all lanes, two per
+//      lane per step, into the LDS K-mer table with count += multiplicity.
+// Weak pass (solid mode, SK24): each distinct record's weak mask from the
+// K-mer slots its instances recorded (in place of the owner map), then every
+// record — its position and record slot kept in registers since phase 1 —
+// ORs its mask into the bitmap (or stores it, multi-GPU): no record re-read.
+// A bucket this kernel cannot finish in LDS — record table full, fingerprint
+// collision, more than kDdRecCap records (weak mode), more than kDdInstCap
+// distinct-record instances — is appended to `redo` for k_sk_bucket; a full
+// K-mer table sends it to the global-table path as there.
+constexpr int kDdThreads = 512;
+constexpr uint64_t kDdBucketKmers = 4096;  // instances per bucket the planner aims for with this kernel
+constexpr uint32_t kDdKTab = 2048;         // K-mer table slots
+constexpr uint32_t kDdTab = 1024;          // record table slots
+constexpr uint32_t kDdChunks = 4;          // weak mode: records per bucket <= kDdChunks * kDdThreads
+constexpr uint32_t kDdRecCap = kDdChunks * kDdThreads;
+constexpr uint32_t kDdInstCap = 4096;      // distinct-record K-mer instances per bucket
+constexpr int kDdMinK = kSkBases + 1 - 20;  // records hold <= 20 K-mers (owner-map loop bound)
+
+__device__ __forceinline__ uint64_t rec_fp(const SK16& h) {
+  const uint64_t x = sk_fmix(h.w1 ^ ((h.w0 >> 32) * 0x9e3779b97f4a7c15ull));
+  return x == ~0ull ? 0ull : x;  // ~0 marks an empty slot
+}
+
+// Find-or-claim in a TS-slot LDS table (as sk_tab_claim); *fresh = this
+// lane's CAS created the entry.  Returns TS when the table is full.
+template <uint32_t TS>
+__device__ __forceinline__ uint32_t lds_claim(unsigned long long* tk, uint64_t c, uint32_t g, bool* fresh) {
+  constexpr unsigned long long EMPTY = ~0ull;
+  *fresh = false;
+  for (uint32_t n = 0; n < TS + kSkGrp;) {
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(&tk[g]);
+    const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(&tk[g + 2]);
+    const unsigned long long k[kSkGrp] = {a.x, a.y, b.x, b.y};
+    uint32_t j = kSkGrp;
+#pragma unroll
+    for (uint32_t q = kSkGrp; q-- > 0;)
+      if (k[q] == c || k[q] == EMPTY) j = q;
+    if (j == kSkGrp) {
+      g = (g + kSkGrp) & (TS - 1);
+      n += kSkGrp;
+      continue;
+    }
+    if (k[j] == c) return g + j;
+    const unsigned long long old = atomicCAS(&tk[g + j], EMPTY, (unsigned long long)c);
+    if (old == EMPTY) {
+      *fresh = true;
+      return g + j;
+    }
+    if (old == c) return g + j;
+    ++n;
+  }
+  return TS;
+}
+
+template <bool SOLID, typename R>
+__global__ void __launch_bounds__(kDdThreads) k_sk_bucket_dd(const R* __restrict__ rec,
+                                                             const uint64_t* __restrict__ boff, uint64_t nbuckets,
+                                                             SkP p, SkOut o, uint32_t* __restrict__ redo) {
+  constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
+  constexpr int NT = kDdThreads;
+  constexpr unsigned long long EMPTY = ~0ull;
+  constexpr int KB = __builtin_ctz(kDdKTab), RB = __builtin_ctz(kDdTab);
+  __shared__ __attribute__((aligned(16))) unsigned long long tkey[kDdKTab];
+  __shared__ uint32_t tcnt[kDdKTab];
+  __shared__ uint16_t klist[kDdKTab];  // claimed K-mer slots (claim order)
+  __shared__ __attribute__((aligned(16))) unsigned long long rkey[kDdTab];
+  __shared__ uint32_t rcnt[kDdTab];  // multiplicity; weak mode: then the record's weak mask
+  __shared__ __attribute__((aligned(16))) SK16 rrec[kDdTab];
+  __shared__ uint16_t rlist[kDdTab];  // claimed record slots (claim order)
+  __shared__ uint16_t doff[kDdTab];   // first instance of distinct record rlist[j], at j
+  __shared__ uint16_t own[kDdInstCap];  // instance -> j; weak mode: then -> its K-mer slot; emit: solid slots
+  __shared__ uint32_t lhist[kSkHistBins];
+  __shared__ uint32_t scan_sm[32];
+  __shared__ uint32_t nk_sh, nr_sh, ns_sh;  // claimed K-mer slots, claimed record slots, solid K-mers
+  __shared__ int flag;  // 1: K-mer table full (global path); 2: hand the bucket back (redo)
+  __shared__ unsigned long long sbase;
+  const uint32_t tid = threadIdx.x;
+  const bool want_hist = o.want_hist != 0;
+  for (uint32_t i = tid; i < kSkHistBins; i += NT) lhist[i] = 0;
+  for (uint32_t s = tid; s < kDdKTab; s += NT) {  // afterwards each bucket clears the slots it claimed
+    tkey[s] = EMPTY;
+    tcnt[s] = 0;
+  }
+  for (uint32_t s = tid; s < kDdTab; s += NT) {
+    rkey[s] = EMPTY;
+    rcnt[s] = 0;
+  }
+  if (tid == 0) {
+    nk_sh = nr_sh = ns_sh = 0;
+    flag = 0;
+  }
+  __syncthreads();
+  unsigned long long nd = 0;
+  // diagnostics: thread 0's clock64 between the phase barriers
+  unsigned long long pt[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;
+  const bool prof = o.prof != nullptr && tid == 0;
+  auto mark = [&](int ph) {
+    if (prof) {
+      const unsigned long long t1 = clock64();
+      if (ph > 0) pt[ph - 1] += t1 - t0;
+      t0 = t1;
+    }
+  };
+  uint64_t bkt = blockIdx.x, off = 0;
+  uint32_t nr = 0;
+  if (bkt < nbuckets) {
+    off = boff[bkt];
+    nr = (uint32_t)(boff[bkt + 1] - off);
+  }
+  R pre{};
+  if (tid < nr) pre = rec[off + tid];
+  while (bkt < nbuckets) {
+    mark(0);
+    const uint64_t nbk = bkt + gridDim.x;
+    uint64_t noff = 0;
+    uint32_t nnr = 0;
+    if (nbk < nbuckets) {
+      noff = boff[nbk];
+      nnr = (uint32_t)(boff[nbk + 1] - noff);
+    }
+    // ends a bucket: the claimed slots back to empty, counters reset
+    auto finish = [&]() {
+      const uint32_t nks = nk_sh, nrs = nr_sh;
+      __syncthreads();  // every thread has read the counters (and flag)
+      if (tid == 0) {
+        nk_sh = nr_sh = ns_sh = 0;
+        flag = 0;
+      }
+      for (uint32_t j = tid; j < nks; j += NT) {
+        tkey[klist[j]] = EMPTY;
+        tcnt[klist[j]] = 0;
+      }
+      for (uint32_t j = tid; j < nrs; j += NT) {
+        rkey[rlist[j]] = EMPTY;
+        rcnt[rlist[j]] = 0;
+      }
+      __syncthreads();
+      bkt = nbk;
+      off = noff;
+      nr = nnr;
+    };
+    auto hand_back = [&](bool global_table) {
+      if (tid == 0) {
+        if (global_table)
+          o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+        else
+          redo[atomicAdd(&o.gstats[4], 1ull)] = (uint32_t)bkt;
+      }
+      finish();
+    };
+    if (nr == 0 || (WEAK && nr > kDdRecCap)) {  // block-uniform
+      if (nr && tid == 0) redo[atomicAdd(&o.gstats[4], 1ull)] = (uint32_t)bkt;
+      if (tid < nnr) pre = rec[noff + tid];
+      bkt = nbk;
+      off = noff;
+      nr = nnr;
+      continue;
+    }
+    // 1. records -> record table (multiplicity), verified against the
+    // claimer's copy after each chunk's barrier.  Weak mode keeps each
+    // record's slot and position in registers for the weak pass.
+    uint64_t rp_[kDdChunks];  // record slot << 52 | position; slot kDdTab = no record
+#pragma unroll
+    for (uint32_t c = 0; c < kDdChunks; ++c) rp_[c] = (uint64_t)kDdTab << 52;
+    for (uint32_t c = 0, c0 = 0; c0 < nr; ++c, c0 += NT) {
+      const bool valid = c0 + tid < nr;
+      SK16 hd{0, 0};
+      uint64_t ps = 0;
+      if (valid) {
+        hd = rec_head(pre);
+        if constexpr (WEAK) ps = pre.pos;
+      }
+      if (c0 + NT < nr) {
+        if (c0 + NT + tid < nr) pre = rec[off + c0 + NT + tid];
+      } else if (tid < nnr) {
+        pre = rec[noff + tid];
+      }
+      uint32_t s = kDdTab;
+      bool fresh = false;
+      if (valid) {
+        const uint64_t fp = rec_fp(hd);
+        s = lds_claim<kDdTab>(rkey, fp, (uint32_t)(fp >> (64 - RB)) & ~(kSkGrp - 1), &fresh);
+        if (s < kDdTab) {
+          if (fresh) rrec[s] = hd;
+          atomicAdd(&rcnt[s], 1u);
+        } else {
+          atomicOr(&flag, 2);
+        }
+      }
+      if (fresh) rlist[atomicAdd(&nr_sh, 1u)] = (uint16_t)s;
+      if constexpr (WEAK) {
+#pragma unroll
+        for (uint32_t q = 0; q < kDdChunks; ++q)
+          if (q == c) rp_[q] = ((uint64_t)(valid ? s : kDdTab) << 52) | ps;
+      }
+      __syncthreads();
+      if (s < kDdTab) {
+        const SK16 q = rrec[s];
+        if (q.w0 != hd.w0 || q.w1 != hd.w1) atomicOr(&flag, 2);  // fingerprint collision
+      }
+    }
+    __syncthreads();
+    mark(1);
+    if (flag) {  // block-uniform
+      hand_back(false);
+      continue;
+    }
+    // 2. distinct records' first instance indices (one block scan; <= NT
+    // distinct records per thread round), owner map
+    const uint32_t nD = nr_sh;
+    uint32_t ni = 0;
+    for (uint32_t j0 = 0; j0 < nD; j0 += NT) {  // block-uniform
+      const uint32_t j = j0 + tid;
+      const uint32_t nk = j < nD ? (uint32_t)(rrec[rlist[j]].w0 >> 32) & 0xff : 0;
+      uint32_t tot;
+      const uint32_t at = ni + block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);
+      if (j < nD) {
+        doff[j] = (uint16_t)min(at, 0xffffu);
+        if (at + nk <= kDdInstCap)
+          for (uint32_t u = 0; u < nk; ++u) own[at + u] = (uint16_t)j;
+      }
+      ni += tot;
+    }
+    __syncthreads();
+    mark(2);
+    if (ni > kDdInstCap) {  // block-uniform
+      hand_back(false);
+      continue;
+    }
+    // 3. instances -> K-mer table (count += multiplicity), two per lane per step
+    auto insert = [&](uint32_t f, bool ok) {
+      bool fresh = false;
+      uint32_t ts = kDdKTab;
+      if (ok) {
+        const uint32_t j = own[f];
+        const uint32_t s = rlist[j];
+        const uint64_t c = rec_kmer(rrec[s], f - doff[j], p);
+        ts = lds_claim<kDdKTab>(tkey, c, sk_slot(c, KB), &fresh);
+        if (ts < kDdKTab) {
+          atomicAdd(&tcnt[ts], rcnt[s]);
+          if constexpr (WEAK) own[f] = (uint16_t)ts;
+        } else {
+          atomicOr(&flag, 1);
+        }
+      }
+      if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)ts;
+    };
+    for (uint32_t f0 = 0; f0 < ni; f0 += 2 * NT) {  // block-uniform trip count
+      insert(f0 + tid, f0 + tid < ni);
+      if (f0 + NT < ni) insert(f0 + NT + tid, f0 + NT + tid < ni);
+    }
+    __syncthreads();
+    mark(3);
+    if (flag) {  // block-uniform: only the K-mer table can have filled here
+      hand_back(true);
+      continue;
+    }
+    if constexpr (WEAK) {
+      if (o.weak || o.wrec) {
+        // (a) distinct record -> weak mask (replaces its multiplicity)
+        for (uint32_t j = tid; j < nD; j += NT) {
+          const uint32_t s = rlist[j];
+          const uint32_t nk = (uint32_t)(rrec[s].w0 >> 32) & 0xff;
+          const uint32_t b0 = doff[j];
+          uint32_t m = 0;
+          for (uint32_t t = 0; t < nk; ++t) m |= (uint32_t)(tcnt[own[b0 + t]] < o.min_solid) << t;
+          rcnt[s] = m;
+        }
+        __syncthreads();
+        // (b) each record (registers) -> its record's mask
+#pragma unroll
+        for (uint32_t c = 0; c < kDdChunks; ++c) {
+          const uint32_t rs = (uint32_t)(rp_[c] >> 52);
+          if (rs >= kDdTab) continue;
+          const uint32_t m = rcnt[rs];
+          if (!m) continue;
+          const uint64_t b = rp_[c] & ((1ull << 52) - 1);
+          if (o.wrec) {
+            o.wrec[b] = m;
+          } else {
+            const uint32_t sh = (uint32_t)(b & 63);
+            atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
+            if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
+          }
+        }
+      }
+    }
+    mark(4);
+    // 4. the claimed K-mers: spectrum bins, solid slots (into `own`, free now)
+    const uint32_t nK = nk_sh;
+    nd += tid == 0 ? nK : 0;
+    for (uint32_t j0 = 0; j0 < nK; j0 += NT) {  // block-uniform trip count
+      const uint32_t j = j0 + tid;
+      const uint32_t cn = j < nK ? tcnt[klist[j]] : 0;
+      if (want_hist && j < nK) sk_spectrum_add(cn, lhist, o);
+      if (SOLID && j < nK && cn >= o.min_solid) own[atomicAdd(&ns_sh, 1u)] = klist[j];
+    }
+    if (SOLID) {
+      __syncthreads();
+      const uint32_t ns = ns_sh;
+      if (tid == 0) sbase = ns ? atomicAdd(&o.gstats[2], (unsigned long long)ns) : 0ull;
+      __syncthreads();
+      const unsigned long long b = sbase;
+      for (uint32_t j = tid; j < ns; j += NT)
+        if (b + j < o.solid_cap) o.solid[b + j] = khash(p.hp, tkey[own[j]]);
+    }
+    __syncthreads();
+    mark(5);
+    finish();
+    mark(6);
+  }
+  if (prof)
+    for (int i = 0; i < 6; ++i) atomicAdd(&o.prof[i], pt[i]);
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
   for (uint32_t i = tid; i < lim; i += NT)
@@ -708,8 +1053,25 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   }
   uint64_t n = 0;
   for (auto c : rec_counts) n += c;
-  const uint64_t need = std::max<uint64_t>(1, (n_kmers + kSkBucketKmers - 1) / kSkBucketKmers);
-  const int bb = std::min(32 - pbits, std::max(l1, sk_ceil_log2(need)));
+  // record dedup (k_sk_bucket_dd, K >= kDdMinK) counts smaller buckets, unless
+  // halving them would cost another partition level
+  // Measured on the C2 step (40 M reads): the solid-set count with the weak
+  // pass 33.4 -> 25.9 ms; the plain spectrum count 18.8 -> 22.9 ms, so by
+  // default (apg_config.kmer_dedup = 0) the spectrum keeps k_sk_bucket;
+  // APG_SK_DEDUP=all / none overrides the context's setting.
+  static const char* dd_env = getenv("APG_SK_DEDUP");
+  int mode = ctx->kmer_dedup;
+  if (dd_env) mode = !strcmp(dd_env, "all") ? 1 : !strcmp(dd_env, "none") ? 2 : mode;
+  const bool dd = K >= kDdMinK && mode != 2 && (solid || mode == 1);
+  auto bits_for = [&](uint64_t per) {
+    const uint64_t need = std::max<uint64_t>(1, (n_kmers + per - 1) / per);
+    return std::min(32 - pbits, std::max(l1, sk_ceil_log2(need)));
+  };
+  int bb = bits_for(kSkBucketKmers);
+  if (dd) {
+    const int bd = bits_for(kDdBucketKmers);
+    if ((bd - l1 + kMaxLevelBits - 1) / kMaxLevelBits <= (bb - l1 + kMaxLevelBits - 1) / kMaxLevelBits) bb = bd;
+  }
   const int rem = bb - l1;
   int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
   if (nlev == 0 && P > 1) nlev = 1;  // regroup the P source segments
@@ -755,10 +1117,12 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   unsigned long long *ghist = nullptr, *gstats = nullptr;
   uint32_t* ovf = nullptr;
   APG_TRY(workspace_t(ctx, "sk_hist", hl, &ghist));
-  APG_TRY(workspace_t(ctx, "sk_gstats", 4, &gstats));
+  uint32_t* redo = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_gstats", 5, &gstats));  // distinct, overflow, solid, scratch, handed back
   APG_TRY(workspace_t(ctx, "sk_ovf", std::max<uint64_t>(nb, 1), &ovf));
+  APG_TRY(workspace_t(ctx, "sk_redo", std::max<uint64_t>(nb, 1), &redo));
   APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 5 * 8, ctx->stream));
   uint64_t solid_cap = 0;
   uint64_t* sl = nullptr;
   if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
@@ -767,13 +1131,25 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
   }
-  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr};
+  static const bool prof = getenv("APG_SK_PROF") != nullptr;
+  unsigned long long* dprof = nullptr;
+  if (prof) {
+    APG_TRY(workspace_t(ctx, "sk_prof", 8, &dprof));
+    APG_CHECK_HIP(hipMemsetAsync(dprof, 0, 64, ctx->stream));
+  }
+  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr, dprof,
+           (uint32_t)(!solid || (hist && hist_len))};
   // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
   // LDS (owner map, recorded slots) and the table amortised over 8 waves give
   // 16 waves per CU, where 256-thread blocks fit only 3 per CU
   constexpr int NTB = sizeof(R) == sizeof(SK24) ? 512 : kSkThreads;
   const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R, NTB>, NTB, nb)
                               : resident_grid(ctx, k_sk_bucket<false, R, NTB>, NTB, nb);
+  // record dedup first (K >= kDdMinK), k_sk_bucket for the buckets it hands back
+  // (a launch over a device-side count: no host round trip in between)
+  const uint64_t grid_dd = !dd ? 0
+                           : solid ? resident_grid(ctx, k_sk_bucket_dd<true, R>, kDdThreads, nb)
+                                   : resident_grid(ctx, k_sk_bucket_dd<false, R>, kDdThreads, nb);
   for (int attempt = 0;; ++attempt) {
     // Algorithmic bytes (inputs read once + outputs written once): the records
     // and bucket offsets; the weak output (one bit per K-mer instance, or a
@@ -782,13 +1158,22 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     // records is not algorithmic and is not counted.
     const uint64_t weak_out = o.weak ? n_kmers / 8 : (o.wrec ? n * 4 : 0);
     kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) + (nb + 1) * 8 + weak_out);
-    if (solid)
+    if (dd) {
+      if (solid) {
+        k_sk_bucket_dd<true, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
+        k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
+      } else {
+        k_sk_bucket_dd<false, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
+        k_sk_bucket<false, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
+      }
+    } else if (solid) {
       k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
-    else
+    } else {
       k_sk_bucket<false, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+    }
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
-    unsigned long long hs[4];
+    unsigned long long hs[5];
     APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
     if (hs[1]) {  // overflowed buckets: one global table
@@ -824,6 +1209,13 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
       APG_TRY(sync(ctx));
     }
+    if (prof) {
+      unsigned long long hp[8];
+      APG_CHECK_HIP(hipMemcpyAsync(hp, dprof, sizeof hp, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      fprintf(stderr, "[sk_prof] K=%d solid=%d dedup %.3g flatten %.3g insert %.3g weak %.3g emit %.3g clear %.3g redo %llu\n", K,
+              (int)solid, (double)hp[0], (double)hp[1], (double)hp[2], (double)hp[3], (double)hp[4], (double)hp[5], hs[4]);
+    }
     if (solid) kbytes_add(ctx, "sk_bucket_solid", std::min<uint64_t>(hs[2], solid_cap) * 8);
     if (!solid || hs[2] <= solid_cap) {
       res->n_distinct = hs[0];
@@ -831,6 +1223,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       res->n_solid = solid ? hs[2] : 0;
       res->solid = sl;
       res->nbuckets = nb;
+      res->n_redo_buckets = dd ? hs[4] : 0;
       break;
     }
     if (attempt >= 2) {
@@ -843,7 +1236,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     o.solid = sl;
     o.solid_cap = solid_cap;
     APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 4 * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 5 * 8, ctx->stream));
   }
   if (hist && hist_len) {
     APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -852,9 +1245,10 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   }
   res->n_kmers = n_kmers;
   res->n_records = n;
-  vlog(ctx, "sk count: K=%d P=%d records=%llu kmers=%llu levels=%d buckets=%llu distinct=%llu", K, P,
-       (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
-       (unsigned long long)res->n_distinct);
+  vlog(ctx, "sk count: K=%d P=%d records=%llu kmers=%llu levels=%d buckets=%llu distinct=%llu redo=%llu ovf=%llu", K,
+       P, (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
+       (unsigned long long)res->n_distinct, (unsigned long long)res->n_redo_buckets,
+       (unsigned long long)res->n_overflow_buckets);
   return APG_OK;
 }
 

@@ -70,11 +70,12 @@ class DeviceReads:
 class Context:
     """One HIP device + stream (apg_ctx).  One per host thread."""
 
-    def __init__(self, device: int = 0, timing: bool = False, verbose: bool = False):
+    def __init__(self, device: int = 0, timing: bool = False, verbose: bool = False, kmer_dedup: int = 0):
         cfg = apg_config()
         cfg.device = device
         cfg.timing = int(timing)
         cfg.verbose = int(verbose)
+        cfg.kmer_dedup = int(kmer_dedup)
         self._h = C.c_void_p()
         check(lib().apg_create(C.byref(cfg), C.byref(self._h)), "apg_create")
         self.device = device

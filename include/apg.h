@@ -50,7 +50,8 @@ typedef struct apg_config {
   int32_t device;   /* HIP device ordinal */
   int32_t timing;   /* 1 = record per-kernel HIP-event durations */
   int32_t verbose;  /* 1 = stage log lines on stderr */
-  int32_t reserved0;
+  int32_t kmer_dedup; /* K >= 21 bucket counts through record dedup:
+                         0 = solid-set counts only (default), 1 = every count, 2 = never */
   uint64_t reserved[6];
 } apg_config;
 
@@ -138,7 +139,9 @@ typedef struct apg_kstats {
   uint64_t n_buckets;  /* hash buckets used */
   uint64_t n_overflow; /* buckets sorted by the out-of-LDS fallback */
   uint64_t max_bucket; /* largest bucket (records) */
-  uint64_t reserved[3];
+  uint64_t n_redo;     /* buckets the record-deduplicating counter (K >= 21) handed
+                          back to the per-instance counter */
+  uint64_t reserved[2];
 } apg_kstats;
 
 uint64_t apg_kmer_hash(int K, uint64_t canonical);

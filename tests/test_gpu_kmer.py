@@ -134,6 +134,60 @@ def test_superkmer_bucket_overflow_takes_global_table(gpu_ctx):
     assert st["n_overflow"] > 0
 
 
+@pytest.fixture(scope="module")
+def dd_ctx():
+    """A context that counts every K >= 21 bucket through the record-dedup
+    kernel (by default only the solid-set counts of PreCorrect do)."""
+    from allpathslg_amd import Context
+
+    with Context(device=0, kmer_dedup=1) as c:
+        yield c
+
+
+def test_record_dedup_active_and_exact(dd_ctx):
+    """K >= 21 counts through the record-deduplicating bucket kernel: at
+    ordinary coverage (60x) it finishes nearly every bucket itself and the
+    spectrum equals the oracle's."""
+    g = synth_genome(300_000, 41)
+    reads = synth_reads(g, 90_000, seed=42)
+    for K in (21, 24, 25, 32):
+        _, st = assert_spectrum_equal(dd_ctx, reads, K)
+        assert st["n_redo"] <= st["n_buckets"] // 100, K
+    _, st = assert_spectrum_equal(dd_ctx, reads, 20)  # below the dedup kernel's K range
+    assert st["n_redo"] == 0
+    rng = np.random.default_rng(43)  # ragged reads, lengths 0..300
+    seqs = []
+    for _ in range(20000):
+        L = int(rng.integers(0, 300))
+        s = int(rng.integers(0, len(g) - 300))
+        seqs.append(g[s : s + L])
+    for K in (21, 25, 32):
+        assert_spectrum_equal(dd_ctx, ReadSet.from_sequences(seqs), K)
+
+
+def test_record_dedup_hands_back_buckets(dd_ctx):
+    """Buckets the dedup kernel cannot finish in LDS.  (1) The globally
+    smallest 13-mer in every read (K = 21, m = 13): one bucket of ~20000
+    distinct records fills the record table -> handed back to k_sk_bucket ->
+    its K-mers overflow the LDS K-mer table -> global table.  (2) 6000 copies
+    of one read: records of multiplicity 6000, counted in LDS."""
+    K, m = 21, 13
+    mm = _min_mmer(m)
+    rng = np.random.default_rng(16)
+    seqs = []
+    for _ in range(20000):
+        r = rng.integers(0, 4, size=100).astype(np.uint8)
+        p = int(rng.integers(0, 100 - m))
+        r[p : p + m] = mm
+        seqs.append(r)
+    _, st = assert_spectrum_equal(dd_ctx, ReadSet.from_sequences(seqs), K)
+    assert st["n_redo"] > 0 and st["n_overflow"] > 0
+    one = rng.integers(0, 4, size=100).astype(np.uint8)
+    seqs = [one] * 6000 + [rng.integers(0, 4, size=100).astype(np.uint8) for _ in range(3000)]
+    hist, st = assert_spectrum_equal(dd_ctx, ReadSet.from_sequences(seqs), 25)
+    assert hist[6000] >= 70
+
+
 def test_small_hist_len_clamps(gpu_ctx):
     g = synth_genome(50_000, 8)
     reads = synth_reads(g, 20_000, seed=9)

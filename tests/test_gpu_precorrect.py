@@ -44,6 +44,26 @@ def test_precorrect_deep_coverage(gpu_ctx, glen, pairs):
     assert np.array_equal(h, oracle.kmer_spectrum(reads, 24))
 
 
+def test_precorrect_identical_copies(gpu_ctx):
+    """3000 copies of each of a few reads among ordinary ones: buckets of
+    more records than the dedup kernel records slots for in its weak pass
+    are handed back to the per-instance kernel; the rest dedup to
+    multiplicity 3000.  Both must give the oracle's corrections."""
+    rng = np.random.default_rng(12)
+    g = synth_genome(100_000, 13)
+    base = synth_reads(g, 20_000, seed=14)
+    B = np.stack([base.read(i) for i in range(base.n_reads)])
+    Q = base.quals.reshape(base.n_reads, -1)
+    rep = np.concatenate([np.arange(base.n_reads), np.repeat(np.arange(3), 3000)])
+    rep = rep[rng.permutation(len(rep))]
+    reads = ReadSet.from_matrix(B[rep], Q[rep])
+    got, st = gpu_ctx.precorrect(reads, K=24)
+    exp, est = oracle.precorrect(reads, K=24)
+    assert_same(got, exp)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+        assert st[k] == est[k], k
+
+
 def test_precorrect_ragged_and_params(gpu_ctx):
     rng = np.random.default_rng(8)
     g = synth_genome(20_000, 9)
