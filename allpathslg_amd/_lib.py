@@ -181,6 +181,7 @@ class apg_unipath_graph(C.Structure):
 
 
 APG_UNIPATH_READ_PATHS = 1
+APG_UNIPATH_GATHER_NODES = 2
 
 
 APG_RPINT_RC = 1

@@ -34,4 +34,10 @@ struct Comm {
 
 Comm* comm_of(apg_comm* c);
 
+// Sharded unipath compaction (unipath.hip / ushard_graph.inc): this rank's
+// distinct nodes (KRec[n_nodes], its minimizer shard) -> the global graph on
+// every rank + KmerPaths of this rank's reads.
+int u_sharded_graph(apg_ctx* ctx, Comm* c, const void* d_nodes, uint64_t n_nodes, const apg_dreads* reads,
+                    const apg_unipath_params& p, apg_unipath_graph* out, apg_unipath_stats* st);
+
 }  // namespace apg

@@ -16,9 +16,12 @@
 //                pass's extension table + clean flags for FillFragments
 //   Fill         pairs are local: no exchange but the counters' sum
 //   unipaths     48-byte K=96 super-k-mer records by owner shard -> alltoallv
-//                -> owner's distinct nodes (OR of extension bits) ->
-//                allgatherv of the node sets -> the graph (same on every
-//                rank) + KmerPaths of this rank's reads
+//                -> owner's distinct nodes (OR of extension bits) -> sharded
+//                compaction (ushard_graph.inc: local chain fragments, their
+//                ends gathered and stitched; no rank holds every node) ->
+//                the graph (same on every rank) + KmerPaths of this rank's
+//                reads.  APG_UNIPATH_GATHER_NODES: allgatherv of the node
+//                sets and the whole graph built on every rank instead.
 // Results equal the single-GPU entry points on the union of the ranks' reads
 // (tests/test_distributed.py).
 #include <cstring>
@@ -265,11 +268,21 @@ int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
     APG_TRY(apg_urec_export(ctx, local));
   else
     APG_TRY(apg_ushard_export(ctx, local));
-  void* nodes = nullptr;
-  uint64_t n_nodes = 0;
-  APG_TRY(gather_all(ctx, c, local, n_local, 32, "x_nodes", &nodes, &n_nodes));
   apg_unipath_stats st;
-  APG_TRY(apg_unipaths_from_nodes(ctx, nodes, n_nodes, reads, &p, out, &st));
+  std::memset(&st, 0, sizeof st);
+  if (rec && !(p.flags & APG_UNIPATH_GATHER_NODES)) {
+    // sharded compaction: local chains, fragment ends gathered and stitched
+    const int rc = u_sharded_graph(ctx, c, local, n_local, reads, p, out, &st);
+    if (rc != APG_OK) {
+      if (out) apg_unipath_graph_free(out);
+      return rc;
+    }
+  } else {
+    void* nodes = nullptr;
+    uint64_t n_nodes = 0;
+    APG_TRY(gather_all(ctx, c, local, n_local, 32, "x_nodes", &nodes, &n_nodes));
+    APG_TRY(apg_unipaths_from_nodes(ctx, nodes, n_nodes, reads, &p, out, &st));
+  }
   APG_TRY(c->allreduce_u64(&n_inst, 1, APG_COMM_SUM));
   st.n_instances = n_inst;
   if (stats) *stats = st;

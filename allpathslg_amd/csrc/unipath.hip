@@ -27,9 +27,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "apg_core.hpp"
+#include "exchange.hpp"
 #include "kmer_common.hpp"
 #include "partition.hpp"
 #include "superkmer.hpp"
@@ -1602,53 +1604,13 @@ static int u_build_nodes(apg_ctx* ctx, const apg_dreads* dr, const KRec* rec, ui
 
 // U4 index + U5..U8 on a complete node set; read KmerPaths for `dr` (may be
 // null when no read paths are requested).
-static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads* dr, const apg_unipath_params& prm,
-                   apg_unipath_graph* out, apg_unipath_stats* st) {
-  const int K = prm.K;
-  const KeyP kp = make_keyp(K);
-  st->n_nodes = N;
-  ctx->gstate.valid = false;
-  if (N >= (1ull << 31)) {
-    set_error("unipaths: more than 2^31 distinct K-mers on one device");
-    return APG_E_UNSUPPORTED;
-  }
+// U6: rank the directed nodes' unique links (rb.dn) by a sparse ruling set;
+// cycles are cut before their minimum K-mer and ranking reruns.  Outputs per
+// directed node its chain head and rank, per head its chain length and tail.
+static int u_rank_all(apg_ctx* ctx, const KRec* nodes, uint64_t N, const KeyP& kp, RankBufs& rb,
+                      unsigned long long* gs, apg_unipath_stats* st, uint32_t** head, uint32_t** rank,
+                      uint32_t** chainlen, uint32_t** tail_of) {
   const uint64_t D = 2 * N;
-  const uint64_t n = st->n_instances;
-  unsigned long long* gs = nullptr;  // general device counters
-  APG_TRY(workspace_t(ctx, "u_gs", 32, &gs));
-  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 32 * 8, ctx->stream));
-  ReadsV rv{nullptr, nullptr, nullptr, 0};
-  if (dr) rv = ReadsV{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-
-  // ---- U4 index --------------------------------------------------------------
-  uint64_t T = 1024;
-  while (T < 2 * N) T <<= 1;
-  uint32_t* idx = nullptr;
-  APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
-  APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 4, ctx->stream));
-  kbegin(ctx, "u_node_insert", N * 40);
-  k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, N, idx, T - 1);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  const NodeIdx ni{nodes, idx, T - 1};
-
-  // ---- U5 --------------------------------------------------------------------
-  RankBufs rb{};
-  APG_TRY(workspace_t(ctx, "u_dn", std::max<uint64_t>(D, 1), &rb.dn));
-  APG_CHECK_HIP(hipMemsetAsync(rb.dn, 0xff, D * sizeof(DN), ctx->stream));
-  kbegin(ctx, "u_links", N * 64);
-  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.dn, gs + 4);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  unsigned long long hl[2];
-  APG_TRY(d2h_u64(ctx, gs + 4, hl, 2));
-  st->n_links = hl[0];
-  if (hl[1]) {
-    set_error("unipaths: read-supported edge to a missing K-mer (internal error)");
-    return APG_E_STATE;
-  }
-
-  // ---- U6 --------------------------------------------------------------------
   APG_TRY(workspace_t(ctx, "u_rnext", std::max<uint64_t>(D, 1), &rb.rnext));
   APG_TRY(workspace_t(ctx, "u_seglen", std::max<uint64_t>(D, 1), &rb.seglen));
   APG_TRY(workspace_t(ctx, "u_state", std::max<uint64_t>(D, 1), &rb.state));
@@ -1711,35 +1673,24 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     st->n_cycles_cut += hcut;
     vlog(ctx, "unipaths: %llu cyclic directed nodes, %llu cuts", hc, hcut);
   }
-  uint32_t *head = nullptr, *rank = nullptr, *chainlen = nullptr, *tail_of = nullptr;
-  APG_TRY(workspace_t(ctx, "u_head", std::max<uint64_t>(D, 1), &head));
-  APG_TRY(workspace_t(ctx, "u_rank", std::max<uint64_t>(D, 1), &rank));
-  APG_TRY(workspace_t(ctx, "u_chainlen", std::max<uint64_t>(D, 1), &chainlen));
-  APG_TRY(workspace_t(ctx, "u_tailof", std::max<uint64_t>(D, 1), &tail_of));
+  APG_TRY(workspace_t(ctx, "u_head", std::max<uint64_t>(D, 1), head));
+  APG_TRY(workspace_t(ctx, "u_rank", std::max<uint64_t>(D, 1), rank));
+  APG_TRY(workspace_t(ctx, "u_chainlen", std::max<uint64_t>(D, 1), chainlen));
+  APG_TRY(workspace_t(ctx, "u_tailof", std::max<uint64_t>(D, 1), tail_of));
   kbegin(ctx, "u_rank_final", D * 24);
-  k_rank_final<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, head, rank, chainlen, tail_of);
+  k_rank_final<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, *head, *rank, *chainlen, *tail_of);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
 
-  // ---- U7 --------------------------------------------------------------------
-  // pair keys (one per (u, rc u)): at most N pairs
-  uint64_t *pk[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  uint32_t *ph = nullptr, *ph2 = nullptr;
-  const uint64_t PM = std::max<uint64_t>(N, 1);
-  const char* pkn[6] = {"u_pk0", "u_pk1", "u_pk2", "u_pk3", "u_pk4", "u_pk5"};
-  for (int i = 0; i < 6; ++i) APG_TRY(workspace_t(ctx, pkn[i], PM, &pk[i]));
-  APG_TRY(workspace_t(ctx, "u_ph", PM, &ph));
-  APG_TRY(workspace_t(ctx, "u_ph2", PM, &ph2));
-  kbegin(ctx, "u_pairs", D * 12);
-  k_pairs<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb.dn, tail_of, nodes, kp, pk[0], pk[1], pk[2], ph, gs + 14,
-                                                     gs + 15);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
-  unsigned long long hp[2];
-  APG_TRY(d2h_u64(ctx, gs + 14, hp, 2));
-  const uint64_t P = hp[0], U = hp[1];
-  st->n_unipaths = U;
-  // LSD radix sort of (k0, k1, k2) with payload h, skipping constant digits
+  return APG_OK;
+}
+
+// Stable LSD radix sort of P 192-bit keys (pk[0..2], scratch pk[3..5]) with
+// a u32 payload (ph, scratch ph2), skipping digits constant over all keys;
+// *sorted = the payload array holding the result.
+static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, uint32_t* ph2,
+                       unsigned long long* gs, uint32_t** sorted) {
+  *sorted = ph;
   {
     APG_CHECK_HIP(hipMemsetAsync(gs + 16, 0, 3 * 8, ctx->stream));
     APG_CHECK_HIP(hipMemsetAsync(gs + 20, 0xff, 3 * 8, ctx->stream));
@@ -1773,8 +1724,81 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
       }
     }
     APG_CHECK_HIP(hipGetLastError());
-    ph = ap;  // sorted heads
+    *sorted = ap;
+    }
+  return APG_OK;
+}
+
+static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads* dr, const apg_unipath_params& prm,
+                   apg_unipath_graph* out, apg_unipath_stats* st) {
+  const int K = prm.K;
+  const KeyP kp = make_keyp(K);
+  st->n_nodes = N;
+  ctx->gstate.valid = false;
+  if (N >= (1ull << 31)) {
+    set_error("unipaths: more than 2^31 distinct K-mers on one device");
+    return APG_E_UNSUPPORTED;
   }
+  const uint64_t D = 2 * N;
+  const uint64_t n = st->n_instances;
+  unsigned long long* gs = nullptr;  // general device counters
+  APG_TRY(workspace_t(ctx, "u_gs", 32, &gs));
+  APG_CHECK_HIP(hipMemsetAsync(gs, 0, 32 * 8, ctx->stream));
+  ReadsV rv{nullptr, nullptr, nullptr, 0};
+  if (dr) rv = ReadsV{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
+
+  // ---- U4 index --------------------------------------------------------------
+  uint64_t T = 1024;
+  while (T < 2 * N) T <<= 1;
+  uint32_t* idx = nullptr;
+  APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
+  APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 4, ctx->stream));
+  kbegin(ctx, "u_node_insert", N * 40);
+  k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, N, idx, T - 1);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  const NodeIdx ni{nodes, idx, T - 1};
+
+  // ---- U5 --------------------------------------------------------------------
+  RankBufs rb{};
+  APG_TRY(workspace_t(ctx, "u_dn", std::max<uint64_t>(D, 1), &rb.dn));
+  APG_CHECK_HIP(hipMemsetAsync(rb.dn, 0xff, D * sizeof(DN), ctx->stream));
+  kbegin(ctx, "u_links", N * 64);
+  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.dn, gs + 4);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hl[2];
+  APG_TRY(d2h_u64(ctx, gs + 4, hl, 2));
+  st->n_links = hl[0];
+  if (hl[1]) {
+    set_error("unipaths: read-supported edge to a missing K-mer (internal error)");
+    return APG_E_STATE;
+  }
+
+  // ---- U6 --------------------------------------------------------------------
+  uint32_t *head = nullptr, *rank = nullptr, *chainlen = nullptr, *tail_of = nullptr;
+  APG_TRY(u_rank_all(ctx, nodes, N, kp, rb, gs, st, &head, &rank, &chainlen, &tail_of));
+
+  // ---- U7 --------------------------------------------------------------------
+  // pair keys (one per (u, rc u)): at most N pairs
+  uint64_t *pk[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  uint32_t *ph = nullptr, *ph2 = nullptr;
+  const uint64_t PM = std::max<uint64_t>(N, 1);
+  const char* pkn[6] = {"u_pk0", "u_pk1", "u_pk2", "u_pk3", "u_pk4", "u_pk5"};
+  for (int i = 0; i < 6; ++i) APG_TRY(workspace_t(ctx, pkn[i], PM, &pk[i]));
+  APG_TRY(workspace_t(ctx, "u_ph", PM, &ph));
+  APG_TRY(workspace_t(ctx, "u_ph2", PM, &ph2));
+  kbegin(ctx, "u_pairs", D * 12);
+  k_pairs<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb.dn, tail_of, nodes, kp, pk[0], pk[1], pk[2], ph, gs + 14,
+                                                     gs + 15);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hp[2];
+  APG_TRY(d2h_u64(ctx, gs + 14, hp, 2));
+  const uint64_t P = hp[0], U = hp[1];
+  st->n_unipaths = U;
+  // LSD radix sort of (k0, k1, k2) with payload h, skipping constant digits
+  APG_TRY(u_sort_keys(ctx, P, pk, ph, ph2, gs, &ph));
   uint32_t *sz = nullptr, *uni_of_head = nullptr, *uhead = nullptr;
   uint64_t *ustart = nullptr, *ulen = nullptr, *urc = nullptr, *id_base = nullptr, *ub_off = nullptr;
   APG_TRY(workspace_t(ctx, "u_sz", PM, &sz));
@@ -2683,3 +2707,5 @@ int apg_urec_export(apg_ctx* ctx, void* d_out) {
 }
 
 }  // extern "C"
+
+#include "ushard_graph.inc"

@@ -140,15 +140,17 @@ def sharded_fill(ctx: Context, comm: Comm, reads: DeviceReads, K: int = 24, min_
 
 
 def sharded_unipaths(ctx: Context, comm: Comm, reads: DeviceReads, K: int = 96, read_paths: bool = True,
-                     fetch: bool = False):
+                     fetch: bool = False, gather_nodes: bool = False):
     """The global unipath graph (identical on every rank) + KmerPaths of this
-    rank's reads.  Returns (graph dict or None, stats)."""
-    from ._lib import APG_UNIPATH_READ_PATHS
+    rank's reads.  Default: sharded compaction (no rank holds every node);
+    gather_nodes=True: every rank gathers all nodes and builds the whole graph.
+    Returns (graph dict or None, stats)."""
+    from ._lib import APG_UNIPATH_GATHER_NODES, APG_UNIPATH_READ_PATHS
 
     p = apg_unipath_params()
     lib().apg_unipath_defaults(C.byref(p))
     p.K = K
-    p.flags = APG_UNIPATH_READ_PATHS if read_paths else 0
+    p.flags = (APG_UNIPATH_READ_PATHS if read_paths else 0) | (APG_UNIPATH_GATHER_NODES if gather_nodes else 0)
     g = apg_unipath_graph()
     st = apg_unipath_stats()
     check(lib().apg_sharded_unipaths(ctx.handle, comm.handle, reads.handle, C.byref(p),

@@ -400,6 +400,9 @@ typedef struct apg_unipath_params {
 } apg_unipath_params;
 
 #define APG_UNIPATH_READ_PATHS 1u /* also compute every read's KmerPath */
+#define APG_UNIPATH_GATHER_NODES 2u /* apg_sharded_unipaths: gather every node to every
+                                       rank and build the whole graph there (the replicated
+                                       build) instead of the sharded compaction */
 
 typedef struct apg_unipath_stats {
   uint64_t n_instances;  /* K-mer occurrences in the reads */

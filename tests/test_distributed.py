@@ -3,8 +3,9 @@ apg_sharded_*), one process per rank, every exchange inside libapg:
 
   * world 2 and 4: ranks share GPU 0 and talk over the TCP communicator;
     spectrum, PreCorrect (1 and 2 passes), FillFragments and the K=96
-    unipath graph + KmerPaths equal the single-GPU entry points on the union
-    of the ranks' reads;
+    unipath graph + KmerPaths (sharded compaction, and once the replicated
+    build) equal the single-GPU entry points on the union of the ranks'
+    reads (the compaction's hard cases: tests/test_sharded_graph.py);
   * world 1 over RCCL with the segment to self routed through ncclSend /
     ncclRecv (APG_COMM_SELF_P2P): the same stages, and one alltoallv of
     2^31 + 4 KiB bytes compared byte for byte (the size at which the old
@@ -36,7 +37,7 @@ def rank_pairs(rank, world):
     return PAIRS * rank // world, PAIRS * (rank + 1) // world
 
 
-def chain(ctx, comm, reads, n_cycles):
+def chain(ctx, comm, reads, n_cycles, gather=False):
     """The sharded chain on this rank's reads; host copies of everything."""
     from allpathslg_amd.distributed import (sharded_fill, sharded_precorrect, sharded_spectrum,
                                             sharded_unipaths)
@@ -47,14 +48,14 @@ def chain(ctx, comm, reads, n_cycles):
     fixed = ctx.download(d)
     filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
     ffrag = ctx.download(filled)
-    graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True)
+    graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True, gather_nodes=gather)
     d.free()
     filled.free()
     return {"hist": hist, "st": st, "pst": pst, "fixed": fixed, "fst": fst, "filled": ffrag, "graph": graph,
             "ust": ust}
 
 
-def worker(rank, world, port, n_cycles, q):
+def worker(rank, world, port, n_cycles, gather, q):
     sys.path.insert(0, ROOT)
     try:
         from allpathslg_amd import Context, synth_genome, synth_reads
@@ -65,18 +66,18 @@ def worker(rank, world, port, n_cycles, q):
         reads = synth_reads(g, b - a, seed=SEED + 1, first_pair=a)
         with Context(device=0) as ctx:
             comm = Comm.tcp(ctx, "127.0.0.1", port, rank, world, timeout_ms=240_000)
-            out = chain(ctx, comm, reads, n_cycles)
+            out = chain(ctx, comm, reads, n_cycles, gather)
             comm.close()
         q.put((rank, out, ""))
     except Exception as e:  # noqa: BLE001
         q.put((rank, None, repr(e)))
 
 
-def run_world(world, n_cycles):
+def run_world(world, n_cycles, gather=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=worker, args=(r, world, port, n_cycles, q)) for r in range(world)]
+    ps = [ctx.Process(target=worker, args=(r, world, port, n_cycles, gather, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
@@ -150,9 +151,11 @@ def check_against_mono(parts, m, world):
     assert f_off == m["filled"].n_reads
 
 
-@pytest.mark.parametrize("world,n_cycles", [(2, 1), (4, 1), (2, 2)])
-def test_sharded_chain_tcp_equals_single_gpu(mono, world, n_cycles):
-    check_against_mono(run_world(world, n_cycles), mono[n_cycles], world)
+@pytest.mark.parametrize("world,n_cycles,gather", [(2, 1, False), (4, 1, False), (2, 2, False), (2, 1, True)])
+def test_sharded_chain_tcp_equals_single_gpu(mono, world, n_cycles, gather):
+    """gather=False: sharded unipath compaction; True: the replicated build
+    (APG_UNIPATH_GATHER_NODES)."""
+    check_against_mono(run_world(world, n_cycles, gather), mono[n_cycles], world)
 
 
 def test_sharded_chain_rccl_world1_equals_single_gpu(gpu_ctx, mono):
