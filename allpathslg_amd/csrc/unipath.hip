@@ -24,6 +24,7 @@
 //   U8 outputs                     ids, unibases, HyperKmerPath vertices
 //      (lock-free union-find over unipath ends), per-read KmerPaths
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>

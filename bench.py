@@ -83,8 +83,15 @@ def parse():
     p.add_argument("--overlap", action="store_true",
                    help="run the K=25 spectrum on a second stream concurrently with correction/fill/unipaths")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--stage-times", action="store_true",
+                   help="print each stage's wall time per step on stderr (synchronises between stages)")
     p.add_argument("--sharded", action="store_true",
                    help="use the multi-GPU (all_to_all) code path even at world size 1 (needs torch.distributed.run)")
+    p.add_argument("--comm", choices=["rccl", "tcp"], default="rccl",
+                   help="communicator of the sharded path; tcp lets several ranks share one GPU (rehearsals)")
+    p.add_argument("--gather-nodes", action="store_true",
+                   help="sharded path: replicated unipath build (every rank gathers all nodes) instead of the "
+                        "sharded compaction")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_v13", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     return p.parse_args()
@@ -495,6 +502,8 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
+    if a.comm == "tcp":  # rehearsal: ranks may share the box's GPUs
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     sharded = world > 1 or a.sharded
     # BASELINE.json configs: one GPU = C2 (chr20, 40 M reads); N > 1 = C4
@@ -524,9 +533,13 @@ def main():
     dfrags = None if frags is None else ctx.upload(frags)
     comm = None
     if sharded:
-        uid = [unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = Comm.rccl(ctx, uid[0], rank, world)
+        if a.comm == "tcp":
+            comm = Comm.tcp(ctx, os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                            int(os.environ.get("MASTER_PORT", "29500")) + 1, rank, world, timeout_ms=600_000)
+        else:
+            uid = [unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = Comm.rccl(ctx, uid[0], rank, world)
     fill = {"out": None}  # device read set of the filled fragments, reused every step
 
     # --overlap: the K=25 spectrum of the pristine reads runs on a second
@@ -540,7 +553,17 @@ def main():
 
         pool = ThreadPoolExecutor(max_workers=1)
 
+    stage_t = [time.perf_counter()]
+
+    def mark(name):
+        if a.stage_times:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            log(rank, f"stage {name:12s} {(t - stage_t[0]) * 1e3:8.2f} ms")
+            stage_t[0] = t
+
     def step():
+        mark("(between)")
         fut = pool.submit(ctx_s.kmer_spectrum, dsrc, a.K) if overlap else None
         ctx.copy_reads(dreads, dsrc)
         if overlap:
@@ -549,26 +572,33 @@ def main():
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
             hist, st = sharded_spectrum(ctx, comm, dreads, a.K)
+        mark("spectrum")
         pst = ust = fst = None
         if not a.spectrum_only:
             if not sharded:
                 _, pst = ctx.precorrect(dreads, K=a.K_correct)
+                mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags
                 else:
                     fill["out"], _, fst = ctx.fill_fragments(dreads, K=a.K_correct, last_solid=True,
                                                              out=fill["out"])
                     uin = fill["out"]
+                mark("fill")
                 _, ust = ctx.unipaths(uin, a.K_unipath, read_paths=True, fetch=False)
+                mark("unipaths")
             else:
                 pst = sharded_precorrect(ctx, comm, dreads, K=a.K_correct)
+                mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags
                 else:
                     fill["out"], fst = sharded_fill(ctx, comm, dreads, K=a.K_correct, out=fill["out"],
                                                    last_solid=True)
                     uin = fill["out"]
-                _, ust = sharded_unipaths(ctx, comm, uin, a.K_unipath)
+                mark("fill")
+                _, ust = sharded_unipaths(ctx, comm, uin, a.K_unipath, gather_nodes=a.gather_nodes)
+                mark("unipaths")
         if fut is not None:
             hist, st = fut.result()
         return hist, st, pst, ust, fst
@@ -747,7 +777,8 @@ def main():
                                   "FillFragments of the corrected pairs (K=24 closures, insert 126-234), on GPU "
                                   "inside the timed step"),
                 "hbm_used_gb": (total_b - free_b) / 1e9,
-                "parallelism": (f"minimizer-key shards x{world}, libapg exchange over RCCL (apg_sharded_*)" if sharded
+                "parallelism": (f"minimizer-key shards x{world}, libapg exchange over {a.comm.upper()} (apg_sharded_*), "
+                                f"{'replicated' if a.gather_nodes else 'sharded'} unipath compaction" if sharded
                                 else "single GPU"),
             },
             "roofline": roofline,
