@@ -215,6 +215,17 @@ APG_ULOCS_RC = 1
 APG_ULOCS_SORTED = 2
 
 
+class apg_ucov_params(C.Structure):
+    _fields_ = [("min_len", C.c_uint64), ("reserved", C.c_uint64 * 3)]
+
+
+class apg_ucov_stats(C.Structure):
+    _fields_ = [("c0", C.c_double), ("n_long", C.c_uint64), ("n_locs", C.c_uint64), ("n_bad", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {"c0": float(self.c0), "n_long": int(self.n_long), "n_locs": int(self.n_locs), "n_bad": int(self.n_bad)}
+
+
 class apg_uloc_stats(C.Structure):
     _fields_ = [("n_reads", C.c_uint64), ("n_placed", C.c_uint64), ("n_locs", C.c_uint64), ("n_missing", C.c_uint64)]
 
@@ -359,6 +370,13 @@ SIGNATURES = {
     "apg_unipath_locs_dev": (
         C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_void_p), _u64p, C.POINTER(apg_uloc_stats)]),
     "apg_unibases_dev": (C.c_int, [_P, C.POINTER(_P)]),
+    "apg_ucov_defaults": (None, [C.POINTER(apg_ucov_params)]),
+    "apg_unipath_coverage_dev": (
+        C.c_int, [_P, C.c_void_p, C.c_uint64, C.POINTER(apg_ucov_params), _u64p, C.POINTER(C.c_double),
+                  C.POINTER(C.c_uint32), C.POINTER(apg_ucov_stats)]),
+    "apg_unipath_coverage": (
+        C.c_int, [_P, C.POINTER(apg_aln_pair), C.c_uint64, C.POINTER(apg_ucov_params), _u64p,
+                  C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(apg_ucov_stats)]),
     "apg_device_copy": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
     "apg_dreads_shape": (C.c_int, [_P, _P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),

@@ -2709,4 +2709,143 @@ int apg_urec_export(apg_ctx* ctx, void* d_out) {
 
 }  // extern "C"
 
+// ---------------------------------------------------------------------------
+// UnipathCoverage (apg_unipath_coverage, spec in include/apg.h; CPU
+// restatement oracle/ucov_oracle.c)
+// ---------------------------------------------------------------------------
+namespace apg {
+
+// placements per unipath: each wave finds runs of equal unipath ids among its
+// 64 consecutive placements (sorted input: long runs) and adds each run with
+// one atomic
+__global__ void __launch_bounds__(256) k_ucov_count(const ULoc* __restrict__ loc, uint64_t n, uint64_t U,
+                                                    unsigned long long* __restrict__ cnt,
+                                                    unsigned long long* __restrict__ bad) {
+  const int lane = lane_id();
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool v = i < n;
+    const uint32_t u = v ? loc[i].unipath : 0xffffffffu;
+    const uint32_t pu = (uint32_t)__shfl_up((int)u, 1, 64);
+    const bool head = v && (lane == 0 || pu != u);
+    const uint64_t heads = __ballot(head);
+    const uint32_t nvalid = (uint32_t)__popcll(__ballot(v));  // valid lanes are a prefix
+    if (head) {
+      const uint64_t above = lane == 63 ? 0 : heads & ~((2ull << lane) - 1);
+      const uint32_t end = min(above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u, nvalid);
+      const unsigned long long len = end - (uint32_t)lane;
+      if (u < U)
+        atomicAdd(&cnt[u], len);
+      else
+        atomicAdd(bad, len);
+    }
+  }
+}
+
+__global__ void k_ucov_cov(uint64_t U, const unsigned long long* __restrict__ cnt, const uint64_t* __restrict__ ulen,
+                           double* __restrict__ cov) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x)
+    cov[u] = ulen[u] ? (double)cnt[u] / (double)ulen[u] : 0.0;
+}
+
+__global__ void k_ucov_cn(uint64_t U, const double* __restrict__ cov, double c0, uint32_t* __restrict__ cn) {
+  for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < U; u += (uint64_t)gridDim.x * blockDim.x)
+    cn[u] = c0 > 0.0 ? (uint32_t)floor(cov[u] / c0 + 0.5) : 0u;
+}
+
+}  // namespace apg
+
+extern "C" {
+
+void apg_ucov_defaults(apg_ucov_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->min_len = 500;
+}
+
+int apg_unipath_coverage_dev(apg_ctx* ctx, const apg_aln_pair* d_locs, uint64_t n_locs, const apg_ucov_params* pp,
+                             uint64_t* counts, double* cov, uint32_t* copy_number, apg_ucov_stats* stats) {
+  using namespace apg;
+  APG_REQUIRE(ctx, "apg_unipath_coverage: NULL ctx");
+  APG_REQUIRE(n_locs == 0 || d_locs, "apg_unipath_coverage: d_locs is NULL");
+  const auto& g = ctx->gstate;
+  APG_REQUIRE(g.valid, "apg_unipath_coverage: no unipath graph on this context (run apg_unipaths first; the "
+                       "sharded compaction keeps no whole graph)");
+  apg_ucov_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_ucov_defaults(&p);
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const uint64_t U = g.n_unipaths;
+  unsigned long long* cnt = nullptr;
+  double* dcov = nullptr;
+  uint32_t* dcn = nullptr;
+  APG_TRY(workspace_t(ctx, "uc_cnt", U + 1, &cnt));  // [U] = rejected placements
+  APG_TRY(workspace_t(ctx, "uc_cov", std::max<uint64_t>(U, 1), &dcov));
+  APG_TRY(workspace_t(ctx, "uc_cn", std::max<uint64_t>(U, 1), &dcn));
+  APG_CHECK_HIP(hipMemsetAsync(cnt, 0, (U + 1) * 8, ctx->stream));
+  kbegin(ctx, "ucov_count", n_locs * 16 + U * 8);
+  if (n_locs)
+    k_ucov_count<<<grid_for(ctx, n_locs), 256, 0, ctx->stream>>>(reinterpret_cast<const ULoc*>(d_locs), n_locs, U, cnt,
+                                                                  cnt + U);
+  kend(ctx);
+  if (U) k_ucov_cov<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(U, cnt, g.ulen, dcov);
+  APG_CHECK_HIP(hipGetLastError());
+  std::vector<double> hc(U);
+  std::vector<uint64_t> hl(U);
+  unsigned long long nbad = 0;
+  if (U) {
+    APG_CHECK_HIP(hipMemcpyAsync(hc.data(), dcov, U * 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_CHECK_HIP(hipMemcpyAsync(hl.data(), g.ulen, U * 8, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  APG_CHECK_HIP(hipMemcpyAsync(&nbad, cnt + U, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  APG_REQUIRE(nbad == 0, "apg_unipath_coverage: placements on unipaths the graph does not have");
+  // length-weighted median of cov over the long unipaths
+  std::vector<std::pair<double, uint64_t>> lv;
+  uint64_t W = 0;
+  for (uint64_t u = 0; u < U; ++u)
+    if (hl[u] >= p.min_len) {
+      lv.emplace_back(hc[u], hl[u]);
+      W += hl[u];
+    }
+  std::sort(lv.begin(), lv.end());
+  double c0 = 0.0;
+  uint64_t acc = 0;
+  for (const auto& x : lv) {
+    acc += x.second;
+    if (2 * acc >= W) {
+      c0 = x.first;
+      break;
+    }
+  }
+  if (U) k_ucov_cn<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(U, dcov, c0, dcn);
+  APG_CHECK_HIP(hipGetLastError());
+  if (counts && U) APG_CHECK_HIP(hipMemcpyAsync(counts, cnt, U * 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (cov && U) std::memcpy(cov, hc.data(), U * 8);
+  if (copy_number && U) APG_CHECK_HIP(hipMemcpyAsync(copy_number, dcn, U * 4, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (stats) {
+    stats->c0 = c0;
+    stats->n_long = lv.size();
+    stats->n_locs = n_locs;
+    stats->n_bad = nbad;
+  }
+  return APG_OK;
+}
+
+int apg_unipath_coverage(apg_ctx* ctx, const apg_aln_pair* locs, uint64_t n_locs, const apg_ucov_params* p,
+                         uint64_t* counts, double* cov, uint32_t* copy_number, apg_ucov_stats* stats) {
+  using namespace apg;
+  APG_REQUIRE(ctx && (n_locs == 0 || locs), "apg_unipath_coverage: NULL argument");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_aln_pair* d = nullptr;
+  APG_TRY(workspace_t(ctx, "uc_locs", std::max<uint64_t>(n_locs, 1), &d));
+  if (n_locs) APG_CHECK_HIP(hipMemcpyAsync(d, locs, n_locs * sizeof(apg_aln_pair), hipMemcpyHostToDevice, ctx->stream));
+  return apg_unipath_coverage_dev(ctx, d, n_locs, p, counts, cov, copy_number, stats);
+}
+
+}  // extern "C"
+
 #include "ushard_graph.inc"

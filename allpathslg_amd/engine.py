@@ -397,6 +397,34 @@ class Context:
                                            C.byref(st)), "apg_error_correct_jump")
         return ReadSet(jumps.base_off.copy(), jumps.byte_off.copy(), pk, q), keep[: jumps.n_reads], st.as_dict()
 
+    def unipath_coverage(self, locs, n_unipaths: int, n_locs: Optional[int] = None, min_len: int = 500):
+        """UnipathCoverage (include/apg.h apg_unipath_coverage): placements per
+        unipath, placements per K-mer, genome-wide coverage c0 and copy-number
+        estimates on this context's last unipath build.  `locs`: (n, 4) int32
+        host placements, or a device pointer from unipath_locs(DeviceReads)
+        with n_locs.  Returns ({"counts", "cov", "cn"}, stats)."""
+        from ._lib import apg_aln_pair, apg_ucov_params, apg_ucov_stats
+
+        p = apg_ucov_params()
+        lib().apg_ucov_defaults(C.byref(p))
+        p.min_len = min_len
+        U = int(n_unipaths)
+        counts = np.zeros(max(U, 1), np.uint64)
+        cov = np.zeros(max(U, 1), np.float64)
+        cn = np.zeros(max(U, 1), np.uint32)
+        st = apg_ucov_stats()
+        outs = (counts.ctypes.data_as(C.POINTER(C.c_uint64)), cov.ctypes.data_as(C.POINTER(C.c_double)),
+                cn.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(st))
+        if isinstance(locs, np.ndarray):
+            a = np.ascontiguousarray(locs, dtype=np.int32)
+            n = len(a)
+            check(lib().apg_unipath_coverage(self._h, a.ctypes.data_as(C.POINTER(apg_aln_pair)) if n else None, n,
+                                             C.byref(p), *outs), "apg_unipath_coverage")
+        else:
+            check(lib().apg_unipath_coverage_dev(self._h, C.c_void_p(int(locs)), int(n_locs), C.byref(p), *outs),
+                  "apg_unipath_coverage_dev")
+        return {"counts": counts[:U], "cov": cov[:U], "cn": cn[:U]}, st.as_dict()
+
     def unipath_locs(self, reads, rc: bool = True, sorted: bool = True):
         """UnipathLocs: placements of `reads` (host ReadSet or DeviceReads) on
         the unipaths of this context's last unipath build (include/apg.h

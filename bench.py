@@ -212,9 +212,10 @@ def align_bench(ctx, genome, a, reps: int = 3):
 def placement_bench(ctx, dreads, a, reps: int = 3):
     """UnipathLocs line: the step's corrected reads placed on
     the step's K=96 unipaths (apg_unipath_locs_dev: one node-index lookup per
-    read K-mer, rc mirrors, stable by-unipath sort), then gap-free and column
-    consensus of those placements against the unibases (apg_unibases_dev),
-    all device-resident; per-kernel times from libapg's HIP events."""
+    read K-mer, rc mirrors, stable by-unipath sort), UnipathCoverage of those
+    placements (copy numbers), then gap-free and column consensus of the
+    placements against the unibases (apg_unibases_dev), all device-resident;
+    per-kernel times from libapg's HIP events."""
     ctx.reset_timing()
     dT = ctx.unibases_dev()
     p, n, st = ctx.unipath_locs(dreads, rc=True, sorted=True)
@@ -224,8 +225,11 @@ def placement_bench(ctx, dreads, a, reps: int = 3):
     cb = torch.empty(max(nt, 1), dtype=torch.uint8, device="cuda")
     cq = torch.empty(max(nt, 1), dtype=torch.uint8, device="cuda")
 
+    cov_out = {}
+
     def run():
         pp, nn, ss = ctx.unipath_locs(dreads, rc=True, sorted=True)
+        cov_out["r"] = ctx.unipath_coverage(pp, dT.n_reads, n_locs=nn)
         ctx.gapfree_dev(dreads, dT, pp, nn, gf.data_ptr())
         ctx.consensus_dev(dreads, dT, pp, nn, cb.data_ptr(), cq.data_ptr())
         return pp, nn, ss
@@ -252,6 +256,7 @@ def placement_bench(ctx, dreads, a, reps: int = 3):
     cbh, cqh = cb[:nt].cpu().numpy(), cq[:nt].cpu().numpy()
     voted = cqh > 0
     dom = "ulocs_count" if ms.get("ulocs_count", 0) >= ms.get("ulocs_write", 0) else "ulocs_write"
+    cn_long = cov_out["r"][0]["cn"][lens - (a.K_unipath - 1) >= 500]  # a repeat-free genome: one copy each
     out = {
         "workload": (f"the step's {dreads.n_reads} corrected reads placed on its {dT.n_reads} K={a.K_unipath} "
                      f"unipaths (+rc mirrors, sorted by unipath), gap-free + consensus on the unibases"),
@@ -265,8 +270,12 @@ def placement_bench(ctx, dreads, a, reps: int = 3):
                                       "frac": nb.get(dom, 0) / max(ms.get(dom, 0) * 1e-3, 1e-12) / 1e9 / HBM_PEAK_GBS}},
         "gapfree": {"ms": ms.get("gapfree", 0.0), "alignments_per_s": n / max(ms.get("gapfree", 0) * 1e-3, 1e-12)},
         "consensus": {"ms": ms.get("consensus_votes", 0.0) + ms.get("consensus_decide", 0.0)},
+        "unipath_coverage": {"ms": ms.get("ucov_count", 0.0), "c0": cov_out["r"][1]["c0"],
+                             "n_long": cov_out["r"][1]["n_long"],
+                             "copy_number_1_among_long": float(np.mean(cn_long == 1)) if cn_long.size else None},
         "kernels_ms": ms,
         "checks": {
+            "long_unipaths_single_copy": bool(cn_long.size and np.mean(cn_long == 1) > 0.99),
             "every_location_covers_a_kmer": bool((gfh[:, 0] >= a.K_unipath).all()) if n else True,
             "mismatches_outside_the_kmer_only": bool((gfh[:, 1] <= 100 - a.K_unipath).all()) if n else True,
             "most_reads_placed": st["n_placed"] > 0.5 * dreads.n_reads,

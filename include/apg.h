@@ -682,6 +682,42 @@ int apg_unipath_locs_dev(apg_ctx* ctx, const apg_dreads* reads, uint32_t flags, 
 int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out);
 
 /* ------------------------------------------------------------------------- */
+/* UnipathCoverage: read coverage and copy number per unipath of the          */
+/* context's last unipath build, from UnipathLocs placements.  Replaces the  */
+/* coverage / copy-number half of UnipathCoverage ([R:M]                     */
+/* src/paths/UnipathCoverage*, grep target only: reference snapshot empty).  */
+/* Spec [D] (restated; CPU restatement oracle/ucov_oracle.c):                */
+/*  - n[u]   = placements with t_id == u (every location counts once; with   */
+/*             APG_ULOCS_RC mirrors n[u] == n[rc(u)]);                        */
+/*  - cov[u] = (double)n[u] / (double)len[u]  (placements per K-mer, IEEE);  */
+/*  - c0     = length-weighted median of cov over the unipaths with len >=   */
+/*             min_len: cov values ascending, the first whose cumulative     */
+/*             length L satisfies 2 L >= the total length (0 if none);       */
+/*  - cn[u]  = c0 > 0 ? floor(cov[u] / c0 + 0.5) : 0  (copy-number estimate; */
+/*             0 = under half the genome-wide coverage, e.g. error paths).   */
+/* Counting runs on the device (wave-aggregated runs of equal unipath ids);  */
+/* the median over the <= n_unipaths long unipaths is selected on the host.  */
+/* ------------------------------------------------------------------------- */
+typedef struct apg_ucov_params {
+  uint64_t min_len; /* default 500 K-mers */
+  uint64_t reserved[3];
+} apg_ucov_params;
+typedef struct apg_ucov_stats {
+  double c0;         /* genome-wide placements per K-mer */
+  uint64_t n_long;   /* unipaths with len >= min_len */
+  uint64_t n_locs;
+  uint64_t n_bad;    /* placements whose t_id is not a unipath (rejected: error) */
+} apg_ucov_stats;
+void apg_ucov_defaults(apg_ucov_params* p);
+/* d_locs: n_locs placements in device memory (apg_unipath_locs_dev).  Host */
+/* outputs, caller-allocated with n_unipaths entries each (any may be NULL). */
+int apg_unipath_coverage_dev(apg_ctx* ctx, const apg_aln_pair* d_locs, uint64_t n_locs, const apg_ucov_params* p,
+                             uint64_t* counts, double* cov, uint32_t* copy_number, apg_ucov_stats* stats);
+/* Host placements (uploaded). */
+int apg_unipath_coverage(apg_ctx* ctx, const apg_aln_pair* locs, uint64_t n_locs, const apg_ucov_params* p,
+                         uint64_t* counts, double* cov, uint32_t* copy_number, apg_ucov_stats* stats);
+
+/* ------------------------------------------------------------------------- */
 /* Sharded module entry points (multi-GPU, one process per GPU):  */
 /* the same modules over the union of every rank's reads, every exchange     */
 /* through `comm` (which must have been made for ctx).  Each rank passes its */

@@ -517,3 +517,33 @@ def error_correct_jump_solid(jumps, solid, K: int = 24, max_q: int = 20, min_kee
     n, bo, yo, pk = _rp(fixed)
     L.oje_trim(n, bo, yo, pk, K, solid.ctypes.data_as(_u64p), len(solid), min_keep, keep.ctypes.data_as(_u32p))
     return fixed, keep[: fixed.n_reads], st
+
+
+def unipath_coverage(g: dict, locs: np.ndarray, min_len: int = 500):
+    """UnipathCoverage restated (oracle/ucov_oracle.c): placements per
+    unipath, per K-mer, genome-wide coverage c0 and copy numbers on graph
+    `g` from (n, 4) int32 placements [read, unipath, start, flags].
+    Returns {"counts", "cov", "cn", "c0", "n_long"}."""
+    L = lib()
+    if not hasattr(L, "_ouc"):
+        L.ouc_coverage.restype = C.c_int
+        L.ouc_coverage.argtypes = [C.c_uint64, _u64p, _u32p, C.c_uint64, C.c_uint64, _u64p,
+                                   C.POINTER(C.c_double), _u32p, C.POINTER(C.c_double), _u64p]
+        L._ouc = True
+    U = int(g["n_unipaths"])
+    ulen = np.ascontiguousarray(g["len"], dtype=np.uint64)
+    pairs = np.ascontiguousarray(locs, dtype=np.int32).view(np.uint32).reshape(-1)
+    if pairs.size == 0:
+        pairs = np.zeros(4, np.uint32)
+    n = len(locs)
+    counts = np.zeros(max(U, 1), np.uint64)
+    cov = np.zeros(max(U, 1), np.float64)
+    cn = np.zeros(max(U, 1), np.uint32)
+    c0 = C.c_double(0)
+    nl = C.c_uint64(0)
+    rc = L.ouc_coverage(U, ulen.ctypes.data_as(_u64p), pairs.ctypes.data_as(_u32p), n, min_len,
+                        counts.ctypes.data_as(_u64p), cov.ctypes.data_as(C.POINTER(C.c_double)),
+                        cn.ctypes.data_as(_u32p), C.byref(c0), C.byref(nl))
+    if rc:
+        raise RuntimeError(f"oracle unipath_coverage failed ({rc})")
+    return {"counts": counts[:U], "cov": cov[:U], "cn": cn[:U], "c0": c0.value, "n_long": int(nl.value)}

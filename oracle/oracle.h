@@ -43,6 +43,9 @@ int orl_locs(uint64_t U, const uint64_t* ulen, const uint64_t* urc, const uint64
              uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
              uint32_t flags, uint32_t** out, uint64_t* n_out, uint64_t* stats);
 
+int ouc_coverage(uint64_t U, const uint64_t* ulen, const uint32_t* pairs, uint64_t n, uint64_t min_len,
+                 uint64_t* counts, double* cov, uint32_t* cn, double* c0_out, uint64_t* n_long);
+
 void oje_trim(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
               const uint64_t* solid, uint64_t ns, uint32_t min_keep, uint32_t* keep);
 
