@@ -215,6 +215,12 @@ APG_ULOCS_RC = 1
 APG_ULOCS_SORTED = 2
 
 
+class apg_repeat_params(C.Structure):
+    _fields_ = [("n_families", C.c_uint32), ("tandem_unit_max", C.c_uint32), ("family_len", C.c_uint32 * 8),
+                ("family_frac", C.c_double * 8), ("family_div", C.c_double * 8), ("tandem_frac", C.c_double),
+                ("tandem_array_max", C.c_uint32), ("reserved0", C.c_uint32)]
+
+
 class apg_ucov_params(C.Structure):
     _fields_ = [("min_len", C.c_uint64), ("reserved", C.c_uint64 * 3)]
 
@@ -380,6 +386,8 @@ SIGNATURES = {
     "apg_device_copy": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
     "apg_dreads_shape": (C.c_int, [_P, _P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
+    "apg_repeat_defaults": (None, [C.POINTER(apg_repeat_params)]),
+    "apg_synth_repeats": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(apg_repeat_params), _u8p]),
     "apg_synth_sizes": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u64p, _u64p]),
     "apg_synth_reads": (C.c_int, [C.POINTER(apg_synth_params), _u8p, _u64p, _u64p, _u8p, _u8p]),
     "apg_synth_layout": (C.c_int, [C.POINTER(apg_synth_params), _u64p, _u32p, C.POINTER(C.c_uint8)]),

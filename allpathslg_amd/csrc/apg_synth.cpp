@@ -121,6 +121,61 @@ int apg_synth_genome(uint64_t genome_len, uint64_t seed, uint8_t* out) {
   return APG_OK;
 }
 
+void apg_repeat_defaults(apg_repeat_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->n_families = 3;
+  const uint32_t len[3] = {300, 6000, 1000};
+  const double frac[3] = {0.10, 0.05, 0.005}, div[3] = {0.12, 0.04, 0.002};
+  for (int f = 0; f < 3; ++f) {
+    p->family_len[f] = len[f];
+    p->family_frac[f] = frac[f];
+    p->family_div[f] = div[f];
+  }
+  p->tandem_frac = 0.01;
+  p->tandem_unit_max = 60;
+  p->tandem_array_max = 4000;
+}
+
+// One sequential stream (salt 2): the injection order fixes the result.
+int apg_synth_repeats(uint64_t genome_len, uint64_t seed, const apg_repeat_params* p, uint8_t* g) {
+  if (!p || (!g && genome_len) || p->n_families > APG_MAX_REPEAT_FAMILIES) return APG_E_ARG;
+  Xoshiro256ss rng(stream_seed(seed, 2, 0));
+  auto mutate = [&](uint8_t b, double rate) -> uint8_t {
+    if (rate > 0 && rng.uniform() < rate) return (uint8_t)((b + 1 + rng.below(3)) & 3);
+    return b;
+  };
+  for (uint32_t f = 0; f < p->n_families; ++f) {
+    const uint64_t L = p->family_len[f];
+    if (L == 0 || L > genome_len) continue;
+    std::vector<uint8_t> cons(L);
+    for (auto& b : cons) b = (uint8_t)(rng.next() & 3);
+    const uint64_t target = (uint64_t)(p->family_frac[f] * (double)genome_len);
+    for (uint64_t covered = 0; covered < target; covered += L) {
+      const uint64_t at = rng.below(genome_len - L + 1);
+      const bool rc = rng.next() & 1;
+      for (uint64_t i = 0; i < L; ++i) {
+        const uint8_t b = rc ? (uint8_t)(3 - cons[L - 1 - i]) : cons[i];
+        g[at + i] = mutate(b, p->family_div[f]);
+      }
+    }
+  }
+  const uint64_t ttarget = (uint64_t)(p->tandem_frac * (double)genome_len);
+  const uint32_t umax = std::max<uint32_t>(1, p->tandem_unit_max);
+  const uint64_t amax = std::max<uint64_t>(2, p->tandem_array_max);
+  std::vector<uint8_t> unit(umax);
+  for (uint64_t covered = 0; covered < ttarget;) {
+    const uint32_t u = 1 + (uint32_t)rng.below(umax);
+    for (uint32_t i = 0; i < u; ++i) unit[i] = (uint8_t)(rng.next() & 3);
+    const uint64_t lo = 2ull * u, hi = std::max<uint64_t>(lo, std::min<uint64_t>(amax, genome_len));
+    const uint64_t len = std::min<uint64_t>(genome_len, lo + rng.below(hi - lo + 1));
+    const uint64_t at = rng.below(genome_len - len + 1);
+    for (uint64_t i = 0; i < len; ++i) g[at + i] = mutate(unit[i % u], 0.01);
+    covered += len;
+  }
+  return APG_OK;
+}
+
 int apg_synth_sizes(const apg_synth_params* p, uint64_t* n_reads, uint64_t* n_bases,
                     uint64_t* n_packed_bytes) {
   if (!p) return APG_E_ARG;

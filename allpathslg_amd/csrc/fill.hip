@@ -174,15 +174,27 @@ __device__ __forceinline__ uint64_t walk_window(uint64_t atail, unsigned __int12
   return ((atail << (2 * d)) | (uint64_t)pv) & t.m1;
 }
 
+// Two passes keep one deep search from holding a whole wave: pass 1 (every
+// pair, list == null) searches with a cap of kFillCap1 expansions and defers
+// the pairs that reach it; pass 2 runs the deferred ones (list, *list_n)
+// with the full max_steps.  The walk is deterministic, so a pair that ends
+// within the cap ends exactly as it would with the full budget.
+constexpr uint32_t kFillCap1 = 96;
+
 __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
                                               uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
-                                              const uint8_t* __restrict__ clean, FillCounters* __restrict__ cnt) {
+                                              const uint8_t* __restrict__ clean, FillCounters* __restrict__ cnt,
+                                              uint32_t cap, const uint32_t* __restrict__ list,
+                                              const unsigned long long* __restrict__ list_n,
+                                              uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rv.n_pairs;
-       i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t nwork = list ? *list_n : rv.n_pairs;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwork;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = list ? list[k] : k;
     const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
     const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
     const uint8_t* A = rv.packed + rv.byte_off[2 * i];
@@ -253,7 +265,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
           }
           bool down = false;
           if (d < gmax) {
-            if (++steps > p.max_steps) {
+            if (++steps > cap) {
               budget = true;
               break;
             }
@@ -278,6 +290,10 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
           pv = (pvd << 2) | b2;
           d = dd + 1;
         }
+      }
+      if (budget && n_clos < 2 && cap < p.max_steps) {  // pass 1: search again with the full budget
+        defer[atomicAdd(ndefer, 1ull)] = (uint32_t)i;
+        continue;
       }
       if (n_clos >= 2)
         st = kFillAmbiguous;
@@ -483,10 +499,21 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   APG_CHECK_HIP(hipMemsetAsync(cnt, 0, 6 * 8, ctx->stream));
   const FillReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, np};
   const FillP fp{p.K, p.min_insert, p.max_insert, p.max_steps};
+  uint32_t* defer = nullptr;
+  unsigned long long* ndefer = nullptr;
+  APG_TRY(workspace_t(ctx, "fill_defer", npc, &defer));
+  APG_TRY(workspace_t(ctx, "fill_ndefer", 1, &ndefer));
+  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, 8, ctx->stream));
   kbegin(ctx, "fill", dr->n_bytes + 16 * dr->n_reads + np * (sizeof(FillRec) + 12));
-  if (np)
-    k_fill<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean,
-                                                        reinterpret_cast<FillCounters*>(cnt));
+  if (np) {
+    FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
+    k_fill<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
+                                                        std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer,
+                                                        ndefer);
+    if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
+      k_fill<<<(uint32_t)ctx->n_cu * 8, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
+                                                               p.max_steps, defer, ndefer, nullptr, nullptr);
+  }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   APG_TRY(scan_u32_u64(ctx, lens, np, bscan, "fb"));

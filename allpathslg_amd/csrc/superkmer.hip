@@ -32,6 +32,7 @@
 // n <= 41 - K.  Algorithmic bytes per 100-bp read at K = 25: ~12 records of
 // 16 B (vs 76 x 8 B hash records).
 #include <algorithm>
+#include <functional>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -55,6 +56,13 @@ constexpr int kSkHistBins = 128;  // LDS spectrum bins (counts above go to globa
 constexpr uint32_t kSkSlotCap = 6144;  // weak pass: instances per bucket with a recorded slot (LDS: 3 blocks/CU)
 constexpr uint32_t kSkWaveSlots = kSkSlotCap / (kSkThreads / 64);  // recorded slots per wave
 constexpr int kSkMaxW = 17;  // w = K - m + 1 <= 17 for K <= 32
+// A table this full is given up on: an insert that finds no room within
+// kSkProbeMax slots marks the bucket for the global table (a full 2048-slot
+// table otherwise costs every further insert a scan of all of it).
+constexpr uint32_t kSkProbeMax = 256;
+// Buckets of more records than this go to the global table without an LDS
+// attempt (repeat-rich genomes: one minimizer shared by thousands of copies).
+constexpr uint32_t kSkHeavyRecords = 8192;
 
 struct SkP {
   int K, m, w, maxnk;
@@ -222,7 +230,7 @@ __device__ __forceinline__ uint32_t sk_slot(uint64_t c, int bits) {
 // to claim with one CAS.  Returns the slot, or kSkTab when the table is full.
 __device__ __forceinline__ uint32_t sk_tab_claim(unsigned long long* tkey, uint64_t c, uint32_t g) {
   constexpr unsigned long long EMPTY = ~0ull;
-  for (uint32_t n = 0; n < kSkTab + kSkGrp;) {
+  for (uint32_t n = 0; n < kSkProbeMax;) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(&tkey[g]);
     const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(&tkey[g + 2]);
     const unsigned long long k[kSkGrp] = {a.x, a.y, b.x, b.y};
@@ -330,7 +338,8 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       noff = boff[bid(nbk)];
       nnr = (uint32_t)(boff[bid(nbk) + 1] - noff);
     }
-    if (nr == 0) {  // block-uniform
+    if (nr == 0 || nr > kSkHeavyRecords) {  // block-uniform
+      if (nr && tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bid(bkt);
       if (tid < nnr) pre = rec[noff + tid];
       bkt = nbk;
       off = noff;
@@ -348,6 +357,10 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     // the bucket's counts are final.
     uint32_t ibw = 0;  // this wave's K-mer instances before this chunk (wave-uniform)
     for (uint32_t c0 = 0; c0 < nr; c0 += NT) {
+      if (__builtin_amdgcn_readfirstlane(*(volatile int*)&ovf)) {  // the table filled: stop, load the next bucket
+        if (tid < nnr) pre = rec[noff + tid];
+        break;
+      }
       uint32_t nk = 0;
       if (c0 + tid < nr) {
         nk = (uint32_t)(pre.w0 >> 32) & 0xff;
@@ -561,7 +574,7 @@ template <uint32_t TS>
 __device__ __forceinline__ uint32_t lds_claim(unsigned long long* tk, uint64_t c, uint32_t g, bool* fresh) {
   constexpr unsigned long long EMPTY = ~0ull;
   *fresh = false;
-  for (uint32_t n = 0; n < TS + kSkGrp;) {
+  for (uint32_t n = 0; n < (TS < kSkProbeMax ? TS : kSkProbeMax);) {
     const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(&tk[g]);
     const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(&tk[g + 2]);
     const unsigned long long k[kSkGrp] = {a.x, a.y, b.x, b.y};
@@ -682,8 +695,13 @@ __global__ void __launch_bounds__(kDdThreads) k_sk_bucket_dd(const R* __restrict
       }
       finish();
     };
-    if (nr == 0 || (WEAK && nr > kDdRecCap)) {  // block-uniform
-      if (nr && tid == 0) redo[atomicAdd(&o.gstats[4], 1ull)] = (uint32_t)bkt;
+    if (nr == 0 || nr > kSkHeavyRecords || (WEAK && nr > kDdRecCap)) {  // block-uniform
+      if (nr && tid == 0) {
+        if (nr > kSkHeavyRecords)
+          o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+        else
+          redo[atomicAdd(&o.gstats[4], 1ull)] = (uint32_t)bkt;
+      }
       if (tid < nnr) pre = rec[noff + tid];
       bkt = nbk;
       off = noff;
@@ -779,7 +797,8 @@ __global__ void __launch_bounds__(kDdThreads) k_sk_bucket_dd(const R* __restrict
       }
       if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)ts;
     };
-    for (uint32_t f0 = 0; f0 < ni; f0 += 2 * NT) {  // block-uniform trip count
+    for (uint32_t f0 = 0; f0 < ni; f0 += 2 * NT) {
+      if (__builtin_amdgcn_readfirstlane(*(volatile int*)&flag)) break;  // the table filled (no barrier inside)
       insert(f0 + tid, f0 + tid < ni);
       if (f0 + NT < ni) insert(f0 + NT + tid, f0 + NT + tid < ni);
     }
@@ -1111,6 +1130,20 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
     }
     cur = dst;
+  }
+  if (ctx->verbose && nb) {  // bucket skew: the largest buckets (records)
+    std::vector<uint64_t> hb(nb + 1);
+    APG_CHECK_HIP(hipMemcpyAsync(hb.data(), boff, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    std::vector<uint64_t> sz(nb);
+    for (uint64_t b = 0; b < nb; ++b) sz[b] = hb[b + 1] - hb[b];
+    std::sort(sz.begin(), sz.end(), std::greater<uint64_t>());
+    uint64_t over = 0;
+    for (uint64_t b = 0; b < nb && sz[b] > 8 * (n / nb + 1); ++b) over += sz[b];
+    vlog(ctx, "sk buckets: %llu, mean %.0f records, largest %llu %llu %llu %llu, %llu records in buckets > 8x mean",
+         (unsigned long long)nb, (double)n / nb, (unsigned long long)sz[0], (unsigned long long)sz[std::min<uint64_t>(1, nb - 1)],
+         (unsigned long long)sz[std::min<uint64_t>(2, nb - 1)], (unsigned long long)sz[std::min<uint64_t>(3, nb - 1)],
+         (unsigned long long)over);
   }
   // outputs
   const uint64_t hl = std::max<uint64_t>(hist_len, 2);

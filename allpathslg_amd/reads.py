@@ -157,9 +157,26 @@ class ReadSet:
             L.apg_reads_release(C.byref(r))
 
 
-def synth_genome(length: int, seed: int) -> np.ndarray:
+def synth_genome(length: int, seed: int, repeats=None) -> np.ndarray:
+    """Uniform iid genome; repeats=True injects apg_repeat_defaults' human-like
+    mix (include/apg.h apg_synth_repeats), or pass a dict of
+    apg_repeat_params fields to override it."""
     g = np.empty(length, dtype=np.uint8)
     check(lib().apg_synth_genome(length, seed, _ptr(g, C.c_uint8)), "apg_synth_genome")
+    if repeats:
+        from ._lib import apg_repeat_params
+
+        p = apg_repeat_params()
+        lib().apg_repeat_defaults(C.byref(p))
+        if isinstance(repeats, dict):
+            for k, v in repeats.items():
+                if isinstance(v, (list, tuple)):
+                    arr = getattr(p, k)
+                    for i, x in enumerate(v):
+                        arr[i] = x
+                else:
+                    setattr(p, k, v)
+        check(lib().apg_synth_repeats(length, seed, C.byref(p), _ptr(g, C.c_uint8)), "apg_synth_repeats")
     return g
 
 

@@ -65,6 +65,9 @@ def parse():
                    help="pairs of the CPU baseline's FillFragments + unipath sample")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="OpenMP threads of the CPU baseline (0: OMP_NUM_THREADS / every CPU of the process)")
+    p.add_argument("--repeat-steps", type=int, default=2,
+                   help="steps of the repeats line: the same step on a repeat-rich chr20-size genome "
+                        "(apg_synth_repeats; 0 = skip)")
     p.add_argument("--c3-jump-pairs", type=int, default=10_000_000,
                    help="jump pairs of the C3 line (BASELINE configs[2]; 0 = skip)")
     p.add_argument("--no-file-to-graph", dest="file_to_graph", action="store_false",
@@ -411,6 +414,68 @@ def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2):
     return out
 
 
+def repeats_bench(ctx, a) -> dict:
+    """Repeats line: the bench step (K=25 spectrum, K=24 PreCorrect,
+    FillFragments, K=96 unipaths + KmerPaths) on a chr20-size genome with
+    apg_synth_repeats' human-like mix injected (Alu-like 300-bp family over
+    10 %, L1-like 6-kb over 5 %, a young near-identical 1-kb family, tandem
+    arrays over 1 %): skewed buckets, counts in the thousands, collapsed
+    repeats — what the iid genome of the main line never shows.  Same read
+    count and simulator; inputs resident in HBM."""
+    g = synth_genome(a.genome_len, a.seed + 31, repeats=True)
+    reads = synth_reads(g, a.reads_per_gpu // 2, seed=a.seed + 32, with_quals=True, threads=16)
+    dsrc, dw = ctx.upload(reads), ctx.upload(reads)
+    st = {"filled": None}
+
+    def step():
+        ctx.copy_reads(dw, dsrc)
+        hist, kst = ctx.kmer_spectrum(dw, a.K)
+        _, pst = ctx.precorrect(dw, K=a.K_correct)
+        st["filled"], _, fst = ctx.fill_fragments(dw, K=a.K_correct, last_solid=True, out=st["filled"])
+        _, ust = ctx.unipaths(st["filled"], a.K_unipath, read_paths=True, fetch=False)
+        return hist, kst, pst, fst, ust
+
+    step()
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(a.repeat_steps):
+        hist, kst, pst, fst, ust = step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / a.repeat_steps
+    kt = ctx.kernel_times()
+    ms = {k: v[0] / a.repeat_steps for k, v in kt.items()}
+    m = np.arange(len(hist), dtype=np.uint64)
+    out = {
+        "workload": (f"the main step on a {a.genome_len}-bp genome with injected repeats (apg_repeat_defaults: "
+                     f"300 bp x 10 % at 12 % divergence, 6 kb x 5 % at 4 %, 1 kb x 0.5 % at 0.2 %, tandem arrays "
+                     f"1 %), {reads.n_reads} reads"),
+        "reads": reads.n_reads,
+        "ms_per_step": wall * 1e3,
+        "reads_per_s": reads.n_reads / wall,
+        "kernels_ms": {k: v for k, v in sorted(ms.items(), key=lambda kv: -kv[1])[:16]},
+        "spectrum_stats": kst,
+        "max_count_bin_used": int(np.nonzero(hist)[0].max()) if hist.any() else 0,
+        "kmers_seen_1000x_or_more": int(hist[1000:].sum()),
+        "precorrect_stats": pst,
+        "fill_stats": fst,
+        "unipath_stats": ust,
+        "checks": {
+            # the last bin collects every count >= hist_len - 1: equality below it, a bound with it
+            "sum_m_h_consistent": (int((m[:-1] * hist[:-1].astype(np.uint64)).sum())
+                                   + int(m[-1]) * int(hist[-1])) <= kst["n_kmers"] if hist[-1] else
+                                  int((m * hist.astype(np.uint64)).sum()) == kst["n_kmers"],
+            "precorrect_corrected_most_suspects": pst["n_corrected"] > 0.5 * pst["n_suspect"],
+            "unipath_instances_equal_sum_len_minus_K_plus_1": ust["n_instances"] == (
+                int(fst["filled_bases"]) - (a.K_unipath - 1) * int(fst["n_filled"])),
+            "repeats_collapse_nodes": ust["n_nodes"] < a.genome_len - a.K_unipath + 1,
+        },
+    }
+    for d in (dsrc, dw, st["filled"]):
+        d.free()
+    return out
+
+
 def file_to_graph(ctx, reads, a) -> dict:
     """The module-boundary rate beside `value`: .fastb/.qualb files (on
     /dev/shm, so parsing and PCIe, not a disk, are what is timed) -> host read
@@ -745,6 +810,10 @@ def main():
     if rank == 0 and world == 1 and not a.spectrum_only and a.c3_jump_pairs > 0 and frags is None:
         c3 = c3_bench(ctx, dsrc, dreads, genome, a)
 
+    rep = None
+    if rank == 0 and world == 1 and not a.spectrum_only and a.repeat_steps > 0 and frags is None:
+        rep = repeats_bench(ctx, a)
+
     f2g = None
     if rank == 0 and world == 1 and not a.spectrum_only and a.file_to_graph and frags is None:
         f2g = file_to_graph(ctx, reads, a)
@@ -796,6 +865,7 @@ def main():
             "aligners": aligners,
             "placement": placement,
             "c3": c3,
+            "repeats": rep,
             "file_to_graph": f2g,
             "stats": {k: st[k] for k in ("n_kmers", "n_distinct", "n_overflow", "max_bucket") if k in st},
             "precorrect_stats": pst,

@@ -764,6 +764,31 @@ typedef struct apg_synth_params {
 
 /* Genome (2 bits/base, one byte per base in out) */
 int apg_synth_genome(uint64_t genome_len, uint64_t seed, uint8_t* out_bases);
+/* Repeats injected into a synthetic genome (in place, deterministic per     */
+/* seed): interspersed families — a random consensus of family_len[f] bases, */
+/* copies at random positions until family_frac[f] of the genome is covered, */
+/* each copy substituted at rate family_div[f] — and tandem arrays (a random */
+/* unit of 1..tandem_unit_max bases repeated to 2 units .. tandem_array_max  */
+/* bases, 1 % substitutions) covering tandem_frac.  Real genomes are not in  */
+/* the container; this gives the counting stages skewed buckets, */
+/* high-count K-mers and collapsed / cyclic unipaths at scale.               */
+#define APG_MAX_REPEAT_FAMILIES 8
+typedef struct apg_repeat_params {
+  uint32_t n_families;
+  uint32_t tandem_unit_max;
+  uint32_t family_len[APG_MAX_REPEAT_FAMILIES];
+  double family_frac[APG_MAX_REPEAT_FAMILIES];
+  double family_div[APG_MAX_REPEAT_FAMILIES];
+  double tandem_frac;
+  uint32_t tandem_array_max;
+  uint32_t reserved0;
+} apg_repeat_params;
+/* A human-like mix: 300-bp family over 10 % at 12 % divergence (Alu-like),  */
+/* 6-kb family over 5 % at 4 % (L1-like), 1-kb family over 0.5 % at 0.2 %   */
+/* (young, near-identical copies), tandem arrays over 1 % (units <= 60 bp,  */
+/* arrays <= 4 kb).                                                          */
+void apg_repeat_defaults(apg_repeat_params* p);
+int apg_synth_repeats(uint64_t genome_len, uint64_t seed, const apg_repeat_params* p, uint8_t* genome);
 /* Sizes for a synth call: n_reads = 2*n_pairs, packed bytes. */
 int apg_synth_sizes(const apg_synth_params* p, uint64_t* n_reads, uint64_t* n_bases,
                     uint64_t* n_packed_bytes);

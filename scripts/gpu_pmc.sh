@@ -5,7 +5,7 @@ set -o pipefail
 R="$GRAFT_REPO_ROOT"
 cd /tmp && export TMPDIR=/tmp
 # main step only: every timed kernel launches once per run, so a per-launch mean is one size
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement ${BENCH_ARGS:-}"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0 ${BENCH_ARGS:-}"
 run() {
   local tag="$1"; shift
   echo "== pmc $tag: $*"

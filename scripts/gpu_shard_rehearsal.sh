@@ -5,12 +5,12 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-L="--steps 3 --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement"
+L="--steps 3 --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0"
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29611 bench.py --sharded $L > gpurun_out/bench_w1_sharded.json 2> gpurun_out/bench_w1_sharded.err \
  && timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29621 bench.py --sharded --gather-nodes $L > gpurun_out/bench_w1_gather.json 2> gpurun_out/bench_w1_gather.err \
  && timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29631 bench.py --gpus 2 --comm tcp --reads-per-gpu ${RPG:-20000000} $L > gpurun_out/bench_w2_tcp.json 2> gpurun_out/bench_w2_tcp.err
 rc=$?
-[ $rc -eq 0 ] && timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29641 bench.py --sharded --verbose --steps 1 --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement > gpurun_out/bench_w1_verbose.json 2> gpurun_out/bench_w1_verbose.err
+[ $rc -eq 0 ] && timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29641 bench.py --sharded --verbose --steps 1 --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0 > gpurun_out/bench_w1_verbose.json 2> gpurun_out/bench_w1_verbose.err
 grep "phase" gpurun_out/bench_w1_verbose.err | tail -9
 for f in bench_w1_sharded bench_w1_gather bench_w2_tcp; do
   python - "$f" <<'PY'

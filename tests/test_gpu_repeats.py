@@ -1,0 +1,50 @@
+"""GPU parity on a repeat-rich synthetic genome (apg_synth_repeats: an
+Alu-like, an L1-like and a young near-identical family plus tandem arrays):
+the bucket skew, high-count K-mers, LDS-table overflow / dedup hand-back and
+collapsed or cyclic unipaths the iid genome never produces.  Everything
+equals the CPU restatement.  Parity vs real ALLPATHS-LG: unpinned."""
+import numpy as np
+import pytest
+
+import oracle
+from allpathslg_amd import Context, synth_fragments, synth_genome, synth_reads
+from tests.test_gpu_unipath import assert_graph_equal
+
+pytestmark = pytest.mark.gpu
+
+G = 1_000_000
+
+
+@pytest.fixture(scope="module")
+def rep_reads():
+    g = synth_genome(G, 51, repeats={"tandem_frac": 0.03})
+    return g, synth_reads(g, 300_000, seed=52)
+
+
+@pytest.mark.parametrize("dedup", [0, 1, 2])
+def test_spectrum_on_repeats(rep_reads, dedup):
+    _, reads = rep_reads
+    with Context(device=0, kmer_dedup=dedup) as ctx:
+        for K in (24, 25):
+            hist, st = ctx.kmer_spectrum(reads, K)
+            assert np.array_equal(hist, oracle.kmer_spectrum(reads, K)), (dedup, K)
+            assert hist[1000:].sum() > 0  # K-mers seen over a thousand times
+
+
+def test_precorrect_on_repeats(gpu_ctx, rep_reads):
+    _, reads = rep_reads
+    got, st = gpu_ctx.precorrect(reads, K=24)
+    exp, est = oracle.precorrect(reads, K=24)
+    assert np.array_equal(got.packed[: int(got.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(got.quals, exp.quals)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+        assert st[k] == est[k], k
+
+
+def test_unipaths_on_repeats(gpu_ctx, rep_reads):
+    g, _ = rep_reads
+    frags = synth_fragments(g, 150_000, seed=53)
+    got, st = gpu_ctx.unipaths(frags, 96)
+    assert_graph_equal(got, oracle.unipaths(frags, 96))
+    # repeats collapse: fewer distinct 96-mers than genome positions
+    assert st["n_nodes"] < 0.99 * (G - 95)

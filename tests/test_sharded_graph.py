@@ -7,7 +7,8 @@ apg_unipaths on the union of the reads, on inputs chosen for the stitch's
 hard cases: a circular genome (a cycle that crosses shards and is cut before
 its minimum K-mer, possibly inside a fragment), a genome folded onto its own
 reverse complement (palindromic junctions), repeats with branching, noisy
-reads (many short unipaths), small K with palindromic K-mers.  Ranks share
+reads (many short unipaths), small K with palindromic K-mers, and the
+repeat-rich synthetic genome (apg_synth_repeats).  Ranks share
 GPU 0 and talk over the TCP communicator."""
 import multiprocessing as mp
 import os
@@ -41,6 +42,11 @@ def case_reads(name):
         return tiling(repeat_genome(seed=34), L=150, step=2), 96
     if name == "noisy":
         return noisy_reads(G=40_000, n=12_000, L=100, err=0.01, seed=35), 25
+    if name == "repeat_genome":  # apg_synth_repeats: collapsed repeats, tandem arrays
+        from allpathslg_amd import synth_fragments
+
+        g = synth_genome(300_000, 36, repeats={"tandem_frac": 0.03})
+        return synth_fragments(g, 60_000, seed=37), 96
     if name == "palindromes":
         r = palindrome_reads()
         return ReadSet.from_sequences([r.read(i) for i in range(r.n_reads)] * 3), 4
@@ -91,7 +97,8 @@ def run_world(world, name):
     return [r[1] for r in res]
 
 
-@pytest.mark.parametrize("name", ["circular", "circular_k31", "folded", "repeats", "noisy", "palindromes"])
+@pytest.mark.parametrize("name", ["circular", "circular_k31", "folded", "repeats", "noisy", "palindromes",
+                                  "repeat_genome"])
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_graph_equals_single_gpu(gpu_ctx, world, name):
     reads, K = case_reads(name)
