@@ -1123,7 +1123,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     R* dst = (cur == bufA) ? bufB : bufA;
     std::vector<uint64_t> hb;
     const bool last = lev + 1 == nlev;
-    APG_TRY(part_level<R>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "s"));
+    APG_TRY(part_level<R>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb,
+                          sizeof(R) == sizeof(SK24) ? "s24" : "s"));
     nb = parents.size() << bits;
     if (!last) {
       parents.assign(nb, {});

@@ -770,13 +770,25 @@ def main():
         "algorithmic_bytes_per_launch": per_launch_bytes,
         "ms_per_launch": per_launch_ms,
     }
-    if os.path.exists(a.traffic_json):
-        tj = json.load(open(a.traffic_json))
-        if name in tj:  # PMC FETCH_SIZE/WRITE_SIZE passes of this kernel (separate rocprofv3 runs)
-            t = tj[name]["traffic_bytes_per_launch"]
-            roofline["traffic"] = t
-            roofline["traffic_source"] = os.path.relpath(a.traffic_json, ROOT)
-            roofline["traffic_over_algorithmic"] = t / max(per_launch_bytes, 1)
+    tj = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
+    if name in tj:  # PMC FETCH_SIZE/WRITE_SIZE passes of this kernel (separate rocprofv3 runs)
+        t = tj[name]["traffic_bytes_per_launch"]
+        roofline["traffic"] = t
+        roofline["traffic_source"] = os.path.relpath(a.traffic_json, ROOT)
+        roofline["traffic_over_algorithmic"] = t / max(per_launch_bytes, 1)
+    # the same figures for the step's largest kernels (time per step), the
+    # dominant one first: where the step's time goes against the HBM roof
+    top = []
+    for k, (kms, kl, kb) in sorted(kt.items(), key=lambda kv: -kv[1][0])[:8]:
+        pl_ms, pl_b = kms / max(kl, 1), kb / max(kl, 1)
+        ach = pl_b / max(pl_ms * 1e-3, 1e-12) / 1e9
+        e = {"kernel": k, "ms_per_step": kms / max(a.steps, 1), "launches_per_step": kl / max(a.steps, 1),
+             "algorithmic_bytes_per_launch": pl_b, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+             "traffic": tj[k]["traffic_bytes_per_launch"] if k in tj else None}
+        if k in tj:
+            e["traffic_over_algorithmic"] = e["traffic"] / max(pl_b, 1)
+        top.append(e)
+    roofline["kernels"] = top
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.spectrum_only and frags is None:

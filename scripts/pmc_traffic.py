@@ -17,55 +17,71 @@ import json
 import os
 import sys
 
-# HIP symbol prefix -> (bench timing label, read pattern)
-KERNELS = {
-    "void apg::k_sk_bucket<true, apg::SK24>": ("sk_bucket_solid", "stream"),
-    "void apg::k_sk_bucket<false, apg::SK16>": ("sk_bucket", "stream"),
-    "apg::k_sk_count": ("sk_count", "stream"),
-    "void apg::k_sk_scatter<apg::SK16>": ("sk_scatter", "stream"),
-    "void apg::k_sk_scatter<apg::SK24>": ("sk_scatter_sk24", "stream"),
-    "void apg::k_part_scatter<apg::SK16>": ("s_part_scatter", "stream"),
-    "void apg::k_part_scatter<apg::SK24>": ("s_part_scatter_sk24", "stream"),
-    "void apg::k_part_count<apg::SK16>": ("s_part_count", "stream"),
-    "apg::k_fill": ("fill", "random"),
-    "apg::k_fill_write": ("fill_write", "stream"),
-    "apg::k_pc_decide": ("precorrect", "random"),
-    "void apg::k_pc_candidates<true>": ("pc_candidates", "stream"),
-    "apg::k_usk_count": ("usk_count", "stream"),
-    "apg::k_usk_scatter": ("usk_scatter", "stream"),
-    "apg::k_usk_bucket": ("usk_bucket", "stream"),
-    "void apg::k_part_scatter<apg::SK48>": ("usk_part_scatter", "stream"),
-    "apg::k_links": ("u_links", "random"),
-    "apg::k_walk": ("u_walk", "random"),
-}
+# HIP symbol prefix -> (bench timing label, read pattern).  Several symbols may
+# share a label (one timed region launching two kernels): their traffic adds,
+# the label's launches are the most frequent symbol's.
+KERNELS = [
+    ("void apg::k_sk_bucket_dd<true, apg::SK24>", "sk_bucket_solid", "stream"),
+    ("void apg::k_sk_bucket<true, apg::SK24>", "sk_bucket_solid", "stream"),
+    ("void apg::k_sk_bucket<false, apg::SK16>", "sk_bucket", "stream"),
+    ("apg::k_sk_count", "sk_count", "stream"),
+    ("void apg::k_sk_scatter<apg::SK16*>", "sk_scatter", "stream"),
+    ("void apg::k_sk_scatter<apg::SK24*>", "sk_scatter", "stream"),
+    ("void apg::k_part_scatter<apg::SK16>", "s_part_scatter", "stream"),
+    ("void apg::k_part_scatter<apg::SK24>", "s24_part_scatter", "stream"),
+    ("void apg::k_part_count<apg::SK16>", "s_part_count", "stream"),
+    ("void apg::k_part_count<apg::SK24>", "s24_part_count", "stream"),
+    ("apg::k_fill(", "fill", "random"),
+    ("apg::k_fill_write", "fill_write", "stream"),
+    ("apg::k_pc_decide", "precorrect", "random"),
+    ("void apg::k_pc_candidates<true>", "pc_candidates", "stream"),
+    ("apg::k_usk_count", "usk_count", "stream"),
+    ("apg::k_usk_scatter", "usk_scatter", "stream"),
+    ("apg::k_usk_bucket", "usk_bucket", "stream"),
+    ("void apg::k_part_scatter<apg::SK48>", "usk_part_scatter", "stream"),
+    ("apg::k_links", "u_links", "random"),
+    ("apg::k_walk", "u_walk", "random"),
+]
 
 
 def load(path):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024.0)  # KB -> bytes
+        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]) * 1024.0)  # KB -> bytes
     return agg
+
+
+def matches(sym, prefix):
+    if prefix.endswith("("):
+        return sym.startswith(prefix)
+    base = sym.split("(")[0]
+    return base == prefix or (prefix.endswith(">") and base.startswith(prefix[:-1] + ","))
 
 
 def main(d):
     f = load(os.path.join(d, "fetch.csv"))
     w = load(os.path.join(d, "write.csv"))
     out = {}
-    for base, (label, pattern) in KERNELS.items():
-        # template kernels may carry extra arguments (k_sk_bucket<true, SK24, 512>)
-        hits = [k for k in f if k == base or (base.endswith(">") and k.startswith(base[:-1] + ","))]
-        if not hits:
-            continue
-        sym = hits[0]
-        fetch = sum(f[sym]) / len(f[sym])
-        write = sum(w.get(sym, [0.0])) / max(len(w.get(sym, [])), 1)
+    for prefix, label, pattern in KERNELS:
         corr = 2.0 if pattern == "stream" else 1.0
-        out[label] = {"symbol": sym, "pattern": pattern, "launches": len(f[sym]),
-                      "fetch_size_bytes": fetch, "fetch_correction": corr, "write_size_bytes": write,
-                      "traffic_bytes_per_launch": fetch * corr + write}
+        for sym in f:
+            if not matches(sym, prefix):
+                continue
+            e = out.setdefault(label, {"symbols": [], "pattern": pattern, "launches": 0, "fetch_size_bytes": 0.0,
+                                       "fetch_correction": corr, "write_size_bytes": 0.0})
+            e["symbols"].append(sym.split("(")[0])
+            e["launches"] = max(e["launches"], len(f[sym]))
+            e["fetch_size_bytes"] += sum(f[sym])
+            e["write_size_bytes"] += sum(w.get(sym, [0.0]))
+    for e in out.values():
+        n = max(e["launches"], 1)
+        e["fetch_size_bytes"] /= n
+        e["write_size_bytes"] /= n
+        e["traffic_bytes_per_launch"] = e["fetch_size_bytes"] * e["fetch_correction"] + e["write_size_bytes"]
     json.dump(out, open(os.path.join(d, "traffic.json"), "w"), indent=1)
     for k, v in out.items():
-        print(f"{k:16s} {v['traffic_bytes_per_launch'] / 1e9:9.2f} GB/launch ({v['pattern']})")
+        print(f"{k:18s} {v['traffic_bytes_per_launch'] / 1e9:9.2f} GB/launch ({v['pattern']}; "
+              f"fetch {v['fetch_size_bytes'] / 1e9:.2f} x{v['fetch_correction']:.0f}, write {v['write_size_bytes'] / 1e9:.2f})")
 
 
 if __name__ == "__main__":
