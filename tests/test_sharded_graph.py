@@ -61,8 +61,10 @@ def free_port() -> int:
     return p
 
 
-def worker(rank, world, port, name, q):
+def worker(rank, world, port, name, q, flush_round=None):
     sys.path.insert(0, ROOT)
+    if flush_round is not None:  # KmerPaths: the all-at-once last round from this round on
+        os.environ["APG_GRAPH_FLUSH_ROUND"] = str(flush_round)
     try:
         from allpathslg_amd import Context
         from allpathslg_amd.distributed import Comm, sharded_unipaths
@@ -81,11 +83,11 @@ def worker(rank, world, port, name, q):
         q.put((rank, None, repr(e)))
 
 
-def run_world(world, name):
+def run_world(world, name, flush_round=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=worker, args=(r, world, port, name, q)) for r in range(world)]
+    ps = [ctx.Process(target=worker, args=(r, world, port, name, q, flush_round)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
@@ -97,13 +99,16 @@ def run_world(world, name):
     return [r[1] for r in res]
 
 
-@pytest.mark.parametrize("name", ["circular", "circular_k31", "folded", "repeats", "noisy", "palindromes",
-                                  "repeat_genome"])
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_graph_equals_single_gpu(gpu_ctx, world, name):
+CASES = [(w, n, None) for w in (2, 4) for n in ("circular", "circular_k31", "folded", "repeats", "noisy",
+                                                 "palindromes", "repeat_genome")]
+CASES += [(2, "noisy", 1), (4, "repeat_genome", 2)]  # KmerPaths resolved by the flush round
+
+
+@pytest.mark.parametrize("world,name,flush_round", CASES)
+def test_sharded_graph_equals_single_gpu(gpu_ctx, world, name, flush_round):
     reads, K = case_reads(name)
     mono, mst = gpu_ctx.unipaths(reads, K)
-    parts = run_world(world, name)
+    parts = run_world(world, name, flush_round)
     for rank, (g, st, a, b) in enumerate(parts):
         for k in GRAPH_KEYS:
             x, y = g[k], mono[k]
