@@ -55,7 +55,7 @@ constexpr uint32_t kSkTab = 2048;          // LDS table slots (u64 canonical K-m
 constexpr int kSkHistBins = 128;  // LDS spectrum bins (counts above go to global atomics); keeps k_sk_bucket<false> under 40 KiB LDS = 4 blocks/CU
 constexpr uint32_t kSkSlotCap = 6144;  // weak pass: instances per bucket with a recorded slot (LDS: 3 blocks/CU)
 constexpr uint32_t kSkWaveSlots = kSkSlotCap / (kSkThreads / 64);  // recorded slots per wave
-constexpr int kSkMaxW = 17;  // w = K - m + 1 <= 17 for K <= 32
+constexpr int kSkListCap = 1024;  // parked records per tile (8 KiB of LDS)
 // A table this full is given up on: an insert that finds no room within
 // kSkProbeMax slots marks the bucket for the global table (a full 2048-slot
 // table otherwise costs every further insert a scan of all of it).
@@ -65,6 +65,7 @@ constexpr uint32_t kSkProbeMax = 256;
 constexpr uint32_t kSkHeavyRecords = 8192;
 
 struct SkP {
+  using U = uint32_t;  // m <= 16
   int K, m, w, maxnk;
   uint64_t mmask;  // 2m bits
   HashP hp;
@@ -104,13 +105,14 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
                                                          unsigned long long* __restrict__ kdig) {
   __shared__ SkTile<kSkThreads> T;
   __shared__ uint32_t hist[256], khist[256];
-  __shared__ uint32_t sbuf[kSkMaxW * kSkThreads];
+  __shared__ SkList<1> lst;  // f runs in place
+  extern __shared__ uint32_t sbuf[];  // p.w x kSkThreads van Herk columns
   const uint32_t ndig = 1u << D;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key) {
+  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key, uint32_t) {
     const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
     atomicAdd(&hist[d], 1u);
     atomicAdd(&khist[d], n);
@@ -118,9 +120,9 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n)
-      sk_walk<kSkThreads, false>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+      sk_walk_tile<kSkThreads, false, false>(p, T, n, sbuf + threadIdx.x, lst, f);
     else
-      sk_walk<kSkThreads, true>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+      sk_walk_global<kSkThreads, false>(rv, p, T, t0, sbuf + threadIdx.x, f);
     __syncthreads();
     t0 += n ? n : 1;
   }
@@ -160,28 +162,27 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
                                                            const uint64_t* __restrict__ omat, O out) {
   __shared__ SkTile<kSkThreads> T;
   __shared__ unsigned long long cur[256];
-  __shared__ uint32_t sbuf[kSkMaxW * kSkThreads];
+  __shared__ SkList<kSkListCap> lst;
+  extern __shared__ uint32_t sbuf[];  // p.w x kSkThreads van Herk columns
   const uint32_t ndig = 1u << D;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
+  if (threadIdx.x == 0) lst.cnt = 0;
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  uint64_t rbase = 0;  // base offset of this thread's read (records with positions)
-  auto f = [&](const uint8_t* rd, uint32_t, uint32_t a, uint32_t n, uint32_t key) {
+  uint64_t t0 = r0;
+  auto f = [&](const uint8_t* rd, uint32_t, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
     const SK16 x = make_rec(rd, a, n, key, p.K);
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
-    rec_put(out, atomicAdd(&cur[d], 1ull), x, rbase + a);
+    const uint64_t pos = OutWantsPos<O>::value ? rv.base_off[t0 + q] + a : 0;  // the read's first base + a
+    rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
   };
-  for (uint64_t t0 = r0; t0 < r1;) {
+  while (t0 < r1) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
-    if constexpr (OutWantsPos<O>::value) {  // once per read, not per record
-      const uint64_t r = t0 + (n ? threadIdx.x : 0);
-      rbase = (n ? threadIdx.x < n : threadIdx.x == 0) ? rv.base_off[r] : 0;
-    }
     if (n)
-      sk_walk<kSkThreads, false>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+      sk_walk_tile<kSkThreads, false, true>(p, T, n, sbuf + threadIdx.x, lst, f);
     else
-      sk_walk<kSkThreads, true>(rv, p, T, t0, n, sbuf + threadIdx.x, f);
+      sk_walk_global<kSkThreads, false>(rv, p, T, t0, sbuf + threadIdx.x, f);
     __syncthreads();
     t0 += n ? n : 1;
   }
@@ -998,7 +999,7 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   if (!dr->n_reads) APG_CHECK_HIP(hipMemsetAsync(cmat, 0, (uint64_t)ndig * G * 4, ctx->stream));
   kbegin(ctx, "sk_count", dr->n_bytes + 16 * dr->n_reads);
   if (dr->n_reads)
-    k_sk_count<<<G, kSkThreads, 0, ctx->stream>>>(rv, p, D, cmat, kdig);
+    k_sk_count<<<G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, cmat, kdig);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "sk"));
@@ -1033,7 +1034,7 @@ static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out,
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)(1u << D) * s.G + 1, &omat));
   kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * out_bytes);
-  if (dr->n_reads) k_sk_scatter<O><<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out);
+  if (dr->n_reads) k_sk_scatter<O><<<s.G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, omat, out);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;

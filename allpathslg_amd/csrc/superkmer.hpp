@@ -52,6 +52,8 @@ __device__ __forceinline__ uint32_t mmer_order(uint64_t c) {  // c < 4^20
   return sk_fmix32(((uint32_t)c ^ 0x2545f491u) ^ ((uint32_t)(c >> 32) * 0x9e3779b1u));
 }
 __device__ __forceinline__ uint32_t part_key(uint32_t v) { return sk_fmix32(v ^ 0x6b43a9b5u); }
+// mmer_order of an m-mer with m <= 16 (c < 2^32: the high word's term is 0).
+__device__ __forceinline__ uint32_t mmer_order32(uint32_t c) { return sk_fmix32(c ^ 0x2545f491u); }
 
 struct SkReads {
   const uint64_t* base_off;
@@ -66,34 +68,39 @@ __device__ __forceinline__ void sk_read_range(uint64_t n, uint32_t G, uint32_t b
 }
 
 // A tile: up to NT consecutive reads whose packed bytes (plus the
-// 12-byte window overrun) fit kSkTileBytes, copied into LDS with one
-// coalesced pass so the walk below never waits on HBM.  A read too long for
-// a tile is walked from global memory on its own.
+// 12-byte window overrun) fit BYTES, copied into LDS with one coalesced pass
+// so the walk below never waits on HBM.  A read too long for a tile is
+// walked from global memory on its own.
 constexpr uint32_t kSkTileBytes = 8192;
-template <int NT>
+template <int NT, uint32_t BYTES = kSkTileBytes>
 struct SkTile {
-  uint32_t words[kSkTileBytes / 4];
+  static constexpr uint32_t kBytes = BYTES;
+  uint32_t words[BYTES / 4];
   uint32_t rlen[NT];
   uint32_t rbo[NT];  // byte offset of the read in `words`
+  uint32_t lmax;     // longest read of the tile (block-uniform walk bound)
 };
 
 // Loads the tile starting at read t0 (< r1); returns its read count, or 0
 // when read t0 alone exceeds a tile.  Block-uniform; ends with a barrier.
-template <int NT>
-__device__ __forceinline__ uint32_t sk_load_tile(const SkReads& rv, uint64_t t0, uint64_t r1, SkTile<NT>& T) {
+template <int NT, uint32_t BYTES>
+__device__ __forceinline__ uint32_t sk_load_tile(const SkReads& rv, uint64_t t0, uint64_t r1, SkTile<NT, BYTES>& T) {
   const uint32_t tid = threadIdx.x;
   const uint64_t b0 = rv.byte_off[t0] & ~3ull;
   const uint64_t r = t0 + tid;
   bool fits = false;
+  uint32_t len = 0;
+  if (tid == 0) T.lmax = 0;
   if (r < r1) {
-    const uint32_t len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
+    len = (uint32_t)(rv.base_off[r + 1] - rv.base_off[r]);
     const uint64_t bo = rv.byte_off[r] - b0;
-    fits = bo + (len + 3) / 4 + 12 <= kSkTileBytes;
+    fits = bo + (len + 3) / 4 + 12 <= BYTES;
     T.rlen[tid] = len;
     T.rbo[tid] = (uint32_t)bo;
   }
   const uint32_t n = (uint32_t)__syncthreads_count(fits);
   if (n) {
+    if (tid < n) atomicMax(&T.lmax, len);
     const uint32_t nw = (T.rbo[n - 1] + (T.rlen[n - 1] + 3) / 4 + 12 + 3) / 4;
     const uint32_t* g = reinterpret_cast<const uint32_t*>(rv.packed + b0);
     for (uint32_t i = tid; i < nw; i += NT) T.words[i] = g[i];
@@ -102,39 +109,113 @@ __device__ __forceinline__ uint32_t sk_load_tile(const SkReads& rv, uint64_t t0,
   return n;
 }
 
-// One thread per read of the tile (a GLOBAL tile: thread 0 walks the one long
-// read from HBM).  The read is rolled base by base (fw / rc m-mer, order of
+// Base accessors: the 16 bases [x, x+16) of a read as 32 bits, LSB-first —
+// from an LDS tile (two aligned words and one v_alignbit) or from HBM.
+template <uint32_t NWORDS>
+struct SkLdsBases {
+  const uint32_t* W;
+  uint32_t bit0;  // the read's first bit in W
+  __device__ __forceinline__ uint32_t at(uint32_t x) const {
+    const uint32_t bo = bit0 + 2 * x;
+    const uint32_t i = min(bo >> 5, NWORDS - 2);  // prefetches past the tile read stale words, never past W
+    return __builtin_amdgcn_alignbit(W[i + 1], W[i], bo & 31);
+  }
+};
+struct SkGlobalBases {
+  const uint8_t* rd;
+  __device__ __forceinline__ uint32_t at(uint32_t x) const { return (uint32_t)sk_lsb64(rd, x); }
+};
+
+// The walk of one read: rolled base by base (fw / rc m-mer, m <= 16, order of
 // the canonical one); the minimum of each window of w orders comes from the
 // van Herk / Gil-Werman block scheme — orders are taken in blocks of w, the
 // finished block is turned into suffix minima in this thread's LDS column
-// (sb[t * NT], conflict-free), and window [i, i+w-1] = min(suffix of
-// block k-1 from i, prefix of block k up to i+w-1) — so every lane does the
-// same work per base with no rescans.  f(rd, L, a, n, key) per record: K-mers
-// [a, a+n) sharing minimizer order `key`, n <= maxnk.
-// P: any parameter struct with K, m, w, maxnk, mmask (2m-bit mask).
-template <int NT, bool GLOBAL, typename P, typename F>
-__device__ __forceinline__ void sk_walk(const SkReads& rv, const P& p, const SkTile<NT>& T, uint64_t t0, uint32_t n,
-                                        uint32_t* sb, F f) {
-  const uint32_t q = threadIdx.x;
-  if (q >= (GLOBAL ? 1u : n)) return;
-  const uint32_t L = T.rlen[q];
-  if (L < (uint32_t)p.K) return;
-  const uint8_t* rd = GLOBAL ? rv.packed + rv.byte_off[t0] : reinterpret_cast<const uint8_t*>(T.words) + T.rbo[q];
-  const uint32_t w = (uint32_t)p.w, m = (uint32_t)p.m, maxnk = (uint32_t)p.maxnk;
-  const int rsh = 2 * p.m - 2;
-  uint64_t fw = 0, rc = 0;
-  uint32_t byte = 0, pre = 0, t = 0, key = 0, ra = 0, rn = 0;
-  for (uint32_t j = 0; j < L; ++j) {  // base j
-    if ((j & 3) == 0) byte = rd[j >> 2];
-    const uint64_t b = (byte >> (2 * (j & 3))) & 3;
-    fw = ((fw << 2) | b) & p.mmask;
-    rc = (rc >> 2) | ((3 - b) << rsh);
-    if (j + 1 < m) continue;
-    const uint32_t v = mmer_order(fw < rc ? fw : rc);  // m-mer x = j + 1 - m, offset t in its block
-    pre = t == 0 ? v : min(pre, v);
-    const uint32_t suf = t + 1 < w ? sb[(t + 1) * NT] : 0xffffffffu;
-    sb[t * NT] = v;
+// (sb[t * NT], conflict-free), and window [i, i+w-1] = min(suffix of block
+// k-1 from i, prefix of block k up to i+w-1) — so every lane does the same
+// work per base with no rescans.  A record is a run of K-mers [a, a+n) that
+// share minimizer order `key`, n <= maxnk.
+//
+// TWO (long windows, the K = 96 walk: w = 81): a two-level column.  The
+// finished block keeps only its coarse suffix minima per segment of SB
+// m-mers (CS); the segment the window's left edge is in gets its fine suffix
+// minima recomputed from the read's bases when the edge enters it (FS: SB
+// orders re-hashed once per SB steps); the current block keeps its running
+// segment minima (SM) and prefix minimum.  Per thread 2 ceil(w/SB) + 1 + SB
+// column words instead of w (31 for w = 81, SB = 8).
+// Column layout at sb (stride NT): SM[0, NS) | CS[0, NS] | FS[0, SB).
+// P: any parameter struct with K, m <= 16, w, maxnk, mmask (2m-bit mask).
+constexpr int kSkSeg = 8;
+__host__ __device__ constexpr int sk_walk2_words(int w) { return 2 * ((w + kSkSeg - 1) / kSkSeg) + 1 + kSkSeg; }
+
+// U: the m-mer register type — uint32_t for m <= 16 (P::U), uint64_t up to 31.
+template <typename U>
+__device__ __forceinline__ uint32_t sk_order(U c) {
+  if constexpr (sizeof(U) == 4)
+    return mmer_order32(c);
+  else
+    return mmer_order(c);
+}
+
+template <int NT, bool TWO, typename B, typename U>
+struct SkWalker {
+  uint32_t w, m, maxnk, rsh, NS;
+  U mmask;
+  uint32_t* sb;
+  B bases;
+  U fw = 0, rc = 0;
+  uint32_t pre = 0, t = 0, key = 0, ra = 0, rn = 0, segmin = 0, blk0 = 0;
+
+  template <typename P>
+  __device__ __forceinline__ SkWalker(const P& p, uint32_t* col, B b)
+      : w((uint32_t)p.w), m((uint32_t)p.m), maxnk((uint32_t)p.maxnk), rsh(2 * (uint32_t)p.m - 2),
+        NS(((uint32_t)p.w + kSkSeg - 1) / kSkSeg), mmask((U)p.mmask), sb(col), bases(b) {}
+
+  // canonical order of the m-mer at base x, from the bases
+  __device__ __forceinline__ uint32_t order_at(uint32_t x) const {
+    if constexpr (sizeof(U) == 4) {
+      const uint32_t Wm = bases.at(x);
+      return mmer_order32(min(sk_rev2_32(Wm) >> (32 - 2 * m), ~Wm & mmask));
+    } else {
+      const uint64_t Wm = (uint64_t)bases.at(x) | ((uint64_t)bases.at(x + 16) << 32);
+      const uint64_t f2 = sk_rev2(Wm) >> (64 - 2 * m), r2 = ~Wm & mmask;
+      return mmer_order(f2 < r2 ? f2 : r2);
+    }
+  }
+
+  // Base j (value b); true when a record closed: K-mers [oa, oa + on), key ok.
+  __device__ __forceinline__ bool step(uint32_t j, uint32_t b, uint32_t& oa, uint32_t& on, uint32_t& ok) {
+    fw = ((fw << 2) | (U)b) & mmask;
+    rc = (rc >> 2) | ((U)(3 - b) << rsh);
+    if (j + 1 < m) return false;
+    const uint32_t v = sk_order<U>(fw < rc ? fw : rc);  // m-mer x = j + 1 - m, offset t in its block
     const uint32_t x = j + 1 - m;
+    pre = t == 0 ? v : min(pre, v);
+    uint32_t suf = 0xffffffffu;
+    if constexpr (TWO) {
+      uint32_t* SM = sb;
+      uint32_t* CS = sb + NS * NT;
+      uint32_t* FS = sb + (2 * NS + 1) * NT;
+      segmin = (t % kSkSeg) == 0 ? v : min(segmin, v);
+      if ((t % kSkSeg) == kSkSeg - 1 || t + 1 == w) SM[(t / kSkSeg) * NT] = segmin;
+      const uint32_t u = t + 1;
+      if (x + 1 >= w && u < w) {  // the previous block's suffix from u
+        const uint32_t sg = u / kSkSeg, uo = u % kSkSeg;
+        if (uo == 0 || t == 0) {  // the edge entered segment sg: its fine suffix minima, re-hashed
+          const uint32_t lo = sg * kSkSeg, ne = min(lo + (uint32_t)kSkSeg, w) - lo;
+          const uint32_t pb = blk0 - w + lo;  // base (= m-mer index) of the segment's first m-mer
+          uint32_t r = 0xffffffffu;
+          for (uint32_t e = ne; e-- > 0;) {
+            r = min(r, order_at(pb + e));
+            FS[e * NT] = r;
+          }
+        }
+        suf = min(FS[uo * NT], CS[(sg + 1) * NT]);
+      }
+    } else {
+      if (t + 1 < w) suf = sb[(t + 1) * NT];
+      sb[t * NT] = v;
+    }
+    bool closed = false;
     if (x + 1 >= w) {  // K-mer i = x + 1 - w
       const uint32_t kk = min(suf, pre);
       if (x + 1 == w) {
@@ -144,18 +225,112 @@ __device__ __forceinline__ void sk_walk(const SkReads& rv, const P& p, const SkT
       } else if (kk == key && rn < maxnk) {
         ++rn;
       } else {
-        f(rd, L, ra, rn, key);
+        oa = ra;
+        on = rn;
+        ok = key;
+        closed = true;
         key = kk;
         ra = x + 1 - w;
         rn = 1;
       }
     }
-    if (++t == w) {  // block done: suffix minima in place
-      for (int u = (int)w - 2; u >= 0; --u) sb[u * NT] = min(sb[u * NT], sb[(u + 1) * NT]);
+    if (++t == w) {  // block done
+      if constexpr (TWO) {  // its coarse suffix minima
+        uint32_t* SM = sb;
+        uint32_t* CS = sb + NS * NT;
+        CS[NS * NT] = 0xffffffffu;
+        for (int g = (int)NS - 1; g >= 0; --g) CS[g * NT] = min(SM[g * NT], CS[(g + 1) * NT]);
+        blk0 += w;
+      } else {  // suffix minima in place
+        for (int u = (int)w - 2; u >= 0; --u) sb[u * NT] = min(sb[u * NT], sb[(u + 1) * NT]);
+      }
       t = 0;
     }
+    return closed;
   }
-  f(rd, L, ra, rn, key);
+};
+
+// A read too long for a tile: thread 0 walks it from HBM and hands each
+// record straight to f(rd, L, a, n, key, q = 0).
+template <int NT, bool TWO, typename P, typename TT, typename F>
+__device__ __forceinline__ void sk_walk_global(const SkReads& rv, const P& p, const TT& T, uint64_t t0, uint32_t* sb,
+                                               F f) {
+  if (threadIdx.x != 0) return;
+  const uint32_t L = T.rlen[0];
+  if (L < (uint32_t)p.K) return;
+  const uint8_t* rd = rv.packed + rv.byte_off[t0];
+  SkWalker<NT, TWO, SkGlobalBases, typename P::U> W(p, sb, SkGlobalBases{rd});
+  uint32_t word = 0, a, n, k;
+  for (uint32_t j = 0; j < L; ++j) {
+    if ((j & 15) == 0) word = W.bases.at(j);
+    if (W.step(j, (word >> (2 * (j & 15))) & 3, a, n, k)) f(rd, L, a, n, k, 0u);
+  }
+  f(rd, L, W.ra, W.rn, W.key, 0u);
+}
+
+// Records of a tile, parked in LDS as they close and handed to f in
+// lane-parallel passes (a record closes on a few lanes per base: called in
+// place, f would run once per closing base with most of the wave idle).
+// Descriptor: key | a << 32 | n << 48 | q << 56 (q = the read's lane).
+template <int CAP>
+struct SkList {
+  uint32_t cnt;
+  uint64_t d[CAP];
+};
+constexpr uint32_t kSkChunk = 16;  // bases per walk chunk (one prefetched word)
+
+// Every thread of the block walks the tile's read q = threadIdx.x (if any)
+// in chunks of kSkChunk bases.  LIST: between chunks the block drains the
+// list when it is half full (and after the last chunk) — for an f that is
+// costly per call (building and storing a record); otherwise f runs in place
+// (a pair of LDS atomics).  f(rd, L, a, n, key, q) per record, in no
+// particular order.  Block-uniform.
+template <int NT, bool TWO, bool LIST, typename P, typename TT, int CAP, typename F>
+__device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n, uint32_t* sb, SkList<CAP>& lst,
+                                             F f) {
+  const uint32_t q = threadIdx.x;
+  const uint32_t L = q < n ? T.rlen[q] : 0;
+  const uint32_t Lw = L >= (uint32_t)p.K ? L : 0;  // bases this thread walks
+  using LB = SkLdsBases<TT::kBytes / 4>;
+  SkWalker<NT, TWO, LB, typename P::U> W(p, sb, LB{T.words, (q < n ? T.rbo[q] : 0u) * 8});
+  auto emit = [&](uint64_t d) {
+    const uint32_t r = (uint32_t)(d >> 56);
+    f(reinterpret_cast<const uint8_t*>(T.words) + T.rbo[r], T.rlen[r], (uint32_t)(d >> 32) & 0xffffu,
+      (uint32_t)(d >> 48) & 0xffu, (uint32_t)d, r);
+  };
+  auto push = [&](uint32_t a, uint32_t nk, uint32_t key) {
+    const uint64_t d = (uint64_t)key | ((uint64_t)a << 32) | ((uint64_t)nk << 48) | ((uint64_t)q << 56);
+    if constexpr (!LIST) {
+      emit(d);
+      return;
+    }
+    const uint32_t i = atomicAdd(&lst.cnt, 1u);
+    if (i < (uint32_t)CAP)
+      lst.d[i] = d;
+    else
+      emit(d);  // list full: this record alone, in place
+  };
+  const uint32_t Lmax = T.lmax;
+  uint32_t nxt = Lw ? W.bases.at(0) : 0;
+  for (uint32_t c0 = 0; c0 < Lmax; c0 += kSkChunk) {
+    const uint32_t cur = nxt;
+    if (c0 + kSkChunk < Lw) nxt = W.bases.at(c0 + kSkChunk);  // in flight during this chunk
+    const uint32_t c1 = min(c0 + kSkChunk, Lw);
+    uint32_t a, nk, k;
+    for (uint32_t j = c0; j < c1; ++j)
+      if (W.step(j, (cur >> (2 * (j - c0))) & 3, a, nk, k)) push(a, nk, k);
+    if (c0 < Lw && Lw <= c0 + kSkChunk) push(W.ra, W.rn, W.key);  // the read's last record
+    if constexpr (!LIST) continue;
+    __syncthreads();
+    const bool last = c0 + kSkChunk >= Lmax;
+    if (__syncthreads_count(q == 0 && lst.cnt >= (uint32_t)CAP / 2) || last) {
+      const uint32_t m = min(lst.cnt, (uint32_t)CAP);
+      for (uint32_t i = q; i < m; i += NT) emit(lst.d[i]);
+      __syncthreads();
+      if (q == 0) lst.cnt = 0;
+      __syncthreads();
+    }
+  }
 }
 
 }  // namespace apg

@@ -1204,15 +1204,29 @@ __global__ void k_read_paths(ReadsV rv, NodeIdx ni, KeyP kp, const uint32_t* __r
 constexpr int kUskThreads = 128;   // walk workgroups: van Herk columns w x 128 x 4 B of LDS
 constexpr int kUskMaxBlocks = 4096;
 constexpr int kUskBases = 160;     // bases per record
-constexpr int kUskMaxW = 66;       // w = K - m + 1
+constexpr int kUskMaxW = 112;      // w = K - m + 1
 constexpr int kUskMaxNk = 63;
 constexpr int kUskDigitBits = 5;
 constexpr uint64_t kUskBucketKmers = 2048;
 constexpr uint32_t kUskTab = 1024;  // LDS table slots: tag u32, key 3 x u64, ext u32
 constexpr int kUskChunk = 128;      // records flattened per round
 constexpr int kUskBThreads = 256;
+constexpr int kUskWalk2MinW = 24;  // windows longer than this walk with sk_walk2 (a third of the LDS column)
+
+constexpr int kUskListCap = 256;   // parked records per tile (2 KiB of LDS)
+using UskTile = SkTile<kUskThreads, 6144>;  // 128 fragments of <= ~180 bases
+
+// dynamic LDS of the walk kernels: the van Herk column of each thread, then
+// the per-digit counters
+__host__ __device__ inline uint32_t usk_column_words(int w) {
+  return (uint32_t)(w > kUskWalk2MinW ? sk_walk2_words(w) : w) * kUskThreads;
+}
+static size_t usk_walk_lds(int w, int D, size_t per_digit) {
+  return (size_t)usk_column_words(w) * 4 + ((size_t)1 << D) * per_digit;
+}
 
 struct UskP {
+  using U = uint64_t;  // m <= 31
   int K, m, w, maxnk;
   uint64_t mmask;
 };
@@ -1243,31 +1257,49 @@ __device__ __forceinline__ SK48 make_urec(const uint8_t* rd, uint32_t L, uint32_
   return r;
 }
 
+// The block's reads [r0, r1), tile by tile: the single-level column for short
+// windows, the two-level one (sk_walk2_words) for long.
+template <bool LIST, int CAP, typename F>
+__device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p, uint64_t r0, uint64_t r1, UskTile& T,
+                                               uint32_t* sb, SkList<CAP>& lst, F f) {
+  const bool two = p.w > kUskWalk2MinW;
+  for (uint64_t t0 = r0; t0 < r1;) {
+    const uint32_t n = sk_load_tile(rv, t0, r1, T);
+    if (n) {
+      if (two)
+        sk_walk_tile<kUskThreads, true, LIST>(p, T, n, sb, lst, f);
+      else
+        sk_walk_tile<kUskThreads, false, LIST>(p, T, n, sb, lst, f);
+    } else if (two) {
+      sk_walk_global<kUskThreads, true>(rv, p, T, t0, sb, f);
+    } else {
+      sk_walk_global<kUskThreads, false>(rv, p, T, t0, sb, f);
+    }
+    __syncthreads();
+    t0 += n ? n : 1;
+  }
+}
+
 // Per-(digit, block) record counts and per-digit K-mer counts.
 __global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, int D, uint32_t* __restrict__ cmat,
                                                            unsigned long long* __restrict__ kdig) {
-  __shared__ SkTile<kUskThreads> T;
-  __shared__ uint32_t hist[256], khist[256];
-  extern __shared__ uint32_t usk_sb[];
+  __shared__ UskTile T;
+  __shared__ SkList<1> lst;  // f runs in place
+  extern __shared__ uint32_t usk_sb[];  // the walk columns, then hist[ndig], khist[ndig]
   const uint32_t ndig = 1u << D;
+  uint32_t* hist = usk_sb + usk_column_words(p.w);
+  uint32_t* khist = hist + ndig;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
+  if (threadIdx.x == 0) lst.cnt = 0;
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key) {
+  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key, uint32_t) {
     const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
     atomicAdd(&hist[d], 1u);
     atomicAdd(&khist[d], n);
   };
-  for (uint64_t t0 = r0; t0 < r1;) {
-    const uint32_t n = sk_load_tile<kUskThreads>(rv, t0, r1, T);
-    if (n)
-      sk_walk<kUskThreads, false>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
-    else
-      sk_walk<kUskThreads, true>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
-    __syncthreads();
-    t0 += n ? n : 1;
-  }
+  usk_walk_tiles<false>(rv, p, r0, r1, T, usk_sb + threadIdx.x, lst, f);
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) {
     cmat[(uint64_t)i * G + b] = hist[i];
     if (khist[i]) atomicAdd(&kdig[i], (unsigned long long)khist[i]);
@@ -1276,28 +1308,22 @@ __global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, i
 
 __global__ void __launch_bounds__(kUskThreads) k_usk_scatter(SkReads rv, UskP p, int D,
                                                              const uint64_t* __restrict__ omat, SK48* __restrict__ out) {
-  __shared__ SkTile<kUskThreads> T;
-  __shared__ unsigned long long cur[256];
-  extern __shared__ uint32_t usk_sb[];
+  __shared__ UskTile T;
+  __shared__ SkList<kUskListCap> lst;
+  extern __shared__ uint32_t usk_sb[];  // the walk columns, then cur[ndig]
   const uint32_t ndig = 1u << D;
+  unsigned long long* cur = reinterpret_cast<unsigned long long*>(usk_sb + usk_column_words(p.w));
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
+  if (threadIdx.x == 0) lst.cnt = 0;
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  auto f = [&](const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key) {
+  auto f = [&](const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key, uint32_t) {
     const SK48 x = make_urec(rd, L, a, n, key, p.K);
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
     out[atomicAdd(&cur[d], 1ull)] = x;
   };
-  for (uint64_t t0 = r0; t0 < r1;) {
-    const uint32_t n = sk_load_tile<kUskThreads>(rv, t0, r1, T);
-    if (n)
-      sk_walk<kUskThreads, false>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
-    else
-      sk_walk<kUskThreads, true>(rv, p, T, t0, n, usk_sb + threadIdx.x, f);
-    __syncthreads();
-    t0 += n ? n : 1;
-  }
+  usk_walk_tiles<true>(rv, p, r0, r1, T, usk_sb + threadIdx.x, lst, f);
 }
 
 __global__ void k_usk_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig, uint32_t G,
@@ -1950,7 +1976,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   const uint32_t G =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUskMaxBlocks, (dr->n_reads + kUskThreads - 1) / kUskThreads));
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  const size_t sb_bytes = (size_t)p.w * kUskThreads * 4;
+  const size_t sb_bytes = usk_walk_lds(p.w, D, 8);  // + hist, khist (count) or cursors (scatter)
   uint32_t* cmat = nullptr;
   uint64_t *omat = nullptr, *ds = nullptr;
   unsigned long long* kdig = nullptr;
@@ -1985,7 +2011,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
 static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, uint32_t G, SK48* out) {
   const int D = ceil_log2_u((uint64_t)P) + kUskDigitBits;
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  const size_t sb_bytes = (size_t)p.w * kUskThreads * 4;
+  const size_t sb_bytes = usk_walk_lds(p.w, D, 8);  // + hist, khist (count) or cursors (scatter)
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "usk_omat", (uint64_t)(1u << D) * G + 1, &omat));
   kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + ctx->urstate.n * sizeof(SK48));
