@@ -100,9 +100,18 @@ struct Chunk {
   uint32_t parent;  // parent group
 };
 
+// Scatter tile: 60 KiB of LDS (2 workgroups per CU).  A tile puts ~tile /
+// 2^bits records in each child run; runs shorter than a few 128-byte L2 lines
+// leave partial lines that the next tile of the same chunk completes only if
+// the line is still in L2 — with 256 children per workgroup and 4 resident
+// workgroups per CU the open lines (32 MiB) overflowed the L2s and the PMC
+// passes showed ~2.3x the algorithmic write + read bytes for SK24
+// (profiles/r02_v5/pmc).  Twice the tile and half the residency: runs twice
+// as long, a quarter of the open lines.
+constexpr int kPartTileBytes = 61440;
 template <typename R>
 struct PartGeom {
-  static constexpr int items = (32768 / (int)sizeof(R)) / kPartThreads;  // 32 KiB LDS tile
+  static constexpr int items = (kPartTileBytes / (int)sizeof(R)) / kPartThreads;
   static constexpr int tile = items * kPartThreads;
 };
 
@@ -162,15 +171,25 @@ __global__ void __launch_bounds__(kPartThreads* kScanGroups) k_part_scan(const u
   if (g == 0 && col) child[(uint64_t)p * ndig + d] = pstart[p] + ex;
 }
 
+// The partition key of a record from its first 64-bit word (rkey).
 template <typename R>
-__global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restrict__ rec,
-                                                               const Chunk* __restrict__ ch, int shift, uint32_t ndig,
-                                                               const uint32_t* __restrict__ pre,
-                                                               const uint64_t* __restrict__ child,
-                                                               R* __restrict__ out) {
+__device__ __forceinline__ uint64_t rkey_w0(uint64_t w0) {
+  if constexpr (sizeof(R) == 8)
+    return w0;
+  else
+    return w0 << 32;  // SK16 / SK24 / SK48: the minimizer key
+}
+
+template <typename R>
+__global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_part_scatter(
+    const R* __restrict__ rec, const Chunk* __restrict__ ch, int shift, uint32_t ndig,
+    const uint32_t* __restrict__ pre, const uint64_t* __restrict__ child, R* __restrict__ out) {
   constexpr int kPartItems = PartGeom<R>::items;
   constexpr int kTile = PartGeom<R>::tile;
-  __shared__ __attribute__((aligned(16))) R stage[kTile];
+  constexpr uint32_t kQ = sizeof(R) / 8;  // 64-bit words per record, held as words (no 24/48-byte
+                                          // aggregates in registers: those went to scratch)
+  static_assert(sizeof(R) % 8 == 0, "record size must be a multiple of 8 bytes");
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kTile * kQ];
   __shared__ unsigned long long cur[256];
   __shared__ uint32_t lcnt[256];
   __shared__ uint32_t lstart[256];
@@ -178,40 +197,37 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restri
   // Records whose size is not 8 or 16 bytes leave the tile as a word stream
   // (lane i -> word i of a digit run) so every store instruction covers
   // whole 64-byte lines; record-per-lane stores of 24/48-byte records write
-  // partial lines, which the PMC passes showed as ~2.3x write and read
-  // traffic (profiles/r01_pmc_v10).  sdig: digit of each staged record.
+  // partial lines (profiles/r01_pmc_v10).  sdig: digit of each staged record.
   constexpr bool kWords = sizeof(R) > 16;
   using W = std::conditional_t<sizeof(R) % 16 == 0, SK16, uint64_t>;
   constexpr uint32_t kWpr = sizeof(R) / sizeof(W);
-  static_assert(sizeof(R) % sizeof(W) == 0, "record size must be a multiple of the word");
   __shared__ uint8_t sdig[kWords ? kTile : 1];
   const Chunk c = ch[blockIdx.x];
   const uint32_t tid = threadIdx.x;
   const uint64_t dmask = ndig - 1;
   if (tid < ndig) cur[tid] = child[(uint64_t)c.parent * ndig + tid] + pre[(uint64_t)blockIdx.x * ndig + tid];
-  const R* base = rec + c.start;
-  R v[kPartItems], vn[kPartItems];
-#pragma unroll
-  for (int i = 0; i < kPartItems; ++i) {
-    const uint32_t idx = i * kPartThreads + tid;
-    if (idx < c.len) v[i] = base[idx];
-  }
-  for (uint32_t t0 = 0; t0 < c.len; t0 += kTile) {
-    const uint32_t tn = min((uint32_t)kTile, c.len - t0);
-    // prefetch the next tile: its loads stay in flight through this tile's work
-    const uint32_t t1 = t0 + kTile;
+  const uint64_t* base = reinterpret_cast<const uint64_t*>(rec + c.start);
+  uint64_t v[kPartItems][kQ];
+  auto load = [&](uint32_t t) {  // tile starting at record t
 #pragma unroll
     for (int i = 0; i < kPartItems; ++i) {
-      const uint32_t idx = i * kPartThreads + tid;
-      if (t1 + idx < c.len) vn[i] = base[t1 + idx];
+      const uint32_t idx = t + i * kPartThreads + tid;
+      if (idx < c.len) {
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; ++q) v[i][q] = base[(uint64_t)idx * kQ + q];
+      }
     }
+  };
+  load(0);
+  for (uint32_t t0 = 0; t0 < c.len; t0 += kTile) {
+    const uint32_t tn = min((uint32_t)kTile, c.len - t0);
     lcnt[tid] = 0;
     __syncthreads();
     uint32_t pos[kPartItems];
 #pragma unroll
     for (int i = 0; i < kPartItems; ++i) {
       const uint32_t idx = i * kPartThreads + tid;
-      if (idx < tn) pos[i] = atomicAdd(&lcnt[(rkey(v[i]) >> shift) & dmask], 1u);
+      if (idx < tn) pos[i] = atomicAdd(&lcnt[(rkey_w0<R>(v[i][0]) >> shift) & dmask], 1u);
     }
     __syncthreads();
     uint32_t tot;
@@ -222,12 +238,15 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restri
     for (int i = 0; i < kPartItems; ++i) {
       const uint32_t idx = i * kPartThreads + tid;
       if (idx < tn) {
-        const uint32_t d = (uint32_t)((rkey(v[i]) >> shift) & dmask);
-        stage[lstart[d] + pos[i]] = v[i];
-        if constexpr (kWords) sdig[lstart[d] + pos[i]] = (uint8_t)d;
+        const uint32_t d = (uint32_t)((rkey_w0<R>(v[i][0]) >> shift) & dmask);
+        const uint32_t sl = lstart[d] + pos[i];
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; ++q) stage[sl * kQ + q] = v[i][q];
+        if constexpr (kWords) sdig[sl] = (uint8_t)d;
       }
     }
     __syncthreads();
+    load(t0 + kTile);  // the next tile's loads: in flight while this tile leaves LDS
     if constexpr (kWords) {
       const W* sw = reinterpret_cast<const W*>(stage);
       W* ow = reinterpret_cast<W*>(out);
@@ -237,16 +256,15 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(const R* __restri
         ow[(cur[d] + (r - lstart[d])) * kWpr + k] = sw[i];
       }
     } else {
+      const R* sr = reinterpret_cast<const R*>(stage);
       for (uint32_t i = tid; i < tn; i += kPartThreads) {
-        const R x = stage[i];
+        const R x = sr[i];
         const uint32_t d = (uint32_t)((rkey(x) >> shift) & dmask);
         out[cur[d] + (i - lstart[d])] = x;
       }
     }
     __syncthreads();
     if (tid < ndig) cur[tid] += lcnt[tid];
-#pragma unroll
-    for (int i = 0; i < kPartItems; ++i) v[i] = vn[i];
   }
 }
 

@@ -47,7 +47,7 @@
 namespace apg {
 
 constexpr int kSkThreads = 256;
-constexpr int kSkMaxBlocks = 2048;
+constexpr int kSkMaxBlocks = 8192;
 constexpr int kSkBases = 40;
 constexpr int kSkDigitBits = 5;
 constexpr uint64_t kSkBucketKmers = 4096;  // K-mer instances per bucket the planner aims for
@@ -975,8 +975,16 @@ static int sk_ceil_log2(uint64_t x) {
   return b;
 }
 
-static uint32_t sk_blocks(uint64_t n_reads) {
-  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kSkMaxBlocks, (n_reads + 255) / 256));
+// Walk grid: two full rounds of the resident k_sk_scatter blocks (the
+// costlier of the pair; k_sk_count must use the same grid for the offsets),
+// so the last round is not a partial one.
+static uint32_t sk_blocks(const apg_ctx* ctx, uint64_t n_reads, const SkP& p) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sk_scatter<SK24*>, kSkThreads,
+                                                   (size_t)p.w * kSkThreads * 4) != hipSuccess || occ < 1)
+    occ = 4;
+  const uint64_t cap = std::min<uint64_t>(kSkMaxBlocks, (uint64_t)std::max(ctx->n_cu, 1) * occ * 2);
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, (n_reads + 255) / 256));
 }
 
 // Pass 1 over reads: per-digit record counts (host) and K-mer counts; leaves
@@ -986,7 +994,7 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   const SkP p = make_skp(K);
   const int D = sk_ceil_log2((uint64_t)P) + kSkDigitBits;
   const uint32_t ndig = 1u << D;
-  const uint32_t G = sk_blocks(dr->n_reads);
+  const uint32_t G = sk_blocks(ctx, dr->n_reads, p);
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   uint32_t* cmat = nullptr;
   uint64_t *omat = nullptr, *ds = nullptr;

@@ -310,6 +310,19 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
     else
       emit(d);  // list full: this record alone, in place
   };
+  if constexpr (!LIST) {  // no barriers: each lane walks its own read to its end
+    uint32_t cur = Lw ? W.bases.at(0) : 0, nxt = Lw > kSkChunk ? W.bases.at(kSkChunk) : 0;
+    uint32_t a, nk, k;
+    for (uint32_t j = 0; j < Lw; ++j) {
+      if ((j % kSkChunk) == 0 && j) {
+        cur = nxt;
+        if (j + kSkChunk < Lw) nxt = W.bases.at(j + kSkChunk);
+      }
+      if (W.step(j, (cur >> (2 * (j % kSkChunk))) & 3, a, nk, k)) push(a, nk, k);
+    }
+    if (Lw) push(W.ra, W.rn, W.key);
+    return;
+  }
   const uint32_t Lmax = T.lmax;
   uint32_t nxt = Lw ? W.bases.at(0) : 0;
   for (uint32_t c0 = 0; c0 < Lmax; c0 += kSkChunk) {
@@ -320,7 +333,6 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
     for (uint32_t j = c0; j < c1; ++j)
       if (W.step(j, (cur >> (2 * (j - c0))) & 3, a, nk, k)) push(a, nk, k);
     if (c0 < Lw && Lw <= c0 + kSkChunk) push(W.ra, W.rn, W.key);  // the read's last record
-    if constexpr (!LIST) continue;
     __syncthreads();
     const bool last = c0 + kSkChunk >= Lmax;
     if (__syncthreads_count(q == 0 && lst.cnt >= (uint32_t)CAP / 2) || last) {

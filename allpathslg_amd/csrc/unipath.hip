@@ -1202,7 +1202,7 @@ __global__ void k_read_paths(ReadsV rv, NodeIdx ni, KeyP kp, const uint32_t* __r
 // through the U2 table instead.
 // ---------------------------------------------------------------------------
 constexpr int kUskThreads = 128;   // walk workgroups: van Herk columns w x 128 x 4 B of LDS
-constexpr int kUskMaxBlocks = 4096;
+constexpr int kUskMaxBlocks = 8192;
 constexpr int kUskBases = 160;     // bases per record
 constexpr int kUskMaxW = 112;      // w = K - m + 1
 constexpr int kUskMaxNk = 63;
@@ -1965,6 +1965,16 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
 //   usk_scatter  the records, grouped by (shard, digit)
 //   usk_stage    partition levels of one shard's records (P source segments
 //                per digit) + LDS buckets -> distinct nodes in "usk_nodes"
+// Walk grid cap: two full rounds of resident k_usk_scatter blocks (see sk_blocks).
+static uint64_t usk_grid_cap(const apg_ctx* ctx, const UskP& p, int D) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_usk_scatter, kUskThreads, usk_walk_lds(p.w, D, 8)) !=
+          hipSuccess ||
+      occ < 1)
+    occ = 4;
+  return std::min<uint64_t>(kUskMaxBlocks, (uint64_t)std::max(ctx->n_cu, 1) * occ * 2);
+}
+
 static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, std::vector<uint64_t>* h,
                     std::vector<uint64_t>* kd, uint32_t* G_out) {
   if (p.w > kUskMaxW) {
@@ -1974,7 +1984,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   const int D = ceil_log2_u((uint64_t)P) + kUskDigitBits;
   const uint32_t ndig = 1u << D;
   const uint32_t G =
-      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kUskMaxBlocks, (dr->n_reads + kUskThreads - 1) / kUskThreads));
+      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(usk_grid_cap(ctx, p, D), (dr->n_reads + kUskThreads - 1) / kUskThreads));
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   const size_t sb_bytes = usk_walk_lds(p.w, D, 8);  // + hist, khist (count) or cursors (scatter)
   uint32_t* cmat = nullptr;
