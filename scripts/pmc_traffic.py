@@ -18,8 +18,10 @@ import os
 import sys
 
 # HIP symbol prefix -> (bench timing label, read pattern).  Several symbols may
-# share a label (one timed region launching two kernels): their traffic adds,
-# the label's launches are the most frequent symbol's.
+# share a label in two ways: one timed region launching two kernels (REGIONS:
+# their traffic adds, the label's launches are the most frequent symbol's), or
+# separate launches of template instantiations under one label (sk_scatter's
+# SK16 spectrum and SK24 solid-set launches: launches add too).
 KERNELS = [
     ("void apg::k_sk_bucket_dd<true, apg::SK24>", "sk_bucket_solid", "stream"),
     ("void apg::k_sk_bucket<true, apg::SK24>", "sk_bucket_solid", "stream"),
@@ -42,6 +44,9 @@ KERNELS = [
     ("apg::k_links", "u_links", "random"),
     ("apg::k_walk", "u_walk", "random"),
 ]
+
+
+REGIONS = {"sk_bucket_solid"}  # k_sk_bucket_dd + the hand-back k_sk_bucket in one timed region
 
 
 def load(path):
@@ -70,7 +75,7 @@ def main(d):
             e = out.setdefault(label, {"symbols": [], "pattern": pattern, "launches": 0, "fetch_size_bytes": 0.0,
                                        "fetch_correction": corr, "write_size_bytes": 0.0})
             e["symbols"].append(sym.split("(")[0])
-            e["launches"] = max(e["launches"], len(f[sym]))
+            e["launches"] = max(e["launches"], len(f[sym])) if label in REGIONS else e["launches"] + len(f[sym])
             e["fetch_size_bytes"] += sum(f[sym])
             e["write_size_bytes"] += sum(w.get(sym, [0.0]))
     for e in out.values():
