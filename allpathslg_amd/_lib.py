@@ -397,6 +397,7 @@ SIGNATURES = {
     "apg_fastb_read": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
     "apg_qualb_read": (C.c_int, [C.c_char_p, C.POINTER(apg_reads)]),
     "apg_reads_release": (None, [C.POINTER(apg_reads)]),
+    "apg_reads_load_dev": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
     "apg_kspec_write": (C.c_int, [C.c_char_p, C.c_int, _u64p, C.c_size_t]),
     "apg_graph_write": (C.c_int, [C.c_char_p, C.POINTER(apg_unipath_graph)]),
     "apg_graph_read": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(apg_unipath_graph)]),

@@ -223,12 +223,15 @@ int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_
   return APG_OK;
 }
 
-int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
-  APG_REQUIRE(ctx && r && out, "apg_reads_upload: NULL argument");
-  APG_REQUIRE(r->n_reads == 0 || (r->base_off && r->byte_off && r->packed),
-              "apg_reads_upload: missing base_off/byte_off/packed");
-  APG_REQUIRE(r->n_reads == 0 || (r->base_off[0] == 0 && r->byte_off[0] == 0),
-              "apg_reads_upload: base_off[0] and byte_off[0] must be 0");
+}  // extern "C"
+
+namespace apg {
+// A device read set with its offsets uploaded and its payload buffers
+// allocated (packed zeroed, +64 bytes of slack; quals if asked): the caller
+// fills packed / quals on the context's stream (apg_reads_upload from host
+// arrays, apg_reads_load_dev from files).
+int dreads_create(apg_ctx* ctx, uint64_t n, const uint64_t* base_off, const uint64_t* byte_off, bool with_quals,
+                  apg_dreads** out) {
   *out = nullptr;
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   auto* d = new (std::nothrow) apg_dreads();
@@ -237,54 +240,77 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
   d->device = ctx->device;
   static std::atomic<uint64_t> g_gen{1};
   d->gen = g_gen.fetch_add(1);
-  const uint64_t n = r->n_reads;
   d->n_reads = n;
-  d->h_base_off.assign(r->base_off ? r->base_off : nullptr, r->base_off ? r->base_off + n + 1 : nullptr);
+  d->h_base_off.assign(base_off ? base_off : nullptr, base_off ? base_off + n + 1 : nullptr);
   if (d->h_base_off.empty()) d->h_base_off.push_back(0);
   d->n_bases = d->h_base_off[n] - d->h_base_off[0];
-  d->n_bytes = n ? r->byte_off[n] : 0;
+  d->n_bytes = n ? byte_off[n] : 0;
   uint64_t sh = 0x9e3779b97f4a7c15ull ^ n;
   for (uint64_t i = 0; i < n; ++i) {
-    const uint64_t len = r->base_off[i + 1] - r->base_off[i];
+    const uint64_t len = base_off[i + 1] - base_off[i];
     // the byte stride too: padded byte_off layouts with equal lengths differ
     sh = (sh ^ len) * 0x100000001b3ull;
-    sh = (sh ^ (r->byte_off[i + 1] - r->byte_off[i])) * 0x100000001b3ull;
-    if ((r->byte_off[i + 1] - r->byte_off[i]) * 4 < len) {
+    sh = (sh ^ (byte_off[i + 1] - byte_off[i])) * 0x100000001b3ull;
+    if ((byte_off[i + 1] - byte_off[i]) * 4 < len) {
       delete d;
-      set_error("apg_reads_upload: byte_off inconsistent with base_off (read " + std::to_string(i) + ")");
+      set_error("read set: byte_off inconsistent with base_off (read " + std::to_string(i) + ")");
       return APG_E_ARG;
     }
     if (len > d->max_len) d->max_len = len;
   }
   d->shape_hash = sh | 1;
   auto fail = [&](hipError_t e) {
-    set_error(std::string("apg_reads_upload: ") + hipGetErrorString(e));
+    set_error(std::string("read set: ") + hipGetErrorString(e));
     apg_reads_free(d);
     return APG_E_HIP;
   };
   hipError_t e;
   if ((e = hipMalloc(&d->d_base_off, (n + 1) * 8)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&d->d_byte_off, (n + 1) * 8)) != hipSuccess) return fail(e);
-  // +16 bytes of slack: kernels may issue aligned 4/16-byte loads past the end.
+  // +64 bytes of slack: kernels may issue aligned 4/16-byte loads past the end.
   if ((e = hipMalloc(&d->d_packed, d->n_bytes + 64)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(d->d_packed, 0, d->n_bytes + 64, ctx->stream)) != hipSuccess) return fail(e);
   if (n) {
-    if ((e = hipMemcpyAsync(d->d_base_off, r->base_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    if ((e = hipMemcpyAsync(d->d_base_off, base_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
       return fail(e);
-    if ((e = hipMemcpyAsync(d->d_byte_off, r->byte_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
-      return fail(e);
-    if ((e = hipMemcpyAsync(d->d_packed, r->packed, d->n_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    if ((e = hipMemcpyAsync(d->d_byte_off, byte_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
       return fail(e);
   } else {
     uint64_t z = 0;
     if ((e = hipMemcpyAsync(d->d_base_off, &z, 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemcpyAsync(d->d_byte_off, &z, 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return fail(e);
+    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail(e);  // &z is a stack value
   }
-  if (r->quals && n) {
+  if (with_quals && n)
     if ((e = hipMalloc(&d->d_quals, d->h_base_off[n] + 64)) != hipSuccess) return fail(e);
-    if ((e = hipMemcpyAsync(d->d_quals, r->quals, d->h_base_off[n], hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
-      return fail(e);
-  }
+  *out = d;
+  return APG_OK;
+}
+}  // namespace apg
+
+extern "C" {
+
+int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
+  APG_REQUIRE(ctx && r && out, "apg_reads_upload: NULL argument");
+  APG_REQUIRE(r->n_reads == 0 || (r->base_off && r->byte_off && r->packed),
+              "apg_reads_upload: missing base_off/byte_off/packed");
+  APG_REQUIRE(r->n_reads == 0 || (r->base_off[0] == 0 && r->byte_off[0] == 0),
+              "apg_reads_upload: base_off[0] and byte_off[0] must be 0");
+  *out = nullptr;
+  const uint64_t n = r->n_reads;
+  apg_dreads* d = nullptr;
+  APG_TRY(dreads_create(ctx, n, r->base_off, r->byte_off, r->quals != nullptr, &d));
+  auto fail = [&](hipError_t e) {
+    set_error(std::string("apg_reads_upload: ") + hipGetErrorString(e));
+    apg_reads_free(d);
+    return APG_E_HIP;
+  };
+  hipError_t e;
+  if (n && (e = hipMemcpyAsync(d->d_packed, r->packed, d->n_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    return fail(e);
+  if (r->quals && n &&
+      (e = hipMemcpyAsync(d->d_quals, r->quals, d->h_base_off[n], hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+    return fail(e);
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail(e);
   *out = d;
   return APG_OK;

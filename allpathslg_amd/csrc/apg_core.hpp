@@ -16,6 +16,10 @@ namespace apg {
 
 // Thread-local last-error message behind apg_last_error().
 void set_error(const std::string& msg);
+// apg_core.cpp: a device read set with offsets uploaded and payload buffers
+// allocated, for the caller to fill on ctx->stream.
+int dreads_create(apg_ctx* ctx, uint64_t n, const uint64_t* base_off, const uint64_t* byte_off, bool with_quals,
+                  apg_dreads** out);
 const char* get_error();
 
 struct Status {

@@ -105,6 +105,21 @@ int read_header(FILE* f, const char* magic, const char* path, uint64_t* n, uint6
 
 }  // namespace
 
+namespace apg {
+// Header + validated offsets of an APG-fastb (qual = false) / APG-qualb file;
+// *payload = the byte offset of its payload in the file (apg_load.cpp).
+int fmt_read_head(const char* path, bool qual, uint64_t* n, std::vector<uint64_t>* base_off, uint64_t* payload) {
+  File fh;
+  fh.f = std::fopen(path, "rb");
+  if (!fh.f) return io_fail(std::string("cannot open ") + path);
+  uint64_t total = 0;
+  const int rc = read_header(fh.f, qual ? kQualbMagic : kFastbMagic, path, n, &total, base_off);
+  if (rc) return rc;
+  *payload = 32 + 8 * (*n + 1);
+  return APG_OK;
+}
+}  // namespace apg
+
 extern "C" {
 
 int apg_fastb_write(const char* path, const apg_reads* r) {

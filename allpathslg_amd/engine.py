@@ -124,6 +124,14 @@ class Context:
     def upload(self, reads: ReadSet) -> DeviceReads:
         return DeviceReads(self, reads)
 
+    def load_reads(self, fastb: str, qualb: Optional[str] = None, threads: int = 0) -> DeviceReads:
+        """.fastb (+ .qualb) files straight into HBM (apg_reads_load_dev):
+        the same device read set as upload(ReadSet.load(fastb, qualb))."""
+        d = DeviceReads(self, None)
+        check(lib().apg_reads_load_dev(self._h, fastb.encode(), qualb.encode() if qualb else None, int(threads),
+                                       C.byref(d._h)), "apg_reads_load_dev")
+        return d
+
     def kmer_spectrum(self, reads, K: int, hist_len: int = DEFAULT_HIST_LEN):
         """Spectrum h[m] of canonical K-mers (K <= 32).  `reads` is a ReadSet
         (host; includes H2D) or DeviceReads (HBM-resident).  Returns

@@ -817,6 +817,15 @@ int apg_qualb_write(const char* path, const apg_reads* reads);
 int apg_fastb_read(const char* path, apg_reads* out);
 int apg_qualb_read(const char* path, apg_reads* inout /* fills quals */);
 void apg_reads_release(apg_reads* r);
+/* .fastb (+ optional .qualb, NULL for none) straight into a device read set:
+ * the module-boundary input of a drop-in stage ([R:M] the RUN-dir
+ * frag_reads_*.fastb / .qualb every module opens; src/feudal/).  Offsets are
+ * read and validated as by apg_fastb_read / apg_qualb_read; the payloads go
+ * file -> pinned staging -> HBM in 16 MiB chunks, `threads` workers (<= 0:
+ * min(4, hardware threads)) each double-buffering pread against its own H2D
+ * stream.  Same device read set as apg_fastb_read + apg_qualb_read +
+ * apg_reads_upload; free with apg_reads_free. */
+int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int threads, apg_dreads** out);
 /* Spectrum text file (.kspec): "m\tcount" lines for nonzero bins. */
 int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_len);
 

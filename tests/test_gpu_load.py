@@ -1,0 +1,102 @@
+"""apg_reads_load_dev: .fastb / .qualb straight into HBM must give the same
+device read set as apg_fastb_read + apg_qualb_read + apg_reads_upload —
+bases, qualities and offsets byte for byte — for ragged and empty reads, for
+payloads of many 16 MiB chunks spread over an odd number of workers, and it
+must refuse the inputs apg_fastb_read refuses (bad magic, truncated payload,
+qualb lengths that do not match the fastb)."""
+import os
+
+import numpy as np
+import pytest
+
+from allpathslg_amd import ApgError, ReadSet, synth_genome, synth_reads
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(ctx, d, ref, quals):
+    a = ctx.download(d, with_quals=quals)
+    assert a.n_reads == ref.n_reads
+    assert np.array_equal(a.base_off, ref.base_off)
+    assert np.array_equal(a.byte_off, ref.byte_off)
+    nb = int(ref.byte_off[-1])
+    assert np.array_equal(a.packed[:nb], ref.packed[:nb])
+    if quals:
+        assert np.array_equal(a.quals[: ref.n_bases], ref.quals[: ref.n_bases])
+
+
+def _write(tmp_path, rs, tag):
+    fb, qb = str(tmp_path / f"{tag}.fastb"), str(tmp_path / f"{tag}.qualb")
+    rs.write_fastb(fb)
+    if rs.quals is not None:
+        rs.write_qualb(qb)
+    return fb, qb
+
+
+def test_ragged_reads(gpu_ctx, tmp_path):
+    rng = np.random.default_rng(3)
+    lens = [0, 1, 3, 4, 5, 31, 32, 33, 99, 100, 250, 0, 7]
+    seqs = [rng.integers(0, 4, size=n) for n in lens]
+    quals = [rng.integers(2, 41, size=n) for n in lens]
+    rs = ReadSet.from_sequences(seqs, quals)
+    fb, qb = _write(tmp_path, rs, "ragged")
+    ref = ReadSet.load(fb, qb)
+    for threads in (0, 1, 3):
+        d = gpu_ctx.load_reads(fb, qb, threads=threads)
+        _same(gpu_ctx, d, ref, True)
+        d.free()
+    d = gpu_ctx.load_reads(fb)  # bases only
+    _same(gpu_ctx, d, ReadSet.load(fb), False)
+    d.free()
+
+
+def test_many_chunks(gpu_ctx, tmp_path):
+    """2 M reads: 50 MB of bases (4 chunks) and 200 MB of qualities (12
+    chunks) over 3 and 8 workers; the loaded set runs the K=25 spectrum to
+    the same histogram as the uploaded one."""
+    g = synth_genome(2_000_000, 41)
+    rs = synth_reads(g, 1_000_000, seed=42)
+    fb, qb = _write(tmp_path, rs, "big")
+    try:
+        ref = ReadSet.load(fb, qb)
+        for threads in (3, 8):
+            d = gpu_ctx.load_reads(fb, qb, threads=threads)
+            _same(gpu_ctx, d, ref, True)
+            h1, s1 = gpu_ctx.kmer_spectrum(d, 25)
+            d.free()
+        du = gpu_ctx.upload(ref)
+        h2, s2 = gpu_ctx.kmer_spectrum(du, 25)
+        du.free()
+        assert np.array_equal(h1, h2) and s1 == s2
+    finally:
+        for p in (fb, qb):
+            os.unlink(p)
+
+
+def test_empty_set(gpu_ctx, tmp_path):
+    rs = ReadSet.from_sequences([], [])
+    fb, qb = _write(tmp_path, rs, "empty")
+    d = gpu_ctx.load_reads(fb, qb)
+    assert d.n_reads == 0
+    d.free()
+
+
+def test_refuses_bad_inputs(gpu_ctx, tmp_path):
+    rng = np.random.default_rng(4)
+    seqs = [rng.integers(0, 4, size=n) for n in (50, 60, 70)]
+    rs = ReadSet.from_sequences(seqs, [rng.integers(0, 41, size=len(s)) for s in seqs])
+    fb, qb = _write(tmp_path, rs, "ok")
+    bad = tmp_path / "bad.fastb"
+    bad.write_bytes(b"NOTAFASTB" * 10)
+    with pytest.raises(ApgError):
+        gpu_ctx.load_reads(str(bad))
+    trunc = tmp_path / "trunc.fastb"
+    trunc.write_bytes(open(fb, "rb").read()[:-5])
+    with pytest.raises(ApgError):
+        gpu_ctx.load_reads(str(trunc))
+    other = ReadSet.from_sequences([s[:-1] for s in seqs], [rng.integers(0, 41, size=len(s) - 1) for s in seqs])
+    _, qo = _write(tmp_path, other, "other")
+    with pytest.raises(ApgError):
+        gpu_ctx.load_reads(fb, qo)
+    with pytest.raises(ApgError):
+        gpu_ctx.load_reads(str(tmp_path / "missing.fastb"))
