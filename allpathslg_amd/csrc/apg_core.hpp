@@ -137,6 +137,7 @@ struct apg_ctx {
     uint32_t G = 0;
     uint64_t n = 0;  // records
     uint64_t n_nodes = 0;  // nodes of the last apg_urec_nodes ("usk_nodes")
+    bool desc = false;  // the count pass kept record descriptors ("usk_desc*")
   } urstate;
 
   // Super-k-mer plan of the last sk_count (reused by sk_scatter).
@@ -146,6 +147,7 @@ struct apg_ctx {
     int K = 0, P = 0;
     uint32_t G = 0;
     uint64_t total = 0;
+    bool desc = false;  // the count pass kept record descriptors ("sk_desc*")
   } skstate;
 
   // Device graph of the last unipath build ("u_*" workspaces + the node

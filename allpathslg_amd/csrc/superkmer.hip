@@ -102,20 +102,24 @@ __device__ __forceinline__ SK16 make_rec(const uint8_t* rd, uint32_t a, uint32_t
 // kdig[digit] += K-mers of those records.  k_sk_scatter walks the same tiles
 // and reads in the same way, so its per-(digit, block) counts match.
 __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int D, uint32_t* __restrict__ cmat,
-                                                         unsigned long long* __restrict__ kdig) {
+                                                         unsigned long long* __restrict__ kdig, SkDesc dd) {
   __shared__ SkTile<kSkThreads> T;
   __shared__ uint32_t hist[256], khist[256];
   __shared__ SkList<1> lst;  // f runs in place
+  __shared__ uint32_t dpos, dovf;
   extern __shared__ uint32_t sbuf[];  // p.w x kSkThreads van Herk columns
   const uint32_t ndig = 1u << D;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
+  if (threadIdx.x == 0) dpos = dovf = 0;
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key, uint32_t) {
+  SkDescWriter W(dd, rv, r0, r1, &dpos, &dovf);
+  auto f = [&](const uint8_t*, uint32_t, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
     const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
     atomicAdd(&hist[d], 1u);
     atomicAdd(&khist[d], n);
+    W.put(a, n, key, q);
   };
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
@@ -124,8 +128,10 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
     else
       sk_walk_global<kSkThreads, false>(rv, p, T, t0, sbuf + threadIdx.x, f);
     __syncthreads();
+    W.tile_done(t0);
     t0 += n ? n : 1;
   }
+  W.block_done();
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) {
     cmat[(uint64_t)i * G + b] = hist[i];
     if (khist[i]) atomicAdd(&kdig[i], (unsigned long long)khist[i]);
@@ -159,7 +165,7 @@ __device__ __forceinline__ SK16 rec_head(const SK24& r) { return SK16{r.w0, r.w1
 // base position of their first K-mer.
 template <typename O>
 __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, int D,
-                                                           const uint64_t* __restrict__ omat, O out) {
+                                                           const uint64_t* __restrict__ omat, O out, SkDesc dd) {
   __shared__ SkTile<kSkThreads> T;
   __shared__ unsigned long long cur[256];
   __shared__ SkList<kSkListCap> lst;
@@ -177,6 +183,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
     const uint64_t pos = OutWantsPos<O>::value ? rv.base_off[t0 + q] + a : 0;  // the read's first base + a
     rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
   };
+  if (sk_replay<kSkThreads>(dd, rv, r0, r1, T, t0, f)) return;  // the count pass's descriptors
   while (t0 < r1) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n)
@@ -987,8 +994,25 @@ static uint32_t sk_blocks(const apg_ctx* ctx, uint64_t n_reads, const SkP& p) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, (n_reads + 255) / 256));
 }
 
+// Descriptor buffers of a read set's walk (SkDesc): one 8-byte slot per
+// kSkDescDiv bases (records average one per ~6.5 bases of 100-bp reads at
+// K = 24-25), per-tile counts by first read, per-block flags.  Off (the
+// scatter pass walks) with APG_SK_DESC=0 or a read set of unknown size.
+constexpr uint32_t kSkDescDiv = 4;
+static int sk_desc_bufs(apg_ctx* ctx, const apg_dreads* dr, uint32_t G, SkDesc* out) {
+  static const bool off = getenv("APG_SK_DESC") && !strcmp(getenv("APG_SK_DESC"), "0");
+  *out = SkDesc{nullptr, nullptr, nullptr, kSkDescDiv, 0};
+  if (off || !dr->n_reads || !dr->n_bases) return APG_OK;
+  out->slots = dr->n_bases / kSkDescDiv + 1;
+  APG_TRY(workspace_t(ctx, "sk_desc", out->slots, &out->desc));
+  APG_TRY(workspace_t(ctx, "sk_dtcnt", dr->n_reads, &out->tcnt));
+  APG_TRY(workspace_t(ctx, "sk_dflag", G, &out->flag));
+  return APG_OK;
+}
+
 // Pass 1 over reads: per-digit record counts (host) and K-mer counts; leaves
-// the scanned [digit][block] matrix in "sk_omat" for sk_scatter.
+// the scanned [digit][block] matrix in "sk_omat" and the records'
+// descriptors in "sk_desc" for sk_scatter.
 int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
              std::vector<uint64_t>* kmer_counts) {
   const SkP p = make_skp(K);
@@ -1005,9 +1029,11 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   APG_TRY(workspace_t(ctx, "sk_kdig", ndig, &kdig));
   APG_CHECK_HIP(hipMemsetAsync(kdig, 0, ndig * 8, ctx->stream));
   if (!dr->n_reads) APG_CHECK_HIP(hipMemsetAsync(cmat, 0, (uint64_t)ndig * G * 4, ctx->stream));
+  SkDesc dd;
+  APG_TRY(sk_desc_bufs(ctx, dr, G, &dd));
   kbegin(ctx, "sk_count", dr->n_bytes + 16 * dr->n_reads);
   if (dr->n_reads)
-    k_sk_count<<<G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, cmat, kdig);
+    k_sk_count<<<G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, cmat, kdig, dd);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "sk"));
@@ -1026,6 +1052,7 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   s.P = P;
   s.G = G;
   s.total = h[ndig];
+  s.desc = dd.desc != nullptr;
   return APG_OK;
 }
 
@@ -1041,8 +1068,11 @@ static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out,
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)(1u << D) * s.G + 1, &omat));
+  SkDesc dd{nullptr, nullptr, nullptr, kSkDescDiv, 0};
+  if (s.desc) APG_TRY(sk_desc_bufs(ctx, dr, s.G, &dd));
   kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * out_bytes);
-  if (dr->n_reads) k_sk_scatter<O><<<s.G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, omat, out);
+  if (dr->n_reads)
+    k_sk_scatter<O><<<s.G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, omat, out, dd);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;

@@ -250,6 +250,84 @@ struct SkWalker {
   }
 };
 
+// Record descriptors the count pass keeps so the scatter pass need not walk
+// the reads again: block b's go to desc[lo(r0), lo(r1)), lo(r) = base_off[r]
+// / div (the block's share of a bases / div budget), tile by tile, with each
+// tile's count at tcnt[t0].  A block with more records than its region, or a
+// record starting past base 65535 of a read, sets flag[b]: the scatter pass
+// walks that block again.  Descriptor: key | a << 32 | n << 48 | q << 56.
+struct SkDesc {
+  uint64_t* desc;  // null: no descriptors (the scatter pass walks)
+  uint32_t* tcnt;
+  uint32_t* flag;
+  uint32_t div;
+  uint64_t slots;  // desc capacity: regions are clamped to it
+  __device__ __forceinline__ uint64_t lo(const SkReads& rv, uint64_t r) const {
+    const uint64_t x = rv.base_off[r] / div;
+    return x < slots ? x : slots;
+  }
+};
+__device__ __forceinline__ uint64_t sk_desc_pack(uint32_t key, uint32_t a, uint32_t n, uint32_t q) {
+  return (uint64_t)key | ((uint64_t)a << 32) | ((uint64_t)n << 48) | ((uint64_t)q << 56);
+}
+
+// The count pass's side of the descriptors: per-block slot counter and
+// overflow flag in LDS, a tile's count written by thread 0 between tiles.
+struct SkDescWriter {
+  const SkDesc& dd;
+  uint64_t lo, cap;
+  uint32_t* pos;   // LDS counter
+  uint32_t* ovf;   // LDS flag
+  uint32_t prev = 0;
+  __device__ __forceinline__ SkDescWriter(const SkDesc& d, const SkReads& rv, uint64_t r0, uint64_t r1, uint32_t* p,
+                                          uint32_t* o)
+      : dd(d), lo(d.desc ? d.lo(rv, r0) : 0), cap(d.desc ? d.lo(rv, r1) - lo : 0), pos(p), ovf(o) {}
+  __device__ __forceinline__ void put(uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
+    if (!dd.desc) return;
+    const uint32_t i = atomicAdd(pos, 1u);
+    if (i < cap && a <= 0xffffu)
+      dd.desc[lo + i] = sk_desc_pack(key, a, n, q);
+    else
+      *ovf = 1;
+  }
+  // thread 0, after the barrier that ends tile t0 (all its records put)
+  __device__ __forceinline__ void tile_done(uint64_t t0) {
+    if (!dd.desc || threadIdx.x != 0) return;
+    const uint32_t now = *pos;
+    dd.tcnt[t0] = now - prev;
+    prev = now;
+  }
+  __device__ __forceinline__ void block_done() {
+    if (dd.desc && threadIdx.x == 0) dd.flag[blockIdx.x] = *ovf || *pos > cap;
+  }
+};
+
+// The scatter pass's side: the block's tiles again (for their bases), each
+// tile's descriptors handed to f lane-parallel, t0 = the tile's first read
+// meanwhile (f may read it).  Returns false (nothing done) when the block
+// must walk.  Block-uniform.
+template <int NT, typename TT, typename F>
+__device__ __forceinline__ bool sk_replay(const SkDesc& dd, const SkReads& rv, uint64_t r0, uint64_t r1, TT& T,
+                                          uint64_t& t0, F f) {
+  if (!dd.desc || dd.flag[blockIdx.x]) return false;
+  uint64_t off = dd.lo(rv, r0);
+  for (t0 = r0; t0 < r1;) {
+    const uint32_t n = sk_load_tile(rv, t0, r1, T);
+    const uint32_t c = dd.tcnt[t0];
+    const uint8_t* g = rv.packed + rv.byte_off[t0];  // a read too long for a tile: from HBM
+    for (uint32_t i = threadIdx.x; i < c; i += NT) {
+      const uint64_t d = dd.desc[off + i];
+      const uint32_t q = (uint32_t)(d >> 56);
+      f(n ? reinterpret_cast<const uint8_t*>(T.words) + T.rbo[q] : g, T.rlen[q], (uint32_t)(d >> 32) & 0xffffu,
+        (uint32_t)(d >> 48) & 0xffu, (uint32_t)d, q);
+    }
+    off += c;
+    __syncthreads();
+    t0 += n ? n : 1;
+  }
+  return true;
+}
+
 // A read too long for a tile: thread 0 walks it from HBM and hands each
 // record straight to f(rd, L, a, n, key, q = 0).
 template <int NT, bool TWO, typename P, typename TT, typename F>

@@ -1259,9 +1259,9 @@ __device__ __forceinline__ SK48 make_urec(const uint8_t* rd, uint32_t L, uint32_
 
 // The block's reads [r0, r1), tile by tile: the single-level column for short
 // windows, the two-level one (sk_walk2_words) for long.
-template <bool LIST, int CAP, typename F>
+template <bool LIST, int CAP, typename F, typename TD>
 __device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p, uint64_t r0, uint64_t r1, UskTile& T,
-                                               uint32_t* sb, SkList<CAP>& lst, F f) {
+                                               uint32_t* sb, SkList<CAP>& lst, F f, TD tile_done) {
   const bool two = p.w > kUskWalk2MinW;
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
@@ -1276,30 +1276,35 @@ __device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p,
       sk_walk_global<kUskThreads, false>(rv, p, T, t0, sb, f);
     }
     __syncthreads();
+    tile_done(t0);
     t0 += n ? n : 1;
   }
 }
 
 // Per-(digit, block) record counts and per-digit K-mer counts.
 __global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, int D, uint32_t* __restrict__ cmat,
-                                                           unsigned long long* __restrict__ kdig) {
+                                                           unsigned long long* __restrict__ kdig, SkDesc dd) {
   __shared__ UskTile T;
   __shared__ SkList<1> lst;  // f runs in place
+  __shared__ uint32_t dpos, dovf;
   extern __shared__ uint32_t usk_sb[];  // the walk columns, then hist[ndig], khist[ndig]
   const uint32_t ndig = 1u << D;
   uint32_t* hist = usk_sb + usk_column_words(p.w);
   uint32_t* khist = hist + ndig;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
-  if (threadIdx.x == 0) lst.cnt = 0;
+  if (threadIdx.x == 0) lst.cnt = dpos = dovf = 0;
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
-  auto f = [&](const uint8_t*, uint32_t, uint32_t, uint32_t n, uint32_t key, uint32_t) {
+  SkDescWriter W(dd, rv, r0, r1, &dpos, &dovf);
+  auto f = [&](const uint8_t*, uint32_t, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
     const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
     atomicAdd(&hist[d], 1u);
     atomicAdd(&khist[d], n);
+    W.put(a, n, key, q);
   };
-  usk_walk_tiles<false>(rv, p, r0, r1, T, usk_sb + threadIdx.x, lst, f);
+  usk_walk_tiles<false>(rv, p, r0, r1, T, usk_sb + threadIdx.x, lst, f, [&](uint64_t t0) { W.tile_done(t0); });
+  W.block_done();
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) {
     cmat[(uint64_t)i * G + b] = hist[i];
     if (khist[i]) atomicAdd(&kdig[i], (unsigned long long)khist[i]);
@@ -1307,7 +1312,8 @@ __global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, i
 }
 
 __global__ void __launch_bounds__(kUskThreads) k_usk_scatter(SkReads rv, UskP p, int D,
-                                                             const uint64_t* __restrict__ omat, SK48* __restrict__ out) {
+                                                             const uint64_t* __restrict__ omat, SK48* __restrict__ out,
+                                                             SkDesc dd) {
   __shared__ UskTile T;
   __shared__ SkList<kUskListCap> lst;
   extern __shared__ uint32_t usk_sb[];  // the walk columns, then cur[ndig]
@@ -1323,7 +1329,9 @@ __global__ void __launch_bounds__(kUskThreads) k_usk_scatter(SkReads rv, UskP p,
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
     out[atomicAdd(&cur[d], 1ull)] = x;
   };
-  usk_walk_tiles<true>(rv, p, r0, r1, T, usk_sb + threadIdx.x, lst, f);
+  uint64_t t0 = r0;
+  if (sk_replay<kUskThreads>(dd, rv, r0, r1, T, t0, f)) return;  // the count pass's descriptors
+  usk_walk_tiles<true>(rv, p, r0, r1, T, usk_sb + threadIdx.x, lst, f, [](uint64_t) {});
 }
 
 __global__ void k_usk_digit_starts(const uint64_t* __restrict__ omat, uint32_t ndig, uint32_t G,
@@ -1975,6 +1983,20 @@ static uint64_t usk_grid_cap(const apg_ctx* ctx, const UskP& p, int D) {
   return std::min<uint64_t>(kUskMaxBlocks, (uint64_t)std::max(ctx->n_cu, 1) * occ * 2);
 }
 
+// Record descriptors of the count pass (SkDesc, superkmer.hpp): fragments
+// carry ~1 record per 48 bases at K = 96; one 8-byte slot per kUskDescDiv.
+constexpr uint32_t kUskDescDiv = 16;
+static int usk_desc_bufs(apg_ctx* ctx, const apg_dreads* dr, uint32_t G, SkDesc* out) {
+  static const bool off = getenv("APG_SK_DESC") && !strcmp(getenv("APG_SK_DESC"), "0");
+  *out = SkDesc{nullptr, nullptr, nullptr, kUskDescDiv, 0};
+  if (off || !dr->n_reads || !dr->n_bases) return APG_OK;
+  out->slots = dr->n_bases / kUskDescDiv + 1;
+  APG_TRY(workspace_t(ctx, "usk_desc", out->slots, &out->desc));
+  APG_TRY(workspace_t(ctx, "usk_dtcnt", dr->n_reads, &out->tcnt));
+  APG_TRY(workspace_t(ctx, "usk_dflag", G, &out->flag));
+  return APG_OK;
+}
+
 static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, std::vector<uint64_t>* h,
                     std::vector<uint64_t>* kd, uint32_t* G_out) {
   if (p.w > kUskMaxW) {
@@ -1996,8 +2018,10 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   APG_TRY(workspace_t(ctx, "usk_kdig", ndig, &kdig));
   APG_CHECK_HIP(hipMemsetAsync(kdig, 0, ndig * 8, ctx->stream));
   if (!dr->n_reads) APG_CHECK_HIP(hipMemsetAsync(cmat, 0, (uint64_t)ndig * G * 4, ctx->stream));
+  SkDesc dd;
+  APG_TRY(usk_desc_bufs(ctx, dr, G, &dd));
   kbegin(ctx, "usk_count", dr->n_bytes + 16 * dr->n_reads);
-  if (dr->n_reads) k_usk_count<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, cmat, kdig);
+  if (dr->n_reads) k_usk_count<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, cmat, kdig, dd);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "usk"));
@@ -2015,6 +2039,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   us.P = P;
   us.G = G;
   us.n = (*h)[ndig];
+  us.desc = dd.desc != nullptr;
   return APG_OK;
 }
 
@@ -2024,8 +2049,12 @@ static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P,
   const size_t sb_bytes = usk_walk_lds(p.w, D, 8);  // + hist, khist (count) or cursors (scatter)
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "usk_omat", (uint64_t)(1u << D) * G + 1, &omat));
+  const auto& us = ctx->urstate;
+  SkDesc dd{nullptr, nullptr, nullptr, kUskDescDiv, 0};
+  if (us.valid && us.desc && us.gen == dr->gen && us.G == G && us.K == p.K && us.P == P)
+    APG_TRY(usk_desc_bufs(ctx, dr, G, &dd));
   kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + ctx->urstate.n * sizeof(SK48));
-  if (dr->n_reads) k_usk_scatter<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, omat, out);
+  if (dr->n_reads) k_usk_scatter<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, omat, out, dd);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;
