@@ -1000,10 +1000,11 @@ static uint32_t sk_blocks(const apg_ctx* ctx, uint64_t n_reads, const SkP& p) {
 // scatter pass walks) with APG_SK_DESC=0 or a read set of unknown size.
 constexpr uint32_t kSkDescDiv = 4;
 static int sk_desc_bufs(apg_ctx* ctx, const apg_dreads* dr, uint32_t G, SkDesc* out) {
-  static const bool off = getenv("APG_SK_DESC") && !strcmp(getenv("APG_SK_DESC"), "0");
-  *out = SkDesc{nullptr, nullptr, nullptr, kSkDescDiv, 0};
-  if (off || !dr->n_reads || !dr->n_bases) return APG_OK;
-  out->slots = dr->n_bases / kSkDescDiv + 1;
+  const char* env = getenv("APG_SK_DESC");  // "0": off; a number: bases per slot (tests force overflow)
+  const uint32_t div = env && atoi(env) > 0 ? (uint32_t)atoi(env) : kSkDescDiv;
+  *out = SkDesc{nullptr, nullptr, nullptr, div, 0};
+  if ((env && !strcmp(env, "0")) || !dr->n_reads || !dr->n_bases) return APG_OK;
+  out->slots = dr->n_bases / div + 1;
   APG_TRY(workspace_t(ctx, "sk_desc", out->slots, &out->desc));
   APG_TRY(workspace_t(ctx, "sk_dtcnt", dr->n_reads, &out->tcnt));
   APG_TRY(workspace_t(ctx, "sk_dflag", G, &out->flag));

@@ -1987,10 +1987,11 @@ static uint64_t usk_grid_cap(const apg_ctx* ctx, const UskP& p, int D) {
 // carry ~1 record per 48 bases at K = 96; one 8-byte slot per kUskDescDiv.
 constexpr uint32_t kUskDescDiv = 16;
 static int usk_desc_bufs(apg_ctx* ctx, const apg_dreads* dr, uint32_t G, SkDesc* out) {
-  static const bool off = getenv("APG_SK_DESC") && !strcmp(getenv("APG_SK_DESC"), "0");
-  *out = SkDesc{nullptr, nullptr, nullptr, kUskDescDiv, 0};
-  if (off || !dr->n_reads || !dr->n_bases) return APG_OK;
-  out->slots = dr->n_bases / kUskDescDiv + 1;
+  const char* env = getenv("APG_SK_DESC");  // "0": off; a number: bases per slot (tests force overflow)
+  const uint32_t div = env && atoi(env) > 0 ? (uint32_t)atoi(env) : kUskDescDiv;
+  *out = SkDesc{nullptr, nullptr, nullptr, div, 0};
+  if ((env && !strcmp(env, "0")) || !dr->n_reads || !dr->n_bases) return APG_OK;
+  out->slots = dr->n_bases / div + 1;
   APG_TRY(workspace_t(ctx, "usk_desc", out->slots, &out->desc));
   APG_TRY(workspace_t(ctx, "usk_dtcnt", dr->n_reads, &out->tcnt));
   APG_TRY(workspace_t(ctx, "usk_dflag", G, &out->flag));
