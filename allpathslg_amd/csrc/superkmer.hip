@@ -1054,6 +1054,7 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   s.G = G;
   s.total = h[ndig];
   s.desc = dd.desc != nullptr;
+  if (s.desc) kbytes_add(ctx, "sk_count", s.total * 8);  // the records' descriptors, written
   return APG_OK;
 }
 
@@ -1071,7 +1072,7 @@ static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out,
   APG_TRY(workspace_t(ctx, "sk_omat", (uint64_t)(1u << D) * s.G + 1, &omat));
   SkDesc dd{nullptr, nullptr, nullptr, kSkDescDiv, 0};
   if (s.desc) APG_TRY(sk_desc_bufs(ctx, dr, s.G, &dd));
-  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * out_bytes);
+  kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * (out_bytes + (dd.desc ? 8 : 0)));
   if (dr->n_reads)
     k_sk_scatter<O><<<s.G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, omat, out, dd);
   kend(ctx);

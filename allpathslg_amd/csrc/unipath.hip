@@ -2041,6 +2041,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   us.G = G;
   us.n = (*h)[ndig];
   us.desc = dd.desc != nullptr;
+  if (us.desc) kbytes_add(ctx, "usk_count", us.n * 8);  // the records' descriptors, written
   return APG_OK;
 }
 
@@ -2054,7 +2055,7 @@ static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P,
   SkDesc dd{nullptr, nullptr, nullptr, kUskDescDiv, 0};
   if (us.valid && us.desc && us.gen == dr->gen && us.G == G && us.K == p.K && us.P == P)
     APG_TRY(usk_desc_bufs(ctx, dr, G, &dd));
-  kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + ctx->urstate.n * sizeof(SK48));
+  kbegin(ctx, "usk_scatter", dr->n_bytes + 16 * dr->n_reads + ctx->urstate.n * (sizeof(SK48) + (dd.desc ? 8 : 0)));
   if (dr->n_reads) k_usk_scatter<<<G, kUskThreads, sb_bytes, ctx->stream>>>(rv, p, D, omat, out, dd);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
