@@ -180,14 +180,21 @@ __device__ __forceinline__ uint64_t rkey_w0(uint64_t w0) {
     return w0 << 32;  // SK16 / SK24 / SK48: the minimizer key
 }
 
-template <typename R>
+// RI -> RO: the same record (RO == RI), or an SK16 that leaves as an SK24
+// carrying its input index (the multi-GPU solid count: the index of a
+// received record is where its weak mask goes back; the first level widens
+// the records instead of a separate pass over them).
+template <typename RI, typename RO = RI>
 __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_part_scatter(
-    const R* __restrict__ rec, const Chunk* __restrict__ ch, int shift, uint32_t ndig,
-    const uint32_t* __restrict__ pre, const uint64_t* __restrict__ child, R* __restrict__ out) {
+    const RI* __restrict__ rec, const Chunk* __restrict__ ch, int shift, uint32_t ndig,
+    const uint32_t* __restrict__ pre, const uint64_t* __restrict__ child, RO* __restrict__ out) {
+  static_assert(std::is_same<RI, RO>::value || (sizeof(RI) == 16 && sizeof(RO) == 24), "RI -> RO: same, or 16 -> 24");
+  using R = RO;
   constexpr int kPartItems = PartGeom<R>::items;
   constexpr int kTile = PartGeom<R>::tile;
-  constexpr uint32_t kQ = sizeof(R) / 8;  // 64-bit words per record, held as words (no 24/48-byte
-                                          // aggregates in registers: those went to scratch)
+  constexpr uint32_t kQ = sizeof(R) / 8;    // 64-bit words per record, held as words (no 24/48-byte
+                                            // aggregates in registers: those went to scratch)
+  constexpr uint32_t kQi = sizeof(RI) / 8;  // words read per record
   static_assert(sizeof(R) % 8 == 0, "record size must be a multiple of 8 bytes");
   __shared__ __attribute__((aligned(16))) uint64_t stage[kTile * kQ];
   __shared__ unsigned long long cur[256];
@@ -214,7 +221,8 @@ __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_
       const uint32_t idx = t + i * kPartThreads + tid;
       if (idx < c.len) {
 #pragma unroll
-        for (uint32_t q = 0; q < kQ; ++q) v[i][q] = base[(uint64_t)idx * kQ + q];
+        for (uint32_t q = 0; q < kQi; ++q) v[i][q] = base[(uint64_t)idx * kQi + q];
+        if constexpr (kQi < kQ) v[i][kQi] = c.start + idx;  // the input index
       }
     }
   };
@@ -271,10 +279,10 @@ __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_
 // One partition level: every parent's segments -> ndig children per parent.
 // Writes the children's start offsets to d_child (nparents*ndig + 1) and, if
 // host_child, copies them to the host.
-template <typename R>
-int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
+template <typename R, typename RO>
+int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag) {
-  constexpr int kTile = PartGeom<R>::tile;
+  constexpr int kTile = PartGeom<RO>::tile;
   const uint32_t ndig = 1u << bits;
   const uint64_t np = parents.size();
   // ~24K chunks per level: enough workgroups, short count-matrix rows
@@ -321,8 +329,9 @@ int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector
                                                                              d_child);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
-  kbegin(ctx, (std::string(tag) + "_part_scatter").c_str(), n * 2 * sizeof(R) + nrow * ndig * 4);
-  k_part_scatter<R><<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, pre, d_child, dst);
+  kbegin(ctx, (std::string(tag) + "_part_scatter").c_str(), n * (sizeof(R) + sizeof(RO)) + nrow * ndig * 4);
+  k_part_scatter<R, RO><<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, pre, d_child,
+                                                                          dst);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   if (host_child) {
@@ -334,13 +343,15 @@ int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector
 }
 
 
-template int part_level<uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&, int, int,
-                                  uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
-template int part_level<SK16>(apg_ctx*, const SK16*, SK16*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
-                              uint64_t*, std::vector<uint64_t>*, const char*);
-template int part_level<SK24>(apg_ctx*, const SK24*, SK24*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
-                              uint64_t*, std::vector<uint64_t>*, const char*);
-template int part_level<SK48>(apg_ctx*, const SK48*, SK48*, const std::vector<std::vector<Seg>>&, int, int, uint64_t,
-                              uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<uint64_t, uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&,
+                                            int, int, uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SK16, SK16>(apg_ctx*, const SK16*, SK16*, const std::vector<std::vector<Seg>>&, int, int,
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SK16, SK24>(apg_ctx*, const SK16*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SK24, SK24>(apg_ctx*, const SK24*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SK48, SK48>(apg_ctx*, const SK48*, SK48*, const std::vector<std::vector<Seg>>&, int, int,
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
 
 }  // namespace apg

@@ -65,8 +65,9 @@ int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out
 // children, written contiguously to `dst` in (parent, digit) order.  Writes
 // the children's starts to d_child[0 .. nparents*ndig] (last = n) and, if
 // host_child, copies them to the host.  Order inside a child is unspecified.
-template <typename R>
-int part_level(apg_ctx* ctx, const R* src, R* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
+// RO: the output record type — R, or SK24 from SK16 (the input index as pos).
+template <typename R, typename RO = R>
+int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag);
 
 // Stable LSD radix sort of (key, val) pairs by key over the key's significant

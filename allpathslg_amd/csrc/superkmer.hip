@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "apg_core.hpp"
@@ -1100,10 +1101,13 @@ int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, 
 // mode leaves the solid hashes in "pc_solid" (res->solid, res->n_solid).
 // weak (SK24 records, solid mode only): per-base bitmap of weak K-mer
 // instances, zeroed by the caller.
+__global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out);
+
 template <typename R>
 static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vector<uint64_t>& rec_counts,
                             uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist,
-                            size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr) {
+                            size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr,
+                            const SK16* src16 = nullptr) {
   const SkP p = make_skp(K);
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
@@ -1153,6 +1157,13 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   const R* cur = src;
   uint64_t nb = B1;
   int consumed = pbits + l1;
+  if constexpr (std::is_same<R, SK24>::value) {  // SK16 input: widened by the first level, or here
+    if (src16 && nlev == 0 && n) {
+      k_sk_index24<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(src16, n, spare);
+      APG_CHECK_HIP(hipGetLastError());
+      cur = spare;
+    }
+  }
   if (nlev == 0) {
     std::vector<uint64_t> hb(B1 + 1, 0);
     for (uint32_t l = 0; l < B1; ++l) hb[l + 1] = hb[l] + rec_counts[l];
@@ -1164,8 +1175,18 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     R* dst = (cur == bufA) ? bufB : bufA;
     std::vector<uint64_t> hb;
     const bool last = lev + 1 == nlev;
-    APG_TRY(part_level<R>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb,
-                          sizeof(R) == sizeof(SK24) ? "s24" : "s"));
+    bool done = false;
+    if constexpr (std::is_same<R, SK24>::value) {
+      if (src16 && lev == 0) {  // SK16 -> SK24 with the input index (the record's mask slot)
+        dst = bufA != spare ? bufA : bufB;
+        APG_TRY((part_level<SK16, SK24>(ctx, src16, dst, parents, 64 - consumed, bits, n, boff,
+                                        last ? nullptr : &hb, "s24")));
+        done = true;
+      }
+    }
+    if (!done)
+      APG_TRY(part_level<R>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb,
+                            sizeof(R) == sizeof(SK24) ? "s24" : "s"));
     nb = parents.size() << bits;
     if (!last) {
       parents.assign(nb, {});
@@ -1374,13 +1395,11 @@ int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64
   for (auto c : rec_counts) n += c;
   SK24* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
-  if (n) {
-    APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
-    k_sk_index24<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(recv, n, buf);
-    APG_CHECK_HIP(hipGetLastError());
-  }
+  if (n) APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
+  // the first partition level reads the SK16 records and writes them as SK24
+  // with their receive index (no separate widening pass)
   return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, nullptr, res,
-                                wrec);
+                                wrec, recv);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {
