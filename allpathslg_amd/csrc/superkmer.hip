@@ -882,72 +882,136 @@ __global__ void __launch_bounds__(kDdThreads) k_sk_bucket_dd(const R* __restrict
 
 // Overflowed buckets: every K-mer of every overflowed bucket into one global
 // open-addressing table keyed by canonical K-mer (distinct buckets never
-// share a K-mer).
-template <typename R>
-__global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
-                               const uint32_t* __restrict__ ovf_list, uint32_t n_ovf,
-                               unsigned long long* __restrict__ n_kmers) {
-  unsigned long long c = 0;
-  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
-    const uint32_t b = ovf_list[q];
-    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) c += (uint32_t)(rec[i].w0 >> 32) & 0xff;
+// share a K-mer).  Their records are processed as one flattened list (opre =
+// exclusive prefix of the listed buckets' record counts), not a workgroup
+// per bucket: the overflowing buckets of a repeat-rich genome are few and
+// huge (one minimizer shared by thousands of copies), and a workgroup per
+// bucket left one CU crunching the largest while the rest idled.
+__global__ void k_sk_ovf_sizes(const uint64_t* __restrict__ boff, const uint32_t* __restrict__ ovf, uint32_t n_ovf,
+                               uint32_t* __restrict__ sz) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n_ovf) sz[q] = (uint32_t)(boff[ovf[q] + 1] - boff[ovf[q]]);
+}
+
+// index of the k-th record of the flattened overflow list
+__device__ __forceinline__ uint64_t sk_ovf_record(const uint64_t* __restrict__ boff, const uint32_t* __restrict__ ovf,
+                                                  const uint64_t* __restrict__ opre, uint32_t n_ovf, uint64_t k) {
+  uint32_t lo = 0, hi = n_ovf;  // last q with opre[q] <= k
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (opre[mid] <= k)
+      lo = mid;
+    else
+      hi = mid;
   }
-  wave_add(n_kmers, c);
+  return boff[ovf[lo]] + (k - opre[lo]);
 }
 
 template <typename R>
-__global__ void k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
-                                const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, SkP p,
-                                unsigned long long* __restrict__ gkey, uint32_t* __restrict__ gcnt, uint64_t gmask) {
-  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
-    const uint32_t b = ovf_list[q];
-    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
-      const SK16 r = rec_head(rec[i]);
+__global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
+                               const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
+                               unsigned long long* __restrict__ n_kmers) {
+  unsigned long long c = 0;
+  const uint64_t tot = opre[n_ovf];
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x)
+    c += (uint32_t)(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)].w0 >> 32) & 0xff;
+  wave_add(n_kmers, c);
+}
+
+__device__ __forceinline__ void sk_big_add(unsigned long long* __restrict__ gkey, uint32_t* __restrict__ gcnt,
+                                           uint64_t gmask, uint64_t c, uint64_t s, uint32_t add) {
+  for (;;) {
+    const unsigned long long old = atomicCAS(&gkey[s], ~0ull, (unsigned long long)c);
+    if (old == ~0ull || old == c) {
+      atomicAdd(&gcnt[s], add);
+      return;
+    }
+    s = (s + 1) & gmask;
+  }
+}
+
+// Instances are first summed in a per-workgroup LDS table, flushed once per
+// chunk of kBigChunk records: a K-mer repeated thousands of times (tandem
+// arrays) costs one global atomic per chunk, not one per instance.
+constexpr uint32_t kBigChunk = 256;
+constexpr uint32_t kBigLds = 4096;
+template <typename R>
+__global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
+                                                             const uint32_t* __restrict__ ovf,
+                                                             const uint64_t* __restrict__ opre, uint32_t n_ovf, SkP p,
+                                                             unsigned long long* __restrict__ gkey,
+                                                             uint32_t* __restrict__ gcnt, uint64_t gmask) {
+  constexpr unsigned long long EMPTY = ~0ull;
+  __shared__ unsigned long long lkey[kBigLds];
+  __shared__ uint32_t lcnt[kBigLds];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t s = tid; s < kBigLds; s += kBigChunk) {
+    lkey[s] = EMPTY;
+    lcnt[s] = 0;
+  }
+  __syncthreads();
+  const uint64_t tot = opre[n_ovf];
+  for (uint64_t k0 = (uint64_t)blockIdx.x * kBigChunk; k0 < tot; k0 += (uint64_t)gridDim.x * kBigChunk) {
+    const uint64_t k = k0 + tid;
+    if (k < tot) {
+      const SK16 r = rec_head(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)]);
       const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
       for (uint32_t t = 0; t < n; ++t) {
         const uint64_t c = rec_kmer(r, t, p);
-        uint64_t s = khash(p.hp, c) & gmask;
-        for (;;) {
-          const unsigned long long old = atomicCAS(&gkey[s], ~0ull, (unsigned long long)c);
-          if (old == ~0ull || old == c) {
-            atomicAdd(&gcnt[s], 1u);
+        const uint64_t h = khash(p.hp, c);
+        uint32_t s = (uint32_t)(h >> 40) & (kBigLds - 1);
+        bool done = false;
+        for (uint32_t pr = 0; pr < 64; ++pr, s = (s + 1) & (kBigLds - 1)) {
+          unsigned long long v = lkey[s];
+          if (v == EMPTY) v = atomicCAS(&lkey[s], EMPTY, (unsigned long long)c);
+          if (v == EMPTY || v == c) {
+            atomicAdd(&lcnt[s], 1u);
+            done = true;
             break;
           }
-          s = (s + 1) & gmask;
         }
+        if (!done) sk_big_add(gkey, gcnt, gmask, c, h & gmask, 1u);  // the chunk's LDS table is crowded
       }
     }
+    __syncthreads();
+    for (uint32_t s = tid; s < kBigLds; s += kBigChunk) {
+      const unsigned long long c = lkey[s];
+      if (c != EMPTY) {
+        sk_big_add(gkey, gcnt, gmask, c, khash(p.hp, c) & gmask, lcnt[s]);
+        lkey[s] = EMPTY;
+        lcnt[s] = 0;
+      }
+    }
+    __syncthreads();
   }
 }
 
 // Weak bits of the overflowed buckets' K-mer instances (counts from the
 // global table built by k_sk_big_insert).
 __global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __restrict__ boff,
-                              const uint32_t* __restrict__ ovf_list, uint32_t n_ovf, SkP p,
-                              const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
+                              const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
+                              SkP p, const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
                               uint64_t gmask, uint32_t min_solid, unsigned long long* __restrict__ weak,
                               uint32_t* __restrict__ wrec) {
-  for (uint32_t q = blockIdx.x; q < n_ovf; q += gridDim.x) {
-    const uint32_t b = ovf_list[q];
-    for (uint64_t i = boff[b] + threadIdx.x; i < boff[b + 1]; i += blockDim.x) {
-      const SK24 r = rec[i];
-      const SK16 h = rec_head(r);
-      const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
-      uint32_t m = 0;
-      for (uint32_t t = 0; t < n; ++t) {
-        const uint64_t c = rec_kmer(h, t, p);
-        uint64_t s = khash(p.hp, c) & gmask;
-        while (gkey[s] != c) s = (s + 1) & gmask;
-        if (gcnt[s] < min_solid) {
-          m |= 1u << t;
-          if (!wrec) {
-            const uint64_t x = r.pos + t;
-            atomicOr(&weak[x >> 6], 1ull << (x & 63));
-          }
+  const uint64_t tot = opre[n_ovf];
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x) {
+    const SK24 r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)];
+    const SK16 h = rec_head(r);
+    const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+    uint32_t m = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+      const uint64_t c = rec_kmer(h, t, p);
+      uint64_t s = khash(p.hp, c) & gmask;
+      while (gkey[s] != c) s = (s + 1) & gmask;
+      if (gcnt[s] < min_solid) {
+        m |= 1u << t;
+        if (!wrec) {
+          const uint64_t x = r.pos + t;
+          atomicOr(&weak[x >> 6], 1ull << (x & 63));
         }
       }
-      if (wrec && m) wrec[r.pos] = m;
     }
+    if (wrec && m) wrec[r.pos] = m;
   }
 }
 
@@ -1275,8 +1339,15 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     if (hs[1]) {  // overflowed buckets: one global table
       unsigned long long* nk = gstats + 3;
       APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
-      const uint32_t g2 = (uint32_t)std::min<unsigned long long>(hs[1], (unsigned long long)ctx->n_cu * 8);
-      k_sk_big_kmers<R><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], nk);
+      const uint32_t n_ovf = (uint32_t)hs[1];
+      uint32_t* osz = nullptr;
+      uint64_t* opre = nullptr;
+      APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
+      APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
+      k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovf, n_ovf, osz);
+      APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
+      const uint32_t g2 = (uint32_t)ctx->n_cu * 8;  // persistent: the flattened list's size stays on the device
+      k_sk_big_kmers<R><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
       unsigned long long nbk = 0;
       APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
       APG_TRY(sync(ctx));
@@ -1290,15 +1361,15 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
       vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
       kbegin(ctx, "sk_bucket_global", nbk * 64);
-      k_sk_big_insert<R><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1);
+      k_sk_big_insert<R><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1);
       if (solid)
         k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
       else
         k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
       if constexpr (sizeof(R) == sizeof(SK24)) {
         if (o.weak || o.wrec)
-          k_sk_big_weak<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, (uint32_t)hs[1], p, gkey, gcnt, T - 1,
-                                                      min_solid, o.weak, o.wrec);
+          k_sk_big_weak<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1, min_solid,
+                                                      o.weak, o.wrec);
       }
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
