@@ -1015,25 +1015,53 @@ __global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __re
   }
 }
 
+// Solid K-mers leave through an LDS buffer: one global reservation per
+// kEmitBuf of them (a same-address atomic per wave over half a billion slots
+// serialised: 14.7 ms of the repeats line's solid pass).
+constexpr uint32_t kEmitBuf = 2048;
 template <bool SOLID>
-__global__ void k_sk_big_emit(const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
-                              uint64_t T, SkP p, SkOut o) {
+__global__ void __launch_bounds__(256) k_sk_big_emit(const unsigned long long* __restrict__ gkey,
+                                                     const uint32_t* __restrict__ gcnt, uint64_t T, SkP p, SkOut o) {
   __shared__ uint32_t lhist[kSkHistBins];
-  for (uint32_t i = threadIdx.x; i < kSkHistBins; i += blockDim.x) lhist[i] = 0;
+  __shared__ unsigned long long sbuf[SOLID ? kEmitBuf : 1];
+  __shared__ uint32_t scnt;
+  __shared__ unsigned long long sbase;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kSkHistBins; i += blockDim.x) lhist[i] = 0;
+  if (tid == 0) scnt = 0;
   __syncthreads();
+  auto flush = [&]() {  // block-uniform
+    const uint32_t n = scnt;
+    if (tid == 0) sbase = n ? atomicAdd(&o.gstats[2], (unsigned long long)n) : 0ull;
+    __syncthreads();
+    const unsigned long long b = sbase;
+    for (uint32_t i = tid; i < n; i += blockDim.x)
+      if (b + i < o.solid_cap) o.solid[b + i] = sbuf[i];
+    __syncthreads();
+    if (tid == 0) scnt = 0;
+    __syncthreads();
+  };
   unsigned long long nd = 0;
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < T; s += (uint64_t)gridDim.x * blockDim.x) {
-    if (gkey[s] == ~0ull) continue;
-    sk_spectrum_add(gcnt[s], lhist, o);
-    ++nd;
-    if (SOLID && gcnt[s] >= o.min_solid) {
-      const unsigned long long at = atomicAdd(&o.gstats[2], 1ull);
-      if (at < o.solid_cap) o.solid[at] = khash(p.hp, gkey[s]);
+  for (uint64_t s0 = (uint64_t)blockIdx.x * blockDim.x; s0 < T; s0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t s = s0 + tid;  // block-uniform trip count (the flushes below have barriers)
+    if (s < T && gkey[s] != ~0ull) {
+      const uint32_t c = gcnt[s];
+      sk_spectrum_add(c, lhist, o);
+      ++nd;
+      if (SOLID && c >= o.min_solid) sbuf[atomicAdd(&scnt, 1u)] = khash(p.hp, gkey[s]);
     }
+    if constexpr (SOLID) {
+      __syncthreads();
+      if (scnt > kEmitBuf - blockDim.x) flush();
+    }
+  }
+  if constexpr (SOLID) {
+    __syncthreads();
+    flush();
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
-  for (uint32_t i = threadIdx.x; i < lim; i += blockDim.x)
+  for (uint32_t i = tid; i < lim; i += blockDim.x)
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
 }
