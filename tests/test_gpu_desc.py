@@ -57,3 +57,23 @@ def test_default_matches_oracle(gpu_ctx, inputs):
     h, _ = gpu_ctx.kmer_spectrum(reads, 25)
     ho = oracle.kmer_spectrum(reads, 25, len(h))
     assert np.array_equal(h, ho)
+
+
+def test_reads_past_a_tile_and_past_16_bit_starts(gpu_ctx):
+    """Reads longer than an LDS tile are walked from HBM by one thread; a
+    record starting past base 65535 cannot be described in 16 bits, so its
+    block walks again in the scatter pass.  Spectrum and unipaths = oracle."""
+    from allpathslg_amd import ReadSet
+    from tests.test_gpu_unipath import assert_graph_equal
+
+    g = synth_genome(300_000, 61)
+    rng = np.random.default_rng(62)
+    seqs = [g[:150_000], g[100_000:170_000]]  # 150 kb and 70 kb reads: past 65535 and past a tile
+    for _ in range(3000):
+        s = int(rng.integers(0, len(g) - 200))
+        seqs.append(g[s : s + 200])
+    reads = ReadSet.from_sequences(seqs)
+    h, _ = gpu_ctx.kmer_spectrum(reads, 25)
+    assert np.array_equal(h, oracle.kmer_spectrum(reads, 25, len(h)))
+    got, _ = gpu_ctx.unipaths(reads, 96)
+    assert_graph_equal(got, oracle.unipaths(reads, 96))
