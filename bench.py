@@ -95,7 +95,7 @@ def parse():
     p.add_argument("--gather-nodes", action="store_true",
                    help="sharded path: replicated unipath build (every rank gathers all nodes) instead of the "
                         "sharded compaction")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_v7", "pmc", "traffic.json"),
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_v8", "pmc", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
     return p.parse_args()
 
