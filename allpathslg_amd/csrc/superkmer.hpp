@@ -391,6 +391,7 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
   if constexpr (!LIST) {  // no barriers: each lane walks its own read to its end
     uint32_t cur = Lw ? W.bases.at(0) : 0, nxt = Lw > kSkChunk ? W.bases.at(kSkChunk) : 0;
     uint32_t a, nk, k;
+#pragma unroll 4  // loop control and uniform-branch SALU per base: 7.0 -> 6.45 ms sk_count (8: same)
     for (uint32_t j = 0; j < Lw; ++j) {
       if ((j % kSkChunk) == 0 && j) {
         cur = nxt;
