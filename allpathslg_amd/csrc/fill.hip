@@ -180,136 +180,40 @@ __device__ __forceinline__ uint64_t walk_window(uint64_t atail, unsigned __int12
 // with the full max_steps.  The walk is deterministic, so a pair that ends
 // within the cap ends exactly as it would with the full budget.
 constexpr uint32_t kFillCap1 = 96;
+// A wave refills its idle lanes with new pairs once at most this many lanes
+// are still walking.
+constexpr int kFillRefill = 32;
 
+// One thread per pair, lanes persistent.  The gap walk is a state machine
+// that makes exactly ONE extension lookup per iteration whatever the lane is
+// doing (visiting a node, testing a closure's K-1 bridge K-mers, re-reading
+// an open branch point), so the wave's lanes issue their lookups together: a
+// loop nest (walk step, then the closure test's up to K-2 lookups, then a
+// backtrack lookup) made every lane wait for the longest closure test of
+// each step.  A lane whose pair is done sits idle until the wave refills
+// (wave-aggregated fetch from *next), so a wave is no longer held by its
+// slowest pair.  Per lane the lookups, their order and the result are the
+// same as the nested search (oracle/fill_oracle.c).
 __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
                                               uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
                                               const uint8_t* __restrict__ clean, FillCounters* __restrict__ cnt,
                                               uint32_t cap, const uint32_t* __restrict__ list,
                                               const unsigned long long* __restrict__ list_n,
-                                              uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer) {
+                                              uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer,
+                                              unsigned long long* __restrict__ next) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
   const uint64_t nwork = list ? *list_n : rv.n_pairs;
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwork;
-       k += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t i = list ? list[k] : k;
-    const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
-    const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
-    const uint8_t* A = rv.packed + rv.byte_off[2 * i];
-    const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
-    const uint32_t lo = max(p.min_insert, max(La, Lf));
-    FillRec out{0, 0, 0, 0};
-    uint32_t st;
-    if (La < (uint32_t)K || Lf < (uint32_t)K || (p.max_insert >= La + Lf && p.max_insert - (La + Lf) > kFillMaxGap)) {
-      st = kFillSkip;
-    } else if (!pair_solid(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
-      st = kFillNone;  // S must be a path of solid K-mers: no closure through a weak read K-mer
-    } else {
-      // A's last K-1 bases, MSB-first; F's first 32 bases, LSB-first
-      const uint64_t atail = f_rev2(bases32(A, La - n1) & lmask(n1)) >> (64 - 2 * n1);
-      const uint64_t f0 = fwin(B, Lf, 0);
-      uint32_t n_clos = 0, clos_I = 0, clos_meta = 0;
-      unsigned __int128 clos_pv = 0;
-      bool budget = false;
-      // overlap closures, I ascending (o descending)
-      const uint32_t hi_ov = min(p.max_insert, La + Lf - 1);
-      for (uint32_t I = lo; I <= hi_ov && n_clos < 2; ++I) {
-        const uint32_t o = La + Lf - I;
-        bool match = true;
-        for (uint32_t c = 0; c < o && match; c += 32) {
-          const uint32_t nb = min(32u, o - c);
-          const uint64_t fw = c == 0 ? f0 : fwin(B, Lf, c);
-          match = ((bases32(A, La - o + c) ^ fw) & lmask(nb)) == 0;
-        }
-        if (!match) continue;
-        if (o + 2 <= (uint32_t)K) {  // bridge K-mers: A's tail rolled through F[o, K-1)
-          uint64_t w = atail;
-          for (uint32_t j = 0; j + o + 2 <= (uint32_t)K && match; ++j) {
-            const uint32_t b = (uint32_t)(f0 >> (2 * (o + j))) & 3;
-            match = (ext_succ(t, w, &nlook) >> b) & 1;
-            w = ((w << 2) | b) & t.m1;
-          }
-        }
-        if (match && ++n_clos == 1) {
-          clos_I = I;
-          clos_meta = o << 16;
-        }
-      }
-      // gap closures: depth-first walk, bases A<C<G<T
-      if (n_clos < 2 && p.max_insert >= La + Lf) {
-        const uint32_t gmax = p.max_insert - (La + Lf);
-        const uint32_t dlo = lo > La + Lf ? lo - (La + Lf) : 0;
-        const uint32_t fb0 = (uint32_t)f0 & 3;
-        unsigned __int128 pv = 0;
-        uint64_t brm = 0;  // depths whose node still has unexplored children
-        uint32_t d = 0, steps = 0;
-        for (;;) {
-          const uint64_t w = walk_window(atail, pv, d, t);
-          const uint32_t m = ext_succ(t, w, &nlook);
-          if (d >= dlo && ((m >> fb0) & 1)) {  // closure test: the K-1 bridge K-mers
-            bool ok = true;
-            uint64_t ww = ((w << 2) | fb0) & t.m1;
-            for (int j = 1; j < n1 && ok; ++j) {
-              const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
-              ok = (ext_succ(t, ww, &nlook) >> b) & 1;
-              ww = ((ww << 2) | b) & t.m1;
-            }
-            if (ok && ++n_clos == 1) {
-              clos_I = La + Lf + d;
-              clos_pv = pv;
-              clos_meta = d << 8;
-            }
-            if (n_clos >= 2) break;
-          }
-          bool down = false;
-          if (d < gmax) {
-            if (++steps > cap) {
-              budget = true;
-              break;
-            }
-            if (m) {
-              const uint32_t b = __ffs(m) - 1;
-              if (m >> (b + 1)) brm |= 1ull << d;
-              pv = (pv << 2) | b;
-              ++d;
-              down = true;
-            }
-          }
-          if (down) continue;
-          if (!brm) break;  // search exhausted
-          const uint32_t dd = 63 - __clzll((long long)brm);
-          const unsigned __int128 pv1 = pv >> (2 * (d - dd - 1));
-          const uint32_t b = (uint32_t)pv1 & 3;
-          const unsigned __int128 pvd = pv1 >> 2;
-          const uint32_t m2 = ext_succ(t, walk_window(atail, pvd, dd, t), &nlook);
-          const uint32_t rest = m2 & ~((2u << b) - 1);
-          const uint32_t b2 = __ffs(rest) - 1;  // rest != 0: dd was marked open
-          if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
-          pv = (pvd << 2) | b2;
-          d = dd + 1;
-        }
-      }
-      if (budget && n_clos < 2 && cap < p.max_steps) {  // pass 1: search again with the full budget
-        defer[atomicAdd(ndefer, 1ull)] = (uint32_t)i;
-        continue;
-      }
-      if (n_clos >= 2)
-        st = kFillAmbiguous;
-      else if (budget)
-        st = kFillBudget;
-      else if (n_clos == 0)
-        st = kFillNone;
-      else {
-        st = kFillOk;
-        out.len = clos_I;
-        out.pv_lo = (uint64_t)clos_pv;
-        out.pv_hi = (uint64_t)(clos_pv >> 64);
-      }
-      out.meta = st | clos_meta;
-    }
-    if (st != kFillOk) out.meta = st;
+  // the lane's pair and its search state
+  bool act = false, budget = false;
+  uint64_t i = 0, atail = 0, f0 = 0, brm = 0, ww = 0;
+  uint32_t LaLf = 0, gmax = 0, dlo = 0, fb0 = 0, d = 0, steps = 0, mode = 0, j = 0, mnode = 0, dd = 0;
+  uint32_t n_clos = 0, clos_I = 0, clos_meta = 0;
+  unsigned __int128 pv = 0, clos_pv = 0;
+
+  auto emit = [&](uint32_t st, const FillRec& out) {
     rec[i] = out;
     lens[i] = out.len;
     nbytes[i] = (out.len + 3) >> 2;
@@ -320,6 +224,193 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     c_amb += st == kFillAmbiguous;
     c_bud += st == kFillBudget;
     c_skip += st == kFillSkip;
+  };
+  // closures counted (overlap phase and walk done): status out, or defer
+  auto conclude = [&]() {
+    if (budget && n_clos < 2 && cap < p.max_steps) {  // pass 1: search again with the full budget
+      defer[atomicAdd(ndefer, 1ull)] = (uint32_t)i;
+      return;
+    }
+    FillRec out{0, 0, 0, 0};
+    uint32_t st;
+    if (n_clos >= 2)
+      st = kFillAmbiguous;
+    else if (budget)
+      st = kFillBudget;
+    else if (n_clos == 0)
+      st = kFillNone;
+    else {
+      st = kFillOk;
+      out.len = clos_I;
+      out.pv_lo = (uint64_t)clos_pv;
+      out.pv_hi = (uint64_t)(clos_pv >> 64);
+    }
+    out.meta = st == kFillOk ? st | clos_meta : st;
+    emit(st, out);
+  };
+  // pair i: checks and overlap closures; act = true if the gap walk follows
+  auto start = [&]() {
+    const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
+    const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
+    LaLf = La + Lf;
+    const uint8_t* A = rv.packed + rv.byte_off[2 * i];
+    const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
+    const uint32_t lo = max(p.min_insert, max(La, Lf));
+    if (La < (uint32_t)K || Lf < (uint32_t)K || (p.max_insert >= La + Lf && p.max_insert - (La + Lf) > kFillMaxGap)) {
+      emit(kFillSkip, FillRec{0, 0, 0, kFillSkip});
+      return;
+    }
+    if (!pair_solid(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
+      emit(kFillNone, FillRec{0, 0, 0, kFillNone});  // S must be a path of solid K-mers
+      return;
+    }
+    // A's last K-1 bases, MSB-first; F's first 32 bases, LSB-first
+    atail = f_rev2(bases32(A, La - n1) & lmask(n1)) >> (64 - 2 * n1);
+    f0 = fwin(B, Lf, 0);
+    n_clos = 0;
+    clos_I = 0;
+    clos_meta = 0;
+    clos_pv = 0;
+    budget = false;
+    // overlap closures, I ascending (o descending).  A's suffix [La - o, La)
+    // starts one base later per step: its first 32 bases slide through a
+    // register window fed from a prefetched word (a load per 32 steps, not
+    // three per step); later words only for a matching first word.
+    const uint32_t hi_ov = min(p.max_insert, La + Lf - 1);
+    uint64_t win = 0, nxt = 0;
+    if (lo <= hi_ov) {
+      win = bases32(A, lo - Lf);  // lo >= Lf
+      nxt = bases32(A, lo - Lf + 32);
+    }
+    for (uint32_t I = lo, used = 0; I <= hi_ov && n_clos < 2; ++I) {
+      const uint32_t o = La + Lf - I;
+      bool match = ((win ^ f0) & lmask(min(32u, o))) == 0;
+      win = (win >> 2) | (nxt << 62);  // A[La - o + 1, La - o + 33) for the next I
+      nxt >>= 2;
+      if (++used == 32) {
+        used = 0;
+        nxt = bases32(A, La - o + 33);
+      }
+      for (uint32_t c = 32; c < o && match; c += 32)
+        match = ((bases32(A, La - o + c) ^ fwin(B, Lf, c)) & lmask(min(32u, o - c))) == 0;
+      if (!match) continue;
+      if (o + 2 <= (uint32_t)K) {  // bridge K-mers: A's tail rolled through F[o, K-1)
+        uint64_t w = atail;
+        for (uint32_t jj = 0; jj + o + 2 <= (uint32_t)K && match; ++jj) {
+          const uint32_t b = (uint32_t)(f0 >> (2 * (o + jj))) & 3;
+          match = (ext_succ(t, w, &nlook) >> b) & 1;
+          w = ((w << 2) | b) & t.m1;
+        }
+      }
+      if (match && ++n_clos == 1) {
+        clos_I = I;
+        clos_meta = o << 16;
+      }
+    }
+    if (n_clos < 2 && p.max_insert >= La + Lf) {  // gap closures: depth-first walk, bases A<C<G<T
+      gmax = p.max_insert - (La + Lf);
+      dlo = lo > La + Lf ? lo - (La + Lf) : 0;
+      fb0 = (uint32_t)f0 & 3;
+      pv = 0;
+      brm = 0;  // depths whose node still has unexplored children
+      d = steps = mode = 0;
+      act = true;
+      return;
+    }
+    conclude();
+  };
+  // a closure at depth d (its bridge K-mers all solid); true if the pair is ambiguous
+  auto closure = [&]() {
+    if (++n_clos == 1) {
+      clos_I = LaLf + d;
+      clos_pv = pv;
+      clos_meta = d << 8;
+    }
+    return n_clos >= 2;
+  };
+
+  bool more = true;
+  for (;;) {
+    while (more && __popcll(__ballot(act)) <= kFillRefill) {  // refill the idle lanes (wave-uniform)
+      const uint64_t idle = __ballot(!act);
+      const unsigned long long k = wave_append(next, !act);  // the wave's next popc(idle) work items
+      more = __shfl(k, 63 - __clzll((long long)idle), 64) + 1 < nwork;
+      if (!act && k < nwork) {
+        i = list ? list[k] : k;
+        start();
+      }
+    }
+    if (!__ballot(act)) break;
+    if (!act) continue;
+    // ---- one lookup
+    // mode 2 (open branch point at depth dd < d): the path to it is pv's first dd bases
+    const uint64_t key = mode == 0   ? walk_window(atail, pv, d, t)
+                         : mode == 1 ? ww
+                                     : walk_window(atail, pv >> (2 * (d - dd)), dd, t);
+    const uint32_t m = ext_succ(t, key, &nlook);
+    bool visit = false, done = false;
+    if (mode == 0) {  // node (pv, d)
+      mnode = m;
+      visit = true;
+      if (d >= dlo && ((m >> fb0) & 1)) {  // closure test: the K-1 bridge K-mers
+        if (n1 > 1) {
+          mode = 1;
+          j = 1;
+          ww = ((key << 2) | fb0) & t.m1;
+          visit = false;
+        } else if (closure()) {
+          done = true;
+          visit = false;
+        }
+      }
+    } else if (mode == 1) {  // bridge K-mer j of the closure test at depth d
+      const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
+      const bool ok = (m >> b) & 1;
+      if (ok && (int)j + 1 < n1) {
+        ww = ((ww << 2) | b) & t.m1;
+        ++j;
+      } else if (ok && closure()) {
+        done = true;
+      } else {
+        mode = 0;
+        visit = true;
+      }
+    } else {  // open branch point at depth dd: the sibling after the base taken there
+      const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
+      const uint32_t rest = m & ~((2u << bb) - 1);
+      const uint32_t b2 = __ffs(rest) - 1;  // rest != 0: dd was marked open
+      if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
+      pv = ((pv >> (2 * (d - dd))) << 2) | b2;
+      d = dd + 1;
+      mode = 0;
+    }
+    if (visit) {  // the walk's step from node (pv, d) with successor mask mnode
+      bool down = false;
+      if (d < gmax) {
+        if (++steps > cap) {
+          budget = true;
+          done = true;
+        } else if (mnode) {
+          const uint32_t b = __ffs(mnode) - 1;
+          if (mnode >> (b + 1)) brm |= 1ull << d;
+          pv = (pv << 2) | b;
+          ++d;
+          down = true;
+        }
+      }
+      if (!done && !down) {
+        if (!brm) {
+          done = true;  // search exhausted
+        } else {
+          dd = 63 - __clzll((long long)brm);
+          mode = 2;
+        }
+      }
+    }
+    if (done) {
+      act = false;
+      conclude();
+    }
   }
   wave_add(&cnt->st[kFillOk], c_ok);
   wave_add(&cnt->st[kFillNone], c_none);
@@ -502,17 +593,19 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   uint32_t* defer = nullptr;
   unsigned long long* ndefer = nullptr;
   APG_TRY(workspace_t(ctx, "fill_defer", npc, &defer));
-  APG_TRY(workspace_t(ctx, "fill_ndefer", 1, &ndefer));
-  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, 8, ctx->stream));
+  APG_TRY(workspace_t(ctx, "fill_ndefer", 3, &ndefer));  // deferred count, next pair of pass 1 / pass 2
+  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, 3 * 8, ctx->stream));
   kbegin(ctx, "fill", dr->n_bytes + 16 * dr->n_reads + np * (sizeof(FillRec) + 12));
   if (np) {
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
-    k_fill<<<grid_for(ctx, np), 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
-                                                        std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer,
-                                                        ndefer);
+    // lanes are persistent (work fetched per wave): one resident round of blocks
+    const uint32_t grid = resident_grid(ctx, k_fill, 256, (np + 255) / 256);
+    k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
+                                          std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
+                                          ndefer + 1);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
-      k_fill<<<(uint32_t)ctx->n_cu * 8, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
-                                                               p.max_steps, defer, ndefer, nullptr, nullptr);
+      k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

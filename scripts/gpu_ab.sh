@@ -1,0 +1,25 @@
+#!/bin/bash
+# A/B on one box: selected parity tests, then the bench step with env A and
+# env B (e.g. A="APG_FILL_MEMO=0" B="").  Kernel table of both in the log.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+BA="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0"
+if [ -n "${PYTEST_SEL:-}" ]; then
+  timeout -k 10 ${T_TEST:-400} python -u -m pytest ${PYTEST_SEL} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
+  tail -2 gpurun_out/ab_pytest.log
+fi
+for V in A B; do
+  E="${!V}"
+  env $E timeout -k 10 ${T_BENCH:-400} python bench.py $BA > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
+  echo "== $V ($E)"
+  python - gpurun_out/ab_$V.json <<'PY'
+import json, sys
+b = json.load(open(sys.argv[1]))
+print("value", round(b["value"] / 1e6, 2), "M reads/s  ms/step", round(b["ms_per_step"], 1), "checks", all(b["checks"].values()))
+print("roofline", b["roofline"]["kernel"], round(b["roofline"]["frac"], 3))
+ks = sorted(b["kernels"].items(), key=lambda kv: -kv[1]["ms_per_launch"] * kv[1]["launches"])
+for k, v in ks[:12]:
+    print(f"  {k:24s} {v['ms_per_launch'] * v['launches'] / b['steps']:9.2f} ms/step  {v['GBps']:8.1f} GB/s")
+PY
+done
