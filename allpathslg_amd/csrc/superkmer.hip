@@ -566,10 +566,14 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
 constexpr int kDdThreads = 512;
 constexpr uint64_t kDdBucketKmers = 4096;  // instances per bucket the planner aims for with this kernel
 constexpr uint32_t kDdKTab = 2048;         // K-mer table slots
-constexpr uint32_t kDdTab = 1024;          // record table slots
+// Table sizes keep the block at 51 KiB of LDS and <= 80 VGPRs, so three
+// 512-thread blocks share a CU (at 1024 record slots and 4096 instances, 70 KiB
+// held it to two: 25.5 -> 22.7 ms for the C2 solid count; ~220 distinct
+// records per bucket there, the rest go back through `redo`)
+constexpr uint32_t kDdTab = 512;           // record table slots
 constexpr uint32_t kDdChunks = 4;          // weak mode: records per bucket <= kDdChunks * kDdThreads
 constexpr uint32_t kDdRecCap = kDdChunks * kDdThreads;
-constexpr uint32_t kDdInstCap = 4096;      // distinct-record K-mer instances per bucket
+constexpr uint32_t kDdInstCap = 3072;      // distinct-record K-mer instances per bucket
 constexpr int kDdMinK = kSkBases + 1 - 20;  // records hold <= 20 K-mers (owner-map loop bound)
 
 __device__ __forceinline__ uint64_t rec_fp(const SK16& h) {
@@ -609,7 +613,7 @@ __device__ __forceinline__ uint32_t lds_claim(unsigned long long* tk, uint64_t c
 }
 
 template <bool SOLID, typename R>
-__global__ void __launch_bounds__(kDdThreads) k_sk_bucket_dd(const R* __restrict__ rec,
+__global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu(6))) k_sk_bucket_dd(const R* __restrict__ rec,
                                                              const uint64_t* __restrict__ boff, uint64_t nbuckets,
                                                              SkP p, SkOut o, uint32_t* __restrict__ redo) {
   constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
