@@ -590,7 +590,10 @@ __device__ __forceinline__ unsigned __int128 pc_window(const uint8_t* __restrict
 // the per-read counts places read r's run at [cstart[r], cstart[r] + ccnt[r]),
 // in read order, and a second scan from LDS writes the records.
 constexpr uint32_t kPcTileReads = 256;
-constexpr uint32_t kPcTileQ = 32768;
+// 28 KiB of staged quals (256 reads of <= 112 bases; longer tiles read global
+// memory) and a 1024-entry candidate list keep the block under 40 KiB of LDS:
+// four blocks per CU instead of three
+constexpr uint32_t kPcTileQ = 28672;
 
 template <typename F>
 __device__ __forceinline__ void pc_scan_read(const uint8_t* qb, uint64_t qbase, uint64_t q0, uint32_t L,
@@ -623,7 +626,7 @@ __device__ __forceinline__ bool pc_all_weak_at(const unsigned long long* wb, uin
 }
 
 constexpr uint32_t kPcTileW = kPcTileQ / 64 + 2;  // weak words of a staged tile
-constexpr uint32_t kPcTileList = 2048;            // candidates of a tile written through LDS
+constexpr uint32_t kPcTileList = 1024;            // candidates of a tile written through LDS
 
 template <bool WRITE>
 __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(

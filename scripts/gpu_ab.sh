@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-BA="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0"
+BA="${BA_OVERRIDE:---steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0}"
 if [ -n "${PYTEST_SEL:-}" ]; then
   timeout -k 10 ${T_TEST:-400} python -u -m pytest ${PYTEST_SEL} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
   tail -2 gpurun_out/ab_pytest.log

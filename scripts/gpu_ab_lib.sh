@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-BA="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0"
+BA="${BA_OVERRIDE:---steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0}"
 cp allpathslg_amd/libapg.so /tmp/libapg_B.so
 for V in B A; do
   if [ $V = A ]; then cp allpathslg_amd/libapg_var.so allpathslg_amd/libapg.so; fi
