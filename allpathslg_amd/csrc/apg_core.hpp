@@ -157,7 +157,8 @@ struct apg_ctx {
     int K = 0;
     uint64_t n_nodes = 0, n_unipaths = 0, tmask = 0;
     const void* nodes = nullptr;  // KRec[n_nodes]
-    const uint32_t *idx = nullptr, *head = nullptr, *rank = nullptr, *uoh = nullptr;
+    const unsigned long long* idx = nullptr;  // node index (unipath.hip NodeIdx)
+    const uint32_t *head = nullptr, *rank = nullptr, *uoh = nullptr;
     const uint64_t *ulen = nullptr, *urc = nullptr, *ub_off = nullptr;
     const uint8_t* ub = nullptr;  // unibases, one base per byte
     const uint64_t* uloc = nullptr;  // apg_unipath_locs' (unipath, rank) table of this graph, once built

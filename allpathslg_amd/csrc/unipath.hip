@@ -528,24 +528,40 @@ __global__ void k_digit_starts_u(const uint64_t* __restrict__ omat, uint32_t ndi
   if (d <= ndig) ds[d] = omat[(uint64_t)d * G];
 }
 
-__global__ void k_node_insert(const KRec* __restrict__ nodes, uint64_t N, uint32_t* __restrict__ idx, uint64_t tmask) {
+// Node index: open addressing over 64-bit slots {32 tag bits of the key hash,
+// node id}, linear probing from the hash's low bits.  A probe reads the node
+// record only when the tag matches, so a lookup is one slot read and
+// (almost always) one record read, where id-only slots made every probe of a
+// collision chain a dependent slot + record pair.
+constexpr uint64_t kIdxEmpty = ~0ull;
+__device__ __forceinline__ uint32_t idx_tag(uint64_t h56) { return (uint32_t)(h56 >> 24); }
+
+__global__ void k_node_insert(const KRec* __restrict__ nodes, uint64_t N, unsigned long long* __restrict__ idx,
+                              uint64_t tmask) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t s = (nodes[i].meta >> 8) & tmask;
-    while (atomicCAS(&idx[s], kNone, (uint32_t)i) != kNone) s = (s + 1) & tmask;
+    const uint64_t h = nodes[i].meta >> 8;
+    const unsigned long long want = ((unsigned long long)idx_tag(h) << 32) | i;  // i < 2^31: never empty
+    uint64_t s = h & tmask;
+    while (atomicCAS(&idx[s], kIdxEmpty, want) != kIdxEmpty) s = (s + 1) & tmask;
   }
 }
 
 struct NodeIdx {
   const KRec* nodes;
-  const uint32_t* idx;
+  const unsigned long long* idx;
   uint64_t tmask;
   __device__ __forceinline__ uint32_t find(const K3& k) const {
-    uint64_t s = (key_hash(k) >> 8) & tmask;
+    const uint64_t h = key_hash(k) >> 8;
+    const uint32_t tag = idx_tag(h);
+    uint64_t s = h & tmask;
     for (;;) {
-      const uint32_t i = idx[s];
-      if (i == kNone) return kNone;
-      const KRec& r = nodes[i];
-      if (r.k0 == k.a && r.k1 == k.b && r.k2 == k.c) return i;
+      const unsigned long long e = idx[s];
+      if (e == kIdxEmpty) return kNone;
+      if ((uint32_t)(e >> 32) == tag) {
+        const uint32_t i = (uint32_t)e;
+        const KRec& r = nodes[i];
+        if (r.k0 == k.a && r.k1 == k.b && r.k2 == k.c) return i;
+      }
       s = (s + 1) & tmask;
     }
   }
@@ -1820,9 +1836,9 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   // ---- U4 index --------------------------------------------------------------
   uint64_t T = 1024;
   while (T < 2 * N) T <<= 1;
-  uint32_t* idx = nullptr;
+  unsigned long long* idx = nullptr;
   APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
-  APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 4, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 8, ctx->stream));
   kbegin(ctx, "u_node_insert", N * 40);
   k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, N, idx, T - 1);
   kend(ctx);
