@@ -424,10 +424,12 @@ __device__ __forceinline__ uint32_t packed_base(const uint8_t* r, uint32_t i) { 
 
 // Filled fragments out: kFillWLanes lanes per pair, lane l writes output
 // bytes l, l + kFillWLanes, ... (4 bases each), so a wave's stores cover
-// contiguous 16-byte runs of four fragments instead of 64 byte-by-byte
-// streams.  S = A ++ F[ov, Lf) (overlap closure) or A ++ path[0, d) ++ F
-// (gap closure, ov = 0), F = rc(B).
-constexpr uint32_t kFillWLanes = 16;
+// contiguous 4-byte runs of 16 fragments.  A wave serves 16 pairs at once:
+// the per-pair chain of dependent loads (record, scans, offsets) is what
+// bounds the kernel, and 16 lanes per pair (4 pairs per wave) took 3.9 ms
+// for the C2 step against 2.7 ms here.  S = A ++ F[ov, Lf) (overlap closure)
+// or A ++ path[0, d) ++ F (gap closure, ov = 0), F = rc(B).
+constexpr uint32_t kFillWLanes = 4;
 
 __global__ void __launch_bounds__(256) k_fill_write(FillReads rv, const FillRec* __restrict__ rec,
                                                     const uint64_t* __restrict__ bscan,
