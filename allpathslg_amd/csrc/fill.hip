@@ -272,39 +272,55 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     clos_meta = 0;
     clos_pv = 0;
     budget = false;
-    // overlap closures, I ascending (o descending).  A's suffix [La - o, La)
-    // starts one base later per step: its first 32 bases slide through a
-    // register window fed from a prefetched word (a load per 32 steps, not
-    // three per step); later words only for a matching first word.
+    // overlap closures, I ascending (o descending): A's suffix [s, La) with
+    // s = La - o = I - Lf against F's prefix.  Candidate offsets come 32 at a
+    // time from a bit-parallel filter — A's bases at s .. s+3 equal F's first
+    // four (one bit per offset from four XOR / OR / AND masks over a word of
+    // A) — and only candidates get the exact word compare; the ~1 in 256
+    // offsets that pass by chance cost a compare each.  Offsets with o < 4
+    // skip the filter.  A per-offset loop (a sliding 32-base window) cost
+    // ~40 % of the kernel.
     const uint32_t hi_ov = min(p.max_insert, La + Lf - 1);
-    uint64_t win = 0, nxt = 0;
     if (lo <= hi_ov) {
-      win = bases32(A, lo - Lf);  // lo >= Lf
-      nxt = bases32(A, lo - Lf + 32);
-    }
-    for (uint32_t I = lo, used = 0; I <= hi_ov && n_clos < 2; ++I) {
-      const uint32_t o = La + Lf - I;
-      bool match = ((win ^ f0) & lmask(min(32u, o))) == 0;
-      win = (win >> 2) | (nxt << 62);  // A[La - o + 1, La - o + 33) for the next I
-      nxt >>= 2;
-      if (++used == 32) {
-        used = 0;
-        nxt = bases32(A, La - o + 33);
-      }
-      for (uint32_t c = 32; c < o && match; c += 32)
-        match = ((bases32(A, La - o + c) ^ fwin(B, Lf, c)) & lmask(min(32u, o - c))) == 0;
-      if (!match) continue;
-      if (o + 2 <= (uint32_t)K) {  // bridge K-mers: A's tail rolled through F[o, K-1)
-        uint64_t w = atail;
-        for (uint32_t jj = 0; jj + o + 2 <= (uint32_t)K && match; ++jj) {
-          const uint32_t b = (uint32_t)(f0 >> (2 * (o + jj))) & 3;
-          match = (ext_succ(t, w, &nlook) >> b) & 1;
-          w = ((w << 2) | b) & t.m1;
+      constexpr uint64_t r0 = 0x5555555555555555ull;  // low bit of every base
+      const uint32_t s_lo = lo - Lf, s_hi = hi_ov - Lf;  // lo >= Lf
+      const uint32_t s_f = La > 3 ? La - 3 : 0;        // offsets from here on have o < 4
+      const uint64_t c0 = (f0 & 3) * r0, c1 = ((f0 >> 2) & 3) * r0, c2 = ((f0 >> 4) & 3) * r0,
+                     c3 = ((f0 >> 6) & 3) * r0;
+      auto eqm = [](uint64_t x, uint64_t c) {  // bases of x equal to c's: their low bits
+        const uint64_t y = x ^ c;
+        return ~(y | (y >> 1)) & r0;
+      };
+      auto from = [](uint32_t t) { return t >= 32 ? 0ull : ~((1ull << (2 * t)) - 1) & r0; };  // offsets >= t
+      uint32_t wb = s_lo & ~31u;
+      uint64_t cur = bases32(A, wb);
+      for (; wb <= s_hi && n_clos < 2; wb += 32) {
+        const uint64_t nx = bases32(A, wb + 32);
+        uint64_t m = eqm(cur, c0) & eqm((cur >> 2) | (nx << 62), c1) & eqm((cur >> 4) | (nx << 60), c2) &
+                     eqm((cur >> 6) | (nx << 58), c3);
+        m |= from(s_f > wb ? s_f - wb : 0);                                 // o < 4: unfiltered
+        m &= from(s_lo > wb ? s_lo - wb : 0) & ~from(s_hi - wb + 1);        // [s_lo, s_hi]
+        cur = nx;
+        for (; m && n_clos < 2; m &= m - 1) {
+          const uint32_t sft = wb + (uint32_t)(__builtin_ctzll(m) >> 1);
+          const uint32_t o = La - sft, I = Lf + sft;
+          bool match = true;
+          for (uint32_t c = 0; c < o && match; c += 32)
+            match = ((bases32(A, sft + c) ^ (c == 0 ? f0 : fwin(B, Lf, c))) & lmask(min(32u, o - c))) == 0;
+          if (!match) continue;
+          if (o + 2 <= (uint32_t)K) {  // bridge K-mers: A's tail rolled through F[o, K-1)
+            uint64_t w = atail;
+            for (uint32_t jj = 0; jj + o + 2 <= (uint32_t)K && match; ++jj) {
+              const uint32_t b = (uint32_t)(f0 >> (2 * (o + jj))) & 3;
+              match = (ext_succ(t, w, &nlook) >> b) & 1;
+              w = ((w << 2) | b) & t.m1;
+            }
+          }
+          if (match && ++n_clos == 1) {
+            clos_I = I;
+            clos_meta = o << 16;
+          }
         }
-      }
-      if (match && ++n_clos == 1) {
-        clos_I = I;
-        clos_meta = o << 16;
       }
     }
     if (n_clos < 2 && p.max_insert >= La + Lf) {  // gap closures: depth-first walk, bases A<C<G<T
