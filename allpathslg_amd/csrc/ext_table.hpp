@@ -55,14 +55,30 @@ struct ExtTab {
   int n1;  // K-1
 };
 
+// Probing starts at the first slot of the key's aligned group of kExtGrp
+// slots (32 bytes) and runs linearly from there, so a lookup reads the group
+// at once (two 16-byte loads in flight together) and almost always finds the
+// key, or the empty slot that proves it absent, in it: one memory round trip
+// per lookup, where slot-by-slot probing paid a second one for every key not
+// in its home slot — and a wave waits for its slowest lane.
+constexpr uint64_t kExtGrp = 4;
+__device__ __forceinline__ uint64_t ext_home(const ExtTab& t, uint64_t c) {
+  return khash(t.h1, c) & t.mask & ~(kExtGrp - 1);
+}
+
 // The 8 extension bits of canonical (K-1)-mer c (0 if absent).
 __device__ __forceinline__ uint32_t ext_bits(const ExtTab& t, uint64_t c) {
-  uint64_t s = khash(t.h1, c) & t.mask;
+  uint64_t g = ext_home(t, c);
   for (;;) {
-    const unsigned long long v = t.slot[s];
-    if (v == kExtEmpty) return 0;
-    if ((v >> 8) == c) return (uint32_t)(v & 0xff);
-    s = (s + 1) & t.mask;
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t.slot + g);
+    const ulonglong2 a = q[0], b = q[1];
+    const unsigned long long v[kExtGrp] = {a.x, a.y, b.x, b.y};
+#pragma unroll
+    for (uint32_t j = 0; j < kExtGrp; ++j) {
+      if (v[j] == kExtEmpty) return 0;
+      if ((v[j] >> 8) == c) return (uint32_t)(v[j] & 0xff);
+    }
+    g = (g + kExtGrp) & t.mask;
   }
 }
 

@@ -38,7 +38,7 @@ constexpr uint32_t kFillMaxGap = 63;
 
 __device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
   const unsigned long long want = (key << 8) | bit;
-  uint64_t s = khash(t.h1, key) & t.mask;
+  uint64_t s = ext_home(t, key);  // linear from the aligned group (ext_bits reads it whole)
   for (;;) {
     unsigned long long v = t.slot[s];
     if (v == kExtEmpty) {
