@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
     const uint64_t pos = OutWantsPos<O>::value ? rv.base_off[t0 + q] + a : 0;  // the read's first base + a
     rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
   };
-  if (sk_replay<kSkThreads>(dd, rv, r0, r1, T, t0, f)) return;  // the count pass's descriptors
+  if (dd.desc && !dd.flag[b]) return;  // k_sk_replay wrote this block's records
   while (t0 < r1) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n)
@@ -192,6 +192,102 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
     else
       sk_walk_global<kSkThreads, false>(rv, p, T, t0, sbuf + threadIdx.x, f);
     __syncthreads();
+    t0 += n ? n : 1;
+  }
+}
+
+// The scatter of the blocks whose count pass kept descriptors (the walk
+// kernel above takes the flagged rest): no van Herk column or record list, so
+// 14 KiB of LDS per block instead of ~30.  Per tile, the descriptor count,
+// the reads' first-base positions and the first batch of descriptors are
+// loaded while the tile streams in; each lane then builds its records from
+// the LDS tile (ds_read, no generic-pointer loads), positions from LDS, with
+// kSkReplayBatch descriptor loads in flight instead of one dependent chain
+// per record.
+constexpr uint32_t kSkReplayBatch = 4;
+template <typename O>
+__global__ void __launch_bounds__(kSkThreads) k_sk_replay(SkReads rv, SkP p, int D, const uint64_t* __restrict__ omat,
+                                                          O out, SkDesc dd) {
+  constexpr bool WP = OutWantsPos<O>::value;
+  constexpr uint32_t NT = kSkThreads;
+  __shared__ SkTile<kSkThreads> T;
+  __shared__ unsigned long long cur[256];
+  __shared__ uint64_t tpos[WP ? NT : 1];
+  const uint32_t ndig = 1u << D;
+  const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  if (!dd.desc || dd.flag[b]) return;  // block-uniform: k_sk_scatter walks this block
+  for (uint32_t d = tid; d < ndig; d += NT) cur[d] = omat[(uint64_t)d * G + b];
+  uint64_t r0, r1;
+  sk_read_range(rv.n_reads, G, b, &r0, &r1);
+  uint64_t off = dd.lo(rv, r0);
+  uint64_t dq[kSkReplayBatch];
+  auto load_batch = [&](uint64_t i0) {
+#pragma unroll
+    for (uint32_t u = 0; u < kSkReplayBatch; ++u) {
+      const uint64_t i = off + i0 + u * NT + tid;
+      dq[u] = i < dd.slots ? dd.desc[i] : 0;  // past the tile's count: unused
+    }
+  };
+  // one record from its descriptor; bases from the LDS tile at bit `bit0`,
+  // or (tile of one over-long read) from HBM
+  auto emit = [&](uint64_t d, uint32_t n_tile, const uint8_t* g) {
+    const uint32_t q = (uint32_t)(d >> 56), a = (uint32_t)(d >> 32) & 0xffffu, nk = (uint32_t)(d >> 48) & 0xffu;
+    SK16 x;
+    if (n_tile) {
+      const uint32_t nb = nk + (uint32_t)p.K - 1;  // <= 40
+      const uint32_t bo = T.rbo[q] * 8 + 2 * a;
+      const uint32_t i = bo >> 5, s = bo & 31;
+      const uint32_t w0 = T.words[i], w1 = T.words[i + 1], w2 = T.words[i + 2], w3 = T.words[i + 3];
+      uint64_t lo = (uint64_t)__builtin_amdgcn_alignbit(w1, w0, s) | ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, s) << 32);
+      uint64_t hi = __builtin_amdgcn_alignbit(w3, w2, s);
+      if (nb < 32) lo &= (1ull << (2 * nb)) - 1;
+      hi = nb > 32 ? hi & ((1ull << (2 * (nb - 32))) - 1) : 0;
+      x.w0 = (uint64_t)part_key((uint32_t)d) | ((uint64_t)nk << 32) | ((lo & 0xffffull) << 48);
+      x.w1 = (lo >> 16) | (hi << 48);
+    } else {
+      x = make_rec(g, a, nk, (uint32_t)d, p.K);
+    }
+    const uint32_t dg = D ? (uint32_t)x.w0 >> (32 - D) : 0;
+    uint64_t pos = 0;
+    if constexpr (WP) pos = tpos[q] + a;
+    // the wave's lanes of one digit take consecutive slots through one
+    // cursor add by the lowest of them (D ballots find the peers): ~2^D
+    // distinct-address atomics per wave instead of 64 on 2^D addresses
+    uint64_t peers = __ballot(1);
+    for (int k = 0; k < D; ++k) {
+      const uint64_t bk = __ballot((dg >> k) & 1u);
+      peers &= ((dg >> k) & 1u) ? bk : ~bk;
+    }
+    const uint32_t ln = __lane_id();
+    const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << ln) - 1));
+    const int leader = __ffsll((long long)peers) - 1;
+    unsigned long long base = 0;
+    if (rank == 0) base = atomicAdd(&cur[dg], (unsigned long long)__popcll(peers));
+    const uint32_t blo = (uint32_t)__shfl((int)(uint32_t)base, leader, 64);
+    const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)(base >> 32), leader, 64);
+    rec_put(out, (((uint64_t)bhi << 32) | blo) + rank, x, pos);
+  };
+  for (uint64_t t0 = r0; t0 < r1;) {
+    const uint32_t c = dd.tcnt[t0];
+    uint64_t pb = 0;
+    if constexpr (WP) {
+      if (t0 + tid < r1) pb = rv.base_off[t0 + tid];
+    }
+    load_batch(0);
+    const uint32_t n = sk_load_tile(rv, t0, r1, T);  // ends with a barrier
+    if constexpr (WP) {
+      if (tid < (n ? n : 1u)) tpos[tid] = pb;
+      __syncthreads();
+    }
+    const uint8_t* g = n ? nullptr : rv.packed + rv.byte_off[t0];  // a read too long for a tile: from HBM
+    for (uint32_t i0 = 0; i0 < c; i0 += kSkReplayBatch * NT) {  // block-uniform
+      if (i0) load_batch(i0);
+#pragma unroll
+      for (uint32_t u = 0; u < kSkReplayBatch; ++u)
+        if (i0 + u * NT + tid < c) emit(dq[u], n, g);
+    }
+    off += c;
+    __syncthreads();  // the next tile overwrites T and tpos
     t0 += n ? n : 1;
   }
 }
@@ -1170,8 +1266,13 @@ static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out,
   SkDesc dd{nullptr, nullptr, nullptr, kSkDescDiv, 0};
   if (s.desc) APG_TRY(sk_desc_bufs(ctx, dr, s.G, &dd));
   kbegin(ctx, "sk_scatter", dr->n_bytes + 16 * dr->n_reads + s.total * (out_bytes + (dd.desc ? 8 : 0)));
-  if (dr->n_reads)
+  if (dr->n_reads) {
+    // k_sk_replay: the blocks with descriptors (15.7 -> 13.3 ms for the two
+    // scatters of the C2 step against the walk kernel's replay); k_sk_scatter
+    // walks the flagged rest (all blocks when descriptors are off)
+    if (dd.desc) k_sk_replay<O><<<s.G, kSkThreads, 0, ctx->stream>>>(rv, p, D, omat, out, dd);
     k_sk_scatter<O><<<s.G, kSkThreads, (size_t)p.w * kSkThreads * 4, ctx->stream>>>(rv, p, D, omat, out, dd);
+  }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;
