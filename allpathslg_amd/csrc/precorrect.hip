@@ -1091,17 +1091,32 @@ __global__ void __launch_bounds__(256) k_ecj_trim(EcjReads rv, ExtTab et, int K,
     const uint8_t* rd = rv.packed + rv.byte_off[r];
     uint32_t k = 0;
     if (L >= (uint32_t)K) {
+      // One lookup per two K-mers: the (K-1)-mer at i+1 answers K-mer i by
+      // its predecessor bit for base i and K-mer i+1 by its successor bit for
+      // base i+K (ext_table.hpp).  i = the first non-solid K-mer, or nk.
       const int n1 = K - 1;
-      uint64_t y = 0;  // (K-1)-mer at i, LSB-first: base i+t at bits 2t
-      for (int t = 0; t < n1; ++t) y |= (uint64_t)((rd[t >> 2] >> (2 * (t & 3))) & 3) << (2 * t);
+      auto base = [&](uint32_t x) -> uint32_t { return (rd[x >> 2] >> (2 * (x & 3))) & 3; };
+      uint64_t y = 0;  // (K-1)-mer at i+1, LSB-first: base i+1+t at bits 2t
+      for (int t = 0; t < n1; ++t) y |= (uint64_t)base(1 + t) << (2 * t);
       const uint32_t nk = L - K + 1;
       uint32_t i = 0;
-      for (; i < nk; ++i) {
-        const uint32_t p = i + n1;
-        const uint32_t b = (rd[p >> 2] >> (2 * (p & 3))) & 3;
+      for (; i < nk; i += 2) {
         ++looks;
-        if (!((ext_masks_lsb(et, y) >> 4) & (1u << b))) break;
-        y = (y >> 2) | ((uint64_t)b << (2 * (n1 - 1)));
+        const uint32_t m = ext_masks_lsb(et, y);
+        if (!(m & (1u << base(i)))) break;
+        if (i + 1 >= nk) {
+          i = nk;
+          break;
+        }
+        const uint32_t bs = base(i + (uint32_t)K);
+        if (!((m >> 4) & (1u << bs))) {
+          i += 1;
+          break;
+        }
+        if (i + 2 < nk) {
+          y = (y >> 2) | ((uint64_t)bs << (2 * (n1 - 1)));
+          y = (y >> 2) | ((uint64_t)base(i + (uint32_t)K + 1) << (2 * (n1 - 1)));
+        }
       }
       k = i == nk ? L : i + (uint32_t)n1;
       if (k < min_keep) k = 0;
