@@ -1179,9 +1179,13 @@ static int sk_ceil_log2(uint64_t x) {
 // costlier of the pair; k_sk_count must use the same grid for the offsets),
 // so the last round is not a partial one.
 static uint32_t sk_blocks(const apg_ctx* ctx, uint64_t n_reads, const SkP& p) {
+  // two full rounds of the count kernel's resident blocks (7 per CU at K=24-25;
+  // sized by the walk kernel's 5 the count ran 1.4 rounds: 13.0 -> 12.1 ms;
+  // the descriptor replay that follows is lighter per block)
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sk_scatter<SK24*>, kSkThreads,
-                                                   (size_t)p.w * kSkThreads * 4) != hipSuccess || occ < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sk_count, kSkThreads, (size_t)p.w * kSkThreads * 4) !=
+          hipSuccess ||
+      occ < 1)
     occ = 4;
   const uint64_t cap = std::min<uint64_t>(kSkMaxBlocks, (uint64_t)std::max(ctx->n_cu, 1) * occ * 2);
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, (n_reads + 255) / 256));
