@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "apg_core.hpp"
+#include "exchange.hpp"
 #include "kmer_common.hpp"
 
 namespace apg {
@@ -513,8 +514,12 @@ constexpr uint32_t kVoteChunk = 128;
 constexpr uint32_t kVoteWin = 2048;        // columns x 4 u32 counters = 32 KiB of LDS
 constexpr uint32_t kVoteStride = kVoteWin + 1;  // one counter plane per base, planes offset by one bank
 
+// Only columns [c0, c1) are counted, into votes[(column - c0) * 4 + base]:
+// the whole target set in one plane (c0 = 0, c1 = columns), or one chunk of
+// it at a time (apg_sharded_consensus bounds its planes that way).
 __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, const AlnPair* __restrict__ plc,
-                                                        uint64_t n, uint32_t* __restrict__ votes) {
+                                                        uint64_t n, uint64_t c0, uint64_t c1,
+                                                        uint32_t* __restrict__ votes) {
   // plane-major counters win[b * kVoteStride + column]: a wave's lanes vote
   // on consecutive columns, mostly for the same base, so their LDS atomics hit
   // consecutive banks (column-major [column][4] was a 4-way bank conflict)
@@ -554,11 +559,12 @@ __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, cons
     auto vote = [&](const VoteMeta& m, int64_t i, uint32_t b, uint32_t qq) {
       const uint64_t col = m.col0 + (uint64_t)i;
       const uint64_t d = col - g0;  // wraps (huge) when col < g0
+      if (col - c0 >= c1 - c0) return;  // outside this plane (also col < c0: wraps)
       if (d < kVoteWin) {
         atomicAdd(&win[b * kVoteStride + d], qq);
         myspan = std::max<uint32_t>(myspan, (uint32_t)d + 1);
       } else {
-        atomicAdd(&votes[col * 4 + b], qq);
+        atomicAdd(&votes[(col - c0) * 4 + b], qq);
       }
     };
     auto fetch = [&](const VoteMeta& m, int64_t i, uint32_t* b, uint32_t* qq) {
@@ -593,17 +599,18 @@ __global__ void __launch_bounds__(kVoteThreads) k_votes(SeqSet R, SeqSet T, cons
     for (uint32_t x = tid; x < sp * 4; x += kVoteThreads) {  // x = column * 4 + base: coalesced global atomics
       const uint32_t w = (x & 3) * kVoteStride + (x >> 2);
       const uint32_t v = win[w];
-      if (v) {
-        atomicAdd(&votes[g0 * 4 + x], v);
+      if (v) {  // only in-plane votes reach the window: g0 + x / 4 lies in [c0, c1)
+        atomicAdd(&votes[(g0 - c0) * 4 + x], v);
         win[w] = 0;
       }
     }
   }
 }
 
-__global__ void k_decide(SeqSet T, uint64_t n_targets, uint64_t NT, const uint32_t* __restrict__ votes,
+// columns [c0, c1) from the plane of k_votes(c0, c1)
+__global__ void k_decide(SeqSet T, uint64_t n_targets, uint64_t c0, uint64_t c1, const uint32_t* __restrict__ votes,
                          uint8_t* __restrict__ cons, uint8_t* __restrict__ cq) {
-  for (uint64_t col = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; col < NT;
+  for (uint64_t col = c0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; col < c1;
        col += (uint64_t)gridDim.x * blockDim.x) {
     // target of this column: binary search over base_off
     uint64_t lo = 0, hi = n_targets;
@@ -615,7 +622,7 @@ __global__ void k_decide(SeqSet T, uint64_t n_targets, uint64_t NT, const uint32
         hi = mid;
     }
     const uint32_t tbase = abase(T.packed + T.byte_off[lo], (uint32_t)(col - T.base_off[lo]));
-    const uint4 v4 = reinterpret_cast<const uint4*>(votes)[col];
+    const uint4 v4 = reinterpret_cast<const uint4*>(votes)[col - c0];
     const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
     uint32_t win = tbase;
     for (uint32_t b = 0; b < 4; ++b)
@@ -788,13 +795,55 @@ int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T, co
   kbegin(ctx, "consensus_votes", n * 16 + R->n_bytes + R->n_bases);
   if (n)
     k_votes<<<resident_grid(ctx, k_votes, kVoteThreads, (n + kVoteChunk - 1) / kVoteChunk), kVoteThreads, 0,
-              ctx->stream>>>(seqset(R), seqset(T), reinterpret_cast<const AlnPair*>(d_plc), n, votes);
+              ctx->stream>>>(seqset(R), seqset(T), reinterpret_cast<const AlnPair*>(d_plc), n, 0, NT, votes);
   kend(ctx);
   kbegin(ctx, "consensus_decide", NT * 18);
   if (NT)
-    k_decide<<<grid_for(ctx, NT), 256, 0, ctx->stream>>>(seqset(T), T->n_reads, NT, votes, d_bases, d_quals);
+    k_decide<<<grid_for(ctx, NT), 256, 0, ctx->stream>>>(seqset(T), T->n_reads, 0, NT, votes, d_bases, d_quals);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
+  return sync(ctx);
+}
+
+// Sharded consensus (SURVEY §8e "alignment": unibases replicated, reads
+// sharded): each rank's placements vote into a plane of the replicated
+// targets' columns, the planes are summed over the ranks (RCCL allreduce),
+// and every rank decides every column.  The plane covers at most
+// 2^28 columns (4 GiB) at a time: larger target sets are voted chunk by chunk,
+// each chunk a pass over the placements restricted to its columns.
+int apg_sharded_consensus(apg_ctx* ctx, apg_comm* comm, const apg_dreads* R, const apg_dreads* T,
+                          const apg_aln_pair* d_plc, uint64_t n, uint8_t* d_bases, uint8_t* d_quals) {
+  APG_REQUIRE(ctx && comm && R && T, "apg_sharded_consensus: NULL argument");
+  Comm* c = comm_of(comm);
+  APG_REQUIRE(c && c->ctx == ctx, "apg_sharded_consensus: the communicator belongs to another context");
+  APG_REQUIRE(n == 0 || d_plc, "apg_sharded_consensus: NULL placements");
+  APG_REQUIRE(n == 0 || R->d_quals, "apg_sharded_consensus: the placed reads need qualities");
+  APG_REQUIRE(T->n_bases == 0 || (d_bases && d_quals), "apg_sharded_consensus: NULL outputs");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  const uint64_t NT = T->n_bases;
+  // every rank must hold the same targets: the planes are summed column by column
+  uint64_t shape[2] = {NT, T->n_reads}, mx[2] = {NT, T->n_reads};
+  APG_TRY(c->allreduce_u64(mx, 2, APG_COMM_MAX));
+  APG_REQUIRE(mx[0] == shape[0] && mx[1] == shape[1], "apg_sharded_consensus: ranks hold different target sets");
+  static const uint64_t kChunk = getenv("APG_CONS_CHUNK") ? strtoull(getenv("APG_CONS_CHUNK"), nullptr, 10) : (1ull << 28);
+  const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(NT, kChunk));
+  uint32_t* votes = nullptr;
+  APG_TRY(workspace_t(ctx, "a_votes", std::max<uint64_t>(4 * chunk, 4), &votes));
+  for (uint64_t c0 = 0; c0 < NT; c0 += chunk) {
+    const uint64_t c1 = std::min(NT, c0 + chunk);
+    APG_CHECK_HIP(hipMemsetAsync(votes, 0, (c1 - c0) * 16, ctx->stream));
+    kbegin(ctx, "consensus_votes", n * 16 + R->n_bytes + R->n_bases);
+    if (n)
+      k_votes<<<resident_grid(ctx, k_votes, kVoteThreads, (n + kVoteChunk - 1) / kVoteChunk), kVoteThreads, 0,
+                ctx->stream>>>(seqset(R), seqset(T), reinterpret_cast<const AlnPair*>(d_plc), n, c0, c1, votes);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    APG_TRY(c->allreduce_dev_u32(votes, 4 * (c1 - c0)));
+    kbegin(ctx, "consensus_decide", (c1 - c0) * 18);
+    k_decide<<<grid_for(ctx, c1 - c0), 256, 0, ctx->stream>>>(seqset(T), T->n_reads, c0, c1, votes, d_bases, d_quals);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+  }
   return sync(ctx);
 }
 

@@ -162,6 +162,13 @@ struct apg_ctx {
     const uint64_t *ulen = nullptr, *urc = nullptr, *ub_off = nullptr;
     const uint8_t* ub = nullptr;  // unibases, one base per byte
     const uint64_t* uloc = nullptr;  // apg_unipath_locs' (unipath, rank) table of this graph, once built
+    // sharded compaction (apg_sharded_unipaths): nodes / idx / n_nodes are this
+    // rank's shard only; vu / vr give each local directed node its (unipath,
+    // rank); unipath arrays and unibases are the replicated global ones
+    bool sharded = false;
+    const uint32_t *vu = nullptr, *vr = nullptr;
+    const void* comm = nullptr;  // the communicator of the sharded build (identity only)
+    int n_shards = 1;
   } gstate;
 
   // Solid K-mer list of the last apg_shard_solid ("pc_solid" workspace).

@@ -16,9 +16,12 @@
 //   ...     payload         fastb: packed 2-bit bases, each read byte-aligned
 //                           (byte_off[i] = sum_{j<i} ceil(len_j/4));
 //                           qualb: one Phred byte per base
+#include <sys/stat.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -94,9 +97,20 @@ int read_header(FILE* f, const char* magic, const char* path, uint64_t* n, uint6
   if (std::fread(n, 8, 1, f) != 1 || std::fread(total, 8, 1, f) != 1)
     return io_fail(std::string("truncated header in ") + path);
   if (*n > (1ull << 40)) return io_fail(std::string("implausible read count in ") + path);
-  base_off->resize(*n + 1);
+  // the offset table must fit in the file before it is allocated: a corrupt
+  // count fails here instead of in a multi-terabyte resize
+  struct stat sb;
+  if (fstat(fileno(f), &sb) != 0) return io_fail(std::string("cannot stat ") + path);
+  if (32 + 8 * (*n + 1) > (uint64_t)sb.st_size) return io_fail(std::string("truncated offsets in ") + path);
+  try {
+    base_off->resize(*n + 1);
+  } catch (const std::bad_alloc&) {
+    return io_fail(std::string("offset table of ") + path + " does not fit in host memory");
+  }
   if (std::fread(base_off->data(), 8, *n + 1, f) != *n + 1)
     return io_fail(std::string("truncated offsets in ") + path);
+  // kernels index qualities by the absolute base offset: the table starts at 0
+  if ((*base_off)[0] != 0) return io_fail(std::string("offset table does not start at 0 in ") + path);
   if ((*base_off)[*n] != *total) return io_fail(std::string("offset table/total mismatch in ") + path);
   for (uint64_t i = 0; i < *n; ++i)
     if ((*base_off)[i + 1] < (*base_off)[i]) return io_fail(std::string("non-monotone offsets in ") + path);

@@ -104,6 +104,24 @@ const char kDb[8] = {'A', 'P', 'G', 'D', 'B', 0, 0, 0};
 
 extern "C" {
 
+// The library-allocated arrays of a graph (host memory; apg_unipaths,
+// apg_sharded_unipaths, apg_graph_read).
+void apg_unipath_graph_free(apg_unipath_graph* g) {
+  if (!g) return;
+  std::free(g->len);
+  std::free(g->id_base);
+  std::free(g->rc);
+  std::free(g->ub_off);
+  std::free(g->unibases);
+  std::free(g->from);
+  std::free(g->to);
+  std::free(g->path_off);
+  std::free(g->path_start);
+  std::free(g->path_len);
+  std::memset(g, 0, sizeof(*g));
+}
+
+
 int apg_kmerpaths_write(const char* path, int K, uint64_t n_paths, const uint64_t* path_off, const uint64_t* start,
                         const uint64_t* len) {
   if (!path || !path_off) return APG_E_ARG;

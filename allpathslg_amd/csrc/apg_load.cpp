@@ -131,8 +131,13 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
   std::thread qt;
   if (qualb)
     qt = std::thread([&] {
-      qrc = fmt_read_head(qualb, true, &nq, &qo, &qpay);
-      if (qrc) qerr = apg_last_error();
+      try {  // nothing may escape a worker thread (std::terminate)
+        qrc = fmt_read_head(qualb, true, &nq, &qo, &qpay);
+        if (qrc) qerr = apg_last_error();
+      } catch (const std::exception& e) {
+        qrc = APG_E_NOMEM;
+        qerr = std::string("reading ") + qualb + ": " + e.what();
+      }
     });
   std::vector<uint64_t> yo(n + 1);
   int rc0 = apg_byte_offsets(bo.data(), n, yo.data());

@@ -52,7 +52,7 @@ typedef struct {
 } NcclId;
 typedef void* NcclComm;
 enum { kNcclSuccess = 0, kNcclInProgress = 7 };
-enum { kNcclUint8 = 1, kNcclUint64 = 5 };  // ncclDataType_t values (rccl.h)
+enum { kNcclUint8 = 1, kNcclUint32 = 3, kNcclUint64 = 5 };  // ncclDataType_t values (rccl.h)
 enum { kNcclSum = 0, kNcclMax = 3 };       // ncclRedOp_t values
 
 struct Nccl {
@@ -150,25 +150,57 @@ struct RcclComm : Comm {
     return APG_OK;
   }
 
-  // every peer's segments in one group: pieces of at most kPiece bytes
+  // every peer's segments in one group: pieces of at most kPiece bytes.  A
+  // failed Send / Recv still closes the group (an open group would swallow
+  // the communicator's next calls).
   int p2p(const uint8_t* send, const uint64_t* sb, const uint64_t* soff, uint8_t* recv, const uint64_t* rb,
           const uint64_t* roff) {
     Nccl& N = nccl();
     APG_CHECK_NCCL(N.GroupStart());
-    for (int q = 0; q < world; ++q) {
+    int r = kNcclSuccess;
+    const char* what = "";
+    for (int q = 0; q < world && r == kNcclSuccess; ++q) {
       if (q == rank && !self_p2p) continue;
-      for (uint64_t o = 0; o < sb[q]; o += kPiece)
-        APG_CHECK_NCCL(N.Send(send + soff[q] + o, std::min<uint64_t>(kPiece, sb[q] - o), kNcclUint8, q, nc,
-                              ctx->stream));
-      for (uint64_t o = 0; o < rb[q]; o += kPiece)
-        APG_CHECK_NCCL(N.Recv(recv + roff[q] + o, std::min<uint64_t>(kPiece, rb[q] - o), kNcclUint8, q, nc,
-                              ctx->stream));
+      for (uint64_t o = 0; o < sb[q] && r == kNcclSuccess; o += kPiece) {
+        r = N.Send(send + soff[q] + o, std::min<uint64_t>(kPiece, sb[q] - o), kNcclUint8, q, nc, ctx->stream);
+        what = "ncclSend";
+      }
+      for (uint64_t o = 0; o < rb[q] && r == kNcclSuccess; o += kPiece) {
+        r = N.Recv(recv + roff[q] + o, std::min<uint64_t>(kPiece, rb[q] - o), kNcclUint8, q, nc, ctx->stream);
+        what = "ncclRecv";
+      }
     }
-    APG_CHECK_NCCL(N.GroupEnd());
+    const int re = N.GroupEnd();
+    if (r != kNcclSuccess) {
+      set_error(std::string("apg_comm(rccl): ") + what + " failed: " + N.GetErrorString(r));
+      return APG_E_HIP;
+    }
+    APG_CHECK_NCCL(re);
+    return APG_OK;
+  }
+
+  // Unlike TCP (a length header per segment), point-to-point RCCL transfers
+  // carry no sizes: a send / receive size mismatch between two ranks would
+  // hang or overrun the receive segment.  Each rank's send sizes go to their
+  // receivers first (a small host-path exchange) and are compared there.
+  int check_sizes(const uint64_t* sb, const uint64_t* rb) {
+    std::vector<uint64_t> peer_sb(world, 0);
+    APG_TRY(alltoall_u64(sb, peer_sb.data(), 1));
+    for (int q = 0; q < world; ++q)
+      if (peer_sb[q] != rb[q]) {
+        set_error("apg_comm(rccl): rank " + std::to_string(q) + " sends " + std::to_string(peer_sb[q]) + " bytes, " +
+                  std::to_string(rb[q]) + " expected by rank " + std::to_string(rank));
+        return APG_E_STATE;
+      }
     return APG_OK;
   }
 
   int alltoallv(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
+    APG_TRY(check_sizes(sb, rb));
+    return alltoallv_raw(send, sb, recv, rb);
+  }
+
+  int alltoallv_raw(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) {
     std::vector<uint64_t> so(world + 1, 0), ro(world + 1, 0);
     for (int q = 0; q < world; ++q) {
       so[q + 1] = so[q] + sb[q];
@@ -185,6 +217,18 @@ struct RcclComm : Comm {
   }
 
   int allgatherv(const void* send, uint64_t bytes, void* recv, const uint64_t* rb) override {
+    std::vector<uint64_t> all;
+    APG_TRY(allgather_u64(bytes, &all));
+    for (int q = 0; q < world; ++q)
+      if (all[q] != rb[q]) {
+        set_error("apg_comm(rccl): rank " + std::to_string(q) + " gathers " + std::to_string(all[q]) + " bytes, " +
+                  std::to_string(rb[q]) + " expected by rank " + std::to_string(rank));
+        return APG_E_STATE;
+      }
+    return allgatherv_raw(send, bytes, recv, rb);
+  }
+
+  int allgatherv_raw(const void* send, uint64_t bytes, void* recv, const uint64_t* rb) {
     // every rank sends its segment to every peer: the all-to-all pattern of
     // xGMI's point-to-point links, exact sizes, no padding
     APG_REQUIRE(rb[rank] == bytes, "apg_comm_allgatherv: recv_bytes[rank] != send bytes");
@@ -209,6 +253,16 @@ struct RcclComm : Comm {
     return APG_OK;
   }
 
+  // in place on a device array (vote planes): ncclAllReduce in pieces
+  int allreduce_dev_u32(uint32_t* d, uint64_t n) override {
+    const uint64_t piece = kPiece / 4;
+    for (uint64_t o = 0; o < n; o += piece)
+      APG_CHECK_NCCL(nccl().AllReduce(d + o, d + o, std::min<uint64_t>(piece, n - o), kNcclUint32, kNcclSum, nc,
+                                      ctx->stream));
+    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return APG_OK;
+  }
+
   // host-array exchanges (counts, sizes): staged through the device
   int alltoallv_host(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
     uint64_t ts = 0, tr = 0;
@@ -216,7 +270,8 @@ struct RcclComm : Comm {
     APG_TRY(stage((ts + tr + 7) / 8 + 2));
     auto* d = reinterpret_cast<uint8_t*>(dsum);
     if (ts) APG_CHECK_HIP(hipMemcpyAsync(d, send, ts, hipMemcpyHostToDevice, ctx->stream));
-    APG_TRY(alltoallv(d, sb, d + ((ts + 7) & ~7ull), rb));
+    // host-path sizes are fixed by the caller's protocol (m u64 per peer)
+    APG_TRY(alltoallv_raw(d, sb, d + ((ts + 7) & ~7ull), rb));
     if (tr) APG_CHECK_HIP(hipMemcpy(recv, d + ((ts + 7) & ~7ull), tr, hipMemcpyDeviceToHost));
     return APG_OK;
   }
@@ -226,7 +281,7 @@ struct RcclComm : Comm {
     APG_TRY(stage((bytes + tr + 7) / 8 + 2));
     auto* d = reinterpret_cast<uint8_t*>(dsum);
     if (bytes) APG_CHECK_HIP(hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, ctx->stream));
-    APG_TRY(allgatherv(d, bytes, d + ((bytes + 7) & ~7ull), rb));
+    APG_TRY(allgatherv_raw(d, bytes, d + ((bytes + 7) & ~7ull), rb));
     if (tr) APG_CHECK_HIP(hipMemcpy(recv, d + ((bytes + 7) & ~7ull), tr, hipMemcpyDeviceToHost));
     return APG_OK;
   }
@@ -539,6 +594,35 @@ struct TcpComm : Comm {
   int barrier() override {
     uint64_t x = 0;
     return allreduce_u64(&x, 1, APG_COMM_SUM);
+  }
+
+  // Device array summed in place: staged through pinned memory, reduced as
+  // a reduce-scatter (rank q sums slice q of every rank's array) followed by
+  // an all-gather of the summed slices, so no rank holds world copies.
+  int allreduce_dev_u32(uint32_t* d, uint64_t n) override {
+    if (!n) return APG_OK;
+    APG_REQUIRE(ctx, "apg_comm(tcp): device allreduce needs a context");
+    std::vector<uint64_t> lo(world + 1);
+    for (int q = 0; q <= world; ++q) lo[q] = n * (uint64_t)q / (uint64_t)world;
+    const uint64_t mine = lo[rank + 1] - lo[rank];
+    APG_TRY(grow(&hs, &hs_n, n * 4));
+    APG_TRY(grow(&hr, &hr_n, std::max<uint64_t>(mine * 4 * world, n * 4)));
+    APG_CHECK_HIP(hipSetDevice(ctx->device));
+    APG_CHECK_HIP(hipMemcpyAsync(hs, d, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<uint64_t> sb(world), rb(world, mine * 4);
+    for (int q = 0; q < world; ++q) sb[q] = (lo[q + 1] - lo[q]) * 4;
+    APG_TRY(alltoallv_host(hs, sb.data(), hr, rb.data()));
+    auto* in = reinterpret_cast<const uint32_t*>(hr);
+    std::vector<uint32_t> sum(in, in + mine);
+    for (int q = 1; q < world; ++q)
+      for (uint64_t i = 0; i < mine; ++i) sum[i] += in[(uint64_t)q * mine + i];
+    std::vector<uint64_t> gb(world);
+    for (int q = 0; q < world; ++q) gb[q] = (lo[q + 1] - lo[q]) * 4;
+    APG_TRY(allgatherv_host(sum.data(), mine * 4, hs, gb.data()));
+    APG_CHECK_HIP(hipMemcpyAsync(d, hs, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return APG_OK;
   }
 
   // Full mesh: every rank listens on an ephemeral port and tells rank 0

@@ -26,6 +26,8 @@ struct Comm {
   virtual int alltoallv_host(const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes) = 0;
   virtual int allgatherv_host(const void* send, uint64_t bytes, void* recv, const uint64_t* recv_bytes) = 0;
   virtual int barrier() = 0;
+  // in place on a device array of the context (e.g. consensus vote planes): element-wise sum
+  virtual int allreduce_dev_u32(uint32_t* d, uint64_t n) = 0;
   uint64_t piece_bytes() const;
   // m u64 to every peer (host arrays [peer * m + i])
   int alltoall_u64(const uint64_t* send, uint64_t* recv, uint64_t m);
@@ -39,5 +41,10 @@ Comm* comm_of(apg_comm* c);
 // every rank + KmerPaths of this rank's reads.
 int u_sharded_graph(apg_ctx* ctx, Comm* c, const void* d_nodes, uint64_t n_nodes, const apg_dreads* reads,
                     const apg_unipath_params& p, apg_unipath_graph* out, apg_unipath_stats* st);
+
+// UnipathLocs of this rank's reads on the context's last sharded unipath
+// build (unipath.hip / ushard_graph.inc); stats summed over the ranks.
+int u_sharded_locs(apg_ctx* ctx, Comm* c, const apg_dreads* reads, uint32_t flags, const apg_aln_pair** d_locs,
+                   uint64_t* n_locs, apg_uloc_stats* st);
 
 }  // namespace apg

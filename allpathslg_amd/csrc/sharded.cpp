@@ -229,6 +229,9 @@ int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, cons
 
 int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, const apg_unipath_params* pp,
                          apg_unipath_graph* out, apg_unipath_stats* stats) {
+  // before anything can fail: the error path below frees *out, which must
+  // then hold nothing but what this call allocated
+  if (out) std::memset(out, 0, sizeof(*out));
   Comm* c = nullptr;
   APG_TRY(check_comm(ctx, comm, &c));
   APG_REQUIRE(reads, "apg_sharded_unipaths: NULL reads");
@@ -262,8 +265,10 @@ int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
     APG_TRY(apg_urec_nodes(ctx, x.recv, x.recv_counts.data(), K, P, &n_local));
   else
     APG_TRY(apg_ushard_nodes(ctx, x.recv, x.recv_counts.data(), K, P, &n_local));
+  // this rank's nodes outlive the call (the sharded graph's node array, for
+  // apg_sharded_unipath_locs): a workspace no other stage writes
   void* local = nullptr;
-  APG_TRY(workspace(ctx, "x_local", std::max<uint64_t>(n_local * 32, 64), &local));
+  APG_TRY(workspace(ctx, "x_unodes", std::max<uint64_t>(n_local * 32, 64), &local));
   if (rec)
     APG_TRY(apg_urec_export(ctx, local));
   else
@@ -287,6 +292,17 @@ int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
   st.n_instances = n_inst;
   if (stats) *stats = st;
   return APG_OK;
+}
+
+int apg_sharded_unipath_locs(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, uint32_t flags,
+                             const apg_aln_pair** d_locs, uint64_t* n_locs, apg_uloc_stats* stats) {
+  Comm* c = nullptr;
+  APG_TRY(check_comm(ctx, comm, &c));
+  APG_REQUIRE(reads && d_locs && n_locs, "apg_sharded_unipath_locs: NULL argument");
+  *d_locs = nullptr;
+  *n_locs = 0;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  return u_sharded_locs(ctx, c, reads, flags, d_locs, n_locs, stats);
 }
 
 }  // extern "C"

@@ -1988,6 +1988,10 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     g.ub_off = ub_off;
     g.ub = ub;
     g.uloc = nullptr;  // rebuilt on the next apg_unipath_locs
+    g.sharded = false;
+    g.vu = g.vr = nullptr;
+    g.comm = nullptr;
+    g.n_shards = 1;
     g.valid = true;
   }
   if (!out) return APG_OK;
@@ -2281,20 +2285,7 @@ void apg_unipath_defaults(apg_unipath_params* p) {
   p->flags = APG_UNIPATH_READ_PATHS;
 }
 
-void apg_unipath_graph_free(apg_unipath_graph* g) {
-  if (!g) return;
-  std::free(g->len);
-  std::free(g->id_base);
-  std::free(g->rc);
-  std::free(g->ub_off);
-  std::free(g->unibases);
-  std::free(g->from);
-  std::free(g->to);
-  std::free(g->path_off);
-  std::free(g->path_start);
-  std::free(g->path_len);
-  std::memset(g, 0, sizeof(*g));
-}
+// apg_unipath_graph_free: apg_graphio.cpp (host memory only)
 
 int apg_unipaths_dev(apg_ctx* ctx, const apg_dreads* reads, const apg_unipath_params* pp, apg_unipath_graph* out,
                      apg_unipath_stats* stats) {
@@ -2305,6 +2296,7 @@ int apg_unipaths_dev(apg_ctx* ctx, const apg_dreads* reads, const apg_unipath_pa
   else
     apg_unipath_defaults(&p);
   APG_REQUIRE(p.K >= 1 && p.K <= 96, "apg_unipaths: K must be in [1, 96]");
+  if (out) std::memset(out, 0, sizeof(*out));  // a failure frees only what this call allocated
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   apg_unipath_stats st;
   const int rc = unipaths_impl(ctx, reads, p, out, &st);
@@ -2432,6 +2424,7 @@ int apg_unipaths_from_nodes(apg_ctx* ctx, const void* d_nodes, uint64_t n_nodes,
   else
     apg_unipath_defaults(&p);
   APG_REQUIRE(p.K >= 1 && p.K <= 96, "apg_unipaths_from_nodes: K must be in [1, 96]");
+  if (out) std::memset(out, 0, sizeof(*out));  // a failure frees only what this call allocated
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   apg_unipath_stats st;
   std::memset(&st, 0, sizeof st);
@@ -2575,6 +2568,7 @@ static int ulocs_run(apg_ctx* ctx, const apg_dreads* dr, uint32_t flags, const U
                      apg_uloc_stats* st) {
   const apg_ctx::GState& gs = ctx->gstate;
   APG_REQUIRE(gs.valid, "apg_unipath_locs: no unipath graph in this context (run apg_unipaths first)");
+  APG_REQUIRE(!gs.sharded, "apg_unipath_locs: the last graph was built sharded (use apg_sharded_unipath_locs)");
   APG_REQUIRE((flags & ~(APG_ULOCS_RC | APG_ULOCS_SORTED)) == 0, "apg_unipath_locs: unknown flags");
   APG_REQUIRE(dr->n_reads < (1ull << 32), "apg_unipath_locs: more than 2^32 reads");
   APG_REQUIRE(dr->max_len < (1ull << 30), "apg_unipath_locs: read longer than 2^30 bases");

@@ -163,3 +163,29 @@ def sharded_unipaths(ctx: Context, comm: Comm, reads: DeviceReads, K: int = 96, 
         return graph_arrays(g), out
     finally:
         lib().apg_unipath_graph_free(C.byref(g))
+
+
+def sharded_unipath_locs(ctx: Context, comm: Comm, reads: DeviceReads, rc: bool = True, sorted: bool = True):
+    """UnipathLocs of this rank's reads on the global graph of the last
+    sharded_unipaths on ctx (include/apg.h apg_sharded_unipath_locs): every
+    K-mer this rank does not own is resolved by one query to its owner shard.
+    Returns (device pointer to n apg_aln_pair, n, stats summed over ranks);
+    s_id = the read's index in `reads`; valid until the next locs call."""
+    from ._lib import APG_ULOCS_RC, APG_ULOCS_SORTED, apg_uloc_stats
+
+    flags = (APG_ULOCS_RC if rc else 0) | (APG_ULOCS_SORTED if sorted else 0)
+    st = apg_uloc_stats()
+    n = C.c_uint64(0)
+    p = C.c_void_p()
+    check(lib().apg_sharded_unipath_locs(ctx.handle, comm.handle, reads.handle, flags, C.byref(p), C.byref(n),
+                                         C.byref(st)), "apg_sharded_unipath_locs")
+    return int(p.value or 0), int(n.value), st.as_dict()
+
+
+def sharded_consensus(ctx: Context, comm: Comm, R: DeviceReads, T: DeviceReads, d_placements: int, n: int,
+                      d_bases: int, d_quals: int) -> None:
+    """Column consensus of every rank's placements on the replicated targets
+    T (include/apg.h apg_sharded_consensus): the vote planes are summed over
+    the ranks; every rank gets every column (device outputs, T.n_bases each)."""
+    check(lib().apg_sharded_consensus(ctx.handle, comm.handle, R.handle, T.handle, C.c_void_p(d_placements), n,
+                                      C.c_void_p(d_bases), C.c_void_p(d_quals)), "apg_sharded_consensus")

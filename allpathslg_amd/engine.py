@@ -52,6 +52,15 @@ class DeviceReads:
         return int(lib().apg_dreads_count(self._h)) if self._h else 0
 
     @property
+    def n_bases(self) -> int:
+        if not self._h:
+            return 0
+        nr, nb, ny = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().apg_dreads_shape(self.ctx.handle, self._h, C.byref(nr), C.byref(nb), C.byref(ny), None, None),
+              "apg_dreads_shape")
+        return int(nb.value)
+
+    @property
     def handle(self):
         return self._h
 

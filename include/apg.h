@@ -741,6 +741,29 @@ int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, cons
                      apg_fill_stats* stats);
 int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, const apg_unipath_params* p,
                          apg_unipath_graph* out, apg_unipath_stats* stats);
+/* Read placement and consensus after a sharded build (SURVEY §8e
+ * "alignment": unibases replicated, reads sharded) — the multi-GPU forms of
+ * apg_unipath_locs_dev and apg_consensus_dev (BuildUnipathLocs /
+ * ReadLocationLG and the aligners feeding CRefMerger / LongReadConsensus,
+ * [R:M]/[R:L]; reference snapshot empty, no file:line).
+ *   unipath_locs  this rank's reads on the global graph of the last
+ *                 apg_sharded_unipaths on ctx (same comm): every K-mer the
+ *                 rank does not own is resolved by one query to its owner
+ *                 shard; the locations are exactly apg_unipath_locs' for
+ *                 these reads on the single-GPU graph (s_id = index in
+ *                 reads).  *d_locs: context workspace, valid until the next
+ *                 locs call.  stats summed over ranks.
+ *   consensus     every rank's placements of its own reads vote on the
+ *                 replicated targets (e.g. apg_unibases_dev, which works after
+ *                 a sharded build); the vote planes are summed over the ranks
+ *                 (in <= 2^28-column chunks) and every rank gets the consensus
+ *                 of every target column = apg_consensus_dev of the union.
+ * Gap-free / banded alignment of the placements needs no exchange
+ * (apg_gapfree_dev / apg_banded_sw_dev on each rank). */
+int apg_sharded_unipath_locs(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, uint32_t flags,
+                             const apg_aln_pair** d_locs, uint64_t* n_locs, apg_uloc_stats* stats);
+int apg_sharded_consensus(apg_ctx* ctx, apg_comm* comm, const apg_dreads* R, const apg_dreads* T,
+                          const apg_aln_pair* d_placements, uint64_t n, uint8_t* d_bases, uint8_t* d_quals);
 
 /* ------------------------------------------------------------------------- */
 /* Synthetic reads: uniform iid genome, frag pairs 100 bp,       */

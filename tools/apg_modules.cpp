@@ -97,7 +97,11 @@ struct Shard {
   int port = 29600;
   apg_comm* comm = nullptr;
   explicit Shard(Args& a) {
-    world = (int)a.num("WORLD", std::atol(env_or("WORLD_SIZE", "1").c_str()));
+    // sharded only on request: WORLD= on the command line, or COMM= with the
+    // launcher's WORLD_SIZE — a single-process call inside a launcher that
+    // exports WORLD_SIZE stays single-process
+    const bool asked = a.kv.count("WORLD") || a.kv.count("COMM");
+    world = (int)a.num("WORLD", asked ? std::atol(env_or("WORLD_SIZE", "1").c_str()) : 1);
     rank = (int)a.num("RANK", std::atol(env_or("RANK", "0").c_str()));
     mode = a.get("COMM", "rccl");
     addr = a.get("MASTER_ADDR", env_or("MASTER_ADDR", "127.0.0.1"));
@@ -352,7 +356,7 @@ int unipaths(Args& a, bool read_paths) {
   Reads rd;
   load_reads(a, head, false, &rd);
   Ctx ctx(a);
-  apg_unipath_graph g;
+  apg_unipath_graph g{};
   apg_unipath_stats st;
   if (sh.sharded()) {
     // the global graph on every rank + KmerPaths of each rank's reads: ranks
@@ -424,7 +428,7 @@ int make_rc_db(Args& a) {
   const std::string head = dir + "/" + a.get("READS", "all_reads");
   const int K = (int)a.num("K", 96);
   a.finish();
-  apg_unipath_graph g;
+  apg_unipath_graph g{};
   a.check(apg_graph_read(head.c_str(), K, &g), "reading unipath files (run CommonPather first)");
   if (!g.path_off) {
     apg_unipath_graph_free(&g);
