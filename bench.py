@@ -95,8 +95,9 @@ def parse():
     p.add_argument("--gather-nodes", action="store_true",
                    help="sharded path: replicated unipath build (every rank gathers all nodes) instead of the "
                         "sharded compaction")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_v8", "pmc", "traffic.json"),
-                   help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "current", "pmc", "traffic.json"),
+                   help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py); the default "
+                        "is the latest round checkpoint's (scripts/gpu_checkpoint.sh), which ships to the GPU box")
     return p.parse_args()
 
 

@@ -145,14 +145,22 @@ def kmer_spectrum(reads, K: int, hist_len: int = 1 << 16) -> np.ndarray:
     return spectrum_from_counts(c, hist_len)
 
 
-def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1):
-    """Corrected copy of `reads` (needs quals) and stats dict."""
+def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1, fast=False):
+    """Corrected copy of `reads` (needs quals) and stats dict.
+    fast=True: ork_precorrect_fast (bench.py's CPU baseline: rolling keys,
+    hash-table solid lookups; same outputs)."""
     from allpathslg_amd.reads import ReadSet  # plain data container
 
+    L = lib()
+    if fast and not hasattr(L, "_ork_fast"):
+        L.ork_precorrect_fast.restype = C.c_int
+        L.ork_precorrect_fast.argtypes = L.ork_precorrect.argtypes
+        L._ork_fast = True
+    fn = L.ork_precorrect_fast if fast else L.ork_precorrect
     pk = reads.packed.copy()
     q = reads.quals.copy()
     st = np.zeros(5, dtype=np.uint64)
-    rc = lib().ork_precorrect(reads.n_reads, reads.base_off.ctypes.data_as(_u64p), reads.byte_off.ctypes.data_as(_u64p),
+    rc = fn(reads.n_reads, reads.base_off.ctypes.data_as(_u64p), reads.byte_off.ctypes.data_as(_u64p),
                               pk.ctypes.data_as(_u8p), q.ctypes.data_as(_u8p), K, min_solid, max_q, n_cycles,
                               st.ctypes.data_as(_u64p))
     if rc:
@@ -161,15 +169,22 @@ def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1):
     return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), {k: int(v) for k, v in zip(keys, st)}
 
 
-def precorrect_solid(reads, solid_hashes, K=24, max_q=20):
-    """One correction pass of `reads` against a given solid hash set."""
+def precorrect_solid(reads, solid_hashes, K=24, max_q=20, fast=False):
+    """One correction pass of `reads` against a given solid hash set
+    (fast=True: rolling keys + hash table, same outputs; for full-size
+    parity checks and the CPU baseline)."""
     from allpathslg_amd.reads import ReadSet
 
+    L = lib()
+    if fast and not hasattr(L, "_ork_sfast"):
+        L.ork_precorrect_solid_fast.restype = C.c_int
+        L.ork_precorrect_solid_fast.argtypes = L.ork_precorrect_solid.argtypes
+        L._ork_sfast = True
     pk = reads.packed.copy()
     q = reads.quals.copy()
     st = np.zeros(5, dtype=np.uint64)
     sh = np.ascontiguousarray(solid_hashes, dtype=np.uint64)
-    rc = lib().ork_precorrect_solid(reads.n_reads, reads.base_off.ctypes.data_as(_u64p),
+    rc = (L.ork_precorrect_solid_fast if fast else L.ork_precorrect_solid)(reads.n_reads, reads.base_off.ctypes.data_as(_u64p),
                                     reads.byte_off.ctypes.data_as(_u64p), pk.ctypes.data_as(_u8p),
                                     q.ctypes.data_as(_u8p), K, max_q, sh.ctypes.data_as(_u64p), len(sh),
                                     st.ctypes.data_as(_u64p))
@@ -189,9 +204,10 @@ def solid_hashes(reads, K: int = 24, min_solid: int = 3) -> np.ndarray:
 
 
 def fill_fragments(reads, solid, K: int = 24, min_insert: int = 126, max_insert: int = 234,
-                   max_steps: int = 1024):
+                   max_steps: int = 1024, fast: bool = False):
     """FillFragments restated (oracle/fill_oracle.c): pairs (2i, 2i+1) closed
-    through the solid K-mer set.  Returns (filled ReadSet in pair order,
+    through the solid K-mer set (fast=True: hash-table lookups, bench.py's
+    CPU baseline; same outputs).  Returns (filled ReadSet in pair order,
     status uint8[n_pairs], length uint32[n_pairs], stats dict)."""
     from allpathslg_amd.reads import ReadSet
 
@@ -200,6 +216,8 @@ def fill_fragments(reads, solid, K: int = 24, min_insert: int = 126, max_insert:
         L.orf_fill.restype = C.c_int
         L.orf_fill.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, C.c_uint64, C.c_uint32, C.c_uint32,
                                C.c_uint32, _u8p, _u32p, C.POINTER(_u8p), _u64p]
+        L.orf_fill_fast.restype = C.c_int
+        L.orf_fill_fast.argtypes = L.orf_fill.argtypes
         L._orf = True
     n, bo, yo, pk = _rp(reads)
     npairs = n // 2
@@ -208,7 +226,7 @@ def fill_fragments(reads, solid, K: int = 24, min_insert: int = 126, max_insert:
     st = np.zeros(7, np.uint64)
     sh = np.ascontiguousarray(solid, dtype=np.uint64)
     outp = _u8p()
-    rc = L.orf_fill(n, bo, yo, pk, K, sh.ctypes.data_as(_u64p), len(sh), min_insert, max_insert, max_steps,
+    rc = (L.orf_fill_fast if fast else L.orf_fill)(n, bo, yo, pk, K, sh.ctypes.data_as(_u64p), len(sh), min_insert, max_insert, max_steps,
                     status.ctypes.data_as(_u8p), flen.ctypes.data_as(_u32p), C.byref(outp), st.ctypes.data_as(_u64p))
     if rc:
         raise RuntimeError("oracle fill_fragments failed (odd read count, bad K or allocation)")

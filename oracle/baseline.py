@@ -3,11 +3,23 @@ cpu_baseline leg imports this; never part of the product path).
 
 Times the CPU restatement (oracle/, OpenMP over its independent per-read /
 per-pair loops and per-partition sorts) on bounded samples of the bench's own
-synthetic reads, stage by stage — K=25 spectrum, K=24 PreCorrect (count +
-correct), FillFragments against the full-size solid set, K=96 unipaths of the
-filled fragments — once with every thread it is given and once on one
-thread, and names the host CPU.  value = 1 / sum(1 / stage rate), as for the
-GPU step.
+synthetic reads, stage by stage — K=25 spectrum (extraction + parallel radix
+sort + run-length), K=24 PreCorrect (count + correct), FillFragments against
+the full-size solid set, K=96 unipaths of the filled fragments — once with
+every thread it is given and once on one thread, and names the host CPU.
+value = 1 / sum(1 / stage rate), as for the GPU step.
+
+PreCorrect and FillFragments run their baseline forms (ork_precorrect_fast,
+orf_fill_fast: rolling K-mer keys and hash-table solid lookups instead of the
+checker's per-position re-hash and binary search; outputs identical,
+tests/test_cpu_baseline.py), so the baseline is not slowed by the checker's
+deliberately simple structures.
+
+Threads: the GPU box allots 16 host CPUs per GPU and sets OMP_NUM_THREADS=16
+for that share (the pool's rule: leave it); os.sched_getaffinity() there
+reports the whole machine, which other jobs share.  The baseline therefore
+runs at OMP_NUM_THREADS threads and reports that count in `cores`, with the
+one-thread figure beside it (`single_core`).
 """
 from __future__ import annotations
 
@@ -41,11 +53,11 @@ def _stages(reads, solid, n_spec, n_pc, n_pairs, K=25, Kc=24, Ku=96):
     ts = time.perf_counter() - t
     pcs = reads.subset(0, min(n_pc, reads.n_reads))
     t = time.perf_counter()
-    fixed, _ = oracle.precorrect(pcs, K=Kc)
+    fixed, _ = oracle.precorrect(pcs, K=Kc, fast=True)
     tp = time.perf_counter() - t
     npairs = min(n_pairs, fixed.n_reads // 2)
     t = time.perf_counter()
-    frags, _, _, _ = oracle.fill_fragments(fixed.subset(0, 2 * npairs), solid, K=Kc)
+    frags, _, _, _ = oracle.fill_fragments(fixed.subset(0, 2 * npairs), solid, K=Kc, fast=True)
     tf = time.perf_counter() - t
     t = time.perf_counter()
     oracle.unipaths(frags, Ku)
@@ -53,8 +65,8 @@ def _stages(reads, solid, n_spec, n_pc, n_pairs, K=25, Kc=24, Ku=96):
     rates = {"spectrum": spec.n_reads / ts, "precorrect": pcs.n_reads / tp, "fill": 2 * npairs / tf,
              "unipaths": 2 * npairs / tu}
     desc = (f"spectrum {spec.n_reads} reads K={K} ({ts:.2f} s); PreCorrect {pcs.n_reads} reads K={Kc}, own "
-            f"solid set ({tp:.2f} s); FillFragments {npairs} restatement-corrected pairs against the full-size "
-            f"solid set ({len(solid)} K-mers, binary search) ({tf:.2f} s); unipaths K={Ku} of the "
+            f"solid set, rolling keys + hash table ({tp:.2f} s); FillFragments {npairs} restatement-corrected pairs against the full-size "
+            f"solid set ({len(solid)} K-mers, hash table) ({tf:.2f} s); unipaths K={Ku} of the "
             f"{frags.n_reads} filled fragments ({tu:.2f} s)")
     return rates, desc, ts + tp + tf + tu
 

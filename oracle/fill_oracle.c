@@ -24,21 +24,22 @@
  *
  * Solid lookup: binary search of the ascending solid-hash array (ork_hash of
  * the canonical K-mer) — a different structure from the GPU's (K-1)-mer
- * extension table.
+ * extension table.  orf_fill_fast (bench.py's CPU baseline only) runs the
+ * same search through a hash table of the same set (solidset.h).
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "oracle.h"
+#include "solidset.h"
 
 enum { FILL_OK = 0, FILL_NONE = 1, FILL_AMBIGUOUS = 2, FILL_BUDGET = 3, FILL_SKIP = 4 };
 #define FILL_MAX_GAP 63
 
 typedef struct {
   int K;
-  const uint64_t* solid;
-  uint64_t ns;
+  const OSolid* solid;
   const uint8_t* A;
   uint32_t La;
   const uint8_t* F;
@@ -56,18 +57,6 @@ static int cmp_hash(const void* a, const void* b) {
   return x < y ? -1 : x > y;
 }
 
-static int has_hash(const uint64_t* h, uint64_t n, uint64_t x) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) / 2;
-    if (h[mid] < x)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  return lo < n && h[lo] == x;
-}
-
 /* solid(K-mer given by K base codes) */
 static int solid_codes(FillState* s, const uint8_t* b) {
   const int K = s->K;
@@ -78,7 +67,7 @@ static int solid_codes(FillState* s, const uint8_t* b) {
     rc = (rc >> 2) | ((uint64_t)(3 - b[t]) << (2 * K - 2));
   }
   s->lookups++;
-  return has_hash(s->solid, s->ns, ork_hash(K, fw < rc ? fw : rc));
+  return osolid_has(s->solid, ork_hash(K, fw < rc ? fw : rc));
 }
 
 /* base pos of A ++ path[0, d) ++ F */
@@ -158,7 +147,7 @@ static void unpack(const uint8_t* pk, uint32_t L, uint8_t* out) {
  * gap closure its bridge bases in path[]; returns the solid lookups made.
  * Pairs are independent: orf_fill runs them on the OpenMP threads. */
 static uint64_t fill_pair(const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
-                          const uint64_t* h, uint64_t ns, uint32_t min_insert, uint32_t max_insert,
+                          const OSolid* h, uint32_t min_insert, uint32_t max_insert,
                           uint32_t max_steps, uint64_t i, uint8_t* A, uint8_t* B, uint8_t* F, uint8_t* status,
                           uint32_t* flen, uint8_t* path) {
   const uint32_t La = (uint32_t)(base_off[2 * i + 1] - base_off[2 * i]);
@@ -176,7 +165,7 @@ static uint64_t fill_pair(const uint64_t* base_off, const uint64_t* byte_off, co
   for (uint32_t t = 0; t < Lf; ++t) F[t] = (uint8_t)(3 - B[Lf - 1 - t]);
   FillState s;
   memset(&s, 0, sizeof s);
-  s.K = K, s.solid = h, s.ns = ns, s.A = A, s.La = La, s.F = F, s.Lf = Lf, s.max_steps = max_steps;
+  s.K = K, s.solid = h, s.A = A, s.La = La, s.F = F, s.Lf = Lf, s.max_steps = max_steps;
   /* S must be a path of solid K-mers: A's own and F's own K-mers first */
   int clean = 1;
   for (uint32_t j = 0; j + (uint32_t)K <= La && clean; ++j) clean = solid_codes(&s, A + j);
@@ -222,16 +211,27 @@ static uint64_t fill_pair(const uint64_t* base_off, const uint64_t* byte_off, co
  * filled, none, ambiguous, budget, skip, filled bases, solid lookups.
  * Returns 0, or -1 on allocation failure / bad arguments.
  */
-int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
-             const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
-             uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats) {
+static int fill_impl(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
+                     int K, const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert,
+                     uint32_t max_steps, uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats,
+                     int table) {
   memset(stats, 0, 7 * sizeof(uint64_t));
   *out_bases = NULL;
   if ((n_reads & 1) || K < 2 || K > 32) return -1;
-  uint64_t* h = (uint64_t*)malloc((ns ? ns : 1) * sizeof(uint64_t));
-  if (!h) return -1;
-  if (ns) memcpy(h, solid, ns * sizeof(uint64_t));
-  qsort(h, ns, sizeof(uint64_t), cmp_hash);
+  OSolid set;
+  memset(&set, 0, sizeof set);
+  uint64_t* h = NULL;
+  if (table) {
+    if (osolid_build_table(&set, solid, ns)) return -1;
+    h = set.tab;
+  } else {
+    h = (uint64_t*)malloc((ns ? ns : 1) * sizeof(uint64_t));
+    if (!h) return -1;
+    if (ns) memcpy(h, solid, ns * sizeof(uint64_t));
+    qsort(h, ns, sizeof(uint64_t), cmp_hash);
+    set.sorted = h;
+    set.n = ns;
+  }
   uint32_t maxL = 0;
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint32_t L = (uint32_t)(base_off[r + 1] - base_off[r]);
@@ -257,7 +257,7 @@ int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_of
 #pragma omp for schedule(dynamic, 64)
     for (uint64_t i = 0; i < n_pairs; ++i)
       if (A && B && F)
-        lookups += fill_pair(base_off, byte_off, packed, K, h, ns, min_insert, max_insert, max_steps, i, A, B, F,
+        lookups += fill_pair(base_off, byte_off, packed, K, &set, min_insert, max_insert, max_steps, i, A, B, F,
                              status, flen, paths + i * (FILL_MAX_GAP + 1));
     free(A), free(B), free(F);
   }
@@ -305,4 +305,19 @@ int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_of
   free(A), free(B), free(paths);
   *out_bases = out;
   return 0;
+}
+
+int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
+             const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
+             uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats) {
+  return fill_impl(n_reads, base_off, byte_off, packed, K, solid, ns, min_insert, max_insert, max_steps, status, flen,
+                   out_bases, stats, 0);
+}
+
+/* bench.py's CPU baseline: the same fill, solid lookups through a hash table */
+int orf_fill_fast(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
+                  const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
+                  uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats) {
+  return fill_impl(n_reads, base_off, byte_off, packed, K, solid, ns, min_insert, max_insert, max_steps, status, flen,
+                   out_bases, stats, 1);
 }

@@ -24,6 +24,16 @@ int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* b
 int ork_precorrect_solid(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
                          uint8_t* quals, int K, uint32_t maxq, const uint64_t* solid, uint64_t ns, uint64_t* stats);
 
+/* bench.py CPU-baseline forms (same outputs, faster structures; solidset.h) */
+int ork_precorrect_fast(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                        uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint32_t n_cycles, uint64_t* stats);
+int ork_precorrect_solid_fast(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
+                              uint8_t* quals, int K, uint32_t maxq, const uint64_t* solid, uint64_t ns,
+                              uint64_t* stats);
+int orf_fill_fast(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
+                  const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
+                  uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats);
+
 int orf_fill(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
              const uint64_t* solid, uint64_t ns, uint32_t min_insert, uint32_t max_insert, uint32_t max_steps,
              uint8_t* status, uint32_t* flen, uint8_t** out_bases, uint64_t* stats);

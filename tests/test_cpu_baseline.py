@@ -45,3 +45,32 @@ def test_restatement_thread_count_invariant():
                 assert a == b
     finally:
         oracle.set_threads(before)
+
+
+def test_fast_baseline_forms_equal_the_restatement():
+    """ork_precorrect_fast (rolling keys, hash-table lookups) and
+    orf_fill_fast give the restatement's outputs exactly: the CPU baseline
+    times the same algorithm, only faster structures."""
+    g = synth_genome(150_000, 21)
+    reads = synth_reads(g, 40_000, seed=22)
+    for n_cycles in (1, 2):
+        a, sa = oracle.precorrect(reads, K=24, n_cycles=n_cycles)
+        b, sb = oracle.precorrect(reads, K=24, n_cycles=n_cycles, fast=True)
+        assert sa == sb and sa["n_corrected"] > 0
+        assert np.array_equal(a.packed, b.packed) and np.array_equal(a.quals, b.quals)
+    solid = oracle.solid_hashes(a, 24, 3)
+    fa, st_a, la, xa = oracle.fill_fragments(a, solid, K=24)
+    fb, st_b, lb, xb = oracle.fill_fragments(a, solid, K=24, fast=True)
+    assert xa == xb and xa["n_filled"] > 0
+    assert np.array_equal(st_a, st_b) and np.array_equal(la, lb)
+    assert np.array_equal(fa.base_off, fb.base_off) and np.array_equal(fa.packed, fb.packed)
+
+
+def test_fast_precorrect_solid_equals_restatement():
+    g = synth_genome(120_000, 23)
+    reads = synth_reads(g, 30_000, seed=24)
+    solid = oracle.solid_hashes(reads, 24, 3)
+    a, sa = oracle.precorrect_solid(reads, solid, K=24)
+    b, sb = oracle.precorrect_solid(reads, solid, K=24, fast=True)
+    assert sa == sb and sa["n_corrected"] > 0
+    assert np.array_equal(a.packed, b.packed) and np.array_equal(a.quals, b.quals)

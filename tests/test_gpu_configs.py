@@ -8,12 +8,15 @@ where the oracle finishes in seconds:
       PreCorrect, FillFragments, K=96 unipaths + HyperKmerPath + KmerPaths)
       against the oracle end to end.
   C2  chr20 64.4 Mb, 40 M reads: the chain twice (byte-identical), the
-      bench's size-independent properties, and sampled parity: one 1/256
-      hash parcel of the K=25 counted table and of the K=24 solid set
-      (oracle kmer_count_range), PreCorrect of the first 100 K reads and
-      FillFragments of the first 4 K pairs against the full-size solid set,
-      and every unipath inside one 200-kb genome window (oracle graph of the
-      filled fragments whose pairs lie in the window).
+      bench's size-independent properties, and whole-table parity of the
+      counting stages: the complete K=25 spectrum of all 40 M reads, the
+      complete K=24 solid set, and PreCorrect of all 40 M reads against it
+      (the oracle's rolling-key form, ork_precorrect_solid_fast, equal to the
+      checker by tests/test_cpu_baseline.py); one 1/256 hash parcel of the
+      K=25 counted table (keys and counts); FillFragments of the first 100 K
+      pairs; and both directions of the unipath graph inside one 200-kb
+      genome window (oracle graph of the filled fragments whose pairs lie in
+      the window).
   C3  chr20 40 M frag + 20 M 3-kb jump reads: ErrorCorrectJump, all_reads =
       filled fragments ++ trimmed jumps, K=96 graph over all of them, run
       twice, ECJ parity on the first 20 K jump reads, window parity with the
@@ -127,26 +130,42 @@ def unipath_seqs(g):
 
 
 def window_parity(gpu_graph, oracle_reads, genome, w0, w1, margin=20_000):
-    """Every unipath of the oracle graph of the window's reads that holds a
-    K-mer of the window interior and is shorter than the margin is also a
-    unipath of the full-size GPU graph (same bases), and such unipaths cover
-    most of the interior — so the GPU graph equals the oracle's there."""
+    """Both directions inside the window interior (the window minus `margin`
+    at each end, so every unipath counted lies wholly inside the window and
+    is built from the window's reads only):
+      - every oracle unipath (of the window's reads) shorter than the margin
+        that holds an interior K-mer is a unipath of the full-size GPU graph,
+        and such unipaths cover most of the interior;
+      - every GPU unipath shorter than the margin that holds an interior
+        K-mer is an oracle unipath (same bases)."""
     og = oracle.unipaths(oracle_reads, K96)
     interior = kmer_set(genome[w0 + margin : w1 - margin], K96)
-    gpu = set(s for s, L in zip(unipath_seqs(gpu_graph), gpu_graph["len"]) if L < 2 * margin)
+
+    def touching(g):
+        out = []
+        for s, L in zip(unipath_seqs(g), g["len"]):
+            if L >= margin:
+                continue
+            ks = [s[i : i + K96] for i in range(len(s) - K96 + 1)]
+            hit = [k for k in ks if k in interior]
+            if hit:
+                out.append((s, hit))
+        return out
+
+    gpu_all = set(s for s, L in zip(unipath_seqs(gpu_graph), gpu_graph["len"]) if L < 2 * margin)
+    ora_all = set(unipath_seqs(og))
     covered, compared = set(), 0
-    for s, L in zip(unipath_seqs(og), og["len"]):
-        if L >= margin:
-            continue
-        ks = [s[i : i + K96] for i in range(len(s) - K96 + 1)]
-        hit = [k for k in ks if k in interior]
-        if not hit:
-            continue
-        assert s in gpu, "an oracle unipath of the window is not a GPU unipath"
+    for s, hit in touching(og):
+        assert s in gpu_all, "an oracle unipath of the window is not a GPU unipath"
         covered.update(hit)
         compared += 1
     assert compared > 0
     assert len(covered) >= 0.9 * len(interior), (len(covered), len(interior))
+    back = 0
+    for s, _ in touching(gpu_graph):
+        assert s in ora_all, "a GPU unipath of the window interior is not an oracle unipath"
+        back += 1
+    assert back == compared, (back, compared)
     return compared
 
 
@@ -227,22 +246,36 @@ def test_c2_parcel_counts_match_oracle(c2, gpu_ctx):
     assert len(oh) > 1_000_000
     assert np.array_equal(khash_np(25, keys), oh)
     assert np.array_equal(counts, oc)
-    # the K=24 solid set of the measured PreCorrect path, restricted to a parcel
-    lo, hi = parcel(24, 0xC3)
-    oh, oc = oracle.kmer_count_range(reads, 24, lo, hi)
-    s = c2["a"]["solid"]
-    assert np.array_equal(s[(s >= np.uint64(lo)) & (s < np.uint64(hi))], oh[oc >= 3])
 
 
-def test_c2_precorrect_and_fill_samples_match_oracle(c2):
+def test_c2_full_spectrum_matches_oracle(c2):
+    """The complete K=25 spectrum of all 40 M reads (3.04 G K-mer instances)."""
+    exp = oracle.kmer_spectrum(c2["reads"], 25)
+    assert np.array_equal(c2["a"]["hist"], exp)
+
+
+def test_c2_full_solid_set_matches_oracle(c2):
+    """The complete K=24 solid set (count >= 3) of all 40 M reads."""
+    exp = np.sort(oracle.solid_hashes(c2["reads"], 24, 3))
+    assert len(exp) > 60_000_000
+    assert np.array_equal(c2["a"]["solid"], exp)
+
+
+def test_c2_full_precorrect_matches_oracle(c2):
+    """PreCorrect of all 40 M reads against the (whole-table-checked) solid
+    set: every base, quality and counter."""
     reads, fixed, solid = c2["reads"], c2["fixed"], c2["a"]["solid"]
-    n = 100_000
-    exp, _ = oracle.precorrect_solid(reads.subset(0, n), solid, K=24)
-    got = fixed.subset(0, n)
-    assert np.array_equal(got.packed[: int(got.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
-    assert np.array_equal(got.quals, exp.quals)
-    npairs = 4000
-    ofill, ostatus, _, _ = oracle.fill_fragments(fixed.subset(0, 2 * npairs), solid, K=24)
+    exp, est = oracle.precorrect_solid(reads, solid, K=24, fast=True)
+    assert np.array_equal(fixed.packed[: int(fixed.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(fixed.quals, exp.quals)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
+        assert c2["a"]["pst"][k] == est[k], k
+
+
+def test_c2_fill_sample_matches_oracle(c2):
+    fixed, solid = c2["fixed"], c2["a"]["solid"]
+    npairs = 100_000
+    ofill, ostatus, _, _ = oracle.fill_fragments(fixed.subset(0, 2 * npairs), solid, K=24, fast=True)
     status = c2["a"]["status"]
     assert np.array_equal(status[:npairs], ostatus)
     hf = filled_subset(c2["filled_a"], status, np.arange(npairs))
