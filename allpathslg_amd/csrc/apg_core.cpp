@@ -43,6 +43,68 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
   return APG_OK;
 }
 
+// Memory pressure (C5-scale inputs, DESIGN.md §7 "Memory model"): the
+// counting stages' record and partition buffers are dead once a count has
+// produced its spectrum, solid list and weak bitmap, but as grow-only named
+// workspaces they would stay allocated under the tables the next stage
+// builds.  When the device lacks `need` bytes (plus a 2 GiB margin) they are
+// released; the next count allocates them again.  Releasing a table some
+// later call may reuse (the extension table, the solid list) invalidates that
+// reuse.  Nothing is freed while memory suffices (the single-GPU bench never
+// releases).
+static const char* const kStageWs[] = {"big0",    "big1",    "big2",    "x_send",  "x_recv",  "x_pos",  "x_rmask",
+                                       "x_smask", "x_local", "sk_gkey", "sk_gcnt", "sk_cmat", "sk_omat"};
+// record descriptors of a count pass: live from the count to its scatter
+static const char* const kDescWs[] = {"sk_desc", "usk_desc"};
+static const char* const kCorrectWs[] = {"pc_ext", "fill_ext", "ecj_ext", "fill_solid", "x_solid", "pc_solid"};
+
+// APG_DEVICE_MEM_LIMIT=<bytes>: act as if the device held only that much for
+// this context's workspaces (tests of the release path on a 288 GB device).
+uint64_t device_free_bytes(apg_ctx* ctx) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    fr = ~(size_t)0;
+  }
+  static const uint64_t limit = getenv("APG_DEVICE_MEM_LIMIT") ? strtoull(getenv("APG_DEVICE_MEM_LIMIT"), nullptr, 10) : 0;
+  if (limit) {
+    uint64_t used = 0;
+    for (auto& kv : ctx->ws) used += kv.second.bytes;
+    const uint64_t emu = used >= limit ? 0 : limit - used;
+    if (emu < fr) fr = emu;
+  }
+  return fr;
+}
+
+static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uint64_t* freed) {
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < n; ++i) {
+    auto it = ctx->ws.find(names[i]);
+    if (it == ctx->ws.end() || !it->second.p) continue;
+    *freed += it->second.bytes;
+    APG_CHECK_HIP(hipFree(it->second.p));
+    ctx->ws.erase(it);
+  }
+  return APG_OK;
+}
+
+int ws_make_room(apg_ctx* ctx, uint64_t need, unsigned what) {
+  const uint64_t margin = 2ull << 30;
+  if (device_free_bytes(ctx) >= need + margin) return APG_OK;
+  uint64_t freed = 0;
+  APG_TRY(ws_release_list(ctx, kStageWs, sizeof kStageWs / sizeof kStageWs[0], &freed));
+  if (what & kRoomDescriptors) APG_TRY(ws_release_list(ctx, kDescWs, sizeof kDescWs / sizeof kDescWs[0], &freed));
+  if ((what & kRoomCorrection) && device_free_bytes(ctx) < need + margin) {
+    APG_TRY(ws_release_list(ctx, kCorrectWs, sizeof kCorrectWs / sizeof kCorrectWs[0], &freed));
+    ctx->pc_ext_valid = false;  // FillFragments / ErrorCorrectJump rebuild their tables
+    ctx->pc_list_valid = false;
+    ctx->solid_valid = false;
+  }
+  ++ctx->mem_releases;
+  vlog(ctx, "memory: %.2f GB of dead stage buffers released for a %.2f GB allocation", freed / 1e9, need / 1e9);
+  return APG_OK;
+}
+
 static hipEvent_t take_event(apg_ctx* ctx) {
   if (!ctx->event_pool.empty()) {
     hipEvent_t e = ctx->event_pool.back();

@@ -193,6 +193,9 @@ struct apg_ctx {
   bool clean_valid = false;
   // Capacity for the next single-pass candidate write (last count + 25 %).
   uint64_t pc_cand_hint = 0;
+  // ws_make_room calls that released buffers (memory pressure; logged with
+  // cfg.verbose)
+  uint64_t mem_releases = 0;
 };
 
 namespace apg {
@@ -236,6 +239,16 @@ int workspace_t(apg_ctx* ctx, const char* name, size_t count, T** out) {
   *out = static_cast<T*>(p);
   return rc;
 }
+
+// Free device memory (hipMemGetInfo; ~0 if unknown).
+uint64_t device_free_bytes(apg_ctx* ctx);
+// Before a large allocation of `need` bytes: when the device lacks it, release
+// the counting stages' dead record / partition workspaces, plus (flags) the
+// count passes' record descriptors (dead once scattered) and the correction
+// stage's extension tables / solid lists (dead once FillFragments ran) —
+// apg_core.cpp.
+constexpr unsigned kRoomDescriptors = 1, kRoomCorrection = 2;
+int ws_make_room(apg_ctx* ctx, uint64_t need, unsigned what = 0);
 
 // Bracket a launch with timing events when ctx->timing.
 void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes);

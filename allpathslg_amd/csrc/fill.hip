@@ -79,9 +79,27 @@ __global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n
 
 int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const char* ws, const char* kname,
               ExtTab* out) {
-  // load <= 0.5 even if no two solid K-mers share a (K-1)-mer (~0.25 on a genome)
+  // 4 slots per solid K-mer: load <= 0.5 even if no two solid K-mers share a
+  // (K-1)-mer, ~0.25 on a genome, so nearly every lookup ends in the home
+  // group.  When that does not fit the device (human-scale replicated solid
+  // sets: 2.6 G solid 24-mers -> 2^34 slots = 137 GB), the counting stages'
+  // dead buffers are released first, and if it still does not fit the table
+  // takes 2 slots per solid K-mer (load <= 0.5 on a genome: 69 GB at human
+  // scale; DESIGN.md §7 memory model).
   uint64_t T = 1024;
   while (T < 4 * n_solid) T <<= 1;
+  {
+    auto it = ctx->ws.find(ws);
+    const uint64_t have = it == ctx->ws.end() ? 0 : it->second.bytes;
+    const uint64_t need = T * 8 + 16;
+    if (need > have) {
+      APG_TRY(ws_make_room(ctx, need - have, kRoomDescriptors));
+      if (device_free_bytes(ctx) < need - have + (2ull << 30) && T > 1024) {
+        T >>= 1;
+        vlog(ctx, "ext table: %llu slots (load <= 0.5 by memory)", (unsigned long long)T);
+      }
+    }
+  }
   unsigned long long* slot = nullptr;
   APG_TRY(workspace_t(ctx, ws, T, &slot));
   APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));

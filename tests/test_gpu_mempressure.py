@@ -1,0 +1,60 @@
+"""Memory pressure (DESIGN.md §7 memory model): a C5-scale
+rank cannot hold the counting stages' record buffers, the replicated solid
+list and the (K-1)-mer extension table at once, so libapg releases the dead
+stage buffers before the correction tables are built (and the correction
+tables before the unipath stage) when the device lacks room, and shrinks the
+extension table to load <= 0.5 when even that does not fit.  Emulated here
+with APG_DEVICE_MEM_LIMIT (the context acts as if the device held only that
+much for its workspaces): the chain's results must not change, and the
+release path must have run."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
+
+CHAIN = r"""
+import json, sys, numpy as np
+sys.path.insert(0, {root!r})
+import torch
+from allpathslg_amd import Context, synth_genome, synth_reads
+g = synth_genome(8_000_000, 0x3E3)
+reads = synth_reads(g, 1_500_000, seed=0x3E4)
+with Context(device=0, verbose=True) as ctx:
+    d = ctx.upload(reads)
+    hist, st = ctx.kmer_spectrum(d, 25)
+    _, pst = ctx.precorrect(d, K=24)
+    filled, _, fst = ctx.fill_fragments(d, K=24, last_solid=True)
+    graph, ust = ctx.unipaths(filled, 96)
+    fixed = ctx.download(d)
+    out = {{"hist": hist.tolist()[:200], "pst": pst, "fst": fst, "ust": ust,
+           "fixed": int(np.frombuffer(fixed.packed.tobytes(), np.uint64).sum() % (1 << 61)),
+           "ub": int(graph["unibases"].astype(np.uint64).sum()), "nu": int(graph["n_unipaths"]),
+           "paths": int(graph["path_start"].astype(np.uint64).sum() % (1 << 61))}}
+print("RESULT " + json.dumps(out))
+"""
+
+
+def run(limit):
+    env = dict(os.environ)
+    if limit:
+        env["APG_DEVICE_MEM_LIMIT"] = str(limit)
+    r = subprocess.run([sys.executable, "-c", CHAIN.format(root=ROOT)], capture_output=True, text=True, env=env,
+                       timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
+    return line, r.stderr
+
+
+def test_release_under_memory_pressure_keeps_results():
+    free_run, log0 = run(0)
+    assert "dead stage buffers released" not in log0
+    # the workspaces this chain reaches without pressure (verbose log)
+    peak = max(float(x.split("all workspaces ")[1].split(" GB")[0]) for x in log0.splitlines()
+               if "all workspaces" in x)
+    tight_run, log1 = run(int(peak * 0.55e9))
+    assert "dead stage buffers released" in log1
+    assert tight_run == free_run
