@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 
 namespace apg {
 
@@ -102,6 +103,95 @@ int ws_make_room(apg_ctx* ctx, uint64_t need, unsigned what) {
   }
   ++ctx->mem_releases;
   vlog(ctx, "memory: %.2f GB of dead stage buffers released for a %.2f GB allocation", freed / 1e9, need / 1e9);
+  return APG_OK;
+}
+
+int staging_get(apg_ctx* ctx, int workers) {
+  auto& S = ctx->staging;
+  while (S.workers < workers) {
+    uint8_t* b[2] = {nullptr, nullptr};
+    hipStream_t st = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    APG_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&b[0]), kStageChunk, 0));
+    APG_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&b[1]), kStageChunk, 0));
+    APG_CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    APG_CHECK_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    APG_CHECK_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    S.buf.push_back(b[0]);
+    S.buf.push_back(b[1]);
+    S.st.push_back(st);
+    S.ev.push_back(ev[0]);
+    S.ev.push_back(ev[1]);
+    ++S.workers;
+  }
+  return APG_OK;
+}
+
+static void staging_free(apg_ctx* ctx) {
+  auto& S = ctx->staging;
+  for (auto* b : S.buf) (void)hipHostFree(b);
+  for (auto s : S.st) (void)hipStreamDestroy(s);
+  for (auto e : S.ev) (void)hipEventDestroy(e);
+  S = apg_ctx::Staging{};
+}
+
+int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers) {
+  struct Chunk {
+    uint8_t* dst;
+    const uint8_t* src;
+    uint64_t n;
+  };
+  std::vector<Chunk> ch;
+  for (const auto& j : jobs)
+    for (uint64_t o = 0; o < j.bytes; o += kStageChunk)
+      ch.push_back(Chunk{static_cast<uint8_t*>(j.dst) + o, static_cast<const uint8_t*>(j.src) + o,
+                         std::min<uint64_t>(kStageChunk, j.bytes - o)});
+  if (ch.empty()) return APG_OK;
+  // small copies: straight (a worker thread costs more than they do)
+  if (ch.size() == 1 && ch[0].n < (1u << 20)) {
+    APG_CHECK_HIP(hipMemcpy(ch[0].dst, ch[0].src, ch[0].n, hipMemcpyDeviceToHost));
+    return APG_OK;
+  }
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)workers, ch.size()));
+  APG_TRY(staging_get(ctx, T));
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> err{0};
+  const int dev = ctx->device;
+  auto worker = [&](int w) {
+    if (hipSetDevice(dev) != hipSuccess) {
+      err = 1;
+      return;
+    }
+    uint8_t* buf[2] = {ctx->staging.buf[2 * w], ctx->staging.buf[2 * w + 1]};
+    hipEvent_t ev[2] = {ctx->staging.ev[2 * w], ctx->staging.ev[2 * w + 1]};
+    hipStream_t st = ctx->staging.st[w];
+    const Chunk* pend[2] = {nullptr, nullptr};
+    int k = 0;
+    auto drain = [&](int b) {
+      if (!pend[b]) return;
+      if (hipEventSynchronize(ev[b]) != hipSuccess) err = 1;
+      std::memcpy(pend[b]->dst, buf[b], pend[b]->n);  // also first-touches the destination pages, in parallel
+      pend[b] = nullptr;
+    };
+    for (uint64_t c; (c = next.fetch_add(1)) < ch.size() && !err.load(); k ^= 1) {
+      drain(k);
+      if (hipMemcpyAsync(buf[k], ch[c].src, ch[c].n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipEventRecord(ev[k], st) != hipSuccess) {
+        err = 1;
+        break;
+      }
+      pend[k] = &ch[c];
+    }
+    drain(k);
+    drain(k ^ 1);
+  };
+  std::vector<std::thread> ts;
+  for (int w = 0; w < T; ++w) ts.emplace_back(worker, w);
+  for (auto& t : ts) t.join();
+  if (err.load()) {
+    set_error("device-to-host copy through the staging buffers failed");
+    return APG_E_HIP;
+  }
   return APG_OK;
 }
 
@@ -246,6 +336,7 @@ void apg_destroy(apg_ctx* ctx) {
     (void)hipEventDestroy(p.b);
   }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  staging_free(ctx);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -288,12 +379,10 @@ int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_
 }  // extern "C"
 
 namespace apg {
-// A device read set with its offsets uploaded and its payload buffers
-// allocated (packed zeroed, +64 bytes of slack; quals if asked): the caller
-// fills packed / quals on the context's stream (apg_reads_upload from host
-// arrays, apg_reads_load_dev from files).
-int dreads_create(apg_ctx* ctx, uint64_t n, const uint64_t* base_off, const uint64_t* byte_off, bool with_quals,
-                  apg_dreads** out) {
+// A device read set with room for its offset tables (n + 1 each); the shape
+// fields are filled by dreads_device_shape (readset.hip) once the tables are
+// on the device.
+int dreads_alloc(apg_ctx* ctx, uint64_t n, apg_dreads** out) {
   *out = nullptr;
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   auto* d = new (std::nothrow) apg_dreads();
@@ -303,48 +392,52 @@ int dreads_create(apg_ctx* ctx, uint64_t n, const uint64_t* base_off, const uint
   static std::atomic<uint64_t> g_gen{1};
   d->gen = g_gen.fetch_add(1);
   d->n_reads = n;
-  d->h_base_off.assign(base_off ? base_off : nullptr, base_off ? base_off + n + 1 : nullptr);
-  if (d->h_base_off.empty()) d->h_base_off.push_back(0);
-  d->n_bases = d->h_base_off[n] - d->h_base_off[0];
-  d->n_bytes = n ? byte_off[n] : 0;
-  uint64_t sh = 0x9e3779b97f4a7c15ull ^ n;
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint64_t len = base_off[i + 1] - base_off[i];
-    // the byte stride too: padded byte_off layouts with equal lengths differ
-    sh = (sh ^ len) * 0x100000001b3ull;
-    sh = (sh ^ (byte_off[i + 1] - byte_off[i])) * 0x100000001b3ull;
-    if ((byte_off[i + 1] - byte_off[i]) * 4 < len) {
-      delete d;
-      set_error("read set: byte_off inconsistent with base_off (read " + std::to_string(i) + ")");
-      return APG_E_ARG;
-    }
-    if (len > d->max_len) d->max_len = len;
-  }
-  d->shape_hash = sh | 1;
-  auto fail = [&](hipError_t e) {
+  hipError_t e;
+  if ((e = hipMalloc(&d->d_base_off, (n + 1) * 8)) != hipSuccess || (e = hipMalloc(&d->d_byte_off, (n + 1) * 8)) != hipSuccess) {
     set_error(std::string("read set: ") + hipGetErrorString(e));
     apg_reads_free(d);
     return APG_E_HIP;
+  }
+  *out = d;
+  return APG_OK;
+}
+
+// Payload buffers of a read set whose shape is known: packed bases zeroed, +64
+// bytes of slack (kernels may issue aligned 4/16-byte loads past the end),
+// qualities if asked.
+int dreads_alloc_payload(apg_ctx* ctx, apg_dreads* d, bool with_quals) {
+  hipError_t e;
+  if ((e = hipMalloc(&d->d_packed, d->n_bytes + 64)) != hipSuccess ||
+      (e = hipMemsetAsync(d->d_packed, 0, d->n_bytes + 64, ctx->stream)) != hipSuccess ||
+      (with_quals && d->n_reads && (e = hipMalloc(&d->d_quals, d->n_bases + 64)) != hipSuccess)) {
+    set_error(std::string("read set: ") + hipGetErrorString(e));
+    return APG_E_HIP;
+  }
+  return APG_OK;
+}
+
+// Host offset tables -> a device read set with its offsets uploaded, its
+// shape checked on the device and its payload buffers allocated (packed
+// zeroed): the caller fills packed / quals on the context's stream.
+int dreads_create(apg_ctx* ctx, uint64_t n, const uint64_t* base_off, const uint64_t* byte_off, bool with_quals,
+                  apg_dreads** out) {
+  *out = nullptr;
+  apg_dreads* d = nullptr;
+  APG_TRY(dreads_alloc(ctx, n, &d));
+  auto fail = [&](int rc) {
+    apg_reads_free(d);
+    return rc;
   };
   hipError_t e;
-  if ((e = hipMalloc(&d->d_base_off, (n + 1) * 8)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&d->d_byte_off, (n + 1) * 8)) != hipSuccess) return fail(e);
-  // +64 bytes of slack: kernels may issue aligned 4/16-byte loads past the end.
-  if ((e = hipMalloc(&d->d_packed, d->n_bytes + 64)) != hipSuccess) return fail(e);
-  if ((e = hipMemsetAsync(d->d_packed, 0, d->n_bytes + 64, ctx->stream)) != hipSuccess) return fail(e);
-  if (n) {
-    if ((e = hipMemcpyAsync(d->d_base_off, base_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
-      return fail(e);
-    if ((e = hipMemcpyAsync(d->d_byte_off, byte_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
-      return fail(e);
-  } else {
-    uint64_t z = 0;
-    if ((e = hipMemcpyAsync(d->d_base_off, &z, 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return fail(e);
-    if ((e = hipMemcpyAsync(d->d_byte_off, &z, 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) return fail(e);
-    if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail(e);  // &z is a stack value
+  const uint64_t z = 0;
+  if ((e = hipMemcpyAsync(d->d_base_off, n ? base_off : &z, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d->d_byte_off, n ? byte_off : &z, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) {
+    set_error(std::string("read set: ") + hipGetErrorString(e));
+    return fail(APG_E_HIP);
   }
-  if (with_quals && n)
-    if ((e = hipMalloc(&d->d_quals, d->h_base_off[n] + 64)) != hipSuccess) return fail(e);
+  int rc = dreads_device_shape(ctx, d, nullptr, false, "read set");  // syncs: &z may be released after
+  if (rc == APG_OK) rc = dreads_alloc_payload(ctx, d, with_quals);
+  if (rc != APG_OK) return fail(rc);
   *out = d;
   return APG_OK;
 }
@@ -371,7 +464,7 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
   if (n && (e = hipMemcpyAsync(d->d_packed, r->packed, d->n_bytes, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
     return fail(e);
   if (r->quals && n &&
-      (e = hipMemcpyAsync(d->d_quals, r->quals, d->h_base_off[n], hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
+      (e = hipMemcpyAsync(d->d_quals, r->quals, d->n_bases, hipMemcpyHostToDevice, ctx->stream)) != hipSuccess)
     return fail(e);
   if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) return fail(e);
   *out = d;
@@ -407,10 +500,18 @@ int apg_dreads_shape(apg_ctx* ctx, const apg_dreads* d, uint64_t* n_reads, uint6
 
 int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
   APG_REQUIRE(ctx && dst && src, "apg_reads_copy_dev: NULL argument");
-  // Shape identity: the uploads' length hashes (an element-wise compare of
-  // two 40 M-entry offset vectors cost 13 ms of host time per bench step).
-  const bool same = dst->shape_hash && src->shape_hash ? dst->shape_hash == src->shape_hash
-                                                       : dst->h_base_off == src->h_base_off;
+  // Shape identity: the sets' length hashes (an element-wise compare of two
+  // 40 M-entry offset vectors cost 13 ms of host time per bench step); a set
+  // produced on the device (fill, concat, unibases) gets its hash computed
+  // here, once.
+  for (apg_dreads* x : {dst, const_cast<apg_dreads*>(src)})
+    if (!x->shape_hash) {
+      const uint64_t nb = x->n_bases, ny = x->n_bytes, ml = x->max_len;
+      APG_TRY(dreads_device_shape(ctx, x, nullptr, false, "apg_reads_copy_dev"));
+      APG_REQUIRE(x->n_bases == nb && x->n_bytes == ny && x->max_len == ml,
+                  "apg_reads_copy_dev: device read set shape inconsistent (internal error)");
+    }
+  const bool same = dst->shape_hash == src->shape_hash;
   APG_REQUIRE(dst->n_reads == src->n_reads && dst->n_bases == src->n_bases && dst->n_bytes == src->n_bytes && same,
               "apg_reads_copy_dev: read sets differ in shape");
   APG_REQUIRE(!src->d_quals || dst->d_quals, "apg_reads_copy_dev: destination has no qualities");

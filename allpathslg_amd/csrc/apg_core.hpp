@@ -20,6 +20,14 @@ void set_error(const std::string& msg);
 // allocated, for the caller to fill on ctx->stream.
 int dreads_create(apg_ctx* ctx, uint64_t n, const uint64_t* base_off, const uint64_t* byte_off, bool with_quals,
                   apg_dreads** out);
+// apg_core.cpp: room for the offset tables only / the payload of a set whose
+// shape is known.
+int dreads_alloc(apg_ctx* ctx, uint64_t n, apg_dreads** out);
+int dreads_alloc_payload(apg_ctx* ctx, apg_dreads* d, bool with_quals);
+// readset.hip: validate the device offset tables of d (byte_off derived from
+// base_off when compute_bytes; d_qoff, if given, must equal base_off) and
+// fill n_bases, n_bytes, max_len, shape_hash.  Synchronous.
+int dreads_device_shape(apg_ctx* ctx, apg_dreads* d, const uint64_t* d_qoff, bool compute_bytes, const char* who);
 const char* get_error();
 
 struct Status {
@@ -71,8 +79,7 @@ struct apg_dreads {
   uint64_t* d_byte_off = nullptr;  // n+1
   uint8_t* d_packed = nullptr;
   uint8_t* d_quals = nullptr;      // optional
-  std::vector<uint64_t> h_base_off;  // kept for host-side sizing (uploads only)
-  uint64_t shape_hash = 0;  // hash of the read lengths and byte strides (uploads; 0 = not known): cheap shape identity
+  uint64_t shape_hash = 0;  // hash of the read lengths and byte strides (dreads_device_shape; 0 = not yet known)
   // device-produced sets (apg_fill_fragments_dev): buffer capacities, reused
   // when the same object is passed back in
   bool fill_owned = false;
@@ -196,6 +203,16 @@ struct apg_ctx {
   // ws_make_room calls that released buffers (memory pressure; logged with
   // cfg.verbose)
   uint64_t mem_releases = 0;
+  // Host <-> device staging of the module boundary (apg_reads_load_dev,
+  // graph egress): per worker two pinned chunks, a stream and two events,
+  // allocated once per context (pinning 256 MB per call cost more than the
+  // copies it staged).
+  struct Staging {
+    int workers = 0;
+    std::vector<uint8_t*> buf;  // 2 per worker, kStageChunk bytes each
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;  // 2 per worker
+  } staging;
 };
 
 namespace apg {
@@ -239,6 +256,20 @@ int workspace_t(apg_ctx* ctx, const char* name, size_t count, T** out) {
   *out = static_cast<T*>(p);
   return rc;
 }
+
+// Module-boundary copies through the context's pinned staging (apg_core.cpp):
+// chunks of kStageChunk bytes spread over `workers` host threads, each
+// double-buffering its copies on its own stream.
+constexpr uint64_t kStageChunk = 16ull << 20;
+int staging_get(apg_ctx* ctx, int workers);
+struct D2HJob {
+  void* dst;        // host (pageable)
+  const void* src;  // device
+  uint64_t bytes;
+};
+// Device arrays -> host arrays (the device data must be complete: call after a
+// sync of ctx->stream).  Synchronous.
+int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers = 4);
 
 // Free device memory (hipMemGetInfo; ~0 if unknown).
 uint64_t device_free_bytes(apg_ctx* ctx);

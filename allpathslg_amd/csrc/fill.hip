@@ -568,7 +568,6 @@ static int filled_alloc(apg_ctx* ctx, apg_dreads** io, uint64_t n, uint64_t nbas
   d->n_reads = n;
   d->n_bases = nbases;
   d->n_bytes = nbytes;
-  d->h_base_off.clear();
   d->shape_hash = 0;  // shape produced on the device: not known to the host
   return APG_OK;
 }

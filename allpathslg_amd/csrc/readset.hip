@@ -29,6 +29,101 @@
 
 namespace apg {
 
+// ---------------------------------------------------------------------------
+// Read-set shape on the device (uploads and .fastb/.qualb loads): the offset
+// tables are validated and summarised by one kernel instead of a host loop
+// over every read (40 M reads: 0.35 s of host time per load in round 2).
+//   k_shape  thread per read: monotone base_off, length < 2^32, byte stride
+//            >= ceil(len / 4) (given byte_off) or ceil(len / 4) into nby (to
+//            be scanned into byte_off), the qualb offsets equal base_off,
+//            longest read, and the shape hash = n + sum_i fmix(len_i, stride_i,
+//            i) (wrapping; order-sensitive through i) that apg_reads_copy_dev
+//            compares instead of the tables.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rs_fmix(uint64_t z) {
+  z ^= z >> 33;
+  z *= 0xff51afd7ed558ccdull;
+  z ^= z >> 33;
+  z *= 0xc4ceb9fe1a85ec53ull;
+  z ^= z >> 33;
+  return z;
+}
+
+__global__ void k_shape(const uint64_t* __restrict__ bo, const uint64_t* __restrict__ yo,
+                        const uint64_t* __restrict__ qo, uint64_t n, uint32_t* __restrict__ nby,
+                        unsigned long long* __restrict__ out) {
+  unsigned long long bad = 0, badq = 0, h = 0, mx = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t a = bo[i], b = bo[i + 1];
+    if (b < a || b - a >= (1ull << 32)) {
+      ++bad;
+      continue;
+    }
+    const uint64_t len = b - a, need = (len + 3) / 4;
+    uint64_t stride = need;
+    if (yo) {
+      const uint64_t ya = yo[i], yb = yo[i + 1];
+      if (yb < ya || yb - ya < need) ++bad;
+      stride = yb - ya;
+    } else {
+      nby[i] = (uint32_t)need;
+    }
+    if (qo && qo[i + 1] != b) ++badq;
+    mx = len > mx ? len : mx;
+    h += rs_fmix(len ^ (stride << 40) ^ (i * 0x9e3779b97f4a7c15ull));
+  }
+  wave_add(&out[0], bad);
+  wave_add(&out[1], badq);
+  wave_add(&out[2], h);
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = (unsigned long long)__shfl_xor((long long)mx, o, 64);
+    mx = y > mx ? y : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(&out[3], mx);
+}
+
+int dreads_device_shape(apg_ctx* ctx, apg_dreads* d, const uint64_t* d_qoff, bool compute_bytes, const char* who) {
+  const uint64_t n = d->n_reads;
+  unsigned long long* out = nullptr;
+  uint32_t* nby = nullptr;
+  APG_TRY(workspace_t(ctx, "rs_shape", 4, &out));
+  if (compute_bytes) APG_TRY(workspace_t(ctx, "rs_nby", std::max<uint64_t>(n, 1), &nby));
+  APG_CHECK_HIP(hipMemsetAsync(out, 0, 32, ctx->stream));
+  kbegin(ctx, "read_shape", (n + 1) * (compute_bytes ? 8 : 16) + (d_qoff ? (n + 1) * 8 : 0) + (compute_bytes ? n * 4 : 0));
+  if (n)
+    k_shape<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(d->d_base_off, compute_bytes ? nullptr : d->d_byte_off, d_qoff,
+                                                        n, nby, out);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  if (compute_bytes) APG_TRY(scan_u32_u64(ctx, nby, n, d->d_byte_off, "rs"));
+  unsigned long long h[4];
+  uint64_t ends[4];
+  APG_CHECK_HIP(hipMemcpyAsync(h, out, 32, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&ends[0], d->d_base_off, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&ends[1], d->d_base_off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&ends[2], d->d_byte_off, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&ends[3], d->d_byte_off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (ends[0] != 0 || ends[2] != 0) {
+    set_error(std::string(who) + ": offset tables must start at 0");
+    return APG_E_ARG;
+  }
+  if (h[0]) {
+    set_error(std::string(who) + ": " + std::to_string(h[0]) +
+              " reads with non-monotone offsets, a length >= 2^32 or a byte stride below ceil(len/4)");
+    return APG_E_ARG;
+  }
+  if (h[1]) {
+    set_error(std::string(who) + ": qualb/fastb length mismatch (" + std::to_string(h[1]) + " reads)");
+    return APG_E_IO;
+  }
+  d->n_bases = ends[1];
+  d->n_bytes = ends[3];
+  d->max_len = h[3];
+  d->shape_hash = (h[2] ^ (n * 0x100000001b3ull)) | 1;
+  return APG_OK;
+}
+
 __global__ void k_cat_len(const uint64_t* __restrict__ base_off, const uint32_t* __restrict__ keep, uint64_t n,
                           uint32_t* __restrict__ lens, uint32_t* __restrict__ nby) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -167,7 +262,6 @@ int apg_reads_concat_dev(apg_ctx* ctx, const apg_dreads* const* sets, const uint
   d->n_bases = nbases;
   d->n_bytes = nbytes;
   d->max_len = max_len;
-  d->h_base_off.clear();
   d->shape_hash = 0;
 
   APG_CHECK_HIP(hipMemcpyAsync(d->d_base_off, bscan, (n + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));

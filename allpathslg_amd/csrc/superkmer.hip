@@ -333,6 +333,7 @@ __device__ __forceinline__ uint32_t sk_slot(uint64_t c, int bits) {
 // Find-or-claim the slot of key c in the LDS table: one 32-byte group read
 // (two ds_read_b128) answers most instances — a hit, or the first empty slot
 // to claim with one CAS.  Returns the slot, or kSkTab when the table is full.
+template <uint32_t TAB = kSkTab>
 __device__ __forceinline__ uint32_t sk_tab_claim(unsigned long long* tkey, uint64_t c, uint32_t g) {
   constexpr unsigned long long EMPTY = ~0ull;
   for (uint32_t n = 0; n < kSkProbeMax;) {
@@ -344,7 +345,7 @@ __device__ __forceinline__ uint32_t sk_tab_claim(unsigned long long* tkey, uint6
     for (uint32_t q = kSkGrp; q-- > 0;)
       if (k[q] == c || k[q] == EMPTY) j = q;  // the first in probe order
     if (j == kSkGrp) {  // group full of other keys: the next group
-      g = (g + kSkGrp) & (kSkTab - 1);
+      g = (g + kSkGrp) & (TAB - 1);
       n += kSkGrp;
       continue;
     }
@@ -353,7 +354,7 @@ __device__ __forceinline__ uint32_t sk_tab_claim(unsigned long long* tkey, uint6
     if (old == EMPTY || old == c) return g + j;
     ++n;  // another key took that slot: look at the group again
   }
-  return kSkTab;
+  return TAB;
 }
 
 struct SkOut {
@@ -387,7 +388,9 @@ __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, con
 // the spectrum; solid mode appends khash of those with count >= min_solid.
 // blist (may be null): count only the buckets blist[0 .. *bcount) — the
 // buckets k_sk_bucket_dd handed back.
-template <bool SOLID, typename R, int NT>
+// TAB: LDS table slots (buckets of ~2 TAB instances); OWN: owner-map bytes per
+// record slot = the most K-mers a record holds (41 - K; 20 covers K >= 21).
+template <bool SOLID, typename R, int NT, uint32_t TAB = kSkTab, int OWN = kSkBases>
 __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
                                                           const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
                                                           SkOut o, const uint32_t* __restrict__ blist = nullptr,
@@ -396,13 +399,13 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   // recorded slots: kSkWaveSlots per wave (NT = 512: each wave sees ~1/8 of a bucket)
   constexpr uint32_t kWaveSlots = NT >= 512 ? 1024 : kSkWaveSlots;
   constexpr uint32_t kSlotCap = kWaveSlots * (NT / 64);
-  __shared__ __attribute__((aligned(16))) unsigned long long tkey[kSkTab];
-  __shared__ uint32_t tcnt[kSkTab];
+  __shared__ __attribute__((aligned(16))) unsigned long long tkey[TAB];
+  __shared__ uint32_t tcnt[TAB];
   __shared__ uint32_t lhist[kSkHistBins];
   __shared__ __attribute__((aligned(16))) SK16 crec[NT];
   __shared__ uint32_t koff[NT];
-  __shared__ __attribute__((aligned(16))) uint8_t owner[NT * kSkBases];
-  static_assert(64 * kSkBases >= kWaveSlots / 8 + 8, "a wave's weak bit array must fit in its owner-map slice");
+  __shared__ __attribute__((aligned(16))) uint8_t owner[NT * OWN];
+  static_assert(64 * OWN >= kWaveSlots / 8 + 8, "a wave's weak bit array must fit in its owner-map slice");
   __shared__ uint32_t scan_sm[32];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
@@ -414,11 +417,11 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   __shared__ __attribute__((aligned(16))) uint16_t islot[WEAK ? kSlotCap : 4];
   static_assert(!WEAK || kSlotCap * 2 >= NT * 4, "fallback scratch must fit in islot");
   const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  uint8_t* wown = owner + wv * (64 * kSkBases);  // this wave's owner-map slice
+  uint8_t* wown = owner + wv * (64 * OWN);  // this wave's owner-map slice
   uint16_t* wslot = islot + (WEAK ? wv * kWaveSlots : 0);  // this wave's recorded slots
   uint32_t* wmask = reinterpret_cast<uint32_t*>(islot);  // [NT] (probing fallback)
   constexpr unsigned long long EMPTY = ~0ull;
-  constexpr int TB = __builtin_ctz(kSkTab);
+  constexpr int TB = __builtin_ctz(TAB);
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kSkHistBins; i += NT) lhist[i] = 0;
   unsigned long long nd = 0;
@@ -451,7 +454,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       nr = nnr;
       continue;
     }
-    for (uint32_t s = tid; s < kSkTab; s += NT) {
+    for (uint32_t s = tid; s < TAB; s += NT) {
       tkey[s] = EMPTY;
       tcnt[s] = 0;
     }
@@ -485,8 +488,8 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       for (uint32_t f = ln; f < tot; f += 64) {
         const uint32_t i = (wv << 6) + wown[f];
         const uint64_t c = rec_kmer(crec[i], f - koff[i], p);
-        const uint32_t s = sk_tab_claim(tkey, c, sk_slot(c, TB));
-        const bool ok = s < kSkTab;
+        const uint32_t s = sk_tab_claim<TAB>(tkey, c, sk_slot(c, TB));
+        const bool ok = s < TAB;
         if (!ok) ovf = 1;  // table full: the bucket goes to the global path
         if (ok) {
           atomicAdd(&tcnt[s], 1u);
@@ -583,7 +586,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
             const uint32_t t = f - koff[i];
             const uint64_t c = rec_kmer(crec[i], t, p);
             uint32_t s = sk_slot(c, TB);
-            while (tkey[s] != c) s = (s + 1) & (kSkTab - 1);  // inserted above: present
+            while (tkey[s] != c) s = (s + 1) & (TAB - 1);  // inserted above: present
             if (tcnt[s] < o.min_solid) atomicOr(&wmask[i], 1u << t);
           }
           wave_lds_sync();
@@ -603,7 +606,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       }
     }
     uint32_t ns = 0;
-    for (uint32_t s = tid; s < kSkTab; s += NT)
+    for (uint32_t s = tid; s < TAB; s += NT)
       if (tkey[s] != EMPTY) {
         sk_spectrum_add(tcnt[s], lhist, o);
         ++nd;
@@ -615,7 +618,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       if (tid == 0) sbase = tot ? atomicAdd(&o.gstats[2], (unsigned long long)tot) : 0ull;
       __syncthreads();
       const unsigned long long b = sbase;
-      for (uint32_t s = tid; s < kSkTab; s += NT)
+      for (uint32_t s = tid; s < TAB; s += NT)
         if (tkey[s] != EMPTY && tcnt[s] >= o.min_solid) {
           const unsigned long long at = b + j++;
           if (at < o.solid_cap) o.solid[at] = khash(p.hp, tkey[s]);
@@ -1332,7 +1335,13 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     const uint64_t need = std::max<uint64_t>(1, (n_kmers + per - 1) / per);
     return std::min(32 - pbits, std::max(l1, sk_ceil_log2(need)));
   };
-  int bb = bits_for(kSkBucketKmers);
+  // The plain spectrum count (no dedup, no solid list) may run the smaller
+  // LDS table: APG_SK_TAB=1024 halves the table and the buckets (more blocks
+  // per CU).  K >= 21 records hold <= 20 K-mers, so the
+  // owner map shrinks with them.
+  static const int tab_env = getenv("APG_SK_TAB") ? atoi(getenv("APG_SK_TAB")) : 2048;
+  const bool small_tab = !solid && tab_env == 1024 && K >= 21;
+  int bb = bits_for(small_tab ? kSkBucketKmers / 2 : kSkBucketKmers);
   if (dd) {
     const int bd = bits_for(kDdBucketKmers);
     if ((bd - l1 + kMaxLevelBits - 1) / kMaxLevelBits <= (bb - l1 + kMaxLevelBits - 1) / kMaxLevelBits) bb = bd;
@@ -1440,8 +1449,13 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   // LDS (owner map, recorded slots) and the table amortised over 8 waves give
   // 16 waves per CU, where 256-thread blocks fit only 3 per CU
   constexpr int NTB = sizeof(R) == sizeof(SK24) ? 512 : kSkThreads;
-  const uint64_t grid = solid ? resident_grid(ctx, k_sk_bucket<true, R, NTB>, NTB, nb)
-                              : resident_grid(ctx, k_sk_bucket<false, R, NTB>, NTB, nb);
+  static const bool own40 = getenv("APG_SK_OWN40") != nullptr;  // A/B: the K <= 20 owner map at K >= 21
+  const bool own20 = K >= 21 && !solid && !own40;  // the plain spectrum count's variants
+  auto plain = [&](auto kern) { return resident_grid(ctx, kern, NTB, nb); };
+  const uint64_t grid = solid        ? resident_grid(ctx, k_sk_bucket<true, R, NTB>, NTB, nb)
+                        : small_tab  ? plain(k_sk_bucket<false, R, NTB, 1024, 20>)
+                        : own20      ? plain(k_sk_bucket<false, R, NTB, kSkTab, 20>)
+                                     : resident_grid(ctx, k_sk_bucket<false, R, NTB>, NTB, nb);
   // record dedup first (K >= kDdMinK), k_sk_bucket for the buckets it hands back
   // (a launch over a device-side count: no host round trip in between)
   const uint64_t grid_dd = !dd ? 0
@@ -1465,6 +1479,10 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       }
     } else if (solid) {
       k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+    } else if (small_tab) {
+      k_sk_bucket<false, R, NTB, 1024, 20><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+    } else if (own20) {
+      k_sk_bucket<false, R, NTB, kSkTab, 20><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
     } else {
       k_sk_bucket<false, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
     }

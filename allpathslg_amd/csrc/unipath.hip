@@ -1557,19 +1557,13 @@ static int ceil_log2_u(uint64_t x) {
 
 
 template <typename T>
-static T* host_dup(const T* d, uint64_t n, apg_ctx* ctx, int* rc) {
+static T* host_dup(const T* d, uint64_t n, std::vector<D2HJob>* jobs, int* rc) {
   T* h = (T*)std::malloc(std::max<uint64_t>(n, 1) * sizeof(T));
   if (!h) {
     *rc = APG_E_NOMEM;
     return nullptr;
   }
-  if (n) {
-    hipError_t e = hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream);
-    if (e != hipSuccess) {
-      set_error(std::string("D2H failed: ") + hipGetErrorString(e));
-      *rc = APG_E_HIP;
-    }
-  }
+  if (n) jobs->push_back(D2HJob{h, d, n * sizeof(T)});
   return h;
 }
 
@@ -1998,26 +1992,28 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
 
   // ---- host copies ------------------------------------------------------------
   int rc = APG_OK;
+  std::vector<D2HJob> jobs;  // every array through the pinned staging, after one sync
   std::memset(out, 0, sizeof(*out));
   out->K = K;
   out->n_nodes = N;
   out->n_unipaths = U;
-  out->len = host_dup(ulen, U, ctx, &rc);
-  out->id_base = host_dup(id_base, U, ctx, &rc);
-  out->rc = host_dup(urc, U, ctx, &rc);
-  out->ub_off = host_dup(ub_off, U + 1, ctx, &rc);
-  out->unibases = host_dup(ub, tot_ub, ctx, &rc);
+  out->len = host_dup(ulen, U, &jobs, &rc);
+  out->id_base = host_dup(id_base, U, &jobs, &rc);
+  out->rc = host_dup(urc, U, &jobs, &rc);
+  out->ub_off = host_dup(ub_off, U + 1, &jobs, &rc);
+  out->unibases = host_dup(ub, tot_ub, &jobs, &rc);
   out->n_vertices = hv[0];
-  out->from = host_dup(from, U, ctx, &rc);
-  out->to = host_dup(to, U, ctx, &rc);
+  out->from = host_dup(from, U, &jobs, &rc);
+  out->to = host_dup(to, U, &jobs, &rc);
   out->n_reads = want_paths ? dr->n_reads : 0;
   out->n_intervals = NI;
   if (want_paths) {
-    out->path_off = host_dup(ioff, dr->n_reads + 1, ctx, &rc);
-    out->path_start = host_dup(istart, NI, ctx, &rc);
-    out->path_len = host_dup(ilen, NI, ctx, &rc);
+    out->path_off = host_dup(ioff, dr->n_reads + 1, &jobs, &rc);
+    out->path_start = host_dup(istart, NI, &jobs, &rc);
+    out->path_len = host_dup(ilen, NI, &jobs, &rc);
   }
   if (rc == APG_OK) rc = sync(ctx);
+  if (rc == APG_OK) rc = d2h_bulk(ctx, jobs);
   return rc;
 }
 
@@ -2720,7 +2716,6 @@ int apg_unibases_dev(apg_ctx* ctx, apg_dreads** out) {
   d->d_base_off = d->d_byte_off = nullptr;
   d->d_packed = nullptr;
   d->n_reads = U;
-  d->h_base_off = hoff;
   d->shape_hash = 0;
   d->n_bases = hoff[U];
   d->n_bytes = hby[U];

@@ -683,26 +683,59 @@ def _arr(p, n, dt):
     return np.ctypeslib.as_array(p, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
 
 
+class _HostArray:
+    """Owns one library-allocated host array (apg_free on release); numpy views
+    keep it alive, so the graph's arrays need no copy."""
+
+    def __init__(self, addr: int):
+        self.addr = addr
+
+    def __del__(self):
+        try:
+            lib().apg_free(C.c_void_p(self.addr))
+        except Exception:
+            pass
+
+
+def _take(g, field: str, n: int, dt) -> np.ndarray:
+    """Take ownership of graph field `field` (n elements): a numpy array over
+    the library's buffer, the struct's pointer cleared (so
+    apg_unipath_graph_free leaves it alone)."""
+    p = getattr(g, field)
+    addr = C.cast(p, C.c_void_p).value if p else None
+    setattr(g, field, type(p)())
+    if not addr:
+        return np.zeros(0, dt)
+    owner = _HostArray(addr)
+    if n == 0:
+        return np.zeros(0, dt)
+    buf = (C.c_uint8 * (n * np.dtype(dt).itemsize)).from_address(addr)
+    buf._owner = owner
+    return np.frombuffer(buf, dtype=dt)
+
+
 def graph_arrays(g) -> dict:
-    """apg_unipath_graph -> dict of numpy arrays (same keys as oracle.unipaths)."""
+    """apg_unipath_graph -> dict of numpy arrays (same keys as oracle.unipaths).
+    The arrays take over the library's host buffers (no copy of the graph,
+    which is ~0.4 GB at the bench config)."""
     U = int(g.n_unipaths)
     out = {
         "n_nodes": int(g.n_nodes),
         "n_unipaths": U,
-        "len": _arr(g.len, U, np.uint64),
-        "id_base": _arr(g.id_base, U, np.uint64),
-        "rc": _arr(g.rc, U, np.uint64),
-        "ub_off": _arr(g.ub_off, U + 1, np.uint64),
+        "len": _take(g, "len", U, np.uint64),
+        "id_base": _take(g, "id_base", U, np.uint64),
+        "rc": _take(g, "rc", U, np.uint64),
+        "ub_off": _take(g, "ub_off", U + 1, np.uint64),
         "n_vertices": int(g.n_vertices),
-        "from": _arr(g.frm, U, np.uint64),
-        "to": _arr(g.to, U, np.uint64),
+        "from": _take(g, "frm", U, np.uint64),
+        "to": _take(g, "to", U, np.uint64),
     }
-    out["unibases"] = _arr(g.unibases, int(out["ub_off"][-1]) if U else 0, np.uint8)
+    out["unibases"] = _take(g, "unibases", int(out["ub_off"][-1]) if U else 0, np.uint8)
     nr = int(g.n_reads)
     if g.path_off:
-        out["path_off"] = _arr(g.path_off, nr + 1, np.uint64)
-        out["path_start"] = _arr(g.path_start, int(g.n_intervals), np.uint64)
-        out["path_len"] = _arr(g.path_len, int(g.n_intervals), np.uint64)
+        out["path_off"] = _take(g, "path_off", nr + 1, np.uint64)
+        out["path_start"] = _take(g, "path_start", int(g.n_intervals), np.uint64)
+        out["path_len"] = _take(g, "path_len", int(g.n_intervals), np.uint64)
     return out
 
 
