@@ -7,16 +7,24 @@
 // one thread); here the payload goes from the file to HBM once: worker
 // threads pread fixed-size chunks into their own pinned buffers and issue the
 // H2D copy on their own stream, double-buffered, so file reads and PCIe
-// transfers overlap across chunks and threads.  The offset tables take the
+// transfers overlap across chunks and threads.  On the MI355X hosts the first
+// read of a just-written page-cache file — what a module boundary reads, the
+// previous module wrote it — runs at ~15-17 GB/s from 16 threads with no GPU
+// involved (tools/microbench/freshread.cpp) and ~100-170 GB/s from the second
+// read on; the load follows (≈12-15 GB/s cold, 35-48 GB/s warm).  Copying out
+// of a mapping instead (APG_LOAD_IO=mmap) measured the same cold and slower
+// warm (24-27 GB/s: page faults on every fresh mapping).  The offset tables take the
 // same path and are validated on the device (apg_fastb_read's rules:
 // monotone, from 0 to the header's total; qualb offsets equal fastb's; file
 // sizes exact), where the byte offsets are also derived.
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -36,8 +44,19 @@ struct Fd {
 };
 
 // bytes [off, off + len) of the file -> dst (device), by `threads` workers,
-// each double-buffering pread into its pinned staging chunk against the H2D
+// each double-buffering its copy out of the mapping into its pinned staging chunk against the H2D
 // copy of its previous chunk on its own stream (the context's staging pool).
+// The caller has checked the file's size against [off, off + len); a file
+// truncated while it is being loaded faults the copy (SIGBUS), as any mapped
+// read would.
+struct Map {
+  void* base = MAP_FAILED;
+  uint64_t bytes = 0;
+  ~Map() {
+    if (base != MAP_FAILED) munmap(base, bytes);
+  }
+};
+
 int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len, uint8_t* dst, int threads) {
   if (!len) return APG_OK;
   Fd f;
@@ -45,6 +64,23 @@ int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len,
   if (f.fd < 0) {
     set_error(std::string("cannot open ") + path);
     return APG_E_IO;
+  }
+  // APG_LOAD_IO=mmap copies out of a read-only mapping instead (A/B knob)
+  static const bool use_pread = [] {
+    const char* e = std::getenv("APG_LOAD_IO");
+    return !(e && std::strcmp(e, "mmap") == 0);
+  }();
+  const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE), moff = off & ~(page - 1);
+  Map m;
+  const uint8_t* src = nullptr;
+  if (!use_pread) {
+    m.bytes = off + len - moff;
+    m.base = mmap(nullptr, m.bytes, PROT_READ, MAP_SHARED, f.fd, (off_t)moff);
+    if (m.base == MAP_FAILED) {
+      set_error(std::string("cannot map ") + path);
+      return APG_E_IO;
+    }
+    src = static_cast<const uint8_t*>(m.base) + (off - moff);
   }
   const uint64_t nch = (len + kStageChunk - 1) / kStageChunk;
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, nch));
@@ -70,17 +106,21 @@ int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len,
         break;
       }
       const uint64_t o = c * kStageChunk, n = std::min(kStageChunk, len - o);
-      bool ok = true;
-      for (uint64_t got = 0; got < n;) {
-        const ssize_t r = pread(f.fd, buf[k] + got, n - got, (off_t)(off + o + got));
-        if (r <= 0) {
-          fail(APG_E_IO, std::string("short read from ") + path);
-          ok = false;
-          break;
+      if (src) {
+        std::memcpy(buf[k], src + o, n);
+      } else {
+        bool ok = true;
+        for (uint64_t got = 0; got < n;) {
+          const ssize_t r = pread(f.fd, buf[k] + got, n - got, (off_t)(off + o + got));
+          if (r <= 0) {
+            fail(APG_E_IO, std::string("short read from ") + path);
+            ok = false;
+            break;
+          }
+          got += (uint64_t)r;
         }
-        got += (uint64_t)r;
+        if (!ok) break;
       }
-      if (!ok) break;
       if (hipMemcpyAsync(dst + o, buf[k], n, hipMemcpyHostToDevice, st) != hipSuccess ||
           hipEventRecord(ev[k], st) != hipSuccess) {
         fail(APG_E_HIP, "hipMemcpyAsync");
@@ -167,7 +207,7 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
     }
   }
   const uint64_t n = hf.n;
-  if (threads <= 0) threads = (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));
+  if (threads <= 0) threads = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   apg_dreads* d = nullptr;
   APG_TRY(dreads_alloc(ctx, n, &d));
