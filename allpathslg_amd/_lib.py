@@ -410,6 +410,7 @@ SIGNATURES = {
     "apg_comm_init_rccl": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_uint32, C.POINTER(_P)]),
     "apg_comm_init_tcp": (C.c_int, [_P, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
     "apg_comm_destroy": (None, [_P]),
+    "apg_comm_abort": (C.c_int, [_P]),
     "apg_comm_rank": (C.c_int, [_P]),
     "apg_comm_world": (C.c_int, [_P]),
     "apg_comm_alltoallv": (C.c_int, [_P, _P, _u64p, _P, _u64p]),

@@ -33,9 +33,11 @@
 
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "apg_core.hpp"
@@ -68,6 +70,7 @@ struct Nccl {
   int (*GroupEnd)() = nullptr;
   int (*AllReduce)(const void*, void*, size_t, int, int, NcclComm, hipStream_t) = nullptr;
   const char* (*GetErrorString)(int) = nullptr;
+  int (*CommGetAsyncError)(NcclComm, int*) = nullptr;
 };
 
 Nccl& nccl() {
@@ -95,6 +98,7 @@ Nccl& nccl() {
     APG_SYM("ncclGroupEnd", GroupEnd)
     APG_SYM("ncclAllReduce", AllReduce)
     APG_SYM("ncclGetErrorString", GetErrorString)
+    APG_SYM("ncclCommGetAsyncError", CommGetAsyncError)
 #undef APG_SYM
     x.ok = true;
     return x;
@@ -136,9 +140,55 @@ struct RcclComm : Comm {
   unsigned long long* dsum = nullptr;  // small device staging (allreduce / host-path exchanges)
   uint64_t dsum_n = 0;
 
+  int timeout_ms = 600000;
+
   ~RcclComm() override {
     if (nc) nccl().CommDestroy(nc);
     if (dsum) (void)hipFree(dsum);
+  }
+
+  void abort() override {
+    if (nc) nccl().CommAbort(nc);
+    nc = nullptr;
+    aborted = true;
+  }
+
+  int live() {
+    if (aborted) {
+      set_error("apg_comm(rccl): the communicator was aborted");
+      return APG_E_STATE;
+    }
+    return APG_OK;
+  }
+
+  // The collective's end: the stream drains, or RCCL reports a failed peer
+  // (ncclCommGetAsyncError), or nothing finishes within timeout_ms — a rank
+  // that died or aborted leaves its peers' kernels waiting forever, so a
+  // plain hipStreamSynchronize would never return.  Failure aborts.
+  int wait(const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; ++spin) {
+      const hipError_t q = hipStreamQuery(ctx->stream);
+      if (q == hipSuccess) return APG_OK;
+      if (q != hipErrorNotReady) {
+        set_error(std::string("apg_comm(rccl): ") + what + ": " + hipGetErrorString(q));
+        abort();
+        return APG_E_HIP;
+      }
+      int e = kNcclSuccess;
+      if (nccl().CommGetAsyncError(nc, &e) == kNcclSuccess && e != kNcclSuccess && e != kNcclInProgress) {
+        set_error(std::string("apg_comm(rccl): ") + what + ": " + nccl().GetErrorString(e));
+        abort();
+        return APG_E_HIP;
+      }
+      if (std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count() >
+          timeout_ms) {
+        set_error(std::string("apg_comm(rccl): ") + what + " timed out (a peer stopped)");
+        abort();
+        return APG_E_HIP;
+      }
+      if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
 
   int stage(uint64_t n) {
@@ -196,6 +246,7 @@ struct RcclComm : Comm {
   }
 
   int alltoallv(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
+    APG_TRY(live());
     APG_TRY(check_sizes(sb, rb));
     return alltoallv_raw(send, sb, recv, rb);
   }
@@ -212,11 +263,11 @@ struct RcclComm : Comm {
     if (!self_p2p && sb[rank])
       APG_CHECK_HIP(hipMemcpyAsync(r + ro[rank], s + so[rank], sb[rank], hipMemcpyDeviceToDevice, ctx->stream));
     APG_TRY(p2p(s, sb, so.data(), r, rb, ro.data()));
-    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    return APG_OK;
+    return wait("alltoallv");
   }
 
   int allgatherv(const void* send, uint64_t bytes, void* recv, const uint64_t* rb) override {
+    APG_TRY(live());
     std::vector<uint64_t> all;
     APG_TRY(allgather_u64(bytes, &all));
     for (int q = 0; q < world; ++q)
@@ -238,33 +289,34 @@ struct RcclComm : Comm {
     if (!self_p2p && bytes)
       APG_CHECK_HIP(hipMemcpyAsync(r + ro[rank], send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     APG_TRY(p2p(static_cast<const uint8_t*>(send), sb.data(), so.data(), r, rb, ro.data()));
-    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    return APG_OK;
+    return wait("allgatherv");
   }
 
   int allreduce_u64(uint64_t* data, uint64_t n, int op) override {
+    APG_TRY(live());
     if (!n) return APG_OK;
     APG_TRY(stage(n));
     APG_CHECK_HIP(hipMemcpyAsync(dsum, data, n * 8, hipMemcpyHostToDevice, ctx->stream));
     APG_CHECK_NCCL(nccl().AllReduce(dsum, dsum, n, kNcclUint64, op == APG_COMM_MAX ? kNcclMax : kNcclSum, nc,
                                     ctx->stream));
-    APG_CHECK_HIP(hipMemcpyAsync(data, dsum, n * 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    APG_TRY(wait("allreduce"));
+    APG_CHECK_HIP(hipMemcpy(data, dsum, n * 8, hipMemcpyDeviceToHost));
     return APG_OK;
   }
 
   // in place on a device array (vote planes): ncclAllReduce in pieces
   int allreduce_dev_u32(uint32_t* d, uint64_t n) override {
+    APG_TRY(live());
     const uint64_t piece = kPiece / 4;
     for (uint64_t o = 0; o < n; o += piece)
       APG_CHECK_NCCL(nccl().AllReduce(d + o, d + o, std::min<uint64_t>(piece, n - o), kNcclUint32, kNcclSum, nc,
                                       ctx->stream));
-    APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    return APG_OK;
+    return wait("allreduce");
   }
 
   // host-array exchanges (counts, sizes): staged through the device
   int alltoallv_host(const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) override {
+    APG_TRY(live());
     uint64_t ts = 0, tr = 0;
     for (int q = 0; q < world; ++q) ts += sb[q], tr += rb[q];
     APG_TRY(stage((ts + tr + 7) / 8 + 2));
@@ -276,6 +328,7 @@ struct RcclComm : Comm {
     return APG_OK;
   }
   int allgatherv_host(const void* send, uint64_t bytes, void* recv, const uint64_t* rb) override {
+    APG_TRY(live());
     uint64_t tr = 0;
     for (int q = 0; q < world; ++q) tr += rb[q];
     APG_TRY(stage((bytes + tr + 7) / 8 + 2));
@@ -398,6 +451,13 @@ struct TcpComm : Comm {
     if (hr) (void)hipHostFree(hr);
   }
 
+  // peers blocked in an exchange with this rank see the connection close
+  void abort() override {
+    for (int f : fd)
+      if (f >= 0) ::shutdown(f, SHUT_RDWR);
+    aborted = true;
+  }
+
   int grow(uint8_t** p, uint64_t* have, uint64_t want) {
     if (*have >= want) return APG_OK;
     if (*p) APG_CHECK_HIP(hipHostFree(*p));
@@ -419,6 +479,10 @@ struct TcpComm : Comm {
       uint64_t hdr_out, hdr_in = 0;
       uint64_t sent = 0, got = 0;  // bytes incl. the 8-byte header
     };
+    if (aborted) {
+      set_error("apg_comm(tcp): the communicator was aborted");
+      return APG_E_STATE;
+    }
     std::vector<St> st(world);
     int pending = 0;
     for (int q = 0; q < world; ++q) {
@@ -770,6 +834,8 @@ int apg_comm_init_rccl(apg_ctx* ctx, const void* id128, int rank, int world, uin
     delete c;
     return APG_E_HIP;
   }
+  if (const char* e = std::getenv("APG_COMM_TIMEOUT_MS"))
+    if (std::atoi(e) > 0) c->timeout_ms = std::atoi(e);
   *out = new (std::nothrow) apg_comm{c};
   if (!*out) {
     delete c;
@@ -800,6 +866,12 @@ int apg_comm_init_tcp(apg_ctx* ctx, const char* master_addr, int master_port, in
     delete c;
     return APG_E_NOMEM;
   }
+  return APG_OK;
+}
+
+int apg_comm_abort(apg_comm* comm) {
+  APG_REQUIRE(comm, "apg_comm_abort: NULL argument");
+  comm->c->abort();
   return APG_OK;
 }
 

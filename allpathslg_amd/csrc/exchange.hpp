@@ -28,6 +28,9 @@ struct Comm {
   virtual int barrier() = 0;
   // in place on a device array of the context (e.g. consensus vote planes): element-wise sum
   virtual int allreduce_dev_u32(uint32_t* d, uint64_t n) = 0;
+  // after a local failure: peers blocked on this rank error out (apg_comm_abort)
+  virtual void abort() = 0;
+  bool aborted = false;
   uint64_t piece_bytes() const;
   // m u64 to every peer (host arrays [peer * m + i])
   int alltoall_u64(const uint64_t* send, uint64_t* recv, uint64_t m);

@@ -67,6 +67,11 @@ class Comm:
     def handle(self):
         return self._h
 
+    def abort(self) -> None:
+        """After a local failure: peers blocked in a collective with this rank
+        error out instead of waiting (apg_comm_abort)."""
+        check(lib().apg_comm_abort(self._h), "apg_comm_abort")
+
     def close(self):
         if self._h:
             lib().apg_comm_destroy(self._h)

@@ -219,6 +219,13 @@ int apg_comm_init_rccl(apg_ctx* ctx, const void* id128, int rank, int world, uin
 int apg_comm_init_tcp(apg_ctx* ctx /* or NULL: host buffers */, const char* master_addr, int master_port,
                       int rank, int world, int timeout_ms /* <= 0: 600 s */, apg_comm** out);
 void apg_comm_destroy(apg_comm* comm);
+/* Tear the communicator down after a local failure so that peers blocked in
+ * a collective with this rank get an error instead of waiting: rccl aborts
+ * the RCCL communicator (ncclCommAbort), tcp shuts its sockets down.  Every
+ * later call on comm returns APG_E_STATE; apg_comm_destroy still frees it.
+ * RCCL collectives wait on the stream while polling ncclCommGetAsyncError,
+ * and give up (aborting) after APG_COMM_TIMEOUT_MS (default 600 000 ms). */
+int apg_comm_abort(apg_comm* comm);
 int apg_comm_rank(const apg_comm* comm);
 int apg_comm_world(const apg_comm* comm);
 /* send: world segments of send_bytes[q] bytes (segment q goes to rank q);

@@ -118,3 +118,55 @@ def test_tcp_missing_peer_times_out():
 
     with pytest.raises(ApgError):
         Comm.tcp(None, "127.0.0.1", free_port(), 1, 2, timeout_ms=1500)
+
+
+def abort_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    try:
+        import time
+
+        from allpathslg_amd.distributed import Comm
+
+        c = Comm.tcp(None, "127.0.0.1", port, rank, world, timeout_ms=600_000)
+        c.barrier()
+        t0 = time.time()
+        if rank == world - 1:  # a local failure on the last rank
+            time.sleep(0.5)
+            c.abort()
+            try:
+                c.barrier()
+                err = "no error"
+            except Exception as e:  # noqa: BLE001
+                err = str(e)
+        else:
+            try:
+                c.barrier()
+                err = "no error"
+            except Exception as e:  # noqa: BLE001
+                err = str(e)
+        q.put((rank, time.time() - t0, err))
+        c.close()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, -1.0, repr(e)))
+
+
+def test_tcp_abort_releases_peers():
+    """apg_comm_abort on one rank (tools/apg_modules.cpp does it before a FATAL
+    exit): its peers, blocked in a barrier with it, get an error within seconds
+    rather than waiting out the 600 s timeout; the aborted communicator refuses
+    further calls."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    ps = [ctx.Process(target=abort_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, dt, err in out:
+        assert err != "no error" and dt >= 0, (rank, err)
+        assert dt < 30, (rank, dt, err)
+        if rank == world - 1:
+            assert "aborted" in err, err

@@ -18,6 +18,8 @@
 
 namespace {
 
+apg_comm* g_comm = nullptr;  // the sharded run's communicator, for Args::fail
+
 struct Args {
   std::string module;
   std::map<std::string, std::string> kv;
@@ -37,6 +39,9 @@ struct Args {
   }
   [[noreturn]] void fail(const std::string& msg) {
     std::fprintf(stderr, "%s: FATAL: %s\n", module.c_str(), msg.c_str());
+    // a sharded rank: peers blocked in a collective with it error out
+    // instead of waiting (RCCL would wait without end)
+    if (g_comm) apg_comm_abort(g_comm);
     std::exit(1);
   }
   void check(int rc, const char* what) {
@@ -109,12 +114,16 @@ struct Shard {
     if (world < 1 || rank < 0 || rank >= world) a.fail("bad RANK / WORLD");
     if (mode != "rccl" && mode != "tcp") a.fail("COMM must be rccl or tcp");
   }
-  ~Shard() { apg_comm_destroy(comm); }
+  ~Shard() {
+    g_comm = nullptr;
+    apg_comm_destroy(comm);
+  }
   bool sharded() const { return world > 1; }
   void connect(Args& a, apg_ctx* ctx) {
     if (world == 1) return;
     if (mode == "tcp") {
       a.check(apg_comm_init_tcp(ctx, addr.c_str(), port, rank, world, 0, &comm), "apg_comm_init_tcp");
+      g_comm = comm;
       return;
     }
     apg_comm* boot = nullptr;
@@ -126,6 +135,7 @@ struct Shard {
     apg_comm_destroy(boot);
     a.check(rc, "bootstrap exchange");
     a.check(apg_comm_init_rccl(ctx, all.data(), rank, world, 0, &comm), "apg_comm_init_rccl");
+    g_comm = comm;
   }
   void barrier(Args& a) {
     if (comm) a.check(apg_comm_barrier(comm), "apg_comm_barrier");
