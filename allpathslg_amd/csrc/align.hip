@@ -9,7 +9,11 @@
 //   gap-free   one thread per (read, target, offset): 32 bases per XOR +
 //              popcount of the 2-bit difference mask; qualities summed only
 //              over mismatch bits.  VALU/latency bound, not HBM.
-//   banded SW  one wavefront per pair, one lane per band diagonal (chunks of
+//   banded SW  w <= 9 (k_banded_sw_lds): one lane per pair, directions kept on
+//              the CU (last 32 rows in VGPRs, the rest in LDS), score and
+//              direction in one min3; w <= 15 (k_banded_sw_lane): one lane per
+//              pair, directions through HBM; above: one wavefront per pair,
+//              one lane per band diagonal (chunks of
 //              64 diagonals): a DP row is one step per lane (diagonal and
 //              vertical predecessors are the lane's own and its neighbour's
 //              previous-row values) plus a wave min-plus prefix scan for the
@@ -20,6 +24,7 @@
 //   consensus  per placed base an atomic add of its quality into the target
 //              column's 4 vote counters, then one thread per column decides.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "apg_core.hpp"
@@ -491,6 +496,322 @@ __global__ void __launch_bounds__(256) k_banded_sw_lane(SeqSet S, SeqSet T, cons
 }
 
 // ---------------------------------------------------------------------------
+// Banded SW, one lane per pair, directions on the CU (w <= 9).
+// Same recurrence, tie order, end rule and outputs as k_banded_sw_lane,
+// re-shaped for the VALU:
+//  * a cell holds 4 * cost + code (code 0 diagonal, 1 gap in S = horizontal,
+//    2 gap in T = vertical), so one min3 over the three candidates is both the
+//    recurrence and the tie rule (diagonal before horizontal before vertical =
+//    the smaller code first); the row keeps 4 * cost (code bits cleared) and
+//    the code goes to the row's direction word;
+//  * the band is a template parameter (W = w): no per-cell band test, and a
+//    wave whose pairs keep the whole band inside their targets (the common
+//    case) runs its rows without validity tests;
+//  * a row's directions are 2 bits x band: diagonals 0..15 in one word, the
+//    rest (band 17 / 19: 2 / 6 bits) packed over rows into side words.  The
+//    last kSwVRows rows of a pair stay in VGPRs and the earlier ones go to LDS
+//    (one wave per workgroup, lane-interleaved words: conflict-free), so no
+//    direction reaches HBM and the LDS a wave needs (18.7 KiB for 100-base
+//    reads at w = 8) lets two waves share each SIMD.  Registers take only
+//    static indices, so the wave's lanes step through rows in lockstep,
+//    aligned at their last row (shorter reads idle first), and the traceback
+//    walks the rows in the same lockstep, each lane taking its horizontal moves
+//    within a row before the move that leaves it.
+// Per cell: mismatch bit, diagonal add, vertical add, horizontal add, min3,
+// two masks and the pack: about 9 VALU.
+// ---------------------------------------------------------------------------
+constexpr int32_t kSw4Inf = 1 << 28;
+constexpr int kSwLdsMaxW = 9;
+constexpr int kSwVRows = 32;  // rows whose directions stay in VGPRs
+
+__host__ __device__ constexpr int sw_lds_side_bits(int w) { return 2 * (2 * w + 1) > 32 ? 2 * (2 * w + 1) - 32 : 0; }
+__host__ __device__ constexpr int sw_lds_rows_per_side(int w) {
+  return sw_lds_side_bits(w) ? 32 / sw_lds_side_bits(w) : 1;
+}
+// 32-bit LDS words per lane for reads of up to rows_cap bases
+__host__ __device__ inline uint32_t sw_lds_words(int w, uint32_t rows_cap) {
+  const uint32_t rows = rows_cap > (uint32_t)kSwVRows ? rows_cap - kSwVRows : 0;
+  const uint32_t rps = (uint32_t)sw_lds_rows_per_side(w);
+  return rows + (sw_lds_side_bits(w) ? (rows + rps - 1) / rps : 0);
+}
+
+// the last kSwVRows rows' direction words: register vectors indexed by a
+// wave-uniform row slot (indirect register moves, no unrolled copies of the
+// row body — those overflowed the instruction cache)
+typedef uint32_t SwV32 __attribute__((ext_vector_type(kSwVRows)));
+typedef uint32_t SwV8 __attribute__((ext_vector_type(8)));
+template <int W>
+struct SwVDirs {
+  SwV32 m;
+  SwV8 s;  // side words (band 17 / 19: 2 / 7 used)
+};
+static_assert((kSwVRows + 4) / 5 <= 8, "side words of the register rows");
+
+// one DP row: G (4 x cost of row i-1, in place -> row i), mm = mismatch bit
+// of diagonal kk at bit 2 kk, j0 = column of diagonal 0
+template <int W, bool CHECK>
+__device__ __forceinline__ void sw_lds_row(int32_t (&G)[2 * W + 1], uint64_t mm, int j0, int Lt, uint32_t& mainw,
+                                           uint32_t& sidew) {
+  constexpr int B = 2 * W + 1;
+  int32_t hz = kSw4Inf;  // horizontal predecessor: row i, diagonal kk - 1
+  mainw = 0;
+  sidew = 0;
+#pragma unroll
+  for (int kk = 0; kk < B; ++kk) {
+    const uint32_t mis = __builtin_amdgcn_ubfe((uint32_t)(mm >> (kk < 16 ? 0 : 32)), (uint32_t)(2 * kk) & 31u, 1u);
+    const int32_t diag = G[kk] + (int32_t)(mis << 3);  // v_bfe + v_lshl_add
+    const int32_t vert = kk + 1 < B ? G[kk + 1 < B ? kk + 1 : kk] + 14 : kSw4Inf;  // 4 * 3 + code 2
+    int32_t d = min(min(diag, vert), hz + 13);                                       // 4 * 3 + code 1
+    if (CHECK && (uint32_t)(j0 + kk) > (uint32_t)Lt) d = kSw4Inf;                   // outside the target
+    const uint32_t code = (uint32_t)d & 3;
+    if (kk < 16)
+      mainw |= code << (2 * kk);
+    else
+      sidew |= code << (2 * (kk - 16));
+    hz = G[kk] = d & ~3;
+  }
+}
+
+// sw_tload without branches (a load under a per-lane branch makes the
+// compiler wait for every load in flight where the branches join): the
+// address is clamped into the target and the result fixed up by selects.
+__device__ __forceinline__ uint64_t sw_tload_nb(const uint8_t* tr, int Lt, int p) {
+  const int pc = min(max(p, 0), max(Lt - 1, 0));
+  const uint64_t v = load_lsb64(tr, (uint32_t)pc);
+  const uint64_t lo = p > -32 ? v << (2 * min(-p, 31)) : 0;  // p < 0: bases before the target read as 0
+  return p >= Lt ? 0 : p < 0 ? lo : v;
+}
+
+// The DP rows of one pair, in blocks of 32 lockstep steps (step t is the
+// lane's row t - off): a block's 32 bases of S and of T were loaded during the
+// previous block and the next block's are loaded at its start, so no global
+// load is waited on inside the row loop (one or two waves per SIMD cannot
+// hide that).  Steps 1 .. nL write their rows to LDS; the final block (steps
+// nL + 1 .. nL + 32, every lane's last 32 rows) keeps them in V.
+template <int W, bool CHECK>
+__device__ __forceinline__ void sw_lds_dp(int32_t (&G)[2 * W + 1], const uint8_t* sr, const uint8_t* tr, int Ls, int Lt,
+                                          bool rc, int dmin, int off, int nL, uint32_t* mainrow, uint32_t* siderow,
+                                          SwVDirs<W>& V) {
+  constexpr int SB = sw_lds_side_bits(W), RPS = sw_lds_rows_per_side(W);
+  // S window of the block whose first row is i0: bases [sq, sq + 32) hold its
+  // rows (rc: S[Ls - i]); clamped at 0 (rows < 1 of idle steps are not used)
+  auto s_start = [&](int i0) { return rc ? max(Ls - i0 - 31, 0) : max(i0 - 1, 0); };
+  int t0 = nL + 1 - 32 * ((nL + 31) / 32);  // first block start (<= 1)
+  int i0 = t0 - off;
+  // T: tb holds T[tp .. tp + 64) at a block's start (tp = i0 + dmin - 1)
+  unsigned __int128 tb = (unsigned __int128)sw_tload_nb(tr, Lt, i0 + dmin - 1) |
+                         ((unsigned __int128)sw_tload_nb(tr, Lt, i0 + dmin - 1 + 32) << 64);
+  int sq = s_start(i0);
+  uint64_t sw64 = load_lsb64(sr, (uint32_t)min(sq, max(Ls - 1, 0)));
+  uint64_t swn = 0, tn = 0;  // the next block's windows, in flight
+  bool first = true;
+  auto next_block = [&]() {
+    if (!first) {  // take the windows loaded during the previous block, before issuing the next
+      sq = s_start(i0);
+      sw64 = swn;
+      tb |= (unsigned __int128)tn << 64;  // 32 rows consumed: T[tp, tp + 32) remain in the low half
+    }
+    first = false;
+    swn = load_lsb64(sr, (uint32_t)min(s_start(i0 + 32), max(Ls - 1, 0)));  // unused past the read's end
+    tn = sw_tload_nb(tr, Lt, i0 + dmin - 1 + 64);
+  };
+  auto row = [&](int i, uint32_t& mw, uint32_t& sw) {
+    const int q = rc ? Ls - i : i - 1;
+    const uint32_t b = (uint32_t)(sw64 >> ((2 * (q - sq)) & 63)) & 3;
+    const uint32_t sb = rc ? 3 - b : b;
+    const uint64_t x = (uint64_t)tb ^ (sb * 0x5555555555555555ull);
+    const uint64_t mm = (x | (x >> 1)) & 0x5555555555555555ull;
+    sw_lds_row<W, CHECK>(G, mm, i + dmin, Lt, mw, sw);
+  };
+  uint32_t sacc = 0;
+  int sfill = 0, sidx = 0;
+  for (; t0 <= nL; t0 += 32, i0 += 32) {  // rows to LDS
+    next_block();
+    for (int r = 0; r < 32; ++r) {
+      const int i = i0 + r;
+      if (i >= 1) {
+        uint32_t mw, sw;
+        row(i, mw, sw);
+        mainrow[(uint32_t)(i - 1) * 64] = mw;
+        if (SB) {
+          sacc |= sw << (SB * sfill);
+          if (++sfill == RPS) {
+            siderow[(uint32_t)sidx * 64] = sacc;
+            ++sidx;
+            sacc = 0;
+            sfill = 0;
+          }
+        }
+      }
+      tb >>= 2;
+    }
+  }
+  if (SB && sfill) siderow[(uint32_t)sidx * 64] = sacc;
+  next_block();  // the last 32 rows: directions in registers
+  V.s = SwV8(0u);
+  for (int r = 0; r < kSwVRows; ++r) {  // r is wave-uniform
+    const int i = i0 + r;
+    uint32_t mw = 0, sw = 0;
+    if (i >= 1 && i <= Ls) row(i, mw, sw);
+    V.m[r] = mw;
+    if (SB) V.s[r / RPS] |= sw << (SB * (r % RPS));
+    tb >>= 2;
+  }
+}
+
+// The traceback from (Ls, kend) in the DP's lockstep: row by row from the
+// last, each lane's horizontal moves inside the row, then the diagonal or
+// vertical move that leaves it; move(d) sees every move in reverse order.
+// Returns the diagonal the path starts on (row 0).
+template <int W, typename F>
+__device__ __forceinline__ int sw_lds_walk(int Ls, int kend, int off, int nL, const uint32_t* mainrow,
+                                           const uint32_t* siderow, const SwVDirs<W>& V, F&& move) {
+  constexpr int SB = sw_lds_side_bits(W), RPS = sw_lds_rows_per_side(W);
+  int kk = kend;
+  auto in_row = [&](uint32_t mw, uint32_t sw) {
+    for (;;) {
+      const uint32_t d = kk < 16 ? (mw >> (2 * kk)) & 3 : (sw >> (2 * (kk - 16))) & 3;
+      move(d);
+      if (d == 1) {
+        --kk;
+        continue;
+      }
+      if (d == 2) ++kk;
+      break;
+    }
+  };
+  for (int r = kSwVRows - 1; r >= 0; --r) {  // r is wave-uniform
+    const int i = nL + 1 + r - off;
+    if (i >= 1 && i <= Ls) in_row(V.m[r], SB ? V.s[r / RPS] >> (SB * (r % RPS)) : 0u);
+  }
+  // LDS rows: the next row's words load while this row is walked
+  auto words = [&](int i, uint32_t& mw, uint32_t& sw) {
+    const uint32_t rr = (uint32_t)max(i - 1, 0);
+    mw = mainrow[rr * 64];
+    sw = SB ? siderow[(rr / RPS) * 64] >> (SB * (rr % RPS)) : 0u;
+  };
+  uint32_t nm, ns;
+  words(nL - off, nm, ns);
+  for (int i = nL - off; i >= 1; --i) {
+    const uint32_t mw = nm, sw = ns;
+    words(i - 1, nm, ns);
+    in_row(mw, sw);
+  }
+  return kk;
+}
+
+template <int W>
+__global__ void __launch_bounds__(64) k_banded_sw_lds(SeqSet S, SeqSet T, const AlnPair* __restrict__ pairs, uint64_t n,
+                                                      uint32_t rows_cap, SwOut o) {
+  constexpr int B = 2 * W + 1;
+  extern __shared__ uint32_t sw_lds[];
+  const int lane = (int)threadIdx.x;
+  const uint32_t lds_rows = rows_cap > (uint32_t)kSwVRows ? rows_cap - kSwVRows : 0;
+  uint32_t* mainrow = sw_lds + lane;                              // word of row i at (i - 1) * 64
+  uint32_t* siderow = sw_lds + (uint64_t)lds_rows * 64 + lane;    // side word (i - 1) / RPS
+  const uint64_t stride = (uint64_t)gridDim.x * 64;
+  uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
+  // the next pair's record and sequence bounds load during this pair's DP
+  AlnPair pr{};
+  int Ls = 0, Lt = 0;
+  const uint8_t* sr = nullptr;
+  const uint8_t* tr = nullptr;
+  auto meta = [&](const AlnPair& a, int& ls, int& lt, const uint8_t*& s_, const uint8_t*& t_) {
+    ls = (int)(S.base_off[a.s + 1] - S.base_off[a.s]);
+    lt = (int)(T.base_off[a.t + 1] - T.base_off[a.t]);
+    s_ = S.packed + S.byte_off[a.s];
+    t_ = T.packed + T.byte_off[a.t];
+  };
+  if (k < n) {
+    pr = pairs[k];
+    meta(pr, Ls, Lt, sr, tr);
+  }
+  AlnPair prn{};
+  int Lsn = 0, Ltn = 0;
+  const uint8_t* srn = nullptr;
+  const uint8_t* trn = nullptr;
+  for (; k < n; k += stride, pr = prn, Ls = Lsn, Lt = Ltn, sr = srn, tr = trn) {
+    prn = pairs[min(k + stride, n - 1)];  // unconditional (see sw_tload_nb); unused past the end
+    const bool rc = pr.flags & 1;
+    const int dmin = pr.off - W;
+    int maxLs = Ls;  // lockstep rows: the wave's longest read
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) maxLs = max(maxLs, __shfl_xor(maxLs, sh, 64));
+    const int off = maxLs - Ls;
+    const int nL = max(maxLs - kSwVRows, 0);
+    int32_t G[B];
+#pragma unroll
+    for (int kk = 0; kk < B; ++kk) G[kk] = (uint32_t)(dmin + kk) <= (uint32_t)Lt ? 0 : kSw4Inf;
+    SwVDirs<W> V;
+    // the whole band inside the target on every row (row 0 included)
+    const bool inside = dmin >= 0 && Ls + dmin + B - 1 <= Lt;
+    if (__all(inside))
+      sw_lds_dp<W, false>(G, sr, tr, Ls, Lt, rc, dmin, off, nL, mainrow, siderow, V);
+    else
+      sw_lds_dp<W, true>(G, sr, tr, Ls, Lt, rc, dmin, off, nL, mainrow, siderow, V);
+    meta(prn, Lsn, Ltn, srn, trn);  // lands during the traceback
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int kk = 0; kk < B; ++kk)
+      if (G[kk] < kSw4Inf / 2) best = min(best, ((unsigned long long)(uint32_t)(G[kk] >> 2) << 32) | (uint32_t)kk);
+    int32_t* r = o.res + 8 * k;
+    if (best == ~0ull) {
+      reinterpret_cast<int4*>(r)[0] = int4{0, 0, 0, 0};
+      reinterpret_cast<int4*>(r)[1] = int4{0, 0, 0, 1};
+      continue;
+    }
+    const int cost = (int)(best >> 32);
+    const int kend = (int)(best & 0xffffffffu);
+    // traceback pass 1: gaps, start, blocks (reverse segmentation, as in k_banded_sw_lane)
+    int gs = 0, gtn = 0, nrev = 0;
+    int lastlen = -1, lastgap = 0;
+    int len = 0, gap = 0;
+    bool inG = false;
+    // (state updates as selects: branches here make the compiler keep the
+    // counters in scratch behind a selected pointer)
+    const int kst = sw_lds_walk<W>(Ls, kend, off, nL, mainrow, siderow, V, [&](uint32_t d) {
+      const bool dg = d == 0, close = dg && inG;
+      const bool keep = close && nrev == 0;
+      lastlen = keep ? len : lastlen;
+      lastgap = keep ? gap : lastgap;
+      nrev += close ? 1 : 0;
+      len = close ? 1 : dg ? len + 1 : len;
+      gap = close ? 0 : gap + (d == 1 ? 1 : d == 2 ? -1 : 0);
+      inG = !dg;
+      gs += d == 1 ? 1 : 0;
+      gtn += d == 2 ? 1 : 0;
+    });
+    const bool emit_r = nrev == 0 ? true : (lastlen > 0 || lastgap != 0);
+    const int nb = nrev + (emit_r ? 1 : 0);
+    reinterpret_cast<int4*>(r)[0] = int4{cost, dmin + kst, Ls + dmin + kend, (cost - 3 * (gs + gtn)) / 2};
+    const bool over = o.blocks && (uint32_t)nb > o.max_blocks;
+    reinterpret_cast<int4*>(r)[1] = int4{gs, gtn, nb, over ? 2 : 0};
+    if (!o.blocks) continue;
+    int32_t* blk = o.blocks + 2 * k * (uint64_t)o.max_blocks;
+    auto put = [&](int idx, int g, int l) {
+      if (idx >= 0 && (uint32_t)idx < o.max_blocks) {
+        blk[2 * idx] = g;
+        blk[2 * idx + 1] = l;
+      }
+    };
+    const int rr = nrev;
+    int q = 0;
+    len = 0;
+    gap = 0;
+    inG = false;
+    sw_lds_walk<W>(Ls, kend, off, nL, mainrow, siderow, V, [&](uint32_t d) {
+      const bool dg = d == 0, close = dg && inG;
+      if (close && (q > 0 || emit_r)) put(rr - q, gap, len);
+      q += close ? 1 : 0;
+      len = close ? 1 : dg ? len + 1 : len;
+      gap = close ? 0 : gap + (d == 1 ? 1 : d == 2 ? -1 : 0);
+      inG = !dg;
+    });
+    if (q > 0 || emit_r) put(rr - q, gap, len);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Consensus
 // ---------------------------------------------------------------------------
 // Votes through an LDS column window: a block takes kVoteChunk consecutive
@@ -717,6 +1038,38 @@ int apg_banded_sw_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T, co
   SwOut o{reinterpret_cast<int32_t*>(d_out), d_blocks, d_blocks ? max_blocks : 0};
   if (d_blocks)  // entries past a pair's n_blocks read as zero
     APG_CHECK_HIP(hipMemsetAsync(d_blocks, 0, n * (uint64_t)max_blocks * 8, ctx->stream));
+  const uint64_t lds_bytes = band_w <= kSwLdsMaxW ? 4ull * 64 * sw_lds_words(band_w, rows_cap) : ~0ull;
+  if (lds_bytes <= 160ull * 1024 && !std::getenv("APG_SW_NO_LDS")) {  // directions in LDS, one wave per block
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 63) / 64, (uint64_t)ctx->n_cu * 64));
+    // pairs + results + the S / T bases: the direction rows never leave the CU
+    kbegin(ctx, "banded_sw", n * (16 + 32) + n * (uint64_t)rows_cap / 4 * 2);
+    const SeqSet ss = seqset(S), ts = seqset(T);
+    const AlnPair* pp = reinterpret_cast<const AlnPair*>(d_pairs);
+    auto go = [&](auto kern) -> int {
+      if (lds_bytes > 64 * 1024)
+        APG_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes));
+      kern<<<grid, 64, (size_t)lds_bytes, ctx->stream>>>(ss, ts, pp, n, rows_cap, o);
+      return APG_OK;
+    };
+    int rc = APG_OK;
+    switch (band_w) {
+      case 0: rc = go(k_banded_sw_lds<0>); break;
+      case 1: rc = go(k_banded_sw_lds<1>); break;
+      case 2: rc = go(k_banded_sw_lds<2>); break;
+      case 3: rc = go(k_banded_sw_lds<3>); break;
+      case 4: rc = go(k_banded_sw_lds<4>); break;
+      case 5: rc = go(k_banded_sw_lds<5>); break;
+      case 6: rc = go(k_banded_sw_lds<6>); break;
+      case 7: rc = go(k_banded_sw_lds<7>); break;
+      case 8: rc = go(k_banded_sw_lds<8>); break;
+      default: rc = go(k_banded_sw_lds<9>); break;
+    }
+    kend(ctx);
+    APG_TRY(rc);
+    APG_CHECK_HIP(hipGetLastError());
+    return sync(ctx);
+  }
   if (band_w <= 15) {  // lane per pair: 64 pairs per wave, the row in registers
     // direction rows for every thread of the grid: <= ~256 MiB
     const uint64_t per_thread = 8ull * (rows_cap + 1);
