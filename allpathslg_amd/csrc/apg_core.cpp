@@ -152,6 +152,8 @@ int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers) {
     APG_CHECK_HIP(hipMemcpy(ch[0].dst, ch[0].src, ch[0].n, hipMemcpyDeviceToHost));
     return APG_OK;
   }
+  if (const char* e = std::getenv("APG_D2H_WORKERS"))
+    if (std::atoi(e) > 0) workers = std::atoi(e);
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)workers, ch.size()));
   APG_TRY(staging_get(ctx, T));
   std::atomic<uint64_t> next{0};

@@ -23,6 +23,8 @@
 //   U7 pairs                       (u, rc u) keys, LSD radix sort on 192 bits
 //   U8 outputs                     ids, unibases, HyperKmerPath vertices
 //      (lock-free union-find over unipath ends), per-read KmerPaths
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -1556,9 +1558,21 @@ static int ceil_log2_u(uint64_t x) {
 }
 
 
+// Host arrays the caller owns (std::free).  Large ones are 2 MiB-aligned and
+// advised as transparent huge pages: the D2H workers' copies first-touch the
+// pages, and 4 KiB faults held the copy to ~13-16 GB/s (scripts/diag/d2h_rate.py).
+static void* host_alloc(uint64_t bytes) {
+  constexpr uint64_t kHuge = 2ull << 20;
+  if (bytes < 2 * kHuge) return std::malloc(std::max<uint64_t>(bytes, 1));
+  const uint64_t b = (bytes + kHuge - 1) & ~(kHuge - 1);
+  void* p = std::aligned_alloc(kHuge, b);
+  if (p && !std::getenv("APG_NO_THP")) (void)madvise(p, b, MADV_HUGEPAGE);
+  return p;
+}
+
 template <typename T>
 static T* host_dup(const T* d, uint64_t n, std::vector<D2HJob>* jobs, int* rc) {
-  T* h = (T*)std::malloc(std::max<uint64_t>(n, 1) * sizeof(T));
+  T* h = (T*)host_alloc(std::max<uint64_t>(n, 1) * sizeof(T));
   if (!h) {
     *rc = APG_E_NOMEM;
     return nullptr;
@@ -2013,7 +2027,14 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     out->path_len = host_dup(ilen, NI, &jobs, &rc);
   }
   if (rc == APG_OK) rc = sync(ctx);
+  const auto t_d2h = std::chrono::steady_clock::now();
   if (rc == APG_OK) rc = d2h_bulk(ctx, jobs);
+  if (ctx->verbose) {
+    uint64_t bytes = 0;
+    for (const auto& j : jobs) bytes += j.bytes;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_d2h).count();
+    vlog(ctx, "unipaths: graph to host %.1f MB in %.1f ms (%.1f GB/s)", bytes / 1e6, ms, bytes / 1e6 / std::max(ms, 1e-3));
+  }
   return rc;
 }
 

@@ -95,6 +95,9 @@ def parse():
     p.add_argument("--gather-nodes", action="store_true",
                    help="sharded path: replicated unipath build (every rank gathers all nodes) instead of the "
                         "sharded compaction")
+    p.add_argument("--lds-json", default=os.path.join(ROOT, "profiles", "current", "pmc", "lds.json"),
+                   help="per-kernel LDS-array utilisation from a rocprofv3 --pmc pass (scripts/pmc_lds.py): the "
+                        "roof of the LDS-hash bucket kernels")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "current", "pmc", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py); the default "
                         "is the latest round checkpoint's (scripts/gpu_checkpoint.sh), which ships to the GPU box")
@@ -788,6 +791,7 @@ def main():
         roofline["traffic_over_algorithmic"] = t / max(per_launch_bytes, 1)
     # the same figures for the step's largest kernels (time per step), the
     # dominant one first: where the step's time goes against the HBM roof
+    lj = json.load(open(a.lds_json)) if os.path.exists(a.lds_json) else {}
     top = []
     for k, (kms, kl, kb) in sorted(kt.items(), key=lambda kv: -kv[1][0])[:8]:
         pl_ms, pl_b = kms / max(kl, 1), kb / max(kl, 1)
@@ -797,6 +801,9 @@ def main():
              "traffic": tj[k]["traffic_bytes_per_launch"] if k in tj else None}
         if k in tj:
             e["traffic_over_algorithmic"] = e["traffic"] / max(pl_b, 1)
+        if k in lj and lj[k].get("lds_util") is not None:
+            e["lds"] = {"bound": "lds", "util": lj[k]["lds_util"], "bank_conflict_share": lj[k]["bank_conflict_share"],
+                        "source": os.path.relpath(a.lds_json, ROOT)}
         top.append(e)
     roofline["kernels"] = top
 
