@@ -526,6 +526,7 @@ def file_to_graph(ctx, reads, a) -> dict:
                                  "involved (tools/microbench/freshread.cpp), later reads at ~100-170 GB/s",
             "files_to_hbm_reread_ms": (t6 - t5) * 1e3,
             "files_to_hbm_reread_GBps": (reads.n_bases * 1.25) / max(t6 - t5, 1e-9) / 1e9,
+            "reads_per_s_with_reread": reads.n_reads / max((t6 - t5) + (t4 - t2), 1e-9),
             "spectrum_precorrect_fill_ms": (t3 - t2) * 1e3, "unipaths_with_d2h_ms": (t4 - t3) * 1e3,
             "graph_bytes_to_host": nb, "n_unipaths": ust["n_unipaths"]}
 
