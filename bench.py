@@ -620,6 +620,9 @@ def main():
     dreads = ctx.upload(reads)
     dfrags = None if frags is None else ctx.upload(frags)
     comm = None
+    # a stuck peer ends the run with an error (libapg polls RCCL's async error
+    # state) well before the driver's own limit
+    os.environ.setdefault("APG_COMM_TIMEOUT_MS", "300000")
     if sharded:
         if a.comm == "tcp":
             comm = Comm.tcp(ctx, os.environ.get("MASTER_ADDR", "127.0.0.1"),
@@ -627,7 +630,21 @@ def main():
         else:
             uid = [unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            comm = Comm.rccl(ctx, uid[0], rank, world)
+            try:
+                comm = Comm.rccl(ctx, uid[0], rank, world)
+                ok = 1
+            except Exception as e:  # noqa: BLE001
+                log(rank, f"RCCL communicator failed ({e}); falling back to the TCP communicator")
+                ok = 0
+            # every rank takes the same transport
+            flags = [None] * world
+            dist.all_gather_object(flags, ok)
+            if not all(flags):
+                if comm is not None:
+                    comm.close()
+                comm = Comm.tcp(ctx, os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                                int(os.environ.get("MASTER_PORT", "29500")) + 1, rank, world, timeout_ms=600_000)
+                a.comm = "tcp (RCCL init failed)"
     fill = {"out": None}  # device read set of the filled fragments, reused every step
 
     # --overlap: the K=25 spectrum of the pristine reads runs on a second
