@@ -1227,6 +1227,9 @@ constexpr int kUskMaxNk = 63;
 constexpr int kUskDigitBits = 5;
 constexpr uint64_t kUskBucketKmers = 2048;
 constexpr uint32_t kUskTab = 1024;  // LDS table slots: tag u32, key 3 x u64, ext u32
+// probes before a bucket is declared full (linear probing at load <= 0.9 stays
+// far below; a full table must not cost every later instance 1024 probes)
+constexpr uint32_t kUskProbeMax = 128;
 // 64 records per round keeps the block at 39.5 KiB of LDS: four blocks per CU
 // instead of three at 128 (usk_bucket 15.9 -> 14.5 ms on the C2 step)
 constexpr int kUskChunk = 64;       // records flattened per round
@@ -1440,6 +1443,13 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
     for (uint32_t s = tid; s < kUskTab; s += kUskBThreads) tag[s] = 0;
     if (tid == 0) ovf = 0;
     for (uint32_t c0 = 0; c0 < nr; c0 += kUskChunk) {
+      // the table filled in an earlier chunk (block-uniform after the chunk's
+      // barrier): the rest of the bucket goes to the global table as well, so
+      // stop here and load the next bucket's first records
+      if (c0 && ovf) {
+        if (tid < kUskChunk && tid < nnr) pre = rec[noff + tid];
+        break;
+      }
       uint32_t nk = 0;
       if (tid < kUskChunk && c0 + tid < nr) {
         nk = (uint32_t)(pre.w0 >> 32) & 0xff;
@@ -1486,7 +1496,7 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
             break;
           }
           s = (s + 1) & (kUskTab - 1);
-          if (++probe == kUskTab) {
+          if (++probe == kUskProbeMax) {
             ovf = 1;  // table full: the bucket goes through the global table
             break;
           }
