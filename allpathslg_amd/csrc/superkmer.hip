@@ -1034,10 +1034,14 @@ __device__ __forceinline__ void sk_big_add(unsigned long long* __restrict__ gkey
 }
 
 // Instances are first summed in a per-workgroup LDS table, flushed once per
-// chunk of kBigChunk records: a K-mer repeated thousands of times (tandem
-// arrays) costs one global atomic per chunk, not one per instance.
+// kBigFlush chunks of kBigChunk records: a K-mer repeated thousands of times
+// (tandem arrays) costs one global atomic per flush, not one per instance.
+// Flushing every 4 chunks took the repeats line's global pass 19.4 -> 36.4 ms:
+// a chunk's K-mers are mostly distinct, so the fuller table sent more
+// instances through 64 failed probes to the global fallback.
 constexpr uint32_t kBigChunk = 256;
 constexpr uint32_t kBigLds = 4096;
+constexpr uint32_t kBigFlush = 1;
 template <typename R>
 __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                                                              const uint32_t* __restrict__ ovf,
@@ -1054,6 +1058,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
   }
   __syncthreads();
   const uint64_t tot = opre[n_ovf];
+  uint32_t since = 0;  // chunks since the last flush
   for (uint64_t k0 = (uint64_t)blockIdx.x * kBigChunk; k0 < tot; k0 += (uint64_t)gridDim.x * kBigChunk) {
     const uint64_t k = k0 + tid;
     if (k < tot) {
@@ -1077,6 +1082,8 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
       }
     }
     __syncthreads();
+    if (++since < kBigFlush && k0 + (uint64_t)gridDim.x * kBigChunk < tot) continue;  // block-uniform
+    since = 0;
     for (uint32_t s = tid; s < kBigLds; s += kBigChunk) {
       const unsigned long long c = lkey[s];
       if (c != EMPTY) {
@@ -1106,15 +1113,16 @@ __global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __re
       const uint64_t c = rec_kmer(h, t, p);
       uint64_t s = khash(p.hp, c) & gmask;
       while (gkey[s] != c) s = (s + 1) & gmask;
-      if (gcnt[s] < min_solid) {
-        m |= 1u << t;
-        if (!wrec) {
-          const uint64_t x = r.pos + t;
-          atomicOr(&weak[x >> 6], 1ull << (x & 63));
-        }
-      }
+      if (gcnt[s] < min_solid) m |= 1u << t;
     }
-    if (wrec && m) wrec[r.pos] = m;
+    if (wrec) {
+      if (m) wrec[r.pos] = m;
+    } else if (m) {  // the record's mask in one or two ORs, as k_sk_bucket
+      const uint64_t b = r.pos;
+      const uint32_t sh = (uint32_t)(b & 63);
+      atomicOr(&weak[b >> 6], (unsigned long long)m << sh);
+      if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
+    }
   }
 }
 
