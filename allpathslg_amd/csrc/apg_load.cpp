@@ -7,13 +7,15 @@
 // one thread); here the payload goes from the file to HBM once: worker
 // threads pread fixed-size chunks into their own pinned buffers and issue the
 // H2D copy on their own stream, double-buffered, so file reads and PCIe
-// transfers overlap across chunks and threads.  On the MI355X hosts the first
-// read of a just-written page-cache file — what a module boundary reads, the
-// previous module wrote it — runs at ~15-17 GB/s from 16 threads with no GPU
-// involved (tools/microbench/freshread.cpp) and ~100-170 GB/s from the second
-// read on; the load follows (≈12-15 GB/s cold, 35-48 GB/s warm).  Copying out
-// of a mapping instead (APG_LOAD_IO=mmap) measured the same cold and slower
-// warm (24-27 GB/s: page faults on every fresh mapping).  The offset tables take the
+// transfers overlap across chunks and threads.  Measured on the MI355X pool
+// (40 M reads, 5 GB): 35-48 GB/s re-reading files already loaded once in the
+// process, 10-14 GB/s on the first load of files written just before
+// (bench.py file_to_graph, scripts/diag/load_rate.py); the host's own pread of
+// /dev/shm files varies ~13-150 GB/s from read to read with no GPU involved
+// (tools/microbench/freshread.cpp), so that first-load figure is not the
+// loader's alone.  Copying out of a mapping instead (APG_LOAD_IO=mmap)
+// measured the same first load and a slower re-read (24-27 GB/s: page faults
+// on every fresh mapping).  The offset tables take the
 // same path and are validated on the device (apg_fastb_read's rules:
 // monotone, from 0 to the header's total; qualb offsets equal fastb's; file
 // sizes exact), where the byte offsets are also derived.

@@ -521,9 +521,9 @@ def file_to_graph(ctx, reads, a) -> dict:
             "ms": total * 1e3, "reads_per_s": reads.n_reads / total,
             "files_to_hbm_ms": (t1 - t0) * 1e3,
             "files_to_hbm_GBps": (reads.n_bases * 1.25) / max(t1 - t0, 1e-9) / 1e9,
-            "files_to_hbm_note": "first read of just-written files (the module-boundary case); the host's own first "
-                                 "read of fresh page-cache pages runs at ~15-17 GB/s with 16 threads and no GPU "
-                                 "involved (tools/microbench/freshread.cpp), later reads at ~100-170 GB/s",
+            "files_to_hbm_note": "first load of the just-written files (the module-boundary case); the re-read of the "
+                                 "same files follows; host pread of /dev/shm files on this pool varies ~13-150 GB/s "
+                                 "from read to read (tools/microbench/freshread.cpp)",
             "files_to_hbm_reread_ms": (t6 - t5) * 1e3,
             "files_to_hbm_reread_GBps": (reads.n_bases * 1.25) / max(t6 - t5, 1e-9) / 1e9,
             "reads_per_s_with_reread": reads.n_reads / max((t6 - t5) + (t4 - t2), 1e-9),
