@@ -307,6 +307,8 @@ SIGNATURES = {
     "apg_pc_defaults": (None, [C.POINTER(apg_pc_params)]),
     "apg_precorrect": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(apg_pc_params), _u8p, _u8p, C.POINTER(apg_pc_stats)]),
     "apg_precorrect_dev": (C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
+    "apg_spectrum_precorrect_dev": (C.c_int, [_P, _P, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats),
+                                              C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
     "apg_reads_download": (C.c_int, [_P, _P, _u8p, _u8p]),
     "apg_shard_solid": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, C.c_uint32, _u64p]),
     "apg_solid_export": (C.c_int, [_P, C.c_void_p]),

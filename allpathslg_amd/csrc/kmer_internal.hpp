@@ -55,8 +55,11 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
                    SkResult* res);
 int sk_spectrum(apg_ctx* ctx, const apg_dreads* dr, int K, bool solid, uint32_t min_solid, uint64_t* hist,
                 size_t hist_len, SkResult* res);
+// up_res != null: also the K+1 spectrum of the same reads from the K records
+// (sk_can_fuse_up(K)), into up_hist (host, may be null) and up_res
 int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid, unsigned long long* weak,
-                  SkResult* res);
+                  SkResult* res, uint64_t* up_hist = nullptr, size_t up_hist_len = 0, SkResult* up_res = nullptr);
+bool sk_can_fuse_up(int K);
 uint64_t sk_sum_kmers(apg_ctx* ctx, const SK16* recs, uint64_t n, int* rc);
 constexpr int kSkShardBins = 32;  // per-shard digit groups of the exchange (2^kSkDigitBits)
 

@@ -1032,12 +1032,15 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   return APG_OK;
 }
 
-static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st) {
+// up_res: the fused K+1 spectrum of the uncorrected reads rides on the count
+// (apg_spectrum_precorrect_dev; sk_can_fuse_up(p.K))
+static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st,
+                           uint64_t* up_hist = nullptr, size_t up_hist_len = 0, SkResult* up_res = nullptr) {
   SkResult sr;
   if (p.K >= 9) {  // count + the weak-instance bitmap (no lookups for the weak tests)
     unsigned long long* weak = nullptr;
     APG_TRY(workspace_t(ctx, "pc_weak", dr->n_bases / 64 + 2, &weak));
-    APG_TRY(sk_solid_weak(ctx, dr, p.K, p.min_solid, weak, &sr));
+    APG_TRY(sk_solid_weak(ctx, dr, p.K, p.min_solid, weak, &sr, up_hist, up_hist_len, up_res));
     ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
     return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak);
   }
@@ -1254,6 +1257,38 @@ int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, ap
   std::memset(&st, 0, sizeof st);
   for (uint32_t c = 0; c < p.n_cycles; ++c) APG_TRY(precorrect_pass(ctx, dr, p, &st));
   if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_spectrum_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, int K_spec, uint64_t* hist, size_t hist_len,
+                                apg_kstats* kstats, const apg_pc_params* pp, apg_pc_stats* pstats) {
+  APG_REQUIRE(ctx && dr, "apg_spectrum_precorrect_dev: NULL argument");
+  apg_pc_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_pc_defaults(&p);
+  APG_TRY(check_pc(p));
+  if (K_spec != p.K + 1 || !sk_can_fuse_up(p.K)) {  // not fusable: the two modules in turn
+    APG_TRY(apg_kmer_spectrum_dev(ctx, dr, K_spec, hist, hist_len, kstats));
+    return apg_precorrect_dev(ctx, dr, &p, pstats);
+  }
+  APG_REQUIRE(hist_len == 0 || hist_len >= 2, "spectrum: hist_len must be 0 or >= 2");
+  APG_REQUIRE(dr->n_reads == 0 || dr->d_quals, "apg_precorrect: read set has no qualities");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  apg_pc_stats st;
+  std::memset(&st, 0, sizeof st);
+  SkResult ur;
+  APG_TRY(precorrect_pass(ctx, dr, p, &st, hist, hist_len, &ur));
+  for (uint32_t c = 1; c < p.n_cycles; ++c) APG_TRY(precorrect_pass(ctx, dr, p, &st));
+  if (kstats) {
+    std::memset(kstats, 0, sizeof(*kstats));
+    kstats->n_kmers = ur.n_kmers;
+    kstats->n_distinct = ur.n_distinct;
+    kstats->n_buckets = ur.nbuckets;
+    kstats->n_overflow = ur.n_overflow_buckets;
+  }
+  if (pstats) *pstats = st;
   return APG_OK;
 }
 

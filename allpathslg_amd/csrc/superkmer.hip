@@ -84,7 +84,17 @@ static SkP make_skp(int K) {
 }
 
 
-__device__ __forceinline__ SK16 make_rec(const uint8_t* rd, uint32_t a, uint32_t n, uint32_t key, int K) {
+// Record flanks (bits 40..45 of w0): the read's bases just before and just
+// after the record's bases, with presence bits.  The K-mer counts ignore them;
+// the fused K / K+1 count (k_sk_bucket<.., UP>) needs them for the K+1-mers
+// that straddle two records.  Record dedup fingerprints and compares a record
+// without them (kSkFlankMask).
+constexpr uint64_t kSkFlankMask = 0x3full << 40;
+__device__ __forceinline__ uint64_t sk_flank_bits(uint32_t lb, uint32_t rb, bool hl, bool hr) {
+  return ((uint64_t)(lb | (rb << 2) | ((uint32_t)hl << 4) | ((uint32_t)hr << 5))) << 40;
+}
+
+__device__ __forceinline__ SK16 make_rec(const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key, int K) {
   const uint32_t nb = n + (uint32_t)K - 1;  // <= 40
   uint64_t lo = sk_lsb64(rd, a);
   uint64_t hi = nb > 32 ? sk_lsb64(rd, a + 32) : 0;
@@ -92,8 +102,11 @@ __device__ __forceinline__ SK16 make_rec(const uint8_t* rd, uint32_t a, uint32_t
     lo &= (1ull << (2 * nb)) - 1;
   else
     hi &= nb == 32 ? 0ull : ((1ull << (2 * (nb - 32))) - 1);
+  const bool hl = a > 0, hr = a + nb < L;
+  const uint32_t lb = hl ? (rd[(a - 1) >> 2] >> (2 * ((a - 1) & 3))) & 3 : 0;
+  const uint32_t rb = hr ? (rd[(a + nb) >> 2] >> (2 * ((a + nb) & 3))) & 3 : 0;
   SK16 r;
-  r.w0 = (uint64_t)part_key(key) | ((uint64_t)n << 32) | ((lo & 0xffffull) << 48);
+  r.w0 = (uint64_t)part_key(key) | ((uint64_t)n << 32) | sk_flank_bits(lb, rb, hl, hr) | ((lo & 0xffffull) << 48);
   r.w1 = (lo >> 16) | (hi << 48);
   return r;
 }
@@ -178,8 +191,8 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
   uint64_t r0, r1;
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
   uint64_t t0 = r0;
-  auto f = [&](const uint8_t* rd, uint32_t, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
-    const SK16 x = make_rec(rd, a, n, key, p.K);
+  auto f = [&](const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
+    const SK16 x = make_rec(rd, L, a, n, key, p.K);
     const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
     const uint64_t pos = OutWantsPos<O>::value ? rv.base_off[t0 + q] + a : 0;  // the read's first base + a
     rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
@@ -242,10 +255,16 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_replay(SkReads rv, SkP p, int
       uint64_t hi = __builtin_amdgcn_alignbit(w3, w2, s);
       if (nb < 32) lo &= (1ull << (2 * nb)) - 1;
       hi = nb > 32 ? hi & ((1ull << (2 * (nb - 32))) - 1) : 0;
-      x.w0 = (uint64_t)part_key((uint32_t)d) | ((uint64_t)nk << 32) | ((lo & 0xffffull) << 48);
+      // flanks from the tile: the base before bit bo, the base at bit bo + 2 nb
+      const bool hl = a > 0, hr = a + nb < T.rlen[q];
+      const uint32_t bl = bo - 2, br = bo + 2 * nb;
+      const uint32_t lb = hl ? (T.words[bl >> 5] >> (bl & 31)) & 3 : 0;
+      const uint32_t rb = hr ? (T.words[br >> 5] >> (br & 31)) & 3 : 0;
+      x.w0 = (uint64_t)part_key((uint32_t)d) | ((uint64_t)nk << 32) | sk_flank_bits(lb, rb, hl, hr) |
+             ((lo & 0xffffull) << 48);
       x.w1 = (lo >> 16) | (hi << 48);
     } else {
-      x = make_rec(g, a, nk, (uint32_t)d, p.K);
+      x = make_rec(g, T.rlen[q], a, nk, (uint32_t)d, p.K);
     }
     const uint32_t dg = D ? (uint32_t)x.w0 >> (32 - D) : 0;
     uint64_t pos = 0;
@@ -322,6 +341,51 @@ __device__ __forceinline__ uint64_t rec_kmer(const SK16& r, uint32_t t, const Sk
   return fw < rc ? fw : rc;
 }
 
+// The K+1-mers of a K-record (the fused count, k_sk_bucket<.., UP>): slot
+// t in [-1, n-1] is the K+1-mer starting at record base t (t = -1 takes the
+// left flank, t = n-1 the right flank).  Every K+1-mer of a read lies on two
+// consecutive K-mers, and the record that holds the first K-mer of its
+// CANONICAL form counts it: that record's minimizer is the minimizer of that
+// K-mer, a function of the canonical K+1-mer alone, so every instance lands
+// in one bucket.  So the n-1 K+1-mers inside the record count here, the one
+// over the left flank counts here iff its reverse complement is canonical (its
+// canonical form starts with this record's first K-mer, reversed), the one
+// over the right flank iff it is canonical as read.  An odd K+1 has no
+// palindromes; for even K+1 a palindrome counts on its left K-mer.
+// p: the K+1 parameters (p.K = K + 1, p.hp.mask its 2(K+1)-bit mask).
+__device__ __forceinline__ uint64_t rec_kmer_up(const SK16& r, int t, const SkP& p, bool* own) {
+  const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff, fl = (uint32_t)(r.w0 >> 40) & 0x3f;
+  const uint32_t nb = n + (uint32_t)p.K - 2;  // record bases (K-mers of K = p.K - 1)
+  uint32_t a0 = (uint32_t)(r.w0 >> 48) | ((uint32_t)r.w1 << 16);
+  uint32_t a1 = (uint32_t)(r.w1 >> 16);
+  uint32_t a2 = (uint32_t)(r.w1 >> 48);
+  if (fl & 32) {  // right flank at base nb (<= 40: bits <= 81)
+    const uint32_t rb = (fl >> 2) & 3, bit = 2 * nb;
+    if (bit < 32)
+      a0 |= rb << bit;
+    else if (bit < 64)
+      a1 |= rb << (bit - 32);
+    else
+      a2 |= rb << (bit - 64);
+  }
+  const uint32_t tt = t < 0 ? 0u : (uint32_t)t;
+  const uint32_t sh = 2 * tt;
+  const bool up = sh >= 32;
+  const uint32_t b0 = up ? a1 : a0, b1 = up ? a2 : a1, b2 = up ? 0u : a2;
+  const uint32_t s5 = sh & 31;
+  uint64_t W = (uint64_t)__builtin_amdgcn_alignbit(b1, b0, s5) | ((uint64_t)__builtin_amdgcn_alignbit(b2, b1, s5) << 32);
+  if (t < 0) W = (W << 2) | (fl & 3);  // the left flank first
+  const uint64_t fw = sk_rev2(W) >> (64 - 2 * p.K);
+  const uint64_t rc = ~W & p.hp.mask;
+  if (t < 0)
+    *own = (fl & 16) && rc < fw;
+  else if ((uint32_t)t + 1 == n)
+    *own = (fl & 32) && fw <= rc;
+  else
+    *own = true;
+  return fw < rc ? fw : rc;
+}
+
 // Home of a canonical K-mer in a 2^bits table: the first slot of its aligned
 // group of kSkGrp slots.  The probe order is linear from there (group by
 // group), so a key sits before any empty slot of its probe sequence.
@@ -370,6 +434,7 @@ struct SkOut {
                                // index record.pos (the multi-GPU owner side: pos = receive index)
   unsigned long long* prof;    // diagnostics (APG_SK_PROF): k_sk_bucket_dd's per-phase clock64 sums, or null
   uint32_t want_hist;          // k_sk_bucket_dd: bin the spectrum (a solid-set count may not need it)
+  unsigned long long* inst;    // k_sk_bucket<.., UP>: K+1-mer instances counted (or null)
 };
 
 __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, const SkOut& o) {
@@ -390,12 +455,17 @@ __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, con
 // buckets k_sk_bucket_dd handed back.
 // TAB: LDS table slots (buckets of ~2 TAB instances); OWN: owner-map bytes per
 // record slot = the most K-mers a record holds (41 - K; 20 covers K >= 21).
-template <bool SOLID, typename R, int NT, uint32_t TAB = kSkTab, int OWN = kSkBases>
+// UP (R = SK24, not SOLID): count the K+1-mers of K-records (rec_kmer_up;
+// p = the K+1 parameters): a record offers n + 1 slots, the ones it does not
+// own are skipped.
+template <bool SOLID, typename R, int NT, uint32_t TAB = kSkTab, int OWN = kSkBases, bool UP = false>
 __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
                                                           const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
                                                           SkOut o, const uint32_t* __restrict__ blist = nullptr,
                                                           const unsigned long long* __restrict__ bcount = nullptr) {
   constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
+  static_assert(!UP || !SOLID, "the K+1 count is a spectrum count");
+  unsigned long long n_up = 0;  // UP: owned K+1-mer instances inserted by this thread
   // recorded slots: kSkWaveSlots per wave (NT = 512: each wave sees ~1/8 of a bucket)
   constexpr uint32_t kWaveSlots = NT >= 512 ? 1024 : kSkWaveSlots;
   constexpr uint32_t kSlotCap = kWaveSlots * (NT / 64);
@@ -464,6 +534,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     // wave scan and its own slice of the owner map: no block barriers until
     // the bucket's counts are final.
     uint32_t ibw = 0;  // this wave's K-mer instances before this chunk (wave-uniform)
+    unsigned long long n_up_b = 0;  // UP: this bucket's owned instances (dropped if it overflows)
     for (uint32_t c0 = 0; c0 < nr; c0 += NT) {
       if (__builtin_amdgcn_readfirstlane(*(volatile int*)&ovf)) {  // the table filled: stop, load the next bucket
         if (tid < nnr) pre = rec[noff + tid];
@@ -471,8 +542,16 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       }
       uint32_t nk = 0;
       if (c0 + tid < nr) {
-        nk = (uint32_t)(pre.w0 >> 32) & 0xff;
-        crec[tid] = rec_head(pre);
+        SK16 h = rec_head(pre);
+        nk = (uint32_t)(h.w0 >> 32) & 0xff;
+        if constexpr (UP) {  // the boundary K+1-mers this record owns, decided once per record
+          bool ol, orr;
+          (void)rec_kmer_up(h, -1, p, &ol);
+          (void)rec_kmer_up(h, (int)nk - 1, p, &orr);
+          nk = nk - 1 + (ol ? 1u : 0u) + (orr ? 1u : 0u);
+          h.w0 |= (uint64_t)ol << 46;  // slot f of the record is the K+1-mer at t = f - ol
+        }
+        crec[tid] = h;
       }
       if (c0 + NT < nr) {
         if (c0 + NT + tid < nr) pre = rec[off + c0 + NT + tid];
@@ -487,7 +566,15 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       wave_lds_sync();
       for (uint32_t f = ln; f < tot; f += 64) {
         const uint32_t i = (wv << 6) + wown[f];
-        const uint64_t c = rec_kmer(crec[i], f - koff[i], p);
+        uint64_t c;
+        if constexpr (UP) {
+          bool own;  // every slot is owned (decided at the chunk load)
+          const SK16 h = crec[i];
+          c = rec_kmer_up(h, (int)(f - koff[i]) - (int)((h.w0 >> 46) & 1), p, &own);
+          ++n_up_b;
+        } else {
+          c = rec_kmer(crec[i], f - koff[i], p);
+        }
         const uint32_t s = sk_tab_claim<TAB>(tkey, c, sk_slot(c, TB));
         const bool ok = s < TAB;
         if (!ok) ovf = 1;  // table full: the bucket goes to the global path
@@ -504,6 +591,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     // counts final; a wave past its recorded-slot capacity sends the whole
     // bucket's weak pass to the probing fallback
     const bool unrecorded = __syncthreads_or(WEAK && ibw > kWaveSlots);
+    if (UP && !ovf) n_up += n_up_b;
     if (ovf) {
       if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bid(bkt);
       __syncthreads();
@@ -634,6 +722,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   for (uint32_t i = tid; i < lim; i += NT)
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
+  if constexpr (UP) wave_add(o.inst, n_up);
 }
 
 // ---------------------------------------------------------------------------
@@ -676,7 +765,7 @@ constexpr uint32_t kDdInstCap = 3072;      // distinct-record K-mer instances pe
 constexpr int kDdMinK = kSkBases + 1 - 20;  // records hold <= 20 K-mers (owner-map loop bound)
 
 __device__ __forceinline__ uint64_t rec_fp(const SK16& h) {
-  const uint64_t x = sk_fmix(h.w1 ^ ((h.w0 >> 32) * 0x9e3779b97f4a7c15ull));
+  const uint64_t x = sk_fmix(h.w1 ^ (((h.w0 & ~kSkFlankMask) >> 32) * 0x9e3779b97f4a7c15ull));
   return x == ~0ull ? 0ull : x;  // ~0 marks an empty slot
 }
 
@@ -860,7 +949,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       __syncthreads();
       if (s < kDdTab) {
         const SK16 q = rrec[s];
-        if (q.w0 != hd.w0 || q.w1 != hd.w1) atomicOr(&flag, 2);  // fingerprint collision
+        if (((q.w0 ^ hd.w0) & ~kSkFlankMask) || q.w1 != hd.w1) atomicOr(&flag, 2);  // fingerprint collision
       }
     }
     __syncthreads();
@@ -1010,14 +1099,15 @@ __device__ __forceinline__ uint64_t sk_ovf_record(const uint64_t* __restrict__ b
   return boff[ovf[lo]] + (k - opre[lo]);
 }
 
-template <typename R>
+// UP: the K+1-mer slots of K-records (n + 1 each, an upper bound for sizing)
+template <typename R, bool UP = false>
 __global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                                const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
                                unsigned long long* __restrict__ n_kmers) {
   unsigned long long c = 0;
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x)
-    c += (uint32_t)(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)].w0 >> 32) & 0xff;
+    c += ((uint32_t)(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)].w0 >> 32) & 0xff) + (UP ? 1u : 0u);
   wave_add(n_kmers, c);
 }
 
@@ -1042,12 +1132,14 @@ __device__ __forceinline__ void sk_big_add(unsigned long long* __restrict__ gkey
 constexpr uint32_t kBigChunk = 256;
 constexpr uint32_t kBigLds = 4096;
 constexpr uint32_t kBigFlush = 1;
-template <typename R>
+template <typename R, bool UP = false>
 __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                                                              const uint32_t* __restrict__ ovf,
                                                              const uint64_t* __restrict__ opre, uint32_t n_ovf, SkP p,
                                                              unsigned long long* __restrict__ gkey,
-                                                             uint32_t* __restrict__ gcnt, uint64_t gmask) {
+                                                             uint32_t* __restrict__ gcnt, uint64_t gmask,
+                                                             unsigned long long* __restrict__ inst = nullptr) {
+  unsigned long long n_up = 0;
   constexpr unsigned long long EMPTY = ~0ull;
   __shared__ unsigned long long lkey[kBigLds];
   __shared__ uint32_t lcnt[kBigLds];
@@ -1063,9 +1155,17 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
     const uint64_t k = k0 + tid;
     if (k < tot) {
       const SK16 r = rec_head(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)]);
-      const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+      const uint32_t n = ((uint32_t)(r.w0 >> 32) & 0xff) + (UP ? 1u : 0u);
       for (uint32_t t = 0; t < n; ++t) {
-        const uint64_t c = rec_kmer(r, t, p);
+        uint64_t c;
+        if constexpr (UP) {
+          bool own;
+          c = rec_kmer_up(r, (int)t - 1, p, &own);
+          if (!own) continue;
+          ++n_up;
+        } else {
+          c = rec_kmer(r, t, p);
+        }
         const uint64_t h = khash(p.hp, c);
         uint32_t s = (uint32_t)(h >> 40) & (kBigLds - 1);
         bool done = false;
@@ -1094,6 +1194,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
     }
     __syncthreads();
   }
+  if constexpr (UP) wave_add(inst, n_up);
 }
 
 // Weak bits of the overflowed buckets' K-mer instances (counts from the
@@ -1315,11 +1416,88 @@ int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, 
 // instances, zeroed by the caller.
 __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out);
 
+// The fused K+1 spectrum (sk_solid_weak with up_K = K + 1): the K-records'
+// buckets, partitioned for the K count, counted again for their K+1-mers
+// (rec_kmer_up): the K+1 pass needs no walk, scatter or partition of its own.
+// Valid when K and K + 1 walk with the same m-mers (make_skp(K).m ==
+// make_skp(K + 1).m), so the records' minimizers are those of both K-mer
+// sizes' definition.  Overflowing buckets go through the global table.
+static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                       uint64_t* hist, size_t hist_len, SkResult* res) {
+  const SkP p = make_skp(K1);
+  const uint64_t hl = std::max<uint64_t>(hist_len, 2);
+  unsigned long long *ghist = nullptr, *gstats = nullptr, *inst = nullptr;
+  uint32_t* ovf = nullptr;
+  APG_TRY(workspace_t(ctx, "sku_hist", hl, &ghist));
+  APG_TRY(workspace_t(ctx, "sku_gstats", 5, &gstats));
+  APG_TRY(workspace_t(ctx, "sku_inst", 1, &inst));
+  APG_TRY(workspace_t(ctx, "sku_ovf", std::max<uint64_t>(nb, 1), &ovf));
+  APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 5 * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(inst, 0, 8, ctx->stream));
+  SkOut o{ghist, hl, gstats, ovf, nullptr, 0, 0, nullptr, nullptr, nullptr, 1u, inst};
+  const uint64_t grid = resident_grid(ctx, k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true>, kSkThreads, nb);
+  kbegin(ctx, "sk_bucket", n_rec * sizeof(SK24) + (nb + 1) * 8);
+  if (nb) k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hs[5];
+  APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (hs[1]) {  // overflowed buckets: one global table, as in sk_stage_count_t
+    unsigned long long* nk = gstats + 3;
+    APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
+    const uint32_t n_ovf = (uint32_t)hs[1];
+    uint32_t* osz = nullptr;
+    uint64_t* opre = nullptr;
+    APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
+    APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
+    k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovf, n_ovf, osz);
+    APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
+    const uint32_t g2 = (uint32_t)ctx->n_cu * 8;
+    k_sk_big_kmers<SK24, true><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
+    unsigned long long nbk = 0;
+    APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    uint64_t T = 1024;
+    while (T < 2 * nbk) T <<= 1;
+    unsigned long long* gkey = nullptr;
+    uint32_t* gcnt = nullptr;
+    APG_TRY(workspace_t(ctx, "sk_gkey", T, &gkey));
+    APG_TRY(workspace_t(ctx, "sk_gcnt", T, &gcnt));
+    APG_CHECK_HIP(hipMemsetAsync(gkey, 0xff, T * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
+    vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> global table", hs[1]);
+    kbegin(ctx, "sk_bucket_global", nbk * 64);
+    k_sk_big_insert<SK24, true><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1,
+                                                                  inst);
+    k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+  }
+  unsigned long long ninst = 0;
+  APG_CHECK_HIP(hipMemcpyAsync(&ninst, inst, 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (hist && hist_len) APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (hist && hist_len) hist[0] = 0;
+  *res = SkResult{};
+  res->n_distinct = hs[0];
+  res->n_overflow_buckets = hs[1];
+  res->nbuckets = nb;
+  res->n_kmers = ninst;
+  res->n_records = n_rec;
+  vlog(ctx, "sk count K=%d from K=%d records: kmers=%llu distinct=%llu ovf=%llu", K1, K1 - 1, ninst, hs[0], hs[1]);
+  return APG_OK;
+}
+
 template <typename R>
 static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vector<uint64_t>& rec_counts,
                             uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist,
                             size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr,
-                            const SK16* src16 = nullptr) {
+                            const SK16* src16 = nullptr, int up_K = 0, uint64_t* up_hist = nullptr,
+                            size_t up_hist_len = 0, SkResult* up_res = nullptr) {
   const SkP p = make_skp(K);
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
@@ -1579,6 +1757,9 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
        P, (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
        (unsigned long long)res->n_distinct, (unsigned long long)res->n_redo_buckets,
        (unsigned long long)res->n_overflow_buckets);
+  if constexpr (std::is_same<R, SK24>::value) {
+    if (up_K) APG_TRY(sk_up_count(ctx, cur, boff, nb, n, up_K, up_hist, up_hist_len, up_res));
+  }
   return APG_OK;
 }
 
@@ -1593,9 +1774,14 @@ int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector
 // base_off[r] + j of `weak` (zeroed here; (n_bases + 63) / 64 + 1 words) is
 // set iff K-mer j of read r has count < min_solid.  Needs K >= 9 (a record's
 // K-mers fit one 32-bit mask).
+bool sk_can_fuse_up(int K) { return K >= 9 && K + 1 <= 32 && make_skp(K).m == make_skp(K + 1).m; }
+
 int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid, unsigned long long* weak,
-                  SkResult* res) {
+                  SkResult* res, uint64_t* up_hist, size_t up_hist_len, SkResult* up_res) {
   APG_REQUIRE(K >= 9 && K <= 32, "sk_solid_weak: K must be in [9, 32]");
+  const bool up = up_res != nullptr;
+  APG_REQUIRE(!up || sk_can_fuse_up(K), "sk_solid_weak: the K+1 spectrum cannot ride on this K");
+  APG_REQUIRE(up_hist_len == 0 || up_hist_len >= 2, "spectrum: hist_len must be 0 or >= 2");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const uint64_t words = dr->n_bases / 64 + 2;
   APG_CHECK_HIP(hipMemsetAsync(weak, 0, words * 8, ctx->stream));
@@ -1607,7 +1793,8 @@ int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid,
   SK24* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
   APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
-  return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res);
+  return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res, nullptr, nullptr,
+                                up ? K + 1 : 0, up_hist, up_hist_len, up_res);
 }
 
 __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out) {

@@ -210,6 +210,19 @@ class Context:
                                    q.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(st)), "apg_precorrect")
         return ReadSet(reads.base_off.copy(), reads.byte_off.copy(), pk, q), st.as_dict()
 
+    def spectrum_precorrect(self, dreads: DeviceReads, K_spec: int = 25, K: int = 24, min_solid: int = 3,
+                            max_q_suspect: int = 20, n_cycles: int = 1, hist_len: int = DEFAULT_HIST_LEN):
+        """KmerSpectrum at K_spec, then PreCorrect at K, of one device read
+        set in one counting pass (apg_spectrum_precorrect_dev; the same
+        results as kmer_spectrum + precorrect).  Returns (hist, spectrum
+        stats, correction stats); the reads are corrected in place."""
+        p = self.pc_params(K, min_solid, max_q_suspect, n_cycles)
+        hist = np.zeros(hist_len, dtype=np.uint64)
+        ks, ps = apg_kstats(), apg_pc_stats()
+        check(lib().apg_spectrum_precorrect_dev(self._h, dreads.handle, K_spec, hist.ctypes.data_as(_u64p), hist_len,
+                                                C.byref(ks), C.byref(p), C.byref(ps)), "apg_spectrum_precorrect_dev")
+        return hist, ks.as_dict(), ps.as_dict()
+
     def copy_reads(self, dst: DeviceReads, src: DeviceReads) -> None:
         """dst := src (device-to-device; same read lengths)."""
         check(lib().apg_reads_copy_dev(self._h, dst.handle, src.handle), "apg_reads_copy_dev")

@@ -83,6 +83,9 @@ def parse():
                    help="jump library of the placement line (0 = none)")
     p.add_argument("--no-placement", dest="placement", action="store_false",
                    help="skip the UnipathLocs line (reads placed on the step's unipaths + aligners)")
+    p.add_argument("--no-fuse", dest="fuse", action="store_false",
+                   help="run KmerSpectrum (K) and PreCorrect (K_correct) as two counting passes instead of "
+                        "apg_spectrum_precorrect_dev's one (same results)")
     p.add_argument("--overlap", action="store_true",
                    help="run the K=25 spectrum on a second stream concurrently with correction/fill/unipaths")
     p.add_argument("--verbose", action="store_true")
@@ -433,8 +436,7 @@ def repeats_bench(ctx, a) -> dict:
 
     def step():
         ctx.copy_reads(dw, dsrc)
-        hist, kst = ctx.kmer_spectrum(dw, a.K)
-        _, pst = ctx.precorrect(dw, K=a.K_correct)
+        hist, kst, pst = spectrum_and_precorrect(ctx, dw, a)
         st["filled"], _, fst = ctx.fill_fragments(dw, K=a.K_correct, last_solid=True, out=st["filled"])
         _, ust = ctx.unipaths(st["filled"], a.K_unipath, read_paths=True, fetch=False)
         return hist, kst, pst, fst, ust
@@ -480,6 +482,17 @@ def repeats_bench(ctx, a) -> dict:
     return out
 
 
+def spectrum_and_precorrect(ctx, d, a):
+    """The step's KmerSpectrum (K) + PreCorrect (K_correct) of one device read
+    set: one counting pass (apg_spectrum_precorrect_dev) unless --no-fuse.
+    Returns (hist, spectrum stats, correction stats)."""
+    if a.fuse:
+        return ctx.spectrum_precorrect(d, K_spec=a.K, K=a.K_correct)
+    hist, kst = ctx.kmer_spectrum(d, a.K)
+    _, pst = ctx.precorrect(d, K=a.K_correct)
+    return hist, kst, pst
+
+
 def file_to_graph(ctx, reads, a) -> dict:
     """The module-boundary rate beside `value`: .fastb/.qualb files (on
     /dev/shm, so reading and PCIe, not a disk, are what is timed) -> HBM
@@ -497,8 +510,7 @@ def file_to_graph(ctx, reads, a) -> dict:
         t0 = time.perf_counter()
         d = ctx.load_reads(head + ".fastb", head + ".qualb")
         t1 = t2 = time.perf_counter()
-        ctx.kmer_spectrum(d, a.K)
-        ctx.precorrect(d, K=a.K_correct)
+        spectrum_and_precorrect(ctx, d, a)
         filled, _, _ = ctx.fill_fragments(d, K=a.K_correct, last_solid=True)
         t3 = time.perf_counter()
         g, ust = ctx.unipaths(filled, a.K_unipath, read_paths=True, fetch=True)
@@ -671,17 +683,21 @@ def main():
         mark("(between)")
         fut = pool.submit(ctx_s.kmer_spectrum, dsrc, a.K) if overlap else None
         ctx.copy_reads(dreads, dsrc)
+        pst = ust = fst = None
+        fused = not overlap and not sharded and not a.spectrum_only and a.fuse
         if overlap:
             pass
+        elif fused:  # one counting pass for both (apg_spectrum_precorrect_dev)
+            hist, st, pst = spectrum_and_precorrect(ctx, dreads, a)
         elif not sharded:
             hist, st = ctx.kmer_spectrum(dreads, a.K)
         else:
             hist, st = sharded_spectrum(ctx, comm, dreads, a.K)
         mark("spectrum")
-        pst = ust = fst = None
         if not a.spectrum_only:
             if not sharded:
-                _, pst = ctx.precorrect(dreads, K=a.K_correct)
+                if not fused:
+                    _, pst = ctx.precorrect(dreads, K=a.K_correct)
                 mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags
@@ -896,6 +912,9 @@ def main():
                 "K": a.K,
                 "K_correct": None if a.spectrum_only else a.K_correct,
                 "K_unipath": None if a.spectrum_only else a.K_unipath,
+                "counting": ("one pass: the K spectrum from PreCorrect's K_correct records "
+                             "(apg_spectrum_precorrect_dev)" if a.fuse and not sharded and not a.spectrum_only
+                             and not a.overlap else "separate K and K_correct passes"),
                 "stages_timed": ["restore_reads", "kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
                     "precorrect"] + ([] if a.oracle_fill else ["fill_fragments"]) + [
                     "unipath_kmers", "unipaths", "unibases", "hyperkmerpath", "fragment_kmerpaths"]),

@@ -278,6 +278,17 @@ int apg_precorrect(apg_ctx* ctx, const apg_reads* reads, const apg_pc_params* p,
 /* In place on a device read set (which must carry qualities). */
 int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
                        apg_pc_stats* stats);
+/* KmerSpectrum at K_spec + PreCorrect at p->K on the same device read set,
+ * one counting pass: the spectrum is taken from the correction's K-mer
+ * records before any base changes (each K_spec-mer counted once, by the
+ * record holding the first K-mer of its canonical form).  Results equal
+ * apg_kmer_spectrum_dev(reads, K_spec) followed by apg_precorrect_dev(reads,
+ * p).  The fused path needs K_spec == p->K + 1 with both K-mer sizes walking
+ * the same m-mers (true for 24 / 25, the module defaults); otherwise, and for
+ * the later cycles of p->n_cycles > 1, the two run one after the other.
+ * hist / stats as apg_kmer_spectrum_dev. */
+int apg_spectrum_precorrect_dev(apg_ctx* ctx, apg_dreads* reads, int K_spec, uint64_t* hist, size_t hist_len,
+                                apg_kstats* kstats, const apg_pc_params* p, apg_pc_stats* pstats);
 /* Copy a device read set's (possibly corrected) bases/quals back to host
  * buffers of the upload's sizes (quals may be NULL). */
 int apg_reads_download(apg_ctx* ctx, const apg_dreads* reads, uint8_t* packed, uint8_t* quals);

@@ -1,0 +1,106 @@
+"""apg_spectrum_precorrect_dev: the K=25 spectrum counted from PreCorrect's
+K=24 records in the same pass (superkmer.hip rec_kmer_up) equals the two
+modules run one after the other — spectrum histogram, its statistics, the
+corrected bases and qualities and the correction statistics — and the CPU
+restatement's spectrum.  Covers reads shorter than K, exactly K and K+1
+long, long reads (tile and global walks), the repeat-rich genome (LDS-table
+overflow of the K+1 pass) and the non-fusable fallback."""
+import numpy as np
+import pytest
+
+import oracle
+from allpathslg_amd import Context, ReadSet, synth_genome, synth_reads
+
+pytestmark = pytest.mark.gpu
+
+
+def mixed_lengths(seed=3, n=4000):
+    """Genome-derived reads with substitutions, lengths 1..300 (many at the
+    K boundaries 23-26), random qualities with low ones on some errors."""
+    rng = np.random.default_rng(seed)
+    g = synth_genome(200_000, seed)
+    lens = np.concatenate([rng.integers(1, 301, n // 2), rng.choice([23, 24, 25, 26, 27, 41, 42, 100], n - n // 2)])
+    seqs, quals = [], []
+    for L in lens:
+        s = int(rng.integers(0, len(g) - L))
+        r = g[s : s + L].copy()
+        q = np.full(L, 40, np.uint8)
+        err = rng.random(L) < 0.01
+        r[err] = (r[err] + rng.integers(1, 4, err.sum())) % 4
+        q[err] = rng.integers(2, 20, err.sum())
+        if rng.random() < 0.5:
+            r, q = (3 - r)[::-1].copy(), q[::-1].copy()
+        seqs.append(r.astype(np.uint8))
+        quals.append(q)
+    return ReadSet.from_sequences(seqs, quals)
+
+
+def both_ways(ctx, reads, K_spec=25, K=24, n_cycles=1):
+    a = ctx.upload(reads)
+    b = ctx.upload(reads)
+    try:
+        hs, ks = ctx.kmer_spectrum(a, K_spec)
+        _, ps = ctx.precorrect(a, K=K, n_cycles=n_cycles)
+        hf, kf, pf = ctx.spectrum_precorrect(b, K_spec=K_spec, K=K, n_cycles=n_cycles)
+        sep, fus = ctx.download(a), ctx.download(b)
+    finally:
+        a.free()
+        b.free()
+    return (hs, ks, ps, sep), (hf, kf, pf, fus)
+
+
+def assert_same(sep, fus):
+    hs, ks, ps, rs = sep
+    hf, kf, pf, rf = fus
+    assert np.array_equal(hs, hf)
+    assert ks["n_kmers"] == kf["n_kmers"] and ks["n_distinct"] == kf["n_distinct"]
+    assert np.array_equal(rs.packed, rf.packed) and np.array_equal(rs.quals, rf.quals)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+        assert ps[k] == pf[k], k
+
+
+def test_fused_equals_separate_mixed_lengths(gpu_ctx):
+    reads = mixed_lengths()
+    sep, fus = both_ways(gpu_ctx, reads)
+    assert_same(sep, fus)
+    assert np.array_equal(fus[0], oracle.kmer_spectrum(reads, 25))
+
+
+def test_fused_equals_separate_genome_reads(gpu_ctx):
+    g = synth_genome(2_000_000, 11)
+    reads = synth_reads(g, 400_000, seed=12)
+    sep, fus = both_ways(gpu_ctx, reads)
+    assert_same(sep, fus)
+    assert fus[1]["n_kmers"] == 76 * reads.n_reads
+
+
+def test_fused_on_repeats_overflow():
+    """Repeat-rich genome: buckets overflow the LDS table in the K+1 pass too
+    (global-table path); with record dedup off and on."""
+    g = synth_genome(1_000_000, 51, repeats={"tandem_frac": 0.03})
+    reads = synth_reads(g, 300_000, seed=52)
+    for dedup in (0, 1):
+        with Context(device=0, kmer_dedup=dedup) as ctx:
+            sep, fus = both_ways(ctx, reads)
+            assert_same(sep, fus)
+            assert fus[0][1000:].sum() > 0
+            assert fus[1]["n_overflow"] > 0
+
+
+def test_fused_findErrors_cycles(gpu_ctx):
+    """n_cycles = 2: the spectrum is the uncorrected reads'; the second cycle
+    recounts as apg_precorrect_dev does."""
+    g = synth_genome(500_000, 21)
+    reads = synth_reads(g, 100_000, seed=22)
+    sep, fus = both_ways(gpu_ctx, reads, n_cycles=2)
+    assert_same(sep, fus)
+
+
+def test_not_fusable_falls_back(gpu_ctx):
+    """K_spec != K + 1, or K / K+1 walking different m-mers (K = 19: m 11 vs
+    12): the two modules in turn, same results."""
+    g = synth_genome(300_000, 31)
+    reads = synth_reads(g, 60_000, seed=32)
+    for K_spec, K in ((31, 24), (20, 19)):
+        sep, fus = both_ways(gpu_ctx, reads, K_spec=K_spec, K=K)
+        assert_same(sep, fus)
