@@ -26,6 +26,7 @@ KERNELS = [
     ("void apg::k_sk_bucket_dd<true, apg::SK24>", "sk_bucket_solid", "stream"),
     ("void apg::k_sk_bucket<true, apg::SK24>", "sk_bucket_solid", "stream"),
     ("void apg::k_sk_bucket<false, apg::SK16>", "sk_bucket", "stream"),
+    ("void apg::k_sk_bucket<false, apg::SK24>", "sk_bucket", "stream"),  # the fused K+1 pass (UP)
     ("apg::k_sk_count", "sk_count", "stream"),
     ("void apg::k_sk_scatter<apg::SK16*>", "sk_scatter", "stream"),
     ("void apg::k_sk_scatter<apg::SK24*>", "sk_scatter", "stream"),
