@@ -326,10 +326,7 @@ __global__ void k_sk_digit_starts(const uint64_t* __restrict__ omat, uint32_t nd
 // Branch-free: the 80-bit string is three 32-bit limbs a0..a2 (a2 holds
 // bases 32..39); t <= 31, so the window is a funnel shift by 2t < 64 —
 // one limb select for 2t >= 32, then two v_alignbit.
-__device__ __forceinline__ uint64_t rec_kmer(const SK16& r, uint32_t t, const SkP& p) {
-  const uint32_t a0 = (uint32_t)(r.w0 >> 48) | ((uint32_t)r.w1 << 16);
-  const uint32_t a1 = (uint32_t)(r.w1 >> 16);
-  const uint32_t a2 = (uint32_t)(r.w1 >> 48);
+__device__ __forceinline__ uint64_t limb_kmer(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t t, const SkP& p) {
   const uint32_t sh = 2 * t;
   const bool up = sh >= 32;
   const uint32_t b0 = up ? a1 : a0, b1 = up ? a2 : a1, b2 = up ? 0u : a2;
@@ -339,6 +336,9 @@ __device__ __forceinline__ uint64_t rec_kmer(const SK16& r, uint32_t t, const Sk
   const uint64_t fw = sk_rev2(W) >> (64 - 2 * p.K);
   const uint64_t rc = ~W & p.hp.mask;
   return fw < rc ? fw : rc;
+}
+__device__ __forceinline__ uint64_t rec_kmer(const SK16& r, uint32_t t, const SkP& p) {
+  return limb_kmer((uint32_t)(r.w0 >> 48) | ((uint32_t)r.w1 << 16), (uint32_t)(r.w1 >> 16), (uint32_t)(r.w1 >> 48), t, p);
 }
 
 // The K+1-mers of a K-record (the fused count, k_sk_bucket<.., UP>): slot
@@ -384,6 +384,33 @@ __device__ __forceinline__ uint64_t rec_kmer_up(const SK16& r, int t, const SkP&
   else
     *own = true;
   return fw < rc ? fw : rc;
+}
+
+// The K+1-mer string of a record as the bucket kernel keeps it in LDS: the
+// record's bases with the owned flanks attached — the left flank as base 0
+// when the record owns that K+1-mer, the right flank after the last base —
+// as three 32-bit limbs (<= 42 bases), so that owned slot f is the K+1-mer at
+// string base f (limb_kmer) with no per-instance flank work.
+__device__ __forceinline__ uint4 rec_up_string(const SK16& r, const SkP& p, bool ol, bool orr) {
+  const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff, fl = (uint32_t)(r.w0 >> 40) & 0x3f;
+  uint32_t a0 = (uint32_t)(r.w0 >> 48) | ((uint32_t)r.w1 << 16);
+  uint32_t a1 = (uint32_t)(r.w1 >> 16);
+  uint32_t a2 = (uint32_t)(r.w1 >> 48);
+  if (orr) {
+    const uint32_t rb = (fl >> 2) & 3, bit = 2 * (n + (uint32_t)p.K - 2);
+    if (bit < 32)
+      a0 |= rb << bit;
+    else if (bit < 64)
+      a1 |= rb << (bit - 32);
+    else
+      a2 |= rb << (bit - 64);
+  }
+  if (ol) {
+    a2 = (a2 << 2) | (a1 >> 30);
+    a1 = (a1 << 2) | (a0 >> 30);
+    a0 = (a0 << 2) | (fl & 3);
+  }
+  return make_uint4(a0, a1, a2, 0u);
 }
 
 // Home of a canonical K-mer in a 2^bits table: the first slot of its aligned
@@ -549,9 +576,10 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
           (void)rec_kmer_up(h, -1, p, &ol);
           (void)rec_kmer_up(h, (int)nk - 1, p, &orr);
           nk = nk - 1 + (ol ? 1u : 0u) + (orr ? 1u : 0u);
-          h.w0 |= (uint64_t)ol << 46;  // slot f of the record is the K+1-mer at t = f - ol
+          *reinterpret_cast<uint4*>(&crec[tid]) = rec_up_string(h, p, ol, orr);  // slot f at string base f
+        } else {
+          crec[tid] = h;
         }
-        crec[tid] = h;
       }
       if (c0 + NT < nr) {
         if (c0 + NT + tid < nr) pre = rec[off + c0 + NT + tid];
@@ -567,10 +595,9 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       for (uint32_t f = ln; f < tot; f += 64) {
         const uint32_t i = (wv << 6) + wown[f];
         uint64_t c;
-        if constexpr (UP) {
-          bool own;  // every slot is owned (decided at the chunk load)
-          const SK16 h = crec[i];
-          c = rec_kmer_up(h, (int)(f - koff[i]) - (int)((h.w0 >> 46) & 1), p, &own);
+        if constexpr (UP) {  // every slot is owned (decided at the chunk load)
+          const uint4 a = *reinterpret_cast<const uint4*>(&crec[i]);
+          c = limb_kmer(a.x, a.y, a.z, f - koff[i], p);
           ++n_up_b;
         } else {
           c = rec_kmer(crec[i], f - koff[i], p);
