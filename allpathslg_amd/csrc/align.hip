@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(256) k_banded_sw_lane(SeqSet S, SeqSet T, cons
 //    walks the rows in the same lockstep, each lane taking its horizontal moves
 //    within a row before the move that leaves it.
 // Per cell: mismatch bit, diagonal add, vertical add, horizontal add, min3,
-// two masks and the pack: about 9 VALU.
+// the cost mask and the pack (v_alignbit): about 7 VALU.
 // ---------------------------------------------------------------------------
 constexpr int32_t kSw4Inf = 1 << 28;
 constexpr int kSwLdsMaxW = 9;
@@ -563,13 +563,15 @@ __device__ __forceinline__ void sw_lds_row(int32_t (&G)[2 * W + 1], uint64_t mm,
     const int32_t vert = kk + 1 < B ? G[kk + 1 < B ? kk + 1 : kk] + 14 : kSw4Inf;  // 4 * 3 + code 2
     int32_t d = min(min(diag, vert), hz + 13);                                       // 4 * 3 + code 1
     if (CHECK && (uint32_t)(j0 + kk) > (uint32_t)Lt) d = kSw4Inf;                   // outside the target
-    const uint32_t code = (uint32_t)d & 3;
+    // the code enters the word from the top (one v_alignbit: no mask + or)
     if (kk < 16)
-      mainw |= code << (2 * kk);
+      mainw = __builtin_amdgcn_alignbit((uint32_t)d, mainw, 2u);
     else
-      sidew |= code << (2 * (kk - 16));
+      sidew = __builtin_amdgcn_alignbit((uint32_t)d, sidew, 2u);
     hz = G[kk] = d & ~3;
   }
+  if constexpr (B < 16) mainw >>= 32 - 2 * B;  // diagonal 0 at bits 0..1
+  if constexpr (B > 16 && B < 32) sidew >>= 32 - 2 * (B - 16);
 }
 
 // sw_tload without branches (a load under a per-lane branch makes the
