@@ -484,12 +484,18 @@ __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, con
 // record slot = the most K-mers a record holds (41 - K; 20 covers K >= 21).
 // UP (R = SK24, not SOLID): count the K+1-mers of K-records (rec_kmer_up;
 // p = the K+1 parameters): a record offers n + 1 slots, the ones it does not
-// own are skipped.
+// own are skipped.  With dcount (UP): bucket b's records are the solid-set
+// count's distinct records (16-byte records at drec + boff[b], dcount[b] of
+// them, the multiplicity in place of the partition key) unless dcount[b] ==
+// ~0u (that bucket was not deduplicated: its records as partitioned,
+// multiplicity 1).
 template <bool SOLID, typename R, int NT, uint32_t TAB = kSkTab, int OWN = kSkBases, bool UP = false>
 __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
                                                           const uint64_t* __restrict__ boff, uint64_t nbuckets, SkP p,
                                                           SkOut o, const uint32_t* __restrict__ blist = nullptr,
-                                                          const unsigned long long* __restrict__ bcount = nullptr) {
+                                                          const unsigned long long* __restrict__ bcount = nullptr,
+                                                          const SK16* __restrict__ drec = nullptr,
+                                                          const uint32_t* __restrict__ dcount = nullptr) {
   constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
   static_assert(!UP || !SOLID, "the K+1 count is a spectrum count");
   unsigned long long n_up = 0;  // UP: owned K+1-mer instances inserted by this thread
@@ -527,30 +533,49 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   // bucket's bounds are loaded while the current chunk is counted.
   if (blist) nbuckets = *bcount;
   auto bid = [&](uint64_t q) -> uint64_t { return blist ? blist[q] : q; };
+  // a bucket's record source: its own records, or (UP with dcount; src =
+  // nullptr) its distinct ones, the multiplicity moved to .pos
+  auto bounds = [&](uint64_t q, const R*& src_, uint64_t& off_, uint32_t& nr_) {
+    const uint64_t b = bid(q);
+    off_ = boff[b];
+    uint32_t dc = ~0u;
+    if constexpr (UP) {
+      if (dcount) dc = dcount[b];
+    }
+    src_ = dc != ~0u ? nullptr : rec;
+    nr_ = dc != ~0u ? dc : (uint32_t)(boff[b + 1] - off_);
+  };
+  auto ld = [&](const R* src_, uint64_t i) -> R {
+    if constexpr (UP && sizeof(R) == sizeof(SK24)) {
+      if (!src_) {
+        const SK16 d = drec[i];
+        return R{d.w0, d.w1, d.w0 & 0xffffffffull};
+      }
+    }
+    return src_[i];
+  };
   uint64_t bkt = blockIdx.x, off = 0;
   uint32_t nr = 0;
-  if (bkt < nbuckets) {
-    off = boff[bid(bkt)];
-    nr = (uint32_t)(boff[bid(bkt) + 1] - off);
-  }
+  const R* src = rec;
+  if (bkt < nbuckets) bounds(bkt, src, off, nr);
   R pre{};
-  if (tid < nr) pre = rec[off + tid];
+  if (tid < nr) pre = ld(src, off + tid);
   for (; bkt < nbuckets;) {
     const uint64_t nbk = bkt + gridDim.x;
     uint64_t noff = 0;
     uint32_t nnr = 0;
-    if (nbk < nbuckets) {
-      noff = boff[bid(nbk)];
-      nnr = (uint32_t)(boff[bid(nbk) + 1] - noff);
-    }
+    const R* nsrc = rec;
+    if (nbk < nbuckets) bounds(nbk, nsrc, noff, nnr);
     if (nr == 0 || nr > kSkHeavyRecords) {  // block-uniform
       if (nr && tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bid(bkt);
-      if (tid < nnr) pre = rec[noff + tid];
+      if (tid < nnr) pre = ld(nsrc, noff + tid);
       bkt = nbk;
       off = noff;
       nr = nnr;
+      src = nsrc;
       continue;
     }
+    const bool mult = UP && !src;  // records carry their multiplicity (block-uniform)
     for (uint32_t s = tid; s < TAB; s += NT) {
       tkey[s] = EMPTY;
       tcnt[s] = 0;
@@ -564,7 +589,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     unsigned long long n_up_b = 0;  // UP: this bucket's owned instances (dropped if it overflows)
     for (uint32_t c0 = 0; c0 < nr; c0 += NT) {
       if (__builtin_amdgcn_readfirstlane(*(volatile int*)&ovf)) {  // the table filled: stop, load the next bucket
-        if (tid < nnr) pre = rec[noff + tid];
+        if (tid < nnr) pre = ld(nsrc, noff + tid);
         break;
       }
       uint32_t nk = 0;
@@ -576,15 +601,17 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
           (void)rec_kmer_up(h, -1, p, &ol);
           (void)rec_kmer_up(h, (int)nk - 1, p, &orr);
           nk = nk - 1 + (ol ? 1u : 0u) + (orr ? 1u : 0u);
-          *reinterpret_cast<uint4*>(&crec[tid]) = rec_up_string(h, p, ol, orr);  // slot f at string base f
+          uint4 str = rec_up_string(h, p, ol, orr);  // slot f at string base f
+          if constexpr (sizeof(R) == sizeof(SK24)) str.w = mult ? (uint32_t)pre.pos : 1u;
+          *reinterpret_cast<uint4*>(&crec[tid]) = str;
         } else {
           crec[tid] = h;
         }
       }
       if (c0 + NT < nr) {
-        if (c0 + NT + tid < nr) pre = rec[off + c0 + NT + tid];
+        if (c0 + NT + tid < nr) pre = ld(src, off + c0 + NT + tid);
       } else if (tid < nnr) {
-        pre = rec[noff + tid];
+        pre = ld(nsrc, noff + tid);
       }
       const uint32_t incl = wave_inclusive_scan<uint32_t>(nk);
       const uint32_t ex = incl - nk;
@@ -595,10 +622,12 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       for (uint32_t f = ln; f < tot; f += 64) {
         const uint32_t i = (wv << 6) + wown[f];
         uint64_t c;
+        uint32_t add = 1;
         if constexpr (UP) {  // every slot is owned (decided at the chunk load)
           const uint4 a = *reinterpret_cast<const uint4*>(&crec[i]);
           c = limb_kmer(a.x, a.y, a.z, f - koff[i], p);
-          ++n_up_b;
+          add = a.w;
+          n_up_b += add;
         } else {
           c = rec_kmer(crec[i], f - koff[i], p);
         }
@@ -606,7 +635,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
         const bool ok = s < TAB;
         if (!ok) ovf = 1;  // table full: the bucket goes to the global path
         if (ok) {
-          atomicAdd(&tcnt[s], 1u);
+          atomicAdd(&tcnt[s], add);
           if constexpr (WEAK) {
             if (ibw + f < kWaveSlots) wslot[ibw + f] = (uint16_t)s;
           }
@@ -625,6 +654,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       bkt = nbk;
       off = noff;
       nr = nnr;
+      src = nsrc;
       continue;
     }
     if constexpr (WEAK) {
@@ -743,6 +773,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     bkt = nbk;
     off = noff;
     nr = nnr;
+    src = nsrc;
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
@@ -778,6 +809,13 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
 // collision, more than kDdRecCap records (weak mode), more than kDdInstCap
 // distinct-record instances — is appended to `redo` for k_sk_bucket; a full
 // K-mer table sends it to the global-table path as there.
+// dout / dcount (SK24, the fused K+1 spectrum): records are folded with their
+// flank bases (so a distinct record fixes its K+1-mers too), and each bucket's
+// distinct records leave as 16-byte records, the multiplicity in place of
+// the partition key, at dout[boff[b] .. + dcount[b]) once its record table is
+// complete (dcount[b] = ~0u for a bucket whose record table could not be
+// completed): the K+1 count then inserts each distinct record's K+1-mers
+// once, with that multiplicity.
 constexpr int kDdThreads = 512;
 constexpr uint64_t kDdBucketKmers = 4096;  // instances per bucket the planner aims for with this kernel
 constexpr uint32_t kDdKTab = 2048;         // K-mer table slots
@@ -791,8 +829,8 @@ constexpr uint32_t kDdRecCap = kDdChunks * kDdThreads;
 constexpr uint32_t kDdInstCap = 3072;      // distinct-record K-mer instances per bucket
 constexpr int kDdMinK = kSkBases + 1 - 20;  // records hold <= 20 K-mers (owner-map loop bound)
 
-__device__ __forceinline__ uint64_t rec_fp(const SK16& h) {
-  const uint64_t x = sk_fmix(h.w1 ^ (((h.w0 & ~kSkFlankMask) >> 32) * 0x9e3779b97f4a7c15ull));
+__device__ __forceinline__ uint64_t rec_fp(const SK16& h, uint64_t keep = ~kSkFlankMask) {
+  const uint64_t x = sk_fmix(h.w1 ^ (((h.w0 & keep) >> 32) * 0x9e3779b97f4a7c15ull));
   return x == ~0ull ? 0ull : x;  // ~0 marks an empty slot
 }
 
@@ -830,8 +868,11 @@ __device__ __forceinline__ uint32_t lds_claim(unsigned long long* tk, uint64_t c
 template <bool SOLID, typename R>
 __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu(6))) k_sk_bucket_dd(const R* __restrict__ rec,
                                                              const uint64_t* __restrict__ boff, uint64_t nbuckets,
-                                                             SkP p, SkOut o, uint32_t* __restrict__ redo) {
+                                                             SkP p, SkOut o, uint32_t* __restrict__ redo,
+                                                             SK16* __restrict__ dout = nullptr,
+                                                             uint32_t* __restrict__ dcount = nullptr) {
   constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
+  const uint64_t keep = dout ? ~0ull : ~kSkFlankMask;  // record identity: with the flanks for the K+1 count
   constexpr int NT = kDdThreads;
   constexpr unsigned long long EMPTY = ~0ull;
   constexpr int KB = __builtin_ctz(kDdKTab), RB = __builtin_ctz(kDdTab);
@@ -865,7 +906,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
     flag = 0;
   }
   __syncthreads();
-  unsigned long long nd = 0;
+  unsigned long long nd = 0, n_dout = 0;  // n_dout: distinct records written (thread 0)
   // diagnostics: thread 0's clock64 between the phase barriers
   unsigned long long pt[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;
   const bool prof = o.prof != nullptr && tid == 0;
@@ -924,6 +965,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       finish();
     };
     if (nr == 0 || nr > kSkHeavyRecords || (WEAK && nr > kDdRecCap)) {  // block-uniform
+      if (dout && tid == 0) dcount[bkt] = nr ? ~0u : 0u;
       if (nr && tid == 0) {
         if (nr > kSkHeavyRecords)
           o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
@@ -958,7 +1000,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       uint32_t s = kDdTab;
       bool fresh = false;
       if (valid) {
-        const uint64_t fp = rec_fp(hd);
+        const uint64_t fp = rec_fp(hd, keep);
         s = lds_claim<kDdTab>(rkey, fp, (uint32_t)(fp >> (64 - RB)) & ~(kSkGrp - 1), &fresh);
         if (s < kDdTab) {
           if (fresh) rrec[s] = hd;
@@ -976,14 +1018,29 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       __syncthreads();
       if (s < kDdTab) {
         const SK16 q = rrec[s];
-        if (((q.w0 ^ hd.w0) & ~kSkFlankMask) || q.w1 != hd.w1) atomicOr(&flag, 2);  // fingerprint collision
+        if (((q.w0 ^ hd.w0) & keep) || q.w1 != hd.w1) atomicOr(&flag, 2);  // fingerprint collision
       }
     }
     __syncthreads();
     mark(1);
     if (flag) {  // block-uniform
+      if (dout && tid == 0) dcount[bkt] = ~0u;
       hand_back(false);
       continue;
+    }
+    if constexpr (sizeof(R) == sizeof(SK24)) {
+      if (dout) {  // the distinct records with their multiplicity, for the K+1 count
+        const uint32_t nD = nr_sh;
+        for (uint32_t j = tid; j < nD; j += NT) {
+          const uint32_t s = rlist[j];
+          const SK16 h = rrec[s];
+          dout[off + j] = SK16{(h.w0 & ~0xffffffffull) | rcnt[s], h.w1};
+        }
+        if (tid == 0) {
+          dcount[bkt] = nD;
+          n_dout += nD;
+        }
+      }
     }
     // 2. distinct records' first instance indices (one block scan; <= NT
     // distinct records per thread round), owner map
@@ -1097,6 +1154,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
   for (uint32_t i = tid; i < lim; i += NT)
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
+  if (dout && tid == 0 && n_dout) atomicAdd(&o.gstats[5], n_dout);  // one same-address atomic per block, not per bucket
 }
 
 // Overflowed buckets: every K-mer of every overflowed bucket into one global
@@ -1449,9 +1507,7 @@ __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __re
 // Valid when K and K + 1 walk with the same m-mers (make_skp(K).m ==
 // make_skp(K + 1).m), so the records' minimizers are those of both K-mer
 // sizes' definition.  Overflowing buckets go through the global table.
-static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
-                       uint64_t* hist, size_t hist_len, SkResult* res) {
-  const SkP p = make_skp(K1);
+static int sk_up_alloc(apg_ctx* ctx, uint64_t nb, size_t hist_len, SkOut* u) {
   const uint64_t hl = std::max<uint64_t>(hist_len, 2);
   unsigned long long *ghist = nullptr, *gstats = nullptr, *inst = nullptr;
   uint32_t* ovf = nullptr;
@@ -1459,30 +1515,43 @@ static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint
   APG_TRY(workspace_t(ctx, "sku_gstats", 5, &gstats));
   APG_TRY(workspace_t(ctx, "sku_inst", 1, &inst));
   APG_TRY(workspace_t(ctx, "sku_ovf", std::max<uint64_t>(nb, 1), &ovf));
-  APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 5 * 8, ctx->stream));
-  APG_CHECK_HIP(hipMemsetAsync(inst, 0, 8, ctx->stream));
-  SkOut o{ghist, hl, gstats, ovf, nullptr, 0, 0, nullptr, nullptr, nullptr, 1u, inst};
+  *u = SkOut{ghist, hl, gstats, ovf, nullptr, 0, 0, nullptr, nullptr, nullptr, 1u, inst};
+  return APG_OK;
+}
+
+// drec / dcount (may be null): the solid-set count's distinct records per
+// bucket (k_sk_bucket_dd's dout), n_drec of them in all.
+static int sk_up_run(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                     const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec, uint64_t* hist,
+                     size_t hist_len, SkResult* res) {
+  const SkP p = make_skp(K1);
+  APG_CHECK_HIP(hipMemsetAsync(u.ghist, 0, u.hist_len * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(u.gstats, 0, 5 * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(u.inst, 0, 8, ctx->stream));
   const uint64_t grid = resident_grid(ctx, k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true>, kSkThreads, nb);
-  kbegin(ctx, "sk_bucket", n_rec * sizeof(SK24) + (nb + 1) * 8);
-  if (nb) k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true><<<grid, kSkThreads, 0, ctx->stream>>>(cur, boff, nb, p, o);
+  // algorithmic bytes: the records read (the distinct ones with their
+  // multiplicity where the solid-set count folded them) and the bucket bounds
+  kbegin(ctx, "sk_bucket", (dcount ? n_drec * sizeof(SK16) : n_rec * sizeof(SK24)) + (nb + 1) * 8 + (dcount ? nb * 4 : 0));
+  if (nb)
+    k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true><<<grid, kSkThreads, 0, ctx->stream>>>(
+        cur, boff, nb, p, u, nullptr, nullptr, drec, dcount);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hs[5];
-  APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  if (hs[1]) {  // overflowed buckets: one global table, as in sk_stage_count_t
-    unsigned long long* nk = gstats + 3;
+  if (hs[1]) {  // overflowed buckets: their own records into one global table, as in sk_stage_count_t
+    unsigned long long* nk = u.gstats + 3;
     APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
     const uint32_t n_ovf = (uint32_t)hs[1];
     uint32_t* osz = nullptr;
     uint64_t* opre = nullptr;
     APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
     APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
-    k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovf, n_ovf, osz);
+    k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, u.ovf_list, n_ovf, osz);
     APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
     const uint32_t g2 = (uint32_t)ctx->n_cu * 8;
-    k_sk_big_kmers<SK24, true><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
+    k_sk_big_kmers<SK24, true><<<g2, 256, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, nk);
     unsigned long long nbk = 0;
     APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
@@ -1496,17 +1565,17 @@ static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint
     APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
     vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> global table", hs[1]);
     kbegin(ctx, "sk_bucket_global", nbk * 64);
-    k_sk_big_insert<SK24, true><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1,
-                                                                  inst);
-    k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+    k_sk_big_insert<SK24, true><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, p, gkey, gcnt,
+                                                                  T - 1, u.inst);
+    k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, u);
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
-    APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+    APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
   }
   unsigned long long ninst = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&ninst, inst, 8, hipMemcpyDeviceToHost, ctx->stream));
-  if (hist && hist_len) APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipMemcpyAsync(&ninst, u.inst, 8, hipMemcpyDeviceToHost, ctx->stream));
+  if (hist && hist_len) APG_CHECK_HIP(hipMemcpyAsync(hist, u.ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
   if (hist && hist_len) hist[0] = 0;
   *res = SkResult{};
@@ -1515,8 +1584,16 @@ static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint
   res->nbuckets = nb;
   res->n_kmers = ninst;
   res->n_records = n_rec;
-  vlog(ctx, "sk count K=%d from K=%d records: kmers=%llu distinct=%llu ovf=%llu", K1, K1 - 1, ninst, hs[0], hs[1]);
+  vlog(ctx, "sk count K=%d from K=%d records%s: kmers=%llu distinct=%llu ovf=%llu", K1, K1 - 1,
+       dcount ? " (distinct records x multiplicity)" : "", ninst, hs[0], hs[1]);
   return APG_OK;
+}
+
+static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                       uint64_t* hist, size_t hist_len, SkResult* res) {
+  SkOut u;
+  APG_TRY(sk_up_alloc(ctx, nb, hist_len, &u));
+  return sk_up_run(ctx, cur, boff, nb, n_rec, K1, u, nullptr, nullptr, 0, hist, hist_len, res);
 }
 
 template <typename R>
@@ -1540,7 +1617,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   // pass 33.4 -> 25.9 ms; the plain spectrum count 18.8 -> 22.9 ms, so by
   // default (apg_config.kmer_dedup = 0) the spectrum keeps k_sk_bucket;
   // APG_SK_DEDUP=all / none overrides the context's setting.
-  static const char* dd_env = getenv("APG_SK_DEDUP");
+  const char* dd_env = getenv("APG_SK_DEDUP");  // per call (tests switch it)
   int mode = ctx->kmer_dedup;
   if (dd_env) mode = !strcmp(dd_env, "all") ? 1 : !strcmp(dd_env, "none") ? 2 : mode;
   const bool dd = K >= kDdMinK && mode != 2 && (solid || mode == 1);
@@ -1637,11 +1714,22 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   uint32_t* ovf = nullptr;
   APG_TRY(workspace_t(ctx, "sk_hist", hl, &ghist));
   uint32_t* redo = nullptr;
-  APG_TRY(workspace_t(ctx, "sk_gstats", 5, &gstats));  // distinct, overflow, solid, scratch, handed back
+  // distinct, overflow, solid, scratch, handed back, distinct records written (dout)
+  APG_TRY(workspace_t(ctx, "sk_gstats", 6, &gstats));
   APG_TRY(workspace_t(ctx, "sk_ovf", std::max<uint64_t>(nb, 1), &ovf));
   APG_TRY(workspace_t(ctx, "sk_redo", std::max<uint64_t>(nb, 1), &redo));
   APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 5 * 8, ctx->stream));
+  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
+  // The fused K+1 spectrum (up_K) rides on the record dedup: the solid-set
+  // count folds records with their flanks and hands each bucket's distinct
+  // records (with multiplicity) to the K+1 pass through the free partition
+  // buffer (APG_SK_UP_DD=0: the K+1 pass reads every record instead).
+  const bool up_dd_env = !getenv("APG_SK_UP_DD") || strcmp(getenv("APG_SK_UP_DD"), "0") != 0;
+  R* dbuf = (cur == bufA) ? bufB : bufA;
+  const bool up_dd = up_K && dd && solid && up_dd_env && std::is_same<R, SK24>::value && dbuf && dbuf != cur &&
+                     (const void*)dbuf != (const void*)src16;
+  uint32_t* dcount = nullptr;
+  if (up_dd) APG_TRY(workspace_t(ctx, "sk_dcount", std::max<uint64_t>(nb, 1), &dcount));
   uint64_t solid_cap = 0;
   uint64_t* sl = nullptr;
   if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
@@ -1674,6 +1762,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   const uint64_t grid_dd = !dd ? 0
                            : solid ? resident_grid(ctx, k_sk_bucket_dd<true, R>, kDdThreads, nb)
                                    : resident_grid(ctx, k_sk_bucket_dd<false, R>, kDdThreads, nb);
+  uint64_t n_drec = 0;
   for (int attempt = 0;; ++attempt) {
     // Algorithmic bytes (inputs read once + outputs written once): the records
     // and bucket offsets; the weak output (one bit per K-mer instance, or a
@@ -1684,7 +1773,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) + (nb + 1) * 8 + weak_out);
     if (dd) {
       if (solid) {
-        k_sk_bucket_dd<true, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
+        k_sk_bucket_dd<true, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(
+            cur, boff, nb, p, o, redo, up_dd ? reinterpret_cast<SK16*>(dbuf) : nullptr, dcount);
         k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
       } else {
         k_sk_bucket_dd<false, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
@@ -1701,9 +1791,10 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     }
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
-    unsigned long long hs[5];
+    unsigned long long hs[6];
     APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
+    n_drec = hs[5];
     if (hs[1]) {  // overflowed buckets: one global table
       unsigned long long* nk = gstats + 3;
       APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
@@ -1752,6 +1843,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
               (int)solid, (double)hp[0], (double)hp[1], (double)hp[2], (double)hp[3], (double)hp[4], (double)hp[5], hs[4]);
     }
     if (solid) kbytes_add(ctx, "sk_bucket_solid", std::min<uint64_t>(hs[2], solid_cap) * 8);
+    if (up_dd) kbytes_add(ctx, "sk_bucket_solid", n_drec * sizeof(SK16) + nb * 4);  // distinct records out
     if (!solid || hs[2] <= solid_cap) {
       res->n_distinct = hs[0];
       res->n_overflow_buckets = hs[1];
@@ -1771,7 +1863,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     o.solid = sl;
     o.solid_cap = solid_cap;
     APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 5 * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
   }
   if (hist && hist_len) {
     APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1785,7 +1877,14 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
        (unsigned long long)res->n_distinct, (unsigned long long)res->n_redo_buckets,
        (unsigned long long)res->n_overflow_buckets);
   if constexpr (std::is_same<R, SK24>::value) {
-    if (up_K) APG_TRY(sk_up_count(ctx, cur, boff, nb, n, up_K, up_hist, up_hist_len, up_res));
+    if (up_K && up_dd) {
+      SkOut u;
+      APG_TRY(sk_up_alloc(ctx, nb, up_hist_len, &u));
+      APG_TRY(sk_up_run(ctx, cur, boff, nb, n, up_K, u, reinterpret_cast<const SK16*>(dbuf), dcount, n_drec, up_hist,
+                        up_hist_len, up_res));
+    } else if (up_K) {
+      APG_TRY(sk_up_count(ctx, cur, boff, nb, n, up_K, up_hist, up_hist_len, up_res));
+    }
   }
   return APG_OK;
 }

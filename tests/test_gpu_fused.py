@@ -104,3 +104,21 @@ def test_not_fusable_falls_back(gpu_ctx):
     for K_spec, K in ((31, 24), (20, 19)):
         sep, fus = both_ways(gpu_ctx, reads, K_spec=K_spec, K=K)
         assert_same(sep, fus)
+
+
+@pytest.mark.parametrize("env", [{"APG_SK_UP_DD": "0"}, {"APG_SK_DEDUP": "none"}])
+def test_fused_kplus1_record_sources(gpu_ctx, monkeypatch, env):
+    """The K+1 pass reads each bucket's distinct records with their
+    multiplicity (the solid-set count's dedup output; buckets it handed back
+    are read as partitioned).  The same results with the K+1 pass reading
+    every record (APG_SK_UP_DD=0) and with no record dedup at all; on a
+    repeat-rich genome, so some buckets take each route."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth_genome(1_000_000, 61, repeats={"tandem_frac": 0.03})
+    reads = synth_reads(g, 300_000, seed=62)
+    sep, fus = both_ways(gpu_ctx, reads)
+    assert_same(sep, fus)
+    monkeypatch.undo()
+    _, fus_dd = both_ways(gpu_ctx, reads)
+    assert_same(sep, fus_dd)
