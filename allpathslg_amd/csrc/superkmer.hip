@@ -462,7 +462,39 @@ struct SkOut {
   unsigned long long* prof;    // diagnostics (APG_SK_PROF): k_sk_bucket_dd's per-phase clock64 sums, or null
   uint32_t want_hist;          // k_sk_bucket_dd: bin the spectrum (a solid-set count may not need it)
   unsigned long long* inst;    // k_sk_bucket<.., UP>: K+1-mer instances counted (or null)
+  uint32_t* sused;             // solid mode: entries written in each kSolidChunk-slot chunk of `solid`
+  uint64_t n_sused;
 };
+
+// Solid-list reservations: a block takes whole chunks of kSolidChunk slots
+// from gstats[2] and fills them bucket by bucket (a same-address atomic per
+// bucket — a million of them per pass — serialised at the L2: a per-bucket
+// counter add in k_sk_bucket_dd cost 4.3 ms); o.solid holds the chunks
+// sparse, o.sused[c] how much of chunk c is used, and sk_solid_compact makes
+// the list dense.  A bucket never has more than kSolidChunk solid K-mers (its
+// LDS table has <= 2048 slots).
+constexpr uint32_t kSolidChunk = 4096;
+struct SolidRes {
+  unsigned long long cs;  // current chunk's first slot (~0: none)
+  uint32_t cu;            // slots of it used
+};
+__device__ __forceinline__ void solid_close(const SolidRes& r, const SkOut& o) {
+  if (r.cs == ~0ull) return;
+  const uint64_t c = r.cs / kSolidChunk;
+  if (c < o.n_sused) o.sused[c] = r.cu;
+}
+// thread 0: first slot for n more solid K-mers of this block (n <= kSolidChunk)
+__device__ __forceinline__ unsigned long long solid_take(SolidRes& r, uint32_t n, const SkOut& o) {
+  if (n == 0) return 0;
+  if (r.cs == ~0ull || r.cu + n > kSolidChunk) {
+    solid_close(r, o);
+    r.cs = atomicAdd(&o.gstats[2], (unsigned long long)kSolidChunk);
+    r.cu = 0;
+  }
+  const unsigned long long b = r.cs + r.cu;
+  r.cu += n;
+  return b;
+}
 
 __device__ __forceinline__ void sk_spectrum_add(uint32_t c, uint32_t* lhist, const SkOut& o) {
   uint64_t m = c;
@@ -512,6 +544,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   __shared__ uint32_t scan_sm[32];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
+  __shared__ SolidRes sres;
   // weak pass: table slot of each of the bucket's first kSlotCap K-mer
   // instances (in record order), recorded while counting — slots never move
   // once claimed, so the weak pass reads final counts without probing.  A
@@ -527,6 +560,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
   constexpr int TB = __builtin_ctz(TAB);
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kSkHistBins; i += NT) lhist[i] = 0;
+  if (tid == 0) sres = SolidRes{~0ull, 0};
   unsigned long long nd = 0;
   // The block's buckets bkt, bkt + grid, ... are one record stream: the next
   // chunk's record (this bucket's or the next bucket's first) and the next
@@ -760,7 +794,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     if (SOLID) {
       uint32_t tot;
       uint32_t j = block_exclusive_scan<uint32_t>(ns, scan_sm, &tot);
-      if (tid == 0) sbase = tot ? atomicAdd(&o.gstats[2], (unsigned long long)tot) : 0ull;
+      if (tid == 0) sbase = solid_take(sres, tot, o);
       __syncthreads();
       const unsigned long long b = sbase;
       for (uint32_t s = tid; s < TAB; s += NT)
@@ -781,6 +815,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
   if constexpr (UP) wave_add(o.inst, n_up);
+  if (SOLID && tid == 0) solid_close(sres, o);
 }
 
 // ---------------------------------------------------------------------------
@@ -890,6 +925,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
   __shared__ uint32_t nk_sh, nr_sh, ns_sh;  // claimed K-mer slots, claimed record slots, solid K-mers
   __shared__ int flag;  // 1: K-mer table full (global path); 2: hand the bucket back (redo)
   __shared__ unsigned long long sbase;
+  __shared__ SolidRes sres;
   const uint32_t tid = threadIdx.x;
   const bool want_hist = o.want_hist != 0;
   for (uint32_t i = tid; i < kSkHistBins; i += NT) lhist[i] = 0;
@@ -904,6 +940,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
   if (tid == 0) {
     nk_sh = nr_sh = ns_sh = 0;
     flag = 0;
+    sres = SolidRes{~0ull, 0};
   }
   __syncthreads();
   unsigned long long nd = 0, n_dout = 0;  // n_dout: distinct records written (thread 0)
@@ -1136,7 +1173,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
     if (SOLID) {
       __syncthreads();
       const uint32_t ns = ns_sh;
-      if (tid == 0) sbase = ns ? atomicAdd(&o.gstats[2], (unsigned long long)ns) : 0ull;
+      if (tid == 0) sbase = solid_take(sres, ns, o);
       __syncthreads();
       const unsigned long long b = sbase;
       for (uint32_t j = tid; j < ns; j += NT)
@@ -1155,6 +1192,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
   if (dout && tid == 0 && n_dout) atomicAdd(&o.gstats[5], n_dout);  // one same-address atomic per block, not per bucket
+  if (SOLID && tid == 0) solid_close(sres, o);
 }
 
 // Overflowed buckets: every K-mer of every overflowed bucket into one global
@@ -1323,13 +1361,17 @@ __global__ void __launch_bounds__(256) k_sk_big_emit(const unsigned long long* _
   __shared__ unsigned long long sbuf[SOLID ? kEmitBuf : 1];
   __shared__ uint32_t scnt;
   __shared__ unsigned long long sbase;
+  __shared__ SolidRes sres;
   const uint32_t tid = threadIdx.x;
   for (uint32_t i = tid; i < kSkHistBins; i += blockDim.x) lhist[i] = 0;
-  if (tid == 0) scnt = 0;
+  if (tid == 0) {
+    scnt = 0;
+    sres = SolidRes{~0ull, 0};
+  }
   __syncthreads();
   auto flush = [&]() {  // block-uniform
     const uint32_t n = scnt;
-    if (tid == 0) sbase = n ? atomicAdd(&o.gstats[2], (unsigned long long)n) : 0ull;
+    if (tid == 0) sbase = solid_take(sres, n, o);
     __syncthreads();
     const unsigned long long b = sbase;
     for (uint32_t i = tid; i < n; i += blockDim.x)
@@ -1355,12 +1397,23 @@ __global__ void __launch_bounds__(256) k_sk_big_emit(const unsigned long long* _
   if constexpr (SOLID) {
     __syncthreads();
     flush();
+    if (tid == 0) solid_close(sres, o);
   }
   __syncthreads();
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
   for (uint32_t i = tid; i < lim; i += blockDim.x)
     if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
   wave_add(&o.gstats[0], nd);
+}
+
+// The solid list dense again: chunk c's used[c] entries to offs[c].
+__global__ void k_solid_compact(const uint64_t* __restrict__ sparse, const uint32_t* __restrict__ used,
+                                const uint64_t* __restrict__ offs, uint64_t n_chunks, uint64_t* __restrict__ out) {
+  for (uint64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    const uint32_t u = used[c];
+    const uint64_t o = offs[c];
+    for (uint32_t i = threadIdx.x; i < u; i += blockDim.x) out[o + i] = sparse[c * kSolidChunk + i];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1736,7 +1789,19 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
     ctx->pc_ext_valid = false;
     solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
-    APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
+  }
+  // the chunked list (kSolidChunk slots per reservation, compacted into
+  // "pc_solid" afterwards): room for every block's partly used chunks
+  uint32_t* sused = nullptr;
+  auto solid_bufs = [&]() -> int {
+    solid_cap = (solid_cap + kSolidChunk - 1) / kSolidChunk * kSolidChunk;
+    APG_TRY(workspace_t(ctx, "sk_solid_sparse", solid_cap, &sl));
+    APG_TRY(workspace_t(ctx, "sk_sused", solid_cap / kSolidChunk, &sused));
+    return APG_OK;
+  };
+  if (solid) {
+    solid_cap += (uint64_t)ctx->n_cu * 16 * kSolidChunk;
+    APG_TRY(solid_bufs());
   }
   static const bool prof = getenv("APG_SK_PROF") != nullptr;
   unsigned long long* dprof = nullptr;
@@ -1746,6 +1811,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   }
   SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr, dprof,
            (uint32_t)(!solid || (hist && hist_len))};
+  o.sused = sused;
+  o.n_sused = solid ? solid_cap / kSolidChunk : 0;
   // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
   // LDS (owner map, recorded slots) and the table amortised over 8 waves give
   // 16 waves per CU, where 256-thread blocks fit only 3 per CU
@@ -1842,13 +1909,30 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       fprintf(stderr, "[sk_prof] K=%d solid=%d dedup %.3g flatten %.3g insert %.3g weak %.3g emit %.3g clear %.3g redo %llu\n", K,
               (int)solid, (double)hp[0], (double)hp[1], (double)hp[2], (double)hp[3], (double)hp[4], (double)hp[5], hs[4]);
     }
-    if (solid) kbytes_add(ctx, "sk_bucket_solid", std::min<uint64_t>(hs[2], solid_cap) * 8);
     if (up_dd) kbytes_add(ctx, "sk_bucket_solid", n_drec * sizeof(SK16) + nb * 4);  // distinct records out
     if (!solid || hs[2] <= solid_cap) {
+      uint64_t n_solid = 0;
+      uint64_t* dense = nullptr;
+      if (solid) {  // the chunked list -> dense "pc_solid"
+        const uint64_t n_chunks = hs[2] / kSolidChunk;
+        uint64_t* offs = nullptr;
+        APG_TRY(workspace_t(ctx, "sk_soffs", n_chunks + 1, &offs));
+        APG_TRY(scan_u32_u64(ctx, sused, n_chunks, offs, "sks"));
+        APG_CHECK_HIP(hipMemcpyAsync(&n_solid, offs + n_chunks, 8, hipMemcpyDeviceToHost, ctx->stream));
+        APG_TRY(sync(ctx));
+        APG_TRY(workspace_t(ctx, "pc_solid", std::max<uint64_t>(n_solid, 1), &dense));
+        kbegin(ctx, "solid_compact", n_solid * 16 + n_chunks * 12);
+        if (n_chunks)
+          k_solid_compact<<<(uint32_t)std::min<uint64_t>(n_chunks, (uint64_t)ctx->n_cu * 8), 256, 0, ctx->stream>>>(
+              sl, sused, offs, n_chunks, dense);
+        kend(ctx);
+        APG_CHECK_HIP(hipGetLastError());
+        kbytes_add(ctx, "sk_bucket_solid", n_solid * 8);
+      }
       res->n_distinct = hs[0];
       res->n_overflow_buckets = hs[1];
-      res->n_solid = solid ? hs[2] : 0;
-      res->solid = sl;
+      res->n_solid = n_solid;
+      res->solid = dense;
       res->nbuckets = nb;
       res->n_redo_buckets = dd ? hs[4] : 0;
       break;
@@ -1859,9 +1943,11 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     }
     vlog(ctx, "sk count: %llu solid K-mers exceed the list (%llu), recounting", hs[2], (unsigned long long)solid_cap);
     solid_cap = hs[2] + hs[2] / 8;
-    APG_TRY(workspace_t(ctx, "pc_solid", solid_cap, &sl));
+    APG_TRY(solid_bufs());
     o.solid = sl;
     o.solid_cap = solid_cap;
+    o.sused = sused;
+    o.n_sused = solid_cap / kSolidChunk;
     APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
     APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
   }
