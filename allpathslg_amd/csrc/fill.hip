@@ -201,12 +201,6 @@ constexpr uint32_t kFillCap1 = 96;
 // A wave refills its idle lanes with new pairs once at most this many lanes
 // are still walking.
 constexpr int kFillRefill = 32;
-// Work cursors: the pairs in kFillSeg contiguous segments, each with its own
-// counter on its own 128-byte line; a wave starts on the segment of its
-// index and moves on when one runs out (one counter for every wave of the
-// chip serialised the refills; the deferred-pair counter shared its line).
-constexpr uint32_t kFillSeg = 8;
-constexpr uint32_t kFillCurStride = 16;  // u64 per cursor line
 
 // One thread per pair, lanes persistent.  The gap walk is a state machine
 // that makes exactly ONE extension lookup per iteration whatever the lane is
@@ -230,7 +224,6 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
   const uint64_t nwork = list ? *list_n : rv.n_pairs;
-  uint32_t seg = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kFillSeg, segs_left = kFillSeg;
   // the lane's pair and its search state
   bool act = false, budget = false;
   uint64_t i = 0, atail = 0, f0 = 0, brm = 0, ww = 0;
@@ -374,16 +367,11 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
   for (;;) {
     while (more && __popcll(__ballot(act)) <= kFillRefill) {  // refill the idle lanes (wave-uniform)
       const uint64_t idle = __ballot(!act);
-      const uint64_t lo = nwork * seg / kFillSeg, hi = nwork * (seg + 1) / kFillSeg;
-      // the wave's next popc(idle) work items of its segment
-      const unsigned long long k = lo + wave_append(next + seg * kFillCurStride, !act);
-      if (!act && k < hi) {
+      const unsigned long long k = wave_append(next, !act);  // the wave's next popc(idle) work items
+      more = __shfl(k, 63 - __clzll((long long)idle), 64) + 1 < nwork;
+      if (!act && k < nwork) {
         i = list ? list[k] : k;
         start();
-      }
-      if (__shfl(k, 63 - __clzll((long long)idle), 64) + 1 >= hi) {  // segment used up: the next one
-        seg = (seg + 1) % kFillSeg;
-        more = --segs_left > 0;
       }
     }
     if (!__ballot(act)) break;
@@ -640,10 +628,8 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   uint32_t* defer = nullptr;
   unsigned long long* ndefer = nullptr;
   APG_TRY(workspace_t(ctx, "fill_defer", npc, &defer));
-  // deferred count, then the work cursors of pass 1 and of pass 2: one 128-byte line each
-  constexpr uint64_t kCurWords = kFillCurStride * (1 + 2 * kFillSeg);
-  APG_TRY(workspace_t(ctx, "fill_ndefer", kCurWords, &ndefer));
-  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, kCurWords * 8, ctx->stream));
+  APG_TRY(workspace_t(ctx, "fill_ndefer", 3, &ndefer));  // deferred count, next pair of pass 1 / pass 2
+  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, 3 * 8, ctx->stream));
   kbegin(ctx, "fill", dr->n_bytes + 16 * dr->n_reads + np * (sizeof(FillRec) + 12));
   if (np) {
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
@@ -651,11 +637,10 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     const uint32_t grid = resident_grid(ctx, k_fill, 256, (np + 255) / 256);
     k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
                                           std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
-                                          ndefer + kFillCurStride);
+                                          ndefer + 1);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
       k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
-                                            defer, ndefer, nullptr, nullptr,
-                                            ndefer + kFillCurStride * (1 + kFillSeg));
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
