@@ -16,6 +16,7 @@ const char* get_error() { return g_err.c_str(); }
 int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
   auto& b = ctx->ws[name];
   if (b.bytes < bytes) {
+    if (b.p && ctx->side_finish) APG_TRY(side_join(ctx));  // the side work may read it
     if (b.p) APG_CHECK_HIP(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
@@ -79,6 +80,7 @@ uint64_t device_free_bytes(apg_ctx* ctx) {
 }
 
 static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uint64_t* freed) {
+  APG_TRY(side_join(ctx));
   APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   for (size_t i = 0; i < n; ++i) {
     auto it = ctx->ws.find(names[i]);
@@ -217,6 +219,7 @@ void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes) {
   p.a = take_event(ctx);
   p.b = take_event(ctx);
   p.closed = false;
+  p.s = ctx->stream;
   (void)hipEventRecord(p.a, ctx->stream);
   ctx->pending.push_back(p);
 }
@@ -240,7 +243,7 @@ void kbytes_add(apg_ctx* ctx, const char* name, uint64_t bytes) {
 int kflush(apg_ctx* ctx) {
   std::vector<apg_ctx::Pending> open;
   for (auto& p : ctx->pending) {
-    if (!p.closed) {  // still bracketing work: keep for a later flush
+    if (!p.closed || p.s != ctx->stream) {  // still bracketing work / another stream's: a later flush
       open.push_back(p);
       continue;
     }
@@ -266,6 +269,21 @@ int sync(apg_ctx* ctx) {
   APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   APG_CHECK_HIP(hipGetLastError());
   return kflush(ctx);
+}
+
+int side_join(apg_ctx* ctx) {
+  if (!ctx->side_finish) return APG_OK;
+  std::function<int()> f;
+  f.swap(ctx->side_finish);  // cleared first: the finish may allocate workspaces
+  return f();
+}
+
+hipStream_t side_stream(apg_ctx* ctx) {
+  if (!ctx->side && hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    ctx->side = nullptr;
+  }
+  return ctx->side;
 }
 
 }  // namespace apg
@@ -316,6 +334,7 @@ int apg_create(const apg_config* cfg, apg_ctx** out) {
 int apg_trim(apg_ctx* ctx) {
   APG_REQUIRE(ctx, "apg_trim: ctx is NULL");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_TRY(side_join(ctx));
   APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
@@ -331,6 +350,8 @@ int apg_trim(apg_ctx* ctx) {
 void apg_destroy(apg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  (void)side_join(ctx);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   (void)hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
@@ -340,6 +361,7 @@ void apg_destroy(apg_ctx* ctx) {
   }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   staging_free(ctx);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -94,6 +95,13 @@ struct apg_ctx {
   int kmer_dedup = 0;  // apg_config.kmer_dedup
   hipStream_t stream = nullptr;
   int n_cu = 0;
+  // Side stream: work that runs beside the main stream inside one module call
+  // (the fused K+1 spectrum pass beside PreCorrect's correction kernels).
+  // side_finish completes it (host syncs of the side stream, outputs); it is
+  // run by apg::side_join before the call returns, and before any workspace
+  // is freed or grown.
+  hipStream_t side = nullptr;
+  std::function<int()> side_finish;
 
   // Grow-only named device workspaces.
   struct Buf {
@@ -110,6 +118,7 @@ struct apg_ctx {
     hipEvent_t a, b;
     uint64_t bytes;
     bool closed;
+    hipStream_t s;  // the stream the events bracket (kflush resolves only ctx->stream's)
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
@@ -290,6 +299,18 @@ void kbytes_add(apg_ctx* ctx, const char* name, uint64_t bytes);
 // Resolve pending events into kstats (call after a stream sync).
 int kflush(apg_ctx* ctx);
 int sync(apg_ctx* ctx);
+// Complete the side-stream work, if any (runs ctx->side_finish once).
+int side_join(apg_ctx* ctx);
+// The side stream (created on first use); 0 on failure.
+hipStream_t side_stream(apg_ctx* ctx);
+// Launches between construction and destruction go to `s` (kbegin / kend /
+// sync included).
+struct StreamSwap {
+  apg_ctx* ctx;
+  hipStream_t saved;
+  StreamSwap(apg_ctx* c, hipStream_t s) : ctx(c), saved(c->stream) { c->stream = s; }
+  ~StreamSwap() { ctx->stream = saved; }
+};
 
 inline void vlog(apg_ctx* ctx, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 

@@ -1042,7 +1042,11 @@ static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p,
     APG_TRY(workspace_t(ctx, "pc_weak", dr->n_bases / 64 + 2, &weak));
     APG_TRY(sk_solid_weak(ctx, dr, p.K, p.min_solid, weak, &sr, up_hist, up_hist_len, up_res));
     ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
-    return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak);
+    // the fused K+1 pass may still run on the side stream: joined here, after
+    // the correction kernels it overlaps
+    const int rc = correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak);
+    const int rj = side_join(ctx);
+    return rc != APG_OK ? rc : rj;
   }
   APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
   ctx->solid_valid = false;

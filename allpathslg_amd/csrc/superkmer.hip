@@ -1573,23 +1573,34 @@ static int sk_up_alloc(apg_ctx* ctx, uint64_t nb, size_t hist_len, SkOut* u) {
 }
 
 // drec / dcount (may be null): the solid-set count's distinct records per
-// bucket (k_sk_bucket_dd's dout), n_drec of them in all.
-static int sk_up_run(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
-                     const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec, uint64_t* hist,
-                     size_t hist_len, SkResult* res) {
+// bucket (k_sk_bucket_dd's dout), n_drec of them in all.  sk_up_launch
+// queues the bucket pass on ctx->stream (grid_frac of a resident round: the
+// side-stream form leaves the rest of each CU to the main stream's kernels);
+// sk_up_finish waits for it, runs the overflowed buckets and reads the
+// results back.
+static int sk_up_launch(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                        const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec,
+                        double grid_frac = 1.0) {
   const SkP p = make_skp(K1);
   APG_CHECK_HIP(hipMemsetAsync(u.ghist, 0, u.hist_len * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(u.gstats, 0, 5 * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(u.inst, 0, 8, ctx->stream));
-  const uint64_t grid = resident_grid(ctx, k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true>, kSkThreads, nb);
+  uint64_t grid = resident_grid(ctx, k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true>, kSkThreads, nb);
+  if (grid_frac < 1.0) grid = std::max<uint64_t>(1, (uint64_t)((double)grid * grid_frac));
   // algorithmic bytes: the records read (the distinct ones with their
   // multiplicity where the solid-set count folded them) and the bucket bounds
   kbegin(ctx, "sk_bucket", (dcount ? n_drec * sizeof(SK16) : n_rec * sizeof(SK24)) + (nb + 1) * 8 + (dcount ? nb * 4 : 0));
   if (nb)
-    k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true><<<grid, kSkThreads, 0, ctx->stream>>>(
+    k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true><<<(uint32_t)grid, kSkThreads, 0, ctx->stream>>>(
         cur, boff, nb, p, u, nullptr, nullptr, drec, dcount);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
+static int sk_up_finish(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                        const SkOut& u, bool folded, uint64_t* hist, size_t hist_len, SkResult* res) {
+  const SkP p = make_skp(K1);
   unsigned long long hs[5];
   APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
@@ -1638,8 +1649,16 @@ static int sk_up_run(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64
   res->n_kmers = ninst;
   res->n_records = n_rec;
   vlog(ctx, "sk count K=%d from K=%d records%s: kmers=%llu distinct=%llu ovf=%llu", K1, K1 - 1,
-       dcount ? " (distinct records x multiplicity)" : "", ninst, hs[0], hs[1]);
+       folded ? " (distinct records x multiplicity)" : "", ninst, hs[0], hs[1]);
   return APG_OK;
+}
+
+
+static int sk_up_run(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                     const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec, uint64_t* hist,
+                     size_t hist_len, SkResult* res) {
+  APG_TRY(sk_up_launch(ctx, cur, boff, nb, n_rec, K1, u, drec, dcount, n_drec));
+  return sk_up_finish(ctx, cur, boff, nb, n_rec, K1, u, dcount != nullptr, hist, hist_len, res);
 }
 
 static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
@@ -1966,8 +1985,34 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     if (up_K && up_dd) {
       SkOut u;
       APG_TRY(sk_up_alloc(ctx, nb, up_hist_len, &u));
-      APG_TRY(sk_up_run(ctx, cur, boff, nb, n, up_K, u, reinterpret_cast<const SK16*>(dbuf), dcount, n_drec, up_hist,
-                        up_hist_len, up_res));
+      const SK16* drec = reinterpret_cast<const SK16*>(dbuf);
+      // Side stream (APG_SK_UP_SIDE=0: in line): the K+1 pass needs nothing the
+      // caller computes next (PreCorrect's candidates, decisions and edits
+      // touch neither the records nor their buckets), so it runs beside them
+      // on APG_SK_UP_FRAC of a resident round of blocks, and the caller joins
+      // it (side_join) before it returns.
+      const char* se = getenv("APG_SK_UP_SIDE");
+      const bool side = !(se && !strcmp(se, "0"));
+      const hipStream_t sd = side ? side_stream(ctx) : nullptr;
+      if (sd) {
+        const char* fe = getenv("APG_SK_UP_FRAC");
+        const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 0.5;
+        hipEvent_t ev = nullptr;
+        APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));  // the records and dout are complete
+        APG_CHECK_HIP(hipStreamWaitEvent(sd, ev, 0));
+        APG_CHECK_HIP(hipEventDestroy(ev));
+        {
+          StreamSwap sw(ctx, sd);
+          APG_TRY(sk_up_launch(ctx, cur, boff, nb, n, up_K, u, drec, dcount, n_drec, frac));
+        }
+        ctx->side_finish = [=]() -> int {
+          StreamSwap sw(ctx, sd);
+          return sk_up_finish(ctx, cur, boff, nb, n, up_K, u, true, up_hist, up_hist_len, up_res);
+        };
+      } else {
+        APG_TRY(sk_up_run(ctx, cur, boff, nb, n, up_K, u, drec, dcount, n_drec, up_hist, up_hist_len, up_res));
+      }
     } else if (up_K) {
       APG_TRY(sk_up_count(ctx, cur, boff, nb, n, up_K, up_hist, up_hist_len, up_res));
     }

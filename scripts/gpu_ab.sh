@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B on one box: selected parity tests, then the bench step with env A and
-# env B (e.g. A="APG_FILL_MEMO=0" B="").  Kernel table of both in the log.
+# env B (e.g. A="APG_FILL_MEMO=0" B=""; more variants: VARIANTS="A B C D").
+# Kernel table of each in the log.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -9,7 +10,7 @@ if [ -n "${PYTEST_SEL:-}" ]; then
   timeout -k 10 ${T_TEST:-400} python -u -m pytest ${PYTEST_SEL} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
   tail -2 gpurun_out/ab_pytest.log
 fi
-for V in A B; do
+for V in ${VARIANTS:-A B}; do
   E="${!V}"
   env $E timeout -k 10 ${T_BENCH:-400} python bench.py $BA > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
   echo "== $V ($E)"
