@@ -243,7 +243,13 @@ void kbytes_add(apg_ctx* ctx, const char* name, uint64_t bytes) {
 int kflush(apg_ctx* ctx) {
   std::vector<apg_ctx::Pending> open;
   for (auto& p : ctx->pending) {
-    if (!p.closed || p.s != ctx->stream) {  // still bracketing work / another stream's: a later flush
+    // still bracketing work, or another stream's still running: a later flush
+    bool later = !p.closed;
+    if (!later && p.s != ctx->stream && hipEventQuery(p.b) != hipSuccess) {
+      (void)hipGetLastError();  // hipErrorNotReady is not an error here
+      later = true;
+    }
+    if (later) {
       open.push_back(p);
       continue;
     }
@@ -278,13 +284,15 @@ int side_join(apg_ctx* ctx) {
   return f();
 }
 
-hipStream_t side_stream(apg_ctx* ctx) {
-  if (!ctx->side && hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+static hipStream_t lazy_stream(hipStream_t* s) {
+  if (!*s && hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
     (void)hipGetLastError();
-    ctx->side = nullptr;
+    *s = nullptr;
   }
-  return ctx->side;
+  return *s;
 }
+hipStream_t side_stream(apg_ctx* ctx) { return lazy_stream(&ctx->side); }
+hipStream_t aux_stream(apg_ctx* ctx) { return lazy_stream(&ctx->aux); }
 
 }  // namespace apg
 
@@ -352,6 +360,7 @@ void apg_destroy(apg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)side_join(ctx);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
   (void)hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
@@ -362,6 +371,7 @@ void apg_destroy(apg_ctx* ctx) {
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   staging_free(ctx);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

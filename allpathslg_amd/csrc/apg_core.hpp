@@ -102,6 +102,10 @@ struct apg_ctx {
   // is freed or grown.
   hipStream_t side = nullptr;
   std::function<int()> side_finish;
+  // Auxiliary stream: a producer that overlaps the main stream's next
+  // kernels and is joined by an event wait (PreCorrect's extension table
+  // built beside its candidate scan).
+  hipStream_t aux = nullptr;
 
   // Grow-only named device workspaces.
   struct Buf {
@@ -301,8 +305,9 @@ int kflush(apg_ctx* ctx);
 int sync(apg_ctx* ctx);
 // Complete the side-stream work, if any (runs ctx->side_finish once).
 int side_join(apg_ctx* ctx);
-// The side stream (created on first use); 0 on failure.
+// The side / auxiliary stream (created on first use); 0 on failure.
 hipStream_t side_stream(apg_ctx* ctx);
+hipStream_t aux_stream(apg_ctx* ctx);
 // Launches between construction and destruction go to `s` (kbegin / kend /
 // sync included).
 struct StreamSwap {

@@ -871,8 +871,59 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   SolidSet ss{};
   ExtTab et{};
   ctx->pc_ext_valid = false;
-  if (ext) {
+  // With the weak bitmap the candidate scan needs no table: APG_PC_EXT_AUX=1
+  // builds the extension table on the auxiliary stream beside it, the
+  // decisions waiting for it by an event.  Off by default: with the fused
+  // K+1 pass already beside these kernels on the side stream, a third stream
+  // measured 172.4 ms per bench step against 171.9 ms without it (DESIGN.md
+  // §4, tried list).
+  hipEvent_t ext_done = nullptr;
+  if (ext && weak) {
+    const char* ae = getenv("APG_PC_EXT_AUX");
+    const hipStream_t ax = (ae && !strcmp(ae, "1")) ? aux_stream(ctx) : nullptr;
+    if (ax) {
+      hipEvent_t ready = nullptr;
+      APG_CHECK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+      APG_CHECK_HIP(hipEventCreateWithFlags(&ext_done, hipEventDisableTiming));
+      APG_CHECK_HIP(hipEventRecord(ready, ctx->stream));  // the solid list is complete
+      APG_CHECK_HIP(hipStreamWaitEvent(ax, ready, 0));
+      APG_CHECK_HIP(hipEventDestroy(ready));
+      int rc;
+      {
+        StreamSwap sw(ctx, ax);
+        rc = ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et);
+        if (rc == APG_OK && hipEventRecord(ext_done, ax) != hipSuccess) rc = APG_E_HIP;
+      }
+      if (rc != APG_OK) {
+        (void)hipStreamSynchronize(ax);
+        (void)hipEventDestroy(ext_done);
+        return rc;
+      }
+    }
+  }
+  // an early return leaves no table build running behind it
+  struct ExtGuard {
+    hipEvent_t* ev;
+    hipStream_t ax;
+    ~ExtGuard() {
+      if (*ev) {
+        (void)hipStreamSynchronize(ax);
+        (void)hipEventDestroy(*ev);
+      }
+    }
+  } ext_guard{&ext_done, ctx->aux};
+  // the main stream's wait for the table (no host sync); idempotent
+  auto ext_wait = [&]() -> int {
+    if (!ext_done) return APG_OK;
+    APG_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ext_done, 0));
+    APG_CHECK_HIP(hipEventDestroy(ext_done));
+    ext_done = nullptr;
+    return APG_OK;
+  };
+  if (ext && !weak) {
     APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
+  } else if (ext) {
+    if (!ext_done) APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
   } else {
     uint64_t T = 1024;
     while (T < 2 * n_solid) T <<= 1;
@@ -963,6 +1014,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     uint8_t* dec = nullptr;
     APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));
     // candidate records in, decisions out (+ 64 B per extension lookup, after the sync)
+    APG_TRY(ext_wait());
     kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 1));
     if (ncand)
       k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups);

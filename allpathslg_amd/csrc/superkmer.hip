@@ -1996,7 +1996,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       const hipStream_t sd = side ? side_stream(ctx) : nullptr;
       if (sd) {
         const char* fe = getenv("APG_SK_UP_FRAC");
-        const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 0.5;
+        const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 0.75;
         hipEvent_t ev = nullptr;
         APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));  // the records and dout are complete

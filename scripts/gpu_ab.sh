@@ -11,9 +11,9 @@ if [ -n "${PYTEST_SEL:-}" ]; then
   tail -2 gpurun_out/ab_pytest.log
 fi
 for V in ${VARIANTS:-A B}; do
-  E="${!V}"
-  env $E timeout -k 10 ${T_BENCH:-400} python bench.py $BA > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
-  echo "== $V ($E)"
+  ENVV="${!V}"
+  env $ENVV timeout -k 10 ${T_BENCH:-400} python bench.py $BA > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
+  echo "== $V ($ENVV)"
   python - gpurun_out/ab_$V.json <<'PY'
 import json, sys
 b = json.load(open(sys.argv[1]))
