@@ -593,17 +593,40 @@ struct DN {
   uint32_t nxt, prv, ruler, lrank;
 };
 
-__global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, DN* __restrict__ dn,
-                        unsigned long long* __restrict__ stat) {
-  unsigned long long nl = 0, bad = 0;
+// Unique links resolved inside a bucket (k_usk_bucket, lsucc): a K-mer's
+// successor in a read almost always has the same minimizer, so it is in the
+// same bucket's LDS table.  Per node and orientation: the successor directed
+// node (2 * id + orientation), kNone (no unique link: the rules of k_links),
+// or kLsGlobal (the successor is in another bucket: k_links looks it up in
+// the node index).
+constexpr uint32_t kLsGlobal = 0xfefefefeu;  // > any directed node id (N < kLsMaxNodes)
+constexpr uint64_t kLsMaxNodes = 0x7f000000ull;
+
+// lsucc (may be null): links the node buckets resolved (k_usk_bucket); only
+// kLsGlobal orientations are looked up here.
+__global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, DN* __restrict__ dn, unsigned long long* __restrict__ stat,
+                        const uint2* __restrict__ lsucc) {
+  unsigned long long nl = 0, bad = 0, ng = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint2 ls = lsucc ? lsucc[i] : make_uint2(kLsGlobal, kLsGlobal);
+#pragma unroll
+    for (uint32_t o = 0; o < 2; ++o) {
+      const uint32_t w = o ? ls.y : ls.x;
+      if (w >= kLsGlobal) continue;  // kNone, kLsGlobal
+      dn[2 * i + o].nxt = w;
+      dn[w].prv = (uint32_t)(2 * i + o);
+      ++nl;
+    }
+    if (ls.x != kLsGlobal && ls.y != kLsGlobal) continue;
     const KRec x = ni.nodes[i];
     const K3 key = rec_key(x);
     if (k3_eq(key, revcomp(key, kp))) continue;  // palindromic K-mers never link
     const uint32_t ext = (uint32_t)(x.meta & 0xff);
     for (uint32_t o = 0; o < 2; ++o) {
+      if ((o ? ls.y : ls.x) != kLsGlobal) continue;
       const uint32_t out = out_set(ext, o);
       if (__popc(out) != 1) continue;
+      ++ng;
       const uint32_t b = __ffs(out) - 1;
       const K3 s = o ? revcomp(key, kp) : key;
       const K3 t = push_right(s, b, kp);
@@ -624,10 +647,12 @@ __global__ void k_links(NodeIdx ni, uint64_t N, KeyP kp, DN* __restrict__ dn,
   for (int s = 32; s > 0; s >>= 1) {
     nl += __shfl_down(nl, s, 64);
     bad += __shfl_down(bad, s, 64);
+    ng += __shfl_down(ng, s, 64);
   }
   if ((threadIdx.x & 63) == 0) {
     if (nl) atomicAdd(&stat[0], nl);
     if (bad) atomicAdd(&stat[1], bad);
+    if (ng) atomicAdd(&stat[2], ng);
   }
 }
 
@@ -1394,7 +1419,9 @@ struct UskOut {
   uint64_t cap;
   unsigned long long* gs;  // [0] nodes appended, [1] overflowed buckets
   uint32_t* ovf_list;
+  uint2* lsucc;  // may be null: per node, its two orientations' local links (usk_links_local)
 };
+
 
 // One workgroup per bucket (grid-stride).
 __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restrict__ rec,
@@ -1403,13 +1430,17 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
   __shared__ uint32_t tag[kUskTab];
   __shared__ uint64_t ka[kUskTab], kb[kUskTab], kc[kUskTab];
   __shared__ uint32_t text[kUskTab];
-  __shared__ __attribute__((aligned(16))) SK48 crec[kUskChunk];
+  __shared__ __attribute__((aligned(16))) SK48 crec[kUskChunk];  // emit: the occupied slots in rank order (u16)
   __shared__ uint32_t koff[kUskChunk];
-  __shared__ uint8_t owner[kUskChunk * kUskMaxNk];
+  __shared__ __attribute__((aligned(16))) uint8_t owner[kUskChunk * kUskMaxNk];
   __shared__ uint32_t scan_sm[64];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
   constexpr int TB = __builtin_ctz(kUskTab);
+  static_assert(kUskChunk * kUskMaxNk >= 2 * kUskTab, "owner doubles as the slot ranks");
+  uint16_t* rnk = reinterpret_cast<uint16_t*>(owner);  // emit: slot -> rank in the bucket's node list
+  static_assert(sizeof(SK48) * kUskChunk >= 2 * kUskTab, "crec doubles as the rank -> slot list");
+  uint16_t* slot_of = reinterpret_cast<uint16_t*>(crec);
   const uint32_t tid = threadIdx.x;
   // The block's buckets bkt, bkt + grid, ... are one record stream: the next
   // chunk's records (this bucket's or the next bucket's first) are loaded
@@ -1519,12 +1550,58 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
     const unsigned long long b = sbase;
     for (uint32_t s = tid; s < kUskTab; s += kUskBThreads)
       if (tag[s] != 0) {
+        rnk[s] = (uint16_t)j;  // owner and crec are free: every instance is inserted
+        slot_of[j] = (uint16_t)s;
         const unsigned long long at = b + j++;
         if (at < o.cap) {
           const K3 k{ka[s], kb[s], kc[s]};
           o.nodes[at] = KRec{k.a, k.b, k.c, key_hash(k) | text[s]};
         }
       }
+    if (o.lsucc) {  // block-uniform
+      __syncthreads();  // every slot's rank
+      for (uint32_t r = tid; r < tot; r += kUskBThreads) {  // the occupied slots only: full lanes
+        const uint32_t s = slot_of[r];
+        const unsigned long long id = b + r;
+        if (id >= o.cap) continue;
+        // the rules of k_links, with the successor looked up in this table
+        const K3 key{ka[s], kb[s], kc[s]};
+        const K3 rk = revcomp(key, kp);
+        const uint32_t ext = text[s];
+        uint32_t res[2] = {kNone, kNone};
+        if (!k3_eq(key, rk)) {  // palindromic K-mers never link
+#pragma unroll
+          for (uint32_t d = 0; d < 2; ++d) {
+            const uint32_t out = out_set(ext, d);
+            if (__popc(out) != 1) continue;
+            const K3 t = push_right(d ? rk : key, __ffs(out) - 1, kp);
+            const K3 tr = revcomp(t, kp);
+            const bool fw = !k3_lt(tr, t);
+            const K3 c = fw ? t : tr;
+            const uint32_t h = usk_slot_hash(c);
+            const uint32_t tv = (h & ~3u) | 2u;
+            uint32_t sl = h >> (32 - TB), hit = kUskTab;
+            for (uint32_t probe = 0; probe < kUskProbeMax; ++probe) {
+              const uint32_t tg = tag[sl];
+              if (tg == 0) break;
+              if (tg == tv && ka[sl] == c.a && kb[sl] == c.b && kc[sl] == c.c) {
+                hit = sl;
+                break;
+              }
+              sl = (sl + 1) & (kUskTab - 1);
+            }
+            if (hit == kUskTab) {
+              res[d] = kLsGlobal;
+              continue;
+            }
+            if (k3_eq(t, tr)) continue;  // palindromic successor
+            if (__popc(in_set(text[hit], fw ? 0u : 1u)) != 1) continue;
+            res[d] = (uint32_t)(2 * (b + rnk[hit])) + (fw ? 0u : 1u);
+          }
+        }
+        o.lsucc[id] = make_uint2(res[0], res[1]);
+      }
+    }
     __syncthreads();
     advance();
   }
@@ -1834,7 +1911,7 @@ static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, 
 }
 
 static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads* dr, const apg_unipath_params& prm,
-                   apg_unipath_graph* out, apg_unipath_stats* st) {
+                   apg_unipath_graph* out, apg_unipath_stats* st, const uint2* lsucc = nullptr) {
   const int K = prm.K;
   const KeyP kp = make_keyp(K);
   st->n_nodes = N;
@@ -1867,12 +1944,16 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   RankBufs rb{};
   APG_TRY(workspace_t(ctx, "u_dn", std::max<uint64_t>(D, 1), &rb.dn));
   APG_CHECK_HIP(hipMemsetAsync(rb.dn, 0xff, D * sizeof(DN), ctx->stream));
-  kbegin(ctx, "u_links", N * 64);
-  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.dn, gs + 4);
+  // algorithmic bytes: ~2 index lookups per node, or with the buckets' local
+  // links the 8-byte link record per node (+ 64 B per remaining lookup, added
+  // below)
+  kbegin(ctx, "u_links", lsucc ? N * 8 : N * 64);
+  k_links<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(ni, N, kp, rb.dn, gs + 4, lsucc);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
-  unsigned long long hl[2];
-  APG_TRY(d2h_u64(ctx, gs + 4, hl, 2));
+  unsigned long long hl[3];
+  APG_TRY(d2h_u64(ctx, gs + 4, hl, 3));
+  if (lsucc) kbytes_add(ctx, "u_links", hl[2] * 64);  // the index lookups left to this pass
   st->n_links = hl[0];
   if (hl[1]) {
     set_error("unipaths: read-supported edge to a missing K-mer (internal error)");
@@ -2148,8 +2229,11 @@ static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P,
 // -> distinct nodes.  The records' top log2(P) + kUskDigitBits key bits are
 // consumed; `spare` (may be src itself when it may be overwritten) is a
 // second record buffer.
+// lsucc_out (may be null): the buckets' local links for k_links (null on
+// return when they could not be kept: overflowed nodes beyond the list, or
+// too many nodes)
 static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>& rc, uint64_t nk, const KeyP& kp,
-                     int P, KRec** nodes_out, uint64_t* N_out) {
+                     int P, KRec** nodes_out, uint64_t* N_out, uint2** lsucc_out = nullptr) {
   const int pbits = ceil_log2_u((uint64_t)P);
   const int D = kUskDigitBits;
   const uint32_t ndig = 1u << D;
@@ -2211,11 +2295,16 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   KRec* nodes = nullptr;
   unsigned long long hs[4];
   const uint64_t grid = resident_grid(ctx, k_usk_bucket, kUskBThreads, nb);
+  // APG_U_LOCAL_LINKS=0: every link through the node index (A/B)
+  const char* le = getenv("APG_U_LOCAL_LINKS");
+  const bool want_ls = lsucc_out && !(le && !strcmp(le, "0"));
+  uint2* ls = nullptr;
   for (;;) {
     APG_TRY(workspace_t(ctx, "usk_nodes", cap, &nodes));
+    if (want_ls) APG_TRY(workspace_t(ctx, "usk_lsucc", cap, &ls));
     APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));
     kbegin(ctx, "usk_bucket", n * sizeof(SK48) + (nb + 1) * 8);
-    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, kp, UskOut{nodes, cap, gs, ovf});
+    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, kp, UskOut{nodes, cap, gs, ovf, ls});
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     APG_TRY(d2h_u64(ctx, gs, hs, 4));
@@ -2224,7 +2313,7 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     cap = hs[0] + hs[0] / 8;
   }
   uint64_t N = hs[0];
-  kbytes_add(ctx, "usk_bucket", N * sizeof(KRec));
+  kbytes_add(ctx, "usk_bucket", N * (sizeof(KRec) + (ls ? sizeof(uint2) : 0)));
   if (hs[1]) {  // overflowed buckets: their instances through the U2 table
     const uint32_t n_ovf = (uint32_t)hs[1];
     const uint32_t g2 = (uint32_t)std::min<uint64_t>(n_ovf, (uint64_t)ctx->n_cu * 8);
@@ -2251,8 +2340,15 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     APG_CHECK_HIP(hipMemcpyAsync(nodes + N, fnodes, fN * sizeof(KRec), hipMemcpyDeviceToDevice, ctx->stream));
     vlog(ctx, "unipaths: %u buckets overflow the LDS table (%llu instances, %llu nodes) -> global table", n_ovf,
          ni[0], (unsigned long long)fN);
+    // the overflowed buckets' nodes link through the index (kLsGlobal bytes)
+    if (ls && N + fN <= cap)
+      APG_CHECK_HIP(hipMemsetAsync(ls + N, 0xfe, fN * sizeof(uint2), ctx->stream));
+    else
+      ls = nullptr;
     N += fN;
   }
+  if (N >= kLsMaxNodes) ls = nullptr;
+  if (lsucc_out) *lsucc_out = ls;
   vlog(ctx, "unipaths: K=%d P=%d records=%llu instances=%llu levels=%d buckets=%llu nodes=%llu", kp.K, P,
        (unsigned long long)n, (unsigned long long)nk, nlev, (unsigned long long)nb, (unsigned long long)N);
   *nodes_out = nodes;
@@ -2269,7 +2365,7 @@ __global__ void k_usk_sum(const SK48* __restrict__ rec, uint64_t n, unsigned lon
 
 // Single-GPU: plan + scatter into kBig0 (usk_stage's first buffer) + stage.
 static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec** nodes_out, uint64_t* N_out,
-                      uint64_t* n_inst) {
+                      uint64_t* n_inst, uint2** lsucc_out) {
   const UskP p = make_uskp(kp.K);
   std::vector<uint64_t> h, kd;
   uint32_t G = 0;
@@ -2287,7 +2383,7 @@ static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec**
   APG_TRY(usk_scatter(ctx, dr, p, 1, G, recs));
   std::vector<uint64_t> rc(ndig);
   for (uint32_t d = 0; d < ndig; ++d) rc[d] = h[d + 1] - h[d];
-  return usk_stage(ctx, recs, rc, nk, kp, 1, nodes_out, N_out);
+  return usk_stage(ctx, recs, rc, nk, kp, 1, nodes_out, N_out, lsucc_out);
 }
 
 static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
@@ -2297,9 +2393,10 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   uint64_t n = 0;
   KRec* nodes = nullptr;
   uint64_t N = 0;
-  APG_TRY(u_sk_nodes(ctx, dr, kp, &nodes, &N, &n));
+  uint2* lsucc = nullptr;
+  APG_TRY(u_sk_nodes(ctx, dr, kp, &nodes, &N, &n, &lsucc));
   st->n_instances = n;
-  return u_graph(ctx, nodes, N, dr, prm, out, st);
+  return u_graph(ctx, nodes, N, dr, prm, out, st, lsucc);
 }
 
 }  // namespace apg
