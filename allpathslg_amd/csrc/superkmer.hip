@@ -76,6 +76,10 @@ static SkP make_skp(int K) {
   SkP p;
   p.K = K;
   p.m = std::min(K, std::max(10, std::min(16, K - 8)));
+  // APG_SK_M=m (10 <= m <= 16, m < K - 1): the minimizer length of every
+  // K <= 32 walk (A/B of records per read against bucket skew)
+  static const int m_env = getenv("APG_SK_M") ? atoi(getenv("APG_SK_M")) : 0;
+  if (m_env >= 10 && m_env <= 16 && m_env < K - 1) p.m = m_env;
   p.w = K - p.m + 1;
   p.maxnk = std::min(kSkBases - K + 1, 255);
   p.mmask = p.m >= 32 ? ~0ull : ((1ull << (2 * p.m)) - 1);
