@@ -1420,7 +1420,17 @@ struct UskOut {
   unsigned long long* gs;  // [0] nodes appended, [1] overflowed buckets
   uint32_t* ovf_list;
   uint2* lsucc;  // may be null: per node, its two orientations' local links (usk_links_local)
+  uint32_t dedup;  // fold identical records of a chunk before flattening
+  unsigned long long* dstat;  // may be null: records, instances, records folded, instances folded
 };
+
+// 32-bit fingerprint of a K=96 record (its full content: n, flank flags, bases)
+__device__ __forceinline__ uint32_t urec_fp(const SK48& r) {
+  uint64_t x = (r.w0 >> 32) * 0x9e3779b97f4a7c15ull;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) x = fmix64(x ^ r.b[k]);
+  return (uint32_t)(x >> 32);
+}
 
 
 // One workgroup per bucket (grid-stride).
@@ -1432,6 +1442,7 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
   __shared__ uint32_t text[kUskTab];
   __shared__ __attribute__((aligned(16))) SK48 crec[kUskChunk];  // emit: the occupied slots in rank order (u16)
   __shared__ uint32_t koff[kUskChunk];
+  __shared__ uint32_t dht[2 * kUskChunk];  // dedup: fingerprint bits | leader lane, 0 = empty
   __shared__ __attribute__((aligned(16))) uint8_t owner[kUskChunk * kUskMaxNk];
   __shared__ uint32_t scan_sm[64];
   __shared__ int ovf;
@@ -1453,6 +1464,8 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
   }
   SK48 pre{};
   if (tid < kUskChunk && tid < nr) pre = rec[off + tid];
+  if (tid < 2 * kUskChunk) dht[tid] = 0;
+  __syncthreads();  // the dedup table is empty before the first chunk's claims
   for (; bkt < nbuckets;) {
     const uint64_t nbk = bkt + gridDim.x;
     uint64_t noff = 0;
@@ -1481,10 +1494,22 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
         if (tid < kUskChunk && tid < nnr) pre = rec[noff + tid];
         break;
       }
-      uint32_t nk = 0;
+      uint32_t nk = 0, lead = tid;
       if (tid < kUskChunk && c0 + tid < nr) {
         nk = (uint32_t)(pre.w0 >> 32) & 0xff;
         crec[tid] = pre;
+        if (o.dedup) {  // claim the record's fingerprint, or find its leader
+          const uint32_t fp = urec_fp(pre);
+          const uint32_t want = ((fp | 64u) & ~63u) | tid;
+          for (uint32_t sl = fp & (2 * kUskChunk - 1);; sl = (sl + 1) & (2 * kUskChunk - 1)) {
+            const uint32_t old = atomicCAS(&dht[sl], 0u, want);
+            if (old == 0) break;
+            if ((old & ~63u) == (want & ~63u)) {
+              lead = old & 63u;
+              break;
+            }
+          }
+        }
       }
       if (tid < kUskChunk) {
         if (c0 + kUskChunk < nr) {
@@ -1492,6 +1517,35 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
         } else if (tid < nnr) {
           pre = rec[noff + tid];
         }
+      }
+      // Record dedup: at fragment coverage c, every fragment that spans a
+      // whole super-k-mer emits the same record (its bases and flanks are the
+      // genome's), so a chunk holds repeated ones (30 % of the bench step's
+      // records, 24 % of its K-mer instances); a record equal to another of the
+      // chunk adds no node and no extension bit, and is not flattened.  Lanes
+      // < 64 own the records: a 128-slot LDS table of fingerprints names each
+      // fingerprint's first claimant, and a record is dropped only if it
+      // equals that leader's record exactly (a fingerprint collision keeps
+      // both).
+      if (o.dedup) {  // block-uniform
+        __syncthreads();  // the chunk's records and claims
+        if (tid < 2 * kUskChunk) dht[tid] = 0;  // for the next chunk (no lane reads the table past the barrier)
+        if (nk && lead != tid) {
+          const SK48& a = crec[lead];
+          const SK48& m = crec[tid];
+          if (a.w0 == m.w0 && a.b[0] == m.b[0] && a.b[1] == m.b[1] && a.b[2] == m.b[2] && a.b[3] == m.b[3] &&
+              a.b[4] == m.b[4]) {
+            if (o.dstat) {
+              atomicAdd(&o.dstat[2], 1ull);
+              atomicAdd(&o.dstat[3], (unsigned long long)nk);
+            }
+            nk = 0;
+          }
+        }
+      }
+      if (o.dstat && tid < kUskChunk && c0 + tid < nr) {
+        atomicAdd(&o.dstat[0], 1ull);
+        atomicAdd(&o.dstat[1], (unsigned long long)((crec[tid].w0 >> 32) & 0xff));
       }
       uint32_t tot;
       const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);  // barrier: table clear visible
@@ -2295,6 +2349,15 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   KRec* nodes = nullptr;
   unsigned long long hs[4];
   const uint64_t grid = resident_grid(ctx, k_usk_bucket, kUskBThreads, nb);
+  // APG_USK_DEDUP=0: every record flattened (A/B)
+  const char* de = getenv("APG_USK_DEDUP");
+  const bool dedup = !(de && !strcmp(de, "0"));
+  // APG_USK_DEDUP_STATS=1: count records / instances and what the dedup folds (stderr)
+  unsigned long long* dstat = nullptr;
+  if (getenv("APG_USK_DEDUP_STATS")) {
+    APG_TRY(workspace_t(ctx, "usk_dstat", 4, &dstat));
+    APG_CHECK_HIP(hipMemsetAsync(dstat, 0, 32, ctx->stream));
+  }
   // APG_U_LOCAL_LINKS=0: every link through the node index (A/B)
   const char* le = getenv("APG_U_LOCAL_LINKS");
   const bool want_ls = lsucc_out && !(le && !strcmp(le, "0"));
@@ -2304,13 +2367,20 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     if (want_ls) APG_TRY(workspace_t(ctx, "usk_lsucc", cap, &ls));
     APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));
     kbegin(ctx, "usk_bucket", n * sizeof(SK48) + (nb + 1) * 8);
-    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, kp, UskOut{nodes, cap, gs, ovf, ls});
+    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, kp,
+                                                         UskOut{nodes, cap, gs, ovf, ls, dedup ? 1u : 0u, dstat});
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     APG_TRY(d2h_u64(ctx, gs, hs, 4));
     if (hs[0] <= cap) break;
     vlog(ctx, "unipaths: %llu nodes exceed the node list (%llu), rerunning", hs[0], (unsigned long long)cap);
     cap = hs[0] + hs[0] / 8;
+  }
+  if (dstat) {
+    unsigned long long d4[4];
+    APG_TRY(d2h_u64(ctx, dstat, d4, 4));
+    fprintf(stderr, "[usk_dedup] records %llu instances %llu folded records %llu folded instances %llu\n", d4[0], d4[1],
+            d4[2], d4[3]);
   }
   uint64_t N = hs[0];
   kbytes_add(ctx, "usk_bucket", N * (sizeof(KRec) + (ls ? sizeof(uint2) : 0)));
