@@ -168,6 +168,7 @@ struct apg_ctx {
     uint32_t G = 0;
     uint64_t total = 0;
     bool desc = false;  // the count pass kept record descriptors ("sk_desc*")
+    uint32_t split = 0;  // records counted as pieces of <= split K-mers (SkP::split)
   } skstate;
 
   // Device graph of the last unipath build ("u_*" workspaces + the node

@@ -43,7 +43,7 @@ struct SkResult {
   uint64_t n_records = 0;
 };
 int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
-             std::vector<uint64_t>* kmer_counts);
+             std::vector<uint64_t>* kmer_counts, uint32_t split = 0);
 int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
 // sk_scatter + pos[i] = global base position of record i's first K-mer
 int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos);

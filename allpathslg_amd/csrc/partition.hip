@@ -174,16 +174,17 @@ __global__ void __launch_bounds__(kPartThreads* kScanGroups) k_part_scan(const u
 // The partition key of a record from its first 64-bit word (rkey).
 template <typename R>
 __device__ __forceinline__ uint64_t rkey_w0(uint64_t w0) {
-  if constexpr (sizeof(R) == 8)
+  if constexpr (sizeof(R) == 8 || std::is_same<R, SKP>::value)
     return w0;
   else
     return w0 << 32;  // SK16 / SK24 / SK48: the minimizer key
 }
 
-// RI -> RO: the same record (RO == RI), or an SK16 that leaves as an SK24
+// RI -> RO: the same record (RO == RI), an SK16 that leaves as an SK24
 // carrying its input index (the multi-GPU solid count: the index of a
 // received record is where its weak mask goes back; the first level widens
-// the records instead of a separate pass over them).
+// the records instead of a separate pass over them), or a packed SKP that
+// leaves unpacked (the single-GPU solid count's last level).
 template <typename RI, typename RO = RI>
 __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_part_scatter(
     const RI* __restrict__ rec, const Chunk* __restrict__ ch, int shift, uint32_t ndig,
@@ -220,9 +221,13 @@ __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_
     for (int i = 0; i < kPartItems; ++i) {
       const uint32_t idx = t + i * kPartThreads + tid;
       if (idx < c.len) {
+        if constexpr (std::is_same<RI, SKP>::value && !std::is_same<RO, SKP>::value) {
+          skp_unpack(base[(uint64_t)idx * 2], base[(uint64_t)idx * 2 + 1], v[i]);
+        } else {
 #pragma unroll
-        for (uint32_t q = 0; q < kQi; ++q) v[i][q] = base[(uint64_t)idx * kQi + q];
-        if constexpr (kQi < kQ) v[i][kQi] = c.start + idx;  // the input index
+          for (uint32_t q = 0; q < kQi; ++q) v[i][q] = base[(uint64_t)idx * kQi + q];
+          if constexpr (kQi < kQ) v[i][kQi] = c.start + idx;  // the input index
+        }
       }
     }
   };
@@ -349,6 +354,10 @@ template int part_level<SK16, SK16>(apg_ctx*, const SK16*, SK16*, const std::vec
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
 template int part_level<SK16, SK24>(apg_ctx*, const SK16*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SKP, SKP>(apg_ctx*, const SKP*, SKP*, const std::vector<std::vector<Seg>>&, int, int,
+                                  uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+template int part_level<SKP, SK24>(apg_ctx*, const SKP*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
+                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
 template int part_level<SK24, SK24>(apg_ctx*, const SK24*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
 template int part_level<SK48, SK48>(apg_ctx*, const SK48*, SK48*, const std::vector<std::vector<Seg>>&, int, int,

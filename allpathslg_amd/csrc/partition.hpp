@@ -34,6 +34,25 @@ struct __attribute__((aligned(8))) SK24 {
   uint64_t w0, w1, pos;
 };
 
+// 16-byte packed form of an SK24 for the partition levels of the
+// single-GPU solid-set count (a record of <= 32 bases: the scatter splits
+// longer ones): w0 = the partition key's top 22 bits << 42 | position (32
+// bits) << 10 | n_kmers << 6 | flank bits (as SK16 bits 40..45); w1 = bases
+// 0..31, 2-bit LSB-first.  The last partition level unpacks it to the SK24
+// the bucket kernels read (skp_unpack), so the levels move 16 bytes per
+// record instead of 24.
+struct __attribute__((aligned(16))) SKP {
+  uint64_t w0, w1;
+};
+constexpr int kSkpKeyBits = 22;
+
+__host__ __device__ inline void skp_unpack(uint64_t w0, uint64_t w1, uint64_t* o) {
+  const uint64_t key32 = (w0 >> (64 - kSkpKeyBits)) << (32 - kSkpKeyBits);
+  o[0] = key32 | (((w0 >> 6) & 15) << 32) | ((w0 & 63) << 40) | ((w1 & 0xffffull) << 48);
+  o[1] = w1 >> 16;
+  o[2] = (w0 >> 10) & 0xffffffffull;
+}
+
 // 48-byte super-k-mer record of the K <= 96 unipath node builder
 // (unipath.hip): w0 = 32-bit minimizer key | n_kmers << 32 | flags << 40
 // (bit 0: b[] starts one base before the first K-mer, bit 1: it ends one base
@@ -50,6 +69,7 @@ __host__ __device__ inline uint64_t rkey(const KRec& r) { return r.meta; }
 __host__ __device__ inline uint64_t rkey(const SK16& r) { return r.w0 << 32; }  // the minimizer key
 __host__ __device__ inline uint64_t rkey(const SK24& r) { return r.w0 << 32; }
 __host__ __device__ inline uint64_t rkey(const SK48& r) { return r.w0 << 32; }
+__host__ __device__ inline uint64_t rkey(const SKP& r) { return r.w0; }  // the key's top bits lead
 
 constexpr int kMaxLevelBits = 8;  // max digit bits of one partition level (LDS-staged scatter)
 
@@ -65,7 +85,8 @@ int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out
 // children, written contiguously to `dst` in (parent, digit) order.  Writes
 // the children's starts to d_child[0 .. nparents*ndig] (last = n) and, if
 // host_child, copies them to the host.  Order inside a child is unspecified.
-// RO: the output record type — R, or SK24 from SK16 (the input index as pos).
+// RO: the output record type — R, SK24 from SK16 (the input index as pos),
+// or SK24 from SKP (unpacked).
 template <typename R, typename RO = R>
 int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag);

@@ -70,7 +70,13 @@ struct SkP {
   int K, m, w, maxnk;
   uint64_t mmask;  // 2m bits
   HashP hp;
+  // > 0: records of more than `split` K-mers leave as pieces of <= split
+  // (the packed SKP form holds <= 32 bases); the count pass counts pieces
+  uint32_t split = 0;
 };
+__host__ __device__ inline uint32_t sk_pieces(uint32_t n, uint32_t split) {
+  return split && n > split ? (n + split - 1) / split : 1u;
+}
 
 static SkP make_skp(int K) {
   SkP p;
@@ -135,7 +141,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
   SkDescWriter W(dd, rv, r0, r1, &dpos, &dovf);
   auto f = [&](const uint8_t*, uint32_t, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
     const uint32_t d = D ? part_key(key) >> (32 - D) : 0;
-    atomicAdd(&hist[d], 1u);
+    atomicAdd(&hist[d], sk_pieces(n, p.split));
     atomicAdd(&khist[d], n);
     W.put(a, n, key, q);
   };
@@ -166,6 +172,14 @@ struct SplitOut {
 template <typename O> struct OutWantsPos { static constexpr bool value = false; };
 template <> struct OutWantsPos<SK24*> { static constexpr bool value = true; };
 template <> struct OutWantsPos<SplitOut> { static constexpr bool value = true; };
+template <> struct OutWantsPos<SKP*> { static constexpr bool value = true; };
+// SK16 layout (<= 32 bases) + position -> the packed partition record
+__device__ __forceinline__ void rec_put(SKP* out, uint64_t i, const SK16& x, uint64_t pos) {
+  const uint64_t b = (x.w0 >> 48) | (x.w1 << 16);  // bases 0..31
+  const uint64_t key = (x.w0 & 0xffffffffull) >> (32 - kSkpKeyBits);
+  const uint64_t n = (x.w0 >> 32) & 15, fl = (x.w0 >> 40) & 63;
+  out[i] = SKP{(key << (64 - kSkpKeyBits)) | (pos << 10) | (n << 6) | fl, b};
+}
 __device__ __forceinline__ void rec_put(SplitOut out, uint64_t i, const SK16& x, uint64_t pos) {
   out.rec[i] = x;
   out.pos[i] = pos;
@@ -196,10 +210,14 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_scatter(SkReads rv, SkP p, in
   sk_read_range(rv.n_reads, G, b, &r0, &r1);
   uint64_t t0 = r0;
   auto f = [&](const uint8_t* rd, uint32_t L, uint32_t a, uint32_t n, uint32_t key, uint32_t q) {
-    const SK16 x = make_rec(rd, L, a, n, key, p.K);
-    const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
-    const uint64_t pos = OutWantsPos<O>::value ? rv.base_off[t0 + q] + a : 0;  // the read's first base + a
-    rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
+    const uint32_t np = sk_pieces(n, p.split);
+    for (uint32_t j = 0; j < np; ++j) {  // pieces of <= p.split K-mers (one piece unless split)
+      const uint32_t aj = a + j * p.split, nj = np == 1 ? n : min(p.split, n - j * p.split);
+      const SK16 x = make_rec(rd, L, aj, nj, key, p.K);
+      const uint32_t d = D ? (uint32_t)x.w0 >> (32 - D) : 0;
+      const uint64_t pos = OutWantsPos<O>::value ? rv.base_off[t0 + q] + aj : 0;  // the read's first base + aj
+      rec_put(out, atomicAdd(&cur[d], 1ull), x, pos);
+    }
   };
   if (dd.desc && !dd.flag[b]) return;  // k_sk_replay wrote this block's records
   while (t0 < r1) {
@@ -247,8 +265,7 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_replay(SkReads rv, SkP p, int
   };
   // one record from its descriptor; bases from the LDS tile at bit `bit0`,
   // or (tile of one over-long read) from HBM
-  auto emit = [&](uint64_t d, uint32_t n_tile, const uint8_t* g) {
-    const uint32_t q = (uint32_t)(d >> 56), a = (uint32_t)(d >> 32) & 0xffffu, nk = (uint32_t)(d >> 48) & 0xffu;
+  auto build = [&](uint32_t q, uint32_t a, uint32_t nk, uint32_t key, uint32_t n_tile, const uint8_t* g) {
     SK16 x;
     if (n_tile) {
       const uint32_t nb = nk + (uint32_t)p.K - 1;  // <= 40
@@ -264,31 +281,50 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_replay(SkReads rv, SkP p, int
       const uint32_t bl = bo - 2, br = bo + 2 * nb;
       const uint32_t lb = hl ? (T.words[bl >> 5] >> (bl & 31)) & 3 : 0;
       const uint32_t rb = hr ? (T.words[br >> 5] >> (br & 31)) & 3 : 0;
-      x.w0 = (uint64_t)part_key((uint32_t)d) | ((uint64_t)nk << 32) | sk_flank_bits(lb, rb, hl, hr) |
+      x.w0 = (uint64_t)part_key(key) | ((uint64_t)nk << 32) | sk_flank_bits(lb, rb, hl, hr) |
              ((lo & 0xffffull) << 48);
       x.w1 = (lo >> 16) | (hi << 48);
     } else {
-      x = make_rec(g, T.rlen[q], a, nk, (uint32_t)d, p.K);
+      x = make_rec(g, T.rlen[q], a, nk, key, p.K);
     }
-    const uint32_t dg = D ? (uint32_t)x.w0 >> (32 - D) : 0;
+    return x;
+  };
+  auto emit = [&](uint64_t d, uint32_t n_tile, const uint8_t* g) {
+    const uint32_t q = (uint32_t)(d >> 56), a = (uint32_t)(d >> 32) & 0xffffu, nk = (uint32_t)(d >> 48) & 0xffu;
+    // a record longer than p.split K-mers leaves as pieces through its own
+    // cursor add (rare: runs longer than the window need a repeated minimizer)
+    const bool piecewise = p.split && nk > p.split;
+    const uint32_t dg = D ? part_key((uint32_t)d) >> (32 - D) : 0;
+    if (piecewise) {
+      const uint32_t np = sk_pieces(nk, p.split);
+      const unsigned long long b0 = atomicAdd(&cur[dg], (unsigned long long)np);
+      for (uint32_t j = 0; j < np; ++j) {
+        const uint32_t aj = a + j * p.split, nj = min(p.split, nk - j * p.split);
+        uint64_t pj = 0;
+        if constexpr (WP) pj = tpos[q] + aj;
+        rec_put(out, b0 + j, build(q, aj, nj, (uint32_t)d, n_tile, g), pj);
+      }
+    }
+    SK16 x{0, 0};
+    if (!piecewise) x = build(q, a, nk, (uint32_t)d, n_tile, g);
     uint64_t pos = 0;
     if constexpr (WP) pos = tpos[q] + a;
     // the wave's lanes of one digit take consecutive slots through one
     // cursor add by the lowest of them (D ballots find the peers): ~2^D
     // distinct-address atomics per wave instead of 64 on 2^D addresses
-    uint64_t peers = __ballot(1);
+    uint64_t peers = __ballot(!piecewise);
     for (int k = 0; k < D; ++k) {
       const uint64_t bk = __ballot((dg >> k) & 1u);
       peers &= ((dg >> k) & 1u) ? bk : ~bk;
     }
     const uint32_t ln = __lane_id();
     const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << ln) - 1));
-    const int leader = __ffsll((long long)peers) - 1;
+    const int leader = peers ? __ffsll((long long)peers) - 1 : 0;
     unsigned long long base = 0;
-    if (rank == 0) base = atomicAdd(&cur[dg], (unsigned long long)__popcll(peers));
+    if (!piecewise && rank == 0) base = atomicAdd(&cur[dg], (unsigned long long)__popcll(peers));
     const uint32_t blo = (uint32_t)__shfl((int)(uint32_t)base, leader, 64);
     const uint32_t bhi = (uint32_t)__shfl((int)(uint32_t)(base >> 32), leader, 64);
-    rec_put(out, (((uint64_t)bhi << 32) | blo) + rank, x, pos);
+    if (!piecewise) rec_put(out, (((uint64_t)bhi << 32) | blo) + rank, x, pos);
   };
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t c = dd.tcnt[t0];
@@ -1466,8 +1502,9 @@ static int sk_desc_bufs(apg_ctx* ctx, const apg_dreads* dr, uint32_t G, SkDesc* 
 // the scanned [digit][block] matrix in "sk_omat" and the records'
 // descriptors in "sk_desc" for sk_scatter.
 int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
-             std::vector<uint64_t>* kmer_counts) {
-  const SkP p = make_skp(K);
+             std::vector<uint64_t>* kmer_counts, uint32_t split) {
+  SkP p = make_skp(K);
+  p.split = split;
   const int D = sk_ceil_log2((uint64_t)P) + kSkDigitBits;
   const uint32_t ndig = 1u << D;
   const uint32_t G = sk_blocks(ctx, dr->n_reads, p);
@@ -1505,18 +1542,21 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   s.G = G;
   s.total = h[ndig];
   s.desc = dd.desc != nullptr;
+  s.split = split;
   if (s.desc) kbytes_add(ctx, "sk_count", s.total * 8);  // the records' descriptors, written
   return APG_OK;
 }
 
 template <typename O>
-static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out, size_t out_bytes) {
+static int sk_scatter_o(apg_ctx* ctx, const apg_dreads* dr, int K, int P, O out, size_t out_bytes,
+                        uint32_t split = 0) {
   auto& s = ctx->skstate;
-  if (!s.valid || s.gen != dr->gen || s.K != K || s.P != P) {
+  if (!s.valid || s.gen != dr->gen || s.K != K || s.P != P || s.split != split) {
     std::vector<uint64_t> rc, kc;
-    APG_TRY(sk_count(ctx, dr, K, P, &rc, &kc));
+    APG_TRY(sk_count(ctx, dr, K, P, &rc, &kc, split));
   }
-  const SkP p = make_skp(K);
+  SkP p = make_skp(K);
+  p.split = split;
   const int D = sk_ceil_log2((uint64_t)P) + kSkDigitBits;
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
   uint64_t* omat = nullptr;
@@ -1557,6 +1597,13 @@ int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, 
 // weak (SK24 records, solid mode only): per-base bitmap of weak K-mer
 // instances, zeroed by the caller.
 __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out);
+__global__ void k_skp_unpack(const SKP* __restrict__ in, uint64_t n, SK24* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t o[3];
+    skp_unpack(in[i].w0, in[i].w1, o);
+    out[i] = SK24{o[0], o[1], o[2]};
+  }
+}
 
 // The fused K+1 spectrum (sk_solid_weak with up_K = K + 1): the K-records'
 // buckets, partitioned for the K count, counted again for their K+1-mers
@@ -1677,7 +1724,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                             uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist,
                             size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr,
                             const SK16* src16 = nullptr, int up_K = 0, uint64_t* up_hist = nullptr,
-                            size_t up_hist_len = 0, SkResult* up_res = nullptr) {
+                            size_t up_hist_len = 0, SkResult* up_res = nullptr, const SKP* srcp = nullptr) {
   const SkP p = make_skp(K);
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
@@ -1739,6 +1786,11 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       APG_CHECK_HIP(hipGetLastError());
       cur = spare;
     }
+    if (srcp && nlev == 0 && n) {  // packed records and no level to unpack them
+      k_skp_unpack<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(srcp, n, bufA);
+      APG_CHECK_HIP(hipGetLastError());
+      cur = bufA;
+    }
   }
   if (nlev == 0) {
     std::vector<uint64_t> hb(B1 + 1, 0);
@@ -1757,6 +1809,14 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         dst = bufA != spare ? bufA : bufB;
         APG_TRY((part_level<SK16, SK24>(ctx, src16, dst, parents, 64 - consumed, bits, n, boff,
                                         last ? nullptr : &hb, "s24")));
+        done = true;
+      } else if (srcp) {  // packed records through the levels, unpacked by the last
+        const SKP* in = reinterpret_cast<const SKP*>(cur);
+        if (last)
+          APG_TRY((part_level<SKP, SK24>(ctx, in, dst, parents, 64 - consumed, bits, n, boff, nullptr, "s24")));
+        else
+          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents, 64 - consumed, bits, n, boff,
+                                        &hb, "s24")));
         done = true;
       }
     }
@@ -2046,16 +2106,26 @@ int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid,
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const uint64_t words = dr->n_bases / 64 + 2;
   APG_CHECK_HIP(hipMemsetAsync(weak, 0, words * 8, ctx->stream));
+  // Packed partition records (SKP, 16 bytes instead of 24 through the
+  // scatter and the partition levels): positions below 2^32, records split
+  // into pieces of <= 32 bases (APG_SK_PACK=0: SK24 throughout)
+  const char* pe = getenv("APG_SK_PACK");
+  const bool pack = !(pe && !strcmp(pe, "0")) && dr->n_bases < (1ull << 32);
+  const uint32_t split = pack ? (uint32_t)std::min(33 - K, 15) : 0u;
   std::vector<uint64_t> rc, kc;
-  APG_TRY(sk_count(ctx, dr, K, 1, &rc, &kc));
+  APG_TRY(sk_count(ctx, dr, K, 1, &rc, &kc, split));
   uint64_t n = 0, nk = 0;
   for (auto c : rc) n += c;
   for (auto c : kc) nk += c;
   SK24* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
-  APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
+  if (pack)
+    APG_TRY(sk_scatter_o<SKP*>(ctx, dr, K, 1, reinterpret_cast<SKP*>(buf), sizeof(SKP), split));
+  else
+    APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
   return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res, nullptr, nullptr,
-                                up ? K + 1 : 0, up_hist, up_hist_len, up_res);
+                                up ? K + 1 : 0, up_hist, up_hist_len, up_res,
+                                pack ? reinterpret_cast<const SKP*>(buf) : nullptr);
 }
 
 __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out) {
