@@ -32,6 +32,10 @@ KERNELS = [
     ("void apg::k_sk_scatter<apg::SK24*>", "sk_scatter", "stream"),
     ("void apg::k_sk_replay<apg::SK16*>", "sk_scatter", "stream"),
     ("void apg::k_sk_replay<apg::SK24*>", "sk_scatter", "stream"),
+    ("void apg::k_sk_scatter<apg::SKP*>", "sk_scatter", "stream"),
+    ("void apg::k_sk_replay<apg::SKP*>", "sk_scatter", "stream"),
+    ("void apg::k_part_scatter<apg::SKP>", "s24_part_scatter", "stream"),  # packed levels (SKP -> SKP / SK24)
+    ("void apg::k_part_count<apg::SKP>", "s24_part_count", "stream"),
     ("void apg::k_part_scatter<apg::SK16>", "s_part_scatter", "stream"),
     ("void apg::k_part_scatter<apg::SK24>", "s24_part_scatter", "stream"),
     ("void apg::k_part_count<apg::SK16>", "s_part_count", "stream"),
