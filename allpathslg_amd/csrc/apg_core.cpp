@@ -277,7 +277,15 @@ int sync(apg_ctx* ctx) {
   return kflush(ctx);
 }
 
+int side_kick(apg_ctx* ctx, int stage) {
+  if (!ctx->side_kick || (stage >= 0 && stage != ctx->side_kick_at)) return APG_OK;
+  std::function<int()> k;
+  k.swap(ctx->side_kick);
+  return k();
+}
+
 int side_join(apg_ctx* ctx) {
+  APG_TRY(side_kick(ctx, -1));  // a pass still waiting for its kick runs now
   if (!ctx->side_finish) return APG_OK;
   std::function<int()> f;
   f.swap(ctx->side_finish);  // cleared first: the finish may allocate workspaces

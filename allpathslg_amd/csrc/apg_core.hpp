@@ -102,6 +102,10 @@ struct apg_ctx {
   // is freed or grown.
   hipStream_t side = nullptr;
   std::function<int()> side_finish;
+  // a side launch deferred to a later point of the same call (side_kick_at:
+  // the caller's stage number that kicks it); side_join kicks it first
+  std::function<int()> side_kick;
+  int side_kick_at = 0;
   // Auxiliary stream: a producer that overlaps the main stream's next
   // kernels and is joined by an event wait (PreCorrect's extension table
   // built beside its candidate scan).
@@ -306,6 +310,8 @@ int kflush(apg_ctx* ctx);
 int sync(apg_ctx* ctx);
 // Complete the side-stream work, if any (runs ctx->side_finish once).
 int side_join(apg_ctx* ctx);
+// Launch a deferred side-stream pass whose kick point is `stage`.
+int side_kick(apg_ctx* ctx, int stage);
 // The side / auxiliary stream (created on first use); 0 on failure.
 hipStream_t side_stream(apg_ctx* ctx);
 hipStream_t aux_stream(apg_ctx* ctx);

@@ -924,6 +924,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
   } else if (ext) {
     if (!ext_done) APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
+    APG_TRY(side_kick(ctx, 1));  // a deferred side pass (the fused K+1 count) starts here
   } else {
     uint64_t T = 1024;
     while (T < 2 * n_solid) T <<= 1;
@@ -1010,6 +1011,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
     }
+    APG_TRY(side_kick(ctx, 2));
     ctx->pc_cand_hint = ncand + ncand / 4 + 4096;
     uint8_t* dec = nullptr;
     APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));

@@ -2053,23 +2053,34 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       // Side stream (APG_SK_UP_SIDE=0: in line): the K+1 pass needs nothing the
       // caller computes next (PreCorrect's candidates, decisions and edits
       // touch neither the records nor their buckets), so it runs beside them
-      // on APG_SK_UP_FRAC of a resident round of blocks, and the caller joins
-      // it (side_join) before it returns.
+      // on APG_SK_UP_FRAC (default 1.0) of a resident round of blocks, and the
+      // caller joins it (side_join) before it returns.
       const char* se = getenv("APG_SK_UP_SIDE");
       const bool side = !(se && !strcmp(se, "0"));
       const hipStream_t sd = side ? side_stream(ctx) : nullptr;
       if (sd) {
         const char* fe = getenv("APG_SK_UP_FRAC");
-        const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 0.75;
-        hipEvent_t ev = nullptr;
-        APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));  // the records and dout are complete
-        APG_CHECK_HIP(hipStreamWaitEvent(sd, ev, 0));
-        APG_CHECK_HIP(hipEventDestroy(ev));
-        {
+        const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 1.0;
+        auto launch = [=]() -> int {
+          hipEvent_t ev = nullptr;
+          APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+          APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));  // the records and dout are complete
+          APG_CHECK_HIP(hipStreamWaitEvent(sd, ev, 0));
+          APG_CHECK_HIP(hipEventDestroy(ev));
           StreamSwap sw(ctx, sd);
-          APG_TRY(sk_up_launch(ctx, cur, boff, nb, n, up_K, u, drec, dcount, n_drec, frac));
-        }
+          return sk_up_launch(ctx, cur, boff, nb, n, up_K, u, drec, dcount, n_drec, frac);
+        };
+        // APG_SK_UP_AT=s: launched at PreCorrect's stage s (0: now, 1: after
+        // the extension table, 2: after the candidate scan — the default: the
+        // pass then runs beside the lookup-bound decisions and edits, not the
+        // LDS-staged candidate scan; same box, APG_SK_UP_FRAC 0.75 / 1.0:
+        // s = 0 160.1 / —, s = 1 163.2 / 162.8, s = 2 160.9 / 158.5 ms)
+        const char* ae = getenv("APG_SK_UP_AT");
+        ctx->side_kick_at = ae ? atoi(ae) : 2;
+        if (ctx->side_kick_at <= 0)
+          APG_TRY(launch());
+        else
+          ctx->side_kick = launch;
         ctx->side_finish = [=]() -> int {
           StreamSwap sw(ctx, sd);
           return sk_up_finish(ctx, cur, boff, nb, n, up_K, u, true, up_hist, up_hist_len, up_res);
