@@ -538,9 +538,10 @@ __global__ void k_digit_starts_u(const uint64_t* __restrict__ omat, uint32_t ndi
 constexpr uint64_t kIdxEmpty = ~0ull;
 __device__ __forceinline__ uint32_t idx_tag(uint64_t h56) { return (uint32_t)(h56 >> 24); }
 
-__global__ void k_node_insert(const KRec* __restrict__ nodes, uint64_t N, unsigned long long* __restrict__ idx,
-                              uint64_t tmask) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
+// nodes [i0, N) into the index
+__global__ void k_node_insert(const KRec* __restrict__ nodes, uint64_t i0, uint64_t N,
+                              unsigned long long* __restrict__ idx, uint64_t tmask) {
+  for (uint64_t i = i0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t h = nodes[i].meta >> 8;
     const unsigned long long want = ((unsigned long long)idx_tag(h) << 32) | i;  // i < 2^31: never empty
     uint64_t s = h & tmask;
@@ -1422,6 +1423,17 @@ struct UskOut {
   uint2* lsucc;  // may be null: per node, its two orientations' local links (usk_links_local)
   uint32_t dedup;  // fold identical records of a chunk before flattening
   unsigned long long* dstat;  // may be null: records, instances, records folded, instances folded
+  // may be null: the node index (k_node_insert's table) built as nodes are
+  // appended, for the nodes with id < idx_lim (gs[4] counts the rest)
+  unsigned long long* idx;
+  uint64_t tmask, idx_lim;
+};
+
+// The node index of the single-GPU build, made by the node buckets
+// (usk_stage) instead of k_node_insert: valid when idx != null.
+struct PreIdx {
+  unsigned long long* idx = nullptr;
+  uint64_t T = 0;
 };
 
 // 32-bit fingerprint of a K=96 record (its full content: n, flank flags, bases)
@@ -1609,7 +1621,18 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
         const unsigned long long at = b + j++;
         if (at < o.cap) {
           const K3 k{ka[s], kb[s], kc[s]};
-          o.nodes[at] = KRec{k.a, k.b, k.c, key_hash(k) | text[s]};
+          const uint64_t kh = key_hash(k);
+          o.nodes[at] = KRec{k.a, k.b, k.c, kh | text[s]};
+          if (o.idx) {  // index entry as k_node_insert makes it; load <= 1/2 by idx_lim
+            if (at < o.idx_lim) {
+              const uint64_t h = kh >> 8;
+              const unsigned long long want = ((unsigned long long)idx_tag(h) << 32) | at;
+              uint64_t q = h & o.tmask;
+              while (atomicCAS(&o.idx[q], kIdxEmpty, want) != kIdxEmpty) q = (q + 1) & o.tmask;
+            } else {
+              atomicAdd(&o.gs[4], 1ull);
+            }
+          }
         }
       }
     if (o.lsucc) {  // block-uniform
@@ -1965,7 +1988,8 @@ static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, 
 }
 
 static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads* dr, const apg_unipath_params& prm,
-                   apg_unipath_graph* out, apg_unipath_stats* st, const uint2* lsucc = nullptr) {
+                   apg_unipath_graph* out, apg_unipath_stats* st, const uint2* lsucc = nullptr,
+                   const PreIdx* pidx = nullptr) {
   const int K = prm.K;
   const KeyP kp = make_keyp(K);
   st->n_nodes = N;
@@ -1984,14 +2008,19 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
 
   // ---- U4 index --------------------------------------------------------------
   uint64_t T = 1024;
-  while (T < 2 * N) T <<= 1;
   unsigned long long* idx = nullptr;
-  APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
-  APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 8, ctx->stream));
-  kbegin(ctx, "u_node_insert", N * 40);
-  k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, N, idx, T - 1);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
+  if (pidx && pidx->idx) {  // built by the node buckets (usk_stage)
+    idx = pidx->idx;
+    T = pidx->T;
+  } else {
+    while (T < 2 * N) T <<= 1;
+    APG_TRY(workspace_t(ctx, "u_idx", T, &idx));
+    APG_CHECK_HIP(hipMemsetAsync(idx, 0xff, T * 8, ctx->stream));
+    kbegin(ctx, "u_node_insert", N * 40);
+    k_node_insert<<<grid_for(ctx, N), 256, 0, ctx->stream>>>(nodes, 0, N, idx, T - 1);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+  }
   const NodeIdx ni{nodes, idx, T - 1};
 
   // ---- U5 --------------------------------------------------------------------
@@ -2287,7 +2316,7 @@ static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P,
 // return when they could not be kept: overflowed nodes beyond the list, or
 // too many nodes)
 static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>& rc, uint64_t nk, const KeyP& kp,
-                     int P, KRec** nodes_out, uint64_t* N_out, uint2** lsucc_out = nullptr) {
+                     int P, KRec** nodes_out, uint64_t* N_out, uint2** lsucc_out = nullptr, PreIdx* pidx = nullptr) {
   const int pbits = ceil_log2_u((uint64_t)P);
   const int D = kUskDigitBits;
   const uint32_t ndig = 1u << D;
@@ -2343,11 +2372,11 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   // buckets -> nodes
   unsigned long long* gs = nullptr;
   uint32_t* ovf = nullptr;
-  APG_TRY(workspace_t(ctx, "usk_gs", 4, &gs));
+  APG_TRY(workspace_t(ctx, "usk_gs", 5, &gs));
   APG_TRY(workspace_t(ctx, "usk_ovf", std::max<uint64_t>(nb, 1), &ovf));
   uint64_t cap = std::max<uint64_t>(1 << 20, nk / 4);
   KRec* nodes = nullptr;
-  unsigned long long hs[4];
+  unsigned long long hs[5];
   const uint64_t grid = resident_grid(ctx, k_usk_bucket, kUskBThreads, nb);
   // APG_USK_DEDUP=0: every record flattened (A/B)
   const char* de = getenv("APG_USK_DEDUP");
@@ -2358,6 +2387,17 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     APG_TRY(workspace_t(ctx, "usk_dstat", 4, &dstat));
     APG_CHECK_HIP(hipMemsetAsync(dstat, 0, 32, ctx->stream));
   }
+  // The node index built by the buckets (APG_U_IDX_BUCKETS=0: by
+  // k_node_insert in u_graph): sized before the node count is known, at
+  // 2 slots per 8 instances (the bench step: 2^28 slots for 65 M nodes); a
+  // build with more nodes than half of it falls back to k_node_insert.
+  const char* ie = getenv("APG_U_IDX_BUCKETS");
+  unsigned long long* pre_idx = nullptr;
+  uint64_t pre_T = 1024;
+  if (pidx && !(ie && !strcmp(ie, "0"))) {
+    while (pre_T < 2 * std::max<uint64_t>(nk / 8, 1)) pre_T <<= 1;
+    APG_TRY(workspace_t(ctx, "u_idx", pre_T, &pre_idx));
+  }
   // APG_U_LOCAL_LINKS=0: every link through the node index (A/B)
   const char* le = getenv("APG_U_LOCAL_LINKS");
   const bool want_ls = lsucc_out && !(le && !strcmp(le, "0"));
@@ -2365,13 +2405,14 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   for (;;) {
     APG_TRY(workspace_t(ctx, "usk_nodes", cap, &nodes));
     if (want_ls) APG_TRY(workspace_t(ctx, "usk_lsucc", cap, &ls));
-    APG_CHECK_HIP(hipMemsetAsync(gs, 0, 4 * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gs, 0, 5 * 8, ctx->stream));
+    if (pre_idx) APG_CHECK_HIP(hipMemsetAsync(pre_idx, 0xff, pre_T * 8, ctx->stream));
     kbegin(ctx, "usk_bucket", n * sizeof(SK48) + (nb + 1) * 8);
-    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, kp,
-                                                         UskOut{nodes, cap, gs, ovf, ls, dedup ? 1u : 0u, dstat});
+    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(
+        cur, boff, nb, kp, UskOut{nodes, cap, gs, ovf, ls, dedup ? 1u : 0u, dstat, pre_idx, pre_T - 1, pre_T / 2});
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
-    APG_TRY(d2h_u64(ctx, gs, hs, 4));
+    APG_TRY(d2h_u64(ctx, gs, hs, 5));
     if (hs[0] <= cap) break;
     vlog(ctx, "unipaths: %llu nodes exceed the node list (%llu), rerunning", hs[0], (unsigned long long)cap);
     cap = hs[0] + hs[0] / 8;
@@ -2383,7 +2424,8 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
             d4[2], d4[3]);
   }
   uint64_t N = hs[0];
-  kbytes_add(ctx, "usk_bucket", N * (sizeof(KRec) + (ls ? sizeof(uint2) : 0)));
+  if (pre_idx && hs[4]) pre_idx = nullptr;  // nodes past half of the index: k_node_insert rebuilds it
+  kbytes_add(ctx, "usk_bucket", N * (sizeof(KRec) + (ls ? sizeof(uint2) : 0) + (pre_idx ? 64 : 0)));
   if (hs[1]) {  // overflowed buckets: their instances through the U2 table
     const uint32_t n_ovf = (uint32_t)hs[1];
     const uint32_t g2 = (uint32_t)std::min<uint64_t>(n_ovf, (uint64_t)ctx->n_cu * 8);
@@ -2415,10 +2457,17 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
       APG_CHECK_HIP(hipMemsetAsync(ls + N, 0xfe, fN * sizeof(uint2), ctx->stream));
     else
       ls = nullptr;
+    if (pre_idx && N + fN <= pre_T / 2) {  // their index entries
+      if (fN) k_node_insert<<<grid_for(ctx, fN), 256, 0, ctx->stream>>>(nodes, N, N + fN, pre_idx, pre_T - 1);
+      APG_CHECK_HIP(hipGetLastError());
+    } else {
+      pre_idx = nullptr;
+    }
     N += fN;
   }
   if (N >= kLsMaxNodes) ls = nullptr;
   if (lsucc_out) *lsucc_out = ls;
+  if (pidx) *pidx = PreIdx{pre_idx, pre_idx ? pre_T : 0};
   vlog(ctx, "unipaths: K=%d P=%d records=%llu instances=%llu levels=%d buckets=%llu nodes=%llu", kp.K, P,
        (unsigned long long)n, (unsigned long long)nk, nlev, (unsigned long long)nb, (unsigned long long)N);
   *nodes_out = nodes;
@@ -2435,7 +2484,7 @@ __global__ void k_usk_sum(const SK48* __restrict__ rec, uint64_t n, unsigned lon
 
 // Single-GPU: plan + scatter into kBig0 (usk_stage's first buffer) + stage.
 static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec** nodes_out, uint64_t* N_out,
-                      uint64_t* n_inst, uint2** lsucc_out) {
+                      uint64_t* n_inst, uint2** lsucc_out, PreIdx* pidx) {
   const UskP p = make_uskp(kp.K);
   std::vector<uint64_t> h, kd;
   uint32_t G = 0;
@@ -2453,7 +2502,7 @@ static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec**
   APG_TRY(usk_scatter(ctx, dr, p, 1, G, recs));
   std::vector<uint64_t> rc(ndig);
   for (uint32_t d = 0; d < ndig; ++d) rc[d] = h[d + 1] - h[d];
-  return usk_stage(ctx, recs, rc, nk, kp, 1, nodes_out, N_out, lsucc_out);
+  return usk_stage(ctx, recs, rc, nk, kp, 1, nodes_out, N_out, lsucc_out, pidx);
 }
 
 static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_params& prm, apg_unipath_graph* out,
@@ -2464,9 +2513,10 @@ static int unipaths_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_unipath_p
   KRec* nodes = nullptr;
   uint64_t N = 0;
   uint2* lsucc = nullptr;
-  APG_TRY(u_sk_nodes(ctx, dr, kp, &nodes, &N, &n, &lsucc));
+  PreIdx pidx;
+  APG_TRY(u_sk_nodes(ctx, dr, kp, &nodes, &N, &n, &lsucc, &pidx));
   st->n_instances = n;
-  return u_graph(ctx, nodes, N, dr, prm, out, st, lsucc);
+  return u_graph(ctx, nodes, N, dr, prm, out, st, lsucc, &pidx);
 }
 
 }  // namespace apg
