@@ -1651,8 +1651,9 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
           for (uint32_t d = 0; d < 2; ++d) {
             const uint32_t out = out_set(ext, d);
             if (__popc(out) != 1) continue;
-            const K3 t = push_right(d ? rk : key, __ffs(out) - 1, kp);
-            const K3 tr = revcomp(t, kp);
+            const uint32_t bo = __ffs(out) - 1;
+            const K3 t = push_right(d ? rk : key, bo, kp);
+            const K3 tr = rc_roll(d ? key : rk, bo, kp);  // revcomp(t) by a shift
             const bool fw = !k3_lt(tr, t);
             const K3 c = fw ? t : tr;
             const uint32_t h = usk_slot_hash(c);
