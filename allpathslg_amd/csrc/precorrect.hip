@@ -626,6 +626,7 @@ __device__ __forceinline__ bool pc_all_weak_at(const unsigned long long* wb, uin
 }
 
 constexpr uint32_t kPcTileW = kPcTileQ / 64 + 2;  // weak words of a staged tile
+constexpr uint32_t kPcKeep = 4;                   // candidate positions a thread keeps from its first scan
 constexpr uint32_t kPcTileList = 1024;            // candidates of a tile written through LDS
 
 template <bool WRITE>
@@ -670,9 +671,16 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     }
     const bool scan = r < n_reads && L >= (uint32_t)K && L <= kPcMaxL;
     uint32_t n = 0;
+    // the first kPcKeep candidates' positions, kept for the list pass (a read
+    // with more scans its quals again)
+    uint32_t keep[kPcKeep / 2] = {};
     if (scan)
       pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
-        if (pc_all_weak_at(wb, wbase, q0, p, L, K)) ++n;
+        if (!pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
+#pragma unroll
+        for (uint32_t k = 0; k < kPcKeep; ++k)
+          if (n == k) keep[k >> 1] |= p << (16 * (k & 1));
+        ++n;
       });
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan<uint32_t>(n, scan_sm, &tot);
@@ -699,10 +707,15 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
         // positions into LDS, then one candidate per thread: independent
         // window loads, consecutive records from consecutive threads
         uint32_t at = ex;
-        if (n)
+        if (n > kPcKeep) {
           pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
             if (pc_all_weak_at(wb, wbase, q0, p, L, K)) list[at++] = tid << 16 | p;
           });
+        } else {
+#pragma unroll
+          for (uint32_t k = 0; k < kPcKeep; ++k)
+            if (k < n) list[at + k] = tid << 16 | ((keep[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+        }
         __syncthreads();
         for (uint32_t i = tid; i < tot; i += kPcTileReads) {
           const uint32_t e = list[i];
