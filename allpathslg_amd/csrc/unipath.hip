@@ -711,18 +711,26 @@ __global__ void __launch_bounds__(256) k_find_rulers(uint64_t D, RankBufs rb, un
 // ruler, so every lane of a wave walks.
 __global__ void k_walk(uint64_t R, uint64_t D, RankBufs rb) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+    // one dependent load per step: the successor's whole record is read once,
+    // for its ruler test (prv) and as the next step's state; the sampled
+    // ruler test (hash bits) needs no load
     const uint32_t v = rb.rlist[i];
     uint32_t x = v, r = 0;
+    uint32_t y = rb.dn[v].nxt;
     for (uint64_t guard = 0; guard <= D; ++guard) {
-      DN& d = rb.dn[x];
-      d.ruler = v;
-      d.lrank = r++;
-      const uint32_t y = d.nxt;
-      if (y == kNone || is_ruler(y, rb.dn)) {
+      rb.dn[x].ruler = v;
+      rb.dn[x].lrank = r++;
+      if (y == kNone || ((uint32_t)fmix64(y) & kRulerMask) == 0) {
+        rb.rnext[v] = y;
+        break;
+      }
+      const DN ny = rb.dn[y];
+      if (ny.prv == kNone) {  // a head (is_ruler's other case)
         rb.rnext[v] = y;
         break;
       }
       x = y;
+      y = ny.nxt;
     }
     rb.seglen[v] = r;
   }
