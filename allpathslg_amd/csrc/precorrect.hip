@@ -884,16 +884,16 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   SolidSet ss{};
   ExtTab et{};
   ctx->pc_ext_valid = false;
-  // With the weak bitmap the candidate scan needs no table: APG_PC_EXT_AUX=1
-  // builds the extension table on the auxiliary stream beside it, the
-  // decisions waiting for it by an event.  Off by default: with the fused
-  // K+1 pass already beside these kernels on the side stream, a third stream
-  // measured 172.4 ms per bench step against 171.9 ms without it (DESIGN.md
-  // §4, tried list).
+  // With the weak bitmap the candidate scan needs no table: the extension
+  // table is built on the auxiliary stream beside it (random atomics beside
+  // a streaming scan), the decisions waiting for it by an event
+  // (APG_PC_EXT_AUX=0: in line).  Same box: 152.3 -> 150.8 ms per bench step
+  // once the fused K+1 pass moved after the scan; with the K+1 pass beside
+  // the scan as well it gained nothing (172.4 vs 171.9 ms).
   hipEvent_t ext_done = nullptr;
   if (ext && weak) {
     const char* ae = getenv("APG_PC_EXT_AUX");
-    const hipStream_t ax = (ae && !strcmp(ae, "1")) ? aux_stream(ctx) : nullptr;
+    const hipStream_t ax = (ae && !strcmp(ae, "0")) ? nullptr : aux_stream(ctx);
     if (ax) {
       hipEvent_t ready = nullptr;
       APG_CHECK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
