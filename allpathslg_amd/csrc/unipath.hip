@@ -2100,6 +2100,36 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   if (U) k_u64_max<<<grid_for(ctx, U), 256, 0, ctx->stream>>>(ulen, U, gs + 26);
   APG_CHECK_HIP(hipGetLastError());
 
+  // Read paths, count pass: on the auxiliary stream beside U8 (unibases and
+  // HyperKmerPath need nothing it writes; APG_U_PATHS_AUX=0: in line after U8)
+  const bool want_paths = dr && (prm.flags & APG_UNIPATH_READ_PATHS) != 0;
+  uint32_t* nint = nullptr;
+  uint64_t *ioff = nullptr, *istart = nullptr, *ilen = nullptr;
+  uint64_t NI = 0;
+  const char* pe = getenv("APG_U_PATHS_AUX");
+  const hipStream_t pax = want_paths && !(pe && !strcmp(pe, "0")) ? aux_stream(ctx) : nullptr;
+  const uint32_t rg = want_paths ? grid_for(ctx, dr->n_reads) : 1;
+  auto paths_count = [&]() -> int {
+    kbegin(ctx, "u_read_paths_count", dr->n_bytes + n * 8);
+    k_read_paths<false><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, ulen, nint,
+                                                     nullptr, nullptr, nullptr, gs + 25);
+    kend(ctx);
+    return scan_u32_u64(ctx, nint, dr->n_reads, ioff, "up");
+  };
+  if (want_paths) {
+    APG_TRY(workspace_t(ctx, "u_nint", std::max<uint64_t>(dr->n_reads, 1), &nint));
+    APG_TRY(workspace_t(ctx, "u_ioff", dr->n_reads + 1, &ioff));
+    if (pax) {
+      hipEvent_t ready = nullptr;
+      APG_CHECK_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+      APG_CHECK_HIP(hipEventRecord(ready, ctx->stream));  // id_base, ulen, uni_of_head complete
+      APG_CHECK_HIP(hipStreamWaitEvent(pax, ready, 0));
+      APG_CHECK_HIP(hipEventDestroy(ready));
+      StreamSwap sw(ctx, pax);
+      APG_TRY(paths_count());
+    }
+  }
+
   // ---- U8 --------------------------------------------------------------------
   uint64_t tot_ub = 0;
   APG_CHECK_HIP(hipMemcpyAsync(&tot_ub, ub_off + U, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -2134,21 +2164,16 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
     return APG_E_STATE;
   }
   // read paths
-  uint32_t* nint = nullptr;
-  uint64_t *ioff = nullptr, *istart = nullptr, *ilen = nullptr;
-  uint64_t NI = 0;
-  const bool want_paths = dr && (prm.flags & APG_UNIPATH_READ_PATHS) != 0;
   if (want_paths) {
-    APG_TRY(workspace_t(ctx, "u_nint", std::max<uint64_t>(dr->n_reads, 1), &nint));
-    APG_TRY(workspace_t(ctx, "u_ioff", dr->n_reads + 1, &ioff));
-    const uint32_t rg = grid_for(ctx, dr->n_reads);
-    kbegin(ctx, "u_read_paths_count", dr->n_bytes + n * 8);
-    k_read_paths<false><<<rg, 256, 0, ctx->stream>>>(rv, ni, kp, head, rank, uni_of_head, id_base, ulen, nint,
-                                                     nullptr, nullptr, nullptr, gs + 25);
-    kend(ctx);
-    APG_TRY(scan_u32_u64(ctx, nint, dr->n_reads, ioff, "up"));
-    APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    if (pax) {  // the count pass ran beside U8: its total, then the write pass here
+      StreamSwap sw(ctx, pax);
+      APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+    } else {
+      APG_TRY(paths_count());
+      APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+    }
     APG_TRY(workspace_t(ctx, "u_istart", std::max<uint64_t>(NI, 1), &istart));
     APG_TRY(workspace_t(ctx, "u_ilen", std::max<uint64_t>(NI, 1), &ilen));
     kbegin(ctx, "u_read_paths_write", dr->n_bytes + n * 8 + NI * 16);
