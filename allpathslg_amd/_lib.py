@@ -421,6 +421,8 @@ SIGNATURES = {
     "apg_comm_barrier": (C.c_int, [_P]),
     "apg_sharded_spectrum": (C.c_int, [_P, _P, _P, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats)]),
     "apg_sharded_precorrect": (C.c_int, [_P, _P, _P, C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
+    "apg_sharded_spectrum_precorrect": (C.c_int, [_P, _P, _P, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats),
+                                                  C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
     "apg_sharded_fill": (C.c_int, [_P, _P, _P, C.POINTER(apg_fill_params), _P, C.c_uint64, C.POINTER(_P), _P,
                                    C.POINTER(apg_fill_stats)]),
     "apg_sharded_unipaths": (C.c_int, [_P, _P, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),

@@ -49,7 +49,16 @@ int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
 int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos);
 // solid set of received records + per-record weak masks (receive order)
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
-                        int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res);
+                        int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res,
+                        int up_K = 0, uint64_t* up_hist = nullptr, size_t up_hist_len = 0,
+                        SkResult* up_res = nullptr);
+bool sk_can_fuse_up(int K);
+// Owner side of the sharded fused spectrum + PreCorrect (precorrect.hip): as
+// apg_shard_solid_weak, plus this shard's K+1 spectrum (up_hist) from the
+// same records; completes before it returns.
+int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+                           uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
+                           SkResult* up_res);
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
                    uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
                    SkResult* res);

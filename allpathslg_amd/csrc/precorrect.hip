@@ -1391,7 +1391,16 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
 
 int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                          uint32_t min_solid, void* d_mask, uint64_t* n_solid) {
+  return shard_solid_weak_fused(ctx, d_recv, recv_counts, K, n_shards, min_solid, d_mask, n_solid, nullptr, 0, nullptr);
+}
+}  // extern "C"
+
+namespace apg {
+int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
+                           uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
+                           SkResult* up_res) {
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid_weak: NULL argument");
+  APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
   ctx->solid_valid = false;
   APG_REQUIRE(K >= 9 && K <= 29 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
@@ -1406,13 +1415,18 @@ int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_
   const uint64_t nk = sk_sum_kmers(ctx, recs, n, &err);
   APG_TRY(err);
   SkResult sr;
-  APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr));
+  APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr,
+                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res));
+  APG_TRY(side_join(ctx));  // the K+1 pass (side stream) completes here
   APG_TRY(sync(ctx));
   ctx->n_solid = sr.n_solid;
   ctx->solid_valid = true;
   *n_solid = sr.n_solid;
   return APG_OK;
 }
+}  // namespace apg
+
+extern "C" {
 
 int apg_precorrect_weak(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, const void* d_solid, uint64_t n_solid,
                         const void* d_pos, const void* d_mask, uint64_t n_rec, apg_pc_stats* stats) {

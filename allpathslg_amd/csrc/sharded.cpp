@@ -30,6 +30,7 @@
 
 #include "apg_core.hpp"
 #include "exchange.hpp"
+#include "kmer_internal.hpp"
 
 namespace apg {
 namespace {
@@ -128,8 +129,15 @@ int apg_sharded_spectrum(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
   return APG_OK;
 }
 
-int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_params* pp,
-                           apg_pc_stats* stats) {
+}  // extern "C"
+
+namespace apg {
+namespace {
+// apg_sharded_precorrect; with up_hist, the first cycle's owner count also
+// yields the K+1 spectrum of the uncorrected reads (the fused
+// apg_sharded_spectrum_precorrect: one exchange of K-records instead of two)
+int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_params* pp, apg_pc_stats* stats,
+               uint64_t* up_hist, size_t up_hist_len, apg_kstats* up_stats) {
   Comm* c = nullptr;
   APG_TRY(check_comm(ctx, comm, &c));
   APG_REQUIRE(reads, "apg_sharded_precorrect: NULL reads");
@@ -162,7 +170,23 @@ int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, cons
                                &x));
       void* rmask = nullptr;
       APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>(x.n_out * 4, 64), &rmask));
-      APG_TRY(apg_shard_solid_weak(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local));
+      if (up_hist && cyc == 0) {
+        SkResult ur;
+        APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, up_hist,
+                                       up_hist_len, &ur));
+        APG_TRY(c->allreduce_u64(up_hist, up_hist_len, APG_COMM_SUM));
+        uint64_t v[4] = {ur.n_kmers, ur.n_distinct, ur.nbuckets, ur.n_overflow_buckets};
+        APG_TRY(c->allreduce_u64(v, 4, APG_COMM_SUM));
+        if (up_stats) {
+          std::memset(up_stats, 0, sizeof(*up_stats));
+          up_stats->n_kmers = v[0];
+          up_stats->n_distinct = v[1];
+          up_stats->n_buckets = v[2];
+          up_stats->n_overflow = v[3];
+        }
+      } else {
+        APG_TRY(apg_shard_solid_weak(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local));
+      }
       // masks travel back: the splits reversed, 4 bytes per record
       std::vector<uint64_t> mb_out(P), mb_in(P);
       for (int q = 0; q < P; ++q) {
@@ -203,6 +227,31 @@ int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, cons
   tot.n_uncorrectable = v[3];
   if (stats) *stats = tot;
   return APG_OK;
+}
+}  // namespace
+}  // namespace apg
+
+extern "C" {
+
+int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_params* pp,
+                           apg_pc_stats* stats) {
+  return sharded_pc(ctx, comm, reads, pp, stats, nullptr, 0, nullptr);
+}
+
+int apg_sharded_spectrum_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, int K_spec, uint64_t* hist,
+                                    size_t hist_len, apg_kstats* kstats, const apg_pc_params* pp,
+                                    apg_pc_stats* pstats) {
+  APG_REQUIRE(ctx && reads && hist && hist_len >= 2, "apg_sharded_spectrum_precorrect: NULL argument or hist_len < 2");
+  apg_pc_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_pc_defaults(&p);
+  if (K_spec != p.K + 1 || p.K < 9 || p.K > 29 || !sk_can_fuse_up(p.K)) {  // not fusable: the two entry points
+    APG_TRY(apg_sharded_spectrum(ctx, comm, reads, K_spec, hist, hist_len, kstats));
+    return apg_sharded_precorrect(ctx, comm, reads, &p, pstats);
+  }
+  return sharded_pc(ctx, comm, reads, &p, pstats, hist, hist_len, kstats);
 }
 
 int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, const apg_fill_params* pp,

@@ -2152,7 +2152,8 @@ __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __re
 // wrec[i] — the records travel with their receive index as position, so the
 // bucket kernel's weak pass writes each mask with a plain store.
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
-                        int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res) {
+                        int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res, int up_K, uint64_t* up_hist,
+                        size_t up_hist_len, SkResult* up_res) {
   APG_REQUIRE(K >= 9 && K <= 32, "sk_shard_solid_weak: K must be in [9, 32]");
   uint64_t n = 0;
   for (auto c : rec_counts) n += c;
@@ -2162,7 +2163,7 @@ int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64
   // the first partition level reads the SK16 records and writes them as SK24
   // with their receive index (no separate widening pass)
   return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, nullptr, res,
-                                wrec, recv);
+                                wrec, recv, up_K, up_hist, up_hist_len, up_res);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {

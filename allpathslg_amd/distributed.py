@@ -131,6 +131,25 @@ def sharded_precorrect(ctx: Context, comm: Comm, reads: DeviceReads, K: int = 24
     return st.as_dict()
 
 
+def sharded_spectrum_precorrect(ctx: Context, comm: Comm, reads: DeviceReads, K_spec: int = 25, K: int = 24,
+                                min_solid: int = 3, max_q_suspect: int = 20, n_cycles: int = 1,
+                                hist_len: int = DEFAULT_HIST_LEN) -> Tuple[np.ndarray, dict, dict]:
+    """sharded_spectrum(K_spec) of the uncorrected reads and
+    sharded_precorrect(K) from one exchange of K-records
+    (apg_sharded_spectrum_precorrect; K_spec = K + 1 fuses, else the two in
+    turn).  Returns (hist, spectrum stats, PreCorrect stats)."""
+    hist = np.zeros(hist_len, dtype=np.uint64)
+    kst = apg_kstats()
+    p = ctx.pc_params(K, min_solid, max_q_suspect, n_cycles)
+    pst = apg_pc_stats()
+    check(lib().apg_sharded_spectrum_precorrect(ctx.handle, comm.handle, reads.handle, K_spec,
+                                                hist.ctypes.data_as(_u64p), hist_len, C.byref(kst), C.byref(p),
+                                                C.byref(pst)), "apg_sharded_spectrum_precorrect")
+    out = kst.as_dict()
+    out["n_shards"] = comm.world
+    return hist, out, pst.as_dict()
+
+
 def sharded_fill(ctx: Context, comm: Comm, reads: DeviceReads, K: int = 24, min_insert: int = 126,
                  max_insert: int = 234, max_steps: int = 1024, last_solid: bool = True, out=None,
                  d_status: Optional[int] = None):

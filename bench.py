@@ -40,7 +40,7 @@ sys.path.insert(0, ROOT)
 
 from allpathslg_amd import Context, synth_fragments, synth_genome, synth_reads  # noqa: E402
 from allpathslg_amd.distributed import (  # noqa: E402
-    Comm, sharded_fill, sharded_precorrect, sharded_spectrum, sharded_unipaths, unique_id)
+    Comm, sharded_fill, sharded_precorrect, sharded_spectrum, sharded_spectrum_precorrect, sharded_unipaths, unique_id)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -685,12 +685,16 @@ def main():
         ctx.copy_reads(dreads, dsrc)
         pst = ust = fst = None
         fused = not overlap and not sharded and not a.spectrum_only and a.fuse
+        # sharded: one exchange of K-records for both (apg_sharded_spectrum_precorrect)
+        sfused = sharded and not overlap and not a.spectrum_only and a.fuse and a.K == a.K_correct + 1
         if overlap:
             pass
         elif fused:  # one counting pass for both (apg_spectrum_precorrect_dev)
             hist, st, pst = spectrum_and_precorrect(ctx, dreads, a)
         elif not sharded:
             hist, st = ctx.kmer_spectrum(dreads, a.K)
+        elif sfused:
+            hist, st, pst = sharded_spectrum_precorrect(ctx, comm, dreads, a.K, K=a.K_correct)
         else:
             hist, st = sharded_spectrum(ctx, comm, dreads, a.K)
         mark("spectrum")
@@ -709,7 +713,8 @@ def main():
                 _, ust = ctx.unipaths(uin, a.K_unipath, read_paths=True, fetch=False)
                 mark("unipaths")
             else:
-                pst = sharded_precorrect(ctx, comm, dreads, K=a.K_correct)
+                if not sfused:
+                    pst = sharded_precorrect(ctx, comm, dreads, K=a.K_correct)
                 mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags

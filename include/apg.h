@@ -745,6 +745,9 @@ int apg_unipath_coverage(apg_ctx* ctx, const apg_aln_pair* locs, uint64_t n_locs
 /*   precorrect every rank's reads corrected in place against the global     */
 /*              solid set (which stays on the context for                    */
 /*              APG_FILL_LAST_SOLID); stats summed, n_solid global           */
+/*   spectrum_precorrect  both of the above from ONE exchange of K-records    */
+/*              (K_spec = p.K + 1, as apg_spectrum_precorrect_dev); falls     */
+/*              back to the two entry points when not fusable                 */
 /*   fill       this rank's pairs (no exchange); stats summed                */
 /*   unipaths   the global graph (identical on every rank, out may be NULL)  */
 /*              + KmerPaths of this rank's reads; n_instances summed         */
@@ -754,6 +757,9 @@ int apg_sharded_spectrum(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
                          size_t hist_len, apg_kstats* stats);
 int apg_sharded_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_params* p,
                            apg_pc_stats* stats);
+int apg_sharded_spectrum_precorrect(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, int K_spec, uint64_t* hist,
+                                    size_t hist_len, apg_kstats* kstats, const apg_pc_params* p,
+                                    apg_pc_stats* pstats);
 int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, const apg_fill_params* p,
                      const void* d_solid, uint64_t n_solid, apg_dreads** filled, uint8_t* d_status,
                      apg_fill_stats* stats);

@@ -79,13 +79,17 @@ def progress(rank, what):
 def chain(ctx, comm, reads, n_cycles, gather=False, placement=True):
     """The sharded chain on this rank's reads; host copies of everything."""
     from allpathslg_amd.distributed import (sharded_consensus, sharded_fill, sharded_precorrect, sharded_spectrum,
-                                            sharded_unipath_locs, sharded_unipaths)
+                                            sharded_spectrum_precorrect, sharded_unipath_locs, sharded_unipaths)
 
     d = ctx.upload(reads)
-    hist, st = sharded_spectrum(ctx, comm, d, 25)
-    progress(comm.rank, "spectrum")
-    pst = sharded_precorrect(ctx, comm, d, K=24, n_cycles=n_cycles)
-    progress(comm.rank, "precorrect")
+    if os.environ.get("APG_TEST_FUSED_SHARDED") == "1":  # one exchange for the K=25 spectrum and the K=24 pass
+        hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24, n_cycles=n_cycles)
+        progress(comm.rank, "spectrum + precorrect")
+    else:
+        hist, st = sharded_spectrum(ctx, comm, d, 25)
+        progress(comm.rank, "spectrum")
+        pst = sharded_precorrect(ctx, comm, d, K=24, n_cycles=n_cycles)
+        progress(comm.rank, "precorrect")
     fixed = ctx.download(d)
     filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
     ffrag = ctx.download(filled)

@@ -45,6 +45,15 @@ def test_sharded_chain_tcp_equals_single_gpu(mono, world, n_cycles, gather, chun
     check_against_mono(run_world(CFG, world, n_cycles, gather, env=env), mono[n_cycles], world, PAIRS)
 
 
+@pytest.mark.parametrize("world,n_cycles", [(2, 1), (4, 2)])
+def test_sharded_fused_spectrum_precorrect_equals_single_gpu(mono, world, n_cycles):
+    """apg_sharded_spectrum_precorrect: the K=25 spectrum rides on the K=24
+    owner count (one exchange); spectrum, corrected reads and everything
+    downstream equal the single-GPU entry points on the union."""
+    check_against_mono(run_world(CFG, world, n_cycles, env={"APG_TEST_FUSED_SHARDED": "1"}), mono[n_cycles], world,
+                       PAIRS)
+
+
 def test_sharded_chain_rccl_world1_equals_single_gpu(gpu_ctx, mono):
     from allpathslg_amd.distributed import Comm, unique_id
 
