@@ -6,8 +6,8 @@ benchmark and the multi-GPU driver.
 """
 from ._lib import ApgError, lib  # noqa: F401
 from .engine import (  # noqa: F401
-    DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, read_graph, read_kmerpaths, shard_bins,
-    write_graph, write_kspec, write_rc_db)
+    DEFAULT_HIST_LEN, Context, DeviceReads, kmer_hash, kmer_unhash, kspec_estimate, read_graph, read_kmerpaths,
+    read_solid, read_unilocs, read_unipath_coverage, shard_bins, write_graph, write_kspec, write_rc_db)
 from .reads import ReadSet, synth_fragments, synth_genome, synth_layout, synth_reads  # noqa: F401
 
 __all__ = [
@@ -26,6 +26,10 @@ __all__ = [
     "synth_layout",
     "read_graph",
     "read_kmerpaths",
+    "kspec_estimate",
+    "read_solid",
+    "read_unilocs",
+    "read_unipath_coverage",
     "write_graph",
     "write_kspec",
     "write_rc_db",

@@ -239,6 +239,17 @@ class apg_uloc_stats(C.Structure):
         return {f: int(getattr(self, f)) for f, _ in self._fields_}
 
 
+class apg_kspec_summary(C.Structure):
+    _fields_ = [("valley", C.c_uint64), ("peak", C.c_uint64), ("genome_size", C.c_uint64),
+                ("genomic_kmers", C.c_uint64), ("genomic_instances", C.c_uint64), ("error_kmers", C.c_uint64),
+                ("error_instances", C.c_uint64), ("coverage", C.c_double), ("repeat_fraction", C.c_double),
+                ("het_ratio", C.c_double), ("reserved", C.c_uint64 * 2)]
+
+    def as_dict(self) -> dict:
+        return {f: (float(getattr(self, f)) if t is C.c_double else int(getattr(self, f)))
+                for f, t in self._fields_ if f != "reserved"}
+
+
 class apg_gapfree_hit(C.Structure):
     _fields_ = [("overlap", C.c_uint32), ("mismatches", C.c_uint32), ("qsum", C.c_uint32), ("offset", C.c_int32)]
 
@@ -313,6 +324,8 @@ SIGNATURES = {
     "apg_shard_solid": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, C.c_uint32, _u64p]),
     "apg_solid_export": (C.c_int, [_P, C.c_void_p]),
     "apg_solid_copy": (C.c_int, [_P, C.c_void_p, _u64p]),
+    "apg_solid_download": (C.c_int, [_P, _u64p, _u64p]),
+    "apg_solid_upload": (C.c_int, [_P, C.c_int, _u64p, C.c_uint64]),
     "apg_precorrect_solid": (
         C.c_int, [_P, _P, C.POINTER(apg_pc_params), C.c_void_p, C.c_uint64, C.POINTER(apg_pc_stats)]
     ),
@@ -386,6 +399,7 @@ SIGNATURES = {
         C.c_int, [_P, C.POINTER(apg_aln_pair), C.c_uint64, C.POINTER(apg_ucov_params), _u64p,
                   C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(apg_ucov_stats)]),
     "apg_device_copy": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "apg_device_to_host": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
     "apg_dreads_shape": (C.c_int, [_P, _P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),
     "apg_repeat_defaults": (None, [C.POINTER(apg_repeat_params)]),
@@ -401,6 +415,14 @@ SIGNATURES = {
     "apg_reads_release": (None, [C.POINTER(apg_reads)]),
     "apg_reads_load_dev": (C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
     "apg_kspec_write": (C.c_int, [C.c_char_p, C.c_int, _u64p, C.c_size_t]),
+    "apg_kspec_estimate": (C.c_int, [_u64p, C.c_size_t, C.POINTER(apg_kspec_summary)]),
+    "apg_solid_write": (C.c_int, [C.c_char_p, C.c_int, _u64p, C.c_uint64]),
+    "apg_solid_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(_u64p), _u64p]),
+    "apg_ulocs_write": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, C.POINTER(apg_aln_pair), C.c_uint64]),
+    "apg_ulocs_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), _u64p, C.POINTER(C.POINTER(apg_aln_pair)), _u64p]),
+    "apg_ucov_write": (C.c_int, [C.c_char_p, C.c_int, C.c_double, C.c_uint64, _u64p, C.POINTER(C.c_double), _u32p]),
+    "apg_ucov_read": (C.c_int, [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_double), _u64p, C.POINTER(_u64p),
+                                C.POINTER(C.POINTER(C.c_double)), C.POINTER(_u32p)]),
     "apg_graph_write": (C.c_int, [C.c_char_p, C.POINTER(apg_unipath_graph)]),
     "apg_graph_read": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(apg_unipath_graph)]),
     "apg_kmerpaths_write": (C.c_int, [C.c_char_p, C.c_int, C.c_uint64, _u64p, _u64p, _u64p]),

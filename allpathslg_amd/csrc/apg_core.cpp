@@ -577,6 +577,16 @@ int apg_device_copy(apg_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes
   return APG_OK;
 }
 
+int apg_device_to_host(apg_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes) {
+  APG_REQUIRE(ctx, "apg_device_to_host: NULL ctx");
+  if (!bytes) return APG_OK;
+  APG_REQUIRE(h_dst && d_src, "apg_device_to_host: NULL pointer");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_CHECK_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  return APG_OK;
+}
+
 void apg_free(void* p) { std::free(p); }
 
 }  // extern "C"

@@ -18,6 +18,7 @@
 //                           qualb: one Phred byte per base
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -232,6 +233,49 @@ void apg_reads_release(apg_reads* r) {
   std::memset(r, 0, sizeof(*r));
 }
 
+// apg_kspec_estimate: the spec is in include/apg.h (restated; checker
+// oracle/kmer_oracle.c ork_kspec_estimate).
+int apg_kspec_estimate(const uint64_t* hist, size_t hist_len, apg_kspec_summary* out) {
+  if (!out || (!hist && hist_len)) return APG_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  if (hist_len < 3) return APG_OK;
+  size_t v = 0;
+  for (size_t m = 1; m < hist_len - 2; ++m)
+    if (hist[m] < hist[m + 1]) {
+      v = m;
+      break;
+    }
+  if (!v) return APG_OK;
+  size_t p = 0;
+  for (size_t m = v + 1; m < hist_len - 1; ++m)
+    if (hist[m] > (p ? hist[p] : 0)) p = m;
+  for (size_t m = 1; m < hist_len; ++m) {
+    const unsigned __int128 inst = (unsigned __int128)m * hist[m];
+    if (m < v) {
+      out->error_kmers += hist[m];
+      out->error_instances += (uint64_t)inst;
+    } else {
+      out->genomic_kmers += hist[m];
+      out->genomic_instances += (uint64_t)inst;
+    }
+  }
+  out->valley = v;
+  out->peak = p;
+  if (!p) return APG_OK;
+  unsigned __int128 s0 = 0, s1 = 0;
+  const size_t hi = std::min<size_t>(2 * p - v, hist_len - 2);
+  for (size_t m = v; m <= hi; ++m) {
+    s0 += hist[m];
+    s1 += (unsigned __int128)m * hist[m];
+  }
+  out->coverage = (double)s1 / (double)s0;
+  out->genome_size = (uint64_t)(((unsigned __int128)out->genomic_instances * s0 + s1 / 2) / s1);
+  if (out->genome_size > out->genomic_kmers)
+    out->repeat_fraction = (double)(out->genome_size - out->genomic_kmers) / (double)out->genome_size;
+  if (p >= 2) out->het_ratio = (double)hist[p / 2] / (double)hist[p];
+  return APG_OK;
+}
+
 int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_len) {
   if (!path || (!hist && hist_len)) return APG_E_ARG;
   const std::string tmp = std::string(path) + ".tmp";
@@ -240,6 +284,15 @@ int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_l
   if (!fh.f) return io_fail("cannot open " + tmp);
   std::fprintf(fh.f, "# KmerSpectrum K=%d bins=%zu (last bin = count >= %zu)\n", K, hist_len,
                hist_len ? hist_len - 1 : 0);
+  apg_kspec_summary e;
+  apg_kspec_estimate(hist, hist_len, &e);
+  std::fprintf(fh.f,
+               "# genome_size_estimate=%llu kmer_coverage=%.4f kmer_coverage_peak=%llu valley=%llu genomic_kmers=%llu "
+               "genomic_instances=%llu error_kmers=%llu error_instances=%llu repeat_fraction=%.6f het_ratio=%.6f\n",
+               (unsigned long long)e.genome_size, e.coverage, (unsigned long long)e.peak, (unsigned long long)e.valley,
+               (unsigned long long)e.genomic_kmers, (unsigned long long)e.genomic_instances,
+               (unsigned long long)e.error_kmers, (unsigned long long)e.error_instances, e.repeat_fraction,
+               e.het_ratio);
   for (size_t m = 0; m < hist_len; ++m)
     if (hist[m]) std::fprintf(fh.f, "%zu\t%llu\n", m, (unsigned long long)hist[m]);
   if (std::fclose(fh.f) != 0) {

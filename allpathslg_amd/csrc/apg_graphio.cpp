@@ -1,7 +1,9 @@
 // apg_graphio.cpp — on-disk unipath-stage objects ("APG v0"):
 // KmerPaths (.paths.kK / .paths_rc.kK), unipaths (.unipaths.kK), unibases
 // (.unibases.kK, APG-fastb), HyperKmerPath (.hkp.kK) and the MakeRcDb index
-// (.pathsdb.kK).  The feudal layouts of ALLPATHS-LG's vecKmerPath /
+// (.pathsdb.kK), plus the correction / placement stages' boundary files:
+// the solid set (.solid.kK), UnipathLocs (.unilocs.kK) and UnipathCoverage
+// (.unipath_cov.kK).  The feudal layouts of ALLPATHS-LG's vecKmerPath /
 // HyperKmerPath / tagged_rpint files are unpinned (reference absent), so these
 // are versioned array containers; a feudal-compatible v1 can be added behind
 // the same calls.
@@ -99,6 +101,9 @@ const char kPaths[8] = {'A', 'P', 'G', 'K', 'P', 0, 0, 0};
 const char kUnip[8] = {'A', 'P', 'G', 'U', 'N', 0, 0, 0};
 const char kHkp[8] = {'A', 'P', 'G', 'H', 'K', 0, 0, 0};
 const char kDb[8] = {'A', 'P', 'G', 'D', 'B', 0, 0, 0};
+const char kSolid[8] = {'A', 'P', 'G', 'S', 'L', 0, 0, 0};
+const char kUlocs[8] = {'A', 'P', 'G', 'U', 'L', 0, 0, 0};
+const char kUcov[8] = {'A', 'P', 'G', 'U', 'C', 0, 0, 0};
 
 }  // namespace
 
@@ -242,6 +247,72 @@ int apg_rc_db_write(const char* head, int K, const apg_rc_db* db) {
   if (rc != APG_OK) return rc;
   return write_container(kname(head, "pathsdb", K), kDb, K, db->n_entries,
                          {{db->entries, db->n_entries, (uint32_t)sizeof(apg_rpint)}});
+}
+
+int apg_solid_write(const char* path, int K, const uint64_t* hashes, uint64_t n) {
+  if (!path || (n && !hashes)) return APG_E_ARG;
+  return write_container(path, kSolid, K, n, {{hashes, n, 8}});
+}
+
+int apg_solid_read(const char* path, int* K, uint64_t** hashes, uint64_t* n) {
+  if (!path || !K || !hashes || !n) return APG_E_ARG;
+  std::vector<void*> a;
+  std::vector<uint64_t> c;
+  uint64_t sc = 0;
+  int rc = read_container(path, kSolid, K, &sc, 1, &a, &c, {8});
+  if (rc != APG_OK) return rc;
+  if (c[0] != sc) {
+    std::free(a[0]);
+    return io_fail(std::string(path) + ": inconsistent solid-set count");
+  }
+  *hashes = static_cast<uint64_t*>(a[0]);
+  *n = sc;
+  return APG_OK;
+}
+
+int apg_ulocs_write(const char* path, int K, uint64_t n_reads, const apg_aln_pair* locs, uint64_t n_locs) {
+  if (!path || (n_locs && !locs)) return APG_E_ARG;
+  return write_container(path, kUlocs, K, n_reads, {{locs, n_locs, (uint32_t)sizeof(apg_aln_pair)}});
+}
+
+int apg_ulocs_read(const char* path, int* K, uint64_t* n_reads, apg_aln_pair** locs, uint64_t* n_locs) {
+  if (!path || !K || !n_reads || !locs || !n_locs) return APG_E_ARG;
+  std::vector<void*> a;
+  std::vector<uint64_t> c;
+  int rc = read_container(path, kUlocs, K, n_reads, 1, &a, &c, {(uint32_t)sizeof(apg_aln_pair)});
+  if (rc != APG_OK) return rc;
+  *locs = static_cast<apg_aln_pair*>(a[0]);
+  *n_locs = c[0];
+  return APG_OK;
+}
+
+int apg_ucov_write(const char* path, int K, double c0, uint64_t n_unipaths, const uint64_t* counts, const double* cov,
+                   const uint32_t* copy_number) {
+  if (!path || (n_unipaths && (!counts || !cov || !copy_number))) return APG_E_ARG;
+  uint64_t bits = 0;
+  std::memcpy(&bits, &c0, 8);
+  return write_container(path, kUcov, K, bits,
+                         {{counts, n_unipaths, 8}, {cov, n_unipaths, 8}, {copy_number, n_unipaths, 4}});
+}
+
+int apg_ucov_read(const char* path, int* K, double* c0, uint64_t* n_unipaths, uint64_t** counts, double** cov,
+                  uint32_t** copy_number) {
+  if (!path || !K || !c0 || !n_unipaths || !counts || !cov || !copy_number) return APG_E_ARG;
+  std::vector<void*> a;
+  std::vector<uint64_t> c;
+  uint64_t bits = 0;
+  int rc = read_container(path, kUcov, K, &bits, 3, &a, &c, {8, 8, 4});
+  if (rc != APG_OK) return rc;
+  if (c[0] != c[1] || c[0] != c[2]) {
+    for (void* p : a) std::free(p);
+    return io_fail(std::string(path) + ": inconsistent coverage arrays");
+  }
+  std::memcpy(c0, &bits, 8);
+  *n_unipaths = c[0];
+  *counts = static_cast<uint64_t*>(a[0]);
+  *cov = static_cast<double*>(a[1]);
+  *copy_number = static_cast<uint32_t*>(a[2]);
+  return APG_OK;
 }
 
 }  // extern "C"

@@ -1480,6 +1480,34 @@ int apg_solid_copy(apg_ctx* ctx, void* d_out, uint64_t* n_solid) {
   return sync(ctx);
 }
 
+int apg_solid_download(apg_ctx* ctx, uint64_t* out, uint64_t* n_solid) {
+  APG_REQUIRE(ctx && n_solid, "apg_solid_download: NULL argument");
+  APG_REQUIRE(ctx->pc_list_valid, "apg_solid_download: no correction pass has run on this context");
+  *n_solid = ctx->pc_n;
+  if (!out || ctx->pc_n == 0) return APG_OK;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_CHECK_HIP(hipMemcpyAsync(out, ctx->pc_list, ctx->pc_n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  return sync(ctx);
+}
+
+int apg_solid_upload(apg_ctx* ctx, int K, const uint64_t* hashes, uint64_t n) {
+  APG_REQUIRE(ctx && (n == 0 || hashes), "apg_solid_upload: NULL argument");
+  APG_REQUIRE(K >= 2 && K <= 32, "apg_solid_upload: K must be in [2, 32]");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  ctx->pc_list_valid = false;  // "x_solid" may hold the current list
+  ctx->pc_ext_valid = false;
+  ctx->clean_valid = false;
+  uint64_t* list = nullptr;
+  APG_TRY(workspace_t(ctx, "x_solid", std::max<uint64_t>(n, 1), &list));
+  if (n) APG_CHECK_HIP(hipMemcpyAsync(list, hashes, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  APG_TRY(sync(ctx));
+  ctx->pc_list = list;
+  ctx->pc_n = n;
+  ctx->pc_K = K;
+  ctx->pc_list_valid = true;
+  return APG_OK;
+}
+
 int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, const void* d_solid,
                          uint64_t n_solid, apg_pc_stats* stats) {
   APG_REQUIRE(ctx && dr, "apg_precorrect_solid: NULL argument");

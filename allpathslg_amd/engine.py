@@ -835,3 +835,58 @@ def read_kmerpaths(path: str):
     finally:
         for p in (po, ps, pl):
             L.apg_free(C.cast(p, C.c_void_p))
+
+
+def kspec_estimate(hist) -> dict:
+    """Genome-size estimate of a spectrum (include/apg.h apg_kspec_estimate)."""
+    from ._lib import apg_kspec_summary
+
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    out = apg_kspec_summary()
+    check(lib().apg_kspec_estimate(h.ctypes.data_as(_u64p), len(h), C.byref(out)), "apg_kspec_estimate")
+    return out.as_dict()
+
+
+def read_solid(path: str):
+    """(K, hashes) of a <head>.solid.k<K> file (ascending apg_kmer_hash values)."""
+    K, n, p = C.c_int(), C.c_uint64(), _u64p()
+    L = lib()
+    check(L.apg_solid_read(path.encode(), C.byref(K), C.byref(p), C.byref(n)), "apg_solid_read")
+    try:
+        return int(K.value), _arr(p, int(n.value), np.uint64)
+    finally:
+        L.apg_free(C.cast(p, C.c_void_p))
+
+
+def read_unilocs(path: str):
+    """(K, n_reads, locs) of a <head>.unilocs.k<K> file; locs (n, 4) int32
+    [read, unipath, start, flags] as Context.unipath_locs returns them."""
+    from ._lib import apg_aln_pair
+
+    K, nr, n = C.c_int(), C.c_uint64(), C.c_uint64()
+    p = C.POINTER(apg_aln_pair)()
+    L = lib()
+    check(L.apg_ulocs_read(path.encode(), C.byref(K), C.byref(nr), C.byref(p), C.byref(n)), "apg_ulocs_read")
+    try:
+        m = int(n.value)
+        locs = (np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), shape=(m * 4,)).reshape(m, 4).copy()
+                if m else np.zeros((0, 4), np.int32))
+        return int(K.value), int(nr.value), locs
+    finally:
+        L.apg_free(C.cast(p, C.c_void_p))
+
+
+def read_unipath_coverage(path: str) -> dict:
+    """A <head>.unipath_cov.k<K> file: {K, c0, counts, cov, cn}."""
+    K, c0, n = C.c_int(), C.c_double(), C.c_uint64()
+    pc, pv, pn = _u64p(), C.POINTER(C.c_double)(), C.POINTER(C.c_uint32)()
+    L = lib()
+    check(L.apg_ucov_read(path.encode(), C.byref(K), C.byref(c0), C.byref(n), C.byref(pc), C.byref(pv), C.byref(pn)),
+          "apg_ucov_read")
+    try:
+        U = int(n.value)
+        return {"K": int(K.value), "c0": float(c0.value), "counts": _arr(pc, U, np.uint64),
+                "cov": _arr(pv, U, np.float64), "cn": _arr(pn, U, np.uint32)}
+    finally:
+        for p in (pc, pv, pn):
+            L.apg_free(C.cast(p, C.c_void_p))

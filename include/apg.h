@@ -118,6 +118,9 @@ int apg_reads_concat_dev(apg_ctx* ctx, const apg_dreads* const* sets, const uint
  * library-owned device output (e.g. apg_unipath_locs_dev) into a caller
  * buffer. */
 int apg_device_copy(apg_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes);
+/* Device-to-host copy (synchronous): a library-owned device output into
+ * caller host memory (the drop-in modules' file writers). */
+int apg_device_to_host(apg_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
 
 /* Fill byte_off[0..n] from base_off[0..n]. */
 int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_off);
@@ -329,6 +332,15 @@ int apg_precorrect_weak(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
  * this context corrected against — what APG_FILL_LAST_SOLID uses.  d_out:
  * device buffer of *n_solid u64, or NULL to query the size. */
 int apg_solid_copy(apg_ctx* ctx, void* d_out, uint64_t* n_solid);
+/* The same set into host memory (out: *n_solid u64 in the set's device order,
+ * or NULL to query the size) — what the PreCorrect / FindErrors modules write
+ * as <HEAD_OUT>.solid.k<K> for the FillFragments module of another process. */
+int apg_solid_download(apg_ctx* ctx, uint64_t* out, uint64_t* n_solid);
+/* Install n solid hashes (host memory, apg_kmer_hash of canonical K-mers) as
+ * the context's last correction pass's set for this K: APG_FILL_LAST_SOLID
+ * (apg_fill_fragments*, apg_sharded_fill) then uses it.  Replaces any earlier
+ * set and its extension table. */
+int apg_solid_upload(apg_ctx* ctx, int K, const uint64_t* hashes, uint64_t n);
 /* One correction pass (p->n_cycles is ignored) against the given solid
  * hashes (apg_kmer_hash of canonical K-mers, device memory). */
 int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* reads, const apg_pc_params* p,
@@ -734,6 +746,13 @@ int apg_unipath_coverage_dev(apg_ctx* ctx, const apg_aln_pair* d_locs, uint64_t 
 /* Host placements (uploaded). */
 int apg_unipath_coverage(apg_ctx* ctx, const apg_aln_pair* locs, uint64_t n_locs, const apg_ucov_params* p,
                          uint64_t* counts, double* cov, uint32_t* copy_number, apg_ucov_stats* stats);
+/* Files (see apg_solid_write): <head>.unilocs.k<K>, <head>.unipath_cov.k<K>. */
+int apg_ulocs_write(const char* path, int K, uint64_t n_reads, const apg_aln_pair* locs, uint64_t n_locs);
+int apg_ulocs_read(const char* path, int* K, uint64_t* n_reads, apg_aln_pair** locs, uint64_t* n_locs);
+int apg_ucov_write(const char* path, int K, double c0, uint64_t n_unipaths, const uint64_t* counts,
+                   const double* cov, const uint32_t* copy_number);
+int apg_ucov_read(const char* path, int* K, double* c0, uint64_t* n_unipaths, uint64_t** counts, double** cov,
+                  uint32_t** copy_number);
 
 /* ------------------------------------------------------------------------- */
 /* Sharded module entry points (multi-GPU, one process per GPU):  */
@@ -873,8 +892,60 @@ void apg_reads_release(apg_reads* r);
  * stream.  Same device read set as apg_fastb_read + apg_qualb_read +
  * apg_reads_upload; free with apg_reads_free. */
 int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int threads, apg_dreads** out);
-/* Spectrum text file (.kspec): "m\tcount" lines for nonzero bins. */
+/* Spectrum text file (.kspec): "m\tcount" lines for nonzero bins, after
+ * '#' header lines that carry apg_kspec_estimate's summary. */
 int apg_kspec_write(const char* path, int K, const uint64_t* hist, size_t hist_len);
+
+/* Genome-size estimate from a K-mer spectrum — the figure KmerSpectrum
+ * reports beside h[m] ([R:M] src/kmers/KmerSpectra.h: the spectrum "also
+ * feeds genome-size/ploidy estimates", SURVEY.md:82; reference snapshot
+ * empty, grep target only).  Host-only.  Spec [D] (restated; the oracle's
+ * ork_kspec_estimate is the checker):
+ *   valley v     = the smallest m in [1, hist_len-2) with hist[m] < hist[m+1]
+ *                  (where the error K-mers' decline ends); 0 if none;
+ *   peak p       = the smallest m in (v, hist_len-1) with the largest hist[m]
+ *                  (the K-mer coverage of single-copy sequence); 0 if v = 0 or
+ *                  that maximum is 0;
+ *   genomic_kmers     = sum over v <= m < hist_len of hist[m];
+ *   genomic_instances = sum over v <= m < hist_len of m * hist[m] (the last
+ *                       bin counts as m = hist_len-1);
+ *   error_kmers / error_instances: the same sums over 1 <= m < v;
+ *   coverage     = S1 / S0 with S1 = sum m * hist[m], S0 = sum hist[m] over
+ *                  v <= m <= min(2p - v, hist_len - 2): the mean K-mer
+ *                  coverage of the single-copy peak (its mode p sits below
+ *                  the mean, by up to 1/p of it);
+ *   genome_size  = round(genomic_instances / coverage) = (genomic_instances *
+ *                  S0 + S1/2) / S1 in 128-bit integers (0 if p = 0): genome
+ *                  positions, every copy of a repeat counted;
+ *   repeat_fraction = genome_size > genomic_kmers ?
+ *                  (genome_size - genomic_kmers) / genome_size : 0;
+ *   het_ratio    = p >= 2 ? hist[p/2] / hist[p] : 0 (a heterozygous peak at
+ *                  half the coverage raises it toward 1: the ploidy hint). */
+typedef struct apg_kspec_summary {
+  uint64_t valley;
+  uint64_t peak;
+  uint64_t genome_size;
+  uint64_t genomic_kmers;
+  uint64_t genomic_instances;
+  uint64_t error_kmers;
+  uint64_t error_instances;
+  double coverage;
+  double repeat_fraction;
+  double het_ratio;
+  uint64_t reserved[2];
+} apg_kspec_summary;
+int apg_kspec_estimate(const uint64_t* hist, size_t hist_len, apg_kspec_summary* out);
+
+/* Module-boundary files of the correction and placement stages (APG v0 array
+ * containers):
+ *   <head>.solid.k<K>        the correction pass's solid set, ascending hashes
+ *   <head>.unilocs.k<K>      UnipathLocs placements (apg_aln_pair; scalar =
+ *                            number of placed-from reads)
+ *   <head>.unipath_cov.k<K>  UnipathCoverage: counts u64, cov f64, copy
+ *                            number u32 per unipath; scalar = c0's IEEE bits
+ * Readers allocate (release each array with apg_free). */
+int apg_solid_write(const char* path, int K, const uint64_t* hashes, uint64_t n);
+int apg_solid_read(const char* path, int* K, uint64_t** hashes, uint64_t* n);
 
 /* Unipath-stage files, "APG v0" array containers:
  *   <head>.unipaths.k<K>  len / id_base / rc per unipath (+ n_nodes)

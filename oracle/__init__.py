@@ -57,6 +57,8 @@ def lib() -> C.CDLL:
         L.ork_precorrect_solid.restype = C.c_int
         L.ork_precorrect_solid.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, _u8p, C.c_int, C.c_uint32, _u64p,
                                            C.c_uint64, _u64p]
+        L.ork_kspec_estimate.restype = None
+        L.ork_kspec_estimate.argtypes = [_u64p, C.c_uint64, _u64p, C.POINTER(C.c_double)]
         L.ork_free.restype = None
         L.ork_free.argtypes = [C.c_void_p]
         _lib = L
@@ -143,6 +145,19 @@ def spectrum_from_counts(counts: np.ndarray, hist_len: int) -> np.ndarray:
 def kmer_spectrum(reads, K: int, hist_len: int = 1 << 16) -> np.ndarray:
     _, c = kmer_count(reads, K)
     return spectrum_from_counts(c, hist_len)
+
+
+def kspec_estimate(hist) -> dict:
+    """Genome-size estimate of a spectrum (ork_kspec_estimate)."""
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    u = np.zeros(7, np.uint64)
+    d = np.zeros(3, np.float64)
+    lib().ork_kspec_estimate(h.ctypes.data_as(_u64p), len(h), u.ctypes.data_as(_u64p),
+                             d.ctypes.data_as(C.POINTER(C.c_double)))
+    names = ("valley", "peak", "genome_size", "genomic_kmers", "genomic_instances", "error_kmers", "error_instances")
+    out = {k: int(x) for k, x in zip(names, u)}
+    out.update(coverage=float(d[0]), repeat_fraction=float(d[1]), het_ratio=float(d[2]))
+    return out
 
 
 def precorrect(reads, K=24, min_solid=3, max_q=20, n_cycles=1, fast=False):

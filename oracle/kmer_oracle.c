@@ -295,6 +295,55 @@ void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t 
   }
 }
 
+/* KmerSpectrum's genome-size estimate (include/apg.h apg_kspec_estimate, the
+ * spec restated; [R:M] src/kmers/KmerSpectra.h, grep target only): the
+ * valley where the error K-mers' decline ends, the single-copy peak after it,
+ * genome positions = genomic instances / the peak's mean coverage (rounded).  u[] = {valley,
+ * peak, genome_size, genomic_kmers, genomic_instances, error_kmers,
+ * error_instances}; d[] = {coverage, repeat_fraction, het_ratio}. */
+void ork_kspec_estimate(const uint64_t* h, uint64_t len, uint64_t* u, double* d) {
+  memset(u, 0, 7 * sizeof(uint64_t));
+  d[0] = d[1] = d[2] = 0.0;
+  if (len < 3) return;
+  uint64_t v = 0;
+  for (uint64_t m = 1; m + 2 < len; ++m)
+    if (h[m] < h[m + 1]) {
+      v = m;
+      break;
+    }
+  if (v == 0) return;
+  uint64_t p = 0, best = 0;
+  for (uint64_t m = v + 1; m + 1 < len; ++m)
+    if (h[m] > best) {
+      best = h[m];
+      p = m;
+    }
+  for (uint64_t m = 1; m < len; ++m) {
+    if (m < v) {
+      u[5] += h[m];
+      u[6] += m * h[m];
+    } else {
+      u[3] += h[m];
+      u[4] += m * h[m];
+    }
+  }
+  u[0] = v;
+  u[1] = p;
+  if (p == 0) return;
+  /* mean coverage of the single-copy peak: m in [v, min(2p - v, len - 2)] */
+  unsigned __int128 s0 = 0, s1 = 0;
+  uint64_t hi = 2 * p - v;
+  if (hi > len - 2) hi = len - 2;
+  for (uint64_t m = v; m <= hi; ++m) {
+    s0 += h[m];
+    s1 += (unsigned __int128)m * h[m];
+  }
+  d[0] = (double)s1 / (double)s0;
+  u[2] = (uint64_t)(((unsigned __int128)u[4] * s0 + s1 / 2) / s1);
+  if (u[2] > u[3]) d[1] = (double)(u[2] - u[3]) / (double)u[2];
+  if (p >= 2) d[2] = (double)h[p / 2] / (double)h[p];
+}
+
 void ork_free(void* p) { free(p); }
 
 /* Host threads of the OpenMP loops (0: OMP_NUM_THREADS / all cores). */

@@ -18,6 +18,7 @@ uint64_t ork_kmer_count_range(uint64_t n_reads, const uint64_t* base_off, const 
 void ork_set_threads(int n);
 int ork_threads(void);
 void ork_spectrum(const uint32_t* counts, uint64_t nd, uint64_t* hist, uint64_t hist_len);
+void ork_kspec_estimate(const uint64_t* hist, uint64_t hist_len, uint64_t* u7, double* d3);
 void ork_free(void* p);
 int ork_precorrect(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, uint8_t* packed,
                    uint8_t* quals, int K, uint32_t min_solid, uint32_t maxq, uint32_t n_cycles, uint64_t* stats);

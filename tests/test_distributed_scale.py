@@ -34,9 +34,12 @@ def mono(gpu_ctx):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_chain_genome_scale_equals_single_gpu(mono, world):
-    parts = run_world(CFG, world, 1, timeout=800)
+@pytest.mark.parametrize("world,fused", [(2, False), (4, False), (2, True), (4, True)])
+def test_sharded_chain_genome_scale_equals_single_gpu(mono, world, fused):
+    """fused: the N > 1 bench step's entry point, apg_sharded_spectrum_precorrect
+    (one exchange of K=24 records for the K=25 spectrum and the solid set)."""
+    env = {"APG_TEST_FUSED_SHARDED": "1"} if fused else None
+    parts = run_world(CFG, world, 1, timeout=800, env=env)
     check_against_mono(parts, mono, world, CFG[1])
     # the workload is what it claims: 6 M reads, most pairs filled, a real graph
     assert mono["st"]["n_kmers"] == 2 * CFG[1] * 76

@@ -223,8 +223,15 @@ def c2(gpu_ctx):
     filled_a = gpu_ctx.download(a["filled"])
     b = run_chain(gpu_ctx, dsrc, dwork, a["filled"], status)
     filled_b = gpu_ctx.download(b["filled"])
+    # the bench's timed entry point with its defaults (bench.py step():
+    # apg_spectrum_precorrect_dev — side-stream K+1 pass with the deferred
+    # kick, extension table on the auxiliary stream, packed SKP records, the
+    # K+1 pass fed by the record dedup)
+    gpu_ctx.copy_reads(dwork, dsrc)
+    fh, fks, fps = gpu_ctx.spectrum_precorrect(dwork, K_spec=25, K=24)
+    fused = {"hist": fh, "st": fks, "pst": fps, "solid": solid_sorted(gpu_ctx), "fixed": gpu_ctx.download(dwork)}
     yield {"genome": g, "reads": reads, "a": a, "b": b, "fixed": fixed_a, "filled_a": filled_a,
-           "filled_b": filled_b, "seed": seed, "dsrc": dsrc}
+           "filled_b": filled_b, "seed": seed, "dsrc": dsrc, "fused": fused}
     for d in (dsrc, dwork, a["filled"]):
         d.free()
 
@@ -248,28 +255,54 @@ def test_c2_parcel_counts_match_oracle(c2, gpu_ctx):
     assert np.array_equal(counts, oc)
 
 
-def test_c2_full_spectrum_matches_oracle(c2):
-    """The complete K=25 spectrum of all 40 M reads (3.04 G K-mer instances)."""
-    exp = oracle.kmer_spectrum(c2["reads"], 25)
-    assert np.array_equal(c2["a"]["hist"], exp)
+@pytest.fixture(scope="module")
+def c2_oracle(c2):
+    """The oracle's whole-table results for all 40 M reads, computed once:
+    K=25 spectrum, K=24 solid set, PreCorrect against that solid set."""
+    reads = c2["reads"]
+    spec = oracle.kmer_spectrum(reads, 25)
+    solid = np.sort(oracle.solid_hashes(reads, 24, 3))
+    fixed, est = oracle.precorrect_solid(reads, solid, K=24, fast=True)
+    return {"hist": spec, "solid": solid, "fixed": fixed, "est": est}
 
 
-def test_c2_full_solid_set_matches_oracle(c2):
-    """The complete K=24 solid set (count >= 3) of all 40 M reads."""
-    exp = np.sort(oracle.solid_hashes(c2["reads"], 24, 3))
-    assert len(exp) > 60_000_000
-    assert np.array_equal(c2["a"]["solid"], exp)
-
-
-def test_c2_full_precorrect_matches_oracle(c2):
-    """PreCorrect of all 40 M reads against the (whole-table-checked) solid
-    set: every base, quality and counter."""
-    reads, fixed, solid = c2["reads"], c2["fixed"], c2["a"]["solid"]
-    exp, est = oracle.precorrect_solid(reads, solid, K=24, fast=True)
+def assert_precorrect_equal(fixed, pst, exp, est):
     assert np.array_equal(fixed.packed[: int(fixed.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
     assert np.array_equal(fixed.quals, exp.quals)
     for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
-        assert c2["a"]["pst"][k] == est[k], k
+        assert pst[k] == est[k], k
+
+
+def test_c2_full_spectrum_matches_oracle(c2, c2_oracle):
+    """The complete K=25 spectrum of all 40 M reads (3.04 G K-mer instances)."""
+    assert np.array_equal(c2["a"]["hist"], c2_oracle["hist"])
+
+
+def test_c2_full_solid_set_matches_oracle(c2, c2_oracle):
+    """The complete K=24 solid set (count >= 3) of all 40 M reads."""
+    assert len(c2_oracle["solid"]) > 60_000_000
+    assert np.array_equal(c2["a"]["solid"], c2_oracle["solid"])
+
+
+def test_c2_full_precorrect_matches_oracle(c2, c2_oracle):
+    """PreCorrect of all 40 M reads against the (whole-table-checked) solid
+    set: every base, quality and counter."""
+    assert_precorrect_equal(c2["fixed"], c2["a"]["pst"], c2_oracle["fixed"], c2_oracle["est"])
+
+
+def test_c2_bench_entry_point_matches_oracle(c2, c2_oracle):
+    """The bench's own timed entry point (apg_spectrum_precorrect_dev at its
+    defaults) at full C2 size against the oracle: the whole K=25 spectrum,
+    the whole K=24 solid set, and every corrected base, quality and counter
+    of the 40 M reads."""
+    f = c2["fused"]
+    assert np.array_equal(f["hist"], c2_oracle["hist"])
+    m = np.arange(len(f["hist"]), dtype=np.uint64)
+    assert int((f["hist"] * m).sum()) == f["st"]["n_kmers"] == c2["reads"].n_reads * 76
+    assert int(f["hist"].sum()) == f["st"]["n_distinct"]
+    assert np.array_equal(f["solid"], c2_oracle["solid"])
+    assert f["pst"]["n_solid"] == len(c2_oracle["solid"])
+    assert_precorrect_equal(f["fixed"], f["pst"], c2_oracle["fixed"], c2_oracle["est"])
 
 
 def test_c2_fill_sample_matches_oracle(c2):

@@ -1,12 +1,14 @@
 // apg_modules.cpp — drop-in command-line modules for RunAllPathsLG's hot
-// path: KmerSpectrum, PreCorrect, FindErrors, ErrorCorrectJump,
-// CommonPather, Unipather, MakeRcDb.  Same module names and KEY=VALUE argument style as the
+// path (SURVEY §8b, §3 call stack): KmerSpectrum, PreCorrect, FindErrors,
+// FillFragments, ErrorCorrectJump, MergeReadSets (all_reads), CommonPather,
+// Unipather, MakeRcDb, UnipathLocs, UnipathCoverage.  Same module names and KEY=VALUE argument style as the
 // reference modules ([R:H] ParsedArgs; PRE/DATA/RUN directories); inputs and
 // outputs are files in the RUN directory (APG v0 formats).
 // One binary, dispatched on the name it is invoked under (bin/<Module> are
 // symlinks).  Exit status 0 on success, 1 with a message on any error.
 #include <sys/stat.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -220,11 +222,64 @@ int kmer_spectrum(Args& a) {
   }
   const std::string out = head + ".kspec.k" + std::to_string(K);
   a.check(apg_kspec_write(out.c_str(), K, hist.data(), hist.size()), "writing .kspec");
-  std::printf("%s: %llu reads, %llu %d-mers, %llu distinct -> %s\n", a.module.c_str(),
-              (unsigned long long)rd.r.n_reads, (unsigned long long)st.n_kmers, K, (unsigned long long)st.n_distinct,
+  apg_kspec_summary e;
+  a.check(apg_kspec_estimate(hist.data(), hist.size(), &e), "apg_kspec_estimate");
+  std::printf("%s: %llu reads, %llu %d-mers, %llu distinct, genome size estimate %llu (K-mer coverage %llu) -> %s\n",
+              a.module.c_str(), (unsigned long long)rd.r.n_reads, (unsigned long long)st.n_kmers, K,
+              (unsigned long long)st.n_distinct, (unsigned long long)e.genome_size, (unsigned long long)e.peak,
               out.c_str());
   return 0;
 }
+
+// <head>.solid.k<K>: the last correction pass's solid set, ascending — what
+// FillFragments (APG_FILL_LAST_SOLID in one process) uses in the next one.
+void write_solid(Args& a, apg_ctx* c, const std::string& head, int K) {
+  uint64_t n = 0;
+  a.check(apg_solid_download(c, nullptr, &n), "apg_solid_download");
+  std::vector<uint64_t> s(n + 1);
+  a.check(apg_solid_download(c, s.data(), &n), "apg_solid_download");
+  s.resize(n);
+  std::sort(s.begin(), s.end());
+  a.check(apg_solid_write((head + ".solid.k" + std::to_string(K)).c_str(), K, s.data(), n), "writing .solid");
+}
+
+struct Solid {
+  uint64_t* h = nullptr;
+  uint64_t n = 0;
+  ~Solid() { apg_free(h); }
+};
+
+// Reads [r0, r1) of a loaded set copied out as a standalone read set (rank
+// parts written by sharded runs).
+void write_reads(Args& a, const std::string& head, const apg_reads& r, bool quals) {
+  a.check(apg_fastb_write((head + ".fastb").c_str(), &r), "writing .fastb");
+  if (quals) a.check(apg_qualb_write((head + ".qualb").c_str(), &r), "writing .qualb");
+}
+
+// Read sets concatenated in order (a part may be empty); quals kept only if
+// every part has them.
+struct Joined {
+  std::vector<uint64_t> bo{0}, yo{0};
+  std::vector<uint8_t> pk, q;
+  bool quals = true;
+  void add(const apg_reads& r) {
+    if (!r.quals) quals = false;
+    const uint64_t n = r.n_reads;
+    if (n == 0) return;
+    const uint64_t b0 = bo.back(), y0 = yo.back();
+    for (uint64_t i = 1; i <= n; ++i) {
+      bo.push_back(b0 + r.base_off[i] - r.base_off[0]);
+      yo.push_back(y0 + r.byte_off[i] - r.byte_off[0]);
+    }
+    pk.insert(pk.end(), r.packed + r.byte_off[0], r.packed + r.byte_off[n]);
+    if (quals) q.insert(q.end(), r.quals + r.base_off[0], r.quals + r.base_off[n]);
+  }
+  apg_reads view() {
+    pk.resize(yo.back() + 64, 0);
+    q.resize(bo.back() + 1, 0);
+    return apg_reads{bo.size() - 1, bo.data(), yo.data(), pk.data(), quals ? q.data() : nullptr};
+  }
+};
 
 int precorrect(Args& a, uint32_t default_cycles, const char* default_out) {
   const std::string dir = a.run_dir();
@@ -295,6 +350,7 @@ int precorrect(Args& a, uint32_t default_cycles, const char* default_out) {
   o.quals = q.data();
   a.check(apg_fastb_write((out + ".fastb").c_str(), &o), "writing .fastb");
   a.check(apg_qualb_write((out + ".qualb").c_str(), &o), "writing .qualb");
+  write_solid(a, ctx.c, out, p.K);
   std::printf("%s: %llu reads, %llu suspect, %llu corrected, %llu ambiguous, %llu uncorrectable -> %s.{fastb,qualb}\n",
               a.module.c_str(), (unsigned long long)n, (unsigned long long)st.n_suspect,
               (unsigned long long)st.n_corrected, (unsigned long long)st.n_ambiguous,
@@ -350,6 +406,287 @@ int error_correct_jump(Args& a) {
   std::printf("%s: %llu jump reads, %llu corrected, %llu whole, %llu trimmed, %llu dropped -> %s.{fastb,qualb}\n",
               a.module.c_str(), (unsigned long long)n, (unsigned long long)st.pc.n_corrected,
               (unsigned long long)st.n_full, (unsigned long long)st.n_trimmed, (unsigned long long)st.n_dropped,
+              out.c_str());
+  return 0;
+}
+
+// FillFragments: frag pairs (reads 2i, 2i+1) closed into the fragments they
+// were read from (apg_fill_fragments), against the solid set the correction
+// module wrote (<SOLID>.solid.k<K>, SOLID defaulting to HEAD_IN) — the
+// APG_FILL_LAST_SOLID set of the in-process chain — or, when no such file
+// exists and SOLID= is not given, the pairs' own K-mers with count >=
+// MIN_SOLID.  Output: <HEAD_OUT>.fastb, the filled fragments in pair order
+// (no qualities).
+int fill_fragments(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string in = dir + "/" + a.get("HEAD_IN", "frag_reads_corr");
+  const std::string out = dir + "/" + a.get("HEAD_OUT", "filled_reads");
+  const bool solid_given = a.kv.count("SOLID") > 0;
+  const std::string sh_in = dir + "/" + a.get("SOLID", a.get("HEAD_IN", "frag_reads_corr"));
+  apg_fill_params p;
+  apg_fill_defaults(&p);
+  p.K = (int)a.num("K", p.K);
+  p.min_insert = (uint32_t)a.num("MIN_INSERT", p.min_insert);
+  p.max_insert = (uint32_t)a.num("MAX_INSERT", p.max_insert);
+  p.max_steps = (uint32_t)a.num("MAX_STEPS", p.max_steps);
+  p.min_solid = (uint32_t)a.num("MIN_SOLID", p.min_solid);
+  Shard sh(a);
+  a.finish();
+  const std::string sf = sh_in + ".solid.k" + std::to_string(p.K);
+  Solid sol;
+  const bool have_solid = exists(sf);
+  if (solid_given && !have_solid) a.fail("missing solid set " + sf);
+  if (have_solid) {
+    int k = 0;
+    a.check(apg_solid_read(sf.c_str(), &k, &sol.h, &sol.n), "reading .solid");
+    if (k != p.K) a.fail(sf + " holds K=" + std::to_string(k) + " K-mers");
+  }
+  Reads rd;
+  load_reads(a, in, false, &rd);
+  if (rd.r.n_reads % 2) a.fail(in + ".fastb: odd read count (pairs are reads 2i, 2i+1)");
+  Ctx ctx(a);
+  apg_fill_stats st;
+  apg_reads filled{};
+  struct Rel {
+    apg_reads* r;
+    ~Rel() { apg_reads_release(r); }
+  } rel{&filled};
+  if (sh.sharded()) {
+    // a rank fills its own pairs (no exchange): the solid set must be the
+    // global one, so the sharded form needs the correction module's file
+    if (!have_solid) a.fail("sharded FillFragments needs the correction pass's solid set (" + sf + ")");
+    sh.connect(a, ctx.c);
+    uint64_t r0, r1;
+    sh.range(rd.r.n_reads, &r0, &r1);
+    Slice sl(rd.r, r0, r1);
+    DReads d, f;
+    a.check(apg_reads_upload(ctx.c, &sl.r, &d.d), "apg_reads_upload");
+    a.check(apg_solid_upload(ctx.c, p.K, sol.h, sol.n), "apg_solid_upload");
+    p.flags |= APG_FILL_LAST_SOLID;
+    a.check(apg_sharded_fill(ctx.c, sh.comm, d.d, &p, nullptr, 0, &f.d, nullptr, &st), "apg_sharded_fill");
+    uint64_t nf = 0, nb = 0, ny = 0;
+    a.check(apg_dreads_shape(ctx.c, f.d, &nf, &nb, &ny, nullptr, nullptr), "apg_dreads_shape");
+    std::vector<uint64_t> bo(nf + 1), yo(nf + 1);
+    a.check(apg_dreads_shape(ctx.c, f.d, nullptr, nullptr, nullptr, bo.data(), yo.data()), "apg_dreads_shape");
+    std::vector<uint8_t> pk(ny + 64, 0);
+    a.check(apg_reads_download(ctx.c, f.d, pk.data(), nullptr), "apg_reads_download");
+    apg_reads mine{nf, bo.data(), yo.data(), pk.data(), nullptr};
+    if (sh.rank != 0) {
+      write_reads(a, part_name(out, sh.rank, sh.world), mine, false);
+      sh.barrier(a);
+      sh.barrier(a);  // rank 0 has read every part
+      return 0;
+    }
+    sh.barrier(a);
+    Joined j;
+    j.add(mine);
+    for (int r = 1; r < sh.world; ++r) {  // ranks hold consecutive pairs: rank order = pair order
+      const std::string h = part_name(out, r, sh.world);
+      Reads pr;
+      load_reads(a, h, false, &pr);
+      j.add(pr.r);
+      std::remove((h + ".fastb").c_str());
+    }
+    sh.barrier(a);
+    apg_reads o = j.view();
+    write_reads(a, out, o, false);
+  } else {
+    if (!have_solid) p.flags &= ~APG_FILL_LAST_SOLID;
+    a.check(apg_fill_fragments(ctx.c, &rd.r, &p, sol.h, sol.n, &filled, nullptr, &st), "apg_fill_fragments");
+    write_reads(a, out, filled, false);
+  }
+  std::printf("%s: %llu pairs, %llu filled, %llu none, %llu ambiguous, %llu over budget, %llu skipped "
+              "(solid set: %s, %llu K-mers) -> %s.fastb\n",
+              a.module.c_str(), (unsigned long long)st.n_pairs, (unsigned long long)st.n_filled,
+              (unsigned long long)st.n_none, (unsigned long long)st.n_ambiguous, (unsigned long long)st.n_budget,
+              (unsigned long long)st.n_skip, have_solid ? sf.c_str() : "own count", (unsigned long long)st.n_solid,
+              out.c_str());
+  return 0;
+}
+
+// MergeReadSets: all_reads = the read sets of HEADS (comma-separated, in
+// order) concatenated — filled fragments ++ ErrorCorrectJump's trimmed jumps
+// in the RunAllPathsLG chain (a dropped jump read stays as a 0-length read, so
+// pair indices hold), as apg_reads_concat_dev does on the device.  Qualities
+// are written only when every input has a .qualb.
+int merge_read_sets(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string heads = a.get("HEADS", "filled_reads,jump_reads_ec");
+  const std::string out = dir + "/" + a.get("HEAD_OUT", "all_reads");
+  a.finish();
+  std::vector<std::string> hs;
+  for (size_t b = 0; b <= heads.size();) {
+    const size_t e = std::min(heads.find(',', b), heads.size());
+    if (e > b) hs.push_back(dir + "/" + heads.substr(b, e - b));
+    b = e + 1;
+  }
+  if (hs.empty()) a.fail("HEADS names no read set");
+  bool quals = true;
+  for (const auto& h : hs) quals = quals && exists(h + ".qualb");
+  Joined j;
+  for (const auto& h : hs) {
+    Reads r;
+    load_reads(a, h, quals, &r);
+    j.add(r.r);
+  }
+  apg_reads o = j.view();
+  write_reads(a, out, o, quals);
+  std::printf("%s: %zu read sets, %llu reads, %llu bases -> %s.fastb%s\n", a.module.c_str(), hs.size(),
+              (unsigned long long)o.n_reads, (unsigned long long)j.bo.back(), out.c_str(), quals ? "/.qualb" : "");
+  return 0;
+}
+
+// The unipath graph of files <head>.*.k<K> rebuilt on the context, so that
+// placements resolve against it (UnipathLocs / UnipathCoverage work on "the
+// context's last unipath build"): the unibases, one read per unipath, give
+// exactly the file's unipaths — every K-mer lies in one unipath and every
+// interior link lies inside a unibase, so no unipath splits or merges, and
+// the order follows the head K-mers — which is checked against the
+// .unipaths / .unibases files before any placement.
+void rebuild_graph(Args& a, apg_ctx* c, const std::string& head, int K, Shard* sh, apg_unipath_graph* file_g) {
+  a.check(apg_graph_read(head.c_str(), K, file_g), "reading unipath files (run Unipather first)");
+  Reads ub;
+  load_reads(a, head + ".unibases.k" + std::to_string(K), false, &ub);
+  apg_unipath_params p;
+  apg_unipath_defaults(&p);
+  p.K = K;
+  apg_unipath_graph g{};
+  apg_unipath_stats st;
+  if (sh && sh->sharded()) {
+    uint64_t r0, r1;
+    // unibases are not pairs: split them evenly by read
+    r0 = ub.r.n_reads * (uint64_t)sh->rank / (uint64_t)sh->world;
+    r1 = ub.r.n_reads * (uint64_t)(sh->rank + 1) / (uint64_t)sh->world;
+    Slice sl(ub.r, r0, r1);
+    DReads d;
+    a.check(apg_reads_upload(c, &sl.r, &d.d), "apg_reads_upload");
+    a.check(apg_sharded_unipaths(c, sh->comm, d.d, &p, &g, &st), "apg_sharded_unipaths");
+  } else {
+    a.check(apg_unipaths(c, &ub.r, &p, &g, &st), "apg_unipaths");
+  }
+  bool same = g.n_unipaths == file_g->n_unipaths;
+  for (uint64_t u = 0; same && u < g.n_unipaths; ++u) same = g.len[u] == file_g->len[u];
+  const uint64_t nb = g.n_unipaths ? g.ub_off[g.n_unipaths] : 0;
+  same = same && nb == (file_g->n_unipaths ? file_g->ub_off[file_g->n_unipaths] : 0) &&
+         (nb == 0 || std::memcmp(g.unibases, file_g->unibases, nb) == 0);
+  apg_unipath_graph_free(&g);
+  if (!same) a.fail(head + ": the unipaths rebuilt from the unibases differ from the .unipaths file");
+}
+
+// UnipathLocs: placements of the reads HEAD_IN on the unipaths READS.*.k<K>
+// (apg_unipath_locs: a location per change of (unipath, start) along the
+// read, RC=1 with rc mirrors, SORTED=1 stably by (unipath, start)) ->
+// <HEAD_IN>.unilocs.k<K>.
+int unipath_locs(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string head = dir + "/" + a.get("READS", "all_reads");
+  const std::string in = dir + "/" + a.get("HEAD_IN", "frag_reads_corr");
+  const int K = (int)a.num("K", 96);
+  const bool rc = a.num("RC", 1) != 0, sorted = a.num("SORTED", 1) != 0;
+  Shard sh(a);
+  a.finish();
+  const uint32_t flags = (rc ? APG_ULOCS_RC : 0u) | (sorted ? APG_ULOCS_SORTED : 0u);
+  Ctx ctx(a);
+  if (sh.sharded()) sh.connect(a, ctx.c);
+  apg_unipath_graph fg{};
+  rebuild_graph(a, ctx.c, head, K, &sh, &fg);
+  apg_unipath_graph_free(&fg);
+  Reads rd;
+  load_reads(a, in, false, &rd);
+  const std::string out = in + ".unilocs.k" + std::to_string(K);
+  apg_uloc_stats st;
+  std::vector<apg_aln_pair> all;
+  if (sh.sharded()) {
+    uint64_t r0, r1;
+    sh.range(rd.r.n_reads, &r0, &r1);
+    Slice sl(rd.r, r0, r1);
+    DReads d;
+    a.check(apg_reads_upload(ctx.c, &sl.r, &d.d), "apg_reads_upload");
+    const apg_aln_pair* dl = nullptr;
+    uint64_t n = 0;
+    a.check(apg_sharded_unipath_locs(ctx.c, sh.comm, d.d, flags, &dl, &n, &st), "apg_sharded_unipath_locs");
+    std::vector<apg_aln_pair> mine(n);
+    if (n) a.check(apg_device_to_host(ctx.c, mine.data(), dl, n * sizeof(apg_aln_pair)), "copying placements");
+    for (auto& l : mine) l.s_id += (uint32_t)r0;  // this rank's reads start at read r0
+    const std::string pp = part_name(in, sh.rank, sh.world) + ".unilocs.k" + std::to_string(K);
+    if (sh.rank != 0) {
+      a.check(apg_ulocs_write(pp.c_str(), K, r1 - r0, mine.data(), n), "writing placement part");
+      sh.barrier(a);
+      sh.barrier(a);
+      return 0;
+    }
+    sh.barrier(a);
+    all = std::move(mine);
+    for (int r = 1; r < sh.world; ++r) {
+      const std::string h = part_name(in, r, sh.world) + ".unilocs.k" + std::to_string(K);
+      int k = 0;
+      uint64_t nr = 0, np = 0;
+      apg_aln_pair* pl = nullptr;
+      a.check(apg_ulocs_read(h.c_str(), &k, &nr, &pl, &np), "reading placement part");
+      all.insert(all.end(), pl, pl + np);
+      apg_free(pl);
+      std::remove(h.c_str());
+    }
+    sh.barrier(a);
+    // ranks hold consecutive reads: the stable (unipath, start) order of the
+    // union is the stable sort of the rank-ordered concatenation
+    if (sorted)
+      std::stable_sort(all.begin(), all.end(), [](const apg_aln_pair& x, const apg_aln_pair& y) {
+        return x.t_id != y.t_id ? x.t_id < y.t_id : x.offset < y.offset;
+      });
+  } else {
+    apg_aln_pair* l = nullptr;
+    uint64_t n = 0;
+    a.check(apg_unipath_locs(ctx.c, &rd.r, flags, &l, &n, &st), "apg_unipath_locs");
+    all.assign(l, l + n);
+    apg_free(l);
+  }
+  a.check(apg_ulocs_write(out.c_str(), K, rd.r.n_reads, all.data(), all.size()), "writing .unilocs");
+  std::printf("%s: %llu reads, %llu placed, %llu locations, %llu K-mers off the graph -> %s\n", a.module.c_str(),
+              (unsigned long long)st.n_reads, (unsigned long long)st.n_placed, (unsigned long long)all.size(),
+              (unsigned long long)st.n_missing, out.c_str());
+  return 0;
+}
+
+// UnipathCoverage: placements per unipath, placements per K-mer and the
+// copy-number estimate (apg_unipath_coverage) of the placements
+// <HEAD_IN>.unilocs.k<K> on the unipaths READS.*.k<K> ->
+// <READS>.unipath_cov.k<K>.
+int unipath_coverage(Args& a) {
+  const std::string dir = a.run_dir();
+  const std::string head = dir + "/" + a.get("READS", "all_reads");
+  const std::string in = dir + "/" + a.get("HEAD_IN", "frag_reads_corr");
+  const int K = (int)a.num("K", 96);
+  apg_ucov_params p;
+  apg_ucov_defaults(&p);
+  p.min_len = (uint64_t)a.num("MIN_LEN", (long)p.min_len);
+  a.finish();
+  const std::string lf = in + ".unilocs.k" + std::to_string(K);
+  if (!exists(lf)) a.fail("missing input " + lf + " (run UnipathLocs first)");
+  int k = 0;
+  uint64_t nr = 0, n = 0;
+  apg_aln_pair* locs = nullptr;
+  a.check(apg_ulocs_read(lf.c_str(), &k, &nr, &locs, &n), "reading .unilocs");
+  struct Fr {
+    void* p;
+    ~Fr() { apg_free(p); }
+  } fr{locs};
+  if (k != K) a.fail(lf + " was placed at K=" + std::to_string(k));
+  Ctx ctx(a);
+  apg_unipath_graph fg{};
+  rebuild_graph(a, ctx.c, head, K, nullptr, &fg);
+  const uint64_t U = fg.n_unipaths;
+  apg_unipath_graph_free(&fg);
+  std::vector<uint64_t> cnt(U + 1);
+  std::vector<double> cov(U + 1);
+  std::vector<uint32_t> cn(U + 1);
+  apg_ucov_stats st;
+  a.check(apg_unipath_coverage(ctx.c, locs, n, &p, cnt.data(), cov.data(), cn.data(), &st), "apg_unipath_coverage");
+  const std::string out = head + ".unipath_cov.k" + std::to_string(K);
+  a.check(apg_ucov_write(out.c_str(), K, st.c0, U, cnt.data(), cov.data(), cn.data()), "writing .unipath_cov");
+  std::printf("%s: %llu placements on %llu unipaths, genome-wide %.4f placements per K-mer over %llu long unipaths "
+              "-> %s\n",
+              a.module.c_str(), (unsigned long long)n, (unsigned long long)U, st.c0, (unsigned long long)st.n_long,
               out.c_str());
   return 0;
 }
@@ -466,8 +803,9 @@ int main(int argc, char** argv) {
   int first = 1;
   if (a.module == "apg_modules") {  // apg_modules <Module> KEY=VALUE ...
     if (argc < 2) {
-      std::fprintf(stderr, "usage: apg_modules <KmerSpectrum|PreCorrect|FindErrors|ErrorCorrectJump|CommonPather|Unipather|MakeRcDb> "
-                           "KEY=VALUE ...\n");
+      std::fprintf(stderr,
+                   "usage: apg_modules <KmerSpectrum|PreCorrect|FindErrors|FillFragments|ErrorCorrectJump|"
+                   "MergeReadSets|CommonPather|Unipather|MakeRcDb|UnipathLocs|UnipathCoverage> KEY=VALUE ...\n");
       return 1;
     }
     a.module = argv[1];
@@ -485,5 +823,9 @@ int main(int argc, char** argv) {
   if (a.module == "Unipather") return unipaths(a, false);
   if (a.module == "MakeRcDb") return make_rc_db(a);
   if (a.module == "ErrorCorrectJump") return error_correct_jump(a);
+  if (a.module == "FillFragments") return fill_fragments(a);
+  if (a.module == "MergeReadSets") return merge_read_sets(a);
+  if (a.module == "UnipathLocs") return unipath_locs(a);
+  if (a.module == "UnipathCoverage") return unipath_coverage(a);
   a.fail("unknown module");
 }
