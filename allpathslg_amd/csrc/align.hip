@@ -1176,10 +1176,14 @@ int apg_sharded_consensus(apg_ctx* ctx, apg_comm* comm, const apg_dreads* R, con
   APG_REQUIRE(T->n_bases == 0 || (d_bases && d_quals), "apg_sharded_consensus: NULL outputs");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const uint64_t NT = T->n_bases;
-  // every rank must hold the same targets: the planes are summed column by column
-  uint64_t shape[2] = {NT, T->n_reads}, mx[2] = {NT, T->n_reads};
-  APG_TRY(c->allreduce_u64(mx, 2, APG_COMM_MAX));
-  APG_REQUIRE(mx[0] == shape[0] && mx[1] == shape[1], "apg_sharded_consensus: ranks hold different target sets");
+  // every rank must hold the same targets: the planes are summed column by
+  // column.  Maxima of the shape and of its complement (= ~minima), so every
+  // rank sees a mismatch and all fail here together, before the vote loop's
+  // collectives (a rank failing alone would leave the others waiting there).
+  uint64_t mx[4] = {NT, T->n_reads, ~NT, ~T->n_reads};
+  APG_TRY(c->allreduce_u64(mx, 4, APG_COMM_MAX));
+  APG_REQUIRE(mx[0] == NT && mx[1] == T->n_reads && ~mx[2] == NT && ~mx[3] == T->n_reads,
+              "apg_sharded_consensus: ranks hold different target sets");
   static const uint64_t kChunk = getenv("APG_CONS_CHUNK") ? strtoull(getenv("APG_CONS_CHUNK"), nullptr, 10) : (1ull << 28);
   const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(NT, kChunk));
   uint32_t* votes = nullptr;

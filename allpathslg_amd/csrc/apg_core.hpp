@@ -162,6 +162,13 @@ struct apg_ctx {
     uint64_t n = 0;  // records
     uint64_t n_nodes = 0;  // nodes of the last apg_urec_nodes ("usk_nodes")
     bool desc = false;  // the count pass kept record descriptors ("usk_desc*")
+    // what the last apg_urec_nodes' buckets built beside the nodes, for the
+    // sharded graph over the exported (same-order) node array: each node's
+    // bucket-resolved links ("usk_lsucc", uint2 per node; null: none) and the
+    // node index ("u_idx" of idx_T slots; null: none)
+    const void* lsucc = nullptr;
+    unsigned long long* idx = nullptr;
+    uint64_t idx_T = 0;
   } urstate;
 
   // Super-k-mer plan of the last sk_count (reused by sk_scatter).
@@ -206,6 +213,16 @@ struct apg_ctx {
   uint64_t pc_n = 0;
   int pc_K = 0;
   bool pc_list_valid = false;
+  // pc_self: pc_list was counted (min_solid pc_min_solid) from the very reads
+  // that pass corrected, whose generation after the pass is pc_self_gen.  A
+  // pass leaves its reads' solid set unchanged (a suspect's covering K-mers
+  // are all weak, an accepted alternative's all solid, and accepted
+  // corrections lie >= K apart: removed instances are of weak K-mers, added
+  // ones of solid K-mers), so pc_list IS the corrected reads' solid set —
+  // ErrorCorrectJump's fragment count reuses it (ecj_run).
+  bool pc_self = false;
+  uint64_t pc_self_gen = 0;
+  uint32_t pc_min_solid = 0;
   // Per-read clean flags of that pass (1: every K-mer solid after correction,
   // 0: not, 2: not derived), valid for the read set while its gen is clean_gen.
   const uint8_t* pc_clean = nullptr;

@@ -660,10 +660,17 @@ struct TcpComm : Comm {
     return allreduce_u64(&x, 1, APG_COMM_SUM);
   }
 
-  // Device array summed in place: staged through pinned memory, reduced as
-  // a reduce-scatter (rank q sums slice q of every rank's array) followed by
-  // an all-gather of the summed slices, so no rank holds world copies.
+  // Device array summed in place, in pieces of <= kDevPiece elements so the
+  // pinned staging stays bounded (a 2^30-element consensus plane would pin
+  // 8 GiB per rank): each piece staged through pinned memory, reduced as a
+  // reduce-scatter (rank q sums slice q of every rank's piece) followed by an
+  // all-gather of the summed slices, so no rank holds world copies.
+  static constexpr uint64_t kDevPiece = 1ull << 25;  // 128 MiB of u32
   int allreduce_dev_u32(uint32_t* d, uint64_t n) override {
+    for (uint64_t o = 0; o < n; o += kDevPiece) APG_TRY(allreduce_dev_piece(d + o, std::min(kDevPiece, n - o)));
+    return APG_OK;
+  }
+  int allreduce_dev_piece(uint32_t* d, uint64_t n) {
     if (!n) return APG_OK;
     APG_REQUIRE(ctx, "apg_comm(tcp): device allreduce needs a context");
     std::vector<uint64_t> lo(world + 1);

@@ -42,8 +42,11 @@ Comm* comm_of(apg_comm* c);
 // Sharded unipath compaction (unipath.hip / ushard_graph.inc): this rank's
 // distinct nodes (KRec[n_nodes], its minimizer shard) -> the global graph on
 // every rank + KmerPaths of this rank's reads.
+// lsucc / idx (may be null): the node buckets' links and node index over
+// d_nodes (ctx->urstate after apg_urec_nodes + apg_urec_export).
 int u_sharded_graph(apg_ctx* ctx, Comm* c, const void* d_nodes, uint64_t n_nodes, const apg_dreads* reads,
-                    const apg_unipath_params& p, apg_unipath_graph* out, apg_unipath_stats* st);
+                    const apg_unipath_params& p, apg_unipath_graph* out, apg_unipath_stats* st,
+                    const void* lsucc = nullptr, unsigned long long* idx = nullptr, uint64_t idx_T = 0);
 
 // UnipathLocs of this rank's reads on the context's last sharded unipath
 // build (unipath.hip / ushard_graph.inc); stats summed over the ranks.

@@ -45,20 +45,27 @@ struct SkResult {
 int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
              std::vector<uint64_t>* kmer_counts, uint32_t split = 0);
 int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
-// sk_scatter + pos[i] = global base position of record i's first K-mer
-int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos);
-// solid set of received records + per-record weak masks (receive order)
+// sk_scatter + pos[i] = global base position of record i's first K-mer;
+// split > 0: records cut into pieces of <= split K-mers (sk_count with the
+// same split first), so that every record fits the packed form (<= 32 bases)
+int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos, uint32_t split = 0);
+// the piece length that keeps a K-mer's records within the packed form
+uint32_t sk_pack_split(int K);
+// solid set of received records + per-record weak masks (receive order).
+// split_recs: the records were cut by sk_pack_split (<= 32 bases), so the
+// owner's partition levels may carry them packed (16 bytes, the receive
+// index in the position field) instead of as 24-byte records.
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
                         int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res,
                         int up_K = 0, uint64_t* up_hist = nullptr, size_t up_hist_len = 0,
-                        SkResult* up_res = nullptr);
+                        SkResult* up_res = nullptr, bool split_recs = false);
 bool sk_can_fuse_up(int K);
 // Owner side of the sharded fused spectrum + PreCorrect (precorrect.hip): as
 // apg_shard_solid_weak, plus this shard's K+1 spectrum (up_hist) from the
-// same records; completes before it returns.
+// same records (on the side stream: side_join before reading up_hist).
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
-                           SkResult* up_res);
+                           SkResult* up_res, bool split_recs = false);
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
                    uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
                    SkResult* res);

@@ -188,8 +188,12 @@ __device__ __forceinline__ uint64_t rkey_w0(uint64_t w0) {
 template <typename RI, typename RO = RI>
 __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_part_scatter(
     const RI* __restrict__ rec, const Chunk* __restrict__ ch, int shift, uint32_t ndig,
-    const uint32_t* __restrict__ pre, const uint64_t* __restrict__ child, RO* __restrict__ out) {
-  static_assert(std::is_same<RI, RO>::value || (sizeof(RI) == 16 && sizeof(RO) == 24), "RI -> RO: same, or 16 -> 24");
+    const uint32_t* __restrict__ pre, const uint64_t* __restrict__ child, RO* __restrict__ out, int kshift, bool wide) {
+  static_assert(std::is_same<RI, RO>::value || (sizeof(RI) == 16 && sizeof(RO) == 24) ||
+                    (std::is_same<RI, SK16>::value && std::is_same<RO, SKP>::value),
+                "RI -> RO: same, 16 -> 24, or SK16 -> SKP");
+  constexpr bool kPack = std::is_same<RI, SK16>::value && std::is_same<RO, SKP>::value;
+  shift += kPack ? kshift : 0;  // the packed key's digits sit kshift bits higher
   using R = RO;
   constexpr int kPartItems = PartGeom<R>::items;
   constexpr int kTile = PartGeom<R>::tile;
@@ -222,7 +226,9 @@ __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_
       const uint32_t idx = t + i * kPartThreads + tid;
       if (idx < c.len) {
         if constexpr (std::is_same<RI, SKP>::value && !std::is_same<RO, SKP>::value) {
-          skp_unpack(base[(uint64_t)idx * 2], base[(uint64_t)idx * 2 + 1], v[i]);
+          skp_unpack(base[(uint64_t)idx * 2], base[(uint64_t)idx * 2 + 1], v[i], wide);
+        } else if constexpr (kPack) {
+          skp_pack(base[(uint64_t)idx * 2], base[(uint64_t)idx * 2 + 1], c.start + idx, kshift, v[i]);
         } else {
 #pragma unroll
           for (uint32_t q = 0; q < kQi; ++q) v[i][q] = base[(uint64_t)idx * kQi + q];
@@ -286,7 +292,8 @@ __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_
 // host_child, copies them to the host.
 template <typename R, typename RO>
 int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
-               uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag) {
+               uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag, int kshift,
+               bool wide) {
   constexpr int kTile = PartGeom<RO>::tile;
   const uint32_t ndig = 1u << bits;
   const uint64_t np = parents.size();
@@ -336,7 +343,7 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vecto
   APG_CHECK_HIP(hipGetLastError());
   kbegin(ctx, (std::string(tag) + "_part_scatter").c_str(), n * (sizeof(R) + sizeof(RO)) + nrow * ndig * 4);
   k_part_scatter<R, RO><<<(uint32_t)nrow, kPartThreads, 0, ctx->stream>>>(src, d_chunks, shift, ndig, pre, d_child,
-                                                                          dst);
+                                                                          dst, kshift, wide);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   if (host_child) {
@@ -349,18 +356,20 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vecto
 
 
 template int part_level<uint64_t, uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&,
-                                            int, int, uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                            int, int, uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 template int part_level<SK16, SK16>(apg_ctx*, const SK16*, SK16*, const std::vector<std::vector<Seg>>&, int, int,
-                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 template int part_level<SK16, SK24>(apg_ctx*, const SK16*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
-                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 template int part_level<SKP, SKP>(apg_ctx*, const SKP*, SKP*, const std::vector<std::vector<Seg>>&, int, int,
-                                  uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                  uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
+template int part_level<SK16, SKP>(apg_ctx*, const SK16*, SKP*, const std::vector<std::vector<Seg>>&, int, int,
+                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 template int part_level<SKP, SK24>(apg_ctx*, const SKP*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
-                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 template int part_level<SK24, SK24>(apg_ctx*, const SK24*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
-                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 template int part_level<SK48, SK48>(apg_ctx*, const SK48*, SK48*, const std::vector<std::vector<Seg>>&, int, int,
-                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*);
+                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 
 }  // namespace apg

@@ -46,11 +46,24 @@ struct __attribute__((aligned(16))) SKP {
 };
 constexpr int kSkpKeyBits = 22;
 
-__host__ __device__ inline void skp_unpack(uint64_t w0, uint64_t w1, uint64_t* o) {
+// An SK16 of <= 32 bases (n <= 15 K-mers) + a 32-bit position -> SKP; the
+// packed key = bits [kshift, kshift + 22) from the top of the 32-bit key.
+__host__ __device__ inline void skp_pack(uint64_t w0, uint64_t w1, uint64_t pos, int kshift, uint64_t* o) {
+  const uint64_t key = (((w0 & 0xffffffffull) << kshift) & 0xffffffffull) >> (32 - kSkpKeyBits);
+  const uint64_t n = (w0 >> 32) & 15, fl = (w0 >> 40) & 63;
+  o[0] = (key << (64 - kSkpKeyBits)) | ((pos & 0xffffffffull) << 10) | (n << 6) | fl;
+  o[1] = (w0 >> 48) | (w1 << 16);
+}
+
+// wide: the record holds <= 31 bases and w1's top two bits carry position
+// bits 32..33 (read sets of 2^32 .. 2^34 bases: the scatter cuts records to
+// <= 32 - K + 1 K-mers for them).
+__host__ __device__ inline void skp_unpack(uint64_t w0, uint64_t w1, uint64_t* o, bool wide = false) {
   const uint64_t key32 = (w0 >> (64 - kSkpKeyBits)) << (32 - kSkpKeyBits);
-  o[0] = key32 | (((w0 >> 6) & 15) << 32) | ((w0 & 63) << 40) | ((w1 & 0xffffull) << 48);
-  o[1] = w1 >> 16;
-  o[2] = (w0 >> 10) & 0xffffffffull;
+  const uint64_t b = wide ? w1 & ((1ull << 62) - 1) : w1;
+  o[0] = key32 | (((w0 >> 6) & 15) << 32) | ((w0 & 63) << 40) | ((b & 0xffffull) << 48);
+  o[1] = b >> 16;
+  o[2] = ((w0 >> 10) & 0xffffffffull) | (wide ? (w1 >> 62) << 32 : 0);
 }
 
 // 48-byte super-k-mer record of the K <= 96 unipath node builder
@@ -86,10 +99,14 @@ int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out
 // the children's starts to d_child[0 .. nparents*ndig] (last = n) and, if
 // host_child, copies them to the host.  Order inside a child is unspecified.
 // RO: the output record type — R, SK24 from SK16 (the input index as pos),
-// or SK24 from SKP (unpacked).
+// SK24 from SKP (unpacked), or SKP from SK16 (<= 32 bases; the input index as
+// pos, the key's bits below its top `kshift` bits as the packed key, so the
+// packed record's digits sit kshift bits higher).
+// wide: SKP records in the 34-bit-position form (skp_unpack).
 template <typename R, typename RO = R>
 int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
-               uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag);
+               uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag, int kshift = 0,
+               bool wide = false);
 
 // Stable LSD radix sort of (key, val) pairs by key over the key's significant
 // bits (pathsdb.hip): ping-pongs between (k, v) and (k2, v2); *in2 tells

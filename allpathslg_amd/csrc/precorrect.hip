@@ -870,8 +870,13 @@ __global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ b
 // 1 every K-mer solid after correction, 0 not, 2 not derived) for
 // FillFragments.
 static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const uint64_t* list, uint64_t n_solid,
-                        apg_pc_stats* st, const unsigned long long* weak = nullptr) {
+                        apg_pc_stats* st, const unsigned long long* weak = nullptr, bool self_count = false) {
   ctx->clean_valid = false;
+  // the previous pass's extension table is this very list's (the jump reads'
+  // pass of ErrorCorrectJump against the fragments' reused solid set)
+  const bool ext_reuse = ctx->pc_ext_valid && ctx->pc_list_valid && ctx->pc_list == list && ctx->pc_n == n_solid &&
+                         ctx->pc_K == p.K && !weak;
+  ctx->pc_self = false;
   uint8_t* clean = nullptr;
   if (weak) APG_TRY(workspace_t(ctx, "pc_clean", std::max<uint64_t>(dr->n_reads, 1), &clean));
   unsigned long long* dcnt = nullptr;
@@ -933,7 +938,9 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     ext_done = nullptr;
     return APG_OK;
   };
-  if (ext && !weak) {
+  if (ext && !weak && ext_reuse) {
+    et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
+  } else if (ext && !weak) {
     APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
   } else if (ext) {
     if (!ext_done) APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
@@ -1091,6 +1098,9 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
        (unsigned long long)n_solid, h[0], h[1], h[2], h[3]);
   static std::atomic<uint64_t> g_edit{1ull << 62};
   dr->gen = g_edit.fetch_add(1);  // bases changed: invalidate per-read-set plans
+  ctx->pc_self = self_count;
+  ctx->pc_self_gen = dr->gen;
+  ctx->pc_min_solid = p.min_solid;
   if (clean) {
     ctx->pc_clean = clean;
     ctx->clean_gen = dr->gen;
@@ -1111,13 +1121,13 @@ static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p,
     ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
     // the fused K+1 pass may still run on the side stream: joined here, after
     // the correction kernels it overlaps
-    const int rc = correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak);
+    const int rc = correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak, true);
     const int rj = side_join(ctx);
     return rc != APG_OK ? rc : rj;
   }
   APG_TRY(sk_spectrum(ctx, dr, p.K, true, p.min_solid, nullptr, 0, &sr));
   ctx->solid_valid = false;
-  return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st);
+  return correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, nullptr, true);
 }
 
 static int check_pc(const apg_pc_params& p) {
@@ -1220,10 +1230,22 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   p.min_solid = e.min_solid;
   p.max_q_suspect = e.max_q_suspect;
   p.n_cycles = 1;
-  // solid set of the fragment reads
+  // solid set of the fragment reads: when they are the output of this
+  // context's last counting correction pass (same K, same min_solid), that
+  // pass's list is their solid set exactly (apg_core.hpp pc_self: a pass
+  // leaves the solid set unchanged) — C3's recount of the 40 M corrected
+  // fragment reads is skipped; else counted here
   SkResult sr;
-  APG_TRY(sk_spectrum(ctx, fr, e.K, true, e.min_solid, nullptr, 0, &sr));
-  ctx->solid_valid = false;  // "pc_solid" now holds the fragments' list
+  if (ctx->pc_list_valid && ctx->pc_self && ctx->pc_self_gen == fr->gen && ctx->pc_K == e.K &&
+      ctx->pc_min_solid == e.min_solid) {
+    sr.solid = const_cast<uint64_t*>(ctx->pc_list);
+    sr.n_solid = ctx->pc_n;
+    vlog(ctx, "error_correct_jump: the fragments' solid set from their correction pass (%llu K-mers)",
+         (unsigned long long)sr.n_solid);
+  } else {
+    APG_TRY(sk_spectrum(ctx, fr, e.K, true, e.min_solid, nullptr, 0, &sr));
+    ctx->solid_valid = false;  // "pc_solid" now holds the fragments' list
+  }
   // one correction pass of the jump reads against it
   std::memset(st, 0, sizeof *st);
   APG_TRY(correct_pass(ctx, jr, p, sr.solid, sr.n_solid, &st->pc));
@@ -1358,6 +1380,7 @@ int apg_spectrum_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, int K_spec, uint64
     kstats->n_distinct = ur.n_distinct;
     kstats->n_buckets = ur.nbuckets;
     kstats->n_overflow = ur.n_overflow_buckets;
+    kstats->n_redo = ur.n_redo_buckets;
   }
   if (pstats) *pstats = st;
   return APG_OK;
@@ -1398,7 +1421,7 @@ int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_
 namespace apg {
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
-                           SkResult* up_res) {
+                           SkResult* up_res, bool split_recs) {
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid_weak: NULL argument");
   APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
@@ -1416,8 +1439,11 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   APG_TRY(err);
   SkResult sr;
   APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr,
-                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res));
-  APG_TRY(side_join(ctx));  // the K+1 pass (side stream) completes here
+                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res, split_recs));
+  // The K+1 pass (side stream, kicked at the correction's stage as on one
+  // GPU) reads only this count's record buffers: the caller's mask return,
+  // solid-set gather and correction run beside it, and the caller joins it
+  // (side_join) before it reads up_hist / up_res.
   APG_TRY(sync(ctx));
   ctx->n_solid = sr.n_solid;
   ctx->solid_valid = true;

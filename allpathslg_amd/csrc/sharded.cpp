@@ -151,11 +151,21 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
   APG_REQUIRE(p.n_cycles >= 1, "apg_sharded_precorrect: n_cycles must be >= 1");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   const bool weak = K >= 9 && K <= 29;  // the weak-mask return (apg_shard_solid_weak)
+  SkResult up_res;
+  bool up_pending = false;
   apg_pc_stats tot;
   std::memset(&tot, 0, sizeof tot);
+  // weak mode: records cut to <= 32 bases (sk_pack_split), so the owner's
+  // partition levels carry them packed (16 bytes with the receive index)
+  const uint32_t split = weak ? sk_pack_split(K) : 0u;
   for (uint32_t cyc = 0; cyc < p.n_cycles; ++cyc) {
     std::vector<uint64_t> counts((size_t)P * B);
-    APG_TRY(apg_shard_count(ctx, reads, K, P, counts.data()));
+    if (weak) {
+      std::vector<uint64_t> kc;
+      APG_TRY(sk_count(ctx, reads, K, P, &counts, &kc, split));
+    } else {
+      APG_TRY(apg_shard_count(ctx, reads, K, P, counts.data()));
+    }
     void* pos = nullptr;
     Exchanged x;
     uint64_t n_local = 0;
@@ -165,27 +175,21 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
                                [&](void* send) {
                                  const uint64_t n = total(seg_bytes(counts, P, B, 1));
                                  APG_TRY(workspace(ctx, "x_pos", std::max<uint64_t>(n * 8, 64), &pos));
-                                 return apg_shard_scatter_pos(ctx, reads, K, P, send, pos);
+                                 return sk_scatter_pos(ctx, reads, K, P, static_cast<SK16*>(send),
+                                                       static_cast<uint64_t*>(pos), split);
                                },
                                &x));
       void* rmask = nullptr;
       APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>(x.n_out * 4, 64), &rmask));
       if (up_hist && cyc == 0) {
-        SkResult ur;
+        // the K+1 pass runs on the side stream beside the mask return, the
+        // solid-set gather and the correction below; joined after them
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, up_hist,
-                                       up_hist_len, &ur));
-        APG_TRY(c->allreduce_u64(up_hist, up_hist_len, APG_COMM_SUM));
-        uint64_t v[4] = {ur.n_kmers, ur.n_distinct, ur.nbuckets, ur.n_overflow_buckets};
-        APG_TRY(c->allreduce_u64(v, 4, APG_COMM_SUM));
-        if (up_stats) {
-          std::memset(up_stats, 0, sizeof(*up_stats));
-          up_stats->n_kmers = v[0];
-          up_stats->n_distinct = v[1];
-          up_stats->n_buckets = v[2];
-          up_stats->n_overflow = v[3];
-        }
+                                       up_hist_len, &up_res, true));
+        up_pending = true;
       } else {
-        APG_TRY(apg_shard_solid_weak(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local));
+        APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, nullptr,
+                                       0, nullptr, true));
       }
       // masks travel back: the splits reversed, 4 bytes per record
       std::vector<uint64_t> mb_out(P), mb_in(P);
@@ -218,6 +222,22 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
     tot.n_ambiguous += st.n_ambiguous;
     tot.n_uncorrectable += st.n_uncorrectable;
     tot.n_solid = n_solid;
+    if (up_pending) {  // the first cycle's K+1 spectrum: side pass complete, summed over ranks
+      up_pending = false;
+      APG_TRY(side_join(ctx));
+      APG_TRY(c->allreduce_u64(up_hist, up_hist_len, APG_COMM_SUM));
+      uint64_t v[5] = {up_res.n_kmers, up_res.n_distinct, up_res.nbuckets, up_res.n_overflow_buckets,
+                       up_res.n_redo_buckets};
+      APG_TRY(c->allreduce_u64(v, 5, APG_COMM_SUM));
+      if (up_stats) {
+        std::memset(up_stats, 0, sizeof(*up_stats));
+        up_stats->n_kmers = v[0];
+        up_stats->n_distinct = v[1];
+        up_stats->n_buckets = v[2];
+        up_stats->n_overflow = v[3];
+        up_stats->n_redo = v[4];
+      }
+    }
   }
   uint64_t v[4] = {tot.n_suspect, tot.n_corrected, tot.n_ambiguous, tot.n_uncorrectable};
   APG_TRY(c->allreduce_u64(v, 4, APG_COMM_SUM));
@@ -326,7 +346,8 @@ int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
   std::memset(&st, 0, sizeof st);
   if (rec && !(p.flags & APG_UNIPATH_GATHER_NODES)) {
     // sharded compaction: local chains, fragment ends gathered and stitched
-    const int rc = u_sharded_graph(ctx, c, local, n_local, reads, p, out, &st);
+    const auto& us = ctx->urstate;  // the buckets' links and node index over the same node order
+    const int rc = u_sharded_graph(ctx, c, local, n_local, reads, p, out, &st, us.lsucc, us.idx, us.idx_T);
     if (rc != APG_OK) {
       if (out) apg_unipath_graph_free(out);
       return rc;

@@ -172,13 +172,19 @@ struct SplitOut {
 template <typename O> struct OutWantsPos { static constexpr bool value = false; };
 template <> struct OutWantsPos<SK24*> { static constexpr bool value = true; };
 template <> struct OutWantsPos<SplitOut> { static constexpr bool value = true; };
-template <> struct OutWantsPos<SKP*> { static constexpr bool value = true; };
+// packed partition records: 32-bit positions, or (wide) 34-bit positions
+// with records of <= 31 bases, position bits 32..33 in w1's top two bits
+struct SkpOut {
+  SKP* rec;
+  bool wide;
+};
+template <> struct OutWantsPos<SkpOut> { static constexpr bool value = true; };
 // SK16 layout (<= 32 bases) + position -> the packed partition record
-__device__ __forceinline__ void rec_put(SKP* out, uint64_t i, const SK16& x, uint64_t pos) {
-  const uint64_t b = (x.w0 >> 48) | (x.w1 << 16);  // bases 0..31
-  const uint64_t key = (x.w0 & 0xffffffffull) >> (32 - kSkpKeyBits);
-  const uint64_t n = (x.w0 >> 32) & 15, fl = (x.w0 >> 40) & 63;
-  out[i] = SKP{(key << (64 - kSkpKeyBits)) | (pos << 10) | (n << 6) | fl, b};
+__device__ __forceinline__ void rec_put(SkpOut out, uint64_t i, const SK16& x, uint64_t pos) {
+  uint64_t o[2];
+  skp_pack(x.w0, x.w1, pos, 0, o);
+  if (out.wide) o[1] = (o[1] & ((1ull << 62) - 1)) | ((pos >> 32) << 62);
+  out.rec[i] = SKP{o[0], o[1]};
 }
 __device__ __forceinline__ void rec_put(SplitOut out, uint64_t i, const SK16& x, uint64_t pos) {
   out.rec[i] = x;
@@ -1585,9 +1591,13 @@ int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out) {
   return sk_scatter_t<SK16>(ctx, dr, K, P, out);
 }
 
-int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos) {
-  return sk_scatter_o<SplitOut>(ctx, dr, K, P, SplitOut{out, pos}, sizeof(SK16) + 8);
+int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos, uint32_t split) {
+  return sk_scatter_o<SplitOut>(ctx, dr, K, P, SplitOut{out, pos}, sizeof(SK16) + 8, split);
 }
+
+// Records of <= 33 - K K-mers span <= 32 bases (the packed SKP's base word),
+// and <= 15 K-mers fit its 4-bit count.
+uint32_t sk_pack_split(int K) { return (uint32_t)std::min(33 - K, 15); }
 
 // Partition levels + bucket counting of records laid out as P source blocks,
 // each grouped by the kSkDigitBits digit below the shard bits:
@@ -1597,10 +1607,10 @@ int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, 
 // weak (SK24 records, solid mode only): per-base bitmap of weak K-mer
 // instances, zeroed by the caller.
 __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out);
-__global__ void k_skp_unpack(const SKP* __restrict__ in, uint64_t n, SK24* __restrict__ out) {
+__global__ void k_skp_unpack(const SKP* __restrict__ in, uint64_t n, SK24* __restrict__ out, bool wide) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t o[3];
-    skp_unpack(in[i].w0, in[i].w1, o);
+    skp_unpack(in[i].w0, in[i].w1, o, wide);
     out[i] = SK24{o[0], o[1], o[2]};
   }
 }
@@ -1724,7 +1734,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                             uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist,
                             size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr,
                             const SK16* src16 = nullptr, int up_K = 0, uint64_t* up_hist = nullptr,
-                            size_t up_hist_len = 0, SkResult* up_res = nullptr, const SKP* srcp = nullptr) {
+                            size_t up_hist_len = 0, SkResult* up_res = nullptr, const SKP* srcp = nullptr,
+                            bool split16 = false, bool wide = false) {
   const SkP p = make_skp(K);
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
@@ -1780,6 +1791,17 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   const R* cur = src;
   uint64_t nb = B1;
   int consumed = pbits + l1;
+  // The multi-GPU owner's records (SK16 + receive index) travel the levels
+  // packed (SKP, 16 bytes instead of 24) when the sender cut them to <= 32
+  // bases (split16), the receive index fits 32 bits and the bucket bits
+  // below the shard bits fit the packed key (22 bits): the first level packs,
+  // the middle ones move SKP, the last unpacks.  The packed key holds the
+  // minimizer key's bits below the shard bits, so its digits sit pbits
+  // higher than in the SK16 key (kshift).
+  const bool pack16 = std::is_same<R, SK24>::value && src16 && split16 && nlev >= 2 && n < (1ull << 32) &&
+                      bb <= kSkpKeyBits;
+  bool packed = srcp != nullptr;
+  const int kshift = pack16 ? pbits : 0;
   if constexpr (std::is_same<R, SK24>::value) {  // SK16 input: widened by the first level, or here
     if (src16 && nlev == 0 && n) {
       k_sk_index24<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(src16, n, spare);
@@ -1787,7 +1809,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       cur = spare;
     }
     if (srcp && nlev == 0 && n) {  // packed records and no level to unpack them
-      k_skp_unpack<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(srcp, n, bufA);
+      k_skp_unpack<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(srcp, n, bufA, wide);
       APG_CHECK_HIP(hipGetLastError());
       cur = bufA;
     }
@@ -1805,18 +1827,25 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     const bool last = lev + 1 == nlev;
     bool done = false;
     if constexpr (std::is_same<R, SK24>::value) {
-      if (src16 && lev == 0) {  // SK16 -> SK24 with the input index (the record's mask slot)
+      if (src16 && lev == 0 && pack16) {  // SK16 -> SKP with the input index (the record's mask slot)
+        dst = bufA != spare ? bufA : bufB;
+        APG_TRY((part_level<SK16, SKP>(ctx, src16, reinterpret_cast<SKP*>(dst), parents, 64 - consumed, bits, n, boff,
+                                       &hb, "s24", kshift)));
+        packed = true;
+        done = true;
+      } else if (src16 && lev == 0) {  // SK16 -> SK24 with the input index (the record's mask slot)
         dst = bufA != spare ? bufA : bufB;
         APG_TRY((part_level<SK16, SK24>(ctx, src16, dst, parents, 64 - consumed, bits, n, boff,
                                         last ? nullptr : &hb, "s24")));
         done = true;
-      } else if (srcp) {  // packed records through the levels, unpacked by the last
+      } else if (packed) {  // packed records through the levels, unpacked by the last
         const SKP* in = reinterpret_cast<const SKP*>(cur);
         if (last)
-          APG_TRY((part_level<SKP, SK24>(ctx, in, dst, parents, 64 - consumed, bits, n, boff, nullptr, "s24")));
+          APG_TRY((part_level<SKP, SK24>(ctx, in, dst, parents, 64 - consumed + kshift, bits, n, boff, nullptr, "s24",
+                                         0, wide)));
         else
-          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents, 64 - consumed, bits, n, boff,
-                                        &hb, "s24")));
+          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents, 64 - consumed + kshift, bits, n,
+                                        boff, &hb, "s24")));
         done = true;
       }
     }
@@ -2118,11 +2147,18 @@ int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid,
   const uint64_t words = dr->n_bases / 64 + 2;
   APG_CHECK_HIP(hipMemsetAsync(weak, 0, words * 8, ctx->stream));
   // Packed partition records (SKP, 16 bytes instead of 24 through the
-  // scatter and the partition levels): positions below 2^32, records split
-  // into pieces of <= 32 bases (APG_SK_PACK=0: SK24 throughout)
+  // scatter and the partition levels): positions below 2^32 with records
+  // split into pieces of <= 32 bases, or (wide) below 2^34 with pieces of
+  // <= 31 bases and two position bits in the base word — 40 M reads of
+  // 100 bp are 4.0 G bases, 50 M (C4 per GPU) 5.0 G, 80 M 8.0 G
+  // (APG_SK_PACK=0: SK24 throughout; APG_SK_PACK=wide: the wide form at any
+  // size, for tests)
   const char* pe = getenv("APG_SK_PACK");
-  const bool pack = !(pe && !strcmp(pe, "0")) && dr->n_bases < (1ull << 32);
-  const uint32_t split = pack ? (uint32_t)std::min(33 - K, 15) : 0u;
+  const bool force_wide = pe && !strcmp(pe, "wide");
+  const bool pack0 = !(pe && !strcmp(pe, "0")) && dr->n_bases < (1ull << 34);
+  const bool wide = pack0 && (force_wide || dr->n_bases >= (1ull << 32));
+  const bool pack = pack0 && (!wide || K <= 31);
+  const uint32_t split = !pack ? 0u : wide ? (uint32_t)std::min(32 - K, 15) : sk_pack_split(K);
   std::vector<uint64_t> rc, kc;
   APG_TRY(sk_count(ctx, dr, K, 1, &rc, &kc, split));
   uint64_t n = 0, nk = 0;
@@ -2131,12 +2167,14 @@ int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid,
   SK24* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
   if (pack)
-    APG_TRY(sk_scatter_o<SKP*>(ctx, dr, K, 1, reinterpret_cast<SKP*>(buf), sizeof(SKP), split));
+    APG_TRY(sk_scatter_o<SkpOut>(ctx, dr, K, 1, SkpOut{reinterpret_cast<SKP*>(buf), wide}, sizeof(SKP), split));
   else
     APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
+  vlog(ctx, "solid count: %s records (%llu bases)", !pack ? "24-byte" : wide ? "packed wide (34-bit position)" : "packed",
+       (unsigned long long)dr->n_bases);
   return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res, nullptr, nullptr,
                                 up ? K + 1 : 0, up_hist, up_hist_len, up_res,
-                                pack ? reinterpret_cast<const SKP*>(buf) : nullptr);
+                                pack ? reinterpret_cast<const SKP*>(buf) : nullptr, false, wide);
 }
 
 __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __restrict__ out) {
@@ -2153,7 +2191,7 @@ __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __re
 // bucket kernel's weak pass writes each mask with a plain store.
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
                         int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res, int up_K, uint64_t* up_hist,
-                        size_t up_hist_len, SkResult* up_res) {
+                        size_t up_hist_len, SkResult* up_res, bool split_recs) {
   APG_REQUIRE(K >= 9 && K <= 32, "sk_shard_solid_weak: K must be in [9, 32]");
   uint64_t n = 0;
   for (auto c : rec_counts) n += c;
@@ -2163,7 +2201,7 @@ int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64
   // the first partition level reads the SK16 records and writes them as SK24
   // with their receive index (no separate widening pass)
   return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, nullptr, res,
-                                wrec, recv, up_K, up_hist, up_hist_len, up_res);
+                                wrec, recv, up_K, up_hist, up_hist_len, up_res, nullptr, split_recs);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {

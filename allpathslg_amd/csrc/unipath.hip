@@ -3070,6 +3070,9 @@ int apg_urec_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   ctx->gstate.valid = false;  // "usk_nodes" is about to be rewritten
   ctx->urstate.n_nodes = 0;
+  ctx->urstate.lsucc = nullptr;
+  ctx->urstate.idx = nullptr;
+  ctx->urstate.idx_T = 0;
   const size_t nc = (size_t)n_shards << kUskDigitBits;
   std::vector<uint64_t> rc(recv_counts, recv_counts + nc);
   uint64_t n = 0;
@@ -3084,8 +3087,17 @@ int apg_urec_nodes(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts
   APG_TRY(d2h_u64(ctx, sum, &nk, 1));
   KRec* nodes = nullptr;
   uint64_t N = 0;
-  APG_TRY(usk_stage(ctx, recs, rc, nk, make_keyp(K), n_shards, &nodes, &N));
+  // the buckets also resolve the links inside themselves and build the node
+  // index as they append nodes (the single-GPU build's two savings): the
+  // sharded graph (ushard_graph.inc) then looks up only the successors in
+  // other buckets, locally or by a query to their owner
+  uint2* ls = nullptr;
+  PreIdx pidx;
+  APG_TRY(usk_stage(ctx, recs, rc, nk, make_keyp(K), n_shards, &nodes, &N, &ls, &pidx));
   ctx->urstate.n_nodes = N;
+  ctx->urstate.lsucc = ls;
+  ctx->urstate.idx = pidx.idx;
+  ctx->urstate.idx_T = pidx.idx ? pidx.T : 0;
   *n_nodes = N;
   return APG_OK;
 }

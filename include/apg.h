@@ -141,7 +141,8 @@ typedef struct apg_kstats {
   uint64_t n_distinct; /* distinct canonical k-mers */
   uint64_t n_buckets;  /* hash buckets used */
   uint64_t n_overflow; /* buckets sorted by the out-of-LDS fallback */
-  uint64_t max_bucket; /* largest bucket (records) */
+  uint64_t max_bucket; /* largest bucket (records); reported by the hash-table counter
+                          (apg_kmer_count*), 0 from the super-k-mer spectrum paths */
   uint64_t n_redo;     /* buckets the record-deduplicating counter (K >= 21) handed
                           back to the per-instance counter */
   uint64_t reserved[2];

@@ -34,7 +34,12 @@ KERNELS = [
     ("void apg::k_sk_replay<apg::SK24*>", "sk_scatter", "stream"),
     ("void apg::k_sk_scatter<apg::SKP*>", "sk_scatter", "stream"),
     ("void apg::k_sk_replay<apg::SKP*>", "sk_scatter", "stream"),
+    ("void apg::k_sk_scatter<apg::SkpOut>", "sk_scatter", "stream"),  # round 4: packed output with the wide form
+    ("void apg::k_sk_replay<apg::SkpOut>", "sk_scatter", "stream"),
+    ("void apg::k_sk_scatter<apg::SplitOut>", "sk_scatter", "stream"),  # multi-GPU: records + positions
+    ("void apg::k_sk_replay<apg::SplitOut>", "sk_scatter", "stream"),
     ("void apg::k_part_scatter<apg::SKP>", "s24_part_scatter", "stream"),  # packed levels (SKP -> SKP / SK24)
+    ("void apg::k_part_scatter<apg::SK16, apg::SKP>", "s24_part_scatter", "stream"),  # multi-GPU owner: packing level
     ("void apg::k_part_count<apg::SKP>", "s24_part_count", "stream"),
     ("void apg::k_part_scatter<apg::SK16>", "s_part_scatter", "stream"),
     ("void apg::k_part_scatter<apg::SK24>", "s24_part_scatter", "stream"),
@@ -43,7 +48,12 @@ KERNELS = [
     ("apg::k_fill(", "fill", "random"),
     ("apg::k_fill_write", "fill_write", "stream"),
     ("apg::k_pc_decide", "precorrect", "random"),
-    ("void apg::k_pc_candidates<true>", "pc_candidates", "stream"),
+    ("void apg::k_pc_candidates<true>", "pc_cand_write", "stream"),  # the bench's timed-region name
+    ("apg::k_pc_apply", "pc_apply", "stream"),
+    ("apg::k_fill_ext_insert", "solid_insert", "random"),
+    ("void apg::k_read_paths<false>", "u_read_paths_count", "random"),
+    ("void apg::k_read_paths<true>", "u_read_paths_write", "random"),
+    ("apg::k_unibases", "u_unibases", "random"),
     ("apg::k_usk_count", "usk_count", "stream"),
     ("apg::k_usk_scatter", "usk_scatter", "stream"),
     ("apg::k_usk_bucket", "usk_bucket", "stream"),

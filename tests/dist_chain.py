@@ -82,11 +82,12 @@ def chain(ctx, comm, reads, n_cycles, gather=False, placement=True):
                                             sharded_spectrum_precorrect, sharded_unipath_locs, sharded_unipaths)
 
     d = ctx.upload(reads)
+    kspec = int(os.environ.get("APG_TEST_KSPEC", "25"))  # != 25: the fused entry point's two-module fallback
     if os.environ.get("APG_TEST_FUSED_SHARDED") == "1":  # one exchange for the K=25 spectrum and the K=24 pass
-        hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24, n_cycles=n_cycles)
+        hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, kspec, K=24, n_cycles=n_cycles)
         progress(comm.rank, "spectrum + precorrect")
     else:
-        hist, st = sharded_spectrum(ctx, comm, d, 25)
+        hist, st = sharded_spectrum(ctx, comm, d, kspec)
         progress(comm.rank, "spectrum")
         pst = sharded_precorrect(ctx, comm, d, K=24, n_cycles=n_cycles)
         progress(comm.rank, "precorrect")
@@ -153,7 +154,7 @@ def run_world(cfg, world, n_cycles, gather=False, placement=True, timeout=300, e
     return [r[1] for r in res]
 
 
-def mono_chain(gpu_ctx, cfg, n_cycles, placement=True):
+def mono_chain(gpu_ctx, cfg, n_cycles, placement=True, kspec=25):
     """The single-GPU entry points on the union of the ranks' reads."""
     from allpathslg_amd import synth_genome, synth_reads
 
@@ -161,7 +162,7 @@ def mono_chain(gpu_ctx, cfg, n_cycles, placement=True):
     g = synth_genome(genome_len, seed)
     reads = synth_reads(g, pairs, seed=seed + 1)
     d = gpu_ctx.upload(reads)
-    hist, st = gpu_ctx.kmer_spectrum(d, 25)
+    hist, st = gpu_ctx.kmer_spectrum(d, kspec)
     _, pst = gpu_ctx.precorrect(d, K=24, n_cycles=n_cycles)
     fixed = gpu_ctx.download(d)
     filled, _, fst = gpu_ctx.fill_fragments(d, K=24, last_solid=True)

@@ -122,3 +122,26 @@ def test_fused_kplus1_record_sources(gpu_ctx, monkeypatch, env):
     monkeypatch.undo()
     _, fus_dd = both_ways(gpu_ctx, reads)
     assert_same(sep, fus_dd)
+
+
+@pytest.mark.parametrize("pack", ["wide", "0"])
+def test_solid_count_record_forms(gpu_ctx, monkeypatch, pack):
+    """The solid-set count's partition records: packed with 32-bit positions
+    (the default below 2^32 bases), packed wide (34-bit positions, records
+    cut to <= 31 bases: the form of read sets of 2^32 .. 2^34 bases, e.g. C4's
+    50 M reads per GPU; APG_SK_PACK=wide forces it) and unpacked 24-byte
+    records (APG_SK_PACK=0) give the same spectrum, solid set and corrections,
+    equal to the oracle's."""
+    g = synth_genome(1_000_000, 71, repeats={"tandem_frac": 0.02})
+    reads = synth_reads(g, 200_000, seed=72)
+    monkeypatch.setenv("APG_SK_PACK", pack)
+    sep, fus = both_ways(gpu_ctx, reads)
+    assert_same(sep, fus)
+    monkeypatch.undo()
+    _, dflt = both_ways(gpu_ctx, reads)
+    assert_same(dflt, fus)
+    assert np.array_equal(fus[0], oracle.kmer_spectrum(reads, 25))
+    exp, est = oracle.precorrect(reads, K=24, fast=True)
+    rf = fus[3]
+    assert np.array_equal(rf.packed[: int(rf.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(rf.quals, exp.quals)

@@ -190,3 +190,28 @@ def test_oracle_stages_against_golden():
     assert np.array_equal(res, z["aln_sw"]) and np.array_equal(blk, z["aln_sw_blocks"])
     b, q = oracle.consensus(S, T, pairs)
     assert np.array_equal(b, z["aln_cons_bases"]) and np.array_equal(q, z["aln_cons_quals"])
+
+
+@pytest.mark.parametrize("case", ["plain", "repeats", "low_q"])
+def test_precorrect_preserves_the_solid_set(case):
+    """The invariant ErrorCorrectJump's reuse of the fragments' solid set
+    rests on (apg_core.hpp pc_self): a PreCorrect pass leaves the reads'
+    solid set unchanged — a suspect's covering K-mers are all weak, an
+    accepted alternative's all solid and accepted corrections lie >= K apart,
+    so only weak K-mer instances are removed and only solid ones added."""
+    from allpathslg_amd import synth_genome, synth_reads
+
+    if case == "repeats":
+        g = synth_genome(300_000, 91, repeats={"tandem_frac": 0.03})
+        reads = synth_reads(g, 60_000, seed=92)
+    elif case == "low_q":
+        g = synth_genome(200_000, 93)
+        reads = synth_reads(g, 40_000, seed=94, err_lo=0.01, err_hi=0.05)
+    else:
+        g = synth_genome(200_000, 95)
+        reads = synth_reads(g, 40_000, seed=96)
+    s0 = np.sort(oracle.solid_hashes(reads, 24, 3))
+    for n_cycles in (1, 2):
+        fixed, st = oracle.precorrect(reads, K=24, n_cycles=n_cycles)
+        assert st["n_corrected"] > 1000
+        assert np.array_equal(np.sort(oracle.solid_hashes(fixed, 24, 3)), s0)
