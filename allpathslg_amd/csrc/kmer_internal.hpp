@@ -65,7 +65,7 @@ bool sk_can_fuse_up(int K);
 // same records (on the side stream: side_join before reading up_hist).
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
-                           SkResult* up_res, bool split_recs = false);
+                           SkResult* up_res, bool split_recs = false, uint64_t n_kmers = ~0ull);
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
                    uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
                    SkResult* res);

@@ -1421,7 +1421,7 @@ int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_
 namespace apg {
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
-                           SkResult* up_res, bool split_recs) {
+                           SkResult* up_res, bool split_recs, uint64_t n_kmers) {
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid_weak: NULL argument");
   APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
@@ -1435,7 +1435,9 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   APG_REQUIRE(n == 0 || (d_recv && d_mask), "apg_shard_solid_weak: d_recv or d_mask is NULL");
   const SK16* recs = static_cast<const SK16*>(d_recv);
   int err = APG_OK;
-  const uint64_t nk = sk_sum_kmers(ctx, recs, n, &err);
+  // the received K-mer instances: given by the caller (the senders' counts,
+  // exchanged beside the record counts), else summed over the records here
+  const uint64_t nk = n_kmers != ~0ull ? n_kmers : sk_sum_kmers(ctx, recs, n, &err);
   APG_TRY(err);
   SkResult sr;
   APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr,

@@ -159,10 +159,13 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
   // partition levels carry them packed (16 bytes with the receive index)
   const uint32_t split = weak ? sk_pack_split(K) : 0u;
   for (uint32_t cyc = 0; cyc < p.n_cycles; ++cyc) {
-    std::vector<uint64_t> counts((size_t)P * B);
+    std::vector<uint64_t> counts((size_t)P * B), kc;
+    uint64_t n_kmers_in = ~0ull;  // K-mer instances this rank receives (the owner count's sizing)
     if (weak) {
-      std::vector<uint64_t> kc;
       APG_TRY(sk_count(ctx, reads, K, P, &counts, &kc, split));
+      std::vector<uint64_t> kin((size_t)P * B);
+      APG_TRY(c->alltoall_u64(kc.data(), kin.data(), (uint64_t)B));
+      n_kmers_in = total(kin);
     } else {
       APG_TRY(apg_shard_count(ctx, reads, K, P, counts.data()));
     }
@@ -185,11 +188,11 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
         // the K+1 pass runs on the side stream beside the mask return, the
         // solid-set gather and the correction below; joined after them
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, up_hist,
-                                       up_hist_len, &up_res, true));
+                                       up_hist_len, &up_res, true, n_kmers_in));
         up_pending = true;
       } else {
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, nullptr,
-                                       0, nullptr, true));
+                                       0, nullptr, true, n_kmers_in));
       }
       // masks travel back: the splits reversed, 4 bytes per record
       std::vector<uint64_t> mb_out(P), mb_in(P);

@@ -73,6 +73,8 @@ struct SkP {
   // > 0: records of more than `split` K-mers leave as pieces of <= split
   // (the packed SKP form holds <= 32 bases); the count pass counts pieces
   uint32_t split = 0;
+  // SKP records in the 34-bit-position form (skp_unpack's `wide`)
+  bool wide = false;
 };
 __host__ __device__ inline uint32_t sk_pieces(uint32_t n, uint32_t split) {
   return split && n > split ? (n + split - 1) / split : 1u;
@@ -196,6 +198,42 @@ __device__ __forceinline__ void rec_put(SK24* out, uint64_t i, const SK16& x, ui
 }
 __device__ __forceinline__ SK16 rec_head(const SK16& r) { return r; }
 __device__ __forceinline__ SK16 rec_head(const SK24& r) { return SK16{r.w0, r.w1}; }
+
+// The bucket kernels' record accessors: SK16 / SK24 (the head is the 16-byte
+// super-k-mer form) and the packed SKP the partition levels carry, unpacked
+// in registers (no unpacking level: 16 bytes per record written by the last
+// level and read by the bucket kernels instead of 24).  RecPos: the record
+// carries a position (a base position, a receive index, or — a distinct
+// record of the fused K+1 pass — its multiplicity).
+template <typename R> struct RecPos { static constexpr bool value = false; };
+template <> struct RecPos<SK24> { static constexpr bool value = true; };
+template <> struct RecPos<SKP> { static constexpr bool value = true; };
+__device__ __forceinline__ SK16 rec_head(const SK16& r, const SkP&) { return r; }
+__device__ __forceinline__ SK16 rec_head(const SK24& r, const SkP&) { return SK16{r.w0, r.w1}; }
+__device__ __forceinline__ SK16 rec_head(const SKP& r, const SkP& p) {
+  uint64_t o[3];
+  skp_unpack(r.w0, r.w1, o, p.wide);
+  return SK16{o[0], o[1]};
+}
+__device__ __forceinline__ uint64_t rec_pos(const SK16&, const SkP&) { return 0; }
+__device__ __forceinline__ uint64_t rec_pos(const SK24& r, const SkP&) { return r.pos; }
+__device__ __forceinline__ uint64_t rec_pos(const SKP& r, const SkP& p) {
+  return ((r.w0 >> 10) & 0xffffffffull) | (p.wide ? (r.w1 >> 62) << 32 : 0ull);
+}
+__device__ __forceinline__ uint32_t rec_nk(const SK16& r) { return (uint32_t)(r.w0 >> 32) & 0xff; }
+__device__ __forceinline__ uint32_t rec_nk(const SK24& r) { return (uint32_t)(r.w0 >> 32) & 0xff; }
+__device__ __forceinline__ uint32_t rec_nk(const SKP& r) { return (uint32_t)(r.w0 >> 6) & 15; }
+// a distinct record of the solid-set count (dout: its multiplicity in the key
+// bits) as a record of type R whose position is that multiplicity
+template <typename R> __device__ __forceinline__ R rec_from_drec(const SK16& d);
+template <> __device__ __forceinline__ SK24 rec_from_drec<SK24>(const SK16& d) {
+  return SK24{d.w0, d.w1, d.w0 & 0xffffffffull};
+}
+template <> __device__ __forceinline__ SKP rec_from_drec<SKP>(const SK16& d) {
+  uint64_t o[2];
+  skp_pack(d.w0, d.w1, d.w0 & 0xffffffffull, 0, o);  // <= 32 bases: it came from a packed record
+  return SKP{o[0], o[1]};
+}
 
 // Each record goes straight to the next slot of its digit's run for this
 // block (omat, LDS cursor): the run's size is fixed by k_sk_count, the order
@@ -574,7 +612,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
                                                           const unsigned long long* __restrict__ bcount = nullptr,
                                                           const SK16* __restrict__ drec = nullptr,
                                                           const uint32_t* __restrict__ dcount = nullptr) {
-  constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
+  constexpr bool WEAK = SOLID && RecPos<R>::value;
   static_assert(!UP || !SOLID, "the K+1 count is a spectrum count");
   unsigned long long n_up = 0;  // UP: owned K+1-mer instances inserted by this thread
   // recorded slots: kSkWaveSlots per wave (NT = 512: each wave sees ~1/8 of a bucket)
@@ -626,11 +664,8 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
     nr_ = dc != ~0u ? dc : (uint32_t)(boff[b + 1] - off_);
   };
   auto ld = [&](const R* src_, uint64_t i) -> R {
-    if constexpr (UP && sizeof(R) == sizeof(SK24)) {
-      if (!src_) {
-        const SK16 d = drec[i];
-        return R{d.w0, d.w1, d.w0 & 0xffffffffull};
-      }
+    if constexpr (UP && RecPos<R>::value) {
+      if (!src_) return rec_from_drec<R>(drec[i]);
     }
     return src_[i];
   };
@@ -674,7 +709,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
       }
       uint32_t nk = 0;
       if (c0 + tid < nr) {
-        SK16 h = rec_head(pre);
+        SK16 h = rec_head(pre, p);
         nk = (uint32_t)(h.w0 >> 32) & 0xff;
         if constexpr (UP) {  // the boundary K+1-mers this record owns, decided once per record
           bool ol, orr;
@@ -682,7 +717,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
           (void)rec_kmer_up(h, (int)nk - 1, p, &orr);
           nk = nk - 1 + (ol ? 1u : 0u) + (orr ? 1u : 0u);
           uint4 str = rec_up_string(h, p, ol, orr);  // slot f at string base f
-          if constexpr (sizeof(R) == sizeof(SK24)) str.w = mult ? (uint32_t)pre.pos : 1u;
+          if constexpr (RecPos<R>::value) str.w = mult ? (uint32_t)rec_pos(pre, p) : 1u;
           *reinterpret_cast<uint4*>(&crec[tid]) = str;
         } else {
           crec[tid] = h;
@@ -764,8 +799,8 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
           uint64_t b = 0;
           if (c0 + tid < nr) {
             const R r = rec[off + c0 + tid];
-            nk = (uint32_t)(r.w0 >> 32) & 0xff;
-            b = r.pos;
+            nk = rec_nk(r);
+            b = rec_pos(r, p);
           }
           const uint32_t incl = wave_inclusive_scan<uint32_t>(nk);
           const uint32_t ex = ib + incl - nk;
@@ -795,9 +830,9 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
           uint64_t b = 0;
           if (c0 + tid < nr) {
             const R r = rec[off + c0 + tid];
-            crec[tid] = rec_head(r);
-            b = r.pos;
-            nk = (uint32_t)(r.w0 >> 32) & 0xff;
+            crec[tid] = rec_head(r, p);
+            b = rec_pos(r, p);
+            nk = rec_nk(r);
           }
           wmask[tid] = 0;
           const uint32_t incl = wave_inclusive_scan<uint32_t>(nk);
@@ -952,7 +987,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
                                                              SkP p, SkOut o, uint32_t* __restrict__ redo,
                                                              SK16* __restrict__ dout = nullptr,
                                                              uint32_t* __restrict__ dcount = nullptr) {
-  constexpr bool WEAK = SOLID && sizeof(R) == sizeof(SK24);
+  constexpr bool WEAK = SOLID && RecPos<R>::value;
   const uint64_t keep = dout ? ~0ull : ~kSkFlankMask;  // record identity: with the flanks for the K+1 count
   constexpr int NT = kDdThreads;
   constexpr unsigned long long EMPTY = ~0ull;
@@ -1072,8 +1107,8 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       SK16 hd{0, 0};
       uint64_t ps = 0;
       if (valid) {
-        hd = rec_head(pre);
-        if constexpr (WEAK) ps = pre.pos;
+        hd = rec_head(pre, p);
+        if constexpr (WEAK) ps = rec_pos(pre, p);
       }
       if (c0 + NT < nr) {
         if (c0 + NT + tid < nr) pre = rec[off + c0 + NT + tid];
@@ -1111,7 +1146,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       hand_back(false);
       continue;
     }
-    if constexpr (sizeof(R) == sizeof(SK24)) {
+    if constexpr (RecPos<R>::value) {
       if (dout) {  // the distinct records with their multiplicity, for the K+1 count
         const uint32_t nD = nr_sh;
         for (uint32_t j = tid; j < nD; j += NT) {
@@ -1276,7 +1311,7 @@ __global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __rest
   unsigned long long c = 0;
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x)
-    c += ((uint32_t)(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)].w0 >> 32) & 0xff) + (UP ? 1u : 0u);
+    c += rec_nk(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)]) + (UP ? 1u : 0u);
   wave_add(n_kmers, c);
 }
 
@@ -1323,7 +1358,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
   for (uint64_t k0 = (uint64_t)blockIdx.x * kBigChunk; k0 < tot; k0 += (uint64_t)gridDim.x * kBigChunk) {
     const uint64_t k = k0 + tid;
     if (k < tot) {
-      const SK16 r = rec_head(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)]);
+      const SK16 r = rec_head(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)], p);
       const uint32_t n = ((uint32_t)(r.w0 >> 32) & 0xff) + (UP ? 1u : 0u);
       for (uint32_t t = 0; t < n; ++t) {
         uint64_t c;
@@ -1368,16 +1403,17 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
 
 // Weak bits of the overflowed buckets' K-mer instances (counts from the
 // global table built by k_sk_big_insert).
-__global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __restrict__ boff,
+template <typename R>
+__global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                               const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
                               SkP p, const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
                               uint64_t gmask, uint32_t min_solid, unsigned long long* __restrict__ weak,
                               uint32_t* __restrict__ wrec) {
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x) {
-    const SK24 r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)];
-    const SK16 h = rec_head(r);
-    const uint32_t n = (uint32_t)(r.w0 >> 32) & 0xff;
+    const R r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)];
+    const SK16 h = rec_head(r, p);
+    const uint32_t n = rec_nk(r);
     uint32_t m = 0;
     for (uint32_t t = 0; t < n; ++t) {
       const uint64_t c = rec_kmer(h, t, p);
@@ -1386,9 +1422,9 @@ __global__ void k_sk_big_weak(const SK24* __restrict__ rec, const uint64_t* __re
       if (gcnt[s] < min_solid) m |= 1u << t;
     }
     if (wrec) {
-      if (m) wrec[r.pos] = m;
+      if (m) wrec[rec_pos(r, p)] = m;
     } else if (m) {  // the record's mask in one or two ORs, as k_sk_bucket
-      const uint64_t b = r.pos;
+      const uint64_t b = rec_pos(r, p);
       const uint32_t sh = (uint32_t)(b & 63);
       atomicOr(&weak[b >> 6], (unsigned long long)m << sh);
       if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
@@ -1639,29 +1675,33 @@ static int sk_up_alloc(apg_ctx* ctx, uint64_t nb, size_t hist_len, SkOut* u) {
 // side-stream form leaves the rest of each CU to the main stream's kernels);
 // sk_up_finish waits for it, runs the overflowed buckets and reads the
 // results back.
-static int sk_up_launch(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
-                        const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec,
+template <typename RB>
+static int sk_up_launch(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                        bool wide, const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec,
                         double grid_frac = 1.0) {
-  const SkP p = make_skp(K1);
+  SkP p = make_skp(K1);
+  p.wide = wide;
   APG_CHECK_HIP(hipMemsetAsync(u.ghist, 0, u.hist_len * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(u.gstats, 0, 5 * 8, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(u.inst, 0, 8, ctx->stream));
-  uint64_t grid = resident_grid(ctx, k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true>, kSkThreads, nb);
+  uint64_t grid = resident_grid(ctx, k_sk_bucket<false, RB, kSkThreads, kSkTab, 20, true>, kSkThreads, nb);
   if (grid_frac < 1.0) grid = std::max<uint64_t>(1, (uint64_t)((double)grid * grid_frac));
   // algorithmic bytes: the records read (the distinct ones with their
   // multiplicity where the solid-set count folded them) and the bucket bounds
-  kbegin(ctx, "sk_bucket", (dcount ? n_drec * sizeof(SK16) : n_rec * sizeof(SK24)) + (nb + 1) * 8 + (dcount ? nb * 4 : 0));
+  kbegin(ctx, "sk_bucket", (dcount ? n_drec * sizeof(SK16) : n_rec * sizeof(RB)) + (nb + 1) * 8 + (dcount ? nb * 4 : 0));
   if (nb)
-    k_sk_bucket<false, SK24, kSkThreads, kSkTab, 20, true><<<(uint32_t)grid, kSkThreads, 0, ctx->stream>>>(
+    k_sk_bucket<false, RB, kSkThreads, kSkTab, 20, true><<<(uint32_t)grid, kSkThreads, 0, ctx->stream>>>(
         cur, boff, nb, p, u, nullptr, nullptr, drec, dcount);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;
 }
 
-static int sk_up_finish(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
-                        const SkOut& u, bool folded, uint64_t* hist, size_t hist_len, SkResult* res) {
-  const SkP p = make_skp(K1);
+template <typename RB>
+static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                        bool wide, const SkOut& u, bool folded, uint64_t* hist, size_t hist_len, SkResult* res) {
+  SkP p = make_skp(K1);
+  p.wide = wide;
   unsigned long long hs[5];
   APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
@@ -1676,7 +1716,7 @@ static int sk_up_finish(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uin
     k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, u.ovf_list, n_ovf, osz);
     APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
     const uint32_t g2 = (uint32_t)ctx->n_cu * 8;
-    k_sk_big_kmers<SK24, true><<<g2, 256, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, nk);
+    k_sk_big_kmers<RB, true><<<g2, 256, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, nk);
     unsigned long long nbk = 0;
     APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
@@ -1690,7 +1730,7 @@ static int sk_up_finish(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uin
     APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
     vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> global table", hs[1]);
     kbegin(ctx, "sk_bucket_global", nbk * 64);
-    k_sk_big_insert<SK24, true><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, p, gkey, gcnt,
+    k_sk_big_insert<RB, true><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, p, gkey, gcnt,
                                                                   T - 1, u.inst);
     k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, u);
     kend(ctx);
@@ -1715,18 +1755,20 @@ static int sk_up_finish(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uin
 }
 
 
-static int sk_up_run(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+template <typename RB>
+static int sk_up_run(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1, bool wide,
                      const SkOut& u, const SK16* drec, const uint32_t* dcount, uint64_t n_drec, uint64_t* hist,
                      size_t hist_len, SkResult* res) {
-  APG_TRY(sk_up_launch(ctx, cur, boff, nb, n_rec, K1, u, drec, dcount, n_drec));
-  return sk_up_finish(ctx, cur, boff, nb, n_rec, K1, u, dcount != nullptr, hist, hist_len, res);
+  APG_TRY(sk_up_launch(ctx, cur, boff, nb, n_rec, K1, wide, u, drec, dcount, n_drec));
+  return sk_up_finish(ctx, cur, boff, nb, n_rec, K1, wide, u, dcount != nullptr, hist, hist_len, res);
 }
 
-static int sk_up_count(apg_ctx* ctx, const SK24* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
-                       uint64_t* hist, size_t hist_len, SkResult* res) {
+template <typename RB>
+static int sk_up_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint64_t nb, uint64_t n_rec, int K1,
+                       bool wide, uint64_t* hist, size_t hist_len, SkResult* res) {
   SkOut u;
   APG_TRY(sk_up_alloc(ctx, nb, hist_len, &u));
-  return sk_up_run(ctx, cur, boff, nb, n_rec, K1, u, nullptr, nullptr, 0, hist, hist_len, res);
+  return sk_up_run(ctx, cur, boff, nb, n_rec, K1, wide, u, nullptr, nullptr, 0, hist, hist_len, res);
 }
 
 template <typename R>
@@ -1736,7 +1778,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                             const SK16* src16 = nullptr, int up_K = 0, uint64_t* up_hist = nullptr,
                             size_t up_hist_len = 0, SkResult* up_res = nullptr, const SKP* srcp = nullptr,
                             bool split16 = false, bool wide = false) {
-  const SkP p = make_skp(K);
+  SkP p = make_skp(K);
+  p.wide = wide;
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
   const uint32_t B1 = 1u << l1;
   if (rec_counts.size() != (size_t)P * B1) {
@@ -1802,6 +1845,13 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                       bb <= kSkpKeyBits;
   bool packed = srcp != nullptr;
   const int kshift = pack16 ? pbits : 0;
+  // Packed records stay packed through the last level: the bucket kernels
+  // read them as they are (rec_head / rec_pos), 16 bytes per record written
+  // by the last level and read by the count instead of 24 (APG_SK_UNPACK=1:
+  // the last level unpacks to SK24, the round-3 form)
+  const char* ue = getenv("APG_SK_UNPACK");
+  const bool keep_packed = std::is_same<R, SK24>::value && !(ue && !strcmp(ue, "1")) && nlev >= 1 &&
+                           (srcp != nullptr || pack16);
   if constexpr (std::is_same<R, SK24>::value) {  // SK16 input: widened by the first level, or here
     if (src16 && nlev == 0 && n) {
       k_sk_index24<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(src16, n, spare);
@@ -1840,7 +1890,10 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         done = true;
       } else if (packed) {  // packed records through the levels, unpacked by the last
         const SKP* in = reinterpret_cast<const SKP*>(cur);
-        if (last)
+        if (last && keep_packed)
+          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents, 64 - consumed + kshift, bits, n,
+                                        boff, nullptr, "s24")));
+        else if (last)
           APG_TRY((part_level<SKP, SK24>(ctx, in, dst, parents, 64 - consumed + kshift, bits, n, boff, nullptr, "s24",
                                          0, wide)));
         else
@@ -1873,255 +1926,264 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
          (unsigned long long)sz[std::min<uint64_t>(2, nb - 1)], (unsigned long long)sz[std::min<uint64_t>(3, nb - 1)],
          (unsigned long long)over);
   }
-  // outputs
-  const uint64_t hl = std::max<uint64_t>(hist_len, 2);
-  unsigned long long *ghist = nullptr, *gstats = nullptr;
-  uint32_t* ovf = nullptr;
-  APG_TRY(workspace_t(ctx, "sk_hist", hl, &ghist));
-  uint32_t* redo = nullptr;
-  // distinct, overflow, solid, scratch, handed back, distinct records written (dout)
-  APG_TRY(workspace_t(ctx, "sk_gstats", 6, &gstats));
-  APG_TRY(workspace_t(ctx, "sk_ovf", std::max<uint64_t>(nb, 1), &ovf));
-  APG_TRY(workspace_t(ctx, "sk_redo", std::max<uint64_t>(nb, 1), &redo));
-  APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-  APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
-  // The fused K+1 spectrum (up_K) rides on the record dedup: the solid-set
-  // count folds records with their flanks and hands each bucket's distinct
-  // records (with multiplicity) to the K+1 pass through the free partition
-  // buffer (APG_SK_UP_DD=0: the K+1 pass reads every record instead).
-  const bool up_dd_env = !getenv("APG_SK_UP_DD") || strcmp(getenv("APG_SK_UP_DD"), "0") != 0;
-  R* dbuf = (cur == bufA) ? bufB : bufA;
-  const bool up_dd = up_K && dd && solid && up_dd_env && std::is_same<R, SK24>::value && dbuf && dbuf != cur &&
-                     (const void*)dbuf != (const void*)src16;
-  uint32_t* dcount = nullptr;
-  if (up_dd) APG_TRY(workspace_t(ctx, "sk_dcount", std::max<uint64_t>(nb, 1), &dcount));
-  uint64_t solid_cap = 0;
-  uint64_t* sl = nullptr;
-  if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
-    ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
-    ctx->pc_ext_valid = false;
-    solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
-  }
-  // the chunked list (kSolidChunk slots per reservation, compacted into
-  // "pc_solid" afterwards): room for every block's partly used chunks
-  uint32_t* sused = nullptr;
-  auto solid_bufs = [&]() -> int {
-    solid_cap = (solid_cap + kSolidChunk - 1) / kSolidChunk * kSolidChunk;
-    APG_TRY(workspace_t(ctx, "sk_solid_sparse", solid_cap, &sl));
-    APG_TRY(workspace_t(ctx, "sk_sused", solid_cap / kSolidChunk, &sused));
-    return APG_OK;
-  };
-  if (solid) {
-    solid_cap += (uint64_t)ctx->n_cu * 16 * kSolidChunk;
-    APG_TRY(solid_bufs());
-  }
-  static const bool prof = getenv("APG_SK_PROF") != nullptr;
-  unsigned long long* dprof = nullptr;
-  if (prof) {
-    APG_TRY(workspace_t(ctx, "sk_prof", 8, &dprof));
-    APG_CHECK_HIP(hipMemsetAsync(dprof, 0, 64, ctx->stream));
-  }
-  SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr, dprof,
-           (uint32_t)(!solid || (hist && hist_len))};
-  o.sused = sused;
-  o.n_sused = solid ? solid_cap / kSolidChunk : 0;
-  // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
-  // LDS (owner map, recorded slots) and the table amortised over 8 waves give
-  // 16 waves per CU, where 256-thread blocks fit only 3 per CU
-  constexpr int NTB = sizeof(R) == sizeof(SK24) ? 512 : kSkThreads;
-  static const bool own40 = getenv("APG_SK_OWN40") != nullptr;  // A/B: the K <= 20 owner map at K >= 21
-  const bool own20 = K >= 21 && !solid && !own40;  // the plain spectrum count's variants
-  auto plain = [&](auto kern) { return resident_grid(ctx, kern, NTB, nb); };
-  const uint64_t grid = solid        ? resident_grid(ctx, k_sk_bucket<true, R, NTB>, NTB, nb)
-                        : small_tab  ? plain(k_sk_bucket<false, R, NTB, 1024, 20>)
-                        : own20      ? plain(k_sk_bucket<false, R, NTB, kSkTab, 20>)
-                                     : resident_grid(ctx, k_sk_bucket<false, R, NTB>, NTB, nb);
-  // record dedup first (K >= kDdMinK), k_sk_bucket for the buckets it hands back
-  // (a launch over a device-side count: no host round trip in between)
-  const uint64_t grid_dd = !dd ? 0
-                           : solid ? resident_grid(ctx, k_sk_bucket_dd<true, R>, kDdThreads, nb)
-                                   : resident_grid(ctx, k_sk_bucket_dd<false, R>, kDdThreads, nb);
-  uint64_t n_drec = 0;
-  for (int attempt = 0;; ++attempt) {
-    // Algorithmic bytes (inputs read once + outputs written once): the records
-    // and bucket offsets; the weak output (one bit per K-mer instance, or a
-    // 4-byte mask per record in the multi-GPU form); the solid list is added
-    // once its length is known.  The weak pass's L2-hot re-read of the
-    // records is not algorithmic and is not counted.
-    const uint64_t weak_out = o.weak ? n_kmers / 8 : (o.wrec ? n * 4 : 0);
-    kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(R) + (nb + 1) * 8 + weak_out);
-    if (dd) {
-      if (solid) {
-        k_sk_bucket_dd<true, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(
-            cur, boff, nb, p, o, redo, up_dd ? reinterpret_cast<SK16*>(dbuf) : nullptr, dcount);
-        k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
-      } else {
-        k_sk_bucket_dd<false, R><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
-        k_sk_bucket<false, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
-      }
-    } else if (solid) {
-      k_sk_bucket<true, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
-    } else if (small_tab) {
-      k_sk_bucket<false, R, NTB, 1024, 20><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
-    } else if (own20) {
-      k_sk_bucket<false, R, NTB, kSkTab, 20><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
-    } else {
-      k_sk_bucket<false, R, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+  // the bucket pass over the partitioned records, as they are: RB = R, or
+  // SKP when the packed records stayed packed (keep_packed)
+  auto buckets = [&](const auto* cur) -> int {
+    using RB = std::remove_const_t<std::remove_pointer_t<decltype(cur)>>;
+    // outputs
+    const uint64_t hl = std::max<uint64_t>(hist_len, 2);
+    unsigned long long *ghist = nullptr, *gstats = nullptr;
+    uint32_t* ovf = nullptr;
+    APG_TRY(workspace_t(ctx, "sk_hist", hl, &ghist));
+    uint32_t* redo = nullptr;
+    // distinct, overflow, solid, scratch, handed back, distinct records written (dout)
+    APG_TRY(workspace_t(ctx, "sk_gstats", 6, &gstats));
+    APG_TRY(workspace_t(ctx, "sk_ovf", std::max<uint64_t>(nb, 1), &ovf));
+    APG_TRY(workspace_t(ctx, "sk_redo", std::max<uint64_t>(nb, 1), &redo));
+    APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
+    // The fused K+1 spectrum (up_K) rides on the record dedup: the solid-set
+    // count folds records with their flanks and hands each bucket's distinct
+    // records (with multiplicity) to the K+1 pass through the free partition
+    // buffer (APG_SK_UP_DD=0: the K+1 pass reads every record instead).
+    const bool up_dd_env = !getenv("APG_SK_UP_DD") || strcmp(getenv("APG_SK_UP_DD"), "0") != 0;
+    R* dbuf = ((const void*)cur == (const void*)bufA) ? bufB : bufA;
+    const bool up_dd = up_K && dd && solid && up_dd_env && RecPos<RB>::value && dbuf && (const void*)dbuf != (const void*)cur &&
+                       (const void*)dbuf != (const void*)src16;
+    uint32_t* dcount = nullptr;
+    if (up_dd) APG_TRY(workspace_t(ctx, "sk_dcount", std::max<uint64_t>(nb, 1), &dcount));
+    uint64_t solid_cap = 0;
+    uint64_t* sl = nullptr;
+    if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
+      ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
+      ctx->pc_ext_valid = false;
+      solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     }
-    kend(ctx);
-    APG_CHECK_HIP(hipGetLastError());
-    unsigned long long hs[6];
-    APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
-    n_drec = hs[5];
-    if (hs[1]) {  // overflowed buckets: one global table
-      unsigned long long* nk = gstats + 3;
-      APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
-      const uint32_t n_ovf = (uint32_t)hs[1];
-      uint32_t* osz = nullptr;
-      uint64_t* opre = nullptr;
-      APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
-      APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
-      k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovf, n_ovf, osz);
-      APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
-      const uint32_t g2 = (uint32_t)ctx->n_cu * 8;  // persistent: the flattened list's size stays on the device
-      k_sk_big_kmers<R><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
-      unsigned long long nbk = 0;
-      APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
-      uint64_t T = 1024;
-      while (T < 2 * nbk) T <<= 1;
-      unsigned long long* gkey = nullptr;
-      uint32_t* gcnt = nullptr;
-      APG_TRY(workspace_t(ctx, "sk_gkey", T, &gkey));
-      APG_TRY(workspace_t(ctx, "sk_gcnt", T, &gcnt));
-      APG_CHECK_HIP(hipMemsetAsync(gkey, 0xff, T * 8, ctx->stream));
-      APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
-      vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
-      kbegin(ctx, "sk_bucket_global", nbk * 64);
-      k_sk_big_insert<R><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1);
-      if (solid)
-        k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
-      else
-        k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
-      if constexpr (sizeof(R) == sizeof(SK24)) {
-        if (o.weak || o.wrec)
-          k_sk_big_weak<<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1, min_solid,
-                                                      o.weak, o.wrec);
+    // the chunked list (kSolidChunk slots per reservation, compacted into
+    // "pc_solid" afterwards): room for every block's partly used chunks
+    uint32_t* sused = nullptr;
+    auto solid_bufs = [&]() -> int {
+      solid_cap = (solid_cap + kSolidChunk - 1) / kSolidChunk * kSolidChunk;
+      APG_TRY(workspace_t(ctx, "sk_solid_sparse", solid_cap, &sl));
+      APG_TRY(workspace_t(ctx, "sk_sused", solid_cap / kSolidChunk, &sused));
+      return APG_OK;
+    };
+    if (solid) {
+      solid_cap += (uint64_t)ctx->n_cu * 16 * kSolidChunk;
+      APG_TRY(solid_bufs());
+    }
+    static const bool prof = getenv("APG_SK_PROF") != nullptr;
+    unsigned long long* dprof = nullptr;
+    if (prof) {
+      APG_TRY(workspace_t(ctx, "sk_prof", 8, &dprof));
+      APG_CHECK_HIP(hipMemsetAsync(dprof, 0, 64, ctx->stream));
+    }
+    SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr, dprof,
+             (uint32_t)(!solid || (hist && hist_len))};
+    o.sused = sused;
+    o.n_sused = solid ? solid_cap / kSolidChunk : 0;
+    // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
+    // LDS (owner map, recorded slots) and the table amortised over 8 waves give
+    // 16 waves per CU, where 256-thread blocks fit only 3 per CU
+    constexpr int NTB = RecPos<RB>::value ? 512 : kSkThreads;
+    static const bool own40 = getenv("APG_SK_OWN40") != nullptr;  // A/B: the K <= 20 owner map at K >= 21
+    const bool own20 = K >= 21 && !solid && !own40;  // the plain spectrum count's variants
+    auto plain = [&](auto kern) { return resident_grid(ctx, kern, NTB, nb); };
+    const uint64_t grid = solid        ? resident_grid(ctx, k_sk_bucket<true, RB, NTB>, NTB, nb)
+                          : small_tab  ? plain(k_sk_bucket<false, RB, NTB, 1024, 20>)
+                          : own20      ? plain(k_sk_bucket<false, RB, NTB, kSkTab, 20>)
+                                       : resident_grid(ctx, k_sk_bucket<false, RB, NTB>, NTB, nb);
+    // record dedup first (K >= kDdMinK), k_sk_bucket for the buckets it hands back
+    // (a launch over a device-side count: no host round trip in between)
+    const uint64_t grid_dd = !dd ? 0
+                             : solid ? resident_grid(ctx, k_sk_bucket_dd<true, RB>, kDdThreads, nb)
+                                     : resident_grid(ctx, k_sk_bucket_dd<false, RB>, kDdThreads, nb);
+    uint64_t n_drec = 0;
+    for (int attempt = 0;; ++attempt) {
+      // Algorithmic bytes (inputs read once + outputs written once): the records
+      // and bucket offsets; the weak output (one bit per K-mer instance, or a
+      // 4-byte mask per record in the multi-GPU form); the solid list is added
+      // once its length is known.  The weak pass's L2-hot re-read of the
+      // records is not algorithmic and is not counted.
+      const uint64_t weak_out = o.weak ? n_kmers / 8 : (o.wrec ? n * 4 : 0);
+      kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(RB) + (nb + 1) * 8 + weak_out);
+      if (dd) {
+        if (solid) {
+          k_sk_bucket_dd<true, RB><<<grid_dd, kDdThreads, 0, ctx->stream>>>(
+              cur, boff, nb, p, o, redo, up_dd ? reinterpret_cast<SK16*>(dbuf) : nullptr, dcount);
+          k_sk_bucket<true, RB, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
+        } else {
+          k_sk_bucket_dd<false, RB><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
+          k_sk_bucket<false, RB, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
+        }
+      } else if (solid) {
+        k_sk_bucket<true, RB, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      } else if (small_tab) {
+        k_sk_bucket<false, RB, NTB, 1024, 20><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      } else if (own20) {
+        k_sk_bucket<false, RB, NTB, kSkTab, 20><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
+      } else {
+        k_sk_bucket<false, RB, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o);
       }
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
+      unsigned long long hs[6];
       APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
       APG_TRY(sync(ctx));
-    }
-    if (prof) {
-      unsigned long long hp[8];
-      APG_CHECK_HIP(hipMemcpyAsync(hp, dprof, sizeof hp, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
-      fprintf(stderr, "[sk_prof] K=%d solid=%d dedup %.3g flatten %.3g insert %.3g weak %.3g emit %.3g clear %.3g redo %llu\n", K,
-              (int)solid, (double)hp[0], (double)hp[1], (double)hp[2], (double)hp[3], (double)hp[4], (double)hp[5], hs[4]);
-    }
-    if (up_dd) kbytes_add(ctx, "sk_bucket_solid", n_drec * sizeof(SK16) + nb * 4);  // distinct records out
-    if (!solid || hs[2] <= solid_cap) {
-      uint64_t n_solid = 0;
-      uint64_t* dense = nullptr;
-      if (solid) {  // the chunked list -> dense "pc_solid"
-        const uint64_t n_chunks = hs[2] / kSolidChunk;
-        uint64_t* offs = nullptr;
-        APG_TRY(workspace_t(ctx, "sk_soffs", n_chunks + 1, &offs));
-        APG_TRY(scan_u32_u64(ctx, sused, n_chunks, offs, "sks"));
-        APG_CHECK_HIP(hipMemcpyAsync(&n_solid, offs + n_chunks, 8, hipMemcpyDeviceToHost, ctx->stream));
+      n_drec = hs[5];
+      if (hs[1]) {  // overflowed buckets: one global table
+        unsigned long long* nk = gstats + 3;
+        APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
+        const uint32_t n_ovf = (uint32_t)hs[1];
+        uint32_t* osz = nullptr;
+        uint64_t* opre = nullptr;
+        APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
+        APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
+        k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovf, n_ovf, osz);
+        APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
+        const uint32_t g2 = (uint32_t)ctx->n_cu * 8;  // persistent: the flattened list's size stays on the device
+        k_sk_big_kmers<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
+        unsigned long long nbk = 0;
+        APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
         APG_TRY(sync(ctx));
-        APG_TRY(workspace_t(ctx, "pc_solid", std::max<uint64_t>(n_solid, 1), &dense));
-        kbegin(ctx, "solid_compact", n_solid * 16 + n_chunks * 12);
-        if (n_chunks)
-          k_solid_compact<<<(uint32_t)std::min<uint64_t>(n_chunks, (uint64_t)ctx->n_cu * 8), 256, 0, ctx->stream>>>(
-              sl, sused, offs, n_chunks, dense);
+        uint64_t T = 1024;
+        while (T < 2 * nbk) T <<= 1;
+        unsigned long long* gkey = nullptr;
+        uint32_t* gcnt = nullptr;
+        APG_TRY(workspace_t(ctx, "sk_gkey", T, &gkey));
+        APG_TRY(workspace_t(ctx, "sk_gcnt", T, &gcnt));
+        APG_CHECK_HIP(hipMemsetAsync(gkey, 0xff, T * 8, ctx->stream));
+        APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
+        vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
+        kbegin(ctx, "sk_bucket_global", nbk * 64);
+        k_sk_big_insert<RB><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1);
+        if (solid)
+          k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+        else
+          k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+        if constexpr (RecPos<RB>::value) {
+          if (o.weak || o.wrec)
+            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1, min_solid,
+                                                        o.weak, o.wrec);
+        }
         kend(ctx);
         APG_CHECK_HIP(hipGetLastError());
-        kbytes_add(ctx, "sk_bucket_solid", n_solid * 8);
+        APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
+        APG_TRY(sync(ctx));
       }
-      res->n_distinct = hs[0];
-      res->n_overflow_buckets = hs[1];
-      res->n_solid = n_solid;
-      res->solid = dense;
-      res->nbuckets = nb;
-      res->n_redo_buckets = dd ? hs[4] : 0;
-      break;
+      if (prof) {
+        unsigned long long hp[8];
+        APG_CHECK_HIP(hipMemcpyAsync(hp, dprof, sizeof hp, hipMemcpyDeviceToHost, ctx->stream));
+        APG_TRY(sync(ctx));
+        fprintf(stderr, "[sk_prof] K=%d solid=%d dedup %.3g flatten %.3g insert %.3g weak %.3g emit %.3g clear %.3g redo %llu\n", K,
+                (int)solid, (double)hp[0], (double)hp[1], (double)hp[2], (double)hp[3], (double)hp[4], (double)hp[5], hs[4]);
+      }
+      if (up_dd) kbytes_add(ctx, "sk_bucket_solid", n_drec * sizeof(SK16) + nb * 4);  // distinct records out
+      if (!solid || hs[2] <= solid_cap) {
+        uint64_t n_solid = 0;
+        uint64_t* dense = nullptr;
+        if (solid) {  // the chunked list -> dense "pc_solid"
+          const uint64_t n_chunks = hs[2] / kSolidChunk;
+          uint64_t* offs = nullptr;
+          APG_TRY(workspace_t(ctx, "sk_soffs", n_chunks + 1, &offs));
+          APG_TRY(scan_u32_u64(ctx, sused, n_chunks, offs, "sks"));
+          APG_CHECK_HIP(hipMemcpyAsync(&n_solid, offs + n_chunks, 8, hipMemcpyDeviceToHost, ctx->stream));
+          APG_TRY(sync(ctx));
+          APG_TRY(workspace_t(ctx, "pc_solid", std::max<uint64_t>(n_solid, 1), &dense));
+          kbegin(ctx, "solid_compact", n_solid * 16 + n_chunks * 12);
+          if (n_chunks)
+            k_solid_compact<<<(uint32_t)std::min<uint64_t>(n_chunks, (uint64_t)ctx->n_cu * 8), 256, 0, ctx->stream>>>(
+                sl, sused, offs, n_chunks, dense);
+          kend(ctx);
+          APG_CHECK_HIP(hipGetLastError());
+          kbytes_add(ctx, "sk_bucket_solid", n_solid * 8);
+        }
+        res->n_distinct = hs[0];
+        res->n_overflow_buckets = hs[1];
+        res->n_solid = n_solid;
+        res->solid = dense;
+        res->nbuckets = nb;
+        res->n_redo_buckets = dd ? hs[4] : 0;
+        break;
+      }
+      if (attempt >= 2) {
+        set_error("sk count: solid list overflow persists");
+        return APG_E_STATE;
+      }
+      vlog(ctx, "sk count: %llu solid K-mers exceed the list (%llu), recounting", hs[2], (unsigned long long)solid_cap);
+      solid_cap = hs[2] + hs[2] / 8;
+      APG_TRY(solid_bufs());
+      o.solid = sl;
+      o.solid_cap = solid_cap;
+      o.sused = sused;
+      o.n_sused = solid_cap / kSolidChunk;
+      APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
+      APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
     }
-    if (attempt >= 2) {
-      set_error("sk count: solid list overflow persists");
-      return APG_E_STATE;
+    if (hist && hist_len) {
+      APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      hist[0] = 0;
     }
-    vlog(ctx, "sk count: %llu solid K-mers exceed the list (%llu), recounting", hs[2], (unsigned long long)solid_cap);
-    solid_cap = hs[2] + hs[2] / 8;
-    APG_TRY(solid_bufs());
-    o.solid = sl;
-    o.solid_cap = solid_cap;
-    o.sused = sused;
-    o.n_sused = solid_cap / kSolidChunk;
-    APG_CHECK_HIP(hipMemsetAsync(ghist, 0, hl * 8, ctx->stream));
-    APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
-  }
-  if (hist && hist_len) {
-    APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
-    hist[0] = 0;
-  }
-  res->n_kmers = n_kmers;
-  res->n_records = n;
-  vlog(ctx, "sk count: K=%d P=%d records=%llu kmers=%llu levels=%d buckets=%llu distinct=%llu redo=%llu ovf=%llu", K,
-       P, (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
-       (unsigned long long)res->n_distinct, (unsigned long long)res->n_redo_buckets,
-       (unsigned long long)res->n_overflow_buckets);
+    res->n_kmers = n_kmers;
+    res->n_records = n;
+    vlog(ctx, "sk count: K=%d P=%d records=%llu kmers=%llu levels=%d buckets=%llu distinct=%llu redo=%llu ovf=%llu", K,
+         P, (unsigned long long)n, (unsigned long long)n_kmers, nlev, (unsigned long long)nb,
+         (unsigned long long)res->n_distinct, (unsigned long long)res->n_redo_buckets,
+         (unsigned long long)res->n_overflow_buckets);
+    if constexpr (RecPos<RB>::value) {
+      if (up_K && up_dd) {
+        SkOut u;
+        APG_TRY(sk_up_alloc(ctx, nb, up_hist_len, &u));
+        const SK16* drec = reinterpret_cast<const SK16*>(dbuf);
+        // Side stream (APG_SK_UP_SIDE=0: in line): the K+1 pass needs nothing the
+        // caller computes next (PreCorrect's candidates, decisions and edits
+        // touch neither the records nor their buckets), so it runs beside them
+        // on APG_SK_UP_FRAC (default 1.0) of a resident round of blocks, and the
+        // caller joins it (side_join) before it returns.
+        const char* se = getenv("APG_SK_UP_SIDE");
+        const bool side = !(se && !strcmp(se, "0"));
+        const hipStream_t sd = side ? side_stream(ctx) : nullptr;
+        if (sd) {
+          const char* fe = getenv("APG_SK_UP_FRAC");
+          const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 1.0;
+          auto launch = [=]() -> int {
+            hipEvent_t ev = nullptr;
+            APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));  // the records and dout are complete
+            APG_CHECK_HIP(hipStreamWaitEvent(sd, ev, 0));
+            APG_CHECK_HIP(hipEventDestroy(ev));
+            StreamSwap sw(ctx, sd);
+            return sk_up_launch(ctx, cur, boff, nb, n, up_K, wide, u, drec, dcount, n_drec, frac);
+          };
+          // APG_SK_UP_AT=s: launched at PreCorrect's stage s (0: now, 1: after
+          // the extension table, 2: after the candidate scan — the default: the
+          // pass then runs beside the lookup-bound decisions and edits, not the
+          // LDS-staged candidate scan; same box, APG_SK_UP_FRAC 0.75 / 1.0:
+          // s = 0 160.1 / —, s = 1 163.2 / 162.8, s = 2 160.9 / 158.5 ms)
+          const char* ae = getenv("APG_SK_UP_AT");
+          ctx->side_kick_at = ae ? atoi(ae) : 2;
+          if (ctx->side_kick_at <= 0)
+            APG_TRY(launch());
+          else
+            ctx->side_kick = launch;
+          ctx->side_finish = [=]() -> int {
+            StreamSwap sw(ctx, sd);
+            return sk_up_finish(ctx, cur, boff, nb, n, up_K, wide, u, true, up_hist, up_hist_len, up_res);
+          };
+        } else {
+          APG_TRY(sk_up_run(ctx, cur, boff, nb, n, up_K, wide, u, drec, dcount, n_drec, up_hist, up_hist_len, up_res));
+        }
+      } else if (up_K) {
+        APG_TRY(sk_up_count(ctx, cur, boff, nb, n, up_K, wide, up_hist, up_hist_len, up_res));
+      }
+    }
+    return APG_OK;
+  };
   if constexpr (std::is_same<R, SK24>::value) {
-    if (up_K && up_dd) {
-      SkOut u;
-      APG_TRY(sk_up_alloc(ctx, nb, up_hist_len, &u));
-      const SK16* drec = reinterpret_cast<const SK16*>(dbuf);
-      // Side stream (APG_SK_UP_SIDE=0: in line): the K+1 pass needs nothing the
-      // caller computes next (PreCorrect's candidates, decisions and edits
-      // touch neither the records nor their buckets), so it runs beside them
-      // on APG_SK_UP_FRAC (default 1.0) of a resident round of blocks, and the
-      // caller joins it (side_join) before it returns.
-      const char* se = getenv("APG_SK_UP_SIDE");
-      const bool side = !(se && !strcmp(se, "0"));
-      const hipStream_t sd = side ? side_stream(ctx) : nullptr;
-      if (sd) {
-        const char* fe = getenv("APG_SK_UP_FRAC");
-        const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 1.0;
-        auto launch = [=]() -> int {
-          hipEvent_t ev = nullptr;
-          APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-          APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));  // the records and dout are complete
-          APG_CHECK_HIP(hipStreamWaitEvent(sd, ev, 0));
-          APG_CHECK_HIP(hipEventDestroy(ev));
-          StreamSwap sw(ctx, sd);
-          return sk_up_launch(ctx, cur, boff, nb, n, up_K, u, drec, dcount, n_drec, frac);
-        };
-        // APG_SK_UP_AT=s: launched at PreCorrect's stage s (0: now, 1: after
-        // the extension table, 2: after the candidate scan — the default: the
-        // pass then runs beside the lookup-bound decisions and edits, not the
-        // LDS-staged candidate scan; same box, APG_SK_UP_FRAC 0.75 / 1.0:
-        // s = 0 160.1 / —, s = 1 163.2 / 162.8, s = 2 160.9 / 158.5 ms)
-        const char* ae = getenv("APG_SK_UP_AT");
-        ctx->side_kick_at = ae ? atoi(ae) : 2;
-        if (ctx->side_kick_at <= 0)
-          APG_TRY(launch());
-        else
-          ctx->side_kick = launch;
-        ctx->side_finish = [=]() -> int {
-          StreamSwap sw(ctx, sd);
-          return sk_up_finish(ctx, cur, boff, nb, n, up_K, u, true, up_hist, up_hist_len, up_res);
-        };
-      } else {
-        APG_TRY(sk_up_run(ctx, cur, boff, nb, n, up_K, u, drec, dcount, n_drec, up_hist, up_hist_len, up_res));
-      }
-    } else if (up_K) {
-      APG_TRY(sk_up_count(ctx, cur, boff, nb, n, up_K, up_hist, up_hist_len, up_res));
-    }
+    if (keep_packed) return buckets(reinterpret_cast<const SKP*>(cur));
   }
-  return APG_OK;
+  return buckets(cur);
 }
 
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
