@@ -124,17 +124,21 @@ def test_fused_kplus1_record_sources(gpu_ctx, monkeypatch, env):
     assert_same(sep, fus_dd)
 
 
-@pytest.mark.parametrize("pack", ["wide", "0"])
-def test_solid_count_record_forms(gpu_ctx, monkeypatch, pack):
+@pytest.mark.parametrize("env", [{"APG_SK_PACK": "wide"}, {"APG_SK_PACK": "0"}, {"APG_SK_UNPACK": "1"},
+                                 {"APG_SK_PACK": "wide", "APG_SK_UNPACK": "1"}])
+def test_solid_count_record_forms(gpu_ctx, monkeypatch, env):
     """The solid-set count's partition records: packed with 32-bit positions
-    (the default below 2^32 bases), packed wide (34-bit positions, records
-    cut to <= 31 bases: the form of read sets of 2^32 .. 2^34 bases, e.g. C4's
-    50 M reads per GPU; APG_SK_PACK=wide forces it) and unpacked 24-byte
-    records (APG_SK_PACK=0) give the same spectrum, solid set and corrections,
-    equal to the oracle's."""
+    and read packed by the bucket kernels (the default below 2^32 bases),
+    packed wide (34-bit positions, records cut to <= 31 bases: the form of
+    read sets of 2^32 .. 2^34 bases, e.g. C4's 50 M reads per GPU;
+    APG_SK_PACK=wide forces it), unpacked by the last partition level
+    (APG_SK_UNPACK=1) and unpacked 24-byte records throughout (APG_SK_PACK=0)
+    give the same spectrum, solid set and corrections, equal to the
+    oracle's."""
     g = synth_genome(1_000_000, 71, repeats={"tandem_frac": 0.02})
     reads = synth_reads(g, 200_000, seed=72)
-    monkeypatch.setenv("APG_SK_PACK", pack)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     sep, fus = both_ways(gpu_ctx, reads)
     assert_same(sep, fus)
     monkeypatch.undo()
