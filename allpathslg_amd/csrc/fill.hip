@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
                                               uint32_t cap, const uint32_t* __restrict__ list,
                                               const unsigned long long* __restrict__ list_n,
                                               uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer,
-                                              unsigned long long* __restrict__ next) {
+                                              unsigned long long* __restrict__ next, bool bcache) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
@@ -230,6 +230,23 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
   uint32_t LaLf = 0, gmax = 0, dlo = 0, fb0 = 0, d = 0, steps = 0, mode = 0, j = 0, mnode = 0, dd = 0;
   uint32_t n_clos = 0, clos_I = 0, clos_meta = 0;
   unsigned __int128 pv = 0, clos_pv = 0;
+  // successor mask of the path's open branch points at depths < 32 (4 bits
+  // per depth, 16 depths per word; 100-bp pairs walk < 35 deep): a
+  // backtrack to one reads its node's mask here instead of looking it up
+  // again — a walk of L leaves re-reads L - 1 branch points, and the
+  // repeat-rich pairs (the BUDGET ones) are wide trees.  Two words and
+  // selects, not an indexed array (that went to scratch), keep the kernel
+  // at 4 waves / SIMD; deeper branch points are looked up as before.
+  uint64_t bm0 = 0, bm1 = 0;
+  auto mask_at = [&](uint32_t dep) -> uint32_t {
+    return (uint32_t)((dep < 16 ? bm0 : bm1) >> (4 * (dep & 15))) & 15u;
+  };
+  auto mask_set = [&](uint32_t dep, uint32_t m) {
+    const uint32_t sh = 4 * (dep & 15);
+    const uint64_t keep = ~(15ull << sh), v = (uint64_t)m << sh;
+    bm0 = dep < 16 ? (bm0 & keep) | v : bm0;
+    bm1 = dep >= 16 ? (bm1 & keep) | v : bm1;
+  };
 
   auto emit = [&](uint32_t st, const FillRec& out) {
     rec[i] = out;
@@ -376,12 +393,13 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     }
     if (!__ballot(act)) break;
     if (!act) continue;
-    // ---- one lookup
-    // mode 2 (open branch point at depth dd < d): the path to it is pv's first dd bases
+    // ---- one lookup (a node or a closure's bridge K-mer; an open branch
+    // point at depth dd < d reads the mask its visit kept)
+    const bool cached = bcache && mode == 2 && dd < 32;
     const uint64_t key = mode == 0   ? walk_window(atail, pv, d, t)
                          : mode == 1 ? ww
                                      : walk_window(atail, pv >> (2 * (d - dd)), dd, t);
-    const uint32_t m = ext_succ(t, key, &nlook);
+    const uint32_t m = cached ? mask_at(dd) : ext_succ(t, key, &nlook);
     bool visit = false, done = false;
     if (mode == 0) {  // node (pv, d)
       mnode = m;
@@ -426,7 +444,10 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
           done = true;
         } else if (mnode) {
           const uint32_t b = __ffs(mnode) - 1;
-          if (mnode >> (b + 1)) brm |= 1ull << d;
+          if (mnode >> (b + 1)) {
+            brm |= 1ull << d;
+            if (d < 32) mask_set(d, mnode);  // an open branch point: its mask for the backtracks
+          }
           pv = (pv << 2) | b;
           ++d;
           down = true;
@@ -635,12 +656,15 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
     // lanes are persistent (work fetched per wave): one resident round of blocks
     const uint32_t grid = resident_grid(ctx, k_fill, 256, (np + 255) / 256);
+    // APG_FILL_BRANCH_CACHE=0: backtracks look their branch point up again (A/B)
+    const char* be = getenv("APG_FILL_BRANCH_CACHE");
+    const bool bcache = !(be && !strcmp(be, "0"));
     k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
                                           std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
-                                          ndefer + 1);
+                                          ndefer + 1, bcache);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
       k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
-                                            defer, ndefer, nullptr, nullptr, ndefer + 2);
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
