@@ -900,6 +900,126 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
 }
 
 // ---------------------------------------------------------------------------
+// The K+1 count by an LDS counting sort (A/B of VERDICT r03 #3, APG_SK_UP_SORT=1)
+// ---------------------------------------------------------------------------
+// The alternative to the hash table that DESIGN.md §4 had only sized: per
+// bucket, every owned K+1-mer instance (key, multiplicity) is flattened into
+// LDS, counting-sorted on the top 12 bits of its khash (4096 bins: a
+// histogram, a block scan, a scatter of the instance indices), and each bin
+// is grouped by full-key equality by one thread (bins hold ~0.4 instances on
+// average, so the grouping is a short scan) — equal keys always share a bin.
+// Same outputs as k_sk_bucket<.., UP>: the spectrum, the distinct count, the
+// instance count, and the buckets of more than kSortCap instances sent to the
+// global table.
+constexpr uint32_t kSortCap = 4096;
+constexpr int kSortDigitBits = 12;
+template <typename R>
+__global__ void __launch_bounds__(256) k_sk_up_sort(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
+                                                    uint64_t nbuckets, SkP p, SkOut o,
+                                                    const SK16* __restrict__ drec,
+                                                    const uint32_t* __restrict__ dcount) {
+  constexpr int NT = 256;
+  constexpr uint32_t NB = 1u << kSortDigitBits;
+  __shared__ unsigned long long key[kSortCap];
+  __shared__ uint32_t wt[kSortCap];
+  __shared__ uint16_t sidx[kSortCap];
+  __shared__ uint32_t cnt[NB];
+  __shared__ uint32_t lhist[kSkHistBins];
+  __shared__ uint32_t scan_sm[32];
+  __shared__ uint32_t ni_sh;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < kSkHistBins; i += NT) lhist[i] = 0;
+  unsigned long long nd = 0, n_up = 0;
+  const int dsh = 2 * p.K - kSortDigitBits;
+  for (uint64_t bkt = blockIdx.x; bkt < nbuckets; bkt += gridDim.x) {
+    const uint64_t off = boff[bkt];
+    const uint32_t dc = dcount ? dcount[bkt] : ~0u;
+    const bool mult = dc != ~0u;  // the solid-set count's distinct records, multiplicity in the key bits
+    const uint32_t nr = mult ? dc : (uint32_t)(boff[bkt + 1] - off);
+    if (tid == 0) ni_sh = 0;
+    __syncthreads();
+    // 1. flatten: each record's owned K+1-mers (as k_sk_bucket<.., UP>)
+    for (uint32_t r = tid; r < nr; r += NT) {
+      R x;
+      if constexpr (RecPos<R>::value) {
+        x = mult ? rec_from_drec<R>(drec[off + r]) : rec[off + r];
+      } else {
+        x = rec[off + r];
+      }
+      const SK16 h = rec_head(x, p);
+      const uint32_t nk = (uint32_t)(h.w0 >> 32) & 0xff;
+      bool ol, orr;
+      (void)rec_kmer_up(h, -1, p, &ol);
+      (void)rec_kmer_up(h, (int)nk - 1, p, &orr);
+      const uint32_t no = nk - 1 + (ol ? 1u : 0u) + (orr ? 1u : 0u);
+      const uint4 str = rec_up_string(h, p, ol, orr);
+      const uint32_t w = mult ? (uint32_t)rec_pos(x, p) : 1u;
+      const uint32_t at = atomicAdd(&ni_sh, no);
+      for (uint32_t f = 0; f < no && at + f < kSortCap; ++f) {
+        key[at + f] = limb_kmer(str.x, str.y, str.z, f, p);
+        wt[at + f] = w;
+      }
+    }
+    __syncthreads();
+    const uint32_t ni = ni_sh;
+    if (ni > kSortCap) {  // block-uniform: the global table counts this bucket
+      if (tid == 0) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+      __syncthreads();
+      continue;
+    }
+    // 2. counting sort of the instance indices on 12 hash bits
+    for (uint32_t b = tid; b < NB; b += NT) cnt[b] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < ni; i += NT) atomicAdd(&cnt[(uint32_t)(khash(p.hp, key[i]) >> dsh)], 1u);
+    __syncthreads();
+    constexpr uint32_t PER = NB / NT;
+    uint32_t loc[PER], tsum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      loc[q] = cnt[tid * PER + q];
+      tsum += loc[q];
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<uint32_t>(tsum, scan_sm, &tot);
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+      cnt[tid * PER + q] = run;
+      run += loc[q];
+    }
+    __syncthreads();
+    unsigned long long wsum = 0;
+    for (uint32_t i = tid; i < ni; i += NT) {
+      sidx[atomicAdd(&cnt[(uint32_t)(khash(p.hp, key[i]) >> dsh)], 1u)] = (uint16_t)i;
+      wsum += wt[i];
+    }
+    n_up += wsum;
+    __syncthreads();
+    // 3. per bin: group equal keys (cnt[b] is now the bin's end)
+    for (uint32_t b = tid; b < NB; b += NT) {
+      const uint32_t e = cnt[b], s0 = b ? cnt[b - 1] : 0u;
+      for (uint32_t j = s0; j < e; ++j) {
+        const unsigned long long kj = key[sidx[j]];
+        bool lead = true;
+        for (uint32_t q = s0; q < j && lead; ++q) lead = key[sidx[q]] != kj;
+        if (!lead) continue;
+        uint32_t c = wt[sidx[j]];
+        for (uint32_t q = j + 1; q < e; ++q)
+          if (key[sidx[q]] == kj) c += wt[sidx[q]];
+        sk_spectrum_add(c, lhist, o);
+        ++nd;
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
+  for (uint32_t i = tid; i < lim; i += NT)
+    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
+  wave_add(&o.gstats[0], nd);
+  wave_add(o.inst, n_up);
+}
+
+// ---------------------------------------------------------------------------
 // Record-deduplicating bucket count (K >= 21)
 // ---------------------------------------------------------------------------
 // At genome coverage c most super-k-mer records of a bucket are exact copies:
@@ -1689,9 +1809,16 @@ static int sk_up_launch(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
   // algorithmic bytes: the records read (the distinct ones with their
   // multiplicity where the solid-set count folded them) and the bucket bounds
   kbegin(ctx, "sk_bucket", (dcount ? n_drec * sizeof(SK16) : n_rec * sizeof(RB)) + (nb + 1) * 8 + (dcount ? nb * 4 : 0));
-  if (nb)
+  // APG_SK_UP_SORT=1: the LDS counting-sort form of the pass (A/B; read per call)
+  const char* se = getenv("APG_SK_UP_SORT");
+  if (nb && se && !strcmp(se, "1")) {
+    uint64_t sg = resident_grid(ctx, k_sk_up_sort<RB>, 256, nb);
+    if (grid_frac < 1.0) sg = std::max<uint64_t>(1, (uint64_t)((double)sg * grid_frac));
+    k_sk_up_sort<RB><<<(uint32_t)sg, 256, 0, ctx->stream>>>(cur, boff, nb, p, u, drec, dcount);
+  } else if (nb) {
     k_sk_bucket<false, RB, kSkThreads, kSkTab, 20, true><<<(uint32_t)grid, kSkThreads, 0, ctx->stream>>>(
         cur, boff, nb, p, u, nullptr, nullptr, drec, dcount);
+  }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;

@@ -106,13 +106,15 @@ def test_not_fusable_falls_back(gpu_ctx):
         assert_same(sep, fus)
 
 
-@pytest.mark.parametrize("env", [{"APG_SK_UP_DD": "0"}, {"APG_SK_DEDUP": "none"}])
+@pytest.mark.parametrize("env", [{"APG_SK_UP_DD": "0"}, {"APG_SK_DEDUP": "none"}, {"APG_SK_UP_SORT": "1"},
+                                 {"APG_SK_UP_SORT": "1", "APG_SK_UP_DD": "0"}])
 def test_fused_kplus1_record_sources(gpu_ctx, monkeypatch, env):
     """The K+1 pass reads each bucket's distinct records with their
     multiplicity (the solid-set count's dedup output; buckets it handed back
     are read as partitioned).  The same results with the K+1 pass reading
-    every record (APG_SK_UP_DD=0) and with no record dedup at all; on a
-    repeat-rich genome, so some buckets take each route."""
+    every record (APG_SK_UP_DD=0), with no record dedup at all, and with the
+    LDS counting-sort form of the pass (APG_SK_UP_SORT=1, the A/B of DESIGN
+    §4); on a repeat-rich genome, so some buckets take each route."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g = synth_genome(1_000_000, 61, repeats={"tandem_frac": 0.03})
