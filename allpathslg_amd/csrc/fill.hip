@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
                                               uint32_t cap, const uint32_t* __restrict__ list,
                                               const unsigned long long* __restrict__ list_n,
                                               uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer,
-                                              unsigned long long* __restrict__ next, bool bcache) {
+                                              unsigned long long* __restrict__ next, bool bcache, bool bfilt) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
@@ -238,6 +238,19 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
   // selects, not an indexed array (that went to scratch), keep the kernel
   // at 4 waves / SIMD; deeper branch points are looked up as before.
   uint64_t bm0 = 0, bm1 = 0;
+  // Bridge filter (bfilt, K >= 3): a closure at a node with window w needs
+  // the bridge K-mers w[j, K-1) ++ F[0, j+1) solid for j = 0 .. K-2.  The
+  // last two depend only on w's last two bases: before its walk a lane
+  // looks up F's first (K-1)-mer G's predecessors c1 and, for each, the
+  // predecessors c2 of c1 ++ G[0, K-2) (mode 3: 1 + |P1| lookups through
+  // the reverse complements' successor masks), and bk holds bit c2*4 + c1
+  // for every solid pair.  A node is a closure candidate only if its
+  // window's last two bases are in bk, and the bridge test then checks
+  // j = 1 .. K-4 only.  The result is the same; the failing bridge tests
+  // (29 % of a walk's lookups on a repeat-rich genome, 30 % on the iid
+  // one: tools/fill_walk_model.c) mostly go — 21 % / 18 % fewer iterations.
+  uint32_t bk = 0xffffu;
+  const int jend = bfilt && n1 >= 2 ? n1 - 2 : n1;  // bridge K-mers [1, jend) by lookup
   auto mask_at = [&](uint32_t dep) -> uint32_t {
     return (uint32_t)((dep < 16 ? bm0 : bm1) >> (4 * (dep & 15))) & 15u;
   };
@@ -365,6 +378,11 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
       pv = 0;
       brm = 0;  // depths whose node still has unexplored children
       d = steps = mode = 0;
+      if (bfilt && n1 >= 2) {  // the bridge filter's lookups first
+        mode = 3;
+        j = 16;
+        bk = 0;
+      }
       act = true;
       return;
     }
@@ -396,16 +414,22 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     // ---- one lookup (a node or a closure's bridge K-mer; an open branch
     // point at depth dd < d reads the mask its visit kept)
     const bool cached = bcache && mode == 2 && dd < 32;
+    // mode 3: the reverse complement of G (j == 16) or of c1 ++ G[0, K-2)
+    // (c1 the lowest pending predecessor in j); an LSB-first value
+    // complemented is the MSB-first value of its reverse complement
+    const uint64_t m1s = t.m1 >> 2;
+    const uint64_t bkey = j == 16 ? (f0 & t.m1) ^ t.m1 : ((((f0 & m1s) ^ m1s) << 2) | (3u - (__ffs(j) - 1)));
     const uint64_t key = mode == 0   ? walk_window(atail, pv, d, t)
                          : mode == 1 ? ww
-                                     : walk_window(atail, pv >> (2 * (d - dd)), dd, t);
+                         : mode == 2 ? walk_window(atail, pv >> (2 * (d - dd)), dd, t)
+                                     : bkey;
     const uint32_t m = cached ? mask_at(dd) : ext_succ(t, key, &nlook);
     bool visit = false, done = false;
     if (mode == 0) {  // node (pv, d)
       mnode = m;
       visit = true;
-      if (d >= dlo && ((m >> fb0) & 1)) {  // closure test: the K-1 bridge K-mers
-        if (n1 > 1) {
+      if (d >= dlo && ((m >> fb0) & 1) && ((bk >> (key & 15)) & 1)) {  // closure test: the K-1 bridge K-mers
+        if (jend > 1) {
           mode = 1;
           j = 1;
           ww = ((key << 2) | fb0) & t.m1;
@@ -418,7 +442,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     } else if (mode == 1) {  // bridge K-mer j of the closure test at depth d
       const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
       const bool ok = (m >> b) & 1;
-      if (ok && (int)j + 1 < n1) {
+      if (ok && (int)j + 1 < jend) {
         ww = ((ww << 2) | b) & t.m1;
         ++j;
       } else if (ok && closure()) {
@@ -427,6 +451,16 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
         mode = 0;
         visit = true;
       }
+    } else if (mode == 3) {  // bridge filter: predecessors of G, then of c1 ++ G[0, K-2)
+      const uint32_t pm = rev4(m);  // pred(x) bit c = succ(rc(x)) bit 3 - c
+      if (j == 16) {
+        j = pm;
+      } else {
+        const uint32_t c1 = __ffs(j) - 1;
+        bk |= ((pm & 1) | ((pm & 2) << 3) | ((pm & 4) << 6) | ((pm & 8) << 9)) << c1;
+        j &= j - 1;
+      }
+      if (j == 0) mode = 0;  // the walk from depth 0
     } else {  // open branch point at depth dd: the sibling after the base taken there
       const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
       const uint32_t rest = m & ~((2u << bb) - 1);
@@ -659,12 +693,15 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     // APG_FILL_BRANCH_CACHE=0: backtracks look their branch point up again (A/B)
     const char* be = getenv("APG_FILL_BRANCH_CACHE");
     const bool bcache = !(be && !strcmp(be, "0"));
+    // APG_FILL_BRIDGE_FILTER=0: every closure candidate tested K-mer by K-mer (A/B)
+    const char* bfe = getenv("APG_FILL_BRIDGE_FILTER");
+    const bool bfilt = !(bfe && !strcmp(bfe, "0"));
     k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
                                           std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
-                                          ndefer + 1, bcache);
+                                          ndefer + 1, bcache, bfilt);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
       k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
-                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache);
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

@@ -1261,6 +1261,10 @@ constexpr int kUskMaxNk = 63;
 constexpr int kUskDigitBits = 5;
 constexpr uint64_t kUskBucketKmers = 2048;
 constexpr uint32_t kUskTab = 1024;  // LDS table slots: tag u32, key 3 x u64, ext u32
+// APG_USK_TAB=512: a first pass with a 512-slot table (24 KiB of LDS per
+// block, five blocks per CU instead of four: the bench buckets hold ~140
+// distinct K-mers) and the buckets it overflows again with kUskTab slots.
+constexpr uint32_t kUskTabSmall = 512;
 // probes before a bucket is declared full (linear probing at load <= 0.9 stays
 // far below; a full table must not cost every later instance 1024 probes)
 constexpr uint32_t kUskProbeMax = 128;
@@ -1426,8 +1430,9 @@ __device__ __forceinline__ uint32_t usk_slot_hash(const K3& k) {
 struct UskOut {
   KRec* nodes;
   uint64_t cap;
-  unsigned long long* gs;  // [0] nodes appended, [1] overflowed buckets
-  uint32_t* ovf_list;
+  unsigned long long* gs;  // [0] nodes appended
+  uint32_t* ovf_list;      // overflowed buckets, counted by *novf
+  unsigned long long* novf;
   uint2* lsucc;  // may be null: per node, its two orientations' local links (usk_links_local)
   uint32_t dedup;  // fold identical records of a chunk before flattening
   unsigned long long* dstat;  // may be null: records, instances, records folded, instances folded
@@ -1453,10 +1458,14 @@ __device__ __forceinline__ uint32_t urec_fp(const SK48& r) {
 }
 
 
-// One workgroup per bucket (grid-stride).
-__global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restrict__ rec,
+// One workgroup per bucket (grid-stride); blist (or null): the buckets to
+// run, nbuckets of them (the ones a smaller table overflowed).
+template <uint32_t TAB, int WPE = 1>
+__global__ void __launch_bounds__(kUskBThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_usk_bucket(const SK48* __restrict__ rec,
                                                              const uint64_t* __restrict__ boff, uint64_t nbuckets,
-                                                             KeyP kp, UskOut o) {
+                                                             const uint32_t* __restrict__ blist, KeyP kp, UskOut o) {
+  constexpr uint32_t kUskTab = TAB;
   __shared__ uint32_t tag[kUskTab];
   __shared__ uint64_t ka[kUskTab], kb[kUskTab], kc[kUskTab];
   __shared__ uint32_t text[kUskTab];
@@ -1468,19 +1477,21 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
   constexpr int TB = __builtin_ctz(kUskTab);
-  static_assert(kUskChunk * kUskMaxNk >= 2 * kUskTab, "owner doubles as the slot ranks");
+  static_assert(kUskChunk * kUskMaxNk >= 2 * TAB, "owner doubles as the slot ranks");
   uint16_t* rnk = reinterpret_cast<uint16_t*>(owner);  // emit: slot -> rank in the bucket's node list
-  static_assert(sizeof(SK48) * kUskChunk >= 2 * kUskTab, "crec doubles as the rank -> slot list");
+  static_assert(sizeof(SK48) * kUskChunk >= 2 * TAB, "crec doubles as the rank -> slot list");
   uint16_t* slot_of = reinterpret_cast<uint16_t*>(crec);
   const uint32_t tid = threadIdx.x;
   // The block's buckets bkt, bkt + grid, ... are one record stream: the next
   // chunk's records (this bucket's or the next bucket's first) are loaded
   // while the current chunk is counted.
-  uint64_t bkt = blockIdx.x, off = 0;
+  auto bucket = [&](uint64_t q) -> uint64_t { return blist ? blist[q] : q; };
+  uint64_t bkt = blockIdx.x, off = 0;  // bkt: index into the bucket list
   uint32_t nr = 0;
   if (bkt < nbuckets) {
-    off = boff[bkt];
-    nr = (uint32_t)(boff[bkt + 1] - off);
+    const uint64_t b0 = bucket(bkt);
+    off = boff[b0];
+    nr = (uint32_t)(boff[b0 + 1] - off);
   }
   SK48 pre{};
   if (tid < kUskChunk && tid < nr) pre = rec[off + tid];
@@ -1491,8 +1502,9 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
     uint64_t noff = 0;
     uint32_t nnr = 0;
     if (nbk < nbuckets) {
-      noff = boff[nbk];
-      nnr = (uint32_t)(boff[nbk + 1] - noff);
+      const uint64_t b1 = bucket(nbk);
+      noff = boff[b1];
+      nnr = (uint32_t)(boff[b1 + 1] - noff);
     }
     auto advance = [&]() {
       bkt = nbk;
@@ -1610,7 +1622,7 @@ __global__ void __launch_bounds__(kUskBThreads) k_usk_bucket(const SK48* __restr
       __syncthreads();
     }
     if (ovf) {
-      if (tid == 0) o.ovf_list[atomicAdd(&o.gs[1], 1ull)] = (uint32_t)bkt;
+      if (tid == 0) o.ovf_list[atomicAdd(o.novf, 1ull)] = (uint32_t)bucket(bkt);
       __syncthreads();
       advance();
       continue;
@@ -2406,12 +2418,21 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   // buckets -> nodes
   unsigned long long* gs = nullptr;
   uint32_t* ovf = nullptr;
-  APG_TRY(workspace_t(ctx, "usk_gs", 5, &gs));
+  APG_TRY(workspace_t(ctx, "usk_gs", 6, &gs));
   APG_TRY(workspace_t(ctx, "usk_ovf", std::max<uint64_t>(nb, 1), &ovf));
+  // APG_USK_TAB=512: small-table first pass, its overflowed buckets again
+  // with the full table (gs[5] counts them, listed in ovf1)
+  const char* te = getenv("APG_USK_TAB");
+  const bool small_tab = te && !strncmp(te, "512", 3);
+  const bool small_w6 = te && !strcmp(te, "512w6");  // VGPRs capped for 6 waves / SIMD (spills)
+  uint32_t* ovf1 = nullptr;
+  if (small_tab) APG_TRY(workspace_t(ctx, "usk_ovf1", std::max<uint64_t>(nb, 1), &ovf1));
   uint64_t cap = std::max<uint64_t>(1 << 20, nk / 4);
   KRec* nodes = nullptr;
   unsigned long long hs[5];
-  const uint64_t grid = resident_grid(ctx, k_usk_bucket, kUskBThreads, nb);
+  const uint64_t grid = resident_grid(ctx, k_usk_bucket<kUskTab>, kUskBThreads, nb);
+  const uint64_t grid_s = small_w6 ? resident_grid(ctx, k_usk_bucket<kUskTabSmall, 6>, kUskBThreads, nb)
+                                   : resident_grid(ctx, k_usk_bucket<kUskTabSmall>, kUskBThreads, nb);
   // APG_USK_DEDUP=0: every record flattened (A/B)
   const char* de = getenv("APG_USK_DEDUP");
   const bool dedup = !(de && !strcmp(de, "0"));
@@ -2439,11 +2460,27 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   for (;;) {
     APG_TRY(workspace_t(ctx, "usk_nodes", cap, &nodes));
     if (want_ls) APG_TRY(workspace_t(ctx, "usk_lsucc", cap, &ls));
-    APG_CHECK_HIP(hipMemsetAsync(gs, 0, 5 * 8, ctx->stream));
+    APG_CHECK_HIP(hipMemsetAsync(gs, 0, 6 * 8, ctx->stream));
     if (pre_idx) APG_CHECK_HIP(hipMemsetAsync(pre_idx, 0xff, pre_T * 8, ctx->stream));
+    const UskOut uo{nodes, cap, gs, ovf, gs + 1, ls, dedup ? 1u : 0u, dstat, pre_idx, pre_T - 1, pre_T / 2};
     kbegin(ctx, "usk_bucket", n * sizeof(SK48) + (nb + 1) * 8);
-    k_usk_bucket<<<grid, kUskBThreads, 0, ctx->stream>>>(
-        cur, boff, nb, kp, UskOut{nodes, cap, gs, ovf, ls, dedup ? 1u : 0u, dstat, pre_idx, pre_T - 1, pre_T / 2});
+    if (small_tab) {
+      UskOut u1 = uo;
+      u1.ovf_list = ovf1;
+      u1.novf = gs + 5;
+      if (small_w6)
+        k_usk_bucket<kUskTabSmall, 6><<<grid_s, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, nullptr, kp, u1);
+      else
+        k_usk_bucket<kUskTabSmall><<<grid_s, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, nullptr, kp, u1);
+      APG_CHECK_HIP(hipGetLastError());
+      unsigned long long n1 = 0;
+      APG_TRY(d2h_u64(ctx, gs + 5, &n1, 1));
+      if (n1)
+        k_usk_bucket<kUskTab><<<std::min<uint64_t>(grid, n1), kUskBThreads, 0, ctx->stream>>>(cur, boff, n1, ovf1,
+                                                                                               kp, uo);
+    } else {
+      k_usk_bucket<kUskTab><<<grid, kUskBThreads, 0, ctx->stream>>>(cur, boff, nb, nullptr, kp, uo);
+    }
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     APG_TRY(d2h_u64(ctx, gs, hs, 5));

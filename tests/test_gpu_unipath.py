@@ -178,3 +178,15 @@ def test_urec_path_loopback(gpu_ctx, P):
         a, b = int(parts[i][0]), int(parts[i][-1]) + 1
         assert np.array_equal(g["path_start"], exp["path_start"][int(exp["path_off"][a]) : int(exp["path_off"][b])])
         d.free()
+
+
+@pytest.mark.parametrize("tab", ["512", "512w6"])
+def test_node_buckets_small_table(gpu_ctx, monkeypatch, tab):
+    """APG_USK_TAB=512: the node buckets' first pass on a 512-slot LDS table,
+    the buckets it overflows rerun through the bucket list with the full
+    table, the rest through the global table — same graph."""
+    monkeypatch.setenv("APG_USK_TAB", tab)
+    g = synth_genome(300_000, 51, repeats=True)
+    run(gpu_ctx, synth_reads(g, 40_000, seed=52), 96)
+    run(gpu_ctx, noisy_reads(G=30_000, n=6000), 96)
+    run(gpu_ctx, tiling(repeat_genome(), L=200, step=5), 96)
