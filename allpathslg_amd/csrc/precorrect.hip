@@ -629,6 +629,22 @@ constexpr uint32_t kPcTileW = kPcTileQ / 64 + 2;  // weak words of a staged tile
 constexpr uint32_t kPcKeep = 4;                   // candidate positions a thread keeps from its first scan
 constexpr uint32_t kPcTileList = 1024;            // candidates of a tile written through LDS
 
+constexpr uint32_t kPcQv = kPcTileQ / 16 / kPcTileReads;  // 16-byte quals chunks a thread stages
+static_assert(kPcQv * 16 * kPcTileReads == kPcTileQ && kPcTileW <= 2 * kPcTileReads, "staging shape");
+
+// A tile's staged quals chunks (kPcQv = 7 per thread) and weak words (2),
+// loaded ahead into named registers: a register array, captured by a lambda
+// or returned in a struct, was kept in scratch.  Loads and stores past the end
+// are clamped to the last chunk / word rather than predicated.
+static_assert(kPcQv == 7, "PC_STAGE names seven chunks");
+#define PC_STAGE_CHUNKS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6)
+
+// Each block walks its tiles r0, r0 + grid, ... (grid = one resident round)
+// with the next tile's inputs — the reads' offsets, then its quals and weak
+// words — loaded into registers while the current tile is scanned and its
+// candidates written, so a tile costs about the candidate window round trip
+// and not a chain of dependent loads (8.7 ms on the bench step when each
+// tile's staging, offset and window loads waited in turn).
 template <bool WRITE>
 __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     const uint64_t* __restrict__ base_off, const uint64_t* __restrict__ byte_off, const uint8_t* __restrict__ packed,
@@ -642,23 +658,64 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
   __shared__ unsigned long long tbase_sm;
   __shared__ __attribute__((aligned(16))) uint8_t qs[kPcTileQ + 16];
   __shared__ unsigned long long ws[kPcTileW];
+  __shared__ uint64_t bo_s[kPcTileReads + 1], yo_s[kPcTileReads];  // the tile's base / byte offsets
   __shared__ uint32_t list[WRITE ? kPcTileList : 1];  // read in tile << 16 | position
   __shared__ uint32_t scan_sm[64];
   const uint32_t tid = threadIdx.x;
-  for (uint64_t r0 = (uint64_t)blockIdx.x * kPcTileReads; r0 < n_reads; r0 += (uint64_t)gridDim.x * kPcTileReads) {
+  const uint64_t stride = (uint64_t)gridDim.x * kPcTileReads;
+  // staged inputs of the next tile
+  uint64_t nbo = 0, nbo_hi = 0, nyo = 0, nQ0 = 0, nQ1 = 0;
+  uint4 ng0, ng1, ng2, ng3, ng4, ng5, ng6;
+  unsigned long long ngw0, ngw1;
+  // the next tile's quals chunks and weak words (after load_offsets)
+  auto stage_load = [&]() {
+    if (nQ1 - nQ0 > kPcTileQ || nQ1 == nQ0) return;  // a long tile reads global memory directly
+    const uint32_t nch = (uint32_t)((nQ1 - nQ0 + 15) >> 4);
+    const uint4* src = reinterpret_cast<const uint4*>(quals + nQ0);
+#define PC_LD(k) ng##k = src[min(tid + (k) * kPcTileReads, nch - 1)];
+    PC_STAGE_CHUNKS(PC_LD)
+#undef PC_LD
+    const uint64_t W0 = nQ0 >> 6;
+    const uint32_t nwd = (uint32_t)(((nQ1 + 63) >> 6) - W0 + 1);  // K-mer bits of the tile lie in [Q0, Q1)
+    ngw0 = weak[W0 + min(tid, nwd - 1)];
+    ngw1 = weak[W0 + min(tid + kPcTileReads, nwd - 1)];
+  };
+  auto load_offsets = [&](uint64_t t0) {
+    const uint64_t te = min(t0 + kPcTileReads, n_reads);
+    nQ0 = base_off[t0] & ~15ull;  // block-uniform: scalar loads
+    nQ1 = base_off[te];
+    nbo = base_off[min(t0 + tid, n_reads)];
+    nbo_hi = base_off[te];
+    nyo = t0 + tid < n_reads ? byte_off[t0 + tid] : 0;
+  };
+  uint64_t r0 = (uint64_t)blockIdx.x * kPcTileReads;
+  if (r0 < n_reads) {
+    load_offsets(r0);
+    stage_load();
+  }
+  for (; r0 < n_reads; r0 += stride) {
     const uint64_t r = r0 + tid;
-    const uint64_t re = min(r0 + kPcTileReads, n_reads);
-    const uint64_t Q0 = base_off[r0] & ~15ull, Q1 = base_off[re];
+    const uint64_t Q0 = nQ0, Q1 = nQ1;
     const bool staged = Q1 - Q0 <= kPcTileQ;
     const uint64_t W0 = Q0 >> 6;
-    if (staged) {
-      const uint4* src = reinterpret_cast<const uint4*>(quals + Q0);
+    bo_s[tid] = nbo;
+    if (tid == 0) bo_s[kPcTileReads] = nbo_hi;
+    yo_s[tid] = nyo;
+    if (staged && Q1 > Q0) {
+      const uint32_t nch = (uint32_t)((Q1 - Q0 + 15) >> 4);
       uint4* dst = reinterpret_cast<uint4*>(qs);
-      for (uint32_t i = tid; i < (uint32_t)((Q1 - Q0 + 15) >> 4); i += kPcTileReads) dst[i] = src[i];
-      // K-mer bits of the tile's reads lie in [Q0, Q1)
-      for (uint32_t i = tid; i < (uint32_t)(((Q1 + 63) >> 6) - W0 + 1); i += kPcTileReads) ws[i] = weak[W0 + i];
+      // past the end every lane rewrites the last chunk / word with the value
+      // its clamped load read
+#define PC_ST(k) dst[min(tid + (k) * kPcTileReads, nch - 1)] = ng##k;
+      PC_STAGE_CHUNKS(PC_ST)
+#undef PC_ST
+      const uint32_t nwd = (uint32_t)(((Q1 + 63) >> 6) - W0 + 1);
+      ws[min(tid, nwd - 1)] = ngw0;
+      ws[min(tid + kPcTileReads, nwd - 1)] = ngw1;
     }
     __syncthreads();
+    const uint64_t nr0 = r0 + stride;
+    if (nr0 < n_reads) load_offsets(nr0);  // in flight during the scan
     const uint8_t* qb = staged ? qs : quals;
     const uint64_t qbase = staged ? Q0 : 0;
     const unsigned long long* wb = staged ? ws : weak;
@@ -666,8 +723,8 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     uint64_t q0 = 0;
     uint32_t L = 0;
     if (r < n_reads) {
-      q0 = base_off[r];
-      L = (uint32_t)(base_off[r + 1] - q0);
+      q0 = bo_s[tid];
+      L = (uint32_t)(bo_s[tid + 1] - q0);
     }
     const bool scan = r < n_reads && L >= (uint32_t)K && L <= kPcMaxL;
     uint32_t n = 0;
@@ -686,53 +743,54 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     const uint32_t ex = block_exclusive_scan<uint32_t>(n, scan_sm, &tot);
     if constexpr (!WRITE) {
       if (tid == 0) tcnt[r0 / kPcTileReads] = tot;
+      if (nr0 < n_reads) stage_load();
     } else {
       uint64_t tb;
+      bool skip = false;
       if (tctr) {
         if (tid == 0) tbase_sm = tot ? atomicAdd(tctr, (unsigned long long)tot) : 0ull;
         __syncthreads();
         tb = tbase_sm;
-        if (tb + tot > cap) {  // over capacity: nothing of this tile is written
-          __syncthreads();
-          continue;
-        }
+        skip = tb + tot > cap;  // over capacity: nothing of this tile is written
       } else {
         tb = toff[r0 / kPcTileReads];
       }
-      if (r < n_reads) {
-        cstart[r] = tb + ex;
-        ccnt[r] = n;
-      }
-      if (tot <= kPcTileList) {
-        // positions into LDS, then one candidate per thread: independent
-        // window loads, consecutive records from consecutive threads
-        uint32_t at = ex;
-        if (n > kPcKeep) {
-          pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
-            if (pc_all_weak_at(wb, wbase, q0, p, L, K)) list[at++] = tid << 16 | p;
-          });
-        } else {
+      if (nr0 < n_reads) stage_load();  // in flight with the candidate windows
+      if (!skip) {
+        if (r < n_reads) {
+          cstart[r] = tb + ex;
+          ccnt[r] = n;
+        }
+        if (tot <= kPcTileList) {
+          // positions into LDS, then one candidate per thread: independent
+          // window loads, consecutive records from consecutive threads
+          uint32_t at = ex;
+          if (n > kPcKeep) {
+            pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
+              if (pc_all_weak_at(wb, wbase, q0, p, L, K)) list[at++] = tid << 16 | p;
+            });
+          } else {
 #pragma unroll
-          for (uint32_t k = 0; k < kPcKeep; ++k)
-            if (k < n) list[at + k] = tid << 16 | ((keep[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+            for (uint32_t k = 0; k < kPcKeep; ++k)
+              if (k < n) list[at + k] = tid << 16 | ((keep[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+          }
+          __syncthreads();
+          for (uint32_t i = tid; i < tot; i += kPcTileReads) {
+            const uint32_t e = list[i];
+            const uint32_t rl = e >> 16, pp = e & 0xffff;
+            const uint32_t LL = (uint32_t)(bo_s[rl + 1] - bo_s[rl]);
+            const unsigned __int128 v = pc_window(packed + yo_s[rl], pp, K);
+            cand[tb + i] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)(r0 + rl), (uint16_t)pp, (uint16_t)LL};
+          }
+        } else if (n) {
+          uint64_t at = tb + ex;
+          const uint8_t* rd = packed + yo_s[tid];
+          pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
+            if (!pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
+            const unsigned __int128 v = pc_window(rd, p, K);
+            cand[at++] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)r, (uint16_t)p, (uint16_t)L};
+          });
         }
-        __syncthreads();
-        for (uint32_t i = tid; i < tot; i += kPcTileReads) {
-          const uint32_t e = list[i];
-          const uint64_t rr = r0 + (e >> 16);
-          const uint32_t pp = e & 0xffff;
-          const uint32_t LL = (uint32_t)(base_off[rr + 1] - base_off[rr]);
-          const unsigned __int128 v = pc_window(packed + byte_off[rr], pp, K);
-          cand[tb + i] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)rr, (uint16_t)pp, (uint16_t)LL};
-        }
-      } else if (n) {
-        uint64_t at = tb + ex;
-        const uint8_t* rd = packed + byte_off[r];
-        pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
-          if (!pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
-          const unsigned __int128 v = pc_window(rd, p, K);
-          cand[at++] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)r, (uint16_t)p, (uint16_t)L};
-        });
       }
     }
     __syncthreads();  // the LDS tiles are rewritten by the next tile
@@ -981,7 +1039,9 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     uint64_t* toff = nullptr;
     APG_TRY(workspace_t(ctx, "pc_tcnt", std::max<uint64_t>(ntiles, 1), &tcnt));
     APG_TRY(workspace_t(ctx, "pc_toff", ntiles + 1, &toff));
-    const uint32_t cgrid = grid_for(ctx, dr->n_reads, kPcTileReads);
+    // one resident round: each block pipelines its tiles
+    const uint32_t cgrid = std::min<uint32_t>(resident_grid(ctx, k_pc_candidates<true>, kPcTileReads, ntiles),
+                                              resident_grid(ctx, k_pc_candidates<false>, kPcTileReads, ntiles));
     // Single pass when the previous call's candidate count gives a capacity:
     // tiles reserve their runs with one atomic each (no counting pass, no
     // scan); an overflow falls back to count + scan + write.
