@@ -797,8 +797,10 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
   }
 }
 
+// dec[i] = the candidate's position << 8 | its decision (a base, kPcAmbiguous
+// or kPcNone): k_pc_apply reads these 4 bytes, not the 32-byte record.
 __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ cand, uint64_t n, int K, ExtTab et,
-                                                   uint8_t* __restrict__ dec, unsigned long long* __restrict__ looks) {
+                                                   uint32_t* __restrict__ dec, unsigned long long* __restrict__ looks) {
   uint32_t nl = 0;
   const unsigned __int128 km = ((unsigned __int128)1 << (2 * (K + 1))) - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -842,7 +844,7 @@ __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ ca
         cb = alt;
       }
     }
-    dec[i] = ncand == 1 ? (uint8_t)cb : ncand > 1 ? kPcAmbiguous : kPcNone;
+    dec[i] = p << 8 | (ncand == 1 ? cb : ncand > 1 ? kPcAmbiguous : kPcNone);
   }
   wave_add(looks, nl);
 }
@@ -851,7 +853,7 @@ __global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ b
                                                   const uint64_t* __restrict__ byte_off, uint8_t* __restrict__ packed,
                                                   uint8_t* __restrict__ quals, uint64_t n_reads, int K,
                                                   const unsigned long long* __restrict__ weak,
-                                                  const PcCand* __restrict__ cand, const uint8_t* __restrict__ dec,
+                                                  const uint32_t* __restrict__ dec,
                                                   const uint64_t* __restrict__ cstart,
                                                   const uint32_t* __restrict__ ccnt, uint8_t* __restrict__ clean,
                                                   PcCounters* __restrict__ cnt) {
@@ -870,10 +872,11 @@ __global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ b
     uint8_t* q = quals + q0;
     int last = -(int)kPcMaxL - 64;  // latest correction
     for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t p = cand[s0 + i].p;
+      const uint32_t pd = dec[s0 + i];
+      const uint32_t p = pd >> 8;
       if ((int)p - last < K) continue;  // a covering K-mer holds a correction: solid
       ++n_sus;
-      const uint8_t d = dec[s0 + i];
+      const uint8_t d = (uint8_t)pd;
       if (d < 4) {
         const uint32_t sh = 2 * (p & 3);
         rd[p >> 2] = (uint8_t)((rd[p >> 2] & ~(3u << sh)) | ((uint32_t)d << sh));
@@ -902,9 +905,10 @@ __global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ b
       uint64_t D = 0;
       int lc = -(int)kPcMaxL - 64;
       for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t p = cand[s0 + i].p;
+        const uint32_t pd = dec[s0 + i];
+        const uint32_t p = pd >> 8;
         if ((int)p - lc < K) continue;
-        if (dec[s0 + i] >= 4) continue;
+        if ((pd & 0xff) >= 4) continue;
         lc = (int)p;
         // covered K-mers [p-K+1, p] relative to b - q0
         const int64_t lo = (int64_t)p - K + 1 - (int64_t)(b - q0), up = (int64_t)p - (int64_t)(b - q0);
@@ -1093,21 +1097,21 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     }
     APG_TRY(side_kick(ctx, 2));
     ctx->pc_cand_hint = ncand + ncand / 4 + 4096;
-    uint8_t* dec = nullptr;
+    uint32_t* dec = nullptr;
     APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));
     // candidate records in, decisions out (+ 64 B per extension lookup, after the sync)
     APG_TRY(ext_wait());
-    kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 1));
+    kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 4));
     if (ncand)
       k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups);
     kend(ctx);
     // offsets, runs, the candidates' positions and decisions, weak bits in;
     // corrected bases and quals, clean flags out
-    kbegin(ctx, "pc_apply", 16 * dr->n_reads + 8 * dr->n_reads + ncand * 9 + dr->n_bases / 8 + dr->n_reads);
+    kbegin(ctx, "pc_apply", 16 * dr->n_reads + 8 * dr->n_reads + ncand * 4 + dr->n_bases / 8 + dr->n_reads);
     if (dr->n_reads)
       k_pc_apply<<<grid_for(ctx, dr->n_reads), 256, 0, ctx->stream>>>(
-          dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, weak, cand, dec, cstart, ccnt,
-          clean, pcnt);
+          dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, weak, dec, cstart, ccnt, clean,
+          pcnt);
     kend(ctx);
   } else {
     // reads + quals (+ the weak bitmap and the clean flags)
