@@ -1593,7 +1593,12 @@ k_usk_bucket(const SK48* __restrict__ rec,
         const uint32_t tv = (h & ~3u) | 2u;
         uint32_t s = h >> (32 - TB);
         for (uint32_t probe = 0;;) {
-          uint32_t tg = tag[s];
+          // the slot's tag, key words and extension bits read together: one
+          // LDS round trip on the common hit path (tag, then each key word
+          // after the previous compare cost four)
+          const uint32_t tg = tag[s];
+          uint64_t xa = ka[s], xb = kb[s], xc = kc[s];
+          const uint32_t xt = text[s];
           if (tg == 0) {
             const uint32_t prev = atomicCAS(&tag[s], 0u, 1u);
             if (prev == 0) {
@@ -1605,12 +1610,22 @@ k_usk_bucket(const SK48* __restrict__ rec,
               __hip_atomic_store(&tag[s], tv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               break;
             }
-            tg = prev;
+            continue;  // claimed meanwhile: read the slot again
           }
           if (tg == 1) continue;  // being written by a lane that publishes in the same pass
-          if (tg == tv && ka[s] == key.a && kb[s] == key.b && kc[s] == key.c) {
-            if (e & ~text[s]) atomicOr(&text[s], e);
-            break;
+          if (tg == tv) {
+            if (xa != key.a || xb != key.b || xc != key.c) {
+              // the key words may have been read before the tag that
+              // published them: read them again, ordered after it
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+              xa = ka[s];
+              xb = kb[s];
+              xc = kc[s];
+            }
+            if (xa == key.a && xb == key.b && xc == key.c) {
+              if (e & ~xt) atomicOr(&text[s], e);  // a stale xt only costs an extra OR
+              break;
+            }
           }
           s = (s + 1) & (kUskTab - 1);
           if (++probe == kUskProbeMax) {
@@ -1680,9 +1695,10 @@ k_usk_bucket(const SK48* __restrict__ rec,
             const uint32_t tv = (h & ~3u) | 2u;
             uint32_t sl = h >> (32 - TB), hit = kUskTab;
             for (uint32_t probe = 0; probe < kUskProbeMax; ++probe) {
-              const uint32_t tg = tag[sl];
+              const uint32_t tg = tag[sl];  // the table is complete: read the slot at once
+              const uint64_t xa = ka[sl], xb = kb[sl], xc = kc[sl];
               if (tg == 0) break;
-              if (tg == tv && ka[sl] == c.a && kb[sl] == c.b && kc[sl] == c.c) {
+              if (tg == tv && xa == c.a && xb == c.b && xc == c.c) {
                 hit = sl;
                 break;
               }
