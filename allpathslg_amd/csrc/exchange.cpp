@@ -120,12 +120,20 @@ Nccl& nccl() {
 uint64_t Comm::piece_bytes() const { return kPiece; }
 
 int Comm::alltoall_u64(const uint64_t* send, uint64_t* recv, uint64_t m) {
+  if (world == 1) {  // a single rank: no staging through the device, no stream drain
+    std::memmove(recv, send, m * 8);
+    return APG_OK;
+  }
   // small host arrays: m u64 per peer, through the host path of the transport
   std::vector<uint64_t> sb(world, m * 8), rb(world, m * 8);
   return alltoallv_host(send, sb.data(), recv, rb.data());
 }
 
 int Comm::allgather_u64(uint64_t v, std::vector<uint64_t>* all) {
+  if (world == 1) {
+    all->assign(1, v);
+    return APG_OK;
+  }
   all->assign(world, 0);
   std::vector<uint64_t> rb(world, 8);
   return allgatherv_host(&v, 8, all->data(), rb.data());
@@ -294,7 +302,7 @@ struct RcclComm : Comm {
 
   int allreduce_u64(uint64_t* data, uint64_t n, int op) override {
     APG_TRY(live());
-    if (!n) return APG_OK;
+    if (!n || world == 1) return APG_OK;
     APG_TRY(stage(n));
     APG_CHECK_HIP(hipMemcpyAsync(dsum, data, n * 8, hipMemcpyHostToDevice, ctx->stream));
     APG_CHECK_NCCL(nccl().AllReduce(dsum, dsum, n, kNcclUint64, op == APG_COMM_MAX ? kNcclMax : kNcclSum, nc,

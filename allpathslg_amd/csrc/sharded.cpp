@@ -73,6 +73,13 @@ int exchange_records(apg_ctx* ctx, Comm* c, const std::vector<uint64_t>& counts,
   void* send = nullptr;
   APG_TRY(workspace(ctx, send_ws, std::max<uint64_t>(x->n_in * rec_bytes, 64), &send));
   APG_TRY(scatter(send));
+  if (P == 1) {  // a single rank receives what it sends: the scatter wrote the receive buffer
+    x->recv_counts = counts;
+    x->rb = x->sb;
+    x->n_out = x->n_in;
+    x->recv = send;
+    return APG_OK;
+  }
   x->recv_counts.assign((size_t)P * B, 0);
   APG_TRY(c->alltoall_u64(counts.data(), x->recv_counts.data(), (uint64_t)B));  // counts[dest * B + g] -> [src * B + g]
   x->rb = seg_bytes(x->recv_counts, P, B, rec_bytes);
@@ -84,6 +91,11 @@ int exchange_records(apg_ctx* ctx, Comm* c, const std::vector<uint64_t>& counts,
 // allgatherv of n_local elements of `bytes` each from every rank into ws.
 int gather_all(apg_ctx* ctx, Comm* c, const void* local, uint64_t n_local, uint64_t bytes, const char* ws,
                void** out, uint64_t* n_all) {
+  if (c->world == 1) {  // the gathered set is this rank's
+    *out = const_cast<void*>(local);
+    *n_all = n_local;
+    return APG_OK;
+  }
   std::vector<uint64_t> sizes;
   APG_TRY(c->allgather_u64(n_local, &sizes));
   std::vector<uint64_t> rb(sizes.size());
@@ -200,8 +212,12 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
         mb_out[q] = x.rb[q] / 16 * 4;
         mb_in[q] = x.sb[q] / 16 * 4;
       }
-      APG_TRY(workspace(ctx, "x_smask", std::max<uint64_t>(x.n_in * 4, 64), &smask));
-      APG_TRY(c->alltoallv(rmask, mb_out.data(), smask, mb_in.data()));
+      if (P == 1) {  // the owner is this rank: the masks are where they were written
+        smask = rmask;
+      } else {
+        APG_TRY(workspace(ctx, "x_smask", std::max<uint64_t>(x.n_in * 4, 64), &smask));
+        APG_TRY(c->alltoallv(rmask, mb_out.data(), smask, mb_in.data()));
+      }
     } else {
       APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
                                [&](void* send) { return apg_shard_scatter(ctx, reads, K, P, send); }, &x));
