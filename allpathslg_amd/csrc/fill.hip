@@ -199,7 +199,8 @@ __device__ __forceinline__ uint64_t walk_window(uint64_t atail, unsigned __int12
 // within the cap ends exactly as it would with the full budget.
 constexpr uint32_t kFillCap1 = 96;
 // A wave refills its idle lanes with new pairs once at most this many lanes
-// are still walking.
+// are still walking (APG_FILL_REFILL for A/B: a higher mark keeps more lanes
+// walking, a lower one batches more lanes into each refill's start phase).
 constexpr int kFillRefill = 32;
 
 // One thread per pair, lanes persistent.  The gap walk is a state machine
@@ -219,7 +220,8 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
                                               uint32_t cap, const uint32_t* __restrict__ list,
                                               const unsigned long long* __restrict__ list_n,
                                               uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer,
-                                              unsigned long long* __restrict__ next, bool bcache, bool bfilt) {
+                                              unsigned long long* __restrict__ next, bool bcache, bool bfilt,
+                                              int refill) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
@@ -400,7 +402,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
 
   bool more = true;
   for (;;) {
-    while (more && __popcll(__ballot(act)) <= kFillRefill) {  // refill the idle lanes (wave-uniform)
+    while (more && __popcll(__ballot(act)) <= refill) {  // refill the idle lanes (wave-uniform)
       const uint64_t idle = __ballot(!act);
       const unsigned long long k = wave_append(next, !act);  // the wave's next popc(idle) work items
       more = __shfl(k, 63 - __clzll((long long)idle), 64) + 1 < nwork;
@@ -696,12 +698,14 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     // APG_FILL_BRIDGE_FILTER=0: every closure candidate tested K-mer by K-mer (A/B)
     const char* bfe = getenv("APG_FILL_BRIDGE_FILTER");
     const bool bfilt = !(bfe && !strcmp(bfe, "0"));
+    const char* rfe = getenv("APG_FILL_REFILL");
+    const int refill = rfe ? std::max(0, std::min(63, atoi(rfe))) : kFillRefill;
     k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
                                           std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
-                                          ndefer + 1, bcache, bfilt);
+                                          ndefer + 1, bcache, bfilt, refill);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
       k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
-                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt);
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
