@@ -235,6 +235,7 @@ struct apg_ctx {
   bool clean_valid = false;
   // Capacity for the next single-pass candidate write (last count + 25 %).
   uint64_t pc_cand_hint = 0;
+  uint64_t pc_cand_hint_lk = 0;  // the same for the passes without a weak bitmap (every low-quality position)
   // ws_make_room calls that released buffers (memory pressure; logged with
   // cfg.verbose)
   uint64_t mem_releases = 0;

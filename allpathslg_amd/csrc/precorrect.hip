@@ -545,7 +545,7 @@ struct PcCand {
   uint32_t r;
   uint16_t p, L;
 };
-constexpr uint8_t kPcAmbiguous = 4, kPcNone = 5;
+constexpr uint8_t kPcAmbiguous = 4, kPcNone = 5, kPcNotSuspect = 6;
 
 // Covering K-mers [jlo, jhi] of read position p all counted weak: bits
 // q0 + jlo .. q0 + jhi of the weak-instance bitmap (nk <= K <= 32 bits).
@@ -675,6 +675,7 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
 #define PC_LD(k) ng##k = src[min(tid + (k) * kPcTileReads, nch - 1)];
     PC_STAGE_CHUNKS(PC_LD)
 #undef PC_LD
+    if (!weak) return;  // every low-quality position is a candidate
     const uint64_t W0 = nQ0 >> 6;
     const uint32_t nwd = (uint32_t)(((nQ1 + 63) >> 6) - W0 + 1);  // K-mer bits of the tile lie in [Q0, Q1)
     ngw0 = weak[W0 + min(tid, nwd - 1)];
@@ -709,9 +710,11 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
 #define PC_ST(k) dst[min(tid + (k) * kPcTileReads, nch - 1)] = ng##k;
       PC_STAGE_CHUNKS(PC_ST)
 #undef PC_ST
-      const uint32_t nwd = (uint32_t)(((Q1 + 63) >> 6) - W0 + 1);
-      ws[min(tid, nwd - 1)] = ngw0;
-      ws[min(tid + kPcTileReads, nwd - 1)] = ngw1;
+      if (weak) {
+        const uint32_t nwd = (uint32_t)(((Q1 + 63) >> 6) - W0 + 1);
+        ws[min(tid, nwd - 1)] = ngw0;
+        ws[min(tid + kPcTileReads, nwd - 1)] = ngw1;
+      }
     }
     __syncthreads();
     const uint64_t nr0 = r0 + stride;
@@ -733,7 +736,7 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
     uint32_t keep[kPcKeep / 2] = {};
     if (scan)
       pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
-        if (!pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
+        if (weak && !pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
 #pragma unroll
         for (uint32_t k = 0; k < kPcKeep; ++k)
           if (n == k) keep[k >> 1] |= p << (16 * (k & 1));
@@ -767,7 +770,7 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
           uint32_t at = ex;
           if (n > kPcKeep) {
             pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
-              if (pc_all_weak_at(wb, wbase, q0, p, L, K)) list[at++] = tid << 16 | p;
+              if (!weak || pc_all_weak_at(wb, wbase, q0, p, L, K)) list[at++] = tid << 16 | p;
             });
           } else {
 #pragma unroll
@@ -786,7 +789,7 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
           uint64_t at = tb + ex;
           const uint8_t* rd = packed + yo_s[tid];
           pc_scan_read(qb, qbase, q0, L, maxq, [&](uint32_t p) {
-            if (!pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
+            if (weak && !pc_all_weak_at(wb, wbase, q0, p, L, K)) return;
             const unsigned __int128 v = pc_window(rd, p, K);
             cand[at++] = PcCand{(uint64_t)v, (uint64_t)(v >> 64), (uint32_t)r, (uint16_t)p, (uint16_t)L};
           });
@@ -799,8 +802,14 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
 
 // dec[i] = the candidate's position << 8 | its decision (a base, kPcAmbiguous
 // or kPcNone): k_pc_apply reads these 4 bytes, not the 32-byte record.
+// wtest (no weak bitmap: ErrorCorrectJump, K < 9, a given solid list): the
+// candidates are all low-quality positions, and one whose covering K-mers are
+// not all weak — by extension lookups on the read as it was, the state the
+// sequential rule sees unless a correction lies within K before it — is
+// kPcNotSuspect.
 __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ cand, uint64_t n, int K, ExtTab et,
-                                                   uint32_t* __restrict__ dec, unsigned long long* __restrict__ looks) {
+                                                   uint32_t* __restrict__ dec, unsigned long long* __restrict__ looks,
+                                                   bool wtest) {
   uint32_t nl = 0;
   const unsigned __int128 km = ((unsigned __int128)1 << (2 * (K + 1))) - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -811,20 +820,36 @@ __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ ca
     const bool hasA = p + 1 >= (uint32_t)K, hasB = p + (uint32_t)K <= L;
     // (A) the (K-1)-mers beside p answer the first and last covering K-mers
     // for all 4 bases at p: succ of bases [p-K+1, p) and pred of [p+1, p+K)
-    uint32_t allowed = 15;
+    uint32_t mA = 15, mB = 15;
     if (hasA) {
-      allowed &= ext_masks_lsb(et, (uint64_t)(win >> 2) & et.m1) >> 4;
+      mA = ext_masks_lsb(et, (uint64_t)(win >> 2) & et.m1) >> 4;
       ++nl;
     }
     if (hasB) {
-      allowed &= ext_masks_lsb(et, (uint64_t)(win >> (2 * K + 2)) & et.m1) & 15;
+      mB = ext_masks_lsb(et, (uint64_t)(win >> (2 * K + 2)) & et.m1) & 15;
       ++nl;
     }
+    const uint32_t allowed = mA & mB;
     uint32_t surv = allowed & ~(1u << orig) & 15u;
     // (B) the other covering K-mers a..b, two per (K-1)-mer lookup
     const uint32_t jlo = p + 1 >= (uint32_t)K ? p + 1 - K : 0;
     const uint32_t jhi = min(p, L - (uint32_t)K);
     const int ia = (int)jlo + (hasA ? 1 : 0), ib = (int)jhi - (hasB ? 1 : 0);
+    if (wtest) {
+      // the weak test: (A) answered the first and last covering K-mers as
+      // read (the original base's bits), the others in pairs as in (B)
+      bool solid = (hasA && ((mA >> orig) & 1)) || (hasB && ((mB >> orig) & 1));
+      for (int t = ia + 1; t <= ib + 1 && !solid; t += 2) {
+        const uint64_t W = (uint64_t)((win >> (2 * (uint32_t)(t - 1 - (int)p + K))) & km);
+        const uint32_t r2 = ext_pair(et, W, K);
+        ++nl;
+        solid = (r2 & 1) || (t <= ib && (r2 & 2));
+      }
+      if (solid) {
+        dec[i] = p << 8 | kPcNotSuspect;
+        continue;
+      }
+    }
     uint32_t ncand = 0, cb = 0;
     while (surv) {
       const uint32_t alt = (uint32_t)(__ffs((int)surv) - 1);
@@ -875,8 +900,9 @@ __global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ b
       const uint32_t pd = dec[s0 + i];
       const uint32_t p = pd >> 8;
       if ((int)p - last < K) continue;  // a covering K-mer holds a correction: solid
-      ++n_sus;
       const uint8_t d = (uint8_t)pd;
+      if (d == kPcNotSuspect) continue;  // a covering K-mer was solid as read
+      ++n_sus;
       if (d < 4) {
         const uint32_t sh = 2 * (p & 3);
         rd[p >> 2] = (uint8_t)((rd[p >> 2] & ~(3u << sh)) | ((uint32_t)d << sh));
@@ -1031,7 +1057,14 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   }
   APG_CHECK_HIP(hipGetLastError());
   PcCounters* pcnt = reinterpret_cast<PcCounters*>(dcnt);
-  if (ext && weak) {
+  // Without a weak bitmap (ErrorCorrectJump's jump reads, K < 9, a given
+  // solid list) the same three kernels run with every low-quality position a
+  // candidate and the weak test by lookups in the decisions; APG_PC_WAVE=1:
+  // the wave-per-read kernel instead (A/B; C3's 20 M jump reads took 29 ms
+  // there, a dependent chain of lookups per read).
+  const char* pwe = getenv("APG_PC_WAVE");
+  const bool cand3 = ext && (weak || !(pwe && !strcmp(pwe, "1")));
+  if (cand3) {
     // candidates -> independent decisions -> sequential rule per read
     uint32_t* ccnt = nullptr;
     uint64_t* cstart = nullptr;
@@ -1052,14 +1085,15 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     uint64_t ncand = 0;
     PcCand* cand = nullptr;
     bool have = false;
-    const uint64_t cap = ctx->pc_cand_hint;
+    uint64_t& hint = weak ? ctx->pc_cand_hint : ctx->pc_cand_hint_lk;
+    const uint64_t cap = hint;
     if (cap && dr->n_reads) {
       unsigned long long* ctr = nullptr;
       APG_TRY(workspace_t(ctx, "pc_cand_ctr", 1, &ctr));
       APG_CHECK_HIP(hipMemsetAsync(ctr, 0, 8, ctx->stream));
       APG_TRY(workspace_t(ctx, "pc_cand", cap, &cand));
       kbegin(ctx, "pc_cand_write",
-             dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads + 12 * dr->n_reads);
+             dr->n_bases + (weak ? dr->n_bases / 8 : 0) + 8 * dr->n_reads + 12 * dr->n_reads);
       k_pc_candidates<true><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
           dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, nullptr,
           nullptr, cand, cstart, ccnt, ctr, cap);
@@ -1074,7 +1108,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     }
     if (!have) {
       // reads' offsets + quals + weak bits in; tile counts out
-      kbegin(ctx, "pc_candidates", dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads);
+      kbegin(ctx, "pc_candidates", dr->n_bases + (weak ? dr->n_bases / 8 : 0) + 8 * dr->n_reads);
       if (dr->n_reads)
         k_pc_candidates<false><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
             dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak, tcnt,
@@ -1086,8 +1120,8 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       APG_TRY(sync(ctx));
       APG_TRY(workspace_t(ctx, "pc_cand", std::max<uint64_t>(ncand, 1), &cand));
       // reads' offsets + quals + weak bits in; runs and records out
-      kbegin(ctx, "pc_cand_write",
-             dr->n_bases + dr->n_bases / 8 + 8 * dr->n_reads + 12 * dr->n_reads + ncand * sizeof(PcCand));
+      kbegin(ctx, "pc_cand_write", dr->n_bases + (weak ? dr->n_bases / 8 : 0) + 8 * dr->n_reads + 12 * dr->n_reads +
+                                       ncand * sizeof(PcCand));
       if (dr->n_reads)
         k_pc_candidates<true><<<cgrid, kPcTileReads, 0, ctx->stream>>>(
             dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, p.max_q_suspect, weak,
@@ -1096,18 +1130,19 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       APG_CHECK_HIP(hipGetLastError());
     }
     APG_TRY(side_kick(ctx, 2));
-    ctx->pc_cand_hint = ncand + ncand / 4 + 4096;
+    hint = ncand + ncand / 4 + 4096;
     uint32_t* dec = nullptr;
     APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));
     // candidate records in, decisions out (+ 64 B per extension lookup, after the sync)
     APG_TRY(ext_wait());
     kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 4));
     if (ncand)
-      k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups);
+      k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups, !weak);
     kend(ctx);
     // offsets, runs, the candidates' positions and decisions, weak bits in;
     // corrected bases and quals, clean flags out
-    kbegin(ctx, "pc_apply", 16 * dr->n_reads + 8 * dr->n_reads + ncand * 4 + dr->n_bases / 8 + dr->n_reads);
+    kbegin(ctx, "pc_apply",
+           16 * dr->n_reads + 8 * dr->n_reads + ncand * 4 + (weak ? dr->n_bases / 8 + dr->n_reads : 0));
     if (dr->n_reads)
       k_pc_apply<<<grid_for(ctx, dr->n_reads), 256, 0, ctx->stream>>>(
           dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, weak, dec, cstart, ccnt, clean,
