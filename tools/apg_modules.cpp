@@ -545,8 +545,10 @@ int merge_read_sets(Args& a) {
 // .unipaths / .unibases files before any placement.
 void rebuild_graph(Args& a, apg_ctx* c, const std::string& head, int K, Shard* sh, apg_unipath_graph* file_g) {
   a.check(apg_graph_read(head.c_str(), K, file_g), "reading unipath files (run Unipather first)");
-  Reads ub;
-  load_reads(a, head + ".unibases.k" + std::to_string(K), false, &ub);
+  Reads ub;  // <head>.unibases.k<K>: an APG-fastb file under the graph's own name (no .fastb suffix)
+  const std::string ubf = head + ".unibases.k" + std::to_string(K);
+  if (!exists(ubf)) a.fail("missing input " + ubf + " (run Unipather first)");
+  a.check(apg_fastb_read(ubf.c_str(), &ub.r), "reading the unibases");
   apg_unipath_params p;
   apg_unipath_defaults(&p);
   p.K = K;
