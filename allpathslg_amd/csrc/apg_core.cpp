@@ -55,7 +55,7 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
 // reuse.  Nothing is freed while memory suffices (the single-GPU bench never
 // releases).
 static const char* const kStageWs[] = {"big0",    "big1",    "big2",    "x_send",  "x_recv",  "x_pos",  "x_rmask",
-                                       "x_smask", "x_local", "sk_gkey", "sk_gcnt", "sk_cmat", "sk_omat",
+                                       "x_smask", "x_local", "sk_gtab", "sk_cmat", "sk_omat",
                                        "sk_solid_sparse", "sk_dcount"};
 // record descriptors of a count pass: live from the count to its scatter
 static const char* const kDescWs[] = {"sk_desc", "usk_desc"};

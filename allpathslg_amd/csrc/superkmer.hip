@@ -1435,16 +1435,35 @@ __global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __rest
   wave_add(n_kmers, c);
 }
 
-__device__ __forceinline__ void sk_big_add(unsigned long long* __restrict__ gkey, uint32_t* __restrict__ gcnt,
-                                           uint64_t gmask, uint64_t c, uint64_t s, uint32_t add) {
-  for (;;) {
-    const unsigned long long old = atomicCAS(&gkey[s], ~0ull, (unsigned long long)c);
+// The global table of the overflowed buckets: key and count side by side in
+// one 16-byte slot, so a claim and its count add touch one line (separate key
+// and count arrays made every insert and every weak-pass lookup two random
+// lines).  It is sized for the distinct K-mers the instances suggest (a
+// quarter of them, load <= 1/2 at 8 instances per distinct K-mer), not for
+// every instance; a claim that probes kBigProbe slots without finding its key
+// or an empty slot gives up and flags the table, and the host redoes the
+// pass with the table sized for every instance.
+struct BigSlot {
+  unsigned long long key;  // ~0: empty
+  unsigned long long cnt;
+};
+struct BigTab {
+  BigSlot* s;
+  uint64_t mask;
+  unsigned long long* full;  // set when a claim gave up
+};
+constexpr uint32_t kBigProbe = 1024;
+
+__device__ __forceinline__ void sk_big_add(const BigTab& g, uint64_t c, uint64_t s, uint32_t add) {
+  for (uint32_t n = 0; n < kBigProbe; ++n) {
+    const unsigned long long old = atomicCAS(&g.s[s].key, ~0ull, (unsigned long long)c);
     if (old == ~0ull || old == c) {
-      atomicAdd(&gcnt[s], add);
+      atomicAdd(&g.s[s].cnt, (unsigned long long)add);
       return;
     }
-    s = (s + 1) & gmask;
+    s = (s + 1) & g.mask;
   }
+  *g.full = 1;  // crowded: the pass is redone on a larger table
 }
 
 // Instances are first summed in a per-workgroup LDS table, flushed once per
@@ -1460,9 +1479,7 @@ template <typename R, bool UP = false>
 __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                                                              const uint32_t* __restrict__ ovf,
                                                              const uint64_t* __restrict__ opre, uint32_t n_ovf, SkP p,
-                                                             unsigned long long* __restrict__ gkey,
-                                                             uint32_t* __restrict__ gcnt, uint64_t gmask,
-                                                             unsigned long long* __restrict__ inst = nullptr) {
+                                                             BigTab g, unsigned long long* __restrict__ inst = nullptr) {
   unsigned long long n_up = 0;
   constexpr unsigned long long EMPTY = ~0ull;
   __shared__ unsigned long long lkey[kBigLds];
@@ -1502,7 +1519,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
             break;
           }
         }
-        if (!done) sk_big_add(gkey, gcnt, gmask, c, h & gmask, 1u);  // the chunk's LDS table is crowded
+        if (!done) sk_big_add(g, c, h & g.mask, 1u);  // the chunk's LDS table is crowded
       }
     }
     __syncthreads();
@@ -1511,7 +1528,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
     for (uint32_t s = tid; s < kBigLds; s += kBigChunk) {
       const unsigned long long c = lkey[s];
       if (c != EMPTY) {
-        sk_big_add(gkey, gcnt, gmask, c, khash(p.hp, c) & gmask, lcnt[s]);
+        sk_big_add(g, c, khash(p.hp, c) & g.mask, lcnt[s]);
         lkey[s] = EMPTY;
         lcnt[s] = 0;
       }
@@ -1526,8 +1543,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
 template <typename R>
 __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                               const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
-                              SkP p, const unsigned long long* __restrict__ gkey, const uint32_t* __restrict__ gcnt,
-                              uint64_t gmask, uint32_t min_solid, unsigned long long* __restrict__ weak,
+                              SkP p, BigTab g, uint32_t min_solid, unsigned long long* __restrict__ weak,
                               uint32_t* __restrict__ wrec) {
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x) {
@@ -1537,9 +1553,13 @@ __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restr
     uint32_t m = 0;
     for (uint32_t t = 0; t < n; ++t) {
       const uint64_t c = rec_kmer(h, t, p);
-      uint64_t s = khash(p.hp, c) & gmask;
-      while (gkey[s] != c) s = (s + 1) & gmask;
-      if (gcnt[s] < min_solid) m |= 1u << t;
+      uint64_t s = khash(p.hp, c) & g.mask;
+      BigSlot x = g.s[s];
+      while (x.key != c) {
+        s = (s + 1) & g.mask;
+        x = g.s[s];
+      }
+      if (x.cnt < min_solid) m |= 1u << t;
     }
     if (wrec) {
       if (m) wrec[rec_pos(r, p)] = m;
@@ -1557,8 +1577,7 @@ __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restr
 // serialised: 14.7 ms of the repeats line's solid pass).
 constexpr uint32_t kEmitBuf = 2048;
 template <bool SOLID>
-__global__ void __launch_bounds__(256) k_sk_big_emit(const unsigned long long* __restrict__ gkey,
-                                                     const uint32_t* __restrict__ gcnt, uint64_t T, SkP p, SkOut o) {
+__global__ void __launch_bounds__(256) k_sk_big_emit(const BigSlot* __restrict__ gs, uint64_t T, SkP p, SkOut o) {
   __shared__ uint32_t lhist[kSkHistBins];
   __shared__ unsigned long long sbuf[SOLID ? kEmitBuf : 1];
   __shared__ uint32_t scnt;
@@ -1585,11 +1604,12 @@ __global__ void __launch_bounds__(256) k_sk_big_emit(const unsigned long long* _
   unsigned long long nd = 0;
   for (uint64_t s0 = (uint64_t)blockIdx.x * blockDim.x; s0 < T; s0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = s0 + tid;  // block-uniform trip count (the flushes below have barriers)
-    if (s < T && gkey[s] != ~0ull) {
-      const uint32_t c = gcnt[s];
+    const BigSlot x = s < T ? gs[s] : BigSlot{~0ull, 0};
+    if (x.key != ~0ull) {
+      const uint32_t c = (uint32_t)x.cnt;
       sk_spectrum_add(c, lhist, o);
       ++nd;
-      if (SOLID && c >= o.min_solid) sbuf[atomicAdd(&scnt, 1u)] = khash(p.hp, gkey[s]);
+      if (SOLID && c >= o.min_solid) sbuf[atomicAdd(&scnt, 1u)] = khash(p.hp, x.key);
     }
     if constexpr (SOLID) {
       __syncthreads();
@@ -1618,9 +1638,55 @@ __global__ void k_solid_compact(const uint64_t* __restrict__ sparse, const uint3
   }
 }
 
+__global__ void k_big_init(BigSlot* __restrict__ g, uint64_t T) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (uint64_t)gridDim.x * blockDim.x)
+    g[i] = BigSlot{~0ull, 0ull};
+}
+__global__ void k_add_u64(unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ src) {
+  atomicAdd(dst, *src);
+}
+
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
+
+// The overflowed buckets' K-mers (or owned K+1-mers, UP) counted into the
+// global table: first on a table for nbk / 8 distinct K-mers at load <= 1/2,
+// redone on one for every instance if a claim gave up.  inst (UP): the owned
+// instances counted, added once the pass stands.
+template <typename RB, bool UP>
+static int big_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const uint32_t* ovf, const uint64_t* opre,
+                     uint32_t n_ovf, const SkP& p, uint64_t nbk, uint32_t g2, unsigned long long* inst, BigTab* out,
+                     uint64_t* T_out) {
+  unsigned long long *full = nullptr, *binst = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_gfull", 2, &full));
+  binst = full + 1;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    uint64_t T = 1024;
+    const uint64_t want = attempt ? 2 * nbk : nbk / 4;
+    while (T < want) T <<= 1;
+    BigSlot* gs = nullptr;
+    APG_TRY(workspace_t(ctx, "sk_gtab", T, &gs));
+    k_big_init<<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gs, T);
+    APG_CHECK_HIP(hipMemsetAsync(full, 0, 16, ctx->stream));
+    const BigTab g{gs, T - 1, full};
+    k_sk_big_insert<RB, UP><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, UP ? binst : nullptr);
+    APG_CHECK_HIP(hipGetLastError());
+    unsigned long long hf = 0;
+    APG_CHECK_HIP(hipMemcpyAsync(&hf, full, 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    if (!hf) {
+      if (UP && inst) k_add_u64<<<1, 1, 0, ctx->stream>>>(inst, binst);
+      *out = g;
+      *T_out = T;
+      return APG_OK;
+    }
+    vlog(ctx, "sk count: the overflow table of %llu slots is crowded (%llu instances): redone at full size",
+         (unsigned long long)T, (unsigned long long)nbk);
+  }
+  set_error("sk count: overflow table full at one slot per two instances (internal error)");
+  return APG_E_STATE;
+}
 static int sk_ceil_log2(uint64_t x) {
   int b = 0;
   while ((1ull << b) < x) ++b;
@@ -1847,19 +1913,12 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
     unsigned long long nbk = 0;
     APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
-    uint64_t T = 1024;
-    while (T < 2 * nbk) T <<= 1;
-    unsigned long long* gkey = nullptr;
-    uint32_t* gcnt = nullptr;
-    APG_TRY(workspace_t(ctx, "sk_gkey", T, &gkey));
-    APG_TRY(workspace_t(ctx, "sk_gcnt", T, &gcnt));
-    APG_CHECK_HIP(hipMemsetAsync(gkey, 0xff, T * 8, ctx->stream));
-    APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
     vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> global table", hs[1]);
     kbegin(ctx, "sk_bucket_global", nbk * 64);
-    k_sk_big_insert<RB, true><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, p, gkey, gcnt,
-                                                                  T - 1, u.inst);
-    k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, u);
+    BigTab g{};
+    uint64_t T = 0;
+    APG_TRY((big_count<RB, true>(ctx, cur, boff, u.ovf_list, opre, n_ovf, p, nbk, g2, u.inst, &g, &T)));
+    k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, u);
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
@@ -2173,25 +2232,19 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         unsigned long long nbk = 0;
         APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
         APG_TRY(sync(ctx));
-        uint64_t T = 1024;
-        while (T < 2 * nbk) T <<= 1;
-        unsigned long long* gkey = nullptr;
-        uint32_t* gcnt = nullptr;
-        APG_TRY(workspace_t(ctx, "sk_gkey", T, &gkey));
-        APG_TRY(workspace_t(ctx, "sk_gcnt", T, &gcnt));
-        APG_CHECK_HIP(hipMemsetAsync(gkey, 0xff, T * 8, ctx->stream));
-        APG_CHECK_HIP(hipMemsetAsync(gcnt, 0, T * 4, ctx->stream));
         vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
         kbegin(ctx, "sk_bucket_global", nbk * 64);
-        k_sk_big_insert<RB><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1);
+        BigTab g{};
+        uint64_t T = 0;
+        APG_TRY((big_count<RB, false>(ctx, cur, boff, ovf, opre, n_ovf, p, nbk, g2, nullptr, &g, &T)));
         if (solid)
-          k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+          k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
         else
-          k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gkey, gcnt, T, p, o);
+          k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
         if constexpr (RecPos<RB>::value) {
           if (o.weak || o.wrec)
-            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, gkey, gcnt, T - 1, min_solid,
-                                                        o.weak, o.wrec);
+            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o.weak,
+                                                        o.wrec);
         }
         kend(ctx);
         APG_CHECK_HIP(hipGetLastError());
