@@ -1409,17 +1409,23 @@ __global__ void k_sk_ovf_sizes(const uint64_t* __restrict__ boff, const uint32_t
   if (q < n_ovf) sz[q] = (uint32_t)(boff[ovf[q] + 1] - boff[ovf[q]]);
 }
 
-// index of the k-th record of the flattened overflow list
+// index of the k-th record of the flattened overflow list, for k >= k0 where
+// k0 is wave-uniform: the binary search runs on k0 (uniform loads, scalar
+// when the compiler sees it), and each lane steps forward from there — the
+// overflowed buckets hold thousands of records, so rarely more than once.  A
+// per-lane search was a dozen dependent loads per record.
 __device__ __forceinline__ uint64_t sk_ovf_record(const uint64_t* __restrict__ boff, const uint32_t* __restrict__ ovf,
-                                                  const uint64_t* __restrict__ opre, uint32_t n_ovf, uint64_t k) {
-  uint32_t lo = 0, hi = n_ovf;  // last q with opre[q] <= k
+                                                  const uint64_t* __restrict__ opre, uint32_t n_ovf, uint64_t k0,
+                                                  uint64_t k) {
+  uint32_t lo = 0, hi = n_ovf;  // last q with opre[q] <= k0
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (opre[mid] <= k)
+    if (opre[mid] <= k0)
       lo = mid;
     else
       hi = mid;
   }
+  while (lo + 1 < n_ovf && opre[lo + 1] <= k) ++lo;
   return boff[ovf[lo]] + (k - opre[lo]);
 }
 
@@ -1430,8 +1436,10 @@ __global__ void k_sk_big_kmers(const R* __restrict__ rec, const uint64_t* __rest
                                unsigned long long* __restrict__ n_kmers) {
   unsigned long long c = 0;
   const uint64_t tot = opre[n_ovf];
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x)
-    c += rec_nk(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)]) + (UP ? 1u : 0u);
+  for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = k0 + threadIdx.x;
+    if (k < tot) c += rec_nk(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)]) + (UP ? 1u : 0u);
+  }
   wave_add(n_kmers, c);
 }
 
@@ -1495,7 +1503,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
   for (uint64_t k0 = (uint64_t)blockIdx.x * kBigChunk; k0 < tot; k0 += (uint64_t)gridDim.x * kBigChunk) {
     const uint64_t k = k0 + tid;
     if (k < tot) {
-      const SK16 r = rec_head(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)], p);
+      const SK16 r = rec_head(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)], p);
       const uint32_t n = ((uint32_t)(r.w0 >> 32) & 0xff) + (UP ? 1u : 0u);
       for (uint32_t t = 0; t < n; ++t) {
         uint64_t c;
@@ -1546,8 +1554,10 @@ __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restr
                               SkP p, BigTab g, uint32_t min_solid, unsigned long long* __restrict__ weak,
                               uint32_t* __restrict__ wrec) {
   const uint64_t tot = opre[n_ovf];
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < tot; k += (uint64_t)gridDim.x * blockDim.x) {
-    const R r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k)];
+  for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = k0 + threadIdx.x;
+    if (k >= tot) continue;
+    const R r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)];
     const SK16 h = rec_head(r, p);
     const uint32_t n = rec_nk(r);
     uint32_t m = 0;
