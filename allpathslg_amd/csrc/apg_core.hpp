@@ -230,7 +230,6 @@ struct apg_ctx {
   // built by the pass when 2 <= K <= 29: FillFragments reuses it.
   unsigned long long* pc_ext_slot = nullptr;
   uint64_t pc_ext_mask = 0;
-  int pc_ext_mz = 0;  // its ExtTab.mz (minimizer homes)
   bool pc_ext_valid = false;
   uint64_t clean_gen = 0;
   bool clean_valid = false;

@@ -36,54 +36,20 @@ namespace apg {
 
 constexpr uint32_t kFillMaxGap = 63;
 
-// Insert (key, bit) probing linearly from slot s (the first slot of the
-// key's aligned home group or minimizer line: ext_bits reads it whole).
-__device__ __forceinline__ void ext_set_at(const ExtTab& t, uint64_t key, uint32_t bit, uint64_t s) {
+__device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
   const unsigned long long want = (key << 8) | bit;
+  uint64_t s = ext_home(t, key);  // linear from the aligned group (ext_bits reads it whole)
   for (;;) {
     unsigned long long v = t.slot[s];
     if (v == kExtEmpty) {
       v = atomicCAS(&t.slot[s], kExtEmpty, want);
       if (v == kExtEmpty) return;
     }
-    if ((v >> 8) == key && (v & 0xff)) {  // (a minimizer marker carries no bits)
+    if ((v >> 8) == key) {
       if (!(v & bit)) atomicOr(&t.slot[s], (unsigned long long)bit);
       return;
     }
     s = (s + 1) & t.mask;
-  }
-}
-__device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
-  ext_set_at(t, key, bit, ext_home(t, key));
-}
-
-// Minimizer homes (ExtTab.mz): the marker of a large class, once per line.
-__device__ __forceinline__ void ext_mark(const ExtTab& t, uint32_t mzv) {
-  const unsigned long long want = (unsigned long long)mzv << 8;
-  for (uint64_t s = ext_mz_home(t, mzv);; s = (s + 1) & t.mask) {
-    unsigned long long v = t.slot[s];
-    if (v == kExtEmpty) {
-      v = atomicCAS(&t.slot[s], kExtEmpty, want);
-      if (v == kExtEmpty) return;
-    }
-    if (v == want) return;
-  }
-}
-// canonical (K-1)-mer u (or its reverse complement) with one extension bit:
-// the pass counting minimizer classes (cnt != null) or the insert
-__device__ __forceinline__ void ext_mz_put(const ExtTab& t, uint64_t key, uint64_t rkey, uint32_t bit,
-                                           uint32_t* __restrict__ ccount, uint64_t cmask, bool count) {
-  const uint32_t mzv = ext_minimizer(t, key, rkey);
-  uint32_t* cc = &ccount[ext_mix((uint64_t)mzv ^ 0x9e3779b97f4a7c15ull) & cmask];
-  if (count) {
-    atomicAdd(cc, 1u);
-    return;
-  }
-  if (*cc > kMzBig) {
-    ext_mark(t, mzv);
-    ext_set(t, key, bit);
-  } else {
-    ext_set_at(t, key, bit, ext_mz_home(t, mzv));
   }
 }
 
@@ -108,29 +74,6 @@ __global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n
     const uint64_t c = kunhash(hK, solid[i]);
     ext_add_right(t, c >> 2, (uint32_t)(c & 3));
     ext_add_left(t, c & t.m1, (uint32_t)(c >> (2 * t.n1)));
-  }
-}
-
-// Minimizer homes: COUNT = true counts each minimizer class's (K-1)-mer
-// instances (ccount, hashed: colliding classes only look larger); false
-// inserts.  Same (K-1)-mers and bits as k_fill_ext_insert.
-template <bool COUNT>
-__global__ void k_ext_insert_mz(const uint64_t* __restrict__ solid, uint64_t n, HashP hK, ExtTab t,
-                                uint32_t* __restrict__ ccount, uint64_t cmask) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t c = kunhash(hK, solid[i]);
-    const uint64_t u = c >> 2, ur = rc_bases(u, t.n1, t.m1);  // successor (c & 3) of u
-    const uint32_t b = (uint32_t)(c & 3);
-    if (u <= ur)
-      ext_mz_put(t, u, ur, 16u << b, ccount, cmask, COUNT);
-    else
-      ext_mz_put(t, ur, u, 1u << (3 - b), ccount, cmask, COUNT);
-    const uint64_t v = c & t.m1, vr = rc_bases(v, t.n1, t.m1);  // predecessor (c's first base) of v
-    const uint32_t a = (uint32_t)(c >> (2 * t.n1));
-    if (v <= vr)
-      ext_mz_put(t, v, vr, 1u << a, ccount, cmask, COUNT);
-    else
-      ext_mz_put(t, vr, v, 16u << (3 - a), ccount, cmask, COUNT);
   }
 }
 
@@ -160,34 +103,13 @@ int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const
   unsigned long long* slot = nullptr;
   APG_TRY(workspace_t(ctx, ws, T, &slot));
   APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));
-  // APG_EXT_MZ=1: minimizer homes (K - 1 >= 17), read per call
-  const char* mze = getenv("APG_EXT_MZ");
-  const int mz = (mze && !strcmp(mze, "1") && K - 1 >= 17) ? 16 : 0;
-  *out = ExtTab{slot, T - 1, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1, mz};
-  uint32_t* ccount = nullptr;
-  uint64_t C = 1024;
-  if (mz) {  // class counts: one counter per solid K-mer, so that classes rarely share one
-    while (C < n_solid) C <<= 1;
-    APG_TRY(workspace_t(ctx, "ext_mzcount", C, &ccount));
-    APG_CHECK_HIP(hipMemsetAsync(ccount, 0, C * 4, ctx->stream));
-  }
+  *out = ExtTab{slot, T - 1, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1};
   kbegin(ctx, kname, n_solid * (8 + 2 * 64));
-  if (n_solid && mz) {
-    k_ext_insert_mz<true><<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out, ccount,
-                                                                            C - 1);
-    k_ext_insert_mz<false><<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out, ccount,
-                                                                             C - 1);
-  } else if (n_solid) {
+  if (n_solid)
     k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out);
-  }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;
-}
-
-ExtTab ext_last(apg_ctx* ctx, int K) {
-  return ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1,
-                ctx->pc_ext_mz};
 }
 
 // 32 bases [pos, pos+32) of a packed read as an LSB-first word (base pos at
@@ -214,7 +136,6 @@ __device__ __forceinline__ uint64_t fwin(const uint8_t* B, uint32_t Lf, uint32_t
 // Every K-mer of a packed read (L >= K) solid: one extension lookup per
 // K-mer (its first K-1 bases hold its last base as a successor).  Bases are
 // streamed 32 at a time from one LSB-first word.
-template <bool MZ>
 __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, uint32_t L, uint32_t* nlook) {
   const int n1 = t.n1;
   uint64_t buf = bases32(R, 0);
@@ -222,7 +143,7 @@ __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, ui
   for (uint32_t i = n1; i < L; ++i) {
     if ((i & 31) == 0) buf = bases32(R, i);
     const uint32_t b = (uint32_t)(((i & 31) == 0 ? buf : buf >> (2 * (i & 31))) & 3);
-    if (!((ext_succ<MZ>(t, w, nlook) >> b) & 1)) return false;
+    if (!((ext_succ(t, w, nlook) >> b) & 1)) return false;
     w = ((w << 2) | b) & t.m1;
   }
   return true;
@@ -231,13 +152,12 @@ __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, ui
 // Both reads of a pair solid throughout.  cl (or null): the pair's clean
 // flags from the correction pass that used this solid set (1 clean, 0 not,
 // 2 not derived -> look the read's K-mers up).
-template <bool MZ>
 __device__ __forceinline__ bool pair_solid(const ExtTab& t, const uint8_t* A, uint32_t La, const uint8_t* B,
                                            uint32_t Lf, const uint8_t* cl, uint32_t* nlook) {
   const uint32_t fa = cl ? cl[0] : 2u, fb = cl ? cl[1] : 2u;
   if (fa == 0 || fb == 0) return false;
-  if (fa == 2 && !read_solid<MZ>(t, A, La, nlook)) return false;
-  if (fb == 2 && !read_solid<MZ>(t, B, Lf, nlook)) return false;
+  if (fa == 2 && !read_solid(t, A, La, nlook)) return false;
+  if (fb == 2 && !read_solid(t, B, Lf, nlook)) return false;
   return true;
 }
 
@@ -293,7 +213,6 @@ constexpr int kFillRefill = 32;
 // (wave-aggregated fetch from *next), so a wave is no longer held by its
 // slowest pair.  Per lane the lookups, their order and the result are the
 // same as the nested search (oracle/fill_oracle.c).
-template <bool MZ>
 __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
                                               uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
@@ -391,7 +310,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
       emit(kFillSkip, FillRec{0, 0, 0, kFillSkip});
       return;
     }
-    if (!pair_solid<MZ>(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
+    if (!pair_solid(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
       emit(kFillNone, FillRec{0, 0, 0, kFillNone});  // S must be a path of solid K-mers
       return;
     }
@@ -443,7 +362,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
             uint64_t w = atail;
             for (uint32_t jj = 0; jj + o + 2 <= (uint32_t)K && match; ++jj) {
               const uint32_t b = (uint32_t)(f0 >> (2 * (o + jj))) & 3;
-              match = (ext_succ<MZ>(t, w, &nlook) >> b) & 1;
+              match = (ext_succ(t, w, &nlook) >> b) & 1;
               w = ((w << 2) | b) & t.m1;
             }
           }
@@ -506,7 +425,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
                          : mode == 1 ? ww
                          : mode == 2 ? walk_window(atail, pv >> (2 * (d - dd)), dd, t)
                                      : bkey;
-    const uint32_t m = cached ? mask_at(dd) : ext_succ<MZ>(t, key, &nlook);
+    const uint32_t m = cached ? mask_at(dd) : ext_succ(t, key, &nlook);
     bool visit = false, done = false;
     if (mode == 0) {  // node (pv, d)
       mnode = m;
@@ -731,7 +650,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
       if (ctx->clean_valid && ctx->clean_gen == dr->gen) clean = ctx->pc_clean;
       // ... and the pass's extension table is this very solid set's
       if (ctx->pc_ext_valid) {
-        et = ext_last(ctx, p.K);
+        et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
         have_ext = true;
       }
     } else {  // the pairs' own solid K-mers
@@ -772,8 +691,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   if (np) {
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
     // lanes are persistent (work fetched per wave): one resident round of blocks
-    const uint32_t grid = et.mz ? resident_grid(ctx, k_fill<true>, 256, (np + 255) / 256)
-                                : resident_grid(ctx, k_fill<false>, 256, (np + 255) / 256);
+    const uint32_t grid = resident_grid(ctx, k_fill, 256, (np + 255) / 256);
     // APG_FILL_BRANCH_CACHE=0: backtracks look their branch point up again (A/B)
     const char* be = getenv("APG_FILL_BRANCH_CACHE");
     const bool bcache = !(be && !strcmp(be, "0"));
@@ -782,13 +700,12 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     const bool bfilt = !(bfe && !strcmp(bfe, "0"));
     const char* rfe = getenv("APG_FILL_REFILL");
     const int refill = rfe ? std::max(0, std::min(63, atoi(rfe))) : kFillRefill;
-    auto kf = et.mz ? k_fill<true> : k_fill<false>;
-    kf<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
-                                      std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer, ndefer + 1,
-                                      bcache, bfilt, refill);
+    k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
+                                          std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
+                                          ndefer + 1, bcache, bfilt, refill);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
-      kf<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps, defer,
-                                        ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill);
+      k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

@@ -222,9 +222,8 @@ __device__ __forceinline__ uint64_t ext_window(uint32_t word, uint32_t i, int K,
 // K-mers i-1 (a read K-mer iff i >= 1) and i of the window W = ext_window(i):
 // bit 0 = K-mer i-1 solid (pred of (K-1)-mer i holds base i-1), bit 1 = K-mer
 // i solid (succ holds base i+K-1).  One extension-table lookup.
-template <bool MZ>
 __device__ __forceinline__ uint32_t ext_pair(const ExtTab& t, uint64_t W, int K) {
-  const uint32_t e = ext_masks_lsb<MZ>(t, (W >> 2) & t.m1);
+  const uint32_t e = ext_masks_lsb(t, (W >> 2) & t.m1);
   const uint32_t pb = (uint32_t)W & 3, sb = (uint32_t)(W >> (2 * K)) & 3;
   return ((e >> pb) & 1) | (((e >> (4 + sb)) & 1) << 1);
 }
@@ -294,7 +293,7 @@ __device__ __forceinline__ PcData pc_data(const PcMeta& m, const uint8_t* __rest
 // take half the lookups, and the first and last covering K-mers of a suspect
 // (the (K-1)-mers beside p do not contain p) are answered for all 4 bases at
 // p by two lookups, before any alternative is tried.
-template <bool EXT, bool MZ = false>
+template <bool EXT>
 __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restrict__ base_off,
                                                          const uint64_t* __restrict__ byte_off,
                                                          uint8_t* __restrict__ packed, uint8_t* __restrict__ quals,
@@ -369,7 +368,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           const uint64_t Wk = ext_window(word, i, K, ~0u, 0);
           bool solid = false;
           if ((uint32_t)lane < G) {
-            const uint32_t r2 = ext_pair<MZ>(et, Wk, K);
+            const uint32_t r2 = ext_pair(et, Wk, K);
             solid = (r2 & 1) || (i <= jhi && (r2 & 2));
           }
           n_look += G;
@@ -394,7 +393,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
           const uint64_t WA = ext_window(word, iA, K, ~0u, 0);
           uint32_t mA = 15;
           if ((lane == 0 && hasA) || (lane == 1 && hasB)) {
-            const uint32_t e = ext_masks_lsb<MZ>(et, (WA >> 2) & et.m1);
+            const uint32_t e = ext_masks_lsb(et, (WA >> 2) & et.m1);
             mA = lane == 0 ? e >> 4 : e & 15;
           }
           const uint32_t allowed = (uint32_t)__shfl((int)mA, 0, 64) & (uint32_t)__shfl((int)mA, 1, 64);
@@ -418,7 +417,7 @@ __global__ void __launch_bounds__(256) k_precorrect_wave(const uint64_t* __restr
             const uint64_t WB = ext_window(word, i, K, p, alt);
             bool bad = false;
             if (act) {
-              const uint32_t r2 = ext_pair<MZ>(et, WB, K);
+              const uint32_t r2 = ext_pair(et, WB, K);
               bad = !(r2 & 1) || ((int)i <= ib && !(r2 & 2));
             }
             const uint64_t badm = __ballot(bad);
@@ -808,7 +807,6 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
 // not all weak — by extension lookups on the read as it was, the state the
 // sequential rule sees unless a correction lies within K before it — is
 // kPcNotSuspect.
-template <bool MZ>
 __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ cand, uint64_t n, int K, ExtTab et,
                                                    uint32_t* __restrict__ dec, unsigned long long* __restrict__ looks,
                                                    bool wtest) {
@@ -824,11 +822,11 @@ __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ ca
     // for all 4 bases at p: succ of bases [p-K+1, p) and pred of [p+1, p+K)
     uint32_t mA = 15, mB = 15;
     if (hasA) {
-      mA = ext_masks_lsb<MZ>(et, (uint64_t)(win >> 2) & et.m1) >> 4;
+      mA = ext_masks_lsb(et, (uint64_t)(win >> 2) & et.m1) >> 4;
       ++nl;
     }
     if (hasB) {
-      mB = ext_masks_lsb<MZ>(et, (uint64_t)(win >> (2 * K + 2)) & et.m1) & 15;
+      mB = ext_masks_lsb(et, (uint64_t)(win >> (2 * K + 2)) & et.m1) & 15;
       ++nl;
     }
     const uint32_t allowed = mA & mB;
@@ -843,7 +841,7 @@ __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ ca
       bool solid = (hasA && ((mA >> orig) & 1)) || (hasB && ((mB >> orig) & 1));
       for (int t = ia + 1; t <= ib + 1 && !solid; t += 2) {
         const uint64_t W = (uint64_t)((win >> (2 * (uint32_t)(t - 1 - (int)p + K))) & km);
-        const uint32_t r2 = ext_pair<MZ>(et, W, K);
+        const uint32_t r2 = ext_pair(et, W, K);
         ++nl;
         solid = (r2 & 1) || (t <= ib && (r2 & 2));
       }
@@ -862,7 +860,7 @@ __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ ca
         // (K-1)-mer j with its pred base j-1 and succ base j+K-1: window bits
         // from base j-1 = p-K + (j-1-p+K)
         const uint64_t W = (uint64_t)((wa >> (2 * (uint32_t)(j - 1 - (int)p + K))) & km);
-        const uint32_t r2 = ext_pair<MZ>(et, W, K);
+        const uint32_t r2 = ext_pair(et, W, K);
         ++nl;
         ok = (r2 & 1) && (j > ib || (r2 & 2));
       }
@@ -1029,7 +1027,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     return APG_OK;
   };
   if (ext && !weak && ext_reuse) {
-    et = ext_last(ctx, p.K);
+    et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
   } else if (ext && !weak) {
     APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
   } else if (ext) {
@@ -1139,8 +1137,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     APG_TRY(ext_wait());
     kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 4));
     if (ncand)
-      (et.mz ? k_pc_decide<true> : k_pc_decide<false>)<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(
-          cand, ncand, p.K, et, dec, &pcnt->lookups, !weak);
+      k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups, !weak);
     kend(ctx);
     // offsets, runs, the candidates' positions and decisions, weak bits in;
     // corrected bases and quals, clean flags out
@@ -1156,8 +1153,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     kbegin(ctx, "precorrect", dr->n_bytes + dr->n_bases + (weak ? dr->n_bases / 8 + dr->n_reads : 0));
     if (dr->n_reads) {
       if (ext)
-        (et.mz ? k_precorrect_wave<true, true> : k_precorrect_wave<true, false>)<<<grid_for(ctx, dr->n_reads, 4), 256, 0,
-                                                                                 ctx->stream>>>(
+        k_precorrect_wave<true><<<grid_for(ctx, dr->n_reads, 4), 256, 0, ctx->stream>>>(
             dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->d_quals, dr->n_reads, p.K, hp, p.max_q_suspect, ss, et,
             weak, clean, reinterpret_cast<PcCounters*>(dcnt));
       else
@@ -1195,7 +1191,6 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   if (ext) {
     ctx->pc_ext_slot = et.slot;
     ctx->pc_ext_mask = et.mask;
-    ctx->pc_ext_mz = et.mz;
     ctx->pc_ext_valid = true;
   }
   vlog(ctx, "precorrect pass: solid=%llu suspect=%llu corrected=%llu ambiguous=%llu none=%llu",
@@ -1270,7 +1265,6 @@ struct EcjReads {
   uint64_t n_reads;
 };
 
-template <bool MZ>
 __global__ void __launch_bounds__(256) k_ecj_trim(EcjReads rv, ExtTab et, int K, uint32_t min_keep,
                                                   uint32_t* __restrict__ keep, unsigned long long* __restrict__ cnt) {
   uint64_t n_full = 0, n_trim = 0, n_drop = 0, kept = 0, looks = 0;
@@ -1291,7 +1285,7 @@ __global__ void __launch_bounds__(256) k_ecj_trim(EcjReads rv, ExtTab et, int K,
       uint32_t i = 0;
       for (; i < nk; i += 2) {
         ++looks;
-        const uint32_t m = ext_masks_lsb<MZ>(et, y);
+        const uint32_t m = ext_masks_lsb(et, y);
         if (!(m & (1u << base(i)))) break;
         if (i + 1 >= nk) {
           i = nk;
@@ -1356,7 +1350,7 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   APG_TRY(correct_pass(ctx, jr, p, sr.solid, sr.n_solid, &st->pc));
   ExtTab et{};
   if (ctx->pc_ext_valid && ctx->pc_list == sr.solid && ctx->pc_K == e.K)
-    et = ext_last(ctx, e.K);
+    et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(e.K - 1), (1ull << (2 * (e.K - 1))) - 1, e.K - 1};
   else
     APG_TRY(ext_build(ctx, sr.solid, sr.n_solid, e.K, "ecj_ext", "ecj_ext", &et));
   unsigned long long* cnt = nullptr;
@@ -1364,7 +1358,7 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   APG_CHECK_HIP(hipMemsetAsync(cnt, 0, 5 * 8, ctx->stream));
   kbegin(ctx, "ecj_trim", jr->n_bytes + 20 * jr->n_reads);
   if (jr->n_reads)
-    (et.mz ? k_ecj_trim<true> : k_ecj_trim<false>)<<<grid_for(ctx, jr->n_reads), 256, 0, ctx->stream>>>(
+    k_ecj_trim<<<grid_for(ctx, jr->n_reads), 256, 0, ctx->stream>>>(
         EcjReads{jr->d_base_off, jr->d_byte_off, jr->d_packed, jr->n_reads}, et, e.K, e.min_keep, d_keep, cnt);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
