@@ -24,6 +24,9 @@ import sys
 # SK16 spectrum and SK24 solid-set launches: launches add too).
 KERNELS = [
     ("void apg::k_sk_bucket_dd<true, apg::SK24>", "sk_bucket_solid", "stream"),
+    ("void apg::k_sk_bucket_dd<true, apg::SKP>", "sk_bucket_solid", "stream"),  # round 4: packed records read directly
+    ("void apg::k_sk_bucket<true, apg::SKP>", "sk_bucket_solid", "stream"),
+    ("void apg::k_sk_bucket<false, apg::SKP>", "sk_bucket", "stream"),  # the fused K+1 pass on packed records
     ("void apg::k_sk_bucket<true, apg::SK24>", "sk_bucket_solid", "stream"),
     ("void apg::k_sk_bucket<false, apg::SK16>", "sk_bucket", "stream"),
     ("void apg::k_sk_bucket<false, apg::SK24>", "sk_bucket", "stream"),  # the fused K+1 pass (UP)
@@ -57,6 +60,8 @@ KERNELS = [
     ("apg::k_usk_count", "usk_count", "stream"),
     ("apg::k_usk_scatter", "usk_scatter", "stream"),
     ("apg::k_usk_bucket", "usk_bucket", "stream"),
+    ("void apg::k_usk_bucket<1024u>", "usk_bucket", "stream"),  # round 4: table size (and waves) as template arguments
+    ("void apg::k_usk_bucket<512u>", "usk_bucket", "stream"),
     ("void apg::k_part_scatter<apg::SK48>", "usk_part_scatter", "stream"),
     ("apg::k_links", "u_links", "random"),
     ("apg::k_walk", "u_walk", "random"),
