@@ -36,11 +36,11 @@ namespace apg {
 
 constexpr uint32_t kFillMaxGap = 63;
 
-__device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
+// (key, bit) from slot s on, v = slot s as already read
+__device__ __forceinline__ void ext_set_from(const ExtTab& t, uint64_t key, uint32_t bit, uint64_t s,
+                                             unsigned long long v) {
   const unsigned long long want = (key << 8) | bit;
-  uint64_t s = ext_home(t, key);  // linear from the aligned group (ext_bits reads it whole)
   for (;;) {
-    unsigned long long v = t.slot[s];
     if (v == kExtEmpty) {
       v = atomicCAS(&t.slot[s], kExtEmpty, want);
       if (v == kExtEmpty) return;
@@ -50,30 +50,32 @@ __device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t 
       return;
     }
     s = (s + 1) & t.mask;
+    v = t.slot[s];
   }
 }
-
-// successor bit b of (K-1)-mer u (MSB-first value) / predecessor bit a
-__device__ __forceinline__ void ext_add_right(const ExtTab& t, uint64_t u, uint32_t b) {
-  const uint64_t r = rc_bases(u, t.n1, t.m1);
-  if (u <= r)
-    ext_set(t, u, 16u << b);
-  else
-    ext_set(t, r, 1u << (3 - b));
-}
-__device__ __forceinline__ void ext_add_left(const ExtTab& t, uint64_t u, uint32_t a) {
-  const uint64_t r = rc_bases(u, t.n1, t.m1);
-  if (u <= r)
-    ext_set(t, u, 1u << a);
-  else
-    ext_set(t, r, 16u << (3 - a));
+__device__ __forceinline__ void ext_set(const ExtTab& t, uint64_t key, uint32_t bit) {
+  const uint64_t s = ext_home(t, key);  // linear from the aligned group (ext_bits reads it whole)
+  ext_set_from(t, key, bit, s, t.slot[s]);
 }
 
+// A solid K-mer's two (K-1)-mers: both home slots read before either is
+// resolved (two table lines in flight per lane instead of one).
 __global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n, HashP hK, ExtTab t) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t c = kunhash(hK, solid[i]);
-    ext_add_right(t, c >> 2, (uint32_t)(c & 3));
-    ext_add_left(t, c & t.m1, (uint32_t)(c >> (2 * t.n1)));
+    // successor c & 3 of u = c >> 2; predecessor (c's first base) of v = c & m1
+    const uint64_t u = c >> 2, ur = rc_bases(u, t.n1, t.m1);
+    const uint32_t b = (uint32_t)(c & 3);
+    const uint64_t ku = u <= ur ? u : ur;
+    const uint32_t bu = u <= ur ? 16u << b : 1u << (3 - b);
+    const uint64_t v = c & t.m1, vr = rc_bases(v, t.n1, t.m1);
+    const uint32_t a = (uint32_t)(c >> (2 * t.n1));
+    const uint64_t kv = v <= vr ? v : vr;
+    const uint32_t bv = v <= vr ? 1u << a : 16u << (3 - a);
+    const uint64_t su = ext_home(t, ku), sv = ext_home(t, kv);
+    const unsigned long long xu = t.slot[su], xv = t.slot[sv];
+    ext_set_from(t, ku, bu, su, xu);
+    ext_set_from(t, kv, bv, sv, xv);
   }
 }
 
