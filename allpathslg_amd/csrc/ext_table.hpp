@@ -11,7 +11,19 @@
 // the (K-1)-mer between them) or all 4 successors of a walk node, where a hash
 // set of K-mers needs one lookup per K-mer.  Linear probing, load <= 0.25
 // (table = 4 slots per solid K-mer): nearly every lookup is one 64-byte line.
+//
+// Two-level slots (K <= 25, the default; APG_EXT_TWO=0 for the one-level
+// layout): key << 16 | pp << 12 | ss << 8 | succ << 4 | pred, where ss is the
+// successor mask of the (K-1)-mer's successor when it has exactly one, and pp
+// the predecessor mask of its predecessor when it has exactly one (a link pass
+// after the inserts, k_ext_link).  A walk through a non-branching (K-1)-mer
+// learns its next node's successors with it, so along a path every other node
+// needs no lookup of its own (tools/fill_walk_model.c: 43 % fewer FillFragments
+// lookups on the repeat-rich genome).
 #pragma once
+
+#include <cstdlib>
+#include <cstring>
 
 #include <hip/hip_runtime.h>
 
@@ -53,7 +65,20 @@ struct ExtTab {
   HashP h1;  // slot hash of canonical (K-1)-mers
   uint64_t m1;
   int n1;  // K-1
+  int ks;  // key shift: 16 with the two-level bits, 8 without
 };
+
+// The slot layout for K (the builder and every reuse of a built table agree).
+inline bool ext_two_level(int K) {
+  static const bool on = [] {
+    const char* e = getenv("APG_EXT_TWO");
+    return !(e && !strcmp(e, "0"));
+  }();
+  return on && 2 * (K - 1) + 16 <= 64;
+}
+inline ExtTab ext_tab(unsigned long long* slot, uint64_t mask, int K) {
+  return ExtTab{slot, mask, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1, ext_two_level(K) ? 16 : 8};
+}
 
 // Probing starts at the first slot of the key's aligned group of kExtGrp
 // slots (32 bytes) and runs linearly from there, so a lookup reads the group
@@ -66,7 +91,8 @@ __device__ __forceinline__ uint64_t ext_home(const ExtTab& t, uint64_t c) {
   return khash(t.h1, c) & t.mask & ~(kExtGrp - 1);
 }
 
-// The 8 extension bits of canonical (K-1)-mer c (0 if absent).
+// The extension bits of canonical (K-1)-mer c (0 if absent): pred | succ << 4,
+// and with two-level slots ss << 8 | pp << 12.
 __device__ __forceinline__ uint32_t ext_bits(const ExtTab& t, uint64_t c) {
   uint64_t g = ext_home(t, c);
   for (;;) {
@@ -76,7 +102,7 @@ __device__ __forceinline__ uint32_t ext_bits(const ExtTab& t, uint64_t c) {
 #pragma unroll
     for (uint32_t j = 0; j < kExtGrp; ++j) {
       if (v[j] == kExtEmpty) return 0;
-      if ((v[j] >> 8) == c) return (uint32_t)(v[j] & 0xff);
+      if ((v[j] >> t.ks) == c) return (uint32_t)(v[j] & ((1u << t.ks) - 1));
     }
     g = (g + kExtGrp) & t.mask;
   }
@@ -88,9 +114,23 @@ __device__ __forceinline__ uint32_t ext_succ(const ExtTab& t, uint64_t w, uint32
   const uint32_t e = ext_bits(t, w < r ? w : r);
   ++*nlook;
   uint32_t m = 0;
-  if (w <= r) m |= e >> 4;
+  if (w <= r) m |= (e >> 4) & 15;
   if (r <= w) m |= rev4(e & 15);
   return m;
+}
+
+// ext_succ | ss << 4 | 256 when ss is known: w has exactly one successor
+// and the table is two-level (palindromes excepted: their two orientations
+// share one slot).
+__device__ __forceinline__ uint32_t ext_succ2(const ExtTab& t, uint64_t w, uint32_t* nlook) {
+  const uint64_t r = rc_bases(w, t.n1, t.m1);
+  const uint32_t e = ext_bits(t, w < r ? w : r);
+  ++*nlook;
+  uint32_t m = 0, x = 0;
+  if (w <= r) m |= (e >> 4) & 15, x = (e >> 8) & 15;
+  if (r <= w) m |= rev4(e & 15), x = rev4((e >> 12) & 15);
+  const bool ok = t.ks == 16 && w != r && __popc(m) == 1;
+  return m | (ok ? (x << 4) | 256u : 0u);
 }
 
 // Predecessor (bits 0-3) and successor (bits 4-7) masks, in read
@@ -102,13 +142,92 @@ __device__ __forceinline__ uint32_t ext_masks_lsb(const ExtTab& t, uint64_t y) {
   const uint64_t rc = y ^ t.m1;
   const uint32_t e = ext_bits(t, fw < rc ? fw : rc);
   uint32_t m = 0;
-  if (fw <= rc) m |= e;
-  if (rc <= fw) m |= rev4(e >> 4) | (rev4(e & 15) << 4);
+  if (fw <= rc) m |= e & 0xff;
+  if (rc <= fw) m |= rev4((e >> 4) & 15) | (rev4(e & 15) << 4);
+  return m;
+}
+
+// ext_masks_lsb | ss << 8 | pp << 12 in read orientation, bit 16 when ss is
+// known (exactly one successor), bit 17 when pp is (exactly one predecessor).
+__device__ __forceinline__ uint32_t ext_masks2_lsb(const ExtTab& t, uint64_t y) {
+  const uint64_t fw = f_rev2(y) >> (64 - 2 * t.n1);
+  const uint64_t rc = y ^ t.m1;
+  const uint32_t e = ext_bits(t, fw < rc ? fw : rc);
+  uint32_t m = e;
+  if (rc < fw) m = rev4((e >> 4) & 15) | (rev4(e & 15) << 4) | (rev4((e >> 12) & 15) << 8) | (rev4((e >> 8) & 15) << 12);
+  if (t.ks != 16 || fw == rc) return m & 0xff;
+  return m | (__popc((m >> 4) & 15) == 1 ? 1u << 16 : 0u) | (__popc(m & 15) == 1 ? 1u << 17 : 0u);
+}
+
+// A lookup split in two, so that a lane can have several in flight: issue
+// reads the home group of an LSB-first (K-1)-mer (ext_masks_lsb's argument),
+// finish scans it (and probes on in the rare case the group holds neither
+// the key nor an empty slot) and returns ext_masks_lsb's value.  Independent
+// lookups issued together cost about one round trip, not one each.
+struct ExtProbe {
+  uint64_t c, g;
+  ulonglong2 a, b;
+  bool fw, rc;  // the (K-1)-mer is its own canonical form / its reverse complement is
+};
+__device__ __forceinline__ ExtProbe ext_issue_lsb(const ExtTab& t, uint64_t y) {
+  ExtProbe p;
+  const uint64_t fw = f_rev2(y) >> (64 - 2 * t.n1);
+  const uint64_t rc = y ^ t.m1;
+  p.fw = fw <= rc;
+  p.rc = rc <= fw;
+  p.c = fw < rc ? fw : rc;
+  p.g = ext_home(t, p.c);
+  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t.slot + p.g);
+  p.a = q[0];
+  p.b = q[1];
+  return p;
+}
+__device__ __forceinline__ uint32_t ext_finish(const ExtTab& t, const ExtProbe& p) {
+  uint32_t e = 0;
+  const unsigned long long v[kExtGrp] = {p.a.x, p.a.y, p.b.x, p.b.y};
+  bool done = false;
+#pragma unroll
+  for (uint32_t j = 0; j < kExtGrp; ++j) {
+    if (done) continue;
+    if (v[j] == kExtEmpty) {
+      done = true;
+    } else if ((v[j] >> t.ks) == p.c) {
+      e = (uint32_t)(v[j] & 0xff);
+      done = true;
+    }
+  }
+  if (!done) {  // the group is full of other keys: on from the next group
+    uint64_t g = (p.g + kExtGrp) & t.mask;
+    for (;;) {
+      const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t.slot + g);
+      const ulonglong2 a = q[0], b = q[1];
+      const unsigned long long w[kExtGrp] = {a.x, a.y, b.x, b.y};
+      bool hit = false;
+#pragma unroll
+      for (uint32_t j = 0; j < kExtGrp; ++j) {
+        if (hit) continue;
+        if (w[j] == kExtEmpty) {
+          hit = true;
+        } else if ((w[j] >> t.ks) == p.c) {
+          e = (uint32_t)(w[j] & 0xff);
+          hit = true;
+        }
+      }
+      if (hit) break;
+      g = (g + kExtGrp) & t.mask;
+    }
+  }
+  uint32_t m = 0;
+  if (p.fw) m |= e;
+  if (p.rc) m |= rev4(e >> 4) | (rev4(e & 15) << 4);
   return m;
 }
 
 // Build the extension table of a solid list (khash(K) of canonical K-mers) in
-// workspace `ws` (2 <= K <= 29); asynchronous on ctx->stream.
+// workspace `ws` (2 <= K <= 29); asynchronous on ctx->stream.  link = false
+// leaves the two-level bits to a later ext_link (readers of the pred / succ
+// bits alone may run beside that pass: it writes only bits 8-15).
 int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const char* ws, const char* kname,
-              ExtTab* out);
+              ExtTab* out, bool link = true);
+int ext_link(apg_ctx* ctx, const ExtTab& t, uint64_t n_solid);
 }  // namespace apg

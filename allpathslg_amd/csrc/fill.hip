@@ -39,13 +39,13 @@ constexpr uint32_t kFillMaxGap = 63;
 // (key, bit) from slot s on, v = slot s as already read
 __device__ __forceinline__ void ext_set_from(const ExtTab& t, uint64_t key, uint32_t bit, uint64_t s,
                                              unsigned long long v) {
-  const unsigned long long want = (key << 8) | bit;
+  const unsigned long long want = (key << t.ks) | bit;
   for (;;) {
     if (v == kExtEmpty) {
       v = atomicCAS(&t.slot[s], kExtEmpty, want);
       if (v == kExtEmpty) return;
     }
-    if ((v >> 8) == key) {
+    if ((v >> t.ks) == key) {
       if (!(v & bit)) atomicOr(&t.slot[s], (unsigned long long)bit);
       return;
     }
@@ -79,8 +79,48 @@ __global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n
   }
 }
 
+// Two-level bits of every occupied slot (ext_table.hpp): the successor mask
+// of its unique successor and the predecessor mask of its unique
+// predecessor, both lookups in flight together.  The inserts are complete,
+// so the pred / succ bits every lookup here reads are final; the store
+// changes only bits 8-15 of the slot's low word.
+__global__ void k_ext_link(ExtTab t) {
+  const int n1 = t.n1;
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= t.mask;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long v = t.slot[s];
+    if (v == kExtEmpty) continue;
+    const uint64_t c = v >> 16;
+    const uint32_t P = (uint32_t)v & 15, S = (uint32_t)(v >> 4) & 15;
+    const bool us = __popc(S) == 1, up = __popc(P) == 1;
+    if (!(us || up) || c == rc_bases(c, n1, t.m1)) continue;
+    // LSB-first forms (ext_issue_lsb's argument) of the successor and the
+    // predecessor, in c's orientation
+    const uint64_t y = f_rev2(c) >> (64 - 2 * n1);
+    const uint64_t ys = (y >> 2) | ((uint64_t)(us ? __ffs(S) - 1 : 0) << (2 * (n1 - 1)));
+    const uint64_t yp = ((y << 2) & t.m1) | (uint64_t)(up ? __ffs(P) - 1 : 0);
+    ExtProbe qs, qp;
+    if (us) qs = ext_issue_lsb(t, ys);
+    if (up) qp = ext_issue_lsb(t, yp);
+    const uint32_t ss = us ? (ext_finish(t, qs) >> 4) & 15 : 0u;
+    const uint32_t pp = up ? ext_finish(t, qp) & 15 : 0u;
+    if (ss | pp) t.slot[s] = v | ((unsigned long long)ss << 8) | ((unsigned long long)pp << 12);
+  }
+}
+
+int ext_link(apg_ctx* ctx, const ExtTab& t, uint64_t n_solid) {
+  if (t.ks != 16 || !n_solid) return APG_OK;
+  // algorithmic bytes: the table read + ~2 (K-1)-mers per solid K-mer, each
+  // with two 32-byte group reads and its slot written back
+  kbegin(ctx, "ext_link", (t.mask + 1) * 8 + n_solid * (2 * 64 + 8));
+  k_ext_link<<<grid_for(ctx, t.mask + 1), 256, 0, ctx->stream>>>(t);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
 int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const char* ws, const char* kname,
-              ExtTab* out) {
+              ExtTab* out, bool link) {
   // 4 slots per solid K-mer: load <= 0.5 even if no two solid K-mers share a
   // (K-1)-mer, ~0.25 on a genome, so nearly every lookup ends in the home
   // group.  When that does not fit the device (human-scale replicated solid
@@ -105,13 +145,13 @@ int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const
   unsigned long long* slot = nullptr;
   APG_TRY(workspace_t(ctx, ws, T, &slot));
   APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));
-  *out = ExtTab{slot, T - 1, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1};
+  *out = ext_tab(slot, T - 1, K);
   kbegin(ctx, kname, n_solid * (8 + 2 * 64));
   if (n_solid)
     k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
-  return APG_OK;
+  return link ? ext_link(ctx, *out, n_solid) : APG_OK;
 }
 
 // 32 bases [pos, pos+32) of a packed read as an LSB-first word (base pos at
@@ -142,10 +182,19 @@ __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, ui
   const int n1 = t.n1;
   uint64_t buf = bases32(R, 0);
   uint64_t w = f_rev2(buf & lmask(n1)) >> (64 - 2 * n1);  // first K-1 bases, MSB-first
+  uint32_t pend = 0;  // the next (K-1)-mer's successors from a two-level slot | 16
   for (uint32_t i = n1; i < L; ++i) {
     if ((i & 31) == 0) buf = bases32(R, i);
     const uint32_t b = (uint32_t)(((i & 31) == 0 ? buf : buf >> (2 * (i & 31))) & 3);
-    if (!((ext_succ(t, w, nlook) >> b) & 1)) return false;
+    uint32_t m = pend & 15;
+    if (!(pend & 16)) {
+      const uint32_t x = ext_succ2(t, w, nlook);
+      m = x & 15;
+      pend = x >> 4;
+    } else {
+      pend = 0;
+    }
+    if (!((m >> b) & 1)) return false;
     w = ((w << 2) | b) & t.m1;
   }
   return true;
@@ -204,6 +253,12 @@ constexpr uint32_t kFillCap1 = 96;
 // are still walking (APG_FILL_REFILL for A/B: a higher mark keeps more lanes
 // walking, a lower one batches more lanes into each refill's start phase).
 constexpr int kFillRefill = 32;
+// Free steps after an iteration's lookup (APG_FILL_XSTEPS; APG_FILL_XCACHED=1
+// lets cached branch points be free steps too).  Same box, fill ms on the
+// iid / repeat-rich genome: 1 step without cached 14.26 / 52.65, 8 with
+// 14.60 / 57.09, none 16.16 / 51.70 (scripts/diag/fill_rep.py): a free step
+// runs while the wave's other lanes wait, so only the short chains pay.
+constexpr int kFillXsteps = 1;
 
 // One thread per pair, lanes persistent.  The gap walk is a state machine
 // that makes exactly ONE extension lookup per iteration whatever the lane is
@@ -223,7 +278,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
                                               const unsigned long long* __restrict__ list_n,
                                               uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer,
                                               unsigned long long* __restrict__ next, bool bcache, bool bfilt,
-                                              int refill) {
+                                              int refill, int xsteps) {
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
@@ -234,6 +289,11 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
   uint32_t LaLf = 0, gmax = 0, dlo = 0, fb0 = 0, d = 0, steps = 0, mode = 0, j = 0, mnode = 0, dd = 0;
   uint32_t n_clos = 0, clos_I = 0, clos_meta = 0;
   unsigned __int128 pv = 0, clos_pv = 0;
+  // Two-level slots (ext_table.hpp): pend = the next iteration's mask | 16
+  // when the last lookup already returned it (the walk's next node or the
+  // next bridge K-mer after a non-branching (K-1)-mer); mnode2 = the visited
+  // node's such bits, for the step down after its closure test.
+  uint32_t pend = 0, mnode2 = 0;
   // successor mask of the path's open branch points at depths < 32 (4 bits
   // per depth, 16 depths per word; 100-bp pairs walk < 35 deep): a
   // backtrack to one reads its node's mask here instead of looking it up
@@ -305,6 +365,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
     const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
     LaLf = La + Lf;
+    pend = 0;
     const uint8_t* A = rv.packed + rv.byte_off[2 * i];
     const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
     const uint32_t lo = max(p.min_insert, max(La, Lf));
@@ -362,9 +423,18 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
           if (!match) continue;
           if (o + 2 <= (uint32_t)K) {  // bridge K-mers: A's tail rolled through F[o, K-1)
             uint64_t w = atail;
+            uint32_t pm = 0;  // two-level: the next bridge (K-1)-mer's successors | 16
             for (uint32_t jj = 0; jj + o + 2 <= (uint32_t)K && match; ++jj) {
               const uint32_t b = (uint32_t)(f0 >> (2 * (o + jj))) & 3;
-              match = (ext_succ(t, w, &nlook) >> b) & 1;
+              uint32_t mm = pm & 15;
+              if (!(pm & 16)) {
+                const uint32_t x = ext_succ2(t, w, &nlook);
+                mm = x & 15;
+                pm = x >> 4;
+              } else {
+                pm = 0;
+              }
+              match = (mm >> b) & 1;
               w = ((w << 2) | b) & t.m1;
             }
           }
@@ -415,94 +485,116 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     }
     if (!__ballot(act)) break;
     if (!act) continue;
-    // ---- one lookup (a node or a closure's bridge K-mer; an open branch
-    // point at depth dd < d reads the mask its visit kept)
-    const bool cached = bcache && mode == 2 && dd < 32;
-    // mode 3: the reverse complement of G (j == 16) or of c1 ++ G[0, K-2)
-    // (c1 the lowest pending predecessor in j); an LSB-first value
-    // complemented is the MSB-first value of its reverse complement
-    const uint64_t m1s = t.m1 >> 2;
-    const uint64_t bkey = j == 16 ? (f0 & t.m1) ^ t.m1 : ((((f0 & m1s) ^ m1s) << 2) | (3u - (__ffs(j) - 1)));
-    const uint64_t key = mode == 0   ? walk_window(atail, pv, d, t)
-                         : mode == 1 ? ww
-                         : mode == 2 ? walk_window(atail, pv >> (2 * (d - dd)), dd, t)
-                                     : bkey;
-    const uint32_t m = cached ? mask_at(dd) : ext_succ(t, key, &nlook);
-    bool visit = false, done = false;
-    if (mode == 0) {  // node (pv, d)
-      mnode = m;
-      visit = true;
-      if (d >= dlo && ((m >> fb0) & 1) && ((bk >> (key & 15)) & 1)) {  // closure test: the K-1 bridge K-mers
-        if (jend > 1) {
-          mode = 1;
-          j = 1;
-          ww = ((key << 2) | fb0) & t.m1;
-          visit = false;
-        } else if (closure()) {
-          done = true;
-          visit = false;
-        }
-      }
-    } else if (mode == 1) {  // bridge K-mer j of the closure test at depth d
-      const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
-      const bool ok = (m >> b) & 1;
-      if (ok && (int)j + 1 < jend) {
-        ww = ((ww << 2) | b) & t.m1;
-        ++j;
-      } else if (ok && closure()) {
-        done = true;
+    // A step whose mask is already known (a two-level slot's next node or
+    // bridge K-mer, or a cached branch point) follows in the same iteration:
+    // at most one lookup per iteration, up to xsteps & 255 free steps after
+    // it (cached branch points among them if xsteps & 256).
+    for (int xs = 0;; ++xs) {
+      // ---- one lookup (a node or a closure's bridge K-mer; an open branch
+      // point at depth dd < d reads the mask its visit kept)
+      const bool cached = bcache && mode == 2 && dd < 32;
+      if (xs > 0 && (xs > (xsteps & 255) || (!(cached && (xsteps & 256)) && !(pend & 16)))) break;
+      // mode 3: the reverse complement of G (j == 16) or of c1 ++ G[0, K-2)
+      // (c1 the lowest pending predecessor in j); an LSB-first value
+      // complemented is the MSB-first value of its reverse complement
+      const uint64_t m1s = t.m1 >> 2;
+      const uint64_t bkey = j == 16 ? (f0 & t.m1) ^ t.m1 : ((((f0 & m1s) ^ m1s) << 2) | (3u - (__ffs(j) - 1)));
+      const uint64_t key = mode == 0   ? walk_window(atail, pv, d, t)
+                           : mode == 1 ? ww
+                           : mode == 2 ? walk_window(atail, pv >> (2 * (d - dd)), dd, t)
+                                       : bkey;
+      uint32_t m, m2 = 0;
+      if (cached) {
+        m = mask_at(dd);
+      } else if (pend & 16) {
+        m = pend & 15;
       } else {
-        mode = 0;
+        const uint32_t x = ext_succ2(t, key, &nlook);
+        m = x & 15;
+        m2 = x >> 4;
+      }
+      pend = 0;
+      bool visit = false, done = false;
+      if (mode == 0) {  // node (pv, d)
+        mnode = m;
+        mnode2 = m2;
         visit = true;
-      }
-    } else if (mode == 3) {  // bridge filter: predecessors of G, then of c1 ++ G[0, K-2)
-      const uint32_t pm = rev4(m);  // pred(x) bit c = succ(rc(x)) bit 3 - c
-      if (j == 16) {
-        j = pm;
-      } else {
-        const uint32_t c1 = __ffs(j) - 1;
-        bk |= ((pm & 1) | ((pm & 2) << 3) | ((pm & 4) << 6) | ((pm & 8) << 9)) << c1;
-        j &= j - 1;
-      }
-      if (j == 0) mode = 0;  // the walk from depth 0
-    } else {  // open branch point at depth dd: the sibling after the base taken there
-      const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
-      const uint32_t rest = m & ~((2u << bb) - 1);
-      const uint32_t b2 = __ffs(rest) - 1;  // rest != 0: dd was marked open
-      if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
-      pv = ((pv >> (2 * (d - dd))) << 2) | b2;
-      d = dd + 1;
-      mode = 0;
-    }
-    if (visit) {  // the walk's step from node (pv, d) with successor mask mnode
-      bool down = false;
-      if (d < gmax) {
-        if (++steps > cap) {
-          budget = true;
-          done = true;
-        } else if (mnode) {
-          const uint32_t b = __ffs(mnode) - 1;
-          if (mnode >> (b + 1)) {
-            brm |= 1ull << d;
-            if (d < 32) mask_set(d, mnode);  // an open branch point: its mask for the backtracks
+        if (d >= dlo && ((m >> fb0) & 1) && ((bk >> (key & 15)) & 1)) {  // closure test: the K-1 bridge K-mers
+          if (jend > 1) {
+            mode = 1;
+            j = 1;
+            ww = ((key << 2) | fb0) & t.m1;
+            pend = m2;  // m2 is set only if fb0 is the one successor
+            visit = false;
+          } else if (closure()) {
+            done = true;
+            visit = false;
           }
-          pv = (pv << 2) | b;
-          ++d;
-          down = true;
         }
-      }
-      if (!done && !down) {
-        if (!brm) {
-          done = true;  // search exhausted
+      } else if (mode == 1) {  // bridge K-mer j of the closure test at depth d
+        const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
+        const bool ok = (m >> b) & 1;
+        if (ok && (int)j + 1 < jend) {
+          ww = ((ww << 2) | b) & t.m1;
+          ++j;
+          pend = m2;
+        } else if (ok && closure()) {
+          done = true;
         } else {
-          dd = 63 - __clzll((long long)brm);
-          mode = 2;
+          mode = 0;
+          visit = true;
+        }
+      } else if (mode == 3) {  // bridge filter: predecessors of G, then of c1 ++ G[0, K-2)
+        const uint32_t pm = rev4(m);  // pred(x) bit c = succ(rc(x)) bit 3 - c
+        if (j == 16) {
+          j = pm;
+        } else {
+          const uint32_t c1 = __ffs(j) - 1;
+          bk |= ((pm & 1) | ((pm & 2) << 3) | ((pm & 4) << 6) | ((pm & 8) << 9)) << c1;
+          j &= j - 1;
+        }
+        if (j == 0) mode = 0;  // the walk from depth 0
+      } else {  // open branch point at depth dd: the sibling after the base taken there
+        const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
+        const uint32_t rest = m & ~((2u << bb) - 1);
+        const uint32_t b2 = __ffs(rest) - 1;  // rest != 0: dd was marked open
+        if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
+        pv = ((pv >> (2 * (d - dd))) << 2) | b2;
+        d = dd + 1;
+        mode = 0;
+      }
+      if (visit) {  // the walk's step from node (pv, d) with successor mask mnode
+        bool down = false;
+        if (d < gmax) {
+          if (++steps > cap) {
+            budget = true;
+            done = true;
+          } else if (mnode) {
+            const uint32_t b = __ffs(mnode) - 1;
+            if (mnode >> (b + 1)) {
+              brm |= 1ull << d;
+              if (d < 32) mask_set(d, mnode);  // an open branch point: its mask for the backtracks
+            }
+            pv = (pv << 2) | b;
+            ++d;
+            down = true;
+            pend = mnode2;  // set only if b is the node's one successor
+          }
+        }
+        if (!done && !down) {
+          if (!brm) {
+            done = true;  // search exhausted
+          } else {
+            dd = 63 - __clzll((long long)brm);
+            mode = 2;
+          }
         }
       }
-    }
-    if (done) {
-      act = false;
-      conclude();
+      if (done) {
+        act = false;
+        conclude();
+        break;
+      }
     }
   }
   wave_add(&cnt->st[kFillOk], c_ok);
@@ -652,7 +744,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
       if (ctx->clean_valid && ctx->clean_gen == dr->gen) clean = ctx->pc_clean;
       // ... and the pass's extension table is this very solid set's
       if (ctx->pc_ext_valid) {
-        et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
+        et = ext_tab(ctx->pc_ext_slot, ctx->pc_ext_mask, p.K);
         have_ext = true;
       }
     } else {  // the pairs' own solid K-mers
@@ -702,12 +794,16 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     const bool bfilt = !(bfe && !strcmp(bfe, "0"));
     const char* rfe = getenv("APG_FILL_REFILL");
     const int refill = rfe ? std::max(0, std::min(63, atoi(rfe))) : kFillRefill;
+    // APG_FILL_XSTEPS: free steps after an iteration's lookup (0: one step per iteration)
+    const char* xse = getenv("APG_FILL_XSTEPS");
+    const char* xce = getenv("APG_FILL_XCACHED");  // 1: cached branch points may be free steps
+    const int xsteps = std::min(255, xse ? std::max(0, atoi(xse)) : kFillXsteps) | (xce && !strcmp(xce, "1") ? 256 : 0);
     k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
                                           std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
-                                          ndefer + 1, bcache, bfilt, refill);
+                                          ndefer + 1, bcache, bfilt, refill, xsteps);
     if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
       k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
-                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill);
+                                            defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill, xsteps);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

@@ -983,7 +983,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   // (APG_PC_EXT_AUX=0: in line).  Same box: 152.3 -> 150.8 ms per bench step
   // once the fused K+1 pass moved after the scan; with the K+1 pass beside
   // the scan as well it gained nothing (172.4 vs 171.9 ms).
-  hipEvent_t ext_done = nullptr;
+  hipEvent_t ext_done = nullptr, link_done = nullptr;
   if (ext && weak) {
     const char* ae = getenv("APG_PC_EXT_AUX");
     const hipStream_t ax = (ae && !strcmp(ae, "0")) ? nullptr : aux_stream(ctx);
@@ -994,30 +994,39 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       APG_CHECK_HIP(hipEventRecord(ready, ctx->stream));  // the solid list is complete
       APG_CHECK_HIP(hipStreamWaitEvent(ax, ready, 0));
       APG_CHECK_HIP(hipEventDestroy(ready));
+      // The decisions read only the pred / succ bits: they wait for the
+      // inserts, and the two-level link pass (FillFragments' bits) runs on
+      // behind them; the pass joins the main stream before PreCorrect returns.
       int rc;
       {
         StreamSwap sw(ctx, ax);
-        rc = ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et);
+        rc = ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et, false);
         if (rc == APG_OK && hipEventRecord(ext_done, ax) != hipSuccess) rc = APG_E_HIP;
+        if (rc == APG_OK) rc = ext_link(ctx, et, n_solid);
+        if (rc == APG_OK && et.ks == 16) {
+          if (hipEventCreateWithFlags(&link_done, hipEventDisableTiming) != hipSuccess ||
+              hipEventRecord(link_done, ax) != hipSuccess)
+            rc = APG_E_HIP;
+        }
       }
       if (rc != APG_OK) {
         (void)hipStreamSynchronize(ax);
         (void)hipEventDestroy(ext_done);
+        if (link_done) (void)hipEventDestroy(link_done);
         return rc;
       }
     }
   }
   // an early return leaves no table build running behind it
   struct ExtGuard {
-    hipEvent_t* ev;
+    hipEvent_t *ev, *lk;
     hipStream_t ax;
     ~ExtGuard() {
-      if (*ev) {
-        (void)hipStreamSynchronize(ax);
-        (void)hipEventDestroy(*ev);
-      }
+      if (*ev || *lk) (void)hipStreamSynchronize(ax);
+      if (*ev) (void)hipEventDestroy(*ev);
+      if (*lk) (void)hipEventDestroy(*lk);
     }
-  } ext_guard{&ext_done, ctx->aux};
+  } ext_guard{&ext_done, &link_done, ctx->aux};
   // the main stream's wait for the table (no host sync); idempotent
   auto ext_wait = [&]() -> int {
     if (!ext_done) return APG_OK;
@@ -1027,7 +1036,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     return APG_OK;
   };
   if (ext && !weak && ext_reuse) {
-    et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(p.K - 1), (1ull << (2 * (p.K - 1))) - 1, p.K - 1};
+    et = ext_tab(ctx->pc_ext_slot, ctx->pc_ext_mask, p.K);
   } else if (ext && !weak) {
     APG_TRY(ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et));
   } else if (ext) {
@@ -1171,6 +1180,11 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     }
   }
   APG_CHECK_HIP(hipGetLastError());
+  if (link_done) {  // the two-level bits complete before the table is handed on
+    APG_CHECK_HIP(hipStreamWaitEvent(ctx->stream, link_done, 0));
+    APG_CHECK_HIP(hipEventDestroy(link_done));
+    link_done = nullptr;
+  }
   unsigned long long h[6];
   APG_CHECK_HIP(hipMemcpyAsync(h, dcnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
@@ -1279,27 +1293,87 @@ __global__ void __launch_bounds__(256) k_ecj_trim(EcjReads rv, ExtTab et, int K,
       // base i+K (ext_table.hpp).  i = the first non-solid K-mer, or nk.
       const int n1 = K - 1;
       auto base = [&](uint32_t x) -> uint32_t { return (rd[x >> 2] >> (2 * (x & 3))) & 3; };
+      const uint32_t nk = L - K + 1;
+      uint32_t i = nk;
+      if (et.ks == 16) {
+        // Two-level slots: the (K-1)-mer at c also answers K-mer c+1 by its
+        // successor's successor mask (when it has one successor) and K-mer
+        // c-2 by its predecessor's predecessor mask (when it has one
+        // predecessor): one lookup per four K-mers along a solid read, in
+        // order, with a lookup of c-1 of its own where the pp bits do not
+        // apply.  u = the first K-mer not yet known solid.
+        uint64_t y = 0;  // (K-1)-mer at c, LSB-first: base c+t at bits 2t
+        for (int t = 0; t < n1; ++t) y |= (uint64_t)base(t) << (2 * t);
+        uint32_t u = 0, c = 0;
+        while (u < nk) {
+          const uint32_t cn = min(u + 2, nk);
+          for (; c < cn; ++c) y = (y >> 2) | ((uint64_t)base(c + (uint32_t)n1) << (2 * (n1 - 1)));
+          ++looks;
+          const uint32_t e = ext_masks2_lsb(et, y);
+          const bool sp = (e >> base(c - 1)) & 1;  // K-mer c-1 (>= u)
+          if (c == u + 2) {                        // K-mer u = c-2 first
+            bool s2;
+            if (sp && ((e >> 17) & 1)) {
+              s2 = (e >> (12 + base(u))) & 1;
+            } else {
+              ++looks;
+              s2 = (ext_masks_lsb(et, ((y << 2) & et.m1) | base(c - 1)) >> base(u)) & 1;
+            }
+            if (!s2) {
+              i = u;
+              break;
+            }
+          }
+          if (!sp) {
+            i = c - 1;
+            break;
+          }
+          if (c == nk) break;  // K-mers [0, nk) all solid
+          if (!((e >> (4 + base(c + (uint32_t)n1))) & 1)) {
+            i = c;
+            break;
+          }
+          u = c + 1;
+          if (u < nk && ((e >> 16) & 1)) {  // K-mer c+1 from the successor's successors
+            if (!((e >> (8 + base(c + (uint32_t)n1 + 1))) & 1)) {
+              i = u;
+              break;
+            }
+            u = c + 2;
+          }
+        }
+      } else {
       uint64_t y = 0;  // (K-1)-mer at i+1, LSB-first: base i+1+t at bits 2t
       for (int t = 0; t < n1; ++t) y |= (uint64_t)base(1 + t) << (2 * t);
-      const uint32_t nk = L - K + 1;
-      uint32_t i = 0;
-      for (; i < nk; i += 2) {
-        ++looks;
-        const uint32_t m = ext_masks_lsb(et, y);
-        if (!(m & (1u << base(i)))) break;
-        if (i + 1 >= nk) {
-          i = nk;
-          break;
+      // kEcjBatch lookups in flight per lane: the (K-1)-mers of a batch
+      // follow from the bases alone, so they are issued together and checked
+      // in order (a read is almost always solid to its end after correction:
+      // the lookups past its first non-solid K-mer are few)
+      constexpr uint32_t kEcjBatch = 4;
+      for (uint32_t i0 = 0; i0 < nk && i == nk; i0 += 2 * kEcjBatch) {
+        ExtProbe pr[kEcjBatch];
+#pragma unroll
+        for (uint32_t b = 0; b < kEcjBatch; ++b) {
+          const uint32_t ib = i0 + 2 * b;
+          if (ib < nk) pr[b] = ext_issue_lsb(et, y);
+          if (ib + 2 < nk) {
+            y = (y >> 2) | ((uint64_t)base(ib + (uint32_t)K) << (2 * (n1 - 1)));
+            y = (y >> 2) | ((uint64_t)base(ib + (uint32_t)K + 1) << (2 * (n1 - 1)));
+          }
         }
-        const uint32_t bs = base(i + (uint32_t)K);
-        if (!((m >> 4) & (1u << bs))) {
-          i += 1;
-          break;
+#pragma unroll
+        for (uint32_t b = 0; b < kEcjBatch; ++b) {
+          const uint32_t ib = i0 + 2 * b;
+          if (i != nk || ib >= nk) continue;
+          ++looks;
+          const uint32_t m = ext_finish(et, pr[b]);
+          if (!(m & (1u << base(ib)))) {
+            i = ib;
+          } else if (ib + 1 < nk && !((m >> 4) & (1u << base(ib + (uint32_t)K)))) {
+            i = ib + 1;
+          }
         }
-        if (i + 2 < nk) {
-          y = (y >> 2) | ((uint64_t)bs << (2 * (n1 - 1)));
-          y = (y >> 2) | ((uint64_t)base(i + (uint32_t)K + 1) << (2 * (n1 - 1)));
-        }
+      }
       }
       k = i == nk ? L : i + (uint32_t)n1;
       if (k < min_keep) k = 0;
@@ -1350,7 +1424,7 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   APG_TRY(correct_pass(ctx, jr, p, sr.solid, sr.n_solid, &st->pc));
   ExtTab et{};
   if (ctx->pc_ext_valid && ctx->pc_list == sr.solid && ctx->pc_K == e.K)
-    et = ExtTab{ctx->pc_ext_slot, ctx->pc_ext_mask, make_hashp(e.K - 1), (1ull << (2 * (e.K - 1))) - 1, e.K - 1};
+    et = ext_tab(ctx->pc_ext_slot, ctx->pc_ext_mask, e.K);
   else
     APG_TRY(ext_build(ctx, sr.solid, sr.n_solid, e.K, "ecj_ext", "ecj_ext", &et));
   unsigned long long* cnt = nullptr;

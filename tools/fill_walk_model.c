@@ -107,6 +107,13 @@ int main(int argc, char** argv) {
   fclose(f);
 
   uint64_t st[4] = {0}, look[4][3] = {{0}}, filt_pre = 0, filt_bridge = 0;
+  /* per-pair caches keyed by position: node windows by depth (1-way, 2-way
+     most-recent-first), bridge K-mer j's window by j */
+  uint64_t hit_n1 = 0, hit_n2 = 0, hit_b = 0, hit_bf = 0;
+  /* two-level slots: a lookup also returns the successor mask of a node's
+     unique successor, so the node after a looked-up non-branching one (walk
+     child or next bridge K-mer) costs no lookup */
+  uint64_t two_node = 0, two_bridge = 0, two_bridge_f = 0;
   for (uint64_t p = 0; p < nr / 2; p++) {
     const uint8_t *A = reads + 2 * p * L, *B = reads + (2 * p + 1) * L;
     uint8_t F[256];
@@ -159,20 +166,44 @@ int main(int argc, char** argv) {
     for (int t = 0; t < n1; t++) atail = (atail << 2) | A[L - n1 + t];
     uint8_t path[64];
     uint32_t mask[64], nextb[64], steps = 0, d = 0;
+    int phys[64], known = 0;
     uint64_t ln = 0, lb = 0, lk = 0;
+    uint64_t ck[64][2], cb[32];
+    for (int t = 0; t < 64; t++) ck[t][0] = ck[t][1] = ~0ull;
+    for (int t = 0; t < 32; t++) cb[t] = ~0ull;
     int budget = 0, stop = 0;
     for (;;) {  /* visit node (path[0, d)) */
       uint64_t w = atail;
       for (uint32_t t = 0; t < d; t++) w = ((w << 2) | path[t]) & m1;
       const uint32_t m = succ(w);
       ln++;
+      phys[d] = !known;
+      two_node += !known;
+      known = 0;
+      if (ck[d][0] == w) hit_n1++, hit_n2++;
+      else {
+        if (ck[d][1] == w) hit_n2++;
+        ck[d][1] = ck[d][0];
+        ck[d][0] = w;
+      }
       mask[d] = m;
       if (d >= dlo && ((m >> F[0]) & 1)) {
         int ok = 1;
         uint64_t ww = ((w << 2) | F[0]) & m1;
+        int bknown = phys[d] && __builtin_popcount(m) == 1, bphys = 0;
         for (int j = 1; j < n1 && ok; j++) {
+          const uint32_t sj = succ(ww);
+          bphys = !bknown;
+          two_bridge += bphys;
+          if (((bk >> (w & 15)) & 1) && j < n1 - 2) two_bridge_f += bphys;
+          bknown = bphys && __builtin_popcount(sj) == 1;
           ok = (succ(ww) >> F[j]) & 1;
           lb++;
+          if (cb[j] == ww) {
+            hit_b++;
+            if (((bk >> (w & 15)) & 1) && j < n1 - 2) hit_bf++;
+          }
+          cb[j] = ww;
           if (((bk >> (w & 15)) & 1) && j < n1 - 2) filt_bridge++;
           ww = ((ww << 2) | F[j]) & m1;
         }
@@ -185,6 +216,7 @@ int main(int argc, char** argv) {
           break;
         }
         if (m) {
+          known = phys[d] && __builtin_popcount(m) == 1;
           path[d] = __builtin_ctz(m);
           nextb[d] = path[d] + 1;
           d++;
@@ -201,6 +233,7 @@ int main(int argc, char** argv) {
         const uint32_t rest = mask[d] >> nextb[d];
         if (rest) {
           lk += d >= 32;
+          known = 0;
           path[d] = nextb[d] + __builtin_ctz(rest);
           nextb[d] = path[d] + 1;
           d++;
@@ -227,5 +260,13 @@ int main(int argc, char** argv) {
          (unsigned long long)tot, (unsigned long long)br, 100.0 * br / (tot ? tot : 1),
          (unsigned long long)filt_bridge, (unsigned long long)filt_pre,
          100.0 * ((double)br - filt_bridge - filt_pre) / (tot ? tot : 1));
+  printf("two-level slots: node lookups %llu of %llu, bridge %llu of %llu (filtered: %llu of %llu)\n",
+         (unsigned long long)two_node, (unsigned long long)(tot - br), (unsigned long long)two_bridge,
+         (unsigned long long)br, (unsigned long long)two_bridge_f, (unsigned long long)filt_bridge);
+  printf("position caches: node by depth 1-way %llu (%.1f %% of node lookups), 2-way %llu (%.1f %%); "
+         "bridge by j %llu (%.1f %% of bridge lookups; %llu of the filtered ones)\n",
+         (unsigned long long)hit_n1, 100.0 * hit_n1 / (tot - br), (unsigned long long)hit_n2,
+         100.0 * hit_n2 / (tot - br), (unsigned long long)hit_b, 100.0 * hit_b / (br ? br : 1),
+         (unsigned long long)hit_bf);
   return 0;
 }
