@@ -92,8 +92,11 @@ __device__ __forceinline__ uint64_t ext_home(const ExtTab& t, uint64_t c) {
 }
 
 // The extension bits of canonical (K-1)-mer c (0 if absent): pred | succ << 4,
-// and with two-level slots ss << 8 | pp << 12.
+// and with two-level slots ss << 8 | pp << 12.  KS: the key shift when the
+// caller knows it at compile time (0: t.ks).
+template <int KS = 0>
 __device__ __forceinline__ uint32_t ext_bits(const ExtTab& t, uint64_t c) {
+  const int ks = KS ? KS : t.ks;
   uint64_t g = ext_home(t, c);
   for (;;) {
     const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t.slot + g);
@@ -102,7 +105,7 @@ __device__ __forceinline__ uint32_t ext_bits(const ExtTab& t, uint64_t c) {
 #pragma unroll
     for (uint32_t j = 0; j < kExtGrp; ++j) {
       if (v[j] == kExtEmpty) return 0;
-      if ((v[j] >> t.ks) == c) return (uint32_t)(v[j] & ((1u << t.ks) - 1));
+      if ((v[j] >> ks) == c) return (uint32_t)(v[j] & ((1u << ks) - 1));
     }
     g = (g + kExtGrp) & t.mask;
   }
@@ -122,14 +125,15 @@ __device__ __forceinline__ uint32_t ext_succ(const ExtTab& t, uint64_t w, uint32
 // ext_succ | ss << 4 | 256 when ss is known: w has exactly one successor
 // and the table is two-level (palindromes excepted: their two orientations
 // share one slot).
+template <int KS = 0>
 __device__ __forceinline__ uint32_t ext_succ2(const ExtTab& t, uint64_t w, uint32_t* nlook) {
   const uint64_t r = rc_bases(w, t.n1, t.m1);
-  const uint32_t e = ext_bits(t, w < r ? w : r);
+  const uint32_t e = ext_bits<KS>(t, w < r ? w : r);
   ++*nlook;
   uint32_t m = 0, x = 0;
   if (w <= r) m |= (e >> 4) & 15, x = (e >> 8) & 15;
   if (r <= w) m |= rev4(e & 15), x = rev4((e >> 12) & 15);
-  const bool ok = t.ks == 16 && w != r && __popc(m) == 1;
+  const bool ok = (KS ? KS : t.ks) == 16 && w != r && __popc(m) == 1;
   return m | (ok ? (x << 4) | 256u : 0u);
 }
 

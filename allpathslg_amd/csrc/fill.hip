@@ -254,11 +254,15 @@ constexpr uint32_t kFillCap1 = 96;
 // walking, a lower one batches more lanes into each refill's start phase).
 constexpr int kFillRefill = 32;
 // Free steps after an iteration's lookup (APG_FILL_XSTEPS; APG_FILL_XCACHED=1
-// lets cached branch points be free steps too).  Same box, fill ms on the
-// iid / repeat-rich genome: 1 step without cached 14.26 / 52.65, 8 with
-// 14.60 / 57.09, none 16.16 / 51.70 (scripts/diag/fill_rep.py): a free step
-// runs while the wave's other lanes wait, so only the short chains pay.
+// lets cached branch points be free steps too), taken only when at least
+// APG_FILL_XPCT % of the wave's lanes have one.  Same box, fill ms on the iid
+// / repeat-rich genome: 1 step without cached 14.26 / 52.65, 8 with 14.60 /
+// 57.09, none 16.16 / 51.70; then (another box) 1 step at 75 % 11.29 / 44.70,
+// at 0 % 11.28 / 48.10, none 12.68 / 43.67 (scripts/diag/fill_rep.py): a
+// free step runs while the wave's other lanes wait, so only the common
+// chains pay.
 constexpr int kFillXsteps = 1;
+constexpr int kFillXpct = 75;
 
 // One thread per pair, lanes persistent.  The gap walk is a state machine
 // that makes exactly ONE extension lookup per iteration whatever the lane is
@@ -270,7 +274,8 @@ constexpr int kFillXsteps = 1;
 // (wave-aggregated fetch from *next), so a wave is no longer held by its
 // slowest pair.  Per lane the lookups, their order and the result are the
 // same as the nested search (oracle/fill_oracle.c).
-__global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
+template <int KS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
                                               uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
                                               const uint8_t* __restrict__ clean, FillCounters* __restrict__ cnt,
@@ -285,15 +290,25 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
   const uint64_t nwork = list ? *list_n : rv.n_pairs;
   // the lane's pair and its search state
   bool act = false, budget = false;
-  uint64_t i = 0, atail = 0, f0 = 0, brm = 0, ww = 0;
+  uint64_t i = 0, atail = 0, f0 = 0, brm = 0;
   uint32_t LaLf = 0, gmax = 0, dlo = 0, fb0 = 0, d = 0, steps = 0, mode = 0, j = 0, mnode = 0, dd = 0;
   uint32_t n_clos = 0, clos_I = 0, clos_meta = 0;
   unsigned __int128 pv = 0, clos_pv = 0;
-  // Two-level slots (ext_table.hpp): pend = the next iteration's mask | 16
-  // when the last lookup already returned it (the walk's next node or the
-  // next bridge K-mer after a non-branching (K-1)-mer); mnode2 = the visited
-  // node's such bits, for the step down after its closure test.
-  uint32_t pend = 0, mnode2 = 0;
+  // Two-level slots (ext_table.hpp), one register: bits 0-4 ("pend") the
+  // next iteration's mask | 16 when the last lookup already returned it (the
+  // walk's next node or the next bridge K-mer after a non-branching (K-1)-mer),
+  // bits 8-12 the visited node's such bits, for the step down after its
+  // closure test.
+  uint32_t pq = 0;
+  // wk: the next lookup's (K-1)-mer, set by each transition
+  uint64_t wk = 0;
+  const uint64_t m1s = t.m1 >> 2;
+  // mode 3's keys: the reverse complement of G (j == 16) or of c1 ++ G[0, K-2)
+  // (c1 the lowest pending predecessor in j); an LSB-first value complemented
+  // is the MSB-first value of its reverse complement
+  auto bkey = [&]() -> uint64_t {
+    return j == 16 ? (f0 & t.m1) ^ t.m1 : ((((f0 & m1s) ^ m1s) << 2) | (3u - (__ffs(j) - 1)));
+  };
   // successor mask of the path's open branch points at depths < 32 (4 bits
   // per depth, 16 depths per word; 100-bp pairs walk < 35 deep): a
   // backtrack to one reads its node's mask here instead of looking it up
@@ -365,7 +380,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
     const uint32_t La = (uint32_t)(rv.base_off[2 * i + 1] - rv.base_off[2 * i]);
     const uint32_t Lf = (uint32_t)(rv.base_off[2 * i + 2] - rv.base_off[2 * i + 1]);
     LaLf = La + Lf;
-    pend = 0;
+    pq = 0;
     const uint8_t* A = rv.packed + rv.byte_off[2 * i];
     const uint8_t* B = rv.packed + rv.byte_off[2 * i + 1];
     const uint32_t lo = max(p.min_insert, max(La, Lf));
@@ -452,10 +467,12 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
       pv = 0;
       brm = 0;  // depths whose node still has unexplored children
       d = steps = mode = 0;
+      wk = atail;  // the walk's root: A's last K-1 bases
       if (bfilt && n1 >= 2) {  // the bridge filter's lookups first
         mode = 3;
         j = 16;
         bk = 0;
+        wk = bkey();
       }
       act = true;
       return;
@@ -493,38 +510,38 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
       // ---- one lookup (a node or a closure's bridge K-mer; an open branch
       // point at depth dd < d reads the mask its visit kept)
       const bool cached = bcache && mode == 2 && dd < 32;
-      if (xs > 0 && (xs > (xsteps & 255) || (!(cached && (xsteps & 256)) && !(pend & 16)))) break;
-      // mode 3: the reverse complement of G (j == 16) or of c1 ++ G[0, K-2)
-      // (c1 the lowest pending predecessor in j); an LSB-first value
-      // complemented is the MSB-first value of its reverse complement
-      const uint64_t m1s = t.m1 >> 2;
-      const uint64_t bkey = j == 16 ? (f0 & t.m1) ^ t.m1 : ((((f0 & m1s) ^ m1s) << 2) | (3u - (__ffs(j) - 1)));
-      const uint64_t key = mode == 0   ? walk_window(atail, pv, d, t)
-                           : mode == 1 ? ww
-                           : mode == 2 ? walk_window(atail, pv >> (2 * (d - dd)), dd, t)
-                                       : bkey;
+      if (xs > 0) {
+        // a free step runs while the wave's other lanes wait: taken only when
+        // at least (xsteps >> 16) % of the lanes still here have one
+        const bool can = (cached && (xsteps & 256)) || (pq & 16);
+        if (xs > (xsteps & 255)) break;
+        if ((uint32_t)__popcll(__ballot(can)) * 100u < (uint32_t)__popcll(__ballot(true)) * ((uint32_t)xsteps >> 16))
+          break;
+        if (!can) break;
+      }
+      const uint64_t key = wk;
       uint32_t m, m2 = 0;
       if (cached) {
         m = mask_at(dd);
-      } else if (pend & 16) {
-        m = pend & 15;
+      } else if (pq & 16) {
+        m = pq & 15;
       } else {
-        const uint32_t x = ext_succ2(t, key, &nlook);
+        const uint32_t x = ext_succ2<KS>(t, key, &nlook);
         m = x & 15;
         m2 = x >> 4;
       }
-      pend = 0;
+      pq &= ~0xffu;
       bool visit = false, done = false;
       if (mode == 0) {  // node (pv, d)
         mnode = m;
-        mnode2 = m2;
+        pq = m2 << 8;
         visit = true;
         if (d >= dlo && ((m >> fb0) & 1) && ((bk >> (key & 15)) & 1)) {  // closure test: the K-1 bridge K-mers
           if (jend > 1) {
             mode = 1;
             j = 1;
-            ww = ((key << 2) | fb0) & t.m1;
-            pend = m2;  // m2 is set only if fb0 is the one successor
+            wk = ((key << 2) | fb0) & t.m1;
+            pq |= m2;  // m2 is set only if fb0 is the one successor
             visit = false;
           } else if (closure()) {
             done = true;
@@ -535,9 +552,9 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
         const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
         const bool ok = (m >> b) & 1;
         if (ok && (int)j + 1 < jend) {
-          ww = ((ww << 2) | b) & t.m1;
+          wk = ((wk << 2) | b) & t.m1;
           ++j;
-          pend = m2;
+          pq |= m2;
         } else if (ok && closure()) {
           done = true;
         } else {
@@ -553,7 +570,12 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
           bk |= ((pm & 1) | ((pm & 2) << 3) | ((pm & 4) << 6) | ((pm & 8) << 9)) << c1;
           j &= j - 1;
         }
-        if (j == 0) mode = 0;  // the walk from depth 0
+        if (j == 0) {
+          mode = 0;  // the walk from depth 0
+          wk = atail;
+        } else {
+          wk = bkey();
+        }
       } else {  // open branch point at depth dd: the sibling after the base taken there
         const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
         const uint32_t rest = m & ~((2u << bb) - 1);
@@ -562,6 +584,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
         pv = ((pv >> (2 * (d - dd))) << 2) | b2;
         d = dd + 1;
         mode = 0;
+        wk = ((key << 2) | b2) & t.m1;  // key: the window at dd
       }
       if (visit) {  // the walk's step from node (pv, d) with successor mask mnode
         bool down = false;
@@ -578,7 +601,8 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
             pv = (pv << 2) | b;
             ++d;
             down = true;
-            pend = mnode2;  // set only if b is the node's one successor
+            wk = walk_window(atail, pv, d, t);  // the child's window
+            pq |= (pq >> 8) & 0xffu;  // set only if b is the node's one successor
           }
         }
         if (!done && !down) {
@@ -587,6 +611,7 @@ __global__ void __launch_bounds__(256) k_fill(FillReads rv, FillP p, ExtTab t, F
           } else {
             dd = 63 - __clzll((long long)brm);
             mode = 2;
+            wk = walk_window(atail, pv >> (2 * (d - dd)), dd, t);
           }
         }
       }
@@ -785,7 +810,9 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   if (np) {
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
     // lanes are persistent (work fetched per wave): one resident round of blocks
-    const uint32_t grid = resident_grid(ctx, k_fill, 256, (np + 255) / 256);
+    const bool two = et.ks == 16;
+    const uint32_t grid = two ? resident_grid(ctx, k_fill<16>, 256, (np + 255) / 256)
+                              : resident_grid(ctx, k_fill<8>, 256, (np + 255) / 256);
     // APG_FILL_BRANCH_CACHE=0: backtracks look their branch point up again (A/B)
     const char* be = getenv("APG_FILL_BRANCH_CACHE");
     const bool bcache = !(be && !strcmp(be, "0"));
@@ -797,13 +824,22 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     // APG_FILL_XSTEPS: free steps after an iteration's lookup (0: one step per iteration)
     const char* xse = getenv("APG_FILL_XSTEPS");
     const char* xce = getenv("APG_FILL_XCACHED");  // 1: cached branch points may be free steps
-    const int xsteps = std::min(255, xse ? std::max(0, atoi(xse)) : kFillXsteps) | (xce && !strcmp(xce, "1") ? 256 : 0);
-    k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
+    const char* xpe = getenv("APG_FILL_XPCT");  // free steps only when this % of the lanes have one
+    const int xpct = std::min(100, std::max(0, xpe ? atoi(xpe) : kFillXpct));
+    const int xsteps = std::min(255, xse ? std::max(0, atoi(xse)) : kFillXsteps) | (xce && !strcmp(xce, "1") ? 256 : 0) |
+                       (xpct << 16);
+    auto fill = [&](auto kern) {
+      kern<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
                                           std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
                                           ndefer + 1, bcache, bfilt, refill, xsteps);
-    if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
-      k_fill<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
+      if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
+        kern<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
                                             defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill, xsteps);
+    };
+    if (two)
+      fill(k_fill<16>);
+    else
+      fill(k_fill<8>);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

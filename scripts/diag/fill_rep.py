@@ -18,7 +18,10 @@ cases = [("base", 1024, {}), ("pass1", 96, {}), ("x0", 1024, {"APG_FILL_XSTEPS":
          ("x64", 1024, {"APG_FILL_XSTEPS": "64"}), ("refill8", 1024, {"APG_FILL_REFILL": "8"}),
          ("refill48", 1024, {"APG_FILL_REFILL": "48"}), ("nocache", 1024, {"APG_FILL_BRANCH_CACHE": "0"}),
          ("x1", 1024, {"APG_FILL_XSTEPS": "1"}), ("x8nc", 1024, {"APG_FILL_XCACHED": "0"}),
-         ("x1nc", 1024, {"APG_FILL_XSTEPS": "1", "APG_FILL_XCACHED": "0"}), ("base2", 1024, {})]
+         ("x1nc", 1024, {"APG_FILL_XSTEPS": "1", "APG_FILL_XCACHED": "0"}),
+         ("p0", 1024, {"APG_FILL_XPCT": "0"}), ("p25", 1024, {"APG_FILL_XPCT": "25"}),
+         ("p75", 1024, {"APG_FILL_XPCT": "75"}), ("p90", 1024, {"APG_FILL_XPCT": "90"}),
+         ("p50x4", 1024, {"APG_FILL_XSTEPS": "4"}), ("base2", 1024, {})]
 sel = os.environ.get("FILL_CASES")
 if sel:
     cases = [c for c in cases if c[0] in sel.split(",")]
