@@ -984,6 +984,16 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   // once the fused K+1 pass moved after the scan; with the K+1 pass beside
   // the scan as well it gained nothing (172.4 vs 171.9 ms).
   hipEvent_t ext_done = nullptr, link_done = nullptr;
+  // The link pass starts once the decisions are launched (their workgroups
+  // dispatched first); APG_PC_LINK_AT=0: right behind the inserts, beside the
+  // decisions.  Same box: 144.5 vs 145.4-146.0 ms per bench step (decisions
+  // 10.6 vs 15.1 ms); the K+1 pass kicked after the decisions too
+  // (APG_SK_UP_AT=3) exposes it: 156.9 ms.
+  static const bool link_late = [] {
+    const char* e = getenv("APG_PC_LINK_AT");
+    return !(e && atoi(e) == 0);
+  }();
+  bool link_pending = false;  // the table's link pass still to launch (link_late)
   if (ext && weak) {
     const char* ae = getenv("APG_PC_EXT_AUX");
     const hipStream_t ax = (ae && !strcmp(ae, "0")) ? nullptr : aux_stream(ctx);
@@ -1002,8 +1012,9 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
         StreamSwap sw(ctx, ax);
         rc = ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et, false);
         if (rc == APG_OK && hipEventRecord(ext_done, ax) != hipSuccess) rc = APG_E_HIP;
-        if (rc == APG_OK) rc = ext_link(ctx, et, n_solid);
-        if (rc == APG_OK && et.ks == 16) {
+        if (rc == APG_OK && !link_late) rc = ext_link(ctx, et, n_solid);
+        link_pending = rc == APG_OK && link_late && et.ks == 16;
+        if (rc == APG_OK && et.ks == 16 && !link_late) {
           if (hipEventCreateWithFlags(&link_done, hipEventDisableTiming) != hipSuccess ||
               hipEventRecord(link_done, ax) != hipSuccess)
             rc = APG_E_HIP;
@@ -1148,6 +1159,23 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     if (ncand)
       k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups, !weak);
     kend(ctx);
+    APG_TRY(side_kick(ctx, 3));  // APG_SK_UP_AT=3: the K+1 pass behind the decisions' dispatch
+    if (link_pending) {
+      link_pending = false;
+      // the table is complete (the decisions waited for it): the link pass on
+      // the auxiliary stream from here, joined before PreCorrect returns
+      hipEvent_t go = nullptr;
+      APG_CHECK_HIP(hipEventCreateWithFlags(&go, hipEventDisableTiming));
+      APG_CHECK_HIP(hipEventRecord(go, ctx->stream));
+      APG_CHECK_HIP(hipStreamWaitEvent(ctx->aux, go, 0));
+      APG_CHECK_HIP(hipEventDestroy(go));
+      APG_CHECK_HIP(hipEventCreateWithFlags(&link_done, hipEventDisableTiming));
+      {
+        StreamSwap sw(ctx, ctx->aux);
+        APG_TRY(ext_link(ctx, et, n_solid));
+      }
+      APG_CHECK_HIP(hipEventRecord(link_done, ctx->aux));
+    }
     // offsets, runs, the candidates' positions and decisions, weak bits in;
     // corrected bases and quals, clean flags out
     kbegin(ctx, "pc_apply",
