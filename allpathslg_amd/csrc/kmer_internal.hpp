@@ -54,18 +54,26 @@ uint32_t sk_pack_split(int K);
 // solid set of received records + per-record weak masks (receive order).
 // split_recs: the records were cut by sk_pack_split (<= 32 bases), so the
 // owner's partition levels may carry them packed (16 bytes, the receive
-// index in the position field) instead of as 24-byte records.
+// index in the position field) instead of as 24-byte records.  weak + wpos
+// (the owner is the reads' own rank): the weak bits ORed straight into the
+// per-base bitmap `weak` at wpos[receive index] + t, wrec unused.
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
                         int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res,
                         int up_K = 0, uint64_t* up_hist = nullptr, size_t up_hist_len = 0,
-                        SkResult* up_res = nullptr, bool split_recs = false);
+                        SkResult* up_res = nullptr, bool split_recs = false, unsigned long long* weak = nullptr,
+                        const uint64_t* wpos = nullptr);
 bool sk_can_fuse_up(int K);
 // Owner side of the sharded fused spectrum + PreCorrect (precorrect.hip): as
 // apg_shard_solid_weak, plus this shard's K+1 spectrum (up_hist) from the
 // same records (on the side stream: side_join before reading up_hist).
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
-                           SkResult* up_res, bool split_recs = false, uint64_t n_kmers = ~0ull);
+                           SkResult* up_res, bool split_recs = false, uint64_t n_kmers = ~0ull,
+                           unsigned long long* weak = nullptr, const uint64_t* wpos = nullptr);
+// PreCorrect's correction pass over reads whose weak bitmap ("pc_weak") the
+// owner count already built (sk_shard_solid_weak with weak + wpos)
+int precorrect_weak_built(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const void* d_solid,
+                          uint64_t n_solid, unsigned long long* weak, apg_pc_stats* st);
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
                    uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
                    SkResult* res);

@@ -1622,7 +1622,8 @@ int apg_shard_solid_weak(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_
 namespace apg {
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
-                           SkResult* up_res, bool split_recs, uint64_t n_kmers) {
+                           SkResult* up_res, bool split_recs, uint64_t n_kmers, unsigned long long* weak,
+                           const uint64_t* wpos) {
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid_weak: NULL argument");
   APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
@@ -1633,7 +1634,7 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   std::vector<uint64_t> rc(recv_counts, recv_counts + (size_t)n_shards * kSkShardBins);
   uint64_t n = 0;
   for (auto c : rc) n += c;
-  APG_REQUIRE(n == 0 || (d_recv && d_mask), "apg_shard_solid_weak: d_recv or d_mask is NULL");
+  APG_REQUIRE(n == 0 || (d_recv && (d_mask || (weak && wpos))), "apg_shard_solid_weak: d_recv or d_mask is NULL");
   const SK16* recs = static_cast<const SK16*>(d_recv);
   int err = APG_OK;
   // the received K-mer instances: given by the caller (the senders' counts,
@@ -1642,7 +1643,7 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   APG_TRY(err);
   SkResult sr;
   APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr,
-                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res, split_recs));
+                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res, split_recs, weak, wpos));
   // The K+1 pass (side stream, kicked at the correction's stage as on one
   // GPU) reads only this count's record buffers: the caller's mask return,
   // solid-set gather and correction run beside it, and the caller joins it
@@ -1652,6 +1653,16 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   ctx->solid_valid = true;
   *n_solid = sr.n_solid;
   return APG_OK;
+}
+
+int precorrect_weak_built(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const void* d_solid,
+                          uint64_t n_solid, unsigned long long* weak, apg_pc_stats* st) {
+  APG_TRY(check_pc(p));
+  APG_REQUIRE(p.K >= 9 && p.K <= 29, "apg_precorrect_weak: K must be in [9, 29]");
+  APG_REQUIRE(dr->n_reads == 0 || dr->d_quals, "apg_precorrect_weak: read set has no qualities");
+  APG_REQUIRE(n_solid == 0 || d_solid, "apg_precorrect_weak: d_solid is NULL");
+  std::memset(st, 0, sizeof *st);
+  return correct_pass(ctx, dr, p, static_cast<const uint64_t*>(d_solid), n_solid, st, weak);
 }
 }  // namespace apg
 

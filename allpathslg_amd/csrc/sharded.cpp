@@ -185,6 +185,7 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
     Exchanged x;
     uint64_t n_local = 0;
     void* smask = nullptr;
+    unsigned long long* wbits = nullptr;  // world size 1: the bitmap the owner count built
     if (weak) {
       APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
                                [&](void* send) {
@@ -195,16 +196,27 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
                                },
                                &x));
       void* rmask = nullptr;
-      APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>(x.n_out * 4, 64), &rmask));
+      if (P == 1) {
+        // the owner is this rank and the receive order the send order: the
+        // count ORs the weak bits straight into the reads' bitmap at
+        // x_pos[receive index] (no masks, no return, no apply pass)
+        void* wb = nullptr;
+        APG_TRY(workspace(ctx, "pc_weak", (reads->n_bases / 64 + 2) * 8, &wb));
+        APG_CHECK_HIP(hipMemsetAsync(wb, 0, (reads->n_bases / 64 + 2) * 8, ctx->stream));
+        wbits = static_cast<unsigned long long*>(wb);
+      } else {
+        APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>(x.n_out * 4, 64), &rmask));
+      }
+      const uint64_t* wpos = wbits ? static_cast<const uint64_t*>(pos) : nullptr;
       if (up_hist && cyc == 0) {
         // the K+1 pass runs on the side stream beside the mask return, the
         // solid-set gather and the correction below; joined after them
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, up_hist,
-                                       up_hist_len, &up_res, true, n_kmers_in));
+                                       up_hist_len, &up_res, true, n_kmers_in, wbits, wpos));
         up_pending = true;
       } else {
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, nullptr,
-                                       0, nullptr, true, n_kmers_in));
+                                       0, nullptr, true, n_kmers_in, wbits, wpos));
       }
       // masks travel back: the splits reversed, 4 bytes per record
       std::vector<uint64_t> mb_out(P), mb_in(P);
@@ -212,8 +224,8 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
         mb_out[q] = x.rb[q] / 16 * 4;
         mb_in[q] = x.sb[q] / 16 * 4;
       }
-      if (P == 1) {  // the owner is this rank: the masks are where they were written
-        smask = rmask;
+      if (P == 1) {  // the weak bits are in the reads' bitmap already
+        smask = nullptr;
       } else {
         APG_TRY(workspace(ctx, "x_smask", std::max<uint64_t>(x.n_in * 4, 64), &smask));
         APG_TRY(c->alltoallv(rmask, mb_out.data(), smask, mb_in.data()));
@@ -232,7 +244,9 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
     uint64_t n_solid = 0;
     APG_TRY(gather_all(ctx, c, local, n_local, 8, "x_solid", &solid, &n_solid));
     apg_pc_stats st;
-    if (weak)
+    if (wbits)
+      APG_TRY(precorrect_weak_built(ctx, reads, p, solid, n_solid, wbits, &st));
+    else if (weak)
       APG_TRY(apg_precorrect_weak(ctx, reads, &p, solid, n_solid, pos, smask, x.n_in, &st));
     else
       APG_TRY(apg_precorrect_solid(ctx, reads, &p, solid, n_solid, &st));

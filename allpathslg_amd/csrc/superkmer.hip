@@ -548,7 +548,24 @@ struct SkOut {
   unsigned long long* inst;    // k_sk_bucket<.., UP>: K+1-mer instances counted (or null)
   uint32_t* sused;             // solid mode: entries written in each kSolidChunk-slot chunk of `solid`
   uint64_t n_sused;
+  // with `weak`: record.pos is a receive index and the record's first base is
+  // at wpos[record.pos] (the sharded count at world size 1, where the owner is
+  // the reads' own rank: no mask return, no separate apply pass)
+  const uint64_t* wpos = nullptr;
 };
+
+// A record's weak-K-mer mask m (bit t: K-mer t) at record position b: into the
+// per-record mask array, or ORed into the per-base bitmap (one or two words).
+__device__ __forceinline__ void sk_weak_write(const SkOut& o, uint64_t b, uint32_t m) {
+  if (o.wrec) {
+    o.wrec[b] = m;
+    return;
+  }
+  if (o.wpos) b = o.wpos[b];
+  const uint32_t sh = (uint32_t)(b & 63);
+  atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
+  if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
+}
 
 // Solid-list reservations: a block takes whole chunks of kSolidChunk slots
 // from gstats[2] and fills them bucket by bucket (a same-address atomic per
@@ -812,13 +829,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
             if (sh + nk > 64) x |= wbits[w + 1] << (64 - sh);
             m = (uint32_t)x & (nk >= 32 ? ~0u : ((1u << nk) - 1));
           }
-          if (o.wrec) {
-            if (m) o.wrec[b] = m;  // zeroed beforehand: only records with weak K-mers write
-          } else if (m) {
-            const uint32_t sh = (uint32_t)(b & 63);
-            atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
-            if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
-          }
+          if (m) sk_weak_write(o, b, m);  // wrec is zeroed beforehand: only records with weak K-mers write
           ib += tot;
         }
         __syncthreads();
@@ -851,15 +862,7 @@ __global__ void __launch_bounds__(NT) k_sk_bucket(const R* __restrict__ rec,
           }
           wave_lds_sync();
           const uint32_t m = wmask[tid];
-          if (c0 + tid < nr && m) {
-            if (o.wrec) {
-              o.wrec[b] = m;
-            } else {
-              const uint32_t sh = (uint32_t)(b & 63);
-              atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
-              if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
-            }
-          }
+          if (c0 + tid < nr && m) sk_weak_write(o, b, m);
           wave_lds_sync();
         }
         __syncthreads();
@@ -1350,14 +1353,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
           if (rs >= kDdTab) continue;
           const uint32_t m = rcnt[rs];
           if (!m) continue;
-          const uint64_t b = rp_[c] & ((1ull << 52) - 1);
-          if (o.wrec) {
-            o.wrec[b] = m;
-          } else {
-            const uint32_t sh = (uint32_t)(b & 63);
-            atomicOr(&o.weak[b >> 6], (unsigned long long)m << sh);
-            if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&o.weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
-          }
+          sk_weak_write(o, rp_[c] & ((1ull << 52) - 1), m);
         }
       }
     }
@@ -1552,7 +1548,7 @@ template <typename R>
 __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                               const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
                               SkP p, BigTab g, uint32_t min_solid, unsigned long long* __restrict__ weak,
-                              uint32_t* __restrict__ wrec) {
+                              uint32_t* __restrict__ wrec, const uint64_t* __restrict__ wpos) {
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = k0 + threadIdx.x;
@@ -1574,7 +1570,7 @@ __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restr
     if (wrec) {
       if (m) wrec[rec_pos(r, p)] = m;
     } else if (m) {  // the record's mask in one or two ORs, as k_sk_bucket
-      const uint64_t b = rec_pos(r, p);
+      const uint64_t b = wpos ? wpos[rec_pos(r, p)] : rec_pos(r, p);
       const uint32_t sh = (uint32_t)(b & 63);
       atomicOr(&weak[b >> 6], (unsigned long long)m << sh);
       if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
@@ -1973,7 +1969,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                             size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr,
                             const SK16* src16 = nullptr, int up_K = 0, uint64_t* up_hist = nullptr,
                             size_t up_hist_len = 0, SkResult* up_res = nullptr, const SKP* srcp = nullptr,
-                            bool split16 = false, bool wide = false) {
+                            bool split16 = false, bool wide = false, const uint64_t* wpos = nullptr) {
   SkP p = make_skp(K);
   p.wide = wide;
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
@@ -2177,6 +2173,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     SkOut o{ghist, hl, gstats, ovf, sl, solid_cap, min_solid, solid ? weak : nullptr, solid ? wrec : nullptr, dprof,
              (uint32_t)(!solid || (hist && hist_len))};
     o.sused = sused;
+    o.wpos = solid ? wpos : nullptr;
     o.n_sused = solid ? solid_cap / kSolidChunk : 0;
     // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
     // LDS (owner map, recorded slots) and the table amortised over 8 waves give
@@ -2254,7 +2251,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         if constexpr (RecPos<RB>::value) {
           if (o.weak || o.wrec)
             k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o.weak,
-                                                        o.wrec);
+                                                        o.wrec, o.wpos);
         }
         kend(ctx);
         APG_CHECK_HIP(hipGetLastError());
@@ -2443,17 +2440,22 @@ __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __re
 // bucket kernel's weak pass writes each mask with a plain store.
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
                         int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res, int up_K, uint64_t* up_hist,
-                        size_t up_hist_len, SkResult* up_res, bool split_recs) {
+                        size_t up_hist_len, SkResult* up_res, bool split_recs, unsigned long long* weak,
+                        const uint64_t* wpos) {
   APG_REQUIRE(K >= 9 && K <= 32, "sk_shard_solid_weak: K must be in [9, 32]");
   uint64_t n = 0;
   for (auto c : rec_counts) n += c;
   SK24* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
-  if (n) APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
+  // weak + wpos (world size 1): the weak bits straight into the reads' bitmap
+  // at wpos[receive index], no per-record masks
+  if (weak) wrec = nullptr;
+  if (n && wrec) APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
   // the first partition level reads the SK16 records and writes them as SK24
   // with their receive index (no separate widening pass)
-  return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, nullptr, res,
-                                wrec, recv, up_K, up_hist, up_hist_len, up_res, nullptr, split_recs);
+  return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, weak, res,
+                                wrec, recv, up_K, up_hist, up_hist_len, up_res, nullptr, split_recs, false,
+                                weak ? wpos : nullptr);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {
