@@ -966,8 +966,13 @@ struct SortCols {
   uint32_t* opay;
 };
 
+// omat: the scanned count matrix, or null: the block's digit bases from the
+// raw counts cmat (few tiles: every block reads the whole matrix, no scan
+// launches — the pass is launch-bound at the unipath counts of a genome)
+constexpr uint32_t kSortFuseTiles = 128;
 __global__ void __launch_bounds__(kSortThreads) k_lsd_scatter(SortCols c, int sel, uint64_t n, int shift,
-                                                              const uint64_t* __restrict__ omat) {
+                                                              const uint64_t* __restrict__ omat,
+                                                              const uint32_t* __restrict__ cmat) {
   constexpr int nw = kSortThreads / 64;
   __shared__ uint32_t wh[nw][256];
   __shared__ unsigned long long base[256];
@@ -975,7 +980,31 @@ __global__ void __launch_bounds__(kSortThreads) k_lsd_scatter(SortCols c, int se
   const uint64_t s = (uint64_t)b * kSortTile, e = min(n, s + kSortTile);
   const uint32_t tn = (uint32_t)(e - s);
   const uint64_t* key = sel == 0 ? c.k0 : sel == 1 ? c.k1 : c.k2;
-  base[threadIdx.x] = omat[(uint64_t)threadIdx.x * G + b];
+  if (omat) {
+    base[threadIdx.x] = omat[(uint64_t)threadIdx.x * G + b];
+  } else {
+    // digit d = thread: its total over all tiles and over the tiles before b
+    const uint32_t* row = cmat + (uint64_t)threadIdx.x * G;
+    uint32_t tot = 0, before = 0;
+    for (uint32_t q = 0; q < G; ++q) {
+      const uint32_t x = row[q];
+      tot += x;
+      before += q < b ? x : 0u;
+    }
+    wh[0][threadIdx.x] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // 256 digit totals, exclusive scan
+      unsigned long long run = 0;
+      for (int d = 0; d < 256; ++d) {
+        const uint32_t x = wh[0][d];
+        base[d] = run;
+        run += x;
+      }
+    }
+    __syncthreads();
+    base[threadIdx.x] += before;
+    __syncthreads();  // wh is cleared below
+  }
   for (int d = lane; d < 256; d += 64) wh[w][d] = 0;
   const uint32_t rows = (tn + 63) / 64, rpw = (rows + nw - 1) / nw;
   const uint32_t r0 = min(rows, w * rpw), r1 = min(rows, r0 + rpw);
@@ -2007,10 +2036,11 @@ static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, 
         kbegin(ctx, "u_sort_count", P * 8);
         k_lsd_count<<<Gs, kSortThreads, 0, ctx->stream>>>(key, P, shift, scm);
         kend(ctx);
-        APG_TRY(scan_u32_u64(ctx, scm, 256 * Gs, som, "us"));
+        const bool fuse = Gs <= kSortFuseTiles;
+        if (!fuse) APG_TRY(scan_u32_u64(ctx, scm, 256 * Gs, som, "us"));
         SortCols c{a0, a1, a2, ap, b0, b1, b2, bp};
         kbegin(ctx, "u_sort_scatter", P * 28 * 2);
-        k_lsd_scatter<<<Gs, kSortThreads, 0, ctx->stream>>>(c, sel, P, shift, som);
+        k_lsd_scatter<<<Gs, kSortThreads, 0, ctx->stream>>>(c, sel, P, shift, fuse ? nullptr : som, scm);
         kend(ctx);
         std::swap(a0, b0);
         std::swap(a1, b1);
