@@ -43,9 +43,14 @@ def test_fill_branches_gpu(gpu_ctx):
     assert list(status) == [3, 3]
 
 
-@pytest.mark.parametrize("seed,K,lo,hi", [(3, 24, 126, 234), (4, 20, 150, 220), (5, 28, 100, 260)])
-def test_fill_matches_oracle_synthetic(gpu_ctx, seed, K, lo, hi):
-    g = synth_genome(150_000, seed)
+# K <= 25: two-level extension slots (successor's successors, a free walk
+# step); K >= 26: the one-level layout.  rep: a repeat-rich genome (branching
+# walks, budget pairs).
+@pytest.mark.parametrize("seed,K,lo,hi,rep", [(3, 24, 126, 234, False), (4, 20, 150, 220, False),
+                                              (5, 28, 100, 260, False), (6, 25, 126, 234, False),
+                                              (7, 26, 126, 234, False), (8, 24, 126, 234, True)])
+def test_fill_matches_oracle_synthetic(gpu_ctx, seed, K, lo, hi, rep):
+    g = synth_genome(150_000, seed, repeats=True if rep else None)
     reads = synth_reads(g, 15_000, seed=seed + 100)
     fixed, _ = oracle.precorrect(reads, K=24)
     solid = oracle.solid_hashes(reads, K, 3)
