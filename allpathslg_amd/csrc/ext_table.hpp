@@ -233,5 +233,6 @@ __device__ __forceinline__ uint32_t ext_finish(const ExtTab& t, const ExtProbe& 
 // bits alone may run beside that pass: it writes only bits 8-15).
 int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const char* ws, const char* kname,
               ExtTab* out, bool link = true);
-int ext_link(apg_ctx* ctx, const ExtTab& t, uint64_t n_solid);
+// frac: of ext_link's usual grid (a trickle beside other work)
+int ext_link(apg_ctx* ctx, const ExtTab& t, uint64_t n_solid, double frac = 1.0);
 }  // namespace apg

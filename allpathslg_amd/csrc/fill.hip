@@ -108,12 +108,13 @@ __global__ void k_ext_link(ExtTab t) {
   }
 }
 
-int ext_link(apg_ctx* ctx, const ExtTab& t, uint64_t n_solid) {
+int ext_link(apg_ctx* ctx, const ExtTab& t, uint64_t n_solid, double frac) {
   if (t.ks != 16 || !n_solid) return APG_OK;
   // algorithmic bytes: the table read + ~2 (K-1)-mers per solid K-mer, each
   // with two 32-byte group reads and its slot written back
   kbegin(ctx, "ext_link", (t.mask + 1) * 8 + n_solid * (2 * 64 + 8));
-  k_ext_link<<<grid_for(ctx, t.mask + 1), 256, 0, ctx->stream>>>(t);
+  const uint64_t g = grid_for(ctx, t.mask + 1);
+  k_ext_link<<<std::max<uint64_t>(1, (uint64_t)(g * frac)), 256, 0, ctx->stream>>>(t);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   return APG_OK;

@@ -989,10 +989,17 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   // decisions.  Same box: 144.5 vs 145.4-146.0 ms per bench step (decisions
   // 10.6 vs 15.1 ms); the K+1 pass kicked after the decisions too
   // (APG_SK_UP_AT=3) exposes it: 156.9 ms.
-  static const bool link_late = [] {
+  // APG_PC_LINK_AT=2: right behind the inserts on APG_PC_LINK_FRAC (0.25)
+  // of its grid, a trickle beside the decisions.
+  static const int link_at = [] {
     const char* e = getenv("APG_PC_LINK_AT");
-    return !(e && atoi(e) == 0);
+    return e ? atoi(e) : 1;
   }();
+  static const double link_frac = [] {
+    const char* e = getenv("APG_PC_LINK_FRAC");
+    return e ? std::min(1.0, std::max(0.01, atof(e))) : 0.25;
+  }();
+  const bool link_late = link_at == 1;
   bool link_pending = false;  // the table's link pass still to launch (link_late)
   if (ext && weak) {
     const char* ae = getenv("APG_PC_EXT_AUX");
@@ -1012,7 +1019,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
         StreamSwap sw(ctx, ax);
         rc = ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et, false);
         if (rc == APG_OK && hipEventRecord(ext_done, ax) != hipSuccess) rc = APG_E_HIP;
-        if (rc == APG_OK && !link_late) rc = ext_link(ctx, et, n_solid);
+        if (rc == APG_OK && !link_late) rc = ext_link(ctx, et, n_solid, link_at == 2 ? link_frac : 1.0);
         link_pending = rc == APG_OK && link_late && et.ks == 16;
         if (rc == APG_OK && et.ks == 16 && !link_late) {
           if (hipEventCreateWithFlags(&link_done, hipEventDisableTiming) != hipSuccess ||
