@@ -244,12 +244,16 @@ __device__ __forceinline__ uint64_t walk_window(uint64_t atail, unsigned __int12
   return ((atail << (2 * d)) | (uint64_t)pv) & t.m1;
 }
 
-// Two passes keep one deep search from holding a whole wave: pass 1 (every
-// pair, list == null) searches with a cap of kFillCap1 expansions and defers
-// the pairs that reach it; pass 2 runs the deferred ones (list, *list_n)
-// with the full max_steps.  The walk is deterministic, so a pair that ends
-// within the cap ends exactly as it would with the full budget.
-constexpr uint32_t kFillCap1 = 96;
+// Optional two passes (APG_FILL_CAP1=c): pass 1 (every pair, list == null)
+// searches with a cap of c expansions and defers the pairs that reach it;
+// pass 2 runs the deferred ones (list, *list_n) with the full max_steps.  The
+// walk is deterministic, so a pair that ends within the cap ends exactly as
+// it would with the full budget.  They kept one deep search from holding a
+// whole wave before lanes refilled one by one; with the refill, one pass is
+// faster (same box, fill ms iid / repeat-rich genome: cap 96 11.29 / 44.5,
+// 48 11.36 / 45.8, 192 11.09 / 46.3, 384 11.10 / 51.0, one pass 11.05 /
+// 42.0 — the second pass re-walked every deferred pair's first c steps).
+constexpr uint32_t kFillCap1 = 1u << 30;
 // A wave refills its idle lanes with new pairs once at most this many lanes
 // are still walking (APG_FILL_REFILL for A/B: a higher mark keeps more lanes
 // walking, a lower one batches more lanes into each refill's start phase).
@@ -829,11 +833,13 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     const int xpct = std::min(100, std::max(0, xpe ? atoi(xpe) : kFillXpct));
     const int xsteps = std::min(255, xse ? std::max(0, atoi(xse)) : kFillXsteps) | (xce && !strcmp(xce, "1") ? 256 : 0) |
                        (xpct << 16);
+    const char* c1e = getenv("APG_FILL_CAP1");  // pass 1's expansion cap (A/B)
+    const uint32_t cap1 = c1e ? (uint32_t)std::max(1, atoi(c1e)) : kFillCap1;
     auto fill = [&](auto kern) {
       kern<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc,
-                                          std::min(kFillCap1, p.max_steps), nullptr, nullptr, defer, ndefer,
+                                          std::min(cap1, p.max_steps), nullptr, nullptr, defer, ndefer,
                                           ndefer + 1, bcache, bfilt, refill, xsteps);
-      if (p.max_steps > kFillCap1)  // the deferred pairs: a device-side count, no host round trip
+      if (p.max_steps > cap1)  // the deferred pairs: a device-side count, no host round trip
         kern<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
                                             defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill, xsteps);
     };

@@ -21,7 +21,9 @@ cases = [("base", 1024, {}), ("pass1", 96, {}), ("x0", 1024, {"APG_FILL_XSTEPS":
          ("x1nc", 1024, {"APG_FILL_XSTEPS": "1", "APG_FILL_XCACHED": "0"}),
          ("p0", 1024, {"APG_FILL_XPCT": "0"}), ("p25", 1024, {"APG_FILL_XPCT": "25"}),
          ("p75", 1024, {"APG_FILL_XPCT": "75"}), ("p90", 1024, {"APG_FILL_XPCT": "90"}),
-         ("p50x4", 1024, {"APG_FILL_XSTEPS": "4"}), ("base2", 1024, {})]
+         ("p50x4", 1024, {"APG_FILL_XSTEPS": "4"}),
+         ("c48", 1024, {"APG_FILL_CAP1": "48"}), ("c192", 1024, {"APG_FILL_CAP1": "192"}),
+         ("c384", 1024, {"APG_FILL_CAP1": "384"}), ("c1024", 1024, {"APG_FILL_CAP1": "1024"}), ("base2", 1024, {})]
 sel = os.environ.get("FILL_CASES")
 if sel:
     cases = [c for c in cases if c[0] in sel.split(",")]
