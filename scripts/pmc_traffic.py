@@ -49,6 +49,9 @@ KERNELS = [
     ("void apg::k_part_count<apg::SK16>", "s_part_count", "stream"),
     ("void apg::k_part_count<apg::SK24>", "s24_part_count", "stream"),
     ("apg::k_fill(", "fill", "random"),
+    ("void apg::k_fill<16>", "fill", "random"),  # round 4: the slot layout as a template parameter
+    ("void apg::k_fill<8>", "fill", "random"),
+    ("apg::k_ext_link", "ext_link", "random"),
     ("apg::k_fill_write", "fill_write", "stream"),
     ("apg::k_pc_decide", "precorrect", "random"),
     ("void apg::k_pc_candidates<true>", "pc_cand_write", "stream"),  # the bench's timed-region name
