@@ -79,6 +79,37 @@ __global__ void k_fill_ext_insert(const uint64_t* __restrict__ solid, uint64_t n
   }
 }
 
+// Sorted inserts: each solid K-mer's two (K-1)-mer entries, key << 8 | bit,
+// with the top D bits of their home slot above them (D <= 8, D <= 64 - 8 -
+// 2(K-1)),
+// are grouped by those bits (one partition level) before they are inserted,
+// so the concurrent inserts work on a few table regions at a time instead of
+// the whole table: the claims and ORs meet lines the last ones left in the
+// caches, where the unsorted inserts read and wrote back a random line each.
+__global__ void k_ext_entries(const uint64_t* __restrict__ solid, uint64_t n, HashP hK, ExtTab t, int lgT, int D,
+                              uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = kunhash(hK, solid[i]);
+    const uint64_t u = c >> 2, ur = rc_bases(u, t.n1, t.m1);
+    const uint32_t b = (uint32_t)(c & 3);
+    const uint64_t ku = u <= ur ? u : ur;
+    const uint32_t bu = u <= ur ? 16u << b : 1u << (3 - b);
+    const uint64_t v = c & t.m1, vr = rc_bases(v, t.n1, t.m1);
+    const uint32_t a = (uint32_t)(c >> (2 * t.n1));
+    const uint64_t kv = v <= vr ? v : vr;
+    const uint32_t bv = v <= vr ? 1u << a : 16u << (3 - a);
+    const uint64_t du = ext_home(t, ku) >> (lgT - D), dv = ext_home(t, kv) >> (lgT - D);
+    out[2 * i] = (du << (64 - D)) | (ku << 8) | bu;
+    out[2 * i + 1] = (dv << (64 - D)) | (kv << 8) | bv;
+  }
+}
+__global__ void k_ext_insert_entries(const uint64_t* __restrict__ e, uint64_t m, ExtTab t, int D) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = e[j];
+    ext_set(t, (x << D) >> (D + 8), (uint32_t)x & 0xffu);
+  }
+}
+
 // Two-level bits of every occupied slot (ext_table.hpp): the successor mask
 // of its unique successor and the predecessor mask of its unique
 // predecessor, both lookups in flight together.  The inserts are complete,
@@ -147,10 +178,41 @@ int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const
   APG_TRY(workspace_t(ctx, ws, T, &slot));
   APG_CHECK_HIP(hipMemsetAsync(slot, 0xff, T * 8, ctx->stream));
   *out = ext_tab(slot, T - 1, K);
-  kbegin(ctx, kname, n_solid * (8 + 2 * 64));
-  if (n_solid)
-    k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out);
-  kend(ctx);
+  // sorted inserts (APG_EXT_SORTED=1; default: in list order) when the digit
+  // fits beside the entry and the two entry buffers (16 B per solid K-mer
+  // each) do.  Measured on the bench step (same box): inserts 9.42 -> 7.36 ms
+  // but entries + partition 2.6-3.4 ms more on the auxiliary stream, step
+  // 144.6 -> 147.2 ms; kept as an A/B switch.
+  int lgT = 0;
+  while ((1ull << lgT) < T) ++lgT;
+  // D <= 8: a partition level splits into at most 256 children (partition.hip)
+  const int D = std::min(8, std::min(lgT - 2, 64 - 8 - 2 * (K - 1)));
+  static const bool sorted_on = getenv("APG_EXT_SORTED") && !strcmp(getenv("APG_EXT_SORTED"), "1");
+  bool sorted = sorted_on && D >= 6 && n_solid >= (1u << 16) && 2 * n_solid < (1ull << 32);  // part_level: < 2^32 per group
+  if (sorted) {
+    const uint64_t need = 2 * 2 * n_solid * 8;
+    if (device_free_bytes(ctx) < need + (4ull << 30)) sorted = false;
+  }
+  if (sorted) {
+    uint64_t *e0 = nullptr, *e1 = nullptr, *child = nullptr;
+    APG_TRY(workspace_t(ctx, "ext_e0", 2 * n_solid, &e0));
+    APG_TRY(workspace_t(ctx, "ext_e1", 2 * n_solid, &e1));
+    APG_TRY(workspace_t(ctx, "ext_child", (1ull << D) + 1, &child));
+    kbegin(ctx, "ext_entries", n_solid * (8 + 16));
+    k_ext_entries<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out, lgT, D, e0);
+    kend(ctx);
+    APG_CHECK_HIP(hipGetLastError());
+    const std::vector<std::vector<Seg>> parents{{Seg{0, 2 * n_solid}}};
+    APG_TRY(part_level<uint64_t>(ctx, e0, e1, parents, 64 - D, D, 2 * n_solid, child, nullptr, "ext"));
+    kbegin(ctx, kname, n_solid * 2 * (8 + 64));
+    k_ext_insert_entries<<<grid_for(ctx, 2 * n_solid), 256, 0, ctx->stream>>>(e1, 2 * n_solid, *out, D);
+    kend(ctx);
+  } else {
+    kbegin(ctx, kname, n_solid * (8 + 2 * 64));
+    if (n_solid)
+      k_fill_ext_insert<<<grid_for(ctx, n_solid), 256, 0, ctx->stream>>>(list, n_solid, make_hashp(K), *out);
+    kend(ctx);
+  }
   APG_CHECK_HIP(hipGetLastError());
   return link ? ext_link(ctx, *out, n_solid) : APG_OK;
 }

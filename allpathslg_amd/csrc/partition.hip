@@ -295,6 +295,8 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vecto
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag, int kshift,
                bool wide) {
   constexpr int kTile = PartGeom<RO>::tile;
+  // the count / scan / scatter kernels keep one LDS counter per child (256)
+  APG_REQUIRE(bits >= 1 && bits <= 8, "part_level: a level splits into 2 .. 256 children");
   const uint32_t ndig = 1u << bits;
   const uint64_t np = parents.size();
   // ~24K chunks per level: enough workgroups, short count-matrix rows
