@@ -296,7 +296,7 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vecto
                bool wide) {
   constexpr int kTile = PartGeom<RO>::tile;
   // the count / scan / scatter kernels keep one LDS counter per child (256)
-  APG_REQUIRE(bits >= 1 && bits <= 8, "part_level: a level splits into 2 .. 256 children");
+  APG_REQUIRE(bits >= 0 && bits <= 8, "part_level: a level splits into 1 .. 256 children");
   const uint32_t ndig = 1u << bits;
   const uint64_t np = parents.size();
   // ~24K chunks per level: enough workgroups, short count-matrix rows
