@@ -6,10 +6,12 @@
 //
 //   1. k_fill_ext_insert: the solid K-mer set (hashes of canonical K-mers) is
 //      turned into a (K-1)-mer extension table: one 8-byte slot per canonical
-//      (K-1)-mer = key << 8 | 4 left + 4 right extension bits.  K-mer x is
-//      solid  <=>  the slot of x's first K-1 bases holds x's last base as a
-//      successor.  One lookup therefore answers all 4 successors of a walk
-//      node, where a hash set of K-mers would need 4.
+//      (K-1)-mer = key << 8 | 4 left + 4 right extension bits (K <= 25:
+//      key << 16 with the two-level bits that k_ext_link adds, ext_table.hpp).
+//      K-mer x is solid  <=>  the slot of x's first K-1 bases holds x's last
+//      base as a successor.  One lookup therefore answers all 4 successors of
+//      a walk node, where a hash set of K-mers would need 4 — and with the
+//      two-level bits, the next node's successors too when the node has one.
 //   2. k_fill: one thread per pair.  Overlap closures (I < La+Lf) by 32-base
 //      word compares of A's suffix with F = rc(B)'s prefix, bridge K-mers by
 //      extension lookups; then the depth-first walk from A's last K-1 bases,

@@ -16,14 +16,15 @@ reads = synth_reads(g, n // 2, seed=0xA11BA7 + 32, with_quals=True, threads=16)
 print("reads ready", flush=True)
 cases = [("base", 1024, {}), ("pass1", 96, {}), ("x0", 1024, {"APG_FILL_XSTEPS": "0"}),
          ("x64", 1024, {"APG_FILL_XSTEPS": "64"}), ("refill8", 1024, {"APG_FILL_REFILL": "8"}),
-         ("refill48", 1024, {"APG_FILL_REFILL": "48"}), ("nocache", 1024, {"APG_FILL_BRANCH_CACHE": "0"}),
+         ("refill48", 1024, {"APG_FILL_REFILL": "48"}),
+         ("refill24", 1024, {"APG_FILL_REFILL": "24"}), ("refill40", 1024, {"APG_FILL_REFILL": "40"}), ("nocache", 1024, {"APG_FILL_BRANCH_CACHE": "0"}),
          ("x1", 1024, {"APG_FILL_XSTEPS": "1"}), ("x8nc", 1024, {"APG_FILL_XCACHED": "0"}),
          ("x1nc", 1024, {"APG_FILL_XSTEPS": "1", "APG_FILL_XCACHED": "0"}),
          ("p0", 1024, {"APG_FILL_XPCT": "0"}), ("p25", 1024, {"APG_FILL_XPCT": "25"}),
          ("p75", 1024, {"APG_FILL_XPCT": "75"}), ("p90", 1024, {"APG_FILL_XPCT": "90"}),
          ("p50x4", 1024, {"APG_FILL_XSTEPS": "4"}),
          ("c48", 1024, {"APG_FILL_CAP1": "48"}), ("c192", 1024, {"APG_FILL_CAP1": "192"}),
-         ("c384", 1024, {"APG_FILL_CAP1": "384"}), ("c1024", 1024, {"APG_FILL_CAP1": "1024"}), ("base2", 1024, {})]
+         ("c384", 1024, {"APG_FILL_CAP1": "384"}), ("c1024", 1024, {"APG_FILL_CAP1": "1024"}), ("hash1", 1024, {"APG_EXT_HASH": "1"}), ("base2", 1024, {})]
 sel = os.environ.get("FILL_CASES")
 if sel:
     cases = [c for c in cases if c[0] in sel.split(",")]
