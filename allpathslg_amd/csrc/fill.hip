@@ -162,8 +162,11 @@ int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const
   // dead buffers are released first, and if it still does not fit the table
   // takes 2 slots per solid K-mer (load <= 0.5 on a genome: 69 GB at human
   // scale; DESIGN.md §7 memory model).
+  // APG_EXT_SLOTS=s: s slots per solid K-mer before rounding to a power of
+  // two (A/B; default 4)
+  static const uint64_t spk = getenv("APG_EXT_SLOTS") ? std::max(1, atoi(getenv("APG_EXT_SLOTS"))) : 4;
   uint64_t T = 1024;
-  while (T < 4 * n_solid) T <<= 1;
+  while (T < spk * n_solid) T <<= 1;
   {
     auto it = ctx->ws.find(ws);
     const uint64_t have = it == ctx->ws.end() ? 0 : it->second.bytes;
