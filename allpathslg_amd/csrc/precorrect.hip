@@ -807,9 +807,49 @@ __global__ void __launch_bounds__(kPcTileReads) k_pc_candidates(
 // not all weak — by extension lookups on the read as it was, the state the
 // sequential rule sees unless a correction lies within K before it — is
 // kPcNotSuspect.
+// Covering K-mers a..b of an alternative's window wa (bases [p-K, p+K],
+// LSB-first) all solid, through two-level slots: the (K-1)-mer at c answers
+// K-mers c-1 and c by its pred / succ bits, c+1 by its successor's successors
+// and c-2 by its predecessor's predecessors where those apply (a lookup of
+// c-1 of its own where they do not) — as k_ecj_trim.  Needs a linked table.
+__device__ __forceinline__ bool pc_all_solid2(const ExtTab& et, unsigned __int128 wa, uint32_t p, int K, int a, int b,
+                                              uint32_t* nl) {
+  const int o = K - (int)p;  // window index of base q: q + o
+  auto bs = [&](int q) { return (uint32_t)(wa >> (2 * (uint32_t)(q + o))) & 3u; };
+  auto y1 = [&](int c) { return (uint64_t)(wa >> (2 * (uint32_t)(c + o))) & et.m1; };
+  int u = a;
+  while (u <= b) {
+    const int c = min(u + 2, b + 1);
+    ++*nl;
+    const uint32_t e = ext_masks2_lsb(et, y1(c));
+    const bool sp = (e >> bs(c - 1)) & 1;  // K-mer c-1 (>= u)
+    if (c == u + 2) {                      // K-mer u = c-2 first
+      bool s2;
+      if (sp && ((e >> 17) & 1)) {
+        s2 = (e >> (12 + bs(u))) & 1;
+      } else {
+        ++*nl;
+        s2 = (ext_masks_lsb(et, y1(c - 1)) >> bs(u)) & 1;
+      }
+      if (!s2) return false;
+    }
+    if (!sp) return false;
+    if (c > b) return true;  // c-1 = b was the last
+    if (!((e >> (4 + bs(c + K - 1))) & 1)) return false;
+    u = c + 1;
+    if (u <= b && ((e >> 16) & 1)) {  // K-mer c+1 from the successor's successors
+      if (!((e >> (8 + bs(c + K))) & 1)) return false;
+      u = c + 2;
+    }
+  }
+  return true;
+}
+
+// two: the table carries linked two-level bits (pc_all_solid2 for the
+// alternatives)
 __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ cand, uint64_t n, int K, ExtTab et,
                                                    uint32_t* __restrict__ dec, unsigned long long* __restrict__ looks,
-                                                   bool wtest) {
+                                                   bool wtest, bool two) {
   uint32_t nl = 0;
   const unsigned __int128 km = ((unsigned __int128)1 << (2 * (K + 1))) - 1;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -856,7 +896,8 @@ __global__ void __launch_bounds__(256) k_pc_decide(const PcCand* __restrict__ ca
       surv &= surv - 1;
       const unsigned __int128 wa = (win & ~((unsigned __int128)3 << (2 * K))) | ((unsigned __int128)alt << (2 * K));
       bool ok = true;
-      for (int j = ia + 1; j <= ib + 1 && ok; j += 2) {
+      if (two) ok = pc_all_solid2(et, wa, p, K, ia, ib, &nl);
+      for (int j = ia + 1; !two && j <= ib + 1 && ok; j += 2) {
         // (K-1)-mer j with its pred base j-1 and succ base j+K-1: window bits
         // from base j-1 = p-K + (j-1-p+K)
         const uint64_t W = (uint64_t)((wa >> (2 * (uint32_t)(j - 1 - (int)p + K))) & km);
@@ -1162,9 +1203,16 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     APG_TRY(workspace_t(ctx, "pc_dec", std::max<uint64_t>(ncand, 1), &dec));
     // candidate records in, decisions out (+ 64 B per extension lookup, after the sync)
     APG_TRY(ext_wait());
+    // the alternatives through the two-level bits when the table is linked
+    // by now: the pass's own inline build or a reused one (ErrorCorrectJump's
+    // jump reads), not the weak path's, whose link pass runs after the
+    // decisions (APG_PC_TWO=0: pairs as before)
+    static const bool two_env = !(getenv("APG_PC_TWO") && !strcmp(getenv("APG_PC_TWO"), "0"));
+    const bool pc_two = two_env && et.ks == 16 && !weak;
     kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 4));
     if (ncand)
-      k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups, !weak);
+      k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups, !weak,
+                                                                  pc_two);
     kend(ctx);
     APG_TRY(side_kick(ctx, 3));  // APG_SK_UP_AT=3: the K+1 pass behind the decisions' dispatch
     if (link_pending) {
