@@ -1025,23 +1025,27 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   // once the fused K+1 pass moved after the scan; with the K+1 pass beside
   // the scan as well it gained nothing (172.4 vs 171.9 ms).
   hipEvent_t ext_done = nullptr, link_done = nullptr;
-  // The link pass starts once the decisions are launched (their workgroups
-  // dispatched first); APG_PC_LINK_AT=0: right behind the inserts, beside the
-  // decisions.  Same box: 144.5 vs 145.4-146.0 ms per bench step (decisions
-  // 10.6 vs 15.1 ms); the K+1 pass kicked after the decisions too
-  // (APG_SK_UP_AT=3) exposes it: 156.9 ms.
-  // APG_PC_LINK_AT=2: right behind the inserts on APG_PC_LINK_FRAC (0.25)
-  // of its grid, a trickle beside the decisions.
+  // Where the two-level link pass runs (APG_PC_LINK_AT): 3 (default) right
+  // behind the inserts, the decisions behind it reading the two-level bits
+  // (4.1 ms instead of 10.5: an alternative's covering K-mers at up to four
+  // per lookup); 1 after the decisions, beside the edits; 0 behind the
+  // inserts beside one-level decisions; 2 as 0 on APG_PC_LINK_FRAC (0.25) of
+  // its grid.  Same box, ms per bench step: 3: 145.95 / 146.0, 1: 146.85 /
+  // 146.94; earlier, 1: 144.5 vs 0: 145.4-146.0 (decisions 10.6 vs 15.1 ms);
+  // the K+1 pass kicked after the decisions (APG_SK_UP_AT=3) exposes it.
   static const int link_at = [] {
     const char* e = getenv("APG_PC_LINK_AT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 3;
   }();
   static const double link_frac = [] {
     const char* e = getenv("APG_PC_LINK_FRAC");
     return e ? std::min(1.0, std::max(0.01, atof(e))) : 0.25;
   }();
+  // APG_PC_LINK_AT=3: the link pass right behind the inserts and the
+  // decisions behind it, so they read the two-level bits too
   const bool link_late = link_at == 1;
   bool link_pending = false;  // the table's link pass still to launch (link_late)
+  bool linked_first = false;  // the decisions wait for the link pass (link_at 3)
   if (ext && weak) {
     const char* ae = getenv("APG_PC_EXT_AUX");
     const hipStream_t ax = (ae && !strcmp(ae, "0")) ? nullptr : aux_stream(ctx);
@@ -1059,10 +1063,14 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       {
         StreamSwap sw(ctx, ax);
         rc = ext_build(ctx, list, n_solid, p.K, "pc_ext", "solid_insert", &et, false);
+        if (rc == APG_OK && link_at == 3) {
+          rc = ext_link(ctx, et, n_solid);
+          linked_first = rc == APG_OK && et.ks == 16;
+        }
         if (rc == APG_OK && hipEventRecord(ext_done, ax) != hipSuccess) rc = APG_E_HIP;
-        if (rc == APG_OK && !link_late) rc = ext_link(ctx, et, n_solid, link_at == 2 ? link_frac : 1.0);
+        if (rc == APG_OK && !link_late && link_at != 3) rc = ext_link(ctx, et, n_solid, link_at == 2 ? link_frac : 1.0);
         link_pending = rc == APG_OK && link_late && et.ks == 16;
-        if (rc == APG_OK && et.ks == 16 && !link_late) {
+        if (rc == APG_OK && et.ks == 16 && !link_late && link_at != 3) {
           if (hipEventCreateWithFlags(&link_done, hipEventDisableTiming) != hipSuccess ||
               hipEventRecord(link_done, ax) != hipSuccess)
             rc = APG_E_HIP;
@@ -1208,7 +1216,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     // jump reads), not the weak path's, whose link pass runs after the
     // decisions (APG_PC_TWO=0: pairs as before)
     static const bool two_env = !(getenv("APG_PC_TWO") && !strcmp(getenv("APG_PC_TWO"), "0"));
-    const bool pc_two = two_env && et.ks == 16 && !weak;
+    const bool pc_two = two_env && et.ks == 16 && (!weak || linked_first);
     kbegin(ctx, "precorrect", ncand * (sizeof(PcCand) + 4));
     if (ncand)
       k_pc_decide<<<grid_for(ctx, ncand), 256, 0, ctx->stream>>>(cand, ncand, p.K, et, dec, &pcnt->lookups, !weak,
