@@ -2333,7 +2333,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         const hipStream_t sd = side ? side_stream(ctx) : nullptr;
         if (sd) {
           const char* fe = getenv("APG_SK_UP_FRAC");
-          const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 1.0;
+          const double frac = fe ? std::min(1.0, std::max(0.05, atof(fe))) : 0.85;
           auto launch = [=]() -> int {
             hipEvent_t ev = nullptr;
             APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -2349,7 +2349,12 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           // LDS-staged candidate scan; same box, APG_SK_UP_FRAC 0.75 / 1.0:
           // s = 0 160.1 / —, s = 1 163.2 / 162.8, s = 2 160.9 / 158.5 ms)
           const char* ae = getenv("APG_SK_UP_AT");
-          ctx->side_kick_at = ae ? atoi(ae) : 2;
+          // Round 4's last layout (PreCorrect's link pass ahead of the
+          // decisions): stage 1 on 0.85 of a round, beside the candidate scan,
+          // the inserts and the link pass — same box 141.5-142.2 vs 145.3-145.8
+          // ms per step for stage 2 on a full round (0.80: 141.6, 0.92: 143.2,
+          // stage 0 at 0.85: 142.2)
+          ctx->side_kick_at = ae ? atoi(ae) : 1;
           if (ctx->side_kick_at <= 0)
             APG_TRY(launch());
           else
