@@ -288,6 +288,7 @@ SIGNATURES = {
     "apg_destroy": (None, [_P]),
     "apg_trim": (C.c_int, [_P]),
     "apg_timing_get": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_double), _u64p, _u64p]),
+    "apg_timing_overlapped": (C.c_int, [_P, C.c_int, _u64p]),
     "apg_timing_reset": (C.c_int, [_P]),
     "apg_reads_upload": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(_P)]),
     "apg_reads_free": (None, [_P]),
@@ -322,6 +323,7 @@ SIGNATURES = {
                                               C.POINTER(apg_pc_params), C.POINTER(apg_pc_stats)]),
     "apg_reads_download": (C.c_int, [_P, _P, _u8p, _u8p]),
     "apg_shard_solid": (C.c_int, [_P, C.c_void_p, _u64p, C.c_int, C.c_int, C.c_uint32, _u64p]),
+    "apg_partition_u64": (C.c_int, [_P, C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "apg_solid_export": (C.c_int, [_P, C.c_void_p]),
     "apg_solid_copy": (C.c_int, [_P, C.c_void_p, _u64p]),
     "apg_solid_download": (C.c_int, [_P, _u64p, _u64p]),

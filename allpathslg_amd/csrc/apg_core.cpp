@@ -220,6 +220,7 @@ void kbegin(apg_ctx* ctx, const char* name, uint64_t bytes) {
   p.b = take_event(ctx);
   p.closed = false;
   p.s = ctx->stream;
+  p.overlapped = ctx->stream != ctx->home;
   (void)hipEventRecord(p.a, ctx->stream);
   ctx->pending.push_back(p);
 }
@@ -264,6 +265,7 @@ int kflush(apg_ctx* ctx) {
     it->second.ms += ms;
     it->second.launches += 1;
     it->second.bytes += p.bytes;
+    it->second.overlapped += p.overlapped ? 1 : 0;
     ctx->event_pool.push_back(p.a);
     ctx->event_pool.push_back(p.b);
   }
@@ -343,6 +345,7 @@ int apg_create(const apg_config* cfg, apg_ctx** out) {
     set_error("apg_create: hipStreamCreate failed");
     return APG_E_HIP;
   }
+  ctx->home = ctx->stream;
   *out = ctx;
   return APG_OK;
 }
@@ -398,6 +401,14 @@ int apg_timing_get(apg_ctx* ctx, int idx, char* name, size_t name_len, double* t
   if (total_ms) *total_ms = s.ms;
   if (launches) *launches = s.launches;
   if (bytes) *bytes = s.bytes;
+  return APG_OK;
+}
+
+int apg_timing_overlapped(apg_ctx* ctx, int idx, uint64_t* overlapped) {
+  APG_REQUIRE(ctx, "apg_timing_overlapped: ctx is NULL");
+  APG_TRY(kflush(ctx));
+  if (idx < 0 || idx >= (int)ctx->korder.size()) return APG_E_ARG;
+  if (overlapped) *overlapped = ctx->kstats[ctx->korder[idx]].overlapped;
   return APG_OK;
 }
 

@@ -63,6 +63,7 @@ struct KernelStat {
   double ms = 0;
   uint64_t launches = 0;
   uint64_t bytes = 0;
+  uint64_t overlapped = 0;  // launches on the side / auxiliary stream (beside the main stream's kernels)
 };
 
 }  // namespace apg
@@ -94,6 +95,7 @@ struct apg_ctx {
   bool verbose = false;
   int kmer_dedup = 0;  // apg_config.kmer_dedup
   hipStream_t stream = nullptr;
+  hipStream_t home = nullptr;  // the main stream (ctx->stream while no StreamSwap is active)
   int n_cu = 0;
   // Side stream: work that runs beside the main stream inside one module call
   // (the fused K+1 spectrum pass beside PreCorrect's correction kernels).
@@ -127,6 +129,7 @@ struct apg_ctx {
     uint64_t bytes;
     bool closed;
     hipStream_t s;  // the stream the events bracket (kflush resolves only ctx->stream's)
+    bool overlapped;  // s is not the main stream
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
@@ -223,6 +226,10 @@ struct apg_ctx {
   bool pc_self = false;
   uint64_t pc_self_gen = 0;
   uint32_t pc_min_solid = 0;
+  // the list and size pc_self was recorded for (any later install of another
+  // list — apg_solid_upload, a sharded pass — no longer matches)
+  const uint64_t* pc_self_list = nullptr;
+  uint64_t pc_self_n = 0;
   // Per-read clean flags of that pass (1: every K-mer solid after correction,
   // 0: not, 2: not derived), valid for the read set while its gen is clean_gen.
   const uint8_t* pc_clean = nullptr;

@@ -169,9 +169,14 @@ __device__ __forceinline__ uint32_t ext_masks2_lsb(const ExtTab& t, uint64_t y) 
   const uint64_t fw = f_rev2(y) >> (64 - 2 * t.n1);
   const uint64_t rc = y ^ t.m1;
   const uint32_t e = ext_bits(t, fw < rc ? fw : rc);
+  // A palindromic (K-1)-mer (fw == rc) shares one slot between its two
+  // orientations: an insert records a K-mer around it as a succ bit or as a
+  // pred bit depending on which orientation is canonical, so both readings
+  // are OR'ed (ext_masks_lsb's rule); its two-level bits are never known.
+  if (fw == rc) return (e & 0xff) | rev4((e >> 4) & 15) | (rev4(e & 15) << 4);
   uint32_t m = e;
   if (rc < fw) m = rev4((e >> 4) & 15) | (rev4(e & 15) << 4) | (rev4((e >> 12) & 15) << 8) | (rev4((e >> 8) & 15) << 12);
-  if (t.ks != 16 || fw == rc) return m & 0xff;
+  if (t.ks != 16) return m & 0xff;
   return m | (__popc((m >> 4) & 15) == 1 ? 1u << 16 : 0u) | (__popc(m & 15) == 1 ? 1u << 17 : 0u);
 }
 

@@ -375,3 +375,17 @@ template int part_level<SK48, SK48>(apg_ctx*, const SK48*, SK48*, const std::vec
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 
 }  // namespace apg
+
+extern "C" int apg_partition_u64(apg_ctx* ctx, const uint64_t* d_in, uint64_t n, int shift, int bits,
+                                 uint64_t* d_out, uint64_t* d_child) {
+  APG_REQUIRE(ctx && d_child && (n == 0 || (d_in && d_out)), "apg_partition_u64: NULL argument");
+  APG_REQUIRE(bits >= 0 && bits <= 8, "apg_partition_u64: bits must be in [0, 8] (one LDS counter per child)");
+  APG_REQUIRE(shift >= 0 && shift + bits <= 64, "apg_partition_u64: bits [shift, shift + bits) outside the key");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::vector<std::vector<apg::Seg>> parents(1);
+  if (n) parents[0].push_back(apg::Seg{0, n});
+  // a 0-bit level is one child: the records copied as they are
+  APG_TRY(apg::part_level<uint64_t>(ctx, d_in, d_out, parents, bits ? shift : 0, bits, n, d_child, nullptr, "pu"));
+  return apg::sync(ctx);
+}
+

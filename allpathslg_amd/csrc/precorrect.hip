@@ -1304,6 +1304,8 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   dr->gen = g_edit.fetch_add(1);  // bases changed: invalidate per-read-set plans
   ctx->pc_self = self_count;
   ctx->pc_self_gen = dr->gen;
+  ctx->pc_self_list = list;
+  ctx->pc_self_n = n_solid;
   ctx->pc_min_solid = p.min_solid;
   if (clean) {
     ctx->pc_clean = clean;
@@ -1501,7 +1503,7 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   // fragment reads is skipped; else counted here
   SkResult sr;
   if (ctx->pc_list_valid && ctx->pc_self && ctx->pc_self_gen == fr->gen && ctx->pc_K == e.K &&
-      ctx->pc_min_solid == e.min_solid) {
+      ctx->pc_min_solid == e.min_solid && ctx->pc_self_list == ctx->pc_list && ctx->pc_self_n == ctx->pc_n) {
     sr.solid = const_cast<uint64_t*>(ctx->pc_list);
     sr.n_solid = ctx->pc_n;
     vlog(ctx, "error_correct_jump: the fragments' solid set from their correction pass (%llu K-mers)",
@@ -1800,6 +1802,7 @@ int apg_solid_upload(apg_ctx* ctx, int K, const uint64_t* hashes, uint64_t n) {
   ctx->pc_list_valid = false;  // "x_solid" may hold the current list
   ctx->pc_ext_valid = false;
   ctx->clean_valid = false;
+  ctx->pc_self = false;  // an uploaded list is no read set's own count (ecj_run's reuse test)
   uint64_t* list = nullptr;
   APG_TRY(workspace_t(ctx, "x_solid", std::max<uint64_t>(n, 1), &list));
   if (n) APG_CHECK_HIP(hipMemcpyAsync(list, hashes, n * 8, hipMemcpyHostToDevice, ctx->stream));

@@ -1451,15 +1451,19 @@ struct BigSlot {
   unsigned long long key;  // ~0: empty
   unsigned long long cnt;
 };
+constexpr uint32_t kBigProbe = 1024;
 struct BigTab {
   BigSlot* s;
   uint64_t mask;
   unsigned long long* full;  // set when a claim gave up
+  // probes before a claim gives up: kBigProbe on the first, small table; no
+  // limit on the full-size retry (more slots than instances: it cannot fill,
+  // so a long linear-probe cluster of repetitive keys costs time, not the pass)
+  uint32_t max_probe = kBigProbe;
 };
-constexpr uint32_t kBigProbe = 1024;
 
 __device__ __forceinline__ void sk_big_add(const BigTab& g, uint64_t c, uint64_t s, uint32_t add) {
-  for (uint32_t n = 0; n < kBigProbe; ++n) {
+  for (uint32_t n = 0; n < g.max_probe; ++n) {
     const unsigned long long old = atomicCAS(&g.s[s].key, ~0ull, (unsigned long long)c);
     if (old == ~0ull || old == c) {
       atomicAdd(&g.s[s].cnt, (unsigned long long)add);
@@ -1675,7 +1679,7 @@ static int big_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const ui
     APG_TRY(workspace_t(ctx, "sk_gtab", T, &gs));
     k_big_init<<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gs, T);
     APG_CHECK_HIP(hipMemsetAsync(full, 0, 16, ctx->stream));
-    const BigTab g{gs, T - 1, full};
+    const BigTab g{gs, T - 1, full, attempt ? ~0u : (getenv("APG_SK_BIG_PROBE") ? (uint32_t)atoi(getenv("APG_SK_BIG_PROBE")) : kBigProbe)};
     k_sk_big_insert<RB, UP><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, UP ? binst : nullptr);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hf = 0;

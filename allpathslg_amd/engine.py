@@ -123,6 +123,21 @@ class Context:
             i += 1
         return out
 
+    def overlapped_kernels(self) -> Dict[str, int]:
+        """name -> launches that ran on the side / auxiliary stream (beside the
+        main stream's kernels, so their event time is not a standalone time)."""
+        out = {}
+        L = lib()
+        i = 0
+        name = C.create_string_buffer(128)
+        ov = C.c_uint64()
+        while L.apg_timing_get(self._h, i, name, 128, None, None, None) == 0:
+            check(L.apg_timing_overlapped(self._h, i, C.byref(ov)), "apg_timing_overlapped")
+            if ov.value:
+                out[name.value.decode()] = int(ov.value)
+            i += 1
+        return out
+
     def reset_timing(self):
         check(lib().apg_timing_reset(self._h), "apg_timing_reset")
 

@@ -104,6 +104,9 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "current", "pmc", "traffic.json"),
                    help="per-kernel HBM traffic from rocprofv3 --pmc passes (scripts/pmc_traffic.py); the default "
                         "is the latest round checkpoint's (scripts/gpu_checkpoint.sh), which ships to the GPU box")
+    p.add_argument("--detail-json", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                   help="every sub-benchmark (kernels, aligners, placement, c3, repeats, file_to_graph, stats) goes "
+                        "here; the stdout line carries the compact result ('' = no file)")
     return p.parse_args()
 
 
@@ -588,6 +591,133 @@ def align_cpu_baseline(S, T, pairs, band_w: int, n: int) -> dict:
                        f"(gap-free, consensus), first {min(n, 2000)} (banded SW)")}
 
 
+def _kentry(k, v, steps, tj, lj):
+    kms, kl, kb = v
+    pl_ms, pl_b = kms / max(kl, 1), kb / max(kl, 1)
+    ach = pl_b / max(pl_ms * 1e-3, 1e-12) / 1e9
+    e = {"kernel": k, "ms_per_step": kms / max(steps, 1), "launches_per_step": kl / max(steps, 1),
+         "ms_per_launch": pl_ms, "algorithmic_bytes_per_launch": pl_b, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+         "traffic": tj[k]["traffic_bytes_per_launch"] if k in tj else None}
+    if k in tj:
+        e["traffic_over_algorithmic"] = e["traffic"] / max(pl_b, 1)
+    if k in lj and lj[k].get("lds_util") is not None:
+        e["lds"] = {"bound": "lds", "util": lj[k]["lds_util"], "bank_conflict_share": lj[k]["bank_conflict_share"]}
+    return e
+
+
+def roofline_summary(kt, ov, tj, lj, a) -> dict:
+    """The `roofline` object: the dominant kernel = the largest time per step
+    among the kernels that ran alone on the main stream (HIP events on that
+    stream, algorithmic bytes per launch ÷ average launch time), its PMC
+    traffic per launch (profiles/current/pmc, tracked), the next largest
+    main-stream kernels, and the side-stream kernels apart."""
+    main = {k: v for k, v in kt.items() if not ov.get(k)}
+    side = {k: v for k, v in kt.items() if ov.get(k)}
+    if not main:
+        main = kt
+    ranked = sorted(main.items(), key=lambda kv: -kv[1][0])
+    name, v = ranked[0]
+    d = _kentry(name, v, a.steps, tj, lj)
+    roofline = {"bound": "hbm", "kernel": name, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": d["frac"], "traffic": d["traffic"],
+                "algorithmic_bytes_per_launch": d["algorithmic_bytes_per_launch"],
+                "ms_per_launch": d["ms_per_launch"]}
+    if d["traffic"] is not None:
+        roofline["traffic_source"] = os.path.relpath(a.traffic_json, ROOT)
+        roofline["traffic_over_algorithmic"] = d["traffic_over_algorithmic"]
+    if "lds" in d:
+        roofline["lds"] = d["lds"]
+        roofline["lds_source"] = os.path.relpath(a.lds_json, ROOT)
+    roofline["kernels"] = [_kentry(k, kv, a.steps, tj, lj) for k, kv in ranked[:8]]
+    roofline["overlapped"] = [dict(_kentry(k, kv, a.steps, tj, lj), overlapped_launches=ov[k])
+                              for k, kv in sorted(side.items(), key=lambda kv: -kv[1][0])[:4]]
+    return roofline
+
+
+RESULT_LINE_MAX = 8192  # the driver reads a bounded tail of stdout: the result line stays well under it
+
+
+def _r(x, nd=4):
+    """Round floats for the compact line."""
+    if isinstance(x, float):
+        return float(f"{x:.{nd}g}")
+    if isinstance(x, dict):
+        return {k: _r(v, nd) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_r(v, nd) for v in x]
+    return x
+
+
+def compact_result(out: dict, detail_path) -> dict:
+    """The ONE result line: the contract's fields, the dominant kernel's
+    roofline with at most 3 more kernels (name / ms / frac / traffic) and the
+    side-stream kernels apart, the CPU baseline's headline, the end-to-end
+    file -> graph rate beside `value`, one number per sub-benchmark, and every
+    check.  Everything else goes to the detail file (`detail`)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: out[k] for k in keep}
+    cfg = out["config"]
+    line["config"] = {k: cfg[k] for k in ("workload", "reads_per_gpu", "genome_len", "coverage", "K", "K_correct",
+                                          "K_unipath", "hbm_used_gb", "parallelism") if k in cfg}
+    rl = out["roofline"]
+    r = {k: rl[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                            "algorithmic_bytes_per_launch", "ms_per_launch", "traffic_source",
+                            "traffic_over_algorithmic", "lds") if k in rl}
+    r["next"] = [{"kernel": e["kernel"], "ms": e["ms_per_launch"], "ms_per_step": e["ms_per_step"], "frac": e["frac"],
+                  "traffic": e["traffic"]} for e in rl["kernels"][1:4]]
+    r["overlapped"] = [{"kernel": e["kernel"], "ms": e["ms_per_launch"], "frac": e["frac"]}
+                       for e in rl.get("overlapped", [])[:2]]
+    line["roofline"] = r
+    cb = out.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb}
+        line["cpu_baseline"]["host"] = cb.get("host", {}).get("model")
+        line["cpu_baseline"]["runs"] = cb.get("runs")
+        line["cpu_baseline"]["sample"] = ("oracle/ restatement on bounded samples of the bench's reads (spectrum, "
+                                          "PreCorrect, FillFragments, K=96 unipaths), 1/sum(1/stage rate); "
+                                          "stage rates and the 1-thread run in `detail`")
+        if cb.get("single_core"):
+            line["cpu_baseline"]["single_core_value"] = cb["single_core"]["value"]
+    else:
+        line["cpu_baseline"] = None
+    f2g = out.get("file_to_graph")
+    line["end_to_end"] = None if not f2g else {
+        "reads_per_s": f2g["reads_per_s"], "ms": f2g["ms"], "files_to_hbm_ms": f2g["files_to_hbm_ms"],
+        "note": "cold .fastb/.qualb on /dev/shm -> HBM -> graph in host memory (PCIe-inclusive; never `value`)"}
+    sub = {}
+    if out.get("c3"):
+        sub["c3"] = {"ms_per_step": out["c3"]["ms_per_step"], "reads_per_s": out["c3"]["reads_per_s"]}
+    if out.get("repeats"):
+        sub["repeats"] = {"ms_per_step": out["repeats"]["ms_per_step"],
+                          "over_main_step": out["repeats"]["ms_per_step"] / out["ms_per_step"]}
+    if out.get("aligners"):
+        sw = out["aligners"]["banded_sw"]
+        sub["banded_sw"] = {"ms": sw["ms"], "gcups": sw["gcups"], "valu_frac": sw["roofline"]["frac"]}
+    if out.get("placement"):
+        sub["unipath_locs"] = {"ms": out["placement"]["unipath_locs"]["ms"]}
+    line["lines"] = sub
+    checks = dict(out.get("checks") or {})
+    for nm in ("c3", "repeats", "aligners", "placement"):
+        if out.get(nm) and out[nm].get("checks"):
+            checks[nm] = all(bool(v) for v in out[nm]["checks"].values())
+    line["checks"] = checks
+    line["detail"] = detail_path
+    exact = {k: line[k] for k in ("value", "ms_per_step")}  # the headline keeps full precision
+    line = _r(line, 5)
+    line.update(exact)
+    return line
+
+
+def result_line(out: dict, detail_path) -> str:
+    """Serialise the compact line; fail loudly rather than print a line the
+    driver cannot read."""
+    s = json.dumps(compact_result(out, detail_path), separators=(",", ":"))
+    if len(s) >= RESULT_LINE_MAX:
+        raise RuntimeError(f"bench result line is {len(s)} bytes (limit {RESULT_LINE_MAX})")
+    return s
+
+
 def main():
     a = parse()
     # Exactly one JSON line on stdout: libraries (RCCL prints a version banner
@@ -796,55 +926,23 @@ def main():
             if coverage <= 100:  # solid recurrent errors shatter the graph at high coverage
                 checks["unipaths_long"] = ust["max_len"] >= 10_000
 
-    # Roofline of the dominant kernel, from HIP events on libapg's stream.
+    # Roofline of the dominant kernel, from HIP events on libapg's streams.
+    # Kernels that ran on the side / auxiliary stream are listed apart: their
+    # event time is stretched by the main stream's kernels beside them, so it
+    # is not a standalone kernel time and never picks the dominant kernel.
     kt = ctx.kernel_times()
+    ov = ctx.overlapped_kernels()
     if ctx_s is not None:  # the concurrent spectrum context's kernels
         for k, v in ctx_s.kernel_times().items():
             o = kt.get(k, (0.0, 0, 0))
             kt[k] = (o[0] + v[0], o[1] + v[1], o[2] + v[2])
-    dom = max(kt.items(), key=lambda kv: kv[1][0])
-    name, (ms, launches, nbytes) = dom
-    per_launch_ms = ms / max(launches, 1)
-    per_launch_bytes = nbytes / max(launches, 1)
-    achieved = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
-    kernels = {k: {"ms_per_launch": v[0] / max(v[1], 1), "launches": v[1],
+            ov[k] = ov.get(k, 0) + v[1]
+    tj = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
+    lj = json.load(open(a.lds_json)) if os.path.exists(a.lds_json) else {}
+    roofline = roofline_summary(kt, ov, tj, lj, a)
+    kernels = {k: {"ms_per_launch": v[0] / max(v[1], 1), "launches": v[1], "overlapped_launches": ov.get(k, 0),
                    "GBps": (v[2] / max(v[1], 1)) / max(v[0] / max(v[1], 1) * 1e-3, 1e-12) / 1e9}
                for k, v in kt.items()}
-
-    roofline = {
-        "bound": "hbm",
-        "kernel": name,
-        "achieved": achieved,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS,
-        "traffic": None,
-        "algorithmic_bytes_per_launch": per_launch_bytes,
-        "ms_per_launch": per_launch_ms,
-    }
-    tj = json.load(open(a.traffic_json)) if os.path.exists(a.traffic_json) else {}
-    if name in tj:  # PMC FETCH_SIZE/WRITE_SIZE passes of this kernel (separate rocprofv3 runs)
-        t = tj[name]["traffic_bytes_per_launch"]
-        roofline["traffic"] = t
-        roofline["traffic_source"] = os.path.relpath(a.traffic_json, ROOT)
-        roofline["traffic_over_algorithmic"] = t / max(per_launch_bytes, 1)
-    # the same figures for the step's largest kernels (time per step), the
-    # dominant one first: where the step's time goes against the HBM roof
-    lj = json.load(open(a.lds_json)) if os.path.exists(a.lds_json) else {}
-    top = []
-    for k, (kms, kl, kb) in sorted(kt.items(), key=lambda kv: -kv[1][0])[:8]:
-        pl_ms, pl_b = kms / max(kl, 1), kb / max(kl, 1)
-        ach = pl_b / max(pl_ms * 1e-3, 1e-12) / 1e9
-        e = {"kernel": k, "ms_per_step": kms / max(a.steps, 1), "launches_per_step": kl / max(a.steps, 1),
-             "algorithmic_bytes_per_launch": pl_b, "achieved": ach, "frac": ach / HBM_PEAK_GBS,
-             "traffic": tj[k]["traffic_bytes_per_launch"] if k in tj else None}
-        if k in tj:
-            e["traffic_over_algorithmic"] = e["traffic"] / max(pl_b, 1)
-        if k in lj and lj[k].get("lds_util") is not None:
-            e["lds"] = {"bound": "lds", "util": lj[k]["lds_util"], "bank_conflict_share": lj[k]["bank_conflict_share"],
-                        "source": os.path.relpath(a.lds_json, ROOT)}
-        top.append(e)
-    roofline["kernels"] = top
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.spectrum_only and frags is None:
@@ -946,7 +1044,13 @@ def main():
             "unipath_stats": ust,
             "checks": checks,
         }
-        print(json.dumps(out), file=result_out, flush=True)
+        detail = None
+        if a.detail_json:
+            os.makedirs(os.path.dirname(os.path.abspath(a.detail_json)), exist_ok=True)
+            with open(a.detail_json, "w") as f:
+                json.dump(out, f)
+            detail = os.path.relpath(os.path.abspath(a.detail_json), ROOT)
+        print(result_line(out, detail), file=result_out, flush=True)
     dreads.free()
     dsrc.free()
     if dfrags is not None:

@@ -67,6 +67,10 @@ int apg_trim(apg_ctx* ctx);
  * once + outputs written once) summed over the launches. */
 int apg_timing_get(apg_ctx* ctx, int idx, char* name, size_t name_len,
                    double* total_ms, uint64_t* launches, uint64_t* bytes);
+/* Launches of kernel idx that ran on the context's side or auxiliary stream,
+ * i.e. beside the main stream's kernels: their HIP-event time is a stretched,
+ * shared-CU time, not a standalone kernel time. */
+int apg_timing_overlapped(apg_ctx* ctx, int idx, uint64_t* overlapped);
 int apg_timing_reset(apg_ctx* ctx);
 
 /* ------------------------------------------------------------------------- */
@@ -172,6 +176,17 @@ void apg_free(void* p);
  * stats: the whole read set's counts. */
 int apg_kmer_count_dev(apg_ctx* ctx, const apg_dreads* reads, int K, uint64_t hash_lo, uint64_t hash_hi,
                        uint64_t** keys, uint32_t** counts, uint64_t* n_out, apg_kstats* stats);
+
+/* One hash-partition level of the counting pipelines (partition.hip: the
+ * LDS-staged count / scan / scatter of NaifKmerizer's block split, [R:M]
+ * src/kmers/naif_kmer/): the n device u64 records of d_in grouped by bits
+ * [shift, shift + bits) into 2^bits child runs of d_out (order inside a child
+ * unspecified); d_child (2^bits + 1 device u64) receives the runs' starts,
+ * d_child[2^bits] = n.  0 <= bits <= 8 and shift + bits <= 64: APG_E_ARG
+ * otherwise, with nothing launched (the kernels keep one LDS counter per
+ * child).  Synchronous. */
+int apg_partition_u64(apg_ctx* ctx, const uint64_t* d_in, uint64_t n, int shift, int bits, uint64_t* d_out,
+                      uint64_t* d_child);
 
 /* ------------------------------------------------------------------------- */
 /* Sharded counting (multi-GPU, one process per GPU).  SURVEY §8e.            */

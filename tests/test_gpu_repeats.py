@@ -48,3 +48,23 @@ def test_unipaths_on_repeats(gpu_ctx, rep_reads):
     assert_graph_equal(got, oracle.unipaths(frags, 96))
     # repeats collapse: fewer distinct 96-mers than genome positions
     assert st["n_nodes"] < 0.99 * (G - 95)
+
+
+@pytest.mark.parametrize("probe", ["1", "4"])
+def test_overflow_table_retry_unbounded(rep_reads, monkeypatch, probe):
+    """the overflowed buckets' global table gives up after
+    APG_SK_BIG_PROBE probes on its first, small attempt; the full-size retry
+    probes without a limit, so a crowded first attempt on tandem-repeat keys
+    still ends in the oracle's spectrum, solid set and corrections."""
+    monkeypatch.setenv("APG_SK_BIG_PROBE", probe)
+    _, reads = rep_reads
+    with Context(device=0, verbose=True) as ctx:
+        for K in (24, 25):
+            hist, st = ctx.kmer_spectrum(reads, K)
+            assert np.array_equal(hist, oracle.kmer_spectrum(reads, K)), K
+            assert st["n_overflow"] > 0  # the global path ran
+        got, pst = ctx.precorrect(reads, K=24)
+    exp, est = oracle.precorrect(reads, K=24)
+    assert np.array_equal(got.packed[: int(got.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
+    assert np.array_equal(got.quals, exp.quals)
+    assert pst["n_solid"] == est["n_solid"]
