@@ -75,6 +75,20 @@ class apg_pc_params(C.Structure):
     ]
 
 
+class apg_mem_stats(C.Structure):
+    _fields_ = [
+        ("workspace_bytes", C.c_uint64),
+        ("workspace_peak", C.c_uint64),
+        ("releases", C.c_uint64),
+        ("device_used", C.c_uint64),
+        ("device_total", C.c_uint64),
+        ("reserved", C.c_uint64 * 3),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != "reserved"}
+
+
 class apg_pc_stats(C.Structure):
     _fields_ = [
         ("n_suspect", C.c_uint64),
@@ -82,7 +96,8 @@ class apg_pc_stats(C.Structure):
         ("n_ambiguous", C.c_uint64),
         ("n_uncorrectable", C.c_uint64),
         ("n_solid", C.c_uint64),
-        ("reserved", C.c_uint64 * 3),
+        ("record_form", C.c_uint64),
+        ("reserved", C.c_uint64 * 2),
     ]
 
     def as_dict(self) -> dict:
@@ -289,6 +304,7 @@ SIGNATURES = {
     "apg_trim": (C.c_int, [_P]),
     "apg_timing_get": (C.c_int, [_P, C.c_int, C.c_char_p, C.c_size_t, C.POINTER(C.c_double), _u64p, _u64p]),
     "apg_timing_overlapped": (C.c_int, [_P, C.c_int, _u64p]),
+    "apg_mem_stats_get": (C.c_int, [_P, C.c_int, C.POINTER(apg_mem_stats)]),
     "apg_timing_reset": (C.c_int, [_P]),
     "apg_reads_upload": (C.c_int, [_P, C.POINTER(apg_reads), C.POINTER(_P)]),
     "apg_reads_free": (None, [_P]),

@@ -1,6 +1,7 @@
 // apg_core.cpp — context lifecycle, errors, workspaces, kernel timing, uploads.
 #include "apg_core.hpp"
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -18,6 +19,7 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
   if (b.bytes < bytes) {
     if (b.p && ctx->side_finish) APG_TRY(side_join(ctx));  // the side work may read it
     if (b.p) APG_CHECK_HIP(hipFree(b.p));
+    ctx->ws_bytes -= b.bytes;
     b.p = nullptr;
     b.bytes = 0;
     // Grow by 1/8 headroom so steadily growing calls do not realloc each time.
@@ -35,6 +37,8 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
       return APG_E_HIP;
     }
     b.bytes = want;
+    ctx->ws_bytes += want;
+    ctx->ws_peak = std::max(ctx->ws_peak, ctx->ws_bytes);
     if (ctx->verbose) {
       size_t tot = 0;
       for (auto& kv : ctx->ws) tot += kv.second.bytes;
@@ -86,6 +90,7 @@ static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uin
     auto it = ctx->ws.find(names[i]);
     if (it == ctx->ws.end() || !it->second.p) continue;
     *freed += it->second.bytes;
+    ctx->ws_bytes -= it->second.bytes;
     APG_CHECK_HIP(hipFree(it->second.p));
     ctx->ws.erase(it);
   }
@@ -358,6 +363,7 @@ int apg_trim(apg_ctx* ctx) {
   for (auto& kv : ctx->ws)
     if (kv.second.p) (void)hipFree(kv.second.p);
   ctx->ws.clear();
+  ctx->ws_bytes = 0;
   ctx->pc_list_valid = false;
   ctx->pc_ext_valid = false;
   ctx->clean_valid = false;
@@ -401,6 +407,21 @@ int apg_timing_get(apg_ctx* ctx, int idx, char* name, size_t name_len, double* t
   if (total_ms) *total_ms = s.ms;
   if (launches) *launches = s.launches;
   if (bytes) *bytes = s.bytes;
+  return APG_OK;
+}
+
+int apg_mem_stats_get(apg_ctx* ctx, int reset_peak, apg_mem_stats* out) {
+  APG_REQUIRE(ctx && out, "apg_mem_stats_get: NULL argument");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  std::memset(out, 0, sizeof *out);
+  out->workspace_bytes = ctx->ws_bytes;
+  out->workspace_peak = ctx->ws_peak;
+  out->releases = ctx->mem_releases;
+  size_t fr = 0, tot = 0;
+  APG_CHECK_HIP(hipMemGetInfo(&fr, &tot));
+  out->device_used = tot - fr;
+  out->device_total = tot;
+  if (reset_peak) ctx->ws_peak = ctx->ws_bytes;
   return APG_OK;
 }
 

@@ -240,12 +240,17 @@ struct apg_ctx {
   bool pc_ext_valid = false;
   uint64_t clean_gen = 0;
   bool clean_valid = false;
+  // record form of the last solid-set count (apg_pc_stats.record_form)
+  uint64_t sk_record_form = 0;
   // Capacity for the next single-pass candidate write (last count + 25 %).
   uint64_t pc_cand_hint = 0;
   uint64_t pc_cand_hint_lk = 0;  // the same for the passes without a weak bitmap (every low-quality position)
   // ws_make_room calls that released buffers (memory pressure; logged with
   // cfg.verbose)
   uint64_t mem_releases = 0;
+  // bytes held by the workspaces now, and the most held at once since the
+  // context was made or apg_mem_stats_get reset it
+  uint64_t ws_bytes = 0, ws_peak = 0;
   // Host <-> device staging of the module boundary (apg_reads_load_dev,
   // graph egress): per worker two pinned chunks, a stream and two events,
   // allocated once per context (pinning 256 MB per call cost more than the

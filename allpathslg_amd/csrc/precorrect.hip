@@ -1289,6 +1289,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
   st->n_ambiguous += h[2];
   st->n_uncorrectable += h[3];
   st->n_solid = n_solid;
+  st->record_form = ctx->sk_record_form;
   ctx->pc_list = list;  // APG_FILL_LAST_SOLID (FillFragments after correction)
   ctx->pc_n = n_solid;
   ctx->pc_K = p.K;

@@ -255,6 +255,7 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
     tot.n_ambiguous += st.n_ambiguous;
     tot.n_uncorrectable += st.n_uncorrectable;
     tot.n_solid = n_solid;
+    tot.record_form = st.record_form;
     if (up_pending) {  // the first cycle's K+1 spectrum: side pass complete, summed over ranks
       up_pending = false;
       APG_TRY(side_join(ctx));

@@ -2430,6 +2430,7 @@ int sk_solid_weak(apg_ctx* ctx, const apg_dreads* dr, int K, uint32_t min_solid,
     APG_TRY(sk_scatter_t<SK24>(ctx, dr, K, 1, buf));
   vlog(ctx, "solid count: %s records (%llu bases)", !pack ? "24-byte" : wide ? "packed wide (34-bit position)" : "packed",
        (unsigned long long)dr->n_bases);
+  ctx->sk_record_form = !pack ? 0 : wide ? 2 : 1;
   return sk_stage_count_t<SK24>(ctx, buf, buf, rc, nk, K, 1, true, min_solid, nullptr, 0, weak, res, nullptr, nullptr,
                                 up ? K + 1 : 0, up_hist, up_hist_len, up_res,
                                 pack ? reinterpret_cast<const SKP*>(buf) : nullptr, false, wide);
@@ -2460,6 +2461,7 @@ int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64
   // at wpos[receive index], no per-record masks
   if (weak) wrec = nullptr;
   if (n && wrec) APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
+  ctx->sk_record_form = 3;
   // the first partition level reads the SK16 records and writes them as SK24
   // with their receive index (no separate widening pass)
   return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, weak, res,

@@ -138,6 +138,14 @@ class Context:
             i += 1
         return out
 
+    def mem_stats(self, reset_peak: bool = False) -> dict:
+        """Device memory of the context (include/apg.h apg_mem_stats_get)."""
+        from ._lib import apg_mem_stats
+
+        m = apg_mem_stats()
+        check(lib().apg_mem_stats_get(self._h, 1 if reset_peak else 0, C.byref(m)), "apg_mem_stats_get")
+        return m.as_dict()
+
     def reset_timing(self):
         check(lib().apg_timing_reset(self._h), "apg_timing_reset")
 

@@ -67,6 +67,20 @@ int apg_trim(apg_ctx* ctx);
  * once + outputs written once) summed over the launches. */
 int apg_timing_get(apg_ctx* ctx, int idx, char* name, size_t name_len,
                    double* total_ms, uint64_t* launches, uint64_t* bytes);
+/* Device memory of the context (DESIGN.md §7 memory model): the workspaces it
+ * holds now, the most it held at once since it was made or since the last
+ * call with reset_peak = 1, how often a stage released dead buffers under
+ * memory pressure, and the device's used / total bytes (all processes). */
+typedef struct apg_mem_stats {
+  uint64_t workspace_bytes;
+  uint64_t workspace_peak;
+  uint64_t releases;
+  uint64_t device_used;
+  uint64_t device_total;
+  uint64_t reserved[3];
+} apg_mem_stats;
+int apg_mem_stats_get(apg_ctx* ctx, int reset_peak, apg_mem_stats* out);
+
 /* Launches of kernel idx that ran on the context's side or auxiliary stream,
  * i.e. beside the main stream's kernels: their HIP-event time is a stretched,
  * shared-CU time, not a standalone kernel time. */
@@ -286,7 +300,12 @@ typedef struct apg_pc_stats {
   uint64_t n_ambiguous;     /* > 1 alternative made every covering K-mer solid */
   uint64_t n_uncorrectable; /* no alternative did */
   uint64_t n_solid;         /* solid K-mers of the last cycle */
-  uint64_t reserved[3];
+  uint64_t record_form;     /* records of the context's last solid-set count:
+                               0 = 24-byte SK24, 1 = packed 16-byte SKP (32-bit read-set
+                               positions), 2 = packed wide SKP (34-bit positions: read sets of
+                               2^32 .. 2^34 bases), 3 = received records by receive index
+                               (the multi-GPU owner count) */
+  uint64_t reserved[2];
 } apg_pc_stats;
 
 void apg_pc_defaults(apg_pc_params* p);

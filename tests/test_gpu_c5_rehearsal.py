@@ -1,0 +1,105 @@
+"""Memory rehearsal of one BASELINE.json configs[4] (C5, human 30x on
+8 x MI355X) rank on one GPU (DESIGN.md §7 memory model).
+
+A C5 rank holds 112.5 M reads (1/8 of 900 M) of a 3.1-Gb genome.  Here one
+process runs the driver's per-rank path at world size 1 over RCCL — the owner
+count then receives exactly the rank's own records, the size a C5 owner
+receives — through the counting, correction, FillFragments and sharded
+unipath stages, logging the context's device memory after each stage
+(apg_mem_stats_get).  min_solid = 2 so that the replicated solid set is of a
+C5 rank's size (~2.4 G K-mers at this rank's 3.6x coverage; ~2.7 G at C5's
+29x with min_solid 3) and the (K-1)-mer extension table takes C5's 2^34 slots
+(137 GB): the correction stage cannot sit beside the counting buffers on a
+288 GB device, so the release path must run (DESIGN.md §7 release point 1).
+
+Asserted: the stages complete, the release ran, no stage's workspaces
+exceeded DESIGN.md §7's per-stage peaks (count 214 GB, correction 196 GB,
+FillFragments 200 GB, unipaths 210 GB — workspace bytes + the reads), and the
+spectrum's size-independent properties hold."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1100)]
+
+GENOME = 3_100_000_000
+PAIRS = 56_250_000  # 112.5 M reads
+
+SCRIPT = r"""
+import json, sys, time
+import numpy as np
+sys.path.insert(0, {root!r})
+import torch
+from allpathslg_amd import Context, synth_genome, synth_reads
+from allpathslg_amd.distributed import Comm, sharded_fill, sharded_spectrum_precorrect, sharded_unipaths, unique_id
+t0 = time.time()
+def log(*a):
+    print("[c5]", f"{{time.time() - t0:7.1f}}s", *a, file=sys.stderr, flush=True)
+g = synth_genome({genome}, 0xC5)
+log("genome")
+reads = synth_reads(g, {pairs}, seed=0xC5 + 1, threads=16)
+del g
+log("reads", reads.n_reads, reads.n_bases)
+stages = {{}}
+with Context(device=0, verbose=True) as ctx:
+    d = ctx.upload(reads)
+    nb = reads.n_bases
+    n_reads = reads.n_reads
+    del reads
+    stages["reads"] = ctx.mem_stats(reset_peak=True)
+    comm = Comm.rccl(ctx, unique_id(), 0, 1)
+    hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24, min_solid=2)
+    stages["count+correct"] = ctx.mem_stats(reset_peak=True)
+    log("count + correction", pst)
+    filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
+    stages["fill"] = ctx.mem_stats(reset_peak=True)
+    log("fill", fst)
+    _, ust = sharded_unipaths(ctx, comm, filled, 96)
+    stages["unipaths"] = ctx.mem_stats(reset_peak=True)
+    log("unipaths", ust)
+    comm.close()
+    m = np.arange(len(hist), dtype=np.uint64)
+    out = {{"stages": stages, "n_reads": n_reads, "n_bases": nb, "st": st, "pst": pst, "fst": fst, "ust": ust,
+           "sum_mh": int((hist[:-1] * m[:-1]).sum()), "last_bin": int(hist[-1]), "hsum": int(hist.sum())}}
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_c5_rank_memory_rehearsal():
+    r = subprocess.run([sys.executable, "-u", "-c", SCRIPT.format(root=ROOT, genome=GENOME, pairs=PAIRS)],
+                       capture_output=True, text=True, timeout=1050)
+    tail = r.stderr[-4000:]
+    assert r.returncode == 0, tail
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1][7:])
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "c5_rehearsal.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    with open(os.path.join(ROOT, "gpurun_out", "c5_rehearsal.log"), "w") as f:
+        f.write(r.stderr)
+    S = out["stages"]
+    # the read set (2-bit bases, quals, offsets) is held outside the workspaces
+    reads_gb = (out["n_bases"] / 4 + out["n_bases"] + 16 * out["n_reads"]) / 1e9
+    print({k: (round(v["workspace_peak"] / 1e9, 1), round(v["device_used"] / 1e9, 1), v["releases"])
+           for k, v in S.items()}, f"reads {reads_gb:.1f} GB")
+    assert out["n_reads"] == 2 * PAIRS
+    # the release path ran (the correction tables could not sit beside the count buffers)
+    assert S["count+correct"]["releases"] >= 1
+    assert "dead stage buffers released" in r.stderr
+    # DESIGN.md §7 stage peaks (GB, the reads included)
+    assert S["count+correct"]["workspace_peak"] / 1e9 + reads_gb <= 214
+    assert S["fill"]["workspace_peak"] / 1e9 + reads_gb <= 200
+    assert S["unipaths"]["workspace_peak"] / 1e9 + reads_gb <= 210
+    assert reads_gb < 32
+    # spectrum properties of the 8.55 G K=25 instances
+    st = out["st"]
+    assert st["n_kmers"] == out["n_reads"] * 76
+    assert out["hsum"] == st["n_distinct"]
+    if out["last_bin"] == 0:
+        assert out["sum_mh"] == st["n_kmers"]
+    # a C5-size replicated solid set
+    assert out["pst"]["n_solid"] > 2_000_000_000
+    assert out["pst"]["record_form"] == 3
