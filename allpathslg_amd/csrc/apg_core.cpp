@@ -85,7 +85,13 @@ uint64_t device_free_bytes(apg_ctx* ctx) {
 
 static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uint64_t* freed) {
   APG_TRY(side_join(ctx));
+  // every stream of the context: a release may be asked for from the
+  // auxiliary stream (StreamSwap) while the main stream's kernels read the
+  // buffers (hipFree does not wait for them)
   APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->home && ctx->home != ctx->stream) APG_CHECK_HIP(hipStreamSynchronize(ctx->home));
+  if (ctx->aux && ctx->aux != ctx->stream) APG_CHECK_HIP(hipStreamSynchronize(ctx->aux));
+  if (ctx->side) APG_CHECK_HIP(hipStreamSynchronize(ctx->side));
   for (size_t i = 0; i < n; ++i) {
     auto it = ctx->ws.find(names[i]);
     if (it == ctx->ws.end() || !it->second.p) continue;
@@ -102,7 +108,11 @@ int ws_make_room(apg_ctx* ctx, uint64_t need, unsigned what) {
   if (device_free_bytes(ctx) >= need + margin) return APG_OK;
   uint64_t freed = 0;
   APG_TRY(ws_release_list(ctx, kStageWs, sizeof kStageWs / sizeof kStageWs[0], &freed));
-  if (what & kRoomDescriptors) APG_TRY(ws_release_list(ctx, kDescWs, sizeof kDescWs / sizeof kDescWs[0], &freed));
+  if (what & kRoomDescriptors) {
+    APG_TRY(ws_release_list(ctx, kDescWs, sizeof kDescWs / sizeof kDescWs[0], &freed));
+    ctx->skstate.desc = false;  // a scatter of the last count must walk again
+    ctx->urstate.desc = false;
+  }
   if ((what & kRoomCorrection) && device_free_bytes(ctx) < need + margin) {
     APG_TRY(ws_release_list(ctx, kCorrectWs, sizeof kCorrectWs / sizeof kCorrectWs[0], &freed));
     ctx->pc_ext_valid = false;  // FillFragments / ErrorCorrectJump rebuild their tables

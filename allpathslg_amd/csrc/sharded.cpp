@@ -235,8 +235,13 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
                                [&](void* send) { return apg_shard_scatter(ctx, reads, K, P, send); }, &x));
       APG_TRY(apg_shard_solid(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, &n_local));
     }
+    // at world size 1 the gathered set IS this rank's list (gather_all
+    // returns it as is), so it goes straight into "x_solid": the pass's list
+    // must survive the release of the counting buffers under memory pressure
+    // (ws_make_room frees "x_local" as a stage buffer before the extension
+    // table is built — the C5-rank rehearsal faulted on exactly that)
     void* local = nullptr;
-    APG_TRY(workspace(ctx, "x_local", std::max<uint64_t>(n_local * 8, 64), &local));
+    APG_TRY(workspace(ctx, P == 1 ? "x_solid" : "x_local", std::max<uint64_t>(n_local * 8, 64), &local));
     APG_TRY(apg_solid_export(ctx, local));
     // the replicated solid set; it stays in "x_solid" as the pass's list
     // (APG_FILL_LAST_SOLID) until the next sharded pass

@@ -25,14 +25,25 @@ g = synth_genome(8_000_000, 0x3E3)
 reads = synth_reads(g, 1_500_000, seed=0x3E4)
 with Context(device=0, verbose=True) as ctx:
     d = ctx.upload(reads)
-    if {fused!r}:  # the bench's entry point: K+1 pass on the side stream (joined before any release)
-        hist, st, pst = ctx.spectrum_precorrect(d, K_spec=25, K=24)
+    if {fused!r} == "sharded":  # the driver's per-rank path at world size 1 over RCCL
+        from allpathslg_amd.distributed import Comm, sharded_fill, sharded_spectrum_precorrect, sharded_unipaths, unique_id
+        comm = Comm.rccl(ctx, unique_id(), 0, 1)
+        hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24)
+        filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
+        graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True)
+        ust = {{k: v for k, v in ust.items() if k != "n_shards"}}
+        comm.close()
     else:
+      if {fused!r}:  # the bench's entry point: K+1 pass on the side stream (joined before any release)
+        hist, st, pst = ctx.spectrum_precorrect(d, K_spec=25, K=24)
+      else:
         hist, st = ctx.kmer_spectrum(d, 25)
         _, pst = ctx.precorrect(d, K=24)
-    filled, _, fst = ctx.fill_fragments(d, K=24, last_solid=True)
-    graph, ust = ctx.unipaths(filled, 96)
+      filled, _, fst = ctx.fill_fragments(d, K=24, last_solid=True)
+      graph, ust = ctx.unipaths(filled, 96)
     fixed = ctx.download(d)
+    fst = {{k: fst[k] for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases")}}
+    ust = {{k: ust[k] for k in ("n_nodes", "n_unipaths", "n_vertices", "n_instances", "max_len")}}
     out = {{"hist": hist.tolist()[:200], "hsum": int(hist.astype(np.uint64).sum()), "n_kmers": st["n_kmers"],
            "pst": {{k: pst[k] for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable")}}, "fst": fst, "ust": ust,
            "fixed": int(np.frombuffer(fixed.packed.tobytes(), np.uint64).sum() % (1 << 61)),
@@ -54,11 +65,14 @@ def run(limit, fused=False):
     return line, r.stderr
 
 
-@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("fused", [False, True, "sharded"])
 def test_release_under_memory_pressure_keeps_results(fused):
     """fused: apg_spectrum_precorrect_dev (the bench's entry point), whose
     K+1 pass on the side stream reads the record buffers the release frees —
-    the side stream must be joined first.  Both forms give the same results."""
+    the side stream must be joined first.  "sharded": the driver's per-rank
+    path at world size 1 over RCCL, whose replicated solid list is the rank's
+    own (the C5-rank rehearsal faulted when the release freed it under the
+    extension-table build).  Every form gives the same results."""
     free_run, log0 = run(0, fused)
     assert "dead stage buffers released" not in log0
     # the workspaces this chain reaches without pressure (verbose log)
