@@ -14,6 +14,30 @@ static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
 
+static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uint64_t* freed,
+                           const char* keep = nullptr);
+static const char* const kCorrectWs[] = {"pc_ext", "fill_ext", "ecj_ext", "fill_solid", "x_solid", "pc_solid"};
+
+// An allocation that fails while the correction stage's tables are dead
+// (ctx->ws_dead, set by the unipath stage): they are released and the
+// allocation retried once.  ws_make_room's estimate before the unipath stage
+// counts its records, not its node tables and graph arrays, which at a
+// C5-rank's 0.4 G nodes need ~180 GB (the rehearsal ran out of memory there
+// holding 112 GB of dead correction tables).
+static int release_dead_for(apg_ctx* ctx, const char* name) {
+  if (!(ctx->ws_dead & kRoomCorrection)) return 0;
+  uint64_t freed = 0;
+  if (ws_release_list(ctx, kCorrectWs, sizeof kCorrectWs / sizeof kCorrectWs[0], &freed, name) != APG_OK) return 0;
+  ctx->ws_dead &= ~kRoomCorrection;
+  ctx->pc_ext_valid = false;
+  ctx->pc_list_valid = false;
+  ctx->solid_valid = false;
+  ++ctx->mem_releases;
+  vlog(ctx, "memory: %.2f GB of dead correction tables released after a failed allocation of '%s'", freed / 1e9,
+       name);
+  return freed > 0;
+}
+
 int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
   auto& b = ctx->ws[name];
   if (b.bytes < bytes) {
@@ -29,6 +53,10 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
       (void)hipGetLastError();
       want = bytes;
       e = hipMalloc(&b.p, want);
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      if (release_dead_for(ctx, name)) e = hipMalloc(&b.p, want);
     }
     if (e != hipSuccess) {
       b.p = nullptr;
@@ -63,8 +91,6 @@ static const char* const kStageWs[] = {"big0",    "big1",    "big2",    "x_send"
                                        "sk_solid_sparse", "sk_dcount", "ext_e0", "ext_e1"};
 // record descriptors of a count pass: live from the count to its scatter
 static const char* const kDescWs[] = {"sk_desc", "usk_desc"};
-static const char* const kCorrectWs[] = {"pc_ext", "fill_ext", "ecj_ext", "fill_solid", "x_solid", "pc_solid"};
-
 // APG_DEVICE_MEM_LIMIT=<bytes>: act as if the device held only that much for
 // this context's workspaces (tests of the release path on a 288 GB device).
 uint64_t device_free_bytes(apg_ctx* ctx) {
@@ -83,7 +109,7 @@ uint64_t device_free_bytes(apg_ctx* ctx) {
   return fr;
 }
 
-static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uint64_t* freed) {
+static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uint64_t* freed, const char* keep) {
   APG_TRY(side_join(ctx));
   // every stream of the context: a release may be asked for from the
   // auxiliary stream (StreamSwap) while the main stream's kernels read the
@@ -93,6 +119,7 @@ static int ws_release_list(apg_ctx* ctx, const char* const* names, size_t n, uin
   if (ctx->aux && ctx->aux != ctx->stream) APG_CHECK_HIP(hipStreamSynchronize(ctx->aux));
   if (ctx->side) APG_CHECK_HIP(hipStreamSynchronize(ctx->side));
   for (size_t i = 0; i < n; ++i) {
+    if (keep && !std::strcmp(keep, names[i])) continue;  // the caller holds a reference to it
     auto it = ctx->ws.find(names[i]);
     if (it == ctx->ws.end() || !it->second.p) continue;
     *freed += it->second.bytes;

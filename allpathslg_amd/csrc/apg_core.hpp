@@ -251,6 +251,10 @@ struct apg_ctx {
   // bytes held by the workspaces now, and the most held at once since the
   // context was made or apg_mem_stats_get reset it
   uint64_t ws_bytes = 0, ws_peak = 0;
+  // workspace classes the running stage no longer needs (kRoomCorrection: the
+  // unipath stage runs after the correction stage's last reader): a
+  // workspace allocation that fails releases them and retries (apg_core.cpp)
+  unsigned ws_dead = 0;
   // Host <-> device staging of the module boundary (apg_reads_load_dev,
   // graph egress): per worker two pinned chunks, a stream and two events,
   // allocated once per context (pinning 256 MB per call cost more than the

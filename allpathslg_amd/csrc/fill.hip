@@ -823,6 +823,7 @@ static int filled_alloc(apg_ctx* ctx, apg_dreads** io, uint64_t n, uint64_t nbas
 static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& p, const uint64_t* d_solid,
                      uint64_t n_solid, apg_dreads** filled, uint8_t* d_status, apg_fill_stats* st) {
   APG_REQUIRE(dr->n_reads % 2 == 0, "apg_fill_fragments: pairs must be an even number of reads (2i, 2i+1)");
+  ctx->ws_dead &= ~kRoomCorrection;  // the correction tables are read again
   const uint64_t np = dr->n_reads / 2;
   std::memset(st, 0, sizeof *st);
   st->n_pairs = np;

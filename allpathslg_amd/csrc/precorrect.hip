@@ -1001,6 +1001,7 @@ __global__ void __launch_bounds__(256) k_pc_apply(const uint64_t* __restrict__ b
 static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const uint64_t* list, uint64_t n_solid,
                         apg_pc_stats* st, const unsigned long long* weak = nullptr, bool self_count = false) {
   ctx->clean_valid = false;
+  ctx->ws_dead &= ~kRoomCorrection;  // the correction tables are live again
   // the previous pass's extension table is this very list's (the jump reads'
   // pass of ErrorCorrectJump against the fragments' reused solid set)
   const bool ext_reuse = ctx->pc_ext_valid && ctx->pc_list_valid && ctx->pc_list == list && ctx->pc_n == n_solid &&
@@ -1491,6 +1492,7 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   APG_REQUIRE(e.min_solid >= 1, "apg_error_correct_jump: min_solid must be >= 1");
   APG_REQUIRE(jr->n_reads == 0 || jr->d_quals, "apg_error_correct_jump: jump reads have no qualities");
   APG_REQUIRE(jr->n_reads == 0 || d_keep, "apg_error_correct_jump: keep_len is NULL");
+  ctx->ws_dead &= ~kRoomCorrection;  // the fragments' solid set and table may be reused
   apg_pc_params p;
   std::memset(&p, 0, sizeof p);
   p.K = e.K;
@@ -1804,6 +1806,7 @@ int apg_solid_upload(apg_ctx* ctx, int K, const uint64_t* hashes, uint64_t n) {
   ctx->pc_ext_valid = false;
   ctx->clean_valid = false;
   ctx->pc_self = false;  // an uploaded list is no read set's own count (ecj_run's reuse test)
+  ctx->ws_dead &= ~kRoomCorrection;
   uint64_t* list = nullptr;
   APG_TRY(workspace_t(ctx, "x_solid", std::max<uint64_t>(n, 1), &list));
   if (n) APG_CHECK_HIP(hipMemcpyAsync(list, hashes, n * 8, hipMemcpyHostToDevice, ctx->stream));

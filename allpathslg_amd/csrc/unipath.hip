@@ -2614,6 +2614,7 @@ static int u_sk_nodes(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, KRec**
   // the correction stage's tables are dead here: released only under memory
   // pressure (record ping-pong + node table ~ 3 record arrays)
   APG_TRY(ws_make_room(ctx, 3 * n * sizeof(SK48), kRoomCorrection));  // descriptors stay: the scatter replays them
+  ctx->ws_dead |= kRoomCorrection;  // and a failed allocation of the graph stages may release them
   SK48* recs = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1) + 1, &recs));
   APG_TRY(usk_scatter(ctx, dr, p, 1, G, recs));
@@ -3128,7 +3129,9 @@ int apg_urec_count(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, u
   if (n_instances) *n_instances = nk;
   // send + receive + partition ping-pong of the 48-byte records; the
   // correction stage's tables are dead by now (released only under pressure)
-  return ws_make_room(ctx, 4 * h[ndig] * sizeof(SK48), kRoomCorrection);  // descriptors stay for the scatter
+  APG_TRY(ws_make_room(ctx, 4 * h[ndig] * sizeof(SK48), kRoomCorrection));  // descriptors stay for the scatter
+  ctx->ws_dead |= kRoomCorrection;  // and a failed allocation of the graph stages may release them
+  return APG_OK;
 }
 
 int apg_urec_scatter(apg_ctx* ctx, const apg_dreads* reads, int K, int n_shards, void* d_send) {
