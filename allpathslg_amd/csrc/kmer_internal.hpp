@@ -51,6 +51,14 @@ int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
 int sk_scatter_pos(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out, uint64_t* pos, uint32_t split = 0);
 // the piece length that keeps a K-mer's records within the packed form
 uint32_t sk_pack_split(int K);
+// The records a multi-GPU owner received from its own rank (P > 1): receive
+// indices [lo, lo + n), sent at send indices [send, send + n).  Their weak
+// bits go straight into the reads' bitmap at wpos[send + (b - lo)] (no mask
+// for them in the return exchange); the other records' masks are written to
+// wrec packed without the self segment (index b, or b - n past it).
+struct SkSelf {
+  uint64_t lo = 0, n = 0, send = 0;
+};
 // solid set of received records + per-record weak masks (receive order).
 // split_recs: the records were cut by sk_pack_split (<= 32 bases), so the
 // owner's partition levels may carry them packed (16 bytes, the receive
@@ -61,7 +69,7 @@ int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64
                         int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res,
                         int up_K = 0, uint64_t* up_hist = nullptr, size_t up_hist_len = 0,
                         SkResult* up_res = nullptr, bool split_recs = false, unsigned long long* weak = nullptr,
-                        const uint64_t* wpos = nullptr);
+                        const uint64_t* wpos = nullptr, SkSelf self = SkSelf{});
 bool sk_can_fuse_up(int K);
 // Owner side of the sharded fused spectrum + PreCorrect (precorrect.hip): as
 // apg_shard_solid_weak, plus this shard's K+1 spectrum (up_hist) from the
@@ -69,11 +77,19 @@ bool sk_can_fuse_up(int K);
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
                            SkResult* up_res, bool split_recs = false, uint64_t n_kmers = ~0ull,
-                           unsigned long long* weak = nullptr, const uint64_t* wpos = nullptr);
+                           unsigned long long* weak = nullptr, const uint64_t* wpos = nullptr,
+                           SkSelf self = SkSelf{});
 // PreCorrect's correction pass over reads whose weak bitmap ("pc_weak") the
 // owner count already built (sk_shard_solid_weak with weak + wpos)
 int precorrect_weak_built(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const void* d_solid,
                           uint64_t n_solid, unsigned long long* weak, apg_pc_stats* st);
+// The same when the owner count built the self-owned records' bits (SkSelf)
+// and the returned masks of the other n_in - n_self sent records are still to
+// be ORed in: mask[0, self_send) for pos[0, self_send), mask[self_send, ...)
+// for pos[self_send + n_self, n_in)
+int precorrect_weak_masks(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const void* d_solid,
+                          uint64_t n_solid, unsigned long long* weak, const uint64_t* pos, const uint32_t* mask,
+                          uint64_t n_in, uint64_t self_send, uint64_t n_self, apg_pc_stats* st);
 int sk_stage_count(apg_ctx* ctx, const SK16* src, SK16* spare, const std::vector<uint64_t>& rec_counts,
                    uint64_t n_kmers, int K, int P, bool solid, uint32_t min_solid, uint64_t* hist, size_t hist_len,
                    SkResult* res);

@@ -1691,7 +1691,7 @@ namespace apg {
 int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                            uint32_t min_solid, void* d_mask, uint64_t* n_solid, uint64_t* up_hist, size_t up_hist_len,
                            SkResult* up_res, bool split_recs, uint64_t n_kmers, unsigned long long* weak,
-                           const uint64_t* wpos) {
+                           const uint64_t* wpos, SkSelf self) {
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid_weak: NULL argument");
   APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
@@ -1711,7 +1711,7 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   APG_TRY(err);
   SkResult sr;
   APG_TRY(sk_shard_solid_weak(ctx, recs, rc, nk, K, n_shards, min_solid, static_cast<uint32_t*>(d_mask), &sr,
-                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res, split_recs, weak, wpos));
+                              up_res ? K + 1 : 0, up_hist, up_hist_len, up_res, split_recs, weak, wpos, self));
   // The K+1 pass (side stream, kicked at the correction's stage as on one
   // GPU) reads only this count's record buffers: the caller's mask return,
   // solid-set gather and correction run beside it, and the caller joins it
@@ -1731,6 +1731,22 @@ int precorrect_weak_built(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, 
   APG_REQUIRE(n_solid == 0 || d_solid, "apg_precorrect_weak: d_solid is NULL");
   std::memset(st, 0, sizeof *st);
   return correct_pass(ctx, dr, p, static_cast<const uint64_t*>(d_solid), n_solid, st, weak);
+}
+
+int precorrect_weak_masks(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const void* d_solid,
+                          uint64_t n_solid, unsigned long long* weak, const uint64_t* pos, const uint32_t* mask,
+                          uint64_t n_in, uint64_t self_send, uint64_t n_self, apg_pc_stats* st) {
+  APG_REQUIRE(self_send + n_self <= n_in, "precorrect_weak_masks: self segment out of range");
+  // the returned masks of the records other ranks owned, around the self
+  // segment whose bits the owner count wrote already
+  const uint64_t n_a = self_send, n_b = n_in - self_send - n_self;
+  kbegin(ctx, "weak_apply", (n_a + n_b) * 12);
+  if (n_a) k_weak_apply<<<grid_for(ctx, n_a), 256, 0, ctx->stream>>>(pos, mask, n_a, weak);
+  if (n_b)
+    k_weak_apply<<<grid_for(ctx, n_b), 256, 0, ctx->stream>>>(pos + self_send + n_self, mask + self_send, n_b, weak);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return precorrect_weak_built(ctx, dr, p, d_solid, n_solid, weak, st);
 }
 }  // namespace apg
 

@@ -24,6 +24,7 @@
 //                sets and the whole graph built on every rank instead.
 // Results equal the single-GPU entry points on the union of the ranks' reads
 // (tests/test_distributed.py).
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -185,7 +186,8 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
     Exchanged x;
     uint64_t n_local = 0;
     void* smask = nullptr;
-    unsigned long long* wbits = nullptr;  // world size 1: the bitmap the owner count built
+    unsigned long long* wbits = nullptr;  // the bitmap the owner count built (all records or the self-owned ones)
+    uint64_t self_send = 0, self_n = 0;
     if (weak) {
       APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
                                [&](void* send) {
@@ -196,40 +198,56 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
                                },
                                &x));
       void* rmask = nullptr;
-      if (P == 1) {
-        // the owner is this rank and the receive order the send order: the
-        // count ORs the weak bits straight into the reads' bitmap at
-        // x_pos[receive index] (no masks, no return, no apply pass)
+      // P == 1: the owner is this rank and the receive order the send order:
+      // the count ORs the weak bits straight into the reads' bitmap at
+      // x_pos[receive index] (no masks, no return, no apply pass).  P > 1: the
+      // same for the 1/P of the records this rank sent to itself (SkSelf);
+      // only the other ranks' records travel back as masks (APG_SHARD_SELF=0:
+      // every record's mask travels, the round-4 form)
+      static const bool self_on = !(getenv("APG_SHARD_SELF") && !strcmp(getenv("APG_SHARD_SELF"), "0"));
+      const bool direct = P == 1 || self_on;
+      SkSelf self;
+      if (P > 1 && direct) {
+        for (int q = 0; q < c->rank; ++q) {
+          self.lo += x.rb[q] / 16;
+          self.send += x.sb[q] / 16;
+        }
+        self.n = x.rb[c->rank] / 16;
+      }
+      if (direct) {
         void* wb = nullptr;
         APG_TRY(workspace(ctx, "pc_weak", (reads->n_bases / 64 + 2) * 8, &wb));
         APG_CHECK_HIP(hipMemsetAsync(wb, 0, (reads->n_bases / 64 + 2) * 8, ctx->stream));
         wbits = static_cast<unsigned long long*>(wb);
-      } else {
-        APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>(x.n_out * 4, 64), &rmask));
       }
+      if (P > 1) APG_TRY(workspace(ctx, "x_rmask", std::max<uint64_t>((x.n_out - self.n) * 4, 64), &rmask));
       const uint64_t* wpos = wbits ? static_cast<const uint64_t*>(pos) : nullptr;
       if (up_hist && cyc == 0) {
         // the K+1 pass runs on the side stream beside the mask return, the
         // solid-set gather and the correction below; joined after them
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, up_hist,
-                                       up_hist_len, &up_res, true, n_kmers_in, wbits, wpos));
+                                       up_hist_len, &up_res, true, n_kmers_in, wbits, wpos, self));
         up_pending = true;
       } else {
         APG_TRY(shard_solid_weak_fused(ctx, x.recv, x.recv_counts.data(), K, P, p.min_solid, rmask, &n_local, nullptr,
-                                       0, nullptr, true, n_kmers_in, wbits, wpos));
+                                       0, nullptr, true, n_kmers_in, wbits, wpos, self));
       }
-      // masks travel back: the splits reversed, 4 bytes per record
+      // masks travel back: the splits reversed, 4 bytes per record (none for
+      // the self segment when its bits are in the bitmap already)
       std::vector<uint64_t> mb_out(P), mb_in(P);
       for (int q = 0; q < P; ++q) {
-        mb_out[q] = x.rb[q] / 16 * 4;
-        mb_in[q] = x.sb[q] / 16 * 4;
+        const bool own = direct && q == c->rank;
+        mb_out[q] = own ? 0 : x.rb[q] / 16 * 4;
+        mb_in[q] = own ? 0 : x.sb[q] / 16 * 4;
       }
       if (P == 1) {  // the weak bits are in the reads' bitmap already
         smask = nullptr;
       } else {
-        APG_TRY(workspace(ctx, "x_smask", std::max<uint64_t>(x.n_in * 4, 64), &smask));
+        APG_TRY(workspace(ctx, "x_smask", std::max<uint64_t>((x.n_in - self.n) * 4, 64), &smask));
         APG_TRY(c->alltoallv(rmask, mb_out.data(), smask, mb_in.data()));
       }
+      self_send = self.send;
+      self_n = self.n;
     } else {
       APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
                                [&](void* send) { return apg_shard_scatter(ctx, reads, K, P, send); }, &x));
@@ -249,7 +267,10 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
     uint64_t n_solid = 0;
     APG_TRY(gather_all(ctx, c, local, n_local, 8, "x_solid", &solid, &n_solid));
     apg_pc_stats st;
-    if (wbits)
+    if (wbits && P > 1)
+      APG_TRY(precorrect_weak_masks(ctx, reads, p, solid, n_solid, wbits, static_cast<const uint64_t*>(pos),
+                                    static_cast<const uint32_t*>(smask), x.n_in, self_send, self_n, &st));
+    else if (wbits)
       APG_TRY(precorrect_weak_built(ctx, reads, p, solid, n_solid, wbits, &st));
     else if (weak)
       APG_TRY(apg_precorrect_weak(ctx, reads, &p, solid, n_solid, pos, smask, x.n_in, &st));

@@ -552,14 +552,26 @@ struct SkOut {
   // at wpos[record.pos] (the sharded count at world size 1, where the owner is
   // the reads' own rank: no mask return, no separate apply pass)
   const uint64_t* wpos = nullptr;
+  // with `weak` AND `wrec` (P > 1, SkSelf): the records received from this
+  // rank itself, receive indices [self_lo, self_lo + self_n), write their bits
+  // into `weak` at wpos[self_send + (b - self_lo)]; the others their masks
+  // into `wrec`, packed without that segment
+  uint64_t self_lo = 0, self_n = 0, self_send = 0;
 };
 
 // A record's weak-K-mer mask m (bit t: K-mer t) at record position b: into the
 // per-record mask array, or ORed into the per-base bitmap (one or two words).
 __device__ __forceinline__ void sk_weak_write(const SkOut& o, uint64_t b, uint32_t m) {
   if (o.wrec) {
-    o.wrec[b] = m;
-    return;
+    if (!o.weak) {
+      o.wrec[b] = m;
+      return;
+    }
+    if (b - o.self_lo >= o.self_n) {  // another rank's record: its mask travels back
+      o.wrec[b < o.self_lo ? b : b - o.self_n] = m;
+      return;
+    }
+    b = o.self_send + (b - o.self_lo);  // a self-owned record: its send index
   }
   if (o.wpos) b = o.wpos[b];
   const uint32_t sh = (uint32_t)(b & 63);
@@ -1551,8 +1563,7 @@ __global__ void __launch_bounds__(kBigChunk) k_sk_big_insert(const R* __restrict
 template <typename R>
 __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                               const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
-                              SkP p, BigTab g, uint32_t min_solid, unsigned long long* __restrict__ weak,
-                              uint32_t* __restrict__ wrec, const uint64_t* __restrict__ wpos) {
+                              SkP p, BigTab g, uint32_t min_solid, SkOut o) {
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = k0 + threadIdx.x;
@@ -1571,14 +1582,7 @@ __global__ void k_sk_big_weak(const R* __restrict__ rec, const uint64_t* __restr
       }
       if (x.cnt < min_solid) m |= 1u << t;
     }
-    if (wrec) {
-      if (m) wrec[rec_pos(r, p)] = m;
-    } else if (m) {  // the record's mask in one or two ORs, as k_sk_bucket
-      const uint64_t b = wpos ? wpos[rec_pos(r, p)] : rec_pos(r, p);
-      const uint32_t sh = (uint32_t)(b & 63);
-      atomicOr(&weak[b >> 6], (unsigned long long)m << sh);
-      if (sh && ((uint64_t)m >> (64 - sh))) atomicOr(&weak[(b >> 6) + 1], (unsigned long long)m >> (64 - sh));
-    }
+    if (m) sk_weak_write(o, rec_pos(r, p), m);  // wrec is zeroed beforehand: only records with weak K-mers write
   }
 }
 
@@ -1973,7 +1977,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                             size_t hist_len, unsigned long long* weak, SkResult* res, uint32_t* wrec = nullptr,
                             const SK16* src16 = nullptr, int up_K = 0, uint64_t* up_hist = nullptr,
                             size_t up_hist_len = 0, SkResult* up_res = nullptr, const SKP* srcp = nullptr,
-                            bool split16 = false, bool wide = false, const uint64_t* wpos = nullptr) {
+                            bool split16 = false, bool wide = false, const uint64_t* wpos = nullptr,
+                            SkSelf self = SkSelf{}) {
   SkP p = make_skp(K);
   p.wide = wide;
   const int pbits = sk_ceil_log2((uint64_t)P), l1 = kSkDigitBits;
@@ -2178,6 +2183,11 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
              (uint32_t)(!solid || (hist && hist_len))};
     o.sused = sused;
     o.wpos = solid ? wpos : nullptr;
+    if (solid && weak && wrec) {
+      o.self_lo = self.lo;
+      o.self_n = self.n;
+      o.self_send = self.send;
+    }
     o.n_sused = solid ? solid_cap / kSolidChunk : 0;
     // the weak-pass variant (SK24 records) runs 512-thread blocks: its per-wave
     // LDS (owner map, recorded slots) and the table amortised over 8 waves give
@@ -2254,8 +2264,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
         if constexpr (RecPos<RB>::value) {
           if (o.weak || o.wrec)
-            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o.weak,
-                                                        o.wrec, o.wpos);
+            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o);
         }
         kend(ctx);
         APG_CHECK_HIP(hipGetLastError());
@@ -2451,22 +2460,24 @@ __global__ void k_sk_index24(const SK16* __restrict__ in, uint64_t n, SK24* __re
 int sk_shard_solid_weak(apg_ctx* ctx, const SK16* recv, const std::vector<uint64_t>& rec_counts, uint64_t n_kmers,
                         int K, int P, uint32_t min_solid, uint32_t* wrec, SkResult* res, int up_K, uint64_t* up_hist,
                         size_t up_hist_len, SkResult* up_res, bool split_recs, unsigned long long* weak,
-                        const uint64_t* wpos) {
+                        const uint64_t* wpos, SkSelf self) {
   APG_REQUIRE(K >= 9 && K <= 32, "sk_shard_solid_weak: K must be in [9, 32]");
   uint64_t n = 0;
   for (auto c : rec_counts) n += c;
   SK24* buf = nullptr;
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &buf));
   // weak + wpos (world size 1): the weak bits straight into the reads' bitmap
-  // at wpos[receive index], no per-record masks
-  if (weak) wrec = nullptr;
-  if (n && wrec) APG_CHECK_HIP(hipMemsetAsync(wrec, 0, n * 4, ctx->stream));
+  // at wpos[receive index], no per-record masks; weak + wpos + wrec (P > 1):
+  // the self-owned records' bits so, the others' masks into wrec (SkSelf)
+  APG_REQUIRE(!weak || wpos, "sk_shard_solid_weak: weak bits need the send positions");
+  APG_REQUIRE(!(weak && wrec) || self.lo + self.n <= n, "sk_shard_solid_weak: self segment out of range");
+  if (n > self.n && wrec) APG_CHECK_HIP(hipMemsetAsync(wrec, 0, (n - self.n) * 4, ctx->stream));
   ctx->sk_record_form = 3;
   // the first partition level reads the SK16 records and writes them as SK24
   // with their receive index (no separate widening pass)
   return sk_stage_count_t<SK24>(ctx, buf, buf, rec_counts, n_kmers, K, P, true, min_solid, nullptr, 0, weak, res,
                                 wrec, recv, up_K, up_hist, up_hist_len, up_res, nullptr, split_recs, false,
-                                weak ? wpos : nullptr);
+                                weak ? wpos : nullptr, self);
 }
 
 __global__ void k_sk_sum_kmers(const SK16* __restrict__ rec, uint64_t n, unsigned long long* __restrict__ out) {
