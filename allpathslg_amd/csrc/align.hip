@@ -990,6 +990,8 @@ extern "C" {
 
 int apg_gapfree_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T, const apg_aln_pair* d_pairs, uint64_t n,
                     apg_gapfree_hit* d_out) {
+  APG_TRY(dreads_quals_ready(S));
+  APG_TRY(dreads_quals_ready(T));
   APG_REQUIRE(ctx && S && T, "apg_gapfree: NULL argument");
   APG_REQUIRE(n == 0 || (d_pairs && d_out), "apg_gapfree: NULL pairs/out");
   static_assert(sizeof(apg_aln_pair) == sizeof(AlnPair), "pair layout");
@@ -1029,6 +1031,8 @@ int apg_gapfree(apg_ctx* ctx, const apg_reads* S, const apg_reads* T, const apg_
 
 int apg_banded_sw_dev(apg_ctx* ctx, const apg_dreads* S, const apg_dreads* T, const apg_aln_pair* d_pairs, uint64_t n,
                       int band_w, apg_sw_hit* d_out, int32_t* d_blocks, uint32_t max_blocks) {
+  APG_TRY(dreads_quals_ready(S));
+  APG_TRY(dreads_quals_ready(T));
   APG_REQUIRE(ctx && S && T, "apg_banded_sw: NULL argument");
   APG_REQUIRE(n == 0 || (d_pairs && d_out), "apg_banded_sw: NULL pairs/out");
   APG_REQUIRE(band_w >= 0 && 2 * band_w + 1 <= 64 * kSwChunks, "apg_banded_sw: band_w must be in [0, 127]");
@@ -1138,6 +1142,8 @@ int apg_banded_sw(apg_ctx* ctx, const apg_reads* S, const apg_reads* T, const ap
 
 int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T, const apg_aln_pair* d_plc, uint64_t n,
                       uint8_t* d_bases, uint8_t* d_quals) {
+  APG_TRY(dreads_quals_ready(R));
+  APG_TRY(dreads_quals_ready(T));
   APG_REQUIRE(ctx && R && T, "apg_consensus: NULL argument");
   APG_REQUIRE(n == 0 || d_plc, "apg_consensus: NULL placements");
   APG_REQUIRE(n == 0 || R->d_quals, "apg_consensus: the placed reads need qualities");
@@ -1168,6 +1174,8 @@ int apg_consensus_dev(apg_ctx* ctx, const apg_dreads* R, const apg_dreads* T, co
 // each chunk a pass over the placements restricted to its columns.
 int apg_sharded_consensus(apg_ctx* ctx, apg_comm* comm, const apg_dreads* R, const apg_dreads* T,
                           const apg_aln_pair* d_plc, uint64_t n, uint8_t* d_bases, uint8_t* d_quals) {
+  APG_TRY(dreads_quals_ready(R));
+  APG_TRY(dreads_quals_ready(T));
   APG_REQUIRE(ctx && comm && R && T, "apg_sharded_consensus: NULL argument");
   Comm* c = comm_of(comm);
   APG_REQUIRE(c && c->ctx == ctx, "apg_sharded_consensus: the communicator belongs to another context");

@@ -181,6 +181,7 @@ static void staging_free(apg_ctx* ctx) {
 }
 
 int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers) {
+  if (ctx->bg_load) APG_TRY(dreads_quals_ready(ctx->bg_load));  // it holds the staging buffers
   struct Chunk {
     uint8_t* dst;
     const uint8_t* src;
@@ -395,6 +396,7 @@ int apg_create(const apg_config* cfg, apg_ctx** out) {
 int apg_trim(apg_ctx* ctx) {
   APG_REQUIRE(ctx, "apg_trim: ctx is NULL");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
+  if (ctx->bg_load) APG_TRY(dreads_quals_ready(ctx->bg_load));
   APG_TRY(side_join(ctx));
   APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   for (auto& kv : ctx->ws)
@@ -412,6 +414,7 @@ int apg_trim(apg_ctx* ctx) {
 void apg_destroy(apg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  if (ctx->bg_load) (void)dreads_quals_ready(ctx->bg_load);
   (void)side_join(ctx);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
@@ -585,6 +588,7 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
 
 void apg_reads_free(apg_dreads* d) {
   if (!d) return;
+  (void)dreads_quals_ready(d);  // no load may still write into it
   (void)hipSetDevice(d->device);
   if (d->d_base_off) (void)hipFree(d->d_base_off);
   if (d->d_byte_off) (void)hipFree(d->d_byte_off);
@@ -627,6 +631,8 @@ int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
   APG_REQUIRE(dst->n_reads == src->n_reads && dst->n_bases == src->n_bases && dst->n_bytes == src->n_bytes && same,
               "apg_reads_copy_dev: read sets differ in shape");
   APG_REQUIRE(!src->d_quals || dst->d_quals, "apg_reads_copy_dev: destination has no qualities");
+  APG_TRY(dreads_quals_ready(src));
+  APG_TRY(dreads_quals_ready(dst));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   if (src->n_bytes)
     APG_CHECK_HIP(hipMemcpyAsync(dst->d_packed, src->d_packed, src->n_bytes, hipMemcpyDeviceToDevice, ctx->stream));

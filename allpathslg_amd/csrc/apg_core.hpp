@@ -68,6 +68,12 @@ struct KernelStat {
 
 }  // namespace apg
 
+namespace apg {
+// A read set's qualities still streaming in from a .qualb file
+// (apg_reads_load_dev): the host thread that loads them, and its outcome.
+struct DreadsPending;
+}  // namespace apg
+
 // Device-resident read set.
 struct apg_dreads {
   apg_ctx* ctx = nullptr;  // producing context: identity only, never dereferenced (it may be destroyed first)
@@ -87,6 +93,9 @@ struct apg_dreads {
   bool fill_owned = false;
   bool concat_owned = false;  // apg_reads_concat_dev output
   uint64_t cap_reads = 0, cap_bytes = 0, cap_quals = 0;
+  // qualities still loading in the background (apg_reads_load_dev): every
+  // reader of d_quals calls apg::dreads_quals_ready first
+  apg::DreadsPending* pending = nullptr;
 };
 
 struct apg_ctx {
@@ -119,6 +128,9 @@ struct apg_ctx {
     size_t bytes = 0;
   };
   std::map<std::string, Buf> ws;
+  // the read set whose qualities a background load is streaming through this
+  // context's staging buffers (apg_load.cpp); any other staging user joins it
+  apg_dreads* bg_load = nullptr;
 
   // Per-kernel timing.
   std::vector<std::string> korder;
@@ -322,6 +334,11 @@ struct D2HJob {
 // Device arrays -> host arrays (the device data must be complete: call after a
 // sync of ctx->stream).  Synchronous.
 int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers = 4);
+
+// Wait for a background load of the read set's qualities (apg_reads_load_dev)
+// to land in HBM; APG_OK at once when none is running.  Every reader of
+// d_quals calls it first (apg_load.cpp).
+int dreads_quals_ready(const apg_dreads* dr);
 
 // Free device memory (hipMemGetInfo; ~0 if unknown).
 uint64_t device_free_bytes(apg_ctx* ctx);

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <new>
 #include <vector>
 
 #include "apg_core.hpp"
@@ -179,6 +180,30 @@ int read_head(const char* path, const char* magic, Head* h) {
 
 }  // namespace
 
+namespace apg {
+struct DreadsPending {
+  std::thread th;
+  int rc = APG_OK;
+  std::string err;
+  apg_ctx* ctx = nullptr;
+  double ms = 0;
+};
+
+int dreads_quals_ready(const apg_dreads* cd) {
+  apg_dreads* d = const_cast<apg_dreads*>(cd);
+  if (!d || !d->pending) return APG_OK;
+  DreadsPending* p = d->pending;
+  p->th.join();
+  d->pending = nullptr;
+  if (p->ctx && p->ctx->bg_load == d) p->ctx->bg_load = nullptr;
+  const int rc = p->rc;
+  if (rc != APG_OK) set_error(p->err);
+  vlog(p->ctx, "load_dev: qualities landed in the background (%.1f ms of streaming)", p->ms);
+  delete p;
+  return rc;
+}
+}  // namespace apg
+
 extern "C" {
 
 // Files -> HBM with no host pass over the reads: the offset tables stream to
@@ -191,6 +216,7 @@ extern "C" {
 int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int threads, apg_dreads** out) {
   APG_REQUIRE(ctx && fastb && out, "apg_reads_load_dev: NULL argument");
   *out = nullptr;
+  if (ctx->bg_load) APG_TRY(dreads_quals_ready(ctx->bg_load));  // one load at a time through the staging buffers
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
@@ -249,11 +275,35 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
   rc = stream_to_device(ctx, fastb, 32 + 8 * (n + 1), d->n_bytes, d->d_packed, threads);
   const double t_bases = ms(t1);
   const auto t2 = clk::now();
-  if (rc == APG_OK && qualb && n)
-    rc = stream_to_device(ctx, qualb, 32 + 8 * (n + 1), d->n_bases, d->d_quals, threads);
-  vlog(ctx, "load_dev: %llu reads, offsets -> HBM + device checks %.1f ms, bases %.1f ms (%.2f GB/s), quals %.1f ms, "
+  // The qualities (4/5 of the bytes) are first read by PreCorrect's
+  // candidate scan, after the whole K-mer count: they keep streaming in on
+  // a host thread while the caller's next module counts the bases, and every
+  // reader of d_quals joins the load first (dreads_quals_ready).
+  // APG_LOAD_SYNC=1: loaded before the call returns (the round-4 form).
+  static const bool sync_load = std::getenv("APG_LOAD_SYNC") && !std::strcmp(std::getenv("APG_LOAD_SYNC"), "1");
+  if (rc == APG_OK && qualb && n) {
+    if (sync_load) {
+      rc = stream_to_device(ctx, qualb, 32 + 8 * (n + 1), d->n_bases, d->d_quals, threads);
+    } else {
+      auto* pend = new (std::nothrow) DreadsPending();
+      if (!pend) return fail(APG_E_NOMEM);
+      pend->ctx = ctx;
+      const std::string qpath(qualb);
+      const uint64_t qo = 32 + 8 * (n + 1), qn = d->n_bases;
+      uint8_t* qdst = d->d_quals;
+      pend->th = std::thread([pend, ctx, qpath, qo, qn, qdst, threads]() {
+        const auto tq = std::chrono::steady_clock::now();
+        pend->rc = stream_to_device(ctx, qpath.c_str(), qo, qn, qdst, threads);
+        if (pend->rc != APG_OK) pend->err = get_error();
+        pend->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count();
+      });
+      d->pending = pend;
+      ctx->bg_load = d;
+    }
+  }
+  vlog(ctx, "load_dev: %llu reads, offsets -> HBM + device checks %.1f ms, bases %.1f ms (%.2f GB/s), quals %.1f ms%s, "
        "%d threads", (unsigned long long)n, t_meta, t_bases, d->n_bytes / std::max(t_bases, 1e-3) / 1e6, ms(t2),
-       threads);
+       d->pending ? " (streaming on)" : "", threads);
   if (rc != APG_OK) return fail(rc);
   *out = d;
   return APG_OK;

@@ -1002,6 +1002,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
                         apg_pc_stats* st, const unsigned long long* weak = nullptr, bool self_count = false) {
   ctx->clean_valid = false;
   ctx->ws_dead &= ~kRoomCorrection;  // the correction tables are live again
+  APG_TRY(dreads_quals_ready(dr));  // the candidate scan reads them (a load may still stream them in)
   // the previous pass's extension table is this very list's (the jump reads'
   // pass of ErrorCorrectJump against the fragments' reused solid set)
   const bool ext_reuse = ctx->pc_ext_valid && ctx->pc_list_valid && ctx->pc_list == list && ctx->pc_n == n_solid &&
@@ -1855,6 +1856,7 @@ int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, 
 
 int apg_reads_download(apg_ctx* ctx, const apg_dreads* dr, uint8_t* packed, uint8_t* quals) {
   APG_REQUIRE(ctx && dr, "apg_reads_download: NULL argument");
+  APG_TRY(dreads_quals_ready(dr));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   if (packed && dr->n_bytes)
     APG_CHECK_HIP(hipMemcpyAsync(packed, dr->d_packed, dr->n_bytes, hipMemcpyDeviceToHost, ctx->stream));

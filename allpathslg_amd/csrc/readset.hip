@@ -186,6 +186,7 @@ int apg_reads_concat_dev(apg_ctx* ctx, const apg_dreads* const* sets, const uint
     n += sets[s]->n_reads;
     max_len = std::max(max_len, sets[s]->max_len);
     quals = quals && sets[s]->d_quals;
+    APG_TRY(dreads_quals_ready(sets[s]));
   }
   uint64_t len_bytes = 0;  // cat_len: offsets read, keep read, two u32 per read written
   for (uint32_t s = 0; s < n_sets; ++s)

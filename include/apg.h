@@ -923,9 +923,17 @@ void apg_reads_release(apg_reads* r);
  * frag_reads_*.fastb / .qualb every module opens; src/feudal/).  Offsets are
  * read and validated as by apg_fastb_read / apg_qualb_read; the payloads go
  * file -> pinned staging -> HBM in 16 MiB chunks, `threads` workers (<= 0:
- * min(4, hardware threads)) each double-buffering pread against its own H2D
+ * min(16, hardware threads)) each double-buffering pread against its own H2D
  * stream.  Same device read set as apg_fastb_read + apg_qualb_read +
- * apg_reads_upload; free with apg_reads_free. */
+ * apg_reads_upload; free with apg_reads_free.  The call returns once the
+ * offsets and bases are in HBM: the qualities (4/5 of the bytes) keep
+ * streaming in on a host thread of the context while the next module counts
+ * the bases, and every entry point that reads them (PreCorrect / FindErrors /
+ * ErrorCorrectJump, apg_reads_copy_dev, apg_reads_download,
+ * apg_reads_concat_dev, the aligners, apg_reads_free, apg_trim,
+ * apg_destroy) waits for that load first; a read error found there is that
+ * call's error (APG_E_IO).  Environment APG_LOAD_SYNC=1: loaded before the
+ * call returns. */
 int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int threads, apg_dreads** out);
 /* Spectrum text file (.kspec): "m\tcount" lines for nonzero bins, after
  * '#' header lines that carry apg_kspec_estimate's summary. */

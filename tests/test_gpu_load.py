@@ -100,3 +100,41 @@ def test_refuses_bad_inputs(gpu_ctx, tmp_path):
         gpu_ctx.load_reads(fb, qo)
     with pytest.raises(ApgError):
         gpu_ctx.load_reads(str(tmp_path / "missing.fastb"))
+
+
+def test_background_qualities_equal_uploaded(gpu_ctx, tmp_path):
+    """apg_reads_load_dev returns once bases and offsets are in HBM; the
+    qualities stream in on a host thread while the next module counts the
+    bases, and every reader of them joins the load first.  The fused K=25
+    spectrum + K=24 PreCorrect called right after the load (the bench's
+    file_to_graph order) gives the uploaded set's spectrum, corrected bases,
+    qualities and counters byte for byte; a set freed, copied or reloaded
+    while its qualities stream is safe."""
+    g = synth_genome(3_000_000, 43)
+    rs = synth_reads(g, 1_500_000, seed=44)  # 300 MB of qualities: many chunks after the call returns
+    fb, qb = _write(tmp_path, rs, "bg")
+    try:
+        d = gpu_ctx.load_reads(fb, qb)
+        h1, k1, p1 = gpu_ctx.spectrum_precorrect(d, K_spec=25, K=24)
+        got = gpu_ctx.download(d, with_quals=True)
+        d.free()
+        du = gpu_ctx.upload(rs)
+        h2, k2, p2 = gpu_ctx.spectrum_precorrect(du, K_spec=25, K=24)
+        exp = gpu_ctx.download(du, with_quals=True)
+        assert np.array_equal(h1, h2) and k1 == k2 and p1 == p2
+        nb = int(exp.byte_off[-1])
+        assert np.array_equal(got.packed[:nb], exp.packed[:nb])
+        assert np.array_equal(got.quals, exp.quals)
+        # freed while streaming; reloaded while the previous load streams;
+        # copied while streaming
+        gpu_ctx.load_reads(fb, qb).free()
+        a = gpu_ctx.load_reads(fb, qb)
+        b = gpu_ctx.load_reads(fb, qb)
+        gpu_ctx.copy_reads(du, b)
+        _same(gpu_ctx, du, ReadSet.load(fb, qb), True)
+        _same(gpu_ctx, a, ReadSet.load(fb, qb), True)
+        for x in (a, b, du):
+            x.free()
+    finally:
+        for p in (fb, qb):
+            os.unlink(p)
