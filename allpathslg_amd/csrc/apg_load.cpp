@@ -178,6 +178,34 @@ int read_head(const char* path, const char* magic, Head* h) {
   return APG_OK;
 }
 
+// The offset tables of a .fastb and its .qualb (both at byte 32, n + 1 u64)
+// are identical: compared chunk by chunk from the files (apg_qualb_read's
+// rule: the qualities follow the bases read by read).
+int qualb_offsets_match(const char* fastb, const char* qualb, uint64_t n) {
+  Fd a, b;
+  a.fd = open(fastb, O_RDONLY);
+  b.fd = open(qualb, O_RDONLY);
+  if (a.fd < 0 || b.fd < 0) {
+    set_error(std::string("cannot open ") + (a.fd < 0 ? fastb : qualb));
+    return APG_E_IO;
+  }
+  constexpr uint64_t kChunk = 8ull << 20;
+  std::vector<uint8_t> x(kChunk), y(kChunk);
+  const uint64_t len = 8 * (n + 1);
+  for (uint64_t o = 0; o < len; o += kChunk) {
+    const uint64_t m = std::min(kChunk, len - o);
+    if (pread(a.fd, x.data(), m, (off_t)(32 + o)) != (ssize_t)m || pread(b.fd, y.data(), m, (off_t)(32 + o)) != (ssize_t)m) {
+      set_error(std::string("short read of the offset tables of ") + qualb);
+      return APG_E_IO;
+    }
+    if (std::memcmp(x.data(), y.data(), m) != 0) {
+      set_error(std::string("qualb/fastb length mismatch: ") + qualb);
+      return APG_E_IO;
+    }
+  }
+  return APG_OK;
+}
+
 }  // namespace
 
 namespace apg {
@@ -243,16 +271,12 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
     apg_reads_free(d);
     return rc;
   };
-  uint64_t* qoff = nullptr;
-  if (qualb) {
-    const int rc = workspace_t(ctx, "ld_qoff", n + 1, &qoff);
-    if (rc != APG_OK) return fail(rc);
-  }
+  // the qualb's offset table only has to equal the fastb's: compared on the
+  // host beside the qualities' load (qualb_offsets_match), off the path to
+  // the bases
   int rc = stream_to_device(ctx, fastb, 32, 8 * (n + 1), reinterpret_cast<uint8_t*>(d->d_base_off), threads);
-  if (rc == APG_OK && qualb)
-    rc = stream_to_device(ctx, qualb, 32, 8 * (n + 1), reinterpret_cast<uint8_t*>(qoff), threads);
   if (rc == APG_OK) {
-    rc = dreads_device_shape(ctx, d, qoff, true, fastb);
+    rc = dreads_device_shape(ctx, d, nullptr, true, fastb);
     if (rc == APG_E_ARG) rc = APG_E_IO;  // a bad table is a bad file
   }
   if (rc == APG_OK && d->n_bases != hf.total) {
@@ -284,6 +308,7 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
   if (rc == APG_OK && qualb && n) {
     if (sync_load) {
       rc = stream_to_device(ctx, qualb, 32 + 8 * (n + 1), d->n_bases, d->d_quals, threads);
+      if (rc == APG_OK) rc = qualb_offsets_match(fastb, qualb, n);
     } else {
       auto* pend = new (std::nothrow) DreadsPending();
       if (!pend) return fail(APG_E_NOMEM);
@@ -291,9 +316,11 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
       const std::string qpath(qualb);
       const uint64_t qo = 32 + 8 * (n + 1), qn = d->n_bases;
       uint8_t* qdst = d->d_quals;
-      pend->th = std::thread([pend, ctx, qpath, qo, qn, qdst, threads]() {
+      const std::string fpath(fastb);
+      pend->th = std::thread([pend, ctx, qpath, fpath, n, qo, qn, qdst, threads]() {
         const auto tq = std::chrono::steady_clock::now();
         pend->rc = stream_to_device(ctx, qpath.c_str(), qo, qn, qdst, threads);
+        if (pend->rc == APG_OK) pend->rc = qualb_offsets_match(fpath.c_str(), qpath.c_str(), n);
         if (pend->rc != APG_OK) pend->err = get_error();
         pend->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count();
       });

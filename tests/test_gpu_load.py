@@ -138,3 +138,30 @@ def test_background_qualities_equal_uploaded(gpu_ctx, tmp_path):
     finally:
         for p in (fb, qb):
             os.unlink(p)
+
+
+def test_qualb_offsets_checked_beside_the_load(gpu_ctx, tmp_path):
+    """A .qualb whose per-read lengths differ from the .fastb's at the same
+    total passes the header checks; its offset table is compared with the
+    fastb's beside the background qualities load, and the first reader of
+    the qualities fails with APG_E_IO (a download, or PreCorrect)."""
+    rng = np.random.default_rng(5)
+    seqs = [rng.integers(0, 4, size=n) for n in (50, 60, 70)]
+    rs = ReadSet.from_sequences(seqs, [rng.integers(0, 41, size=len(s)) for s in seqs])
+    fb, _ = _write(tmp_path, rs, "okq")
+    swapped = ReadSet.from_sequences([s for s in (seqs[1], seqs[0], seqs[2])],
+                                     [rng.integers(0, 41, size=len(s)) for s in (seqs[1], seqs[0], seqs[2])])
+    _, qb = _write(tmp_path, swapped, "swapped")
+    d = gpu_ctx.load_reads(fb, qb)
+    with pytest.raises(ApgError):
+        gpu_ctx.download(d, with_quals=True)
+    d.free()
+    d = gpu_ctx.load_reads(fb, qb)
+    with pytest.raises(ApgError):
+        gpu_ctx.precorrect(d, K=24)
+    d.free()
+    # a good pair still loads on the same context
+    fb2, qb2 = _write(tmp_path, rs, "good")
+    d = gpu_ctx.load_reads(fb2, qb2)
+    _same(gpu_ctx, d, ReadSet.load(fb2, qb2), True)
+    d.free()
