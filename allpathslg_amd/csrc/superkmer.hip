@@ -1116,59 +1116,7 @@ __device__ __forceinline__ uint32_t lds_claim(unsigned long long* tk, uint64_t c
   return TS;
 }
 
-// 32-bit record fingerprint (V & 1): the record table keyed by it, one
-// 16-byte LDS read per 4-slot group instead of two; identity stays exact (the
-// verification after the barrier compares every record with its claimer's
-// copy, and a 32-bit collision hands the bucket back like any other).
-__device__ __forceinline__ uint32_t rec_fp32(const SK16& h, uint64_t keep) {
-  const uint32_t a = (uint32_t)h.w1, b = (uint32_t)(h.w1 >> 32), c = (uint32_t)((h.w0 & keep) >> 32);
-  const uint32_t x = sk_fmix32(a ^ __builtin_amdgcn_alignbit(b, b, 13) * 0x85ebca6bu ^ c * 0x9e3779b1u);
-  return x == ~0u ? 0u : x;  // ~0 marks an empty slot
-}
-template <uint32_t TS>
-__device__ __forceinline__ uint32_t lds_claim32(uint32_t* tk, uint32_t c, uint32_t g, bool* fresh) {
-  constexpr uint32_t EMPTY = ~0u;
-  *fresh = false;
-  for (uint32_t n = 0; n < (TS < kSkProbeMax ? TS : kSkProbeMax);) {
-    const uint4 a = *reinterpret_cast<const uint4*>(&tk[g]);
-    const uint32_t k[kSkGrp] = {a.x, a.y, a.z, a.w};
-    uint32_t j = kSkGrp;
-#pragma unroll
-    for (uint32_t q = kSkGrp; q-- > 0;)
-      if (k[q] == c || k[q] == EMPTY) j = q;
-    if (j == kSkGrp) {
-      g = (g + kSkGrp) & (TS - 1);
-      n += kSkGrp;
-      continue;
-    }
-    if (k[j] == c) return g + j;
-    const uint32_t old = atomicCAS(&tk[g + j], EMPTY, c);
-    if (old == EMPTY) {
-      *fresh = true;
-      return g + j;
-    }
-    if (old == c) return g + j;
-    ++n;
-  }
-  return TS;
-}
-// A list append taken by the lanes of a wave with `take`: one LDS atomic per
-// wave (the first taking lane's), each lane's slot by its rank among them.
-// Call from converged code (every lane of the wave executes it).
-__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool take) {
-  const uint64_t bal = __ballot(take);
-  if (!bal) return 0;
-  const uint32_t first = __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(bal));
-  uint32_t base = 0;
-  if (__lane_id() == first) base = atomicAdd(ctr, (uint32_t)__popcll(bal));
-  base = __builtin_amdgcn_readlane(base, first);
-  return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-}
-
-// V (A/B variants, APG_DD_VAR): 1 32-bit record table; 2 the weak masks from
-// independent slot loads (no dependent chain per K-mer); 4 the solid K-mers'
-// list appends wave-aggregated; 8 the claimed-slot list appends too.
-template <bool SOLID, typename R, int V = 0>
+template <bool SOLID, typename R>
 __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu(6))) k_sk_bucket_dd(const R* __restrict__ rec,
                                                              const uint64_t* __restrict__ boff, uint64_t nbuckets,
                                                              SkP p, SkOut o, uint32_t* __restrict__ redo,
@@ -1182,8 +1130,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
   __shared__ __attribute__((aligned(16))) unsigned long long tkey[kDdKTab];
   __shared__ uint32_t tcnt[kDdKTab];
   __shared__ uint16_t klist[kDdKTab];  // claimed K-mer slots (claim order)
-  __shared__ __attribute__((aligned(16))) unsigned long long rkey[(V & 1) ? 1 : kDdTab];
-  __shared__ __attribute__((aligned(16))) uint32_t rkey32[(V & 1) ? kDdTab : 1];
+  __shared__ __attribute__((aligned(16))) unsigned long long rkey[kDdTab];
   __shared__ uint32_t rcnt[kDdTab];  // multiplicity; weak mode: then the record's weak mask
   __shared__ __attribute__((aligned(16))) SK16 rrec[kDdTab];
   __shared__ uint16_t rlist[kDdTab];  // claimed record slots (claim order)
@@ -1203,10 +1150,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
     tcnt[s] = 0;
   }
   for (uint32_t s = tid; s < kDdTab; s += NT) {
-    if constexpr ((V & 1) != 0)
-      rkey32[s] = ~0u;
-    else
-      rkey[s] = EMPTY;
+    rkey[s] = EMPTY;
     rcnt[s] = 0;
   }
   if (tid == 0) {
@@ -1256,10 +1200,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
         tcnt[klist[j]] = 0;
       }
       for (uint32_t j = tid; j < nrs; j += NT) {
-        if constexpr ((V & 1) != 0)
-          rkey32[rlist[j]] = ~0u;
-        else
-          rkey[rlist[j]] = EMPTY;
+        rkey[rlist[j]] = EMPTY;
         rcnt[rlist[j]] = 0;
       }
       __syncthreads();
@@ -1312,13 +1253,8 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       uint32_t s = kDdTab;
       bool fresh = false;
       if (valid) {
-        if constexpr ((V & 1) != 0) {
-          const uint32_t fp = rec_fp32(hd, keep);
-          s = lds_claim32<kDdTab>(rkey32, fp, (fp >> (32 - RB)) & ~(kSkGrp - 1), &fresh);
-        } else {
-          const uint64_t fp = rec_fp(hd, keep);
-          s = lds_claim<kDdTab>(rkey, fp, (uint32_t)(fp >> (64 - RB)) & ~(kSkGrp - 1), &fresh);
-        }
+        const uint64_t fp = rec_fp(hd, keep);
+        s = lds_claim<kDdTab>(rkey, fp, (uint32_t)(fp >> (64 - RB)) & ~(kSkGrp - 1), &fresh);
         if (s < kDdTab) {
           if (fresh) rrec[s] = hd;
           atomicAdd(&rcnt[s], 1u);
@@ -1326,12 +1262,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
           atomicOr(&flag, 2);
         }
       }
-      if constexpr ((V & 8) != 0) {
-        const uint32_t at = wave_append(&nr_sh, fresh);
-        if (fresh) rlist[at] = (uint16_t)s;
-      } else {
-        if (fresh) rlist[atomicAdd(&nr_sh, 1u)] = (uint16_t)s;
-      }
+      if (fresh) rlist[atomicAdd(&nr_sh, 1u)] = (uint16_t)s;
       if constexpr (WEAK) {
 #pragma unroll
         for (uint32_t q = 0; q < kDdChunks; ++q)
@@ -1402,12 +1333,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
           atomicOr(&flag, 1);
         }
       }
-      if constexpr ((V & 8) != 0) {
-        const uint32_t at = wave_append(&nk_sh, fresh);
-        if (fresh) klist[at] = (uint16_t)ts;
-      } else {
-        if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)ts;
-      }
+      if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)ts;
     };
     for (uint32_t f0 = 0; f0 < ni; f0 += 2 * NT) {
       if (__builtin_amdgcn_readfirstlane(*(volatile int*)&flag)) break;  // the table filled (no barrier inside)
@@ -1428,22 +1354,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
           const uint32_t nk = (uint32_t)(rrec[s].w0 >> 32) & 0xff;
           const uint32_t b0 = doff[j];
           uint32_t m = 0;
-          if constexpr ((V & 2) != 0) {
-            // the record's slots, then their counts, each group of loads
-            // independent (two LDS round trips per 10 K-mers, not two per K-mer)
-            for (uint32_t t0 = 0; t0 < nk; t0 += 10) {
-              uint32_t sl[10];
-#pragma unroll
-              for (uint32_t u = 0; u < 10; ++u) sl[u] = t0 + u < nk ? own[b0 + t0 + u] : own[b0];
-#pragma unroll
-              for (uint32_t u = 0; u < 10; ++u) {
-                const uint32_t c = tcnt[sl[u]];
-                if (t0 + u < nk) m |= (uint32_t)(c < o.min_solid) << (t0 + u);
-              }
-            }
-          } else {
-            for (uint32_t t = 0; t < nk; ++t) m |= (uint32_t)(tcnt[own[b0 + t]] < o.min_solid) << t;
-          }
+          for (uint32_t t = 0; t < nk; ++t) m |= (uint32_t)(tcnt[own[b0 + t]] < o.min_solid) << t;
           rcnt[s] = m;
         }
         __syncthreads();
@@ -1466,13 +1377,7 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
       const uint32_t j = j0 + tid;
       const uint32_t cn = j < nK ? tcnt[klist[j]] : 0;
       if (want_hist && j < nK) sk_spectrum_add(cn, lhist, o);
-      if constexpr ((V & 4) != 0) {
-        const bool sol = SOLID && j < nK && cn >= o.min_solid;
-        const uint32_t at = wave_append(&ns_sh, sol);
-        if (sol) own[at] = klist[j];
-      } else {
-        if (SOLID && j < nK && cn >= o.min_solid) own[atomicAdd(&ns_sh, 1u)] = klist[j];
-      }
+      if (SOLID && j < nK && cn >= o.min_solid) own[atomicAdd(&ns_sh, 1u)] = klist[j];
     }
     if (SOLID) {
       __syncthreads();
@@ -2297,26 +2202,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
                                        : resident_grid(ctx, k_sk_bucket<false, RB, NTB>, NTB, nb);
     // record dedup first (K >= kDdMinK), k_sk_bucket for the buckets it hands back
     // (a launch over a device-side count: no host round trip in between)
-    // APG_DD_VAR (A/B of k_sk_bucket_dd variants; k_sk_bucket_dd's V)
-    static const int dd_var = getenv("APG_DD_VAR") ? atoi(getenv("APG_DD_VAR")) : 0;
-    auto dd_grid = [&](auto kern) { return resident_grid(ctx, kern, kDdThreads, nb); };
-    auto dd_solid = [&](uint64_t g, auto* drec_out) -> int {
-      switch (dd_var) {
-#define APG_DD_CASE(v)                                                                                         \
-  case v:                                                                                                      \
-    if (g == 0) return (int)dd_grid(k_sk_bucket_dd<true, RB, v>);                                            \
-    k_sk_bucket_dd<true, RB, v><<<g, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, drec_out, dcount); \
-    return 0;
-        APG_DD_CASE(1) APG_DD_CASE(2) APG_DD_CASE(4) APG_DD_CASE(8) APG_DD_CASE(6) APG_DD_CASE(14) APG_DD_CASE(15)
-#undef APG_DD_CASE
-        default:
-          if (g == 0) return (int)dd_grid(k_sk_bucket_dd<true, RB>);
-          k_sk_bucket_dd<true, RB><<<g, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, drec_out, dcount);
-          return 0;
-      }
-    };
     const uint64_t grid_dd = !dd ? 0
-                             : solid ? (uint64_t)dd_solid(0, (SK16*)nullptr)
+                             : solid ? resident_grid(ctx, k_sk_bucket_dd<true, RB>, kDdThreads, nb)
                                      : resident_grid(ctx, k_sk_bucket_dd<false, RB>, kDdThreads, nb);
     uint64_t n_drec = 0;
     for (int attempt = 0;; ++attempt) {
@@ -2329,7 +2216,8 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       kbegin(ctx, solid ? "sk_bucket_solid" : "sk_bucket", n * sizeof(RB) + (nb + 1) * 8 + weak_out);
       if (dd) {
         if (solid) {
-          (void)dd_solid(grid_dd, up_dd ? reinterpret_cast<SK16*>(dbuf) : nullptr);
+          k_sk_bucket_dd<true, RB><<<grid_dd, kDdThreads, 0, ctx->stream>>>(
+              cur, boff, nb, p, o, redo, up_dd ? reinterpret_cast<SK16*>(dbuf) : nullptr, dcount);
           k_sk_bucket<true, RB, NTB><<<grid, NTB, 0, ctx->stream>>>(cur, boff, nb, p, o, redo, gstats + 4);
         } else {
           k_sk_bucket_dd<false, RB><<<grid_dd, kDdThreads, 0, ctx->stream>>>(cur, boff, nb, p, o, redo);
