@@ -88,7 +88,7 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
 // releases).
 static const char* const kStageWs[] = {"big0",    "big1",    "big2",    "x_send",  "x_recv",  "x_pos",  "x_rmask",
                                        "x_smask", "x_local", "sk_gtab", "sk_cmat", "sk_omat",
-                                       "sk_solid_sparse", "sk_dcount", "ext_e0", "ext_e1"};
+                                       "sk_solid_sparse", "sk_dcount", "ext_e0", "ext_e1", "sk_ovf_e0", "sk_ovf_e1"};
 // record descriptors of a count pass: live from the count to its scatter
 static const char* const kDescWs[] = {"sk_desc", "usk_desc"};
 // APG_DEVICE_MEM_LIMIT=<bytes>: act as if the device held only that much for

@@ -1642,6 +1642,233 @@ __global__ void __launch_bounds__(256) k_sk_big_emit(const BigSlot* __restrict__
   wave_add(&o.gstats[0], nd);
 }
 
+// ---------------------------------------------------------------------------
+// Overflowed buckets by sub-bucket counting (default; APG_SK_OVF=global: the
+// global-table path above).  Distinct overflowed buckets never share a K-mer
+// (their minimizers differ), and inside one the K-mers split by a hash of the
+// canonical K-mer, so each (bucket, hash digit) sub-bucket counts alone in an
+// LDS table: every K-mer instance of the overflowed buckets leaves as a
+// 16-byte entry (k_ovf_expand), one partition level groups each bucket's
+// entries by the top 8 bits of the hash, and a workgroup per sub-bucket
+// counts it, re-reads it for the weak bits and emits the spectrum bins and
+// solid K-mers.  A sub-bucket whose distinct K-mers fill the LDS table (the
+// one K-mer of a tandem array seen 10^5 times is one slot; what fills it is
+// ~2000 different K-mers of one minimizer and hash digit) goes through a
+// global table, listed in `bad`.  The repeat-rich genome's 3.2 K overflowed
+// buckets (162 M instances) took 17.6 ms in the global table per pass.
+//   entry: w1 = the canonical K-mer; w0 = record position bits 0..23 | hash
+//   digit << 24 | position bits 24..33 << 32 | K-mer index in the record << 48
+__device__ __forceinline__ uint32_t ovf_digit(uint64_t c) {
+  return sk_fmix32((uint32_t)c ^ ((uint32_t)(c >> 32) * 0x85ebca6bu) ^ 0x5bd1e995u) >> 24;
+}
+__device__ __forceinline__ uint64_t ovf_w0(uint64_t rpos, uint32_t t, uint32_t dig) {
+  return (rpos & 0xffffffull) | ((uint64_t)dig << 24) | ((rpos >> 24) << 32) | ((uint64_t)t << 48);
+}
+__device__ __forceinline__ uint64_t ovf_pos(uint64_t w0) { return (w0 & 0xffffffull) | (((w0 >> 32) & 0xffffull) << 24); }
+__device__ __forceinline__ uint32_t ovf_t(uint64_t w0) { return (uint32_t)(w0 >> 48) & 63; }
+
+// the weak bit of one instance: ORed (several sub-buckets may write one
+// record's mask)
+__device__ __forceinline__ void sk_weak_or(const SkOut& o, uint64_t b, uint32_t t) {
+  if (o.wrec) {
+    if (!o.weak) {
+      atomicOr(&o.wrec[b], 1u << t);
+      return;
+    }
+    if (b - o.self_lo >= o.self_n) {
+      atomicOr(&o.wrec[b < o.self_lo ? b : b - o.self_n], 1u << t);
+      return;
+    }
+    b = o.self_send + (b - o.self_lo);
+  }
+  if (o.wpos) b = o.wpos[b];
+  b += t;
+  atomicOr(&o.weak[b >> 6], 1ull << (b & 63));
+}
+
+template <typename R>
+__global__ void k_ovf_nk(const R* __restrict__ rec, const uint64_t* __restrict__ boff, const uint32_t* __restrict__ ovf,
+                         const uint64_t* __restrict__ opre, uint32_t n_ovf, uint32_t* __restrict__ nk) {
+  const uint64_t tot = opre[n_ovf];
+  for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = k0 + threadIdx.x;
+    if (k < tot) nk[k] = rec_nk(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)]);
+  }
+}
+// each overflowed bucket's first entry: ipre at its first flattened record
+__global__ void k_ovf_starts(const uint64_t* __restrict__ opre, const uint64_t* __restrict__ ipre, uint32_t n_ovf,
+                             uint64_t* __restrict__ out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q <= n_ovf) out[q] = ipre[opre[q]];
+}
+template <typename R>
+__global__ void k_ovf_expand(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
+                             const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
+                             const uint64_t* __restrict__ ipre, SkP p, SK16* __restrict__ out) {
+  const uint64_t tot = opre[n_ovf];
+  for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = k0 + threadIdx.x;
+    if (k >= tot) continue;
+    const R r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)];
+    const SK16 h = rec_head(r, p);
+    const uint32_t n = rec_nk(r);
+    const uint64_t pos = RecPos<R>::value ? rec_pos(r, p) : 0;
+    const uint64_t at = ipre[k];
+    for (uint32_t t = 0; t < n; ++t) {
+      const uint64_t c = rec_kmer(h, t, p);
+      out[at + t] = SK16{ovf_w0(pos, t, ovf_digit(c)), c};
+    }
+  }
+}
+
+// the slot of a key the table holds (probe without claiming)
+template <uint32_t TS>
+__device__ __forceinline__ uint32_t lds_find(const unsigned long long* tk, uint64_t c, uint32_t g) {
+  for (uint32_t n = 0; n < TS; n += kSkGrp) {
+    const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(&tk[g]);
+    const ulonglong2 b = *reinterpret_cast<const ulonglong2*>(&tk[g + 2]);
+    if (a.x == c) return g;
+    if (a.y == c) return g + 1;
+    if (b.x == c) return g + 2;
+    if (b.y == c) return g + 3;
+    g = (g + kSkGrp) & (TS - 1);
+  }
+  return TS;
+}
+
+// One workgroup per sub-bucket (grid-stride over the n_sb = n_ovf x 256
+// children of the partition level, child[] their entry offsets).
+constexpr uint32_t kOvfTab = 2048;
+constexpr int kOvfThreads = 256;
+template <bool SOLID>
+__global__ void __launch_bounds__(kOvfThreads) k_ovf_count(const SK16* __restrict__ e, const uint64_t* __restrict__ child,
+                                                           uint64_t n_sb, SkP p, SkOut o, uint32_t* __restrict__ bad,
+                                                           unsigned long long* __restrict__ n_bad, bool force_bad) {
+  constexpr unsigned long long EMPTY = ~0ull;
+  constexpr int KB = __builtin_ctz(kOvfTab);
+  __shared__ __attribute__((aligned(16))) unsigned long long tk[kOvfTab];
+  __shared__ uint32_t tc[kOvfTab];
+  __shared__ uint16_t klist[kOvfTab];
+  __shared__ uint16_t slist[kOvfTab];
+  __shared__ uint32_t lhist[kSkHistBins];
+  __shared__ uint32_t nk_sh, ns_sh;
+  __shared__ int flag;
+  __shared__ unsigned long long sbase;
+  __shared__ SolidRes sres;
+  const uint32_t tid = threadIdx.x;
+  const bool want_hist = o.want_hist != 0;
+  for (uint32_t i = tid; i < kSkHistBins; i += kOvfThreads) lhist[i] = 0;
+  for (uint32_t s = tid; s < kOvfTab; s += kOvfThreads) {
+    tk[s] = EMPTY;
+    tc[s] = 0;
+  }
+  if (tid == 0) {
+    nk_sh = ns_sh = 0;
+    flag = 0;
+    sres = SolidRes{~0ull, 0};
+  }
+  __syncthreads();
+  unsigned long long nd = 0;
+  for (uint64_t sb = blockIdx.x; sb < n_sb; sb += gridDim.x) {  // block-uniform
+    const uint64_t a = child[sb], b = child[sb + 1];
+    if (a == b) continue;
+    // 1. count
+    for (uint64_t i0 = a; i0 < b; i0 += kOvfThreads) {
+      if (__builtin_amdgcn_readfirstlane(*(volatile int*)&flag)) break;
+      const uint64_t i = i0 + tid;
+      bool fresh = false;
+      uint32_t sl = kOvfTab;
+      if (i < b) {
+        const uint64_t c = e[i].w1;
+        sl = lds_claim<kOvfTab>(tk, c, sk_slot(c, KB), &fresh);
+        if (sl < kOvfTab)
+          atomicAdd(&tc[sl], 1u);
+        else
+          atomicOr(&flag, 1);
+      }
+      if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)sl;
+    }
+    __syncthreads();
+    const bool full = flag != 0 || force_bad;  // force_bad: tests of the global fallback
+    if (!full) {
+      // 2. the weak bits, instance by instance (the entries again: L2-hot)
+      if (SOLID && (o.weak || o.wrec)) {
+        for (uint64_t i = a + tid; i < b; i += kOvfThreads) {
+          const SK16 x = e[i];
+          const uint32_t sl = lds_find<kOvfTab>(tk, x.w1, sk_slot(x.w1, KB));
+          if (tc[sl] < o.min_solid) sk_weak_or(o, ovf_pos(x.w0), ovf_t(x.w0));
+        }
+      }
+      // 3. spectrum bins, solid K-mers
+      const uint32_t nK = nk_sh;
+      nd += tid == 0 ? nK : 0;
+      for (uint32_t j = tid; j < nK; j += kOvfThreads) {
+        const uint32_t cn = tc[klist[j]];
+        if (want_hist) sk_spectrum_add(cn, lhist, o);
+        if (SOLID && cn >= o.min_solid) slist[atomicAdd(&ns_sh, 1u)] = klist[j];
+      }
+      if (SOLID) {
+        __syncthreads();
+        const uint32_t ns = ns_sh;
+        if (tid == 0) sbase = solid_take(sres, ns, o);
+        __syncthreads();
+        const unsigned long long sbs = sbase;
+        for (uint32_t j = tid; j < ns; j += kOvfThreads)
+          if (sbs + j < o.solid_cap) o.solid[sbs + j] = khash(p.hp, tk[slist[j]]);
+      }
+    } else if (tid == 0) {
+      bad[atomicAdd(n_bad, 1ull)] = (uint32_t)sb;  // a global table counts it
+    }
+    // clear the claimed slots
+    __syncthreads();
+    const uint32_t nks = nk_sh;
+    for (uint32_t j = tid; j < nks; j += kOvfThreads) {
+      tk[klist[j]] = EMPTY;
+      tc[klist[j]] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      nk_sh = ns_sh = 0;
+      flag = 0;
+    }
+    __syncthreads();
+  }
+  const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
+  for (uint32_t i = tid; i < lim; i += kOvfThreads)
+    if (lhist[i]) atomicAdd(&o.ghist[i], (unsigned long long)lhist[i]);
+  wave_add(&o.gstats[0], nd);
+  if (SOLID && tid == 0) solid_close(sres, o);
+}
+
+// the sub-buckets the LDS table could not hold: their entries into a global
+// table (as k_sk_big_insert, one entry per instance), then their weak bits
+__global__ void k_ovf_big_insert(const SK16* __restrict__ e, const uint64_t* __restrict__ child,
+                                 const uint32_t* __restrict__ bad, uint32_t n_bad, SkP p, BigTab g) {
+  for (uint32_t q = blockIdx.x; q < n_bad; q += gridDim.x) {
+    const uint64_t a = child[bad[q]], b = child[bad[q] + 1];
+    for (uint64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+      const uint64_t c = e[i].w1;
+      sk_big_add(g, c, khash(p.hp, c) & g.mask, 1u);
+    }
+  }
+}
+__global__ void k_ovf_big_weak(const SK16* __restrict__ e, const uint64_t* __restrict__ child,
+                               const uint32_t* __restrict__ bad, uint32_t n_bad, SkP p, BigTab g, SkOut o) {
+  for (uint32_t q = blockIdx.x; q < n_bad; q += gridDim.x) {
+    const uint64_t a = child[bad[q]], b = child[bad[q] + 1];
+    for (uint64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+      const SK16 x = e[i];
+      uint64_t s = khash(p.hp, x.w1) & g.mask;
+      BigSlot y = g.s[s];
+      while (y.key != x.w1) {
+        s = (s + 1) & g.mask;
+        y = g.s[s];
+      }
+      if (y.cnt < o.min_solid) sk_weak_or(o, ovf_pos(x.w0), ovf_t(x.w0));
+    }
+  }
+}
+
 // The solid list dense again: chunk c's used[c] entries to offs[c].
 __global__ void k_solid_compact(const uint64_t* __restrict__ sparse, const uint32_t* __restrict__ used,
                                 const uint64_t* __restrict__ offs, uint64_t n_chunks, uint64_t* __restrict__ out) {
@@ -1701,6 +1928,89 @@ static int big_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const ui
   set_error("sk count: overflow table full at one slot per two instances (internal error)");
   return APG_E_STATE;
 }
+// The overflowed buckets by sub-bucket counting (k_ovf_*): entries out, one
+// partition level by hash digit within each bucket, an LDS count per
+// sub-bucket; the ones that fill the LDS table through a global table.
+template <typename RB>
+static int ovf_lds_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const uint32_t* ovf, const uint64_t* opre,
+                         uint32_t n_ovf, const SkP& p, uint64_t nbk, bool solid, const SkOut& o, uint32_t g2) {
+  uint64_t tot = 0;  // flattened records
+  APG_CHECK_HIP(hipMemcpyAsync(&tot, opre + n_ovf, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  uint32_t* nk = nullptr;
+  uint64_t *ipre = nullptr, *qs = nullptr, *child = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_ovf_nk", std::max<uint64_t>(tot, 1), &nk));
+  APG_TRY(workspace_t(ctx, "sk_ovf_ipre", tot + 1, &ipre));
+  APG_TRY(workspace_t(ctx, "sk_ovf_qs", (uint64_t)n_ovf + 1, &qs));
+  k_ovf_nk<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
+  APG_CHECK_HIP(hipGetLastError());
+  APG_TRY(scan_u32_u64(ctx, nk, tot, ipre, "skoi"));
+  k_ovf_starts<<<(n_ovf + 256) / 256, 256, 0, ctx->stream>>>(opre, ipre, n_ovf, qs);
+  std::vector<uint64_t> hq((size_t)n_ovf + 1);
+  APG_CHECK_HIP(hipMemcpyAsync(hq.data(), qs, ((size_t)n_ovf + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (hq[n_ovf] != nbk) {
+    set_error("sk count: overflowed buckets' instances disagree (internal error)");
+    return APG_E_STATE;
+  }
+  SK16 *e0 = nullptr, *e1 = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_ovf_e0", std::max<uint64_t>(nbk, 1), &e0));
+  APG_TRY(workspace_t(ctx, "sk_ovf_e1", std::max<uint64_t>(nbk, 1), &e1));
+  k_ovf_expand<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, ipre, p, e0);
+  APG_CHECK_HIP(hipGetLastError());
+  std::vector<std::vector<Seg>> parents(n_ovf);
+  for (uint32_t q = 0; q < n_ovf; ++q) parents[q].push_back(Seg{hq[q], hq[q + 1] - hq[q]});
+  constexpr int kOvfBits = 8;
+  const uint64_t n_sb = (uint64_t)n_ovf << kOvfBits;
+  APG_TRY(workspace_t(ctx, "sk_ovf_child", n_sb + 1, &child));
+  APG_TRY(part_level<SK16>(ctx, e0, e1, parents, 64 - kOvfBits, kOvfBits, nbk, child, nullptr, "ovf"));
+  uint32_t* bad = nullptr;
+  unsigned long long* nbad = nullptr;
+  APG_TRY(workspace_t(ctx, "sk_ovf_bad", n_sb, &bad));
+  APG_TRY(workspace_t(ctx, "sk_ovf_nbad", 1, &nbad));
+  APG_CHECK_HIP(hipMemsetAsync(nbad, 0, 8, ctx->stream));
+  const uint64_t grid = solid ? resident_grid(ctx, k_ovf_count<true>, kOvfThreads, n_sb)
+                              : resident_grid(ctx, k_ovf_count<false>, kOvfThreads, n_sb);
+  // APG_SK_OVF=bad (tests): every sub-bucket through the global fallback
+  const bool force_bad = getenv("APG_SK_OVF") && !strcmp(getenv("APG_SK_OVF"), "bad");
+  if (solid)
+    k_ovf_count<true><<<grid, kOvfThreads, 0, ctx->stream>>>(e1, child, n_sb, p, o, bad, nbad, force_bad);
+  else
+    k_ovf_count<false><<<grid, kOvfThreads, 0, ctx->stream>>>(e1, child, n_sb, p, o, bad, nbad, force_bad);
+  APG_CHECK_HIP(hipGetLastError());
+  unsigned long long hb = 0;
+  APG_CHECK_HIP(hipMemcpyAsync(&hb, nbad, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (hb) {  // sub-buckets past the LDS table: a global table over their entries
+    std::vector<uint32_t> hbad(hb);
+    std::vector<uint64_t> hc(n_sb + 1);
+    APG_CHECK_HIP(hipMemcpyAsync(hbad.data(), bad, hb * 4, hipMemcpyDeviceToHost, ctx->stream));
+    APG_CHECK_HIP(hipMemcpyAsync(hc.data(), child, (n_sb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    uint64_t inst = 0;
+    for (uint32_t sb : hbad) inst += hc[sb + 1] - hc[sb];
+    uint64_t T = 1024;
+    while (T < 2 * inst) T <<= 1;  // more slots than instances: a claim always ends
+    BigSlot* gs = nullptr;
+    unsigned long long* full = nullptr;
+    APG_TRY(workspace_t(ctx, "sk_gtab", T, &gs));
+    APG_TRY(workspace_t(ctx, "sk_gfull", 2, &full));
+    k_big_init<<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gs, T);
+    const BigTab g{gs, T - 1, full, ~0u};
+    const uint32_t gb = (uint32_t)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8);
+    k_ovf_big_insert<<<gb, 256, 0, ctx->stream>>>(e1, child, bad, (uint32_t)hb, p, g);
+    if (solid)
+      k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gs, T, p, o);
+    else
+      k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(gs, T, p, o);
+    if (solid && (o.weak || o.wrec)) k_ovf_big_weak<<<gb, 256, 0, ctx->stream>>>(e1, child, bad, (uint32_t)hb, p, g, o);
+    APG_CHECK_HIP(hipGetLastError());
+    vlog(ctx, "sk count: %llu of %llu overflow sub-buckets (%llu instances) past the LDS table -> global table",
+         hb, (unsigned long long)n_sb, (unsigned long long)inst);
+  }
+  return APG_OK;
+}
+
 static int sk_ceil_log2(uint64_t x) {
   int b = 0;
   while ((1ull << b) < x) ++b;
@@ -2254,17 +2564,28 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
         APG_TRY(sync(ctx));
         vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
-        kbegin(ctx, "sk_bucket_global", nbk * 64);
-        BigTab g{};
-        uint64_t T = 0;
-        APG_TRY((big_count<RB, false>(ctx, cur, boff, ovf, opre, n_ovf, p, nbk, g2, nullptr, &g, &T)));
-        if (solid)
-          k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
-        else
-          k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
-        if constexpr (RecPos<RB>::value) {
-          if (o.weak || o.wrec)
-            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o);
+        // APG_SK_OVF=global: every overflowed K-mer through one global table
+        // (the round-4 path); default: sub-bucket counting in LDS
+        const char* oe = getenv("APG_SK_OVF");
+        const bool ovf_global = oe && !strcmp(oe, "global");
+        if (!ovf_global) {
+          // entries written once, moved by one level (count read + move), read
+          // by the count and the weak pass
+          kbegin(ctx, "sk_bucket_global", nbk * 16 * 6);
+          APG_TRY(ovf_lds_count<RB>(ctx, cur, boff, ovf, opre, n_ovf, p, nbk, solid, o, g2));
+        } else {
+          kbegin(ctx, "sk_bucket_global", nbk * 64);
+          BigTab g{};
+          uint64_t T = 0;
+          APG_TRY((big_count<RB, false>(ctx, cur, boff, ovf, opre, n_ovf, p, nbk, g2, nullptr, &g, &T)));
+          if (solid)
+            k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
+          else
+            k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
+          if constexpr (RecPos<RB>::value) {
+            if (o.weak || o.wrec)
+              k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o);
+          }
         }
         kend(ctx);
         APG_CHECK_HIP(hipGetLastError());

@@ -52,11 +52,13 @@ def test_unipaths_on_repeats(gpu_ctx, rep_reads):
 
 @pytest.mark.parametrize("probe", ["1", "4"])
 def test_overflow_table_retry_unbounded(rep_reads, monkeypatch, probe):
-    """the overflowed buckets' global table gives up after
-    APG_SK_BIG_PROBE probes on its first, small attempt; the full-size retry
-    probes without a limit, so a crowded first attempt on tandem-repeat keys
-    still ends in the oracle's spectrum, solid set and corrections."""
+    """the overflowed buckets' global table (APG_SK_OVF=
+    global; the fused K+1 pass always) gives up after APG_SK_BIG_PROBE probes
+    on its first, small attempt; the full-size retry probes without a limit,
+    so a crowded first attempt on tandem-repeat keys still ends in the
+    oracle's spectrum, solid set and corrections."""
     monkeypatch.setenv("APG_SK_BIG_PROBE", probe)
+    monkeypatch.setenv("APG_SK_OVF", "global")
     _, reads = rep_reads
     with Context(device=0, verbose=True) as ctx:
         for K in (24, 25):
@@ -68,3 +70,36 @@ def test_overflow_table_retry_unbounded(rep_reads, monkeypatch, probe):
     assert np.array_equal(got.packed[: int(got.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
     assert np.array_equal(got.quals, exp.quals)
     assert pst["n_solid"] == est["n_solid"]
+
+
+@pytest.mark.parametrize("mode", ["lds", "bad"])
+def test_overflow_sub_buckets(rep_reads, monkeypatch, mode):
+    """Overflowed buckets counted by sub-bucket (the default): their K-mer
+    instances as entries, one partition level by hash digit inside each
+    bucket, an LDS count per sub-bucket and the weak bits from a second read
+    of its entries; "bad" sends every sub-bucket through the global-table
+    fallback of the ones that fill the LDS table.  Spectrum (K=24, 25, every
+    dedup mode's overflow), solid set, corrections and the fused entry point
+    equal the oracle."""
+    if mode == "bad":
+        monkeypatch.setenv("APG_SK_OVF", "bad")
+    else:
+        monkeypatch.delenv("APG_SK_OVF", raising=False)
+    _, reads = rep_reads
+    with Context(device=0) as ctx:
+        for K in (24, 25):
+            hist, st = ctx.kmer_spectrum(reads, K)
+            assert np.array_equal(hist, oracle.kmer_spectrum(reads, K)), K
+            assert st["n_overflow"] > 0
+        got, pst = ctx.precorrect(reads, K=24)
+        d = ctx.upload(reads)
+        fh, fks, fps = ctx.spectrum_precorrect(d, K_spec=25, K=24)
+        fixed = ctx.download(d, with_quals=True)
+        d.free()
+    exp, est = oracle.precorrect(reads, K=24)
+    for g in (got, fixed):
+        assert np.array_equal(g.packed[: int(g.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
+        assert np.array_equal(g.quals, exp.quals)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+        assert pst[k] == est[k] and fps[k] == est[k], k
+    assert np.array_equal(fh, oracle.kmer_spectrum(reads, 25))
