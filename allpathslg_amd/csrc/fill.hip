@@ -346,7 +346,12 @@ constexpr int kFillXpct = 75;
 // (wave-aggregated fetch from *next), so a wave is no longer held by its
 // slowest pair.  Per lane the lookups, their order and the result are the
 // same as the nested search (oracle/fill_oracle.c).
-template <int KS>
+// LEAN (the default): the knobs at their defaults, folded at compile time —
+// one pass (cap = max_steps), the branch cache and the bridge filter on,
+// kFillRefill, kFillXsteps free steps at kFillXpct % — which frees the
+// scalar registers the runtime knobs held (the general form spills SGPRs to
+// VGPR lanes); any APG_FILL_* A/B knob set selects the general form.
+template <int KS, bool LEAN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
                                               uint32_t* __restrict__ ones, uint8_t* __restrict__ status_out,
@@ -355,7 +360,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                                               const unsigned long long* __restrict__ list_n,
                                               uint32_t* __restrict__ defer, unsigned long long* __restrict__ ndefer,
                                               unsigned long long* __restrict__ next, bool bcache, bool bfilt,
-                                              int refill, int xsteps) {
+                                              int refill_, int xsteps_) {
+  if constexpr (LEAN) {
+    cap = p.max_steps;
+    list = nullptr;
+    list_n = nullptr;
+    defer = nullptr;
+    ndefer = nullptr;
+    bcache = true;
+    bfilt = true;
+  }
+  const int refill = LEAN ? kFillRefill : refill_;
+  const int xsteps = LEAN ? (kFillXsteps | (kFillXpct << 16)) : xsteps_;
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
   uint32_t nlook = 0;
   const int K = p.K, n1 = t.n1;
@@ -426,7 +442,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   };
   // closures counted (overlap phase and walk done): status out, or defer
   auto conclude = [&]() {
-    if (budget && n_clos < 2 && cap < p.max_steps) {  // pass 1: search again with the full budget
+    if (!LEAN && budget && n_clos < 2 && cap < p.max_steps) {  // pass 1: search again with the full budget
       defer[atomicAdd(ndefer, 1ull)] = (uint32_t)i;
       return;
     }
@@ -884,8 +900,8 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
     // lanes are persistent (work fetched per wave): one resident round of blocks
     const bool two = et.ks == 16;
-    const uint32_t grid = two ? resident_grid(ctx, k_fill<16>, 256, (np + 255) / 256)
-                              : resident_grid(ctx, k_fill<8>, 256, (np + 255) / 256);
+    const uint32_t grid = two ? resident_grid(ctx, k_fill<16, true>, 256, (np + 255) / 256)
+                              : resident_grid(ctx, k_fill<8, true>, 256, (np + 255) / 256);
     // APG_FILL_BRANCH_CACHE=0: backtracks look their branch point up again (A/B)
     const char* be = getenv("APG_FILL_BRANCH_CACHE");
     const bool bcache = !(be && !strcmp(be, "0"));
@@ -911,10 +927,18 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
         kern<<<grid, 256, 0, ctx->stream>>>(rv, fp, et, rec, lens, nby, ones, d_status, clean, fc, p.max_steps,
                                             defer, ndefer, nullptr, nullptr, ndefer + 2, bcache, bfilt, refill, xsteps);
     };
-    if (two)
-      fill(k_fill<16>);
+    // the general form when any A/B knob is set (APG_FILL_LEAN=0 forces it)
+    const char* le = getenv("APG_FILL_LEAN");
+    const bool lean = !(le && !strcmp(le, "0")) && bcache && bfilt && refill == kFillRefill &&
+                      xsteps == (kFillXsteps | (kFillXpct << 16)) && cap1 >= p.max_steps;
+    if (two && lean)
+      fill(k_fill<16, true>);
+    else if (two)
+      fill(k_fill<16, false>);
+    else if (lean)
+      fill(k_fill<8, true>);
     else
-      fill(k_fill<8>);
+      fill(k_fill<8, false>);
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());

@@ -1308,18 +1308,19 @@ using UskTile = SkTile<kUskThreads, 6144>;  // 128 fragments of <= ~180 bases
 
 // dynamic LDS of the walk kernels: the van Herk column of each thread, then
 // the per-digit counters
-__host__ __device__ inline uint32_t usk_column_words(int w) {
-  return (uint32_t)(w > kUskWalk2MinW ? sk_walk2_words(w) : w) * kUskThreads;
-}
-static size_t usk_walk_lds(int w, int D, size_t per_digit) {
-  return (size_t)usk_column_words(w) * 4 + ((size_t)1 << D) * per_digit;
-}
-
 struct UskP {
   using U = uint64_t;  // m <= 31
   int K, m, w, maxnk;
   uint64_t mmask;
+  int two;  // the two-level column (w > kUskWalk2MinW; APG_USK_FLAT=1: single-level for every w)
 };
+
+__host__ __device__ inline uint32_t usk_column_words(const UskP& p) {
+  return (uint32_t)(p.two ? sk_walk2_words(p.w) : p.w) * kUskThreads;
+}
+static size_t usk_walk_lds(const UskP& p, int D, size_t per_digit) {
+  return (size_t)usk_column_words(p) * 4 + ((size_t)1 << D) * per_digit;
+}
 
 static UskP make_uskp(int K) {
   UskP p;
@@ -1328,6 +1329,11 @@ static UskP make_uskp(int K) {
   p.w = K - p.m + 1;
   p.maxnk = std::min(kUskBases - K - 1, kUskMaxNk);
   p.mmask = (1ull << (2 * p.m)) - 1;
+  static const bool flat = [] {
+    const char* e = getenv("APG_USK_FLAT");
+    return e && !strcmp(e, "1");
+  }();
+  p.two = !flat && p.w > kUskWalk2MinW;
   return p;
 }
 
@@ -1352,7 +1358,7 @@ __device__ __forceinline__ SK48 make_urec(const uint8_t* rd, uint32_t L, uint32_
 template <bool LIST, int CAP, typename F, typename TD>
 __device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p, uint64_t r0, uint64_t r1, UskTile& T,
                                                uint32_t* sb, SkList<CAP>& lst, F f, TD tile_done) {
-  const bool two = p.w > kUskWalk2MinW;
+  const bool two = p.two;
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n) {
@@ -1379,7 +1385,7 @@ __global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, i
   __shared__ uint32_t dpos, dovf;
   extern __shared__ uint32_t usk_sb[];  // the walk columns, then hist[ndig], khist[ndig]
   const uint32_t ndig = 1u << D;
-  uint32_t* hist = usk_sb + usk_column_words(p.w);
+  uint32_t* hist = usk_sb + usk_column_words(p);
   uint32_t* khist = hist + ndig;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
@@ -1408,7 +1414,7 @@ __global__ void __launch_bounds__(kUskThreads) k_usk_scatter(SkReads rv, UskP p,
   __shared__ SkList<kUskListCap> lst;
   extern __shared__ uint32_t usk_sb[];  // the walk columns, then cur[ndig]
   const uint32_t ndig = 1u << D;
-  unsigned long long* cur = reinterpret_cast<unsigned long long*>(usk_sb + usk_column_words(p.w));
+  unsigned long long* cur = reinterpret_cast<unsigned long long*>(usk_sb + usk_column_words(p));
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t d = threadIdx.x; d < ndig; d += blockDim.x) cur[d] = omat[(uint64_t)d * G + b];
   if (threadIdx.x == 0) lst.cnt = 0;
@@ -2314,7 +2320,7 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
 // Walk grid cap: two full rounds of resident k_usk_scatter blocks (see sk_blocks).
 static uint64_t usk_grid_cap(const apg_ctx* ctx, const UskP& p, int D) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_usk_scatter, kUskThreads, usk_walk_lds(p.w, D, 8)) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_usk_scatter, kUskThreads, usk_walk_lds(p, D, 8)) !=
           hipSuccess ||
       occ < 1)
     occ = 4;
@@ -2347,7 +2353,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   const uint32_t G =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(usk_grid_cap(ctx, p, D), (dr->n_reads + kUskThreads - 1) / kUskThreads));
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  const size_t sb_bytes = usk_walk_lds(p.w, D, 8);  // + hist, khist (count) or cursors (scatter)
+  const size_t sb_bytes = usk_walk_lds(p, D, 8);  // + hist, khist (count) or cursors (scatter)
   uint32_t* cmat = nullptr;
   uint64_t *omat = nullptr, *ds = nullptr;
   unsigned long long* kdig = nullptr;
@@ -2386,7 +2392,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
 static int usk_scatter(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, uint32_t G, SK48* out) {
   const int D = ceil_log2_u((uint64_t)P) + kUskDigitBits;
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  const size_t sb_bytes = usk_walk_lds(p.w, D, 8);  // + hist, khist (count) or cursors (scatter)
+  const size_t sb_bytes = usk_walk_lds(p, D, 8);  // + hist, khist (count) or cursors (scatter)
   uint64_t* omat = nullptr;
   APG_TRY(workspace_t(ctx, "usk_omat", (uint64_t)(1u << D) * G + 1, &omat));
   const auto& us = ctx->urstate;

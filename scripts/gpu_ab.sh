@@ -7,14 +7,14 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 BA="${BA_OVERRIDE:---steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps 0}"
 if [ -n "${PYTEST_SEL:-}" ]; then
-  timeout -k 10 ${T_TEST:-400} python -u -m pytest ${PYTEST_SEL} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
+  env ${PYTEST_ENV:-} timeout -k 10 ${T_TEST:-400} python -u -m pytest ${PYTEST_SEL} -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
   tail -2 gpurun_out/ab_pytest.log
 fi
 for V in ${VARIANTS:-A B}; do
   ENVV="${!V}"
-  env $ENVV timeout -k 10 ${T_BENCH:-400} python bench.py $BA > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
+  env $ENVV timeout -k 10 ${T_BENCH:-400} python bench.py $BA --detail-json gpurun_out/ab_$V.detail.json > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; exit 1; }
   echo "== $V ($ENVV)"
-  python - gpurun_out/ab_$V.json <<'PY'
+  python - gpurun_out/ab_$V.detail.json <<'PY'
 import json, sys
 b = json.load(open(sys.argv[1]))
 print("value", round(b["value"] / 1e6, 2), "M reads/s  ms/step", round(b["ms_per_step"], 1), "checks", all(b["checks"].values()))
