@@ -1686,13 +1686,31 @@ __device__ __forceinline__ void sk_weak_or(const SkOut& o, uint64_t b, uint32_t 
   atomicOr(&o.weak[b >> 6], 1ull << (b & 63));
 }
 
-template <typename R>
+// UP (the K+1 pass; p = the K+1 parameters): a record's owned K+1-mers
+// (rec_kmer_up over its n + 1 slots) instead of its K-mers.
+template <typename R, bool UP>
+__device__ __forceinline__ uint32_t ovf_rec_n(const R& x, const SkP& p) {
+  if constexpr (!UP) {
+    return rec_nk(x);
+  } else {
+    const SK16 r = rec_head(x, p);
+    const uint32_t n = ((uint32_t)(r.w0 >> 32) & 0xff) + 1u;
+    uint32_t c = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+      bool own;
+      rec_kmer_up(r, (int)t - 1, p, &own);
+      c += own;
+    }
+    return c;
+  }
+}
+template <typename R, bool UP>
 __global__ void k_ovf_nk(const R* __restrict__ rec, const uint64_t* __restrict__ boff, const uint32_t* __restrict__ ovf,
-                         const uint64_t* __restrict__ opre, uint32_t n_ovf, uint32_t* __restrict__ nk) {
+                         const uint64_t* __restrict__ opre, uint32_t n_ovf, SkP p, uint32_t* __restrict__ nk) {
   const uint64_t tot = opre[n_ovf];
   for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < tot; k0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = k0 + threadIdx.x;
-    if (k < tot) nk[k] = rec_nk(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)]);
+    if (k < tot) nk[k] = ovf_rec_n<R, UP>(rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)], p);
   }
 }
 // each overflowed bucket's first entry: ipre at its first flattened record
@@ -1701,7 +1719,7 @@ __global__ void k_ovf_starts(const uint64_t* __restrict__ opre, const uint64_t* 
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q <= n_ovf) out[q] = ipre[opre[q]];
 }
-template <typename R>
+template <typename R, bool UP>
 __global__ void k_ovf_expand(const R* __restrict__ rec, const uint64_t* __restrict__ boff,
                              const uint32_t* __restrict__ ovf, const uint64_t* __restrict__ opre, uint32_t n_ovf,
                              const uint64_t* __restrict__ ipre, SkP p, SK16* __restrict__ out) {
@@ -1711,12 +1729,22 @@ __global__ void k_ovf_expand(const R* __restrict__ rec, const uint64_t* __restri
     if (k >= tot) continue;
     const R r = rec[sk_ovf_record(boff, ovf, opre, n_ovf, k0, k)];
     const SK16 h = rec_head(r, p);
-    const uint32_t n = rec_nk(r);
-    const uint64_t pos = RecPos<R>::value ? rec_pos(r, p) : 0;
     const uint64_t at = ipre[k];
-    for (uint32_t t = 0; t < n; ++t) {
-      const uint64_t c = rec_kmer(h, t, p);
-      out[at + t] = SK16{ovf_w0(pos, t, ovf_digit(c)), c};
+    if constexpr (UP) {  // owned K+1-mers only; no weak bits, so no position
+      const uint32_t n = ((uint32_t)(h.w0 >> 32) & 0xff) + 1u;
+      uint32_t j = 0;
+      for (uint32_t t = 0; t < n; ++t) {
+        bool own;
+        const uint64_t c = rec_kmer_up(h, (int)t - 1, p, &own);
+        if (own) out[at + j++] = SK16{ovf_w0(0, 0, ovf_digit(c)), c};
+      }
+    } else {
+      const uint32_t n = rec_nk(r);
+      const uint64_t pos = RecPos<R>::value ? rec_pos(r, p) : 0;
+      for (uint32_t t = 0; t < n; ++t) {
+        const uint64_t c = rec_kmer(h, t, p);
+        out[at + t] = SK16{ovf_w0(pos, t, ovf_digit(c)), c};
+      }
     }
   }
 }
@@ -1737,7 +1765,12 @@ __device__ __forceinline__ uint32_t lds_find(const unsigned long long* tk, uint6
 }
 
 // One workgroup per sub-bucket (grid-stride over the n_sb = n_ovf x 256
-// children of the partition level, child[] their entry offsets).
+// children of the partition level, child[] their entry offsets).  A
+// sub-bucket holds ~200 entries, so its chain of dependent global loads
+// (bounds, entries, the entries again for the weak bits) was what the
+// kernel waited on: the next sub-bucket's bounds and first entries are
+// loaded while the current one counts, and a thread keeps its first-chunk
+// entry in registers for the weak pass.
 constexpr uint32_t kOvfTab = 2048;
 constexpr int kOvfThreads = 256;
 template <bool SOLID>
@@ -1757,6 +1790,7 @@ __global__ void __launch_bounds__(kOvfThreads) k_ovf_count(const SK16* __restric
   __shared__ SolidRes sres;
   const uint32_t tid = threadIdx.x;
   const bool want_hist = o.want_hist != 0;
+  const bool want_weak = SOLID && (o.weak || o.wrec);
   for (uint32_t i = tid; i < kSkHistBins; i += kOvfThreads) lhist[i] = 0;
   for (uint32_t s = tid; s < kOvfTab; s += kOvfThreads) {
     tk[s] = EMPTY;
@@ -1767,71 +1801,94 @@ __global__ void __launch_bounds__(kOvfThreads) k_ovf_count(const SK16* __restric
     flag = 0;
     sres = SolidRes{~0ull, 0};
   }
-  __syncthreads();
   unsigned long long nd = 0;
-  for (uint64_t sb = blockIdx.x; sb < n_sb; sb += gridDim.x) {  // block-uniform
-    const uint64_t a = child[sb], b = child[sb + 1];
-    if (a == b) continue;
-    // 1. count
-    for (uint64_t i0 = a; i0 < b; i0 += kOvfThreads) {
-      if (__builtin_amdgcn_readfirstlane(*(volatile int*)&flag)) break;
-      const uint64_t i = i0 + tid;
-      bool fresh = false;
-      uint32_t sl = kOvfTab;
-      if (i < b) {
-        const uint64_t c = e[i].w1;
-        sl = lds_claim<kOvfTab>(tk, c, sk_slot(c, KB), &fresh);
-        if (sl < kOvfTab)
-          atomicAdd(&tc[sl], 1u);
-        else
-          atomicOr(&flag, 1);
-      }
-      if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)sl;
+  uint64_t sb = blockIdx.x, a = 0, b = 0;
+  if (sb < n_sb) {
+    a = child[sb];
+    b = child[sb + 1];
+  }
+  SK16 x0{0, EMPTY};  // this thread's entry of the sub-bucket's first chunk
+  if (a + tid < b) x0 = e[a + tid];
+  __syncthreads();
+  while (sb < n_sb) {  // block-uniform
+    const uint64_t nsb = sb + gridDim.x;
+    uint64_t na = 0, nb = 0;
+    if (nsb < n_sb) {  // in flight while this sub-bucket counts
+      na = child[nsb];
+      nb = child[nsb + 1];
     }
-    __syncthreads();
-    const bool full = flag != 0 || force_bad;  // force_bad: tests of the global fallback
-    if (!full) {
-      // 2. the weak bits, instance by instance (the entries again: L2-hot)
-      if (SOLID && (o.weak || o.wrec)) {
+    const bool any = a != b;
+    bool full = false;
+    if (any) {
+      // 1. count
+      for (uint64_t i0 = a; i0 < b; i0 += kOvfThreads) {
+        if (__builtin_amdgcn_readfirstlane(*(volatile int*)&flag)) break;
+        const uint64_t i = i0 + tid;
+        bool fresh = false;
+        uint32_t sl = kOvfTab;
+        if (i < b) {
+          const uint64_t c = i0 == a ? x0.w1 : e[i].w1;
+          sl = lds_claim<kOvfTab>(tk, c, sk_slot(c, KB), &fresh);
+          if (sl < kOvfTab)
+            atomicAdd(&tc[sl], 1u);
+          else
+            atomicOr(&flag, 1);
+        }
+        if (fresh) klist[atomicAdd(&nk_sh, 1u)] = (uint16_t)sl;
+      }
+      __syncthreads();
+      full = flag != 0 || force_bad;  // force_bad: tests of the global fallback
+      // 2. the weak bits, instance by instance (the first chunk from registers)
+      if (!full && want_weak) {
         for (uint64_t i = a + tid; i < b; i += kOvfThreads) {
-          const SK16 x = e[i];
+          const SK16 x = i < a + kOvfThreads ? x0 : e[i];
           const uint32_t sl = lds_find<kOvfTab>(tk, x.w1, sk_slot(x.w1, KB));
           if (tc[sl] < o.min_solid) sk_weak_or(o, ovf_pos(x.w0), ovf_t(x.w0));
         }
       }
-      // 3. spectrum bins, solid K-mers
-      const uint32_t nK = nk_sh;
-      nd += tid == 0 ? nK : 0;
-      for (uint32_t j = tid; j < nK; j += kOvfThreads) {
-        const uint32_t cn = tc[klist[j]];
-        if (want_hist) sk_spectrum_add(cn, lhist, o);
-        if (SOLID && cn >= o.min_solid) slist[atomicAdd(&ns_sh, 1u)] = klist[j];
+    }
+    // the next sub-bucket's first chunk: in flight during the emission
+    x0 = SK16{0, EMPTY};
+    if (na + tid < nb) x0 = e[na + tid];
+    if (any) {
+      if (!full) {
+        // 3. spectrum bins, solid K-mers
+        const uint32_t nK = nk_sh;
+        nd += tid == 0 ? nK : 0;
+        for (uint32_t j = tid; j < nK; j += kOvfThreads) {
+          const uint32_t cn = tc[klist[j]];
+          if (want_hist) sk_spectrum_add(cn, lhist, o);
+          if (SOLID && cn >= o.min_solid) slist[atomicAdd(&ns_sh, 1u)] = klist[j];
+        }
+        if (SOLID) {
+          __syncthreads();
+          const uint32_t ns = ns_sh;
+          if (tid == 0) sbase = solid_take(sres, ns, o);
+          __syncthreads();
+          const unsigned long long sbs = sbase;
+          for (uint32_t j = tid; j < ns; j += kOvfThreads)
+            if (sbs + j < o.solid_cap) o.solid[sbs + j] = khash(p.hp, tk[slist[j]]);
+        }
+      } else if (tid == 0) {
+        bad[atomicAdd(n_bad, 1ull)] = (uint32_t)sb;  // a global table counts it
       }
-      if (SOLID) {
-        __syncthreads();
-        const uint32_t ns = ns_sh;
-        if (tid == 0) sbase = solid_take(sres, ns, o);
-        __syncthreads();
-        const unsigned long long sbs = sbase;
-        for (uint32_t j = tid; j < ns; j += kOvfThreads)
-          if (sbs + j < o.solid_cap) o.solid[sbs + j] = khash(p.hp, tk[slist[j]]);
+      // clear the claimed slots
+      __syncthreads();
+      const uint32_t nks = nk_sh;
+      for (uint32_t j = tid; j < nks; j += kOvfThreads) {
+        tk[klist[j]] = EMPTY;
+        tc[klist[j]] = 0;
       }
-    } else if (tid == 0) {
-      bad[atomicAdd(n_bad, 1ull)] = (uint32_t)sb;  // a global table counts it
+      __syncthreads();
+      if (tid == 0) {
+        nk_sh = ns_sh = 0;
+        flag = 0;
+      }
+      __syncthreads();
     }
-    // clear the claimed slots
-    __syncthreads();
-    const uint32_t nks = nk_sh;
-    for (uint32_t j = tid; j < nks; j += kOvfThreads) {
-      tk[klist[j]] = EMPTY;
-      tc[klist[j]] = 0;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      nk_sh = ns_sh = 0;
-      flag = 0;
-    }
-    __syncthreads();
+    sb = nsb;
+    a = na;
+    b = nb;
   }
   const uint64_t lim = o.hist_len < (uint64_t)kSkHistBins ? o.hist_len : (uint64_t)kSkHistBins;
   for (uint32_t i = tid; i < lim; i += kOvfThreads)
@@ -1931,9 +1988,12 @@ static int big_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const ui
 // The overflowed buckets by sub-bucket counting (k_ovf_*): entries out, one
 // partition level by hash digit within each bucket, an LDS count per
 // sub-bucket; the ones that fill the LDS table through a global table.
-template <typename RB>
+// UP: the K+1 pass's overflowed buckets (owned K+1-mers; nbk an upper bound
+// of them); *n_inst (may be null) receives the instances counted.
+template <typename RB, bool UP = false>
 static int ovf_lds_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const uint32_t* ovf, const uint64_t* opre,
-                         uint32_t n_ovf, const SkP& p, uint64_t nbk, bool solid, const SkOut& o, uint32_t g2) {
+                         uint32_t n_ovf, const SkP& p, uint64_t nbk, bool solid, const SkOut& o, uint32_t g2,
+                         uint64_t* n_inst = nullptr) {
   uint64_t tot = 0;  // flattened records
   APG_CHECK_HIP(hipMemcpyAsync(&tot, opre + n_ovf, 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
@@ -1942,21 +2002,23 @@ static int ovf_lds_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, cons
   APG_TRY(workspace_t(ctx, "sk_ovf_nk", std::max<uint64_t>(tot, 1), &nk));
   APG_TRY(workspace_t(ctx, "sk_ovf_ipre", tot + 1, &ipre));
   APG_TRY(workspace_t(ctx, "sk_ovf_qs", (uint64_t)n_ovf + 1, &qs));
-  k_ovf_nk<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
+  k_ovf_nk<RB, UP><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, nk);
   APG_CHECK_HIP(hipGetLastError());
   APG_TRY(scan_u32_u64(ctx, nk, tot, ipre, "skoi"));
   k_ovf_starts<<<(n_ovf + 256) / 256, 256, 0, ctx->stream>>>(opre, ipre, n_ovf, qs);
   std::vector<uint64_t> hq((size_t)n_ovf + 1);
   APG_CHECK_HIP(hipMemcpyAsync(hq.data(), qs, ((size_t)n_ovf + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  if (hq[n_ovf] != nbk) {
+  if (UP ? hq[n_ovf] > nbk : hq[n_ovf] != nbk) {
     set_error("sk count: overflowed buckets' instances disagree (internal error)");
     return APG_E_STATE;
   }
+  nbk = hq[n_ovf];
+  if (n_inst) *n_inst = nbk;
   SK16 *e0 = nullptr, *e1 = nullptr;
   APG_TRY(workspace_t(ctx, "sk_ovf_e0", std::max<uint64_t>(nbk, 1), &e0));
   APG_TRY(workspace_t(ctx, "sk_ovf_e1", std::max<uint64_t>(nbk, 1), &e1));
-  k_ovf_expand<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, ipre, p, e0);
+  k_ovf_expand<RB, UP><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, ipre, p, e0);
   APG_CHECK_HIP(hipGetLastError());
   std::vector<std::vector<Seg>> parents(n_ovf);
   for (uint32_t q = 0; q < n_ovf; ++q) parents[q].push_back(Seg{hq[q], hq[q + 1] - hq[q]});
@@ -2220,9 +2282,10 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
   SkP p = make_skp(K1);
   p.wide = wide;
   unsigned long long hs[5];
+  uint64_t up_inst = 0;  // owned K+1-mer instances the sub-bucket pass counted
   APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
   APG_TRY(sync(ctx));
-  if (hs[1]) {  // overflowed buckets: their own records into one global table, as in sk_stage_count_t
+  if (hs[1]) {  // overflowed buckets: by sub-bucket, as in sk_stage_count_t
     unsigned long long* nk = u.gstats + 3;
     APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
     const uint32_t n_ovf = (uint32_t)hs[1];
@@ -2237,12 +2300,20 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
     unsigned long long nbk = 0;
     APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
     APG_TRY(sync(ctx));
-    vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> global table", hs[1]);
-    kbegin(ctx, "sk_bucket_global", nbk * 64);
-    BigTab g{};
-    uint64_t T = 0;
-    APG_TRY((big_count<RB, true>(ctx, cur, boff, u.ovf_list, opre, n_ovf, p, nbk, g2, u.inst, &g, &T)));
-    k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, u);
+    // APG_SK_OVF=global: the owned K+1-mers through one global table
+    const char* oe = getenv("APG_SK_OVF");
+    if (!(oe && !strcmp(oe, "global"))) {
+      vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> sub-buckets", hs[1]);
+      kbegin(ctx, "sk_bucket_global", nbk * 16 * 5);
+      APG_TRY((ovf_lds_count<RB, true>(ctx, cur, boff, u.ovf_list, opre, n_ovf, p, nbk, false, u, g2, &up_inst)));
+    } else {
+      vlog(ctx, "sk count (K+1 of K records): %llu buckets overflow the LDS table -> global table", hs[1]);
+      kbegin(ctx, "sk_bucket_global", nbk * 64);
+      BigTab g{};
+      uint64_t T = 0;
+      APG_TRY((big_count<RB, true>(ctx, cur, boff, u.ovf_list, opre, n_ovf, p, nbk, g2, u.inst, &g, &T)));
+      k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, u);
+    }
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
@@ -2257,10 +2328,10 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
   res->n_distinct = hs[0];
   res->n_overflow_buckets = hs[1];
   res->nbuckets = nb;
-  res->n_kmers = ninst;
+  res->n_kmers = ninst + up_inst;
   res->n_records = n_rec;
   vlog(ctx, "sk count K=%d from K=%d records%s: kmers=%llu distinct=%llu ovf=%llu", K1, K1 - 1,
-       folded ? " (distinct records x multiplicity)" : "", ninst, hs[0], hs[1]);
+       folded ? " (distinct records x multiplicity)" : "", (unsigned long long)res->n_kmers, hs[0], hs[1]);
   return APG_OK;
 }
 

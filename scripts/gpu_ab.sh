@@ -22,5 +22,11 @@ print("roofline", b["roofline"]["kernel"], round(b["roofline"]["frac"], 3))
 ks = sorted(b["kernels"].items(), key=lambda kv: -kv[1]["ms_per_launch"] * kv[1]["launches"])
 for k, v in ks[:12]:
     print(f"  {k:24s} {v['ms_per_launch'] * v['launches'] / b['steps']:9.2f} ms/step  {v['GBps']:8.1f} GB/s")
+r = b.get("repeats")
+if r:
+    print("repeats ms/step", round(r["ms_per_step"], 1), "x main", round(r["ms_per_step"] / b["ms_per_step"], 3),
+          "checks", all(r["checks"].values()))
+    for k, v in list(r["kernels_ms"].items())[:10]:
+        print(f"  rep {k:20s} {v:9.2f} ms/step")
 PY
 done

@@ -53,7 +53,7 @@ def test_unipaths_on_repeats(gpu_ctx, rep_reads):
 @pytest.mark.parametrize("probe", ["1", "4"])
 def test_overflow_table_retry_unbounded(rep_reads, monkeypatch, probe):
     """the overflowed buckets' global table (APG_SK_OVF=
-    global; the fused K+1 pass always) gives up after APG_SK_BIG_PROBE probes
+    global, for the K pass and the fused K+1 pass) gives up after APG_SK_BIG_PROBE probes
     on its first, small attempt; the full-size retry probes without a limit,
     so a crowded first attempt on tandem-repeat keys still ends in the
     oracle's spectrum, solid set and corrections."""
@@ -66,6 +66,11 @@ def test_overflow_table_retry_unbounded(rep_reads, monkeypatch, probe):
             assert np.array_equal(hist, oracle.kmer_spectrum(reads, K)), K
             assert st["n_overflow"] > 0  # the global path ran
         got, pst = ctx.precorrect(reads, K=24)
+        d = ctx.upload(reads)
+        fh, fks, _ = ctx.spectrum_precorrect(d, K_spec=25, K=24)  # the K+1 pass's global table
+        d.free()
+    assert np.array_equal(fh, oracle.kmer_spectrum(reads, 25))
+    assert fks["n_kmers"] == st["n_kmers"] and fks["n_overflow"] > 0
     exp, est = oracle.precorrect(reads, K=24)
     assert np.array_equal(got.packed[: int(got.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
     assert np.array_equal(got.quals, exp.quals)
@@ -80,7 +85,8 @@ def test_overflow_sub_buckets(rep_reads, monkeypatch, mode):
     of its entries; "bad" sends every sub-bucket through the global-table
     fallback of the ones that fill the LDS table.  Spectrum (K=24, 25, every
     dedup mode's overflow), solid set, corrections and the fused entry point
-    equal the oracle."""
+    (whose K+1 pass counts its overflowed buckets' owned K+1-mers the same
+    way) equal the oracle."""
     if mode == "bad":
         monkeypatch.setenv("APG_SK_OVF", "bad")
     else:
@@ -96,6 +102,7 @@ def test_overflow_sub_buckets(rep_reads, monkeypatch, mode):
         fh, fks, fps = ctx.spectrum_precorrect(d, K_spec=25, K=24)
         fixed = ctx.download(d, with_quals=True)
         d.free()
+    assert fks["n_kmers"] == st["n_kmers"] and fks["n_distinct"] == st["n_distinct"] and fks["n_overflow"] > 0
     exp, est = oracle.precorrect(reads, K=24)
     for g in (got, fixed):
         assert np.array_equal(g.packed[: int(g.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
