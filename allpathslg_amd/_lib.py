@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libapg.so")
+# APG_LIB_VARIANT=name loads libapg_<name>.so (diagnostics builds, scripts/build_fill_variants.sh)
+LIB_PATH = os.path.join(_HERE, f"libapg_{os.environ['APG_LIB_VARIANT']}.so" if os.environ.get("APG_LIB_VARIANT") else "libapg.so")
 
 APG_OK = 0
 ERRORS = {

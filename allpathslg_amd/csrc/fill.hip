@@ -370,6 +370,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     bcache = true;
     bfilt = true;
   }
+  // cached backtracks fused into the visit that ends a branch (bcache; the
+  // general form: xsteps bit 9 clear)
+  const bool fuse = LEAN || (bcache && !(xsteps_ & 512));
   const int refill = LEAN ? kFillRefill : refill_;
   const int xsteps = LEAN ? (kFillXsteps | (kFillXpct << 16)) : xsteps_;
   uint32_t c_ok = 0, c_none = 0, c_amb = 0, c_bud = 0, c_skip = 0;  // registers, not a scratch array
@@ -698,8 +701,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             done = true;  // search exhausted
           } else {
             dd = 63 - __clzll((long long)brm);
-            mode = 2;
-            wk = walk_window(atail, pv >> (2 * (d - dd)), dd, t);
+            const uint64_t wdd = walk_window(atail, pv >> (2 * (d - dd)), dd, t);
+            if (fuse && dd < 32) {
+              // the backtrack to a branch point whose mask its visit kept:
+              // taken now (mode 2's transition), so the sibling's lookup is
+              // the next iteration's, not the one after an iteration with
+              // no lookup for this lane
+              const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
+              const uint32_t rest = mask_at(dd) & ~((2u << bb) - 1);
+              const uint32_t b2 = __ffs(rest) - 1;
+              if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
+              pv = ((pv >> (2 * (d - dd))) << 2) | b2;
+              d = dd + 1;
+              mode = 0;
+              wk = ((wdd << 2) | b2) & t.m1;
+            } else {
+              mode = 2;
+              wk = wdd;
+            }
           }
         }
       }
@@ -733,7 +752,8 @@ __global__ void __launch_bounds__(256) k_fill_write(FillReads rv, const FillRec*
                                                     const uint64_t* __restrict__ bscan,
                                                     const uint64_t* __restrict__ yscan,
                                                     const uint64_t* __restrict__ iscan, uint64_t* __restrict__ out_boff,
-                                                    uint64_t* __restrict__ out_yoff, uint8_t* __restrict__ out) {
+                                                    uint64_t* __restrict__ out_yoff, uint8_t* __restrict__ out,
+                                                    unsigned long long* __restrict__ n_bad) {
   const uint32_t lane = threadIdx.x % kFillWLanes;
   const uint64_t groups = (uint64_t)gridDim.x * (blockDim.x / kFillWLanes);
   for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / kFillWLanes) + threadIdx.x / kFillWLanes; i < rv.n_pairs;
@@ -754,6 +774,12 @@ __global__ void __launch_bounds__(256) k_fill_write(FillReads rv, const FillRec*
     const uint32_t I = r.len;
     const unsigned __int128 pv = ((unsigned __int128)r.pv_hi << 64) | r.pv_lo;
     const uint32_t ov = r.meta >> 16, d = (r.meta >> 8) & 0xff;
+    // a record is S = A ++ path[0, d) ++ F[ov, Lf): anything else is an
+    // internal error, reported, and its bases are not read
+    if ((uint64_t)La + Lf + d != (uint64_t)I + ov || ov > Lf || ov > La) {
+      if (lane == 0) atomicAdd(n_bad, 1ull);
+      continue;
+    }
     const uint32_t nby = (I + 3) / 4;
     for (uint32_t y = lane; y < nby; y += kFillWLanes) {
       const uint32_t t0 = 4 * y;
@@ -893,8 +919,9 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   uint32_t* defer = nullptr;
   unsigned long long* ndefer = nullptr;
   APG_TRY(workspace_t(ctx, "fill_defer", npc, &defer));
-  APG_TRY(workspace_t(ctx, "fill_ndefer", 3, &ndefer));  // deferred count, next pair of pass 1 / pass 2
-  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, 3 * 8, ctx->stream));
+  // deferred count, next pair of pass 1 / pass 2, inconsistent records (k_fill_write)
+  APG_TRY(workspace_t(ctx, "fill_ndefer", 4, &ndefer));
+  APG_CHECK_HIP(hipMemsetAsync(ndefer, 0, 4 * 8, ctx->stream));
   kbegin(ctx, "fill", dr->n_bytes + 16 * dr->n_reads + np * (sizeof(FillRec) + 12));
   if (np) {
     FillCounters* fc = reinterpret_cast<FillCounters*>(cnt);
@@ -915,8 +942,9 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     const char* xce = getenv("APG_FILL_XCACHED");  // 1: cached branch points may be free steps
     const char* xpe = getenv("APG_FILL_XPCT");  // free steps only when this % of the lanes have one
     const int xpct = std::min(100, std::max(0, xpe ? atoi(xpe) : kFillXpct));
+    const char* fbe = getenv("APG_FILL_FUSE_BT");  // 0: a cached backtrack takes an iteration of its own (A/B)
     const int xsteps = std::min(255, xse ? std::max(0, atoi(xse)) : kFillXsteps) | (xce && !strcmp(xce, "1") ? 256 : 0) |
-                       (xpct << 16);
+                       (fbe && !strcmp(fbe, "0") ? 512 : 0) | (xpct << 16);
     const char* c1e = getenv("APG_FILL_CAP1");  // pass 1's expansion cap (A/B)
     const uint32_t cap1 = c1e ? (uint32_t)std::max(1, atoi(c1e)) : kFillCap1;
     auto fill = [&](auto kern) {
@@ -969,13 +997,20 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   if (np)
     k_fill_write<<<grid_for(ctx, np, 256 / kFillWLanes), 256, 0, ctx->stream>>>(rv, rec, bscan, yscan, iscan,
                                                                                  fd->d_base_off, fd->d_byte_off,
-                                                                                 fd->d_packed);
+                                                                                 fd->d_packed, ndefer + 3);
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   APG_CHECK_HIP(hipMemcpyAsync(fd->d_base_off + nf, bscan + np, 8, hipMemcpyDeviceToDevice, ctx->stream));
   APG_CHECK_HIP(hipMemcpyAsync(fd->d_byte_off + nf, yscan + np, 8, hipMemcpyDeviceToDevice, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(fd->d_packed + tot[1], 0, 64, ctx->stream));
-  return sync(ctx);
+  unsigned long long nbad = 0;
+  APG_CHECK_HIP(hipMemcpyAsync(&nbad, ndefer + 3, 8, hipMemcpyDeviceToHost, ctx->stream));
+  APG_TRY(sync(ctx));
+  if (nbad) {
+    set_error("apg_fill_fragments: inconsistent fill records (internal error)");
+    return APG_E_STATE;
+  }
+  return APG_OK;
 }
 
 }  // namespace apg

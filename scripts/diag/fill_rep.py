@@ -24,7 +24,7 @@ cases = [("base", 1024, {}), ("pass1", 96, {}), ("x0", 1024, {"APG_FILL_XSTEPS":
          ("p75", 1024, {"APG_FILL_XPCT": "75"}), ("p90", 1024, {"APG_FILL_XPCT": "90"}),
          ("p50x4", 1024, {"APG_FILL_XSTEPS": "4"}),
          ("c48", 1024, {"APG_FILL_CAP1": "48"}), ("c192", 1024, {"APG_FILL_CAP1": "192"}),
-         ("c384", 1024, {"APG_FILL_CAP1": "384"}), ("c1024", 1024, {"APG_FILL_CAP1": "1024"}), ("hash1", 1024, {"APG_EXT_HASH": "1"}), ("nolean", 1024, {"APG_FILL_LEAN": "0"}), ("base2", 1024, {})]
+         ("c384", 1024, {"APG_FILL_CAP1": "384"}), ("c1024", 1024, {"APG_FILL_CAP1": "1024"}), ("hash1", 1024, {"APG_EXT_HASH": "1"}), ("nolean", 1024, {"APG_FILL_LEAN": "0"}), ("nofuse", 1024, {"APG_FILL_FUSE_BT": "0"}), ("base2", 1024, {})]
 sel = os.environ.get("FILL_CASES")
 if sel:
     cases = [c for c in cases if c[0] in sel.split(",")]
