@@ -77,15 +77,16 @@ inline bool ext_two_level(int K) {
   }();
   return on && 2 * (K - 1) + 16 <= 64;
 }
-// APG_EXT_HASH=1: homes by a xorshift + one 64-bit multiply whose top bits
-// index the table (a third of the instructions of khash's two multiply
-// rounds).  Same box: main step 144.3 / 145.0 vs 144.1 ms with khash (fill
-// -0.2 ms, inserts +0.5, decisions +0.4), repeat-rich step 187.2 vs 189.6 ms;
-// khash stays the default.
+// Homes by a xorshift + one 64-bit multiply whose top bits index the table
+// (a third of the instructions of khash's two multiply rounds; APG_EXT_HASH=0
+// for khash).  Round 4, same box: main step 144.3 / 145.0 vs 144.1 ms with
+// khash (fill -0.2 ms, inserts +0.5, decisions +0.4), repeat-rich step 187.2
+// vs 189.6 ms; round 5, same box: main 142.3 vs 142.4 ms, repeat-rich 181.0
+// vs 181.9 ms (fill 38.4 vs 39.6 ms) — the default since.
 inline ExtTab ext_tab(unsigned long long* slot, uint64_t mask, int K) {
   static const bool mul = [] {
     const char* e = getenv("APG_EXT_HASH");
-    return e && !strcmp(e, "1");
+    return !(e && !strcmp(e, "0"));
   }();
   return ExtTab{slot, mask, make_hashp(K - 1), (1ull << (2 * (K - 1))) - 1, K - 1, ext_two_level(K) ? 16 : 8,
                 mul ? 64 - __builtin_popcountll(mask) : 0};
