@@ -99,18 +99,21 @@ inline ExtTab ext_tab(unsigned long long* slot, uint64_t mask, int K) {
 // per lookup, where slot-by-slot probing paid a second one for every key not
 // in its home slot — and a wave waits for its slowest lane.
 constexpr uint64_t kExtGrp = 4;
+// HM: 1 when the caller knows the table uses the multiplicative home (t.hs
+// != 0), so no khash constants are held for the other form
+template <int HM = 0>
 __device__ __forceinline__ uint64_t ext_home(const ExtTab& t, uint64_t c) {
-  if (t.hs) return (((c ^ (c >> 29)) * 0x9e3779b97f4a7c15ull) >> t.hs) & ~(kExtGrp - 1);
+  if (HM || t.hs) return (((c ^ (c >> 29)) * 0x9e3779b97f4a7c15ull) >> t.hs) & ~(kExtGrp - 1);
   return khash(t.h1, c) & t.mask & ~(kExtGrp - 1);
 }
 
 // The extension bits of canonical (K-1)-mer c (0 if absent): pred | succ << 4,
 // and with two-level slots ss << 8 | pp << 12.  KS: the key shift when the
 // caller knows it at compile time (0: t.ks).
-template <int KS = 0>
+template <int KS = 0, int HM = 0>
 __device__ __forceinline__ uint32_t ext_bits(const ExtTab& t, uint64_t c) {
   const int ks = KS ? KS : t.ks;
-  uint64_t g = ext_home(t, c);
+  uint64_t g = ext_home<HM>(t, c);
   for (;;) {
     const ulonglong2* q = reinterpret_cast<const ulonglong2*>(t.slot + g);
     const ulonglong2 a = q[0], b = q[1];
@@ -138,10 +141,10 @@ __device__ __forceinline__ uint32_t ext_succ(const ExtTab& t, uint64_t w, uint32
 // ext_succ | ss << 4 | 256 when ss is known: w has exactly one successor
 // and the table is two-level (palindromes excepted: their two orientations
 // share one slot).
-template <int KS = 0>
+template <int KS = 0, int HM = 0>
 __device__ __forceinline__ uint32_t ext_succ2(const ExtTab& t, uint64_t w, uint32_t* nlook) {
   const uint64_t r = rc_bases(w, t.n1, t.m1);
-  const uint32_t e = ext_bits<KS>(t, w < r ? w : r);
+  const uint32_t e = ext_bits<KS, HM>(t, w < r ? w : r);
   ++*nlook;
   uint32_t m = 0, x = 0;
   if (w <= r) m |= (e >> 4) & 15, x = (e >> 8) & 15;

@@ -246,6 +246,7 @@ __device__ __forceinline__ uint64_t fwin(const uint8_t* B, uint32_t Lf, uint32_t
 // Every K-mer of a packed read (L >= K) solid: one extension lookup per
 // K-mer (its first K-1 bases hold its last base as a successor).  Bases are
 // streamed 32 at a time from one LSB-first word.
+template <int HM = 0>
 __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, uint32_t L, uint32_t* nlook) {
   const int n1 = t.n1;
   uint64_t buf = bases32(R, 0);
@@ -256,7 +257,7 @@ __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, ui
     const uint32_t b = (uint32_t)(((i & 31) == 0 ? buf : buf >> (2 * (i & 31))) & 3);
     uint32_t m = pend & 15;
     if (!(pend & 16)) {
-      const uint32_t x = ext_succ2(t, w, nlook);
+      const uint32_t x = ext_succ2<0, HM>(t, w, nlook);
       m = x & 15;
       pend = x >> 4;
     } else {
@@ -271,12 +272,13 @@ __device__ __forceinline__ bool read_solid(const ExtTab& t, const uint8_t* R, ui
 // Both reads of a pair solid throughout.  cl (or null): the pair's clean
 // flags from the correction pass that used this solid set (1 clean, 0 not,
 // 2 not derived -> look the read's K-mers up).
+template <int HM = 0>
 __device__ __forceinline__ bool pair_solid(const ExtTab& t, const uint8_t* A, uint32_t La, const uint8_t* B,
                                            uint32_t Lf, const uint8_t* cl, uint32_t* nlook) {
   const uint32_t fa = cl ? cl[0] : 2u, fb = cl ? cl[1] : 2u;
   if (fa == 0 || fb == 0) return false;
-  if (fa == 2 && !read_solid(t, A, La, nlook)) return false;
-  if (fb == 2 && !read_solid(t, B, Lf, nlook)) return false;
+  if (fa == 2 && !read_solid<HM>(t, A, La, nlook)) return false;
+  if (fb == 2 && !read_solid<HM>(t, B, Lf, nlook)) return false;
   return true;
 }
 
@@ -348,9 +350,10 @@ constexpr int kFillXpct = 75;
 // same as the nested search (oracle/fill_oracle.c).
 // LEAN (the default): the knobs at their defaults, folded at compile time —
 // one pass (cap = max_steps), the branch cache and the bridge filter on,
-// kFillRefill, kFillXsteps free steps at kFillXpct % — which frees the
-// scalar registers the runtime knobs held (the general form spills SGPRs to
-// VGPR lanes); any APG_FILL_* A/B knob set selects the general form.
+// kFillRefill, kFillXsteps free steps at kFillXpct %, the multiplicative
+// table home — which frees scalar registers the runtime knobs held (the
+// general form spills more SGPRs to VGPR lanes); any APG_FILL_* A/B knob
+// set (or APG_EXT_HASH=0) selects the general form.
 template <int KS, bool LEAN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_fill(FillReads rv, FillP p, ExtTab t, FillRec* __restrict__ rec,
                                               uint32_t* __restrict__ lens, uint32_t* __restrict__ nbytes,
@@ -479,7 +482,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       emit(kFillSkip, FillRec{0, 0, 0, kFillSkip});
       return;
     }
-    if (!pair_solid(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
+    if (!pair_solid<LEAN ? 1 : 0>(t, A, La, B, Lf, clean ? clean + 2 * i : nullptr, &nlook)) {
       emit(kFillNone, FillRec{0, 0, 0, kFillNone});  // S must be a path of solid K-mers
       return;
     }
@@ -534,7 +537,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
               const uint32_t b = (uint32_t)(f0 >> (2 * (o + jj))) & 3;
               uint32_t mm = pm & 15;
               if (!(pm & 16)) {
-                const uint32_t x = ext_succ2(t, w, &nlook);
+                const uint32_t x = ext_succ2<0, LEAN ? 1 : 0>(t, w, &nlook);
                 mm = x & 15;
                 pm = x >> 4;
               } else {
@@ -617,7 +620,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       } else if (pq & 16) {
         m = pq & 15;
       } else {
-        const uint32_t x = ext_succ2<KS>(t, key, &nlook);
+        const uint32_t x = ext_succ2<KS, LEAN ? 1 : 0>(t, key, &nlook);
         m = x & 15;
         m2 = x >> 4;
       }
@@ -957,7 +960,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
     };
     // the general form when any A/B knob is set (APG_FILL_LEAN=0 forces it)
     const char* le = getenv("APG_FILL_LEAN");
-    const bool lean = !(le && !strcmp(le, "0")) && bcache && bfilt && refill == kFillRefill &&
+    const bool lean = !(le && !strcmp(le, "0")) && et.hs != 0 && bcache && bfilt && refill == kFillRefill &&
                       xsteps == (kFillXsteps | (kFillXpct << 16)) && cap1 >= p.max_steps;
     if (two && lean)
       fill(k_fill<16, true>);
