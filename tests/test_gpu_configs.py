@@ -13,10 +13,10 @@ where the oracle finishes in seconds:
       complete K=24 solid set, and PreCorrect of all 40 M reads against it
       (the oracle's rolling-key form, ork_precorrect_solid_fast, equal to the
       checker by tests/test_cpu_baseline.py); one 1/256 hash parcel of the
-      K=25 counted table (keys and counts); FillFragments of the first 100 K
-      pairs; and both directions of the unipath graph inside one 200-kb
-      genome window (oracle graph of the filled fragments whose pairs lie in
-      the window).
+      K=25 counted table (keys and counts); FillFragments of all 20 M pairs
+      (every status and filled byte); and both directions of the unipath
+      graph inside five 400-kb genome windows (oracle graph of the filled
+      fragments whose pairs lie in each window).
   C3  chr20 40 M frag + 20 M 3-kb jump reads: ErrorCorrectJump, all_reads =
       filled fragments ++ trimmed jumps, K=96 graph over all of them, run
       twice, ECJ parity on the first 20 K jump reads, window parity with the
@@ -305,21 +305,31 @@ def test_c2_bench_entry_point_matches_oracle(c2, c2_oracle):
     assert_precorrect_equal(f["fixed"], f["pst"], c2_oracle["fixed"], c2_oracle["est"])
 
 
-def test_c2_fill_sample_matches_oracle(c2):
+def test_c2_full_fill_matches_oracle(c2, c2_oracle):
+    """FillFragments of all 20 M pairs (the whole-table-checked corrected
+    reads and solid set) against the oracle's hash-table form: every status,
+    every filled fragment byte for byte, every counter."""
     fixed, solid = c2["fixed"], c2["a"]["solid"]
-    npairs = 100_000
-    ofill, ostatus, _, _ = oracle.fill_fragments(fixed.subset(0, 2 * npairs), solid, K=24, fast=True)
+    assert np.array_equal(solid, c2_oracle["solid"])
+    ofill, ostatus, _, ost = oracle.fill_fragments(fixed, solid, K=24, fast=True)
     status = c2["a"]["status"]
-    assert np.array_equal(status[:npairs], ostatus)
-    hf = filled_subset(c2["filled_a"], status, np.arange(npairs))
+    assert np.array_equal(status, ostatus)
+    hf = c2["filled_a"]
     assert np.array_equal(hf.base_off, ofill.base_off)
     assert np.array_equal(hf.packed[: int(hf.byte_off[-1])], ofill.packed[: int(ofill.byte_off[-1])])
+    for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases"):
+        assert c2["a"]["fst"][k] == ost[k], k
 
 
-def test_c2_window_unipaths_match_oracle(c2):
+# five windows of 400 kb spread over the chromosome (2 Mb, 3 % of it; round 4
+# checked one 200-kb window)
+C2_WINDOWS = [int(CHR20 * f) for f in (0.07, 0.29, 0.5, 0.71, 0.9)]
+
+
+@pytest.mark.parametrize("w0", C2_WINDOWS)
+def test_c2_window_unipaths_match_oracle(c2, w0):
     g = c2["genome"]
-    w0 = CHR20 // 2
-    w1 = w0 + 200_000
+    w1 = w0 + 400_000
     start, flen, _ = synth_layout(CHR20, 20_000_000, seed=c2["seed"] + 100, threads=16)
     pairs = pairs_in_window(start, flen, w0, w1)
     sub = filled_subset(c2["filled_a"], c2["a"]["status"], pairs)
