@@ -536,16 +536,18 @@ def error_correct_jump(frags, jumps, K: int = 24, min_solid: int = 3, max_q: int
     return error_correct_jump_solid(jumps, solid, K, max_q, min_keep)
 
 
-def error_correct_jump_solid(jumps, solid, K: int = 24, max_q: int = 20, min_keep: int = 40):
+def error_correct_jump_solid(jumps, solid, K: int = 24, max_q: int = 20, min_keep: int = 40, fast: bool = False):
     """error_correct_jump against a given solid hash set (e.g. the GPU's
-    frag-read set, itself checked against kmer_count_range parcels)."""
+    frag-read set, itself checked against kmer_count_range parcels).
+    fast=True: the correction pass in precorrect_solid's rolling-key form
+    (same outputs; full-size inputs)."""
     L = lib()
     if not hasattr(L, "_oje"):
         L.oje_trim.restype = None
         L.oje_trim.argtypes = [C.c_uint64, _u64p, _u64p, _u8p, C.c_int, _u64p, C.c_uint64, C.c_uint32, _u32p]
         L._oje = True
     solid = np.sort(np.ascontiguousarray(solid, dtype=np.uint64))
-    fixed, st = precorrect_solid(jumps, solid, K, max_q)
+    fixed, st = precorrect_solid(jumps, solid, K, max_q, fast=fast) if fast else precorrect_solid(jumps, solid, K, max_q)
     keep = np.zeros(max(fixed.n_reads, 1), dtype=np.uint32)
     n, bo, yo, pk = _rp(fixed)
     L.oje_trim(n, bo, yo, pk, K, solid.ctypes.data_as(_u64p), len(solid), min_keep, keep.ctypes.data_as(_u32p))

@@ -32,6 +32,8 @@ static int has(const uint64_t* s, uint64_t n, uint64_t x) {
 void oje_trim(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
               const uint64_t* solid, uint64_t ns, uint32_t min_keep, uint32_t* keep) {
   const uint64_t mask = K == 32 ? ~0ull : (1ull << (2 * K)) - 1;
+  /* reads are independent: OpenMP over them (full-size C3 parity) */
+#pragma omp parallel for schedule(dynamic, 4096)
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint64_t L = base_off[r + 1] - base_off[r];
     const uint8_t* p = packed + byte_off[r];

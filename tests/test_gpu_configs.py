@@ -19,8 +19,8 @@ where the oracle finishes in seconds:
       fragments whose pairs lie in each window).
   C3  chr20 40 M frag + 20 M 3-kb jump reads: ErrorCorrectJump, all_reads =
       filled fragments ++ trimmed jumps, K=96 graph over all of them, run
-      twice, ECJ parity on the first 20 K jump reads, window parity with the
-      window's jump reads included.
+      twice, ECJ parity on all 20 M jump reads (bases, qualities, trim
+      lengths, counters), window parity with the window's jump reads included.
 """
 import numpy as np
 import pytest
@@ -368,14 +368,16 @@ def test_c3_frag_plus_jump_graph(gpu_ctx):
     inst = int(fa["filled_bases"]) - (K96 - 1) * fa["n_filled"] + int(np.maximum(jl - K96 + 1, 0).sum())
     assert ua["n_instances"] == inst
     assert ua["n_nodes"] >= CHR20 - K96 + 1 - 1000
-    # ErrorCorrectJump parity on the first 20 K jump reads (frag solid set)
-    n = 20_000
+    # ErrorCorrectJump parity on all 20 M jump reads (the fragments' solid set):
+    # every corrected base and quality, every trim length, every counter
     dJ_host = gpu_ctx.download(dJ)
-    fixed, okeep, _ = oracle.error_correct_jump_solid(jumps.subset(0, n), ecj_solid, K=24)
-    got = dJ_host.subset(0, n)
-    assert np.array_equal(got.packed[: int(got.byte_off[-1])], fixed.packed[: int(fixed.byte_off[-1])])
-    assert np.array_equal(got.quals, fixed.quals)
-    assert np.array_equal(ka[:n], okeep)
+    fixed, okeep, ost = oracle.error_correct_jump_solid(jumps, ecj_solid, K=24, fast=True)
+    assert np.array_equal(dJ_host.packed[: int(dJ_host.byte_off[-1])], fixed.packed[: int(fixed.byte_off[-1])])
+    assert np.array_equal(dJ_host.quals, fixed.quals)
+    assert np.array_equal(ka, okeep)
+    for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
+        assert ea["precorrect"][k] == ost[k], k
+    assert ea["bases_kept"] == int(okeep.astype(np.uint64).sum())
     # window parity with the window's jump reads in the oracle's input
     w0 = CHR20 // 3
     w1 = w0 + 200_000
