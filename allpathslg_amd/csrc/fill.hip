@@ -326,7 +326,10 @@ constexpr uint32_t kFillCap1 = 1u << 30;
 // A wave refills its idle lanes with new pairs once at most this many lanes
 // are still walking (APG_FILL_REFILL for A/B: a higher mark keeps more lanes
 // walking, a lower one batches more lanes into each refill's start phase).
-constexpr int kFillRefill = 32;
+#ifndef APG_FILL_REFILL_DEF  // compile-time A/B (scripts/build_fill_variants.sh)
+#define APG_FILL_REFILL_DEF 32
+#endif
+constexpr int kFillRefill = APG_FILL_REFILL_DEF;
 // Free steps after an iteration's lookup (APG_FILL_XSTEPS; APG_FILL_XCACHED=1
 // lets cached branch points be free steps too), taken only when at least
 // APG_FILL_XPCT % of the wave's lanes have one.  Same box, fill ms on the iid
@@ -334,9 +337,20 @@ constexpr int kFillRefill = 32;
 // 57.09, none 16.16 / 51.70; then (another box) 1 step at 75 % 11.29 / 44.70,
 // at 0 % 11.28 / 48.10, none 12.68 / 43.67 (scripts/diag/fill_rep.py): a
 // free step runs while the wave's other lanes wait, so only the common
-// chains pay.
-constexpr int kFillXsteps = 1;
-constexpr int kFillXpct = 75;
+// chains pay.  Round 5 (lean form, fused backtracks; compile-time variants,
+// one box): 75 % 10.57 / 37.77, 60 % 10.60 / 38.40, 50 % 10.58 / 37.29,
+// 40 % 10.55 / 37.10 -> 40 %; 2 free steps no change; a refill mark of 24
+// 10.91 / 43.31, 44 12.06 / 36.65, 40 with 50 % 11.06 / 35.10, and a mark
+// raised to 40 after 32-128 refill-free iterations 10.78 / 37.6-38.5 (the
+// main step's genome prefers 32).
+#ifndef APG_FILL_XSTEPS_DEF  // compile-time A/B (scripts/build_fill_variants.sh)
+#define APG_FILL_XSTEPS_DEF 1
+#endif
+constexpr int kFillXsteps = APG_FILL_XSTEPS_DEF;
+#ifndef APG_FILL_XPCT_DEF  // compile-time A/B (scripts/build_fill_variants.sh)
+#define APG_FILL_XPCT_DEF 40
+#endif
+constexpr int kFillXpct = APG_FILL_XPCT_DEF;
 
 // One thread per pair, lanes persistent.  The gap walk is a state machine
 // that makes exactly ONE extension lookup per iteration whatever the lane is
