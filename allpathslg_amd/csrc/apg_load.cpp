@@ -60,7 +60,10 @@ struct Map {
   }
 };
 
-int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len, uint8_t* dst, int threads) {
+// w0: the first staging worker used (a load streaming two files at once gives
+// each its own workers; the caller has made the pool large enough).
+int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len, uint8_t* dst, int threads,
+                     int w0 = 0) {
   if (!len) return APG_OK;
   Fd f;
   f.fd = open(path, O_RDONLY);
@@ -87,7 +90,7 @@ int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len,
   }
   const uint64_t nch = (len + kStageChunk - 1) / kStageChunk;
   const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, nch));
-  APG_TRY(staging_get(ctx, T));
+  if (w0 == 0) APG_TRY(staging_get(ctx, T));
   std::atomic<int> err{APG_OK};
   std::atomic<uint64_t> next{0};
   std::vector<std::string> msg(T);
@@ -98,9 +101,10 @@ int stream_to_device(apg_ctx* ctx, const char* path, uint64_t off, uint64_t len,
       if (err.compare_exchange_strong(ok, code)) msg[w] = m;
     };
     if (hipSetDevice(device) != hipSuccess) return fail(APG_E_HIP, "hipSetDevice failed");
-    uint8_t* buf[2] = {ctx->staging.buf[2 * w], ctx->staging.buf[2 * w + 1]};
-    hipEvent_t ev[2] = {ctx->staging.ev[2 * w], ctx->staging.ev[2 * w + 1]};
-    hipStream_t st = ctx->staging.st[w];
+    const int sw = w0 + w;
+    uint8_t* buf[2] = {ctx->staging.buf[2 * sw], ctx->staging.buf[2 * sw + 1]};
+    hipEvent_t ev[2] = {ctx->staging.ev[2 * sw], ctx->staging.ev[2 * sw + 1]};
+    hipStream_t st = ctx->staging.st[sw];
     bool used[2] = {false, false};
     int k = 0;
     for (uint64_t c; (c = next.fetch_add(1)) < nch && err.load() == APG_OK; k ^= 1) {
@@ -295,37 +299,50 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
   }
   if (rc != APG_OK) return fail(rc);
   const double t_meta = ms(t0);
+  // The qualities (4/5 of the bytes) are first read by PreCorrect's
+  // candidate scan, after the whole K-mer count: they stream in on a host
+  // thread while the caller's next module counts the bases, and every
+  // reader of d_quals joins the load first (dreads_quals_ready).
+  // APG_LOAD_SYNC=1: loaded before the call returns (the round-4 form).
+  // APG_LOAD_EARLY=1: the qualities' thread starts beside the bases' load,
+  // on staging workers of its own, instead of after it.
+  static const bool sync_load = std::getenv("APG_LOAD_SYNC") && !std::strcmp(std::getenv("APG_LOAD_SYNC"), "1");
+  static const bool early = std::getenv("APG_LOAD_EARLY") && !std::strcmp(std::getenv("APG_LOAD_EARLY"), "1");
+  auto start_quals = [&](int w0) -> int {
+    auto* pend = new (std::nothrow) DreadsPending();
+    if (!pend) return APG_E_NOMEM;
+    pend->ctx = ctx;
+    const std::string qpath(qualb);
+    const uint64_t qo = 32 + 8 * (n + 1), qn = d->n_bases;
+    uint8_t* qdst = d->d_quals;
+    const std::string fpath(fastb);
+    pend->th = std::thread([pend, ctx, qpath, fpath, n, qo, qn, qdst, threads, w0]() {
+      const auto tq = std::chrono::steady_clock::now();
+      pend->rc = stream_to_device(ctx, qpath.c_str(), qo, qn, qdst, threads, w0);
+      if (pend->rc == APG_OK) pend->rc = qualb_offsets_match(fpath.c_str(), qpath.c_str(), n);
+      if (pend->rc != APG_OK) pend->err = get_error();
+      pend->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count();
+    });
+    d->pending = pend;
+    ctx->bg_load = d;
+    return APG_OK;
+  };
+  const bool bg = qualb && n && !sync_load;
+  if (bg && early) {
+    APG_TRY(staging_get(ctx, 2 * threads));  // workers [threads, 2 threads) for the qualities
+    rc = start_quals(threads);
+    if (rc != APG_OK) return fail(rc);
+  }
   const auto t1 = clk::now();
   rc = stream_to_device(ctx, fastb, 32 + 8 * (n + 1), d->n_bytes, d->d_packed, threads);
   const double t_bases = ms(t1);
   const auto t2 = clk::now();
-  // The qualities (4/5 of the bytes) are first read by PreCorrect's
-  // candidate scan, after the whole K-mer count: they keep streaming in on
-  // a host thread while the caller's next module counts the bases, and every
-  // reader of d_quals joins the load first (dreads_quals_ready).
-  // APG_LOAD_SYNC=1: loaded before the call returns (the round-4 form).
-  static const bool sync_load = std::getenv("APG_LOAD_SYNC") && !std::strcmp(std::getenv("APG_LOAD_SYNC"), "1");
   if (rc == APG_OK && qualb && n) {
     if (sync_load) {
       rc = stream_to_device(ctx, qualb, 32 + 8 * (n + 1), d->n_bases, d->d_quals, threads);
       if (rc == APG_OK) rc = qualb_offsets_match(fastb, qualb, n);
-    } else {
-      auto* pend = new (std::nothrow) DreadsPending();
-      if (!pend) return fail(APG_E_NOMEM);
-      pend->ctx = ctx;
-      const std::string qpath(qualb);
-      const uint64_t qo = 32 + 8 * (n + 1), qn = d->n_bases;
-      uint8_t* qdst = d->d_quals;
-      const std::string fpath(fastb);
-      pend->th = std::thread([pend, ctx, qpath, fpath, n, qo, qn, qdst, threads]() {
-        const auto tq = std::chrono::steady_clock::now();
-        pend->rc = stream_to_device(ctx, qpath.c_str(), qo, qn, qdst, threads);
-        if (pend->rc == APG_OK) pend->rc = qualb_offsets_match(fpath.c_str(), qpath.c_str(), n);
-        if (pend->rc != APG_OK) pend->err = get_error();
-        pend->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq).count();
-      });
-      d->pending = pend;
-      ctx->bg_load = d;
+    } else if (!early) {
+      rc = start_quals(0);
     }
   }
   vlog(ctx, "load_dev: %llu reads, offsets -> HBM + device checks %.1f ms, bases %.1f ms (%.2f GB/s), quals %.1f ms%s, "
