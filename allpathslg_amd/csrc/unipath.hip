@@ -1475,6 +1475,9 @@ struct UskOut {
   // appended, for the nodes with id < idx_lim (gs[4] counts the rest)
   unsigned long long* idx;
   uint64_t tmask, idx_lim;
+  // diagnostics (APG_USK_PROF): thread 0's clock64 sums per phase — chunk
+  // load + dedup, scan + owner map, inserts, node emission, local links
+  unsigned long long* prof = nullptr;
 };
 
 // The node index of the single-GPU build, made by the node buckets
@@ -1517,6 +1520,15 @@ k_usk_bucket(const SK48* __restrict__ rec,
   static_assert(sizeof(SK48) * kUskChunk >= 2 * TAB, "crec doubles as the rank -> slot list");
   uint16_t* slot_of = reinterpret_cast<uint16_t*>(crec);
   const uint32_t tid = threadIdx.x;
+  unsigned long long pt[5] = {0, 0, 0, 0, 0}, t0 = 0;
+  const bool prof = o.prof != nullptr && tid == 0;
+  auto mark = [&](int ph) {
+    if (prof) {
+      const unsigned long long t1 = clock64();
+      if (ph > 0) pt[ph - 1] += t1 - t0;
+      t0 = t1;
+    }
+  };
   // The block's buckets bkt, bkt + grid, ... are one record stream: the next
   // chunk's records (this bucket's or the next bucket's first) are loaded
   // while the current chunk is counted.
@@ -1553,6 +1565,7 @@ k_usk_bucket(const SK48* __restrict__ rec,
     }
     for (uint32_t s = tid; s < kUskTab; s += kUskBThreads) tag[s] = 0;
     if (tid == 0) ovf = 0;
+    mark(0);
     for (uint32_t c0 = 0; c0 < nr; c0 += kUskChunk) {
       // the table filled in an earlier chunk (block-uniform after the chunk's
       // barrier): the rest of the bucket goes to the global table as well, so
@@ -1614,11 +1627,13 @@ k_usk_bucket(const SK48* __restrict__ rec,
         atomicAdd(&o.dstat[0], 1ull);
         atomicAdd(&o.dstat[1], (unsigned long long)((crec[tid].w0 >> 32) & 0xff));
       }
+      mark(1);
       uint32_t tot;
       const uint32_t ex = block_exclusive_scan<uint32_t>(nk, scan_sm, &tot);  // barrier: table clear visible
       if (tid < kUskChunk) koff[tid] = ex;
       for (uint32_t u = 0; u < nk; ++u) owner[ex + u] = (uint8_t)tid;
       __syncthreads();
+      mark(2);
       for (uint32_t f = tid; f < tot; f += kUskBThreads) {
         const uint32_t i = owner[f];
         K3 key;
@@ -1670,6 +1685,7 @@ k_usk_bucket(const SK48* __restrict__ rec,
         }
       }
       __syncthreads();
+      mark(3);
     }
     if (ovf) {
       if (tid == 0) o.ovf_list[atomicAdd(o.novf, 1ull)] = (uint32_t)bucket(bkt);
@@ -1705,6 +1721,7 @@ k_usk_bucket(const SK48* __restrict__ rec,
           }
         }
       }
+    mark(4);
     if (o.lsucc) {  // block-uniform
       __syncthreads();  // every slot's rank
       for (uint32_t r = tid; r < tot; r += kUskBThreads) {  // the occupied slots only: full lanes
@@ -1752,8 +1769,11 @@ k_usk_bucket(const SK48* __restrict__ rec,
       }
     }
     __syncthreads();
+    mark(5);
     advance();
   }
+  if (prof)
+    for (int i = 0; i < 5; ++i) atomicAdd(&o.prof[i], pt[i]);
 }
 
 // Instances of the overflowed buckets as 32-byte KRecs (for the U2 table).
@@ -2428,7 +2448,10 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1) + 1, &bufA));
   APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1) + 1, &bufB));
   // partition levels on the key bits below the shard + digit bits
-  const uint64_t need = std::max<uint64_t>(1, (nk + kUskBucketKmers - 1) / kUskBucketKmers);
+  // APG_USK_BUCKET_KMERS=n: instances per node bucket the levels aim for (A/B)
+  static const uint64_t bk_kmers = getenv("APG_USK_BUCKET_KMERS") ? std::max(64, atoi(getenv("APG_USK_BUCKET_KMERS")))
+                                                                  : kUskBucketKmers;
+  const uint64_t need = std::max<uint64_t>(1, (nk + bk_kmers - 1) / bk_kmers);
   const int bb = std::min(32 - pbits, std::max(D, ceil_log2_u(need)));
   const int rem = bb - D;
   int nlev = (rem + kMaxLevelBits - 1) / kMaxLevelBits;
@@ -2514,7 +2537,12 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     if (want_ls) APG_TRY(workspace_t(ctx, "usk_lsucc", cap, &ls));
     APG_CHECK_HIP(hipMemsetAsync(gs, 0, 6 * 8, ctx->stream));
     if (pre_idx) APG_CHECK_HIP(hipMemsetAsync(pre_idx, 0xff, pre_T * 8, ctx->stream));
-    const UskOut uo{nodes, cap, gs, ovf, gs + 1, ls, dedup ? 1u : 0u, dstat, pre_idx, pre_T - 1, pre_T / 2};
+    UskOut uo{nodes, cap, gs, ovf, gs + 1, ls, dedup ? 1u : 0u, dstat, pre_idx, pre_T - 1, pre_T / 2};
+    static const bool uprof = getenv("APG_USK_PROF") != nullptr;
+    if (uprof) {
+      APG_TRY(workspace_t(ctx, "usk_prof", 8, &uo.prof));
+      APG_CHECK_HIP(hipMemsetAsync(uo.prof, 0, 64, ctx->stream));
+    }
     kbegin(ctx, "usk_bucket", n * sizeof(SK48) + (nb + 1) * 8);
     if (small_tab) {
       UskOut u1 = uo;
@@ -2539,6 +2567,18 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     if (hs[0] <= cap) break;
     vlog(ctx, "unipaths: %llu nodes exceed the node list (%llu), rerunning", hs[0], (unsigned long long)cap);
     cap = hs[0] + hs[0] / 8;
+  }
+  {
+    static const bool uprof = getenv("APG_USK_PROF") != nullptr;
+    if (uprof) {
+      unsigned long long* dp = nullptr;
+      APG_TRY(workspace_t(ctx, "usk_prof", 8, &dp));
+      unsigned long long hp[5];
+      APG_TRY(d2h_u64(ctx, dp, hp, 5));
+      const double tot = (double)(hp[0] + hp[1] + hp[2] + hp[3] + hp[4]) + 1e-9;
+      fprintf(stderr, "[usk_prof] load+dedup %.3f scan+owner %.3f insert %.3f emit %.3f links %.3f (shares of thread 0's clocks)\n",
+              hp[0] / tot, hp[1] / tot, hp[2] / tot, hp[3] / tot, hp[4] / tot);
+    }
   }
   if (dstat) {
     unsigned long long d4[4];
