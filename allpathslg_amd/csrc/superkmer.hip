@@ -557,6 +557,7 @@ struct SkOut {
   // into `weak` at wpos[self_send + (b - self_lo)]; the others their masks
   // into `wrec`, packed without that segment
   uint64_t self_lo = 0, self_n = 0, self_send = 0;
+  uint32_t skip_heavy = 0;  // k_sk_bucket_dd: buckets over kSkHeavyRecords are counted elsewhere (not listed)
 };
 
 // A record's weak-K-mer mask m (bit t: K-mer t) at record position b: into the
@@ -1220,10 +1221,11 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
     if (nr == 0 || nr > kSkHeavyRecords || (WEAK && nr > kDdRecCap)) {  // block-uniform
       if (dout && tid == 0) dcount[bkt] = nr ? ~0u : 0u;
       if (nr && tid == 0) {
-        if (nr > kSkHeavyRecords)
-          o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
-        else
+        if (nr > kSkHeavyRecords) {
+          if (!o.skip_heavy) o.ovf_list[atomicAdd(&o.gstats[1], 1ull)] = (uint32_t)bkt;
+        } else {
           redo[atomicAdd(&o.gstats[4], 1ull)] = (uint32_t)bkt;
+        }
       }
       if (tid < nnr) pre = rec[noff + tid];
       bkt = nbk;
@@ -1411,6 +1413,17 @@ __global__ void __launch_bounds__(kDdThreads) __attribute__((amdgpu_waves_per_eu
 // per bucket: the overflowing buckets of a repeat-rich genome are few and
 // huge (one minimizer shared by thousands of copies), and a workgroup per
 // bucket left one CU crunching the largest while the rest idled.
+// The buckets over kSkHeavyRecords records (known from the bucket bounds
+// before any counting): their overflow path can start beside the bucket pass.
+__global__ void k_sk_heavy(const uint64_t* __restrict__ boff, uint64_t nb, uint32_t* __restrict__ list,
+                           unsigned long long* __restrict__ n) {
+  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = b0 + threadIdx.x;
+    const bool h = b < nb && boff[b + 1] - boff[b] > kSkHeavyRecords;
+    const unsigned long long at = wave_append(n, h);
+    if (h) list[at] = (uint32_t)b;
+  }
+}
 __global__ void k_sk_ovf_sizes(const uint64_t* __restrict__ boff, const uint32_t* __restrict__ ovf, uint32_t n_ovf,
                                uint32_t* __restrict__ sz) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2586,8 +2599,87 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     const uint64_t grid_dd = !dd ? 0
                              : solid ? resident_grid(ctx, k_sk_bucket_dd<true, RB>, kDdThreads, nb)
                                      : resident_grid(ctx, k_sk_bucket_dd<false, RB>, kDdThreads, nb);
+    // An overflow list (buckets ovl[0, n_ovf)) counted on ctx->stream: the
+    // sub-bucket LDS path, or the global table (APG_SK_OVF=global).
+    auto run_ovf = [&](const uint32_t* ovl, uint32_t n_ovf) -> int {
+      unsigned long long* nk = gstats + 3;
+      APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
+      uint32_t* osz = nullptr;
+      uint64_t* opre = nullptr;
+      APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
+      APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
+      k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovl, n_ovf, osz);
+      APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
+      const uint32_t g2 = (uint32_t)ctx->n_cu * 8;  // persistent: the flattened list's size stays on the device
+      k_sk_big_kmers<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovl, opre, n_ovf, nk);
+      unsigned long long nbk = 0;
+      APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      vlog(ctx, "sk count: %u buckets overflow the LDS table (%llu K-mers)", n_ovf, nbk);
+      // APG_SK_OVF=global: every overflowed K-mer through one global table
+      // (the round-4 path); default: sub-bucket counting in LDS
+      const char* oe = getenv("APG_SK_OVF");
+      const bool ovf_global = oe && !strcmp(oe, "global");
+      if (!ovf_global) {
+        // entries written once, moved by one level (count read + move), read
+        // by the count and the weak pass
+        kbegin(ctx, "sk_bucket_global", nbk * 16 * 6);
+        APG_TRY(ovf_lds_count<RB>(ctx, cur, boff, ovl, opre, n_ovf, p, nbk, solid, o, g2));
+      } else {
+        kbegin(ctx, "sk_bucket_global", nbk * 64);
+        BigTab g{};
+        uint64_t T = 0;
+        APG_TRY((big_count<RB, false>(ctx, cur, boff, ovl, opre, n_ovf, p, nbk, g2, nullptr, &g, &T)));
+        if (solid)
+          k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
+        else
+          k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
+        if constexpr (RecPos<RB>::value) {
+          if (o.weak || o.wrec)
+            k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovl, opre, n_ovf, p, g, min_solid, o);
+        }
+      }
+      kend(ctx);
+      APG_CHECK_HIP(hipGetLastError());
+      return APG_OK;
+    };
     uint64_t n_drec = 0;
     for (int attempt = 0;; ++attempt) {
+      // The heavy buckets (over kSkHeavyRecords records: repeat families,
+      // tandem arrays) always overflow; with record dedup they are listed
+      // before the bucket pass and counted on the side stream beside it
+      // (APG_SK_HEAVY_SIDE=0: after it, with the rest of the overflow).
+      uint32_t n_heavy = 0;
+      uint32_t* heavy = nullptr;
+      hipStream_t hs_side = nullptr;
+      o.skip_heavy = 0;
+      {
+        static const bool heavy_side = !(getenv("APG_SK_HEAVY_SIDE") && !strcmp(getenv("APG_SK_HEAVY_SIDE"), "0"));
+        if (heavy_side && dd && solid && attempt == 0 && nb) {
+          unsigned long long* nh = nullptr;
+          APG_TRY(workspace_t(ctx, "sk_heavy", std::max<uint64_t>(nb, 1), &heavy));
+          APG_TRY(workspace_t(ctx, "sk_nheavy", 1, &nh));
+          APG_CHECK_HIP(hipMemsetAsync(nh, 0, 8, ctx->stream));
+          k_sk_heavy<<<grid_for(ctx, nb), 256, 0, ctx->stream>>>(boff, nb, heavy, nh);
+          unsigned long long h = 0;
+          APG_CHECK_HIP(hipMemcpyAsync(&h, nh, 8, hipMemcpyDeviceToHost, ctx->stream));
+          APG_TRY(sync(ctx));
+          n_heavy = (uint32_t)h;
+          hs_side = n_heavy ? side_stream(ctx) : nullptr;
+          if (hs_side) {
+            // every workspace the overflow path uses is allocated before the
+            // bucket pass is queued (a grow would free under it)
+            o.skip_heavy = 1;
+            hipEvent_t ev = nullptr;
+            APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            APG_CHECK_HIP(hipEventRecord(ev, ctx->stream));
+            APG_CHECK_HIP(hipStreamWaitEvent(hs_side, ev, 0));
+            APG_CHECK_HIP(hipEventDestroy(ev));
+          } else {
+            n_heavy = 0;
+          }
+        }
+      }
       // Algorithmic bytes (inputs read once + outputs written once): the records
       // and bucket offsets; the weak output (one bit per K-mer instance, or a
       // 4-byte mask per record in the multi-GPU form); the solid list is added
@@ -2615,51 +2707,23 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       }
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
+      if (n_heavy) {  // beside the bucket pass, then joined into the main stream
+        {
+          StreamSwap sw(ctx, hs_side);
+          APG_TRY(run_ovf(heavy, n_heavy));
+        }
+        hipEvent_t ev = nullptr;
+        APG_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        APG_CHECK_HIP(hipEventRecord(ev, hs_side));
+        APG_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ev, 0));
+        APG_CHECK_HIP(hipEventDestroy(ev));
+      }
       unsigned long long hs[6];
       APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
       APG_TRY(sync(ctx));
       n_drec = hs[5];
-      if (hs[1]) {  // overflowed buckets: one global table
-        unsigned long long* nk = gstats + 3;
-        APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
-        const uint32_t n_ovf = (uint32_t)hs[1];
-        uint32_t* osz = nullptr;
-        uint64_t* opre = nullptr;
-        APG_TRY(workspace_t(ctx, "sk_osz", n_ovf, &osz));
-        APG_TRY(workspace_t(ctx, "sk_opre", (uint64_t)n_ovf + 1, &opre));
-        k_sk_ovf_sizes<<<(n_ovf + 255) / 256, 256, 0, ctx->stream>>>(boff, ovf, n_ovf, osz);
-        APG_TRY(scan_u32_u64(ctx, osz, n_ovf, opre, "sko"));
-        const uint32_t g2 = (uint32_t)ctx->n_cu * 8;  // persistent: the flattened list's size stays on the device
-        k_sk_big_kmers<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, nk);
-        unsigned long long nbk = 0;
-        APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
-        APG_TRY(sync(ctx));
-        vlog(ctx, "sk count: %llu buckets overflow the LDS table (%llu K-mers) -> global table", hs[1], nbk);
-        // APG_SK_OVF=global: every overflowed K-mer through one global table
-        // (the round-4 path); default: sub-bucket counting in LDS
-        const char* oe = getenv("APG_SK_OVF");
-        const bool ovf_global = oe && !strcmp(oe, "global");
-        if (!ovf_global) {
-          // entries written once, moved by one level (count read + move), read
-          // by the count and the weak pass
-          kbegin(ctx, "sk_bucket_global", nbk * 16 * 6);
-          APG_TRY(ovf_lds_count<RB>(ctx, cur, boff, ovf, opre, n_ovf, p, nbk, solid, o, g2));
-        } else {
-          kbegin(ctx, "sk_bucket_global", nbk * 64);
-          BigTab g{};
-          uint64_t T = 0;
-          APG_TRY((big_count<RB, false>(ctx, cur, boff, ovf, opre, n_ovf, p, nbk, g2, nullptr, &g, &T)));
-          if (solid)
-            k_sk_big_emit<true><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
-          else
-            k_sk_big_emit<false><<<grid_for(ctx, T), 256, 0, ctx->stream>>>(g.s, T, p, o);
-          if constexpr (RecPos<RB>::value) {
-            if (o.weak || o.wrec)
-              k_sk_big_weak<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, min_solid, o);
-          }
-        }
-        kend(ctx);
-        APG_CHECK_HIP(hipGetLastError());
+      if (hs[1]) {  // overflowed buckets (the LDS table filled)
+        APG_TRY(run_ovf(ovf, (uint32_t)hs[1]));
         APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
         APG_TRY(sync(ctx));
       }
@@ -2691,7 +2755,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           kbytes_add(ctx, "sk_bucket_solid", n_solid * 8);
         }
         res->n_distinct = hs[0];
-        res->n_overflow_buckets = hs[1];
+        res->n_overflow_buckets = hs[1] + n_heavy;
         res->n_solid = n_solid;
         res->solid = dense;
         res->nbuckets = nb;
