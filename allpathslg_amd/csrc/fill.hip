@@ -614,6 +614,139 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     // bridge K-mer, or a cached branch point) follows in the same iteration:
     // at most one lookup per iteration, up to xsteps & 255 free steps after
     // it (cached branch points among them if xsteps & 256).
+    // one walk step (LEAN: the lookup step, then at most one free step,
+    // written out twice instead of an inner loop — fewer values carried
+    // around a back edge: repeat-rich `fill` 38.1 -> 35.3 ms, iid 10.55 ->
+    // 10.21 ms on one box); true when the pair's search ended
+    auto step = [&]() -> bool {
+      const bool cached = bcache && mode == 2 && dd < 32;
+      const uint64_t key = wk;
+      uint32_t m, m2 = 0;
+      if (cached) {
+        m = mask_at(dd);
+      } else if (pq & 16) {
+        m = pq & 15;
+      } else {
+        const uint32_t x = ext_succ2<KS, LEAN ? 1 : 0>(t, key, &nlook);
+        m = x & 15;
+        m2 = x >> 4;
+      }
+      pq &= ~0xffu;
+      bool visit = false, done = false;
+      if (mode == 0) {  // node (pv, d)
+        mnode = m;
+        pq = m2 << 8;
+        visit = true;
+        if (d >= dlo && ((m >> fb0) & 1) && ((bk >> (key & 15)) & 1)) {  // closure test: the K-1 bridge K-mers
+          if (jend > 1) {
+            mode = 1;
+            j = 1;
+            wk = ((key << 2) | fb0) & t.m1;
+            pq |= m2;  // m2 is set only if fb0 is the one successor
+            visit = false;
+          } else if (closure()) {
+            done = true;
+            visit = false;
+          }
+        }
+      } else if (mode == 1) {  // bridge K-mer j of the closure test at depth d
+        const uint32_t b = (uint32_t)(f0 >> (2 * j)) & 3;
+        const bool ok = (m >> b) & 1;
+        if (ok && (int)j + 1 < jend) {
+          wk = ((wk << 2) | b) & t.m1;
+          ++j;
+          pq |= m2;
+        } else if (ok && closure()) {
+          done = true;
+        } else {
+          mode = 0;
+          visit = true;
+        }
+      } else if (mode == 3) {  // bridge filter: predecessors of G, then of c1 ++ G[0, K-2)
+        const uint32_t pm = rev4(m);  // pred(x) bit c = succ(rc(x)) bit 3 - c
+        if (j == 16) {
+          j = pm;
+        } else {
+          const uint32_t c1 = __ffs(j) - 1;
+          bk |= ((pm & 1) | ((pm & 2) << 3) | ((pm & 4) << 6) | ((pm & 8) << 9)) << c1;
+          j &= j - 1;
+        }
+        if (j == 0) {
+          mode = 0;  // the walk from depth 0
+          wk = atail;
+        } else {
+          wk = bkey();
+        }
+      } else {  // open branch point at depth dd: the sibling after the base taken there
+        const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
+        const uint32_t rest = m & ~((2u << bb) - 1);
+        const uint32_t b2 = __ffs(rest) - 1;  // rest != 0: dd was marked open
+        if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
+        pv = ((pv >> (2 * (d - dd))) << 2) | b2;
+        d = dd + 1;
+        mode = 0;
+        wk = ((key << 2) | b2) & t.m1;  // key: the window at dd
+      }
+      if (visit) {  // the walk's step from node (pv, d) with successor mask mnode
+        bool down = false;
+        if (d < gmax) {
+          if (++steps > cap) {
+            budget = true;
+            done = true;
+          } else if (mnode) {
+            const uint32_t b = __ffs(mnode) - 1;
+            if (mnode >> (b + 1)) {
+              brm |= 1ull << d;
+              if (d < 32) mask_set(d, mnode);  // an open branch point: its mask for the backtracks
+            }
+            pv = (pv << 2) | b;
+            ++d;
+            down = true;
+            wk = walk_window(atail, pv, d, t);  // the child's window
+            pq |= (pq >> 8) & 0xffu;  // set only if b is the node's one successor
+          }
+        }
+        if (!done && !down) {
+          if (!brm) {
+            done = true;  // search exhausted
+          } else {
+            dd = 63 - __clzll((long long)brm);
+            const uint64_t wdd = walk_window(atail, pv >> (2 * (d - dd)), dd, t);
+            if (fuse && dd < 32) {
+              // the backtrack to a branch point whose mask its visit kept:
+              // taken now (mode 2's transition), so the sibling's lookup is
+              // the next iteration's, not the one after an iteration with
+              // no lookup for this lane
+              const uint32_t bb = (uint32_t)(pv >> (2 * (d - dd - 1))) & 3;
+              const uint32_t rest = mask_at(dd) & ~((2u << bb) - 1);
+              const uint32_t b2 = __ffs(rest) - 1;
+              if (!(rest >> (b2 + 1))) brm &= ~(1ull << dd);
+              pv = ((pv >> (2 * (d - dd))) << 2) | b2;
+              d = dd + 1;
+              mode = 0;
+              wk = ((wdd << 2) | b2) & t.m1;
+            } else {
+              mode = 2;
+              wk = wdd;
+            }
+          }
+        }
+      }
+      return done;
+    };
+    if constexpr (LEAN) {
+      bool done = step();
+      if (!done) {
+        const bool can = (pq & 16) != 0;
+        if ((uint32_t)__popcll(__ballot(can)) * 100u >= (uint32_t)__popcll(__ballot(true)) * (uint32_t)kFillXpct && can)
+          done = step();
+      }
+      if (done) {
+        act = false;
+        conclude();
+      }
+      continue;
+    }
     for (int xs = 0;; ++xs) {
       // ---- one lookup (a node or a closure's bridge K-mer; an open branch
       // point at depth dd < d reads the mask its visit kept)
