@@ -598,8 +598,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   };
 
   bool more = true;
+  bool fin = false;  // LEAN: a finished pair not concluded yet
   for (;;) {
     while (more && __popcll(__ballot(act)) <= refill) {  // refill the idle lanes (wave-uniform)
+      if (LEAN && fin) {  // a finished pair's status, before its lane takes new work
+        conclude();
+        fin = false;
+      }
       const uint64_t idle = __ballot(!act);
       const unsigned long long k = wave_append(next, !act);  // the wave's next popc(idle) work items
       more = __shfl(k, 63 - __clzll((long long)idle), 64) + 1 < nwork;
@@ -619,7 +624,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     // around a back edge: repeat-rich `fill` 38.1 -> 35.3 ms, iid 10.55 ->
     // 10.21 ms on one box); true when the pair's search ended
     auto step = [&]() -> bool {
-      const bool cached = bcache && mode == 2 && dd < 32;
+      // LEAN fuses every backtrack to a cached branch point into its visit:
+      // mode 2 is left only for depths >= 32, which are never cached
+      const bool cached = !LEAN && bcache && mode == 2 && dd < 32;
       const uint64_t key = wk;
       uint32_t m, m2 = 0;
       if (cached) {
@@ -741,9 +748,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if ((uint32_t)__popcll(__ballot(can)) * 100u >= (uint32_t)__popcll(__ballot(true)) * (uint32_t)kFillXpct && can)
           done = step();
       }
-      if (done) {
+      if (done) {  // its status goes out at the wave's next refill (or at the end)
         act = false;
-        conclude();
+        fin = true;
       }
       continue;
     }
@@ -879,6 +886,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       }
     }
   }
+  if (LEAN && fin) conclude();
   wave_add(&cnt->st[kFillOk], c_ok);
   wave_add(&cnt->st[kFillNone], c_none);
   wave_add(&cnt->st[kFillAmbiguous], c_amb);
