@@ -250,6 +250,70 @@ struct SkWalker {
   }
 };
 
+constexpr uint32_t kSkChunk = 16;  // bases per walk chunk (one prefetched word)
+
+// The walk with the van Herk column in registers, for a window length WN = w
+// known at compile time: a block of w m-mers is one unrolled pass whose
+// offset t is a constant, so the column col[t] is a register — no LDS column
+// and, for long windows, no second-level re-hash (the two-level column
+// hashes every m-mer twice; this walk hashes it once).  Records as SkWalker's
+// over the read's Lw bases (Lw = 0: none; else Lw >= K), handed to
+// push(a, n, key).  Lanes past their read run on with their records frozen;
+// the block loop ends when no lane of the wave has m-mers left (the base
+// accessor must tolerate reads past the read: SkLdsBases clamps to its tile).
+template <int WN, typename U, typename P, typename LB, typename F>
+__device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32_t Lw, F push) {
+  if (__ballot(Lw != 0) == 0) return;
+  const uint32_t m = (uint32_t)p.m, maxnk = (uint32_t)p.maxnk, rsh = 2 * m - 2;
+  const U mmask = (U)p.mmask;
+  const uint32_t nm = Lw ? Lw + 1 - m : 0;  // the read's m-mers
+  uint32_t cur = bases.at(0), nxt = bases.at(kSkChunk), j = 0;
+  U fw = 0, rc = 0;
+  auto roll = [&]() {  // base j (wave-uniform: every lane is at the same base)
+    if (j % kSkChunk == 0 && j) {
+      cur = nxt;
+      nxt = bases.at(j + kSkChunk);
+    }
+    const uint32_t b = (cur >> (2 * (j % kSkChunk))) & 3u;
+    fw = ((fw << 2) | (U)b) & mmask;
+    rc = (rc >> 2) | ((U)(3u - b) << rsh);
+    ++j;
+  };
+  while (j + 1 < m) roll();
+  uint32_t col[WN], pre = 0;
+#pragma unroll
+  for (int t = 0; t < WN; ++t) {  // block 0: m-mers [0, w), the first K-mer at its end
+    roll();
+    const uint32_t v = sk_order<U>(fw < rc ? fw : rc);
+    pre = t == 0 ? v : min(pre, v);
+    col[t] = v;
+  }
+  uint32_t key = pre, ra = 0, rn = 1;
+  for (uint32_t x0 = WN; __ballot(x0 < nm) != 0; x0 += WN) {
+#pragma unroll
+    for (int u = WN - 2; u >= 0; --u) col[u] = min(col[u], col[u + 1]);  // the finished block's suffix minima
+#pragma unroll
+    for (int t = 0; t < WN; ++t) {  // m-mer x0 + t closes K-mer x0 + t + 1 - w
+      roll();
+      const uint32_t v = sk_order<U>(fw < rc ? fw : rc);
+      pre = t == 0 ? v : min(pre, v);
+      const uint32_t kk = t + 1 < WN ? min(col[t + 1], pre) : pre;
+      col[t] = v;  // the previous block's col[t] was read one step ago
+      if (x0 + t < nm) {
+        if (kk == key && rn < maxnk) {
+          ++rn;
+        } else {
+          push(ra, rn, key);
+          key = kk;
+          ra = x0 + t + 1 - WN;
+          rn = 1;
+        }
+      }
+    }
+  }
+  if (Lw) push(ra, rn, key);
+}
+
 // Record descriptors the count pass keeps so the scatter pass need not walk
 // the reads again: block b's go to desc[lo(r0), lo(r1)), lo(r) = base_off[r]
 // / div (the block's share of a bases / div budget), tile by tile, with each
@@ -355,15 +419,14 @@ struct SkList {
   uint32_t cnt;
   uint64_t d[CAP];
 };
-constexpr uint32_t kSkChunk = 16;  // bases per walk chunk (one prefetched word)
-
 // Every thread of the block walks the tile's read q = threadIdx.x (if any)
 // in chunks of kSkChunk bases.  LIST: between chunks the block drains the
 // list when it is half full (and after the last chunk) — for an f that is
 // costly per call (building and storing a record); otherwise f runs in place
 // (a pair of LDS atomics).  f(rd, L, a, n, key, q) per record, in no
-// particular order.  Block-uniform.
-template <int NT, bool TWO, bool LIST, typename P, typename TT, int CAP, typename F>
+// particular order.  Block-uniform.  WN > 0 (no LIST, WN == p.w): the walk
+// with the column in registers (sk_walk_regs).
+template <int NT, bool TWO, bool LIST, int WN = 0, typename P, typename TT, int CAP, typename F>
 __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n, uint32_t* sb, SkList<CAP>& lst,
                                              F f) {
   const uint32_t q = threadIdx.x;
@@ -388,6 +451,10 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
     else
       emit(d);  // list full: this record alone, in place
   };
+  if constexpr (!LIST && WN > 0) {
+    sk_walk_regs<WN, typename P::U>(p, W.bases, Lw, push);
+    return;
+  }
   if constexpr (!LIST) {  // no barriers: each lane walks its own read to its end
     uint32_t cur = Lw ? W.bases.at(0) : 0, nxt = Lw > kSkChunk ? W.bases.at(kSkChunk) : 0;
     uint32_t a, nk, k;

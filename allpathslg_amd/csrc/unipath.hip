@@ -101,11 +101,10 @@ __device__ __forceinline__ K3 rc_roll(const K3& r, uint64_t base, const KeyP& p)
   return o;
 }
 
-__device__ __forceinline__ uint64_t rev2(uint64_t x) {  // reverse the 32 2-bit groups
-  x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
-  x = ((x >> 4) & 0x0f0f0f0f0f0f0f0full) | ((x & 0x0f0f0f0f0f0f0f0full) << 4);
-  return __builtin_bswap64(x);
-}
+// reverse the 32 2-bit groups: per 32-bit half a bit reverse, then the bits
+// of each pair swapped back (v_bfrev + two shifts + one v_bfi: 8 VALU for the
+// 64 bits, against 17 for the mask-and-shift ladder with a byte swap)
+__device__ __forceinline__ uint64_t rev2(uint64_t x) { return sk_rev2(x); }
 
 // x >> s for a 192-bit (a:b:c) value, 0 <= s <= 192
 __device__ __forceinline__ K3 shr192(const K3& x, int s) {
@@ -1313,7 +1312,9 @@ struct UskP {
   int K, m, w, maxnk;
   uint64_t mmask;
   int two;  // the two-level column (w > kUskWalk2MinW; APG_USK_FLAT=1: single-level for every w)
+  int reg;  // the count walk keeps its column in registers (w == kUskRegW; APG_USK_REG=0: off)
 };
+constexpr int kUskRegW = 66;  // the window of the K = 96 walk (m = 31)
 
 __host__ __device__ inline uint32_t usk_column_words(const UskP& p) {
   return (uint32_t)(p.two ? sk_walk2_words(p.w) : p.w) * kUskThreads;
@@ -1334,6 +1335,11 @@ static UskP make_uskp(int K) {
     return e && !strcmp(e, "1");
   }();
   p.two = !flat && p.w > kUskWalk2MinW;
+  static const bool reg = [] {
+    const char* e = getenv("APG_USK_REG");
+    return !(e && !strcmp(e, "0"));
+  }();
+  p.reg = reg && p.w == kUskRegW;
   return p;
 }
 
@@ -1362,7 +1368,9 @@ __device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p,
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n) {
-      if (two)
+      if (!LIST && p.reg)
+        sk_walk_tile<kUskThreads, true, LIST, kUskRegW>(p, T, n, sb, lst, f);
+      else if (two)
         sk_walk_tile<kUskThreads, true, LIST>(p, T, n, sb, lst, f);
       else
         sk_walk_tile<kUskThreads, false, LIST>(p, T, n, sb, lst, f);
