@@ -252,18 +252,52 @@ struct SkWalker {
 
 constexpr uint32_t kSkChunk = 16;  // bases per walk chunk (one prefetched word)
 
+// A wave's record queue: a ring of CAPW descriptors in LDS.  Lanes whose
+// record closed at this base append it (ballot + mbcnt); every few bases the
+// wave hands the pending ones out 64 at a time — emission (the digit counts,
+// the descriptor store) then runs on full waves, not once per base for the
+// few lanes whose record closed there.  head / tail are wave-uniform; the
+// caller drains often enough that fewer than CAPW are ever pending.
+template <uint32_t CAPW>
+struct SkWaveQ {
+  uint64_t* q;
+  uint32_t head = 0, tail = 0;
+  __device__ __forceinline__ void push(bool c, uint64_t d) {
+    const uint64_t m = __ballot(c);
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (c) q[(tail + r) & (CAPW - 1)] = d;
+    tail += (uint32_t)__popcll(m);
+  }
+  template <typename E>
+  __device__ __forceinline__ void drain(E emit) {  // every full wave's worth
+    for (; tail - head >= 64; head += 64) emit(q[(head + __lane_id()) & (CAPW - 1)]);
+  }
+  template <typename E>
+  __device__ __forceinline__ void flush(E emit) {
+    drain(emit);
+    if (__lane_id() < tail - head) emit(q[(head + __lane_id()) & (CAPW - 1)]);
+    head = tail;
+  }
+};
+
 // The walk with the van Herk column in registers, for a window length WN = w
 // known at compile time: a block of w m-mers is one unrolled pass whose
 // offset t is a constant, so the column col[t] is a register — no LDS column
 // and, for long windows, no second-level re-hash (the two-level column
 // hashes every m-mer twice; this walk hashes it once).  Records as SkWalker's
-// over the read's Lw bases (Lw = 0: none; else Lw >= K), handed to
-// push(a, n, key).  Lanes past their read run on with their records frozen;
-// the block loop ends when no lane of the wave has m-mers left (the base
-// accessor must tolerate reads past the read: SkLdsBases clamps to its tile).
-template <int WN, typename U, typename P, typename LB, typename F>
-__device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32_t Lw, F push) {
+// over the read's Lw bases (Lw = 0: none; else Lw >= K), as descriptors
+// key | a << 32 | n << 48 | q << 56 through the wave's queue `wq`
+// (SkWaveQ<CAPW>, drained every S bases: 64 + 64 S <= CAPW) to emit(d).  Lanes past their read run on with their records frozen; the
+// block loop ends when no lane of the wave has m-mers left (the base accessor
+// must tolerate reads past the read: SkLdsBases clamps to its tile).  Every
+// lane of the wave calls it.
+template <int WN, int S, uint32_t CAPW, typename U, typename P, typename LB, typename E>
+__device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32_t Lw, uint32_t q, uint64_t* wq,
+                                             E emit) {
+  static_assert(64 + 64 * S <= CAPW && (CAPW & (CAPW - 1)) == 0, "queue ring");
   if (__ballot(Lw != 0) == 0) return;
+  SkWaveQ<CAPW> Q{wq};
+  const uint64_t qd = (uint64_t)q << 56;
   const uint32_t m = (uint32_t)p.m, maxnk = (uint32_t)p.maxnk, rsh = 2 * m - 2;
   const U mmask = (U)p.mmask;
   const uint32_t nm = Lw ? Lw + 1 - m : 0;  // the read's m-mers
@@ -278,6 +312,9 @@ __device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32
     fw = ((fw << 2) | (U)b) & mmask;
     rc = (rc >> 2) | ((U)(3u - b) << rsh);
     ++j;
+  };
+  auto desc = [&](uint32_t a, uint32_t n, uint32_t key) {
+    return (uint64_t)key | ((uint64_t)a << 32) | ((uint64_t)n << 48) | qd;
   };
   while (j + 1 < m) roll();
   uint32_t col[WN], pre = 0;
@@ -299,19 +336,20 @@ __device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32
       pre = t == 0 ? v : min(pre, v);
       const uint32_t kk = t + 1 < WN ? min(col[t + 1], pre) : pre;
       col[t] = v;  // the previous block's col[t] was read one step ago
-      if (x0 + t < nm) {
-        if (kk == key && rn < maxnk) {
-          ++rn;
-        } else {
-          push(ra, rn, key);
-          key = kk;
-          ra = x0 + t + 1 - WN;
-          rn = 1;
-        }
+      const bool live = x0 + t < nm;
+      const bool closed = live && !(kk == key && rn < maxnk);
+      const uint64_t d = desc(ra, rn, key);
+      if (live) {
+        rn = closed ? 1u : rn + 1;
+        ra = closed ? x0 + t + 1 - WN : ra;
+        key = kk;
       }
+      Q.push(closed, d);
+      if (t % S == S - 1 || t == WN - 1) Q.drain(emit);
     }
   }
-  if (Lw) push(ra, rn, key);
+  Q.push(Lw != 0, desc(ra, rn, key));
+  Q.flush(emit);
 }
 
 // Record descriptors the count pass keeps so the scatter pass need not walk
@@ -451,8 +489,12 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
     else
       emit(d);  // list full: this record alone, in place
   };
-  if constexpr (!LIST && WN > 0) {
-    sk_walk_regs<WN, typename P::U>(p, W.bases, Lw, push);
+  if constexpr (!LIST && WN > 0) {  // the waves' queues in the (unused) LDS column
+    constexpr int S = WN >= 32 ? 4 : 2;
+    constexpr uint32_t CAPW = S == 4 ? 512 : 256;
+    static_assert((TWO ? sk_walk2_words(WN) : WN) * 32 >= (int)CAPW, "the column holds the waves' queues");
+    uint64_t* wq = reinterpret_cast<uint64_t*>(sb - q) + (q / 64) * CAPW;
+    sk_walk_regs<WN, S, CAPW, typename P::U>(p, W.bases, Lw, q, wq, emit);
     return;
   }
   if constexpr (!LIST) {  // no barriers: each lane walks its own read to its end
