@@ -78,7 +78,8 @@ struct SkP {
   // the count walk keeps its column in registers (w == kSkRegW or kSkRegW + 1; APG_SK_REG=0: off)
   bool reg = false;
 };
-constexpr int kSkRegW = 9;  // the windows of the K = 24 and K = 25 walks (m = 16)
+constexpr int kSkRegW = 9;  // the windows of the K = 24 and K = 25 walks (m = kSkRegM)
+constexpr int kSkRegM = 16;
 __host__ __device__ inline uint32_t sk_pieces(uint32_t n, uint32_t split) {
   return split && n > split ? (n + split - 1) / split : 1u;
 }
@@ -99,7 +100,7 @@ static SkP make_skp(int K) {
     const char* e = getenv("APG_SK_REG");
     return !(e && !strcmp(e, "0"));
   }();
-  p.reg = reg && (p.w == kSkRegW || p.w == kSkRegW + 1);
+  p.reg = reg && p.m == kSkRegM && (p.w == kSkRegW || p.w == kSkRegW + 1);
   return p;
 }
 
@@ -158,9 +159,9 @@ __global__ void __launch_bounds__(kSkThreads) k_sk_count(SkReads rv, SkP p, int 
   for (uint64_t t0 = r0; t0 < r1;) {
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n && p.reg && p.w == kSkRegW)
-      sk_walk_tile<kSkThreads, false, false, kSkRegW>(p, T, n, sbuf + threadIdx.x, lst, f);
+      sk_walk_tile<kSkThreads, false, false, kSkRegW, kSkRegM>(p, T, n, sbuf + threadIdx.x, lst, f);
     else if (n && p.reg)
-      sk_walk_tile<kSkThreads, false, false, kSkRegW + 1>(p, T, n, sbuf + threadIdx.x, lst, f);
+      sk_walk_tile<kSkThreads, false, false, kSkRegW + 1, kSkRegM>(p, T, n, sbuf + threadIdx.x, lst, f);
     else if (n)
       sk_walk_tile<kSkThreads, false, false>(p, T, n, sbuf + threadIdx.x, lst, f);
     else

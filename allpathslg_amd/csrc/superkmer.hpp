@@ -120,6 +120,14 @@ struct SkLdsBases {
     const uint32_t i = min(bo >> 5, NWORDS - 2);  // prefetches past the tile read stale words, never past W
     return __builtin_amdgcn_alignbit(W[i + 1], W[i], bo & 31);
   }
+  // at(x) in two halves for x a multiple of 16 (bit offset bit0 mod 32): the
+  // aligned words now, joined when needed, so a prefetch's LDS latency is
+  // not waited on at the load
+  __device__ __forceinline__ uint2 words(uint32_t x) const {
+    const uint32_t i = min((bit0 + 2 * x) >> 5, NWORDS - 2);
+    return make_uint2(W[i], W[i + 1]);
+  }
+  __device__ __forceinline__ uint32_t join(uint2 w) const { return __builtin_amdgcn_alignbit(w.y, w.x, bit0 & 31); }
 };
 struct SkGlobalBases {
   const uint8_t* rd;
@@ -291,22 +299,26 @@ struct SkWaveQ {
 // block loop ends when no lane of the wave has m-mers left (the base accessor
 // must tolerate reads past the read: SkLdsBases clamps to its tile).  Every
 // lane of the wave calls it.
-template <int WN, int S, uint32_t CAPW, typename U, typename P, typename LB, typename E>
+// MM = p.m, also fixed at compile time (the rolls' shifts and mask constant).
+template <int WN, int MM, int S, uint32_t CAPW, typename U, typename P, typename LB, typename E>
 __device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32_t Lw, uint32_t q, uint64_t* wq,
                                              E emit) {
   static_assert(64 + 64 * S <= CAPW && (CAPW & (CAPW - 1)) == 0, "queue ring");
+  static_assert(2 * MM <= 8 * (int)sizeof(U), "m-mer register");
   if (__ballot(Lw != 0) == 0) return;
   SkWaveQ<CAPW> Q{wq};
   const uint64_t qd = (uint64_t)q << 56;
-  const uint32_t m = (uint32_t)p.m, maxnk = (uint32_t)p.maxnk, rsh = 2 * m - 2;
-  const U mmask = (U)p.mmask;
+  constexpr uint32_t m = MM, rsh = 2 * MM - 2;
+  const uint32_t maxnk = (uint32_t)p.maxnk;
+  constexpr U mmask = 2 * MM == 8 * sizeof(U) ? ~(U)0 : (((U)1 << (2 * MM)) - 1);
   const uint32_t nm = Lw ? Lw + 1 - m : 0;  // the read's m-mers
-  uint32_t cur = bases.at(0), nxt = bases.at(kSkChunk), j = 0;
+  uint32_t cur = bases.at(0), j = 0;
+  uint2 nxt = bases.words(kSkChunk);
   U fw = 0, rc = 0;
   auto roll = [&]() {  // base j (wave-uniform: every lane is at the same base)
     if (j % kSkChunk == 0 && j) {
-      cur = nxt;
-      nxt = bases.at(j + kSkChunk);
+      cur = bases.join(nxt);
+      nxt = bases.words(j + kSkChunk);
     }
     const uint32_t b = (cur >> (2 * (j % kSkChunk))) & 3u;
     fw = ((fw << 2) | (U)b) & mmask;
@@ -462,9 +474,9 @@ struct SkList {
 // list when it is half full (and after the last chunk) — for an f that is
 // costly per call (building and storing a record); otherwise f runs in place
 // (a pair of LDS atomics).  f(rd, L, a, n, key, q) per record, in no
-// particular order.  Block-uniform.  WN > 0 (no LIST, WN == p.w): the walk
-// with the column in registers (sk_walk_regs).
-template <int NT, bool TWO, bool LIST, int WN = 0, typename P, typename TT, int CAP, typename F>
+// particular order.  Block-uniform.  WN > 0 (no LIST, WN == p.w, MM == p.m):
+// the walk with the column in registers (sk_walk_regs).
+template <int NT, bool TWO, bool LIST, int WN = 0, int MM = 0, typename P, typename TT, int CAP, typename F>
 __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n, uint32_t* sb, SkList<CAP>& lst,
                                              F f) {
   const uint32_t q = threadIdx.x;
@@ -494,7 +506,7 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
     constexpr uint32_t CAPW = S == 4 ? 512 : 256;
     static_assert((TWO ? sk_walk2_words(WN) : WN) * 32 >= (int)CAPW, "the column holds the waves' queues");
     uint64_t* wq = reinterpret_cast<uint64_t*>(sb - q) + (q / 64) * CAPW;
-    sk_walk_regs<WN, S, CAPW, typename P::U>(p, W.bases, Lw, q, wq, emit);
+    sk_walk_regs<WN, MM, S, CAPW, typename P::U>(p, W.bases, Lw, q, wq, emit);
     return;
   }
   if constexpr (!LIST) {  // no barriers: each lane walks its own read to its end

@@ -1314,7 +1314,8 @@ struct UskP {
   int two;  // the two-level column (w > kUskWalk2MinW; APG_USK_FLAT=1: single-level for every w)
   int reg;  // the count walk keeps its column in registers (w == kUskRegW; APG_USK_REG=0: off)
 };
-constexpr int kUskRegW = 66;  // the window of the K = 96 walk (m = 31)
+constexpr int kUskRegW = 66;  // the window of the K = 96 walk (m = kUskRegM)
+constexpr int kUskRegM = 31;
 
 __host__ __device__ inline uint32_t usk_column_words(const UskP& p) {
   return (uint32_t)(p.two ? sk_walk2_words(p.w) : p.w) * kUskThreads;
@@ -1339,7 +1340,7 @@ static UskP make_uskp(int K) {
     const char* e = getenv("APG_USK_REG");
     return !(e && !strcmp(e, "0"));
   }();
-  p.reg = reg && p.w == kUskRegW;
+  p.reg = reg && p.w == kUskRegW && p.m == kUskRegM;
   return p;
 }
 
@@ -1369,7 +1370,7 @@ __device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p,
     const uint32_t n = sk_load_tile(rv, t0, r1, T);
     if (n) {
       if (!LIST && p.reg)
-        sk_walk_tile<kUskThreads, true, LIST, kUskRegW>(p, T, n, sb, lst, f);
+        sk_walk_tile<kUskThreads, true, LIST, kUskRegW, kUskRegM>(p, T, n, sb, lst, f);
       else if (two)
         sk_walk_tile<kUskThreads, true, LIST>(p, T, n, sb, lst, f);
       else

@@ -106,7 +106,7 @@ int main(int argc, char** argv) {
   if (!rd(reads, 1, nr * L, f)) return 1;
   fclose(f);
 
-  uint64_t st[4] = {0}, look[4][3] = {{0}}, filt_pre = 0, filt_bridge = 0;
+  uint64_t st[4] = {0}, look[4][3] = {{0}}, filt_pre = 0, filt_bridge = 0, vis_tot[4] = {0}, vis_dist[4] = {0};
   /* per-pair caches keyed by position: node windows by depth (1-way, 2-way
      most-recent-first), bridge K-mer j's window by j */
   uint64_t hit_n1 = 0, hit_n2 = 0, hit_b = 0, hit_bf = 0;
@@ -172,11 +172,28 @@ int main(int argc, char** argv) {
     for (int t = 0; t < 64; t++) ck[t][0] = ck[t][1] = ~0ull;
     for (int t = 0; t < 32; t++) cb[t] = ~0ull;
     int budget = 0, stop = 0;
+    /* distinct walk states (depth, window) of this pair: what a memoised
+       walk would look up (duplicates share their subtree) */
+    static uint64_t vs_k[4096];
+    memset(vs_k, 0xff, sizeof vs_k);
+    uint64_t nvis = 0, ndist = 0;
     for (;;) {  /* visit node (path[0, d)) */
       uint64_t w = atail;
       for (uint32_t t = 0; t < d; t++) w = ((w << 2) | path[t]) & m1;
       const uint32_t m = succ(w);
       ln++;
+      {
+        const uint64_t key = (w << 6) | d;
+        nvis++;
+        for (uint64_t g = mix(key) & 4095;; g = (g + 1) & 4095) {
+          if (vs_k[g] == key) break;
+          if (vs_k[g] == ~0ull) {
+            vs_k[g] = key;
+            ndist++;
+            break;
+          }
+        }
+      }
       phys[d] = !known;
       two_node += !known;
       known = 0;
@@ -244,9 +261,13 @@ int main(int argc, char** argv) {
     }
     const int s = nclos >= 2 ? 2 : budget ? 3 : nclos ? 0 : 1;
     st[s]++;
+    vis_tot[s] += nvis, vis_dist[s] += ndist;
     look[s][0] += ln, look[s][1] += lb, look[s][2] += lk;
   }
   static const char* nm[4] = {"filled", "none", "ambiguous", "budget"};
+  for (int s = 0; s < 4; s++)
+    printf("%-9s node visits %11llu, distinct (depth, window) states %11llu\n", nm[s],
+           (unsigned long long)vis_tot[s], (unsigned long long)vis_dist[s]);
   uint64_t tot = 0, br = 0;
   for (int s = 0; s < 4; s++) {
     printf("%-9s pairs %10llu  walk lookups: node %11llu bridge %11llu backtrack %9llu\n", nm[s],
