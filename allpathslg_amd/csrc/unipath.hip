@@ -1485,7 +1485,7 @@ struct UskOut {
   unsigned long long* idx;
   uint64_t tmask, idx_lim;
   // diagnostics (APG_USK_PROF): thread 0's clock64 sums per phase — chunk
-  // load + dedup, scan + owner map, inserts, node emission, local links
+  // load + dedup, scan + owner map, inserts, node ranks, nodes + index + local links
   unsigned long long* prof = nullptr;
 };
 
@@ -1706,41 +1706,46 @@ k_usk_bucket(const SK48* __restrict__ rec,
     for (uint32_t s = tid; s < kUskTab; s += kUskBThreads) nn += tag[s] != 0;
     uint32_t tot;
     uint32_t j = block_exclusive_scan<uint32_t>(nn, scan_sm, &tot);
-    if (tid == 0) sbase = tot ? atomicAdd(&o.gs[0], (unsigned long long)tot) : 0ull;
-    __syncthreads();
-    const unsigned long long b = sbase;
+    // the bucket's node ids: the add is in flight while the ranks are written
+    unsigned long long b0 = 0;
+    if (tid == 0 && tot) b0 = atomicAdd(&o.gs[0], (unsigned long long)tot);
     for (uint32_t s = tid; s < kUskTab; s += kUskBThreads)
       if (tag[s] != 0) {
         rnk[s] = (uint16_t)j;  // owner and crec are free: every instance is inserted
-        slot_of[j] = (uint16_t)s;
-        const unsigned long long at = b + j++;
-        if (at < o.cap) {
-          const K3 k{ka[s], kb[s], kc[s]};
-          const uint64_t kh = key_hash(k);
-          o.nodes[at] = KRec{k.a, k.b, k.c, kh | text[s]};
-          if (o.idx) {  // index entry as k_node_insert makes it; load <= 1/2 by idx_lim
-            if (at < o.idx_lim) {
-              const uint64_t h = kh >> 8;
-              const unsigned long long want = ((unsigned long long)idx_tag(h) << 32) | at;
-              uint64_t q = h & o.tmask;
-              while (atomicCAS(&o.idx[q], kIdxEmpty, want) != kIdxEmpty) q = (q + 1) & o.tmask;
-            } else {
-              atomicAdd(&o.gs[4], 1ull);
-            }
-          }
+        slot_of[j++] = (uint16_t)s;
+      }
+    if (tid == 0) sbase = b0;
+    __syncthreads();  // every slot's rank, the base
+    const unsigned long long b = sbase;
+    mark(4);
+    // The nodes by rank (full lanes): the node, its index entry, its local
+    // links.  The index insert's first probe is in flight during the links;
+    // a taken slot probes on after them (load <= 1/2 by idx_lim).
+    for (uint32_t r = tid; r < tot; r += kUskBThreads) {
+      const uint32_t s = slot_of[r];
+      const unsigned long long id = b + r;
+      if (id >= o.cap) continue;
+      const K3 key{ka[s], kb[s], kc[s]};
+      const uint32_t ext = text[s];
+      const uint64_t kh = key_hash(key);
+      o.nodes[id] = KRec{key.a, key.b, key.c, kh | ext};
+      bool ix = false;  // index entry as k_node_insert makes it
+      uint64_t q = 0;
+      unsigned long long want = 0, prev = kIdxEmpty;
+      if (o.idx) {
+        if (id < o.idx_lim) {
+          const uint64_t h = kh >> 8;
+          want = ((unsigned long long)idx_tag(h) << 32) | id;
+          q = h & o.tmask;
+          prev = atomicCAS(&o.idx[q], kIdxEmpty, want);
+          ix = true;
+        } else {
+          atomicAdd(&o.gs[4], 1ull);
         }
       }
-    mark(4);
-    if (o.lsucc) {  // block-uniform
-      __syncthreads();  // every slot's rank
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) {  // the occupied slots only: full lanes
-        const uint32_t s = slot_of[r];
-        const unsigned long long id = b + r;
-        if (id >= o.cap) continue;
+      if (o.lsucc) {  // block-uniform
         // the rules of k_links, with the successor looked up in this table
-        const K3 key{ka[s], kb[s], kc[s]};
         const K3 rk = revcomp(key, kp);
-        const uint32_t ext = text[s];
         uint32_t res[2] = {kNone, kNone};
         if (!k3_eq(key, rk)) {  // palindromic K-mers never link
 #pragma unroll
@@ -1775,6 +1780,11 @@ k_usk_bucket(const SK48* __restrict__ rec,
           }
         }
         o.lsucc[id] = make_uint2(res[0], res[1]);
+      }
+      if (ix && prev != kIdxEmpty) {
+        do {
+          q = (q + 1) & o.tmask;
+        } while (atomicCAS(&o.idx[q], kIdxEmpty, want) != kIdxEmpty);
       }
     }
     __syncthreads();
@@ -2585,7 +2595,7 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
       unsigned long long hp[5];
       APG_TRY(d2h_u64(ctx, dp, hp, 5));
       const double tot = (double)(hp[0] + hp[1] + hp[2] + hp[3] + hp[4]) + 1e-9;
-      fprintf(stderr, "[usk_prof] load+dedup %.3f scan+owner %.3f insert %.3f emit %.3f links %.3f (shares of thread 0's clocks)\n",
+      fprintf(stderr, "[usk_prof] load+dedup %.3f scan+owner %.3f insert %.3f ranks %.3f nodes+index+links %.3f (shares of thread 0's clocks)\n",
               hp[0] / tot, hp[1] / tot, hp[2] / tot, hp[3] / tot, hp[4] / tot);
     }
   }
