@@ -80,6 +80,10 @@ struct SkP {
 };
 constexpr int kSkRegW = 9;  // the windows of the K = 24 and K = 25 walks (m = kSkRegM)
 constexpr int kSkRegM = 16;
+// the record queues live in the count pass's p.w x kSkThreads column words
+static_assert(kSkRegW * kSkThreads >= (int)sk_regq_words(kSkThreads, kSkRegW) &&
+                  (kSkRegW + 1) * kSkThreads >= (int)sk_regq_words(kSkThreads, kSkRegW + 1),
+              "register walk queues exceed the count pass's LDS");
 __host__ __device__ inline uint32_t sk_pieces(uint32_t n, uint32_t split) {
   return split && n > split ? (n + split - 1) / split : 1u;
 }

@@ -469,6 +469,14 @@ struct SkList {
   uint32_t cnt;
   uint64_t d[CAP];
 };
+// LDS words the register walk's record queues take (sk_walk_tile, WN > 0):
+// one SkWaveQ ring per wave at the start of the walk's dynamic LDS.
+__host__ __device__ constexpr int sk_regq_drain(int WN) { return WN >= 32 ? 4 : 2; }
+__host__ __device__ constexpr uint32_t sk_regq_capw(int WN) { return WN >= 32 ? 512u : 256u; }
+__host__ __device__ constexpr uint32_t sk_regq_words(int NT, int WN) {
+  return (uint32_t)(NT / 64) * sk_regq_capw(WN) * 2u;
+}
+
 // Every thread of the block walks the tile's read q = threadIdx.x (if any)
 // in chunks of kSkChunk bases.  LIST: between chunks the block drains the
 // list when it is half full (and after the last chunk) — for an f that is
@@ -501,10 +509,9 @@ __device__ __forceinline__ void sk_walk_tile(const P& p, const TT& T, uint32_t n
     else
       emit(d);  // list full: this record alone, in place
   };
-  if constexpr (!LIST && WN > 0) {  // the waves' queues in the (unused) LDS column
-    constexpr int S = WN >= 32 ? 4 : 2;
-    constexpr uint32_t CAPW = S == 4 ? 512 : 256;
-    static_assert((TWO ? sk_walk2_words(WN) : WN) * 32 >= (int)CAPW, "the column holds the waves' queues");
+  if constexpr (!LIST && WN > 0) {  // the waves' queues: sk_regq_words(NT, WN) words from sb - q
+    constexpr int S = sk_regq_drain(WN);
+    constexpr uint32_t CAPW = sk_regq_capw(WN);
     uint64_t* wq = reinterpret_cast<uint64_t*>(sb - q) + (q / 64) * CAPW;
     sk_walk_regs<WN, MM, S, CAPW, typename P::U>(p, W.bases, Lw, q, wq, emit);
     return;

@@ -1320,6 +1320,15 @@ constexpr int kUskRegM = 31;
 __host__ __device__ inline uint32_t usk_column_words(const UskP& p) {
   return (uint32_t)(p.two ? sk_walk2_words(p.w) : p.w) * kUskThreads;
 }
+// the count pass's walk LDS: with the register column only the waves' record
+// queues and one column of the two-level walk for a read too long for a tile
+// (thread 0, stride 1): 8 KiB instead of the 13.5 KiB column, so eight
+// blocks per CU fit instead of seven
+__host__ __device__ inline uint32_t usk_count_words(const UskP& p) {
+  if (!p.reg) return usk_column_words(p);
+  const uint32_t q = sk_regq_words(kUskThreads, kUskRegW), c = (uint32_t)sk_walk2_words(p.w);
+  return q > c ? q : c;
+}
 static size_t usk_walk_lds(const UskP& p, int D, size_t per_digit) {
   return (size_t)usk_column_words(p) * 4 + ((size_t)1 << D) * per_digit;
 }
@@ -1375,6 +1384,8 @@ __device__ __forceinline__ void usk_walk_tiles(const SkReads& rv, const UskP& p,
         sk_walk_tile<kUskThreads, true, LIST>(p, T, n, sb, lst, f);
       else
         sk_walk_tile<kUskThreads, false, LIST>(p, T, n, sb, lst, f);
+    } else if (!LIST && p.reg) {  // the count pass's column: stride 1 (usk_count_words)
+      sk_walk_global<1, true>(rv, p, T, t0, sb - threadIdx.x, f);
     } else if (two) {
       sk_walk_global<kUskThreads, true>(rv, p, T, t0, sb, f);
     } else {
@@ -1394,7 +1405,7 @@ __global__ void __launch_bounds__(kUskThreads) k_usk_count(SkReads rv, UskP p, i
   __shared__ uint32_t dpos, dovf;
   extern __shared__ uint32_t usk_sb[];  // the walk columns, then hist[ndig], khist[ndig]
   const uint32_t ndig = 1u << D;
-  uint32_t* hist = usk_sb + usk_column_words(p);
+  uint32_t* hist = usk_sb + usk_count_words(p);
   uint32_t* khist = hist + ndig;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   for (uint32_t i = threadIdx.x; i < ndig; i += blockDim.x) hist[i] = khist[i] = 0;
@@ -2356,13 +2367,24 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
 //   usk_scatter  the records, grouped by (shard, digit)
 //   usk_stage    partition levels of one shard's records (P source segments
 //                per digit) + LDS buckets -> distinct nodes in "usk_nodes"
-// Walk grid cap: two full rounds of resident k_usk_scatter blocks (see sk_blocks).
+// The count pass's dynamic LDS: its walk words, then hist[ndig], khist[ndig].
+static size_t usk_count_lds(const UskP& p, int D) { return (size_t)usk_count_words(p) * 4 + ((size_t)1 << D) * 8; }
+
+// Walk grid cap: two full rounds of the resident blocks of the count pass or
+// of the scatter pass, whichever holds more per CU (see sk_blocks; the two
+// passes share the grid: the scatter replays the count's per-block
+// descriptor regions)
 static uint64_t usk_grid_cap(const apg_ctx* ctx, const UskP& p, int D) {
-  int occ = 0;
+  int occ = 0, occ_c = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_usk_scatter, kUskThreads, usk_walk_lds(p, D, 8)) !=
           hipSuccess ||
       occ < 1)
     occ = 4;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_c, k_usk_count, kUskThreads, usk_count_lds(p, D)) ==
+      hipSuccess)
+    occ = std::max(occ, occ_c);
+  else
+    (void)hipGetLastError();
   return std::min<uint64_t>(kUskMaxBlocks, (uint64_t)std::max(ctx->n_cu, 1) * occ * 2);
 }
 
@@ -2392,7 +2414,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   const uint32_t G =
       (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(usk_grid_cap(ctx, p, D), (dr->n_reads + kUskThreads - 1) / kUskThreads));
   SkReads rv{dr->d_base_off, dr->d_byte_off, dr->d_packed, dr->n_reads};
-  const size_t sb_bytes = usk_walk_lds(p, D, 8);  // + hist, khist (count) or cursors (scatter)
+  const size_t sb_bytes = usk_count_lds(p, D);
   uint32_t* cmat = nullptr;
   uint64_t *omat = nullptr, *ds = nullptr;
   unsigned long long* kdig = nullptr;

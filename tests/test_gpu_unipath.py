@@ -72,6 +72,20 @@ def test_synthetic_library_and_device_path(gpu_ctx):
     d.free()
 
 
+def test_reads_longer_than_a_walk_tile(gpu_ctx):
+    """Reads past the K=96 walk's LDS tile (6 KiB = 24,576 bases) are walked
+    from HBM by one thread of the block (superkmer.hpp sk_walk_global) — with
+    the register-column count walk, on a one-column stride of its own — beside
+    tiles of ordinary reads walked by every lane."""
+    from allpathslg_amd import ReadSet
+
+    g = synth_genome(90_000, 17)
+    seqs = [g[0:30_000], g[20_000:55_000]]
+    seqs += [g[s : s + 150] for s in range(30_000, 90_000 - 150, 9)]
+    seqs.append(g[60_000:90_000])
+    run(gpu_ctx, ReadSet.from_sequences(seqs), 96)
+
+
 def test_empty_and_short(gpu_ctx):
     from allpathslg_amd import ReadSet
 
