@@ -301,11 +301,12 @@ struct SkWaveQ {
 // hashes every m-mer twice; this walk hashes it once).  Records as SkWalker's
 // over the read's Lw bases (Lw = 0: none; else Lw >= K), as descriptors
 // key | a << 32 | n << 48 | q << 56 through the wave's queue `wq`
-// (SkWaveQ<CAPW>, drained every S bases: 64 + 64 S <= CAPW) to emit(d).  Lanes past their read run on with their records frozen; the
-// block loop ends when no lane of the wave has m-mers left (the base accessor
-// must tolerate reads past the read: SkLdsBases clamps to its tile).  Every
-// lane of the wave calls it.
-// MM = p.m, also fixed at compile time (the rolls' shifts and mask constant).
+// (SkWaveQ<CAPW>, drained every S bases: 64 + 64 S <= CAPW) to emit(d).
+// Lanes past their read run on with their records frozen; the block loop
+// ends when no lane of the wave has m-mers left (the base accessor must
+// tolerate reads past the read: SkLdsBases clamps to its tile).  Every lane
+// of the wave calls it.  MM = p.m, also fixed at compile time (the rolls'
+// shifts and mask constant).
 template <int WN, int MM, int S, uint32_t CAPW, typename U, typename P, typename LB, typename E>
 __device__ __forceinline__ void sk_walk_regs(const P& p, const LB& bases, uint32_t Lw, uint32_t q, uint64_t* wq,
                                              E emit) {
