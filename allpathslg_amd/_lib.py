@@ -8,11 +8,28 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import re
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# APG_LIB_VARIANT=name loads libapg_<name>.so (diagnostics builds, scripts/build_fill_variants.sh)
-LIB_PATH = os.path.join(_HERE, f"libapg_{os.environ['APG_LIB_VARIANT']}.so" if os.environ.get("APG_LIB_VARIANT") else "libapg.so")
+
+
+def _lib_path() -> str:
+    """libapg.so, or libapg_<name>.so for APG_LIB_VARIANT=name (diagnostics
+    builds, scripts/build_fill_variants.sh): the name is [A-Za-z0-9_]+ only,
+    so the variant always comes from this directory."""
+    v = os.environ.get("APG_LIB_VARIANT")
+    if not v:
+        return os.path.join(_HERE, "libapg.so")
+    if not re.fullmatch(r"[A-Za-z0-9_]+", v):
+        raise ValueError(f"APG_LIB_VARIANT={v!r}: only [A-Za-z0-9_] is allowed")
+    path = os.path.join(_HERE, f"libapg_{v}.so")
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"APG_LIB_VARIANT={v!r}: {path} is not built")
+    return path
+
+
+LIB_PATH = _lib_path()
 
 APG_OK = 0
 ERRORS = {

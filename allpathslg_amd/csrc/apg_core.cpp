@@ -48,15 +48,25 @@ int workspace(apg_ctx* ctx, const char* name, size_t bytes, void** out) {
     b.bytes = 0;
     // Grow by 1/8 headroom so steadily growing calls do not realloc each time.
     size_t want = bytes + bytes / 8;
-    hipError_t e = hipMalloc(&b.p, want);
+    // APG_DEVICE_MEM_LIMIT with APG_DEVICE_MEM_HARD=1 (tests): an allocation
+    // past the emulated device fails as a real one would, so the
+    // failed-allocation release runs on a small input
+    static const uint64_t hard = getenv("APG_DEVICE_MEM_HARD") && getenv("APG_DEVICE_MEM_LIMIT")
+                                     ? strtoull(getenv("APG_DEVICE_MEM_LIMIT"), nullptr, 10)
+                                     : 0;
+    auto alloc = [&](size_t n) -> hipError_t {
+      if (hard && ctx->ws_bytes + n > hard) return hipErrorOutOfMemory;
+      return hipMalloc(&b.p, n);
+    };
+    hipError_t e = alloc(want);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       want = bytes;
-      e = hipMalloc(&b.p, want);
+      e = alloc(want);
     }
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      if (release_dead_for(ctx, name)) e = hipMalloc(&b.p, want);
+      if (release_dead_for(ctx, name)) e = alloc(want);
     }
     if (e != hipSuccess) {
       b.p = nullptr;
@@ -91,6 +101,23 @@ static const char* const kStageWs[] = {"big0",    "big1",    "big2",    "x_send"
                                        "sk_solid_sparse", "sk_dcount", "ext_e0", "ext_e1", "sk_ovf_e0", "sk_ovf_e1"};
 // record descriptors of a count pass: live from the count to its scatter
 static const char* const kDescWs[] = {"sk_desc", "usk_desc"};
+// The name of the releasable workspace (a stage buffer, a descriptor buffer
+// or a correction table: the lists above) whose allocation holds p, or null.
+const char* ws_releasable(apg_ctx* ctx, const void* p) {
+  if (!p) return nullptr;
+  const char* const* lists[] = {kStageWs, kDescWs, kCorrectWs};
+  const size_t lens[] = {sizeof kStageWs / sizeof kStageWs[0], sizeof kDescWs / sizeof kDescWs[0],
+                         sizeof kCorrectWs / sizeof kCorrectWs[0]};
+  for (int l = 0; l < 3; ++l)
+    for (size_t i = 0; i < lens[l]; ++i) {
+      auto it = ctx->ws.find(lists[l][i]);
+      if (it == ctx->ws.end() || !it->second.p) continue;
+      const char* b = static_cast<const char*>(it->second.p);
+      if (static_cast<const char*>(p) >= b && static_cast<const char*>(p) < b + it->second.bytes) return lists[l][i];
+    }
+  return nullptr;
+}
+
 // APG_DEVICE_MEM_LIMIT=<bytes>: act as if the device held only that much for
 // this context's workspaces (tests of the release path on a 288 GB device).
 uint64_t device_free_bytes(apg_ctx* ctx) {
@@ -181,7 +208,7 @@ static void staging_free(apg_ctx* ctx) {
 }
 
 int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers) {
-  if (ctx->bg_load) APG_TRY(dreads_quals_ready(ctx->bg_load));  // it holds the staging buffers
+  if (ctx->bg_load) dreads_join(ctx->bg_load);  // it holds the staging buffers
   struct Chunk {
     uint8_t* dst;
     const uint8_t* src;
@@ -396,7 +423,7 @@ int apg_create(const apg_config* cfg, apg_ctx** out) {
 int apg_trim(apg_ctx* ctx) {
   APG_REQUIRE(ctx, "apg_trim: ctx is NULL");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
-  if (ctx->bg_load) APG_TRY(dreads_quals_ready(ctx->bg_load));
+  if (ctx->bg_load) dreads_join(ctx->bg_load);
   APG_TRY(side_join(ctx));
   APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   for (auto& kv : ctx->ws)
@@ -414,7 +441,7 @@ int apg_trim(apg_ctx* ctx) {
 void apg_destroy(apg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->bg_load) (void)dreads_quals_ready(ctx->bg_load);
+  if (ctx->bg_load) dreads_join(ctx->bg_load);
   (void)side_join(ctx);
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
@@ -588,7 +615,7 @@ int apg_reads_upload(apg_ctx* ctx, const apg_reads* r, apg_dreads** out) {
 
 void apg_reads_free(apg_dreads* d) {
   if (!d) return;
-  (void)dreads_quals_ready(d);  // no load may still write into it
+  dreads_join(d);  // no load may still write into it
   (void)hipSetDevice(d->device);
   if (d->d_base_off) (void)hipFree(d->d_base_off);
   if (d->d_byte_off) (void)hipFree(d->d_byte_off);
@@ -632,12 +659,17 @@ int apg_reads_copy_dev(apg_ctx* ctx, apg_dreads* dst, const apg_dreads* src) {
               "apg_reads_copy_dev: read sets differ in shape");
   APG_REQUIRE(!src->d_quals || dst->d_quals, "apg_reads_copy_dev: destination has no qualities");
   APG_TRY(dreads_quals_ready(src));
-  APG_TRY(dreads_quals_ready(dst));
+  dreads_join(dst);  // its own load's outcome is overwritten below when src has qualities
+  if (!src->d_quals) APG_TRY(dreads_quals_ready(dst));
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   if (src->n_bytes)
     APG_CHECK_HIP(hipMemcpyAsync(dst->d_packed, src->d_packed, src->n_bytes, hipMemcpyDeviceToDevice, ctx->stream));
   if (src->d_quals && src->n_bases)
     APG_CHECK_HIP(hipMemcpyAsync(dst->d_quals, src->d_quals, src->n_bases, hipMemcpyDeviceToDevice, ctx->stream));
+  if (src->d_quals) {  // dst's qualities are src's now
+    dst->quals_rc = APG_OK;
+    dst->quals_err.clear();
+  }
   dst->gen = src->gen;  // same bases: plans made for src are valid for dst's contents
   return APG_OK;
 }

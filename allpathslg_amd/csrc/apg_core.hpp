@@ -96,6 +96,10 @@ struct apg_dreads {
   // qualities still loading in the background (apg_reads_load_dev): every
   // reader of d_quals calls apg::dreads_quals_ready first
   apg::DreadsPending* pending = nullptr;
+  // the background load's outcome, kept once joined: every later reader of
+  // the qualities gets the same error
+  int quals_rc = 0;
+  std::string quals_err;
 };
 
 struct apg_ctx {
@@ -339,9 +343,15 @@ int d2h_bulk(apg_ctx* ctx, const std::vector<D2HJob>& jobs, int workers = 4);
 // to land in HBM; APG_OK at once when none is running.  Every reader of
 // d_quals calls it first (apg_load.cpp).
 int dreads_quals_ready(const apg_dreads* dr);
+// Joins a background load without taking on its error (context-level joins:
+// another load, a bulk D2H, trim, destroy); the set's readers still get it.
+void dreads_join(const apg_dreads* dr);
 
 // Free device memory (hipMemGetInfo; ~0 if unknown).
 uint64_t device_free_bytes(apg_ctx* ctx);
+// Name of the workspace ws_make_room / a failed allocation may release that
+// holds device pointer p (nullptr: none does).
+const char* ws_releasable(apg_ctx* ctx, const void* p);
 // Before a large allocation of `need` bytes: when the device lacks it, release
 // the counting stages' dead record / partition workspaces, plus (flags) the
 // count passes' record descriptors (dead once scattered) and the correction

@@ -221,18 +221,24 @@ struct DreadsPending {
   double ms = 0;
 };
 
-int dreads_quals_ready(const apg_dreads* cd) {
+void dreads_join(const apg_dreads* cd) {
   apg_dreads* d = const_cast<apg_dreads*>(cd);
-  if (!d || !d->pending) return APG_OK;
+  if (!d || !d->pending) return;
   DreadsPending* p = d->pending;
   p->th.join();
   d->pending = nullptr;
   if (p->ctx && p->ctx->bg_load == d) p->ctx->bg_load = nullptr;
-  const int rc = p->rc;
-  if (rc != APG_OK) set_error(p->err);
+  d->quals_rc = p->rc;
+  if (p->rc != APG_OK) d->quals_err = p->err;
   vlog(p->ctx, "load_dev: qualities landed in the background (%.1f ms of streaming)", p->ms);
   delete p;
-  return rc;
+}
+
+int dreads_quals_ready(const apg_dreads* cd) {
+  if (!cd) return APG_OK;
+  dreads_join(cd);
+  if (cd->quals_rc != APG_OK) set_error(cd->quals_err);
+  return cd->quals_rc;
 }
 }  // namespace apg
 
@@ -248,7 +254,7 @@ extern "C" {
 int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int threads, apg_dreads** out) {
   APG_REQUIRE(ctx && fastb && out, "apg_reads_load_dev: NULL argument");
   *out = nullptr;
-  if (ctx->bg_load) APG_TRY(dreads_quals_ready(ctx->bg_load));  // one load at a time through the staging buffers
+  if (ctx->bg_load) dreads_join(ctx->bg_load);  // one load at a time through the staging buffers
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
@@ -329,7 +335,8 @@ int apg_reads_load_dev(apg_ctx* ctx, const char* fastb, const char* qualb, int t
   };
   const bool bg = qualb && n && !sync_load;
   if (bg && early) {
-    APG_TRY(staging_get(ctx, 2 * threads));  // workers [threads, 2 threads) for the qualities
+    rc = staging_get(ctx, 2 * threads);  // workers [threads, 2 threads) for the qualities
+    if (rc != APG_OK) return fail(rc);
     rc = start_quals(threads);
     if (rc != APG_OK) return fail(rc);
   }

@@ -1661,6 +1661,7 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid: NULL argument");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid: min_solid must be >= 1");
   ctx->solid_valid = false;
+  ctx->ws_dead &= ~kRoomCorrection;  // this pass writes "pc_solid": live from here on
   APG_REQUIRE(K >= 1 && K <= 32 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
               "apg_shard_solid: K must be in [1, 32], n_shards a power of two <= 8");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
@@ -1697,6 +1698,7 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
   ctx->solid_valid = false;
+  ctx->ws_dead &= ~kRoomCorrection;  // this pass writes "pc_solid": live from here on
   APG_REQUIRE(K >= 9 && K <= 29 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
               "apg_shard_solid_weak: K must be in [9, 29], n_shards a power of two <= 8");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
@@ -1856,7 +1858,10 @@ int apg_precorrect_solid(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, 
 
 int apg_reads_download(apg_ctx* ctx, const apg_dreads* dr, uint8_t* packed, uint8_t* quals) {
   APG_REQUIRE(ctx && dr, "apg_reads_download: NULL argument");
-  APG_TRY(dreads_quals_ready(dr));
+  if (quals)
+    APG_TRY(dreads_quals_ready(dr));
+  else
+    dreads_join(dr);  // the bases are loaded; only a failed qualities load fails a download of them
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   if (packed && dr->n_bytes)
     APG_CHECK_HIP(hipMemcpyAsync(packed, dr->d_packed, dr->n_bytes, hipMemcpyDeviceToHost, ctx->stream));

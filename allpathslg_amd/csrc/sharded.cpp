@@ -93,7 +93,19 @@ int exchange_records(apg_ctx* ctx, Comm* c, const std::vector<uint64_t>& counts,
 int gather_all(apg_ctx* ctx, Comm* c, const void* local, uint64_t n_local, uint64_t bytes, const char* ws,
                void** out, uint64_t* n_all) {
   if (c->world == 1) {  // the gathered set is this rank's
-    *out = const_cast<void*>(local);
+    // handed back as is only when no memory-pressure release can free it
+    // under the caller (the C5 rehearsal's fault was a
+    // world-1 solid list in the stage buffer "x_local"); a releasable buffer
+    // other than `ws` itself is copied into `ws`
+    const char* rel = ws_releasable(ctx, local);
+    if (!rel || !std::strcmp(rel, ws)) {
+      *out = const_cast<void*>(local);
+      *n_all = n_local;
+      return APG_OK;
+    }
+    APG_TRY(workspace(ctx, ws, std::max<uint64_t>(n_local * bytes, 64), out));
+    if (n_local)
+      APG_CHECK_HIP(hipMemcpyAsync(*out, local, n_local * bytes, hipMemcpyDeviceToDevice, ctx->stream));
     *n_all = n_local;
     return APG_OK;
   }

@@ -2569,6 +2569,10 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
       ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
       ctx->pc_ext_valid = false;
+      // the correction tables are live again: a failed allocation of this
+      // count must not release the list it writes (the unipath stage had
+      // marked them dead)
+      ctx->ws_dead &= ~kRoomCorrection;
       solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     }
     // the chunked list (kSolidChunk slots per reservation, compacted into

@@ -31,6 +31,15 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <cstdio>
+
+static double oru_t0 = 0;
+static void oru_phase(const char* what) {
+  if (!std::getenv("ORU_VERBOSE")) return;
+  const double t = omp_get_wtime();
+  std::fprintf(stderr, "[oru] %-12s %8.2f s\n", what, oru_t0 ? t - oru_t0 : 0.0);
+  oru_t0 = t;
+}
 
 namespace {
 
@@ -45,30 +54,30 @@ struct Key {
 };
 
 int g_K;
+uint64_t g_ma, g_mb, g_mc;  // per-limb masks of the 2K-bit value (set_k)
+
+void set_k(int K) {
+  g_K = K;
+  const int bits = 2 * K;
+  auto lm = [](int n) { return n >= 64 ? ~0ull : n <= 0 ? 0ull : ((1ull << n) - 1); };
+  g_mc = lm(bits);
+  g_mb = lm(bits - 64);
+  g_ma = lm(bits - 128);
+}
 
 Key mask_key(Key k) {
-  const int bits = 2 * g_K;
-  if (bits < 192) {
-    if (bits <= 64) {
-      k.a = 0;
-      k.b = 0;
-      k.c &= bits == 64 ? ~0ull : ((1ull << bits) - 1);
-    } else if (bits <= 128) {
-      k.a = 0;
-      k.b &= bits == 128 ? ~0ull : ((1ull << (bits - 64)) - 1);
-    } else {
-      k.a &= (1ull << (bits - 128)) - 1;
-    }
-  }
+  k.a &= g_ma;
+  k.b &= g_mb;
+  k.c &= g_mc;
   return k;
 }
 
 Key push_right(Key k, uint64_t base) {  // (k << 2 | base) & mask
   Key r;
-  r.a = (k.a << 2) | (k.b >> 62);
-  r.b = (k.b << 2) | (k.c >> 62);
-  r.c = (k.c << 2) | base;
-  return mask_key(r);
+  r.a = ((k.a << 2) | (k.b >> 62)) & g_ma;
+  r.b = ((k.b << 2) | (k.c >> 62)) & g_mb;
+  r.c = ((k.c << 2) | base) & g_mc;
+  return r;
 }
 
 uint64_t get_base(const Key& k, int i) {  // base i (0 = first) of the K-mer
@@ -107,20 +116,66 @@ struct Node {
   Key key;
   uint8_t left, right;  // ext bit sets (bit b = base b)
   uint64_t count;
+  uint64_t id[2];  // K-mer id of each orientation (set once the unipaths are numbered)
 };
 
 std::vector<Node> g_nodes;
 
-int64_t find_node(const Key& k) {
-  size_t lo = 0, hi = g_nodes.size();
-  while (lo < hi) {
-    size_t mid = (lo + hi) / 2;
-    if (g_nodes[mid].key < k)
-      lo = mid + 1;
-    else
-      hi = mid;
+// Node lookup: an open-addressing index over g_nodes (load <= 0.5, linear
+// probing) keyed by a mix of the key's limbs — O(1) where a binary search over
+// a C2-size node array (64 M) made the read paths dominate the oracle's time.
+std::vector<int64_t> g_index;
+uint64_t g_index_mask = 0;
+
+uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+uint64_t key_mix(const Key& k) {
+  return mix64(k.a * 0x9e3779b97f4a7c15ull ^ k.b * 0xc2b2ae3d27d4eb4full ^ (k.c + 0x165667b19e3779f9ull));
+}
+
+void build_index() {
+  uint64_t T = 2;
+  while (T < 2 * (uint64_t)g_nodes.size()) T <<= 1;
+  g_index.assign(T, -1);
+  g_index_mask = T - 1;
+  const int64_t N = (int64_t)g_nodes.size();
+  int64_t* tab = g_index.data();
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < N; ++i) {
+    for (uint64_t h = key_mix(g_nodes[i].key) & g_index_mask;; h = (h + 1) & g_index_mask) {
+      int64_t expect = -1;
+      if (__atomic_compare_exchange_n(&tab[h], &expect, i, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) break;
+    }
   }
-  return lo < g_nodes.size() && g_nodes[lo].key == k ? (int64_t)lo : -1;
+}
+
+int64_t find_node(const Key& k) {
+  for (uint64_t h = key_mix(k) & g_index_mask;; h = (h + 1) & g_index_mask) {
+    const int64_t i = g_index[h];
+    if (i < 0) return -1;
+    if (g_nodes[i].key == k) return i;
+  }
+}
+
+// Rolling reverse complement: rc of (window << 2 | b) = rc >> 2 with the
+// complement of b as the first (most significant) base.
+Key push_left_rc(Key r, uint64_t b) {
+  Key o;
+  o.c = (r.c >> 2) | (r.b << 62);
+  o.b = (r.b >> 2) | (r.a << 62);
+  o.a = r.a >> 2;
+  const int bit = 2 * (g_K - 1);
+  const uint64_t v = (3 - b) << (bit & 63);
+  if (bit >= 128)
+    o.a |= v;
+  else if (bit >= 64)
+    o.b |= v;
+  else
+    o.c |= v;
+  return o;
 }
 
 Key seq(int64_t v) {
@@ -189,58 +244,106 @@ extern "C" {
 int oru_build(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
               oru_result* out) {
   if (K < 1 || K > 96 || !out) return -1;
-  g_K = K;
+  set_k(K);
   std::memset(out, 0, sizeof(*out));
   // ---- 1. instances -> nodes with extension bits -------------------------
+  // In hash parcels of the canonical key (the reference's KmerParcels idea,
+  // here only to bound the checker's memory: a C2-size input has 1.6 G
+  // instances): each pass re-rolls every read, keeps the instances of its
+  // parcel, sorts them and folds equal keys into nodes.
   struct Inst {
     Key key;
+    uint32_t h;  // low bits of key_mix(key): the bucket table's slot
     uint8_t left, right;
   };
-  std::vector<uint64_t> ioff(n_reads + 1, 0);
+  uint64_t n_inst = 0;
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint64_t L = base_off[r + 1] - base_off[r];
-    ioff[r + 1] = ioff[r] + (L >= (uint64_t)K ? L - K + 1 : 0);
+    n_inst += L >= (uint64_t)K ? L - K + 1 : 0;
   }
-  std::vector<Inst> inst(ioff[n_reads]);
-#pragma omp parallel for schedule(dynamic, 1024)
-  for (uint64_t r = 0; r < n_reads; ++r) {
-    const uint64_t L = base_off[r + 1] - base_off[r];
-    const uint8_t* rd = packed + byte_off[r];
-    if (L < (uint64_t)K) continue;
-    Key f{0, 0, 0};
-    for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) f = push_right(f, read_base(rd, i));
-    for (uint64_t i = 0; i + K <= L; ++i) {
-      f = push_right(f, read_base(rd, i + K - 1));
-      const Key rc = revcomp(f);
-      const int a = i > 0 ? read_base(rd, i - 1) : -1;
-      const int b = i + K < L ? read_base(rd, i + K) : -1;
-      const uint8_t la = a >= 0 ? 1 << a : 0, rb = b >= 0 ? 1 << b : 0;
-      const uint8_t ca = a >= 0 ? 1 << (3 - a) : 0, cb = b >= 0 ? 1 << (3 - b) : 0;
-      Inst x;
-      if (f == rc) {
-        x = {f, (uint8_t)(la | cb), (uint8_t)(rb | ca)};
-      } else if (f < rc) {
-        x = {f, la, rb};
-      } else {
-        x = {rc, cb, ca};
-      }
-      inst[ioff[r] + i] = x;
-    }
-  }
-  __gnu_parallel::sort(inst.begin(), inst.end(), [](const Inst& x, const Inst& y) { return x.key < y.key; });
+  // ORU_PARCEL_INSTANCES (tests): a smaller parcel, so that small inputs take several passes
+  uint64_t per_parcel = 1ull << 28;
+  if (const char* e = std::getenv("ORU_PARCEL_INSTANCES")) per_parcel = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  const uint64_t parcels = std::max<uint64_t>(1, (n_inst + per_parcel - 1) / per_parcel);
+  oru_phase("start");
   g_nodes.clear();
-  for (size_t i = 0; i < inst.size();) {
-    Node n{inst[i].key, 0, 0, 0};
-    size_t j = i;
-    for (; j < inst.size() && inst[j].key == inst[i].key; ++j) {
-      n.left |= inst[j].left;
-      n.right |= inst[j].right;
-      n.count++;
+  const int nt = omp_get_max_threads();
+  constexpr int kBuckets = 256;  // by the top 8 bits of key_mix: each folded by one thread in its own table
+  for (uint64_t pc = 0; pc < parcels; ++pc) {
+    std::vector<std::vector<Inst>> part((size_t)nt * kBuckets);
+#pragma omp parallel
+    {
+      std::vector<Inst>* mine = &part[(size_t)omp_get_thread_num() * kBuckets];
+#pragma omp for schedule(dynamic, 1024)
+      for (uint64_t r = 0; r < n_reads; ++r) {
+        const uint64_t L = base_off[r + 1] - base_off[r];
+        const uint8_t* rd = packed + byte_off[r];
+        if (L < (uint64_t)K) continue;
+        Key f{0, 0, 0}, rc{0, 0, 0};
+        for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) {
+          f = push_right(f, read_base(rd, i));
+          rc = push_left_rc(rc, read_base(rd, i));
+        }
+        for (uint64_t i = 0; i + K <= L; ++i) {
+          f = push_right(f, read_base(rd, i + K - 1));
+          rc = push_left_rc(rc, read_base(rd, i + K - 1));
+          const Key& canon = rc < f ? rc : f;
+          const uint64_t h = key_mix(canon);
+          if (parcels > 1 && (h >> 20) % parcels != pc) continue;
+          const int a = i > 0 ? read_base(rd, i - 1) : -1;
+          const int b = i + K < L ? read_base(rd, i + K) : -1;
+          const uint8_t la = a >= 0 ? 1 << a : 0, rb = b >= 0 ? 1 << b : 0;
+          const uint8_t ca = a >= 0 ? 1 << (3 - a) : 0, cb = b >= 0 ? 1 << (3 - b) : 0;
+          Inst x;
+          if (f == rc) {
+            x = {f, (uint32_t)h, (uint8_t)(la | cb), (uint8_t)(rb | ca)};
+          } else if (f < rc) {
+            x = {f, (uint32_t)h, la, rb};
+          } else {
+            x = {rc, (uint32_t)h, cb, ca};
+          }
+          mine[h >> 56].push_back(x);
+        }
+      }
     }
-    g_nodes.push_back(n);
-    i = j;
+    oru_phase("  extract");
+    // fold equal keys: per bucket an open-addressing table over its nodes
+    std::vector<std::vector<Node>> bn(kBuckets);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int bk = 0; bk < kBuckets; ++bk) {
+      size_t cnt = 0;
+      for (int t = 0; t < nt; ++t) cnt += part[(size_t)t * kBuckets + bk].size();
+      uint64_t T = 16;
+      while (T < 2 * cnt) T <<= 1;
+      std::vector<int64_t> tab(T, -1);
+      std::vector<Node>& nodes = bn[bk];
+      for (int t = 0; t < nt; ++t) {
+        std::vector<Inst>& v = part[(size_t)t * kBuckets + bk];
+        for (const Inst& x : v) {
+          for (uint64_t sl = x.h & (T - 1);; sl = (sl + 1) & (T - 1)) {
+            const int64_t i = tab[sl];
+            if (i < 0) {
+              tab[sl] = (int64_t)nodes.size();
+              nodes.push_back(Node{x.key, x.left, x.right, 1, {0, 0}});
+              break;
+            }
+            Node& n = nodes[i];
+            if (n.key == x.key) {
+              n.left |= x.left;
+              n.right |= x.right;
+              n.count++;
+              break;
+            }
+          }
+        }
+        std::vector<Inst>().swap(v);
+      }
+    }
+    oru_phase("  fold");
+    for (auto& v : bn) g_nodes.insert(g_nodes.end(), v.begin(), v.end());
   }
-  std::vector<Inst>().swap(inst);
+  __gnu_parallel::sort(g_nodes.begin(), g_nodes.end(), [](const Node& x, const Node& y) { return x.key < y.key; });
+  oru_phase("nodes");
   return build_graph(n_reads, base_off, byte_off, packed, K, out);
 }
 
@@ -250,12 +353,12 @@ int oru_graph_from_nodes(uint64_t n_nodes, const uint64_t* keys, const uint8_t* 
                          const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed, int K,
                          oru_result* out) {
   if (K < 1 || K > 96 || !out) return -1;
-  g_K = K;
+  set_k(K);
   std::memset(out, 0, sizeof(*out));
   g_nodes.clear();
   for (uint64_t i = 0; i < n_nodes; ++i)
     g_nodes.push_back(Node{Key{keys[3 * i], keys[3 * i + 1], keys[3 * i + 2]}, (uint8_t)(ext[i] & 15),
-                           (uint8_t)(ext[i] >> 4), 0});
+                           (uint8_t)(ext[i] >> 4), 0, {0, 0}});
   std::sort(g_nodes.begin(), g_nodes.end(), [](const Node& x, const Node& y) { return x.key < y.key; });
   out->n_nodes = n_nodes;
   return build_graph(n_reads, base_off, byte_off, packed, K, out);
@@ -273,7 +376,7 @@ static uint64_t fmix64(uint64_t z) {
 // outputs may be NULL to size.
 uint64_t oru_instances(uint64_t n_reads, const uint64_t* base_off, const uint64_t* byte_off, const uint8_t* packed,
                        int K, uint64_t* keys, uint8_t* ext, uint64_t* hash) {
-  g_K = K;
+  set_k(K);
   uint64_t n = 0;
   for (uint64_t r = 0; r < n_reads; ++r) {
     const uint64_t L = base_off[r + 1] - base_off[r];
@@ -314,6 +417,8 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
                        int K, oru_result* out) {
   const int64_t N = (int64_t)g_nodes.size(), D = 2 * N;
   out->n_nodes = (uint64_t)N;
+  build_index();
+  oru_phase("index");
   // ---- 2. unique links --------------------------------------------------
   std::vector<int64_t> nxt(D, -1), prv(D, -1);
   int bad = 0;
@@ -334,9 +439,11 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
     prv[w] = v;
   }
   if (bad) return -2;
+  oru_phase("links");
   // ---- 3. cut cycles ------------------------------------------------------
   {
-    std::vector<char> onpath(D, 0);
+    std::vector<char> onpath(D, 0);  // chains from distinct heads are disjoint: no write races
+#pragma omp parallel for schedule(dynamic, 4096)
     for (int64_t v = 0; v < D; ++v)
       if (prv[v] < 0)
         for (int64_t x = v; x >= 0 && !onpath[x]; x = nxt[x]) onpath[x] = 1;
@@ -372,22 +479,24 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
       }
     }
   }
+  oru_phase("cycles");
   // ---- 4. paths -> unipath pairs ------------------------------------------
   struct PathRec {
     int64_t head, tail;
     uint64_t len;
   };
-  std::vector<PathRec> paths;
+  std::vector<PathRec> paths;  // one per head, in directed-node order
+  for (int64_t v = 0; v < D; ++v)
+    if (prv[v] < 0) paths.push_back(PathRec{v, v, 0});
   std::vector<int64_t> path_of(D, -1), rank_of(D, -1);
-  for (int64_t v = 0; v < D; ++v) {
-    if (prv[v] >= 0) continue;
-    PathRec p{v, v, 0};
-    for (int64_t x = v; x >= 0; x = nxt[x]) {
-      path_of[x] = (int64_t)paths.size();
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (size_t pi = 0; pi < paths.size(); ++pi) {
+    PathRec& p = paths[pi];
+    for (int64_t x = p.head; x >= 0; x = nxt[x]) {
+      path_of[x] = (int64_t)pi;
       rank_of[x] = (int64_t)p.len++;
       p.tail = x;
     }
-    paths.push_back(p);
   }
   struct Pair {
     Key key;
@@ -428,14 +537,18 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
     idb += len[i];
     ub_off[i + 1] = ub_off[i] + (uint64_t)K - 1 + len[i];
   }
+  oru_phase("paths");
   std::vector<uint8_t> ub(ub_off[U]);
+#pragma omp parallel for schedule(dynamic, 64)
   for (uint64_t i = 0; i < U; ++i) {
     uint64_t o = ub_off[i];
     const int64_t h = paths[order[i]].head;
     const Key hs = seq(h);
     for (int t = 0; t < K - 1; ++t) ub[o++] = (uint8_t)get_base(hs, t);
-    for (int64_t x = h; x >= 0; x = nxt[x]) ub[o++] = (uint8_t)get_base(seq(x), K - 1);
+    for (int64_t x = h; x >= 0; x = nxt[x])  // last base of seq(x): rc's is the complement of the key's first
+      ub[o++] = (uint8_t)((x & 1) ? 3 - get_base(g_nodes[x >> 1].key, 0) : get_base(g_nodes[x >> 1].key, K - 1));
   }
+  oru_phase("unibases");
   // ---- 5. HyperKmerPath vertices -------------------------------------------
   std::vector<uint64_t> par(2 * U);
   for (uint64_t i = 0; i < 2 * U; ++i) par[i] = i;
@@ -474,43 +587,92 @@ static int build_graph(uint64_t n_reads, const uint64_t* base_off, const uint64_
     from[i] = vid[findp(2 * i)];
     to[i] = vid[findp(2 * i + 1)];
   }
+  oru_phase("hkp");
   // ---- 6. read paths ---------------------------------------------------------
-  // per read: its id intervals (runs of consecutive ids), then concatenated
-  std::vector<uint64_t> poff(n_reads + 1, 0), pst, pln;
-  std::vector<std::vector<uint64_t>> rst(n_reads), rln(n_reads);
+  // per read: its id intervals (runs of consecutive ids); two passes over the
+  // reads (count, then write at the prefix-summed offsets), each K-mer looked
+  // up on its own — in chunks of 64 K-mers whose index slots and then node
+  // records are prefetched before they are read
+#pragma omp parallel for schedule(static)
+  for (int64_t v = 0; v < D; ++v) g_nodes[v >> 1].id[v & 1] = base[uni_of_path[path_of[v]]] + (uint64_t)rank_of[v];
+  // one pass: each thread logs its reads' runs as (read, start id, length);
+  // the runs of a read are contiguous in one thread's log
+  struct Run {
+    uint64_t read, start, len;
+  };
+  const int nthr = omp_get_max_threads();
+  std::vector<std::vector<Run>> runs(nthr);
   int miss = 0;
-#pragma omp parallel for schedule(dynamic, 1024)
-  for (uint64_t r = 0; r < n_reads; ++r) {
-    const uint64_t L = base_off[r + 1] - base_off[r];
-    const uint8_t* rd = packed + byte_off[r];
-    if (L < (uint64_t)K) continue;
-    Key f{0, 0, 0};
-    for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) f = push_right(f, read_base(rd, i));
-    for (uint64_t i = 0; i + K <= L; ++i) {
-      f = push_right(f, read_base(rd, i + K - 1));
-      const int64_t v = directed_of(f);
-      if (v < 0) {
-#pragma omp atomic write
-        miss = 1;
-        break;
+  constexpr int kChunk = 64;
+#pragma omp parallel
+  {
+    std::vector<Run>& log = runs[omp_get_thread_num()];
+    Key ck[kChunk];
+    bool fw[kChunk];
+    uint64_t slot[kChunk];
+    int64_t idx[kChunk];
+#pragma omp for schedule(dynamic, 1024)
+    for (uint64_t r = 0; r < n_reads; ++r) {
+      const uint64_t L = base_off[r + 1] - base_off[r];
+      const uint8_t* rd = packed + byte_off[r];
+      if (L < (uint64_t)K) continue;
+      Key f{0, 0, 0}, rc{0, 0, 0};
+      for (uint64_t i = 0; i < (uint64_t)K - 1; ++i) {
+        f = push_right(f, read_base(rd, i));
+        rc = push_left_rc(rc, read_base(rd, i));
       }
-      const uint64_t id = base[uni_of_path[path_of[v]]] + (uint64_t)rank_of[v];
-      if (!rst[r].empty() && rst[r].back() + rln[r].back() == id)
-        rln[r].back()++;
-      else {
-        rst[r].push_back(id);
-        rln[r].push_back(1);
+      bool open = false;
+      for (uint64_t i0 = 0; i0 + K <= L && !miss; i0 += kChunk) {
+        const int m = (int)std::min<uint64_t>(kChunk, L - K + 1 - i0);
+        for (int j = 0; j < m; ++j) {
+          f = push_right(f, read_base(rd, i0 + j + K - 1));
+          rc = push_left_rc(rc, read_base(rd, i0 + j + K - 1));
+          fw[j] = !(rc < f);  // canonical = min(s, rc s); palindrome -> o = 0
+          ck[j] = fw[j] ? f : rc;
+          slot[j] = key_mix(ck[j]) & g_index_mask;
+          __builtin_prefetch(&g_index[slot[j]]);
+        }
+        for (int j = 0; j < m; ++j) {
+          idx[j] = g_index[slot[j]];
+          if (idx[j] >= 0) __builtin_prefetch(&g_nodes[idx[j]]);
+        }
+        for (int j = 0; j < m; ++j) {
+          int64_t nd = idx[j];
+          if (nd >= 0 && !(g_nodes[nd].key == ck[j])) nd = find_node(ck[j]);
+          if (nd < 0) {
+#pragma omp atomic write
+            miss = 1;
+            break;
+          }
+          const uint64_t id = g_nodes[nd].id[fw[j] ? 0 : 1];
+          if (open && log.back().start + log.back().len == id)
+            log.back().len++;
+          else
+            log.push_back(Run{r, id, 1});
+          open = true;
+        }
       }
     }
   }
   if (miss) return -4;
-  for (uint64_t r = 0; r < n_reads; ++r) {
-    pst.insert(pst.end(), rst[r].begin(), rst[r].end());
-    pln.insert(pln.end(), rln[r].begin(), rln[r].end());
-    poff[r + 1] = pst.size();
-    std::vector<uint64_t>().swap(rst[r]);
-    std::vector<uint64_t>().swap(rln[r]);
+  std::vector<uint64_t> poff(n_reads + 1, 0);
+#pragma omp parallel for schedule(static, 1)
+  for (int t = 0; t < nthr; ++t)
+    for (const Run& x : runs[t]) poff[x.read + 1]++;
+  for (uint64_t r = 0; r < n_reads; ++r) poff[r + 1] += poff[r];
+  std::vector<uint64_t> pst(poff[n_reads]), pln(poff[n_reads]);
+#pragma omp parallel for schedule(static, 1)
+  for (int t = 0; t < nthr; ++t) {
+    uint64_t prev = UINT64_MAX, o = 0;
+    for (const Run& x : runs[t]) {
+      if (x.read != prev) o = poff[x.read], prev = x.read;
+      pst[o] = x.start;
+      pln[o++] = x.len;
+    }
+    std::vector<Run>().swap(runs[t]);
   }
+  oru_phase("read paths");
+  oru_phase("concat");
   out->n_unipaths = U;
   out->len = dup(len);
   out->id_base = dup(base);

@@ -146,3 +146,21 @@ def test_synth_fragments_are_the_pairs_inserts():
         assert np.array_equal(f[-100:], (3 - b)[::-1])
     part = synth_fragments(g, 100, seed=6, first_pair=200)
     assert np.array_equal(part.read(7), frags.read(207))
+
+
+def test_lib_variant_name_is_validated():
+    """APG_LIB_VARIANT only selects libapg_<[A-Za-z0-9_]+>.so in the package
+    directory, and a missing variant fails loudly."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import sys; sys.path.insert(0, %r); import allpathslg_amd._lib as L; print(L.LIB_PATH)" % root
+    for bad, err in (("../x", "ValueError"), ("a/b", "ValueError"), ("nope_not_built", "FileNotFoundError")):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, APG_LIB_VARIANT=bad),
+                           capture_output=True, text=True)
+        assert r.returncode != 0 and err in r.stderr, (bad, r.stderr[-500:])
+    env = dict(os.environ)
+    env.pop("APG_LIB_VARIANT", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip().endswith("libapg.so")

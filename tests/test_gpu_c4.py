@@ -19,7 +19,8 @@ ALLPATHS-LG); PreCorrect of a 2 M-read slice against that solid set equals
 the oracle; the bench's size-independent properties; and the sharded path
 equals the single-GPU path everywhere (spectrum, solid set, every corrected
 base and quality, fill statuses and counters, the whole graph, unibases,
-HyperKmerPath and KmerPaths)."""
+HyperKmerPath and KmerPaths); and the whole single-GPU graph equals the
+oracle's graph of the same filled fragments (round 6)."""
 import numpy as np
 import pytest
 import torch
@@ -45,6 +46,7 @@ def _chain_single(ctx, dsrc, dwork, status):
     out["fst"], out["status"] = fst, status.cpu().numpy().copy()
     out["graph"], out["ust"] = ctx.unipaths(filled, K96, fetch=True)
     out["mem"] = ctx.mem_stats()
+    out["filled"] = ctx.download(filled)
     filled.free()
     return out
 
@@ -137,6 +139,16 @@ def test_c4_sharded_equals_single_gpu(c4):
     for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases"):
         assert a["fst"][k] == b["fst"][k], k
     assert_graph_equal(b["graph"], a["graph"])
+
+
+def test_c4_whole_graph_matches_oracle(c4):
+    """The whole single-GPU K=96 graph of the rank's filled fragments (2 G
+    instances, 143.6 M nodes) against the oracle's graph of the same
+    fragments (C4 had been checked only sharded against
+    single); the sharded graph equals it by test_c4_sharded_equals_single_gpu."""
+    og = oracle.unipaths(c4["single"]["filled"], K96)
+    assert og["n_nodes"] >= DMEL - K96 + 1 - 1000
+    assert_graph_equal(c4["single"]["graph"], og)
 
 
 def test_c4_properties(c4):

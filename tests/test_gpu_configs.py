@@ -14,13 +14,15 @@ where the oracle finishes in seconds:
       (the oracle's rolling-key form, ork_precorrect_solid_fast, equal to the
       checker by tests/test_cpu_baseline.py); one 1/256 hash parcel of the
       K=25 counted table (keys and counts); FillFragments of all 20 M pairs
-      (every status and filled byte); and both directions of the unipath
-      graph inside five 400-kb genome windows (oracle graph of the filled
-      fragments whose pairs lie in each window).
+      (every status and filled byte); the whole K=96 graph of all filled
+      fragments (round 6: unipaths, ids, rc partners, unibases, HKP,
+      every KmerPath); and, as a fast smoke, both directions of the unipath
+      graph inside five 400-kb genome windows.
   C3  chr20 40 M frag + 20 M 3-kb jump reads: ErrorCorrectJump, all_reads =
       filled fragments ++ trimmed jumps, K=96 graph over all of them, run
       twice, ECJ parity on all 20 M jump reads (bases, qualities, trim
-      lengths, counters), window parity with the window's jump reads included.
+      lengths, counters), the whole all_reads graph against the oracle
+      (round 6), window parity with the window's jump reads included.
 """
 import numpy as np
 import pytest
@@ -321,6 +323,17 @@ def test_c2_full_fill_matches_oracle(c2, c2_oracle):
         assert c2["a"]["fst"][k] == ost[k], k
 
 
+def test_c2_whole_graph_matches_oracle(c2):
+    """The whole K=96 graph of all filled fragments of the 40 M reads (SURVEY
+    §8a a8-a11): node count, every unipath's length, id
+    base and rc partner, every unibase, the HyperKmerPath's vertices and
+    edges, and every fragment's KmerPath, against the oracle's graph of the
+    same (whole-table-checked) filled fragments."""
+    og = oracle.unipaths(c2["filled_a"], K96)
+    assert og["n_nodes"] >= CHR20 - K96 + 1 - 1000
+    assert_graph_equal(c2["a"]["graph"], og)
+
+
 # five windows of 400 kb spread over the chromosome (2 Mb, 3 % of it; round 4
 # checked one 200-kb window)
 C2_WINDOWS = [int(CHR20 * f) for f in (0.07, 0.29, 0.5, 0.71, 0.9)]
@@ -378,6 +391,13 @@ def test_c3_frag_plus_jump_graph(gpu_ctx):
     for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable"):
         assert ea["precorrect"][k] == ost[k], k
     assert ea["bases_kept"] == int(okeep.astype(np.uint64).sum())
+    # the whole all_reads graph (filled fragments ++ trimmed jumps) against the
+    # oracle's graph of the same reads: every unipath, unibase, HKP vertex /
+    # edge and every read's KmerPath
+    allr_host = gpu_ctx.download(allr)
+    assert allr_host.n_reads == n_all
+    assert_graph_equal(ga, oracle.unipaths(allr_host, K96))
+    del allr_host
     # window parity with the window's jump reads in the oracle's input
     w0 = CHR20 // 3
     w1 = w0 + 200_000

@@ -165,3 +165,19 @@ def test_qualb_offsets_checked_beside_the_load(gpu_ctx, tmp_path):
     d = gpu_ctx.load_reads(fb2, qb2)
     _same(gpu_ctx, d, ReadSet.load(fb2, qb2), True)
     d.free()
+    # the bad set's error sticks to it.  A second load on the
+    # context joins the first (without failing itself), and every later
+    # reader of the bad set's qualities still fails.
+    bad = gpu_ctx.load_reads(fb, qb)
+    good = gpu_ctx.load_reads(fb2, qb2)
+    _same(gpu_ctx, good, ReadSet.load(fb2, qb2), True)
+    for _ in range(2):
+        with pytest.raises(ApgError):
+            gpu_ctx.precorrect(bad, K=24)
+    with pytest.raises(ApgError):
+        gpu_ctx.download(bad, with_quals=True)
+    # overwriting its qualities from a good set clears it
+    gpu_ctx.copy_reads(bad, good)
+    _same(gpu_ctx, bad, ReadSet.load(fb2, qb2), True)
+    bad.free()
+    good.free()

@@ -23,16 +23,31 @@ import torch
 from allpathslg_amd import Context, synth_genome, synth_reads
 g = synth_genome(8_000_000, 0x3E3)
 reads = synth_reads(g, 1_500_000, seed=0x3E4)
+again = None
 with Context(device=0, verbose=True) as ctx:
     d = ctx.upload(reads)
-    if {fused!r} == "sharded":  # the driver's per-rank path at world size 1 over RCCL
+    if {fused!r} in ("sharded", "sharded_gather"):  # the driver's per-rank path at world size 1 over RCCL
         from allpathslg_amd.distributed import Comm, sharded_fill, sharded_spectrum_precorrect, sharded_unipaths, unique_id
         comm = Comm.rccl(ctx, unique_id(), 0, 1)
         hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24)
         filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
-        graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True)
+        graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True, gather_nodes={fused!r} == "sharded_gather")
         ust = {{k: v for k, v in ust.items() if k != "n_shards"}}
         comm.close()
+    elif {fused!r} == "again":  # the bench loop: a second counting pass after the unipath stage (ADVICE r05)
+        d0 = ctx.upload(reads)
+        hist, st, pst = ctx.spectrum_precorrect(d, K_spec=25, K=24)
+        filled, _, fst = ctx.fill_fragments(d, K=24, last_solid=True)
+        graph, ust = ctx.unipaths(filled, 96)
+        ctx.copy_reads(d, d0)
+        h2, st2, pst2 = ctx.spectrum_precorrect(d, K_spec=25, K=24)
+        f2 = ctx.download(d)
+        filled2, _, fst2 = ctx.fill_fragments(d, K=24, last_solid=True, out=filled)
+        again = {{"hsum": int(h2.astype(np.uint64).sum()), "pst": {{k: pst2[k] for k in ("n_suspect", "n_corrected", "n_solid")}},
+                 "fixed": int(np.frombuffer(f2.packed.tobytes(), np.uint64).sum() % (1 << 61)),
+                 "filled": fst2["n_filled"], "filled_bases": fst2["filled_bases"]}}
+        ctx.copy_reads(d, d0)
+        ctx.spectrum_precorrect(d, K_spec=25, K=24)  # leaves d as the first pass did
     else:
       if {fused!r}:  # the bench's entry point: K+1 pass on the side stream (joined before any release)
         hist, st, pst = ctx.spectrum_precorrect(d, K_spec=25, K=24)
@@ -48,15 +63,17 @@ with Context(device=0, verbose=True) as ctx:
            "pst": {{k: pst[k] for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable")}}, "fst": fst, "ust": ust,
            "fixed": int(np.frombuffer(fixed.packed.tobytes(), np.uint64).sum() % (1 << 61)),
            "ub": int(graph["unibases"].astype(np.uint64).sum()), "nu": int(graph["n_unipaths"]),
-           "paths": int(graph["path_start"].astype(np.uint64).sum() % (1 << 61))}}
+           "paths": int(graph["path_start"].astype(np.uint64).sum() % (1 << 61)), "again": again}}
 print("RESULT " + json.dumps(out))
 """
 
 
-def run(limit, fused=False):
+def run(limit, fused=False, hard=False):
     env = dict(os.environ)
     if limit:
         env["APG_DEVICE_MEM_LIMIT"] = str(limit)
+        if hard:
+            env["APG_DEVICE_MEM_HARD"] = "1"
     r = subprocess.run([sys.executable, "-c", CHAIN.format(root=ROOT, fused=fused)], capture_output=True, text=True,
                        env=env,
                        timeout=500)
@@ -65,7 +82,7 @@ def run(limit, fused=False):
     return line, r.stderr
 
 
-@pytest.mark.parametrize("fused", [False, True, "sharded"])
+@pytest.mark.parametrize("fused", [False, True, "sharded", "sharded_gather"])
 def test_release_under_memory_pressure_keeps_results(fused):
     """fused: apg_spectrum_precorrect_dev (the bench's entry point), whose
     K+1 pass on the side stream reads the record buffers the release frees —
@@ -83,3 +100,23 @@ def test_release_under_memory_pressure_keeps_results(fused):
     assert tight_run == free_run
     if fused:
         assert run(0, False)[0] == free_run
+
+
+def test_second_count_after_unipaths_under_a_hard_limit():
+    """the unipath stage marks the correction tables dead; a
+    counting pass after it (the bench loop's next step) writes its solid list
+    into one of them, so a failed allocation inside that count must not
+    release it.  APG_DEVICE_MEM_HARD makes allocations past the emulated
+    device fail as real ones do; the second pass's results must equal the
+    first's and the unconstrained run's."""
+    free_run, log0 = run(0, "again")
+    peak = max(float(x.split("all workspaces ")[1].split(" GB")[0]) for x in log0.splitlines()
+               if "all workspaces" in x)
+    import json
+
+    free = json.loads(free_run[7:])
+    assert free["again"]["hsum"] == free["hsum"] and free["again"]["pst"]["n_corrected"] == free["pst"]["n_corrected"]
+    for frac in (0.8, 0.65):
+        tight_run, log1 = run(int(peak * frac * 1e9), "again", hard=True)
+        print(frac, [x for x in log1.splitlines() if "released" in x])
+        assert tight_run == free_run, frac

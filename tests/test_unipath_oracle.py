@@ -87,3 +87,34 @@ def test_noisy_reads_invariants(K):
     u = oracle.unipaths(reads, K)
     assert u["n_unipaths"] > 10
     check_invariants(u, reads, K)
+
+
+GOLDEN_KEYS = ("len", "id_base", "rc", "ub_off", "unibases", "from", "to", "path_off", "path_start", "path_len")
+
+
+@pytest.mark.parametrize("threads,parcel", [(1, None), (8, None), (3, "5000"), (8, "777")])
+def test_oracle_graph_equals_golden_fixture(threads, parcel, monkeypatch):
+    """The restatement (hash-parcelled node fold, hash node index, one-pass
+    read paths since round 6) against the committed golden graphs
+    (tests/golden/stages_small.npz, written by the round-1 sort-based form):
+    at one and several threads, and with parcels forced small so that the
+    node fold takes several passes."""
+    import os
+
+    from allpathslg_amd import ReadSet
+
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    z = np.load(os.path.join(gold, "stages_small.npz"))
+    reads = ReadSet.load(os.path.join(gold, "frag_small.fastb"), os.path.join(gold, "frag_small.qualb"))
+    frags = ReadSet.load(os.path.join(gold, "frag_small_fill.fastb"))
+    if parcel:
+        monkeypatch.setenv("ORU_PARCEL_INSTANCES", parcel)
+    before = oracle.threads()
+    oracle.set_threads(threads)
+    try:
+        for K, src in ((31, reads), (96, frags)):
+            g = oracle.unipaths(src, K)
+            for key in GOLDEN_KEYS:
+                assert np.array_equal(np.asarray(g[key]), z[f"u{K}_{key}"]), (K, key)
+    finally:
+        oracle.set_threads(before)
