@@ -485,6 +485,8 @@ SIGNATURES = {
                                    C.POINTER(apg_fill_stats)]),
     "apg_sharded_unipaths": (C.c_int, [_P, _P, _P, C.POINTER(apg_unipath_params), C.POINTER(apg_unipath_graph),
                                        C.POINTER(apg_unipath_stats)]),
+    "apg_sharded_error_correct_jump": (
+        C.c_int, [_P, _P, _P, _P, C.POINTER(apg_ecj_params), C.c_void_p, C.POINTER(apg_ecj_stats)]),
     "apg_sharded_unipath_locs": (
         C.c_int, [_P, _P, _P, C.c_uint32, C.POINTER(C.c_void_p), _u64p, C.POINTER(apg_uloc_stats)]),
     "apg_sharded_consensus": (C.c_int, [_P, _P, _P, _P, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),

@@ -246,6 +246,16 @@ struct apg_ctx {
   // list — apg_solid_upload, a sharded pass — no longer matches)
   const uint64_t* pc_self_list = nullptr;
   uint64_t pc_self_n = 0;
+  // pc_shard: pc_list is the replicated solid set a sharded correction pass
+  // over `pc_shard_comm` gathered — the global solid set of every rank's
+  // corrected reads; this rank's part of them has generation pc_shard_gen
+  // (apg_sharded_error_correct_jump reuses it, as ecj_run does pc_self)
+  bool pc_shard = false;
+  const void* pc_shard_comm = nullptr;
+  uint64_t pc_shard_gen = 0;
+  const uint64_t* pc_shard_list = nullptr;
+  uint64_t pc_shard_n = 0;
+  uint32_t pc_shard_min_solid = 0;
   // Per-read clean flags of that pass (1: every K-mer solid after correction,
   // 0: not, 2: not derived), valid for the read set while its gen is clean_gen.
   const uint8_t* pc_clean = nullptr;

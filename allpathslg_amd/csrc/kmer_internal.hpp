@@ -79,6 +79,10 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
                            SkResult* up_res, bool split_recs = false, uint64_t n_kmers = ~0ull,
                            unsigned long long* weak = nullptr, const uint64_t* wpos = nullptr,
                            SkSelf self = SkSelf{});
+// ErrorCorrectJump's correction pass and trim of the jump reads against a
+// given solid list of the fragment reads (precorrect.hip)
+int ecj_with_solid(apg_ctx* ctx, apg_dreads* jr, const apg_ecj_params& e, const uint64_t* solid, uint64_t n_solid,
+                   uint32_t* d_keep, apg_ecj_stats* st);
 // PreCorrect's correction pass over reads whose weak bitmap ("pc_weak") the
 // owner count already built (sk_shard_solid_weak with weak + wpos)
 int precorrect_weak_built(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, const void* d_solid,

@@ -1494,12 +1494,6 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
   APG_REQUIRE(jr->n_reads == 0 || jr->d_quals, "apg_error_correct_jump: jump reads have no qualities");
   APG_REQUIRE(jr->n_reads == 0 || d_keep, "apg_error_correct_jump: keep_len is NULL");
   ctx->ws_dead &= ~kRoomCorrection;  // the fragments' solid set and table may be reused
-  apg_pc_params p;
-  std::memset(&p, 0, sizeof p);
-  p.K = e.K;
-  p.min_solid = e.min_solid;
-  p.max_q_suspect = e.max_q_suspect;
-  p.n_cycles = 1;
   // solid set of the fragment reads: when they are the output of this
   // context's last counting correction pass (same K, same min_solid), that
   // pass's list is their solid set exactly (apg_core.hpp pc_self: a pass
@@ -1516,6 +1510,30 @@ static int ecj_run(apg_ctx* ctx, const apg_dreads* fr, apg_dreads* jr, const apg
     APG_TRY(sk_spectrum(ctx, fr, e.K, true, e.min_solid, nullptr, 0, &sr));
     ctx->solid_valid = false;  // "pc_solid" now holds the fragments' list
   }
+  return ecj_with_solid(ctx, jr, e, sr.solid, sr.n_solid, d_keep, st);
+}
+
+}  // namespace apg
+
+namespace apg {
+// ErrorCorrectJump's correction pass and trim of the jump reads against a
+// given solid list of the fragment reads (ecj_run's count, or the replicated
+// list of a sharded pass: apg_sharded_error_correct_jump)
+int ecj_with_solid(apg_ctx* ctx, apg_dreads* jr, const apg_ecj_params& e, const uint64_t* solid, uint64_t n_solid,
+                   uint32_t* d_keep, apg_ecj_stats* st) {
+  APG_REQUIRE(e.K >= 2 && e.K <= 29, "apg_error_correct_jump: K must be in [2, 29]");
+  APG_REQUIRE(jr->n_reads == 0 || jr->d_quals, "apg_error_correct_jump: jump reads have no qualities");
+  APG_REQUIRE(jr->n_reads == 0 || d_keep, "apg_error_correct_jump: keep_len is NULL");
+  apg_pc_params p;
+  std::memset(&p, 0, sizeof p);
+  p.K = e.K;
+  p.min_solid = e.min_solid;
+  p.max_q_suspect = e.max_q_suspect;
+  p.n_cycles = 1;
+  struct {
+    uint64_t* solid;
+    uint64_t n_solid;
+  } sr{const_cast<uint64_t*>(solid), n_solid};
   // one correction pass of the jump reads against it
   std::memset(st, 0, sizeof *st);
   APG_TRY(correct_pass(ctx, jr, p, sr.solid, sr.n_solid, &st->pc));
@@ -1661,7 +1679,6 @@ int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_count
   APG_REQUIRE(ctx && recv_counts && n_solid, "apg_shard_solid: NULL argument");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid: min_solid must be >= 1");
   ctx->solid_valid = false;
-  ctx->ws_dead &= ~kRoomCorrection;  // this pass writes "pc_solid": live from here on
   APG_REQUIRE(K >= 1 && K <= 32 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
               "apg_shard_solid: K must be in [1, 32], n_shards a power of two <= 8");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
@@ -1698,7 +1715,6 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
   APG_REQUIRE(!up_res || sk_can_fuse_up(K), "apg_shard_solid_weak: the K+1 spectrum cannot ride on this K");
   APG_REQUIRE(min_solid >= 1, "apg_shard_solid_weak: min_solid must be >= 1");
   ctx->solid_valid = false;
-  ctx->ws_dead &= ~kRoomCorrection;  // this pass writes "pc_solid": live from here on
   APG_REQUIRE(K >= 9 && K <= 29 && n_shards >= 1 && n_shards <= 8 && (n_shards & (n_shards - 1)) == 0,
               "apg_shard_solid_weak: K must be in [9, 29], n_shards a power of two <= 8");
   APG_CHECK_HIP(hipSetDevice(ctx->device));

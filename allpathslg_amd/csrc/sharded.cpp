@@ -318,6 +318,37 @@ int sharded_pc(apg_ctx* ctx, apg_comm* comm, apg_dreads* reads, const apg_pc_par
   tot.n_ambiguous = v[2];
   tot.n_uncorrectable = v[3];
   if (stats) *stats = tot;
+  // the replicated list the last cycle corrected against is the global solid
+  // set of the corrected reads (a pass leaves it unchanged): recorded for
+  // apg_sharded_error_correct_jump
+  ctx->pc_shard = ctx->pc_list_valid;
+  ctx->pc_shard_comm = comm;
+  ctx->pc_shard_gen = reads->gen;
+  ctx->pc_shard_list = ctx->pc_list;
+  ctx->pc_shard_n = ctx->pc_n;
+  ctx->pc_shard_min_solid = p.min_solid;
+  return APG_OK;
+}
+
+// The global solid set of every rank's reads, replicated on every rank
+// ("x_solid"): owner counts of the exchanged records, then all-gathered.
+int sharded_solid(apg_ctx* ctx, Comm* c, const apg_dreads* reads, int K, uint32_t min_solid, const uint64_t** solid,
+                  uint64_t* n_solid) {
+  const int P = c->world, B = apg_shard_bins(K, P);
+  APG_REQUIRE(B > 0, "sharded solid set: K / world size unsupported (K <= 32, world <= 8)");
+  std::vector<uint64_t> counts((size_t)P * B);
+  APG_TRY(apg_shard_count(ctx, reads, K, P, counts.data()));
+  Exchanged x;
+  APG_TRY(exchange_records(ctx, c, counts, B, 16, "x_send", "x_recv",
+                           [&](void* send) { return apg_shard_scatter(ctx, reads, K, P, send); }, &x));
+  uint64_t n_local = 0;
+  APG_TRY(apg_shard_solid(ctx, x.recv, x.recv_counts.data(), K, P, min_solid, &n_local));
+  void* local = nullptr;
+  APG_TRY(workspace(ctx, P == 1 ? "x_solid" : "x_local", std::max<uint64_t>(n_local * 8, 64), &local));
+  APG_TRY(apg_solid_export(ctx, local));
+  void* all = nullptr;
+  APG_TRY(gather_all(ctx, c, local, n_local, 8, "x_solid", &all, n_solid));
+  *solid = static_cast<const uint64_t*>(all);
   return APG_OK;
 }
 }  // namespace
@@ -406,6 +437,12 @@ int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
     APG_TRY(apg_urec_nodes(ctx, x.recv, x.recv_counts.data(), K, P, &n_local));
   else
     APG_TRY(apg_ushard_nodes(ctx, x.recv, x.recv_counts.data(), K, P, &n_local));
+  // the graph stage's per-node arrays to come (a copy of the nodes, index,
+  // directed state, ranking and stitch arrays: ~256 bytes per node measured
+  // on the C5-rank rehearsal): the dead record buffers and correction tables
+  // go now if they would not fit beside them, instead of on a failed
+  // allocation later
+  APG_TRY(ws_make_room(ctx, n_local * 256, kRoomCorrection));
   // this rank's nodes outlive the call (the sharded graph's node array, for
   // apg_sharded_unipath_locs): a workspace no other stage writes
   void* local = nullptr;
@@ -432,6 +469,54 @@ int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, 
   }
   APG_TRY(c->allreduce_u64(&n_inst, 1, APG_COMM_SUM));
   st.n_instances = n_inst;
+  if (stats) *stats = st;
+  return APG_OK;
+}
+
+int apg_sharded_error_correct_jump(apg_ctx* ctx, apg_comm* comm, const apg_dreads* frags, apg_dreads* jumps,
+                                   const apg_ecj_params* pp, uint32_t* d_keep_len, apg_ecj_stats* stats) {
+  Comm* c = nullptr;
+  APG_TRY(check_comm(ctx, comm, &c));
+  APG_REQUIRE(frags && jumps, "apg_sharded_error_correct_jump: NULL argument");
+  apg_ecj_params e;
+  if (pp)
+    e = *pp;
+  else
+    apg_ecj_defaults(&e);
+  APG_REQUIRE(e.K >= 2 && e.K <= 29 && e.min_solid >= 1,
+              "apg_sharded_error_correct_jump: K must be in [2, 29], min_solid >= 1");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  ctx->ws_dead &= ~kRoomCorrection;  // the fragments' solid set and table are read again
+  // the global solid set of the fragment reads: the replicated list of their
+  // sharded correction pass over this communicator when it is still the
+  // context's list, else counted across the ranks
+  const uint64_t* solid = nullptr;
+  uint64_t n_solid = 0;
+  if (ctx->pc_shard && ctx->pc_list_valid && ctx->pc_shard_comm == comm && ctx->pc_shard_gen == frags->gen &&
+      ctx->pc_list == ctx->pc_shard_list && ctx->pc_n == ctx->pc_shard_n && ctx->pc_K == e.K &&
+      ctx->pc_shard_min_solid == e.min_solid) {
+    solid = ctx->pc_list;
+    n_solid = ctx->pc_n;
+    vlog(ctx, "sharded error_correct_jump: the fragments' replicated solid set (%llu K-mers)",
+         (unsigned long long)n_solid);
+  } else {
+    APG_TRY(sharded_solid(ctx, c, frags, e.K, e.min_solid, &solid, &n_solid));
+  }
+  apg_ecj_stats st;
+  APG_TRY(ecj_with_solid(ctx, jumps, e, solid, n_solid, d_keep_len, &st));
+  uint64_t v[9] = {st.pc.n_suspect, st.pc.n_corrected, st.pc.n_ambiguous, st.pc.n_uncorrectable, st.n_reads,
+                   st.n_full, st.n_trimmed, st.n_dropped, st.bases_kept};
+  APG_TRY(c->allreduce_u64(v, 9, APG_COMM_SUM));
+  st.pc.n_suspect = v[0];
+  st.pc.n_corrected = v[1];
+  st.pc.n_ambiguous = v[2];
+  st.pc.n_uncorrectable = v[3];
+  st.pc.n_solid = n_solid;
+  st.n_reads = v[4];
+  st.n_full = v[5];
+  st.n_trimmed = v[6];
+  st.n_dropped = v[7];
+  st.bases_kept = v[8];
   if (stats) *stats = st;
   return APG_OK;
 }

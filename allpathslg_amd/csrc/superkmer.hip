@@ -2439,8 +2439,6 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       }
   }
   R *bufA = nullptr, *bufB = spare;
-  APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(n, 1), &bufA));
-  if (!bufB) APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(n, 1), &bufB));
   uint64_t* boff = nullptr;
   APG_TRY(workspace_t(ctx, "sk_boff", (1ull << bb) + 1, &boff));
   const R* cur = src;
@@ -2464,6 +2462,12 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   const char* ue = getenv("APG_SK_UNPACK");
   const bool keep_packed = std::is_same<R, SK24>::value && !(ue && !strcmp(ue, "1")) && nlev >= 1 &&
                            (srcp != nullptr || pack16);
+  // the ping-pong buffers hold what the levels write: 16-byte SKP records
+  // when every level keeps them packed (a C5 rank's count: 2 x 29 GB less
+  // than 24-byte records), else n records of R
+  const uint64_t nbuf = keep_packed ? (n * sizeof(SKP) + sizeof(R) - 1) / sizeof(R) : n;
+  APG_TRY(workspace_t(ctx, kBig1, std::max<uint64_t>(nbuf, 1), &bufA));
+  if (!bufB) APG_TRY(workspace_t(ctx, kBig0, std::max<uint64_t>(nbuf, 1), &bufB));
   if constexpr (std::is_same<R, SK24>::value) {  // SK16 input: widened by the first level, or here
     if (src16 && nlev == 0 && n) {
       k_sk_index24<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(src16, n, spare);
@@ -2569,10 +2573,10 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     if (solid) {  // capacity: each solid K-mer has >= min_solid instances; grown and rerun if exceeded
       ctx->pc_list_valid = false;  // "pc_solid" is about to be overwritten
       ctx->pc_ext_valid = false;
-      // the correction tables are live again: a failed allocation of this
-      // count must not release the list it writes (the unipath stage had
-      // marked them dead)
-      ctx->ws_dead &= ~kRoomCorrection;
+      // the previous pass's correction tables are dead from here until this
+      // count has written its own list into "pc_solid" (cleared there): a
+      // failed allocation may release them before, never after
+      ctx->ws_dead |= kRoomCorrection;
       solid_cap = std::max<uint64_t>(1024, n_kmers / std::max<uint32_t>(min_solid, 1) / 8);
     }
     // the chunked list (kSolidChunk slots per reservation, compacted into
@@ -2774,6 +2778,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           kend(ctx);
           APG_CHECK_HIP(hipGetLastError());
           kbytes_add(ctx, "sk_bucket_solid", n_solid * 8);
+          ctx->ws_dead &= ~kRoomCorrection;  // "pc_solid" holds this pass's list: live
         }
         res->n_distinct = hs[0];
         res->n_overflow_buckets = hs[1] + n_heavy;

@@ -189,6 +189,25 @@ def sharded_unipaths(ctx: Context, comm: Comm, reads: DeviceReads, K: int = 96, 
         lib().apg_unipath_graph_free(C.byref(g))
 
 
+def sharded_error_correct_jump(ctx: Context, comm: Comm, frags: DeviceReads, jumps: DeviceReads, d_keep: int,
+                               K: int = 24, min_solid: int = 3, max_q_suspect: int = 20, min_keep: int = 40) -> dict:
+    """ErrorCorrectJump of this rank's jump reads against the global solid set
+    of every rank's fragment reads (include/apg.h
+    apg_sharded_error_correct_jump): the replicated set of their sharded
+    correction pass when `frags` are its output, else counted across the
+    ranks.  Jumps corrected in place, keep lengths into device d_keep (u32
+    per read); stats summed over ranks."""
+    from ._lib import apg_ecj_params, apg_ecj_stats
+
+    p = apg_ecj_params()
+    lib().apg_ecj_defaults(C.byref(p))
+    p.K, p.min_solid, p.max_q_suspect, p.min_keep = K, min_solid, max_q_suspect, min_keep
+    st = apg_ecj_stats()
+    check(lib().apg_sharded_error_correct_jump(ctx.handle, comm.handle, frags.handle, jumps.handle, C.byref(p),
+                                               C.c_void_p(d_keep), C.byref(st)), "apg_sharded_error_correct_jump")
+    return st.as_dict()
+
+
 def sharded_unipath_locs(ctx: Context, comm: Comm, reads: DeviceReads, rc: bool = True, sorted: bool = True):
     """UnipathLocs of this rank's reads on the global graph of the last
     sharded_unipaths on ctx (include/apg.h apg_sharded_unipath_locs): every

@@ -819,6 +819,17 @@ int apg_sharded_fill(apg_ctx* ctx, apg_comm* comm, const apg_dreads* pairs, cons
                      apg_fill_stats* stats);
 int apg_sharded_unipaths(apg_ctx* ctx, apg_comm* comm, const apg_dreads* reads, const apg_unipath_params* p,
                          apg_unipath_graph* out, apg_unipath_stats* stats);
+/* ErrorCorrectJump of this rank's jump reads against the GLOBAL solid set  */
+/* of every rank's fragment reads (replaces ErrorCorrectJump [R:M]          */
+/* src/paths/ErrorCorrectJump.cc in the sharded flow; grep target only:      */
+/* reference snapshot empty).  When `frags` are the output of this context's */
+/* last apg_sharded_(spectrum_)precorrect over `comm` (same K, min_solid),   */
+/* that pass's replicated solid set is reused (a pass leaves the solid set  */
+/* unchanged), else it is counted across the ranks first.  Jump reads are    */
+/* corrected in place and trimmed exactly as apg_error_correct_jump_dev      */
+/* does on the union; stats summed over ranks (pc.n_solid: the global set).  */
+int apg_sharded_error_correct_jump(apg_ctx* ctx, apg_comm* comm, const apg_dreads* frags, apg_dreads* jumps,
+                                   const apg_ecj_params* p, uint32_t* d_keep_len, apg_ecj_stats* stats);
 /* Read placement and consensus after a sharded build (SURVEY §8e
  * "alignment": unibases replicated, reads sharded) — the multi-GPU forms of
  * apg_unipath_locs_dev and apg_consensus_dev (BuildUnipathLocs /

@@ -76,10 +76,38 @@ def progress(rank, what):
     print(f"[rank {rank}] {what}", file=sys.stderr, flush=True)
 
 
-def chain(ctx, comm, reads, n_cycles, gather=False, placement=True):
-    """The sharded chain on this rank's reads; host copies of everything."""
-    from allpathslg_amd.distributed import (sharded_consensus, sharded_fill, sharded_precorrect, sharded_spectrum,
-                                            sharded_spectrum_precorrect, sharded_unipath_locs, sharded_unipaths)
+JUMP_INSERT = (3000, 300)
+
+
+def jump_reads(g, seed, n_pairs, first_pair=0):
+    """A 3-kb jump library (BASELINE configs[2]) of the simulated genome."""
+    from allpathslg_amd import synth_reads
+
+    return synth_reads(g, n_pairs, seed=seed + 2, insert_mean=JUMP_INSERT[0], insert_sd=JUMP_INSERT[1],
+                       first_pair=first_pair)
+
+
+def ecj_outputs(ctx, dF, jumps, fn):
+    """ErrorCorrectJump of host jump reads against device fragments through
+    fn(dF, dJ, d_keep) -> stats: (corrected jumps with quals, keep, stats)."""
+    import torch
+
+    dJ = ctx.upload(jumps)
+    keep = torch.zeros(max(jumps.n_reads, 1), dtype=torch.int32, device="cuda")
+    st = fn(dF, dJ, keep.data_ptr())
+    out = (ctx.download(dJ, with_quals=True), keep.cpu().numpy()[: jumps.n_reads].view(np.uint32).copy(), st)
+    dJ.free()
+    return out
+
+
+def chain(ctx, comm, reads, n_cycles, gather=False, placement=True, jumps=None):
+    """The sharded chain on this rank's reads; host copies of everything.
+    jumps: this rank's jump pairs, corrected and trimmed by the sharded
+    ErrorCorrectJump after FillFragments (APG_TEST_ECJ_RECOUNT=1: the
+    context's solid set dropped first, so the ranks count it again)."""
+    from allpathslg_amd.distributed import (sharded_consensus, sharded_error_correct_jump, sharded_fill,
+                                            sharded_precorrect, sharded_spectrum, sharded_spectrum_precorrect,
+                                            sharded_unipath_locs, sharded_unipaths)
 
     d = ctx.upload(reads)
     kspec = int(os.environ.get("APG_TEST_KSPEC", "25"))  # != 25: the fused entry point's two-module fallback
@@ -95,10 +123,18 @@ def chain(ctx, comm, reads, n_cycles, gather=False, placement=True):
     filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
     ffrag = ctx.download(filled)
     progress(comm.rank, "fill")
+    ecj = None
+    if jumps is not None:
+        if os.environ.get("APG_TEST_ECJ_RECOUNT") == "1":
+            ctx.trim()
+        ecj = ecj_outputs(ctx, d, jumps, lambda dF, dJ, k: sharded_error_correct_jump(ctx, comm, dF, dJ, k))
+        progress(comm.rank, "error_correct_jump")
     graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True, gather_nodes=gather)
     progress(comm.rank, "unipaths")
     out = {"hist": hist, "st": st, "pst": pst, "fixed": fixed, "fst": fst, "filled": ffrag, "graph": graph,
            "ust": ust}
+    if ecj is not None:
+        out["ecj"] = ecj
     if placement:
         out.update(placement_outputs(
             ctx, d, lambda dd: sharded_unipath_locs(ctx, comm, dd, rc=True, sorted=True),
@@ -109,7 +145,7 @@ def chain(ctx, comm, reads, n_cycles, gather=False, placement=True):
     return out
 
 
-def worker(rank, world, port, cfg, n_cycles, gather, placement, env, q):
+def worker(rank, world, port, cfg, n_cycles, gather, placement, env, q, jump_pairs=0):
     sys.path.insert(0, ROOT)
     os.environ.update(env or {})
     try:
@@ -124,9 +160,13 @@ def worker(rank, world, port, cfg, n_cycles, gather, placement, env, q):
         g = synth_genome(genome_len, seed)
         a, b = rank_pairs(pairs, rank, world)
         reads = synth_reads(g, b - a, seed=seed + 1, first_pair=a)
+        jumps = None
+        if jump_pairs:
+            ja, jb = rank_pairs(jump_pairs, rank, world)
+            jumps = jump_reads(g, seed, jb - ja, first_pair=ja)
         with Context(device=0) as ctx:
             comm = Comm.tcp(ctx, "127.0.0.1", port, rank, world, timeout_ms=600_000)
-            out = chain(ctx, comm, reads, n_cycles, gather, placement)
+            out = chain(ctx, comm, reads, n_cycles, gather, placement, jumps)
             comm.close()
         q.put((rank, out, ""))
     except Exception as e:  # noqa: BLE001
@@ -135,13 +175,14 @@ def worker(rank, world, port, cfg, n_cycles, gather, placement, env, q):
         q.put((rank, None, repr(e) + traceback.format_exc()))
 
 
-def run_world(cfg, world, n_cycles, gather=False, placement=True, timeout=300, env=None):
+def run_world(cfg, world, n_cycles, gather=False, placement=True, timeout=300, env=None, jump_pairs=0):
     """env: extra environment of the rank processes (e.g. APG_CONS_CHUNK, a
-    consensus plane smaller than the targets; APG_GRAPH_FLUSH_ROUND)."""
+    consensus plane smaller than the targets; APG_GRAPH_FLUSH_ROUND).
+    jump_pairs: a jump library of that many pairs, split over the ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    ps = [ctx.Process(target=worker, args=(r, world, port, cfg, n_cycles, gather, placement, env, q))
+    ps = [ctx.Process(target=worker, args=(r, world, port, cfg, n_cycles, gather, placement, env, q, jump_pairs))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -154,7 +195,7 @@ def run_world(cfg, world, n_cycles, gather=False, placement=True, timeout=300, e
     return [r[1] for r in res]
 
 
-def mono_chain(gpu_ctx, cfg, n_cycles, placement=True, kspec=25):
+def mono_chain(gpu_ctx, cfg, n_cycles, placement=True, kspec=25, jump_pairs=0):
     """The single-GPU entry points on the union of the ranks' reads."""
     from allpathslg_amd import synth_genome, synth_reads
 
@@ -167,9 +208,15 @@ def mono_chain(gpu_ctx, cfg, n_cycles, placement=True, kspec=25):
     fixed = gpu_ctx.download(d)
     filled, _, fst = gpu_ctx.fill_fragments(d, K=24, last_solid=True)
     ffrag = gpu_ctx.download(filled)
+    ecj = None
+    if jump_pairs:
+        ecj = ecj_outputs(gpu_ctx, d, jump_reads(g, seed, jump_pairs),
+                          lambda dF, dJ, k: gpu_ctx.error_correct_jump(dF, dJ, d_keep=k))
     graph, ust = gpu_ctx.unipaths(filled, 96)
     out = {"reads": reads, "hist": hist, "st": st, "pst": pst, "fixed": fixed, "fst": fst, "filled": ffrag,
            "graph": graph, "ust": ust}
+    if ecj is not None:
+        out["ecj"] = ecj
     if placement:
         out.update(placement_outputs(gpu_ctx, d, lambda dd: gpu_ctx.unipath_locs(dd, rc=True, sorted=True),
                                      gpu_ctx.consensus_dev))
@@ -182,6 +229,23 @@ def rows(r, a, b):
     """Reads [a, b) of a host read set as (lengths, packed bytes, quals)."""
     s = r.subset(a, b)
     return s.lengths(), s.packed[: int(s.byte_off[-1])], s.quals
+
+
+def check_ecj_against_mono(parts, m, world, jump_pairs):
+    """Each rank's corrected, trimmed jump reads = its slice of the single-GPU
+    ErrorCorrectJump of the union; stats summed over ranks equal."""
+    mj, mk, ms = m["ecj"]
+    for rank, p in enumerate(parts):
+        gj, gk, gs = p["ecj"]
+        a, b = rank_pairs(jump_pairs, rank, world)
+        for x, y in zip(rows(gj, 0, gj.n_reads), rows(mj, 2 * a, 2 * b)):
+            assert np.array_equal(x, y), rank
+        assert np.array_equal(gk, mk[2 * a : 2 * b]), rank
+        for k in ("n_reads", "n_full", "n_trimmed", "n_dropped", "bases_kept"):
+            assert gs[k] == ms[k], (rank, k)
+        for k in ("n_suspect", "n_corrected", "n_ambiguous", "n_uncorrectable", "n_solid"):
+            assert gs["precorrect"][k] == ms["precorrect"][k], (rank, k)
+    assert ms["precorrect"]["n_corrected"] > 0 and ms["n_trimmed"] + ms["n_dropped"] > 0
 
 
 def check_against_mono(parts, m, world, pairs):

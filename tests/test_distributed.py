@@ -58,6 +58,30 @@ def test_sharded_fused_spectrum_precorrect_equals_single_gpu(mono, world, n_cycl
     check_against_mono(run_world(CFG, world, n_cycles, env=env), mono[n_cycles], world, PAIRS)
 
 
+JUMP_PAIRS = 6_000
+
+
+@pytest.fixture(scope="module")
+def mono_jumps(gpu_ctx):
+    return mono_chain(gpu_ctx, CFG, 1, placement=False, jump_pairs=JUMP_PAIRS)
+
+
+@pytest.mark.parametrize("world,extra", [(2, {"APG_TEST_FUSED_SHARDED": "1"}), (4, None),
+                                         (2, {"APG_TEST_ECJ_RECOUNT": "1"})])
+def test_sharded_error_correct_jump_equals_single_gpu(mono_jumps, world, extra):
+    """apg_sharded_error_correct_jump (BASELINE configs[2]/[4]'s jump library
+    on N ranks): every rank's corrected and trimmed jump reads equal its slice
+    of the single-GPU ErrorCorrectJump of the union — against the replicated
+    solid set of the fragments' sharded correction pass, and (RECOUNT) with
+    that set dropped, counted across the ranks again."""
+    from dist_chain import check_ecj_against_mono
+
+    env = {"APG_CONS_CHUNK": "100003"} if extra is None else dict(extra)
+    parts = run_world(CFG, world, 1, placement=False, env=env, jump_pairs=JUMP_PAIRS)
+    check_against_mono(parts, mono_jumps, world, PAIRS)
+    check_ecj_against_mono(parts, mono_jumps, world, JUMP_PAIRS)
+
+
 @pytest.fixture(scope="module")
 def mono31(gpu_ctx):
     return mono_chain(gpu_ctx, CFG, 1, placement=False, kspec=31)

@@ -1,28 +1,42 @@
 """Memory rehearsal of one BASELINE.json configs[4] (C5, human 30x on
-8 x MI355X) rank on one GPU (DESIGN.md §7 memory model).
+8 x MI355X) rank on one GPU (DESIGN.md §7 memory
+model): "full spectrum -> unipath -> LongReadConsensus", pairs + jumps.
 
-A C5 rank holds 112.5 M reads (1/8 of 900 M) of a 3.1-Gb genome.  Here one
-process runs the driver's per-rank path at world size 1 over RCCL — the owner
-count then receives exactly the rank's own records, the size a C5 owner
-receives — through the counting, correction, FillFragments and sharded
-unipath stages, logging the context's device memory after each stage
-(apg_mem_stats_get).  min_solid = 2 so that the solid set approaches a C5
-rank's replicated one (1.95 G K-mers at this rank's 3.6x coverage; ~2.7 G at
-C5's 29x with min_solid 3) and the (K-1)-mer extension table takes 2^33 slots
-(69 GB; C5: 2^34, or 2^33 at load 0.5 under pressure): the correction stage
-cannot sit beside the counting buffers on a 288 GB device, so the release
-path must run (DESIGN.md §7 release point 1).
+A C5 rank holds 112.5 M frag reads (1/8 of 900 M) of a 3.1-Gb genome and its
+share of a 3-kb jump library (12.5 M pairs here).  One process runs the
+driver's per-rank path at world size 1 over RCCL — the owner count then
+receives exactly the rank's own records, the size a C5 owner receives —
+through every stage, logging the context's device memory after each
+(apg_mem_stats_get):
 
-Asserted: the stages complete, both release paths ran (the stage buffers
-before the extension table; the dead correction tables on the unipath
-stage's failed allocation), the count / correction / fill stages stay under
-260 GB with the read set, the unipath stage under 300 GB of the device's
-309 GB (DESIGN.md §7 records the measured peaks), and the spectrum's
-size-independent properties hold.  The
-first run of this rehearsal faulted the GPU: at world size 1 the replicated
-solid list was the rank's own "x_local" buffer, which the release freed under
-the extension-table build (fixed in sharded.cpp; small-scale regression:
-test_gpu_mempressure.py's "sharded" case)."""
+  K=25 spectrum + K=24 PreCorrect (one exchange) -> FillFragments ->
+  ErrorCorrectJump of the jump reads against the replicated solid set
+  (apg_sharded_error_correct_jump) -> all_reads = filled fragments ++ trimmed
+  jumps -> sharded K=96 unipaths of all_reads -> UnipathLocs of the rank's
+  corrected frag reads on that graph (apg_sharded_unipath_locs) ->
+  consensus of the placements over the whole unibase column range
+  (apg_sharded_consensus) in 24 vote-plane chunks, the number C5's ~6.2 G
+  replicated columns take at 2^28 columns per chunk.
+
+min_solid = 2 so that the solid set approaches a C5 rank's replicated one
+(1.95 G K-mers at this rank's 3.6x coverage; ~2.7 G at C5's 29x with
+min_solid 3) and the (K-1)-mer extension table takes 2^33 slots (69 GB; C5:
+2^34, or 2^33 at load 0.5 under pressure): the correction stage cannot sit
+beside the counting buffers on a 288 GB device, so the release path must run
+(DESIGN.md §7 release point 1).
+
+Asserted: the stages complete; the count stage's release ran; every stage
+stays under 270 GB of workspaces + reads (round 5's unipath stage reached
+287.6 GB of workspaces and finished only because a failed allocation released
+the dead correction tables: round 6 sizes the chain-fragment records by
+their count, the count stage's ping-pong buffers for 16-byte packed records,
+and releases dead tables by an up-front estimate, so no allocation fails);
+the consensus equals the unibase on > 99.9 % of the voted columns; the
+spectrum's size-independent properties hold.  The first run of this
+rehearsal (round 5) faulted the GPU: at world size 1 the replicated solid
+list was the rank's own "x_local" buffer, which the release freed under the
+extension-table build (fixed in sharded.cpp; small-scale regression:
+test_gpu_mempressure.py's "sharded" cases)."""
 import json
 import os
 import subprocess
@@ -35,49 +49,113 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1100)]
 
 GENOME = 3_100_000_000
 PAIRS = 56_250_000  # 112.5 M reads
+JUMP_PAIRS = 12_500_000  # 25 M 3-kb jump reads
+PLANE_CHUNKS = 24
 
 SCRIPT = r"""
-import json, sys, time
+import json, os, sys, time
 import numpy as np
 sys.path.insert(0, {root!r})
 import torch
 from allpathslg_amd import Context, synth_genome, synth_reads
-from allpathslg_amd.distributed import Comm, sharded_fill, sharded_spectrum_precorrect, sharded_unipaths, unique_id
+from allpathslg_amd.distributed import (Comm, sharded_consensus, sharded_error_correct_jump, sharded_fill,
+                                        sharded_spectrum_precorrect, sharded_unipath_locs, sharded_unipaths,
+                                        unique_id)
 t0 = time.time()
 def log(*a):
     print("[c5]", f"{{time.time() - t0:7.1f}}s", *a, file=sys.stderr, flush=True)
 g = synth_genome({genome}, 0xC5)
 log("genome")
 reads = synth_reads(g, {pairs}, seed=0xC5 + 1, threads=16)
+jumps = synth_reads(g, {jpairs}, seed=0xC5 + 2, insert_mean=3000, insert_sd=300, threads=16)
 del g
-log("reads", reads.n_reads, reads.n_bases)
+log("reads", reads.n_reads, reads.n_bases, "jumps", jumps.n_reads)
 stages = {{}}
+times = {{}}
+def stage(name, t):
+    stages[name] = ctx.mem_stats(reset_peak=True)
+    times[name] = round(time.time() - t, 2)
+    log(name, {{k: round(v / 1e9, 1) for k, v in stages[name].items() if k != "releases"}}, "releases",
+        stages[name]["releases"])
 with Context(device=0, verbose=True) as ctx:
     d = ctx.upload(reads)
     nb = reads.n_bases
     n_reads = reads.n_reads
     del reads
+    dJ = ctx.upload(jumps)
+    nj = jumps.n_reads
+    del jumps
     stages["reads"] = ctx.mem_stats(reset_peak=True)
     comm = Comm.rccl(ctx, unique_id(), 0, 1)
+    t = time.time()
     hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24, min_solid=2)
-    stages["count+correct"] = ctx.mem_stats(reset_peak=True)
+    stage("count+correct", t)
     log("count + correction", pst)
+    t = time.time()
     filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
-    stages["fill"] = ctx.mem_stats(reset_peak=True)
+    stage("fill", t)
     log("fill", fst)
-    _, ust = sharded_unipaths(ctx, comm, filled, 96)
-    stages["unipaths"] = ctx.mem_stats(reset_peak=True)
+    t = time.time()
+    keep = torch.zeros(nj, dtype=torch.int32, device="cuda")
+    est = sharded_error_correct_jump(ctx, comm, d, dJ, keep.data_ptr(), min_solid=2)
+    stage("ecj", t)
+    log("ecj", est)
+    t = time.time()
+    allr = ctx.concat_reads([filled, dJ], [None, keep.data_ptr()])
+    n_all = allr.n_reads
+    filled.free()
+    dJ.free()
+    del keep
+    _, ust = sharded_unipaths(ctx, comm, allr, 96)
+    stage("unipaths", t)
     log("unipaths", ust)
+    allr.free()
+    t = time.time()
+    p, n, lst = sharded_unipath_locs(ctx, comm, d, rc=True, sorted=True)
+    stage("locs", t)
+    log("locs", n, lst)
+    t = time.time()
+    dT = ctx.unibases_dev()
+    nt = dT.n_bases
+    os.environ["APG_CONS_CHUNK"] = str((nt + {chunks} - 1) // {chunks})  # read at the first consensus call
+    cb = torch.zeros(nt, dtype=torch.uint8, device="cuda")
+    cq = torch.zeros(nt, dtype=torch.uint8, device="cuda")
+    sharded_consensus(ctx, comm, d, dT, p, n, cb.data_ptr(), cq.data_ptr())
+    torch.cuda.synchronize()
+    stage("consensus", t)
     comm.close()
+    # consensus vs the unibases on the voted columns (host, in read chunks)
+    ub = ctx.download(dT)
+    dT.free()
+    cbh, cqh = cb.cpu().numpy(), cq.cpu().numpy()
+    del cb, cq
+    voted = agree = 0
+    shifts = np.array([0, 2, 4, 6], dtype=np.uint8)
+    for r0 in range(0, ub.n_reads, 200_000):
+        r1 = min(ub.n_reads, r0 + 200_000)
+        b0, b1 = int(ub.base_off[r0]), int(ub.base_off[r1])
+        y0, y1 = int(ub.byte_off[r0]), int(ub.byte_off[r1])
+        allb = ((ub.packed[y0:y1, None] >> shifts) & 3).reshape(-1)
+        lens = (ub.base_off[r0 + 1:r1 + 1] - ub.base_off[r0:r1]).astype(np.int64)
+        starts = (ub.byte_off[r0:r1].astype(np.int64) - y0) * 4
+        idx = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(b1 - b0)
+        tb = allb[idx]
+        v = cqh[b0:b1] > 0
+        voted += int(v.sum())
+        agree += int((cbh[b0:b1][v] == tb[v]).sum())
     m = np.arange(len(hist), dtype=np.uint64)
-    out = {{"stages": stages, "n_reads": n_reads, "n_bases": nb, "st": st, "pst": pst, "fst": fst, "ust": ust,
-           "sum_mh": int((hist[:-1] * m[:-1]).sum()), "last_bin": int(hist[-1]), "hsum": int(hist.sum())}}
+    out = {{"stages": stages, "times_s": times, "n_reads": n_reads, "n_bases": nb, "n_jump_reads": nj,
+           "n_all_reads": n_all, "st": st, "pst": pst, "fst": fst, "ecj": est, "ust": ust, "lst": lst, "n_locs": n,
+           "unibase_columns": nt, "plane_chunk": int(os.environ["APG_CONS_CHUNK"]), "voted": voted,
+           "agree": agree, "sum_mh": int((hist[:-1] * m[:-1]).sum()), "last_bin": int(hist[-1]),
+           "hsum": int(hist.sum())}}
 print("RESULT " + json.dumps(out))
 """
 
 
 def test_c5_rank_memory_rehearsal():
-    r = subprocess.run([sys.executable, "-u", "-c", SCRIPT.format(root=ROOT, genome=GENOME, pairs=PAIRS)],
+    r = subprocess.run([sys.executable, "-u", "-c", SCRIPT.format(root=ROOT, genome=GENOME, pairs=PAIRS,
+                                                                  jpairs=JUMP_PAIRS, chunks=PLANE_CHUNKS)],
                        capture_output=True, text=True, timeout=1050)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "c5_rehearsal.log"), "w") as f:
@@ -87,28 +165,31 @@ def test_c5_rank_memory_rehearsal():
     with open(os.path.join(ROOT, "gpurun_out", "c5_rehearsal.json"), "w") as f:
         json.dump(out, f, indent=1)
     S = out["stages"]
-    # the read set (2-bit bases, quals, offsets) is held outside the workspaces
-    reads_gb = (out["n_bases"] / 4 + out["n_bases"] + 16 * out["n_reads"]) / 1e9
+    # the read sets (2-bit bases, quals, offsets) are held outside the workspaces
+    nb = out["n_bases"] + 100 * out["n_jump_reads"]
+    reads_gb = (nb / 4 + nb + 16 * (out["n_reads"] + out["n_jump_reads"])) / 1e9
     print({k: (round(v["workspace_peak"] / 1e9, 1), round(v["device_used"] / 1e9, 1), v["releases"])
-           for k, v in S.items()}, f"reads {reads_gb:.1f} GB")
-    assert out["n_reads"] == 2 * PAIRS
+           for k, v in S.items()}, f"reads {reads_gb:.1f} GB", out["times_s"])
+    assert out["n_reads"] == 2 * PAIRS and out["n_jump_reads"] == 2 * JUMP_PAIRS
     # the release path ran (the correction tables could not sit beside the count buffers)
     assert S["count+correct"]["releases"] >= 1
     assert "dead stage buffers released" in r.stderr
-    # DESIGN.md §7 stage peaks (GB, the reads included), measured on this
-    # rehearsal: every stage leaves room on the 288 GB device
-    # (measured: count + correction 231.5 GB of workspaces at the count, 120 GB
-    # after the release; fill 124; the unipath stage ran into the device
-    # limit with the dead correction tables held, released them (112 GB) and
-    # finished at 274 GB — this rank's 3.6x K=96 coverage leaves 0.41 G nodes
-    # mostly distinct per bucket, so 130 K node buckets overflowed to the
-    # 52 GB global table, which a 29x C5 rank does not need)
-    assert S["count+correct"]["workspace_peak"] / 1e9 + reads_gb <= 260
-    assert S["fill"]["workspace_peak"] / 1e9 + reads_gb <= 260
-    assert S["unipaths"]["releases"] >= 2  # the dead correction tables went on a failed allocation
-    assert S["unipaths"]["workspace_bytes"] / 1e9 + reads_gb <= 300
+    # no stage relied on a failed allocation (round 5's unipath stage did)
+    assert "after a failed allocation" not in r.stderr
+    # DESIGN.md §7 stage peaks (GB, the reads included): every stage leaves
+    # room on the 288 GB device
+    for k in ("count+correct", "fill", "ecj", "unipaths", "locs", "consensus"):
+        assert S[k]["workspace_peak"] / 1e9 + reads_gb <= 270, (k, S[k]["workspace_peak"] / 1e9, reads_gb)
     assert out["ust"]["n_nodes"] > 300_000_000  # a C5 rank's share of the 2.9 G-node graph
-    assert reads_gb < 32
+    assert reads_gb < 40
+    # the jump library went through ErrorCorrectJump into all_reads
+    e = out["ecj"]
+    assert e["n_reads"] == out["n_jump_reads"] and e["precorrect"]["n_corrected"] > 0
+    assert out["n_all_reads"] == out["fst"]["n_filled"] + out["n_jump_reads"]
+    # LongReadConsensus leg: every plane chunk, consensus = unibase where voted
+    assert out["plane_chunk"] * PLANE_CHUNKS >= out["unibase_columns"] > out["plane_chunk"] * (PLANE_CHUNKS - 1)
+    assert out["lst"]["n_placed"] > 0 and out["voted"] > 0
+    assert out["agree"] > 0.999 * out["voted"], (out["agree"], out["voted"])
     # spectrum properties of the 8.55 G K=25 instances
     st = out["st"]
     assert st["n_kmers"] == out["n_reads"] * 76

@@ -102,21 +102,40 @@ def test_release_under_memory_pressure_keeps_results(fused):
         assert run(0, False)[0] == free_run
 
 
+def _final_sizes(log):
+    """Each workspace's last size and the last total (GB) from a verbose log."""
+    sizes, total = {}, 0.0
+    for x in log.splitlines():
+        if "all workspaces" not in x or "] workspace " not in x:
+            continue
+        name, rest = x.split("] workspace ")[1].split(" -> ")
+        sizes[name] = float(rest.split(" GB")[0])
+        total = float(x.split("all workspaces ")[1].split(" GB")[0])
+    return sizes, total
+
+
 def test_second_count_after_unipaths_under_a_hard_limit():
     """the unipath stage marks the correction tables dead; a
     counting pass after it (the bench loop's next step) writes its solid list
-    into one of them, so a failed allocation inside that count must not
-    release it.  APG_DEVICE_MEM_HARD makes allocations past the emulated
-    device fail as real ones do; the second pass's results must equal the
-    first's and the unconstrained run's."""
-    free_run, log0 = run(0, "again")
-    peak = max(float(x.split("all workspaces ")[1].split(" GB")[0]) for x in log0.splitlines()
-               if "all workspaces" in x)
+    into one of them, so a failed allocation inside that count may release the
+    previous pass's tables but never the list it has written.
+    APG_DEVICE_MEM_HARD makes allocations past the emulated device fail as
+    real ones do; the limit sits half the correction tables below the free
+    run's final total, so the unipath stage's last allocations fail and
+    release them, and the second pass allocates beside the unipath stage's
+    workspaces.  Every result equals the unconstrained run's, and the second
+    pass's equal the first's."""
     import json
 
+    free_run, log0 = run(0, "again")
     free = json.loads(free_run[7:])
     assert free["again"]["hsum"] == free["hsum"] and free["again"]["pst"]["n_corrected"] == free["pst"]["n_corrected"]
-    for frac in (0.8, 0.65):
-        tight_run, log1 = run(int(peak * frac * 1e9), "again", hard=True)
-        print(frac, [x for x in log1.splitlines() if "released" in x])
-        assert tight_run == free_run, frac
+    sizes, total = _final_sizes(log0)
+    corr = sum(sizes.get(k, 0.0) for k in ("pc_ext", "fill_ext", "ecj_ext", "fill_solid", "x_solid", "pc_solid"))
+    assert corr > 0
+    limit = int((total - corr / 2) * 1e9)
+    tight_run, log1 = run(limit, "again", hard=True)
+    print(f"total {total:.2f} GB, correction tables {corr:.2f} GB, limit {limit / 1e9:.2f} GB")
+    print([x for x in log1.splitlines() if "released" in x])
+    assert "after a failed allocation" in log1
+    assert tight_run == free_run
