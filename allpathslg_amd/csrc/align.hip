@@ -1194,6 +1194,7 @@ int apg_sharded_consensus(apg_ctx* ctx, apg_comm* comm, const apg_dreads* R, con
               "apg_sharded_consensus: ranks hold different target sets");
   static const uint64_t kChunk = getenv("APG_CONS_CHUNK") ? strtoull(getenv("APG_CONS_CHUNK"), nullptr, 10) : (1ull << 28);
   const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(NT, kChunk));
+  APG_TRY(ws_release_graph_temps(ctx, 16 * chunk));  // the vote plane beside a sharded build's dead temporaries
   uint32_t* votes = nullptr;
   APG_TRY(workspace_t(ctx, "a_votes", std::max<uint64_t>(4 * chunk, 4), &votes));
   for (uint64_t c0 = 0; c0 < NT; c0 += chunk) {

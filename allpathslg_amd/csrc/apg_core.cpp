@@ -178,6 +178,57 @@ int ws_make_room(apg_ctx* ctx, uint64_t need, unsigned what) {
   return APG_OK;
 }
 
+// After a unipath build the graph stage's temporaries (record buffers,
+// overflow node tables, ranking and stitch arrays) are dead: only what the
+// graph state (and the sharded build's urstate) points at is read again —
+// by UnipathLocs, apg_unibases_dev, consensus.  Under memory pressure they
+// are released before such a call allocates: every "u_" / "g_" / "usk" /
+// "big" workspace that holds none of those pointers (descriptor buffers
+// stay, for a scatter replay).  A C5-rank's placement stage: ~90 GB.
+int ws_release_graph_temps(apg_ctx* ctx, uint64_t need) {
+  const uint64_t margin = 2ull << 30;
+  if (device_free_bytes(ctx) >= need + margin) return APG_OK;
+  const auto& g = ctx->gstate;
+  const auto& u = ctx->urstate;
+  const void* keep[] = {g.nodes, g.idx, g.head, g.rank, g.uoh, g.ulen, g.urc, g.ub_off, g.ub, g.uloc, g.vu, g.vr,
+                        u.lsucc, u.idx};
+  auto holds = [&](const apg_ctx::Buf& w) {
+    const char* b = static_cast<const char*>(w.p);
+    for (const void* k : keep)
+      if (k && static_cast<const char*>(k) >= b && static_cast<const char*>(k) < b + w.bytes) return true;
+    return false;
+  };
+  APG_TRY(side_join(ctx));
+  APG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->aux && ctx->aux != ctx->stream) APG_CHECK_HIP(hipStreamSynchronize(ctx->aux));
+  if (ctx->side) APG_CHECK_HIP(hipStreamSynchronize(ctx->side));
+  uint64_t freed = 0;
+  for (auto it = ctx->ws.begin(); it != ctx->ws.end();) {
+    const std::string& n = it->first;
+    const bool graph = !n.compare(0, 2, "u_") || !n.compare(0, 2, "g_") || !n.compare(0, 3, "usk") ||
+                       !n.compare(0, 3, "big");
+    if (!graph || n.find("desc") != std::string::npos || !it->second.p || holds(it->second)) {
+      ++it;
+      continue;
+    }
+    freed += it->second.bytes;
+    ctx->ws_bytes -= it->second.bytes;
+    APG_CHECK_HIP(hipFree(it->second.p));
+    it = ctx->ws.erase(it);
+  }
+  // plans whose buffers may be gone: made again on their next use
+  ctx->urstate.valid = false;
+  ctx->urstate.desc = false;
+  ctx->urstate.lsucc = nullptr;
+  ctx->urstate.idx = nullptr;
+  ctx->ustate.valid = false;
+  ctx->ustate.local_ready = false;
+  ++ctx->mem_releases;
+  vlog(ctx, "memory: %.2f GB of dead graph-stage workspaces released for a %.2f GB allocation", freed / 1e9,
+       need / 1e9);
+  return APG_OK;
+}
+
 int staging_get(apg_ctx* ctx, int workers) {
   auto& S = ctx->staging;
   while (S.workers < workers) {

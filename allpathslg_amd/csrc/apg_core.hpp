@@ -362,6 +362,10 @@ uint64_t device_free_bytes(apg_ctx* ctx);
 // Name of the workspace ws_make_room / a failed allocation may release that
 // holds device pointer p (nullptr: none does).
 const char* ws_releasable(apg_ctx* ctx, const void* p);
+// Under memory pressure (device free < need + 2 GiB): the last unipath
+// build's dead temporaries released (everything but what the graph state
+// points at); placement / consensus call it before they allocate.
+int ws_release_graph_temps(apg_ctx* ctx, uint64_t need);
 // Before a large allocation of `need` bytes: when the device lacks it, release
 // the counting stages' dead record / partition workspaces, plus (flags) the
 // count passes' record descriptors (dead once scattered) and the correction

@@ -3107,6 +3107,7 @@ int apg_unipath_locs_dev(apg_ctx* ctx, const apg_dreads* reads, uint32_t flags, 
                          uint64_t* n_locs, apg_uloc_stats* stats) {
   APG_REQUIRE(ctx && reads && d_locs && n_locs, "apg_unipath_locs_dev: NULL argument");
   APG_CHECK_HIP(hipSetDevice(ctx->device));
+  APG_TRY(ws_release_graph_temps(ctx, (reads->n_bases + 16 * reads->n_reads) * 64));
   const ULoc* p = nullptr;
   APG_TRY(ulocs_run(ctx, reads, flags, &p, n_locs, stats));
   *d_locs = reinterpret_cast<const apg_aln_pair*>(p);

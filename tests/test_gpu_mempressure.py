@@ -7,6 +7,7 @@ extension table to load <= 0.5 when even that does not fit.  Emulated here
 with APG_DEVICE_MEM_LIMIT (the context acts as if the device held only that
 much for its workspaces): the chain's results must not change, and the
 release path must have run."""
+import json
 import os
 import subprocess
 import sys
@@ -27,12 +28,27 @@ again = None
 with Context(device=0, verbose=True) as ctx:
     d = ctx.upload(reads)
     if {fused!r} in ("sharded", "sharded_gather"):  # the driver's per-rank path at world size 1 over RCCL
-        from allpathslg_amd.distributed import Comm, sharded_fill, sharded_spectrum_precorrect, sharded_unipaths, unique_id
+        from allpathslg_amd.distributed import (Comm, sharded_consensus, sharded_fill, sharded_spectrum_precorrect,
+                                                sharded_unipath_locs, sharded_unipaths, unique_id)
         comm = Comm.rccl(ctx, unique_id(), 0, 1)
         hist, st, pst = sharded_spectrum_precorrect(ctx, comm, d, 25, K=24)
         filled, fst = sharded_fill(ctx, comm, d, K=24, last_solid=True)
         graph, ust = sharded_unipaths(ctx, comm, filled, 96, fetch=True, gather_nodes={fused!r} == "sharded_gather")
         ust = {{k: v for k, v in ust.items() if k != "n_shards"}}
+        # placement + consensus after the build: under pressure the graph
+        # stage's dead temporaries are released first (ws_release_graph_temps)
+        pl, nl, lst = sharded_unipath_locs(ctx, comm, d, rc=True, sorted=True)
+        locs = torch.empty(max(nl, 1) * 4, dtype=torch.int32, device="cuda")
+        if nl:
+            ctx.device_copy(locs.data_ptr(), pl, 16 * nl)
+        dT = ctx.unibases_dev()
+        cb = torch.zeros(max(dT.n_bases, 1), dtype=torch.uint8, device="cuda")
+        cq = torch.zeros(max(dT.n_bases, 1), dtype=torch.uint8, device="cuda")
+        sharded_consensus(ctx, comm, d, dT, pl, nl, cb.data_ptr(), cq.data_ptr())
+        torch.cuda.synchronize()
+        again = {{"n_locs": nl, "locs": int(locs[: 4 * nl].cpu().numpy().astype(np.int64).sum()),
+                 "cons": int(cb.cpu().numpy().astype(np.uint64).sum()), "consq": int(cq.cpu().numpy().astype(np.uint64).sum())}}
+        dT.free()
         comm.close()
     elif {fused!r} == "again":  # the bench loop: a second counting pass after the unipath stage (ADVICE r05)
         d0 = ctx.upload(reads)
@@ -97,8 +113,13 @@ def test_release_under_memory_pressure_keeps_results(fused):
                if "all workspaces" in x)
     tight_run, log1 = run(int(peak * 0.55e9), fused)
     assert "dead stage buffers released" in log1
+    if fused in ("sharded", "sharded_gather"):
+        assert "dead graph-stage workspaces released" in log1
     assert tight_run == free_run
-    if fused:
+    if fused in ("sharded", "sharded_gather"):  # the placement outputs are the sharded runs' own
+        strip = lambda r: json.dumps(dict(json.loads(r[7:]), again=None))  # noqa: E731
+        assert strip(run(0, False)[0]) == strip(free_run)
+    elif fused:
         assert run(0, False)[0] == free_run
 
 
