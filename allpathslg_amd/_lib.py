@@ -372,6 +372,10 @@ SIGNATURES = {
     "apg_fill_fragments_dev": (
         C.c_int, [_P, _P, C.POINTER(apg_fill_params), C.c_void_p, C.c_uint64, C.POINTER(_P), C.c_void_p,
                   C.POINTER(apg_fill_stats)]),
+    "apg_spectrum_precorrect_fill_dev": (
+        C.c_int, [_P, _P, C.c_int, _u64p, C.c_size_t, C.POINTER(apg_kstats), C.POINTER(apg_pc_params),
+                  C.POINTER(apg_pc_stats), C.POINTER(apg_fill_params), C.POINTER(_P), C.c_void_p,
+                  C.POINTER(apg_fill_stats)]),
     "apg_unipath_defaults": (None, [C.POINTER(apg_unipath_params)]),
     "apg_unipaths": (
         C.c_int,

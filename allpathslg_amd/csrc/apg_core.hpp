@@ -72,6 +72,18 @@ namespace apg {
 // A read set's qualities still streaming in from a .qualb file
 // (apg_reads_load_dev): the host thread that loads them, and its outcome.
 struct DreadsPending;
+// Result of a minimizer-partitioned count (superkmer.hip; device pointers
+// into ctx workspaces, valid until the next counting call on the context).
+struct SkResult {
+  uint64_t* solid = nullptr;  // solid mode: hashes with count >= min_solid ("pc_solid" workspace)
+  uint64_t n_solid = 0;
+  uint64_t n_distinct = 0;
+  uint64_t n_overflow_buckets = 0;  // buckets counted by the global-table fallback
+  uint64_t n_redo_buckets = 0;      // buckets the record-dedup kernel handed back to k_sk_bucket
+  uint64_t nbuckets = 0;
+  uint64_t n_kmers = 0;
+  uint64_t n_records = 0;
+};
 }  // namespace apg
 
 // Device-resident read set.
@@ -121,6 +133,13 @@ struct apg_ctx {
   // the caller's stage number that kicks it); side_join kicks it first
   std::function<int()> side_kick;
   int side_kick_at = 0;
+  // the stage a fused K+1 pass is kicked at when APG_SK_UP_AT is not set
+  // (1; apg_spectrum_precorrect_fill_dev: APG_SK_UP_AT_FILL's or its own)
+  int side_kick_default = 1;
+  // apg_spectrum_precorrect_dev's K+1 count result, written by the side
+  // pass's finish; kstats filled from it once joined (spectrum_precorrect_impl)
+  apg::SkResult up_res_pending;
+  apg_kstats* up_kstats = nullptr;
   // Auxiliary stream: a producer that overlaps the main stream's next
   // kernels and is joined by an event wait (PreCorrect's extension table
   // built beside its candidate scan).

@@ -37,6 +37,9 @@
 namespace apg {
 
 constexpr uint32_t kFillMaxGap = 63;
+// apg_spectrum_precorrect_fill_dev: the PreCorrect stage that kicks the fused
+// K+1 count onto the side stream (APG_SK_UP_AT_FILL overrides)
+constexpr int kFillUpKick = 1;
 
 // (key, bit) from slot s on, v = slot s as already read
 __device__ __forceinline__ void ext_set_from(const ExtTab& t, uint64_t key, uint32_t bit, uint64_t s,
@@ -1202,6 +1205,46 @@ int apg_fill_fragments_dev(apg_ctx* ctx, const apg_dreads* pairs, const apg_fill
                     &st));
   if (stats) *stats = st;
   return APG_OK;
+}
+
+int apg_spectrum_precorrect_fill_dev(apg_ctx* ctx, apg_dreads* reads, int K_spec, uint64_t* hist, size_t hist_len,
+                                     apg_kstats* kstats, const apg_pc_params* pp, apg_pc_stats* pstats,
+                                     const apg_fill_params* fp, apg_dreads** filled, uint8_t* d_status,
+                                     apg_fill_stats* fstats) {
+  APG_REQUIRE(ctx && reads, "apg_spectrum_precorrect_fill_dev: NULL argument");
+  apg_fill_params f;
+  if (fp)
+    f = *fp;
+  else
+    apg_fill_defaults(&f);
+  f.flags |= APG_FILL_LAST_SOLID;
+  APG_TRY(fill_check(f));
+  apg_pc_params p;
+  if (pp)
+    p = *pp;
+  else
+    apg_pc_defaults(&p);
+  APG_REQUIRE(f.K == p.K, "apg_spectrum_precorrect_fill_dev: FillFragments and PreCorrect need the same K");
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  // the fused K+1 count stays on the side stream past PreCorrect, beside
+  // FillFragments' kernels (FillFragments reads the corrected reads and the
+  // pass's extension table, never the K-records or their buckets), and is
+  // kicked at stage APG_SK_UP_AT_FILL (default kFillUpKick) of the pass
+  // unless APG_SK_UP_AT says otherwise; stage 4 = after PreCorrect
+  static const int kick = getenv("APG_SK_UP_AT_FILL") ? atoi(getenv("APG_SK_UP_AT_FILL")) : kFillUpKick;
+  ctx->side_kick_default = kick;
+  int rc = spectrum_precorrect_impl(ctx, reads, K_spec, hist, hist_len, kstats, &p, pstats, false);
+  ctx->side_kick_default = 1;
+  if (rc == APG_OK) rc = side_kick(ctx, 4);
+  apg_fill_stats st;
+  std::memset(&st, 0, sizeof st);
+  if (rc == APG_OK) rc = fill_impl(ctx, reads, f, nullptr, 0, filled, d_status, &st);
+  const int rj = side_join(ctx);  // the K+1 spectrum lands here
+  if (rc == APG_OK) rc = rj;
+  if (rc == APG_OK) rc = up_kstats_fill(ctx);
+  ctx->up_kstats = nullptr;
+  if (rc == APG_OK && fstats) *fstats = st;
+  return rc;
 }
 
 int apg_fill_fragments(apg_ctx* ctx, const apg_reads* pairs, const apg_fill_params* pp, const uint64_t* solid,

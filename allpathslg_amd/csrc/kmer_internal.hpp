@@ -32,16 +32,7 @@ int spectrum_impl(apg_ctx* ctx, const apg_dreads* dr, int K, int mode, uint64_t*
 
 // Minimizer-partitioned counting (superkmer.hip), K <= 32.
 struct SK16;
-struct SkResult {
-  uint64_t* solid = nullptr;  // solid mode: hashes with count >= min_solid ("pc_solid" workspace)
-  uint64_t n_solid = 0;
-  uint64_t n_distinct = 0;
-  uint64_t n_overflow_buckets = 0;  // buckets counted by the global-table fallback
-  uint64_t n_redo_buckets = 0;      // buckets the record-dedup kernel handed back to k_sk_bucket
-  uint64_t nbuckets = 0;
-  uint64_t n_kmers = 0;
-  uint64_t n_records = 0;
-};
+// (SkResult: apg_core.hpp, the context holds a pending one)
 int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint64_t>* rec_counts,
              std::vector<uint64_t>* kmer_counts, uint32_t split = 0);
 int sk_scatter(apg_ctx* ctx, const apg_dreads* dr, int K, int P, SK16* out);
@@ -79,6 +70,11 @@ int shard_solid_weak_fused(apg_ctx* ctx, const void* d_recv, const uint64_t* rec
                            SkResult* up_res, bool split_recs = false, uint64_t n_kmers = ~0ull,
                            unsigned long long* weak = nullptr, const uint64_t* wpos = nullptr,
                            SkSelf self = SkSelf{});
+// apg_spectrum_precorrect_dev; join = false leaves the fused K+1 pass on the
+// side stream (its stats land at up_kstats_fill after the caller's side_join)
+int spectrum_precorrect_impl(apg_ctx* ctx, apg_dreads* dr, int K_spec, uint64_t* hist, size_t hist_len,
+                             apg_kstats* kstats, const apg_pc_params* pp, apg_pc_stats* pstats, bool join);
+int up_kstats_fill(apg_ctx* ctx);
 // ErrorCorrectJump's correction pass and trim of the jump reads against a
 // given solid list of the fragment reads (precorrect.hip)
 int ecj_with_solid(apg_ctx* ctx, apg_dreads* jr, const apg_ecj_params& e, const uint64_t* solid, uint64_t n_solid,

@@ -1321,7 +1321,8 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
 // up_res: the fused K+1 spectrum of the uncorrected reads rides on the count
 // (apg_spectrum_precorrect_dev; sk_can_fuse_up(p.K))
 static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, apg_pc_stats* st,
-                           uint64_t* up_hist = nullptr, size_t up_hist_len = 0, SkResult* up_res = nullptr) {
+                           uint64_t* up_hist = nullptr, size_t up_hist_len = 0, SkResult* up_res = nullptr,
+                           bool join = true) {
   SkResult sr;
   if (p.K >= 9) {  // count + the weak-instance bitmap (no lookups for the weak tests)
     unsigned long long* weak = nullptr;
@@ -1329,8 +1330,10 @@ static int precorrect_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p,
     APG_TRY(sk_solid_weak(ctx, dr, p.K, p.min_solid, weak, &sr, up_hist, up_hist_len, up_res));
     ctx->solid_valid = false;  // "pc_solid" now holds this pass's list
     // the fused K+1 pass may still run on the side stream: joined here, after
-    // the correction kernels it overlaps
+    // the correction kernels it overlaps (join = false: by the caller, after
+    // FillFragments — apg_spectrum_precorrect_fill_dev)
     const int rc = correct_pass(ctx, dr, p, sr.solid, sr.n_solid, st, weak, true);
+    if (!join && rc == APG_OK) return APG_OK;
     const int rj = side_join(ctx);
     return rc != APG_OK ? rc : rj;
   }
@@ -1643,6 +1646,17 @@ int apg_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params* pp, ap
 
 int apg_spectrum_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, int K_spec, uint64_t* hist, size_t hist_len,
                                 apg_kstats* kstats, const apg_pc_params* pp, apg_pc_stats* pstats) {
+  return spectrum_precorrect_impl(ctx, dr, K_spec, hist, hist_len, kstats, pp, pstats, true);
+}
+}  // extern "C"
+
+namespace apg {
+// apg_spectrum_precorrect_dev; join = false (one cycle only) leaves the fused
+// K+1 pass on the side stream for the caller to join (side_join) — its
+// records and buckets must stay untouched until then, and hist / kstats are
+// filled by that join
+int spectrum_precorrect_impl(apg_ctx* ctx, apg_dreads* dr, int K_spec, uint64_t* hist, size_t hist_len,
+                             apg_kstats* kstats, const apg_pc_params* pp, apg_pc_stats* pstats, bool join) {
   APG_REQUIRE(ctx && dr, "apg_spectrum_precorrect_dev: NULL argument");
   apg_pc_params p;
   if (pp)
@@ -1659,20 +1673,35 @@ int apg_spectrum_precorrect_dev(apg_ctx* ctx, apg_dreads* dr, int K_spec, uint64
   APG_CHECK_HIP(hipSetDevice(ctx->device));
   apg_pc_stats st;
   std::memset(&st, 0, sizeof st);
-  SkResult ur;
-  APG_TRY(precorrect_pass(ctx, dr, p, &st, hist, hist_len, &ur));
+  // the K+1 result lands at the join: held by the context until then
+  ctx->up_res_pending = SkResult{};
+  SkResult& ur = ctx->up_res_pending;
+  const bool defer = !join && p.n_cycles == 1;
+  APG_TRY(precorrect_pass(ctx, dr, p, &st, hist, hist_len, &ur, !defer));
   for (uint32_t c = 1; c < p.n_cycles; ++c) APG_TRY(precorrect_pass(ctx, dr, p, &st));
-  if (kstats) {
-    std::memset(kstats, 0, sizeof(*kstats));
-    kstats->n_kmers = ur.n_kmers;
-    kstats->n_distinct = ur.n_distinct;
-    kstats->n_buckets = ur.nbuckets;
-    kstats->n_overflow = ur.n_overflow_buckets;
-    kstats->n_redo = ur.n_redo_buckets;
-  }
+  ctx->up_kstats = kstats;
+  if (!defer) APG_TRY(up_kstats_fill(ctx));
   if (pstats) *pstats = st;
   return APG_OK;
 }
+
+// the fused K+1 count's stats, once its pass is joined
+int up_kstats_fill(apg_ctx* ctx) {
+  apg_kstats* kstats = ctx->up_kstats;
+  ctx->up_kstats = nullptr;
+  if (!kstats) return APG_OK;
+  const SkResult& ur = ctx->up_res_pending;
+  std::memset(kstats, 0, sizeof(*kstats));
+  kstats->n_kmers = ur.n_kmers;
+  kstats->n_distinct = ur.n_distinct;
+  kstats->n_buckets = ur.nbuckets;
+  kstats->n_overflow = ur.n_overflow_buckets;
+  kstats->n_redo = ur.n_redo_buckets;
+  return APG_OK;
+}
+}  // namespace apg
+
+extern "C" {
 
 int apg_shard_solid(apg_ctx* ctx, const void* d_recv, const uint64_t* recv_counts, int K, int n_shards,
                     uint32_t min_solid, uint64_t* n_solid) {

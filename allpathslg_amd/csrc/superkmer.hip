@@ -2849,7 +2849,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           // the inserts and the link pass — same box 141.5-142.2 vs 145.3-145.8
           // ms per step for stage 2 on a full round (0.80: 141.6, 0.92: 143.2,
           // stage 0 at 0.85: 142.2)
-          ctx->side_kick_at = ae ? atoi(ae) : 1;
+          ctx->side_kick_at = ae ? atoi(ae) : ctx->side_kick_default;
           if (ctx->side_kick_at <= 0)
             APG_TRY(launch());
           else

@@ -246,6 +246,28 @@ class Context:
                                                 C.byref(ks), C.byref(p), C.byref(ps)), "apg_spectrum_precorrect_dev")
         return hist, ks.as_dict(), ps.as_dict()
 
+    def spectrum_precorrect_fill(self, dreads: DeviceReads, K_spec: int = 25, K: int = 24, min_solid: int = 3,
+                                 max_q_suspect: int = 20, hist_len: int = DEFAULT_HIST_LEN, min_insert: int = 126,
+                                 max_insert: int = 234, max_steps: int = 1024, out: Optional[DeviceReads] = None,
+                                 d_status: Optional[int] = None):
+        """spectrum_precorrect, then fill_fragments of the corrected pairs
+        against the pass's solid set, in one call
+        (apg_spectrum_precorrect_fill_dev: the fused K+1 count also runs
+        beside FillFragments).  Returns (hist, spectrum stats, correction
+        stats, filled DeviceReads (reusing `out`), fill stats)."""
+        from ._lib import apg_fill_stats
+
+        p = self.pc_params(K, min_solid, max_q_suspect, 1)
+        fp = self.fill_params(K, min_insert, max_insert, max_steps, min_solid, True)
+        hist = np.zeros(hist_len, dtype=np.uint64)
+        ks, ps, fs = apg_kstats(), apg_pc_stats(), apg_fill_stats()
+        fd = out if out is not None else DeviceReads(self, None)
+        check(lib().apg_spectrum_precorrect_fill_dev(self._h, dreads.handle, K_spec, hist.ctypes.data_as(_u64p),
+                                                     hist_len, C.byref(ks), C.byref(p), C.byref(ps), C.byref(fp),
+                                                     C.byref(fd._h), C.c_void_p(d_status) if d_status else None,
+                                                     C.byref(fs)), "apg_spectrum_precorrect_fill_dev")
+        return hist, ks.as_dict(), ps.as_dict(), fd, fs.as_dict()
+
     def copy_reads(self, dst: DeviceReads, src: DeviceReads) -> None:
         """dst := src (device-to-device; same read lengths)."""
         check(lib().apg_reads_copy_dev(self._h, dst.handle, src.handle), "apg_reads_copy_dev")

@@ -86,6 +86,9 @@ def parse():
     p.add_argument("--no-fuse", dest="fuse", action="store_false",
                    help="run KmerSpectrum (K) and PreCorrect (K_correct) as two counting passes instead of "
                         "apg_spectrum_precorrect_dev's one (same results)")
+    p.add_argument("--no-fuse-fill", dest="fuse_fill", action="store_false",
+                   help="call FillFragments as its own module instead of apg_spectrum_precorrect_fill_dev "
+                        "(the fused K+1 count then also runs beside FillFragments; same results)")
     p.add_argument("--overlap", action="store_true",
                    help="run the K=25 spectrum on a second stream concurrently with correction/fill/unipaths")
     p.add_argument("--verbose", action="store_true")
@@ -821,6 +824,11 @@ def main():
         sfused = sharded and not overlap and not a.spectrum_only and a.fuse and a.K == a.K_correct + 1
         if overlap:
             pass
+        elif fused and a.fuse_fill and not a.oracle_fill and a.K == a.K_correct + 1:
+            # one counting pass for both and FillFragments in the same call
+            # (apg_spectrum_precorrect_fill_dev: the K+1 count beside the fill)
+            hist, st, pst, fill["out"], fst = ctx.spectrum_precorrect_fill(dreads, K_spec=a.K, K=a.K_correct,
+                                                                             out=fill["out"])
         elif fused:  # one counting pass for both (apg_spectrum_precorrect_dev)
             hist, st, pst = spectrum_and_precorrect(ctx, dreads, a)
         elif not sharded:
@@ -837,6 +845,8 @@ def main():
                 mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags
+                elif fst is not None:  # filled by apg_spectrum_precorrect_fill_dev
+                    uin = fill["out"]
                 else:
                     fill["out"], _, fst = ctx.fill_fragments(dreads, K=a.K_correct, last_solid=True,
                                                              out=fill["out"])
@@ -1018,7 +1028,9 @@ def main():
                 "K_correct": None if a.spectrum_only else a.K_correct,
                 "K_unipath": None if a.spectrum_only else a.K_unipath,
                 "counting": ("one pass: the K spectrum from PreCorrect's K_correct records "
-                             "(apg_spectrum_precorrect_dev)" if a.fuse and not sharded and not a.spectrum_only
+                             + ("+ FillFragments in the same call (apg_spectrum_precorrect_fill_dev)"
+                                if a.fuse_fill and not a.oracle_fill else "(apg_spectrum_precorrect_dev)")
+                             if a.fuse and not sharded and not a.spectrum_only
                              and not a.overlap else "separate K and K_correct passes"),
                 "stages_timed": ["restore_reads", "kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
                     "precorrect"] + ([] if a.oracle_fill else ["fill_fragments"]) + [

@@ -446,6 +446,17 @@ int apg_fill_fragments(apg_ctx* ctx, const apg_reads* pairs, const apg_fill_para
 int apg_fill_fragments_dev(apg_ctx* ctx, const apg_dreads* pairs, const apg_fill_params* p,
                            const void* d_solid, uint64_t n_solid, apg_dreads** filled,
                            uint8_t* d_status, apg_fill_stats* stats);
+/* KmerSpectrum + PreCorrect + FillFragments of the corrected pairs in one
+ * call (the module chain of SURVEY.md:126-127 on device-resident reads):
+ * results equal apg_spectrum_precorrect_dev(reads, K_spec, hist, ..., pp)
+ * followed by apg_fill_fragments_dev(reads, fp | APG_FILL_LAST_SOLID, NULL,
+ * 0, filled, d_status).  The fused K+1 spectrum count then runs beside
+ * FillFragments' kernels as well as PreCorrect's, joined before the call
+ * returns (hist / kstats complete on return).  fp->K must equal pp->K. */
+int apg_spectrum_precorrect_fill_dev(apg_ctx* ctx, apg_dreads* reads, int K_spec, uint64_t* hist,
+                                     size_t hist_len, apg_kstats* kstats, const apg_pc_params* pp,
+                                     apg_pc_stats* pstats, const apg_fill_params* fp,
+                                     apg_dreads** filled, uint8_t* d_status, apg_fill_stats* fstats);
 
 /* ------------------------------------------------------------------------- */
 /* Unipath graph, 1 <= K <= 96 (default 96).  Replaces CommonPather /        */

@@ -232,8 +232,15 @@ def c2(gpu_ctx):
     gpu_ctx.copy_reads(dwork, dsrc)
     fh, fks, fps = gpu_ctx.spectrum_precorrect(dwork, K_spec=25, K=24)
     fused = {"hist": fh, "st": fks, "pst": fps, "solid": solid_sorted(gpu_ctx), "fixed": gpu_ctx.download(dwork)}
+    # ... and the step's entry point since round 6, with FillFragments in the
+    # same call (apg_spectrum_precorrect_fill_dev)
+    gpu_ctx.copy_reads(dwork, dsrc)
+    ffh, ffks, ffps, ffd, ffst = gpu_ctx.spectrum_precorrect_fill(dwork, K_spec=25, K=24, d_status=status.data_ptr())
+    fused_fill = {"hist": ffh, "st": ffks, "pst": ffps, "fst": ffst, "status": status.cpu().numpy().copy(),
+                  "filled": gpu_ctx.download(ffd), "fixed": gpu_ctx.download(dwork)}
+    ffd.free()
     yield {"genome": g, "reads": reads, "a": a, "b": b, "fixed": fixed_a, "filled_a": filled_a,
-           "filled_b": filled_b, "seed": seed, "dsrc": dsrc, "fused": fused}
+           "filled_b": filled_b, "seed": seed, "dsrc": dsrc, "fused": fused, "fused_fill": fused_fill}
     for d in (dsrc, dwork, a["filled"]):
         d.free()
 
@@ -305,6 +312,21 @@ def test_c2_bench_entry_point_matches_oracle(c2, c2_oracle):
     assert np.array_equal(f["solid"], c2_oracle["solid"])
     assert f["pst"]["n_solid"] == len(c2_oracle["solid"])
     assert_precorrect_equal(f["fixed"], f["pst"], c2_oracle["fixed"], c2_oracle["est"])
+
+
+def test_c2_fused_fill_entry_point_equals_modules(c2, c2_oracle):
+    """apg_spectrum_precorrect_fill_dev at full C2 size (the bench's timed
+    entry point since round 6): spectrum = oracle, corrected reads = oracle,
+    and every fill status, filled fragment and counter equal the modules' run
+    (which test_c2_full_fill_matches_oracle checks against the oracle)."""
+    f = c2["fused_fill"]
+    assert np.array_equal(f["hist"], c2_oracle["hist"])
+    assert_precorrect_equal(f["fixed"], f["pst"], c2_oracle["fixed"], c2_oracle["est"])
+    assert np.array_equal(f["status"], c2["a"]["status"])
+    assert f["fst"] == c2["a"]["fst"]
+    hf, hb = f["filled"], c2["filled_a"]
+    assert np.array_equal(hf.base_off, hb.base_off)
+    assert np.array_equal(hf.packed[: int(hf.byte_off[-1])], hb.packed[: int(hb.byte_off[-1])])
 
 
 def test_c2_full_fill_matches_oracle(c2, c2_oracle):

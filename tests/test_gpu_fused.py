@@ -151,3 +151,36 @@ def test_solid_count_record_forms(gpu_ctx, monkeypatch, env):
     rf = fus[3]
     assert np.array_equal(rf.packed[: int(rf.byte_off[-1])], exp.packed[: int(exp.byte_off[-1])])
     assert np.array_equal(rf.quals, exp.quals)
+
+
+@pytest.mark.parametrize("kick", [None, "0", "2", "3", "4"])
+def test_spectrum_precorrect_fill_equals_modules(gpu_ctx, monkeypatch, kick):
+    """apg_spectrum_precorrect_fill_dev (the bench step's entry point since
+    round 6: the fused K+1 count runs beside FillFragments too) equals
+    apg_spectrum_precorrect_dev followed by apg_fill_fragments_dev with the
+    pass's solid set: spectrum + stats, corrected bases / qualities, every
+    fill status, filled fragment and counter — at every kick stage of the
+    K+1 pass (APG_SK_UP_AT_FILL; 4 = after PreCorrect, beside the fill only)."""
+    import torch
+
+    if kick is not None:
+        monkeypatch.setenv("APG_SK_UP_AT", kick)  # read per call (APG_SK_UP_AT_FILL is read once)
+    g = synth_genome(2_000_000, 41)
+    reads = synth_reads(g, 250_000, seed=42)
+    a, b = gpu_ctx.upload(reads), gpu_ctx.upload(reads)
+    sa = torch.zeros(reads.n_reads // 2, dtype=torch.uint8, device="cuda")
+    sb = torch.zeros(reads.n_reads // 2, dtype=torch.uint8, device="cuda")
+    h1, k1, p1 = gpu_ctx.spectrum_precorrect(a, K_spec=25, K=24)
+    f1, _, fs1 = gpu_ctx.fill_fragments(a, K=24, last_solid=True, d_status=sa.data_ptr())
+    h2, k2, p2, f2, fs2 = gpu_ctx.spectrum_precorrect_fill(b, K_spec=25, K=24, d_status=sb.data_ptr())
+    assert np.array_equal(h1, h2) and k1 == k2 and p1 == p2 and fs1 == fs2
+    assert np.array_equal(h1, oracle.kmer_spectrum(reads, 25))
+    ra, rb = gpu_ctx.download(a, with_quals=True), gpu_ctx.download(b, with_quals=True)
+    assert np.array_equal(ra.packed, rb.packed) and np.array_equal(ra.quals, rb.quals)
+    assert np.array_equal(sa.cpu().numpy(), sb.cpu().numpy())
+    x, y = gpu_ctx.download(f1), gpu_ctx.download(f2)
+    assert np.array_equal(x.base_off, y.base_off)
+    assert np.array_equal(x.packed[: int(x.byte_off[-1])], y.packed[: int(y.byte_off[-1])])
+    assert fs2["n_filled"] > 0
+    for d in (a, b, f1, f2):
+        d.free()
