@@ -188,3 +188,27 @@ def test_fill_last_solid_long_and_short_reads(gpu_ctx):
         same_reads(host, exp)
         out.free()
         d.free()
+
+
+# The general (non-LEAN) k_fill form runs whenever an APG_FILL_* A/B knob is
+# set; round 5 never tested it against the oracle (a two-pass
+# split had diverged).  Every form must give the oracle's statuses and bases.
+@pytest.mark.parametrize("env", [{"APG_FILL_LEAN": "0"}, {"APG_FILL_CAP1": "50"}, {"APG_FILL_CAP1": "1"},
+                                 {"APG_FILL_XSTEPS": "0"}, {"APG_FILL_FUSE_BT": "0"},
+                                 {"APG_FILL_BRANCH_CACHE": "0"}, {"APG_FILL_BRIDGE_FILTER": "0"},
+                                 {"APG_FILL_REFILL": "8"}])
+def test_fill_general_forms_match_oracle(gpu_ctx, monkeypatch, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth_genome(150_000, 5, repeats=True)
+    reads = synth_reads(g, 15_000, seed=105)
+    fixed, _ = oracle.precorrect(reads, K=24)
+    solid = oracle.solid_hashes(reads, 24, 3)
+    args = dict(K=24, min_insert=100, max_insert=260, max_steps=300)
+    got, status, st = gpu_ctx.fill_fragments(fixed, solid, status=True, **args)
+    ef, es, _, est = oracle.fill_fragments(fixed, solid, **args)
+    bad = np.nonzero(status != es)[0]
+    assert len(bad) == 0, (len(bad), list(zip(es[bad[:8]].tolist(), status[bad[:8]].tolist())))
+    same_reads(got, ef)
+    for k in ("n_filled", "n_none", "n_ambiguous", "n_budget", "n_skip", "filled_bases"):
+        assert st[k] == est[k], k
