@@ -6,11 +6,16 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 ${T_TEST:-700} python -u -m pytest ${TESTS} -m gpu -x -v -s --timeout ${T_CASE:-400} \
+  timeout -k 10 ${T_TEST:-700} python -u -m pytest ${TESTS} -m gpu ${XFLAG--x} -v -s --timeout ${T_CASE:-400} \
     --timeout-method thread > gpurun_out/${LOG:-r6_ab}_pytest.log 2>&1
   rc=$?
   tail -4 gpurun_out/${LOG:-r6_ab}_pytest.log
-  [ $rc -eq 0 ] || exit $rc
+  # ordinary test failures (rc 1) go on to the bench; a timeout, fault or
+  # abort ends the call here
+  if [ $rc -ne 0 ]; then
+    if [ $rc -ne 1 ] || grep -q "Timeout" gpurun_out/${LOG:-r6_ab}_pytest.log; then exit $rc; fi
+    FAILED=1
+  fi
 fi
 BA="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --c3-jump-pairs 0 --no-file-to-graph --align-pairs 0 --jump-pairs 0 --no-placement --repeat-steps ${REPS:-0}"
 for V in ${VARIANTS:-}; do
@@ -23,3 +28,4 @@ for V in ${VARIANTS:-}; do
   echo "== $V ($SPEC)"
   python scripts/ab_summary.py gpurun_out/${LOG:-r6_ab}_$V.detail.json
 done
+exit ${FAILED:-0}
