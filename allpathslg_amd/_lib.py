@@ -439,6 +439,8 @@ SIGNATURES = {
         C.c_int, [_P, C.POINTER(apg_aln_pair), C.c_uint64, C.POINTER(apg_ucov_params), _u64p,
                   C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(apg_ucov_stats)]),
     "apg_device_copy": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "apg_device_alloc": (C.c_int, [_P, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "apg_device_free": (None, [_P, C.c_void_p]),
     "apg_device_to_host": (C.c_int, [_P, C.c_void_p, C.c_void_p, C.c_uint64]),
     "apg_dreads_shape": (C.c_int, [_P, _P, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "apg_synth_genome": (C.c_int, [C.c_uint64, C.c_uint64, _u8p]),

@@ -735,6 +735,28 @@ int apg_device_copy(apg_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes
   return APG_OK;
 }
 
+int apg_device_alloc(apg_ctx* ctx, uint64_t bytes, void** d_out) {
+  APG_REQUIRE(ctx && d_out, "apg_device_alloc: NULL argument");
+  *d_out = nullptr;
+  APG_CHECK_HIP(hipSetDevice(ctx->device));
+  void* p = nullptr;
+  APG_CHECK_HIP(hipMalloc(&p, std::max<uint64_t>(bytes, 1)));
+  const hipError_t e = hipMemsetAsync(p, 0, std::max<uint64_t>(bytes, 1), ctx->stream);
+  if (e == hipSuccess && hipStreamSynchronize(ctx->stream) == hipSuccess) {
+    *d_out = p;
+    return APG_OK;
+  }
+  (void)hipFree(p);
+  set_error("apg_device_alloc: zero fill failed");
+  return APG_E_HIP;
+}
+
+void apg_device_free(apg_ctx* ctx, void* d) {
+  if (!d) return;
+  if (ctx) (void)hipSetDevice(ctx->device);
+  (void)hipFree(d);
+}
+
 int apg_device_to_host(apg_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes) {
   APG_REQUIRE(ctx, "apg_device_to_host: NULL ctx");
   if (!bytes) return APG_OK;

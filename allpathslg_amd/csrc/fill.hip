@@ -175,7 +175,11 @@ int ext_build(apg_ctx* ctx, const uint64_t* list, uint64_t n_solid, int K, const
     const uint64_t have = it == ctx->ws.end() ? 0 : it->second.bytes;
     const uint64_t need = T * 8 + 16;
     if (need > have) {
-      APG_TRY(ws_make_room(ctx, need - have, kRoomDescriptors));
+      // room for the table and what the correction pass allocates after it
+      // (candidates, decisions, the fused K+1 count's buffers: a few GB at a
+      // C5 rank, which ran out of memory on 2.8 GB of candidates with only
+      // the 2 GiB margin)
+      APG_TRY(ws_make_room(ctx, need - have + (8ull << 30), kRoomDescriptors));
       if (device_free_bytes(ctx) < need - have + (2ull << 30) && T > 1024) {
         T >>= 1;
         vlog(ctx, "ext table: %llu slots (load <= 0.5 by memory)", (unsigned long long)T);

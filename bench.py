@@ -86,9 +86,10 @@ def parse():
     p.add_argument("--no-fuse", dest="fuse", action="store_false",
                    help="run KmerSpectrum (K) and PreCorrect (K_correct) as two counting passes instead of "
                         "apg_spectrum_precorrect_dev's one (same results)")
-    p.add_argument("--no-fuse-fill", dest="fuse_fill", action="store_false",
-                   help="call FillFragments as its own module instead of apg_spectrum_precorrect_fill_dev "
-                        "(the fused K+1 count then also runs beside FillFragments; same results)")
+    p.add_argument("--fuse-fill", dest="fuse_fill", action="store_true",
+                   help="FillFragments in the same call as the spectrum + PreCorrect "
+                        "(apg_spectrum_precorrect_fill_dev: the fused K+1 count also runs beside FillFragments; "
+                        "same results; measured no faster on the bench step, DESIGN.md §10)")
     p.add_argument("--overlap", action="store_true",
                    help="run the K=25 spectrum on a second stream concurrently with correction/fill/unipaths")
     p.add_argument("--verbose", action="store_true")

@@ -139,6 +139,11 @@ int apg_device_copy(apg_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes
 /* Device-to-host copy (synchronous): a library-owned device output into
  * caller host memory (the drop-in modules' file writers). */
 int apg_device_to_host(apg_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
+/* Device buffers for the *_dev entry points' caller-owned arguments (keep
+ * lengths, statuses, placements) without a HIP dependency in the caller:
+ * bytes on ctx's device, zero-filled; release with apg_device_free. */
+int apg_device_alloc(apg_ctx* ctx, uint64_t bytes, void** d_out);
+void apg_device_free(apg_ctx* ctx, void* d);
 
 /* Fill byte_off[0..n] from base_off[0..n]. */
 int apg_byte_offsets(const uint64_t* base_off, uint64_t n_reads, uint64_t* byte_off);

@@ -143,6 +143,16 @@ def test_cli_error_correct_jump_matches_oracle(tmp_path):
         assert np.array_equal(out.read(r), fixed.read(r)[:k])
         assert np.array_equal(out.quals[int(out.base_off[r]) : int(out.base_off[r + 1])],
                               fixed.quals[int(fixed.base_off[r]) : int(fixed.base_off[r]) + k])
+    # sharded (WORLD=2 / 4 over TCP): the same files byte for byte
+    # (apg_sharded_error_correct_jump: the frags' solid set counted across ranks)
+    ref = {e: (tmp_path / f"jump_reads_ec.{e}").read_bytes() for e in ("fastb", "qualb")}
+    for world in (2, 4):
+        for e in ("fastb", "qualb"):
+            (tmp_path / f"jump_reads_ec.{e}").unlink()
+        for rc, o, e in _run_ranks("ErrorCorrectJump", world, f"RUN={tmp_path}", "K=24"):
+            assert rc == 0, (world, e)
+        for e in ("fastb", "qualb"):
+            assert (tmp_path / f"jump_reads_ec.{e}").read_bytes() == ref[e], (world, e)
 
 
 @pytest.mark.gpu

@@ -372,28 +372,56 @@ int error_correct_jump(Args& a) {
   p.min_solid = (uint32_t)a.num("MIN_SOLID", p.min_solid);
   p.max_q_suspect = (uint32_t)a.num("MAX_Q_SUSPECT", p.max_q_suspect);
   p.min_keep = (uint32_t)a.num("MIN_KEEP", p.min_keep);
+  Shard sh(a);
   a.finish();
-  Reads fr, jr;
+  Reads fr, jr_all;
   load_reads(a, fin, false, &fr);
-  load_reads(a, jin, true, &jr);
+  load_reads(a, jin, true, &jr_all);
   Ctx ctx(a);
-  const uint64_t n = jr.r.n_reads;
-  const uint64_t nbytes = n ? jr.r.byte_off[n] : 0, nbases = n ? jr.r.base_off[n] : 0;
+  apg_ecj_stats st;
+  // a sharded rank corrects its slice of the jump pairs against the global
+  // solid set of every rank's frag pairs (apg_sharded_error_correct_jump:
+  // counted across the ranks); rank 0 joins the parts
+  uint64_t j0 = 0, j1 = jr_all.r.n_reads;
+  if (sh.sharded()) {
+    if (jr_all.r.n_reads % 2 || fr.r.n_reads % 2) a.fail("sharded ErrorCorrectJump needs whole pairs (2i, 2i+1)");
+    sh.connect(a, ctx.c);
+    sh.range(jr_all.r.n_reads, &j0, &j1);
+  }
+  Slice js(jr_all.r, j0, j1);
+  const apg_reads& jr = js.r;  // this rank's jump reads (all of them single-process)
+  const uint64_t n = jr.n_reads;
+  const uint64_t nbytes = n ? jr.byte_off[n] : 0, nbases = n ? jr.base_off[n] : 0;
   std::vector<uint8_t> pk(nbytes + 64), q(nbases + 1);
   std::vector<uint32_t> keep(n + 1);
-  apg_ecj_stats st;
-  a.check(apg_error_correct_jump(ctx.c, &fr.r, &jr.r, &p, pk.data(), q.data(), keep.data(), &st),
-          "apg_error_correct_jump");
+  if (sh.sharded()) {
+    uint64_t f0 = 0, f1 = 0;
+    sh.range(fr.r.n_reads, &f0, &f1);
+    Slice fs(fr.r, f0, f1);
+    DReads dF, dJ, dK;
+    a.check(apg_reads_upload(ctx.c, &fs.r, &dF.d), "apg_reads_upload");
+    a.check(apg_reads_upload(ctx.c, &jr, &dJ.d), "apg_reads_upload");
+    void* d_keep = nullptr;
+    a.check(apg_device_alloc(ctx.c, (n + 1) * 4, &d_keep), "apg_device_alloc");
+    int rc = apg_sharded_error_correct_jump(ctx.c, sh.comm, dF.d, dJ.d, &p, static_cast<uint32_t*>(d_keep), &st);
+    if (rc == APG_OK) rc = apg_reads_download(ctx.c, dJ.d, pk.data(), q.data());
+    if (rc == APG_OK) rc = apg_device_to_host(ctx.c, keep.data(), d_keep, n * 4);
+    apg_device_free(ctx.c, d_keep);
+    a.check(rc, "apg_sharded_error_correct_jump");
+  } else {
+    a.check(apg_error_correct_jump(ctx.c, &fr.r, &jr, &p, pk.data(), q.data(), keep.data(), &st),
+            "apg_error_correct_jump");
+  }
   // trimmed layout: read r = its first keep[r] bases
   std::vector<uint64_t> bo(n + 1, 0), yo(n + 1, 0);
   for (uint64_t r = 0; r < n; ++r) bo[r + 1] = bo[r] + keep[r];
   a.check(apg_byte_offsets(bo.data(), n, yo.data()), "apg_byte_offsets");
   std::vector<uint8_t> tp(yo[n] + 64, 0), tq(bo[n] + 1);
   for (uint64_t r = 0; r < n; ++r) {
-    const uint8_t* src = pk.data() + jr.r.byte_off[r];
+    const uint8_t* src = pk.data() + jr.byte_off[r];
     std::memcpy(tp.data() + yo[r], src, (keep[r] + 3) / 4);
     if (keep[r] % 4) tp[yo[r] + keep[r] / 4] &= (uint8_t)((1u << (2 * (keep[r] % 4))) - 1);
-    std::memcpy(tq.data() + bo[r], q.data() + jr.r.base_off[r], keep[r]);
+    std::memcpy(tq.data() + bo[r], q.data() + jr.base_off[r], keep[r]);
   }
   apg_reads o{};
   o.n_reads = n;
@@ -401,10 +429,31 @@ int error_correct_jump(Args& a) {
   o.byte_off = yo.data();
   o.packed = tp.data();
   o.quals = tq.data();
+  Joined jn;
+  if (sh.sharded()) {  // ranks hold consecutive pairs: rank order = read order
+    if (sh.rank != 0) {
+      write_reads(a, part_name(out, sh.rank, sh.world), o, true);
+      sh.barrier(a);
+      sh.barrier(a);  // rank 0 has read every part
+      return 0;
+    }
+    sh.barrier(a);
+    jn.add(o);
+    for (int r = 1; r < sh.world; ++r) {
+      const std::string h = part_name(out, r, sh.world);
+      Reads pr;
+      load_reads(a, h, true, &pr);
+      jn.add(pr.r);
+      std::remove((h + ".fastb").c_str());
+      std::remove((h + ".qualb").c_str());
+    }
+    sh.barrier(a);
+    o = jn.view();
+  }
   a.check(apg_fastb_write((out + ".fastb").c_str(), &o), "writing .fastb");
   a.check(apg_qualb_write((out + ".qualb").c_str(), &o), "writing .qualb");
   std::printf("%s: %llu jump reads, %llu corrected, %llu whole, %llu trimmed, %llu dropped -> %s.{fastb,qualb}\n",
-              a.module.c_str(), (unsigned long long)n, (unsigned long long)st.pc.n_corrected,
+              a.module.c_str(), (unsigned long long)st.n_reads, (unsigned long long)st.pc.n_corrected,
               (unsigned long long)st.n_full, (unsigned long long)st.n_trimmed, (unsigned long long)st.n_dropped,
               out.c_str());
   return 0;
