@@ -1498,13 +1498,7 @@ struct UskOut {
   // diagnostics (APG_USK_PROF): thread 0's clock64 sums per phase — chunk
   // load + dedup, scan + owner map, inserts, node ranks, nodes + index + local links
   unsigned long long* prof = nullptr;
-  // with lsucc: node ids in local chain order (APG_USK_CHAIN=0: slot order)
-  uint32_t chain = 1;
 };
-// k_usk_bucket's chain ordering: a slot's links in text bits 8..31 (12 bits
-// per orientation) and its path mark in tag
-constexpr uint32_t kTxNone = 0xfffu, kTxGlobal = 0xffeu;
-constexpr uint32_t kChainMark = 0x80000000u, kChainUnreached = 0x100000u;
 
 // The node index of the single-GPU build, made by the node buckets
 // (usk_stage) instead of k_node_insert: valid when idx != null.
@@ -1524,7 +1518,7 @@ __device__ __forceinline__ uint32_t urec_fp(const SK48& r) {
 
 // One workgroup per bucket (grid-stride); blist (or null): the buckets to
 // run, nbuckets of them (the ones a smaller table overflowed).
-template <uint32_t TAB, int WPE = 4>
+template <uint32_t TAB, int WPE = 1>
 __global__ void __launch_bounds__(kUskBThreads) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_usk_bucket(const SK48* __restrict__ rec,
                                                              const uint64_t* __restrict__ boff, uint64_t nbuckets,
@@ -1540,9 +1534,6 @@ k_usk_bucket(const SK48* __restrict__ rec,
   __shared__ uint32_t scan_sm[64];
   __shared__ int ovf;
   __shared__ unsigned long long sbase;
-  __shared__ uint32_t chain_cur;  // chain-ordered ids: the next path's base rank
-  __shared__ int chain_bad;
-  const bool chain_order = o.chain != 0;
   constexpr int TB = __builtin_ctz(kUskTab);
   static_assert(kUskChunk * kUskMaxNk >= 2 * TAB, "owner doubles as the slot ranks");
   uint16_t* rnk = reinterpret_cast<uint16_t*>(owner);  // emit: slot -> rank in the bucket's node list
@@ -1734,146 +1725,10 @@ k_usk_bucket(const SK48* __restrict__ rec,
         rnk[s] = (uint16_t)j;  // owner and crec are free: every instance is inserted
         slot_of[j++] = (uint16_t)s;
       }
-    if (tid == 0) {
-      sbase = b0;
-      chain_cur = 0;
-      chain_bad = 0;
-    }
+    if (tid == 0) sbase = b0;
     __syncthreads();  // every slot's rank, the base
     const unsigned long long b = sbase;
     mark(4);
-    if (o.lsucc && chain_order) {  // block-uniform
-      // (1) every node's unique links, resolved in this table as k_links
-      // would (the successor is almost always in the same bucket), kept in
-      // text's upper 24 bits: per orientation d, 12 bits = kTxNone,
-      // kTxGlobal, or the successor's slot | its orientation << 11
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) {
-        const uint32_t s = slot_of[r];
-        const K3 key{ka[s], kb[s], kc[s]};
-        const uint32_t ext = text[s] & 0xffu;
-        const K3 rk = revcomp(key, kp);
-        uint32_t enc[2] = {kTxNone, kTxNone};
-        if (!k3_eq(key, rk)) {  // palindromic K-mers never link
-#pragma unroll
-          for (uint32_t d = 0; d < 2; ++d) {
-            const uint32_t out = out_set(ext, d);
-            if (__popc(out) != 1) continue;
-            const uint32_t bo = __ffs(out) - 1;
-            const K3 t = push_right(d ? rk : key, bo, kp);
-            const K3 tr = rc_roll(d ? key : rk, bo, kp);  // revcomp(t) by a shift
-            const bool fw = !k3_lt(tr, t);
-            const K3 c = fw ? t : tr;
-            const uint32_t h = usk_slot_hash(c);
-            const uint32_t tv = (h & ~3u) | 2u;
-            uint32_t sl = h >> (32 - TB), hit = kUskTab;
-            for (uint32_t probe = 0; probe < kUskProbeMax; ++probe) {
-              const uint32_t tg = tag[sl];  // the table is complete: read the slot at once
-              const uint64_t xa = ka[sl], xb = kb[sl], xc = kc[sl];
-              if (tg == 0) break;
-              if (tg == tv && xa == c.a && xb == c.b && xc == c.c) {
-                hit = sl;
-                break;
-              }
-              sl = (sl + 1) & (kUskTab - 1);
-            }
-            if (hit == kUskTab) {
-              enc[d] = kTxGlobal;
-              continue;
-            }
-            if (k3_eq(t, tr)) continue;  // palindromic successor
-            if (__popc(in_set(text[hit] & 0xffu, fw ? 0u : 1u)) != 1) continue;
-            enc[d] = hit | (fw ? 0u : 0x800u);
-          }
-        }
-        text[s] = ext | (enc[0] << 8) | (enc[1] << 20);
-      }
-      __syncthreads();
-      // (2) node ids in chain order: the local links make paths (each node
-      // has <= 2 linked neighbours, mutually); each path end walks it and
-      // marks every node with (end slot, position) — the smaller end's
-      // marks win (atomicMin) — so consecutive nodes of a chain get
-      // consecutive ids and the ranking walks, unibases and KmerPath writes
-      // after the bucket pass touch neighbouring records instead of random
-      // ones.  tag[] is free for it (no probe reads it any more): empty
-      // slots stay 0, every node holds kChainMark | end << 10 | position.
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) tag[slot_of[r]] = kChainMark | kChainUnreached;
-      __syncthreads();
-      auto nbr = [&](uint32_t x, uint32_t d) -> uint32_t {  // x's linked neighbour slot through d, or kUskTab
-        const uint32_t f = (text[x] >> (8 + 12 * d)) & 0xfffu;
-        return f >= kTxGlobal ? kUskTab : (f & 0x7ffu);
-      };
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) {
-        const uint32_t s = slot_of[r];
-        const uint32_t n0 = nbr(s, 0), n1 = nbr(s, 1);
-        if (n0 < kUskTab && n1 < kUskTab) continue;  // interior (or on a cycle)
-        uint32_t prev = kUskTab, cur = s, pos = 0;
-        for (;;) {
-          atomicMin(&tag[cur], kChainMark | (s << 10) | pos);
-          const uint32_t a0 = nbr(cur, 0), a1 = nbr(cur, 1);
-          const uint32_t nx = a0 != prev && a0 < kUskTab ? a0 : (a1 != prev && a1 < kUskTab ? a1 : kUskTab);
-          if (nx == kUskTab || nx == s || pos + 1 >= tot) break;
-          prev = cur;
-          cur = nx;
-          ++pos;
-        }
-        if (s <= cur) rnk[s] = (uint16_t)atomicAdd(&chain_cur, pos + 1);  // the smaller end numbers the path
-      }
-      __syncthreads();
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) {  // on cycles: reached by no walk
-        const uint32_t s = slot_of[r];
-        if (tag[s] & kChainUnreached) {
-          rnk[s] = (uint16_t)atomicAdd(&chain_cur, 1u);
-          tag[s] = kChainMark | (s << 10);
-        }
-      }
-      __syncthreads();
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) {  // rank = the path's base + position
-        const uint32_t s = slot_of[r];
-        const uint32_t v = tag[s], e = (v >> 10) & 0x3ffu;
-        const uint32_t rk = e != s ? rnk[e] + (v & 0x3ffu) : rnk[s];
-        if (rk >= tot) chain_bad = 1;  // paths that do not partition the nodes (links not mutual): never seen
-        if (e != s) rnk[s] = (uint16_t)rk;
-      }
-      __syncthreads();
-      if (chain_bad) {  // block-uniform: the slot-order ranks instead
-        for (uint32_t r = tid; r < tot; r += kUskBThreads) rnk[slot_of[r]] = (uint16_t)r;
-        __syncthreads();
-      }
-      // (3) the nodes (lanes in slot order, each node at its chain-ordered
-      // id): node, index entry, links
-      for (uint32_t r = tid; r < tot; r += kUskBThreads) {
-        const uint32_t s = slot_of[r];
-        const unsigned long long id = b + rnk[s];
-        if (id >= o.cap) continue;
-        const K3 key{ka[s], kb[s], kc[s]};
-        const uint32_t tx = text[s];
-        const uint64_t kh = key_hash(key);
-        o.nodes[id] = KRec{key.a, key.b, key.c, kh | (tx & 0xffu)};
-        uint32_t res[2];
-#pragma unroll
-        for (uint32_t d = 0; d < 2; ++d) {
-          const uint32_t f = (tx >> (8 + 12 * d)) & 0xfffu;
-          res[d] = f == kTxNone ? kNone
-                 : f == kTxGlobal ? kLsGlobal
-                                  : (uint32_t)(2 * (b + rnk[f & 0x7ffu])) + (f >> 11);
-        }
-        o.lsucc[id] = make_uint2(res[0], res[1]);
-        if (o.idx) {
-          if (id < o.idx_lim) {
-            const uint64_t h = kh >> 8;
-            const unsigned long long want = ((unsigned long long)idx_tag(h) << 32) | id;
-            uint64_t q = h & o.tmask;
-            while (atomicCAS(&o.idx[q], kIdxEmpty, want) != kIdxEmpty) q = (q + 1) & o.tmask;
-          } else {
-            atomicAdd(&o.gs[4], 1ull);
-          }
-        }
-      }
-      __syncthreads();
-      mark(5);
-      advance();
-      continue;
-    }
     // The nodes by rank (full lanes): the node, its index entry, its local
     // links.  The index insert's first probe is in flight during the links;
     // a taken slot probes on after them (load <= 1/2 by idx_lim).
@@ -2724,9 +2579,6 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
     APG_CHECK_HIP(hipMemsetAsync(gs, 0, 6 * 8, ctx->stream));
     if (pre_idx) APG_CHECK_HIP(hipMemsetAsync(pre_idx, 0xff, pre_T * 8, ctx->stream));
     UskOut uo{nodes, cap, gs, ovf, gs + 1, ls, dedup ? 1u : 0u, dstat, pre_idx, pre_T - 1, pre_T / 2};
-    // node ids in local chain order (APG_USK_CHAIN=0: slot order, the round-5 form; read per call)
-    const char* ce = getenv("APG_USK_CHAIN");
-    uo.chain = !(ce && !strcmp(ce, "0"));
     static const bool uprof = getenv("APG_USK_PROF") != nullptr;
     if (uprof) {
       APG_TRY(workspace_t(ctx, "usk_prof", 8, &uo.prof));
