@@ -415,15 +415,28 @@ int side_join(apg_ctx* ctx) {
   return f();
 }
 
-static hipStream_t lazy_stream(hipStream_t* s) {
-  if (!*s && hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
+// APG_{MAIN,SIDE,AUX}_PRIO=high|low: that stream's queue priority (A/B knob;
+// unset = normal).  The CP prefers a high-priority queue's workgroups when
+// kernels of several streams wait for CUs.
+static hipError_t make_stream(hipStream_t* s, const char* env) {
+  const char* e = getenv(env);
+  if (e && (!strcmp(e, "high") || !strcmp(e, "low"))) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      return hipStreamCreateWithPriority(s, hipStreamNonBlocking, !strcmp(e, "high") ? greatest : least);
+    (void)hipGetLastError();
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+static hipStream_t lazy_stream(hipStream_t* s, const char* env) {
+  if (!*s && make_stream(s, env) != hipSuccess) {
     (void)hipGetLastError();
     *s = nullptr;
   }
   return *s;
 }
-hipStream_t side_stream(apg_ctx* ctx) { return lazy_stream(&ctx->side); }
-hipStream_t aux_stream(apg_ctx* ctx) { return lazy_stream(&ctx->aux); }
+hipStream_t side_stream(apg_ctx* ctx) { return lazy_stream(&ctx->side, "APG_SIDE_PRIO"); }
+hipStream_t aux_stream(apg_ctx* ctx) { return lazy_stream(&ctx->aux, "APG_AUX_PRIO"); }
 
 }  // namespace apg
 
@@ -461,7 +474,7 @@ int apg_create(const apg_config* cfg, apg_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) == hipSuccess) ctx->n_cu = prop.multiProcessorCount;
   if (ctx->n_cu <= 0) ctx->n_cu = 256;
-  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (make_stream(&ctx->stream, "APG_MAIN_PRIO") != hipSuccess) {
     delete ctx;
     set_error("apg_create: hipStreamCreate failed");
     return APG_E_HIP;
