@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_
 // Writes the children's start offsets to d_child (nparents*ndig + 1) and, if
 // host_child, copies them to the host.
 template <typename R, typename RO>
-int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
+int part_level(apg_ctx* ctx, const R* src, RO* dst, const PartParents& parents, int shift, int bits,
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag, int kshift,
                bool wide) {
   constexpr int kTile = PartGeom<RO>::tile;
@@ -301,21 +301,37 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vecto
   const uint64_t np = parents.size();
   // ~24K chunks per level: enough workgroups, short count-matrix rows
   const uint64_t chunk = std::max<uint64_t>(4 * kTile, ((n / 24576) + kTile - 1) / kTile * kTile);
-  std::vector<Chunk> chunks;
-  std::vector<uint32_t> prow(np + 1);
-  std::vector<uint64_t> pstart(np);
+  // host scratch kept across calls (capacity reused: the chunk list of a
+  // 648 M-record level is ~25 K entries, rebuilt between levels on the
+  // critical path)
+  static thread_local std::vector<Chunk> chunks;
+  static thread_local std::vector<uint32_t> prow;
+  static thread_local std::vector<uint64_t> pstart;
+  chunks.clear();
+  chunks.reserve(n / chunk + np + 1);
+  prow.resize(np + 1);
+  pstart.resize(np);
   uint64_t pos = 0;
+  auto add = [&](uint64_t p, const Seg& s) -> bool {
+    if (s.len >= (1ull << 32)) return false;
+    for (uint64_t o = 0; o < s.len; o += chunk)
+      chunks.push_back(Chunk{s.start + o, (uint32_t)std::min<uint64_t>(chunk, s.len - o), (uint32_t)p});
+    pos += s.len;
+    return true;
+  };
   for (uint64_t p = 0; p < np; ++p) {
     prow[p] = (uint32_t)chunks.size();
     pstart[p] = pos;
-    for (const Seg& s : parents[p]) {
-      if (s.len >= (1ull << 32)) {
-        set_error("part_level: parent group exceeds 2^32 records");
-        return APG_E_UNSUPPORTED;
-      }
-      for (uint64_t o = 0; o < s.len; o += chunk)
-        chunks.push_back(Chunk{s.start + o, (uint32_t)std::min<uint64_t>(chunk, s.len - o), (uint32_t)p});
-      pos += s.len;
+    bool ok = true;
+    if (parents.lists) {
+      for (const Seg& s : (*parents.lists)[p]) ok = ok && add(p, s);
+    } else {
+      const std::vector<uint64_t>& b = *parents.bounds;
+      ok = add(p, Seg{b[p], b[p + 1] - b[p]});
+    }
+    if (!ok) {
+      set_error("part_level: parent group exceeds 2^32 records");
+      return APG_E_UNSUPPORTED;
     }
   }
   prow[np] = (uint32_t)chunks.size();
@@ -357,21 +373,21 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vecto
 }
 
 
-template int part_level<uint64_t, uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const std::vector<std::vector<Seg>>&,
+template int part_level<uint64_t, uint64_t>(apg_ctx*, const uint64_t*, uint64_t*, const PartParents&,
                                             int, int, uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SK16, SK16>(apg_ctx*, const SK16*, SK16*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SK16, SK16>(apg_ctx*, const SK16*, SK16*, const PartParents&, int, int,
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SK16, SK24>(apg_ctx*, const SK16*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SK16, SK24>(apg_ctx*, const SK16*, SK24*, const PartParents&, int, int,
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SKP, SKP>(apg_ctx*, const SKP*, SKP*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SKP, SKP>(apg_ctx*, const SKP*, SKP*, const PartParents&, int, int,
                                   uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SK16, SKP>(apg_ctx*, const SK16*, SKP*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SK16, SKP>(apg_ctx*, const SK16*, SKP*, const PartParents&, int, int,
                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SKP, SK24>(apg_ctx*, const SKP*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SKP, SK24>(apg_ctx*, const SKP*, SK24*, const PartParents&, int, int,
                                    uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SK24, SK24>(apg_ctx*, const SK24*, SK24*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SK24, SK24>(apg_ctx*, const SK24*, SK24*, const PartParents&, int, int,
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
-template int part_level<SK48, SK48>(apg_ctx*, const SK48*, SK48*, const std::vector<std::vector<Seg>>&, int, int,
+template int part_level<SK48, SK48>(apg_ctx*, const SK48*, SK48*, const PartParents&, int, int,
                                     uint64_t, uint64_t*, std::vector<uint64_t>*, const char*, int, bool);
 
 }  // namespace apg

@@ -103,8 +103,20 @@ int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out
 // pos, the key's bits below its top `kshift` bits as the packed key, so the
 // packed record's digits sit kshift bits higher).
 // wide: SKP records in the 34-bit-position form (skp_unpack).
+// The parents of a level: lists of segments, or (every level after a
+// level's own children) one segment per parent, [bounds[q], bounds[q+1]) —
+// the child offsets the level before copied back, with no per-parent vector
+// built on the host between levels.
+struct PartParents {
+  const std::vector<std::vector<Seg>>* lists = nullptr;
+  const std::vector<uint64_t>* bounds = nullptr;
+  PartParents(const std::vector<std::vector<Seg>>& l) : lists(&l) {}
+  PartParents(const std::vector<uint64_t>& b) : bounds(&b) {}
+  uint64_t size() const { return lists ? lists->size() : (bounds->empty() ? 0 : bounds->size() - 1); }
+};
+
 template <typename R, typename RO = R>
-int part_level(apg_ctx* ctx, const R* src, RO* dst, const std::vector<std::vector<Seg>>& parents, int shift, int bits,
+int part_level(apg_ctx* ctx, const R* src, RO* dst, const PartParents& parents, int shift, int bits,
                uint64_t n, uint64_t* d_child, std::vector<uint64_t>* host_child, const char* tag, int kshift = 0,
                bool wide = false);
 

@@ -2485,47 +2485,46 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
     for (uint32_t l = 0; l < B1; ++l) hb[l + 1] = hb[l] + rec_counts[l];
     APG_CHECK_HIP(hipMemcpyAsync(boff, hb.data(), (B1 + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
   }
+  std::vector<uint64_t> bounds;  // after the first level: one segment per parent
   for (int lev = 0; lev < nlev; ++lev) {
     const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
     consumed += bits;
     R* dst = (cur == bufA) ? bufB : bufA;
     std::vector<uint64_t> hb;
     const bool last = lev + 1 == nlev;
+    const PartParents parents_v = lev ? PartParents(bounds) : PartParents(parents);
     bool done = false;
     if constexpr (std::is_same<R, SK24>::value) {
       if (src16 && lev == 0 && pack16) {  // SK16 -> SKP with the input index (the record's mask slot)
         dst = bufA != spare ? bufA : bufB;
-        APG_TRY((part_level<SK16, SKP>(ctx, src16, reinterpret_cast<SKP*>(dst), parents, 64 - consumed, bits, n, boff,
+        APG_TRY((part_level<SK16, SKP>(ctx, src16, reinterpret_cast<SKP*>(dst), parents_v, 64 - consumed, bits, n, boff,
                                        &hb, "s24", kshift)));
         packed = true;
         done = true;
       } else if (src16 && lev == 0) {  // SK16 -> SK24 with the input index (the record's mask slot)
         dst = bufA != spare ? bufA : bufB;
-        APG_TRY((part_level<SK16, SK24>(ctx, src16, dst, parents, 64 - consumed, bits, n, boff,
+        APG_TRY((part_level<SK16, SK24>(ctx, src16, dst, parents_v, 64 - consumed, bits, n, boff,
                                         last ? nullptr : &hb, "s24")));
         done = true;
       } else if (packed) {  // packed records through the levels, unpacked by the last
         const SKP* in = reinterpret_cast<const SKP*>(cur);
         if (last && keep_packed)
-          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents, 64 - consumed + kshift, bits, n,
+          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents_v, 64 - consumed + kshift, bits, n,
                                         boff, nullptr, "s24")));
         else if (last)
-          APG_TRY((part_level<SKP, SK24>(ctx, in, dst, parents, 64 - consumed + kshift, bits, n, boff, nullptr, "s24",
+          APG_TRY((part_level<SKP, SK24>(ctx, in, dst, parents_v, 64 - consumed + kshift, bits, n, boff, nullptr, "s24",
                                          0, wide)));
         else
-          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents, 64 - consumed + kshift, bits, n,
+          APG_TRY((part_level<SKP, SKP>(ctx, in, reinterpret_cast<SKP*>(dst), parents_v, 64 - consumed + kshift, bits, n,
                                         boff, &hb, "s24")));
         done = true;
       }
     }
     if (!done)
-      APG_TRY(part_level<R>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb,
+      APG_TRY(part_level<R>(ctx, cur, dst, parents_v, 64 - consumed, bits, n, boff, last ? nullptr : &hb,
                             sizeof(R) == sizeof(SK24) ? "s24" : "s"));
-    nb = parents.size() << bits;
-    if (!last) {
-      parents.assign(nb, {});
-      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
-    }
+    nb = parents_v.size() << bits;
+    if (!last) bounds.swap(hb);
     cur = dst;
   }
   if (ctx->verbose && nb) {  // bucket skew: the largest buckets (records)

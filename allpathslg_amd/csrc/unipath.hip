@@ -2517,18 +2517,17 @@ static int usk_stage(apg_ctx* ctx, const SK48* src, const std::vector<uint64_t>&
   const SK48* cur = src;
   uint64_t nb = ndig;
   int consumed = pbits + D;
+  std::vector<uint64_t> bounds;  // after the first level: one segment per parent
   for (int lev = 0; lev < nlev; ++lev) {
     const int bits = rem / nlev + (lev < rem % nlev ? 1 : 0);
     consumed += bits;
     SK48* dst = cur == bufA ? bufB : bufA;
     std::vector<uint64_t> hb;
     const bool last = lev + 1 == nlev;
-    APG_TRY(part_level<SK48>(ctx, cur, dst, parents, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "usk"));
-    nb = parents.size() << bits;
-    if (!last) {
-      parents.assign(nb, {});
-      for (uint64_t q = 0; q < nb; ++q) parents[q].push_back(Seg{hb[q], hb[q + 1] - hb[q]});
-    }
+    const PartParents pp = lev ? PartParents(bounds) : PartParents(parents);
+    APG_TRY(part_level<SK48>(ctx, cur, dst, pp, 64 - consumed, bits, n, boff, last ? nullptr : &hb, "usk"));
+    nb = pp.size() << bits;
+    if (!last) bounds.swap(hb);
     cur = dst;
   }
   // buckets -> nodes
