@@ -13,7 +13,8 @@ if [ -n "${TESTS:-}" ]; then
   # ordinary test failures (rc 1) go on to the bench; a timeout, fault or
   # abort ends the call here
   if [ $rc -ne 0 ]; then
-    if [ $rc -ne 1 ] || grep -q "Timeout" gpurun_out/${LOG:-r6_ab}_pytest.log; then exit $rc; fi
+    # a timeout, a GPU fault or an abort: nothing more on the GPU in this call
+    if [ $rc -ne 1 ] || grep -q -E "Timeout|illegal memory access|Memory access fault|hipErrorLaunchFailure" gpurun_out/${LOG:-r6_ab}_pytest.log; then exit $rc; fi
     FAILED=1
   fi
 fi
