@@ -1062,6 +1062,82 @@ __global__ void k_digit_or(const uint64_t* __restrict__ k0, const uint64_t* __re
   }
 }
 
+// The pair-key sort's one-pass form (u_sort_keys): keys binned by their most
+// significant varying bits, each bin ranked in LDS by full 192-bit
+// comparison with ties by input position — the same order as the stable LSD
+// passes, in a handful of launches instead of ~22 launch-bound passes.
+// The bin digit: bits [lo, lo + bits) of the most significant varying key
+// word, which the host hands over as its own pointer `kw` (a per-thread
+// select among the three words, uniform as it is, was compiled on gfx950
+// into a path that loaded through an unset address register for word 2).
+struct MsdDigit {
+  int lo;  // lowest bit of the bin digit
+  uint32_t mask;
+};
+__device__ __forceinline__ uint32_t msd_bin(const uint64_t* kw, uint64_t i, MsdDigit d) {
+  return (uint32_t)(kw[i] >> d.lo) & d.mask;
+}
+__global__ void k_msd_count(const uint64_t* __restrict__ kw, uint64_t n, MsdDigit d, uint32_t* __restrict__ cnt) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[msd_bin(kw, i, d)], 1u);
+}
+// bin cursors start at 0 (cur zeroed); the largest bin goes to *mx
+__global__ void k_msd_scatter(SortCols c, const uint64_t* __restrict__ kw, uint64_t n, MsdDigit d,
+                              const uint64_t* __restrict__ off, uint32_t* __restrict__ cur, uint32_t* __restrict__ sidx,
+                              const uint32_t* __restrict__ cnt, uint64_t nbins, unsigned int* __restrict__ mx) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = t0; i < n; i += st) {
+    const uint32_t b = msd_bin(kw, i, d);
+    const uint64_t pos = off[b] + atomicAdd(&cur[b], 1u);
+    if (pos >= n) {  // cannot happen with consistent counts; refuses the one-pass form
+      atomicMax(mx, 0xffffffffu);
+      continue;
+    }
+    c.o0[pos] = c.k0[i];
+    c.o1[pos] = c.k1[i];
+    c.o2[pos] = c.k2[i];
+    c.opay[pos] = c.pay[i];
+    sidx[pos] = (uint32_t)i;
+  }
+  unsigned int m = 0;
+  for (uint64_t b = t0; b < nbins; b += st) m = max(m, cnt[b]);
+  if (m) atomicMax(mx, m);
+}
+constexpr uint32_t kBinSortMax = 1024;
+// one workgroup per bin: out[bin start + rank] = payload, rank = keys below
+// it (input position breaking ties)
+__global__ void __launch_bounds__(256) k_bin_sort(const uint64_t* __restrict__ b0, const uint64_t* __restrict__ b1,
+                                                  const uint64_t* __restrict__ b2, const uint32_t* __restrict__ bp,
+                                                  const uint32_t* __restrict__ sidx, const uint64_t* __restrict__ off,
+                                                  uint32_t* __restrict__ out) {
+  __shared__ uint64_t s0[kBinSortMax], s1[kBinSortMax], s2[kBinSortMax];
+  __shared__ uint32_t si[kBinSortMax];
+  const uint64_t beg = off[blockIdx.x];
+  const uint32_t m = (uint32_t)(off[blockIdx.x + 1] - beg);
+  if (m > kBinSortMax) return;  // the host checked the largest bin
+  if (m <= 1) {
+    if (m == 1 && threadIdx.x == 0) out[beg] = bp[beg];
+    return;
+  }
+  for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+    s0[t] = b0[beg + t];
+    s1[t] = b1[beg + t];
+    s2[t] = b2[beg + t];
+    si[t] = sidx[beg + t];
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+    const uint64_t x0 = s0[t], x1 = s1[t], x2 = s2[t];
+    const uint32_t xi = si[t];
+    uint32_t r = 0;
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint64_t y0 = s0[j], y1 = s1[j], y2 = s2[j];
+      r += y0 < x0 || (y0 == x0 && (y1 < x1 || (y1 == x1 && (y2 < x2 || (y2 == x2 && si[j] < xi)))));
+    }
+    out[beg + r] = bp[beg + t];
+  }
+}
+
 // emitted unipath indices of every pair and of both paths' heads
 __global__ void k_assign(uint64_t P, const uint32_t* __restrict__ ph, const uint32_t* __restrict__ tail_of,
                          const uint64_t* __restrict__ ustart, const uint32_t* __restrict__ chainlen,
@@ -2084,6 +2160,52 @@ static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, 
     APG_TRY(workspace_t(ctx, "u_som", 256 * Gs + 1, &som));
     uint64_t *a0 = pk[0], *a1 = pk[1], *a2 = pk[2], *b0 = pk[3], *b1 = pk[4], *b2 = pk[5];
     uint32_t *ap = ph, *bp = ph2;
+    // One-pass form (APG_U_SORT=lsd: the LSD passes only): bins on the most
+    // significant varying bits (~32 keys each), ranked in LDS; a bin over
+    // kBinSortMax keys sends the whole sort to the LSD passes below.
+    static const bool lsd_only = getenv("APG_U_SORT") && !strcmp(getenv("APG_U_SORT"), "lsd");
+    int top = -1;
+    for (int sel = 0; sel < 3 && top < 0; ++sel)
+      if (ho[sel] ^ ho[4 + sel]) top = sel;
+    if (!lsd_only && P > 1 && P < (1ull << 32) && top >= 0) {
+      const uint64_t vary = ho[top] ^ ho[4 + top];
+      const int hi = 63 - __builtin_clzll(vary);
+      const int want = std::max(1, std::min(16, ceil_log2_u((P + 31) / 32)));
+      const int lo = std::max(0, hi - want + 1);
+      const MsdDigit dg{lo, (uint32_t)((1ull << (hi - lo + 1)) - 1)};
+      const uint64_t* kw = top == 0 ? a0 : top == 1 ? a1 : a2;
+      const uint64_t nbins = (uint64_t)dg.mask + 1;
+      uint32_t *bcnt = nullptr, *bcur = nullptr, *sidx = nullptr;
+      uint64_t* boff = nullptr;
+      unsigned int* bmax = nullptr;
+      APG_TRY(workspace_t(ctx, "u_sbcnt", 2 * nbins + 2, &bcnt));
+      APG_TRY(workspace_t(ctx, "u_sboff", nbins + 1, &boff));
+      APG_TRY(workspace_t(ctx, "u_sidx", P, &sidx));
+      bcur = bcnt + nbins;
+      bmax = bcnt + 2 * nbins;
+      APG_CHECK_HIP(hipMemsetAsync(bcnt, 0, (2 * nbins + 2) * 4, ctx->stream));
+      kbegin(ctx, "u_sort_bins", P * 24 * 3 + P * 8);
+      k_msd_count<<<grid_for(ctx, P), 256, 0, ctx->stream>>>(kw, P, dg, bcnt);
+      APG_TRY(scan_u32_u64(ctx, bcnt, nbins, boff, "usb"));
+      k_msd_scatter<<<grid_for(ctx, P), 256, 0, ctx->stream>>>(SortCols{a0, a1, a2, ap, b0, b1, b2, bp}, kw, P, dg, boff,
+                                                               bcur, sidx, bcnt, nbins, bmax);
+      kend(ctx);
+      APG_CHECK_HIP(hipGetLastError());
+      unsigned int hmax = 0;
+      APG_CHECK_HIP(hipMemcpyAsync(&hmax, bmax, 4, hipMemcpyDeviceToHost, ctx->stream));
+      APG_TRY(sync(ctx));
+      vlog(ctx, "unipaths: pair keys %llu, bins %llu (word %d bits %d-%d), largest %u", (unsigned long long)P,
+           (unsigned long long)nbins, top, lo, hi, hmax);
+      if (hmax <= kBinSortMax) {
+        kbegin(ctx, "u_sort_rank", P * 28 * 2);
+        k_bin_sort<<<(uint32_t)nbins, 256, 0, ctx->stream>>>(b0, b1, b2, bp, sidx, boff, ap);
+        kend(ctx);
+        APG_CHECK_HIP(hipGetLastError());
+        *sorted = ap;
+        return APG_OK;
+      }
+      vlog(ctx, "unipaths: pair-key bin of %u keys: LSD passes", hmax);
+    }
       for (int sel = 2; sel >= 0 && P > 1; --sel) {
       const uint64_t varying = ho[sel] ^ ho[4 + sel];  // bits not constant over all keys
       for (int shift = 0; shift < 64; shift += 8) {
