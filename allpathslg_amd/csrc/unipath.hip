@@ -774,11 +774,15 @@ __global__ void __launch_bounds__(256) k_ruler_state1(uint64_t R, RankBufs rb, u
 // Asynchronous pointer jumping over the still-active rulers.  A state word is
 // a consistent (pointer, distance) pair read and written as one 8-byte
 // access, so a stale read is still a valid jump.
-__global__ void __launch_bounds__(256) k_ruler_jump(uint64_t n, const uint32_t* __restrict__ ain,
+// nin: the active-list length on the device (the previous round's nout), so
+// rounds queue back to back without a host read of each count
+__global__ void __launch_bounds__(256) k_ruler_jump(const unsigned long long* __restrict__ nin,
+                                                    const uint32_t* __restrict__ ain,
                                                     unsigned long long* __restrict__ state, uint32_t* __restrict__ aout,
                                                     unsigned long long* __restrict__ nout) {
   __shared__ uint32_t sm[64];
   __shared__ unsigned long long sb;
+  const uint64_t n = *nin;
   const uint64_t ntiles = (n + kTileN - 1) / kTileN;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     uint32_t flags = 0, cnt = 0;
@@ -2091,13 +2095,20 @@ static int u_rank_all(apg_ctx* ctx, const KRec* nodes, uint64_t N, const KeyP& k
     APG_TRY(d2h_u64(ctx, gs + 9, &na, 1));
     uint32_t *ain = rb.alist0, *aout = rb.alist1;
     const int max_rounds = ceil_log2_u(R + 1) + 2;
+    // rounds in batches of kJumpBatch between host reads of the active count
+    // (a round after the list empties is an empty launch); round it reads
+    // its length from jc[it - 1] (round 0: k_ruler_state1's count, gs + 9)
+    constexpr int kJumpBatch = 3;
+    unsigned long long* jc = nullptr;
+    APG_TRY(workspace_t(ctx, "u_jcnt", (uint64_t)max_rounds + 1, &jc));
+    APG_CHECK_HIP(hipMemsetAsync(jc, 0, ((uint64_t)max_rounds + 1) * 8, ctx->stream));
+    const uint32_t jgrid = grid_for(ctx, na);
     for (int it = 0; it < max_rounds && na; ++it) {
-      APG_CHECK_HIP(hipMemsetAsync(gs + 11, 0, 8, ctx->stream));
       kbegin(ctx, "u_ruler_jump", na * 48);
-      k_ruler_jump<<<grid_for(ctx, na), 256, 0, ctx->stream>>>(na, ain, rb.state, aout, gs + 11);
+      k_ruler_jump<<<jgrid, 256, 0, ctx->stream>>>(it ? jc + it - 1 : gs + 9, ain, rb.state, aout, jc + it);
       kend(ctx);
-      APG_TRY(d2h_u64(ctx, gs + 11, &na, 1));
       std::swap(ain, aout);
+      if ((it + 1) % kJumpBatch == 0 || it + 1 == max_rounds) APG_TRY(d2h_u64(ctx, jc + it, &na, 1));
     }
     APG_CHECK_HIP(hipGetLastError());
     // cycles?
