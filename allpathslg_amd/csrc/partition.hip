@@ -108,7 +108,15 @@ struct Chunk {
 // passes showed ~2.3x the algorithmic write + read bytes for SK24
 // (profiles/r02_v5/pmc).  Twice the tile and half the residency: runs twice
 // as long, a quarter of the open lines.
-constexpr int kPartTileBytes = 61440;
+// APG_PART_TILE_BYTES / APG_PART_WPE: compile-time A/B of the scatter tile
+// (LDS bytes per block) and its waves-per-EU bound (scripts/build_variants.sh)
+#ifndef APG_PART_TILE_BYTES
+#define APG_PART_TILE_BYTES 61440
+#endif
+#ifndef APG_PART_WPE
+#define APG_PART_WPE 2
+#endif
+constexpr int kPartTileBytes = APG_PART_TILE_BYTES;
 template <typename R>
 struct PartGeom {
   static constexpr int items = (kPartTileBytes / (int)sizeof(R)) / kPartThreads;
@@ -186,7 +194,7 @@ __device__ __forceinline__ uint64_t rkey_w0(uint64_t w0) {
 // the records instead of a separate pass over them), or a packed SKP that
 // leaves unpacked (the single-GPU solid count's last level).
 template <typename RI, typename RO = RI>
-__global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) k_part_scatter(
+__global__ void __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(1, APG_PART_WPE))) k_part_scatter(
     const RI* __restrict__ rec, const Chunk* __restrict__ ch, int shift, uint32_t ndig,
     const uint32_t* __restrict__ pre, const uint64_t* __restrict__ child, RO* __restrict__ out, int kshift, bool wide) {
   static_assert(std::is_same<RI, RO>::value || (sizeof(RI) == 16 && sizeof(RO) == 24) ||
