@@ -812,8 +812,14 @@ __global__ void __launch_bounds__(256) k_ruler_jump(const unsigned long long* __
 }
 
 // cyclic directed nodes: unvisited, or on a ruler that never reached a head
-__global__ void __launch_bounds__(256) k_mark_cyclic(uint64_t D, RankBufs rb, uint32_t* __restrict__ clist,
-                                                     unsigned long long* __restrict__ ncyc) {
+// cyclic directed nodes (unvisited, or on a ruler that never reached a head)
+// to clist; every other node's head, rank and (at a chain's tail) the chain
+// length and tail in the same pass — when no node is cyclic (the rule) the
+// ranking is final, and after a cycle cut the pass runs again
+__global__ void __launch_bounds__(256) k_rank_mark(uint64_t D, RankBufs rb, uint32_t* __restrict__ clist,
+                                                   unsigned long long* __restrict__ ncyc, uint32_t* __restrict__ head,
+                                                   uint32_t* __restrict__ rank, uint32_t* __restrict__ chainlen,
+                                                   uint32_t* __restrict__ tail_of) {
   __shared__ uint32_t sm[64];
   __shared__ unsigned long long sb;
   const uint64_t ntiles = (D + kTileN - 1) / kTileN;
@@ -823,10 +829,20 @@ __global__ void __launch_bounds__(256) k_mark_cyclic(uint64_t D, RankBufs rb, ui
     for (int i = 0; i < kTI; ++i) {
       const uint64_t v = t * kTileN + (uint64_t)i * 256 + threadIdx.x;
       if (v < D) {
-        const uint32_t r = rb.dn[v].ruler;
-        if (r == kNone || !st_done(rb.state[r])) {
+        const DN d = rb.dn[v];
+        const unsigned long long s = d.ruler == kNone ? 0ull : rb.state[d.ruler];
+        if (d.ruler == kNone || !st_done(s)) {
           flags |= 1u << i;
           ++cnt;
+        } else {
+          const uint32_t h = st_x(s);
+          const uint32_t k = (uint32_t)(st_off(s) + d.lrank);
+          head[v] = h;
+          rank[v] = k;
+          if (d.nxt == kNone) {
+            chainlen[h] = k + 1;
+            tail_of[h] = (uint32_t)v;
+          }
         }
       }
     }
@@ -880,23 +896,6 @@ __global__ void k_cyc_cut(uint64_t C, const uint32_t* __restrict__ clist, const 
 }
 
 // final per-node head and rank; tails record their chain's length
-__global__ void k_rank_final(uint64_t D, RankBufs rb, uint32_t* __restrict__ head, uint32_t* __restrict__ rank,
-                             uint32_t* __restrict__ chainlen, uint32_t* __restrict__ tail_of) {
-  for (uint64_t v0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v0 < D; v0 += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t v = (uint32_t)v0;
-    const DN d = rb.dn[v];
-    const unsigned long long s = rb.state[d.ruler];
-    const uint32_t h = st_x(s);
-    const uint32_t k = (uint32_t)(st_off(s) + d.lrank);
-    head[v] = h;
-    rank[v] = k;
-    if (d.nxt == kNone) {
-      chainlen[h] = k + 1;
-      tail_of[h] = v;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // U7: unipath pairs and their order
 // ---------------------------------------------------------------------------
@@ -2111,10 +2110,16 @@ static int u_rank_all(apg_ctx* ctx, const KRec* nodes, uint64_t N, const KeyP& k
       if ((it + 1) % kJumpBatch == 0 || it + 1 == max_rounds) APG_TRY(d2h_u64(ctx, jc + it, &na, 1));
     }
     APG_CHECK_HIP(hipGetLastError());
-    // cycles?
+    // cycles? (and the final ranks of every other node)
     uint32_t* clist = nullptr;
     APG_TRY(workspace_t(ctx, "u_clist", std::max<uint64_t>(D, 1), &clist));
-    k_mark_cyclic<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, clist, gs + 12);
+    APG_TRY(workspace_t(ctx, "u_head", std::max<uint64_t>(D, 1), head));
+    APG_TRY(workspace_t(ctx, "u_rank", std::max<uint64_t>(D, 1), rank));
+    APG_TRY(workspace_t(ctx, "u_chainlen", std::max<uint64_t>(D, 1), chainlen));
+    APG_TRY(workspace_t(ctx, "u_tailof", std::max<uint64_t>(D, 1), tail_of));
+    kbegin(ctx, "u_rank_final", D * 24);
+    k_rank_mark<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, clist, gs + 12, *head, *rank, *chainlen, *tail_of);
+    kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hc;
     APG_TRY(d2h_u64(ctx, gs + 12, &hc, 1));
@@ -2140,14 +2145,6 @@ static int u_rank_all(apg_ctx* ctx, const KRec* nodes, uint64_t N, const KeyP& k
     st->n_cycles_cut += hcut;
     vlog(ctx, "unipaths: %llu cyclic directed nodes, %llu cuts", hc, hcut);
   }
-  APG_TRY(workspace_t(ctx, "u_head", std::max<uint64_t>(D, 1), head));
-  APG_TRY(workspace_t(ctx, "u_rank", std::max<uint64_t>(D, 1), rank));
-  APG_TRY(workspace_t(ctx, "u_chainlen", std::max<uint64_t>(D, 1), chainlen));
-  APG_TRY(workspace_t(ctx, "u_tailof", std::max<uint64_t>(D, 1), tail_of));
-  kbegin(ctx, "u_rank_final", D * 24);
-  k_rank_final<<<grid_for(ctx, D), 256, 0, ctx->stream>>>(D, rb, *head, *rank, *chainlen, *tail_of);
-  kend(ctx);
-  APG_CHECK_HIP(hipGetLastError());
 
   return APG_OK;
 }
