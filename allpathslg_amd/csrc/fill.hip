@@ -1135,9 +1135,11 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   }
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
-  APG_TRY(scan_u32_u64(ctx, lens, np, bscan, "fb"));
-  APG_TRY(scan_u32_u64(ctx, nby, np, yscan, "fy"));
-  APG_TRY(scan_u32_u64(ctx, ones, np, iscan, "fi"));
+  {
+    const uint32_t* const ins[3] = {lens, nby, ones};
+    uint64_t* const outs[3] = {bscan, yscan, iscan};
+    APG_TRY(scan_cols_u32_u64(ctx, 3, ins, np, outs, "fby"));
+  }
   unsigned long long hc[6];
   uint64_t tot[3];
   APG_CHECK_HIP(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, ctx->stream));

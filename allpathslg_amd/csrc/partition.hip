@@ -82,6 +82,71 @@ int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out
   return APG_OK;
 }
 
+// Several scans of the same length at once (FillFragments' lengths, bytes
+// and filled flags): one launch per phase for all columns instead of one per
+// column; column c's tile sums at tsum[c * (nt + 1)].
+struct ScanCols {
+  const uint32_t* in[kScanColsMax];
+  uint64_t* out[kScanColsMax];
+};
+__global__ void __launch_bounds__(kScanThreads) k_scanc_tiles(ScanCols c, uint64_t n, uint64_t nt,
+                                                              uint64_t* __restrict__ tsum) {
+  __shared__ uint64_t sm[32];
+  const uint32_t col = blockIdx.y;
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i)
+    if (base + i < n) s += c.in[col][base + i];
+  uint64_t tot;
+  block_exclusive_scan<uint64_t>(s, sm, &tot);
+  if (threadIdx.x == 0) tsum[col * (nt + 1) + blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(kScanThreads) k_scanc_apply(ScanCols c, uint64_t n, uint64_t nt,
+                                                              const uint64_t* __restrict__ tsum) {
+  __shared__ uint64_t sm[32];
+  const uint32_t col = blockIdx.y;
+  const uint64_t* ts = tsum + col * (nt + 1);
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    v[i] = base + i < n ? c.in[col][base + i] : 0;
+    s += v[i];
+  }
+  uint64_t tot;
+  uint64_t run = block_exclusive_scan<uint64_t>(s, sm, &tot) + ts[blockIdx.x];
+  uint64_t* out = c.out[col];
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = ts[nt];
+}
+
+int scan_cols_u32_u64(apg_ctx* ctx, int ncol, const uint32_t* const* d_in, uint64_t n, uint64_t* const* d_out,
+                      const char* tag) {
+  APG_REQUIRE(ncol >= 1 && ncol <= kScanColsMax, "scan_cols_u32_u64: 1 .. kScanColsMax columns");
+  const uint64_t nt = std::max<uint64_t>(1, (n + kScanTile - 1) / kScanTile);
+  APG_REQUIRE(nt < (1ull << 31), "scan_cols_u32_u64: too many tiles");
+  uint64_t* tsum = nullptr;
+  APG_TRY(workspace_t(ctx, (std::string("scan_tsum_") + tag).c_str(), (nt + 1) * ncol, &tsum));
+  ScanCols c{};
+  for (int i = 0; i < ncol; ++i) {
+    c.in[i] = d_in[i];
+    c.out[i] = d_out[i];
+  }
+  kbegin(ctx, "scan", ncol * (n * 4 * 2 + (n + 1) * 8));
+  k_scanc_tiles<<<dim3((uint32_t)nt, ncol), kScanThreads, 0, ctx->stream>>>(c, n, nt, tsum);
+  for (int i = 0; i < ncol; ++i) k_scan_tsum<<<1, 1024, 0, ctx->stream>>>(tsum + i * (nt + 1), nt);
+  k_scanc_apply<<<dim3((uint32_t)nt, ncol), kScanThreads, 0, ctx->stream>>>(c, n, nt, tsum);
+  kend(ctx);
+  APG_CHECK_HIP(hipGetLastError());
+  return APG_OK;
+}
+
 // ------------------------------------------------------------------------
 // Stage B: partition levels.  Records of each parent group are split by the
 // next `bits` (<= 8) hash bits.  Chunks (runs of records inside one parent)

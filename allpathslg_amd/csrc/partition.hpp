@@ -92,6 +92,10 @@ struct Seg {
 
 // d_out[0..n] = exclusive prefix sums of d_in[0..n) (d_out[n] = total).
 int scan_u32_u64(apg_ctx* ctx, const uint32_t* d_in, uint64_t n, uint64_t* d_out, const char* tag);
+// ncol (<= kScanColsMax) such scans of the same length, launched together.
+constexpr int kScanColsMax = 4;
+int scan_cols_u32_u64(apg_ctx* ctx, int ncol, const uint32_t* const* d_in, uint64_t n, uint64_t* const* d_out,
+                      const char* tag);
 
 // One partition level: the records of every parent (a list of segments of
 // `src`) are split by bits [shift, shift+bits) of rkey() into ndig = 2^bits
