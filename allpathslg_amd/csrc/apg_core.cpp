@@ -400,6 +400,23 @@ int sync(apg_ctx* ctx) {
   return kflush(ctx);
 }
 
+int d2h_sync(apg_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  static const bool pageable = getenv("APG_D2H_PAGEABLE") && !strcmp(getenv("APG_D2H_PAGEABLE"), "1");  // A/B
+  if (!pageable && bytes && bytes <= kPinBytes && !ctx->pin &&
+      hipHostMalloc(&ctx->pin, kPinBytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    ctx->pin = nullptr;
+  }
+  if (!pageable && ctx->pin && bytes <= kPinBytes) {
+    if (bytes) APG_CHECK_HIP(hipMemcpyAsync(ctx->pin, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    APG_TRY(sync(ctx));
+    if (bytes) std::memcpy(dst, ctx->pin, bytes);
+    return APG_OK;
+  }
+  if (bytes) APG_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return sync(ctx);
+}
+
 int side_kick(apg_ctx* ctx, int stage) {
   if (!ctx->side_kick || (stage >= 0 && stage != ctx->side_kick_at)) return APG_OK;
   std::function<int()> k;
@@ -518,6 +535,8 @@ void apg_destroy(apg_ctx* ctx) {
   }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   staging_free(ctx);
+  if (ctx->pin) (void)hipHostFree(ctx->pin);
+  ctx->pin = nullptr;
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   (void)hipStreamDestroy(ctx->stream);

@@ -144,6 +144,10 @@ struct apg_ctx {
   // kernels and is joined by an event wait (PreCorrect's extension table
   // built beside its candidate scan).
   hipStream_t aux = nullptr;
+  // Pinned host scratch for the small device-to-host reads between kernels
+  // (d2h_sync): a pageable destination costs ~27 us per round trip against
+  // ~16 us pinned (tools/microbench/d2h_latency.hip).
+  void* pin = nullptr;
 
   // Grow-only named device workspaces.
   struct Buf {
@@ -402,6 +406,10 @@ void kbytes_add(apg_ctx* ctx, const char* name, uint64_t bytes);
 // Resolve pending events into kstats (call after a stream sync).
 int kflush(apg_ctx* ctx);
 int sync(apg_ctx* ctx);
+// Copy `bytes` from device `src` to host `dst` on ctx->stream and sync(ctx),
+// through the context's pinned scratch when it fits (kPinBytes).
+constexpr size_t kPinBytes = 1u << 20;
+int d2h_sync(apg_ctx* ctx, void* dst, const void* src, size_t bytes);
 // Complete the side-stream work, if any (runs ctx->side_finish once).
 int side_join(apg_ctx* ctx);
 // Launch a deferred side-stream pass whose kick point is `stage`.

@@ -1145,8 +1145,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   APG_CHECK_HIP(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, ctx->stream));
   APG_CHECK_HIP(hipMemcpyAsync(&tot[0], bscan + np, 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_CHECK_HIP(hipMemcpyAsync(&tot[1], yscan + np, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(&tot[2], iscan + np, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &tot[2], iscan + np, 8));
   kbytes_add(ctx, "fill", hc[5] * 64);  // one random 64-byte table line per extension lookup
   st->n_filled = hc[kFillOk];
   st->n_none = hc[kFillNone];
@@ -1171,8 +1170,7 @@ static int fill_impl(apg_ctx* ctx, const apg_dreads* dr, const apg_fill_params& 
   APG_CHECK_HIP(hipMemcpyAsync(fd->d_byte_off + nf, yscan + np, 8, hipMemcpyDeviceToDevice, ctx->stream));
   APG_CHECK_HIP(hipMemsetAsync(fd->d_packed + tot[1], 0, 64, ctx->stream));
   unsigned long long nbad = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&nbad, ndefer + 3, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &nbad, ndefer + 3, 8));
   if (nbad) {
     set_error("apg_fill_fragments: inconsistent fill records (internal error)");
     return APG_E_STATE;

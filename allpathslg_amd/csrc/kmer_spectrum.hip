@@ -553,8 +553,7 @@ static int extract_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::
   k_digit_starts<<<(ndig + 1 + 255) / 256, 256, 0, ctx->stream>>>(omat, ndig, G, dstart);
   APG_CHECK_HIP(hipGetLastError());
   std::vector<uint64_t> ds(ndig + 1);
-  APG_CHECK_HIP(hipMemcpyAsync(ds.data(), dstart, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, ds.data(), dstart, (ndig + 1) * 8));
   digit_counts->resize(ndig);
   for (uint32_t d = 0; d < ndig; ++d) (*digit_counts)[d] = ds[d + 1] - ds[d];
   auto& xs = ctx->xstate;
@@ -696,8 +695,7 @@ static int stage_count(apg_ctx* ctx, const uint64_t* src, uint64_t* spare, const
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hs[4];
-  APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, hs, gstats, sizeof hs));
   if (hs[1]) {
     // Oversized buckets: radix sort in global scratch (the ping-pong buffer not
     // holding rec is free now).
@@ -830,8 +828,7 @@ int apg_kmer_count_dev(apg_ctx* ctx, const apg_dreads* dr, int K, uint64_t hash_
   k_hash_bounds<<<1, 64, 0, ctx->stream>>>(d_keys, nd, hp, hash_lo, hash_hi, d_bounds);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hb[2];
-  APG_CHECK_HIP(hipMemcpyAsync(hb, d_bounds, sizeof hb, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, hb, d_bounds, sizeof hb));
   const uint64_t a = hb[0], n = hb[1] > hb[0] ? hb[1] - hb[0] : 0;
   auto* hk = (uint64_t*)std::malloc(std::max<uint64_t>(n, 1) * 8);
   auto* hc = (uint32_t*)std::malloc(std::max<uint64_t>(n, 1) * 4);

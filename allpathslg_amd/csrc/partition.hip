@@ -439,8 +439,7 @@ int part_level(apg_ctx* ctx, const R* src, RO* dst, const PartParents& parents, 
   APG_CHECK_HIP(hipGetLastError());
   if (host_child) {
     host_child->resize(nb + 1);
-    APG_CHECK_HIP(hipMemcpyAsync(host_child->data(), d_child, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, host_child->data(), d_child, (nb + 1) * 8));
   }
   return APG_OK;
 }

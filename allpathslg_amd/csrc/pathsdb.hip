@@ -109,8 +109,7 @@ int sort_u64_u32(apg_ctx* ctx, uint64_t* k, uint32_t* v, uint64_t* k2, uint32_t*
   APG_CHECK_HIP(hipMemsetAsync(orv, 0, 8, ctx->stream));
   k_rs_or<<<grid_for(ctx, n), 256, 0, ctx->stream>>>(k, n, orv);
   unsigned long long bits = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&bits, orv, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &bits, orv, 8));
   int nbits = 0;
   while (nbits < 64 && (bits >> nbits)) ++nbits;
   const uint32_t G = (uint32_t)((n + kRsTile - 1) / kRsTile);
@@ -309,8 +308,7 @@ int apg_make_rc_db(apg_ctx* ctx, const apg_unipath_graph* g, apg_rc_db* out) {
                                                                        nullptr);
   APG_TRY(scan_u32_u64(ctx, nrc, R, rcoff, "db"));
   uint64_t NR = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&NR, rcoff + R, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &NR, rcoff + R, 8));
   uint64_t *rs = nullptr, *rl = nullptr;
   APG_TRY(workspace_t(ctx, "db_rs", std::max<uint64_t>(NR, 1), &rs));
   APG_TRY(workspace_t(ctx, "db_rl", std::max<uint64_t>(NR, 1), &rl));

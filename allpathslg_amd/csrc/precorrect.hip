@@ -1178,8 +1178,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
       unsigned long long hn = 0;
-      APG_CHECK_HIP(hipMemcpyAsync(&hn, ctr, 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, &hn, ctr, 8));
       ncand = hn;
       have = ncand <= cap;
       if (have) kbytes_add(ctx, "pc_cand_write", ncand * sizeof(PcCand));
@@ -1194,8 +1193,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
       APG_TRY(scan_u32_u64(ctx, tcnt, ntiles, toff, "pct"));
-      APG_CHECK_HIP(hipMemcpyAsync(&ncand, toff + ntiles, 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, &ncand, toff + ntiles, 8));
       APG_TRY(workspace_t(ctx, "pc_cand", std::max<uint64_t>(ncand, 1), &cand));
       // reads' offsets + quals + weak bits in; runs and records out
       kbegin(ctx, "pc_cand_write", dr->n_bases + (weak ? dr->n_bases / 8 : 0) + 8 * dr->n_reads + 12 * dr->n_reads +
@@ -1279,8 +1277,7 @@ static int correct_pass(apg_ctx* ctx, apg_dreads* dr, const apg_pc_params& p, co
     link_done = nullptr;
   }
   unsigned long long h[6];
-  APG_CHECK_HIP(hipMemcpyAsync(h, dcnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, h, dcnt, sizeof h));
   // extension lookup: a random 64-byte HBM line; K-mer set: a bitmap query
   // reads one word of an L3-resident bitmap (counted 4 B), a table probe a
   // random 64-byte line
@@ -1555,8 +1552,7 @@ int ecj_with_solid(apg_ctx* ctx, apg_dreads* jr, const apg_ecj_params& e, const 
   kend(ctx);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long h[5];
-  APG_CHECK_HIP(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, h, cnt, sizeof h));
   kbytes_add(ctx, "ecj_trim", h[4] * 64);
   st->n_reads = jr->n_reads;
   st->n_full = h[0];

@@ -102,8 +102,7 @@ int dreads_device_shape(apg_ctx* ctx, apg_dreads* d, const uint64_t* d_qoff, boo
   APG_CHECK_HIP(hipMemcpyAsync(&ends[0], d->d_base_off, 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_CHECK_HIP(hipMemcpyAsync(&ends[1], d->d_base_off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
   APG_CHECK_HIP(hipMemcpyAsync(&ends[2], d->d_byte_off, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(&ends[3], d->d_byte_off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &ends[3], d->d_byte_off + n, 8));
   if (ends[0] != 0 || ends[2] != 0) {
     set_error(std::string(who) + ": offset tables must start at 0");
     return APG_E_ARG;
@@ -213,8 +212,7 @@ int apg_reads_concat_dev(apg_ctx* ctx, const apg_dreads* const* sets, const uint
   APG_TRY(scan_u32_u64(ctx, nby, n, yscan, "cat_y"));
   uint64_t tot[2];
   APG_CHECK_HIP(hipMemcpyAsync(&tot[0], bscan + n, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(&tot[1], yscan + n, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &tot[1], yscan + n, 8));
   const uint64_t nbases = tot[0], nbytes = tot[1];
 
   // output buffers (grow-only when an earlier output is passed back)

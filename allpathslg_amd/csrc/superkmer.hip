@@ -2001,8 +2001,7 @@ static int big_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, const ui
     k_sk_big_insert<RB, UP><<<g2, kBigChunk, 0, ctx->stream>>>(cur, boff, ovf, opre, n_ovf, p, g, UP ? binst : nullptr);
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long hf = 0;
-    APG_CHECK_HIP(hipMemcpyAsync(&hf, full, 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, &hf, full, 8));
     if (!hf) {
       if (UP && inst) k_add_u64<<<1, 1, 0, ctx->stream>>>(inst, binst);
       *out = g;
@@ -2025,8 +2024,7 @@ static int ovf_lds_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, cons
                          uint32_t n_ovf, const SkP& p, uint64_t nbk, bool solid, const SkOut& o, uint32_t g2,
                          uint64_t* n_inst = nullptr) {
   uint64_t tot = 0;  // flattened records
-  APG_CHECK_HIP(hipMemcpyAsync(&tot, opre + n_ovf, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &tot, opre + n_ovf, 8));
   uint32_t* nk = nullptr;
   uint64_t *ipre = nullptr, *qs = nullptr, *child = nullptr;
   APG_TRY(workspace_t(ctx, "sk_ovf_nk", std::max<uint64_t>(tot, 1), &nk));
@@ -2037,8 +2035,7 @@ static int ovf_lds_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, cons
   APG_TRY(scan_u32_u64(ctx, nk, tot, ipre, "skoi"));
   k_ovf_starts<<<(n_ovf + 256) / 256, 256, 0, ctx->stream>>>(opre, ipre, n_ovf, qs);
   std::vector<uint64_t> hq((size_t)n_ovf + 1);
-  APG_CHECK_HIP(hipMemcpyAsync(hq.data(), qs, ((size_t)n_ovf + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, hq.data(), qs, ((size_t)n_ovf + 1) * 8));
   if (UP ? hq[n_ovf] > nbk : hq[n_ovf] != nbk) {
     set_error("sk count: overflowed buckets' instances disagree (internal error)");
     return APG_E_STATE;
@@ -2071,14 +2068,12 @@ static int ovf_lds_count(apg_ctx* ctx, const RB* cur, const uint64_t* boff, cons
     k_ovf_count<false><<<grid, kOvfThreads, 0, ctx->stream>>>(e1, child, n_sb, p, o, bad, nbad, force_bad);
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hb = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&hb, nbad, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &hb, nbad, 8));
   if (hb) {  // sub-buckets past the LDS table: a global table over their entries
     std::vector<uint32_t> hbad(hb);
     std::vector<uint64_t> hc(n_sb + 1);
     APG_CHECK_HIP(hipMemcpyAsync(hbad.data(), bad, hb * 4, hipMemcpyDeviceToHost, ctx->stream));
-    APG_CHECK_HIP(hipMemcpyAsync(hc.data(), child, (n_sb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, hc.data(), child, (n_sb + 1) * 8));
     uint64_t inst = 0;
     for (uint32_t sb : hbad) inst += hc[sb + 1] - hc[sb];
     uint64_t T = 1024;
@@ -2173,8 +2168,7 @@ int sk_count(apg_ctx* ctx, const apg_dreads* dr, int K, int P, std::vector<uint6
   k_sk_digit_starts<<<(ndig + 256) / 256, 256, 0, ctx->stream>>>(omat, ndig, G, ds);
   std::vector<uint64_t> h(ndig + 1), kd(ndig);
   APG_CHECK_HIP(hipMemcpyAsync(h.data(), ds, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(kd.data(), kdig, ndig * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, kd.data(), kdig, ndig * 8));
   rec_counts->resize(ndig);
   for (uint32_t d = 0; d < ndig; ++d) (*rec_counts)[d] = h[d + 1] - h[d];
   *kmer_counts = kd;
@@ -2313,8 +2307,7 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
   p.wide = wide;
   unsigned long long hs[5];
   uint64_t up_inst = 0;  // owned K+1-mer instances the sub-bucket pass counted
-  APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, hs, u.gstats, sizeof hs));
   if (hs[1]) {  // overflowed buckets: by sub-bucket, as in sk_stage_count_t
     unsigned long long* nk = u.gstats + 3;
     APG_CHECK_HIP(hipMemsetAsync(nk, 0, 8, ctx->stream));
@@ -2328,8 +2321,7 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
     const uint32_t g2 = (uint32_t)ctx->n_cu * 8;
     k_sk_big_kmers<RB, true><<<g2, 256, 0, ctx->stream>>>(cur, boff, u.ovf_list, opre, n_ovf, nk);
     unsigned long long nbk = 0;
-    APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, &nbk, nk, 8));
     // APG_SK_OVF=global: the owned K+1-mers through one global table
     const char* oe = getenv("APG_SK_OVF");
     if (!(oe && !strcmp(oe, "global"))) {
@@ -2346,8 +2338,7 @@ static int sk_up_finish(apg_ctx* ctx, const RB* cur, const uint64_t* boff, uint6
     }
     kend(ctx);
     APG_CHECK_HIP(hipGetLastError());
-    APG_CHECK_HIP(hipMemcpyAsync(hs, u.gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, hs, u.gstats, sizeof hs));
   }
   unsigned long long ninst = 0;
   APG_CHECK_HIP(hipMemcpyAsync(&ninst, u.inst, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -2529,8 +2520,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
   }
   if (ctx->verbose && nb) {  // bucket skew: the largest buckets (records)
     std::vector<uint64_t> hb(nb + 1);
-    APG_CHECK_HIP(hipMemcpyAsync(hb.data(), boff, (nb + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, hb.data(), boff, (nb + 1) * 8));
     std::vector<uint64_t> sz(nb);
     for (uint64_t b = 0; b < nb; ++b) sz[b] = hb[b + 1] - hb[b];
     std::sort(sz.begin(), sz.end(), std::greater<uint64_t>());
@@ -2637,8 +2627,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       const uint32_t g2 = (uint32_t)ctx->n_cu * 8;  // persistent: the flattened list's size stays on the device
       k_sk_big_kmers<RB><<<g2, 256, 0, ctx->stream>>>(cur, boff, ovl, opre, n_ovf, nk);
       unsigned long long nbk = 0;
-      APG_CHECK_HIP(hipMemcpyAsync(&nbk, nk, 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, &nbk, nk, 8));
       vlog(ctx, "sk count: %u buckets overflow the LDS table (%llu K-mers)", n_ovf, nbk);
       // APG_SK_OVF=global: every overflowed K-mer through one global table
       // (the round-4 path); default: sub-bucket counting in LDS
@@ -2686,8 +2675,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           APG_CHECK_HIP(hipMemsetAsync(nh, 0, 8, ctx->stream));
           k_sk_heavy<<<grid_for(ctx, nb), 256, 0, ctx->stream>>>(boff, nb, heavy, nh);
           unsigned long long h = 0;
-          APG_CHECK_HIP(hipMemcpyAsync(&h, nh, 8, hipMemcpyDeviceToHost, ctx->stream));
-          APG_TRY(sync(ctx));
+          APG_TRY(d2h_sync(ctx, &h, nh, 8));
           n_heavy = (uint32_t)h;
           hs_side = n_heavy ? side_stream(ctx) : nullptr;
           if (hs_side) {
@@ -2743,18 +2731,15 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
         APG_CHECK_HIP(hipEventDestroy(ev));
       }
       unsigned long long hs[6];
-      APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, hs, gstats, sizeof hs));
       n_drec = hs[5];
       if (hs[1]) {  // overflowed buckets (the LDS table filled)
         APG_TRY(run_ovf(ovf, (uint32_t)hs[1]));
-        APG_CHECK_HIP(hipMemcpyAsync(hs, gstats, sizeof hs, hipMemcpyDeviceToHost, ctx->stream));
-        APG_TRY(sync(ctx));
+        APG_TRY(d2h_sync(ctx, hs, gstats, sizeof hs));
       }
       if (prof) {
         unsigned long long hp[8];
-        APG_CHECK_HIP(hipMemcpyAsync(hp, dprof, sizeof hp, hipMemcpyDeviceToHost, ctx->stream));
-        APG_TRY(sync(ctx));
+        APG_TRY(d2h_sync(ctx, hp, dprof, sizeof hp));
         fprintf(stderr, "[sk_prof] K=%d solid=%d dedup %.3g flatten %.3g insert %.3g weak %.3g emit %.3g clear %.3g redo %llu\n", K,
                 (int)solid, (double)hp[0], (double)hp[1], (double)hp[2], (double)hp[3], (double)hp[4], (double)hp[5], hs[4]);
       }
@@ -2767,8 +2752,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
           uint64_t* offs = nullptr;
           APG_TRY(workspace_t(ctx, "sk_soffs", n_chunks + 1, &offs));
           APG_TRY(scan_u32_u64(ctx, sused, n_chunks, offs, "sks"));
-          APG_CHECK_HIP(hipMemcpyAsync(&n_solid, offs + n_chunks, 8, hipMemcpyDeviceToHost, ctx->stream));
-          APG_TRY(sync(ctx));
+          APG_TRY(d2h_sync(ctx, &n_solid, offs + n_chunks, 8));
           APG_TRY(workspace_t(ctx, "pc_solid", std::max<uint64_t>(n_solid, 1), &dense));
           kbegin(ctx, "solid_compact", n_solid * 16 + n_chunks * 12);
           if (n_chunks)
@@ -2802,8 +2786,7 @@ static int sk_stage_count_t(apg_ctx* ctx, const R* src, R* spare, const std::vec
       APG_CHECK_HIP(hipMemsetAsync(gstats, 0, 6 * 8, ctx->stream));
     }
     if (hist && hist_len) {
-      APG_CHECK_HIP(hipMemcpyAsync(hist, ghist, hist_len * 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, hist, ghist, hist_len * 8));
       hist[0] = 0;
     }
     res->n_kmers = n_kmers;

@@ -1947,8 +1947,7 @@ static T* host_dup(const T* d, uint64_t n, std::vector<D2HJob>* jobs, int* rc) {
 }
 
 static int d2h_u64(apg_ctx* ctx, const unsigned long long* d, unsigned long long* h, int n) {
-  APG_CHECK_HIP(hipMemcpyAsync(h, d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
-  return sync(ctx);
+  return d2h_sync(ctx, h, d, (size_t)n * 8);
 }
 
 // HyperLogLog estimate of the distinct count from 2^kHllBits registers.
@@ -1982,8 +1981,7 @@ static int u_size(apg_ctx* ctx, const apg_dreads* dr, const KeyP& kp, uint64_t* 
   std::vector<uint32_t> reg(1u << kHllBits);
   unsigned long long n = 0;
   APG_CHECK_HIP(hipMemcpyAsync(reg.data(), hll, reg.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(&n, cnt, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &n, cnt, 8));
   *n_inst = n;
   *est = n ? std::min<double>((double)n, hll_estimate(reg)) : 0.0;
   return APG_OK;
@@ -2019,8 +2017,7 @@ static int u_build_nodes(apg_ctx* ctx, const apg_dreads* dr, const KRec* rec, ui
     }
     APG_CHECK_HIP(hipGetLastError());
     unsigned long long of[2] = {0, 0};
-    APG_CHECK_HIP(hipMemcpyAsync(of, ovf, 16, hipMemcpyDeviceToHost, ctx->stream));
-    APG_TRY(sync(ctx));
+    APG_TRY(d2h_sync(ctx, of, ovf, 16));
     kbytes_add(ctx, dr ? "u_insert" : "u_insert_recs", of[1] * 64);  // one 64-byte slot line per probe
     if (!of[0]) break;
     if (attempt >= 6) {
@@ -2042,8 +2039,7 @@ static int u_build_nodes(apg_ctx* ctx, const apg_dreads* dr, const KRec* rec, ui
   APG_TRY(scan_u32_u64(ctx, cmat, (uint64_t)ndig * G, omat, "ut"));
   k_digit_starts_u<<<1, 64, 0, ctx->stream>>>(omat, ndig, G, dstart);
   std::vector<uint64_t> ds(ndig + 1);
-  APG_CHECK_HIP(hipMemcpyAsync(ds.data(), dstart, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, ds.data(), dstart, (ndig + 1) * 8));
   const uint64_t N = ds[ndig];
   KRec* nodes = nullptr;
   APG_TRY(workspace_t(ctx, "u_nodes", std::max<uint64_t>(N, 1), &nodes));
@@ -2200,8 +2196,7 @@ static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, 
       kend(ctx);
       APG_CHECK_HIP(hipGetLastError());
       unsigned int hmax = 0;
-      APG_CHECK_HIP(hipMemcpyAsync(&hmax, bmax, 4, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, &hmax, bmax, 4));
       vlog(ctx, "unipaths: pair keys %llu, bins %llu (word %d bits %d-%d), largest %u", (unsigned long long)P,
            (unsigned long long)nbins, top, lo, hi, hmax);
       if (hmax <= kBinSortMax) {
@@ -2376,8 +2371,7 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
 
   // ---- U8 --------------------------------------------------------------------
   uint64_t tot_ub = 0;
-  APG_CHECK_HIP(hipMemcpyAsync(&tot_ub, ub_off + U, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &tot_ub, ub_off + U, 8));
   uint8_t* ub = nullptr;
   APG_TRY(workspace_t(ctx, "u_ub", std::max<uint64_t>(tot_ub, 1), &ub));
   kbegin(ctx, "u_unibases", D * 16 + tot_ub);
@@ -2400,8 +2394,7 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   APG_CHECK_HIP(hipGetLastError());
   unsigned long long hv[2];
   APG_CHECK_HIP(hipMemcpyAsync(hv, vid + 2 * U, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(hv + 1, gs + 24, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, hv + 1, gs + 24, 8));
   st->n_vertices = hv[0];
   if (hv[1]) {
     set_error("unipaths: adjacency edge to a missing K-mer (internal error)");
@@ -2411,12 +2404,10 @@ static int u_graph(apg_ctx* ctx, const KRec* nodes, uint64_t N, const apg_dreads
   if (want_paths) {
     if (pax) {  // the count pass ran beside U8: its total, then the write pass here
       StreamSwap sw(ctx, pax);
-      APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, &NI, ioff + dr->n_reads, 8));
     } else {
       APG_TRY(paths_count());
-      APG_CHECK_HIP(hipMemcpyAsync(&NI, ioff + dr->n_reads, 8, hipMemcpyDeviceToHost, ctx->stream));
-      APG_TRY(sync(ctx));
+      APG_TRY(d2h_sync(ctx, &NI, ioff + dr->n_reads, 8));
     }
     APG_TRY(workspace_t(ctx, "u_istart", std::max<uint64_t>(NI, 1), &istart));
     APG_TRY(workspace_t(ctx, "u_ilen", std::max<uint64_t>(NI, 1), &ilen));
@@ -2565,8 +2556,7 @@ static int usk_plan(apg_ctx* ctx, const apg_dreads* dr, const UskP& p, int P, st
   h->assign(ndig + 1, 0);
   kd->assign(ndig, 0);
   APG_CHECK_HIP(hipMemcpyAsync(h->data(), ds, (ndig + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(kd->data(), kdig, ndig * 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, kd->data(), kdig, ndig * 8));
   *G_out = G;
   auto& us = ctx->urstate;
   us.valid = true;
@@ -3186,8 +3176,7 @@ static int ulocs_run(apg_ctx* ctx, const apg_dreads* dr, uint32_t flags, const U
   uint64_t NL = 0;
   unsigned long long hc[3] = {0, 0, 0};
   APG_CHECK_HIP(hipMemcpyAsync(&NL, loff + R, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_CHECK_HIP(hipMemcpyAsync(hc, cnt, 24, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, hc, cnt, 24));
   const uint64_t nk = hc[2];
   kbytes_add(ctx, "ulocs_count", nk * 64);
   APG_REQUIRE(NL < (1ull << 32), "apg_unipath_locs: more than 2^32 locations");
@@ -3508,8 +3497,7 @@ int apg_unipath_coverage_dev(apg_ctx* ctx, const apg_aln_pair* d_locs, uint64_t 
     APG_CHECK_HIP(hipMemcpyAsync(hc.data(), dcov, U * 8, hipMemcpyDeviceToHost, ctx->stream));
     APG_CHECK_HIP(hipMemcpyAsync(hl.data(), g.ulen, U * 8, hipMemcpyDeviceToHost, ctx->stream));
   }
-  APG_CHECK_HIP(hipMemcpyAsync(&nbad, cnt + U, 8, hipMemcpyDeviceToHost, ctx->stream));
-  APG_TRY(sync(ctx));
+  APG_TRY(d2h_sync(ctx, &nbad, cnt + U, 8));
   APG_REQUIRE(nbad == 0, "apg_unipath_coverage: placements on unipaths the graph does not have");
   // length-weighted median of cov over the long unipaths
   std::vector<std::pair<double, uint64_t>> lv;
