@@ -379,7 +379,7 @@ def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2):
     keep = torch.empty(max(jumps.n_reads, 1), dtype=torch.int32, device="cuda")
     st = {"filled": None, "all": None}
 
-    def step(work=None):
+    def step():
         ctx.copy_reads(dwork, dsrc)
         ctx.copy_reads(dJ, dJ0)
         _, pst = ctx.precorrect(dwork, K=a.K_correct)
@@ -818,7 +818,7 @@ def main():
             log(rank, f"stage {name:12s} {(t - stage_t[0]) * 1e3:8.2f} ms")
             stage_t[0] = t
 
-    def step():
+    def step(work=None):
         mark("(between)")
         fut = pool.submit(ctx_s.kmer_spectrum, dsrc, a.K) if overlap else None
         # the working copy: a pristine read set staged before the timed region
