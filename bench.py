@@ -367,7 +367,7 @@ def jump_bench(ctx, dsrc, genome, a, reps: int = 2):
     return out
 
 
-def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2):
+def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2, reads=None):
     """C3 line (BASELINE configs[2]): chr20 frag reads (the
     step's 40 M) + a 3-kb jump library (10 M pairs = 20 M reads): PreCorrect
     of the frags, FillFragments, ErrorCorrectJump of the jumps against the
@@ -379,23 +379,35 @@ def c3_bench(ctx, dsrc, dwork, genome, a, reps: int = 2):
     keep = torch.empty(max(jumps.n_reads, 1), dtype=torch.int32, device="cuda")
     st = {"filled": None, "all": None}
 
-    def step():
-        ctx.copy_reads(dwork, dsrc)
-        ctx.copy_reads(dJ, dJ0)
-        _, pst = ctx.precorrect(dwork, K=a.K_correct)
-        st["filled"], _, fst = ctx.fill_fragments(dwork, K=a.K_correct, last_solid=True, out=st["filled"])
-        est = ctx.error_correct_jump(dwork, dJ, K=a.K_correct, d_keep=keep.data_ptr())
-        st["all"] = ctx.concat_reads([st["filled"], dJ], [None, keep.data_ptr()], out=st["all"])
+    def step(work=None):
+        fr, jr = work if work is not None else (dwork, dJ)
+        if work is None:
+            ctx.copy_reads(dwork, dsrc)
+            ctx.copy_reads(dJ, dJ0)
+        _, pst = ctx.precorrect(fr, K=a.K_correct)
+        st["filled"], _, fst = ctx.fill_fragments(fr, K=a.K_correct, last_solid=True, out=st["filled"])
+        est = ctx.error_correct_jump(fr, jr, K=a.K_correct, d_keep=keep.data_ptr())
+        st["all"] = ctx.concat_reads([st["filled"], jr], [None, keep.data_ptr()], out=st["all"])
         _, ust = ctx.unipaths(st["all"], a.K_unipath, read_paths=True, fetch=False)
         return pst, fst, est, ust
 
     step()
+    # pristine resident (frag, jump) read sets per timed step, as the main
+    # line stages them (needs the frags' host set)
+    staged = []
+    if reads is not None and not a.no_stage:
+        per = int((reads.n_reads + jumps.n_reads) * 16 + (int(dsrc.n_bases) + jumps.n_bases) * 1.25) + (64 << 20)
+        n_stage = max(0, min(reps, int((torch.cuda.mem_get_info()[0] - (24 << 30)) // per)))
+        staged = [(ctx.upload(reads), ctx.upload(jumps)) for _ in range(n_stage)]
     torch.cuda.synchronize()
     ctx.reset_timing()
     t0 = time.perf_counter()
-    for _ in range(reps):
-        pst, fst, est, ust = step()
+    for i in range(reps):
+        pst, fst, est, ust = step(staged[i] if i < len(staged) else None)
     torch.cuda.synchronize()
+    for fr, jr in staged:
+        fr.free()
+        jr.free()
     wall = (time.perf_counter() - t0) / reps
     kt = ctx.kernel_times()
     ms = {k: v[0] / max(v[1], 1) * v[1] / reps for k, v in kt.items()}
@@ -1016,7 +1028,7 @@ def main():
 
     c3 = None
     if rank == 0 and world == 1 and not a.spectrum_only and a.c3_jump_pairs > 0 and frags is None:
-        c3 = c3_bench(ctx, dsrc, dreads, genome, a)
+        c3 = c3_bench(ctx, dsrc, dreads, genome, a, reads=reads)
 
     rep = None
     if rank == 0 and world == 1 and not a.spectrum_only and a.repeat_steps > 0 and frags is None:
