@@ -2199,7 +2199,12 @@ static int u_sort_keys(apg_ctx* ctx, uint64_t P, uint64_t* pk[6], uint32_t* ph, 
       APG_TRY(d2h_sync(ctx, &hmax, bmax, 4));
       vlog(ctx, "unipaths: pair keys %llu, bins %llu (word %d bits %d-%d), largest %u", (unsigned long long)P,
            (unsigned long long)nbins, top, lo, hi, hmax);
-      if (hmax <= kBinSortMax) {
+      // APG_U_SORT_BINMAX (tests): a lower bin limit, so the LSD fallback runs
+      static const uint32_t binmax = [] {
+        const char* e = getenv("APG_U_SORT_BINMAX");
+        return e ? std::min<uint32_t>(kBinSortMax, (uint32_t)std::max(0, atoi(e))) : kBinSortMax;
+      }();
+      if (hmax <= binmax) {
         kbegin(ctx, "u_sort_rank", P * 28 * 2);
         k_bin_sort<<<(uint32_t)nbins, 256, 0, ctx->stream>>>(b0, b1, b2, bp, sidx, boff, ap);
         kend(ctx);
